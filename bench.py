@@ -1,0 +1,185 @@
+#!/usr/bin/env python3
+"""bench.py -- Mray/s of the ray-march hot path on 1..N MI355X GPUs.
+
+Workload (BASELINE.json configs[4], the reference algorithm at the metric's
+1920x1080x128 point): 512^3 RGBA8 density grid built by the reference recipe
+(TestMain.cpp:43-92, frequencies scaled by 128/512), reference camera
+(TestMain.cpp:219-245, aspect 16:9), 128 steps (frag.glsl:30), RGBA8 output.
+One "step" of this bench = one frame.  The frame is sharded over the ranks as
+interleaved 16-row bands.  With N > 1, each frame's bands are gathered to rank 0
+over RCCL and assembled there.  The volume is resident in HBM before timing.
+
+value = W*H*max_steps*frames / wall time (nominal Mray/s, the BASELINE
+metric), max over ranks.  roofline: algorithmic gather bytes of the march
+kernel (32 B per executed ray-step) / its mean HIP-event
+duration.  cpu_baseline: the CPU oracle (oracle/, a port) on the same workload.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config grid512|grid128]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import volumetricrenderer_amd as vr  # noqa: E402
+from volumetricrenderer_amd import distributed as vrdist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+BYTES_PER_STEP = 32        # 4 trilinear taps x 8 texels x 1 B
+
+CONFIGS = {
+    # name: (volume N, width, height, max_steps, BASELINE configs index)
+    "grid512": (512, 1920, 1080, 128, 4),
+    "grid128": (128, 1920, 1080, 128, None),
+}
+
+
+def cpu_baseline(volume_host: np.ndarray, osd, gsd, march, width, height, budget_s=10.0):
+    """Time the oracle on the same frame (all cores it is allowed), ~budget_s."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import vr_oracle as oracle
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    threads = max(1, min(threads, len(os.sched_getaffinity(0))))
+    obj, glob = vr.shader_data_arrays(osd, gsd)
+    m = oracle.from_params(march)
+    # sample: every 8th 16-row band of the frame (1/8 of the rows, spread
+    # over the whole silhouette), repeated until the budget is spent.
+    t0 = time.perf_counter()
+    rows = 0
+    steps = 0
+    reps = 0
+    while True:
+        _, s = oracle.render(volume_host, obj, glob, m, width, height, oracle.FMT_RGBA8_UNORM,
+                             band_rows=16, band_stride=8, band_first=reps % 8, threads=threads)
+        rows += vr.band_rows_packed(height, 16, 8, reps % 8)
+        steps += s
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or reps >= 64:
+            break
+    mray = rows * width * march.max_steps / el / 1e6
+    return {"value": round(mray, 3), "unit": "Mray/s", "cores": threads, "kind": "port",
+            "sample": f"{reps} band sets of every 8th 16-row band ({rows} rows of {height}) of the same "
+                      f"{width}x{height}x{march.max_steps} frame and volume, {el:.1f} s; "
+                      f"executed steps/s {steps / el:.4g}"}
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="grid512", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=10.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    N, W, H, S, cfg_idx = CONFIGS[args.config]
+
+    r = vr.Renderer(local)
+    r.generate_volume(vr.scaled_recipe(N))
+    osd, gsd = vr.reference_shader_data(1280.0 / 720.0)
+    r.set_shader_data(osd, gsd)
+    march = vr.march_defaults(max_steps=S)
+    r.set_march(march)
+    fmt = vr.FMT_RGBA8_UNORM
+    sharder = vrdist.BandSharder(r, W, H, fmt, band_rows=16, world=world, rank=rank)
+    stream = torch.cuda.current_stream()
+
+    # executed ray-steps per launch (this rank's bands), one untimed pass
+    counter = torch.zeros(1, dtype=torch.int64, device="cuda")
+    sharder.render_local(step_counter=counter)
+    torch.cuda.synchronize()
+    local_steps = int(counter.item())
+    tot = torch.tensor([local_steps], dtype=torch.int64, device="cuda")
+    if world > 1:
+        dist.all_reduce(tot)
+    frame_steps = int(tot.item())
+
+    for _ in range(args.warmup):
+        sharder.frame()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        sharder.frame(events=ev[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    tt = torch.tensor([el, kern_ms], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    el, kern_ms_max = float(tt[0]), float(tt[1])
+
+    if rank == 0:
+        ms_per_step = el / args.steps * 1e3
+        value = W * H * S * args.steps / el / 1e6
+        achieved = local_steps * BYTES_PER_STEP / (kern_ms * 1e-3) / 1e9
+        traffic = None
+        tfile = os.path.join(ROOT, "profiles", "traffic.json")
+        if os.path.exists(tfile):
+            with open(tfile) as f:
+                tj = json.load(f)
+            if tj.get("config") == args.config and world == 1:
+                traffic = tj.get("hbm_bytes_per_launch")
+        out = {
+            "metric": "Mray/s (= W*H*steps/s) at 1080p x 128 steps",
+            "value": round(value, 3),
+            "unit": "Mray/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: reference noise recipe volume generated on the GPU (FastNoise2-style restatement)",
+            "config": {"workload": f"{args.config}: {N}^3 RGBA8 grid, {W}x{H}, {S} steps, RGBA8 out",
+                       "baseline_config_index": cfg_idx, "width": W, "height": H, "max_steps": S,
+                       "volume": f"{N}^3 RGBA8", "camera": "reference (TestMain.cpp:219-245)",
+                       "kernel": r.kernel_variant, "parallelism": f"bands16x{world}",
+                       "executed_steps_per_frame": frame_steps},
+            "executed_steps_per_s": round(frame_steps * args.steps / el, 1),
+            "kernel_ms_mean": round(kern_ms, 5),
+            "kernel_ms_mean_max_rank": round(kern_ms_max, 5),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "achieved_def": "32 B algorithmic gather per executed ray-step x steps per launch "
+                                         "/ mean march-kernel duration (HIP events on its stream)"},
+        }
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline(r.get_volume(), osd, gsd, march, W, H, args.cpu_budget)
+        print(json.dumps(out), flush=True)
+    sharder.close()
+    r.close()
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

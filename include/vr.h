@@ -1,0 +1,178 @@
+/*
+ * vr.h -- C-ABI of the MI355X-native volumetric ray-march integrator
+ *         (libvr.so, built from volumetricrenderer_amd/csrc/).
+ *
+ * The reference runs its hot path, shaders/frag.glsl, behind the Vulkan
+ * render-pass / descriptor API.  Each entry point below
+ * replaces one piece of that API; the reference interface it replaces is cited
+ * in the comment above it.  Plain C types only: device buffers are passed as
+ * void*, streams as void* (hipStream_t), no torch and no C++ types.
+ *
+ * Errors: every call returns a vr_status.  0 is success.  On failure,
+ * vr_last_error() holds a message for the calling thread.  Exceptions never
+ * cross the ABI.  (The reference instead throws from Error(), Utils.h:22-29.)
+ *
+ * Threading: one vr_ctx per device and host thread.  Calls on one vr_ctx are
+ * not reentrant.  vr_render is asynchronous on the given stream.  It does not
+ * allocate or synchronise, so a caller may capture it in a hipGraph.
+ */
+#ifndef VR_H
+#define VR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VR_ABI_VERSION 1
+
+typedef enum {
+    VR_OK = 0,
+    VR_ERR_INVALID = 1,     /* bad argument (null pointer, bad size or enum) */
+    VR_ERR_HIP = 2,         /* HIP runtime error (see vr_last_error)       */
+    VR_ERR_NO_VOLUME = 3,   /* vr_render before vr_set_volume/generate     */
+    VR_ERR_NO_CAMERA = 4,   /* vr_render before vr_set_shader_data         */
+    VR_ERR_OOM = 5,         /* device allocation failed                    */
+    VR_ERR_NO_DEVICE = 6    /* no HIP device / bad device index            */
+} vr_status;
+
+typedef enum {
+    VR_FMT_RGBA32F = 0,      /* 16 B/pixel, linear                          */
+    VR_FMT_RGBA8_UNORM = 1,  /* 4 B/pixel, linear, round-to-nearest-even    */
+    VR_FMT_RGBA8_SRGB = 2    /* 4 B/pixel, sRGB-encoded on store, as the
+                                reference's swapchain format
+                                (VulkanSwapchain.cpp:181-191)               */
+} vr_format;
+
+/* Replaces the binding-0 UBO `ObjectShaderData` (TestMain.cpp:27-32,
+ * vert.glsl:4-9).  Column-major mat4, as in GLM.  192 bytes.              */
+typedef struct {
+    float model[16];
+    float view[16];
+    float projection[16];
+} vr_object_shader_data;
+
+/* Replaces the binding-1 UBO `GlobalShaderData` (TestMain.cpp:34-39,
+ * frag.glsl:9-14).  The std140 layout is made explicit: the vec3 is padded
+ * to 16 bytes, so media_scroll sits at byte 80.  The reference's C++ struct
+ * put it at byte 76.  144 bytes.                     */
+typedef struct {
+    float world_to_local[16];
+    float camera_position[3];
+    float _pad0;
+    float media_scroll[16];
+} vr_global_shader_data;
+
+/* Constants that the reference hard-codes in frag.glsl.  Fill it with
+ * vr_march_defaults() to get the reference values.                        */
+typedef struct {
+    int32_t max_steps;      /* frag.glsl:30  maxSteps = 128                 */
+    float   step_scale;     /* frag.glsl:42  stepSize = (1/maxSteps) * 4    */
+    float   density;        /* frag.glsl:29  density = 1                    */
+    float   scale;          /* frag.glsl:63  scale = 0.2                    */
+    float   box_min[3];     /* frag.glsl:31  (-1,-1,-1)                     */
+    float   box_max[3];     /* frag.glsl:32  ( 1, 1, 1)                     */
+    float   tap_scale[4];   /* frag.glsl:66-69  Pin * {1, .8, .75, .7}      */
+    float   tap_weight[4];  /* frag.glsl:66-69  MediaScroll * {0,.2,.25,.3} */
+    float   early_out;      /* stop a ray once its transmittance is below this
+                               value.  0 = off, which is the reference.      */
+    int32_t reserved[3];    /* must be 0                                    */
+} vr_march_params;
+
+/* The volume recipe of TestMain.cpp:43-92: four FastNoise2-style grids
+ * (Cellular f=.01 s1, Cellular f=.03 s2, Perlin f=.19 s3, Simplex f=.15 s4),
+ * normalised, inverted, R raised to the 4th power, packed to RGBA8.       */
+typedef struct {
+    int32_t size;               /* N, for an N^3 volume (TestMain.cpp:51: 128) */
+    float   freq[4];            /* TestMain.cpp:59-62                        */
+    int32_t seed[4];
+    int32_t literal_overwrite;  /* 1: replicate TestMain.cpp:60, where the
+                                   f=.03 grid is written into noiseOutput1   */
+} vr_volume_recipe;
+
+/* A render target.  `pixels` is a DEVICE pointer that the caller owns.
+ * With band_rows > 0 only bands b = band_first, band_first + band_stride, ...
+ * are rendered.  Band b covers frame rows [b*band_rows, (b+1)*band_rows).
+ * The bands are written packed and in order, from row 0 of `pixels`.  This
+ * is how the frame is split across GPUs.  band_rows = 0 renders the whole
+ * frame.  step_counter (device u64, may be NULL) has the executed ray-steps
+ * added to it (the sum of n, frag.glsl:46).                                */
+typedef struct {
+    int32_t   width, height;
+    int32_t   format;        /* vr_format */
+    int32_t   band_rows, band_stride, band_first;
+    void*     pixels;
+    size_t    row_pitch;     /* bytes; 0 = tightly packed                  */
+    uint64_t* step_counter;
+} vr_target;
+
+/* ---- context (replaces Renderer::Init/Shutdown, VulkanRenderer.h:68-72) */
+vr_status   vr_create(int device, void** out_ctx);
+vr_status   vr_destroy(void* ctx);
+const char* vr_last_error(void);
+int         vr_abi_version(void);
+
+/* ---- volume: replaces vkc::Texture3D(unsigned char*, VkExtent3D)
+ *      (VulkanTexture.h:55-60, VulkanTexture.cpp:111-156).  RGBA8 UNORM,
+ *      x fastest (the TestMain.cpp:69-73 pack order).  The library copies the
+ *      data into its own device layout.  The host call is synchronous.     */
+vr_status vr_set_volume(void* ctx, const uint8_t* rgba8, int nx, int ny, int nz);
+vr_status vr_set_volume_device(void* ctx, const void* d_rgba8, int nx, int ny, int nz, void* stream);
+/* read the volume back as RGBA8 (host); for tests and tools             */
+vr_status vr_get_volume(void* ctx, uint8_t* rgba8_out);
+vr_status vr_volume_dims(void* ctx, int* nx, int* ny, int* nz);
+
+/* ---- volume generation on the GPU: replaces the host start-up loops of
+ *      TestMain.cpp:43-92.  Synchronous.             */
+vr_status vr_volume_recipe_defaults(vr_volume_recipe* r);
+vr_status vr_generate_volume(void* ctx, const vr_volume_recipe* r, void* stream);
+/* one noise grid, for parity tests: kind 0 cellular, 1 perlin, 2 simplex.
+ * d_out: device float[nx*ny*nz] (may be NULL); min/max to host.           */
+vr_status vr_noise_grid(void* ctx, int kind, void* d_out, int x0, int y0, int z0,
+                        int nx, int ny, int nz, float freq, int32_t seed,
+                        float* out_min, float* out_max, void* stream);
+
+/* ---- uniforms: replaces UniformBuffer<T>::Update x2 (TestMain.cpp:248-249,
+ *      VulkanUniformBuffer.h:58-61).  The data is copied.                  */
+vr_status vr_set_shader_data(void* ctx, const vr_object_shader_data* osd,
+                             const vr_global_shader_data* gsd);
+/* host camera producer of TestMain.cpp:219-245: Model = rotZ(phi)*rotY(theta),
+ * lookAt((3,3,3), 0, +Z), perspective(45deg, aspect, .1, 10) with y flipped,
+ * W2L = inverse(Model), MediaScroll[0][0] = -frame_time.                   */
+vr_status vr_reference_shader_data(float aspect, float phi_deg, float theta_deg,
+                                   float frame_time, vr_object_shader_data* osd,
+                                   vr_global_shader_data* gsd);
+
+/* ---- march constants (frag.glsl:29-32, 42, 63-69) ---------------------- */
+vr_status vr_march_defaults(vr_march_params* m);
+vr_status vr_set_march(void* ctx, const vr_march_params* m);
+
+/* ---- the hot path: replaces EnqueueRenderPass("BasePass") + the draw of
+ *      TestMain.cpp:194-217 + vert.glsl/frag.glsl (VulkanRenderer.h:84-87).
+ *      stream = hipStream_t (NULL = default stream).                       */
+vr_status vr_render(void* ctx, const vr_target* target, void* stream);
+
+/* ---- multi-GPU frame assembly.  The band sets of `nranks` ranks are
+ *      gathered into one device buffer, d_gathered = [rank][packed rows].
+ *      Each rank's set holds `rows_per_rank` rows.  This call scatters them
+ *      into the full frame.  Rank r rendered with band_stride = nranks and
+ *      band_first = r.  The layout matches vr_render's packed output.      */
+vr_status vr_assemble_bands(void* ctx, const void* d_gathered, size_t rows_per_rank,
+                            int nranks, int width, int height, int band_rows,
+                            int bytes_per_pixel, void* d_frame, void* stream);
+/* rows that vr_render writes for a band set (for sizing buffers)          */
+int vr_band_rows_packed(int height, int band_rows, int band_stride, int band_first);
+
+/* ---- introspection: the kernel variant vr_render will launch ----------- */
+/* returns a static string, e.g. "grid_pad16_clamp"                        */
+const char* vr_kernel_variant(void* ctx);
+/* Force a volume layout: 0 = auto, 1 = planar u8 + mirrored repeat,
+ * 2 = padded pairs + clamp.  2 is used only when clamp is exact.          */
+vr_status vr_set_layout_preference(void* ctx, int pref);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VR_H */

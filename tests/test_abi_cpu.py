@@ -1,0 +1,80 @@
+"""C-ABI checks that need no GPU: the library loads, exports exactly what
+include/vr.h declares, and its host-only entry points behave."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "vr.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(vr_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    from volumetricrenderer_amd import _lib
+    lib = _lib.load()
+    declared = header_functions()
+    assert len(declared) >= 20
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert sorted(declared) == _lib.exported_symbols()
+
+
+def test_abi_struct_layouts():
+    from volumetricrenderer_amd import _lib
+    assert ctypes.sizeof(_lib.ObjectShaderData) == 192
+    assert ctypes.sizeof(_lib.GlobalShaderData) == 144
+    assert _lib.GlobalShaderData.media_scroll.offset == 80  # std140
+    assert ctypes.sizeof(_lib.MarchParams) == 88
+    assert ctypes.sizeof(_lib.Target) == 48
+    assert _lib.load().vr_abi_version() == 1
+
+
+def test_no_device_is_a_clean_error():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    import volumetricrenderer_amd as vr
+    with pytest.raises(vr.VRError) as e:
+        vr.Renderer(0)
+    assert e.value.status == 6  # VR_ERR_NO_DEVICE
+
+
+def test_defaults_are_the_reference_constants():
+    import volumetricrenderer_amd as vr
+    m = vr.march_defaults()
+    assert m.max_steps == 128 and m.step_scale == 4.0 and m.density == 1.0  # frag.glsl:29-30,42
+    assert abs(m.scale - 0.2) < 1e-7                                       # :63
+    assert list(m.box_min) == [-1, -1, -1] and list(m.box_max) == [1, 1, 1]  # :31-32
+    np.testing.assert_allclose(list(m.tap_scale), [1, .8, .75, .7], rtol=1e-7)   # :66-69
+    np.testing.assert_allclose(list(m.tap_weight), [0, .2, .25, .3], rtol=1e-7)
+    r = vr.volume_recipe_defaults()
+    assert r.size == 128 and list(r.seed) == [1, 2, 3, 4] and r.literal_overwrite == 1  # TestMain.cpp:51-62
+    np.testing.assert_allclose(list(r.freq), [.01, .03, .19, .15], rtol=1e-7)
+
+
+@pytest.mark.parametrize("aspect,phi,theta,t", [(16 / 9, 0, 0, 0), (1.0, 30, -20, 1.5), (2.0, 123, 45, 0)])
+def test_reference_shader_data_matches_oracle(oracle, aspect, phi, theta, t):
+    import volumetricrenderer_amd as vr
+    osd, gsd = vr.reference_shader_data(aspect, phi, theta, t)
+    obj, glob = vr.shader_data_arrays(osd, gsd)
+    o2, g2 = oracle.reference_shader_data(aspect, phi, theta, t)
+    assert obj.tobytes() == o2.tobytes()
+    assert glob.tobytes() == g2.tobytes()
+
+
+def test_band_rows_packed():
+    import volumetricrenderer_amd as vr
+    from volumetricrenderer_amd.distributed import rows_for_rank
+    for H in (1, 15, 16, 17, 720, 1080, 2160):
+        for n in (1, 2, 3, 8):
+            rows = [vr.band_rows_packed(H, 16, n, k) for k in range(n)]
+            assert rows == [rows_for_rank(H, 16, n, k) for k in range(n)]
+            assert sum(rows) >= H and sum(rows) - H < 16
+    assert vr.band_rows_packed(1080, 0, 1, 0) == 1080

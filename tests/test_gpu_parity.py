@@ -1,0 +1,258 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle.
+
+The bar is bit-exact for fp32 output (both sides execute
+the same fp32 operation sequence with explicit fma only), bit-exact for
+RGBA8 UNORM, and <= 1 LSB for sRGB (powf differs between libm and the device
+library).  Executed step counts must match exactly.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if torch.cuda.is_available():
+    import volumetricrenderer_amd as vr
+    from volumetricrenderer_amd import VRError
+
+
+@pytest.fixture(scope="module")
+def r():
+    with vr.Renderer(0) as rr:
+        yield rr
+
+
+@pytest.fixture(scope="module")
+def vol128(oracle):
+    return oracle.build_volume(128)
+
+
+def render_both(r, oracle, vol, W, H, osd=None, gsd=None, march=None, fmt=0, **band):
+    if osd is None:
+        osd, gsd = vr.reference_shader_data(W / H)
+    march = march if march is not None else vr.march_defaults()
+    r.set_volume(vol)
+    r.set_shader_data(osd, gsd)
+    r.set_march(march)
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    img = r.render(W, H, fmt, step_counter=cnt, **band)
+    torch.cuda.synchronize()
+    obj, glob = vr.shader_data_arrays(osd, gsd)
+    ref, steps = oracle.render(vol, obj, glob, oracle.from_params(march), W, H, fmt, **band)
+    return img.cpu().numpy(), ref, int(cnt.item()), steps
+
+
+def assert_exact(img, ref):
+    assert img.shape == ref.shape
+    bad = np.argwhere(img != ref)
+    assert bad.size == 0, f"{len(bad)} mismatches, first {bad[:5].tolist()}: " \
+                          f"{img[tuple(bad[0])]} vs {ref[tuple(bad[0])]}"
+
+
+def perlin_cube_volume(oracle, n=128):
+    """BASELINE config 1 volume: single-octave Perlin (f=.19, seed 3),
+    normalised and inverted as TestMain.cpp:64-78, in all four channels."""
+    g, mn, mx = oracle.noise_grid(oracle.NOISE_PERLIN, n, n, n, 0.19, 3)
+    inv = np.float32(1.0) / (np.float32(mx) - np.float32(mn))
+    s = (np.float32(1.0) - (g - np.float32(mn)) * inv).astype(np.float32)
+    b = (s * np.float32(255.0)).astype(np.int32).astype(np.uint8)
+    return np.repeat(b[..., None], 4, axis=3)
+
+
+def test_config1_perlin_cube_256_32(r, oracle):
+    vol = perlin_cube_volume(oracle)
+    osd, gsd = vr.reference_shader_data(1.0)
+    img, ref, c, s = render_both(r, oracle, vol, 256, 256, osd, gsd, vr.march_defaults(max_steps=32))
+    assert_exact(img, ref)
+    assert c == s == 225872  # 2.26e5
+    img8, ref8, _, _ = render_both(r, oracle, vol, 256, 256, osd, gsd, vr.march_defaults(max_steps=32),
+                                   fmt=vr.FMT_RGBA8_UNORM)
+    assert_exact(img8, ref8)
+
+
+def test_reference_frame_1080p_128(r, oracle, vol128):
+    img, ref, c, s = render_both(r, oracle, vol128, 1920, 1080)
+    assert r.kernel_variant == "grid_pad16_clamp"
+    assert_exact(img, ref)
+    assert c == s
+    assert 16_700_000 < s < 16_780_000  # 1.674e7 executed steps
+
+
+@pytest.mark.parametrize("phi,theta", [(30.0, 10.0), (45.0, 45.0), (90.0, 0.0), (-120.0, 77.0), (0.0, 180.0)])
+def test_rotated_cube(r, oracle, vol128, phi, theta):
+    osd, gsd = vr.reference_shader_data(16 / 9, phi, theta)
+    img, ref, c, s = render_both(r, oracle, vol128, 320, 180, osd, gsd)
+    assert_exact(img, ref)
+    assert c == s
+
+
+def test_media_scroll_mirrored_repeat(r, oracle, vol128):
+    osd, gsd = vr.reference_shader_data(16 / 9)
+    # per-tap offsets well outside [0,1]: exercises MIRRORED_REPEAT
+    for col, vals in enumerate([(0.0, 3.7, -2.2, 1.3), (0.0, -0.6, 5.1, -7.9), (0.0, 1.9, 0.4, -1.1)]):
+        for row, v in enumerate(vals):
+            gsd.media_scroll[col * 4 + row] = v
+    r.set_volume(vol128)
+    r.set_shader_data(osd, gsd)
+    r.set_march(vr.march_defaults())
+    assert r.kernel_variant == "grid_planar_mirror"
+    img, ref, c, s = render_both(r, oracle, vol128, 320, 180, osd, gsd)
+    assert_exact(img, ref)
+
+
+def test_layouts_agree(r, oracle, vol128):
+    osd, gsd = vr.reference_shader_data(16 / 9, 20.0, -35.0)
+    r.set_volume(vol128)
+    r.set_shader_data(osd, gsd)
+    r.set_march(vr.march_defaults())
+    a = r.render(480, 270, vr.FMT_RGBA32F).cpu().numpy()
+    v1 = r.kernel_variant
+    r.set_layout_preference(1)
+    b = r.render(480, 270, vr.FMT_RGBA32F).cpu().numpy()
+    v2 = r.kernel_variant
+    r.set_layout_preference(0)
+    assert (v1, v2) == ("grid_pad16_clamp", "grid_planar_clamp")
+    assert_exact(a, b)
+
+
+@pytest.mark.parametrize("dims", [(37, 50, 23), (1, 1, 1), (2, 3, 5), (129, 64, 96)])
+def test_odd_volume_dims(r, oracle, dims):
+    rng = np.random.default_rng(sum(dims))
+    nx, ny, nz = dims
+    vol = rng.integers(0, 256, size=(nz, ny, nx, 4), dtype=np.uint8)
+    img, ref, c, s = render_both(r, oracle, vol, 200, 120)
+    assert_exact(img, ref)
+    assert c == s
+
+
+@pytest.mark.parametrize("steps", [1, 7, 100, 256, 300])
+def test_max_steps(r, oracle, vol128, steps):
+    img, ref, c, s = render_both(r, oracle, vol128, 256, 144, march=vr.march_defaults(max_steps=steps))
+    assert_exact(img, ref)
+    assert c == s
+
+
+def test_box_and_constants(r, oracle, vol128):
+    m = vr.march_defaults(box_min=[-1.5, -0.5, -1.0], box_max=[1.0, 0.7, 1.8], density=2.5, scale=0.35,
+                          step_scale=3.0, tap_scale=[0.9, 1.1, 0.5, 1.0])
+    img, ref, c, s = render_both(r, oracle, vol128, 300, 200, march=m)
+    assert_exact(img, ref)
+    assert c == s
+
+
+def test_early_out(r, oracle, vol128):
+    m = vr.march_defaults(density=40.0, early_out=0.05)
+    img, ref, c, s = render_both(r, oracle, vol128, 320, 180, march=m)
+    assert r.kernel_variant.endswith("_early")
+    assert_exact(img, ref)
+    assert c == s
+    m0 = vr.march_defaults(density=40.0)
+    full, _, c0, _ = render_both(r, oracle, vol128, 320, 180, march=m0)
+    assert c < c0                                     # the early-out fired
+    assert np.abs(full - img).max() <= 0.05 + 1e-6    # and cost < eps
+
+
+def test_formats(r, oracle, vol128):
+    img, ref, _, _ = render_both(r, oracle, vol128, 320, 180, fmt=vr.FMT_RGBA8_UNORM)
+    assert img.dtype == np.uint8
+    assert_exact(img, ref)
+    img, ref, _, _ = render_both(r, oracle, vol128, 320, 180, fmt=vr.FMT_RGBA8_SRGB)
+    assert np.abs(img.astype(int) - ref.astype(int)).max() <= 1
+
+
+def test_band_sharding_and_assembly(r, oracle, vol128):
+    W, H, br, n = 320, 200, 16, 3
+    osd, gsd = vr.reference_shader_data(W / H, 15.0, 5.0)
+    r.set_volume(vol128)
+    r.set_shader_data(osd, gsd)
+    r.set_march(vr.march_defaults())
+    full = r.render(W, H, vr.FMT_RGBA32F)
+    rows0 = vr.band_rows_packed(H, br, n, 0)
+    gathered = torch.zeros((n, rows0, W, 4), dtype=torch.float32, device="cuda")
+    total = 0
+    for k in range(n):
+        rows = vr.band_rows_packed(H, br, n, k)
+        r.render(W, H, vr.FMT_RGBA32F, out=gathered[k, :rows], band_rows=br, band_stride=n, band_first=k)
+        obj, glob = vr.shader_data_arrays(osd, gsd)
+        ref, _ = oracle.render(vol128, obj, glob, oracle.march(), W, H, oracle.FMT_RGBA32F, band_rows=br,
+                               band_stride=n, band_first=k)
+        got = gathered[k, :rows].cpu().numpy()
+        valid = [i for i in range(rows) if ((k + (i // br) * n) * br + i % br) < H]
+        assert_exact(got[valid], ref[valid])
+        total += rows
+    frame = r.assemble_bands(gathered, n, W, H, br)
+    torch.cuda.synchronize()
+    assert_exact(frame.cpu().numpy(), full.cpu().numpy())
+
+
+def test_volume_generator_matches_oracle(r, oracle):
+    for literal in (True, False):
+        rec = vr.volume_recipe_defaults(size=48, literal_overwrite=int(literal))
+        r.generate_volume(rec)
+        got = r.get_volume()
+        ref = oracle.build_volume(48, literal=literal)
+        assert_exact(got, ref)
+        if literal:
+            assert (got[..., 1] == got[0, 0, 0, 1]).all()  # G constant (TestMain.cpp:60, :76)
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2])
+def test_noise_grid_matches_oracle(r, oracle, kind):
+    out = torch.empty((20, 24, 28), dtype=torch.float32, device="cuda")
+    _, mn, mx = r.noise_grid(kind, 28, 24, 20, 0.173, 77, origin=(-9, 5, 1000), out=out)
+    ref, rmn, rmx = oracle.noise_grid(kind, 28, 24, 20, 0.173, 77, origin=(-9, 5, 1000))
+    assert_exact(out.cpu().numpy(), ref)
+    assert (mn, mx) == (rmn, rmx)
+
+
+def test_random_cases(r, oracle):
+    rng = np.random.default_rng(1234)
+    for case in range(8):
+        dims = tuple(int(x) for x in rng.integers(8, 80, size=3))
+        vol = rng.integers(0, 256, size=dims[::-1] + (4,), dtype=np.uint8)
+        W, H = int(rng.integers(17, 300)), int(rng.integers(9, 200))
+        osd, gsd = vr.reference_shader_data(float(W) / H, float(rng.uniform(-180, 180)), float(rng.uniform(-90, 90)))
+        m = vr.march_defaults(max_steps=int(rng.integers(1, 200)))
+        img, ref, c, s = render_both(r, oracle, vol, W, H, osd, gsd, m)
+        assert_exact(img, ref)
+        assert c == s, case
+
+
+def test_errors(oracle):
+    with vr.Renderer(0) as rr:
+        with pytest.raises(VRError) as e:
+            rr.render(64, 64)
+        assert e.value.status == 3  # VR_ERR_NO_VOLUME
+        rr.set_volume(np.zeros((4, 4, 4, 4), np.uint8))
+        with pytest.raises(VRError) as e:
+            rr.render(64, 64)
+        assert e.value.status == 4  # VR_ERR_NO_CAMERA
+        osd, gsd = vr.reference_shader_data(1.0)
+        gsd.camera_position[0] = 7.0  # not the View eye
+        with pytest.raises(VRError):
+            rr.set_shader_data(osd, gsd)
+        with pytest.raises(VRError):
+            rr.set_march(vr.march_defaults(max_steps=0))
+        with pytest.raises(ValueError):
+            rr.set_volume(np.zeros((4, 4, 4), np.uint8))
+
+
+def test_config5_grid512_bands(r, oracle):
+    """BASELINE config 5: 512^3 recipe volume (GPU-generated), 1080p x 128.
+    Checked against the oracle on every 24th 16-row band, plus determinism."""
+    r.generate_volume(vr.scaled_recipe(512))
+    vol = r.get_volume()
+    osd, gsd = vr.reference_shader_data(16 / 9)
+    r.set_shader_data(osd, gsd)
+    r.set_march(vr.march_defaults())
+    W, H = 1920, 1080
+    a = r.render(W, H, vr.FMT_RGBA32F).cpu().numpy()
+    b = r.render(W, H, vr.FMT_RGBA32F).cpu().numpy()
+    assert_exact(a, b)
+    obj, glob = vr.shader_data_arrays(osd, gsd)
+    for first in (0, 11, 17):
+        ref, _ = oracle.render(vol, obj, glob, oracle.march(), W, H, oracle.FMT_RGBA32F, band_rows=16,
+                               band_stride=24, band_first=first)
+        rows = [(first + (i // 16) * 24) * 16 + i % 16 for i in range(ref.shape[0])]
+        keep = [i for i, y in enumerate(rows) if y < H]
+        assert_exact(a[[rows[i] for i in keep]], ref[keep])

@@ -1,0 +1,17 @@
+"""volumetricrenderer_amd -- MI355X-native volumetric ray-march integrator.
+
+The hot path of Raspy-Py/VolumetricRenderer (shaders/frag.glsl), re-built as
+hand-written HIP kernels for gfx950 behind a C ABI (include/vr.h, libvr.so).
+This package is the Python host side: ctypes bindings (_lib), the renderer
+interface (renderer) and the multi-GPU band sharding (distributed).
+"""
+from ._lib import (FMT_RGBA8_SRGB, FMT_RGBA8_UNORM, FMT_RGBA32F, GlobalShaderData, MarchParams,  # noqa: F401
+                   ObjectShaderData, Target, VolumeRecipe, VRError)
+from .renderer import (Renderer, band_rows_packed, march_defaults, reference_shader_data,  # noqa: F401
+                       scaled_recipe, shader_data_arrays, volume_recipe_defaults)
+
+__all__ = [
+    "Renderer", "VRError", "march_defaults", "reference_shader_data", "volume_recipe_defaults",
+    "scaled_recipe", "band_rows_packed", "shader_data_arrays", "FMT_RGBA32F", "FMT_RGBA8_UNORM",
+    "FMT_RGBA8_SRGB", "ObjectShaderData", "GlobalShaderData", "MarchParams", "VolumeRecipe", "Target",
+]

@@ -1,0 +1,503 @@
+// vr_api.cpp -- implementation of the C ABI declared in include/vr.h.
+//
+// Owns the device copy of the volume (replaces vkc::Texture3D,
+// VulkanTexture.cpp:111-156) and the per-frame uniforms (replaces
+// UniformBuffer<T>, VulkanUniformBuffer.h:37-61).  It turns them into one
+// MarchArgs block per vr_render and launches the HIP march kernel.  That last
+// step replaces the EnqueueRenderPass + vkCmdDrawIndexed path of
+// TestMain.cpp:194-217.  No exception crosses the ABI; errors go through
+// vr_last_error().
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "../../include/vr.h"
+#include "vr_internal.h"
+
+using namespace vr;
+
+namespace {
+
+thread_local std::string g_err;
+
+vr_status fail(vr_status st, const char* fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    std::vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return st;
+}
+
+#define HIP_TRY(expr)                                                                        \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess)                                                                \
+            return fail(e_ == hipErrorOutOfMemory ? VR_ERR_OOM : VR_ERR_HIP, "%s: %s (%s:%d)", \
+                        #expr, hipGetErrorString(e_), __FILE__, __LINE__);                   \
+    } while (0)
+
+struct Ctx {
+    int device = 0;
+    // volume (channel planes; see vr_internal.h Layout)
+    int nx = 0, ny = 0, nz = 0;
+    uint8_t* d_planar = nullptr;
+    uint8_t* d_pad16 = nullptr;
+    // uniforms
+    bool has_camera = false;
+    float obj[48];
+    float glob[36];
+    vr_march_params march;
+    int layout_pref = 0;
+};
+
+Ctx* as_ctx(void* p) { return static_cast<Ctx*>(p); }
+
+void free_volume(Ctx* c)
+{
+    if (c->d_planar) (void)hipFree(c->d_planar);
+    if (c->d_pad16) (void)hipFree(c->d_pad16);
+    c->d_planar = c->d_pad16 = nullptr;
+    c->nx = c->ny = c->nz = 0;
+}
+
+bool dims_ok(int nx, int ny, int nz)
+{
+    if (nx <= 0 || ny <= 0 || nz <= 0) return false;
+    const long long pt = (long long)(nx + 2) * (ny + 2) * (nz + 2);
+    return pt < (1ll << 31);  // kernels index a plane with 32-bit ints
+}
+
+// Allocate the planes and repack from a device RGBA8 buffer.
+vr_status install_volume(Ctx* c, const uint8_t* d_rgba, int nx, int ny, int nz, hipStream_t s)
+{
+    free_volume(c);
+    const size_t total = (size_t)nx * ny * nz;
+    const size_t ptotal = (size_t)(nx + 2) * (ny + 2) * (nz + 2);
+    HIP_TRY(hipMalloc(&c->d_planar, 4 * total));
+    HIP_TRY(hipMalloc(&c->d_pad16, 4 * ptotal + 16));
+    HIP_TRY(launch_repack(d_rgba, nx, ny, nz, c->d_planar, c->d_pad16, s));
+    c->nx = nx; c->ny = ny; c->nz = nz;
+    return VR_OK;
+}
+
+// Is clamp-to-edge identical to mirrored repeat for every tap of every ray?
+// Both agree while each tap's base texel floor(u*N - .5) stays in [-1, N-1],
+// i.e. u in [-.5/N, 1 + .5/N).  Ray points P lie in [0,1]^3 (box entry/exit
+// normalised, frag.glsl:49-54) up to rounding drift bounded by `slack`.
+bool clamp_is_exact(const Ctx* c, const float tap_off[4][3])
+{
+    const vr_march_params& m = c->march;
+    const double slack = (double)(m.max_steps + 16) * 1.2e-7;
+    const int dims[3] = {c->nx, c->ny, c->nz};
+    for (int t = 0; t < 4; ++t) {
+        const double s = m.tap_scale[t];
+        for (int a = 0; a < 3; ++a) {
+            const double o = tap_off[t][a];
+            const double lo = std::fmin(o, s + o) - std::fabs(s) * slack - 1e-6;
+            const double hi = std::fmax(o, s + o) + std::fabs(s) * slack + 1e-6;
+            const double h = 0.5 / dims[a];
+            if (!(lo >= -h && hi < 1.0 + h)) return false;
+        }
+    }
+    return true;
+}
+
+int band_rows_packed(int height, int band_rows, int band_stride, int band_first)
+{
+    if (band_rows <= 0) return height;
+    if (band_stride <= 0) band_stride = 1;
+    const int nb = (height + band_rows - 1) / band_rows;
+    if (band_first < 0 || band_first >= nb) return 0;
+    const int nsel = (nb - 1 - band_first) / band_stride + 1;
+    return nsel * band_rows;
+}
+
+struct Plan {
+    int layout, wrap;
+    bool early;
+};
+
+vr_status make_plan(Ctx* c, MarchArgs* a, Plan* p)
+{
+    const vr_march_params& m = c->march;
+    const float* ms = c->glob + 20;  // MediaScroll, column-major; tap t reads row t
+    for (int t = 0; t < 4; ++t)
+        for (int ax = 0; ax < 3; ++ax) a->tap_off[t][ax] = ms[ax * 4 + t] * m.tap_weight[t];
+    const bool exact = clamp_is_exact(c, a->tap_off);
+    if (c->layout_pref == 1) {
+        p->layout = LAYOUT_PLANAR;
+        p->wrap = exact ? WRAP_CLAMP : WRAP_MIRROR;
+    } else if (exact) {
+        p->layout = LAYOUT_PAD16;
+        p->wrap = WRAP_CLAMP;
+    } else {
+        p->layout = LAYOUT_PLANAR;
+        p->wrap = WRAP_MIRROR;
+    }
+    p->early = m.early_out > 0.0f;
+    return VR_OK;
+}
+
+const char* variant_name(const Plan& p)
+{
+    if (p.layout == LAYOUT_PAD16) return p.early ? "grid_pad16_clamp_early" : "grid_pad16_clamp";
+    if (p.wrap == WRAP_CLAMP) return p.early ? "grid_planar_clamp_early" : "grid_planar_clamp";
+    return p.early ? "grid_planar_mirror_early" : "grid_planar_mirror";
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* vr_last_error(void) { return g_err.c_str(); }
+int vr_abi_version(void) { return VR_ABI_VERSION; }
+
+vr_status vr_march_defaults(vr_march_params* m)
+{
+    if (!m) return fail(VR_ERR_INVALID, "vr_march_defaults: null");
+    std::memset(m, 0, sizeof *m);
+    m->max_steps = 128;        // frag.glsl:30
+    m->step_scale = 4.0f;      // :42
+    m->density = 1.0f;         // :29
+    m->scale = 0.2f;           // :63
+    for (int a = 0; a < 3; ++a) { m->box_min[a] = -1.0f; m->box_max[a] = 1.0f; }  // :31-32
+    const float ts[4] = {1.0f, 0.8f, 0.75f, 0.7f}, tw[4] = {0.0f, 0.2f, 0.25f, 0.3f};  // :66-69
+    for (int t = 0; t < 4; ++t) { m->tap_scale[t] = ts[t]; m->tap_weight[t] = tw[t]; }
+    m->early_out = 0.0f;
+    return VR_OK;
+}
+
+vr_status vr_volume_recipe_defaults(vr_volume_recipe* r)
+{
+    if (!r) return fail(VR_ERR_INVALID, "vr_volume_recipe_defaults: null");
+    r->size = 128;  // TestMain.cpp:51
+    const float f[4] = {0.01f, 0.03f, 0.19f, 0.15f};  // :59-62
+    for (int k = 0; k < 4; ++k) { r->freq[k] = f[k]; r->seed[k] = k + 1; }
+    r->literal_overwrite = 1;
+    return VR_OK;
+}
+
+vr_status vr_create(int device, void** out)
+{
+    if (!out) return fail(VR_ERR_INVALID, "vr_create: out is null");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(VR_ERR_NO_DEVICE, "vr_create: no HIP device");
+    if (device < 0 || device >= n) return fail(VR_ERR_NO_DEVICE, "vr_create: device %d of %d", device, n);
+    HIP_TRY(hipSetDevice(device));
+    Ctx* c = new (std::nothrow) Ctx();
+    if (!c) return fail(VR_ERR_OOM, "vr_create: host allocation failed");
+    c->device = device;
+    vr_march_defaults(&c->march);
+    *out = c;
+    return VR_OK;
+}
+
+vr_status vr_destroy(void* p)
+{
+    if (!p) return VR_OK;
+    Ctx* c = as_ctx(p);
+    (void)hipSetDevice(c->device);
+    free_volume(c);
+    delete c;
+    return VR_OK;
+}
+
+vr_status vr_set_volume(void* p, const uint8_t* rgba8, int nx, int ny, int nz)
+{
+    if (!p || !rgba8) return fail(VR_ERR_INVALID, "vr_set_volume: null argument");  // VulkanTexture.cpp:121-124
+    if (!dims_ok(nx, ny, nz)) return fail(VR_ERR_INVALID, "vr_set_volume: bad extent %dx%dx%d", nx, ny, nz);
+    Ctx* c = as_ctx(p);
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t bytes = (size_t)nx * ny * nz * 4;
+    uint8_t* staging = nullptr;
+    HIP_TRY(hipMalloc(&staging, bytes));
+    hipError_t e = hipMemcpy(staging, rgba8, bytes, hipMemcpyHostToDevice);
+    vr_status st = VR_OK;
+    if (e == hipSuccess) st = install_volume(c, staging, nx, ny, nz, nullptr);
+    if (e == hipSuccess && st == VR_OK) e = hipDeviceSynchronize();
+    (void)hipFree(staging);
+    if (st != VR_OK) return st;
+    if (e != hipSuccess) return fail(VR_ERR_HIP, "vr_set_volume: %s", hipGetErrorString(e));
+    return VR_OK;
+}
+
+vr_status vr_set_volume_device(void* p, const void* d_rgba8, int nx, int ny, int nz, void* stream)
+{
+    if (!p || !d_rgba8) return fail(VR_ERR_INVALID, "vr_set_volume_device: null argument");
+    if (!dims_ok(nx, ny, nz)) return fail(VR_ERR_INVALID, "vr_set_volume_device: bad extent %dx%dx%d", nx, ny, nz);
+    Ctx* c = as_ctx(p);
+    HIP_TRY(hipSetDevice(c->device));
+    return install_volume(c, static_cast<const uint8_t*>(d_rgba8), nx, ny, nz, static_cast<hipStream_t>(stream));
+}
+
+vr_status vr_volume_dims(void* p, int* nx, int* ny, int* nz)
+{
+    if (!p || !nx || !ny || !nz) return fail(VR_ERR_INVALID, "vr_volume_dims: null argument");
+    Ctx* c = as_ctx(p);
+    *nx = c->nx; *ny = c->ny; *nz = c->nz;
+    return VR_OK;
+}
+
+vr_status vr_get_volume(void* p, uint8_t* out)
+{
+    if (!p || !out) return fail(VR_ERR_INVALID, "vr_get_volume: null argument");
+    Ctx* c = as_ctx(p);
+    if (!c->d_planar) return fail(VR_ERR_NO_VOLUME, "vr_get_volume: no volume set");
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t bytes = (size_t)c->nx * c->ny * c->nz * 4;
+    uint8_t* staging = nullptr;
+    HIP_TRY(hipMalloc(&staging, bytes));
+    hipError_t e = launch_unpack(c->d_planar, c->nx, c->ny, c->nz, staging, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(out, staging, bytes, hipMemcpyDeviceToHost);
+    (void)hipFree(staging);
+    if (e != hipSuccess) return fail(VR_ERR_HIP, "vr_get_volume: %s", hipGetErrorString(e));
+    return VR_OK;
+}
+
+vr_status vr_noise_grid(void* p, int kind, void* d_out, int x0, int y0, int z0, int nx, int ny, int nz,
+                        float freq, int32_t seed, float* out_min, float* out_max, void* stream)
+{
+    if (!p) return fail(VR_ERR_INVALID, "vr_noise_grid: null ctx");
+    if (kind < 0 || kind > 2) return fail(VR_ERR_INVALID, "vr_noise_grid: kind %d", kind);
+    if (nx <= 0 || ny <= 0 || nz <= 0) return fail(VR_ERR_INVALID, "vr_noise_grid: bad extent");
+    Ctx* c = as_ctx(p);
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int np = noise_partials_needed(nx, ny, nz);
+    float* part = nullptr;
+    float* mm = nullptr;
+    HIP_TRY(hipMalloc(&part, (size_t)np * 2 * sizeof(float)));
+    hipError_t e = hipMalloc(&mm, 2 * sizeof(float));
+    int used = 0;
+    if (e == hipSuccess) e = launch_noise(kind, static_cast<float*>(d_out), x0, y0, z0, nx, ny, nz, freq, seed, part, &used, s);
+    if (e == hipSuccess) e = launch_minmax_reduce(part, used, mm, s);
+    float h[2] = {0.f, 0.f};
+    if (e == hipSuccess) e = hipMemcpyAsync(h, mm, sizeof h, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    (void)hipFree(part);
+    if (mm) (void)hipFree(mm);
+    if (e != hipSuccess) return fail(VR_ERR_HIP, "vr_noise_grid: %s", hipGetErrorString(e));
+    if (out_min) *out_min = h[0];
+    if (out_max) *out_max = h[1];
+    return VR_OK;
+}
+
+vr_status vr_generate_volume(void* p, const vr_volume_recipe* r, void* stream)
+{
+    if (!p || !r) return fail(VR_ERR_INVALID, "vr_generate_volume: null argument");
+    const int N = r->size;
+    if (!dims_ok(N, N, N)) return fail(VR_ERR_INVALID, "vr_generate_volume: bad size %d", N);
+    Ctx* c = as_ctx(p);
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const size_t total = (size_t)N * N * N;
+    const int np = noise_partials_needed(N, N, N);
+    float *g1 = nullptr, *g2 = nullptr, *g3 = nullptr, *g4 = nullptr, *part = nullptr, *mm = nullptr;
+    uint8_t* rgba = nullptr;
+    hipError_t e = hipSuccess;
+    auto alloc = [&](void** ptr, size_t bytes) { if (e == hipSuccess) e = hipMalloc(ptr, bytes); };
+    alloc((void**)&g1, total * sizeof(float));
+    if (!r->literal_overwrite) alloc((void**)&g2, total * sizeof(float));
+    alloc((void**)&g3, total * sizeof(float));
+    alloc((void**)&g4, total * sizeof(float));
+    alloc((void**)&part, (size_t)np * 2 * sizeof(float));
+    alloc((void**)&mm, 8 * sizeof(float));
+    alloc((void**)&rgba, total * 4);
+    int used = 0;
+    // TestMain.cpp:59-62.  Literal recipe: run 1's values are overwritten by
+    // run 2 (both target noiseOutput1), so run 1 only yields its min/max.
+    float* outs[4] = {r->literal_overwrite ? nullptr : g1, r->literal_overwrite ? g1 : g2, g3, g4};
+    const int kinds[4] = {0, 0, 1, 2};
+    for (int k = 0; k < 4 && e == hipSuccess; ++k) {
+        e = launch_noise(kinds[k], outs[k], 0, 0, 0, N, N, N, r->freq[k], r->seed[k], part, &used, s);
+        if (e == hipSuccess) e = launch_minmax_reduce(part, used, mm + 2 * k, s);
+    }
+    if (e == hipSuccess) e = launch_pack_recipe(g1, g2, g3, g4, mm, (long long)total, rgba, s);
+    vr_status st = VR_OK;
+    if (e == hipSuccess) st = install_volume(c, rgba, N, N, N, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    for (void* q : {(void*)g1, (void*)g2, (void*)g3, (void*)g4, (void*)part, (void*)mm, (void*)rgba})
+        if (q) (void)hipFree(q);
+    if (st != VR_OK) return st;
+    if (e != hipSuccess) {
+        free_volume(c);
+        return fail(e == hipErrorOutOfMemory ? VR_ERR_OOM : VR_ERR_HIP, "vr_generate_volume: %s", hipGetErrorString(e));
+    }
+    return VR_OK;
+}
+
+vr_status vr_set_shader_data(void* p, const vr_object_shader_data* osd, const vr_global_shader_data* gsd)
+{
+    if (!p || !osd || !gsd) return fail(VR_ERR_INVALID, "vr_set_shader_data: null argument");
+    Ctx* c = as_ctx(p);
+    // The fragment ray runs from CameraPosition through the rasterised point
+    // of the View eye's pixel ray (frag.glsl:36-38, vert.glsl:20).  Both agree
+    // only if CameraPosition is the View eye, as at TestMain.cpp:225 / :242.
+    {
+        double V[16], Vi[16];
+        for (int i = 0; i < 16; ++i) V[i] = osd->view[i];
+        if (!vr::invert4_d(V, Vi)) return fail(VR_ERR_INVALID, "vr_set_shader_data: View is singular");
+        double err = 0.0, mag = 1.0;
+        for (int i = 0; i < 3; ++i) {
+            const double e = Vi[12 + i] / Vi[15];   // eye = inverse(View) * (0,0,0,1)
+            err = std::fmax(err, std::fabs(e - (double)gsd->camera_position[i]));
+            mag = std::fmax(mag, std::fabs(e));
+        }
+        if (!(err <= 1e-4 * mag))
+            return fail(VR_ERR_INVALID, "vr_set_shader_data: CameraPosition differs from the View eye by %g", err);
+    }
+    std::memcpy(c->obj, osd, sizeof(float) * 48);
+    std::memcpy(c->glob, gsd, sizeof(float) * 36);
+    RayBasis b;
+    if (!make_ray_basis(c->obj, c->glob, 16, 16, &b)) {
+        c->has_camera = false;
+        return fail(VR_ERR_INVALID, "vr_set_shader_data: Projection*View is singular");
+    }
+    c->has_camera = true;
+    return VR_OK;
+}
+
+vr_status vr_reference_shader_data(float aspect, float phi_deg, float theta_deg, float frame_time,
+                                   vr_object_shader_data* osd, vr_global_shader_data* gsd)
+{
+    if (!osd || !gsd) return fail(VR_ERR_INVALID, "vr_reference_shader_data: null argument");
+    if (!(aspect > 0.0f)) return fail(VR_ERR_INVALID, "vr_reference_shader_data: aspect must be > 0");
+    reference_shader_data(aspect, phi_deg, theta_deg, frame_time, reinterpret_cast<float*>(osd),
+                          reinterpret_cast<float*>(gsd));
+    return VR_OK;
+}
+
+vr_status vr_set_march(void* p, const vr_march_params* m)
+{
+    if (!p || !m) return fail(VR_ERR_INVALID, "vr_set_march: null argument");
+    if (m->max_steps <= 0) return fail(VR_ERR_INVALID, "vr_set_march: max_steps must be > 0");
+    if (!(m->step_scale > 0.0f) || !std::isfinite(m->step_scale))
+        return fail(VR_ERR_INVALID, "vr_set_march: step_scale must be finite and > 0");
+    if (!(m->early_out >= 0.0f && m->early_out < 1.0f)) return fail(VR_ERR_INVALID, "vr_set_march: early_out in [0,1)");
+    if (m->early_out > 0.0f && !(m->density > 0.0f))
+        return fail(VR_ERR_INVALID, "vr_set_march: early_out needs density > 0");
+    for (int a = 0; a < 3; ++a)
+        if (!(m->box_max[a] != m->box_min[a])) return fail(VR_ERR_INVALID, "vr_set_march: empty box on axis %d", a);
+    if (m->reserved[0] || m->reserved[1] || m->reserved[2]) return fail(VR_ERR_INVALID, "vr_set_march: reserved must be 0");
+    as_ctx(p)->march = *m;
+    return VR_OK;
+}
+
+int vr_band_rows_packed(int height, int band_rows, int band_stride, int band_first)
+{
+    return band_rows_packed(height, band_rows, band_stride, band_first);
+}
+
+vr_status vr_set_layout_preference(void* p, int pref)
+{
+    if (!p || pref < 0 || pref > 2) return fail(VR_ERR_INVALID, "vr_set_layout_preference: bad argument");
+    as_ctx(p)->layout_pref = pref;
+    return VR_OK;
+}
+
+const char* vr_kernel_variant(void* p)
+{
+    if (!p) return "none";
+    Ctx* c = as_ctx(p);
+    if (!c->d_planar || !c->has_camera) return "none";
+    MarchArgs a{};
+    Plan pl{};
+    make_plan(c, &a, &pl);
+    return variant_name(pl);
+}
+
+vr_status vr_render(void* p, const vr_target* t, void* stream)
+{
+    if (!p || !t) return fail(VR_ERR_INVALID, "vr_render: null argument");
+    Ctx* c = as_ctx(p);
+    if (!c->d_planar) return fail(VR_ERR_NO_VOLUME, "vr_render: no volume (vr_set_volume / vr_generate_volume)");
+    if (!c->has_camera) return fail(VR_ERR_NO_CAMERA, "vr_render: no shader data (vr_set_shader_data)");
+    if (t->width <= 0 || t->height <= 0) return fail(VR_ERR_INVALID, "vr_render: bad size %dx%d", t->width, t->height);
+    if (t->format < 0 || t->format > 2) return fail(VR_ERR_INVALID, "vr_render: bad format %d", t->format);
+    if (!t->pixels) return fail(VR_ERR_INVALID, "vr_render: pixels is null");
+    const int bpp = t->format == VR_FMT_RGBA32F ? 16 : 4;
+    const size_t pitch = t->row_pitch ? t->row_pitch : (size_t)t->width * bpp;
+    if (pitch < (size_t)t->width * bpp || pitch % bpp != 0 || ((uintptr_t)t->pixels % bpp) != 0)
+        return fail(VR_ERR_INVALID, "vr_render: pitch/alignment (pitch %zu, bpp %d)", pitch, bpp);
+    if (t->band_rows < 0 || (t->band_rows > 0 && (t->band_stride <= 0 || t->band_first < 0)))
+        return fail(VR_ERR_INVALID, "vr_render: bad band selection");
+
+    MarchArgs a{};
+    RayBasis b;
+    if (!make_ray_basis(c->obj, c->glob, t->width, t->height, &b))
+        return fail(VR_ERR_INVALID, "vr_render: Projection*View is singular");
+    std::memcpy(a.org, b.org, sizeof a.org); std::memcpy(a.o, b.o, sizeof a.o);
+    std::memcpy(a.px, b.px, sizeof a.px); std::memcpy(a.py, b.py, sizeof a.py);
+    std::memcpy(a.r2, b.r2, sizeof a.r2); std::memcpy(a.r3, b.r3, sizeof a.r3);
+    const vr_march_params& m = c->march;
+    a.step_size = (1.0f / (float)m.max_steps) * m.step_scale;   // frag.glsl:42
+    for (int ax = 0; ax < 3; ++ax) {
+        a.box_min[ax] = m.box_min[ax];
+        a.box_max[ax] = m.box_max[ax];
+        a.box_range[ax] = std::fabs(m.box_max[ax] - m.box_min[ax]);   // :51
+    }
+    a.density = m.density;
+    a.scale = m.scale;
+    a.max_steps = m.max_steps;
+    a.acc_limit = m.early_out > 0.0f
+                      ? (float)(-std::log((double)m.early_out) / ((double)m.density * (double)a.step_size))
+                      : INFINITY;
+    for (int k = 0; k < 4; ++k) a.tap_scale[k] = m.tap_scale[k];
+    Plan pl{};
+    make_plan(c, &a, &pl);
+    a.nx = c->nx; a.ny = c->ny; a.nz = c->nz;
+    a.fnx = (float)c->nx; a.fny = (float)c->ny; a.fnz = (float)c->nz;
+    if (pl.layout == LAYOUT_PAD16) {
+        a.vol = c->d_pad16;
+        a.prow = c->nx + 2;
+        a.pslice = (c->nx + 2) * (c->ny + 2);
+        a.plane_stride = (long long)a.pslice * (c->nz + 2);
+    } else {
+        a.vol = c->d_planar;
+        a.plane_stride = (long long)c->nx * c->ny * c->nz;
+    }
+    a.width = t->width;
+    a.height = t->height;
+    if (t->band_rows > 0) {
+        a.band_rows = t->band_rows; a.band_stride = t->band_stride; a.band_first = t->band_first;
+    } else {
+        a.band_rows = t->height; a.band_stride = 1; a.band_first = 0;
+    }
+    a.out_rows = band_rows_packed(t->height, a.band_rows, a.band_stride, a.band_first);
+    a.tiles_x = (t->width + 15) / 16;
+    a.tiles_y = (a.out_rows + 15) / 16;
+    a.num_tiles = a.tiles_x * a.tiles_y;
+    a.out = t->pixels;
+    a.pitch = (long long)pitch;
+    a.format = t->format;
+    a.step_counter = reinterpret_cast<unsigned long long*>(t->step_counter);
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(launch_march(a, pl.layout, pl.wrap, pl.early, static_cast<hipStream_t>(stream)));
+    return VR_OK;
+}
+
+vr_status vr_assemble_bands(void* p, const void* d_gathered, size_t rows_per_rank, int nranks, int width,
+                            int height, int band_rows, int bytes_per_pixel, void* d_frame, void* stream)
+{
+    if (!p || !d_gathered || !d_frame) return fail(VR_ERR_INVALID, "vr_assemble_bands: null argument");
+    if (nranks <= 0 || width <= 0 || height <= 0 || band_rows <= 0 || (bytes_per_pixel != 4 && bytes_per_pixel != 16))
+        return fail(VR_ERR_INVALID, "vr_assemble_bands: bad geometry");
+    for (int r = 0; r < nranks; ++r)
+        if ((size_t)band_rows_packed(height, band_rows, nranks, r) > rows_per_rank)
+            return fail(VR_ERR_INVALID, "vr_assemble_bands: rows_per_rank %zu too small for rank %d", rows_per_rank, r);
+    Ctx* c = as_ctx(p);
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(launch_assemble(static_cast<const uint8_t*>(d_gathered), rows_per_rank, nranks, width, height,
+                            band_rows, bytes_per_pixel, static_cast<uint8_t*>(d_frame),
+                            static_cast<hipStream_t>(stream)));
+    return VR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,76 @@
+// vr_internal.h -- internal structures shared by the HIP kernels and the C ABI
+// (not installed; the public interface is include/vr.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+namespace vr {
+
+// Volume layouts in HBM.  Both keep one byte plane per
+// channel, so a tap reads only the channel it needs (frag.glsl:66-69 read
+// .x, .y, .z and .w from four different coordinates).
+enum Layout : int {
+    LAYOUT_PLANAR = 1,   // plane[c][z][y][x], u8.  Any wrap.  8 byte loads per tap.
+    LAYOUT_PAD16 = 2,    // plane[c][z+1][y+1][x+1] with a 1-texel clamp apron.
+                         // A tap does 4 u16 loads (x-pairs) and needs no
+                         // index clamping.  Exact only where clamp == mirror.
+};
+
+enum Wrap : int { WRAP_CLAMP = 0, WRAP_MIRROR = 1 };
+
+// Everything one launch of the march kernel needs.  Passed by value
+// (kernarg segment), computed on the host per vr_render call.
+struct MarchArgs {
+    // ray basis in box-local space: dir(x,y) = o + (x+.5)*px + (y+.5)*py
+    float org[3], o[3], px[3], py[3];
+    float r2[4], r3[4];          // rows 2/3 of P*V*M (coverage clip test)
+    float box_min[3], box_max[3], box_range[3];
+    float step_size, density, scale, acc_limit;
+    int max_steps;
+    float tap_scale[4];
+    float tap_off[4][3];
+    // volume
+    int nx, ny, nz;
+    float fnx, fny, fnz;
+    const uint8_t* vol;          // channel plane 0; plane c at vol + c*plane_stride
+    long long plane_stride;
+    int prow, pslice;            // PAD16: (nx+2), (nx+2)*(ny+2)
+    // target
+    int width, height, band_rows, band_stride, band_first, out_rows;
+    int tiles_x, tiles_y, num_tiles;
+    void* out;
+    long long pitch;
+    int format;
+    unsigned long long* step_counter;
+};
+
+// launchers (vr_march.hip / vr_volume.hip); return hipError_t
+hipError_t launch_march(const MarchArgs& a, int layout, int wrap, bool early, hipStream_t s);
+hipError_t launch_repack(const uint8_t* d_rgba, int nx, int ny, int nz, uint8_t* d_planar,
+                         uint8_t* d_pad16, hipStream_t s);
+hipError_t launch_unpack(const uint8_t* d_planar, int nx, int ny, int nz, uint8_t* d_rgba,
+                         hipStream_t s);
+hipError_t launch_noise(int kind, float* d_out, int x0, int y0, int z0, int nx, int ny, int nz,
+                        float freq, int32_t seed, float* d_partials, int* num_partials,
+                        hipStream_t s);
+hipError_t launch_minmax_reduce(const float* d_partials, int num_partials, float* d_minmax,
+                                hipStream_t s);
+hipError_t launch_pack_recipe(const float* d_g1, const float* d_g2, const float* d_g3,
+                              const float* d_g4, const float* d_minmax, long long total,
+                              uint8_t* d_rgba, hipStream_t s);
+hipError_t launch_assemble(const uint8_t* d_gathered, size_t rows_per_rank, int nranks,
+                           int width, int height, int band_rows, int bpp, uint8_t* d_frame,
+                           hipStream_t s);
+int noise_partials_needed(int nx, int ny, int nz);
+
+// host camera math (vr_camera.cpp)
+struct RayBasis {
+    float org[3], o[3], px[3], py[3], r2[4], r3[4];
+};
+bool invert4_d(const double* m, double* inv);
+bool make_ray_basis(const float* obj48, const float* glob36, int width, int height, RayBasis* b);
+void reference_shader_data(float aspect, float phi_deg, float theta_deg, float frame_time,
+                           float* obj48, float* glob36);
+
+}  // namespace vr

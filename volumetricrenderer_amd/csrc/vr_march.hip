@@ -1,0 +1,239 @@
+// vr_march.hip -- the hot path: per-pixel volumetric ray march for gfx950.
+//
+// Replaces shaders/frag.glsl:34-81 (and the coverage that vert.glsl:17-22
+// plus rasterisation provide).  Each lane traces one ray; a wave64 owns an
+// 8x8 pixel tile; a 256-thread workgroup owns a 16x16 tile.  There is no LDS
+// and no barrier: neighbouring rays share the volume through L1/L2.  Work is
+// ALU/gather-bound, so nothing here uses MFMA.
+//
+// The op sequence is the fp32 spec of DESIGN.md sec. 3.  The oracle
+// (oracle/vr_oracle.c) restates the same spec, and results agree bit for bit.
+// Build with -ffp-contract=off: the only fused ops are the explicit fmaf().
+#include "vr_internal.h"
+
+namespace vr {
+namespace {
+
+constexpr int kTile = 16;           // workgroup tile edge, pixels
+constexpr int kThreads = 256;       // 4 waves, each an 8x8 sub-tile
+
+__device__ __forceinline__ float lerp_(float a, float b, float t) { return fmaf(t, b - a, a); }
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return min(max(v, lo), hi); }
+
+// VK_SAMPLER_ADDRESS_MODE_MIRRORED_REPEAT on an integer texel index
+// (VulkanCore.cpp:683-685; Vulkan spec "Texel coordinate wrapping").
+__device__ __forceinline__ int mirror_(int i, int n)
+{
+    int two = n + n;
+    int m = i % two;
+    m = m < 0 ? m + two : m;
+    return m < n ? m : two - 1 - m;
+}
+
+// exp(x) for x <= 0, the fma-only polynomial of the spec.
+__device__ __forceinline__ float spec_expf(float x)
+{
+    if (x < -80.0f) return 0.0f;
+    float k = rintf(x * 1.44269504088896341f);
+    float r = fmaf(k, -0.693359375f, x);
+    r = fmaf(k, 2.12194440e-4f, r);
+    float p = 1.9875691500e-4f;
+    p = fmaf(p, r, 1.3981999507e-3f);
+    p = fmaf(p, r, 8.3334519073e-3f);
+    p = fmaf(p, r, 4.1665795894e-2f);
+    p = fmaf(p, r, 1.6666665459e-1f);
+    p = fmaf(p, r, 5.0000001201e-1f);
+    p = fmaf(p, r * r, r);
+    p = p + 1.0f;
+    return p * __int_as_float(((int)k + 127) << 23);
+}
+
+// One trilinear tap of one channel plane: Vulkan LINEAR filter, LOD 0.
+// texel space u*N - 0.5, floor / frac, then 8 texels and 7 lerps.
+template <int LAYOUT, int WRAP>
+__device__ __forceinline__ float tap(const uint8_t* __restrict__ pl, const MarchArgs& a,
+                                     float qx, float qy, float qz)
+{
+    const float gx = fmaf(qx, a.fnx, -0.5f), gy = fmaf(qy, a.fny, -0.5f), gz = fmaf(qz, a.fnz, -0.5f);
+    const float fx = floorf(gx), fy = floorf(gy), fz = floorf(gz);
+    const float ax = gx - fx, ay = gy - fy, az = gz - fz;
+    const int ix = (int)fx, iy = (int)fy, iz = (int)fz;
+    float c000, c100, c010, c110, c001, c101, c011, c111;
+    if constexpr (LAYOUT == LAYOUT_PAD16) {
+        // padded index = texel index + 1; the apron holds the clamped edge,
+        // so (a0, a0+1) is always the clamp-to-edge pair, read as one u16.
+        const int a0 = clampi(ix + 1, 0, a.nx);
+        const int b0 = clampi(iy + 1, 0, a.ny);
+        const int c0 = clampi(iz + 1, 0, a.nz);
+        const uint8_t* p = pl + ((c0 * a.pslice) + b0 * a.prow + a0);
+        uint16_t v00, v10, v01, v11;
+        __builtin_memcpy(&v00, p, 2);
+        __builtin_memcpy(&v10, p + a.prow, 2);
+        __builtin_memcpy(&v01, p + a.pslice, 2);
+        __builtin_memcpy(&v11, p + a.pslice + a.prow, 2);
+        c000 = (float)(v00 & 0xffu); c100 = (float)(v00 >> 8);
+        c010 = (float)(v10 & 0xffu); c110 = (float)(v10 >> 8);
+        c001 = (float)(v01 & 0xffu); c101 = (float)(v01 >> 8);
+        c011 = (float)(v11 & 0xffu); c111 = (float)(v11 >> 8);
+    } else {
+        int i0, i1, j0, j1, k0, k1;
+        if constexpr (WRAP == WRAP_CLAMP) {
+            i0 = clampi(ix, 0, a.nx - 1); i1 = clampi(ix + 1, 0, a.nx - 1);
+            j0 = clampi(iy, 0, a.ny - 1); j1 = clampi(iy + 1, 0, a.ny - 1);
+            k0 = clampi(iz, 0, a.nz - 1); k1 = clampi(iz + 1, 0, a.nz - 1);
+        } else {
+            i0 = mirror_(ix, a.nx); i1 = mirror_(ix + 1, a.nx);
+            j0 = mirror_(iy, a.ny); j1 = mirror_(iy + 1, a.ny);
+            k0 = mirror_(iz, a.nz); k1 = mirror_(iz + 1, a.nz);
+        }
+        const int r00 = (k0 * a.ny + j0) * a.nx, r10 = (k0 * a.ny + j1) * a.nx;
+        const int r01 = (k1 * a.ny + j0) * a.nx, r11 = (k1 * a.ny + j1) * a.nx;
+        c000 = pl[r00 + i0]; c100 = pl[r00 + i1];
+        c010 = pl[r10 + i0]; c110 = pl[r10 + i1];
+        c001 = pl[r01 + i0]; c101 = pl[r01 + i1];
+        c011 = pl[r11 + i0]; c111 = pl[r11 + i1];
+    }
+    const float x00 = lerp_(c000, c100, ax), x10 = lerp_(c010, c110, ax);
+    const float x01 = lerp_(c001, c101, ax), x11 = lerp_(c011, c111, ax);
+    const float y0 = lerp_(x00, x10, ay), y1 = lerp_(x01, x11, ay);
+    return lerp_(y0, y1, az) * (1.0f / 255.0f);
+}
+
+// Bijective XCD-aware block remap (cdna_hip_programming.md T1): consecutive
+// tiles land on one XCD, so one XCD's L2 serves a compact image region and
+// hence a compact region of the volume.
+__device__ __forceinline__ int xcd_remap(int b, int nb)
+{
+    const int q = nb >> 3, r = nb & 7, xcd = b & 7, idx = b >> 3;
+    return xcd < r ? xcd * (q + 1) + idx : r * (q + 1) + (xcd - r) * q + idx;
+}
+
+template <int LAYOUT, int WRAP, bool EARLY>
+__global__ __launch_bounds__(kThreads) void march_grid(const MarchArgs a)
+{
+    const int tile = xcd_remap(blockIdx.x, a.num_tiles);
+    const int tx = tile % a.tiles_x, ty = tile / a.tiles_x;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int x = tx * kTile + (wave & 1) * 8 + (lane & 7);
+    const int orow = ty * kTile + (wave >> 1) * 8 + (lane >> 3);
+    const bool inside = x < a.width && orow < a.out_rows;
+    int y = 0;
+    if (inside) {
+        const int bl = orow / a.band_rows;
+        y = (a.band_first + bl * a.band_stride) * a.band_rows + (orow - bl * a.band_rows);
+    }
+    const bool live = inside && y < a.height;
+
+    // ---- ray setup: frag.glsl:36-55 ---------------------------------------
+    int n = -1;
+    float P0 = 0.f, P1 = 0.f, P2 = 0.f, s0 = 0.f, s1 = 0.f, s2 = 0.f;
+    if (live) {
+        const float fx = (float)x + 0.5f, fy = (float)y + 0.5f;
+        const float v0 = fmaf(fy, a.py[0], fmaf(fx, a.px[0], a.o[0]));
+        const float v1 = fmaf(fy, a.py[1], fmaf(fx, a.px[1], a.o[1]));
+        const float v2 = fmaf(fy, a.py[2], fmaf(fx, a.px[2], a.o[2]));
+        const float len = sqrtf(fmaf(v2, v2, fmaf(v1, v1, v0 * v0)));
+        const float d0 = v0 / len, d1 = v1 / len, d2 = v2 / len;
+        // IntersectAABB, frag.glsl:18-27
+        const float ta0 = (a.box_min[0] - a.org[0]) / d0, tb0 = (a.box_max[0] - a.org[0]) / d0;
+        const float ta1 = (a.box_min[1] - a.org[1]) / d1, tb1 = (a.box_max[1] - a.org[1]) / d1;
+        const float ta2 = (a.box_min[2] - a.org[2]) / d2, tb2 = (a.box_max[2] - a.org[2]) / d2;
+        const float tn = fmaxf(fmaxf(fminf(ta0, tb0), fminf(ta1, tb1)), fminf(ta2, tb2));
+        const float tf = fminf(fminf(fmaxf(ta0, tb0), fmaxf(ta1, tb1)), fmaxf(ta2, tb2));
+        if (tn <= tf) {
+            const float pi0 = fmaf(d0, tn, a.org[0]), pi1 = fmaf(d1, tn, a.org[1]), pi2 = fmaf(d2, tn, a.org[2]);
+            const float zc = fmaf(a.r2[2], pi2, fmaf(a.r2[1], pi1, fmaf(a.r2[0], pi0, a.r2[3])));
+            const float wc = fmaf(a.r3[2], pi2, fmaf(a.r3[1], pi1, fmaf(a.r3[0], pi0, a.r3[3])));
+            if (wc > 0.0f && zc >= 0.0f && zc <= wc) {
+                const float po0 = fmaf(d0, tf, a.org[0]), po1 = fmaf(d1, tf, a.org[1]), po2 = fmaf(d2, tf, a.org[2]);
+                const float e0 = po0 - pi0, e1 = po1 - pi1, e2 = po2 - pi2;
+                const float dist = sqrtf(fmaf(e2, e2, fmaf(e1, e1, e0 * e0)));
+                const float q = dist / a.step_size;                                   // :46
+                n = q >= (float)a.max_steps ? a.max_steps : (int)q;
+                P0 = (pi0 - a.box_min[0]) / a.box_range[0];                           // :49-54
+                P1 = (pi1 - a.box_min[1]) / a.box_range[1];
+                P2 = (pi2 - a.box_min[2]) / a.box_range[2];
+                s0 = (a.step_size * d0) / a.box_range[0];                             // :45
+                s1 = (a.step_size * d1) / a.box_range[1];
+                s2 = (a.step_size * d2) / a.box_range[2];
+            }
+        }
+    }
+
+    // ---- the hot loop: frag.glsl:57-75 ------------------------------------
+    const uint8_t* __restrict__ pl0 = a.vol;
+    const uint8_t* __restrict__ pl1 = a.vol + a.plane_stride;
+    const uint8_t* __restrict__ pl2 = a.vol + 2 * a.plane_stride;
+    const uint8_t* __restrict__ pl3 = a.vol + 3 * a.plane_stride;
+    float acc = 0.0f;
+    int i = 0;
+    for (; i < n; ++i) {
+        const float t0 = tap<LAYOUT, WRAP>(pl0, a, fmaf(P0, a.tap_scale[0], a.tap_off[0][0]),
+                                           fmaf(P1, a.tap_scale[0], a.tap_off[0][1]),
+                                           fmaf(P2, a.tap_scale[0], a.tap_off[0][2]));
+        const float t1 = tap<LAYOUT, WRAP>(pl1, a, fmaf(P0, a.tap_scale[1], a.tap_off[1][0]),
+                                           fmaf(P1, a.tap_scale[1], a.tap_off[1][1]),
+                                           fmaf(P2, a.tap_scale[1], a.tap_off[1][2]));
+        const float t2 = tap<LAYOUT, WRAP>(pl2, a, fmaf(P0, a.tap_scale[2], a.tap_off[2][0]),
+                                           fmaf(P1, a.tap_scale[2], a.tap_off[2][1]),
+                                           fmaf(P2, a.tap_scale[2], a.tap_off[2][2]));
+        const float t3 = tap<LAYOUT, WRAP>(pl3, a, fmaf(P0, a.tap_scale[3], a.tap_off[3][0]),
+                                           fmaf(P1, a.tap_scale[3], a.tap_off[3][1]),
+                                           fmaf(P2, a.tap_scale[3], a.tap_off[3][2]));
+        acc = acc + ((t0 * t1) * (t2 + t3)) * a.scale;                               // :71-73
+        P0 = P0 + s0; P1 = P1 + s1; P2 = P2 + s2;                                     // :74
+        if constexpr (EARLY) {
+            if (acc > a.acc_limit) { ++i; break; }
+        }
+    }
+
+    // ---- epilogue: frag.glsl:76-80 + the render-target format --------------
+    if (a.step_counter) {
+        unsigned long long cnt = (n > 0) ? (unsigned long long)i : 0ull;
+        for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+        if (lane == 0 && cnt) atomicAdd(a.step_counter, cnt);
+    }
+    if (!live) return;
+    float g = 0.0f;
+    if (n >= 0) {
+        const float at = acc * a.step_size;
+        const float e = spec_expf(a.density * fminf(-at, 0.0f));
+        g = 1.0f - e;
+    }
+    char* row = (char*)a.out + (long long)orow * a.pitch;
+    if (a.format == 0) {
+        reinterpret_cast<float4*>(row)[x] = make_float4(g, g, g, 1.0f);
+    } else {
+        unsigned int q = 0;
+        if (n >= 0) {
+            float c = fminf(fmaxf(g, 0.0f), 1.0f);
+            if (a.format == 2)
+                c = c <= 0.0031308f ? c * 12.92f : fmaf(1.055f, powf(c, 1.0f / 2.4f), -0.055f);
+            q = (unsigned int)rintf(c * 255.0f);
+        }
+        reinterpret_cast<unsigned int*>(row)[x] = q | (q << 8) | (q << 16) | 0xff000000u;
+    }
+}
+
+template <int L, int W>
+hipError_t launch_lw(const MarchArgs& a, bool early, hipStream_t s)
+{
+    dim3 grid(a.num_tiles), block(kThreads);
+    if (early)
+        hipLaunchKernelGGL((march_grid<L, W, true>), grid, block, 0, s, a);
+    else
+        hipLaunchKernelGGL((march_grid<L, W, false>), grid, block, 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_march(const MarchArgs& a, int layout, int wrap, bool early, hipStream_t s)
+{
+    if (a.num_tiles <= 0) return hipSuccess;
+    if (layout == LAYOUT_PAD16) return launch_lw<LAYOUT_PAD16, WRAP_CLAMP>(a, early, s);
+    if (wrap == WRAP_CLAMP) return launch_lw<LAYOUT_PLANAR, WRAP_CLAMP>(a, early, s);
+    return launch_lw<LAYOUT_PLANAR, WRAP_MIRROR>(a, early, s);
+}
+
+}  // namespace vr

@@ -1,0 +1,135 @@
+// vr_noise.h -- device noise generators for the volume producer
+// (reference call sites TestMain.cpp:43-45, 59-62).
+//
+// FastNoise2 (vendor/noise) is absent from the reference mount and its commit
+// is unknown (.gitmodules:10-12).  These are restatements of its published
+// generators -- HashPrimes with primes 501125321 / 1136930381 / 1720413743 and
+// multiplier 0x27d4eb2d, the hash&13 gradient set, quintic interpolation,
+// 3D simplex with the 0.6 falloff, cellular F1 with hash-derived jitter --
+// with a fixed fp32 operation order.  Values are pinned
+// to our own known-answer fixtures, not to FastNoise2 (parity unpinned).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace vr {
+namespace noise {
+
+constexpr int32_t kPX = 501125321, kPY = 1136930381, kPZ = 1720413743;
+
+__device__ __forceinline__ int32_t wmul(int32_t a, int32_t b) { return (int32_t)((uint32_t)a * (uint32_t)b); }
+__device__ __forceinline__ int32_t wadd(int32_t a, int32_t b) { return (int32_t)((uint32_t)a + (uint32_t)b); }
+
+__device__ __forceinline__ int32_t hash(int32_t seed, int32_t x, int32_t y, int32_t z)
+{
+    const int32_t h = wmul(seed ^ x ^ y ^ z, 0x27d4eb2d);
+    return (h >> 15) ^ h;
+}
+__device__ __forceinline__ int32_t hash_hb(int32_t seed, int32_t x, int32_t y, int32_t z)
+{
+    return wmul(seed ^ x ^ y ^ z, 0x27d4eb2d);
+}
+__device__ __forceinline__ float grad(int32_t h, float fx, float fy, float fz)
+{
+    const int32_t h13 = h & 13;
+    float u = h13 < 8 ? fx : fy;
+    float v = h13 < 2 ? fy : (h13 == 12 ? fx : fz);
+    u = (h & 1) ? -u : u;
+    v = (h & 2) ? -v : v;
+    return u + v;
+}
+__device__ __forceinline__ float quintic(float t)
+{
+    float q = fmaf(t, 6.0f, -15.0f);
+    q = fmaf(t, q, 10.0f);
+    return ((t * t) * t) * q;
+}
+__device__ __forceinline__ float lerp(float a, float b, float t) { return fmaf(t, b - a, a); }
+
+__device__ inline float perlin(int32_t seed, float x, float y, float z)
+{
+    const float xs = floorf(x), ys = floorf(y), zs = floorf(z);
+    const int32_t x0 = wmul((int32_t)xs, kPX), y0 = wmul((int32_t)ys, kPY), z0 = wmul((int32_t)zs, kPZ);
+    const int32_t x1 = wadd(x0, kPX), y1 = wadd(y0, kPY), z1 = wadd(z0, kPZ);
+    const float xf0 = x - xs, yf0 = y - ys, zf0 = z - zs;
+    const float xf1 = xf0 - 1.0f, yf1 = yf0 - 1.0f, zf1 = zf0 - 1.0f;
+    const float u = quintic(xf0), v = quintic(yf0), w = quintic(zf0);
+    const float l00 = lerp(grad(hash(seed, x0, y0, z0), xf0, yf0, zf0), grad(hash(seed, x1, y0, z0), xf1, yf0, zf0), u);
+    const float l10 = lerp(grad(hash(seed, x0, y1, z0), xf0, yf1, zf0), grad(hash(seed, x1, y1, z0), xf1, yf1, zf0), u);
+    const float l01 = lerp(grad(hash(seed, x0, y0, z1), xf0, yf0, zf1), grad(hash(seed, x1, y0, z1), xf1, yf0, zf1), u);
+    const float l11 = lerp(grad(hash(seed, x0, y1, z1), xf0, yf1, zf1), grad(hash(seed, x1, y1, z1), xf1, yf1, zf1), u);
+    return 0.964921414852142333984375f * lerp(lerp(l00, l10, v), lerp(l01, l11, v), w);
+}
+
+__device__ __forceinline__ float simplex_corner(int32_t seed, int32_t xp, int32_t yp, int32_t zp,
+                                                float x, float y, float z)
+{
+    const float t = 0.6f - fmaf(z, z, fmaf(y, y, x * x));
+    if (!(t > 0.0f)) return 0.0f;
+    const float t2 = t * t;
+    return (t2 * t2) * grad(hash(seed, xp, yp, zp), x, y, z);
+}
+
+__device__ inline float simplex(int32_t seed, float x, float y, float z)
+{
+    const float F3 = 1.0f / 3.0f, G3 = 1.0f / 6.0f, G3x2 = 1.0f / 3.0f;
+    const float s = ((x + y) + z) * F3;
+    const float xs = floorf(x + s), ys = floorf(y + s), zs = floorf(z + s);
+    const float t = ((xs + ys) + zs) * G3;
+    const float x0 = (x - xs) + t, y0 = (y - ys) + t, z0 = (z - zs) + t;
+    int i1, j1, k1, i2, j2, k2;
+    if (x0 >= y0) {
+        if (y0 >= z0)      { i1 = 1; j1 = 0; k1 = 0; i2 = 1; j2 = 1; k2 = 0; }
+        else if (x0 >= z0) { i1 = 1; j1 = 0; k1 = 0; i2 = 1; j2 = 0; k2 = 1; }
+        else               { i1 = 0; j1 = 0; k1 = 1; i2 = 1; j2 = 0; k2 = 1; }
+    } else {
+        if (y0 < z0)       { i1 = 0; j1 = 0; k1 = 1; i2 = 0; j2 = 1; k2 = 1; }
+        else if (x0 < z0)  { i1 = 0; j1 = 1; k1 = 0; i2 = 0; j2 = 1; k2 = 1; }
+        else               { i1 = 0; j1 = 1; k1 = 0; i2 = 1; j2 = 1; k2 = 0; }
+    }
+    const float x1 = (x0 - (float)i1) + G3, y1 = (y0 - (float)j1) + G3, z1 = (z0 - (float)k1) + G3;
+    const float x2 = (x0 - (float)i2) + G3x2, y2 = (y0 - (float)j2) + G3x2, z2 = (z0 - (float)k2) + G3x2;
+    const float x3 = (x0 - 1.0f) + 0.5f, y3 = (y0 - 1.0f) + 0.5f, z3 = (z0 - 1.0f) + 0.5f;
+    const int32_t xp = wmul((int32_t)xs, kPX), yp = wmul((int32_t)ys, kPY), zp = wmul((int32_t)zs, kPZ);
+    const float n0 = simplex_corner(seed, xp, yp, zp, x0, y0, z0);
+    const float n1 = simplex_corner(seed, wadd(xp, i1 ? kPX : 0), wadd(yp, j1 ? kPY : 0), wadd(zp, k1 ? kPZ : 0), x1, y1, z1);
+    const float n2 = simplex_corner(seed, wadd(xp, i2 ? kPX : 0), wadd(yp, j2 ? kPY : 0), wadd(zp, k2 ? kPZ : 0), x2, y2, z2);
+    const float n3 = simplex_corner(seed, wadd(xp, kPX), wadd(yp, kPY), wadd(zp, kPZ), x3, y3, z3);
+    return 32.69428253173828125f * (((n0 + n1) + n2) + n3);
+}
+
+__device__ inline float cellular(int32_t seed, float x, float y, float z)
+{
+    const float jitter = 0.39614353f;
+    const float xr = rintf(x), yr = rintf(y), zr = rintf(z);
+    const int32_t xc = wmul((int32_t)xr, kPX), yc = wmul((int32_t)yr, kPY), zc = wmul((int32_t)zr, kPZ);
+    float d0 = 3.402823466e+38f;
+#pragma unroll
+    for (int xi = -1; xi <= 1; ++xi) {
+        const float xcf = (xr + (float)xi) - x;
+        const int32_t xp = wadd(xc, wmul(xi, kPX));
+#pragma unroll
+        for (int yi = -1; yi <= 1; ++yi) {
+            const float ycf = (yr + (float)yi) - y;
+            const int32_t yp = wadd(yc, wmul(yi, kPY));
+#pragma unroll
+            for (int zi = -1; zi <= 1; ++zi) {
+                const float zcf = (zr + (float)zi) - z;
+                const int32_t zp = wadd(zc, wmul(zi, kPZ));
+                const int32_t h = hash_hb(seed, xp, yp, zp);
+                float xd = (float)(h & 0x3ff) - 511.5f;
+                float yd = (float)((h >> 10) & 0x3ff) - 511.5f;
+                float zd = (float)((h >> 20) & 0x3ff) - 511.5f;
+                const float inv = jitter / sqrtf(fmaf(zd, zd, fmaf(yd, yd, xd * xd)));
+                xd = fmaf(xd, inv, xcf);
+                yd = fmaf(yd, inv, ycf);
+                zd = fmaf(zd, inv, zcf);
+                d0 = fminf(d0, fmaf(zd, zd, fmaf(yd, yd, xd * xd)));
+            }
+        }
+    }
+    return d0 - 1.0f;
+}
+
+}  // namespace noise
+}  // namespace vr

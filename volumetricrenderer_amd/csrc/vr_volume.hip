@@ -1,0 +1,242 @@
+// vr_volume.hip -- volume producer and layout kernels, plus band assembly.
+//
+//  * repack: RGBA8 interleaved (the Texture3D input, TestMain.cpp:69-87)
+//    -> per-channel planes (planar and padded), the layouts vr_march reads.
+//  * noise + min/max + pack: TestMain.cpp:43-92 on the GPU.
+//  * assemble: gathered band sets of N ranks -> one frame (SURVEY.md e).
+// All are HBM-bound streaming kernels: wide coalesced accesses, grid-stride.
+#include "vr_internal.h"
+#include "vr_noise.h"
+
+namespace vr {
+namespace {
+
+constexpr int kBlock = 256;
+
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return min(max(v, lo), hi); }
+
+// One thread per texel: read 4 B, write 1 B to each of 4 planes.  The padded
+// planes get their own pass over (nx+2)(ny+2)(nz+2) positions.
+__global__ __launch_bounds__(kBlock) void k_repack_planar(const uchar4* __restrict__ src, long long total,
+                                                          uint8_t* __restrict__ dst)
+{
+    for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < total;
+         i += (long long)gridDim.x * kBlock) {
+        const uchar4 v = src[i];
+        dst[i] = v.x;
+        dst[i + total] = v.y;
+        dst[i + 2 * total] = v.z;
+        dst[i + 3 * total] = v.w;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_repack_pad16(const uchar4* __restrict__ src, int nx, int ny, int nz,
+                                                         uint8_t* __restrict__ dst)
+{
+    const int px = nx + 2, py = ny + 2, pz = nz + 2;
+    const long long ptotal = (long long)px * py * pz;
+    for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < ptotal;
+         i += (long long)gridDim.x * kBlock) {
+        const int a = (int)(i % px);
+        const long long t = i / px;
+        const int b = (int)(t % py), c = (int)(t / py);
+        const int sx = clampi(a - 1, 0, nx - 1), sy = clampi(b - 1, 0, ny - 1), sz = clampi(c - 1, 0, nz - 1);
+        const uchar4 v = src[((long long)sz * ny + sy) * nx + sx];
+        dst[i] = v.x;
+        dst[i + ptotal] = v.y;
+        dst[i + 2 * ptotal] = v.z;
+        dst[i + 3 * ptotal] = v.w;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_unpack_planar(const uint8_t* __restrict__ src, long long total,
+                                                          uchar4* __restrict__ dst)
+{
+    for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < total;
+         i += (long long)gridDim.x * kBlock)
+        dst[i] = make_uchar4(src[i], src[i + total], src[i + 2 * total], src[i + 3 * total]);
+}
+
+// GenUniformGrid3D: pos = (start + idx) * freq, x fastest.  Each block also
+// writes its {min, max}; k_minmax folds them (exact, order-independent).
+__global__ __launch_bounds__(kBlock) void k_noise(int kind, float* __restrict__ out, int x0, int y0, int z0,
+                                                  int nx, int ny, int nz, float freq, int32_t seed,
+                                                  float2* __restrict__ partials)
+{
+    const long long total = (long long)nx * ny * nz;
+    float mn = __builtin_inff(), mx = -__builtin_inff();
+    for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < total;
+         i += (long long)gridDim.x * kBlock) {
+        const int x = (int)(i % nx);
+        const long long t = i / nx;
+        const int y = (int)(t % ny), z = (int)(t / ny);
+        const float px = (float)(x0 + x) * freq, py = (float)(y0 + y) * freq, pz = (float)(z0 + z) * freq;
+        float v;
+        if (kind == 0) v = noise::cellular(seed, px, py, pz);
+        else if (kind == 1) v = noise::perlin(seed, px, py, pz);
+        else v = noise::simplex(seed, px, py, pz);
+        if (out) out[i] = v;
+        mn = fminf(mn, v);
+        mx = fmaxf(mx, v);
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        mn = fminf(mn, __shfl_xor(mn, off));
+        mx = fmaxf(mx, __shfl_xor(mx, off));
+    }
+    __shared__ float2 red[kBlock / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) red[wave] = make_float2(mn, mx);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float2 r = red[0];
+        for (int w = 1; w < kBlock / 64; ++w) { r.x = fminf(r.x, red[w].x); r.y = fmaxf(r.y, red[w].y); }
+        partials[blockIdx.x] = r;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_minmax(const float2* __restrict__ partials, int n, float* __restrict__ out)
+{
+    float mn = __builtin_inff(), mx = -__builtin_inff();
+    for (int i = threadIdx.x; i < n; i += kBlock) { mn = fminf(mn, partials[i].x); mx = fmaxf(mx, partials[i].y); }
+    for (int off = 32; off > 0; off >>= 1) {
+        mn = fminf(mn, __shfl_xor(mn, off));
+        mx = fmaxf(mx, __shfl_xor(mx, off));
+    }
+    __shared__ float2 red[kBlock / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) red[wave] = make_float2(mn, mx);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float2 r = red[0];
+        for (int w = 1; w < kBlock / 64; ++w) { r.x = fminf(r.x, red[w].x); r.y = fmaxf(r.y, red[w].y); }
+        out[0] = r.x;
+        out[1] = r.y;
+    }
+}
+
+// static_cast<unsigned char>(float) as x86-64 compiles it (cvttss2si, keep
+// the low byte): TestMain.cpp:84-87.
+__device__ __forceinline__ unsigned int f2u8_trunc(float f)
+{
+    if (!(f > -2147483648.0f && f < 2147483648.0f)) return 0u;
+    return (unsigned int)(int)f & 0xffu;
+}
+
+// TestMain.cpp:64-92.  g2 == nullptr means the zero-filled noiseOutput2 of
+// the literal recipe.  minmax = {min1,max1, min2,max2, min3,max3, min4,max4}.
+__global__ __launch_bounds__(kBlock) void k_pack_recipe(const float* __restrict__ g1, const float* __restrict__ g2,
+                                                        const float* __restrict__ g3, const float* __restrict__ g4,
+                                                        const float* __restrict__ mm, long long total,
+                                                        uchar4* __restrict__ out)
+{
+    const float inv1 = 1.0f / (mm[1] - mm[0]), inv2 = 1.0f / (mm[3] - mm[2]);
+    const float inv3 = 1.0f / (mm[5] - mm[4]), inv4 = 1.0f / (mm[7] - mm[6]);
+    for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < total;
+         i += (long long)gridDim.x * kBlock) {
+        float s1 = 1.0f - (g1[i] - mm[0]) * inv1;
+        const float s2 = 1.0f - ((g2 ? g2[i] : 0.0f) - mm[2]) * inv2;
+        const float s3 = 1.0f - (g3[i] - mm[4]) * inv3;
+        const float s4 = 1.0f - (g4[i] - mm[6]) * inv4;
+        s1 = s1 * ((s1 * s1) * s1);
+        out[i] = make_uchar4(f2u8_trunc(s1 * 255.0f), f2u8_trunc(s2 * 255.0f), f2u8_trunc(s3 * 255.0f),
+                             f2u8_trunc(s4 * 255.0f));
+    }
+}
+
+// frame row y lives in band b = y / band_rows, rendered by rank b % nranks as
+// its (b / nranks)-th band.  16-byte chunks when rows allow it.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_assemble(const T* __restrict__ src, long long rows_per_rank,
+                                                     int nranks, int row_elems, int height, int band_rows,
+                                                     T* __restrict__ dst)
+{
+    const long long total = (long long)height * row_elems;
+    for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < total;
+         i += (long long)gridDim.x * kBlock) {
+        const int y = (int)(i / row_elems), e = (int)(i % row_elems);
+        const int b = y / band_rows, r = y - b * band_rows;
+        const int rank = b % nranks, lb = b / nranks;
+        const long long srow = (long long)rank * rows_per_rank + (long long)lb * band_rows + r;
+        dst[i] = src[srow * row_elems + e];
+    }
+}
+
+int grid_for(long long n)
+{
+    long long g = (n + kBlock - 1) / kBlock;
+    if (g > 256 * 16) g = 256 * 16;
+    if (g < 1) g = 1;
+    return (int)g;
+}
+
+}  // namespace
+
+hipError_t launch_repack(const uint8_t* d_rgba, int nx, int ny, int nz, uint8_t* d_planar, uint8_t* d_pad16,
+                         hipStream_t s)
+{
+    const long long total = (long long)nx * ny * nz;
+    if (d_planar)
+        hipLaunchKernelGGL(k_repack_planar, dim3(grid_for(total)), dim3(kBlock), 0, s,
+                           reinterpret_cast<const uchar4*>(d_rgba), total, d_planar);
+    if (d_pad16) {
+        const long long pt = (long long)(nx + 2) * (ny + 2) * (nz + 2);
+        hipLaunchKernelGGL(k_repack_pad16, dim3(grid_for(pt)), dim3(kBlock), 0, s,
+                           reinterpret_cast<const uchar4*>(d_rgba), nx, ny, nz, d_pad16);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_unpack(const uint8_t* d_planar, int nx, int ny, int nz, uint8_t* d_rgba, hipStream_t s)
+{
+    const long long total = (long long)nx * ny * nz;
+    hipLaunchKernelGGL(k_unpack_planar, dim3(grid_for(total)), dim3(kBlock), 0, s, d_planar, total,
+                       reinterpret_cast<uchar4*>(d_rgba));
+    return hipGetLastError();
+}
+
+int noise_partials_needed(int nx, int ny, int nz) { return grid_for((long long)nx * ny * nz); }
+
+hipError_t launch_noise(int kind, float* d_out, int x0, int y0, int z0, int nx, int ny, int nz, float freq,
+                        int32_t seed, float* d_partials, int* num_partials, hipStream_t s)
+{
+    const int g = grid_for((long long)nx * ny * nz);
+    *num_partials = g;
+    hipLaunchKernelGGL(k_noise, dim3(g), dim3(kBlock), 0, s, kind, d_out, x0, y0, z0, nx, ny, nz, freq, seed,
+                       reinterpret_cast<float2*>(d_partials));
+    return hipGetLastError();
+}
+
+hipError_t launch_minmax_reduce(const float* d_partials, int num_partials, float* d_minmax, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_minmax, dim3(1), dim3(kBlock), 0, s, reinterpret_cast<const float2*>(d_partials),
+                       num_partials, d_minmax);
+    return hipGetLastError();
+}
+
+hipError_t launch_pack_recipe(const float* d_g1, const float* d_g2, const float* d_g3, const float* d_g4,
+                              const float* d_minmax, long long total, uint8_t* d_rgba, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_pack_recipe, dim3(grid_for(total)), dim3(kBlock), 0, s, d_g1, d_g2, d_g3, d_g4,
+                       d_minmax, total, reinterpret_cast<uchar4*>(d_rgba));
+    return hipGetLastError();
+}
+
+hipError_t launch_assemble(const uint8_t* d_gathered, size_t rows_per_rank, int nranks, int width, int height,
+                           int band_rows, int bpp, uint8_t* d_frame, hipStream_t s)
+{
+    const long long row_bytes = (long long)width * bpp;
+    if (row_bytes % 16 == 0) {
+        const int elems = (int)(row_bytes / 16);
+        hipLaunchKernelGGL(k_assemble<uint4>, dim3(grid_for((long long)height * elems)), dim3(kBlock), 0, s,
+                           reinterpret_cast<const uint4*>(d_gathered), (long long)rows_per_rank, nranks, elems,
+                           height, band_rows, reinterpret_cast<uint4*>(d_frame));
+    } else {
+        const int elems = (int)(row_bytes / 4);
+        hipLaunchKernelGGL(k_assemble<unsigned int>, dim3(grid_for((long long)height * elems)), dim3(kBlock), 0,
+                           s, reinterpret_cast<const unsigned int*>(d_gathered), (long long)rows_per_rank, nranks,
+                           elems, height, band_rows, reinterpret_cast<unsigned int*>(d_frame));
+    }
+    return hipGetLastError();
+}
+
+}  // namespace vr

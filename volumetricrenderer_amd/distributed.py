@@ -1,0 +1,87 @@
+"""Multi-GPU frame sharding: interleaved screen bands + gather to rank 0.
+
+SURVEY.md sec. 8e.  Pixels are independent: a1-a6 read only the uniforms and
+a read-only volume.  So a frame shards by screen rows and the volume is
+replicated on every rank.  The silhouette of the reference cube is a centred
+hexagon, so contiguous strips are badly imbalanced (2.45x at 8 ranks).
+Interleaved 16-row bands, where band b goes to rank b mod N, are balanced to
+within 1-2 %.  The only exchange is one gather per frame.  Each rank's packed
+band set goes to rank 0, over RCCL (torch.distributed "nccl") on GPUs or gloo
+in the CPU tests.  Rank 0 then scatters the sets into the frame with
+vr_assemble_bands.
+
+One process per GPU; the reference has no distributed code at all.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def rows_for_rank(height: int, band_rows: int, world: int, rank: int) -> int:
+    nb = (height + band_rows - 1) // band_rows
+    return len(range(rank, nb, world)) * band_rows
+
+
+class BandSharder:
+    """Renders this rank's bands of a W x H frame and gathers them on rank 0.
+
+    `renderer` provides ``alloc_target``, ``render`` and ``assemble_bands``.
+    That is :class:`volumetricrenderer_amd.Renderer`, or a CPU stand-in in
+    the gloo tests.
+    """
+
+    def __init__(self, renderer, width: int, height: int, fmt: int, band_rows: int = 16, world: int = 1,
+                 rank: int = 0, group=None):
+        self.r = renderer
+        self.width, self.height, self.fmt = width, height, fmt
+        self.world, self.rank, self.group = world, rank, group
+        self.band_rows = band_rows if world > 1 else 0
+        if world > 1:
+            self.my_rows = rows_for_rank(height, band_rows, world, rank)
+            # every rank's buffer has rank 0's row count (the most rows), so
+            # the gather moves equal-sized messages
+            self.rows_per_rank = rows_for_rank(height, band_rows, world, 0)
+            buf = renderer.alloc_target(width, height, fmt, band_rows, world, 0)
+            assert buf.shape[0] == self.rows_per_rank
+            self.local = buf
+            if rank == 0:
+                self.gathered = torch.empty((world,) + tuple(buf.shape), dtype=buf.dtype, device=buf.device)
+                self.frame_buf = torch.empty((height, width, buf.shape[-1]), dtype=buf.dtype, device=buf.device)
+        else:
+            self.my_rows = height
+            self.rows_per_rank = height
+            self.local = renderer.alloc_target(width, height, fmt)
+            self.frame_buf = self.local
+
+    def render_local(self, step_counter=None, events=None):
+        """Launch this rank's bands (async on the current stream)."""
+        if events is not None:
+            events[0].record()
+        if self.world > 1:
+            self.r.render(self.width, self.height, self.fmt, out=self.local[: self.my_rows],
+                          band_rows=self.band_rows, band_stride=self.world, band_first=self.rank,
+                          step_counter=step_counter)
+        else:
+            self.r.render(self.width, self.height, self.fmt, out=self.local, step_counter=step_counter)
+        if events is not None:
+            events[1].record()
+
+    def frame(self, events=None):
+        """One frame: render local bands, gather to rank 0, assemble there.
+        Returns the full frame on rank 0 and the local band set elsewhere."""
+        self.render_local(events=events)
+        if self.world == 1:
+            return self.frame_buf
+        gl = list(self.gathered.unbind(0)) if self.rank == 0 else None
+        dist.gather(self.local, gather_list=gl, dst=0, group=self.group)
+        if self.rank == 0:
+            self.r.assemble_bands(self.gathered, self.world, self.width, self.height, self.band_rows,
+                                  frame=self.frame_buf)
+            return self.frame_buf
+        return self.local
+
+    def close(self):
+        self.local = None
+        self.gathered = None
+        self.frame_buf = None

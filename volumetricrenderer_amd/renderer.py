@@ -1,0 +1,218 @@
+"""Host-side interface of the ray-march path, over the C ABI (include/vr.h).
+
+This mirrors the part of the reference interface that feeds shaders/frag.glsl:
+
+==========================================  =====================================
+reference (file:line)                       here
+==========================================  =====================================
+``vkc::Texture3D(data, extent)``            :meth:`Renderer.set_volume`
+(VulkanTexture.h:55-60)
+noise -> pixelData loops                    :meth:`Renderer.generate_volume`
+(TestMain.cpp:43-92)
+``UniformBuffer<T>::Update`` x2             :meth:`Renderer.set_shader_data`
+(TestMain.cpp:248-249)
+Model/View/Projection/W2L producer          :func:`reference_shader_data`
+(TestMain.cpp:219-245)
+frag.glsl constants (:29-32, :42, :63-69)   :func:`march_defaults`, :meth:`Renderer.set_march`
+``EnqueueRenderPass("BasePass")`` + draw    :meth:`Renderer.render`
+(TestMain.cpp:194-217)
+==========================================  =====================================
+
+torch is used only for device memory and streams.  All arithmetic runs in
+libvr.so, and a missing library raises at import.  Errors are raised as
+:class:`VRError`.  The reference throws from ``Error()`` instead (Utils.h:22-29).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import (BYTES_PER_PIXEL, FMT_RGBA8_SRGB, FMT_RGBA8_UNORM, FMT_RGBA32F,  # noqa: F401
+                   GlobalShaderData, MarchParams, ObjectShaderData, Target, VolumeRecipe, VRError, call)
+
+_lib.load()  # fail at import if the HIP library is missing
+
+
+def _stream_handle(stream) -> ctypes.c_void_p:
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    if isinstance(stream, torch.cuda.Stream):
+        return ctypes.c_void_p(stream.cuda_stream)
+    return ctypes.c_void_p(int(stream))
+
+
+def march_defaults(**overrides) -> MarchParams:
+    """The reference's frag.glsl constants, with field overrides."""
+    m = MarchParams()
+    call("vr_march_defaults", ctypes.byref(m))
+    for k, v in overrides.items():
+        if isinstance(v, (list, tuple)):
+            getattr(m, k)[:] = list(v)
+        else:
+            setattr(m, k, v)
+    return m
+
+
+def volume_recipe_defaults(**overrides) -> VolumeRecipe:
+    """TestMain.cpp:51-62: N=128, freqs (.01,.03,.19,.15), seeds 1..4, literal."""
+    r = VolumeRecipe()
+    call("vr_volume_recipe_defaults", ctypes.byref(r))
+    for k, v in overrides.items():
+        if isinstance(v, (list, tuple)):
+            getattr(r, k)[:] = list(v)
+        else:
+            setattr(r, k, v)
+    return r
+
+
+def scaled_recipe(size: int, literal: bool = True) -> VolumeRecipe:
+    """Reference recipe at N = size, with frequencies scaled by 128/size so that
+    the continuous field matches the 128^3 one (BASELINE config 5)."""
+    r = volume_recipe_defaults(size=size, literal_overwrite=int(literal))
+    s = 128.0 / size
+    r.freq[:] = [float(np.float32(f) * np.float32(s)) for f in (0.01, 0.03, 0.19, 0.15)]
+    return r
+
+
+def reference_shader_data(aspect: float = 1280.0 / 720.0, phi_deg: float = 0.0, theta_deg: float = 0.0,
+                          frame_time: float = 0.0):
+    """TestMain.cpp:219-245 computed by libvr's host code (GLM semantics)."""
+    osd, gsd = ObjectShaderData(), GlobalShaderData()
+    call("vr_reference_shader_data", ctypes.c_float(aspect), ctypes.c_float(phi_deg),
+         ctypes.c_float(theta_deg), ctypes.c_float(frame_time), ctypes.byref(osd), ctypes.byref(gsd))
+    return osd, gsd
+
+
+def band_rows_packed(height: int, band_rows: int, band_stride: int = 1, band_first: int = 0) -> int:
+    return _lib.load().vr_band_rows_packed(height, band_rows, band_stride, band_first)
+
+
+def shader_data_arrays(osd: ObjectShaderData, gsd: GlobalShaderData):
+    """(obj48, glob36) float32 arrays, the layout the oracle takes."""
+    obj = np.ctypeslib.as_array(ctypes.cast(ctypes.byref(osd), ctypes.POINTER(ctypes.c_float)), (48,)).copy()
+    glob = np.ctypeslib.as_array(ctypes.cast(ctypes.byref(gsd), ctypes.POINTER(ctypes.c_float)), (36,)).copy()
+    return obj, glob
+
+
+class Renderer:
+    """Offscreen ray-march renderer on one HIP device (one per process/rank)."""
+
+    def __init__(self, device: int = 0):
+        self._ctx = ctypes.c_void_p()
+        call("vr_create", int(device), ctypes.byref(self._ctx))
+        self.device = int(device)
+        self.march = march_defaults()
+
+    # -- lifetime --------------------------------------------------------
+    def close(self) -> None:
+        if self._ctx:
+            _lib.load().vr_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- volume (Texture3D) ------------------------------------------------
+    def set_volume(self, rgba) -> None:
+        """Upload an RGBA8 volume shaped (nz, ny, nx, 4), x fastest (TestMain.cpp:69-87)."""
+        if isinstance(rgba, torch.Tensor) and rgba.is_cuda:
+            return self.set_volume_device(rgba)
+        a = np.ascontiguousarray(rgba, dtype=np.uint8)
+        if a.ndim != 4 or a.shape[3] != 4:
+            raise ValueError("volume must be shaped (nz, ny, nx, 4)")
+        nz, ny, nx, _ = a.shape
+        call("vr_set_volume", self._ctx, a.ctypes.data_as(ctypes.c_void_p), nx, ny, nz)
+
+    def set_volume_device(self, t: torch.Tensor, stream=None) -> None:
+        if t.dtype != torch.uint8 or t.dim() != 4 or t.shape[3] != 4 or not t.is_contiguous():
+            raise ValueError("device volume must be a contiguous uint8 tensor (nz, ny, nx, 4)")
+        nz, ny, nx, _ = t.shape
+        h = _stream_handle(stream)
+        call("vr_set_volume_device", self._ctx, ctypes.c_void_p(t.data_ptr()), nx, ny, nz, h)
+        (stream if stream is not None else torch.cuda.current_stream()).synchronize()
+
+    def generate_volume(self, recipe: VolumeRecipe | None = None) -> None:
+        """Build the TestMain.cpp:43-92 volume on the GPU."""
+        r = recipe if recipe is not None else volume_recipe_defaults()
+        call("vr_generate_volume", self._ctx, ctypes.byref(r), _stream_handle(None))
+
+    def get_volume(self) -> np.ndarray:
+        nx, ny, nz = self.volume_dims()
+        out = np.empty((nz, ny, nx, 4), np.uint8)
+        call("vr_get_volume", self._ctx, out.ctypes.data_as(ctypes.c_void_p))
+        return out
+
+    def volume_dims(self):
+        nx, ny, nz = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        call("vr_volume_dims", self._ctx, ctypes.byref(nx), ctypes.byref(ny), ctypes.byref(nz))
+        return nx.value, ny.value, nz.value
+
+    def noise_grid(self, kind: int, nx: int, ny: int, nz: int, freq: float, seed: int,
+                   origin=(0, 0, 0), out: torch.Tensor | None = None):
+        """One GenUniformGrid3D on the GPU -> (tensor or None, min, max)."""
+        mn, mx = ctypes.c_float(), ctypes.c_float()
+        ptr = ctypes.c_void_p(out.data_ptr()) if out is not None else None
+        call("vr_noise_grid", self._ctx, int(kind), ptr, origin[0], origin[1], origin[2], nx, ny, nz,
+             ctypes.c_float(freq), int(seed), ctypes.byref(mn), ctypes.byref(mx), _stream_handle(None))
+        return out, mn.value, mx.value
+
+    # -- uniforms / constants ----------------------------------------------
+    def set_shader_data(self, osd: ObjectShaderData, gsd: GlobalShaderData) -> None:
+        call("vr_set_shader_data", self._ctx, ctypes.byref(osd), ctypes.byref(gsd))
+        self.osd, self.gsd = osd, gsd
+
+    def set_march(self, m: MarchParams | None = None, **overrides) -> None:
+        m = m if m is not None else march_defaults(**overrides)
+        call("vr_set_march", self._ctx, ctypes.byref(m))
+        self.march = m
+
+    def set_layout_preference(self, pref: int) -> None:
+        call("vr_set_layout_preference", self._ctx, int(pref))
+
+    @property
+    def kernel_variant(self) -> str:
+        return _lib.load().vr_kernel_variant(self._ctx).decode()
+
+    # -- the hot path ------------------------------------------------------
+    def alloc_target(self, width: int, height: int, fmt: int = FMT_RGBA8_UNORM, band_rows: int = 0,
+                     band_stride: int = 1, band_first: int = 0) -> torch.Tensor:
+        rows = band_rows_packed(height, band_rows, band_stride, band_first)
+        dev = torch.device("cuda", self.device)
+        if fmt == FMT_RGBA32F:
+            return torch.empty((rows, width, 4), dtype=torch.float32, device=dev)
+        return torch.empty((rows, width, 4), dtype=torch.uint8, device=dev)
+
+    def render(self, width: int, height: int, fmt: int = FMT_RGBA8_UNORM, out: torch.Tensor | None = None,
+               band_rows: int = 0, band_stride: int = 1, band_first: int = 0, stream=None,
+               step_counter: torch.Tensor | None = None) -> torch.Tensor:
+        """Launch the march kernel (asynchronous on `stream`); returns `out`."""
+        if out is None:
+            out = self.alloc_target(width, height, fmt, band_rows, band_stride, band_first)
+        t = Target(width=width, height=height, format=fmt, band_rows=band_rows, band_stride=band_stride,
+                   band_first=band_first, pixels=out.data_ptr(), row_pitch=out.stride(0) * out.element_size(),
+                   step_counter=step_counter.data_ptr() if step_counter is not None else None)
+        call("vr_render", self._ctx, ctypes.byref(t), _stream_handle(stream))
+        return out
+
+    def assemble_bands(self, gathered: torch.Tensor, nranks: int, width: int, height: int, band_rows: int,
+                       frame: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+        """Scatter [rank][packed rows] band sets into one frame (SURVEY.md e)."""
+        bpp = gathered.element_size() * gathered.shape[-1]
+        rows_per_rank = gathered.shape[1]
+        if frame is None:
+            frame = torch.empty((height, width, gathered.shape[-1]), dtype=gathered.dtype, device=gathered.device)
+        call("vr_assemble_bands", self._ctx, ctypes.c_void_p(gathered.data_ptr()), rows_per_rank, nranks,
+             width, height, band_rows, bpp, ctypes.c_void_p(frame.data_ptr()), _stream_handle(stream))
+        return frame
