@@ -168,8 +168,11 @@ int vr_band_rows_packed(int height, int band_rows, int band_stride, int band_fir
 /* ---- introspection: the kernel variant vr_render will launch ----------- */
 /* returns a static string, e.g. "grid_pad16_clamp"                        */
 const char* vr_kernel_variant(void* ctx);
-/* Force a volume layout: 0 = auto, 1 = planar u8 + mirrored repeat,
- * 2 = padded pairs + clamp.  2 is used only when clamp is exact.          */
+/* Choose the device volume layout: 0 = auto (default),
+ * 1 = planar only, 2 = padded u16 pairs, 3 = 4^3 apron bricks (128-B
+ * lines), 4 = 8-corner words, 5 = xy quads.  Layouts 2-5 are used only
+ * where clamp-to-edge equals mirrored repeat.  Otherwise the planar,
+ * mirrored-repeat kernel runs.  Rebuilds the layout (synchronous).        */
 vr_status vr_set_layout_preference(void* ctx, int pref);
 
 #ifdef __cplusplus

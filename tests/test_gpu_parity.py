@@ -72,7 +72,7 @@ def test_config1_perlin_cube_256_32(r, oracle):
 
 def test_reference_frame_1080p_128(r, oracle, vol128):
     img, ref, c, s = render_both(r, oracle, vol128, 1920, 1080)
-    assert r.kernel_variant == "grid_pad16_clamp"
+    assert r.kernel_variant.endswith("_clamp")
     assert_exact(img, ref)
     assert c == s
     assert 16_700_000 < s < 16_780_000  # 1.674e7 executed steps
@@ -100,19 +100,23 @@ def test_media_scroll_mirrored_repeat(r, oracle, vol128):
     assert_exact(img, ref)
 
 
-def test_layouts_agree(r, oracle, vol128):
+@pytest.mark.parametrize("layout,name", [(1, "planar"), (2, "pad16"), (3, "brick5"), (4, "corner8"), (5, "quad")])
+def test_every_layout_bitexact(r, oracle, vol128, layout, name):
     osd, gsd = vr.reference_shader_data(16 / 9, 20.0, -35.0)
     r.set_volume(vol128)
-    r.set_shader_data(osd, gsd)
-    r.set_march(vr.march_defaults())
-    a = r.render(480, 270, vr.FMT_RGBA32F).cpu().numpy()
-    v1 = r.kernel_variant
-    r.set_layout_preference(1)
-    b = r.render(480, 270, vr.FMT_RGBA32F).cpu().numpy()
-    v2 = r.kernel_variant
-    r.set_layout_preference(0)
-    assert (v1, v2) == ("grid_pad16_clamp", "grid_planar_clamp")
-    assert_exact(a, b)
+    r.set_layout_preference(layout)
+    try:
+        img, ref, c, s = render_both(r, oracle, vol128, 480, 270, osd, gsd)
+        assert r.kernel_variant == f"grid_{name}_clamp"
+        assert_exact(img, ref)
+        assert c == s
+        # odd, non-power-of-two extents exercise the brick edges
+        rng = np.random.default_rng(layout)
+        vol = rng.integers(0, 256, size=(13, 22, 9, 4), dtype=np.uint8)
+        img, ref, c, s = render_both(r, oracle, vol, 160, 90, osd, gsd)
+        assert_exact(img, ref)
+    finally:
+        r.set_layout_preference(0)
 
 
 @pytest.mark.parametrize("dims", [(37, 50, 23), (1, 1, 1), (2, 3, 5), (129, 64, 96)])
@@ -141,12 +145,12 @@ def test_box_and_constants(r, oracle, vol128):
 
 
 def test_early_out(r, oracle, vol128):
-    m = vr.march_defaults(density=40.0, early_out=0.05)
+    m = vr.march_defaults(density=400.0, early_out=0.05)
     img, ref, c, s = render_both(r, oracle, vol128, 320, 180, march=m)
     assert r.kernel_variant.endswith("_early")
     assert_exact(img, ref)
     assert c == s
-    m0 = vr.march_defaults(density=40.0)
+    m0 = vr.march_defaults(density=400.0)
     full, _, c0, _ = render_both(r, oracle, vol128, 320, 180, march=m0)
     assert c < c0                                     # the early-out fired
     assert np.abs(full - img).max() <= 0.05 + 1e-6    # and cost < eps

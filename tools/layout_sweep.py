@@ -1,0 +1,76 @@
+"""Time the march kernel for each volume layout, interleaved in one process.
+
+    python tools/layout_sweep.py [--sizes 128,512] [--rounds 5] [--frames 10]
+
+Prints median ms per frame and nominal Mray/s, and checks that every layout
+produces the same image as the first one.
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import volumetricrenderer_amd as vr  # noqa: E402
+
+NAMES = {1: "planar", 2: "pad16", 3: "brick5", 4: "corner8", 5: "quad"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sizes", default="128,512")
+    ap.add_argument("--layouts", default="2,3,4,5,1")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--frames", type=int, default=10)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--steps", type=int, default=128)
+    args = ap.parse_args()
+    W, H, S = args.width, args.height, args.steps
+    layouts = [int(x) for x in args.layouts.split(",")]
+    res = {}
+    with vr.Renderer(0) as r:
+        osd, gsd = vr.reference_shader_data(W / H)
+        r.set_shader_data(osd, gsd)
+        r.set_march(vr.march_defaults(max_steps=S))
+        for n in [int(x) for x in args.sizes.split(",")]:
+            if n <= 2:
+                r.set_volume(np.full((n, n, n, 4), 200, np.uint8))
+            else:
+                r.generate_volume(vr.scaled_recipe(n))
+            out = r.alloc_target(W, H, vr.FMT_RGBA8_UNORM)
+            ref = None
+            times = {lay: [] for lay in layouts}
+            for lay in layouts:  # build + parity
+                r.set_layout_preference(lay)
+                img = r.render(W, H, vr.FMT_RGBA8_UNORM, out=out).cpu().numpy()
+                if ref is None:
+                    ref = img
+                assert np.array_equal(img, ref), f"layout {lay} differs at N={n}"
+            for _ in range(args.rounds):
+                for lay in layouts:
+                    r.set_layout_preference(lay)
+                    r.render(W, H, vr.FMT_RGBA8_UNORM, out=out)
+                    ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.frames + 1)]
+                    ev[0].record()
+                    for k in range(args.frames):
+                        r.render(W, H, vr.FMT_RGBA8_UNORM, out=out)
+                        ev[k + 1].record()
+                    torch.cuda.synchronize()
+                    times[lay] += [ev[k].elapsed_time(ev[k + 1]) for k in range(args.frames)]
+            for lay in layouts:
+                t = float(np.median(times[lay]))
+                key = f"N{n}_{NAMES[lay]}"
+                res[key] = {"ms": round(t, 4), "min_ms": round(float(np.min(times[lay])), 4),
+                            "mray_s": round(W * H * S / (t * 1e-3) / 1e6, 1), "variant": None}
+                print(f"{key:>16}: median {t:.4f} ms  min {np.min(times[lay]):.4f} ms  "
+                      f"{W * H * S / (t * 1e-3) / 1e6:,.0f} Mray/s", flush=True)
+            r.set_layout_preference(0)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

@@ -46,23 +46,29 @@ struct Ctx {
     int device = 0;
     // volume (channel planes; see vr_internal.h Layout)
     int nx = 0, ny = 0, nz = 0;
-    uint8_t* d_planar = nullptr;
-    uint8_t* d_pad16 = nullptr;
+    uint8_t* d_planar = nullptr;   // canonical planes (LAYOUT_PLANAR)
+    uint8_t* d_fast = nullptr;     // one fast layout, built from d_planar
+    int fast_layout = 0;           // which one (0 = none)
+    size_t fast_plane_bytes = 0;
     // uniforms
     bool has_camera = false;
     float obj[48];
     float glob[36];
     vr_march_params march;
-    int layout_pref = 0;
+    int layout_pref = 0;           // 0 = auto (kDefaultFastLayout), else a Layout
 };
+
+constexpr int kDefaultFastLayout = LAYOUT_BRICK5;
 
 Ctx* as_ctx(void* p) { return static_cast<Ctx*>(p); }
 
 void free_volume(Ctx* c)
 {
     if (c->d_planar) (void)hipFree(c->d_planar);
-    if (c->d_pad16) (void)hipFree(c->d_pad16);
-    c->d_planar = c->d_pad16 = nullptr;
+    if (c->d_fast) (void)hipFree(c->d_fast);
+    c->d_planar = c->d_fast = nullptr;
+    c->fast_layout = 0;
+    c->fast_plane_bytes = 0;
     c->nx = c->ny = c->nz = 0;
 }
 
@@ -73,17 +79,42 @@ bool dims_ok(int nx, int ny, int nz)
     return pt < (1ll << 31);  // kernels index a plane with 32-bit ints
 }
 
+int wanted_fast_layout(const Ctx* c)
+{
+    const int want = c->layout_pref == 0 ? kDefaultFastLayout : c->layout_pref;
+    if (want == LAYOUT_PLANAR) return 0;
+    // 32-bit offsets inside the kernels: fall back to PAD16 if too large
+    if (layout_plane_bytes(want, c->nx, c->ny, c->nz) >= (1ull << 31)) return LAYOUT_PAD16;
+    return want;
+}
+
+// (Re)build the fast layout the preference asks for, from the planar planes.
+vr_status ensure_fast_layout(Ctx* c, hipStream_t s)
+{
+    const int want = c->d_planar ? wanted_fast_layout(c) : 0;
+    if (want == c->fast_layout) return VR_OK;
+    if (c->d_fast) (void)hipFree(c->d_fast);
+    c->d_fast = nullptr;
+    c->fast_layout = 0;
+    c->fast_plane_bytes = 0;
+    if (!want) return VR_OK;
+    const size_t pb = layout_plane_bytes(want, c->nx, c->ny, c->nz);
+    HIP_TRY(hipMalloc(&c->d_fast, 4 * pb));
+    HIP_TRY(launch_build_layout(want, c->d_planar, c->nx, c->ny, c->nz, c->d_fast, s));
+    c->fast_layout = want;
+    c->fast_plane_bytes = pb;
+    return VR_OK;
+}
+
 // Allocate the planes and repack from a device RGBA8 buffer.
 vr_status install_volume(Ctx* c, const uint8_t* d_rgba, int nx, int ny, int nz, hipStream_t s)
 {
     free_volume(c);
     const size_t total = (size_t)nx * ny * nz;
-    const size_t ptotal = (size_t)(nx + 2) * (ny + 2) * (nz + 2);
     HIP_TRY(hipMalloc(&c->d_planar, 4 * total));
-    HIP_TRY(hipMalloc(&c->d_pad16, 4 * ptotal + 16));
-    HIP_TRY(launch_repack(d_rgba, nx, ny, nz, c->d_planar, c->d_pad16, s));
+    HIP_TRY(launch_repack(d_rgba, nx, ny, nz, c->d_planar, s));
     c->nx = nx; c->ny = ny; c->nz = nz;
-    return VR_OK;
+    return ensure_fast_layout(c, s);
 }
 
 // Is clamp-to-edge identical to mirrored repeat for every tap of every ray?
@@ -130,11 +161,11 @@ vr_status make_plan(Ctx* c, MarchArgs* a, Plan* p)
     for (int t = 0; t < 4; ++t)
         for (int ax = 0; ax < 3; ++ax) a->tap_off[t][ax] = ms[ax * 4 + t] * m.tap_weight[t];
     const bool exact = clamp_is_exact(c, a->tap_off);
-    if (c->layout_pref == 1) {
+    if (!c->fast_layout) {
         p->layout = LAYOUT_PLANAR;
         p->wrap = exact ? WRAP_CLAMP : WRAP_MIRROR;
     } else if (exact) {
-        p->layout = LAYOUT_PAD16;
+        p->layout = c->fast_layout;
         p->wrap = WRAP_CLAMP;
     } else {
         p->layout = LAYOUT_PLANAR;
@@ -146,9 +177,17 @@ vr_status make_plan(Ctx* c, MarchArgs* a, Plan* p)
 
 const char* variant_name(const Plan& p)
 {
-    if (p.layout == LAYOUT_PAD16) return p.early ? "grid_pad16_clamp_early" : "grid_pad16_clamp";
-    if (p.wrap == WRAP_CLAMP) return p.early ? "grid_planar_clamp_early" : "grid_planar_clamp";
-    return p.early ? "grid_planar_mirror_early" : "grid_planar_mirror";
+    static const char* names[kNumLayouts][2] = {
+        {"none", "none"},
+        {"grid_planar_clamp", "grid_planar_clamp_early"},
+        {"grid_pad16_clamp", "grid_pad16_clamp_early"},
+        {"grid_brick5_clamp", "grid_brick5_clamp_early"},
+        {"grid_corner8_clamp", "grid_corner8_clamp_early"},
+        {"grid_quad_clamp", "grid_quad_clamp_early"},
+    };
+    if (p.layout == LAYOUT_PLANAR && p.wrap == WRAP_MIRROR)
+        return p.early ? "grid_planar_mirror_early" : "grid_planar_mirror";
+    return names[p.layout][p.early ? 1 : 0];
 }
 
 }  // namespace
@@ -397,9 +436,13 @@ int vr_band_rows_packed(int height, int band_rows, int band_stride, int band_fir
 
 vr_status vr_set_layout_preference(void* p, int pref)
 {
-    if (!p || pref < 0 || pref > 2) return fail(VR_ERR_INVALID, "vr_set_layout_preference: bad argument");
-    as_ctx(p)->layout_pref = pref;
-    return VR_OK;
+    if (!p || pref < 0 || pref >= kNumLayouts) return fail(VR_ERR_INVALID, "vr_set_layout_preference: bad argument");
+    Ctx* c = as_ctx(p);
+    HIP_TRY(hipSetDevice(c->device));
+    c->layout_pref = pref;
+    vr_status st = ensure_fast_layout(c, nullptr);
+    if (st == VR_OK && hipDeviceSynchronize() != hipSuccess) return fail(VR_ERR_HIP, "vr_set_layout_preference: sync");
+    return st;
 }
 
 const char* vr_kernel_variant(void* p)
@@ -454,11 +497,13 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
     make_plan(c, &a, &pl);
     a.nx = c->nx; a.ny = c->ny; a.nz = c->nz;
     a.fnx = (float)c->nx; a.fny = (float)c->ny; a.fnz = (float)c->nz;
-    if (pl.layout == LAYOUT_PAD16) {
-        a.vol = c->d_pad16;
+    if (pl.layout != LAYOUT_PLANAR) {
+        a.vol = c->d_fast;
+        a.plane_stride = (long long)c->fast_plane_bytes;
         a.prow = c->nx + 2;
         a.pslice = (c->nx + 2) * (c->ny + 2);
-        a.plane_stride = (long long)a.pslice * (c->nz + 2);
+        a.nbx = (c->nx >> 2) + 1;
+        a.nby = (c->ny >> 2) + 1;
     } else {
         a.vol = c->d_planar;
         a.plane_stride = (long long)c->nx * c->ny * c->nz;

@@ -7,15 +7,25 @@
 
 namespace vr {
 
-// Volume layouts in HBM.  Both keep one byte plane per
-// channel, so a tap reads only the channel it needs (frag.glsl:66-69 read
-// .x, .y, .z and .w from four different coordinates).
+// Volume layouts in HBM.  All keep one array per channel,
+// so a tap reads only the channel it needs (frag.glsl:66-69 read .x, .y, .z,
+// .w at four different coordinates).  LAYOUT_PLANAR is the canonical copy:
+// any wrap mode, and the source of every other layout.  The others are
+// indexed by the *padded* base texel a = floor(u*N - .5) + 1, clamped to
+// [0, N].  They store the clamp-to-edge values of the 2x2x2 trilinear
+// footprint, so a tap needs no index clamping.  They are exact wherever
+// clamp-to-edge equals mirrored repeat (checked per frame on the host).
 enum Layout : int {
-    LAYOUT_PLANAR = 1,   // plane[c][z][y][x], u8.  Any wrap.  8 byte loads per tap.
-    LAYOUT_PAD16 = 2,    // plane[c][z+1][y+1][x+1] with a 1-texel clamp apron.
-                         // A tap does 4 u16 loads (x-pairs) and needs no
-                         // index clamping.  Exact only where clamp == mirror.
+    LAYOUT_PLANAR = 1,   // u8 plane[z][y][x]; 8 byte loads per tap
+    LAYOUT_PAD16 = 2,    // u8 plane[z+1][y+1][x+1] with a 1-texel apron; 4 u16 loads
+    LAYOUT_BRICK5 = 3,   // 4^3 bricks + 1-texel apron = 5^3 B in one 128-B line;
+                         // a footprint never leaves its line; 4 u16 loads
+    LAYOUT_CORNER8 = 4,  // per base texel the 8 footprint bytes (u64), in 4^3
+                         // position bricks of 512 B; 1 dwordx2 load per tap
+    LAYOUT_QUAD = 5,     // per base texel the 2x2 xy quad (u32), 4x4x5 position
+                         // bricks of 320 B; 2 dword loads per tap
 };
+constexpr int kNumLayouts = 6;
 
 enum Wrap : int { WRAP_CLAMP = 0, WRAP_MIRROR = 1 };
 
@@ -36,6 +46,7 @@ struct MarchArgs {
     const uint8_t* vol;          // channel plane 0; plane c at vol + c*plane_stride
     long long plane_stride;
     int prow, pslice;            // PAD16: (nx+2), (nx+2)*(ny+2)
+    int nbx, nby;                // bricked layouts: bricks along x, y
     // target
     int width, height, band_rows, band_stride, band_first, out_rows;
     int tiles_x, tiles_y, num_tiles;
@@ -47,8 +58,11 @@ struct MarchArgs {
 
 // launchers (vr_march.hip / vr_volume.hip); return hipError_t
 hipError_t launch_march(const MarchArgs& a, int layout, int wrap, bool early, hipStream_t s);
-hipError_t launch_repack(const uint8_t* d_rgba, int nx, int ny, int nz, uint8_t* d_planar,
-                         uint8_t* d_pad16, hipStream_t s);
+hipError_t launch_repack(const uint8_t* d_rgba, int nx, int ny, int nz, uint8_t* d_planar, hipStream_t s);
+// Build a fast layout (PAD16/BRICK5/CORNER8/QUAD) from the planar planes.
+hipError_t launch_build_layout(int layout, const uint8_t* d_planar, int nx, int ny, int nz, uint8_t* d_out,
+                               hipStream_t s);
+size_t layout_plane_bytes(int layout, int nx, int ny, int nz);
 hipError_t launch_unpack(const uint8_t* d_planar, int nx, int ny, int nz, uint8_t* d_rgba,
                          hipStream_t s);
 hipError_t launch_noise(int kind, float* d_out, int x0, int y0, int z0, int nx, int ny, int nz,

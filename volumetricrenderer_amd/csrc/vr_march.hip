@@ -20,6 +20,19 @@ constexpr int kThreads = 256;       // 4 waves, each an 8x8 sub-tile
 __device__ __forceinline__ float lerp_(float a, float b, float t) { return fmaf(t, b - a, a); }
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return min(max(v, lo), hi); }
 
+// unaligned u16 load at a 32-bit byte offset from a wave-uniform base
+// (gfx950 runs in unaligned-access mode; one global_load_ushort)
+__device__ __forceinline__ unsigned ld_u16(const uint8_t* __restrict__ base, unsigned off)
+{
+    uint16_t v;
+    __builtin_memcpy(&v, base + off, 2);
+    return v;
+}
+
+// byte k of a dword as float (v_cvt_f32_ubyteK)
+template <int K>
+__device__ __forceinline__ float ubyte(unsigned v) { return (float)((v >> (8 * K)) & 0xffu); }
+
 // VK_SAMPLER_ADDRESS_MODE_MIRRORED_REPEAT on an integer texel index
 // (VulkanCore.cpp:683-685; Vulkan spec "Texel coordinate wrapping").
 __device__ __forceinline__ int mirror_(int i, int n)
@@ -59,22 +72,48 @@ __device__ __forceinline__ float tap(const uint8_t* __restrict__ pl, const March
     const float ax = gx - fx, ay = gy - fy, az = gz - fz;
     const int ix = (int)fx, iy = (int)fy, iz = (int)fz;
     float c000, c100, c010, c110, c001, c101, c011, c111;
-    if constexpr (LAYOUT == LAYOUT_PAD16) {
-        // padded index = texel index + 1; the apron holds the clamped edge,
-        // so (a0, a0+1) is always the clamp-to-edge pair, read as one u16.
-        const int a0 = clampi(ix + 1, 0, a.nx);
-        const int b0 = clampi(iy + 1, 0, a.ny);
-        const int c0 = clampi(iz + 1, 0, a.nz);
-        const uint8_t* p = pl + ((c0 * a.pslice) + b0 * a.prow + a0);
-        uint16_t v00, v10, v01, v11;
-        __builtin_memcpy(&v00, p, 2);
-        __builtin_memcpy(&v10, p + a.prow, 2);
-        __builtin_memcpy(&v01, p + a.pslice, 2);
-        __builtin_memcpy(&v11, p + a.pslice + a.prow, 2);
-        c000 = (float)(v00 & 0xffu); c100 = (float)(v00 >> 8);
-        c010 = (float)(v10 & 0xffu); c110 = (float)(v10 >> 8);
-        c001 = (float)(v01 & 0xffu); c101 = (float)(v01 >> 8);
-        c011 = (float)(v11 & 0xffu); c111 = (float)(v11 >> 8);
+    if constexpr (LAYOUT != LAYOUT_PLANAR) {
+        // padded base position: a0 = floor(u*N - .5) + 1, clamped to [0, N]
+        const int a0 = clampi(ix + 1, 0, a.nx), b0 = clampi(iy + 1, 0, a.ny), c0 = clampi(iz + 1, 0, a.nz);
+        if constexpr (LAYOUT == LAYOUT_PAD16) {
+            const unsigned off = __umul24((unsigned)c0, (unsigned)a.pslice) + __umul24((unsigned)b0, (unsigned)a.prow) + (unsigned)a0;
+            const unsigned v00 = ld_u16(pl, off), v10 = ld_u16(pl, off + a.prow);
+            const unsigned v01 = ld_u16(pl, off + a.pslice), v11 = ld_u16(pl, off + a.pslice + a.prow);
+            c000 = (float)(v00 & 0xffu); c100 = (float)(v00 >> 8);
+            c010 = (float)(v10 & 0xffu); c110 = (float)(v10 >> 8);
+            c001 = (float)(v01 & 0xffu); c101 = (float)(v01 >> 8);
+            c011 = (float)(v11 & 0xffu); c111 = (float)(v11 >> 8);
+        } else if constexpr (LAYOUT == LAYOUT_BRICK5) {
+            // 5x5x5 bytes of brick (a0>>2, b0>>2, c0>>2) hold the whole footprint
+            const unsigned brick = __umul24(__umul24((unsigned)(c0 >> 2), (unsigned)a.nby) + (unsigned)(b0 >> 2),
+                                            (unsigned)a.nbx) + (unsigned)(a0 >> 2);
+            const unsigned off = (brick << 7) + (unsigned)((c0 & 3) * 25 + (b0 & 3) * 5 + (a0 & 3));
+            const unsigned v00 = ld_u16(pl, off), v10 = ld_u16(pl, off + 5);
+            const unsigned v01 = ld_u16(pl, off + 25), v11 = ld_u16(pl, off + 30);
+            c000 = (float)(v00 & 0xffu); c100 = (float)(v00 >> 8);
+            c010 = (float)(v10 & 0xffu); c110 = (float)(v10 >> 8);
+            c001 = (float)(v01 & 0xffu); c101 = (float)(v01 >> 8);
+            c011 = (float)(v11 & 0xffu); c111 = (float)(v11 >> 8);
+        } else if constexpr (LAYOUT == LAYOUT_CORNER8) {
+            const unsigned brick = __umul24(__umul24((unsigned)(c0 >> 2), (unsigned)a.nby) + (unsigned)(b0 >> 2),
+                                            (unsigned)a.nbx) + (unsigned)(a0 >> 2);
+            const unsigned off = (brick << 9) + ((unsigned)(((c0 & 3) << 4) + ((b0 & 3) << 2) + (a0 & 3)) << 3);
+            const uint2 q = *reinterpret_cast<const uint2*>(pl + off);
+            c000 = ubyte<0>(q.x); c100 = ubyte<1>(q.x);
+            c010 = ubyte<2>(q.x); c110 = ubyte<3>(q.x);
+            c001 = ubyte<0>(q.y); c101 = ubyte<1>(q.y);
+            c011 = ubyte<2>(q.y); c111 = ubyte<3>(q.y);
+        } else {  // LAYOUT_QUAD: 4x4x5 positions x 4 B per brick; z0 quad then z1 quad at +64 B
+            const unsigned brick = __umul24(__umul24((unsigned)(c0 >> 2), (unsigned)a.nby) + (unsigned)(b0 >> 2),
+                                            (unsigned)a.nbx) + (unsigned)(a0 >> 2);
+            const unsigned off = __umul24(brick, 320u) + ((unsigned)(((c0 & 3) << 4) + ((b0 & 3) << 2) + (a0 & 3)) << 2);
+            const unsigned q0 = *reinterpret_cast<const unsigned*>(pl + off);
+            const unsigned q1 = *reinterpret_cast<const unsigned*>(pl + off + 64);
+            c000 = ubyte<0>(q0); c100 = ubyte<1>(q0);
+            c010 = ubyte<2>(q0); c110 = ubyte<3>(q0);
+            c001 = ubyte<0>(q1); c101 = ubyte<1>(q1);
+            c011 = ubyte<2>(q1); c111 = ubyte<3>(q1);
+        }
     } else {
         int i0, i1, j0, j1, k0, k1;
         if constexpr (WRAP == WRAP_CLAMP) {
@@ -232,6 +271,9 @@ hipError_t launch_march(const MarchArgs& a, int layout, int wrap, bool early, hi
 {
     if (a.num_tiles <= 0) return hipSuccess;
     if (layout == LAYOUT_PAD16) return launch_lw<LAYOUT_PAD16, WRAP_CLAMP>(a, early, s);
+    if (layout == LAYOUT_BRICK5) return launch_lw<LAYOUT_BRICK5, WRAP_CLAMP>(a, early, s);
+    if (layout == LAYOUT_CORNER8) return launch_lw<LAYOUT_CORNER8, WRAP_CLAMP>(a, early, s);
+    if (layout == LAYOUT_QUAD) return launch_lw<LAYOUT_QUAD, WRAP_CLAMP>(a, early, s);
     if (wrap == WRAP_CLAMP) return launch_lw<LAYOUT_PLANAR, WRAP_CLAMP>(a, early, s);
     return launch_lw<LAYOUT_PLANAR, WRAP_MIRROR>(a, early, s);
 }
