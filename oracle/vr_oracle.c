@@ -412,12 +412,14 @@ static inline float texel(const uint8_t* v, int nx, int ny, int c, int i, int j,
     return (float)v[4 * (((size_t)k * ny + j) * nx + i) + c];
 }
 
-float vro_sample(const uint8_t* v, int nx, int ny, int nz, int c, float px, float py, float pz)
+/* One tap at padded texel coordinate g = u*N - 0.5 + 1 (so that floor(g) is
+ * the base texel + 1): weight = fract(g) clamped below 1 (v_fract_f32
+ * semantics), base texel floor(g) - 1, mirrored repeat on both indices.   */
+static float sample_g(const uint8_t* v, int nx, int ny, int nz, int c, float gx, float gy, float gz)
 {
-    float gx = fmaf(px, (float)nx, -0.5f), gy = fmaf(py, (float)ny, -0.5f), gz = fmaf(pz, (float)nz, -0.5f);
     float fx = floorf(gx), fy = floorf(gy), fz = floorf(gz);
-    float ax = gx - fx, ay = gy - fy, az = gz - fz;
-    int ix = (int)fx, iy = (int)fy, iz = (int)fz;
+    float ax = fminf(gx - fx, 0x1.fffffep-1f), ay = fminf(gy - fy, 0x1.fffffep-1f), az = fminf(gz - fz, 0x1.fffffep-1f);
+    int ix = (int)fx - 1, iy = (int)fy - 1, iz = (int)fz - 1;
     int i0 = vro_mirror(ix, nx), i1 = vro_mirror(ix + 1, nx);
     int j0 = vro_mirror(iy, ny), j1 = vro_mirror(iy + 1, ny);
     int k0 = vro_mirror(iz, nz), k1 = vro_mirror(iz + 1, nz);
@@ -429,6 +431,12 @@ float vro_sample(const uint8_t* v, int nx, int ny, int nz, int c, float px, floa
     float x01 = lerpf_(c001, c101, ax), x11 = lerpf_(c011, c111, ax);
     float y0 = lerpf_(x00, x10, ay), y1 = lerpf_(x01, x11, ay);
     return lerpf_(y0, y1, az) * (1.0f / 255.0f);
+}
+
+float vro_sample(const uint8_t* v, int nx, int ny, int nz, int c, float px, float py, float pz)
+{
+    return sample_g(v, nx, ny, nz, c, fmaf(px, (float)nx, 0.5f), fmaf(py, (float)ny, 0.5f),
+                    fmaf(pz, (float)nz, 0.5f));
 }
 
 /* exp for x <= 0, fma-only polynomial (Cephes expf coefficients): an exactly
@@ -458,12 +466,15 @@ float vro_expf(float x)
  * ==================================================================== */
 typedef struct {
     float step_size, box_min[3], box_range[3];
-    float tap_off[4][3];
+    float tap_S[4][3], tap_T[4][3]; /* padded texel coordinate g = fma(P, S, T) */
     float acc_limit;   /* early-out threshold on acc, +inf when off */
 } march_consts;
 
-static void make_consts(const vro_march* m, const float* glob36, march_consts* k)
+/* tap t at ray point P samples u = P*s_t + o_t (frag.glsl:66-69); in padded
+ * texel space g = u*N + 0.5 = fma(P, s_t*N, o_t*N + 0.5).                   */
+static void make_consts(const vro_march* m, const float* glob36, int nx, int ny, int nz, march_consts* k)
 {
+    const float dims[3] = {(float)nx, (float)ny, (float)nz};
     k->step_size = (1.0f / (float)m->max_steps) * m->step_scale;          /* :42 */
     for (int a = 0; a < 3; ++a) {
         k->box_min[a] = m->box_min[a];
@@ -471,7 +482,11 @@ static void make_consts(const vro_march* m, const float* glob36, march_consts* k
     }
     const float* ms = glob36 + 20;  /* MediaScroll, column-major; tap t uses row t */
     for (int t = 0; t < 4; ++t)
-        for (int a = 0; a < 3; ++a) k->tap_off[t][a] = ms[a * 4 + t] * m->tap_weight[t];
+        for (int a = 0; a < 3; ++a) {
+            const float off = ms[a * 4 + t] * m->tap_weight[t];
+            k->tap_S[t][a] = m->tap_scale[t] * dims[a];
+            k->tap_T[t][a] = off * dims[a] + 0.5f;
+        }
     if (m->early_out > 0.0f)
         k->acc_limit = (float)(-log((double)m->early_out) / ((double)m->density * (double)k->step_size));
     else
@@ -523,7 +538,7 @@ int vro_step_counts(const float* obj48, const float* glob36, const vro_march* m,
     ray_basis b;
     march_consts k;
     if (make_basis(obj48, glob36, width, height, &b)) return 1;
-    make_consts(m, glob36, &k);
+    make_consts(m, glob36, 1, 1, 1, &k);
 #pragma omp parallel for schedule(dynamic, 4)
     for (int y = 0; y < height; ++y)
         for (int x = 0; x < width; ++x) {
@@ -564,7 +579,7 @@ int vro_render(const uint8_t* vol, int nx, int ny, int nz,
     march_consts k;
     if (m->max_steps <= 0 || nx <= 0 || ny <= 0 || nz <= 0 || width <= 0 || height <= 0) return 2;
     if (make_basis(obj48, glob36, width, height, &b)) return 1;
-    make_consts(m, glob36, &k);
+    make_consts(m, glob36, nx, ny, nz, &k);
     if (band_rows <= 0) { band_rows = height; band_stride = 1; band_first = 0; }
     if (band_stride <= 0) band_stride = 1;
     const int nbands = (height + band_rows - 1) / band_rows;
@@ -591,12 +606,10 @@ int vro_render(const uint8_t* vol, int nx, int ny, int nz,
             int i = 0;
             for (; i < n; ++i) {                                              /* :57-75 */
                 float s[4];
-                for (int t = 0; t < 4; ++t) {
-                    float qx = fmaf(P[0], m->tap_scale[t], k.tap_off[t][0]);
-                    float qy = fmaf(P[1], m->tap_scale[t], k.tap_off[t][1]);
-                    float qz = fmaf(P[2], m->tap_scale[t], k.tap_off[t][2]);
-                    s[t] = vro_sample(vol, nx, ny, nz, t, qx, qy, qz);
-                }
+                for (int t = 0; t < 4; ++t)
+                    s[t] = sample_g(vol, nx, ny, nz, t, fmaf(P[0], k.tap_S[t][0], k.tap_T[t][0]),
+                                    fmaf(P[1], k.tap_S[t][1], k.tap_T[t][1]),
+                                    fmaf(P[2], k.tap_S[t][2], k.tap_T[t][2]));
                 float cur = ((s[0] * s[1]) * (s[2] + s[3])) * m->scale;      /* :71 */
                 acc = acc + cur;                                             /* :73 */
                 P[0] = P[0] + st[0]; P[1] = P[1] + st[1]; P[2] = P[2] + st[2]; /* :74 */

@@ -117,25 +117,38 @@ vr_status install_volume(Ctx* c, const uint8_t* d_rgba, int nx, int ny, int nz, 
     return ensure_fast_layout(c, s);
 }
 
+// Tap constants of spec v2: tap t samples padded texel
+// coordinate g = fma(P, S, T) with S = s_t*N and T = o_t*N + 0.5, where
+// o_t = MediaScroll row t * weight_t (frag.glsl:66-69).
+void tap_constants(const Ctx* c, float S[4][3], float T[4][3])
+{
+    const vr_march_params& m = c->march;
+    const float* ms = c->glob + 20;  // MediaScroll, column-major; tap t reads row t
+    const float dims[3] = {(float)c->nx, (float)c->ny, (float)c->nz};
+    for (int t = 0; t < 4; ++t)
+        for (int ax = 0; ax < 3; ++ax) {
+            const float off = ms[ax * 4 + t] * m.tap_weight[t];
+            S[t][ax] = m.tap_scale[t] * dims[ax];
+            T[t][ax] = off * dims[ax] + 0.5f;
+        }
+}
+
 // Is clamp-to-edge identical to mirrored repeat for every tap of every ray?
-// Both agree while each tap's base texel floor(u*N - .5) stays in [-1, N-1],
-// i.e. u in [-.5/N, 1 + .5/N).  Ray points P lie in [0,1]^3 (box entry/exit
-// normalised, frag.glsl:49-54) up to rounding drift bounded by `slack`.
-bool clamp_is_exact(const Ctx* c, const float tap_off[4][3])
+// Both agree while the base texel floor(g) - 1 stays in [-1, N-1], i.e.
+// g in [0, N+1).  Ray points P lie in [0,1]^3 (box entry/exit normalised,
+// frag.glsl:49-54) up to rounding drift bounded by `slack`.
+bool clamp_is_exact(const Ctx* c, const float S[4][3], const float T[4][3])
 {
     const vr_march_params& m = c->march;
     const double slack = (double)(m.max_steps + 16) * 1.2e-7;
     const int dims[3] = {c->nx, c->ny, c->nz};
-    for (int t = 0; t < 4; ++t) {
-        const double s = m.tap_scale[t];
+    for (int t = 0; t < 4; ++t)
         for (int a = 0; a < 3; ++a) {
-            const double o = tap_off[t][a];
-            const double lo = std::fmin(o, s + o) - std::fabs(s) * slack - 1e-6;
-            const double hi = std::fmax(o, s + o) + std::fabs(s) * slack + 1e-6;
-            const double h = 0.5 / dims[a];
-            if (!(lo >= -h && hi < 1.0 + h)) return false;
+            const double s = S[t][a], o = T[t][a];
+            const double margin = std::fabs(s) * slack + (dims[a] + 2.0) * 2.4e-7 + 1e-6;
+            const double lo = std::fmin(o, s + o) - margin, hi = std::fmax(o, s + o) + margin;
+            if (!(lo >= 0.0 && hi < dims[a] + 1.0)) return false;
         }
-    }
     return true;
 }
 
@@ -157,10 +170,8 @@ struct Plan {
 vr_status make_plan(Ctx* c, MarchArgs* a, Plan* p)
 {
     const vr_march_params& m = c->march;
-    const float* ms = c->glob + 20;  // MediaScroll, column-major; tap t reads row t
-    for (int t = 0; t < 4; ++t)
-        for (int ax = 0; ax < 3; ++ax) a->tap_off[t][ax] = ms[ax * 4 + t] * m.tap_weight[t];
-    const bool exact = clamp_is_exact(c, a->tap_off);
+    tap_constants(c, a->tap_S, a->tap_T);
+    const bool exact = clamp_is_exact(c, a->tap_S, a->tap_T);
     if (!c->fast_layout) {
         p->layout = LAYOUT_PLANAR;
         p->wrap = exact ? WRAP_CLAMP : WRAP_MIRROR;
@@ -492,11 +503,9 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
     a.acc_limit = m.early_out > 0.0f
                       ? (float)(-std::log((double)m.early_out) / ((double)m.density * (double)a.step_size))
                       : INFINITY;
-    for (int k = 0; k < 4; ++k) a.tap_scale[k] = m.tap_scale[k];
     Plan pl{};
     make_plan(c, &a, &pl);
     a.nx = c->nx; a.ny = c->ny; a.nz = c->nz;
-    a.fnx = (float)c->nx; a.fny = (float)c->ny; a.fnz = (float)c->nz;
     if (pl.layout != LAYOUT_PLANAR) {
         a.vol = c->d_fast;
         a.plane_stride = (long long)c->fast_plane_bytes;
@@ -518,7 +527,7 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
     a.out_rows = band_rows_packed(t->height, a.band_rows, a.band_stride, a.band_first);
     a.tiles_x = (t->width + 15) / 16;
     a.tiles_y = (a.out_rows + 15) / 16;
-    a.num_tiles = a.tiles_x * a.tiles_y;
+    a.num_blocks = 8 * ((a.tiles_y + 7) / 8) * a.tiles_x;
     a.out = t->pixels;
     a.pitch = (long long)pitch;
     a.format = t->format;

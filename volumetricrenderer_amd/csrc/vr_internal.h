@@ -38,18 +38,18 @@ struct MarchArgs {
     float box_min[3], box_max[3], box_range[3];
     float step_size, density, scale, acc_limit;
     int max_steps;
-    float tap_scale[4];
-    float tap_off[4][3];
+    // tap t samples padded texel coordinate g = fma(P, tap_S, tap_T)
+    // (= u*N + 0.5 with u = P*s_t + o_t, frag.glsl:66-69)
+    float tap_S[4][3], tap_T[4][3];
     // volume
     int nx, ny, nz;
-    float fnx, fny, fnz;
     const uint8_t* vol;          // channel plane 0; plane c at vol + c*plane_stride
     long long plane_stride;
     int prow, pslice;            // PAD16: (nx+2), (nx+2)*(ny+2)
     int nbx, nby;                // bricked layouts: bricks along x, y
     // target
     int width, height, band_rows, band_stride, band_first, out_rows;
-    int tiles_x, tiles_y, num_tiles;
+    int tiles_x, tiles_y, num_blocks;   // 16x16 tiles; blocks = 8 XCD row-groups
     void* out;
     long long pitch;
     int format;

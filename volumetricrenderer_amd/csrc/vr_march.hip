@@ -19,6 +19,13 @@ constexpr int kThreads = 256;       // 4 waves, each an 8x8 sub-tile
 
 __device__ __forceinline__ float lerp_(float a, float b, float t) { return fmaf(t, b - a, a); }
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return min(max(v, lo), hi); }
+// clamp to [0, hi] in one v_med3_i32
+__device__ __forceinline__ int clamp0(int v, int hi)
+{
+    int r;
+    asm("v_med3_i32 %0, %1, 0, %2" : "=v"(r) : "v"(v), "v"(hi));
+    return r;
+}
 
 // unaligned u16 load at a 32-bit byte offset from a wave-uniform base
 // (gfx950 runs in unaligned-access mode; one global_load_ushort)
@@ -28,6 +35,17 @@ __device__ __forceinline__ unsigned ld_u16(const uint8_t* __restrict__ base, uns
     __builtin_memcpy(&v, base + off, 2);
     return v;
 }
+
+// floor(x) as int in one instruction, and x - floor(x) clamped below 1.0
+// (v_fract_f32).  The spec defines the tap weight as
+// fminf(g - floorf(g), 0x1.fffffep-1f), which is what v_fract_f32 returns.
+__device__ __forceinline__ int cvt_flr(float x)
+{
+    int r;
+    asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+__device__ __forceinline__ float fract_(float x) { return __builtin_amdgcn_fractf(x); }
 
 // byte k of a dword as float (v_cvt_f32_ubyteK)
 template <int K>
@@ -61,20 +79,19 @@ __device__ __forceinline__ float spec_expf(float x)
     return p * __int_as_float(((int)k + 127) << 23);
 }
 
-// One trilinear tap of one channel plane: Vulkan LINEAR filter, LOD 0.
-// texel space u*N - 0.5, floor / frac, then 8 texels and 7 lerps.
+// One trilinear tap of one channel: Vulkan LINEAR filter, LOD 0, at padded
+// texel coordinate g = u*N - 0.5 + 1.  floor(g) is the padded base texel,
+// fract(g) the weight.  Then 8 texels and 7 lerps.
 template <int LAYOUT, int WRAP>
 __device__ __forceinline__ float tap(const uint8_t* __restrict__ pl, const MarchArgs& a,
-                                     float qx, float qy, float qz)
+                                     float gx, float gy, float gz)
 {
-    const float gx = fmaf(qx, a.fnx, -0.5f), gy = fmaf(qy, a.fny, -0.5f), gz = fmaf(qz, a.fnz, -0.5f);
-    const float fx = floorf(gx), fy = floorf(gy), fz = floorf(gz);
-    const float ax = gx - fx, ay = gy - fy, az = gz - fz;
-    const int ix = (int)fx, iy = (int)fy, iz = (int)fz;
+    const float ax = fract_(gx), ay = fract_(gy), az = fract_(gz);
+    const int px = cvt_flr(gx), py = cvt_flr(gy), pz = cvt_flr(gz);
     float c000, c100, c010, c110, c001, c101, c011, c111;
     if constexpr (LAYOUT != LAYOUT_PLANAR) {
-        // padded base position: a0 = floor(u*N - .5) + 1, clamped to [0, N]
-        const int a0 = clampi(ix + 1, 0, a.nx), b0 = clampi(iy + 1, 0, a.ny), c0 = clampi(iz + 1, 0, a.nz);
+        // padded base position, clamped to [0, N]
+        const int a0 = clamp0(px, a.nx), b0 = clamp0(py, a.ny), c0 = clamp0(pz, a.nz);
         if constexpr (LAYOUT == LAYOUT_PAD16) {
             const unsigned off = __umul24((unsigned)c0, (unsigned)a.pslice) + __umul24((unsigned)b0, (unsigned)a.prow) + (unsigned)a0;
             const unsigned v00 = ld_u16(pl, off), v10 = ld_u16(pl, off + a.prow);
@@ -115,6 +132,7 @@ __device__ __forceinline__ float tap(const uint8_t* __restrict__ pl, const March
             c011 = ubyte<2>(q1); c111 = ubyte<3>(q1);
         }
     } else {
+        const int ix = px - 1, iy = py - 1, iz = pz - 1;
         int i0, i1, j0, j1, k0, k1;
         if constexpr (WRAP == WRAP_CLAMP) {
             i0 = clampi(ix, 0, a.nx - 1); i1 = clampi(ix + 1, 0, a.nx - 1);
@@ -138,20 +156,17 @@ __device__ __forceinline__ float tap(const uint8_t* __restrict__ pl, const March
     return lerp_(y0, y1, az) * (1.0f / 255.0f);
 }
 
-// Bijective XCD-aware block remap (cdna_hip_programming.md T1): consecutive
-// tiles land on one XCD, so one XCD's L2 serves a compact image region and
-// hence a compact region of the volume.
-__device__ __forceinline__ int xcd_remap(int b, int nb)
-{
-    const int q = nb >> 3, r = nb & 7, xcd = b & 7, idx = b >> 3;
-    return xcd < r ? xcd * (q + 1) + idx : r * (q + 1) + (xcd - r) * q + idx;
-}
-
 template <int LAYOUT, int WRAP, bool EARLY>
 __global__ __launch_bounds__(kThreads) void march_grid(const MarchArgs a)
 {
-    const int tile = xcd_remap(blockIdx.x, a.num_tiles);
-    const int tx = tile % a.tiles_x, ty = tile / a.tiles_x;
+    // Tile rows are dealt to XCDs round-robin: XCD x (= blockIdx % 8 under
+    // the observed dispatch, a speed-only assumption) walks tile rows
+    // x, x+8, ...  Work is balanced (the silhouette is centred) and
+    // horizontally adjacent tiles share one L2.
+    const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+    const int k = j / a.tiles_x, tx = j - k * a.tiles_x;
+    const int ty = xcd + 8 * k;
+    if (ty >= a.tiles_y) return;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int x = tx * kTile + (wave & 1) * 8 + (lane & 7);
     const int orow = ty * kTile + (wave >> 1) * 8 + (lane >> 3);
@@ -207,18 +222,18 @@ __global__ __launch_bounds__(kThreads) void march_grid(const MarchArgs a)
     float acc = 0.0f;
     int i = 0;
     for (; i < n; ++i) {
-        const float t0 = tap<LAYOUT, WRAP>(pl0, a, fmaf(P0, a.tap_scale[0], a.tap_off[0][0]),
-                                           fmaf(P1, a.tap_scale[0], a.tap_off[0][1]),
-                                           fmaf(P2, a.tap_scale[0], a.tap_off[0][2]));
-        const float t1 = tap<LAYOUT, WRAP>(pl1, a, fmaf(P0, a.tap_scale[1], a.tap_off[1][0]),
-                                           fmaf(P1, a.tap_scale[1], a.tap_off[1][1]),
-                                           fmaf(P2, a.tap_scale[1], a.tap_off[1][2]));
-        const float t2 = tap<LAYOUT, WRAP>(pl2, a, fmaf(P0, a.tap_scale[2], a.tap_off[2][0]),
-                                           fmaf(P1, a.tap_scale[2], a.tap_off[2][1]),
-                                           fmaf(P2, a.tap_scale[2], a.tap_off[2][2]));
-        const float t3 = tap<LAYOUT, WRAP>(pl3, a, fmaf(P0, a.tap_scale[3], a.tap_off[3][0]),
-                                           fmaf(P1, a.tap_scale[3], a.tap_off[3][1]),
-                                           fmaf(P2, a.tap_scale[3], a.tap_off[3][2]));
+        const float t0 = tap<LAYOUT, WRAP>(pl0, a, fmaf(P0, a.tap_S[0][0], a.tap_T[0][0]),
+                                           fmaf(P1, a.tap_S[0][1], a.tap_T[0][1]),
+                                           fmaf(P2, a.tap_S[0][2], a.tap_T[0][2]));
+        const float t1 = tap<LAYOUT, WRAP>(pl1, a, fmaf(P0, a.tap_S[1][0], a.tap_T[1][0]),
+                                           fmaf(P1, a.tap_S[1][1], a.tap_T[1][1]),
+                                           fmaf(P2, a.tap_S[1][2], a.tap_T[1][2]));
+        const float t2 = tap<LAYOUT, WRAP>(pl2, a, fmaf(P0, a.tap_S[2][0], a.tap_T[2][0]),
+                                           fmaf(P1, a.tap_S[2][1], a.tap_T[2][1]),
+                                           fmaf(P2, a.tap_S[2][2], a.tap_T[2][2]));
+        const float t3 = tap<LAYOUT, WRAP>(pl3, a, fmaf(P0, a.tap_S[3][0], a.tap_T[3][0]),
+                                           fmaf(P1, a.tap_S[3][1], a.tap_T[3][1]),
+                                           fmaf(P2, a.tap_S[3][2], a.tap_T[3][2]));
         acc = acc + ((t0 * t1) * (t2 + t3)) * a.scale;                               // :71-73
         P0 = P0 + s0; P1 = P1 + s1; P2 = P2 + s2;                                     // :74
         if constexpr (EARLY) {
@@ -257,7 +272,7 @@ __global__ __launch_bounds__(kThreads) void march_grid(const MarchArgs a)
 template <int L, int W>
 hipError_t launch_lw(const MarchArgs& a, bool early, hipStream_t s)
 {
-    dim3 grid(a.num_tiles), block(kThreads);
+    dim3 grid(a.num_blocks), block(kThreads);
     if (early)
         hipLaunchKernelGGL((march_grid<L, W, true>), grid, block, 0, s, a);
     else
@@ -269,7 +284,7 @@ hipError_t launch_lw(const MarchArgs& a, bool early, hipStream_t s)
 
 hipError_t launch_march(const MarchArgs& a, int layout, int wrap, bool early, hipStream_t s)
 {
-    if (a.num_tiles <= 0) return hipSuccess;
+    if (a.num_blocks <= 0) return hipSuccess;
     if (layout == LAYOUT_PAD16) return launch_lw<LAYOUT_PAD16, WRAP_CLAMP>(a, early, s);
     if (layout == LAYOUT_BRICK5) return launch_lw<LAYOUT_BRICK5, WRAP_CLAMP>(a, early, s);
     if (layout == LAYOUT_CORNER8) return launch_lw<LAYOUT_CORNER8, WRAP_CLAMP>(a, early, s);
