@@ -119,6 +119,20 @@ def test_every_layout_bitexact(r, oracle, vol128, layout, name):
         r.set_layout_preference(0)
 
 
+@pytest.mark.parametrize("schedule,wps", [(0, 4), (1, 1), (1, 3), (1, 8)])
+def test_schedules_bitexact(r, oracle, vol128, schedule, wps):
+    r.set_option("schedule", schedule)
+    r.set_option("waves_per_simd", wps)
+    try:
+        for W, H, band in [(333, 187, {}), (640, 360, dict(band_rows=16, band_stride=3, band_first=2))]:
+            img, ref, c, s = render_both(r, oracle, vol128, W, H, **band)
+            assert_exact(img, ref)
+            assert c == s
+    finally:
+        r.set_option("schedule", 1)
+        r.set_option("waves_per_simd", 4)
+
+
 @pytest.mark.parametrize("dims", [(37, 50, 23), (1, 1, 1), (2, 3, 5), (129, 64, 96)])
 def test_odd_volume_dims(r, oracle, dims):
     rng = np.random.default_rng(sum(dims))

@@ -23,6 +23,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--sizes", default="128,512")
     ap.add_argument("--layouts", default="2,3,4,5,1")
+    ap.add_argument("--variants", default="",
+                    help="comma list of layout:schedule:waves_per_simd, overrides --layouts")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--frames", type=int, default=10)
     ap.add_argument("--width", type=int, default=1920)
@@ -30,7 +32,19 @@ def main():
     ap.add_argument("--steps", type=int, default=128)
     args = ap.parse_args()
     W, H, S = args.width, args.height, args.steps
-    layouts = [int(x) for x in args.layouts.split(",")]
+    if args.variants:
+        layouts = [tuple(int(v) for v in x.split(":")) for x in args.variants.split(",")]
+    else:
+        layouts = [(int(x), 1, 4) for x in args.layouts.split(",")]
+
+    def apply(r, lay):
+        r.set_layout_preference(lay[0])
+        r.set_option("schedule", lay[1])
+        if lay[2] > 0:
+            r.set_option("waves_per_simd", lay[2])
+
+    def name(lay):
+        return f"{NAMES[lay[0]]}/{'queue' + str(lay[2]) if lay[1] else 'static'}"
     res = {}
     with vr.Renderer(0) as r:
         osd, gsd = vr.reference_shader_data(W / H)
@@ -45,14 +59,14 @@ def main():
             ref = None
             times = {lay: [] for lay in layouts}
             for lay in layouts:  # build + parity
-                r.set_layout_preference(lay)
+                apply(r, lay)
                 img = r.render(W, H, vr.FMT_RGBA8_UNORM, out=out).cpu().numpy()
                 if ref is None:
                     ref = img
                 assert np.array_equal(img, ref), f"layout {lay} differs at N={n}"
             for _ in range(args.rounds):
                 for lay in layouts:
-                    r.set_layout_preference(lay)
+                    apply(r, lay)
                     r.render(W, H, vr.FMT_RGBA8_UNORM, out=out)
                     ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.frames + 1)]
                     ev[0].record()
@@ -63,10 +77,10 @@ def main():
                     times[lay] += [ev[k].elapsed_time(ev[k + 1]) for k in range(args.frames)]
             for lay in layouts:
                 t = float(np.median(times[lay]))
-                key = f"N{n}_{NAMES[lay]}"
+                key = f"N{n}_{name(lay)}"
                 res[key] = {"ms": round(t, 4), "min_ms": round(float(np.min(times[lay])), 4),
                             "mray_s": round(W * H * S / (t * 1e-3) / 1e6, 1), "variant": None}
-                print(f"{key:>16}: median {t:.4f} ms  min {np.min(times[lay]):.4f} ms  "
+                print(f"{key:>24}: median {t:.4f} ms  min {np.min(times[lay]):.4f} ms  "
                       f"{W * H * S / (t * 1e-3) / 1e6:,.0f} Mray/s", flush=True)
             r.set_layout_preference(0)
     print(json.dumps(res))

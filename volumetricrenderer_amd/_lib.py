@@ -106,9 +106,11 @@ _SIGS = {
     "vr_band_rows_packed": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "vr_kernel_variant": (ctypes.c_char_p, [_vp]),
     "vr_set_layout_preference": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "vr_set_option": (ctypes.c_int, [_vp, ctypes.c_char_p, ctypes.c_int]),
+    "vr_get_option": (ctypes.c_int, [_vp, ctypes.c_char_p]),
 }
 # functions whose int return is a value, not a vr_status
-_VALUE_RETURNS = {"vr_abi_version", "vr_band_rows_packed"}
+_VALUE_RETURNS = {"vr_abi_version", "vr_band_rows_packed", "vr_get_option"}
 
 _lib = None
 

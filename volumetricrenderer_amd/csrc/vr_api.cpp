@@ -42,6 +42,9 @@ vr_status fail(vr_status st, const char* fmt, ...)
                         #expr, hipGetErrorString(e_), __FILE__, __LINE__);                   \
     } while (0)
 
+constexpr int kDefaultSchedule = 1;      // 1 = persistent queue, 0 = static tiles
+constexpr int kDefaultWavesPerSimd = 4;
+
 struct Ctx {
     int device = 0;
     // volume (channel planes; see vr_internal.h Layout)
@@ -56,6 +59,10 @@ struct Ctx {
     float glob[36];
     vr_march_params march;
     int layout_pref = 0;           // 0 = auto (kDefaultFastLayout), else a Layout
+    // schedule of the march kernel (vr_set_option "schedule", "waves_per_simd")
+    int schedule = kDefaultSchedule;
+    int waves_per_simd = kDefaultWavesPerSimd;
+    int* d_heads = nullptr;        // 8 queue heads (+ padding), zeroed per launch
 };
 
 constexpr int kDefaultFastLayout = LAYOUT_BRICK5;
@@ -245,6 +252,10 @@ vr_status vr_create(int device, void** out)
     if (!c) return fail(VR_ERR_OOM, "vr_create: host allocation failed");
     c->device = device;
     vr_march_defaults(&c->march);
+    if (hipMalloc(&c->d_heads, 64) != hipSuccess) {
+        delete c;
+        return fail(VR_ERR_OOM, "vr_create: queue heads");
+    }
     *out = c;
     return VR_OK;
 }
@@ -255,6 +266,7 @@ vr_status vr_destroy(void* p)
     Ctx* c = as_ctx(p);
     (void)hipSetDevice(c->device);
     free_volume(c);
+    if (c->d_heads) (void)hipFree(c->d_heads);
     delete c;
     return VR_OK;
 }
@@ -456,6 +468,36 @@ vr_status vr_set_layout_preference(void* p, int pref)
     return st;
 }
 
+vr_status vr_set_option(void* p, const char* name, int value)
+{
+    if (!p || !name) return fail(VR_ERR_INVALID, "vr_set_option: null argument");
+    Ctx* c = as_ctx(p);
+    const std::string n(name);
+    if (n == "layout") return vr_set_layout_preference(p, value);
+    if (n == "schedule") {
+        if (value < 0 || value > 1) return fail(VR_ERR_INVALID, "vr_set_option: schedule is 0 (static) or 1 (queue)");
+        c->schedule = value;
+        return VR_OK;
+    }
+    if (n == "waves_per_simd") {
+        if (value < 1 || value > 8) return fail(VR_ERR_INVALID, "vr_set_option: waves_per_simd in [1, 8]");
+        c->waves_per_simd = value;
+        return VR_OK;
+    }
+    return fail(VR_ERR_INVALID, "vr_set_option: unknown option '%s'", name);
+}
+
+int vr_get_option(void* p, const char* name)
+{
+    if (!p || !name) return -1;
+    const Ctx* c = as_ctx(p);
+    const std::string n(name);
+    if (n == "layout") return c->fast_layout ? c->fast_layout : LAYOUT_PLANAR;
+    if (n == "schedule") return c->schedule;
+    if (n == "waves_per_simd") return c->waves_per_simd;
+    return -1;
+}
+
 const char* vr_kernel_variant(void* p)
 {
     if (!p) return "none";
@@ -533,7 +575,8 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
     a.format = t->format;
     a.step_counter = reinterpret_cast<unsigned long long*>(t->step_counter);
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(launch_march(a, pl.layout, pl.wrap, pl.early, static_cast<hipStream_t>(stream)));
+    const Schedule sc{c->schedule == 1, c->waves_per_simd, c->d_heads};
+    HIP_TRY(launch_march(a, pl.layout, pl.wrap, pl.early, sc, static_cast<hipStream_t>(stream)));
     return VR_OK;
 }
 

@@ -56,8 +56,15 @@ struct MarchArgs {
     unsigned long long* step_counter;
 };
 
+// How the march kernel maps tiles to waves.
+struct Schedule {
+    bool queue;            // false: static 16x16 tile per workgroup
+    int waves_per_simd;    // queue: persistent waves per SIMD (grid = 256 CUs x this)
+    int* heads;            // queue: 8 device ints, zeroed before each launch
+};
+
 // launchers (vr_march.hip / vr_volume.hip); return hipError_t
-hipError_t launch_march(const MarchArgs& a, int layout, int wrap, bool early, hipStream_t s);
+hipError_t launch_march(const MarchArgs& a, int layout, int wrap, bool early, const Schedule& sc, hipStream_t s);
 hipError_t launch_repack(const uint8_t* d_rgba, int nx, int ny, int nz, uint8_t* d_planar, hipStream_t s);
 // Build a fast layout (PAD16/BRICK5/CORNER8/QUAD) from the planar planes.
 hipError_t launch_build_layout(int layout, const uint8_t* d_planar, int nx, int ny, int nz, uint8_t* d_out,

@@ -156,20 +156,11 @@ __device__ __forceinline__ float tap(const uint8_t* __restrict__ pl, const March
     return lerp_(y0, y1, az) * (1.0f / 255.0f);
 }
 
+// One ray: ray setup (frag.glsl:36-55), the march (:57-75), the epilogue
+// (:76-80) and the store.  Returns the executed steps (0 if uncovered).
 template <int LAYOUT, int WRAP, bool EARLY>
-__global__ __launch_bounds__(kThreads) void march_grid(const MarchArgs a)
+__device__ __forceinline__ unsigned march_pixel(const MarchArgs& a, int x, int orow)
 {
-    // Tile rows are dealt to XCDs round-robin: XCD x (= blockIdx % 8 under
-    // the observed dispatch, a speed-only assumption) walks tile rows
-    // x, x+8, ...  Work is balanced (the silhouette is centred) and
-    // horizontally adjacent tiles share one L2.
-    const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
-    const int k = j / a.tiles_x, tx = j - k * a.tiles_x;
-    const int ty = xcd + 8 * k;
-    if (ty >= a.tiles_y) return;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int x = tx * kTile + (wave & 1) * 8 + (lane & 7);
-    const int orow = ty * kTile + (wave >> 1) * 8 + (lane >> 3);
     const bool inside = x < a.width && orow < a.out_rows;
     int y = 0;
     if (inside) {
@@ -242,36 +233,95 @@ __global__ __launch_bounds__(kThreads) void march_grid(const MarchArgs a)
     }
 
     // ---- epilogue: frag.glsl:76-80 + the render-target format --------------
-    if (a.step_counter) {
-        unsigned long long cnt = (n > 0) ? (unsigned long long)i : 0ull;
-        for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
-        if (lane == 0 && cnt) atomicAdd(a.step_counter, cnt);
-    }
-    if (!live) return;
-    float g = 0.0f;
-    if (n >= 0) {
-        const float at = acc * a.step_size;
-        const float e = spec_expf(a.density * fminf(-at, 0.0f));
-        g = 1.0f - e;
-    }
-    char* row = (char*)a.out + (long long)orow * a.pitch;
-    if (a.format == 0) {
-        reinterpret_cast<float4*>(row)[x] = make_float4(g, g, g, 1.0f);
-    } else {
-        unsigned int q = 0;
+    if (live) {
+        float g = 0.0f;
         if (n >= 0) {
-            float c = fminf(fmaxf(g, 0.0f), 1.0f);
-            if (a.format == 2)
-                c = c <= 0.0031308f ? c * 12.92f : fmaf(1.055f, powf(c, 1.0f / 2.4f), -0.055f);
-            q = (unsigned int)rintf(c * 255.0f);
+            const float at = acc * a.step_size;
+            const float e = spec_expf(a.density * fminf(-at, 0.0f));
+            g = 1.0f - e;
         }
-        reinterpret_cast<unsigned int*>(row)[x] = q | (q << 8) | (q << 16) | 0xff000000u;
+        char* row = (char*)a.out + (long long)orow * a.pitch;
+        if (a.format == 0) {
+            reinterpret_cast<float4*>(row)[x] = make_float4(g, g, g, 1.0f);
+        } else {
+            unsigned int q = 0;
+            if (n >= 0) {
+                float c = fminf(fmaxf(g, 0.0f), 1.0f);
+                if (a.format == 2)
+                    c = c <= 0.0031308f ? c * 12.92f : fmaf(1.055f, powf(c, 1.0f / 2.4f), -0.055f);
+                q = (unsigned int)rintf(c * 255.0f);
+            }
+            reinterpret_cast<unsigned int*>(row)[x] = q | (q << 8) | (q << 16) | 0xff000000u;
+        }
     }
+    return n > 0 ? (unsigned)i : 0u;
+}
+
+__device__ __forceinline__ void add_steps(const MarchArgs& a, unsigned long long cnt)
+{
+    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+    if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(a.step_counter, cnt);
+}
+
+// Static schedule: one 16x16 tile per workgroup, one 8x8 sub-tile per wave.
+template <int LAYOUT, int WRAP, bool EARLY>
+__global__ __launch_bounds__(kThreads) void march_grid(const MarchArgs a)
+{
+    // Tile rows are dealt to XCDs round-robin: XCD x (= blockIdx % 8 under
+    // the observed dispatch, a speed-only assumption) walks tile rows
+    // x, x+8, ...  Work is balanced (the silhouette is centred) and
+    // horizontally adjacent tiles share one L2.
+    const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+    const int k = j / a.tiles_x, tx = j - k * a.tiles_x;
+    const int ty = xcd + 8 * k;
+    if (ty >= a.tiles_y) return;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int x = tx * kTile + (wave & 1) * 8 + (lane & 7);
+    const int orow = ty * kTile + (wave >> 1) * 8 + (lane >> 3);
+    const unsigned steps = march_pixel<LAYOUT, WRAP, EARLY>(a, x, orow);
+    if (a.step_counter) add_steps(a, steps);
+}
+
+// Dynamic schedule: persistent waves pull 8x8 tiles from 8 queues, one per
+// XCD group (blockIdx % 8, speed-only).  Queue q owns the 16-row tile pairs
+// p = q, q+8, ..., walked column by column.  heads[] is zeroed by a memset
+// before every launch.  Every wave leaves once its queue is drained, so the
+// grid always completes.
+template <int LAYOUT, int WRAP, bool EARLY>
+__global__ __launch_bounds__(kThreads) void march_queue(const MarchArgs a, int* __restrict__ heads)
+{
+    const int q = blockIdx.x & 7, lane = threadIdx.x & 63;
+    const int tiles_x8 = (a.width + 7) >> 3, rows8 = (a.out_rows + 7) >> 3;
+    const int pairs = (rows8 + 1) >> 1;
+    const int per_pair = 2 * tiles_x8;
+    const int count = q < pairs ? ((pairs - q + 7) >> 3) * per_pair : 0;
+    unsigned long long steps = 0;
+    for (;;) {
+        int k = 0;
+        if (lane == 0) k = atomicAdd(&heads[q], 1);
+        k = __shfl(k, 0);
+        if (k >= count) break;
+        const int m = k / per_pair, rem = k - m * per_pair;
+        const int row8 = 2 * (q + 8 * m) + (rem & 1), tx = rem >> 1;
+        if (row8 >= rows8) continue;
+        steps += march_pixel<LAYOUT, WRAP, EARLY>(a, tx * 8 + (lane & 7), row8 * 8 + (lane >> 3));
+    }
+    if (a.step_counter) add_steps(a, steps);
 }
 
 template <int L, int W>
-hipError_t launch_lw(const MarchArgs& a, bool early, hipStream_t s)
+hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStream_t s)
 {
+    if (sc.queue) {
+        hipError_t e = hipMemsetAsync(sc.heads, 0, 32, s);
+        if (e != hipSuccess) return e;
+        dim3 grid(256 * sc.waves_per_simd), block(kThreads);
+        if (early)
+            hipLaunchKernelGGL((march_queue<L, W, true>), grid, block, 0, s, a, sc.heads);
+        else
+            hipLaunchKernelGGL((march_queue<L, W, false>), grid, block, 0, s, a, sc.heads);
+        return hipGetLastError();
+    }
     dim3 grid(a.num_blocks), block(kThreads);
     if (early)
         hipLaunchKernelGGL((march_grid<L, W, true>), grid, block, 0, s, a);
@@ -282,15 +332,15 @@ hipError_t launch_lw(const MarchArgs& a, bool early, hipStream_t s)
 
 }  // namespace
 
-hipError_t launch_march(const MarchArgs& a, int layout, int wrap, bool early, hipStream_t s)
+hipError_t launch_march(const MarchArgs& a, int layout, int wrap, bool early, const Schedule& sc, hipStream_t s)
 {
     if (a.num_blocks <= 0) return hipSuccess;
-    if (layout == LAYOUT_PAD16) return launch_lw<LAYOUT_PAD16, WRAP_CLAMP>(a, early, s);
-    if (layout == LAYOUT_BRICK5) return launch_lw<LAYOUT_BRICK5, WRAP_CLAMP>(a, early, s);
-    if (layout == LAYOUT_CORNER8) return launch_lw<LAYOUT_CORNER8, WRAP_CLAMP>(a, early, s);
-    if (layout == LAYOUT_QUAD) return launch_lw<LAYOUT_QUAD, WRAP_CLAMP>(a, early, s);
-    if (wrap == WRAP_CLAMP) return launch_lw<LAYOUT_PLANAR, WRAP_CLAMP>(a, early, s);
-    return launch_lw<LAYOUT_PLANAR, WRAP_MIRROR>(a, early, s);
+    if (layout == LAYOUT_PAD16) return launch_lw<LAYOUT_PAD16, WRAP_CLAMP>(a, early, sc, s);
+    if (layout == LAYOUT_BRICK5) return launch_lw<LAYOUT_BRICK5, WRAP_CLAMP>(a, early, sc, s);
+    if (layout == LAYOUT_CORNER8) return launch_lw<LAYOUT_CORNER8, WRAP_CLAMP>(a, early, sc, s);
+    if (layout == LAYOUT_QUAD) return launch_lw<LAYOUT_QUAD, WRAP_CLAMP>(a, early, sc, s);
+    if (wrap == WRAP_CLAMP) return launch_lw<LAYOUT_PLANAR, WRAP_CLAMP>(a, early, sc, s);
+    return launch_lw<LAYOUT_PLANAR, WRAP_MIRROR>(a, early, sc, s);
 }
 
 }  // namespace vr

@@ -181,6 +181,13 @@ class Renderer:
     def set_layout_preference(self, pref: int) -> None:
         call("vr_set_layout_preference", self._ctx, int(pref))
 
+    def set_option(self, name: str, value: int) -> None:
+        """Tuning knobs of vr_set_option: "layout", "schedule", "waves_per_simd"."""
+        call("vr_set_option", self._ctx, name.encode(), int(value))
+
+    def get_option(self, name: str) -> int:
+        return _lib.load().vr_get_option(self._ctx, name.encode())
+
     @property
     def kernel_variant(self) -> str:
         return _lib.load().vr_kernel_variant(self._ctx).decode()
