@@ -119,17 +119,19 @@ def test_every_layout_bitexact(r, oracle, vol128, layout, name):
         r.set_layout_preference(0)
 
 
-@pytest.mark.parametrize("schedule,wps", [(0, 4), (1, 1), (1, 3), (1, 8)])
+@pytest.mark.parametrize("schedule,wps", [(0, 4), (1, 1), (1, 3), (1, 8), (2, 1), (2, 3), (2, 16)])
 def test_schedules_bitexact(r, oracle, vol128, schedule, wps):
+    sched0, tpw0 = r.get_option("schedule"), r.get_option("tiles_per_wave")
     r.set_option("schedule", schedule)
-    r.set_option("waves_per_simd", wps)
+    r.set_option("waves_per_simd" if schedule == 1 else "tiles_per_wave", wps)
     try:
         for W, H, band in [(333, 187, {}), (640, 360, dict(band_rows=16, band_stride=3, band_first=2))]:
             img, ref, c, s = render_both(r, oracle, vol128, W, H, **band)
             assert_exact(img, ref)
             assert c == s
     finally:
-        r.set_option("schedule", 1)
+        r.set_option("schedule", sched0)
+        r.set_option("tiles_per_wave", tpw0)
         r.set_option("waves_per_simd", 4)
 
 

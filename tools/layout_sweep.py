@@ -40,11 +40,13 @@ def main():
     def apply(r, lay):
         r.set_layout_preference(lay[0])
         r.set_option("schedule", lay[1])
-        if lay[2] > 0:
+        if lay[1] == 1 and lay[2] > 0:
             r.set_option("waves_per_simd", lay[2])
+        if lay[1] == 2 and lay[2] > 0:
+            r.set_option("tiles_per_wave", lay[2])
 
     def name(lay):
-        return f"{NAMES[lay[0]]}/{'queue' + str(lay[2]) if lay[1] else 'static'}"
+        return f"{NAMES[lay[0]]}/{['static', 'queue', 'strided'][lay[1]]}{lay[2] if lay[1] else ''}"
     res = {}
     with vr.Renderer(0) as r:
         osd, gsd = vr.reference_shader_data(W / H)

@@ -42,8 +42,9 @@ vr_status fail(vr_status st, const char* fmt, ...)
                         #expr, hipGetErrorString(e_), __FILE__, __LINE__);                   \
     } while (0)
 
-constexpr int kDefaultSchedule = 1;      // 1 = persistent queue, 0 = static tiles
+constexpr int kDefaultSchedule = 2;      // 0 = static tiles, 1 = persistent queue, 2 = strided
 constexpr int kDefaultWavesPerSimd = 4;
+constexpr int kDefaultTilesPerWave = 4;
 
 struct Ctx {
     int device = 0;
@@ -62,6 +63,7 @@ struct Ctx {
     // schedule of the march kernel (vr_set_option "schedule", "waves_per_simd")
     int schedule = kDefaultSchedule;
     int waves_per_simd = kDefaultWavesPerSimd;
+    int tiles_per_wave = kDefaultTilesPerWave;
     int* d_heads = nullptr;        // 8 queue heads (+ padding), zeroed per launch
 };
 
@@ -475,13 +477,19 @@ vr_status vr_set_option(void* p, const char* name, int value)
     const std::string n(name);
     if (n == "layout") return vr_set_layout_preference(p, value);
     if (n == "schedule") {
-        if (value < 0 || value > 1) return fail(VR_ERR_INVALID, "vr_set_option: schedule is 0 (static) or 1 (queue)");
+        if (value < 0 || value > 2)
+            return fail(VR_ERR_INVALID, "vr_set_option: schedule is 0 (static), 1 (queue) or 2 (strided)");
         c->schedule = value;
         return VR_OK;
     }
     if (n == "waves_per_simd") {
         if (value < 1 || value > 8) return fail(VR_ERR_INVALID, "vr_set_option: waves_per_simd in [1, 8]");
         c->waves_per_simd = value;
+        return VR_OK;
+    }
+    if (n == "tiles_per_wave") {
+        if (value < 1 || value > 64) return fail(VR_ERR_INVALID, "vr_set_option: tiles_per_wave in [1, 64]");
+        c->tiles_per_wave = value;
         return VR_OK;
     }
     return fail(VR_ERR_INVALID, "vr_set_option: unknown option '%s'", name);
@@ -495,6 +503,7 @@ int vr_get_option(void* p, const char* name)
     if (n == "layout") return c->fast_layout ? c->fast_layout : LAYOUT_PLANAR;
     if (n == "schedule") return c->schedule;
     if (n == "waves_per_simd") return c->waves_per_simd;
+    if (n == "tiles_per_wave") return c->tiles_per_wave;
     return -1;
 }
 
@@ -575,7 +584,7 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
     a.format = t->format;
     a.step_counter = reinterpret_cast<unsigned long long*>(t->step_counter);
     HIP_TRY(hipSetDevice(c->device));
-    const Schedule sc{c->schedule == 1, c->waves_per_simd, c->d_heads};
+    const Schedule sc{c->schedule == 2, c->tiles_per_wave, c->schedule == 1, c->waves_per_simd, c->d_heads};
     HIP_TRY(launch_march(a, pl.layout, pl.wrap, pl.early, sc, static_cast<hipStream_t>(stream)));
     return VR_OK;
 }

@@ -58,6 +58,8 @@ struct MarchArgs {
 
 // How the march kernel maps tiles to waves.
 struct Schedule {
+    bool strided;          // true: each wave renders tiles_per_wave strided 8x8 tiles
+    int tiles_per_wave;
     bool queue;            // false: static 16x16 tile per workgroup
     int waves_per_simd;    // queue: persistent waves per SIMD (grid = 256 CUs x this)
     int* heads;            // queue: 8 device ints, zeroed before each launch

@@ -309,9 +309,38 @@ __global__ __launch_bounds__(kThreads) void march_queue(const MarchArgs a, int* 
     if (a.step_counter) add_steps(a, steps);
 }
 
+// Strided static schedule: wave g (of nw) renders 8x8 tiles g, g + nw,
+// g + 2nw, ... of the row-major tile grid.  Its T = ceil(ntiles / nw) tiles
+// sit 1/T of the image apart, so every wave mixes silhouette centre and edge.
+// Per-wave (and per-SIMD) work evens out without atomics.
+template <int LAYOUT, int WRAP, bool EARLY>
+__global__ __launch_bounds__(kThreads) void march_strided(const MarchArgs a, int nw)
+{
+    const int lane = threadIdx.x & 63;
+    const int g = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+    const int tiles_x8 = (a.width + 7) >> 3, rows8 = (a.out_rows + 7) >> 3;
+    const int ntiles = tiles_x8 * rows8;
+    unsigned long long steps = 0;
+    for (int t = g; t < ntiles; t += nw) {
+        const int ty = t / tiles_x8, tx = t - ty * tiles_x8;
+        steps += march_pixel<LAYOUT, WRAP, EARLY>(a, tx * 8 + (lane & 7), ty * 8 + (lane >> 3));
+    }
+    if (a.step_counter) add_steps(a, steps);
+}
+
 template <int L, int W>
 hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStream_t s)
 {
+    if (sc.strided) {
+        const int tiles = ((a.width + 7) >> 3) * ((a.out_rows + 7) >> 3);
+        const int nw = (tiles + sc.tiles_per_wave - 1) / sc.tiles_per_wave;
+        dim3 grid((nw + 3) / 4), block(kThreads);
+        if (early)
+            hipLaunchKernelGGL((march_strided<L, W, true>), grid, block, 0, s, a, 4 * (int)grid.x);
+        else
+            hipLaunchKernelGGL((march_strided<L, W, false>), grid, block, 0, s, a, 4 * (int)grid.x);
+        return hipGetLastError();
+    }
     if (sc.queue) {
         hipError_t e = hipMemsetAsync(sc.heads, 0, 32, s);
         if (e != hipSuccess) return e;
