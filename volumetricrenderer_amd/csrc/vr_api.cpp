@@ -44,7 +44,7 @@ vr_status fail(vr_status st, const char* fmt, ...)
 
 constexpr int kDefaultSchedule = 2;      // 0 = static tiles, 1 = persistent queue, 2 = strided
 constexpr int kDefaultWavesPerSimd = 4;
-constexpr int kDefaultTilesPerWave = 4;
+constexpr int kDefaultTilesPerWave = 1;
 
 struct Ctx {
     int device = 0;
