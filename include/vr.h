@@ -169,10 +169,11 @@ int vr_band_rows_packed(int height, int band_rows, int band_stride, int band_fir
 /* returns a static string, e.g. "grid_pad16_clamp"                        */
 const char* vr_kernel_variant(void* ctx);
 /* Choose the device volume layout: 0 = auto (default),
- * 1 = planar only, 2 = padded u16 pairs, 3 = 4^3 apron bricks (128-B
- * lines), 4 = 8-corner words, 5 = xy quads.  Layouts 2-5 are used only
- * where clamp-to-edge equals mirrored repeat.  Otherwise the planar,
- * mirrored-repeat kernel runs.  Rebuilds the layout (synchronous).        */
+ * 1 = planar only, 2 = 4^3 apron bricks in 128-B lines ("brick5"),
+ * 3 = 7^3 apron bricks of 512 B ("brick8"), 4 = 15^3 apron bricks of 4 KiB
+ * ("brick16"), 5 = 8-corner footprint words ("corner8").  Layouts 2-5 are
+ * used only where clamp-to-edge equals mirrored repeat.  Otherwise the
+ * planar, mirrored-repeat kernel runs.  Rebuilds the layout (synchronous). */
 vr_status vr_set_layout_preference(void* ctx, int pref);
 /* Tuning knobs: "layout" (as above), "schedule"
  * (0 = one static 16x16 tile per workgroup, 1 = persistent waves pulling

@@ -93,7 +93,9 @@ int wanted_fast_layout(const Ctx* c)
     const int want = c->layout_pref == 0 ? kDefaultFastLayout : c->layout_pref;
     if (want == LAYOUT_PLANAR) return 0;
     // 32-bit offsets inside the kernels: fall back to PAD16 if too large
-    if (layout_plane_bytes(want, c->nx, c->ny, c->nz) >= (1ull << 31)) return LAYOUT_PAD16;
+    // and LDS offset tables of (nx+ny+nz+3) words: fall back to planar
+    if (layout_plane_bytes(want, c->nx, c->ny, c->nz) >= (1ull << 31)) return 0;
+    if ((size_t)(c->nx + c->ny + c->nz + 3) * 4 > 48 * 1024) return 0;
     return want;
 }
 
@@ -200,10 +202,10 @@ const char* variant_name(const Plan& p)
     static const char* names[kNumLayouts][2] = {
         {"none", "none"},
         {"grid_planar_clamp", "grid_planar_clamp_early"},
-        {"grid_pad16_clamp", "grid_pad16_clamp_early"},
         {"grid_brick5_clamp", "grid_brick5_clamp_early"},
+        {"grid_brick8_clamp", "grid_brick8_clamp_early"},
+        {"grid_brick16_clamp", "grid_brick16_clamp_early"},
         {"grid_corner8_clamp", "grid_corner8_clamp_early"},
-        {"grid_quad_clamp", "grid_quad_clamp_early"},
     };
     if (p.layout == LAYOUT_PLANAR && p.wrap == WRAP_MIRROR)
         return p.early ? "grid_planar_mirror_early" : "grid_planar_mirror";
@@ -559,14 +561,11 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
     a.nx = c->nx; a.ny = c->ny; a.nz = c->nz;
     if (pl.layout != LAYOUT_PLANAR) {
         a.vol = c->d_fast;
-        a.plane_stride = (long long)c->fast_plane_bytes;
-        a.prow = c->nx + 2;
-        a.pslice = (c->nx + 2) * (c->ny + 2);
-        a.nbx = (c->nx >> 2) + 1;
-        a.nby = (c->ny >> 2) + 1;
+        a.plane_stride = (unsigned)c->fast_plane_bytes;
+        a.geom = layout_geom(pl.layout, c->nx, c->ny, c->nz);
     } else {
         a.vol = c->d_planar;
-        a.plane_stride = (long long)c->nx * c->ny * c->nz;
+        a.plane_stride = (unsigned)((size_t)c->nx * c->ny * c->nz);
     }
     a.width = t->width;
     a.height = t->height;
@@ -584,7 +583,7 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
     a.format = t->format;
     a.step_counter = reinterpret_cast<unsigned long long*>(t->step_counter);
     HIP_TRY(hipSetDevice(c->device));
-    const Schedule sc{c->schedule == 2, c->tiles_per_wave, c->schedule == 1, c->waves_per_simd, c->d_heads};
+    const Schedule sc{c->schedule, c->tiles_per_wave, c->waves_per_simd, c->d_heads};
     HIP_TRY(launch_march(a, pl.layout, pl.wrap, pl.early, sc, static_cast<hipStream_t>(stream)));
     return VR_OK;
 }

@@ -7,27 +7,66 @@
 
 namespace vr {
 
-// Volume layouts in HBM.  All keep one array per channel,
-// so a tap reads only the channel it needs (frag.glsl:66-69 read .x, .y, .z,
-// .w at four different coordinates).  LAYOUT_PLANAR is the canonical copy:
-// any wrap mode, and the source of every other layout.  The others are
-// indexed by the *padded* base texel a = floor(u*N - .5) + 1, clamped to
-// [0, N].  They store the clamp-to-edge values of the 2x2x2 trilinear
-// footprint, so a tap needs no index clamping.  They are exact wherever
-// clamp-to-edge equals mirrored repeat (checked per frame on the host).
+// Volume layouts in HBM.  Each keeps one array per
+// channel, so a tap reads only the channel it needs (frag.glsl:66-69 read
+// .x, .y, .z, .w at four different coordinates).
+//
+// LAYOUT_PLANAR is the canonical copy and the source of every other layout.
+// It is u8 plane[z][y][x], takes any wrap mode, and does 8 byte loads per tap.
+//
+// The fast layouts are indexed by the *padded* base texel a = floor(g), with
+// g = u*N + 0.5 and a in [0, N].  They store the clamp-to-edge values of the
+// 2x2x2 trilinear footprint, so a tap needs no index wrapping.  They are
+// exact wherever clamp-to-edge equals mirrored repeat.  The host checks that
+// per frame; otherwise LAYOUT_PLANAR runs.  A tap's byte offset is
+// TX[a] + TY[b] + TZ[c], from three per-axis tables the kernel keeps in LDS,
+// so the brick geometry costs two adds per tap.
 enum Layout : int {
-    LAYOUT_PLANAR = 1,   // u8 plane[z][y][x]; 8 byte loads per tap
-    LAYOUT_PAD16 = 2,    // u8 plane[z+1][y+1][x+1] with a 1-texel apron; 4 u16 loads
-    LAYOUT_BRICK5 = 3,   // 4^3 bricks + 1-texel apron = 5^3 B in one 128-B line;
-                         // a footprint never leaves its line; 4 u16 loads
-    LAYOUT_CORNER8 = 4,  // per base texel the 8 footprint bytes (u64), in 4^3
-                         // position bricks of 512 B; 1 dwordx2 load per tap
-    LAYOUT_QUAD = 5,     // per base texel the 2x2 xy quad (u32), 4x4x5 position
-                         // bricks of 320 B; 2 dword loads per tap
+    LAYOUT_PLANAR = 1,
+    LAYOUT_BRICK5 = 2,    // B=4: 4^3 texels + 1-texel apron = 5^3 B in one 128-B
+                          // line (2.0x bytes); a footprint never leaves its line
+    LAYOUT_BRICK8 = 3,    // B=7: 8^3 = 512 B bricks (1.49x bytes)
+    LAYOUT_BRICK16 = 4,   // B=15: 16^3 = 4 KiB bricks (1.21x bytes)
+    LAYOUT_CORNER8 = 5,   // per base texel its 8 footprint bytes (u64) in 4^3
+                          // position bricks of 512 B (8x bytes); 1 load per tap
 };
 constexpr int kNumLayouts = 6;
 
 enum Wrap : int { WRAP_CLAMP = 0, WRAP_MIRROR = 1 };
+
+// Geometry of a fast layout for one channel (host and device).
+struct LayoutGeom {
+    int B;          // useful positions per brick edge
+    int R;          // stored edge of an apron brick, R = B + 1
+    unsigned brick; // bytes per brick
+    int nbx, nby, nbz;
+};
+__host__ __device__ inline LayoutGeom layout_geom(int layout, int nx, int ny, int nz)
+{
+    LayoutGeom g{};
+    if (layout == LAYOUT_CORNER8) {
+        g.B = 4; g.R = 4; g.brick = 512;
+    } else {
+        g.B = layout == LAYOUT_BRICK5 ? 4 : layout == LAYOUT_BRICK8 ? 7 : 15;
+        g.R = g.B + 1;
+        const unsigned r3 = (unsigned)(g.R * g.R * g.R);
+        g.brick = (r3 + 127u) & ~127u;   // whole 128-B lines
+    }
+    // padded base positions a in [0, N] -> bricks a / B in [0, N / B]
+    g.nbx = nx / g.B + 1;
+    g.nby = ny / g.B + 1;
+    g.nbz = nz / g.B + 1;
+    return g;
+}
+// byte offset of padded position a along axis 0/1/2 inside one channel plane
+__host__ __device__ inline unsigned axis_offset(const LayoutGeom& g, int layout, int axis, int a)
+{
+    const unsigned q = (unsigned)(a / g.B), r = (unsigned)(a % g.B);
+    const unsigned stride = axis == 0 ? g.brick : axis == 1 ? g.brick * (unsigned)g.nbx
+                                                            : g.brick * (unsigned)g.nbx * (unsigned)g.nby;
+    if (layout == LAYOUT_CORNER8) return q * stride + (r << (3 + 2 * axis));   // 8 B per position
+    return q * stride + r * (axis == 0 ? 1u : axis == 1 ? (unsigned)g.R : (unsigned)(g.R * g.R));
+}
 
 // Everything one launch of the march kernel needs.  Passed by value
 // (kernarg segment), computed on the host per vr_render call.
@@ -44,12 +83,11 @@ struct MarchArgs {
     // volume
     int nx, ny, nz;
     const uint8_t* vol;          // channel plane 0; plane c at vol + c*plane_stride
-    long long plane_stride;
-    int prow, pslice;            // PAD16: (nx+2), (nx+2)*(ny+2)
-    int nbx, nby;                // bricked layouts: bricks along x, y
+    unsigned plane_stride;       // bytes (< 2^31)
+    LayoutGeom geom;             // fast layouts
     // target
     int width, height, band_rows, band_stride, band_first, out_rows;
-    int tiles_x, tiles_y, num_blocks;   // 16x16 tiles; blocks = 8 XCD row-groups
+    int tiles_x, tiles_y, num_blocks;   // static schedule: 16x16 tiles
     void* out;
     long long pitch;
     int format;
@@ -57,10 +95,10 @@ struct MarchArgs {
 };
 
 // How the march kernel maps tiles to waves.
+enum ScheduleKind : int { SCHED_STATIC = 0, SCHED_QUEUE = 1, SCHED_STRIDED = 2 };
 struct Schedule {
-    bool strided;          // true: each wave renders tiles_per_wave strided 8x8 tiles
-    int tiles_per_wave;
-    bool queue;            // false: static 16x16 tile per workgroup
+    int kind;
+    int tiles_per_wave;    // strided: 8x8 tiles per wave
     int waves_per_simd;    // queue: persistent waves per SIMD (grid = 256 CUs x this)
     int* heads;            // queue: 8 device ints, zeroed before each launch
 };
@@ -68,7 +106,7 @@ struct Schedule {
 // launchers (vr_march.hip / vr_volume.hip); return hipError_t
 hipError_t launch_march(const MarchArgs& a, int layout, int wrap, bool early, const Schedule& sc, hipStream_t s);
 hipError_t launch_repack(const uint8_t* d_rgba, int nx, int ny, int nz, uint8_t* d_planar, hipStream_t s);
-// Build a fast layout (PAD16/BRICK5/CORNER8/QUAD) from the planar planes.
+// Build a fast layout from the planar planes.
 hipError_t launch_build_layout(int layout, const uint8_t* d_planar, int nx, int ny, int nz, uint8_t* d_out,
                                hipStream_t s);
 size_t layout_plane_bytes(int layout, int nx, int ny, int nz);

@@ -1,40 +1,28 @@
 // vr_march.hip -- the hot path: per-pixel volumetric ray march for gfx950.
 //
 // Replaces shaders/frag.glsl:34-81 (and the coverage that vert.glsl:17-22
-// plus rasterisation provide).  Each lane traces one ray; a wave64 owns an
-// 8x8 pixel tile; a 256-thread workgroup owns a 16x16 tile.  There is no LDS
-// and no barrier: neighbouring rays share the volume through L1/L2.  Work is
-// ALU/gather-bound, so nothing here uses MFMA.
+// plus rasterisation provide).  Each lane traces one ray and a wave64 owns an
+// 8x8 pixel tile.  The work is gather + fp32 VALU; there is no dense
+// contraction, so nothing here uses MFMA.
 //
 // The op sequence is the fp32 spec of DESIGN.md sec. 3.  The oracle
 // (oracle/vr_oracle.c) restates the same spec, and results agree bit for bit.
-// Build with -ffp-contract=off: the only fused ops are the explicit fmaf().
+// Packed fp32 ops (v_pk_fma_f32 / v_pk_add_f32) compute two independent IEEE
+// lerps per instruction.  Built with -ffp-contract=off: the only fused ops
+// are the explicit fma calls.
 #include "vr_internal.h"
 
 namespace vr {
 namespace {
 
-constexpr int kTile = 16;           // workgroup tile edge, pixels
-constexpr int kThreads = 256;       // 4 waves, each an 8x8 sub-tile
+constexpr int kTile = 16;           // static schedule: workgroup tile edge, pixels
+constexpr int kThreads = 256;       // 4 waves
+
+typedef float f2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ float lerp_(float a, float b, float t) { return fmaf(t, b - a, a); }
+__device__ __forceinline__ f2 lerp2(f2 a, f2 b, f2 t) { return __builtin_elementwise_fma(t, b - a, a); }
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return min(max(v, lo), hi); }
-// clamp to [0, hi] in one v_med3_i32
-__device__ __forceinline__ int clamp0(int v, int hi)
-{
-    int r;
-    asm("v_med3_i32 %0, %1, 0, %2" : "=v"(r) : "v"(v), "v"(hi));
-    return r;
-}
-
-// unaligned u16 load at a 32-bit byte offset from a wave-uniform base
-// (gfx950 runs in unaligned-access mode; one global_load_ushort)
-__device__ __forceinline__ unsigned ld_u16(const uint8_t* __restrict__ base, unsigned off)
-{
-    uint16_t v;
-    __builtin_memcpy(&v, base + off, 2);
-    return v;
-}
 
 // floor(x) as int in one instruction, and x - floor(x) clamped below 1.0
 // (v_fract_f32).  The spec defines the tap weight as
@@ -47,9 +35,19 @@ __device__ __forceinline__ int cvt_flr(float x)
 }
 __device__ __forceinline__ float fract_(float x) { return __builtin_amdgcn_fractf(x); }
 
-// byte k of a dword as float (v_cvt_f32_ubyteK)
+// byte k of a dword as float: one v_cvt_f32_ubyteK.  Opaque on purpose: given
+// (float)hi - (float)lo of two bytes, hipcc otherwise subtracts in packed
+// int16 and converts the difference, which costs more instructions.
 template <int K>
-__device__ __forceinline__ float ubyte(unsigned v) { return (float)((v >> (8 * K)) & 0xffu); }
+__device__ __forceinline__ float ubyte(unsigned v)
+{
+    float r;
+    if constexpr (K == 0) asm("v_cvt_f32_ubyte0 %0, %1" : "=v"(r) : "v"(v));
+    else if constexpr (K == 1) asm("v_cvt_f32_ubyte1 %0, %1" : "=v"(r) : "v"(v));
+    else if constexpr (K == 2) asm("v_cvt_f32_ubyte2 %0, %1" : "=v"(r) : "v"(v));
+    else asm("v_cvt_f32_ubyte3 %0, %1" : "=v"(r) : "v"(v));
+    return r;
+}
 
 // VK_SAMPLER_ADDRESS_MODE_MIRRORED_REPEAT on an integer texel index
 // (VulkanCore.cpp:683-685; Vulkan spec "Texel coordinate wrapping").
@@ -79,87 +77,92 @@ __device__ __forceinline__ float spec_expf(float x)
     return p * __int_as_float(((int)k + 127) << 23);
 }
 
-// One trilinear tap of one channel: Vulkan LINEAR filter, LOD 0, at padded
-// texel coordinate g = u*N - 0.5 + 1.  floor(g) is the padded base texel,
-// fract(g) the weight.  Then 8 texels and 7 lerps.
-template <int LAYOUT, int WRAP>
-__device__ __forceinline__ float tap(const uint8_t* __restrict__ pl, const MarchArgs& a,
-                                     float gx, float gy, float gz)
+// Trilinear blend of the 8 footprint texels, two lerps per packed op:
+// x-lerps of (y0,z0|y0,z1) and (y1,z0|y1,z1), then y, then z.  Each element
+// is the spec's fma(t, b - a, a), in the spec's order.
+__device__ __forceinline__ float blend(f2 lo_a, f2 hi_a, f2 lo_b, f2 hi_b, float wx, float wy, float wz)
 {
-    const float ax = fract_(gx), ay = fract_(gy), az = fract_(gz);
-    const int px = cvt_flr(gx), py = cvt_flr(gy), pz = cvt_flr(gz);
-    float c000, c100, c010, c110, c001, c101, c011, c111;
-    if constexpr (LAYOUT != LAYOUT_PLANAR) {
-        // padded base position, clamped to [0, N]
-        const int a0 = clamp0(px, a.nx), b0 = clamp0(py, a.ny), c0 = clamp0(pz, a.nz);
-        if constexpr (LAYOUT == LAYOUT_PAD16) {
-            const unsigned off = __umul24((unsigned)c0, (unsigned)a.pslice) + __umul24((unsigned)b0, (unsigned)a.prow) + (unsigned)a0;
-            const unsigned v00 = ld_u16(pl, off), v10 = ld_u16(pl, off + a.prow);
-            const unsigned v01 = ld_u16(pl, off + a.pslice), v11 = ld_u16(pl, off + a.pslice + a.prow);
-            c000 = (float)(v00 & 0xffu); c100 = (float)(v00 >> 8);
-            c010 = (float)(v10 & 0xffu); c110 = (float)(v10 >> 8);
-            c001 = (float)(v01 & 0xffu); c101 = (float)(v01 >> 8);
-            c011 = (float)(v11 & 0xffu); c111 = (float)(v11 >> 8);
-        } else if constexpr (LAYOUT == LAYOUT_BRICK5) {
-            // 5x5x5 bytes of brick (a0>>2, b0>>2, c0>>2) hold the whole footprint
-            const unsigned brick = __umul24(__umul24((unsigned)(c0 >> 2), (unsigned)a.nby) + (unsigned)(b0 >> 2),
-                                            (unsigned)a.nbx) + (unsigned)(a0 >> 2);
-            const unsigned off = (brick << 7) + (unsigned)((c0 & 3) * 25 + (b0 & 3) * 5 + (a0 & 3));
-            const unsigned v00 = ld_u16(pl, off), v10 = ld_u16(pl, off + 5);
-            const unsigned v01 = ld_u16(pl, off + 25), v11 = ld_u16(pl, off + 30);
-            c000 = (float)(v00 & 0xffu); c100 = (float)(v00 >> 8);
-            c010 = (float)(v10 & 0xffu); c110 = (float)(v10 >> 8);
-            c001 = (float)(v01 & 0xffu); c101 = (float)(v01 >> 8);
-            c011 = (float)(v11 & 0xffu); c111 = (float)(v11 >> 8);
-        } else if constexpr (LAYOUT == LAYOUT_CORNER8) {
-            const unsigned brick = __umul24(__umul24((unsigned)(c0 >> 2), (unsigned)a.nby) + (unsigned)(b0 >> 2),
-                                            (unsigned)a.nbx) + (unsigned)(a0 >> 2);
-            const unsigned off = (brick << 9) + ((unsigned)(((c0 & 3) << 4) + ((b0 & 3) << 2) + (a0 & 3)) << 3);
-            const uint2 q = *reinterpret_cast<const uint2*>(pl + off);
-            c000 = ubyte<0>(q.x); c100 = ubyte<1>(q.x);
-            c010 = ubyte<2>(q.x); c110 = ubyte<3>(q.x);
-            c001 = ubyte<0>(q.y); c101 = ubyte<1>(q.y);
-            c011 = ubyte<2>(q.y); c111 = ubyte<3>(q.y);
-        } else {  // LAYOUT_QUAD: 4x4x5 positions x 4 B per brick; z0 quad then z1 quad at +64 B
-            const unsigned brick = __umul24(__umul24((unsigned)(c0 >> 2), (unsigned)a.nby) + (unsigned)(b0 >> 2),
-                                            (unsigned)a.nbx) + (unsigned)(a0 >> 2);
-            const unsigned off = __umul24(brick, 320u) + ((unsigned)(((c0 & 3) << 4) + ((b0 & 3) << 2) + (a0 & 3)) << 2);
-            const unsigned q0 = *reinterpret_cast<const unsigned*>(pl + off);
-            const unsigned q1 = *reinterpret_cast<const unsigned*>(pl + off + 64);
-            c000 = ubyte<0>(q0); c100 = ubyte<1>(q0);
-            c010 = ubyte<2>(q0); c110 = ubyte<3>(q0);
-            c001 = ubyte<0>(q1); c101 = ubyte<1>(q1);
-            c011 = ubyte<2>(q1); c111 = ubyte<3>(q1);
-        }
+    const f2 xa = lerp2(lo_a, hi_a, f2{wx, wx});   // {x00, x01}
+    const f2 xb = lerp2(lo_b, hi_b, f2{wx, wx});   // {x10, x11}
+    const f2 y = lerp2(xa, xb, f2{wy, wy});        // {y0, y1}
+    return lerp_(y.x, y.y, wz) * (1.0f / 255.0f);
+}
+
+// Per-launch state of a fast-layout tap: the channel's buffer descriptor and
+// the LDS offset tables TX | TY | TZ (vr_internal.h Layout).
+struct FastCtx {
+    __amdgpu_buffer_rsrc_t rsrc[4];
+    const unsigned* tx;
+    const unsigned* ty;
+    const unsigned* tz;
+};
+
+// One trilinear tap of one channel from a fast layout, at padded texel
+// coordinate g (floor(g) = base texel + 1, fract(g) = weight).  Loads go
+// through a range-checked buffer descriptor: an offset outside the plane
+// reads 0 instead of faulting.
+template <int LAYOUT>
+__device__ __forceinline__ float tap_fast(const FastCtx& f, int ch, float gx, float gy, float gz)
+{
+    const float wx = fract_(gx), wy = fract_(gy), wz = fract_(gz);
+    const unsigned off = f.tx[cvt_flr(gx)] + f.ty[cvt_flr(gy)] + f.tz[cvt_flr(gz)];
+    if constexpr (LAYOUT == LAYOUT_CORNER8) {
+        const unsigned q0 = __builtin_amdgcn_raw_buffer_load_b32(f.rsrc[ch], off, 0, 0);
+        const unsigned q1 = __builtin_amdgcn_raw_buffer_load_b32(f.rsrc[ch], off + 4, 0, 0);
+        // q0 = c000 c100 c010 c110, q1 = c001 c101 c011 c111
+        return blend(f2{ubyte<0>(q0), ubyte<0>(q1)}, f2{ubyte<1>(q0), ubyte<1>(q1)},
+                     f2{ubyte<2>(q0), ubyte<2>(q1)}, f2{ubyte<3>(q0), ubyte<3>(q1)}, wx, wy, wz);
     } else {
-        const int ix = px - 1, iy = py - 1, iz = pz - 1;
-        int i0, i1, j0, j1, k0, k1;
-        if constexpr (WRAP == WRAP_CLAMP) {
-            i0 = clampi(ix, 0, a.nx - 1); i1 = clampi(ix + 1, 0, a.nx - 1);
-            j0 = clampi(iy, 0, a.ny - 1); j1 = clampi(iy + 1, 0, a.ny - 1);
-            k0 = clampi(iz, 0, a.nz - 1); k1 = clampi(iz + 1, 0, a.nz - 1);
-        } else {
-            i0 = mirror_(ix, a.nx); i1 = mirror_(ix + 1, a.nx);
-            j0 = mirror_(iy, a.ny); j1 = mirror_(iy + 1, a.ny);
-            k0 = mirror_(iz, a.nz); k1 = mirror_(iz + 1, a.nz);
-        }
-        const int r00 = (k0 * a.ny + j0) * a.nx, r10 = (k0 * a.ny + j1) * a.nx;
-        const int r01 = (k1 * a.ny + j0) * a.nx, r11 = (k1 * a.ny + j1) * a.nx;
-        c000 = pl[r00 + i0]; c100 = pl[r00 + i1];
-        c010 = pl[r10 + i0]; c110 = pl[r10 + i1];
-        c001 = pl[r01 + i0]; c101 = pl[r01 + i1];
-        c011 = pl[r11 + i0]; c111 = pl[r11 + i1];
+        constexpr int R = LAYOUT == LAYOUT_BRICK5 ? 5 : LAYOUT == LAYOUT_BRICK8 ? 8 : 16;
+        const unsigned v00 = __builtin_amdgcn_raw_buffer_load_b16(f.rsrc[ch], off, 0, 0);
+        const unsigned v10 = __builtin_amdgcn_raw_buffer_load_b16(f.rsrc[ch], off + R, 0, 0);
+        const unsigned v01 = __builtin_amdgcn_raw_buffer_load_b16(f.rsrc[ch], off + R * R, 0, 0);
+        const unsigned v11 = __builtin_amdgcn_raw_buffer_load_b16(f.rsrc[ch], off + R * R + R, 0, 0);
+        return blend(f2{ubyte<0>(v00), ubyte<0>(v01)}, f2{ubyte<1>(v00), ubyte<1>(v01)},
+                     f2{ubyte<0>(v10), ubyte<0>(v11)}, f2{ubyte<1>(v10), ubyte<1>(v11)}, wx, wy, wz);
     }
-    const float x00 = lerp_(c000, c100, ax), x10 = lerp_(c010, c110, ax);
-    const float x01 = lerp_(c001, c101, ax), x11 = lerp_(c011, c111, ax);
-    const float y0 = lerp_(x00, x10, ay), y1 = lerp_(x01, x11, ay);
-    return lerp_(y0, y1, az) * (1.0f / 255.0f);
+}
+
+// One trilinear tap from the planar layout with full wrap semantics.
+template <int WRAP>
+__device__ __forceinline__ float tap_planar(const uint8_t* __restrict__ pl, const MarchArgs& a, float gx,
+                                            float gy, float gz)
+{
+    const float wx = fract_(gx), wy = fract_(gy), wz = fract_(gz);
+    const int ix = cvt_flr(gx) - 1, iy = cvt_flr(gy) - 1, iz = cvt_flr(gz) - 1;
+    int i0, i1, j0, j1, k0, k1;
+    if constexpr (WRAP == WRAP_CLAMP) {
+        i0 = clampi(ix, 0, a.nx - 1); i1 = clampi(ix + 1, 0, a.nx - 1);
+        j0 = clampi(iy, 0, a.ny - 1); j1 = clampi(iy + 1, 0, a.ny - 1);
+        k0 = clampi(iz, 0, a.nz - 1); k1 = clampi(iz + 1, 0, a.nz - 1);
+    } else {
+        i0 = mirror_(ix, a.nx); i1 = mirror_(ix + 1, a.nx);
+        j0 = mirror_(iy, a.ny); j1 = mirror_(iy + 1, a.ny);
+        k0 = mirror_(iz, a.nz); k1 = mirror_(iz + 1, a.nz);
+    }
+    const int r00 = (k0 * a.ny + j0) * a.nx, r10 = (k0 * a.ny + j1) * a.nx;
+    const int r01 = (k1 * a.ny + j0) * a.nx, r11 = (k1 * a.ny + j1) * a.nx;
+    return blend(f2{ubyte<0>(pl[r00 + i0]), ubyte<0>(pl[r01 + i0])}, f2{ubyte<0>(pl[r00 + i1]), ubyte<0>(pl[r01 + i1])},
+                 f2{ubyte<0>(pl[r10 + i0]), ubyte<0>(pl[r11 + i0])}, f2{ubyte<0>(pl[r10 + i1]), ubyte<0>(pl[r11 + i1])},
+                 wx, wy, wz);
+}
+
+// Tap t at ray point P: padded texel coordinate g = fma(P, S_t, T_t).
+template <int LAYOUT, int WRAP>
+__device__ __forceinline__ float tap(const MarchArgs& a, const FastCtx& f, int t, f2 pxy, float pz)
+{
+    const f2 gxy = __builtin_elementwise_fma(pxy, f2{a.tap_S[t][0], a.tap_S[t][1]}, f2{a.tap_T[t][0], a.tap_T[t][1]});
+    const float gz = fmaf(pz, a.tap_S[t][2], a.tap_T[t][2]);
+    if constexpr (LAYOUT == LAYOUT_PLANAR)
+        return tap_planar<WRAP>(a.vol + (size_t)t * a.plane_stride, a, gxy.x, gxy.y, gz);
+    else
+        return tap_fast<LAYOUT>(f, t, gxy.x, gxy.y, gz);
 }
 
 // One ray: ray setup (frag.glsl:36-55), the march (:57-75), the epilogue
 // (:76-80) and the store.  Returns the executed steps (0 if uncovered).
 template <int LAYOUT, int WRAP, bool EARLY>
-__device__ __forceinline__ unsigned march_pixel(const MarchArgs& a, int x, int orow)
+__device__ __forceinline__ unsigned march_pixel(const MarchArgs& a, const FastCtx& f, int x, int orow)
 {
     const bool inside = x < a.width && orow < a.out_rows;
     int y = 0;
@@ -206,27 +209,19 @@ __device__ __forceinline__ unsigned march_pixel(const MarchArgs& a, int x, int o
     }
 
     // ---- the hot loop: frag.glsl:57-75 ------------------------------------
-    const uint8_t* __restrict__ pl0 = a.vol;
-    const uint8_t* __restrict__ pl1 = a.vol + a.plane_stride;
-    const uint8_t* __restrict__ pl2 = a.vol + 2 * a.plane_stride;
-    const uint8_t* __restrict__ pl3 = a.vol + 3 * a.plane_stride;
+    f2 pxy{P0, P1};
+    const f2 sxy{s0, s1};
+    float pz = P2;
     float acc = 0.0f;
     int i = 0;
     for (; i < n; ++i) {
-        const float t0 = tap<LAYOUT, WRAP>(pl0, a, fmaf(P0, a.tap_S[0][0], a.tap_T[0][0]),
-                                           fmaf(P1, a.tap_S[0][1], a.tap_T[0][1]),
-                                           fmaf(P2, a.tap_S[0][2], a.tap_T[0][2]));
-        const float t1 = tap<LAYOUT, WRAP>(pl1, a, fmaf(P0, a.tap_S[1][0], a.tap_T[1][0]),
-                                           fmaf(P1, a.tap_S[1][1], a.tap_T[1][1]),
-                                           fmaf(P2, a.tap_S[1][2], a.tap_T[1][2]));
-        const float t2 = tap<LAYOUT, WRAP>(pl2, a, fmaf(P0, a.tap_S[2][0], a.tap_T[2][0]),
-                                           fmaf(P1, a.tap_S[2][1], a.tap_T[2][1]),
-                                           fmaf(P2, a.tap_S[2][2], a.tap_T[2][2]));
-        const float t3 = tap<LAYOUT, WRAP>(pl3, a, fmaf(P0, a.tap_S[3][0], a.tap_T[3][0]),
-                                           fmaf(P1, a.tap_S[3][1], a.tap_T[3][1]),
-                                           fmaf(P2, a.tap_S[3][2], a.tap_T[3][2]));
+        const float t0 = tap<LAYOUT, WRAP>(a, f, 0, pxy, pz);
+        const float t1 = tap<LAYOUT, WRAP>(a, f, 1, pxy, pz);
+        const float t2 = tap<LAYOUT, WRAP>(a, f, 2, pxy, pz);
+        const float t3 = tap<LAYOUT, WRAP>(a, f, 3, pxy, pz);
         acc = acc + ((t0 * t1) * (t2 + t3)) * a.scale;                               // :71-73
-        P0 = P0 + s0; P1 = P1 + s1; P2 = P2 + s2;                                     // :74
+        pxy = pxy + sxy;                                                              // :74
+        pz = pz + s2;
         if constexpr (EARLY) {
             if (acc > a.acc_limit) { ++i; break; }
         }
@@ -263,26 +258,72 @@ __device__ __forceinline__ void add_steps(const MarchArgs& a, unsigned long long
     if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(a.step_counter, cnt);
 }
 
+// Kernel prologue for the fast layouts: buffer descriptors (wave-uniform,
+// from kernargs only) and the per-axis offset tables, built in LDS by the
+// whole workgroup.  The tables are the only LDS use and are read-only after
+// the barrier.
+template <int LAYOUT>
+__device__ __forceinline__ FastCtx fast_prologue(const MarchArgs& a, unsigned* lds)
+{
+    FastCtx f{};
+    if constexpr (LAYOUT != LAYOUT_PLANAR) {
+        for (int c = 0; c < 4; ++c)
+            f.rsrc[c] = __builtin_amdgcn_make_buffer_rsrc((void*)(a.vol + (size_t)c * a.plane_stride), (short)0,
+                                                          (int)a.plane_stride, 0x00020000);
+        const int nx1 = a.nx + 1, ny1 = a.ny + 1, nz1 = a.nz + 1;
+        for (int i = threadIdx.x; i < nx1 + ny1 + nz1; i += kThreads) {
+            const int axis = i < nx1 ? 0 : i < nx1 + ny1 ? 1 : 2;
+            const int pos = axis == 0 ? i : axis == 1 ? i - nx1 : i - nx1 - ny1;
+            lds[i] = axis_offset(a.geom, LAYOUT, axis, pos);   // once per workgroup
+        }
+        __syncthreads();
+        f.tx = lds;
+        f.ty = lds + nx1;
+        f.tz = lds + nx1 + ny1;
+    }
+    return f;
+}
+
 // Static schedule: one 16x16 tile per workgroup, one 8x8 sub-tile per wave.
+// Tile rows are dealt to XCDs round-robin: XCD x (= blockIdx % 8 under the
+// observed dispatch, a speed-only assumption) walks tile rows x, x+8, ...
 template <int LAYOUT, int WRAP, bool EARLY>
 __global__ __launch_bounds__(kThreads) void march_grid(const MarchArgs a)
 {
-    // Tile rows are dealt to XCDs round-robin: XCD x (= blockIdx % 8 under
-    // the observed dispatch, a speed-only assumption) walks tile rows
-    // x, x+8, ...  Work is balanced (the silhouette is centred) and
-    // horizontally adjacent tiles share one L2.
+    extern __shared__ __attribute__((aligned(16))) unsigned lds[];
     const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
     const int k = j / a.tiles_x, tx = j - k * a.tiles_x;
     const int ty = xcd + 8 * k;
-    if (ty >= a.tiles_y) return;
+    if (ty >= a.tiles_y) return;   // whole workgroup: uniform, before the barrier
+    const FastCtx f = fast_prologue<LAYOUT>(a, lds);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int x = tx * kTile + (wave & 1) * 8 + (lane & 7);
     const int orow = ty * kTile + (wave >> 1) * 8 + (lane >> 3);
-    const unsigned steps = march_pixel<LAYOUT, WRAP, EARLY>(a, x, orow);
+    const unsigned steps = march_pixel<LAYOUT, WRAP, EARLY>(a, f, x, orow);
     if (a.step_counter) add_steps(a, steps);
 }
 
-// Dynamic schedule: persistent waves pull 8x8 tiles from 8 queues, one per
+// Strided schedule: wave g (of nw) renders 8x8 tiles g, g + nw, g + 2nw, ...
+// of the row-major tile grid.  Its tiles sit 1/T of the image apart, so the
+// per-wave (and per-SIMD) work evens out without atomics.
+template <int LAYOUT, int WRAP, bool EARLY>
+__global__ __launch_bounds__(kThreads) void march_strided(const MarchArgs a, int nw)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned lds[];
+    const FastCtx f = fast_prologue<LAYOUT>(a, lds);
+    const int lane = threadIdx.x & 63;
+    const int g = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+    const int tiles_x8 = (a.width + 7) >> 3, rows8 = (a.out_rows + 7) >> 3;
+    const int ntiles = tiles_x8 * rows8;
+    unsigned long long steps = 0;
+    for (int t = g; t < ntiles; t += nw) {
+        const int ty = t / tiles_x8, tx = t - ty * tiles_x8;
+        steps += march_pixel<LAYOUT, WRAP, EARLY>(a, f, tx * 8 + (lane & 7), ty * 8 + (lane >> 3));
+    }
+    if (a.step_counter) add_steps(a, steps);
+}
+
+// Queue schedule: persistent waves pull 8x8 tiles from 8 queues, one per
 // XCD group (blockIdx % 8, speed-only).  Queue q owns the 16-row tile pairs
 // p = q, q+8, ..., walked column by column.  heads[] is zeroed by a memset
 // before every launch.  Every wave leaves once its queue is drained, so the
@@ -290,6 +331,8 @@ __global__ __launch_bounds__(kThreads) void march_grid(const MarchArgs a)
 template <int LAYOUT, int WRAP, bool EARLY>
 __global__ __launch_bounds__(kThreads) void march_queue(const MarchArgs a, int* __restrict__ heads)
 {
+    extern __shared__ __attribute__((aligned(16))) unsigned lds[];
+    const FastCtx f = fast_prologue<LAYOUT>(a, lds);
     const int q = blockIdx.x & 7, lane = threadIdx.x & 63;
     const int tiles_x8 = (a.width + 7) >> 3, rows8 = (a.out_rows + 7) >> 3;
     const int pairs = (rows8 + 1) >> 1;
@@ -304,26 +347,7 @@ __global__ __launch_bounds__(kThreads) void march_queue(const MarchArgs a, int* 
         const int m = k / per_pair, rem = k - m * per_pair;
         const int row8 = 2 * (q + 8 * m) + (rem & 1), tx = rem >> 1;
         if (row8 >= rows8) continue;
-        steps += march_pixel<LAYOUT, WRAP, EARLY>(a, tx * 8 + (lane & 7), row8 * 8 + (lane >> 3));
-    }
-    if (a.step_counter) add_steps(a, steps);
-}
-
-// Strided static schedule: wave g (of nw) renders 8x8 tiles g, g + nw,
-// g + 2nw, ... of the row-major tile grid.  Its T = ceil(ntiles / nw) tiles
-// sit 1/T of the image apart, so every wave mixes silhouette centre and edge.
-// Per-wave (and per-SIMD) work evens out without atomics.
-template <int LAYOUT, int WRAP, bool EARLY>
-__global__ __launch_bounds__(kThreads) void march_strided(const MarchArgs a, int nw)
-{
-    const int lane = threadIdx.x & 63;
-    const int g = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
-    const int tiles_x8 = (a.width + 7) >> 3, rows8 = (a.out_rows + 7) >> 3;
-    const int ntiles = tiles_x8 * rows8;
-    unsigned long long steps = 0;
-    for (int t = g; t < ntiles; t += nw) {
-        const int ty = t / tiles_x8, tx = t - ty * tiles_x8;
-        steps += march_pixel<LAYOUT, WRAP, EARLY>(a, tx * 8 + (lane & 7), ty * 8 + (lane >> 3));
+        steps += march_pixel<LAYOUT, WRAP, EARLY>(a, f, tx * 8 + (lane & 7), row8 * 8 + (lane >> 3));
     }
     if (a.step_counter) add_steps(a, steps);
 }
@@ -331,31 +355,34 @@ __global__ __launch_bounds__(kThreads) void march_strided(const MarchArgs a, int
 template <int L, int W>
 hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStream_t s)
 {
-    if (sc.strided) {
+    const size_t lds = L == LAYOUT_PLANAR ? 0 : (size_t)(a.nx + a.ny + a.nz + 3) * sizeof(unsigned);
+    const dim3 block(kThreads);
+    if (sc.kind == SCHED_STRIDED) {
         const int tiles = ((a.width + 7) >> 3) * ((a.out_rows + 7) >> 3);
-        const int nw = (tiles + sc.tiles_per_wave - 1) / sc.tiles_per_wave;
-        dim3 grid((nw + 3) / 4), block(kThreads);
+        const int tpw = sc.tiles_per_wave > 0 ? sc.tiles_per_wave : 1;
+        const int nw = (tiles + tpw - 1) / tpw;
+        const dim3 grid((nw + 3) / 4);
         if (early)
-            hipLaunchKernelGGL((march_strided<L, W, true>), grid, block, 0, s, a, 4 * (int)grid.x);
+            hipLaunchKernelGGL((march_strided<L, W, true>), grid, block, lds, s, a, 4 * (int)grid.x);
         else
-            hipLaunchKernelGGL((march_strided<L, W, false>), grid, block, 0, s, a, 4 * (int)grid.x);
+            hipLaunchKernelGGL((march_strided<L, W, false>), grid, block, lds, s, a, 4 * (int)grid.x);
         return hipGetLastError();
     }
-    if (sc.queue) {
+    if (sc.kind == SCHED_QUEUE) {
         hipError_t e = hipMemsetAsync(sc.heads, 0, 32, s);
         if (e != hipSuccess) return e;
-        dim3 grid(256 * sc.waves_per_simd), block(kThreads);
+        const dim3 grid(256 * sc.waves_per_simd);
         if (early)
-            hipLaunchKernelGGL((march_queue<L, W, true>), grid, block, 0, s, a, sc.heads);
+            hipLaunchKernelGGL((march_queue<L, W, true>), grid, block, lds, s, a, sc.heads);
         else
-            hipLaunchKernelGGL((march_queue<L, W, false>), grid, block, 0, s, a, sc.heads);
+            hipLaunchKernelGGL((march_queue<L, W, false>), grid, block, lds, s, a, sc.heads);
         return hipGetLastError();
     }
-    dim3 grid(a.num_blocks), block(kThreads);
+    const dim3 grid(a.num_blocks);
     if (early)
-        hipLaunchKernelGGL((march_grid<L, W, true>), grid, block, 0, s, a);
+        hipLaunchKernelGGL((march_grid<L, W, true>), grid, block, lds, s, a);
     else
-        hipLaunchKernelGGL((march_grid<L, W, false>), grid, block, 0, s, a);
+        hipLaunchKernelGGL((march_grid<L, W, false>), grid, block, lds, s, a);
     return hipGetLastError();
 }
 
@@ -363,11 +390,14 @@ hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStre
 
 hipError_t launch_march(const MarchArgs& a, int layout, int wrap, bool early, const Schedule& sc, hipStream_t s)
 {
-    if (a.num_blocks <= 0) return hipSuccess;
-    if (layout == LAYOUT_PAD16) return launch_lw<LAYOUT_PAD16, WRAP_CLAMP>(a, early, sc, s);
-    if (layout == LAYOUT_BRICK5) return launch_lw<LAYOUT_BRICK5, WRAP_CLAMP>(a, early, sc, s);
-    if (layout == LAYOUT_CORNER8) return launch_lw<LAYOUT_CORNER8, WRAP_CLAMP>(a, early, sc, s);
-    if (layout == LAYOUT_QUAD) return launch_lw<LAYOUT_QUAD, WRAP_CLAMP>(a, early, sc, s);
+    if (a.width <= 0 || a.out_rows <= 0) return hipSuccess;
+    switch (layout) {
+    case LAYOUT_BRICK5: return launch_lw<LAYOUT_BRICK5, WRAP_CLAMP>(a, early, sc, s);
+    case LAYOUT_BRICK8: return launch_lw<LAYOUT_BRICK8, WRAP_CLAMP>(a, early, sc, s);
+    case LAYOUT_BRICK16: return launch_lw<LAYOUT_BRICK16, WRAP_CLAMP>(a, early, sc, s);
+    case LAYOUT_CORNER8: return launch_lw<LAYOUT_CORNER8, WRAP_CLAMP>(a, early, sc, s);
+    default: break;
+    }
     if (wrap == WRAP_CLAMP) return launch_lw<LAYOUT_PLANAR, WRAP_CLAMP>(a, early, sc, s);
     return launch_lw<LAYOUT_PLANAR, WRAP_MIRROR>(a, early, sc, s);
 }

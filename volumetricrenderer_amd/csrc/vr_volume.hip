@@ -43,61 +43,44 @@ struct PlaneSrc {
     }
 };
 
-// one thread per output element (byte, u16-pair source byte, u32 or u64)
+// One thread per output element: a byte of an apron brick, or one 8-byte
+// footprint word (CORNER8).  Brick order and in-brick order match
+// axis_offset() in vr_internal.h, which the march kernel's LDS tables use.
 template <int LAYOUT>
 __global__ __launch_bounds__(kBlock) void k_build_layout(const uint8_t* __restrict__ planar, int nx, int ny,
-                                                         int nz, long long plane_elems, long long plane_bytes,
-                                                         uint8_t* __restrict__ out)
+                                                         int nz, LayoutGeom g, long long plane_elems,
+                                                         long long plane_bytes, uint8_t* __restrict__ out)
 {
     const long long total_planar = (long long)nx * ny * nz;
-    const int nbx = (nx >> 2) + 1, nby = (ny >> 2) + 1;
     for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < 4 * plane_elems;
          i += (long long)gridDim.x * kBlock) {
         const int ch = (int)(i / plane_elems);
         const long long e = i - ch * plane_elems;
         const PlaneSrc src{planar + ch * total_planar, nx, ny, nz};
         uint8_t* dst = out + ch * plane_bytes;
-        if constexpr (LAYOUT == LAYOUT_PAD16) {
-            const int px = nx + 2, py = ny + 2;
-            const int a = (int)(e % px);
-            const long long t = e / px;
-            const int b = (int)(t % py), c = (int)(t / py);
-            dst[e] = (uint8_t)src.at(a, b, c);
-        } else if constexpr (LAYOUT == LAYOUT_BRICK5) {
-            const long long brick = e >> 7;
-            const int byte = (int)(e & 127);
-            unsigned int v = 0;
-            if (byte < 125) {
-                const int u = byte % 5, vv = (byte / 5) % 5, w = byte / 25;
-                const int bx = (int)(brick % nbx);
-                const long long t = brick / nbx;
-                const int by = (int)(t % nby), bz = (int)(t / nby);
-                v = src.at(4 * bx + u, 4 * by + vv, 4 * bz + w);
-            }
-            dst[e] = (uint8_t)v;
-        } else if constexpr (LAYOUT == LAYOUT_CORNER8) {
+        if constexpr (LAYOUT == LAYOUT_CORNER8) {
             const long long brick = e >> 6;
             const int pos = (int)(e & 63);
-            const int lx = pos & 3, ly = (pos >> 2) & 3, lz = pos >> 4;
-            const int bx = (int)(brick % nbx);
-            const long long t = brick / nbx;
-            const int by = (int)(t % nby), bz = (int)(t / nby);
-            const int a = 4 * bx + lx, b = 4 * by + ly, c = 4 * bz + lz;
+            const int bx = (int)(brick % g.nbx);
+            const long long t = brick / g.nbx;
+            const int by = (int)(t % g.nby), bz = (int)(t / g.nby);
+            const int a = 4 * bx + (pos & 3), b = 4 * by + ((pos >> 2) & 3), c = 4 * bz + (pos >> 4);
             unsigned long long q = 0;
             for (int k = 0; k < 8; ++k)
                 q |= (unsigned long long)src.at(a + (k & 1), b + ((k >> 1) & 1), c + (k >> 2)) << (8 * k);
             reinterpret_cast<unsigned long long*>(dst)[e] = q;
-        } else {  // LAYOUT_QUAD: 4x4x5 positions per brick
-            const long long brick = e / 80;
-            const int pos = (int)(e - brick * 80);
-            const int lx = pos & 3, ly = (pos >> 2) & 3, lz = pos >> 4;
-            const int bx = (int)(brick % nbx);
-            const long long t = brick / nbx;
-            const int by = (int)(t % nby), bz = (int)(t / nby);
-            const int a = 4 * bx + lx, b = 4 * by + ly, c = 4 * bz + lz;
-            unsigned int q = 0;
-            for (int k = 0; k < 4; ++k) q |= src.at(a + (k & 1), b + (k >> 1), c) << (8 * k);
-            reinterpret_cast<unsigned int*>(dst)[e] = q;
+        } else {
+            const long long brick = e / g.brick;
+            const int byte = (int)(e - brick * g.brick);
+            unsigned int v = 0;
+            if (byte < g.R * g.R * g.R) {
+                const int u = byte % g.R, vv = (byte / g.R) % g.R, w = byte / (g.R * g.R);
+                const int bx = (int)(brick % g.nbx);
+                const long long t = brick / g.nbx;
+                const int by = (int)(t % g.nby), bz = (int)(t / g.nby);
+                v = src.at(g.B * bx + u, g.B * by + vv, g.B * bz + w);
+            }
+            dst[e] = (uint8_t)v;
         }
     }
 }
@@ -235,35 +218,31 @@ hipError_t launch_repack(const uint8_t* d_rgba, int nx, int ny, int nz, uint8_t*
 namespace {
 long long layout_elems(int layout, int nx, int ny, int nz)
 {
-    const long long nb = (long long)((nx >> 2) + 1) * ((ny >> 2) + 1) * ((nz >> 2) + 1);
-    switch (layout) {
-    case LAYOUT_PAD16: return (long long)(nx + 2) * (ny + 2) * (nz + 2);
-    case LAYOUT_BRICK5: return nb * 128;
-    case LAYOUT_CORNER8: return nb * 64;
-    case LAYOUT_QUAD: return nb * 80;
-    default: return 0;
-    }
+    const LayoutGeom g = layout_geom(layout, nx, ny, nz);
+    const long long nb = (long long)g.nbx * g.nby * g.nbz;
+    return layout == LAYOUT_CORNER8 ? nb * 64 : nb * g.brick;
 }
-int elem_bytes(int layout) { return layout == LAYOUT_CORNER8 ? 8 : layout == LAYOUT_QUAD ? 4 : 1; }
+int elem_bytes(int layout) { return layout == LAYOUT_CORNER8 ? 8 : 1; }
 }  // namespace
 
 size_t layout_plane_bytes(int layout, int nx, int ny, int nz)
 {
     const size_t b = (size_t)layout_elems(layout, nx, ny, nz) * elem_bytes(layout);
-    return (b + 16 + 255) & ~(size_t)255;  // +16: the last u16 pair may read one byte past the data
+    return (b + 255) & ~(size_t)255;
 }
 
 hipError_t launch_build_layout(int layout, const uint8_t* d_planar, int nx, int ny, int nz, uint8_t* d_out,
                                hipStream_t s)
 {
+    const LayoutGeom g = layout_geom(layout, nx, ny, nz);
     const long long elems = layout_elems(layout, nx, ny, nz);
     const long long pb = (long long)layout_plane_bytes(layout, nx, ny, nz);
-    const dim3 g(grid_for(4 * elems)), b(kBlock);
+    const dim3 gr(grid_for(4 * elems)), b(kBlock);
     switch (layout) {
-    case LAYOUT_PAD16: hipLaunchKernelGGL(k_build_layout<LAYOUT_PAD16>, g, b, 0, s, d_planar, nx, ny, nz, elems, pb, d_out); break;
-    case LAYOUT_BRICK5: hipLaunchKernelGGL(k_build_layout<LAYOUT_BRICK5>, g, b, 0, s, d_planar, nx, ny, nz, elems, pb, d_out); break;
-    case LAYOUT_CORNER8: hipLaunchKernelGGL(k_build_layout<LAYOUT_CORNER8>, g, b, 0, s, d_planar, nx, ny, nz, elems, pb, d_out); break;
-    case LAYOUT_QUAD: hipLaunchKernelGGL(k_build_layout<LAYOUT_QUAD>, g, b, 0, s, d_planar, nx, ny, nz, elems, pb, d_out); break;
+    case LAYOUT_BRICK5: hipLaunchKernelGGL(k_build_layout<LAYOUT_BRICK5>, gr, b, 0, s, d_planar, nx, ny, nz, g, elems, pb, d_out); break;
+    case LAYOUT_BRICK8: hipLaunchKernelGGL(k_build_layout<LAYOUT_BRICK8>, gr, b, 0, s, d_planar, nx, ny, nz, g, elems, pb, d_out); break;
+    case LAYOUT_BRICK16: hipLaunchKernelGGL(k_build_layout<LAYOUT_BRICK16>, gr, b, 0, s, d_planar, nx, ny, nz, g, elems, pb, d_out); break;
+    case LAYOUT_CORNER8: hipLaunchKernelGGL(k_build_layout<LAYOUT_CORNER8>, gr, b, 0, s, d_planar, nx, ny, nz, g, elems, pb, d_out); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
