@@ -175,10 +175,12 @@ const char* vr_kernel_variant(void* ctx);
  * used only where clamp-to-edge equals mirrored repeat.  Otherwise the
  * planar, mirrored-repeat kernel runs.  Rebuilds the layout (synchronous). */
 vr_status vr_set_layout_preference(void* ctx, int pref);
-/* Tuning knobs: "layout" (as above), "schedule"
- * (0 = one static 16x16 tile per workgroup, 1 = persistent waves pulling
- * 8x8 tiles from per-XCD queues, the default) and "waves_per_simd" (1-8,
- * for the queue schedule).  vr_get_option returns -1 for an unknown name.  */
+/* Tuning knobs: "layout" (as above); "schedule"
+ * (-1 = auto, the default; 0 = one static 16x16 tile per workgroup, with
+ * tile rows dealt to XCDs; 1 = persistent waves pulling 8x8 tiles from
+ * per-XCD queues; 2 = each wave renders "tiles_per_wave" strided 8x8
+ * tiles); "waves_per_simd" (1-8, queue schedule); "tiles_per_wave" (1-64,
+ * strided schedule).  vr_get_option returns -1 for an unknown name.        */
 vr_status vr_set_option(void* ctx, const char* name, int value);
 int       vr_get_option(void* ctx, const char* name);
 

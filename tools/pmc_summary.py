@@ -1,0 +1,43 @@
+"""Summarise tools/pmc.sh output: mean per march-kernel dispatch + derived."""
+import collections
+import csv
+import glob
+import json
+import sys
+
+
+def load(tag, kernel="march"):
+    agg = collections.defaultdict(list)
+    for f in sorted(glob.glob(f"gpurun_out/pmc_{tag}/p*/run_counter_collection.csv")):
+        for row in csv.DictReader(open(f)):
+            if kernel not in row["Kernel_Name"]:
+                continue
+            agg[row["Counter_Name"]].append(float(row["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in agg.items()}
+
+
+def derived(c):
+    d = {}
+    if "GRBM_GUI_ACTIVE" in c:
+        d["gpu_cycles_per_xcd"] = c["GRBM_GUI_ACTIVE"] / 8
+    if "SQ_ACTIVE_INST_VALU" in c and "GRBM_GUI_ACTIVE" in c:
+        # quad-cycles of VALU issue over all SIMDs vs SIMD quad-cycles available
+        d["valu_busy"] = c["SQ_ACTIVE_INST_VALU"] / (1024 * c["GRBM_GUI_ACTIVE"] / 8 / 4)
+    for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+        if k in c and "SQ_WAVE_CYCLES" in c:
+            d[k + "_frac"] = c[k] / c["SQ_WAVE_CYCLES"]
+    if "TCC_HIT_sum" in c:
+        d["l2_hit"] = c["TCC_HIT_sum"] / max(1.0, c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
+    if "TCP_TCC_READ_REQ_sum" in c and "TCP_TOTAL_CACHE_ACCESSES_sum" in c:
+        d["l1_miss_ratio"] = c["TCP_TCC_READ_REQ_sum"] / max(1.0, c["TCP_TOTAL_CACHE_ACCESSES_sum"])
+    if "FETCH_SIZE" in c:
+        d["fetch_MB_x2"] = c["FETCH_SIZE"] * 1024 * 2 / 1e6   # gfx950: FETCH_SIZE under-counts 2x
+    if "TCC_EA0_RDREQ_sum" in c:
+        d["ea_rdreq_MB_64B"] = c["TCC_EA0_RDREQ_sum"] * 64 / 1e6
+    return d
+
+
+if __name__ == "__main__":
+    for tag in sys.argv[1:]:
+        c = load(tag)
+        print(tag, json.dumps({k: round(v, 4) for k, v in {**c, **derived(c)}.items()}, indent=0))

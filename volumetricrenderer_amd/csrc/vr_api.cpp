@@ -42,7 +42,7 @@ vr_status fail(vr_status st, const char* fmt, ...)
                         #expr, hipGetErrorString(e_), __FILE__, __LINE__);                   \
     } while (0)
 
-constexpr int kDefaultSchedule = 2;      // 0 = static tiles, 1 = persistent queue, 2 = strided
+constexpr int kDefaultSchedule = -1;     // -1 auto, 0 static tiles, 1 persistent queue, 2 strided
 constexpr int kDefaultWavesPerSimd = 4;
 constexpr int kDefaultTilesPerWave = 1;
 
@@ -67,7 +67,14 @@ struct Ctx {
     int* d_heads = nullptr;        // 8 queue heads (+ padding), zeroed per launch
 };
 
-constexpr int kDefaultFastLayout = LAYOUT_BRICK5;
+// Auto layout (measured): CORNER8 does one load per tap but
+// stores 8 bytes per texel.  It wins while the volume fits the 256 MiB
+// Infinity Cache.  Past that it is HBM-bound, and BRICK8 (1.49x bytes) wins.
+constexpr size_t kCorner8MaxBytes = 160ull << 20;
+int auto_layout(int nx, int ny, int nz)
+{
+    return 4 * layout_plane_bytes(LAYOUT_CORNER8, nx, ny, nz) <= kCorner8MaxBytes ? LAYOUT_CORNER8 : LAYOUT_BRICK8;
+}
 
 Ctx* as_ctx(void* p) { return static_cast<Ctx*>(p); }
 
@@ -90,7 +97,7 @@ bool dims_ok(int nx, int ny, int nz)
 
 int wanted_fast_layout(const Ctx* c)
 {
-    const int want = c->layout_pref == 0 ? kDefaultFastLayout : c->layout_pref;
+    const int want = c->layout_pref == 0 ? auto_layout(c->nx, c->ny, c->nz) : c->layout_pref;
     if (want == LAYOUT_PLANAR) return 0;
     // 32-bit offsets inside the kernels: fall back to PAD16 if too large
     // and LDS offset tables of (nx+ny+nz+3) words: fall back to planar
@@ -479,8 +486,8 @@ vr_status vr_set_option(void* p, const char* name, int value)
     const std::string n(name);
     if (n == "layout") return vr_set_layout_preference(p, value);
     if (n == "schedule") {
-        if (value < 0 || value > 2)
-            return fail(VR_ERR_INVALID, "vr_set_option: schedule is 0 (static), 1 (queue) or 2 (strided)");
+        if (value < -1 || value > 2)
+            return fail(VR_ERR_INVALID, "vr_set_option: schedule is -1 (auto), 0 (static), 1 (queue) or 2 (strided)");
         c->schedule = value;
         return VR_OK;
     }
@@ -583,7 +590,10 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
     a.format = t->format;
     a.step_counter = reinterpret_cast<unsigned long long*>(t->step_counter);
     HIP_TRY(hipSetDevice(c->device));
-    const Schedule sc{c->schedule, c->tiles_per_wave, c->waves_per_simd, c->d_heads};
+    // auto schedule (measured): static XCD-row tiles for the cache-resident
+    // CORNER8 volume, strided single tiles otherwise
+    const int kind = c->schedule >= 0 ? c->schedule : (pl.layout == LAYOUT_CORNER8 ? SCHED_STATIC : SCHED_STRIDED);
+    const Schedule sc{kind, c->tiles_per_wave, c->waves_per_simd, c->d_heads};
     HIP_TRY(launch_march(a, pl.layout, pl.wrap, pl.early, sc, static_cast<hipStream_t>(stream)));
     return VR_OK;
 }
