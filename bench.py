@@ -66,7 +66,7 @@ def cpu_baseline(volume_host: np.ndarray, osd, gsd, march, width, height, budget
         steps += s
         reps += 1
         el = time.perf_counter() - t0
-        if el >= budget_s or reps >= 64:
+        if el >= budget_s or reps >= 2000:
             break
     mray = rows * width * march.max_steps / el / 1e6
     return {"value": round(mray, 3), "unit": "Mray/s", "cores": threads, "kind": "port",
