@@ -277,3 +277,19 @@ def test_config5_grid512_bands(r, oracle):
         rows = [(first + (i // 16) * 24) * 16 + i % 16 for i in range(ref.shape[0])]
         keep = [i for i, y in enumerate(rows) if y < H]
         assert_exact(a[[rows[i] for i in keep]], ref[keep])
+
+
+def test_config1_matches_golden_fixture(r):
+    """The HIP path against the committed config-1 frame (tests/golden)."""
+    import os
+    import sys
+    golden = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    sys.path.insert(0, golden)
+    from make_golden import perlin_cube_volume
+    ref = np.load(os.path.join(golden, "config1_256x256x32.npy"))
+    r.set_volume(perlin_cube_volume())
+    osd, gsd = vr.reference_shader_data(1.0)
+    r.set_shader_data(osd, gsd)
+    r.set_march(vr.march_defaults(max_steps=32))
+    img = r.render(256, 256, vr.FMT_RGBA32F).cpu().numpy()
+    assert np.array_equal(img[..., 0], ref)

@@ -1,0 +1,182 @@
+"""Known-answer tests that pin the CPU oracle to the reference's semantics.
+
+The reference ships no tests or golden vectors and cannot be run here
+(SURVEY.md sec. 4, sec. 8c).  So the oracle is pinned by answers derived
+independently of its code:
+  * geometry: SURVEY.md sec. 6 analytic coverage / step-count figures for the
+    reference camera (TestMain.cpp:225-226) and march constants
+    (frag.glsl:29-46);
+  * closed forms: constant and linear-ramp volumes, where trilinear filtering
+    and the march have exact answers;
+  * Vulkan MIRRORED_REPEAT addressing (VulkanCore.cpp:683-685), restated here
+    straight from the Vulkan spec formula;
+  * the volume recipe's quirks (TestMain.cpp:60, :76);
+  * committed fixtures (tests/golden/make_golden.py), against regressions.
+"""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+# -- geometry vs SURVEY.md sec. 6 --------------------------------------------
+@pytest.mark.parametrize("W,H,steps,aspect,cov,maxn,mean,executed", [
+    (256, 256, 32, 1.0, 0.379, 27, 9.1, 2.26e5),
+    (1280, 720, 128, 1280 / 720, 0.213, 110, 37.9, 7.44e6),
+    (1920, 1080, 128, 1280 / 720, 0.213, 110, 37.9, 1.674e7),
+    (3840, 2160, 256, 1280 / 720, 0.213, 221, 76.3, 1.348e8),
+])
+def test_geometry_matches_survey(oracle, W, H, steps, aspect, cov, maxn, mean, executed):
+    obj, glob = oracle.reference_shader_data(aspect)
+    n = oracle.step_counts(obj, glob, oracle.march(steps), W, H)
+    covered = n >= 0
+    assert abs(covered.mean() - cov) < 0.0006
+    assert n.max() == maxn
+    assert abs(n[covered].mean() - mean) < 0.06
+    assert abs(n[covered].sum() / executed - 1) < 0.003
+
+
+def slab_n(obj, glob, W, H, steps):
+    """Independent float64 restatement of frag.glsl:18-46 for the reference
+    camera (Model = I): per-pixel step counts."""
+    eye = np.array([3.0, 3.0, 3.0])
+    f = -eye / np.linalg.norm(eye)
+    s = np.cross(f, [0, 0, 1.0]); s /= np.linalg.norm(s)
+    u = np.cross(s, f)
+    th = math.tan(math.radians(45.0) / 2)
+    aspect = W / H
+    xs = ((np.arange(W) + 0.5) / W * 2 - 1) * th * aspect
+    ys = -((np.arange(H) + 0.5) / H * 2 - 1) * th
+    d = f[None, None, :] + xs[None, :, None] * s[None, None, :] + ys[:, None, None] * u[None, None, :]
+    d /= np.linalg.norm(d, axis=2, keepdims=True)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        t0 = (-1 - eye) / d
+        t1 = (1 - eye) / d
+    tn = np.minimum(t0, t1).max(axis=2)
+    tf = np.maximum(t0, t1).min(axis=2)
+    hit = tn <= tf
+    n = np.where(hit, np.minimum(steps, np.floor((tf - tn) / (4.0 / steps))), -1)
+    return n.astype(np.int64)
+
+
+def test_step_counts_match_float64_restatement(oracle):
+    obj, glob = oracle.reference_shader_data(16 / 9)
+    W, H = 640, 360
+    n = oracle.step_counts(obj, glob, oracle.march(128), W, H)
+    ref = slab_n(obj, glob, W, H, 128)
+    # truncation boundaries may flip by one step where fp32 and fp64 disagree
+    diff = np.abs(n - ref)
+    assert (diff > 1).sum() == 0
+    assert (diff == 1).mean() < 1e-3
+    assert ((n >= 0) != (ref >= 0)).mean() < 1e-3   # silhouette edge pixels only
+
+
+# -- closed forms ----------------------------------------------------------------
+def test_constant_volume_closed_form(oracle):
+    v = 173
+    vol = np.full((8, 8, 8, 4), v, np.uint8)
+    obj, glob = oracle.reference_shader_data(1.0)
+    W = H = 96
+    img, _ = oracle.render(vol, obj, glob, oracle.march(32), W, H, oracle.FMT_RGBA32F)
+    n = oracle.step_counts(obj, glob, oracle.march(32), W, H)
+    s = v / 255.0
+    cur = s * s * (2 * s) * 0.2                    # frag.glsl:71
+    expect = np.where(n >= 0, 1 - np.exp(-np.maximum(n, 0) * cur * (4.0 / 32)), 0.0)   # :76-79
+    assert np.abs(img[..., 0] - expect).max() < 2e-6
+    assert (img[..., 3] == 1.0).all()
+    assert (img[..., 0] == img[..., 1]).all() and (img[..., 0] == img[..., 2]).all()
+
+
+def test_linear_ramp_is_filtered_exactly(oracle):
+    N = 64
+    x = np.arange(N, dtype=np.uint8)
+    vol = np.broadcast_to(x[None, None, :, None], (N, N, N, 4)).copy()
+    rng = np.random.default_rng(3)
+    for _ in range(200):
+        p = rng.uniform(0.0, 1.0, size=3)
+        got = oracle.sample(vol, 0, p)
+        g = p[0] * N - 0.5
+        expect = min(max(g, 0.0), N - 1.0) / 255.0
+        assert abs(got - expect) < 3e-6, (p, got, expect)
+
+
+def vulkan_mirror(i, n):
+    """Vulkan spec: mirror(a) = a >= 0 ? a : -(1+a); (size-1) - mirror((i mod 2size) - size)."""
+    a = (i % (2 * n)) - n
+    m = a if a >= 0 else -(1 + a)
+    return (n - 1) - m
+
+
+@pytest.mark.parametrize("n", [1, 2, 4, 7, 128])
+def test_mirrored_repeat_index(oracle, n):
+    L = oracle.lib()
+    for i in range(-3 * n - 2, 3 * n + 3):
+        assert L.vro_mirror(i, n) == vulkan_mirror(i, n), (i, n)
+
+
+def test_mirrored_repeat_sampling_symmetry(oracle):
+    vol = np.random.default_rng(5).integers(0, 256, size=(10, 12, 14, 4), dtype=np.uint8)
+    rng = np.random.default_rng(6)
+    for _ in range(200):
+        p = rng.uniform(0.05, 0.95, size=3)
+        a = oracle.sample(vol, 2, p)
+        b = oracle.sample(vol, 2, (2.0 - p[0], -p[1], 2.0 + p[2]))   # reflected / shifted by 2
+        assert abs(a - b) < 2e-5
+
+
+def test_expf_accuracy(oracle):
+    L = oracle.lib()
+    for x in np.linspace(-80.0, 0.0, 4001, dtype=np.float32):
+        got = L.vro_expf(float(x))
+        ref = math.exp(float(x))
+        assert abs(got - ref) <= 4e-7 * ref + 1e-38, (x, got, ref)
+
+
+# -- volume recipe (TestMain.cpp:43-92) -----------------------------------------
+def test_volume_recipe_quirks(oracle):
+    lit = oracle.build_volume(32, literal=True)
+    fixed = oracle.build_volume(32, literal=False)
+    # G comes from the all-zero noiseOutput2 (TestMain.cpp:76): constant
+    assert (lit[..., 1] == lit[0, 0, 0, 1]).all()
+    assert not (fixed[..., 1] == fixed[0, 0, 0, 1]).all()
+    # B and A do not depend on the overwrite
+    assert (lit[..., 2] == fixed[..., 2]).all() and (lit[..., 3] == fixed[..., 3]).all()
+    # normalised + inverted: the extremes reach 0 and 255 (255*(1-0) truncates to 255)
+    for c in (2, 3):
+        assert fixed[..., c].max() == 255 and fixed[..., c].min() == 0
+
+
+def test_perlin_vanishes_on_the_lattice(oracle):
+    L = oracle.lib()
+    for p in [(0, 0, 0), (3, -7, 11), (100, 200, -300)]:
+        assert L.vro_perlin3(3, *map(float, p)) == 0.0
+
+
+# -- committed fixtures -------------------------------------------------------------
+def test_golden_noise_kat(oracle):
+    kat = json.load(open(os.path.join(GOLDEN, "noise_kat.json")))
+    L = oracle.lib()
+    for name, f in (("perlin", L.vro_perlin3), ("simplex", L.vro_simplex3), ("cellular", L.vro_cellular3)):
+        for seed, vals in kat[name].items():
+            got = [float(np.float32(f(int(seed), *p))) for p in kat["points"]]
+            assert got == vals, name
+
+
+def test_golden_volume16(oracle):
+    ref = np.load(os.path.join(GOLDEN, "volume16_literal.npy"))
+    assert np.array_equal(oracle.build_volume(16), ref)
+
+
+def test_golden_config1_frame(oracle):
+    import sys
+    sys.path.insert(0, GOLDEN)
+    from make_golden import perlin_cube_volume
+    ref = np.load(os.path.join(GOLDEN, "config1_256x256x32.npy"))
+    obj, glob = oracle.reference_shader_data(1.0)
+    img, steps = oracle.render(perlin_cube_volume(), obj, glob, oracle.march(32), 256, 256, oracle.FMT_RGBA32F)
+    assert np.array_equal(img[..., 0], ref)
+    assert steps == json.load(open(os.path.join(GOLDEN, "noise_kat.json")))["config1_steps"]
