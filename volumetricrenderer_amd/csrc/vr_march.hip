@@ -252,6 +252,13 @@ __device__ __forceinline__ unsigned march_pixel(const MarchArgs& a, const FastCt
     return n > 0 ? (unsigned)i : 0u;
 }
 
+// Lane -> pixel inside an 8x8 wave tile.  The TA serves a gather in 16-lane
+// groups, and its cost tracks the distinct cache lines per group
+// (tools/tcp_calib.hip).  Each group is therefore a compact 4x4 pixel block,
+// not an 8x2 strip.
+__device__ __forceinline__ int lane_x(int lane) { return (lane & 3) | ((lane >> 2) & 4); }
+__device__ __forceinline__ int lane_y(int lane) { return ((lane >> 2) & 3) | ((lane >> 3) & 4); }
+
 __device__ __forceinline__ void add_steps(const MarchArgs& a, unsigned long long cnt)
 {
     for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
@@ -297,8 +304,8 @@ __global__ __launch_bounds__(kThreads) void march_grid(const MarchArgs a)
     if (ty >= a.tiles_y) return;   // whole workgroup: uniform, before the barrier
     const FastCtx f = fast_prologue<LAYOUT>(a, lds);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int x = tx * kTile + (wave & 1) * 8 + (lane & 7);
-    const int orow = ty * kTile + (wave >> 1) * 8 + (lane >> 3);
+    const int x = tx * kTile + (wave & 1) * 8 + lane_x(lane);
+    const int orow = ty * kTile + (wave >> 1) * 8 + lane_y(lane);
     const unsigned steps = march_pixel<LAYOUT, WRAP, EARLY>(a, f, x, orow);
     if (a.step_counter) add_steps(a, steps);
 }
@@ -318,7 +325,7 @@ __global__ __launch_bounds__(kThreads) void march_strided(const MarchArgs a, int
     unsigned long long steps = 0;
     for (int t = g; t < ntiles; t += nw) {
         const int ty = t / tiles_x8, tx = t - ty * tiles_x8;
-        steps += march_pixel<LAYOUT, WRAP, EARLY>(a, f, tx * 8 + (lane & 7), ty * 8 + (lane >> 3));
+        steps += march_pixel<LAYOUT, WRAP, EARLY>(a, f, tx * 8 + lane_x(lane), ty * 8 + lane_y(lane));
     }
     if (a.step_counter) add_steps(a, steps);
 }
@@ -347,7 +354,7 @@ __global__ __launch_bounds__(kThreads) void march_queue(const MarchArgs a, int* 
         const int m = k / per_pair, rem = k - m * per_pair;
         const int row8 = 2 * (q + 8 * m) + (rem & 1), tx = rem >> 1;
         if (row8 >= rows8) continue;
-        steps += march_pixel<LAYOUT, WRAP, EARLY>(a, f, tx * 8 + (lane & 7), row8 * 8 + (lane >> 3));
+        steps += march_pixel<LAYOUT, WRAP, EARLY>(a, f, tx * 8 + lane_x(lane), row8 * 8 + lane_y(lane));
     }
     if (a.step_counter) add_steps(a, steps);
 }
