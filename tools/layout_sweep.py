@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--steps", type=int, default=128)
+    ap.add_argument("--no-check", action="store_true", help="skip the cross-layout image check (timing builds)")
     args = ap.parse_args()
     W, H, S = args.width, args.height, args.steps
     if args.variants:
@@ -65,7 +66,7 @@ def main():
                 img = r.render(W, H, vr.FMT_RGBA8_UNORM, out=out).cpu().numpy()
                 if ref is None:
                     ref = img
-                assert np.array_equal(img, ref), f"layout {lay} differs at N={n}"
+                assert args.no_check or np.array_equal(img, ref), f"layout {lay} differs at N={n}"
             for _ in range(args.rounds):
                 for lay in layouts:
                     apply(r, lay)
