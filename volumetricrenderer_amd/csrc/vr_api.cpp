@@ -486,8 +486,9 @@ vr_status vr_set_option(void* p, const char* name, int value)
     const std::string n(name);
     if (n == "layout") return vr_set_layout_preference(p, value);
     if (n == "schedule") {
-        if (value < -1 || value > 2)
-            return fail(VR_ERR_INVALID, "vr_set_option: schedule is -1 (auto), 0 (static), 1 (queue) or 2 (strided)");
+        if (value < -1 || value > 3)
+            return fail(VR_ERR_INVALID,
+                        "vr_set_option: schedule is -1 (auto), 0 (static), 1 (queue), 2 (strided) or 3 (xcd rows)");
         c->schedule = value;
         return VR_OK;
     }

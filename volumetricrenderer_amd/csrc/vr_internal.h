@@ -95,7 +95,7 @@ struct MarchArgs {
 };
 
 // How the march kernel maps tiles to waves.
-enum ScheduleKind : int { SCHED_STATIC = 0, SCHED_QUEUE = 1, SCHED_STRIDED = 2 };
+enum ScheduleKind : int { SCHED_STATIC = 0, SCHED_QUEUE = 1, SCHED_STRIDED = 2, SCHED_XCDROWS = 3 };
 struct Schedule {
     int kind;
     int tiles_per_wave;    // strided: 8x8 tiles per wave

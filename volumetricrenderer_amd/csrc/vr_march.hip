@@ -112,8 +112,17 @@ __device__ __forceinline__ float tap_fast(const FastCtx& f, int ch, float gx, fl
         // q0 = c000 c100 c010 c110, q1 = c001 c101 c011 c111
         return blend(f2{ubyte<0>(q0), ubyte<0>(q1)}, f2{ubyte<1>(q0), ubyte<1>(q1)},
                      f2{ubyte<2>(q0), ubyte<2>(q1)}, f2{ubyte<3>(q0), ubyte<3>(q1)}, wx, wy, wz);
+    } else if constexpr (LAYOUT == LAYOUT_BRICK5) {
+        // R = 5: the two rows of a z-slice sit 5 bytes apart, so one 8-byte
+        // load at `off` covers c000 c100 . . . c010 c110 and one at off+25
+        // covers the z1 slice.  Two loads per tap; they never leave the
+        // brick's 128-B line (bytes <= 125).
+        const uint2 z0 = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(f.rsrc[ch], off, 0, 0));
+        const uint2 z1 = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(f.rsrc[ch], off + 25, 0, 0));
+        return blend(f2{ubyte<0>(z0.x), ubyte<0>(z1.x)}, f2{ubyte<1>(z0.x), ubyte<1>(z1.x)},
+                     f2{ubyte<1>(z0.y), ubyte<1>(z1.y)}, f2{ubyte<2>(z0.y), ubyte<2>(z1.y)}, wx, wy, wz);
     } else {
-        constexpr int R = LAYOUT == LAYOUT_BRICK5 ? 5 : LAYOUT == LAYOUT_BRICK8 ? 8 : 16;
+        constexpr int R = LAYOUT == LAYOUT_BRICK8 ? 8 : 16;
         const unsigned v00 = __builtin_amdgcn_raw_buffer_load_b16(f.rsrc[ch], off, 0, 0);
         const unsigned v10 = __builtin_amdgcn_raw_buffer_load_b16(f.rsrc[ch], off + R, 0, 0);
         const unsigned v01 = __builtin_amdgcn_raw_buffer_load_b16(f.rsrc[ch], off + R * R, 0, 0);
@@ -330,6 +339,27 @@ __global__ __launch_bounds__(kThreads) void march_strided(const MarchArgs a, int
     if (a.step_counter) add_steps(a, steps);
 }
 
+// XCD-row schedule: one 8x8 tile per wave, 4 horizontally adjacent tiles per
+// workgroup.  8-px tile rows are dealt to XCDs round-robin: XCD x walks rows
+// x, x+8, ... (blockIdx % 8, speed-only).  Rows interleave, so the balance
+// holds, and a row's neighbours share one L2.
+template <int LAYOUT, int WRAP, bool EARLY>
+__global__ __launch_bounds__(kThreads) void march_xcdrows(const MarchArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned lds[];
+    const int tiles_x8 = (a.width + 7) >> 3, rows8 = (a.out_rows + 7) >> 3;
+    const int groups = (tiles_x8 + 3) >> 2;
+    const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+    const int k = j / groups, gx = j - k * groups;
+    const int ty = xcd + 8 * k;
+    if (ty >= rows8) return;   // whole workgroup, before the barrier
+    const FastCtx f = fast_prologue<LAYOUT>(a, lds);
+    const int lane = threadIdx.x & 63, tx = gx * 4 + (threadIdx.x >> 6);
+    unsigned long long steps = 0;
+    if (tx < tiles_x8) steps = march_pixel<LAYOUT, WRAP, EARLY>(a, f, tx * 8 + lane_x(lane), ty * 8 + lane_y(lane));
+    if (a.step_counter) add_steps(a, steps);
+}
+
 // Queue schedule: persistent waves pull 8x8 tiles from 8 queues, one per
 // XCD group (blockIdx % 8, speed-only).  Queue q owns the 16-row tile pairs
 // p = q, q+8, ..., walked column by column.  heads[] is zeroed by a memset
@@ -373,6 +403,15 @@ hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStre
             hipLaunchKernelGGL((march_strided<L, W, true>), grid, block, lds, s, a, 4 * (int)grid.x);
         else
             hipLaunchKernelGGL((march_strided<L, W, false>), grid, block, lds, s, a, 4 * (int)grid.x);
+        return hipGetLastError();
+    }
+    if (sc.kind == SCHED_XCDROWS) {
+        const int groups = (((a.width + 7) >> 3) + 3) >> 2, rows8 = (a.out_rows + 7) >> 3;
+        const dim3 grid(8 * ((rows8 + 7) / 8) * groups);
+        if (early)
+            hipLaunchKernelGGL((march_xcdrows<L, W, true>), grid, block, lds, s, a);
+        else
+            hipLaunchKernelGGL((march_xcdrows<L, W, false>), grid, block, lds, s, a);
         return hipGetLastError();
     }
     if (sc.kind == SCHED_QUEUE) {
