@@ -83,19 +83,26 @@ def main() -> int:
     ap.add_argument("--config", default="grid512", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: rehearse the N>1 path with several ranks on one GPU")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
+    dev = local % max(1, ndev)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group("gloo")
     else:
         torch.cuda.set_device(0)
     N, W, H, S, cfg_idx = CONFIGS[args.config]
 
-    r = vr.Renderer(local)
+    r = vr.Renderer(dev)
     r.generate_volume(vr.scaled_recipe(N))
     osd, gsd = vr.reference_shader_data(1280.0 / 720.0)
     r.set_shader_data(osd, gsd)
@@ -110,7 +117,8 @@ def main() -> int:
     sharder.render_local(step_counter=counter)
     torch.cuda.synchronize()
     local_steps = int(counter.item())
-    tot = torch.tensor([local_steps], dtype=torch.int64, device="cuda")
+    red_dev = "cuda" if args.backend == "nccl" else "cpu"
+    tot = torch.tensor([local_steps], dtype=torch.int64, device=red_dev)
     if world > 1:
         dist.all_reduce(tot)
     frame_steps = int(tot.item())
@@ -129,7 +137,7 @@ def main() -> int:
         dist.barrier()
     el = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    tt = torch.tensor([el, kern_ms], dtype=torch.float64, device="cuda")
+    tt = torch.tensor([el, kern_ms], dtype=torch.float64, device=red_dev)
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     el, kern_ms_max = float(tt[0]), float(tt[1])
@@ -162,6 +170,7 @@ def main() -> int:
                        "baseline_config_index": cfg_idx, "width": W, "height": H, "max_steps": S,
                        "volume": f"{N}^3 RGBA8", "camera": "reference (TestMain.cpp:219-245)",
                        "kernel": r.kernel_variant, "parallelism": f"bands16x{world}",
+                       "collective": f"gather to rank 0 ({args.backend})" if world > 1 else None,
                        "executed_steps_per_frame": frame_steps},
             "executed_steps_per_s": round(frame_steps * args.steps / el, 1),
             "kernel_ms_mean": round(kern_ms, 5),

@@ -261,12 +261,13 @@ __device__ __forceinline__ unsigned march_pixel(const MarchArgs& a, const FastCt
     return n > 0 ? (unsigned)i : 0u;
 }
 
-// Lane -> pixel inside an 8x8 wave tile.  The TA serves a gather in 16-lane
-// groups, and its cost tracks the distinct cache lines per group
-// (tools/tcp_calib.hip).  Each group is therefore a compact 4x4 pixel block,
-// not an 8x2 strip.
-__device__ __forceinline__ int lane_x(int lane) { return (lane & 3) | ((lane >> 2) & 4); }
-__device__ __forceinline__ int lane_y(int lane) { return ((lane >> 2) & 3) | ((lane >> 3) & 4); }
+// Lane -> pixel inside an 8x8 wave tile: row-major, so each 16-lane TA
+// group (tools/tcp_calib.hip) is an 8x2 strip.  Compact 4x4 groups were
+// measured and are no better for brick5 and 15 % slower for brick8: brick8's
+// 128-B lines are z-slabs, and a screen-horizontal strip stays inside one
+// (DESIGN.md sec. 5.1).
+__device__ __forceinline__ int lane_x(int lane) { return lane & 7; }
+__device__ __forceinline__ int lane_y(int lane) { return lane >> 3; }
 
 __device__ __forceinline__ void add_steps(const MarchArgs& a, unsigned long long cnt)
 {

@@ -73,8 +73,17 @@ class BandSharder:
         self.render_local(events=events)
         if self.world == 1:
             return self.frame_buf
-        gl = list(self.gathered.unbind(0)) if self.rank == 0 else None
-        dist.gather(self.local, gather_list=gl, dst=0, group=self.group)
+        if self.local.is_cuda and dist.get_backend(self.group) == "gloo":
+            # gloo moves host memory only: stage through the host (tests and
+            # one-GPU rehearsals; RCCL gathers device buffers directly)
+            loc = self.local.cpu()
+            gl = [torch.empty_like(loc) for _ in range(self.world)] if self.rank == 0 else None
+            dist.gather(loc, gather_list=gl, dst=0, group=self.group)
+            if self.rank == 0:
+                self.gathered.copy_(torch.stack(gl))
+        else:
+            gl = list(self.gathered.unbind(0)) if self.rank == 0 else None
+            dist.gather(self.local, gather_list=gl, dst=0, group=self.group)
         if self.rank == 0:
             self.r.assemble_bands(self.gathered, self.world, self.width, self.height, self.band_rows,
                                   frame=self.frame_buf)
