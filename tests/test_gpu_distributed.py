@@ -1,0 +1,67 @@
+"""Multi-rank frame path on a real GPU: 2 ranks share the one GPU of the test
+box and gather over gloo.  The 8-GPU RCCL run is the driver's.  The rank-0
+frame, assembled by vr_assemble_bands, must equal a one-rank render."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+
+    import volumetricrenderer_amd as vr
+    from volumetricrenderer_amd.distributed import BandSharder
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        W, H = 640, 360
+        with vr.Renderer(0) as r:
+            r.generate_volume(vr.volume_recipe_defaults(size=64))
+            osd, gsd = vr.reference_shader_data(W / H, 10.0, 20.0)
+            r.set_shader_data(osd, gsd)
+            r.set_march(vr.march_defaults())
+            sh = BandSharder(r, W, H, vr.FMT_RGBA32F, band_rows=16, world=world, rank=rank)
+            frame = sh.frame()
+            torch.cuda.synchronize()
+            if rank == 0:
+                full = r.render(W, H, vr.FMT_RGBA32F).cpu().numpy()
+                q.put(("ok", bool(np.array_equal(frame.cpu().numpy(), full))))
+            else:
+                q.put(("ok", True))
+            sh.close()
+    except Exception as e:  # pragma: no cover
+        q.put(("err", repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_ranks_on_one_gpu_assemble_the_frame(world):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(rk, world, port, q)) for rk in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r == ("ok", True) for r in res), res
