@@ -123,15 +123,13 @@ def main() -> int:
         dist.all_reduce(tot)
     frame_steps = int(tot.item())
 
-    for _ in range(args.warmup):
-        sharder.frame()
+    sharder.run_frames(args.warmup)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        sharder.frame(events=ev[k])
+    sharder.run_frames(args.steps, events=ev)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -64,7 +64,7 @@ def _worker(rank, world, port, W, H, q):
         obj, glob = oracle.reference_shader_data(W / H, 25.0, -10.0)
         r = OracleRenderer(oracle, vol, obj, glob, oracle.march(64))
         sh = BandSharder(r, W, H, 0, band_rows=16, world=world, rank=rank)
-        frame = sh.frame()
+        frame = sh.run_frames(3)
         if rank == 0:
             ref, _ = oracle.render(vol, obj, glob, oracle.march(64), W, H, 0)
             q.put(("ok", bool(np.array_equal(frame.numpy(), ref)), int(sh.my_rows)))

@@ -90,7 +90,56 @@ class BandSharder:
             return self.frame_buf
         return self.local
 
+    def run_frames(self, k: int, events=None):
+        """Render k frames with two in flight, mirroring the reference's
+        2 frames in flight (VulkanRenderer.cpp:13).  Frame i's gather (RCCL
+        stream) overlaps frame i+1's render (compute stream).  Band sets,
+        gather buffers and frames are double-buffered.  Each buffer of a
+        parity is reused only after the stream order has retired its last
+        reader.  Returns the last frame (rank 0) or band set."""
+        if self.world == 1 or (self.local.is_cuda and dist.get_backend(self.group) == "gloo"):
+            out = None
+            for i in range(k):
+                out = self.frame(events=events[i] if events else None)
+            return out
+        if not hasattr(self, "_pipe"):
+            self._pipe = {
+                "local": [self.local, torch.empty_like(self.local)],
+                "gathered": [self.gathered, torch.empty_like(self.gathered)] if self.rank == 0 else [None, None],
+                "frame": [self.frame_buf, torch.empty_like(self.frame_buf)] if self.rank == 0 else [None, None],
+            }
+        P = self._pipe
+        pending = None
+
+        def finish(p):
+            work, par = p
+            work.wait()   # the current stream waits for the gather
+            if self.rank == 0:
+                self.r.assemble_bands(P["gathered"][par], self.world, self.width, self.height, self.band_rows,
+                                      frame=P["frame"][par])
+
+        last = None
+        for i in range(k):
+            par = i & 1
+            loc = P["local"][par]
+            ev = events[i] if events else None
+            if ev is not None:
+                ev[0].record()
+            self.r.render(self.width, self.height, self.fmt, out=loc[: self.my_rows], band_rows=self.band_rows,
+                          band_stride=self.world, band_first=self.rank)
+            if ev is not None:
+                ev[1].record()
+            gl = list(P["gathered"][par].unbind(0)) if self.rank == 0 else None
+            work = dist.gather(loc, gather_list=gl, dst=0, group=self.group, async_op=True)
+            if pending is not None:
+                finish(pending)
+            pending = (work, par)
+            last = par
+        finish(pending)
+        return P["frame"][last] if self.rank == 0 else P["local"][last]
+
     def close(self):
         self.local = None
         self.gathered = None
         self.frame_buf = None
+        self._pipe = None
