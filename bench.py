@@ -14,7 +14,14 @@ metric), max over ranks.  roofline: algorithmic gather bytes of the march
 kernel (32 B per executed ray-step) / its mean HIP-event
 duration.  cpu_baseline: the CPU oracle (oracle/, a port) on the same workload.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config grid512|grid128]
+The procedural configs (BASELINE configs 2-4: "cloud", "cloud_shadow",
+"cloud4k") march the build-defined Perlin-fBm x Worley medium instead of a
+grid.  They are ALU-bound, so their roofline is VALU: FLOP_PER_DENSITY
+algorithmic fp32 FLOP per density evaluation x the
+evaluations per launch (vr option "count" = 1) / mean kernel duration, against
+the 157.3 TFLOP/s fp32 vector peak.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config grid512|grid128|cloud|cloud_shadow|cloud4k]
 """
 from __future__ import annotations
 
@@ -35,16 +42,29 @@ import volumetricrenderer_amd as vr  # noqa: E402
 from volumetricrenderer_amd import distributed as vrdist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: fp32 vector peak
 BYTES_PER_STEP = 32        # 4 trilinear taps x 8 texels x 1 B
 
 CONFIGS = {
-    # name: (volume N, width, height, max_steps, BASELINE configs index)
-    "grid512": (512, 1920, 1080, 128, 4),
-    "grid128": (128, 1920, 1080, 128, None),
+    # name: (volume N or None = procedural, width, height, max_steps, shadow steps, BASELINE configs index)
+    "grid512": (512, 1920, 1080, 128, 0, 4),
+    "grid128": (128, 1920, 1080, 128, 0, None),
+    "cloud": (None, 1920, 1080, 128, 0, 1),
+    "cloud_shadow": (None, 1920, 1080, 128, 8, 2),
+    "cloud4k": (None, 3840, 2160, 256, 0, 3),
 }
 
 
-def cpu_baseline(volume_host: np.ndarray, osd, gsd, march, width, height, budget_s=10.0):
+def flop_per_density(octaves: int) -> int:
+    """Algorithmic fp32 FLOP of one procedural density evaluation (FMA = 2;
+    add, sub, mul, min, max, floor, rint, sqrt, div = 1; integer hashing and
+    int<->float conversions not counted).  Per Perlin octave 67 (noise 60 +
+    3 coordinate scales + fbm FMA + 2 parameter updates), Worley F1 over 27
+    cells 676, the rest 11."""
+    return 67 * octaves + 676 + 11
+
+
+def cpu_baseline(volume_host, osd, gsd, march, width, height, budget_s=10.0, procedural=None):
     """Time the oracle on the same frame (all cores it is allowed), ~budget_s."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import vr_oracle as oracle
@@ -60,8 +80,13 @@ def cpu_baseline(volume_host: np.ndarray, osd, gsd, march, width, height, budget
     steps = 0
     reps = 0
     while True:
-        _, s = oracle.render(volume_host, obj, glob, m, width, height, oracle.FMT_RGBA8_UNORM,
-                             band_rows=16, band_stride=8, band_first=reps % 8, threads=threads)
+        if procedural is not None:
+            _, s = oracle.render_procedural(oracle.procedural_from(procedural), obj, glob, m, width, height,
+                                            oracle.FMT_RGBA8_UNORM, band_rows=16, band_stride=8,
+                                            band_first=reps % 8, threads=threads)
+        else:
+            _, s = oracle.render(volume_host, obj, glob, m, width, height, oracle.FMT_RGBA8_UNORM,
+                                 band_rows=16, band_stride=8, band_first=reps % 8, threads=threads)
         rows += vr.band_rows_packed(height, 16, 8, reps % 8)
         steps += s
         reps += 1
@@ -71,7 +96,8 @@ def cpu_baseline(volume_host: np.ndarray, osd, gsd, march, width, height, budget
     mray = rows * width * march.max_steps / el / 1e6
     return {"value": round(mray, 3), "unit": "Mray/s", "cores": threads, "kind": "port",
             "sample": f"{reps} band sets of every 8th 16-row band ({rows} rows of {height}) of the same "
-                      f"{width}x{height}x{march.max_steps} frame and volume, {el:.1f} s; "
+                      f"{width}x{height}x{march.max_steps} frame and {'medium' if procedural else 'volume'}, "
+                      f"{el:.1f} s; "
                       f"executed steps/s {steps / el:.4g}"}
 
 
@@ -100,10 +126,15 @@ def main() -> int:
             dist.init_process_group("gloo")
     else:
         torch.cuda.set_device(0)
-    N, W, H, S, cfg_idx = CONFIGS[args.config]
+    N, W, H, S, shadow, cfg_idx = CONFIGS[args.config]
 
     r = vr.Renderer(dev)
-    r.generate_volume(vr.scaled_recipe(N))
+    proc = None
+    if N is None:
+        r.set_procedural(shadow_steps=shadow)
+        proc = r.procedural
+    else:
+        r.generate_volume(vr.scaled_recipe(N))
     osd, gsd = vr.reference_shader_data(1280.0 / 720.0)
     r.set_shader_data(osd, gsd)
     march = vr.march_defaults(max_steps=S)
@@ -117,6 +148,14 @@ def main() -> int:
     sharder.render_local(step_counter=counter)
     torch.cuda.synchronize()
     local_steps = int(counter.item())
+    local_evals = local_steps
+    if proc is not None:
+        r.set_option("count", 1)
+        counter.zero_()
+        sharder.render_local(step_counter=counter)
+        torch.cuda.synchronize()
+        local_evals = int(counter.item())
+        r.set_option("count", 0)
     red_dev = "cuda" if args.backend == "nccl" else "cpu"
     tot = torch.tensor([local_steps], dtype=torch.int64, device=red_dev)
     if world > 1:
@@ -143,7 +182,20 @@ def main() -> int:
     if rank == 0:
         ms_per_step = el / args.steps * 1e3
         value = W * H * S * args.steps / el / 1e6
-        achieved = local_steps * BYTES_PER_STEP / (kern_ms * 1e-3) / 1e9
+        if proc is None:
+            achieved = local_steps * BYTES_PER_STEP / (kern_ms * 1e-3) / 1e9
+            roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                        "achieved_def": "32 B algorithmic gather per executed ray-step x steps per launch "
+                                        "/ mean march-kernel duration (HIP events on its stream)"}
+        else:
+            fpd = flop_per_density(proc.octaves)
+            achieved = local_evals * fpd / (kern_ms * 1e-3) / 1e12
+            roofline = {"bound": "valu", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS,
+                        "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None,
+                        "achieved_def": f"{fpd} algorithmic fp32 FLOP per density evaluation x "
+                                        f"{local_evals} evaluations per launch / mean march-kernel duration "
+                                        "(HIP events on its stream); no volume is read"}
         traffic = None
         tfile = os.path.join(ROOT, "profiles", "traffic.json")
         if os.path.exists(tfile):
@@ -163,23 +215,24 @@ def main() -> int:
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic: reference noise recipe volume generated on the GPU (FastNoise2-style restatement)",
-            "config": {"workload": f"{args.config}: {N}^3 RGBA8 grid, {W}x{H}, {S} steps, RGBA8 out",
+            "data": ("synthetic: reference noise recipe volume generated on the GPU (FastNoise2-style restatement)"
+                     if proc is None else "synthetic: procedural Perlin-fBm x Worley medium evaluated per step"),
+            "config": {"workload": (f"{args.config}: {N}^3 RGBA8 grid, {W}x{H}, {S} steps, RGBA8 out" if proc is None
+                                    else f"{args.config}: procedural {proc.octaves}-octave Perlin-Worley cloud, "
+                                         f"{W}x{H}, {S} steps, shadow {shadow} steps, RGBA8 out"),
                        "baseline_config_index": cfg_idx, "width": W, "height": H, "max_steps": S,
-                       "volume": f"{N}^3 RGBA8", "camera": "reference (TestMain.cpp:219-245)",
+                       "volume": f"{N}^3 RGBA8" if N else "procedural", "camera": "reference (TestMain.cpp:219-245)",
                        "kernel": r.kernel_variant, "parallelism": f"bands16x{world}",
                        "collective": f"gather to rank 0 ({args.backend})" if world > 1 else None,
                        "executed_steps_per_frame": frame_steps},
             "executed_steps_per_s": round(frame_steps * args.steps / el, 1),
             "kernel_ms_mean": round(kern_ms, 5),
             "kernel_ms_mean_max_rank": round(kern_ms_max, 5),
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "achieved_def": "32 B algorithmic gather per executed ray-step x steps per launch "
-                                         "/ mean march-kernel duration (HIP events on its stream)"},
+            "roofline": dict(roofline, traffic=traffic),
         }
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline(r.get_volume(), osd, gsd, march, W, H, args.cpu_budget)
+            out["cpu_baseline"] = cpu_baseline(None if proc is not None else r.get_volume(), osd, gsd, march, W, H,
+                                               args.cpu_budget, procedural=proc)
         print(json.dumps(out), flush=True)
     sharder.close()
     r.close()

@@ -92,6 +92,32 @@ typedef struct {
                                    f=.03 grid is written into noiseOutput1   */
 } vr_volume_recipe;
 
+/* Procedural medium: BASELINE configs 2/3, build-defined extensions with no
+ * reference counterpart.  When enabled, vr_render
+ * marches a density evaluated in-kernel instead of the volume:
+ *   q = P * grid_scale              (P: box point in [0,1]^3)
+ *   fbm = sum_o gain^o * perlin(seed_fbm, q * freq0 * lacunarity^o)
+ *   F1  = cellular(seed_worley, q * worley_freq) + 1
+ *   rho = max(fbm * (1 - F1), 0) * march.scale
+ * With shadow_steps = 0, the output is Beer-Lambert 1 - exp(-density*sum(rho)*ds).
+ * With shadow_steps > 0, each step adds single scatter lit from sun_dir
+ * (box-local): Tview * rho*ds*density * exp(-density*ds*sum rho_sun), with
+ * shadow_steps sun samples at P + k*ds*sun_dir, inside the box only.       */
+typedef struct {
+    int32_t enabled;
+    float   grid_scale;     /* 128 */
+    int32_t octaves;        /* 4 */
+    float   freq0;          /* 0.19 */
+    float   lacunarity;     /* 2 */
+    float   gain;           /* 0.5 */
+    int32_t seed_fbm;       /* 3 */
+    float   worley_freq;    /* 0.03 */
+    int32_t seed_worley;    /* 2 */
+    int32_t shadow_steps;   /* 0 (config 2) or 8 (config 3) */
+    float   sun_dir[3];     /* normalize(1,1,2); normalised by the library */
+    int32_t reserved;       /* must be 0 */
+} vr_procedural;
+
 /* A render target.  `pixels` is a DEVICE pointer that the caller owns.
  * With band_rows > 0 only bands b = band_first, band_first + band_stride, ...
  * are rendered.  Band b covers frame rows [b*band_rows, (b+1)*band_rows).
@@ -145,12 +171,18 @@ vr_status vr_reference_shader_data(float aspect, float phi_deg, float theta_deg,
                                    float frame_time, vr_object_shader_data* osd,
                                    vr_global_shader_data* gsd);
 
+/* ---- procedural medium (configs 2/3) ----------------------------------- */
+vr_status vr_procedural_defaults(vr_procedural* p);   /* enabled = 0 */
+vr_status vr_set_procedural(void* ctx, const vr_procedural* p);
+
 /* ---- march constants (frag.glsl:29-32, 42, 63-69) ---------------------- */
 vr_status vr_march_defaults(vr_march_params* m);
 vr_status vr_set_march(void* ctx, const vr_march_params* m);
 
 /* ---- the hot path: replaces EnqueueRenderPass("BasePass") + the draw of
  *      TestMain.cpp:194-217 + vert.glsl/frag.glsl (VulkanRenderer.h:84-87).
+ *      A procedural medium, when enabled, needs no volume.
+
  *      stream = hipStream_t (NULL = default stream).                       */
 vr_status vr_render(void* ctx, const vr_target* target, void* stream);
 
@@ -180,7 +212,10 @@ vr_status vr_set_layout_preference(void* ctx, int pref);
  * tile rows dealt to XCDs; 1 = persistent waves pulling 8x8 tiles from
  * per-XCD queues; 2 = each wave renders "tiles_per_wave" strided 8x8
  * tiles); "waves_per_simd" (1-8, queue schedule); "tiles_per_wave" (1-64,
- * strided schedule).  vr_get_option returns -1 for an unknown name.        */
+ * strided schedule); "count" (0 = vr_target.step_counter sums executed
+ * ray-steps, the default; 1 = it sums density evaluations, i.e. ray-steps
+ * plus the procedural shadow samples -- the unit of the procedural
+ * roofline).  vr_get_option returns -1 for an unknown name.               */
 vr_status vr_set_option(void* ctx, const char* name, int value);
 int       vr_get_option(void* ctx, const char* name);
 

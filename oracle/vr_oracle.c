@@ -624,3 +624,100 @@ int vro_render(const uint8_t* vol, int nx, int ny, int nz,
     if (steps_out) *steps_out = total;
     return 0;
 }
+
+/* ======================================================================
+ * Procedural medium (BASELINE configs 2/3): build-defined, no reference
+ * counterpart.  Same ray setup and march as the
+ * grid path; the density comes from the noise functions above.
+ * ==================================================================== */
+float vro_procedural_density(const vro_procedural* p, float scale, float px, float py, float pz)
+{
+    const float qx = px * p->grid_scale, qy = py * p->grid_scale, qz = pz * p->grid_scale;
+    float f = p->freq0, amp = 1.0f, fbm = 0.0f;
+    for (int o = 0; o < p->octaves; ++o) {
+        fbm = fmaf(amp, vro_perlin3(p->seed_fbm, qx * f, qy * f, qz * f), fbm);
+        f = f * p->lacunarity;
+        amp = amp * p->gain;
+    }
+    const float wf = p->worley_freq;
+    const float f1 = vro_cellular3(p->seed_worley, qx * wf, qy * wf, qz * wf) + 1.0f;
+    return fmaxf(fbm * (1.0f - f1), 0.0f) * scale;
+}
+
+static inline int inside01(const float q[3])
+{
+    return q[0] >= 0.0f && q[0] <= 1.0f && q[1] >= 0.0f && q[1] <= 1.0f && q[2] >= 0.0f && q[2] <= 1.0f;
+}
+
+int vro_render_procedural(const vro_procedural* p, const float* obj48, const float* glob36, const vro_march* m,
+                          int width, int height, int format, void* out, size_t pitch,
+                          int band_rows, int band_stride, int band_first, int64_t* steps_out,
+                          int64_t* evals_out, int threads)
+{
+    ray_basis b;
+    march_consts k;
+    if (m->max_steps <= 0 || width <= 0 || height <= 0) return 2;
+    if (make_basis(obj48, glob36, width, height, &b)) return 1;
+    make_consts(m, glob36, 1, 1, 1, &k);
+    float lstep[3];
+    for (int a = 0; a < 3; ++a) lstep[a] = (k.step_size * p->sun_dir[a]) / k.box_range[a];
+    const float od = k.step_size * m->density;   /* optical depth per unit density */
+    if (band_rows <= 0) { band_rows = height; band_stride = 1; band_first = 0; }
+    if (band_stride <= 0) band_stride = 1;
+    const int nbands = (height + band_rows - 1) / band_rows;
+    int nsel = 0;
+    for (int bb = band_first; bb < nbands; bb += band_stride) nsel++;
+    const int out_rows = nsel * band_rows;
+    int64_t total = 0, shadow_total = 0;
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#else
+    (void)threads;
+#endif
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : total, shadow_total)
+    for (int orow = 0; orow < out_rows; ++orow) {
+        const int sel = orow / band_rows, r = orow % band_rows;
+        const int y = (band_first + sel * band_stride) * band_rows + r;
+        if (y >= height) continue;
+        for (int x = 0; x < width; ++x) {
+            float P[3], st[3];
+            int n = ray_setup(&b, m, &k, x, y, P, st);
+            if (n < 0) { store_px(out, pitch, orow, x, format, 0.0f, 0); continue; }
+            float acc = 0.0f, rad = 0.0f, tv = 1.0f;
+            int64_t shadow = 0;
+            int i = 0;
+            for (; i < n; ++i) {
+                const float rho = vro_procedural_density(p, m->scale, P[0], P[1], P[2]);
+                if (p->shadow_steps > 0 && rho > 0.0f) {
+                    float q[3] = {P[0], P[1], P[2]}, sl = 0.0f;
+                    for (int j = 0; j < p->shadow_steps; ++j) {
+                        q[0] = q[0] + lstep[0]; q[1] = q[1] + lstep[1]; q[2] = q[2] + lstep[2];
+                        if (inside01(q)) {
+                            sl = sl + vro_procedural_density(p, m->scale, q[0], q[1], q[2]);
+                            ++shadow;
+                        }
+                    }
+                    const float tl = vro_expf(-(sl * od));
+                    rad = fmaf((tv * (rho * od)), tl, rad);
+                }
+                acc = acc + rho;
+                if (p->shadow_steps > 0) tv = vro_expf(-(acc * od));
+                P[0] = P[0] + st[0]; P[1] = P[1] + st[1]; P[2] = P[2] + st[2];
+                if (acc > k.acc_limit) { ++i; break; }
+            }
+            total += i;
+            if (n > 0) shadow_total += shadow;
+            float g;
+            if (p->shadow_steps > 0) {
+                g = rad;
+            } else {
+                const float a = acc * k.step_size;
+                g = 1.0f - vro_expf(m->density * fminf(-a, 0.0f));
+            }
+            store_px(out, pitch, orow, x, format, g, 1);
+        }
+    }
+    if (steps_out) *steps_out = total;
+    if (evals_out) *evals_out = total + shadow_total;
+    return 0;
+}

@@ -94,6 +94,37 @@ int vro_render(const uint8_t* rgba, int nx, int ny, int nz,
                int band_rows, int band_stride, int band_first,
                int64_t* steps_out, int threads);
 
+/* ---- procedural medium (BASELINE configs 2/3; build-defined, SURVEY.md
+ * sec. 8d: no reference counterpart).  Density at box point P in [0,1]^3:
+ *   q = P * grid_scale
+ *   fbm = sum_o gain^o * perlin(seed_fbm, q * freq0 * lacunarity^o)
+ *   F1  = cellular(seed_worley, q * worley_freq) + 1
+ *   rho = max(fbm * (1 - F1), 0) * march.scale
+ * shadow_steps = 0: Beer-Lambert of frag.glsl:76-80 on sum(rho).
+ * shadow_steps > 0: single scatter toward sun_dir (box-local, normalised),
+ *   L += Tview * (rho*ds*density) * Tsun, Tsun = exp(-density*ds*sum rho_sun)
+ *   over shadow_steps samples at P + k*ds*sun (inside the box only).       */
+typedef struct {
+    int32_t enabled;
+    float   grid_scale;     /* 128: the reference's texel-grid frequency units */
+    int32_t octaves;        /* 4 */
+    float   freq0;          /* 0.19 (TestMain.cpp:61 Perlin frequency) */
+    float   lacunarity;     /* 2 */
+    float   gain;           /* 0.5 */
+    int32_t seed_fbm;       /* 3 */
+    float   worley_freq;    /* 0.03 (TestMain.cpp:60) */
+    int32_t seed_worley;    /* 2 */
+    int32_t shadow_steps;   /* 0 (config 2) or 8 (config 3) */
+    float   sun_dir[3];     /* normalize(1,1,2) */
+    int32_t reserved;
+} vro_procedural;
+float vro_procedural_density(const vro_procedural* p, float scale, float px, float py, float pz);
+int vro_render_procedural(const vro_procedural* p, const float* obj48, const float* glob36, const vro_march* m,
+                          int width, int height, int format, void* out, size_t pitch,
+                          int band_rows, int band_stride, int band_first, int64_t* steps_out,
+                          int64_t* evals_out, int threads);
+/* evals_out (nullable): density evaluations = executed steps + shadow samples. */
+
 /* Per-pixel step count n (frag.glsl:46) and coverage, for KAT tests.
  * n_out[y*width+x] = -1 for uncovered pixels.                              */
 int vro_step_counts(const float* obj48, const float* glob36, const vro_march* m,

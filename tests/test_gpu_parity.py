@@ -293,3 +293,89 @@ def test_config1_matches_golden_fixture(r):
     r.set_march(vr.march_defaults(max_steps=32))
     img = r.render(256, 256, vr.FMT_RGBA32F).cpu().numpy()
     assert np.array_equal(img[..., 0], ref)
+
+
+# ---- procedural medium (BASELINE configs 2/3; build-defined) ----
+
+def render_proc_both(r, oracle, W, H, march, fmt=0, osd=None, gsd=None, **proc):
+    if osd is None:
+        osd, gsd = vr.reference_shader_data(W / H, 20.0, 15.0)
+    r.set_shader_data(osd, gsd)
+    r.set_march(march)
+    r.set_procedural(**proc)
+    try:
+        cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+        img = r.render(W, H, fmt, step_counter=cnt)
+        torch.cuda.synchronize()
+        variant = r.kernel_variant
+    finally:
+        r.set_procedural(enabled=0)
+    obj, glob = vr.shader_data_arrays(osd, gsd)
+    ref, steps = oracle.render_procedural(oracle.procedural_from(r.procedural), obj, glob,
+                                          oracle.from_params(march), W, H, fmt)
+    return img.cpu().numpy(), ref, int(cnt.item()), steps, variant
+
+
+def test_procedural_config2_cloud(r, oracle):
+    img, ref, c, s, var = render_proc_both(r, oracle, 192, 108, vr.march_defaults(max_steps=128))
+    assert var == "procedural"
+    assert_exact(img, ref)
+    assert c == s > 0
+    assert img[..., 0].max() > 0.05   # the cloud is not empty
+
+
+def test_procedural_config3_shadow(r, oracle):
+    img, ref, c, s, var = render_proc_both(r, oracle, 128, 72, vr.march_defaults(max_steps=128), shadow_steps=8)
+    assert var == "procedural_shadow"
+    assert_exact(img, ref)
+    assert c == s > 0
+    assert img[..., 0].max() > 0.0
+
+
+@pytest.mark.parametrize("kw", [dict(octaves=1, seed_fbm=11), dict(octaves=6, gain=0.6, worley_freq=0.05),
+                                dict(shadow_steps=3, sun_dir=(0.0, 1.0, 0.0))])
+def test_procedural_parameters(r, oracle, kw):
+    img, ref, c, s, _ = render_proc_both(r, oracle, 96, 64, vr.march_defaults(max_steps=48, density=3.0), **kw)
+    assert_exact(img, ref)
+    assert c == s
+
+
+def test_procedural_early_out_and_rgba8(r, oracle):
+    m = vr.march_defaults(max_steps=96, density=400.0, early_out=0.01)
+    img, ref, c, s, _ = render_proc_both(r, oracle, 96, 64, m, fmt=vr.FMT_RGBA8_UNORM)
+    assert_exact(img, ref)
+    assert c == s
+    full = vr.march_defaults(max_steps=96, density=400.0)
+    _, _, c2, _, _ = render_proc_both(r, oracle, 96, 64, full, fmt=vr.FMT_RGBA8_UNORM)
+    assert c < c2   # the early-out really skipped steps
+
+
+def test_procedural_rejects_bad_parameters(r):
+    with pytest.raises(VRError):
+        r.set_procedural(octaves=17)
+    with pytest.raises(VRError):
+        r.set_procedural(shadow_steps=8, sun_dir=(0.0, 0.0, 0.0))
+    r.set_procedural(enabled=0)
+
+
+def test_procedural_density_evaluation_count(r, oracle):
+    """count=1: the step counter sums density evaluations (ray-steps + shadow
+    samples), the unit of bench.py's procedural roofline."""
+    W, H = 96, 64
+    m = vr.march_defaults(max_steps=64)
+    osd, gsd = vr.reference_shader_data(W / H, 20.0, 15.0)
+    r.set_shader_data(osd, gsd)
+    r.set_march(m)
+    r.set_procedural(shadow_steps=8)
+    r.set_option("count", 1)
+    try:
+        cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+        r.render(W, H, 0, step_counter=cnt)
+        torch.cuda.synchronize()
+    finally:
+        r.set_option("count", 0)
+        r.set_procedural(enabled=0)
+    obj, glob = vr.shader_data_arrays(osd, gsd)
+    _, steps, evals = oracle.render_procedural(oracle.procedural_from(r.procedural), obj, glob,
+                                               oracle.from_params(m), W, H, 0, with_evals=True)
+    assert int(cnt.item()) == evals > steps

@@ -7,11 +7,12 @@ interface (renderer) and the multi-GPU band sharding (distributed).
 """
 from ._lib import (FMT_RGBA8_SRGB, FMT_RGBA8_UNORM, FMT_RGBA32F, GlobalShaderData, MarchParams,  # noqa: F401
                    ObjectShaderData, Target, VolumeRecipe, VRError)
-from .renderer import (Renderer, band_rows_packed, march_defaults, reference_shader_data,  # noqa: F401
-                       scaled_recipe, shader_data_arrays, volume_recipe_defaults)
+from ._lib import Procedural  # noqa: F401
+from .renderer import (Renderer, band_rows_packed, march_defaults, procedural_defaults,  # noqa: F401
+                       reference_shader_data, scaled_recipe, shader_data_arrays, volume_recipe_defaults)
 
 __all__ = [
-    "Renderer", "VRError", "march_defaults", "reference_shader_data", "volume_recipe_defaults",
+    "Renderer", "VRError", "march_defaults", "procedural_defaults", "Procedural", "reference_shader_data", "volume_recipe_defaults",
     "scaled_recipe", "band_rows_packed", "shader_data_arrays", "FMT_RGBA32F", "FMT_RGBA8_UNORM",
     "FMT_RGBA8_SRGB", "ObjectShaderData", "GlobalShaderData", "MarchParams", "VolumeRecipe", "Target",
 ]

@@ -70,6 +70,14 @@ class VolumeRecipe(ctypes.Structure):
                 ("seed", ctypes.c_int32 * 4), ("literal_overwrite", ctypes.c_int32)]
 
 
+class Procedural(ctypes.Structure):
+    """vr_procedural: BASELINE configs 2/3 (build-defined procedural medium)."""
+    _fields_ = [("enabled", ctypes.c_int32), ("grid_scale", ctypes.c_float), ("octaves", ctypes.c_int32),
+                ("freq0", ctypes.c_float), ("lacunarity", ctypes.c_float), ("gain", ctypes.c_float),
+                ("seed_fbm", ctypes.c_int32), ("worley_freq", ctypes.c_float), ("seed_worley", ctypes.c_int32),
+                ("shadow_steps", ctypes.c_int32), ("sun_dir", ctypes.c_float * 3), ("reserved", ctypes.c_int32)]
+
+
 class Target(ctypes.Structure):
     """vr_target: device render target + band selection."""
     _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32), ("format", ctypes.c_int32),
@@ -99,6 +107,8 @@ _SIGS = {
                                                 ctypes.c_float, ctypes.POINTER(ObjectShaderData),
                                                 ctypes.POINTER(GlobalShaderData)]),
     "vr_march_defaults": (ctypes.c_int, [ctypes.POINTER(MarchParams)]),
+    "vr_procedural_defaults": (ctypes.c_int, [ctypes.POINTER(Procedural)]),
+    "vr_set_procedural": (ctypes.c_int, [_vp, ctypes.POINTER(Procedural)]),
     "vr_set_march": (ctypes.c_int, [_vp, ctypes.POINTER(MarchParams)]),
     "vr_render": (ctypes.c_int, [_vp, ctypes.POINTER(Target), _vp]),
     "vr_assemble_bands": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,

@@ -65,6 +65,8 @@ struct Ctx {
     int waves_per_simd = kDefaultWavesPerSimd;
     int tiles_per_wave = kDefaultTilesPerWave;
     int* d_heads = nullptr;        // 8 queue heads (+ padding), zeroed per launch
+    vr_procedural proc{};          // procedural medium (configs 2/3), off by default
+    int count = 0;                 // step_counter: 0 = executed ray-steps, 1 = density evaluations
 };
 
 // Auto layout (measured): CORNER8 does one load per tap but
@@ -248,6 +250,47 @@ vr_status vr_volume_recipe_defaults(vr_volume_recipe* r)
     const float f[4] = {0.01f, 0.03f, 0.19f, 0.15f};  // :59-62
     for (int k = 0; k < 4; ++k) { r->freq[k] = f[k]; r->seed[k] = k + 1; }
     r->literal_overwrite = 1;
+    return VR_OK;
+}
+
+vr_status vr_procedural_defaults(vr_procedural* p)
+{
+    if (!p) return fail(VR_ERR_INVALID, "vr_procedural_defaults: null");
+    std::memset(p, 0, sizeof *p);
+    p->enabled = 0;
+    p->grid_scale = 128.0f;     // TestMain.cpp:51 grid, frequencies in texel units
+    p->octaves = 4;
+    p->freq0 = 0.19f;           // TestMain.cpp:61
+    p->lacunarity = 2.0f;
+    p->gain = 0.5f;
+    p->seed_fbm = 3;
+    p->worley_freq = 0.03f;     // TestMain.cpp:60
+    p->seed_worley = 2;
+    p->shadow_steps = 0;
+    const double n = std::sqrt(1.0 + 1.0 + 4.0);
+    p->sun_dir[0] = (float)(1.0 / n); p->sun_dir[1] = (float)(1.0 / n); p->sun_dir[2] = (float)(2.0 / n);
+    return VR_OK;
+}
+
+vr_status vr_set_procedural(void* ctx, const vr_procedural* p)
+{
+    if (!ctx || !p) return fail(VR_ERR_INVALID, "vr_set_procedural: null argument");
+    if (p->enabled) {
+        if (p->octaves < 0 || p->octaves > 16) return fail(VR_ERR_INVALID, "vr_set_procedural: octaves in [0,16]");
+        if (p->shadow_steps < 0 || p->shadow_steps > 256)
+            return fail(VR_ERR_INVALID, "vr_set_procedural: shadow_steps in [0,256]");
+        const double l = std::sqrt((double)p->sun_dir[0] * p->sun_dir[0] + (double)p->sun_dir[1] * p->sun_dir[1] +
+                                   (double)p->sun_dir[2] * p->sun_dir[2]);
+        if (p->shadow_steps > 0 && !(l > 0.0)) return fail(VR_ERR_INVALID, "vr_set_procedural: zero sun_dir");
+        if (p->reserved) return fail(VR_ERR_INVALID, "vr_set_procedural: reserved must be 0");
+    }
+    Ctx* c = as_ctx(ctx);
+    c->proc = *p;
+    if (p->enabled && p->shadow_steps > 0) {   // normalise in double, round once
+        const double l = std::sqrt((double)p->sun_dir[0] * p->sun_dir[0] + (double)p->sun_dir[1] * p->sun_dir[1] +
+                                   (double)p->sun_dir[2] * p->sun_dir[2]);
+        for (int a = 0; a < 3; ++a) c->proc.sun_dir[a] = (float)((double)p->sun_dir[a] / l);
+    }
     return VR_OK;
 }
 
@@ -502,6 +545,11 @@ vr_status vr_set_option(void* p, const char* name, int value)
         c->tiles_per_wave = value;
         return VR_OK;
     }
+    if (n == "count") {
+        if (value < 0 || value > 1) return fail(VR_ERR_INVALID, "vr_set_option: count is 0 (steps) or 1 (evals)");
+        c->count = value;
+        return VR_OK;
+    }
     return fail(VR_ERR_INVALID, "vr_set_option: unknown option '%s'", name);
 }
 
@@ -514,6 +562,7 @@ int vr_get_option(void* p, const char* name)
     if (n == "schedule") return c->schedule;
     if (n == "waves_per_simd") return c->waves_per_simd;
     if (n == "tiles_per_wave") return c->tiles_per_wave;
+    if (n == "count") return c->count;
     return -1;
 }
 
@@ -521,6 +570,7 @@ const char* vr_kernel_variant(void* p)
 {
     if (!p) return "none";
     Ctx* c = as_ctx(p);
+    if (c->proc.enabled) return c->proc.shadow_steps > 0 ? "procedural_shadow" : "procedural";
     if (!c->d_planar || !c->has_camera) return "none";
     MarchArgs a{};
     Plan pl{};
@@ -532,7 +582,8 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
 {
     if (!p || !t) return fail(VR_ERR_INVALID, "vr_render: null argument");
     Ctx* c = as_ctx(p);
-    if (!c->d_planar) return fail(VR_ERR_NO_VOLUME, "vr_render: no volume (vr_set_volume / vr_generate_volume)");
+    if (!c->d_planar && !c->proc.enabled)
+        return fail(VR_ERR_NO_VOLUME, "vr_render: no volume (vr_set_volume / vr_generate_volume)");
     if (!c->has_camera) return fail(VR_ERR_NO_CAMERA, "vr_render: no shader data (vr_set_shader_data)");
     if (t->width <= 0 || t->height <= 0) return fail(VR_ERR_INVALID, "vr_render: bad size %dx%d", t->width, t->height);
     if (t->format < 0 || t->format > 2) return fail(VR_ERR_INVALID, "vr_render: bad format %d", t->format);
@@ -564,8 +615,18 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
     a.acc_limit = m.early_out > 0.0f
                       ? (float)(-std::log((double)m.early_out) / ((double)m.density * (double)a.step_size))
                       : INFINITY;
-    Plan pl{};
-    make_plan(c, &a, &pl);
+    if (c->proc.enabled) {
+        ProcParams& q = a.proc;
+        q.grid_scale = c->proc.grid_scale; q.octaves = c->proc.octaves; q.freq0 = c->proc.freq0;
+        q.lacunarity = c->proc.lacunarity; q.gain = c->proc.gain; q.seed_fbm = c->proc.seed_fbm;
+        q.worley_freq = c->proc.worley_freq; q.seed_worley = c->proc.seed_worley;
+        q.shadow_steps = c->proc.shadow_steps;
+        for (int ax = 0; ax < 3; ++ax) q.lstep[ax] = (a.step_size * c->proc.sun_dir[ax]) / a.box_range[ax];
+        q.od = a.step_size * m.density;
+        q.count_evals = c->count;
+    }
+    Plan pl{LAYOUT_PLANAR, WRAP_CLAMP, false};
+    if (!c->proc.enabled) make_plan(c, &a, &pl);
     a.nx = c->nx; a.ny = c->ny; a.nz = c->nz;
     if (pl.layout != LAYOUT_PLANAR) {
         a.vol = c->d_fast;
@@ -591,6 +652,10 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
     a.format = t->format;
     a.step_counter = reinterpret_cast<unsigned long long*>(t->step_counter);
     HIP_TRY(hipSetDevice(c->device));
+    if (c->proc.enabled) {
+        HIP_TRY(launch_march_procedural(a, m.early_out > 0.0f, static_cast<hipStream_t>(stream)));
+        return VR_OK;
+    }
     // auto schedule (measured): static XCD-row tiles for the cache-resident
     // CORNER8 volume, strided single tiles otherwise
     const int kind = c->schedule >= 0 ? c->schedule : (pl.layout == LAYOUT_CORNER8 ? SCHED_STATIC : SCHED_STRIDED);

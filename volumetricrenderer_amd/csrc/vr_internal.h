@@ -68,6 +68,20 @@ __host__ __device__ inline unsigned axis_offset(const LayoutGeom& g, int layout,
     return q * stride + r * (axis == 0 ? 1u : axis == 1 ? (unsigned)g.R : (unsigned)(g.R * g.R));
 }
 
+// Procedural medium parameters (vr_procedural; BASELINE configs 2/3).
+struct ProcParams {
+    float grid_scale;
+    int octaves;
+    float freq0, lacunarity, gain;
+    int seed_fbm;
+    float worley_freq;
+    int seed_worley;
+    int shadow_steps;
+    float lstep[3];   // (step_size * sun_dir) / box_range
+    float od;         // step_size * density
+    int count_evals;  // step_counter counts density evaluations (incl. shadow samples)
+};
+
 // Everything one launch of the march kernel needs.  Passed by value
 // (kernarg segment), computed on the host per vr_render call.
 struct MarchArgs {
@@ -92,6 +106,7 @@ struct MarchArgs {
     long long pitch;
     int format;
     unsigned long long* step_counter;
+    ProcParams proc;
 };
 
 // How the march kernel maps tiles to waves.
@@ -105,6 +120,7 @@ struct Schedule {
 
 // launchers (vr_march.hip / vr_volume.hip); return hipError_t
 hipError_t launch_march(const MarchArgs& a, int layout, int wrap, bool early, const Schedule& sc, hipStream_t s);
+hipError_t launch_march_procedural(const MarchArgs& a, bool early, hipStream_t s);
 hipError_t launch_repack(const uint8_t* d_rgba, int nx, int ny, int nz, uint8_t* d_planar, hipStream_t s);
 // Build a fast layout from the planar planes.
 hipError_t launch_build_layout(int layout, const uint8_t* d_planar, int nx, int ny, int nz, uint8_t* d_out,

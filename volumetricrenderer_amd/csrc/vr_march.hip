@@ -11,6 +11,7 @@
 // lerps per instruction.  Built with -ffp-contract=off: the only fused ops
 // are the explicit fma calls.
 #include "vr_internal.h"
+#include "vr_noise.h"
 
 namespace vr {
 namespace {
@@ -168,97 +169,167 @@ __device__ __forceinline__ float tap(const MarchArgs& a, const FastCtx& f, int t
         return tap_fast<LAYOUT>(f, t, gxy.x, gxy.y, gz);
 }
 
-// One ray: ray setup (frag.glsl:36-55), the march (:57-75), the epilogue
-// (:76-80) and the store.  Returns the executed steps (0 if uncovered).
-template <int LAYOUT, int WRAP, bool EARLY>
-__device__ __forceinline__ unsigned march_pixel(const MarchArgs& a, const FastCtx& f, int x, int orow)
+// Per-ray state after ray setup (frag.glsl:36-55).
+struct Ray {
+    bool live;     // pixel exists (inside the target and the frame)
+    int n;         // steps (frag.glsl:46); -1 = not covered
+    f2 pxy;        // box-normalised ray point (frag.glsl:49-54)
+    float pz;
+    f2 sxy;        // step vector (frag.glsl:45, 54)
+    float sz;
+};
+
+__device__ __forceinline__ Ray setup_ray(const MarchArgs& a, int x, int orow)
 {
+    Ray r{};
+    r.n = -1;
     const bool inside = x < a.width && orow < a.out_rows;
     int y = 0;
     if (inside) {
         const int bl = orow / a.band_rows;
         y = (a.band_first + bl * a.band_stride) * a.band_rows + (orow - bl * a.band_rows);
     }
-    const bool live = inside && y < a.height;
+    r.live = inside && y < a.height;
+    if (!r.live) return r;
+    const float fx = (float)x + 0.5f, fy = (float)y + 0.5f;
+    const float v0 = fmaf(fy, a.py[0], fmaf(fx, a.px[0], a.o[0]));
+    const float v1 = fmaf(fy, a.py[1], fmaf(fx, a.px[1], a.o[1]));
+    const float v2 = fmaf(fy, a.py[2], fmaf(fx, a.px[2], a.o[2]));
+    const float len = sqrtf(fmaf(v2, v2, fmaf(v1, v1, v0 * v0)));
+    const float d0 = v0 / len, d1 = v1 / len, d2 = v2 / len;
+    // IntersectAABB, frag.glsl:18-27
+    const float ta0 = (a.box_min[0] - a.org[0]) / d0, tb0 = (a.box_max[0] - a.org[0]) / d0;
+    const float ta1 = (a.box_min[1] - a.org[1]) / d1, tb1 = (a.box_max[1] - a.org[1]) / d1;
+    const float ta2 = (a.box_min[2] - a.org[2]) / d2, tb2 = (a.box_max[2] - a.org[2]) / d2;
+    const float tn = fmaxf(fmaxf(fminf(ta0, tb0), fminf(ta1, tb1)), fminf(ta2, tb2));
+    const float tf = fminf(fminf(fmaxf(ta0, tb0), fmaxf(ta1, tb1)), fmaxf(ta2, tb2));
+    if (!(tn <= tf)) return r;
+    const float pi0 = fmaf(d0, tn, a.org[0]), pi1 = fmaf(d1, tn, a.org[1]), pi2 = fmaf(d2, tn, a.org[2]);
+    // coverage: the front-face fragment survives clipping (0 <= z <= w)
+    const float zc = fmaf(a.r2[2], pi2, fmaf(a.r2[1], pi1, fmaf(a.r2[0], pi0, a.r2[3])));
+    const float wc = fmaf(a.r3[2], pi2, fmaf(a.r3[1], pi1, fmaf(a.r3[0], pi0, a.r3[3])));
+    if (!(wc > 0.0f && zc >= 0.0f && zc <= wc)) return r;
+    const float po0 = fmaf(d0, tf, a.org[0]), po1 = fmaf(d1, tf, a.org[1]), po2 = fmaf(d2, tf, a.org[2]);
+    const float e0 = po0 - pi0, e1 = po1 - pi1, e2 = po2 - pi2;
+    const float dist = sqrtf(fmaf(e2, e2, fmaf(e1, e1, e0 * e0)));
+    const float q = dist / a.step_size;                                   // :46
+    r.n = q >= (float)a.max_steps ? a.max_steps : (int)q;
+    r.pxy = f2{(pi0 - a.box_min[0]) / a.box_range[0], (pi1 - a.box_min[1]) / a.box_range[1]};   // :49-54
+    r.pz = (pi2 - a.box_min[2]) / a.box_range[2];
+    r.sxy = f2{(a.step_size * d0) / a.box_range[0], (a.step_size * d1) / a.box_range[1]};       // :45
+    r.sz = (a.step_size * d2) / a.box_range[2];
+    return r;
+}
 
-    // ---- ray setup: frag.glsl:36-55 ---------------------------------------
-    int n = -1;
-    float P0 = 0.f, P1 = 0.f, P2 = 0.f, s0 = 0.f, s1 = 0.f, s2 = 0.f;
-    if (live) {
-        const float fx = (float)x + 0.5f, fy = (float)y + 0.5f;
-        const float v0 = fmaf(fy, a.py[0], fmaf(fx, a.px[0], a.o[0]));
-        const float v1 = fmaf(fy, a.py[1], fmaf(fx, a.px[1], a.o[1]));
-        const float v2 = fmaf(fy, a.py[2], fmaf(fx, a.px[2], a.o[2]));
-        const float len = sqrtf(fmaf(v2, v2, fmaf(v1, v1, v0 * v0)));
-        const float d0 = v0 / len, d1 = v1 / len, d2 = v2 / len;
-        // IntersectAABB, frag.glsl:18-27
-        const float ta0 = (a.box_min[0] - a.org[0]) / d0, tb0 = (a.box_max[0] - a.org[0]) / d0;
-        const float ta1 = (a.box_min[1] - a.org[1]) / d1, tb1 = (a.box_max[1] - a.org[1]) / d1;
-        const float ta2 = (a.box_min[2] - a.org[2]) / d2, tb2 = (a.box_max[2] - a.org[2]) / d2;
-        const float tn = fmaxf(fmaxf(fminf(ta0, tb0), fminf(ta1, tb1)), fminf(ta2, tb2));
-        const float tf = fminf(fminf(fmaxf(ta0, tb0), fmaxf(ta1, tb1)), fmaxf(ta2, tb2));
-        if (tn <= tf) {
-            const float pi0 = fmaf(d0, tn, a.org[0]), pi1 = fmaf(d1, tn, a.org[1]), pi2 = fmaf(d2, tn, a.org[2]);
-            const float zc = fmaf(a.r2[2], pi2, fmaf(a.r2[1], pi1, fmaf(a.r2[0], pi0, a.r2[3])));
-            const float wc = fmaf(a.r3[2], pi2, fmaf(a.r3[1], pi1, fmaf(a.r3[0], pi0, a.r3[3])));
-            if (wc > 0.0f && zc >= 0.0f && zc <= wc) {
-                const float po0 = fmaf(d0, tf, a.org[0]), po1 = fmaf(d1, tf, a.org[1]), po2 = fmaf(d2, tf, a.org[2]);
-                const float e0 = po0 - pi0, e1 = po1 - pi1, e2 = po2 - pi2;
-                const float dist = sqrtf(fmaf(e2, e2, fmaf(e1, e1, e0 * e0)));
-                const float q = dist / a.step_size;                                   // :46
-                n = q >= (float)a.max_steps ? a.max_steps : (int)q;
-                P0 = (pi0 - a.box_min[0]) / a.box_range[0];                           // :49-54
-                P1 = (pi1 - a.box_min[1]) / a.box_range[1];
-                P2 = (pi2 - a.box_min[2]) / a.box_range[2];
-                s0 = (a.step_size * d0) / a.box_range[0];                             // :45
-                s1 = (a.step_size * d1) / a.box_range[1];
-                s2 = (a.step_size * d2) / a.box_range[2];
-            }
+// Render-target store: grey g (frag.glsl:80), uncovered pixels keep the
+// clear colour (0,0,0,1) (VulkanRenderPass.cpp:17-24).
+__device__ __forceinline__ void store_pixel(const MarchArgs& a, int x, int orow, bool covered, float g)
+{
+    char* row = (char*)a.out + (long long)orow * a.pitch;
+    if (a.format == 0) {
+        g = covered ? g : 0.0f;
+        reinterpret_cast<float4*>(row)[x] = make_float4(g, g, g, 1.0f);
+    } else {
+        unsigned int q = 0;
+        if (covered) {
+            float c = fminf(fmaxf(g, 0.0f), 1.0f);
+            if (a.format == 2)
+                c = c <= 0.0031308f ? c * 12.92f : fmaf(1.055f, powf(c, 1.0f / 2.4f), -0.055f);
+            q = (unsigned int)rintf(c * 255.0f);
         }
+        reinterpret_cast<unsigned int*>(row)[x] = q | (q << 8) | (q << 16) | 0xff000000u;
     }
+}
 
-    // ---- the hot loop: frag.glsl:57-75 ------------------------------------
-    f2 pxy{P0, P1};
-    const f2 sxy{s0, s1};
-    float pz = P2;
+// One ray of the grid path: setup, the march (frag.glsl:57-75), the
+// epilogue (:76-80) and the store.  Returns the executed steps.
+template <int LAYOUT, int WRAP, bool EARLY>
+__device__ __forceinline__ unsigned march_pixel(const MarchArgs& a, const FastCtx& f, int x, int orow)
+{
+    const Ray r = setup_ray(a, x, orow);
+    f2 pxy = r.pxy;
+    float pz = r.pz;
     float acc = 0.0f;
     int i = 0;
-    for (; i < n; ++i) {
+    for (; i < r.n; ++i) {
         const float t0 = tap<LAYOUT, WRAP>(a, f, 0, pxy, pz);
         const float t1 = tap<LAYOUT, WRAP>(a, f, 1, pxy, pz);
         const float t2 = tap<LAYOUT, WRAP>(a, f, 2, pxy, pz);
         const float t3 = tap<LAYOUT, WRAP>(a, f, 3, pxy, pz);
         acc = acc + ((t0 * t1) * (t2 + t3)) * a.scale;                               // :71-73
-        pxy = pxy + sxy;                                                              // :74
-        pz = pz + s2;
+        pxy = pxy + r.sxy;                                                            // :74
+        pz = pz + r.sz;
         if constexpr (EARLY) {
             if (acc > a.acc_limit) { ++i; break; }
         }
     }
+    if (r.live) {
+        const float at = acc * a.step_size;                                          // :76
+        store_pixel(a, x, orow, r.n >= 0, 1.0f - spec_expf(a.density * fminf(-at, 0.0f)));   // :79
+    }
+    return r.n > 0 ? (unsigned)i : 0u;
+}
 
-    // ---- epilogue: frag.glsl:76-80 + the render-target format --------------
-    if (live) {
-        float g = 0.0f;
-        if (n >= 0) {
-            const float at = acc * a.step_size;
-            const float e = spec_expf(a.density * fminf(-at, 0.0f));
-            g = 1.0f - e;
-        }
-        char* row = (char*)a.out + (long long)orow * a.pitch;
-        if (a.format == 0) {
-            reinterpret_cast<float4*>(row)[x] = make_float4(g, g, g, 1.0f);
-        } else {
-            unsigned int q = 0;
-            if (n >= 0) {
-                float c = fminf(fmaxf(g, 0.0f), 1.0f);
-                if (a.format == 2)
-                    c = c <= 0.0031308f ? c * 12.92f : fmaf(1.055f, powf(c, 1.0f / 2.4f), -0.055f);
-                q = (unsigned int)rintf(c * 255.0f);
+// Procedural medium (BASELINE configs 2/3, build-defined; spec in
+// oracle/vr_oracle.h vro_procedural): fBm Perlin x (1 - Worley F1).
+__device__ __forceinline__ float proc_density(const ProcParams& p, float scale, float px, float py, float pz)
+{
+    const float qx = px * p.grid_scale, qy = py * p.grid_scale, qz = pz * p.grid_scale;
+    float f = p.freq0, amp = 1.0f, fbm = 0.0f;
+    for (int o = 0; o < p.octaves; ++o) {
+        fbm = fmaf(amp, noise::perlin(p.seed_fbm, qx * f, qy * f, qz * f), fbm);
+        f = f * p.lacunarity;
+        amp = amp * p.gain;
+    }
+    const float wf = p.worley_freq;
+    const float f1 = noise::cellular(p.seed_worley, qx * wf, qy * wf, qz * wf) + 1.0f;
+    return fmaxf(fbm * (1.0f - f1), 0.0f) * scale;
+}
+
+template <bool SHADOW, bool EARLY>
+__device__ __forceinline__ unsigned march_pixel_proc(const MarchArgs& a, int x, int orow)
+{
+    const Ray r = setup_ray(a, x, orow);
+    const ProcParams& p = a.proc;
+    float P0 = r.pxy.x, P1 = r.pxy.y, P2 = r.pz;
+    float acc = 0.0f, rad = 0.0f, tv = 1.0f;
+    int i = 0;
+    unsigned evals = 0;   // shadow density evaluations
+    for (; i < r.n; ++i) {
+        const float rho = proc_density(p, a.scale, P0, P1, P2);
+        if constexpr (SHADOW) {
+            if (rho > 0.0f) {
+                float q0 = P0, q1 = P1, q2 = P2, sl = 0.0f;
+                for (int j = 0; j < p.shadow_steps; ++j) {
+                    q0 = q0 + p.lstep[0]; q1 = q1 + p.lstep[1]; q2 = q2 + p.lstep[2];
+                    if (q0 >= 0.0f && q0 <= 1.0f && q1 >= 0.0f && q1 <= 1.0f && q2 >= 0.0f && q2 <= 1.0f) {
+                        sl = sl + proc_density(p, a.scale, q0, q1, q2);
+                        ++evals;
+                    }
+                }
+                const float tl = spec_expf(-(sl * p.od));
+                rad = fmaf((tv * (rho * p.od)), tl, rad);
             }
-            reinterpret_cast<unsigned int*>(row)[x] = q | (q << 8) | (q << 16) | 0xff000000u;
+        }
+        acc = acc + rho;
+        if constexpr (SHADOW) tv = spec_expf(-(acc * p.od));
+        P0 = P0 + r.sxy.x; P1 = P1 + r.sxy.y; P2 = P2 + r.sz;
+        if constexpr (EARLY) {
+            if (acc > a.acc_limit) { ++i; break; }
         }
     }
-    return n > 0 ? (unsigned)i : 0u;
+    if (r.live) {
+        float g;
+        if constexpr (SHADOW) {
+            g = rad;
+        } else {
+            const float at = acc * a.step_size;
+            g = 1.0f - spec_expf(a.density * fminf(-at, 0.0f));
+        }
+        store_pixel(a, x, orow, r.n >= 0, g);
+    }
+    if (r.n <= 0) return 0u;
+    return p.count_evals ? (unsigned)i + evals : (unsigned)i;
 }
 
 // Lane -> pixel inside an 8x8 wave tile: row-major, so each 16-lane TA
@@ -390,6 +461,21 @@ __global__ __launch_bounds__(kThreads) void march_queue(const MarchArgs a, int* 
     if (a.step_counter) add_steps(a, steps);
 }
 
+// Procedural medium: one 8x8 tile per wave (compute-bound; no volume).
+template <bool SHADOW, bool EARLY>
+__global__ __launch_bounds__(kThreads) void march_proc(const MarchArgs a)
+{
+    const int lane = threadIdx.x & 63;
+    const int t = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+    const int tiles_x8 = (a.width + 7) >> 3, rows8 = (a.out_rows + 7) >> 3;
+    unsigned long long steps = 0;
+    if (t < tiles_x8 * rows8) {
+        const int ty = t / tiles_x8, tx = t - ty * tiles_x8;
+        steps = march_pixel_proc<SHADOW, EARLY>(a, tx * 8 + lane_x(lane), ty * 8 + lane_y(lane));
+    }
+    if (a.step_counter) add_steps(a, steps);
+}
+
 template <int L, int W>
 hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStream_t s)
 {
@@ -434,6 +520,19 @@ hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStre
 }
 
 }  // namespace
+
+hipError_t launch_march_procedural(const MarchArgs& a, bool early, hipStream_t s)
+{
+    if (a.width <= 0 || a.out_rows <= 0) return hipSuccess;
+    const int tiles = ((a.width + 7) >> 3) * ((a.out_rows + 7) >> 3);
+    const dim3 grid((tiles + 3) / 4), block(kThreads);
+    const bool shadow = a.proc.shadow_steps > 0;
+    if (shadow && early) hipLaunchKernelGGL((march_proc<true, true>), grid, block, 0, s, a);
+    else if (shadow) hipLaunchKernelGGL((march_proc<true, false>), grid, block, 0, s, a);
+    else if (early) hipLaunchKernelGGL((march_proc<false, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((march_proc<false, false>), grid, block, 0, s, a);
+    return hipGetLastError();
+}
 
 hipError_t launch_march(const MarchArgs& a, int layout, int wrap, bool early, const Schedule& sc, hipStream_t s)
 {

@@ -31,7 +31,8 @@ import torch
 
 from . import _lib
 from ._lib import (BYTES_PER_PIXEL, FMT_RGBA8_SRGB, FMT_RGBA8_UNORM, FMT_RGBA32F,  # noqa: F401
-                   GlobalShaderData, MarchParams, ObjectShaderData, Target, VolumeRecipe, VRError, call)
+                   GlobalShaderData, MarchParams, ObjectShaderData, Procedural, Target, VolumeRecipe, VRError,
+                   call)
 
 _lib.load()  # fail at import if the HIP library is missing
 
@@ -66,6 +67,19 @@ def volume_recipe_defaults(**overrides) -> VolumeRecipe:
         else:
             setattr(r, k, v)
     return r
+
+
+def procedural_defaults(**overrides) -> Procedural:
+    """BASELINE config 2 medium (enabled=1); shadow_steps=8 gives config 3."""
+    p = Procedural()
+    call("vr_procedural_defaults", ctypes.byref(p))
+    p.enabled = 1
+    for k, v in overrides.items():
+        if isinstance(v, (list, tuple)):
+            getattr(p, k)[:] = list(v)
+        else:
+            setattr(p, k, v)
+    return p
 
 
 def scaled_recipe(size: int, literal: bool = True) -> VolumeRecipe:
@@ -177,6 +191,12 @@ class Renderer:
         m = m if m is not None else march_defaults(**overrides)
         call("vr_set_march", self._ctx, ctypes.byref(m))
         self.march = m
+
+    def set_procedural(self, p: Procedural | None = None, **overrides) -> None:
+        """Enable the procedural medium (configs 2/3); pass enabled=0 to return to the volume."""
+        p = p if p is not None else procedural_defaults(**overrides)
+        call("vr_set_procedural", self._ctx, ctypes.byref(p))
+        self.procedural = p
 
     def set_layout_preference(self, pref: int) -> None:
         call("vr_set_layout_preference", self._ctx, int(pref))
