@@ -14,14 +14,13 @@ metric), max over ranks.  roofline: algorithmic gather bytes of the march
 kernel (32 B per executed ray-step) / its mean HIP-event
 duration.  cpu_baseline: the CPU oracle (oracle/, a port) on the same workload.
 
-The procedural configs (BASELINE configs 2-4: "cloud", "cloud_shadow",
-"cloud4k") march the build-defined Perlin-fBm x Worley medium instead of a
+The procedural configs (BASELINE configs 2/3: "cloud", "cloud_shadow") march the build-defined Perlin-fBm x Worley medium instead of a
 grid.  They are ALU-bound, so their roofline is VALU: FLOP_PER_DENSITY
 algorithmic fp32 FLOP per density evaluation x the
 evaluations per launch (vr option "count" = 1) / mean kernel duration, against
 the 157.3 TFLOP/s fp32 vector peak.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config grid512|grid128|cloud|cloud_shadow|cloud4k]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config grid512|grid128|grid4k|cloud|cloud_shadow]
 """
 from __future__ import annotations
 
@@ -51,7 +50,7 @@ CONFIGS = {
     "grid128": (128, 1920, 1080, 128, 0, None),
     "cloud": (None, 1920, 1080, 128, 0, 1),
     "cloud_shadow": (None, 1920, 1080, 128, 8, 2),
-    "cloud4k": (None, 3840, 2160, 256, 0, 3),
+    "grid4k": (128, 3840, 2160, 256, 0, 3),
 }
 
 
@@ -109,6 +108,7 @@ def main() -> int:
     ap.add_argument("--config", default="grid512", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--schedule", type=int, default=-1, help="vr option 'schedule' (-1 = auto)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse the N>1 path with several ranks on one GPU")
     args = ap.parse_args()
@@ -136,6 +136,7 @@ def main() -> int:
     else:
         r.generate_volume(vr.scaled_recipe(N))
     osd, gsd = vr.reference_shader_data(1280.0 / 720.0)
+    r.set_option("schedule", args.schedule)
     r.set_shader_data(osd, gsd)
     march = vr.march_defaults(max_steps=S)
     r.set_march(march)

@@ -297,57 +297,86 @@ def test_config1_matches_golden_fixture(r):
 
 # ---- procedural medium (BASELINE configs 2/3; build-defined) ----
 
-def render_proc_both(r, oracle, W, H, march, fmt=0, osd=None, gsd=None, **proc):
+def render_proc_both(r, oracle, W, H, march, fmt=0, osd=None, gsd=None, schedule=-1, band=None, **proc):
     if osd is None:
         osd, gsd = vr.reference_shader_data(W / H, 20.0, 15.0)
+    band = band or {}
     r.set_shader_data(osd, gsd)
     r.set_march(march)
     r.set_procedural(**proc)
+    r.set_option("schedule", schedule)
+    p = oracle.procedural_from(r.procedural)
     try:
         cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
-        img = r.render(W, H, fmt, step_counter=cnt)
+        img = r.render(W, H, fmt, step_counter=cnt, **band)
         torch.cuda.synchronize()
         variant = r.kernel_variant
     finally:
         r.set_procedural(enabled=0)
+        r.set_option("schedule", -1)
     obj, glob = vr.shader_data_arrays(osd, gsd)
-    ref, steps = oracle.render_procedural(oracle.procedural_from(r.procedural), obj, glob,
-                                          oracle.from_params(march), W, H, fmt)
+    ref, steps = oracle.render_procedural(p, obj, glob,
+                                          oracle.from_params(march), W, H, fmt, **band)
     return img.cpu().numpy(), ref, int(cnt.item()), steps, variant
 
 
-def test_procedural_config2_cloud(r, oracle):
-    img, ref, c, s, var = render_proc_both(r, oracle, 192, 108, vr.march_defaults(max_steps=128))
-    assert var == "procedural"
+@pytest.mark.parametrize("schedule,suffix", [(-1, ""), (0, "_tiles")])
+def test_procedural_config2_cloud(r, oracle, schedule, suffix):
+    img, ref, c, s, var = render_proc_both(r, oracle, 192, 108, vr.march_defaults(max_steps=128), schedule=schedule)
+    assert var == "procedural" + suffix
     assert_exact(img, ref)
     assert c == s > 0
     assert img[..., 0].max() > 0.05   # the cloud is not empty
 
 
-def test_procedural_config3_shadow(r, oracle):
-    img, ref, c, s, var = render_proc_both(r, oracle, 128, 72, vr.march_defaults(max_steps=128), shadow_steps=8)
-    assert var == "procedural_shadow"
+@pytest.mark.parametrize("schedule,suffix", [(-1, ""), (0, "_tiles")])
+def test_procedural_config3_shadow(r, oracle, schedule, suffix):
+    img, ref, c, s, var = render_proc_both(r, oracle, 128, 72, vr.march_defaults(max_steps=128), schedule=schedule,
+                                           shadow_steps=8)
+    assert var == "procedural_shadow" + suffix
     assert_exact(img, ref)
     assert c == s > 0
     assert img[..., 0].max() > 0.0
 
 
 @pytest.mark.parametrize("kw", [dict(octaves=1, seed_fbm=11), dict(octaves=6, gain=0.6, worley_freq=0.05),
-                                dict(shadow_steps=3, sun_dir=(0.0, 1.0, 0.0))])
+                                dict(shadow_steps=3, sun_dir=(0.0, 1.0, 0.0)),
+                                dict(shadow_steps=16, sun_dir=(-1.0, 0.5, 0.25)),
+                                dict(shadow_steps=21, sun_dir=(0.3, -1.0, 2.0)),     # > compaction limit
+                                dict(shadow_steps=5, schedule=0)])
 def test_procedural_parameters(r, oracle, kw):
     img, ref, c, s, _ = render_proc_both(r, oracle, 96, 64, vr.march_defaults(max_steps=48, density=3.0), **kw)
     assert_exact(img, ref)
     assert c == s
 
 
-def test_procedural_early_out_and_rgba8(r, oracle):
+@pytest.mark.parametrize("shadow", [0, 4])
+def test_procedural_early_out_and_rgba8(r, oracle, shadow):
     m = vr.march_defaults(max_steps=96, density=400.0, early_out=0.01)
-    img, ref, c, s, _ = render_proc_both(r, oracle, 96, 64, m, fmt=vr.FMT_RGBA8_UNORM)
+    img, ref, c, s, _ = render_proc_both(r, oracle, 96, 64, m, fmt=vr.FMT_RGBA8_UNORM, shadow_steps=shadow)
     assert_exact(img, ref)
     assert c == s
     full = vr.march_defaults(max_steps=96, density=400.0)
-    _, _, c2, _, _ = render_proc_both(r, oracle, 96, 64, full, fmt=vr.FMT_RGBA8_UNORM)
+    _, _, c2, _, _ = render_proc_both(r, oracle, 96, 64, full, fmt=vr.FMT_RGBA8_UNORM, shadow_steps=shadow)
     assert c < c2   # the early-out really skipped steps
+
+
+@pytest.mark.parametrize("shadow", [0, 8])
+def test_procedural_bands(r, oracle, shadow):
+    band = dict(band_rows=16, band_stride=3, band_first=1)
+    img, ref, c, s, _ = render_proc_both(r, oracle, 200, 150, vr.march_defaults(max_steps=64), band=band,
+                                         shadow_steps=shadow)
+    assert_exact(img, ref)
+    assert c == s
+
+
+def test_procedural_1080p_config2_full_frame(r, oracle):
+    """BASELINE config 2 at its full size (the oracle takes a few seconds)."""
+    osd, gsd = vr.reference_shader_data(1280.0 / 720.0)
+    img, ref, c, s, _ = render_proc_both(r, oracle, 1920, 1080, vr.march_defaults(), fmt=vr.FMT_RGBA8_UNORM,
+                                         osd=osd, gsd=gsd)
+    assert_exact(img, ref)
+    assert c == s == 16737882
 
 
 def test_procedural_rejects_bad_parameters(r):
@@ -367,15 +396,21 @@ def test_procedural_density_evaluation_count(r, oracle):
     r.set_shader_data(osd, gsd)
     r.set_march(m)
     r.set_procedural(shadow_steps=8)
+    p = oracle.procedural_from(r.procedural)
     r.set_option("count", 1)
+    got = []
     try:
-        cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
-        r.render(W, H, 0, step_counter=cnt)
-        torch.cuda.synchronize()
+        for sched in (-1, 0):
+            r.set_option("schedule", sched)
+            cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+            r.render(W, H, 0, step_counter=cnt)
+            torch.cuda.synchronize()
+            got.append(int(cnt.item()))
     finally:
         r.set_option("count", 0)
+        r.set_option("schedule", -1)
         r.set_procedural(enabled=0)
     obj, glob = vr.shader_data_arrays(osd, gsd)
-    _, steps, evals = oracle.render_procedural(oracle.procedural_from(r.procedural), obj, glob,
+    _, steps, evals = oracle.render_procedural(p, obj, glob,
                                                oracle.from_params(m), W, H, 0, with_evals=True)
-    assert int(cnt.item()) == evals > steps
+    assert got == [evals, evals] and evals > steps

@@ -23,13 +23,18 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--steps", type=int, default=128)
+    ap.add_argument("--proc", action="store_true", help="procedural medium (config 2)")
+    ap.add_argument("--shadow", type=int, default=0, help="procedural shadow steps (config 3: 8)")
     a = ap.parse_args()
     with vr.Renderer(0) as r:
-        if a.size <= 2:
+        if a.proc:
+            r.set_procedural(shadow_steps=a.shadow)
+        elif a.size <= 2:
             r.set_volume(np.full((a.size,) * 3 + (4,), 200, np.uint8))
         else:
             r.generate_volume(vr.scaled_recipe(a.size))
-        r.set_layout_preference(a.layout)
+        if not a.proc:
+            r.set_layout_preference(a.layout)
         if a.schedule >= 0:
             r.set_option("schedule", a.schedule)
         if a.tpw > 0:

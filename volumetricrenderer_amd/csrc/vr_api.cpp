@@ -67,6 +67,8 @@ struct Ctx {
     int* d_heads = nullptr;        // 8 queue heads (+ padding), zeroed per launch
     vr_procedural proc{};          // procedural medium (configs 2/3), off by default
     int count = 0;                 // step_counter: 0 = executed ray-steps, 1 = density evaluations
+    void* d_sort = nullptr;        // procedural cost-sort scratch (proc_sort_bytes), grown on demand
+    size_t sort_bytes = 0;
 };
 
 // Auto layout (measured): CORNER8 does one load per tap but
@@ -321,6 +323,7 @@ vr_status vr_destroy(void* p)
     (void)hipSetDevice(c->device);
     free_volume(c);
     if (c->d_heads) (void)hipFree(c->d_heads);
+    if (c->d_sort) (void)hipFree(c->d_sort);
     delete c;
     return VR_OK;
 }
@@ -570,7 +573,10 @@ const char* vr_kernel_variant(void* p)
 {
     if (!p) return "none";
     Ctx* c = as_ctx(p);
-    if (c->proc.enabled) return c->proc.shadow_steps > 0 ? "procedural_shadow" : "procedural";
+    if (c->proc.enabled) {
+        if (c->schedule == SCHED_STATIC) return c->proc.shadow_steps > 0 ? "procedural_shadow_tiles" : "procedural_tiles";
+        return c->proc.shadow_steps > 0 ? "procedural_shadow" : "procedural";
+    }
     if (!c->d_planar || !c->has_camera) return "none";
     MarchArgs a{};
     Plan pl{};
@@ -653,7 +659,22 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
     a.step_counter = reinterpret_cast<unsigned long long*>(t->step_counter);
     HIP_TRY(hipSetDevice(c->device));
     if (c->proc.enabled) {
-        HIP_TRY(launch_march_procedural(a, m.early_out > 0.0f, static_cast<hipStream_t>(stream)));
+        // schedule 0 = one 8x8 tile per wave; otherwise (auto) the cost-sorted schedule
+        void* sort_buf = nullptr;
+        if (c->schedule != SCHED_STATIC && a.width < 65536 && a.out_rows < 65536) {
+            const size_t need = proc_sort_bytes(a.width, a.out_rows);
+            if (need > c->sort_bytes) {
+                // the old buffer may still be read by queued work on another stream
+                HIP_TRY(hipDeviceSynchronize());
+                if (c->d_sort) (void)hipFree(c->d_sort);
+                c->d_sort = nullptr;
+                c->sort_bytes = 0;
+                if (hipMalloc(&c->d_sort, need) != hipSuccess) return fail(VR_ERR_OOM, "vr_render: sort buffer");
+                c->sort_bytes = need;
+            }
+            sort_buf = c->d_sort;
+        }
+        HIP_TRY(launch_march_procedural(a, m.early_out > 0.0f, sort_buf, static_cast<hipStream_t>(stream)));
         return VR_OK;
     }
     // auto schedule (measured): static XCD-row tiles for the cache-resident

@@ -332,6 +332,86 @@ __device__ __forceinline__ unsigned march_pixel_proc(const MarchArgs& a, int x, 
     return p.count_evals ? (unsigned)i + evals : (unsigned)i;
 }
 
+// Shadow-ray compaction (config 3).  In march_pixel_proc a wave runs all
+// shadow_steps density evaluations whenever ANY lane has rho > 0, so most
+// lanes idle.  Here a wave instead deals the (lane, shadow step) pairs of the
+// lanes that need them over all 64 lanes: cnt lanes need cnt * S evaluations,
+// done in ceil(cnt * S / 64) rounds.  The results go through LDS and each lane
+// then sums its own S values in step order, so the arithmetic (and the
+// repeated-addition shadow positions) is exactly march_pixel_proc's.
+// Requires wave-uniform control flow: every lane of the wave calls it.
+constexpr int kMaxCompactShadow = 16;
+struct ShadowLds {
+    float p[64][3];                      // positions of the lanes that need shadow rays (compacted)
+    float d[64 * kMaxCompactShadow];     // densities, [compact lane][shadow step]
+};
+
+template <bool EARLY>
+__device__ __forceinline__ unsigned march_pixel_proc_compact(const MarchArgs& a, int x, int orow, bool valid,
+                                                             ShadowLds* sh, unsigned* shadow_evals)
+{
+    Ray r{};
+    r.n = -1;
+    if (valid) r = setup_ray(a, x, orow);
+    const ProcParams& p = a.proc;
+    const int S = p.shadow_steps;
+    const int lane = threadIdx.x & 63;
+    float P0 = r.pxy.x, P1 = r.pxy.y, P2 = r.pz;
+    float acc = 0.0f, rad = 0.0f, tv = 1.0f;
+    int i = 0;
+    bool act = r.n > 0;
+    unsigned evals = 0;
+    for (;;) {
+        act = act && i < r.n;
+        if (__ballot(act) == 0) break;
+        float rho = 0.0f;
+        if (act) rho = proc_density(p, a.scale, P0, P1, P2);
+        const bool need = act && rho > 0.0f;
+        const unsigned long long m = __ballot(need);
+        if (m) {
+            const int cnt = __popcll(m);
+            const int k = __popcll(m & ((1ull << lane) - 1ull));   // compact index of this lane
+            if (need) { sh->p[k][0] = P0; sh->p[k][1] = P1; sh->p[k][2] = P2; }
+            __builtin_amdgcn_wave_barrier();
+            const int total = cnt * S;
+            for (int base = 0; base < total; base += 64) {
+                const int pid = base + lane;
+                if (pid < total) {
+                    const int kk = pid / S, j = pid - kk * S;
+                    float q0 = sh->p[kk][0], q1 = sh->p[kk][1], q2 = sh->p[kk][2];
+                    for (int jj = 0; jj <= j; ++jj) { q0 = q0 + p.lstep[0]; q1 = q1 + p.lstep[1]; q2 = q2 + p.lstep[2]; }
+                    float d = 0.0f;   // outside the box: contributes exactly +0
+                    if (q0 >= 0.0f && q0 <= 1.0f && q1 >= 0.0f && q1 <= 1.0f && q2 >= 0.0f && q2 <= 1.0f) {
+                        d = proc_density(p, a.scale, q0, q1, q2);
+                        ++evals;
+                    }
+                    sh->d[kk * S + j] = d;
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (need) {
+                float sl = 0.0f;
+                for (int j = 0; j < S; ++j) sl = sl + sh->d[k * S + j];
+                const float tl = spec_expf(-(sl * p.od));
+                rad = fmaf((tv * (rho * p.od)), tl, rad);
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (act) {
+            acc = acc + rho;
+            tv = spec_expf(-(acc * p.od));
+            P0 = P0 + r.sxy.x; P1 = P1 + r.sxy.y; P2 = P2 + r.sz;
+            ++i;
+            if constexpr (EARLY) {
+                if (acc > a.acc_limit) act = false;
+            }
+        }
+    }
+    if (r.live) store_pixel(a, x, orow, r.n >= 0, rad);
+    *shadow_evals = evals;
+    return r.n > 0 ? (unsigned)i : 0u;
+}
+
 // Lane -> pixel inside an 8x8 wave tile: row-major, so each 16-lane TA
 // group (tools/tcp_calib.hip) is an 8x2 strip.  Compact 4x4 groups were
 // measured and are no better for brick5 and 15 % slower for brick8: brick8's
@@ -476,6 +556,109 @@ __global__ __launch_bounds__(kThreads) void march_proc(const MarchArgs a)
     if (a.step_counter) add_steps(a, steps);
 }
 
+// ---- procedural, cost-sorted schedule ----
+// A ray's cost is its step count n (a3), known after the ray setup.  Pass 1
+// writes every pixel with n <= 0 and builds a histogram of n; pass 2 turns it
+// into descending-n offsets; pass 3 scatters the packed pixel ids (orow << 16
+// | x) in that order; the march then gives wave w the sorted pixels
+// [64w, 64w + 64).  Lanes of a wave share n (no loop divergence) and the
+// longest rays start first (longest-processing-time order, no tail).
+constexpr int kKeyBins = 1024;
+__device__ __forceinline__ int cost_key(int n) { return n < kKeyBins - 1 ? n : kKeyBins - 1; }
+
+template <bool SHADOW>
+__global__ __launch_bounds__(256) void proc_bin(const MarchArgs a, unsigned* __restrict__ hist)
+{
+    __shared__ unsigned h[kKeyBins];
+    for (int i = threadIdx.x; i < kKeyBins; i += 256) h[i] = 0;
+    __syncthreads();
+    const long long pix = (long long)blockIdx.x * 256 + threadIdx.x;
+    const int orow = (int)(pix / a.width), x = (int)(pix - (long long)orow * a.width);
+    if (orow < a.out_rows) {
+        const Ray r = setup_ray(a, x, orow);
+        if (r.n > 0) atomicAdd(&h[cost_key(r.n)], 1u);
+        else if (r.live) march_pixel_proc<SHADOW, false>(a, x, orow);   // 0 steps: epilogue + store
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kKeyBins; i += 256)
+        if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+
+// hist[kKeyBins] -> cursor[kKeyBins] (start of each key, descending keys) and
+// total at cursor[kKeyBins].  One workgroup of kKeyBins threads.
+__global__ __launch_bounds__(kKeyBins) void proc_scan(const unsigned* __restrict__ hist, unsigned* __restrict__ cursor)
+{
+    __shared__ unsigned sc[kKeyBins];
+    const int t = threadIdx.x;
+    sc[t] = hist[kKeyBins - 1 - t];   // descending key order
+    __syncthreads();
+    for (int off = 1; off < kKeyBins; off <<= 1) {
+        const unsigned v = t >= off ? sc[t - off] : 0u;
+        __syncthreads();
+        sc[t] += v;
+        __syncthreads();
+    }
+    const int key = kKeyBins - 1 - t;
+    cursor[key] = sc[t] - hist[key];   // exclusive
+    if (t == kKeyBins - 1) cursor[kKeyBins] = sc[t];
+}
+
+__global__ __launch_bounds__(256) void proc_scatter(const MarchArgs a, unsigned* __restrict__ cursor,
+                                                    unsigned* __restrict__ order)
+{
+    __shared__ unsigned h[kKeyBins];
+    for (int i = threadIdx.x; i < kKeyBins; i += 256) h[i] = 0;
+    __syncthreads();
+    const long long pix = (long long)blockIdx.x * 256 + threadIdx.x;
+    const int orow = (int)(pix / a.width), x = (int)(pix - (long long)orow * a.width);
+    int key = -1;
+    unsigned rank = 0;
+    if (orow < a.out_rows) {
+        const Ray r = setup_ray(a, x, orow);
+        if (r.n > 0) {
+            key = cost_key(r.n);
+            rank = atomicAdd(&h[key], 1u);
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kKeyBins; i += 256)
+        if (h[i]) h[i] = atomicAdd(&cursor[i], h[i]);   // block's base in the sorted list
+    __syncthreads();
+    if (key >= 0) order[h[key] + rank] = ((unsigned)orow << 16) | (unsigned)x;
+}
+
+template <bool SHADOW, bool EARLY>
+__global__ __launch_bounds__(kThreads) void march_proc_sorted(const MarchArgs a, const unsigned* __restrict__ order,
+                                                              const unsigned* __restrict__ total_ptr)
+{
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const unsigned total = *total_ptr;
+    const unsigned base = (blockIdx.x * (kThreads / 64) + wave) * 64u;
+    if (base >= total) return;   // wave-uniform
+    const unsigned idx = base + lane;
+    const bool valid = idx < total;
+    int x = 0, orow = 0;
+    if (valid) {
+        const unsigned pk = order[idx];
+        x = (int)(pk & 0xffffu);
+        orow = (int)(pk >> 16);
+    }
+    unsigned long long steps;
+    if constexpr (SHADOW) {
+        __shared__ ShadowLds sh[kThreads / 64];
+        if (a.proc.shadow_steps <= kMaxCompactShadow) {
+            unsigned ev = 0;
+            steps = march_pixel_proc_compact<EARLY>(a, x, orow, valid, &sh[wave], &ev);
+            if (a.proc.count_evals) steps += ev;
+        } else {
+            steps = valid ? march_pixel_proc<true, EARLY>(a, x, orow) : 0u;
+        }
+    } else {
+        steps = valid ? march_pixel_proc<false, EARLY>(a, x, orow) : 0u;
+    }
+    if (a.step_counter) add_steps(a, steps);
+}
+
 template <int L, int W>
 hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStream_t s)
 {
@@ -521,12 +704,38 @@ hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStre
 
 }  // namespace
 
-hipError_t launch_march_procedural(const MarchArgs& a, bool early, hipStream_t s)
+size_t proc_sort_bytes(int width, int out_rows)
+{
+    return (size_t)(2 * kKeyBins + 64) * sizeof(unsigned) + (size_t)width * (size_t)out_rows * sizeof(unsigned);
+}
+
+hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_buf, hipStream_t s)
 {
     if (a.width <= 0 || a.out_rows <= 0) return hipSuccess;
+    const bool shadow = a.proc.shadow_steps > 0;
+    if (sort_buf) {
+        unsigned* hist = static_cast<unsigned*>(sort_buf);
+        unsigned* cursor = hist + kKeyBins;            // kKeyBins + 1 entries
+        unsigned* order = hist + 2 * kKeyBins + 64;
+        hipError_t e = hipMemsetAsync(hist, 0, kKeyBins * sizeof(unsigned), s);
+        if (e != hipSuccess) return e;
+        const long long pixels = (long long)a.width * a.out_rows;
+        const dim3 g1((unsigned)((pixels + 255) / 256));
+        if (shadow) hipLaunchKernelGGL((proc_bin<true>), g1, dim3(256), 0, s, a, hist);
+        else hipLaunchKernelGGL((proc_bin<false>), g1, dim3(256), 0, s, a, hist);
+        hipLaunchKernelGGL(proc_scan, dim3(1), dim3(kKeyBins), 0, s, hist, cursor);
+        hipLaunchKernelGGL(proc_scatter, g1, dim3(256), 0, s, a, cursor, order);
+        // the scatter advanced cursor[k] to the end of key k; total stays at cursor[kKeyBins]
+        const dim3 g4((unsigned)((pixels + kThreads - 1) / kThreads));
+        const unsigned* total = cursor + kKeyBins;
+        if (shadow && early) hipLaunchKernelGGL((march_proc_sorted<true, true>), g4, dim3(kThreads), 0, s, a, order, total);
+        else if (shadow) hipLaunchKernelGGL((march_proc_sorted<true, false>), g4, dim3(kThreads), 0, s, a, order, total);
+        else if (early) hipLaunchKernelGGL((march_proc_sorted<false, true>), g4, dim3(kThreads), 0, s, a, order, total);
+        else hipLaunchKernelGGL((march_proc_sorted<false, false>), g4, dim3(kThreads), 0, s, a, order, total);
+        return hipGetLastError();
+    }
     const int tiles = ((a.width + 7) >> 3) * ((a.out_rows + 7) >> 3);
     const dim3 grid((tiles + 3) / 4), block(kThreads);
-    const bool shadow = a.proc.shadow_steps > 0;
     if (shadow && early) hipLaunchKernelGGL((march_proc<true, true>), grid, block, 0, s, a);
     else if (shadow) hipLaunchKernelGGL((march_proc<true, false>), grid, block, 0, s, a);
     else if (early) hipLaunchKernelGGL((march_proc<false, true>), grid, block, 0, s, a);
