@@ -159,6 +159,11 @@ vr_status vr_generate_volume(void* ctx, const vr_volume_recipe* r, void* stream)
 vr_status vr_noise_grid(void* ctx, int kind, void* d_out, int x0, int y0, int z0,
                         int nx, int ny, int nz, float freq, int32_t seed,
                         float* out_min, float* out_max, void* stream);
+/* Exhaustive device self-test of an arithmetic shortcut against its IEEE
+ * definition; *failures = number of mismatching inputs (synchronous).
+ * "cell_inv" (the cellular cell-point magnitude that the noise kernels use)
+ * and the candidates "cell_inv_a", "cell_inv_b", "cell_inv_c".           */
+vr_status vr_selftest(void* ctx, const char* name, long long* failures);
 
 /* ---- uniforms: replaces UniformBuffer<T>::Update x2 (TestMain.cpp:248-249,
  *      VulkanUniformBuffer.h:58-61).  The data is copied.                  */

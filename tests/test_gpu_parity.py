@@ -414,3 +414,11 @@ def test_procedural_density_evaluation_count(r, oracle):
     _, steps, evals = oracle.render_procedural(p, obj, glob,
                                                oracle.from_params(m), W, H, 0, with_evals=True)
     assert got == [evals, evals] and evals > steps
+
+
+def test_cellular_inv_shortcut_exhaustive(r):
+    """The cellular cell-point magnitude the noise kernels use equals
+    jitter / sqrtf(d2) (IEEE) on every input of its domain."""
+    assert r.selftest("cell_inv") == 0
+    with pytest.raises(VRError):
+        r.selftest("nope")

@@ -107,6 +107,7 @@ _SIGS = {
                                                 ctypes.c_float, ctypes.POINTER(ObjectShaderData),
                                                 ctypes.POINTER(GlobalShaderData)]),
     "vr_march_defaults": (ctypes.c_int, [ctypes.POINTER(MarchParams)]),
+    "vr_selftest": (ctypes.c_int, [_vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_longlong)]),
     "vr_procedural_defaults": (ctypes.c_int, [ctypes.POINTER(Procedural)]),
     "vr_set_procedural": (ctypes.c_int, [_vp, ctypes.POINTER(Procedural)]),
     "vr_set_march": (ctypes.c_int, [_vp, ctypes.POINTER(MarchParams)]),

@@ -408,6 +408,28 @@ vr_status vr_noise_grid(void* p, int kind, void* d_out, int x0, int y0, int z0, 
     return VR_OK;
 }
 
+vr_status vr_selftest(void* p, const char* name, long long* failures)
+{
+    if (!p || !name || !failures) return fail(VR_ERR_INVALID, "vr_selftest: null argument");
+    static const char* const kNames[] = {"cell_inv_a", "cell_inv_b", "cell_inv_c", "cell_inv"};
+    int variant = -1;
+    for (int i = 0; i < 4; ++i)
+        if (std::strcmp(name, kNames[i]) == 0) variant = i;
+    if (variant < 0) return fail(VR_ERR_INVALID, "vr_selftest: unknown test '%s'", name);
+    Ctx* c = as_ctx(p);
+    HIP_TRY(hipSetDevice(c->device));
+    unsigned long long* d = nullptr;
+    HIP_TRY(hipMalloc(&d, sizeof *d));
+    unsigned long long h = 0;
+    hipError_t e = hipMemset(d, 0, sizeof *d);
+    if (e == hipSuccess) e = launch_selftest_cell_inv(variant, d, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(&h, d, sizeof h, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(VR_ERR_HIP, "vr_selftest: %s", hipGetErrorString(e));
+    *failures = (long long)h;
+    return VR_OK;
+}
+
 vr_status vr_generate_volume(void* p, const vr_volume_recipe* r, void* stream)
 {
     if (!p || !r) return fail(VR_ERR_INVALID, "vr_generate_volume: null argument");

@@ -98,9 +98,37 @@ __device__ inline float simplex(int32_t seed, float x, float y, float z)
     return 32.69428253173828125f * (((n0 + n1) + n2) + n3);
 }
 
+// Cell-point magnitude jitter / sqrt(d2) (correctly rounded division of the
+// correctly rounded square root, as the oracle computes it).  d2 is a sum of
+// three squared half-integers in [-511.5, 511.5]: d2 = K / 4 with integer
+// K = 3 (mod 8), K <= 3 * 1023^2, always exact in fp32.  Candidate fast
+// sequences are verified exhaustively over that domain by vr_selftest
+// ("cell_inv_a" .. "cell_inv_c"); the one cellular() uses must report 0.
+constexpr float kCellJitter = 0.39614353f;
+__device__ __forceinline__ float cell_inv_ieee(float d2) { return kCellJitter / sqrtf(d2); }
+__device__ __forceinline__ float cell_inv_a(float d2) { return kCellJitter * __builtin_amdgcn_rsqf(d2); }
+__device__ __forceinline__ float cell_inv_b(float d2)
+{
+    const float s = __builtin_amdgcn_sqrtf(d2);
+    const float r = __builtin_amdgcn_rcpf(s);
+    const float q = kCellJitter * r;
+    return fmaf(fmaf(-q, s, kCellJitter), r, q);
+}
+__device__ __forceinline__ float cell_inv_c(float d2)
+{
+    float s = __builtin_amdgcn_sqrtf(d2);   // <= 1 ulp; d2 is normal, no scaling needed
+    const float sdn = __uint_as_float(__float_as_uint(s) - 1u), sup = __uint_as_float(__float_as_uint(s) + 1u);
+    const float rdn = fmaf(-sdn, s, d2), rup = fmaf(-sup, s, d2);
+    s = rdn <= 0.0f ? sdn : s;
+    s = rup > 0.0f ? sup : s;
+    const float r = __builtin_amdgcn_rcpf(s);
+    const float q = kCellJitter * r;
+    return fmaf(fmaf(-q, s, kCellJitter), r, q);
+}
+__device__ __forceinline__ float cell_inv(float d2) { return cell_inv_ieee(d2); }
+
 __device__ inline float cellular(int32_t seed, float x, float y, float z)
 {
-    const float jitter = 0.39614353f;
     const float xr = rintf(x), yr = rintf(y), zr = rintf(z);
     const int32_t xc = wmul((int32_t)xr, kPX), yc = wmul((int32_t)yr, kPY), zc = wmul((int32_t)zr, kPZ);
     float d0 = 3.402823466e+38f;
@@ -120,7 +148,7 @@ __device__ inline float cellular(int32_t seed, float x, float y, float z)
                 float xd = (float)(h & 0x3ff) - 511.5f;
                 float yd = (float)((h >> 10) & 0x3ff) - 511.5f;
                 float zd = (float)((h >> 20) & 0x3ff) - 511.5f;
-                const float inv = jitter / sqrtf(fmaf(zd, zd, fmaf(yd, yd, xd * xd)));
+                const float inv = cell_inv(fmaf(zd, zd, fmaf(yd, yd, xd * xd)));
                 xd = fmaf(xd, inv, xcf);
                 yd = fmaf(yd, inv, ycf);
                 zd = fmaf(zd, inv, zcf);

@@ -301,4 +301,32 @@ hipError_t launch_assemble(const uint8_t* d_gathered, size_t rows_per_rank, int 
     return hipGetLastError();
 }
 
+// ---- self tests (vr_selftest) ----
+namespace {
+__global__ __launch_bounds__(256) void k_selftest_cell_inv(int variant, unsigned long long* __restrict__ bad)
+{
+    constexpr unsigned kMaxK = 3u * 1023u * 1023u;
+    const unsigned i = blockIdx.x * 256u + threadIdx.x;
+    const unsigned K = 8u * i + 3u;
+    unsigned miss = 0;
+    if (K <= kMaxK) {
+        const float d2 = (float)K * 0.25f;
+        const float want = noise::cell_inv_ieee(d2);
+        const float got = variant == 0 ? noise::cell_inv_a(d2) : variant == 1 ? noise::cell_inv_b(d2)
+                        : variant == 2 ? noise::cell_inv_c(d2) : noise::cell_inv(d2);
+        miss = __float_as_uint(got) != __float_as_uint(want);
+    }
+    unsigned long long c = miss;
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(bad, c);
+}
+}  // namespace
+
+hipError_t launch_selftest_cell_inv(int variant, unsigned long long* d_bad, hipStream_t s)
+{
+    constexpr unsigned kCount = (3u * 1023u * 1023u - 3u) / 8u + 1u;
+    hipLaunchKernelGGL(k_selftest_cell_inv, dim3((kCount + 255) / 256), dim3(256), 0, s, variant, d_bad);
+    return hipGetLastError();
+}
+
 }  // namespace vr

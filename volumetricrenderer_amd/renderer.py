@@ -192,6 +192,12 @@ class Renderer:
         call("vr_set_march", self._ctx, ctypes.byref(m))
         self.march = m
 
+    def selftest(self, name: str) -> int:
+        """Mismatch count of a device arithmetic shortcut (vr_selftest)."""
+        n = ctypes.c_longlong()
+        call("vr_selftest", self._ctx, name.encode(), ctypes.byref(n))
+        return int(n.value)
+
     def set_procedural(self, p: Procedural | None = None, **overrides) -> None:
         """Enable the procedural medium (configs 2/3); pass enabled=0 to return to the volume."""
         p = p if p is not None else procedural_defaults(**overrides)
