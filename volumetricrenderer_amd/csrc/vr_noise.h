@@ -125,7 +125,7 @@ __device__ __forceinline__ float cell_inv_c(float d2)
     const float q = kCellJitter * r;
     return fmaf(fmaf(-q, s, kCellJitter), r, q);
 }
-__device__ __forceinline__ float cell_inv(float d2) { return cell_inv_ieee(d2); }
+__device__ __forceinline__ float cell_inv(float d2) { return cell_inv_c(d2); }
 
 __device__ inline float cellular(int32_t seed, float x, float y, float z)
 {
