@@ -205,7 +205,8 @@ def main() -> int:
             if tj.get("config") == args.config and world == 1:
                 traffic = tj.get("hbm_bytes_per_launch")
         out = {
-            "metric": "Mray/s (= W*H*steps/s) at 1080p x 128 steps",
+            "metric": "Mray/s (= W*H*steps/s) at 1080p x 128 steps" if (W, H, S) == (1920, 1080, 128)
+                      else f"Mray/s (= W*H*steps/s) at {W}x{H} x {S} steps",
             "value": round(value, 3),
             "unit": "Mray/s",
             "n_gpus": world,

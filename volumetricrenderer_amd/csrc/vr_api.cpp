@@ -683,7 +683,8 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
     if (c->proc.enabled) {
         // schedule 0 = one 8x8 tile per wave; otherwise (auto) the cost-sorted schedule
         void* sort_buf = nullptr;
-        if (c->schedule != SCHED_STATIC && a.width < 65536 && a.out_rows < 65536) {
+        if (c->schedule != SCHED_STATIC && a.width < 65536 && a.out_rows < 65536 &&
+            (long long)a.width * a.out_rows < (1ll << 31)) {
             const size_t need = proc_sort_bytes(a.width, a.out_rows);
             if (need > c->sort_bytes) {
                 // the old buffer may still be read by queued work on another stream

@@ -567,17 +567,24 @@ constexpr int kKeyBins = 1024;
 __device__ __forceinline__ int cost_key(int n) { return n < kKeyBins - 1 ? n : kKeyBins - 1; }
 
 template <bool SHADOW>
-__global__ __launch_bounds__(256) void proc_bin(const MarchArgs a, unsigned* __restrict__ hist)
+__global__ __launch_bounds__(256) void proc_bin(const MarchArgs a, unsigned* __restrict__ hist,
+                                                unsigned short* __restrict__ keys)
 {
     __shared__ unsigned h[kKeyBins];
     for (int i = threadIdx.x; i < kKeyBins; i += 256) h[i] = 0;
     __syncthreads();
-    const long long pix = (long long)blockIdx.x * 256 + threadIdx.x;
-    const int orow = (int)(pix / a.width), x = (int)(pix - (long long)orow * a.width);
+    const unsigned pix = blockIdx.x * 256u + threadIdx.x;   // < 2^31 (host check)
+    const int orow = (int)(pix / (unsigned)a.width), x = (int)(pix - (unsigned)orow * (unsigned)a.width);
     if (orow < a.out_rows) {
         const Ray r = setup_ray(a, x, orow);
-        if (r.n > 0) atomicAdd(&h[cost_key(r.n)], 1u);
-        else if (r.live) march_pixel_proc<SHADOW, false>(a, x, orow);   // 0 steps: epilogue + store
+        int key = 0;
+        if (r.n > 0) {
+            key = cost_key(r.n);
+            atomicAdd(&h[key], 1u);
+        } else if (r.live) {
+            march_pixel_proc<SHADOW, false>(a, x, orow);   // 0 steps: epilogue + store
+        }
+        keys[pix] = (unsigned short)key;
     }
     __syncthreads();
     for (int i = threadIdx.x; i < kKeyBins; i += 256)
@@ -603,20 +610,20 @@ __global__ __launch_bounds__(kKeyBins) void proc_scan(const unsigned* __restrict
     if (t == kKeyBins - 1) cursor[kKeyBins] = sc[t];
 }
 
-__global__ __launch_bounds__(256) void proc_scatter(const MarchArgs a, unsigned* __restrict__ cursor,
-                                                    unsigned* __restrict__ order)
+__global__ __launch_bounds__(256) void proc_scatter(const MarchArgs a, const unsigned short* __restrict__ keys,
+                                                    unsigned* __restrict__ cursor, unsigned* __restrict__ order)
 {
     __shared__ unsigned h[kKeyBins];
     for (int i = threadIdx.x; i < kKeyBins; i += 256) h[i] = 0;
     __syncthreads();
-    const long long pix = (long long)blockIdx.x * 256 + threadIdx.x;
-    const int orow = (int)(pix / a.width), x = (int)(pix - (long long)orow * a.width);
+    const unsigned pix = blockIdx.x * 256u + threadIdx.x;
+    const int orow = (int)(pix / (unsigned)a.width), x = (int)(pix - (unsigned)orow * (unsigned)a.width);
     int key = -1;
     unsigned rank = 0;
     if (orow < a.out_rows) {
-        const Ray r = setup_ray(a, x, orow);
-        if (r.n > 0) {
-            key = cost_key(r.n);
+        const int k = keys[pix];
+        if (k > 0) {
+            key = k;
             rank = atomicAdd(&h[key], 1u);
         }
     }
@@ -706,7 +713,8 @@ hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStre
 
 size_t proc_sort_bytes(int width, int out_rows)
 {
-    return (size_t)(2 * kKeyBins + 64) * sizeof(unsigned) + (size_t)width * (size_t)out_rows * sizeof(unsigned);
+    // hist, cursor (+ total), order (u32 per pixel), keys (u16 per pixel)
+    return (size_t)(2 * kKeyBins + 64) * sizeof(unsigned) + (size_t)width * (size_t)out_rows * 6u;
 }
 
 hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_buf, hipStream_t s)
@@ -717,14 +725,15 @@ hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_bu
         unsigned* hist = static_cast<unsigned*>(sort_buf);
         unsigned* cursor = hist + kKeyBins;            // kKeyBins + 1 entries
         unsigned* order = hist + 2 * kKeyBins + 64;
+        unsigned short* keys = reinterpret_cast<unsigned short*>(order + (size_t)a.width * a.out_rows);
         hipError_t e = hipMemsetAsync(hist, 0, kKeyBins * sizeof(unsigned), s);
         if (e != hipSuccess) return e;
         const long long pixels = (long long)a.width * a.out_rows;
         const dim3 g1((unsigned)((pixels + 255) / 256));
-        if (shadow) hipLaunchKernelGGL((proc_bin<true>), g1, dim3(256), 0, s, a, hist);
-        else hipLaunchKernelGGL((proc_bin<false>), g1, dim3(256), 0, s, a, hist);
+        if (shadow) hipLaunchKernelGGL((proc_bin<true>), g1, dim3(256), 0, s, a, hist, keys);
+        else hipLaunchKernelGGL((proc_bin<false>), g1, dim3(256), 0, s, a, hist, keys);
         hipLaunchKernelGGL(proc_scan, dim3(1), dim3(kKeyBins), 0, s, hist, cursor);
-        hipLaunchKernelGGL(proc_scatter, g1, dim3(256), 0, s, a, cursor, order);
+        hipLaunchKernelGGL(proc_scatter, g1, dim3(256), 0, s, a, keys, cursor, order);
         // the scatter advanced cursor[k] to the end of key k; total stays at cursor[kKeyBins]
         const dim3 g4((unsigned)((pixels + kThreads - 1) / kThreads));
         const unsigned* total = cursor + kKeyBins;
