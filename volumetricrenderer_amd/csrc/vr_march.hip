@@ -564,6 +564,7 @@ __global__ __launch_bounds__(kThreads) void march_proc(const MarchArgs a)
 // [64w, 64w + 64).  Lanes of a wave share n (no loop divergence) and the
 // longest rays start first (longest-processing-time order, no tail).
 constexpr int kKeyBins = 1024;
+constexpr int kSortPixelsPerThread = 8;   // fewer blocks -> fewer global atomics on hot bins
 __device__ __forceinline__ int cost_key(int n) { return n < kKeyBins - 1 ? n : kKeyBins - 1; }
 
 template <bool SHADOW>
@@ -573,9 +574,10 @@ __global__ __launch_bounds__(256) void proc_bin(const MarchArgs a, unsigned* __r
     __shared__ unsigned h[kKeyBins];
     for (int i = threadIdx.x; i < kKeyBins; i += 256) h[i] = 0;
     __syncthreads();
-    const unsigned pix = blockIdx.x * 256u + threadIdx.x;   // < 2^31 (host check)
-    const int orow = (int)(pix / (unsigned)a.width), x = (int)(pix - (unsigned)orow * (unsigned)a.width);
-    if (orow < a.out_rows) {
+    for (int it = 0; it < kSortPixelsPerThread; ++it) {
+        const unsigned pix = (blockIdx.x * kSortPixelsPerThread + it) * 256u + threadIdx.x;   // < 2^31 (host check)
+        const int orow = (int)(pix / (unsigned)a.width), x = (int)(pix - (unsigned)orow * (unsigned)a.width);
+        if (orow >= a.out_rows) break;
         const Ray r = setup_ray(a, x, orow);
         int key = 0;
         if (r.n > 0) {
@@ -616,22 +618,27 @@ __global__ __launch_bounds__(256) void proc_scatter(const MarchArgs a, const uns
     __shared__ unsigned h[kKeyBins];
     for (int i = threadIdx.x; i < kKeyBins; i += 256) h[i] = 0;
     __syncthreads();
-    const unsigned pix = blockIdx.x * 256u + threadIdx.x;
-    const int orow = (int)(pix / (unsigned)a.width), x = (int)(pix - (unsigned)orow * (unsigned)a.width);
-    int key = -1;
-    unsigned rank = 0;
-    if (orow < a.out_rows) {
-        const int k = keys[pix];
-        if (k > 0) {
-            key = k;
-            rank = atomicAdd(&h[key], 1u);
+    int key[kSortPixelsPerThread];
+    unsigned rank[kSortPixelsPerThread], packed[kSortPixelsPerThread];
+    for (int it = 0; it < kSortPixelsPerThread; ++it) {
+        key[it] = -1;
+        const unsigned pix = (blockIdx.x * kSortPixelsPerThread + it) * 256u + threadIdx.x;
+        const int orow = (int)(pix / (unsigned)a.width), x = (int)(pix - (unsigned)orow * (unsigned)a.width);
+        if (orow < a.out_rows) {
+            const int k = keys[pix];
+            if (k > 0) {
+                key[it] = k;
+                rank[it] = atomicAdd(&h[k], 1u);
+                packed[it] = ((unsigned)orow << 16) | (unsigned)x;
+            }
         }
     }
     __syncthreads();
     for (int i = threadIdx.x; i < kKeyBins; i += 256)
         if (h[i]) h[i] = atomicAdd(&cursor[i], h[i]);   // block's base in the sorted list
     __syncthreads();
-    if (key >= 0) order[h[key] + rank] = ((unsigned)orow << 16) | (unsigned)x;
+    for (int it = 0; it < kSortPixelsPerThread; ++it)
+        if (key[it] >= 0) order[h[key[it]] + rank[it]] = packed[it];
 }
 
 template <bool SHADOW, bool EARLY>
@@ -729,7 +736,7 @@ hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_bu
         hipError_t e = hipMemsetAsync(hist, 0, kKeyBins * sizeof(unsigned), s);
         if (e != hipSuccess) return e;
         const long long pixels = (long long)a.width * a.out_rows;
-        const dim3 g1((unsigned)((pixels + 255) / 256));
+        const dim3 g1((unsigned)((pixels + 256 * kSortPixelsPerThread - 1) / (256 * kSortPixelsPerThread)));
         if (shadow) hipLaunchKernelGGL((proc_bin<true>), g1, dim3(256), 0, s, a, hist, keys);
         else hipLaunchKernelGGL((proc_bin<false>), g1, dim3(256), 0, s, a, hist, keys);
         hipLaunchKernelGGL(proc_scan, dim3(1), dim3(kKeyBins), 0, s, hist, cursor);
