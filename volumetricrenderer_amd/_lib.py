@@ -21,7 +21,8 @@ except ImportError:  # pragma: no cover - torch is always present in this image
     torch = None
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libvr.so")
+# VR_LIB overrides the library path (timing experiments with variant builds)
+LIB_PATH = os.environ.get("VR_LIB") or os.path.join(HERE, "libvr.so")
 
 VR_OK = 0
 STATUS_NAMES = {

@@ -71,13 +71,14 @@ struct Ctx {
     size_t sort_bytes = 0;
 };
 
-// Auto layout (measured, DESIGN.md sec. 4.2): CORNER8 does one load per tap but
+// Auto layout (measured, DESIGN.md sec. 4): CORNER8 does one load per tap but
 // stores 8 bytes per texel.  It wins while the volume fits the 256 MiB
-// Infinity Cache.  Past that it is HBM-bound, and BRICK8 (1.49x bytes) wins.
+// Infinity Cache.  Past that it is HBM-bound, and BRICK5 (2x bytes, two loads
+// per tap, each footprint inside one 128-B line) wins with the pipelined march.
 constexpr size_t kCorner8MaxBytes = 160ull << 20;
 int auto_layout(int nx, int ny, int nz)
 {
-    return 4 * layout_plane_bytes(LAYOUT_CORNER8, nx, ny, nz) <= kCorner8MaxBytes ? LAYOUT_CORNER8 : LAYOUT_BRICK8;
+    return 4 * layout_plane_bytes(LAYOUT_CORNER8, nx, ny, nz) <= kCorner8MaxBytes ? LAYOUT_CORNER8 : LAYOUT_BRICK5;
 }
 
 Ctx* as_ctx(void* p) { return static_cast<Ctx*>(p); }
