@@ -202,7 +202,7 @@ def main() -> int:
         if os.path.exists(tfile):
             with open(tfile) as f:
                 tj = json.load(f)
-            if tj.get("config") == args.config and world == 1:
+            if tj.get("config") == args.config and tj.get("kernel") == r.kernel_variant and world == 1:
                 traffic = tj.get("hbm_bytes_per_launch")
         out = {
             "metric": "Mray/s (= W*H*steps/s) at 1080p x 128 steps" if (W, H, S) == (1920, 1080, 128)

@@ -13,9 +13,13 @@ from pmc_summary import load  # noqa: E402
 
 tag, config, out = sys.argv[1], sys.argv[2], sys.argv[3]
 c = load(tag)
+kernel = None
+for line in open(f"gpurun_out/pmc_{tag}/p1.log"):
+    if line.startswith("variant "):
+        kernel = line.split()[1]
 fetch = c["FETCH_SIZE"] * 1024 * 2
 write = c["WRITE_SIZE"] * 1024
-res = {"config": config, "hbm_bytes_per_launch": round(fetch + write),
+res = {"config": config, "kernel": kernel, "hbm_bytes_per_launch": round(fetch + write),
        "fetch_bytes": round(fetch), "write_bytes": round(write),
        "raw": {k: c[k] for k in ("FETCH_SIZE", "WRITE_SIZE") if k in c},
        "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over tools/prof_case.py "
