@@ -297,12 +297,13 @@ __device__ __forceinline__ void store_pixel(const MarchArgs& a, int x, int orow,
 
 // One ray of the grid path: setup, the march (frag.glsl:57-75), the
 // epilogue (:76-80) and the store.  Returns the executed steps.
-// Fast layouts run software-pipelined: step i+1's loads are issued before
-// step i is blended, so a wave has two steps of gathers in flight.  This
-// costs VGPRs (84-107, 4-5 waves/SIMD) and is still faster: at 512^3 brick5
-// 0.334 -> 0.280 ms, corner8 0.497 -> 0.468 ms, brick8 and 128^3 corner8
-// unchanged.  Forcing 6 or 8 waves/SIMD (amdgpu_waves_per_eu) was slower in
-// every case, with or without pipelining.
+// The brick layouts run software-pipelined: step i+1's loads are issued
+// before step i is blended, so a wave has two steps of gathers in flight.
+// This costs VGPRs (84-107, 4-5 waves/SIMD) and is still faster: at 512^3
+// brick5 0.334 -> 0.280 ms, brick8 unchanged.  CORNER8 (the cache-resident
+// layout, one load per tap) is not: 0.51 -> 0.56 ms at 3840x2160x256.
+// Forcing 6 or 8 waves/SIMD (amdgpu_waves_per_eu) was slower in every case,
+// with or without pipelining.
 #ifndef VR_PIPE
 #define VR_PIPE 1
 #endif
@@ -310,7 +311,7 @@ template <int LAYOUT, int WRAP, bool EARLY>
 __device__ __forceinline__ unsigned march_pixel(const MarchArgs& a, const FastCtx& f, int x, int orow)
 {
     const Ray r = setup_ray(a, x, orow);
-    if constexpr (VR_PIPE && LAYOUT != LAYOUT_PLANAR) {
+    if constexpr (VR_PIPE && LAYOUT != LAYOUT_PLANAR && LAYOUT != LAYOUT_CORNER8) {
         f2 pxy = r.pxy;
         float pz = r.pz;
         float acc = 0.0f;
