@@ -555,9 +555,9 @@ vr_status vr_set_option(void* p, const char* name, int value)
     const std::string n(name);
     if (n == "layout") return vr_set_layout_preference(p, value);
     if (n == "schedule") {
-        if (value < -1 || value > 3)
-            return fail(VR_ERR_INVALID,
-                        "vr_set_option: schedule is -1 (auto), 0 (static), 1 (queue), 2 (strided) or 3 (xcd rows)");
+        if (value < -1 || value > 4)
+            return fail(VR_ERR_INVALID, "vr_set_option: schedule is -1 (auto), 0 (static), 1 (queue), "
+                                        "2 (strided), 3 (xcd rows) or 4 (rings)");
         c->schedule = value;
         return VR_OK;
     }
@@ -605,6 +605,37 @@ const char* vr_kernel_variant(void* p)
     Plan pl{};
     make_plan(c, &a, &pl);
     return variant_name(pl);
+}
+
+// Target pixel (x, packed output row) under the projected box centre: the
+// centre of the ring schedule.  Model, View, Projection are column-major
+// (vr_object_shader_data); the product is applied to the box-centre point.
+void box_centre_pixel(const Ctx* c, const MarchArgs& a, int* px, int* prow)
+{
+    const float* M = c->obj;
+    const float* V = c->obj + 16;
+    const float* P = c->obj + 32;
+    double v[4] = {0.5 * ((double)a.box_min[0] + a.box_max[0]), 0.5 * ((double)a.box_min[1] + a.box_max[1]),
+                   0.5 * ((double)a.box_min[2] + a.box_max[2]), 1.0};
+    for (const float* m : {M, V, P}) {
+        double o[4];
+        for (int r = 0; r < 4; ++r) o[r] = m[r] * v[0] + m[4 + r] * v[1] + m[8 + r] * v[2] + m[12 + r] * v[3];
+        for (int r = 0; r < 4; ++r) v[r] = o[r];
+    }
+    double sx = 0.5 * a.width, sy = 0.5 * a.height;
+    if (v[3] > 0.0) {
+        sx = (v[0] / v[3] * 0.5 + 0.5) * a.width;
+        sy = (v[1] / v[3] * 0.5 + 0.5) * a.height;
+    }
+    const int y = (int)std::min(std::max(sy, 0.0), (double)(a.height - 1));
+    int row = y;
+    if (a.band_rows > 0 && a.band_stride > 1) {   // the nearest of this rank's packed rows
+        const int b = y / a.band_rows;
+        const int sel = b >= a.band_first ? (b - a.band_first) / a.band_stride : 0;
+        row = sel * a.band_rows + y % a.band_rows;
+    }
+    *px = (int)std::min(std::max(sx, 0.0), (double)(a.width - 1));
+    *prow = std::min(std::max(row, 0), std::max(a.out_rows - 1, 0));
 }
 
 vr_status vr_render(void* p, const vr_target* t, void* stream)
@@ -704,7 +735,8 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
     // auto schedule (measured): static XCD-row tiles for the cache-resident
     // CORNER8 volume, strided single tiles otherwise
     const int kind = c->schedule >= 0 ? c->schedule : (pl.layout == LAYOUT_CORNER8 ? SCHED_STATIC : SCHED_STRIDED);
-    const Schedule sc{kind, c->tiles_per_wave, c->waves_per_simd, c->d_heads};
+    Schedule sc{kind, 0, 0, c->tiles_per_wave, c->waves_per_simd, c->d_heads};
+    if (kind == SCHED_RINGS) box_centre_pixel(c, a, &sc.center_x, &sc.center_y);
     HIP_TRY(launch_march(a, pl.layout, pl.wrap, pl.early, sc, static_cast<hipStream_t>(stream)));
     return VR_OK;
 }

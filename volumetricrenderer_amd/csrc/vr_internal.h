@@ -110,9 +110,10 @@ struct MarchArgs {
 };
 
 // How the march kernel maps tiles to waves.
-enum ScheduleKind : int { SCHED_STATIC = 0, SCHED_QUEUE = 1, SCHED_STRIDED = 2, SCHED_XCDROWS = 3 };
+enum ScheduleKind : int { SCHED_STATIC = 0, SCHED_QUEUE = 1, SCHED_STRIDED = 2, SCHED_XCDROWS = 3, SCHED_RINGS = 4 };
 struct Schedule {
     int kind;
+    int center_x, center_y;   // rings: target pixel under the projected box centre
     int tiles_per_wave;    // strided: 8x8 tiles per wave
     int waves_per_simd;    // queue: persistent waves per SIMD (grid = 256 CUs x this)
     int* heads;            // queue: 8 device ints, zeroed before each launch

@@ -592,6 +592,39 @@ __global__ __launch_bounds__(kThreads) void march_strided(const MarchArgs a, int
     if (a.step_counter) add_steps(a, steps);
 }
 
+// Ring schedule: wave k renders the k-th 8x8 tile of square rings around the
+// tile (cx, cy) under the projected box centre, where rays are longest.  The
+// longest-running waves start first (longest-processing-time order), so no
+// long wave is left to run alone at the end.  Ring r >= 1 holds 8r tiles and
+// starts at wave (2r-1)^2; waves whose tile is off the target exit at once.
+__device__ __forceinline__ bool ring_tile(int k, int cx, int cy, int* tx, int* ty)
+{
+    if (k == 0) { *tx = cx; *ty = cy; return true; }
+    const int r = (int)((sqrtf((float)k) + 1.0f) * 0.5f);
+    const int j = k - (2 * r - 1) * (2 * r - 1), side = j / (2 * r), t = j - side * 2 * r;
+    if (side == 0) { *tx = cx - r + t; *ty = cy - r; }
+    else if (side == 1) { *tx = cx + r; *ty = cy - r + t; }
+    else if (side == 2) { *tx = cx + r - t; *ty = cy + r; }
+    else { *tx = cx - r; *ty = cy + r - t; }
+    return true;
+}
+
+template <int LAYOUT, int WRAP, bool EARLY>
+__global__ __launch_bounds__(kThreads) void march_rings(const MarchArgs a, int cx, int cy)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned lds[];
+    const FastCtx f = fast_prologue<LAYOUT>(a, lds);
+    const int lane = threadIdx.x & 63;
+    const int k = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+    const int tiles_x8 = (a.width + 7) >> 3, rows8 = (a.out_rows + 7) >> 3;
+    int tx, ty;
+    ring_tile(k, cx, cy, &tx, &ty);
+    unsigned long long steps = 0;
+    if (tx >= 0 && tx < tiles_x8 && ty >= 0 && ty < rows8)
+        steps = march_pixel<LAYOUT, WRAP, EARLY>(a, f, tx * 8 + lane_x(lane), ty * 8 + lane_y(lane));
+    if (a.step_counter) add_steps(a, steps);
+}
+
 // XCD-row schedule: one 8x8 tile per wave, 4 horizontally adjacent tiles per
 // workgroup.  8-px tile rows are dealt to XCDs round-robin: XCD x walks rows
 // x, x+8, ... (blockIdx % 8, speed-only).  Rows interleave, so the balance
@@ -788,6 +821,18 @@ hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStre
             hipLaunchKernelGGL((march_strided<L, W, true>), grid, block, lds, s, a, 4 * (int)grid.x);
         else
             hipLaunchKernelGGL((march_strided<L, W, false>), grid, block, lds, s, a, 4 * (int)grid.x);
+        return hipGetLastError();
+    }
+    if (sc.kind == SCHED_RINGS) {
+        const int tiles_x8 = (a.width + 7) >> 3, rows8 = (a.out_rows + 7) >> 3;
+        const int cx = min(max(sc.center_x >> 3, 0), tiles_x8 - 1), cy = min(max(sc.center_y >> 3, 0), rows8 - 1);
+        const int R = max(max(cx, tiles_x8 - 1 - cx), max(cy, rows8 - 1 - cy));
+        const long long waves = (2ll * R + 1) * (2ll * R + 1);
+        const dim3 grid((unsigned)((waves + 3) / 4));
+        if (early)
+            hipLaunchKernelGGL((march_rings<L, W, true>), grid, block, lds, s, a, cx, cy);
+        else
+            hipLaunchKernelGGL((march_rings<L, W, false>), grid, block, lds, s, a, cx, cy);
         return hipGetLastError();
     }
     if (sc.kind == SCHED_XCDROWS) {
