@@ -732,9 +732,8 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
         HIP_TRY(launch_march_procedural(a, m.early_out > 0.0f, sort_buf, static_cast<hipStream_t>(stream)));
         return VR_OK;
     }
-    // auto schedule (measured): static XCD-row tiles for the cache-resident
-    // CORNER8 volume, strided single tiles otherwise
-    const int kind = c->schedule >= 0 ? c->schedule : (pl.layout == LAYOUT_CORNER8 ? SCHED_STATIC : SCHED_STRIDED);
+    // auto schedule (measured): rings, longest rays first
+    const int kind = c->schedule >= 0 ? c->schedule : SCHED_RINGS;
     Schedule sc{kind, 0, 0, c->tiles_per_wave, c->waves_per_simd, c->d_heads};
     if (kind == SCHED_RINGS) box_centre_pixel(c, a, &sc.center_x, &sc.center_y);
     HIP_TRY(launch_march(a, pl.layout, pl.wrap, pl.early, sc, static_cast<hipStream_t>(stream)));
