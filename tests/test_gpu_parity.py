@@ -320,7 +320,7 @@ def render_proc_both(r, oracle, W, H, march, fmt=0, osd=None, gsd=None, schedule
     return img.cpu().numpy(), ref, int(cnt.item()), steps, variant
 
 
-@pytest.mark.parametrize("schedule,suffix", [(-1, ""), (0, "_tiles")])
+@pytest.mark.parametrize("schedule,suffix", [(-1, ""), (0, "_tiles"), (4, "_rings")])
 def test_procedural_config2_cloud(r, oracle, schedule, suffix):
     img, ref, c, s, var = render_proc_both(r, oracle, 192, 108, vr.march_defaults(max_steps=128), schedule=schedule)
     assert var == "procedural" + suffix
@@ -329,7 +329,7 @@ def test_procedural_config2_cloud(r, oracle, schedule, suffix):
     assert img[..., 0].max() > 0.05   # the cloud is not empty
 
 
-@pytest.mark.parametrize("schedule,suffix", [(-1, ""), (0, "_tiles")])
+@pytest.mark.parametrize("schedule,suffix", [(-1, ""), (0, "_tiles"), (4, "_rings")])
 def test_procedural_config3_shadow(r, oracle, schedule, suffix):
     img, ref, c, s, var = render_proc_both(r, oracle, 128, 72, vr.march_defaults(max_steps=128), schedule=schedule,
                                            shadow_steps=8)

@@ -598,6 +598,7 @@ const char* vr_kernel_variant(void* p)
     Ctx* c = as_ctx(p);
     if (c->proc.enabled) {
         if (c->schedule == SCHED_STATIC) return c->proc.shadow_steps > 0 ? "procedural_shadow_tiles" : "procedural_tiles";
+        if (c->schedule == SCHED_RINGS) return c->proc.shadow_steps > 0 ? "procedural_shadow_rings" : "procedural_rings";
         return c->proc.shadow_steps > 0 ? "procedural_shadow" : "procedural";
     }
     if (!c->d_planar || !c->has_camera) return "none";
@@ -713,9 +714,12 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
     a.step_counter = reinterpret_cast<unsigned long long*>(t->step_counter);
     HIP_TRY(hipSetDevice(c->device));
     if (c->proc.enabled) {
-        // schedule 0 = one 8x8 tile per wave; otherwise (auto) the cost-sorted schedule
+        // schedule 0 = one 8x8 tile per wave in row order, 4 = in rings;
+        // otherwise (auto) the cost-sorted schedule
         void* sort_buf = nullptr;
-        if (c->schedule != SCHED_STATIC && a.width < 65536 && a.out_rows < 65536 &&
+        Schedule sc{c->schedule == SCHED_RINGS ? SCHED_RINGS : SCHED_STATIC, 0, 0, 1, 1, nullptr};
+        if (sc.kind == SCHED_RINGS) box_centre_pixel(c, a, &sc.center_x, &sc.center_y);
+        if (c->schedule != SCHED_STATIC && c->schedule != SCHED_RINGS && a.width < 65536 && a.out_rows < 65536 &&
             (long long)a.width * a.out_rows < (1ll << 31)) {
             const size_t need = proc_sort_bytes(a.width, a.out_rows);
             if (need > c->sort_bytes) {
@@ -729,7 +733,7 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
             }
             sort_buf = c->d_sort;
         }
-        HIP_TRY(launch_march_procedural(a, m.early_out > 0.0f, sort_buf, static_cast<hipStream_t>(stream)));
+        HIP_TRY(launch_march_procedural(a, m.early_out > 0.0f, sort_buf, sc, static_cast<hipStream_t>(stream)));
         return VR_OK;
     }
     // auto schedule (measured): rings, longest rays first

@@ -121,8 +121,9 @@ struct Schedule {
 
 // launchers (vr_march.hip / vr_volume.hip); return hipError_t
 hipError_t launch_march(const MarchArgs& a, int layout, int wrap, bool early, const Schedule& sc, hipStream_t s);
-// sort_buf (proc_sort_bytes) selects the cost-sorted schedule; null = 8x8 tiles
-hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_buf, hipStream_t s);
+// sort_buf (proc_sort_bytes) selects the cost-sorted schedule; null = 8x8
+// tiles, in rings when sc.kind == SCHED_RINGS, else in row order
+hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_buf, const Schedule& sc, hipStream_t s);
 size_t proc_sort_bytes(int width, int out_rows);
 hipError_t launch_repack(const uint8_t* d_rgba, int nx, int ny, int nz, uint8_t* d_planar, hipStream_t s);
 // Build a fast layout from the planar planes.

@@ -675,16 +675,23 @@ __global__ __launch_bounds__(kThreads) void march_queue(const MarchArgs a, int* 
     if (a.step_counter) add_steps(a, steps);
 }
 
-// Procedural medium: one 8x8 tile per wave (compute-bound; no volume).
+// Procedural medium: one 8x8 tile per wave (compute-bound; no volume), in
+// row order (cx < 0) or in rings around tile (cx, cy) (see march_rings).
 template <bool SHADOW, bool EARLY>
-__global__ __launch_bounds__(kThreads) void march_proc(const MarchArgs a)
+__global__ __launch_bounds__(kThreads) void march_proc(const MarchArgs a, int cx, int cy)
 {
     const int lane = threadIdx.x & 63;
     const int t = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
     const int tiles_x8 = (a.width + 7) >> 3, rows8 = (a.out_rows + 7) >> 3;
     unsigned long long steps = 0;
-    if (t < tiles_x8 * rows8) {
-        const int ty = t / tiles_x8, tx = t - ty * tiles_x8;
+    int tx, ty;
+    if (cx >= 0) {
+        ring_tile(t, cx, cy, &tx, &ty);
+    } else {
+        ty = t / tiles_x8;
+        tx = t - ty * tiles_x8;
+    }
+    if (tx >= 0 && tx < tiles_x8 && ty >= 0 && ty < rows8) {
         steps = march_pixel_proc<SHADOW, EARLY>(a, tx * 8 + lane_x(lane), ty * 8 + lane_y(lane));
     }
     if (a.step_counter) add_steps(a, steps);
@@ -870,7 +877,7 @@ size_t proc_sort_bytes(int width, int out_rows)
     return (size_t)(2 * kKeyBins + 64) * sizeof(unsigned) + (size_t)width * (size_t)out_rows * 6u;
 }
 
-hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_buf, hipStream_t s)
+hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_buf, const Schedule& sc, hipStream_t s)
 {
     if (a.width <= 0 || a.out_rows <= 0) return hipSuccess;
     const bool shadow = a.proc.shadow_steps > 0;
@@ -896,12 +903,20 @@ hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_bu
         else hipLaunchKernelGGL((march_proc_sorted<false, false>), g4, dim3(kThreads), 0, s, a, order, total);
         return hipGetLastError();
     }
-    const int tiles = ((a.width + 7) >> 3) * ((a.out_rows + 7) >> 3);
-    const dim3 grid((tiles + 3) / 4), block(kThreads);
-    if (shadow && early) hipLaunchKernelGGL((march_proc<true, true>), grid, block, 0, s, a);
-    else if (shadow) hipLaunchKernelGGL((march_proc<true, false>), grid, block, 0, s, a);
-    else if (early) hipLaunchKernelGGL((march_proc<false, true>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((march_proc<false, false>), grid, block, 0, s, a);
+    const int tiles_x8 = (a.width + 7) >> 3, rows8 = (a.out_rows + 7) >> 3;
+    long long waves = (long long)tiles_x8 * rows8;
+    int cx = -1, cy = -1;
+    if (sc.kind == SCHED_RINGS) {
+        cx = min(max(sc.center_x >> 3, 0), tiles_x8 - 1);
+        cy = min(max(sc.center_y >> 3, 0), rows8 - 1);
+        const int R = max(max(cx, tiles_x8 - 1 - cx), max(cy, rows8 - 1 - cy));
+        waves = (2ll * R + 1) * (2ll * R + 1);
+    }
+    const dim3 grid((unsigned)((waves + 3) / 4)), block(kThreads);
+    if (shadow && early) hipLaunchKernelGGL((march_proc<true, true>), grid, block, 0, s, a, cx, cy);
+    else if (shadow) hipLaunchKernelGGL((march_proc<true, false>), grid, block, 0, s, a, cx, cy);
+    else if (early) hipLaunchKernelGGL((march_proc<false, true>), grid, block, 0, s, a, cx, cy);
+    else hipLaunchKernelGGL((march_proc<false, false>), grid, block, 0, s, a, cx, cy);
     return hipGetLastError();
 }
 
