@@ -12,6 +12,10 @@ Fixtures:
   config1_256x256x32.png   the same frame as RGBA8 UNORM (for viewing)
   volume16_literal.npy     16^3 RGBA8 volume of the TestMain.cpp:43-92 recipe
   noise_kat.json           noise values at fixed points, per generator
+  config2_crop64.npy       grey channel (float32) of a 64x64 crop of BASELINE
+                           config 2 (procedural cloud, 1920x1080x128): rows
+                           512-575 (band 8 of 64-row bands), cols 928-991
+  config3_crop64.npy       the same crop of config 3 (+ 8 shadow steps)
 """
 import json
 import os
@@ -49,6 +53,27 @@ def write_png(path, rgba):
         f.write(png)
 
 
+CROP_BAND = dict(band_rows=64, band_stride=1000, band_first=8)   # rows 512..575 only
+CROP_COLS = (928, 992)
+
+
+def procedural(shadow_steps):
+    """vr_procedural_defaults (include/vr.h) with enabled = 1."""
+    p = oracle.Procedural()
+    p.enabled, p.grid_scale, p.octaves, p.freq0, p.lacunarity, p.gain = 1, 128.0, 4, 0.19, 2.0, 0.5
+    p.seed_fbm, p.worley_freq, p.seed_worley, p.shadow_steps = 3, 0.03, 2, shadow_steps
+    n = (1.0 + 1.0 + 4.0) ** 0.5
+    p.sun_dir[:] = [float(np.float32(1.0 / n)), float(np.float32(1.0 / n)), float(np.float32(2.0 / n))]
+    return p
+
+
+def procedural_crop(shadow_steps):
+    obj, glob = oracle.reference_shader_data(1280.0 / 720.0)
+    img, _ = oracle.render_procedural(oracle.procedural_from(procedural(shadow_steps)), obj, glob, oracle.march(128),
+                                      1920, 1080, oracle.FMT_RGBA32F, **CROP_BAND)
+    return img[:, CROP_COLS[0]:CROP_COLS[1], 0].astype(np.float32)
+
+
 NOISE_POINTS = [(0.0, 0.0, 0.0), (0.5, 0.25, 0.125), (1.3, -2.7, 5.9), (12.34, 56.78, -9.1),
                 (-100.5, 33.3, 0.001), (127.0 * 0.19, 3.0 * 0.19, 64.0 * 0.19), (1e3, -1e3, 0.5)]
 
@@ -67,6 +92,8 @@ def main():
         kat[name] = {str(seed): [float(np.float32(f(seed, *p))) for p in NOISE_POINTS] for seed in (1, 2, 3, 1337)}
     with open(os.path.join(HERE, "noise_kat.json"), "w") as fh:
         json.dump(kat, fh, indent=1)
+    np.save(os.path.join(HERE, "config2_crop64.npy"), procedural_crop(0))
+    np.save(os.path.join(HERE, "config3_crop64.npy"), procedural_crop(8))
     print("wrote fixtures; config-1 executed steps", steps)
 
 

@@ -452,3 +452,23 @@ def test_ring_schedule_off_centre(r, oracle, vol128, t, layout):
     finally:
         r.set_option("schedule", -1)
         r.set_layout_preference(0)
+
+
+@pytest.mark.parametrize("shadow,name", [(0, "config2_crop64"), (8, "config3_crop64")])
+def test_procedural_matches_golden_crops(r, shadow, name):
+    """The HIP path against the committed config-2/3 crops (tests/golden)."""
+    import os
+    import sys
+    golden = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    sys.path.insert(0, golden)
+    from make_golden import CROP_BAND, CROP_COLS
+    ref = np.load(os.path.join(golden, name + ".npy"))
+    osd, gsd = vr.reference_shader_data(1280.0 / 720.0)
+    r.set_shader_data(osd, gsd)
+    r.set_march(vr.march_defaults())
+    r.set_procedural(shadow_steps=shadow)
+    try:
+        img = r.render(1920, 1080, vr.FMT_RGBA32F, **CROP_BAND).cpu().numpy()
+    finally:
+        r.set_procedural(enabled=0)
+    assert np.array_equal(img[:, CROP_COLS[0]:CROP_COLS[1], 0], ref)

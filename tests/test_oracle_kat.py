@@ -180,3 +180,33 @@ def test_golden_config1_frame(oracle):
     img, steps = oracle.render(perlin_cube_volume(), obj, glob, oracle.march(32), 256, 256, oracle.FMT_RGBA32F)
     assert np.array_equal(img[..., 0], ref)
     assert steps == json.load(open(os.path.join(GOLDEN, "noise_kat.json")))["config1_steps"]
+
+
+@pytest.mark.parametrize("shadow,name", [(0, "config2_crop64"), (8, "config3_crop64")])
+def test_golden_procedural_crops(oracle, shadow, name):
+    """BASELINE configs 2/3 (build-defined medium): the oracle's 64x64 crop is
+    unchanged (tests/golden/make_golden.py)."""
+    import sys
+    sys.path.insert(0, GOLDEN)
+    from make_golden import procedural_crop
+    assert np.array_equal(procedural_crop(shadow), np.load(os.path.join(GOLDEN, name + ".npy")))
+
+
+def test_procedural_density_known_answers(oracle):
+    """Density KATs: fbm of one octave at frequency 1 vanishes on the Perlin
+    lattice (q = P * grid_scale integer), the density is never negative, and
+    scale multiplies it."""
+    L = oracle.lib()
+    p = oracle.Procedural()
+    p.enabled, p.grid_scale, p.octaves, p.freq0, p.lacunarity, p.gain = 1, 128.0, 1, 1.0, 2.0, 0.5
+    p.seed_fbm, p.worley_freq, p.seed_worley = 3, 0.03, 2
+    for k in [(0, 0, 0), (5, 17, 100), (127, 1, 64)]:
+        P = [c / 128.0 for c in k]
+        assert L.vro_procedural_density(p, 0.2, *P) == 0.0
+    p.octaves, p.freq0 = 4, 0.19
+    rng = np.random.default_rng(3)
+    vals = [L.vro_procedural_density(p, 0.2, *map(float, rng.random(3))) for _ in range(2000)]
+    assert min(vals) >= 0.0 and max(vals) > 0.0
+    P = (0.3, 0.6, 0.45)
+    d1, d2 = L.vro_procedural_density(p, 0.2, *P), L.vro_procedural_density(p, 0.4, *P)
+    assert d2 == pytest.approx(2.0 * d1, rel=1e-6)
