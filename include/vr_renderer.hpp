@@ -69,6 +69,9 @@ public:
         Flush();
     }
     void SetMarch(const vr_march_params& m) { Check(vr_set_march(ctx_, &m), "vr_set_march"); }
+    // BASELINE configs 2/3: the procedural medium replaces the volume (enabled = 0 restores it)
+    void SetProcedural(const vr_procedural& p) { Check(vr_set_procedural(ctx_, &p), "vr_set_procedural"); }
+    void SetOption(const char* name, int value) { Check(vr_set_option(ctx_, name, value), "vr_set_option"); }
 
     // Render the whole frame (or a band set) into a device buffer.
     void EnqueueRenderPass(const Rect2D& rect, vr_format fmt, void* d_pixels, void* stream = nullptr,

@@ -8,6 +8,7 @@
 //   --width W --height H --steps S --size N --frames F
 //   --phi DEG --theta DEG --spin DEG_PER_FRAME   (the A/D keys, :177-180)
 //   --format unorm|srgb  --out frame.png
+//   --procedural 0|1 --shadow K   (BASELINE configs 2/3: in-kernel Perlin-Worley medium)
 // and it prints one timing line (hipEvent per frame, median).
 #include <hip/hip_runtime.h>
 
@@ -34,6 +35,7 @@ int main(int argc, char** argv)
 {
     int width = 1280, height = 720, steps = 128, size = 128, frames = 10;
     float phi = 0.f, theta = 0.f, spin = 0.f;
+    int procedural = 0, shadow = 0;
     std::string out = "frame.png", fmt = "unorm";
     for (int i = 1; i + 1 < argc; i += 2) {
         const std::string k = argv[i], v = argv[i + 1];
@@ -47,6 +49,8 @@ int main(int argc, char** argv)
         else if (k == "--spin") spin = (float)std::atof(v.c_str());
         else if (k == "--format") fmt = v;
         else if (k == "--out") out = v;
+        else if (k == "--procedural") procedural = std::atoi(v.c_str());
+        else if (k == "--shadow") shadow = std::atoi(v.c_str());
         else {
             std::fprintf(stderr, "unknown option %s\n", k.c_str());
             return 1;
@@ -59,7 +63,15 @@ int main(int argc, char** argv)
         vr_volume_recipe_defaults(&recipe);
         recipe.size = size;
         for (int k = 0; k < 4; ++k) recipe.freq[k] *= 128.0f / (float)size;  // same field at any N
-        renderer.GenerateVolume(recipe);
+        if (procedural) {
+            vr_procedural p;
+            vr_procedural_defaults(&p);
+            p.enabled = 1;
+            p.shadow_steps = shadow;
+            renderer.SetProcedural(p);
+        } else {
+            renderer.GenerateVolume(recipe);
+        }
         vr_march_params m;
         vr_march_defaults(&m);
         m.max_steps = steps;
