@@ -98,43 +98,8 @@ struct FastCtx {
     const unsigned* tz;
 };
 
-// One trilinear tap of one channel from a fast layout, at padded texel
-// coordinate g (floor(g) = base texel + 1, fract(g) = weight).  Loads go
-// through a range-checked buffer descriptor: an offset outside the plane
-// reads 0 instead of faulting.
-template <int LAYOUT>
-__device__ __forceinline__ float tap_fast(const FastCtx& f, int ch, float gx, float gy, float gz)
-{
-    const float wx = fract_(gx), wy = fract_(gy), wz = fract_(gz);
-    const unsigned off = f.tx[cvt_flr(gx)] + f.ty[cvt_flr(gy)] + f.tz[cvt_flr(gz)];
-    if constexpr (LAYOUT == LAYOUT_CORNER8) {
-        const unsigned q0 = __builtin_amdgcn_raw_buffer_load_b32(f.rsrc[ch], off, 0, 0);
-        const unsigned q1 = __builtin_amdgcn_raw_buffer_load_b32(f.rsrc[ch], off + 4, 0, 0);
-        // q0 = c000 c100 c010 c110, q1 = c001 c101 c011 c111
-        return blend(f2{ubyte<0>(q0), ubyte<0>(q1)}, f2{ubyte<1>(q0), ubyte<1>(q1)},
-                     f2{ubyte<2>(q0), ubyte<2>(q1)}, f2{ubyte<3>(q0), ubyte<3>(q1)}, wx, wy, wz);
-    } else if constexpr (LAYOUT == LAYOUT_BRICK5) {
-        // R = 5: the two rows of a z-slice sit 5 bytes apart, so one 8-byte
-        // load at `off` covers c000 c100 . . . c010 c110 and one at off+25
-        // covers the z1 slice.  Two loads per tap; they never leave the
-        // brick's 128-B line (bytes <= 125).
-        const uint2 z0 = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(f.rsrc[ch], off, 0, 0));
-        const uint2 z1 = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(f.rsrc[ch], off + 25, 0, 0));
-        return blend(f2{ubyte<0>(z0.x), ubyte<0>(z1.x)}, f2{ubyte<1>(z0.x), ubyte<1>(z1.x)},
-                     f2{ubyte<1>(z0.y), ubyte<1>(z1.y)}, f2{ubyte<2>(z0.y), ubyte<2>(z1.y)}, wx, wy, wz);
-    } else {
-        constexpr int R = LAYOUT == LAYOUT_BRICK8 ? 8 : 16;
-        const unsigned v00 = __builtin_amdgcn_raw_buffer_load_b16(f.rsrc[ch], off, 0, 0);
-        const unsigned v10 = __builtin_amdgcn_raw_buffer_load_b16(f.rsrc[ch], off + R, 0, 0);
-        const unsigned v01 = __builtin_amdgcn_raw_buffer_load_b16(f.rsrc[ch], off + R * R, 0, 0);
-        const unsigned v11 = __builtin_amdgcn_raw_buffer_load_b16(f.rsrc[ch], off + R * R + R, 0, 0);
-        return blend(f2{ubyte<0>(v00), ubyte<0>(v01)}, f2{ubyte<1>(v00), ubyte<1>(v01)},
-                     f2{ubyte<0>(v10), ubyte<0>(v11)}, f2{ubyte<1>(v10), ubyte<1>(v11)}, wx, wy, wz);
-    }
-}
-
-// The same tap split in two: fetch (issue the loads, keep the weights) and
-// blend.  The pipelined march issues step i+1's fetches before blending
+// A fast-layout tap in two parts: fetch (issue the loads, keep the weights)
+// and blend.  The pipelined march issues step i+1's fetches before blending
 // step i, so each wave keeps two steps of loads in flight.
 struct TapRaw {
     unsigned q0, q1, q2, q3;
@@ -150,12 +115,35 @@ __device__ __forceinline__ TapRaw tap_fetch(const FastCtx& f, int ch, float gx, 
         r.q0 = __builtin_amdgcn_raw_buffer_load_b32(f.rsrc[ch], off, 0, 0);
         r.q1 = __builtin_amdgcn_raw_buffer_load_b32(f.rsrc[ch], off + 4, 0, 0);
     } else if constexpr (LAYOUT == LAYOUT_BRICK5) {
-        // R = 5: two unaligned 8-byte loads per tap, one per z-slice (see
-        // tap_fast).  Four narrow row loads (u16 or u32) were measured 20 %
-        // slower at 512^3: more load instructions cost more L1 lookups.
-        const uint2 z0 = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(f.rsrc[ch], off, 0, 0));
-        const uint2 z1 = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(f.rsrc[ch], off + 25, 0, 0));
-        r.q0 = z0.x; r.q1 = z0.y; r.q2 = z1.x; r.q3 = z1.y;
+        // R = 5: one load per z-slice, bytes off..off+6 (c000 c100 . . . c010
+        // c110) and the same 25 bytes on.  Each is a dword-ALIGNED 12-byte
+        // load from off & ~3 and two v_alignbyte_b32 that shift the slice
+        // down by off & 3: an 8-byte load at a byte-granular offset costs
+        // the L1 twice the tag lookups of a dword-aligned one, and a 12-byte
+        // one costs the same as 8 bytes (tools/tcp_calib.hip, DESIGN.md
+        // sec. 5.1): 0.264 -> 0.225 ms at 512^3, 0.195 -> 0.122 ms at 256^3.
+        // Narrow row loads (4 x u16 or u32 per tap) were 20 % slower than the
+        // byte-offset 8-byte loads: more instructions, more lookups.
+        const unsigned o1 = off + 25;
+        const auto s0 = __builtin_amdgcn_raw_buffer_load_b96(f.rsrc[ch], off & ~3u, 0, 0);
+        const auto s1 = __builtin_amdgcn_raw_buffer_load_b96(f.rsrc[ch], o1 & ~3u, 0, 0);
+        r.q0 = __builtin_amdgcn_alignbyte(s0[1], s0[0], off);
+        r.q1 = __builtin_amdgcn_alignbyte(s0[2], s0[1], off);
+        r.q2 = __builtin_amdgcn_alignbyte(s1[1], s1[0], o1);
+        r.q3 = __builtin_amdgcn_alignbyte(s1[2], s1[1], o1);
+    } else if constexpr (LAYOUT == LAYOUT_BRICK8) {
+        // R = 8: rows y and y+1 of a slice are 8 bytes apart, so one
+        // dword-aligned 16-byte load from off & ~3 holds both (bytes off,
+        // off+1, off+8, off+9); the z+1 slice is 64 bytes on.  Two loads per
+        // tap instead of four byte-offset u16 loads: 0.271 -> 0.235 ms at
+        // 512^3, 0.185 -> 0.119 ms at 128^3.
+        const unsigned o1 = off + 64;
+        const auto s0 = __builtin_amdgcn_raw_buffer_load_b128(f.rsrc[ch], off & ~3u, 0, 0);
+        const auto s1 = __builtin_amdgcn_raw_buffer_load_b128(f.rsrc[ch], o1 & ~3u, 0, 0);
+        r.q0 = __builtin_amdgcn_alignbyte(s0[1], s0[0], off);   // c000 c100 in bytes 0-1
+        r.q1 = __builtin_amdgcn_alignbyte(s0[3], s0[2], off);   // c010 c110
+        r.q2 = __builtin_amdgcn_alignbyte(s1[1], s1[0], o1);    // c001 c101
+        r.q3 = __builtin_amdgcn_alignbyte(s1[3], s1[2], o1);    // c011 c111
     } else {
         constexpr int R = LAYOUT == LAYOUT_BRICK8 ? 8 : 16;
         r.q0 = __builtin_amdgcn_raw_buffer_load_b16(f.rsrc[ch], off, 0, 0);
@@ -179,6 +167,16 @@ __device__ __forceinline__ float tap_blend(const TapRaw& r)
                      f2{ubyte<0>(r.q1), ubyte<0>(r.q3)}, f2{ubyte<1>(r.q1), ubyte<1>(r.q3)}, r.wx, r.wy, r.wz);
     }
 }
+// One trilinear tap of one channel from a fast layout, at padded texel
+// coordinate g (floor(g) = base texel + 1, fract(g) = weight).  Loads go
+// through a range-checked buffer descriptor: an offset outside the plane
+// reads 0 instead of faulting.
+template <int LAYOUT>
+__device__ __forceinline__ float tap_fast(const FastCtx& f, int ch, float gx, float gy, float gz)
+{
+    return tap_blend<LAYOUT>(tap_fetch<LAYOUT>(f, ch, gx, gy, gz));
+}
+
 template <int LAYOUT>
 __device__ __forceinline__ TapRaw tap_fetch_at(const MarchArgs& a, const FastCtx& f, int t, f2 pxy, float pz)
 {
