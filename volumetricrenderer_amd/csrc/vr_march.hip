@@ -297,8 +297,9 @@ __device__ __forceinline__ void store_pixel(const MarchArgs& a, int x, int orow,
 // epilogue (:76-80) and the store.  Returns the executed steps.
 // The brick layouts run software-pipelined: step i+1's loads are issued
 // before step i is blended, so a wave has two steps of gathers in flight.
-// This costs VGPRs (84-107, 4-5 waves/SIMD) and is still faster: at 512^3
-// brick5 0.334 -> 0.280 ms, brick8 unchanged.  CORNER8 (the cache-resident
+// This costs VGPRs (67-73, 6-7 waves/SIMD) and is still faster: at 512^3
+// brick5 0.334 -> 0.280 ms (before the aligned loads), brick8 unchanged.
+// Fetching two steps ahead spilled to scratch and was 2.6x slower.  CORNER8 (the cache-resident
 // layout, one load per tap) is not: 0.51 -> 0.56 ms at 3840x2160x256.
 // Forcing 6 or 8 waves/SIMD (amdgpu_waves_per_eu) was slower in every case,
 // with or without pipelining.
