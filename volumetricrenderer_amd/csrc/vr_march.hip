@@ -512,13 +512,24 @@ __device__ __forceinline__ unsigned march_pixel_proc_compact(const MarchArgs& a,
     return r.n > 0 ? (unsigned)i : 0u;
 }
 
-// Lane -> pixel inside an 8x8 wave tile: row-major, so each 16-lane TA
-// group (tools/tcp_calib.hip) is an 8x2 strip.  Compact 4x4 groups were
-// measured and are no better for brick5 and 15 % slower for brick8: brick8's
-// 128-B lines are z-slabs, and a screen-horizontal strip stays inside one
-// (DESIGN.md sec. 5.1).
-__device__ __forceinline__ int lane_x(int lane) { return lane & 7; }
-__device__ __forceinline__ int lane_y(int lane) { return lane >> 3; }
+// Lane -> pixel inside an 8x8 wave tile.  Default row-major, so each 16-lane
+// TA group of a narrow load (tools/tcp_calib.hip) is an 8x2 strip; compact
+// 4x4 groups were measured no better for brick5 and 15 % slower for brick8's
+// u16 loads.  BRICK5's 12-byte loads are looked up per 4 lanes, and there 2x2
+// pixel quads (4x4 of them per tile) are 2.6 % faster at 512^3 than 4x1 rows
+// (neutral for the other layouts, 20 % slower for planar).
+template <int LAYOUT = 0>
+__device__ __forceinline__ int lane_x(int lane)
+{
+    if constexpr (LAYOUT == LAYOUT_BRICK5) return ((lane >> 2) & 3) * 2 + (lane & 1);
+    else return lane & 7;
+}
+template <int LAYOUT = 0>
+__device__ __forceinline__ int lane_y(int lane)
+{
+    if constexpr (LAYOUT == LAYOUT_BRICK5) return (lane >> 4) * 2 + ((lane >> 1) & 1);
+    else return lane >> 3;
+}
 
 __device__ __forceinline__ void add_steps(const MarchArgs& a, unsigned long long cnt)
 {
@@ -565,8 +576,8 @@ __global__ __launch_bounds__(kThreads) void march_grid(const MarchArgs a)
     if (ty >= a.tiles_y) return;   // whole workgroup: uniform, before the barrier
     const FastCtx f = fast_prologue<LAYOUT>(a, lds);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int x = tx * kTile + (wave & 1) * 8 + lane_x(lane);
-    const int orow = ty * kTile + (wave >> 1) * 8 + lane_y(lane);
+    const int x = tx * kTile + (wave & 1) * 8 + lane_x<LAYOUT>(lane);
+    const int orow = ty * kTile + (wave >> 1) * 8 + lane_y<LAYOUT>(lane);
     const unsigned steps = march_pixel<LAYOUT, WRAP, EARLY>(a, f, x, orow);
     if (a.step_counter) add_steps(a, steps);
 }
@@ -586,7 +597,7 @@ __global__ __launch_bounds__(kThreads) void march_strided(const MarchArgs a, int
     unsigned long long steps = 0;
     for (int t = g; t < ntiles; t += nw) {
         const int ty = t / tiles_x8, tx = t - ty * tiles_x8;
-        steps += march_pixel<LAYOUT, WRAP, EARLY>(a, f, tx * 8 + lane_x(lane), ty * 8 + lane_y(lane));
+        steps += march_pixel<LAYOUT, WRAP, EARLY>(a, f, tx * 8 + lane_x<LAYOUT>(lane), ty * 8 + lane_y<LAYOUT>(lane));
     }
     if (a.step_counter) add_steps(a, steps);
 }
@@ -620,7 +631,7 @@ __global__ __launch_bounds__(kThreads) void march_rings(const MarchArgs a, int c
     ring_tile(k, cx, cy, &tx, &ty);
     unsigned long long steps = 0;
     if (tx >= 0 && tx < tiles_x8 && ty >= 0 && ty < rows8)
-        steps = march_pixel<LAYOUT, WRAP, EARLY>(a, f, tx * 8 + lane_x(lane), ty * 8 + lane_y(lane));
+        steps = march_pixel<LAYOUT, WRAP, EARLY>(a, f, tx * 8 + lane_x<LAYOUT>(lane), ty * 8 + lane_y<LAYOUT>(lane));
     if (a.step_counter) add_steps(a, steps);
 }
 
@@ -641,7 +652,7 @@ __global__ __launch_bounds__(kThreads) void march_xcdrows(const MarchArgs a)
     const FastCtx f = fast_prologue<LAYOUT>(a, lds);
     const int lane = threadIdx.x & 63, tx = gx * 4 + (threadIdx.x >> 6);
     unsigned long long steps = 0;
-    if (tx < tiles_x8) steps = march_pixel<LAYOUT, WRAP, EARLY>(a, f, tx * 8 + lane_x(lane), ty * 8 + lane_y(lane));
+    if (tx < tiles_x8) steps = march_pixel<LAYOUT, WRAP, EARLY>(a, f, tx * 8 + lane_x<LAYOUT>(lane), ty * 8 + lane_y<LAYOUT>(lane));
     if (a.step_counter) add_steps(a, steps);
 }
 
@@ -669,7 +680,7 @@ __global__ __launch_bounds__(kThreads) void march_queue(const MarchArgs a, int* 
         const int m = k / per_pair, rem = k - m * per_pair;
         const int row8 = 2 * (q + 8 * m) + (rem & 1), tx = rem >> 1;
         if (row8 >= rows8) continue;
-        steps += march_pixel<LAYOUT, WRAP, EARLY>(a, f, tx * 8 + lane_x(lane), row8 * 8 + lane_y(lane));
+        steps += march_pixel<LAYOUT, WRAP, EARLY>(a, f, tx * 8 + lane_x<LAYOUT>(lane), row8 * 8 + lane_y<LAYOUT>(lane));
     }
     if (a.step_counter) add_steps(a, steps);
 }
