@@ -7,6 +7,7 @@
 // step replaces the EnqueueRenderPass + vkCmdDrawIndexed path of
 // TestMain.cpp:194-217.  No exception crosses the ABI; errors go through
 // vr_last_error().
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -275,6 +276,8 @@ vr_status vr_procedural_defaults(vr_procedural* p)
     return VR_OK;
 }
 
+constexpr long long kMaxWorleyTableBytes = 32 << 10;   // LDS per workgroup for the cell table
+
 vr_status vr_set_procedural(void* ctx, const vr_procedural* p)
 {
     if (!ctx || !p) return fail(VR_ERR_INVALID, "vr_set_procedural: null argument");
@@ -286,6 +289,10 @@ vr_status vr_set_procedural(void* ctx, const vr_procedural* p)
                                    (double)p->sun_dir[2] * p->sun_dir[2]);
         if (p->shadow_steps > 0 && !(l > 0.0)) return fail(VR_ERR_INVALID, "vr_set_procedural: zero sun_dir");
         if (p->reserved) return fail(VR_ERR_INVALID, "vr_set_procedural: reserved must be 0");
+        if (!std::isfinite(p->grid_scale) || !std::isfinite(p->freq0) || !std::isfinite(p->lacunarity) ||
+            !std::isfinite(p->gain) || !std::isfinite(p->worley_freq) || !std::isfinite(p->sun_dir[0]) ||
+            !std::isfinite(p->sun_dir[1]) || !std::isfinite(p->sun_dir[2]))
+            return fail(VR_ERR_INVALID, "vr_set_procedural: parameters must be finite");
     }
     Ctx* c = as_ctx(ctx);
     c->proc = *p;
@@ -685,6 +692,14 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
         for (int ax = 0; ax < 3; ++ax) q.lstep[ax] = (a.step_size * c->proc.sun_dir[ax]) / a.box_range[ax];
         q.od = a.step_size * m.density;
         q.count_evals = c->count;
+        // Worley cell table (LDS): box points P in [0,1]^3 give cellular
+        // coordinates in [0, G] per axis, G = grid_scale * worley_freq; the
+        // 3x3x3 neighbourhood of rint() of those, with 2 cells of margin.
+        const double G = (double)q.grid_scale * (double)q.worley_freq;
+        const int lo = (int)std::floor(std::min(0.0, G)) - 2, hi = (int)std::ceil(std::max(0.0, G)) + 2;
+        const int n = hi - lo + 1;
+        q.wt_lo = lo;
+        q.wt_n = (std::fabs(G) < 64.0 && (long long)n * n * n * 16 <= kMaxWorleyTableBytes) ? n : 0;
     }
     Plan pl{LAYOUT_PLANAR, WRAP_CLAMP, false};
     if (!c->proc.enabled) make_plan(c, &a, &pl);

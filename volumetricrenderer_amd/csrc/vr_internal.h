@@ -80,6 +80,7 @@ struct ProcParams {
     float lstep[3];   // (step_size * sun_dir) / box_range
     float od;         // step_size * density
     int count_evals;  // step_counter counts density evaluations (incl. shadow samples)
+    int wt_lo, wt_n;  // Worley cell table in LDS: cells [wt_lo, wt_lo + wt_n)^3; wt_n = 0: none
 };
 
 // Everything one launch of the march kernel needs.  Passed by value

@@ -369,7 +369,8 @@ __device__ __forceinline__ unsigned march_pixel(const MarchArgs& a, const FastCt
 
 // Procedural medium (BASELINE configs 2/3, build-defined; spec in
 // oracle/vr_oracle.h vro_procedural): fBm Perlin x (1 - Worley F1).
-__device__ __forceinline__ float proc_density(const ProcParams& p, float scale, float px, float py, float pz)
+__device__ __forceinline__ float proc_density(const ProcParams& p, const float4* wt, float scale, float px, float py,
+                                              float pz)
 {
     const float qx = px * p.grid_scale, qy = py * p.grid_scale, qz = pz * p.grid_scale;
     float f = p.freq0, amp = 1.0f, fbm = 0.0f;
@@ -379,7 +380,8 @@ __device__ __forceinline__ float proc_density(const ProcParams& p, float scale, 
         amp = amp * p.gain;
     }
     const float wf = p.worley_freq;
-    const float f1 = noise::cellular(p.seed_worley, qx * wf, qy * wf, qz * wf) + 1.0f;
+    const float f1 = (wt ? noise::cellular_table(wt, p.wt_lo, p.wt_n, qx * wf, qy * wf, qz * wf)
+                         : noise::cellular(p.seed_worley, qx * wf, qy * wf, qz * wf)) + 1.0f;
     return fmaxf(fbm * (1.0f - f1), 0.0f) * scale;
 }
 
@@ -396,7 +398,7 @@ __device__ __forceinline__ float proc_epilogue(const MarchArgs& a, float acc, fl
 }
 
 template <bool SHADOW, bool EARLY>
-__device__ __forceinline__ unsigned march_pixel_proc(const MarchArgs& a, int x, int orow)
+__device__ __forceinline__ unsigned march_pixel_proc(const MarchArgs& a, const float4* wt, int x, int orow)
 {
     const Ray r = setup_ray(a, x, orow);
     const ProcParams& p = a.proc;
@@ -405,14 +407,14 @@ __device__ __forceinline__ unsigned march_pixel_proc(const MarchArgs& a, int x, 
     int i = 0;
     unsigned evals = 0;   // shadow density evaluations
     for (; i < r.n; ++i) {
-        const float rho = proc_density(p, a.scale, P0, P1, P2);
+        const float rho = proc_density(p, wt, a.scale, P0, P1, P2);
         if constexpr (SHADOW) {
             if (rho > 0.0f) {
                 float q0 = P0, q1 = P1, q2 = P2, sl = 0.0f;
                 for (int j = 0; j < p.shadow_steps; ++j) {
                     q0 = q0 + p.lstep[0]; q1 = q1 + p.lstep[1]; q2 = q2 + p.lstep[2];
                     if (q0 >= 0.0f && q0 <= 1.0f && q1 >= 0.0f && q1 <= 1.0f && q2 >= 0.0f && q2 <= 1.0f) {
-                        sl = sl + proc_density(p, a.scale, q0, q1, q2);
+                        sl = sl + proc_density(p, wt, a.scale, q0, q1, q2);
                         ++evals;
                     }
                 }
@@ -440,14 +442,15 @@ __device__ __forceinline__ unsigned march_pixel_proc(const MarchArgs& a, int x, 
 // then sums its own S values in step order, so the arithmetic (and the
 // repeated-addition shadow positions) is exactly march_pixel_proc's.
 // Requires wave-uniform control flow: every lane of the wave calls it.
-constexpr int kMaxCompactShadow = 16;
+constexpr int kMaxCompactShadow = 8;
 struct ShadowLds {
     float p[64][3];                      // positions of the lanes that need shadow rays (compacted)
     float d[64 * kMaxCompactShadow];     // densities, [compact lane][shadow step]
 };
 
 template <bool EARLY>
-__device__ __forceinline__ unsigned march_pixel_proc_compact(const MarchArgs& a, int x, int orow, bool valid,
+__device__ __forceinline__ unsigned march_pixel_proc_compact(const MarchArgs& a, const float4* wt, int x, int orow,
+                                                             bool valid,
                                                              ShadowLds* sh, unsigned* shadow_evals)
 {
     Ray r{};
@@ -465,7 +468,7 @@ __device__ __forceinline__ unsigned march_pixel_proc_compact(const MarchArgs& a,
         act = act && i < r.n;
         if (__ballot(act) == 0) break;
         float rho = 0.0f;
-        if (act) rho = proc_density(p, a.scale, P0, P1, P2);
+        if (act) rho = proc_density(p, wt, a.scale, P0, P1, P2);
         const bool need = act && rho > 0.0f;
         const unsigned long long m = __ballot(need);
         if (m) {
@@ -482,7 +485,7 @@ __device__ __forceinline__ unsigned march_pixel_proc_compact(const MarchArgs& a,
                     for (int jj = 0; jj <= j; ++jj) { q0 = q0 + p.lstep[0]; q1 = q1 + p.lstep[1]; q2 = q2 + p.lstep[2]; }
                     float d = 0.0f;   // outside the box: contributes exactly +0
                     if (q0 >= 0.0f && q0 <= 1.0f && q1 >= 0.0f && q1 <= 1.0f && q2 >= 0.0f && q2 <= 1.0f) {
-                        d = proc_density(p, a.scale, q0, q1, q2);
+                        d = proc_density(p, wt, a.scale, q0, q1, q2);
                         ++evals;
                     }
                     sh->d[kk * S + j] = d;
@@ -687,9 +690,25 @@ __global__ __launch_bounds__(kThreads) void march_queue(const MarchArgs a, int* 
 
 // Procedural medium: one 8x8 tile per wave (compute-bound; no volume), in
 // row order (cx < 0) or in rings around tile (cx, cy) (see march_rings).
+// Worley cell table for the workgroup (dynamic LDS, wt_n^3 float4), built
+// before any wave may leave.  Returns null when the table is off (wt_n = 0).
+__device__ __forceinline__ const float4* worley_table(const ProcParams& p, float4* lds)
+{
+    if (p.wt_n <= 0) return nullptr;
+    const int n = p.wt_n, cells = n * n * n;
+    for (int i = threadIdx.x; i < cells; i += kThreads) {
+        const int ix = i % n, iy = (i / n) % n, iz = i / (n * n);
+        lds[i] = noise::cellular_cell(p.seed_worley, p.wt_lo + ix, p.wt_lo + iy, p.wt_lo + iz);
+    }
+    __syncthreads();
+    return lds;
+}
+
 template <bool SHADOW, bool EARLY>
 __global__ __launch_bounds__(kThreads) void march_proc(const MarchArgs a, int cx, int cy)
 {
+    extern __shared__ float4 wt_lds[];
+    const float4* wt = worley_table(a.proc, wt_lds);
     const int lane = threadIdx.x & 63;
     const int t = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
     const int tiles_x8 = (a.width + 7) >> 3, rows8 = (a.out_rows + 7) >> 3;
@@ -702,7 +721,7 @@ __global__ __launch_bounds__(kThreads) void march_proc(const MarchArgs a, int cx
         tx = t - ty * tiles_x8;
     }
     if (tx >= 0 && tx < tiles_x8 && ty >= 0 && ty < rows8) {
-        steps = march_pixel_proc<SHADOW, EARLY>(a, tx * 8 + lane_x(lane), ty * 8 + lane_y(lane));
+        steps = march_pixel_proc<SHADOW, EARLY>(a, wt, tx * 8 + lane_x(lane), ty * 8 + lane_y(lane));
     }
     if (a.step_counter) add_steps(a, steps);
 }
@@ -796,6 +815,8 @@ template <bool SHADOW, bool EARLY>
 __global__ __launch_bounds__(kThreads) void march_proc_sorted(const MarchArgs a, const unsigned* __restrict__ order,
                                                               const unsigned* __restrict__ total_ptr)
 {
+    extern __shared__ float4 wt_lds[];
+    const float4* wt = worley_table(a.proc, wt_lds);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const unsigned total = *total_ptr;
     const unsigned base = (blockIdx.x * (kThreads / 64) + wave) * 64u;
@@ -813,13 +834,13 @@ __global__ __launch_bounds__(kThreads) void march_proc_sorted(const MarchArgs a,
         __shared__ ShadowLds sh[kThreads / 64];
         if (a.proc.shadow_steps <= kMaxCompactShadow) {
             unsigned ev = 0;
-            steps = march_pixel_proc_compact<EARLY>(a, x, orow, valid, &sh[wave], &ev);
+            steps = march_pixel_proc_compact<EARLY>(a, wt, x, orow, valid, &sh[wave], &ev);
             if (a.proc.count_evals) steps += ev;
         } else {
-            steps = valid ? march_pixel_proc<true, EARLY>(a, x, orow) : 0u;
+            steps = valid ? march_pixel_proc<true, EARLY>(a, wt, x, orow) : 0u;
         }
     } else {
-        steps = valid ? march_pixel_proc<false, EARLY>(a, x, orow) : 0u;
+        steps = valid ? march_pixel_proc<false, EARLY>(a, wt, x, orow) : 0u;
     }
     if (a.step_counter) add_steps(a, steps);
 }
@@ -891,6 +912,7 @@ hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_bu
 {
     if (a.width <= 0 || a.out_rows <= 0) return hipSuccess;
     const bool shadow = a.proc.shadow_steps > 0;
+    const size_t wt_bytes = (size_t)a.proc.wt_n * a.proc.wt_n * a.proc.wt_n * sizeof(float4);
     if (sort_buf) {
         unsigned* hist = static_cast<unsigned*>(sort_buf);
         unsigned* cursor = hist + kKeyBins;            // kKeyBins + 1 entries
@@ -907,10 +929,10 @@ hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_bu
         // the scatter advanced cursor[k] to the end of key k; total stays at cursor[kKeyBins]
         const dim3 g4((unsigned)((pixels + kThreads - 1) / kThreads));
         const unsigned* total = cursor + kKeyBins;
-        if (shadow && early) hipLaunchKernelGGL((march_proc_sorted<true, true>), g4, dim3(kThreads), 0, s, a, order, total);
-        else if (shadow) hipLaunchKernelGGL((march_proc_sorted<true, false>), g4, dim3(kThreads), 0, s, a, order, total);
-        else if (early) hipLaunchKernelGGL((march_proc_sorted<false, true>), g4, dim3(kThreads), 0, s, a, order, total);
-        else hipLaunchKernelGGL((march_proc_sorted<false, false>), g4, dim3(kThreads), 0, s, a, order, total);
+        if (shadow && early) hipLaunchKernelGGL((march_proc_sorted<true, true>), g4, dim3(kThreads), wt_bytes, s, a, order, total);
+        else if (shadow) hipLaunchKernelGGL((march_proc_sorted<true, false>), g4, dim3(kThreads), wt_bytes, s, a, order, total);
+        else if (early) hipLaunchKernelGGL((march_proc_sorted<false, true>), g4, dim3(kThreads), wt_bytes, s, a, order, total);
+        else hipLaunchKernelGGL((march_proc_sorted<false, false>), g4, dim3(kThreads), wt_bytes, s, a, order, total);
         return hipGetLastError();
     }
     const int tiles_x8 = (a.width + 7) >> 3, rows8 = (a.out_rows + 7) >> 3;
@@ -923,10 +945,10 @@ hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_bu
         waves = (2ll * R + 1) * (2ll * R + 1);
     }
     const dim3 grid((unsigned)((waves + 3) / 4)), block(kThreads);
-    if (shadow && early) hipLaunchKernelGGL((march_proc<true, true>), grid, block, 0, s, a, cx, cy);
-    else if (shadow) hipLaunchKernelGGL((march_proc<true, false>), grid, block, 0, s, a, cx, cy);
-    else if (early) hipLaunchKernelGGL((march_proc<false, true>), grid, block, 0, s, a, cx, cy);
-    else hipLaunchKernelGGL((march_proc<false, false>), grid, block, 0, s, a, cx, cy);
+    if (shadow && early) hipLaunchKernelGGL((march_proc<true, true>), grid, block, wt_bytes, s, a, cx, cy);
+    else if (shadow) hipLaunchKernelGGL((march_proc<true, false>), grid, block, wt_bytes, s, a, cx, cy);
+    else if (early) hipLaunchKernelGGL((march_proc<false, true>), grid, block, wt_bytes, s, a, cx, cy);
+    else hipLaunchKernelGGL((march_proc<false, false>), grid, block, wt_bytes, s, a, cx, cy);
     return hipGetLastError();
 }
 

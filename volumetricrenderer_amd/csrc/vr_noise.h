@@ -159,5 +159,48 @@ __device__ inline float cellular(int32_t seed, float x, float y, float z)
     return d0 - 1.0f;
 }
 
+// Cellular F1 from a table of per-cell feature-point data (the LDS table of
+// the procedural march; vr_march.hip).  Entry (ix, iy, iz) - lo holds
+// {xd, yd, zd, inv} of cellular() for that integer cell, so each of the 27
+// cells costs one 16-byte LDS read and 7 VALU ops instead of the hash,
+// bit-field, sqrt and reciprocal.  The arithmetic per cell is cellular()'s,
+// op for op, and fminf is exact, so the result is bit-identical.  The caller
+// guarantees every cell rint(coord) - 1 .. + 1 lies in [lo, lo + n).
+__device__ inline float cellular_table(const float4* __restrict__ tab, int lo, int n, float x, float y, float z)
+{
+    const float xr = rintf(x), yr = rintf(y), zr = rintf(z);
+    const int ix = (int)xr - 1 - lo, iy = (int)yr - 1 - lo, iz = (int)zr - 1 - lo;
+    const float4* t0 = tab + (iz * n + iy) * n + ix;
+    float d0 = 3.402823466e+38f;
+#pragma unroll
+    for (int xi = -1; xi <= 1; ++xi) {
+        const float xcf = (xr + (float)xi) - x;
+#pragma unroll
+        for (int yi = -1; yi <= 1; ++yi) {
+            const float ycf = (yr + (float)yi) - y;
+#pragma unroll
+            for (int zi = -1; zi <= 1; ++zi) {
+                const float zcf = (zr + (float)zi) - z;
+                const float4 c = t0[((zi + 1) * n + (yi + 1)) * n + (xi + 1)];
+                const float xd = fmaf(c.x, c.w, xcf);
+                const float yd = fmaf(c.y, c.w, ycf);
+                const float zd = fmaf(c.z, c.w, zcf);
+                d0 = fminf(d0, fmaf(zd, zd, fmaf(yd, yd, xd * xd)));
+            }
+        }
+    }
+    return d0 - 1.0f;
+}
+
+// One table entry: cellular()'s feature-point data for integer cell (ix, iy, iz).
+__device__ inline float4 cellular_cell(int32_t seed, int ix, int iy, int iz)
+{
+    const int32_t h = hash_hb(seed, wmul(ix, kPX), wmul(iy, kPY), wmul(iz, kPZ));
+    const float xd = (float)(h & 0x3ff) - 511.5f;
+    const float yd = (float)((h >> 10) & 0x3ff) - 511.5f;
+    const float zd = (float)((h >> 20) & 0x3ff) - 511.5f;
+    return make_float4(xd, yd, zd, cell_inv(fmaf(zd, zd, fmaf(yd, yd, xd * xd))));
+}
+
 }  // namespace noise
 }  // namespace vr
