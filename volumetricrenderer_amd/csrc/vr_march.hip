@@ -369,6 +369,7 @@ __device__ __forceinline__ unsigned march_pixel(const MarchArgs& a, const FastCt
 
 // Procedural medium (BASELINE configs 2/3, build-defined; spec in
 // oracle/vr_oracle.h vro_procedural): fBm Perlin x (1 - Worley F1).
+template <bool TABLE>
 __device__ __forceinline__ float proc_density(const ProcParams& p, const float4* wt, float scale, float px, float py,
                                               float pz)
 {
@@ -380,8 +381,9 @@ __device__ __forceinline__ float proc_density(const ProcParams& p, const float4*
         amp = amp * p.gain;
     }
     const float wf = p.worley_freq;
-    const float f1 = (wt ? noise::cellular_table(wt, p.wt_lo, p.wt_n, qx * wf, qy * wf, qz * wf)
-                         : noise::cellular(p.seed_worley, qx * wf, qy * wf, qz * wf)) + 1.0f;
+    float f1;
+    if constexpr (TABLE) f1 = noise::cellular_table(wt, p.wt_lo, p.wt_n, qx * wf, qy * wf, qz * wf) + 1.0f;
+    else f1 = noise::cellular(p.seed_worley, qx * wf, qy * wf, qz * wf) + 1.0f;
     return fmaxf(fbm * (1.0f - f1), 0.0f) * scale;
 }
 
@@ -397,7 +399,7 @@ __device__ __forceinline__ float proc_epilogue(const MarchArgs& a, float acc, fl
     }
 }
 
-template <bool SHADOW, bool EARLY>
+template <bool SHADOW, bool EARLY, bool TABLE>
 __device__ __forceinline__ unsigned march_pixel_proc(const MarchArgs& a, const float4* wt, int x, int orow)
 {
     const Ray r = setup_ray(a, x, orow);
@@ -407,14 +409,14 @@ __device__ __forceinline__ unsigned march_pixel_proc(const MarchArgs& a, const f
     int i = 0;
     unsigned evals = 0;   // shadow density evaluations
     for (; i < r.n; ++i) {
-        const float rho = proc_density(p, wt, a.scale, P0, P1, P2);
+        const float rho = proc_density<TABLE>(p, wt, a.scale, P0, P1, P2);
         if constexpr (SHADOW) {
             if (rho > 0.0f) {
                 float q0 = P0, q1 = P1, q2 = P2, sl = 0.0f;
                 for (int j = 0; j < p.shadow_steps; ++j) {
                     q0 = q0 + p.lstep[0]; q1 = q1 + p.lstep[1]; q2 = q2 + p.lstep[2];
                     if (q0 >= 0.0f && q0 <= 1.0f && q1 >= 0.0f && q1 <= 1.0f && q2 >= 0.0f && q2 <= 1.0f) {
-                        sl = sl + proc_density(p, wt, a.scale, q0, q1, q2);
+                        sl = sl + proc_density<TABLE>(p, wt, a.scale, q0, q1, q2);
                         ++evals;
                     }
                 }
@@ -448,7 +450,7 @@ struct ShadowLds {
     float d[64 * kMaxCompactShadow];     // densities, [compact lane][shadow step]
 };
 
-template <bool EARLY>
+template <bool EARLY, bool TABLE>
 __device__ __forceinline__ unsigned march_pixel_proc_compact(const MarchArgs& a, const float4* wt, int x, int orow,
                                                              bool valid,
                                                              ShadowLds* sh, unsigned* shadow_evals)
@@ -468,7 +470,7 @@ __device__ __forceinline__ unsigned march_pixel_proc_compact(const MarchArgs& a,
         act = act && i < r.n;
         if (__ballot(act) == 0) break;
         float rho = 0.0f;
-        if (act) rho = proc_density(p, wt, a.scale, P0, P1, P2);
+        if (act) rho = proc_density<TABLE>(p, wt, a.scale, P0, P1, P2);
         const bool need = act && rho > 0.0f;
         const unsigned long long m = __ballot(need);
         if (m) {
@@ -485,7 +487,7 @@ __device__ __forceinline__ unsigned march_pixel_proc_compact(const MarchArgs& a,
                     for (int jj = 0; jj <= j; ++jj) { q0 = q0 + p.lstep[0]; q1 = q1 + p.lstep[1]; q2 = q2 + p.lstep[2]; }
                     float d = 0.0f;   // outside the box: contributes exactly +0
                     if (q0 >= 0.0f && q0 <= 1.0f && q1 >= 0.0f && q1 <= 1.0f && q2 >= 0.0f && q2 <= 1.0f) {
-                        d = proc_density(p, wt, a.scale, q0, q1, q2);
+                        d = proc_density<TABLE>(p, wt, a.scale, q0, q1, q2);
                         ++evals;
                     }
                     sh->d[kk * S + j] = d;
@@ -704,7 +706,7 @@ __device__ __forceinline__ const float4* worley_table(const ProcParams& p, float
     return lds;
 }
 
-template <bool SHADOW, bool EARLY>
+template <bool SHADOW, bool EARLY, bool TABLE>
 __global__ __launch_bounds__(kThreads) void march_proc(const MarchArgs a, int cx, int cy)
 {
     extern __shared__ float4 wt_lds[];
@@ -721,7 +723,7 @@ __global__ __launch_bounds__(kThreads) void march_proc(const MarchArgs a, int cx
         tx = t - ty * tiles_x8;
     }
     if (tx >= 0 && tx < tiles_x8 && ty >= 0 && ty < rows8) {
-        steps = march_pixel_proc<SHADOW, EARLY>(a, wt, tx * 8 + lane_x(lane), ty * 8 + lane_y(lane));
+        steps = march_pixel_proc<SHADOW, EARLY, TABLE>(a, wt, tx * 8 + lane_x(lane), ty * 8 + lane_y(lane));
     }
     if (a.step_counter) add_steps(a, steps);
 }
@@ -811,7 +813,7 @@ __global__ __launch_bounds__(256) void proc_scatter(const MarchArgs a, const uns
         if (key[it] >= 0) order[h[key[it]] + rank[it]] = packed[it];
 }
 
-template <bool SHADOW, bool EARLY>
+template <bool SHADOW, bool EARLY, bool TABLE>
 __global__ __launch_bounds__(kThreads) void march_proc_sorted(const MarchArgs a, const unsigned* __restrict__ order,
                                                               const unsigned* __restrict__ total_ptr)
 {
@@ -834,13 +836,13 @@ __global__ __launch_bounds__(kThreads) void march_proc_sorted(const MarchArgs a,
         __shared__ ShadowLds sh[kThreads / 64];
         if (a.proc.shadow_steps <= kMaxCompactShadow) {
             unsigned ev = 0;
-            steps = march_pixel_proc_compact<EARLY>(a, wt, x, orow, valid, &sh[wave], &ev);
+            steps = march_pixel_proc_compact<EARLY, TABLE>(a, wt, x, orow, valid, &sh[wave], &ev);
             if (a.proc.count_evals) steps += ev;
         } else {
-            steps = valid ? march_pixel_proc<true, EARLY>(a, wt, x, orow) : 0u;
+            steps = valid ? march_pixel_proc<true, EARLY, TABLE>(a, wt, x, orow) : 0u;
         }
     } else {
-        steps = valid ? march_pixel_proc<false, EARLY>(a, wt, x, orow) : 0u;
+        steps = valid ? march_pixel_proc<false, EARLY, TABLE>(a, wt, x, orow) : 0u;
     }
     if (a.step_counter) add_steps(a, steps);
 }
@@ -929,10 +931,19 @@ hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_bu
         // the scatter advanced cursor[k] to the end of key k; total stays at cursor[kKeyBins]
         const dim3 g4((unsigned)((pixels + kThreads - 1) / kThreads));
         const unsigned* total = cursor + kKeyBins;
-        if (shadow && early) hipLaunchKernelGGL((march_proc_sorted<true, true>), g4, dim3(kThreads), wt_bytes, s, a, order, total);
-        else if (shadow) hipLaunchKernelGGL((march_proc_sorted<true, false>), g4, dim3(kThreads), wt_bytes, s, a, order, total);
-        else if (early) hipLaunchKernelGGL((march_proc_sorted<false, true>), g4, dim3(kThreads), wt_bytes, s, a, order, total);
-        else hipLaunchKernelGGL((march_proc_sorted<false, false>), g4, dim3(kThreads), wt_bytes, s, a, order, total);
+        const int v = (shadow ? 4 : 0) | (early ? 2 : 0) | (wt_bytes ? 1 : 0);
+#define VR_PS(S, E, T) hipLaunchKernelGGL((march_proc_sorted<S, E, T>), g4, dim3(kThreads), wt_bytes, s, a, order, total)
+        switch (v) {
+        case 0: VR_PS(false, false, false); break;
+        case 1: VR_PS(false, false, true); break;
+        case 2: VR_PS(false, true, false); break;
+        case 3: VR_PS(false, true, true); break;
+        case 4: VR_PS(true, false, false); break;
+        case 5: VR_PS(true, false, true); break;
+        case 6: VR_PS(true, true, false); break;
+        default: VR_PS(true, true, true); break;
+        }
+#undef VR_PS
         return hipGetLastError();
     }
     const int tiles_x8 = (a.width + 7) >> 3, rows8 = (a.out_rows + 7) >> 3;
@@ -945,10 +956,19 @@ hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_bu
         waves = (2ll * R + 1) * (2ll * R + 1);
     }
     const dim3 grid((unsigned)((waves + 3) / 4)), block(kThreads);
-    if (shadow && early) hipLaunchKernelGGL((march_proc<true, true>), grid, block, wt_bytes, s, a, cx, cy);
-    else if (shadow) hipLaunchKernelGGL((march_proc<true, false>), grid, block, wt_bytes, s, a, cx, cy);
-    else if (early) hipLaunchKernelGGL((march_proc<false, true>), grid, block, wt_bytes, s, a, cx, cy);
-    else hipLaunchKernelGGL((march_proc<false, false>), grid, block, wt_bytes, s, a, cx, cy);
+    const int v = (shadow ? 4 : 0) | (early ? 2 : 0) | (wt_bytes ? 1 : 0);
+#define VR_PT(S, E, T) hipLaunchKernelGGL((march_proc<S, E, T>), grid, block, wt_bytes, s, a, cx, cy)
+    switch (v) {
+    case 0: VR_PT(false, false, false); break;
+    case 1: VR_PT(false, false, true); break;
+    case 2: VR_PT(false, true, false); break;
+    case 3: VR_PT(false, true, true); break;
+    case 4: VR_PT(true, false, false); break;
+    case 5: VR_PT(true, false, true); break;
+    case 6: VR_PT(true, true, false); break;
+    default: VR_PT(true, true, true); break;
+    }
+#undef VR_PT
     return hipGetLastError();
 }
 
