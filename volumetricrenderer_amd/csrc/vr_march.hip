@@ -376,7 +376,10 @@ __device__ __forceinline__ float proc_density(const ProcParams& p, const float4*
     const float qx = px * p.grid_scale, qy = py * p.grid_scale, qz = pz * p.grid_scale;
     float f = p.freq0, amp = 1.0f, fbm = 0.0f;
     for (int o = 0; o < p.octaves; ++o) {
-        fbm = fmaf(amp, noise::perlin(p.seed_fbm, qx * f, qy * f, qz * f), fbm);
+        float pn;
+        if constexpr (TABLE) pn = noise::perlin_gt(wt + p.wt_n * p.wt_n * p.wt_n, p.seed_fbm, qx * f, qy * f, qz * f);
+        else pn = noise::perlin(p.seed_fbm, qx * f, qy * f, qz * f);
+        fbm = fmaf(amp, pn, fbm);
         f = f * p.lacunarity;
         amp = amp * p.gain;
     }
@@ -692,8 +695,9 @@ __global__ __launch_bounds__(kThreads) void march_queue(const MarchArgs a, int* 
 
 // Procedural medium: one 8x8 tile per wave (compute-bound; no volume), in
 // row order (cx < 0) or in rings around tile (cx, cy) (see march_rings).
-// Worley cell table for the workgroup (dynamic LDS, wt_n^3 float4), built
-// before any wave may leave.  Returns null when the table is off (wt_n = 0).
+// Noise tables for the workgroup (dynamic LDS): the Worley cell table
+// (wt_n^3 float4) followed by the 16 Perlin gradient vectors, built before
+// any wave may leave.  Returns null when the tables are off (wt_n = 0).
 __device__ __forceinline__ const float4* worley_table(const ProcParams& p, float4* lds)
 {
     if (p.wt_n <= 0) return nullptr;
@@ -702,6 +706,7 @@ __device__ __forceinline__ const float4* worley_table(const ProcParams& p, float
         const int ix = i % n, iy = (i / n) % n, iz = i / (n * n);
         lds[i] = noise::cellular_cell(p.seed_worley, p.wt_lo + ix, p.wt_lo + iy, p.wt_lo + iz);
     }
+    if (threadIdx.x < 16) lds[cells + threadIdx.x] = noise::grad_entry(threadIdx.x);
     __syncthreads();
     return lds;
 }
@@ -914,7 +919,8 @@ hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_bu
 {
     if (a.width <= 0 || a.out_rows <= 0) return hipSuccess;
     const bool shadow = a.proc.shadow_steps > 0;
-    const size_t wt_bytes = (size_t)a.proc.wt_n * a.proc.wt_n * a.proc.wt_n * sizeof(float4);
+    const size_t wt_bytes =
+        a.proc.wt_n > 0 ? ((size_t)a.proc.wt_n * a.proc.wt_n * a.proc.wt_n + 16) * sizeof(float4) : 0;
     if (sort_buf) {
         unsigned* hist = static_cast<unsigned*>(sort_buf);
         unsigned* cursor = hist + kKeyBins;            // kKeyBins + 1 entries
