@@ -55,12 +55,16 @@ CONFIGS = {
 
 
 def flop_per_density(octaves: int) -> int:
-    """Algorithmic fp32 FLOP of one procedural density evaluation (FMA = 2;
-    add, sub, mul, min, max, floor, rint, sqrt, div = 1; integer hashing and
-    int<->float conversions not counted).  Per Perlin octave 67 (noise 60 +
-    3 coordinate scales + fbm FMA + 2 parameter updates), Worley F1 over 27
-    cells 676, the rest 11."""
-    return 67 * octaves + 676 + 11
+    """Algorithmic fp32 FLOP of one procedural density evaluation, counted on
+    the minimal per-sample form (FMA = 2; add, sub, mul, min, max, floor,
+    rint = 1; integer hashing, table reads and int<->float conversions not
+    counted).  Per Perlin octave 67: floor 3, fraction subs 6, quintic 3 x 7,
+    8 gradient dots x 1 (u + v), 7 lerps x 3, scale 1, coordinate scale 3,
+    fbm fma 2, parameter updates 2.  Worley F1 346: rint 3, per-axis cell
+    offsets 18, per cell 12 (3 fma + squared distance 5 + min) x 27, final 1;
+    the cell's feature-point normalisation (hash, sqrt, divide) is per cell,
+    not per sample, and is not counted.  The rest 11."""
+    return 67 * octaves + 346 + 11
 
 
 def cpu_baseline(volume_host, osd, gsd, march, width, height, budget_s=10.0, procedural=None):
