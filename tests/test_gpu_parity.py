@@ -120,8 +120,7 @@ def test_every_layout_bitexact(r, oracle, vol128, layout, name):
         r.set_layout_preference(0)
 
 
-@pytest.mark.parametrize("schedule,wps", [(0, 4), (1, 1), (1, 3), (1, 8), (2, 1), (2, 3), (2, 16), (3, 1), (4, 1),
-                                          (5, 1)])
+@pytest.mark.parametrize("schedule,wps", [(0, 4), (1, 1), (1, 3), (1, 8), (2, 1), (2, 3), (2, 16), (3, 1), (4, 1)])
 def test_schedules_bitexact(r, oracle, vol128, schedule, wps):
     sched0, tpw0 = r.get_option("schedule"), r.get_option("tiles_per_wave")
     r.set_option("schedule", schedule)
@@ -439,12 +438,12 @@ def translated_shader_data(W, H, t):
 
 
 @pytest.mark.parametrize("t", [(0.9, -0.4, 0.2), (1.8, -1.8, 0.0), (0.0, 0.0, 3.5)])
-@pytest.mark.parametrize("layout,schedule", [(2, 4), (5, 4), (2, 5)])
-def test_ring_schedule_off_centre(r, oracle, vol128, t, layout, schedule):
+@pytest.mark.parametrize("layout", [2, 5])
+def test_ring_schedule_off_centre(r, oracle, vol128, t, layout):
     W, H = 400, 240
     osd, gsd = translated_shader_data(W, H, t)
     r.set_layout_preference(layout)
-    r.set_option("schedule", schedule)
+    r.set_option("schedule", 4)
     try:
         for band in ({}, dict(band_rows=16, band_stride=2, band_first=1)):
             img, ref, c, s = render_both(r, oracle, vol128, W, H, osd, gsd, **band)

@@ -47,7 +47,7 @@ def main():
             r.set_option("tiles_per_wave", lay[2])
 
     def name(lay):
-        return f"{NAMES[lay[0]]}/{['static', 'queue', 'strided', 'xcdrows', 'rings', 'xcdrings'][lay[1]]}{lay[2] if lay[1] else ''}"
+        return f"{NAMES[lay[0]]}/{['static', 'queue', 'strided', 'xcdrows', 'rings'][lay[1]]}{lay[2] if lay[1] else ''}"
     res = {}
     with vr.Renderer(0) as r:
         osd, gsd = vr.reference_shader_data(W / H)

@@ -562,9 +562,9 @@ vr_status vr_set_option(void* p, const char* name, int value)
     const std::string n(name);
     if (n == "layout") return vr_set_layout_preference(p, value);
     if (n == "schedule") {
-        if (value < -1 || value > 5)
+        if (value < -1 || value > 4)
             return fail(VR_ERR_INVALID, "vr_set_option: schedule is -1 (auto), 0 (static), 1 (queue), "
-                                        "2 (strided), 3 (xcd rows), 4 (rings) or 5 (xcd-sector rings)");
+                                        "2 (strided), 3 (xcd rows) or 4 (rings)");
         c->schedule = value;
         return VR_OK;
     }
@@ -754,7 +754,7 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
     // auto schedule (measured): rings, longest rays first
     const int kind = c->schedule >= 0 ? c->schedule : SCHED_RINGS;
     Schedule sc{kind, 0, 0, c->tiles_per_wave, c->waves_per_simd, c->d_heads};
-    if (kind == SCHED_RINGS || kind == SCHED_XCDRINGS) box_centre_pixel(c, a, &sc.center_x, &sc.center_y);
+    if (kind == SCHED_RINGS) box_centre_pixel(c, a, &sc.center_x, &sc.center_y);
     HIP_TRY(launch_march(a, pl.layout, pl.wrap, pl.early, sc, static_cast<hipStream_t>(stream)));
     return VR_OK;
 }

@@ -111,9 +111,7 @@ struct MarchArgs {
 };
 
 // How the march kernel maps tiles to waves.
-enum ScheduleKind : int {
-    SCHED_STATIC = 0, SCHED_QUEUE = 1, SCHED_STRIDED = 2, SCHED_XCDROWS = 3, SCHED_RINGS = 4, SCHED_XCDRINGS = 5
-};
+enum ScheduleKind : int { SCHED_STATIC = 0, SCHED_QUEUE = 1, SCHED_STRIDED = 2, SCHED_XCDROWS = 3, SCHED_RINGS = 4 };
 struct Schedule {
     int kind;
     int center_x, center_y;   // rings: target pixel under the projected box centre

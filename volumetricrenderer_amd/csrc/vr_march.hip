@@ -643,35 +643,6 @@ __global__ __launch_bounds__(kThreads) void march_rings(const MarchArgs a, int c
     if (a.step_counter) add_steps(a, steps);
 }
 
-// XCD-sector rings: like march_rings, but XCD s (blockIdx % 8, speed-only)
-// takes the arc [s*r, (s+1)*r) of every ring r, so the tiles one L2 serves
-// are spatial neighbours; each XCD still walks its rings inside-out.
-template <int LAYOUT, int WRAP, bool EARLY>
-__global__ __launch_bounds__(kThreads) void march_xcdrings(const MarchArgs a, int cx, int cy)
-{
-    extern __shared__ __attribute__((aligned(16))) unsigned lds[];
-    const FastCtx f = fast_prologue<LAYOUT>(a, lds);
-    const int lane = threadIdx.x & 63;
-    const int s = blockIdx.x & 7;
-    int m = (int)(blockIdx.x >> 3) * (kThreads / 64) + (threadIdx.x >> 6);   // this XCD's tile sequence
-    const int tiles_x8 = (a.width + 7) >> 3, rows8 = (a.out_rows + 7) >> 3;
-    int tx = -1, ty = -1;
-    if (s == 0 && m == 0) {
-        tx = cx; ty = cy;
-    } else {
-        if (s == 0) --m;
-        int r = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)m)) * 0.5f);   // r(r-1)/2 <= m < r(r+1)/2
-        while (r * (r - 1) / 2 > m) --r;
-        while (r * (r + 1) / 2 <= m) ++r;
-        const int t = m - r * (r - 1) / 2;
-        ring_tile((2 * r - 1) * (2 * r - 1) + s * r + t, cx, cy, &tx, &ty);
-    }
-    unsigned long long steps = 0;
-    if (tx >= 0 && tx < tiles_x8 && ty >= 0 && ty < rows8)
-        steps = march_pixel<LAYOUT, WRAP, EARLY>(a, f, tx * 8 + lane_x<LAYOUT>(lane), ty * 8 + lane_y<LAYOUT>(lane));
-    if (a.step_counter) add_steps(a, steps);
-}
-
 // XCD-row schedule: one 8x8 tile per wave, 4 horizontally adjacent tiles per
 // workgroup.  8-px tile rows are dealt to XCDs round-robin: XCD x walks rows
 // x, x+8, ... (blockIdx % 8, speed-only).  Rows interleave, so the balance
@@ -907,18 +878,6 @@ hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStre
             hipLaunchKernelGGL((march_rings<L, W, true>), grid, block, lds, s, a, cx, cy);
         else
             hipLaunchKernelGGL((march_rings<L, W, false>), grid, block, lds, s, a, cx, cy);
-        return hipGetLastError();
-    }
-    if (sc.kind == SCHED_XCDRINGS) {
-        const int tiles_x8 = (a.width + 7) >> 3, rows8 = (a.out_rows + 7) >> 3;
-        const int cx = min(max(sc.center_x >> 3, 0), tiles_x8 - 1), cy = min(max(sc.center_y >> 3, 0), rows8 - 1);
-        const long long R = max(max(cx, tiles_x8 - 1 - cx), max(cy, rows8 - 1 - cy));
-        const long long per_xcd = R * (R + 1) / 2 + 1;
-        const dim3 grid((unsigned)(8 * ((per_xcd + 3) / 4)));
-        if (early)
-            hipLaunchKernelGGL((march_xcdrings<L, W, true>), grid, block, lds, s, a, cx, cy);
-        else
-            hipLaunchKernelGGL((march_xcdrings<L, W, false>), grid, block, lds, s, a, cx, cy);
         return hipGetLastError();
     }
     if (sc.kind == SCHED_XCDROWS) {
