@@ -29,26 +29,6 @@ __device__ __forceinline__ int32_t hash_hb(int32_t seed, int32_t x, int32_t y, i
 {
     return wmul(seed ^ x ^ y ^ z, 0x27d4eb2d);
 }
-// Gradient hashes through 24-bit multiplies.  grad() reads only bits 0-3 of
-// hash() = (v*C >> 15) ^ v*C, i.e. bits 0-18 of the product v*C, and bits
-// 0..k of a product depend only on bits 0..k of its factors.  So the lattice
-// products x*kPX (which enter v through XOR) and v*C may be formed from the
-// low 24 bits with v_mul_u32_u24 (full rate) instead of v_mul_lo_u32 (quarter
-// rate): every bit grad() uses is unchanged.
-__device__ __forceinline__ int32_t mul24(int32_t a, int32_t b)
-{
-    // inline asm: with only low result bits demanded, the optimizer drops a
-    // 24-bit mask and selects the quarter-rate v_mul_lo_u32 again
-    int32_t r;
-    asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-__device__ __forceinline__ int32_t hash_grad(int32_t seed, int32_t x, int32_t y, int32_t z)
-{
-    const int32_t h = mul24(seed ^ x ^ y ^ z, 0x27d4eb2d);
-    return (h >> 15) ^ h;   // bits 0-3 exact (bits 15-18 of h are exact)
-}
-
 __device__ __forceinline__ float grad(int32_t h, float fx, float fy, float fz)
 {
     const int32_t h13 = h & 13;
@@ -69,15 +49,15 @@ __device__ __forceinline__ float lerp(float a, float b, float t) { return fmaf(t
 __device__ inline float perlin(int32_t seed, float x, float y, float z)
 {
     const float xs = floorf(x), ys = floorf(y), zs = floorf(z);
-    const int32_t x0 = mul24((int32_t)xs, kPX), y0 = mul24((int32_t)ys, kPY), z0 = mul24((int32_t)zs, kPZ);
+    const int32_t x0 = wmul((int32_t)xs, kPX), y0 = wmul((int32_t)ys, kPY), z0 = wmul((int32_t)zs, kPZ);
     const int32_t x1 = wadd(x0, kPX), y1 = wadd(y0, kPY), z1 = wadd(z0, kPZ);
     const float xf0 = x - xs, yf0 = y - ys, zf0 = z - zs;
     const float xf1 = xf0 - 1.0f, yf1 = yf0 - 1.0f, zf1 = zf0 - 1.0f;
     const float u = quintic(xf0), v = quintic(yf0), w = quintic(zf0);
-    const float l00 = lerp(grad(hash_grad(seed, x0, y0, z0), xf0, yf0, zf0), grad(hash_grad(seed, x1, y0, z0), xf1, yf0, zf0), u);
-    const float l10 = lerp(grad(hash_grad(seed, x0, y1, z0), xf0, yf1, zf0), grad(hash_grad(seed, x1, y1, z0), xf1, yf1, zf0), u);
-    const float l01 = lerp(grad(hash_grad(seed, x0, y0, z1), xf0, yf0, zf1), grad(hash_grad(seed, x1, y0, z1), xf1, yf0, zf1), u);
-    const float l11 = lerp(grad(hash_grad(seed, x0, y1, z1), xf0, yf1, zf1), grad(hash_grad(seed, x1, y1, z1), xf1, yf1, zf1), u);
+    const float l00 = lerp(grad(hash(seed, x0, y0, z0), xf0, yf0, zf0), grad(hash(seed, x1, y0, z0), xf1, yf0, zf0), u);
+    const float l10 = lerp(grad(hash(seed, x0, y1, z0), xf0, yf1, zf0), grad(hash(seed, x1, y1, z0), xf1, yf1, zf0), u);
+    const float l01 = lerp(grad(hash(seed, x0, y0, z1), xf0, yf0, zf1), grad(hash(seed, x1, y0, z1), xf1, yf0, zf1), u);
+    const float l11 = lerp(grad(hash(seed, x0, y1, z1), xf0, yf1, zf1), grad(hash(seed, x1, y1, z1), xf1, yf1, zf1), u);
     return 0.964921414852142333984375f * lerp(lerp(l00, l10, v), lerp(l01, l11, v), w);
 }
 
