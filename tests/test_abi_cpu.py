@@ -78,3 +78,37 @@ def test_band_rows_packed():
             assert rows == [rows_for_rank(H, 16, n, k) for k in range(n)]
             assert sum(rows) >= H and sum(rows) - H < 16
     assert vr.band_rows_packed(1080, 0, 1, 0) == 1080
+
+
+def test_header_layouts_match_ctypes(tmp_path):
+    """Compile include/vr.h with gcc and compare every struct's size (and the
+    std140 MediaScroll offset) with the ctypes mirrors."""
+    import subprocess
+    from volumetricrenderer_amd import _lib
+    src = tmp_path / "sizes.c"
+    src.write_text(
+        '#include <stdio.h>\n#include <stddef.h>\n#include "vr.h"\n'
+        "int main(void){printf(\"%zu %zu %zu %zu %zu %zu %zu %zu\\n\","
+        "sizeof(vr_object_shader_data), sizeof(vr_global_shader_data),"
+        "offsetof(vr_global_shader_data, media_scroll), sizeof(vr_march_params),"
+        "sizeof(vr_target), sizeof(vr_volume_recipe), sizeof(vr_procedural), offsetof(vr_procedural, sun_dir));"
+        "return 0;}\n")
+    exe = tmp_path / "sizes"
+    subprocess.run(["gcc", "-std=c99", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = [int(v) for v in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
+    want = [ctypes.sizeof(_lib.ObjectShaderData), ctypes.sizeof(_lib.GlobalShaderData),
+            _lib.GlobalShaderData.media_scroll.offset, ctypes.sizeof(_lib.MarchParams), ctypes.sizeof(_lib.Target),
+            ctypes.sizeof(_lib.VolumeRecipe), ctypes.sizeof(_lib.Procedural), _lib.Procedural.sun_dir.offset]
+    assert got == want
+
+
+def test_procedural_defaults_and_oracle_mirror(oracle):
+    import volumetricrenderer_amd as vr
+    p = vr.procedural_defaults()
+    assert p.enabled == 1 and p.octaves == 4 and p.seed_fbm == 3 and p.seed_worley == 2 and p.shadow_steps == 0
+    np.testing.assert_allclose([p.grid_scale, p.freq0, p.lacunarity, p.gain, p.worley_freq],
+                               [128, .19, 2, .5, .03], rtol=1e-7)
+    np.testing.assert_allclose(list(p.sun_dir), np.array([1, 1, 2]) / np.sqrt(6), rtol=1e-7)
+    assert ctypes.sizeof(oracle.Procedural) == ctypes.sizeof(vr.Procedural)
+    q = oracle.procedural_from(p)
+    assert bytes(q) == bytes(p)   # already unit length: normalising again changes nothing
