@@ -631,20 +631,10 @@ template <int LAYOUT, int WRAP, bool EARLY>
 __global__ __launch_bounds__(kThreads) void march_rings(const MarchArgs a, int cx, int cy)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned lds[];
-    const int tiles_x8 = (a.width + 7) >> 3, rows8 = (a.out_rows + 7) >> 3;
-    // A workgroup whose 4 ring positions are all off the target leaves before
-    // building its LDS tables (block-uniform, so before any barrier).  At
-    // 16:9 about 45 % of the square rings' positions are off-screen.
-    bool any = false;
-    for (int w = 0; w < kThreads / 64; ++w) {
-        int bx, by;
-        ring_tile(blockIdx.x * (kThreads / 64) + w, cx, cy, &bx, &by);
-        any |= bx >= 0 && bx < tiles_x8 && by >= 0 && by < rows8;
-    }
-    if (!any) return;
     const FastCtx f = fast_prologue<LAYOUT>(a, lds);
     const int lane = threadIdx.x & 63;
     const int k = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+    const int tiles_x8 = (a.width + 7) >> 3, rows8 = (a.out_rows + 7) >> 3;
     int tx, ty;
     ring_tile(k, cx, cy, &tx, &ty);
     unsigned long long steps = 0;
