@@ -472,3 +472,32 @@ def test_procedural_matches_golden_crops(r, shadow, name):
     finally:
         r.set_procedural(enabled=0)
     assert np.array_equal(img[:, CROP_COLS[0]:CROP_COLS[1], 0], ref)
+
+
+@pytest.mark.parametrize("procedural", [False, True])
+def test_render_is_graph_capturable(r, vol128, procedural):
+    """vr_render neither allocates nor synchronises once warm, so a frame can
+    be captured in a hipGraph (torch.cuda.CUDAGraph) and replayed."""
+    W, H = 320, 200
+    osd, gsd = vr.reference_shader_data(W / H, 10.0, 5.0)
+    r.set_volume(vol128)
+    r.set_shader_data(osd, gsd)
+    r.set_march(vr.march_defaults(max_steps=64))
+    if procedural:
+        r.set_procedural()
+    try:
+        out = r.alloc_target(W, H, vr.FMT_RGBA8_UNORM)
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            r.render(W, H, vr.FMT_RGBA8_UNORM, out=out, stream=s)   # warm-up (allocates scratch)
+        torch.cuda.synchronize()
+        ref = out.clone()
+        out.zero_()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            r.render(W, H, vr.FMT_RGBA8_UNORM, out=out, stream=s)
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref)
+    finally:
+        r.set_procedural(enabled=0)
