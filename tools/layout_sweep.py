@@ -43,7 +43,7 @@ def main():
         r.set_option("schedule", lay[1])
         if lay[1] == 1 and lay[2] > 0:
             r.set_option("waves_per_simd", lay[2])
-        if lay[1] == 2 and lay[2] > 0:
+        if lay[1] in (2, 4) and lay[2] > 0:
             r.set_option("tiles_per_wave", lay[2])
 
     def name(lay):

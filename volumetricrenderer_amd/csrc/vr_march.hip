@@ -628,18 +628,22 @@ __device__ __forceinline__ bool ring_tile(int k, int cx, int cy, int* tx, int* t
 }
 
 template <int LAYOUT, int WRAP, bool EARLY>
-__global__ __launch_bounds__(kThreads) void march_rings(const MarchArgs a, int cx, int cy)
+__global__ __launch_bounds__(kThreads) void march_rings(const MarchArgs a, int cx, int cy, int nw, int npos)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned lds[];
     const FastCtx f = fast_prologue<LAYOUT>(a, lds);
     const int lane = threadIdx.x & 63;
-    const int k = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
     const int tiles_x8 = (a.width + 7) >> 3, rows8 = (a.out_rows + 7) >> 3;
-    int tx, ty;
-    ring_tile(k, cx, cy, &tx, &ty);
     unsigned long long steps = 0;
-    if (tx >= 0 && tx < tiles_x8 && ty >= 0 && ty < rows8)
-        steps = march_pixel<LAYOUT, WRAP, EARLY>(a, f, tx * 8 + lane_x<LAYOUT>(lane), ty * 8 + lane_y<LAYOUT>(lane));
+    // wave g takes ring positions g, g + nw, ... (nw = all waves): fewer
+    // workgroups, so fewer LDS-table prologues, in the same inside-out order
+    for (int k = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6); k < npos; k += nw) {
+        int tx, ty;
+        ring_tile(k, cx, cy, &tx, &ty);
+        if (tx >= 0 && tx < tiles_x8 && ty >= 0 && ty < rows8)
+            steps += march_pixel<LAYOUT, WRAP, EARLY>(a, f, tx * 8 + lane_x<LAYOUT>(lane),
+                                                      ty * 8 + lane_y<LAYOUT>(lane));
+    }
     if (a.step_counter) add_steps(a, steps);
 }
 
@@ -872,12 +876,14 @@ hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStre
         const int tiles_x8 = (a.width + 7) >> 3, rows8 = (a.out_rows + 7) >> 3;
         const int cx = min(max(sc.center_x >> 3, 0), tiles_x8 - 1), cy = min(max(sc.center_y >> 3, 0), rows8 - 1);
         const int R = max(max(cx, tiles_x8 - 1 - cx), max(cy, rows8 - 1 - cy));
-        const long long waves = (2ll * R + 1) * (2ll * R + 1);
-        const dim3 grid((unsigned)((waves + 3) / 4));
+        const int npos = (2 * R + 1) * (2 * R + 1);
+        const int tpw = sc.tiles_per_wave > 0 ? sc.tiles_per_wave : 1;
+        const int nw = (npos + tpw - 1) / tpw;
+        const dim3 grid((unsigned)((nw + 3) / 4));
         if (early)
-            hipLaunchKernelGGL((march_rings<L, W, true>), grid, block, lds, s, a, cx, cy);
+            hipLaunchKernelGGL((march_rings<L, W, true>), grid, block, lds, s, a, cx, cy, 4 * (int)grid.x, npos);
         else
-            hipLaunchKernelGGL((march_rings<L, W, false>), grid, block, lds, s, a, cx, cy);
+            hipLaunchKernelGGL((march_rings<L, W, false>), grid, block, lds, s, a, cx, cy, 4 * (int)grid.x, npos);
         return hipGetLastError();
     }
     if (sc.kind == SCHED_XCDROWS) {
