@@ -120,7 +120,8 @@ def test_every_layout_bitexact(r, oracle, vol128, layout, name):
         r.set_layout_preference(0)
 
 
-@pytest.mark.parametrize("schedule,wps", [(0, 4), (1, 1), (1, 3), (1, 8), (2, 1), (2, 3), (2, 16), (3, 1), (4, 1)])
+@pytest.mark.parametrize("schedule,wps", [(0, 4), (1, 1), (1, 3), (1, 8), (2, 1), (2, 3), (2, 16), (3, 1), (4, 1), (4, 2),
+                                          (4, 5)])
 def test_schedules_bitexact(r, oracle, vol128, schedule, wps):
     sched0, tpw0 = r.get_option("schedule"), r.get_option("tiles_per_wave")
     r.set_option("schedule", schedule)

@@ -45,7 +45,7 @@ vr_status fail(vr_status st, const char* fmt, ...)
 
 constexpr int kDefaultSchedule = -1;     // -1 auto, 0 static tiles, 1 persistent queue, 2 strided
 constexpr int kDefaultWavesPerSimd = 4;
-constexpr int kDefaultTilesPerWave = 1;
+constexpr int kDefaultTilesPerWave = 0;   // 0 = auto: 2 for rings, 1 for strided (measured)
 
 struct Ctx {
     int device = 0;
@@ -574,7 +574,8 @@ vr_status vr_set_option(void* p, const char* name, int value)
         return VR_OK;
     }
     if (n == "tiles_per_wave") {
-        if (value < 1 || value > 64) return fail(VR_ERR_INVALID, "vr_set_option: tiles_per_wave in [1, 64]");
+        if (value < 0 || value > 64)
+            return fail(VR_ERR_INVALID, "vr_set_option: tiles_per_wave in [1, 64], or 0 for auto");
         c->tiles_per_wave = value;
         return VR_OK;
     }
@@ -753,7 +754,8 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
     }
     // auto schedule (measured): rings, longest rays first
     const int kind = c->schedule >= 0 ? c->schedule : SCHED_RINGS;
-    Schedule sc{kind, 0, 0, c->tiles_per_wave, c->waves_per_simd, c->d_heads};
+    const int tpw = c->tiles_per_wave > 0 ? c->tiles_per_wave : (kind == SCHED_RINGS ? 2 : 1);
+    Schedule sc{kind, 0, 0, tpw, c->waves_per_simd, c->d_heads};
     if (kind == SCHED_RINGS) box_centre_pixel(c, a, &sc.center_x, &sc.center_y);
     HIP_TRY(launch_march(a, pl.layout, pl.wrap, pl.early, sc, static_cast<hipStream_t>(stream)));
     return VR_OK;
