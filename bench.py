@@ -234,7 +234,12 @@ def main() -> int:
             "executed_steps_per_s": round(frame_steps * args.steps / el, 1),
             "kernel_ms_mean": round(kern_ms, 5),
             "kernel_ms_mean_max_rank": round(kern_ms_max, 5),
-            "roofline": dict(roofline, traffic=traffic),
+            "roofline": dict(roofline, traffic=traffic,
+                             **({"traffic_GBs": round(traffic / (kern_ms * 1e-3) / 1e9, 1),
+                                 "traffic_frac": round(traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                 "traffic_def": "PMC HBM bytes per launch (profiles/traffic.json) / the same "
+                                                "mean kernel duration: the bytes the kernel really moves"}
+                                if traffic else {})),
         }
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(None if proc is not None else r.get_volume(), osd, gsd, march, W, H,
