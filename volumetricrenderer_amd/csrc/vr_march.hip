@@ -377,7 +377,7 @@ __device__ __forceinline__ float proc_density(const ProcParams& p, const float4*
     float f = p.freq0, amp = 1.0f, fbm = 0.0f;
     for (int o = 0; o < p.octaves; ++o) {
         float pn;
-        if constexpr (TABLE) pn = noise::perlin_gt(wt + 2 * p.wt_n * p.wt_n * (p.wt_n - 1), p.seed_fbm, qx * f, qy * f, qz * f);
+        if constexpr (TABLE) pn = noise::perlin_gt(wt + p.wt_n * p.wt_n * p.wt_n, p.seed_fbm, qx * f, qy * f, qz * f);
         else pn = noise::perlin(p.seed_fbm, qx * f, qy * f, qz * f);
         fbm = fmaf(amp, pn, fbm);
         f = f * p.lacunarity;
@@ -699,19 +699,18 @@ __global__ __launch_bounds__(kThreads) void march_queue(const MarchArgs a, int* 
 
 // Procedural medium: one 8x8 tile per wave (compute-bound; no volume), in
 // row order (cx < 0) or in rings around tile (cx, cy) (see march_rings).
-// Noise tables for the workgroup (dynamic LDS): the Worley cell-pair table
-// (wt_n^2 (wt_n - 1) pairs of 2 float4) followed by the 16 Perlin gradient
-// vectors, built before any wave may leave.  Returns null when the tables
-// are off (wt_n = 0).
+// Noise tables for the workgroup (dynamic LDS): the Worley cell table
+// (wt_n^3 float4) followed by the 16 Perlin gradient vectors, built before
+// any wave may leave.  Returns null when the tables are off (wt_n = 0).
 __device__ __forceinline__ const float4* worley_table(const ProcParams& p, float4* lds)
 {
     if (p.wt_n <= 0) return nullptr;
-    const int n = p.wt_n, pairs = n * n * (n - 1);
-    for (int i = threadIdx.x; i < pairs; i += kThreads) {
+    const int n = p.wt_n, cells = n * n * n;
+    for (int i = threadIdx.x; i < cells; i += kThreads) {
         const int ix = i % n, iy = (i / n) % n, iz = i / (n * n);
-        noise::cellular_pair(p.seed_worley, p.wt_lo + ix, p.wt_lo + iy, p.wt_lo + iz, lds + 2 * i);
+        lds[i] = noise::cellular_cell(p.seed_worley, p.wt_lo + ix, p.wt_lo + iy, p.wt_lo + iz);
     }
-    if (threadIdx.x < 16) lds[2 * pairs + threadIdx.x] = noise::grad_entry(threadIdx.x);
+    if (threadIdx.x < 16) lds[cells + threadIdx.x] = noise::grad_entry(threadIdx.x);
     __syncthreads();
     return lds;
 }
@@ -927,7 +926,7 @@ hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_bu
     if (a.width <= 0 || a.out_rows <= 0) return hipSuccess;
     const bool shadow = a.proc.shadow_steps > 0;
     const size_t wt_bytes =
-        a.proc.wt_n > 0 ? (2 * (size_t)a.proc.wt_n * a.proc.wt_n * (a.proc.wt_n - 1) + 16) * sizeof(float4) : 0;
+        a.proc.wt_n > 0 ? ((size_t)a.proc.wt_n * a.proc.wt_n * a.proc.wt_n + 16) * sizeof(float4) : 0;
     if (sort_buf) {
         unsigned* hist = static_cast<unsigned*>(sort_buf);
         unsigned* cursor = hist + kKeyBins;            // kKeyBins + 1 entries

@@ -199,26 +199,17 @@ __device__ inline float cellular(int32_t seed, float x, float y, float z)
 }
 
 // Cellular F1 from a table of per-cell feature-point data (the LDS table of
-// the procedural march; vr_march.hip).  The table holds z-adjacent cell
-// PAIRS: pair (ix, iy, iz) is two float4, {xd_a, xd_b, yd_a, yd_b} and
-// {zd_a, zd_b, inv_a, inv_b}, for cells a = (ix, iy, iz) and b = (ix, iy,
-// iz + 1), where {xd, yd, zd, inv} is what cellular() derives from the cell
-// hash.  A column (xi, yi) of the 3x3x3 neighbourhood is the pairs at
-// z0 - 1 and z0 (the middle cell twice), so each column is two register
-// pairs and packed math: 3 v_pk_fma for the cell-point offsets and 3 packed
-// ops for the squared distance, for two cells at a time.  Each cell's
-// arithmetic is cellular()'s, op for op (a packed fma is two fmas), and
-// fminf is exact, so F1 is bit-identical.  The caller guarantees every cell
-// rint(coord) - 1 .. + 1 lies in [lo, lo + n).
-typedef float vr_f2 __attribute__((ext_vector_type(2)));
+// the procedural march; vr_march.hip).  Entry (ix, iy, iz) - lo holds
+// {xd, yd, zd, inv} of cellular() for that integer cell, so each of the 27
+// cells costs one 16-byte LDS read and 7 VALU ops instead of the hash,
+// bit-field, sqrt and reciprocal.  The arithmetic per cell is cellular()'s,
+// op for op, and fminf is exact, so the result is bit-identical.  The caller
+// guarantees every cell rint(coord) - 1 .. + 1 lies in [lo, lo + n).
 __device__ inline float cellular_table(const float4* __restrict__ tab, int lo, int n, float x, float y, float z)
 {
     const float xr = rintf(x), yr = rintf(y), zr = rintf(z);
     const int ix = (int)xr - 1 - lo, iy = (int)yr - 1 - lo, iz = (int)zr - 1 - lo;
-    const vr_f2 zc_m = {(zr + -1.0f) - z, (zr + 0.0f) - z};
-    const vr_f2 zc_p = {(zr + 0.0f) - z, (zr + 1.0f) - z};
-    const float4* t0 = tab + 2 * ((iz * n + iy) * n + ix);
-    const int zstride = 2 * n * n;
+    const float4* t0 = tab + (iz * n + iy) * n + ix;
     float d0 = 3.402823466e+38f;
 #pragma unroll
     for (int xi = -1; xi <= 1; ++xi) {
@@ -226,36 +217,28 @@ __device__ inline float cellular_table(const float4* __restrict__ tab, int lo, i
 #pragma unroll
         for (int yi = -1; yi <= 1; ++yi) {
             const float ycf = (yr + (float)yi) - y;
-            const float4* c = t0 + 2 * ((yi + 1) * n + (xi + 1));
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const float4 p0 = c[h * zstride], p1 = c[h * zstride + 1];
-                const vr_f2 w = {p1.z, p1.w};
-                const vr_f2 xd = __builtin_elementwise_fma(vr_f2{p0.x, p0.y}, w, vr_f2{xcf, xcf});
-                const vr_f2 yd = __builtin_elementwise_fma(vr_f2{p0.z, p0.w}, w, vr_f2{ycf, ycf});
-                const vr_f2 zd = __builtin_elementwise_fma(vr_f2{p1.x, p1.y}, w, h ? zc_p : zc_m);
-                const vr_f2 dd = __builtin_elementwise_fma(zd, zd, __builtin_elementwise_fma(yd, yd, xd * xd));
-                d0 = fminf(d0, fminf(dd.x, dd.y));
+            for (int zi = -1; zi <= 1; ++zi) {
+                const float zcf = (zr + (float)zi) - z;
+                const float4 c = t0[((zi + 1) * n + (yi + 1)) * n + (xi + 1)];
+                const float xd = fmaf(c.x, c.w, xcf);
+                const float yd = fmaf(c.y, c.w, ycf);
+                const float zd = fmaf(c.z, c.w, zcf);
+                d0 = fminf(d0, fmaf(zd, zd, fmaf(yd, yd, xd * xd)));
             }
         }
     }
     return d0 - 1.0f;
 }
 
-// Pair entry of the table: cells (ix, iy, iz) and (ix, iy, iz + 1).
-__device__ inline void cellular_pair(int32_t seed, int ix, int iy, int iz, float4* out)
+// One table entry: cellular()'s feature-point data for integer cell (ix, iy, iz).
+__device__ inline float4 cellular_cell(int32_t seed, int ix, int iy, int iz)
 {
-    float v[2][4];
-    for (int k = 0; k < 2; ++k) {
-        const int32_t h = hash_hb(seed, wmul(ix, kPX), wmul(iy, kPY), wmul(iz + k, kPZ));
-        const float xd = (float)(h & 0x3ff) - 511.5f;
-        const float yd = (float)((h >> 10) & 0x3ff) - 511.5f;
-        const float zd = (float)((h >> 20) & 0x3ff) - 511.5f;
-        v[k][0] = xd; v[k][1] = yd; v[k][2] = zd;
-        v[k][3] = cell_inv(fmaf(zd, zd, fmaf(yd, yd, xd * xd)));
-    }
-    out[0] = make_float4(v[0][0], v[1][0], v[0][1], v[1][1]);
-    out[1] = make_float4(v[0][2], v[1][2], v[0][3], v[1][3]);
+    const int32_t h = hash_hb(seed, wmul(ix, kPX), wmul(iy, kPY), wmul(iz, kPZ));
+    const float xd = (float)(h & 0x3ff) - 511.5f;
+    const float yd = (float)((h >> 10) & 0x3ff) - 511.5f;
+    const float zd = (float)((h >> 20) & 0x3ff) - 511.5f;
+    return make_float4(xd, yd, zd, cell_inv(fmaf(zd, zd, fmaf(yd, yd, xd * xd))));
 }
 
 }  // namespace noise
