@@ -43,6 +43,11 @@ from volumetricrenderer_amd import distributed as vrdist  # noqa: E402
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: fp32 vector peak
 BYTES_PER_STEP = 32        # 4 trilinear taps x 8 texels x 1 B
+# fp32 FLOP per executed grid ray-step (FMA = 2): per tap, texel coordinate 3 fma (6),
+# 3 fractions (3), 7 lerps x (sub + fma) (21), x 1/255 (1) = 31; x 4 taps = 124;
+# combine t0*t1*(t2+t3)*scale + acc (5); advance the ray point (3).  (SURVEY.md 8d
+# estimates ~90.)
+FLOP_PER_STEP = 132
 
 CONFIGS = {
     # name: (volume N or None = procedural, width, height, max_steps, shadow steps, BASELINE configs index)
@@ -187,12 +192,23 @@ def main() -> int:
     if rank == 0:
         ms_per_step = el / args.steps * 1e3
         value = W * H * S * args.steps / el / 1e6
-        if proc is None:
-            achieved = local_steps * BYTES_PER_STEP / (kern_ms * 1e-3) / 1e9
-            roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+        gather = local_steps * BYTES_PER_STEP / (kern_ms * 1e-3) / 1e9
+        if proc is None and "corner8" not in r.kernel_variant:
+            roofline = {"bound": "hbm", "achieved": round(gather, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(gather / HBM_PEAK_GBS, 4), "traffic": None,
                         "achieved_def": "32 B algorithmic gather per executed ray-step x steps per launch "
                                         "/ mean march-kernel duration (HIP events on its stream)"}
+        elif proc is None:
+            # cache-resident volume (corner8 is auto only when it fits the
+            # Infinity Cache): the march is VALU-bound (VALUBusy ~100 %,
+            # profiles/r01_pmc/c8_4k.json), so the roofline is fp32 VALU
+            tf = local_steps * FLOP_PER_STEP / (kern_ms * 1e-3) / 1e12
+            roofline = {"bound": "valu", "achieved": round(tf, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": round(tf / FP32_PEAK_TFLOPS, 4), "traffic": None,
+                        "achieved_def": f"{FLOP_PER_STEP} algorithmic fp32 FLOP per executed ray-step x steps per "
+                                        "launch / mean march-kernel duration (HIP events on its stream); the volume "
+                                        "is cache-resident",
+                        "gather_GBs": round(gather, 1)}
         else:
             fpd = flop_per_density(proc.octaves)
             achieved = local_evals * fpd / (kern_ms * 1e-3) / 1e12
