@@ -502,3 +502,22 @@ def test_render_is_graph_capturable(r, vol128, procedural):
         assert torch.equal(out, ref)
     finally:
         r.set_procedural(enabled=0)
+
+
+def test_prepared_launchers_match_render(r, vol128):
+    """prepare_render / prepare_assemble (the multi-GPU frame loop's fixed
+    launchers) give the same pixels as render / assemble_bands."""
+    W, H, nr, br = 300, 170, 3, 16
+    osd, gsd = vr.reference_shader_data(W / H, 30.0, 10.0)
+    r.set_volume(vol128)
+    r.set_shader_data(osd, gsd)
+    r.set_march(vr.march_defaults(max_steps=96))
+    rows = vr.band_rows_packed(H, br, nr, 0)
+    g = torch.zeros((nr, rows, W, 4), dtype=torch.uint8, device="cuda")
+    for k in range(nr):
+        r.prepare_render(W, H, vr.FMT_RGBA8_UNORM, g[k], band_rows=br, band_stride=nr, band_first=k)()
+    frame = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
+    r.prepare_assemble(g, nr, W, H, br, frame)()
+    full = r.render(W, H, vr.FMT_RGBA8_UNORM)
+    torch.cuda.synchronize()
+    assert torch.equal(frame, full)

@@ -108,10 +108,20 @@ class BandSharder:
                 "gathered": [self.gathered, torch.empty_like(self.gathered)] if self.rank == 0 else [None, None],
                 "frame": [self.frame_buf, torch.empty_like(self.frame_buf)] if self.rank == 0 else [None, None],
             }
-            # per-rank views of the gather buffers, made once (host time per frame
-            # is what limits strong scaling of a ~0.03 ms/rank frame)
+            # per-rank views of the gather buffers and the render / assemble
+            # launchers, made once (host time per frame is what limits strong
+            # scaling of a ~0.03 ms/rank frame)
             self._pipe["lists"] = ([list(g.unbind(0)) for g in self._pipe["gathered"]] if self.rank == 0
                                    else [None, None])
+            if hasattr(self.r, "prepare_render"):
+                self._pipe["render"] = [
+                    self.r.prepare_render(self.width, self.height, self.fmt, loc[: self.my_rows],
+                                          band_rows=self.band_rows, band_stride=self.world, band_first=self.rank)
+                    for loc in self._pipe["local"]]
+                self._pipe["assemble"] = ([
+                    self.r.prepare_assemble(g, self.world, self.width, self.height, self.band_rows, fr)
+                    for g, fr in zip(self._pipe["gathered"], self._pipe["frame"])] if self.rank == 0
+                    else [None, None])
         P = self._pipe
         pending = None
 
@@ -119,8 +129,11 @@ class BandSharder:
             work, par = p
             work.wait()   # the current stream waits for the gather
             if self.rank == 0:
-                self.r.assemble_bands(P["gathered"][par], self.world, self.width, self.height, self.band_rows,
-                                      frame=P["frame"][par])
+                if "assemble" in P:
+                    P["assemble"][par]()
+                else:
+                    self.r.assemble_bands(P["gathered"][par], self.world, self.width, self.height,
+                                          self.band_rows, frame=P["frame"][par])
 
         last = None
         for i in range(k):
@@ -129,8 +142,11 @@ class BandSharder:
             ev = events[i] if events else None
             if ev is not None:
                 ev[0].record()
-            self.r.render(self.width, self.height, self.fmt, out=loc[: self.my_rows], band_rows=self.band_rows,
-                          band_stride=self.world, band_first=self.rank)
+            if "render" in P:
+                P["render"][par]()
+            else:
+                self.r.render(self.width, self.height, self.fmt, out=loc[: self.my_rows],
+                              band_rows=self.band_rows, band_stride=self.world, band_first=self.rank)
             if ev is not None:
                 ev[1].record()
             work = dist.gather(loc, gather_list=P["lists"][par], dst=0, group=self.group, async_op=True)

@@ -239,6 +239,37 @@ class Renderer:
         call("vr_render", self._ctx, ctypes.byref(t), _stream_handle(stream))
         return out
 
+    def prepare_render(self, width: int, height: int, fmt: int, out: torch.Tensor, band_rows: int = 0,
+                       band_stride: int = 1, band_first: int = 0, stream=None):
+        """A zero-argument launcher for one fixed render (target, bands,
+        stream): the ctypes arguments are built once, so a frame loop pays
+        only the call (host time per frame bounds multi-GPU strong scaling)."""
+        t = Target(width=width, height=height, format=fmt, band_rows=band_rows, band_stride=band_stride,
+                   band_first=band_first, pixels=out.data_ptr(), row_pitch=out.stride(0) * out.element_size(),
+                   step_counter=None)
+        fn, ctx, tref, sh = _lib.load().vr_render, self._ctx, ctypes.byref(t), _stream_handle(stream)
+
+        def launch():
+            st = fn(ctx, tref, sh)
+            if st:
+                _lib.check(st, "vr_render")
+        launch.target = t   # keep the struct alive with the closure
+        return launch
+
+    def prepare_assemble(self, gathered: torch.Tensor, nranks: int, width: int, height: int, band_rows: int,
+                         frame: torch.Tensor, stream=None):
+        """Zero-argument launcher for one fixed vr_assemble_bands call."""
+        bpp = gathered.element_size() * gathered.shape[-1]
+        args = (self._ctx, ctypes.c_void_p(gathered.data_ptr()), gathered.shape[1], nranks, width, height, band_rows,
+                bpp, ctypes.c_void_p(frame.data_ptr()), _stream_handle(stream))
+        fn = _lib.load().vr_assemble_bands
+
+        def launch():
+            st = fn(*args)
+            if st:
+                _lib.check(st, "vr_assemble_bands")
+        return launch
+
     def assemble_bands(self, gathered: torch.Tensor, nranks: int, width: int, height: int, band_rows: int,
                        frame: torch.Tensor | None = None, stream=None) -> torch.Tensor:
         """Scatter [rank][packed rows] band sets into one frame (SURVEY.md e)."""
