@@ -745,29 +745,7 @@ __global__ __launch_bounds__(kThreads) void march_proc(const MarchArgs a, int cx
 // [64w, 64w + 64).  Lanes of a wave share n (no loop divergence) and the
 // longest rays start first (longest-processing-time order, no tail).
 constexpr int kKeyBins = 1024;
-constexpr int kSortPixelsPerThread = 16;   // fewer blocks -> fewer global atomics on hot bins (measured 2-16)
-
-// Wave-aggregated LDS increment: neighbouring pixels mostly share a key, so
-// instead of up to 64 serialised atomics on one address, each distinct key
-// of the wave takes one atomic and the lanes rank themselves by popcount.
-// Returns this lane's slot (old value + rank) for lanes with key >= 0.
-__device__ __forceinline__ unsigned wave_increment(unsigned* h, int key)
-{
-    const int lane = threadIdx.x & 63;
-    unsigned long long todo = __ballot(key >= 0);
-    unsigned slot = 0;
-    while (todo) {
-        const int leader = __ffsll((long long)todo) - 1;
-        const int k = __shfl(key, leader);
-        const unsigned long long m = __ballot(key == k);
-        unsigned base = 0;
-        if (lane == leader) base = atomicAdd(&h[k], (unsigned)__popcll(m));
-        base = __shfl(base, leader);
-        if (key == k) slot = base + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
-        todo &= ~m;
-    }
-    return slot;
-}
+constexpr int kSortPixelsPerThread = 8;   // fewer blocks -> fewer global atomics on hot bins
 __device__ __forceinline__ int cost_key(int n) { return n < kKeyBins - 1 ? n : kKeyBins - 1; }
 
 template <bool SHADOW>
@@ -782,11 +760,14 @@ __global__ __launch_bounds__(256) void proc_bin(const MarchArgs a, unsigned* __r
         const int orow = (int)(pix / (unsigned)a.width), x = (int)(pix - (unsigned)orow * (unsigned)a.width);
         if (orow >= a.out_rows) break;
         const Ray r = setup_ray(a, x, orow);
-        int key = -1;
-        if (r.n > 0) key = cost_key(r.n);
-        else if (r.live) store_pixel(a, x, orow, r.n >= 0, proc_epilogue<SHADOW>(a, 0.0f, 0.0f));   // 0 steps
-        wave_increment(h, key);
-        keys[pix] = (unsigned short)(key > 0 ? key : 0);
+        int key = 0;
+        if (r.n > 0) {
+            key = cost_key(r.n);
+            atomicAdd(&h[key], 1u);
+        } else if (r.live) {
+            store_pixel(a, x, orow, r.n >= 0, proc_epilogue<SHADOW>(a, 0.0f, 0.0f));   // 0 steps
+        }
+        keys[pix] = (unsigned short)key;
     }
     __syncthreads();
     for (int i = threadIdx.x; i < kKeyBins; i += 256)
@@ -826,10 +807,12 @@ __global__ __launch_bounds__(256) void proc_scatter(const MarchArgs a, const uns
         const int orow = (int)(pix / (unsigned)a.width), x = (int)(pix - (unsigned)orow * (unsigned)a.width);
         if (orow < a.out_rows) {
             const int k = keys[pix];
-            if (k > 0) key[it] = k;
-            packed[it] = ((unsigned)orow << 16) | (unsigned)x;
+            if (k > 0) {
+                key[it] = k;
+                rank[it] = atomicAdd(&h[k], 1u);
+                packed[it] = ((unsigned)orow << 16) | (unsigned)x;
+            }
         }
-        rank[it] = wave_increment(h, key[it]);
     }
     __syncthreads();
     for (int i = threadIdx.x; i < kKeyBins; i += 256)
