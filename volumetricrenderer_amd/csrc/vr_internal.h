@@ -122,6 +122,7 @@ struct Schedule {
 
 // launchers (vr_march.hip / vr_volume.hip); return hipError_t
 hipError_t launch_march(const MarchArgs& a, int layout, int wrap, bool early, const Schedule& sc, hipStream_t s);
+hipError_t launch_march_corner8(const MarchArgs& a, bool early, const Schedule& sc, hipStream_t s);   // vr_march_c8.hip
 // sort_buf (proc_sort_bytes) selects the cost-sorted schedule; null = 8x8
 // tiles, in rings when sc.kind == SCHED_RINGS, else in row order
 hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_buf, const Schedule& sc, hipStream_t s);

@@ -1,0 +1,16 @@
+// vr_march_c8.hip -- the CORNER8 (cache-resident volume) instantiation of
+// the ray march.  A separate translation unit because it is built with
+// -fno-slp-vectorize: the SLP vectoriser packs pairs of scalar lerps into
+// v_pk_* ops whose operands then need v_mov pairs; for this VALU-bound
+// kernel that is 5 % slower at 128^3 (0.097 -> 0.092 ms), while the brick
+// kernels gain from it.
+#include "vr_march_kernels.h"
+
+namespace vr {
+
+hipError_t launch_march_corner8(const MarchArgs& a, bool early, const Schedule& sc, hipStream_t s)
+{
+    return launch_lw<LAYOUT_CORNER8, WRAP_CLAMP>(a, early, sc, s);
+}
+
+}  // namespace vr

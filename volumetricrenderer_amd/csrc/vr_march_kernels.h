@@ -1,0 +1,916 @@
+// vr_march_kernels.h -- device code of the ray march: the tap and blend
+// helpers, the per-pixel march for the grid layouts and the procedural
+// medium, and the kernels with their templated launcher launch_lw.  Included
+// by vr_march.hip (all launchers) and vr_march_c8.hip (the CORNER8 launcher,
+// compiled with different vectoriser flags).  Everything
+// is in an anonymous namespace, so each translation unit keeps its own copy.
+#pragma once
+#include "vr_internal.h"
+#include "vr_noise.h"
+
+namespace vr {
+namespace {
+
+constexpr int kTile = 16;           // static schedule: workgroup tile edge, pixels
+constexpr int kThreads = 256;       // 4 waves
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float lerp_(float a, float b, float t) { return fmaf(t, b - a, a); }
+__device__ __forceinline__ f2 lerp2(f2 a, f2 b, f2 t) { return __builtin_elementwise_fma(t, b - a, a); }
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return min(max(v, lo), hi); }
+
+// floor(x) as int in one instruction, and x - floor(x) clamped below 1.0
+// (v_fract_f32).  The spec defines the tap weight as
+// fminf(g - floorf(g), 0x1.fffffep-1f), which is what v_fract_f32 returns.
+__device__ __forceinline__ int cvt_flr(float x)
+{
+    int r;
+    asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+__device__ __forceinline__ float fract_(float x) { return __builtin_amdgcn_fractf(x); }
+
+// byte k of a dword as float: one v_cvt_f32_ubyteK.  Opaque on purpose: given
+// (float)hi - (float)lo of two bytes, hipcc otherwise subtracts in packed
+// int16 and converts the difference, which costs more instructions.
+template <int K>
+__device__ __forceinline__ float ubyte(unsigned v)
+{
+    float r;
+    if constexpr (K == 0) asm("v_cvt_f32_ubyte0 %0, %1" : "=v"(r) : "v"(v));
+    else if constexpr (K == 1) asm("v_cvt_f32_ubyte1 %0, %1" : "=v"(r) : "v"(v));
+    else if constexpr (K == 2) asm("v_cvt_f32_ubyte2 %0, %1" : "=v"(r) : "v"(v));
+    else asm("v_cvt_f32_ubyte3 %0, %1" : "=v"(r) : "v"(v));
+    return r;
+}
+
+// VK_SAMPLER_ADDRESS_MODE_MIRRORED_REPEAT on an integer texel index
+// (VulkanCore.cpp:683-685; Vulkan spec "Texel coordinate wrapping").
+__device__ __forceinline__ int mirror_(int i, int n)
+{
+    int two = n + n;
+    int m = i % two;
+    m = m < 0 ? m + two : m;
+    return m < n ? m : two - 1 - m;
+}
+
+// exp(x) for x <= 0, the fma-only polynomial of the spec.
+__device__ __forceinline__ float spec_expf(float x)
+{
+    if (x < -80.0f) return 0.0f;
+    float k = rintf(x * 1.44269504088896341f);
+    float r = fmaf(k, -0.693359375f, x);
+    r = fmaf(k, 2.12194440e-4f, r);
+    float p = 1.9875691500e-4f;
+    p = fmaf(p, r, 1.3981999507e-3f);
+    p = fmaf(p, r, 8.3334519073e-3f);
+    p = fmaf(p, r, 4.1665795894e-2f);
+    p = fmaf(p, r, 1.6666665459e-1f);
+    p = fmaf(p, r, 5.0000001201e-1f);
+    p = fmaf(p, r * r, r);
+    p = p + 1.0f;
+    return p * __int_as_float(((int)k + 127) << 23);
+}
+
+// Trilinear blend of the 8 footprint texels, two lerps per packed op:
+// x-lerps of (y0,z0|y0,z1) and (y1,z0|y1,z1), then y, then z.  Each element
+// is the spec's fma(t, b - a, a), in the spec's order.
+__device__ __forceinline__ float blend(f2 lo_a, f2 hi_a, f2 lo_b, f2 hi_b, float wx, float wy, float wz)
+{
+    const f2 xa = lerp2(lo_a, hi_a, f2{wx, wx});   // {x00, x01}
+    const f2 xb = lerp2(lo_b, hi_b, f2{wx, wx});   // {x10, x11}
+    const f2 y = lerp2(xa, xb, f2{wy, wy});        // {y0, y1}
+    return lerp_(y.x, y.y, wz) * (1.0f / 255.0f);
+}
+
+// Per-launch state of a fast-layout tap: the channel's buffer descriptor and
+// the LDS offset tables TX | TY | TZ (vr_internal.h Layout).
+struct FastCtx {
+    __amdgpu_buffer_rsrc_t rsrc[4];
+    const unsigned* tx;
+    const unsigned* ty;
+    const unsigned* tz;
+};
+
+// A fast-layout tap in two parts: fetch (issue the loads, keep the weights)
+// and blend.  The pipelined march issues step i+1's fetches before blending
+// step i, so each wave keeps two steps of loads in flight.
+struct TapRaw {
+    unsigned q0, q1, q2, q3;
+    float wx, wy, wz;
+};
+template <int LAYOUT>
+__device__ __forceinline__ TapRaw tap_fetch(const FastCtx& f, int ch, float gx, float gy, float gz)
+{
+    TapRaw r{};
+    r.wx = fract_(gx); r.wy = fract_(gy); r.wz = fract_(gz);
+    const unsigned off = f.tx[cvt_flr(gx)] + f.ty[cvt_flr(gy)] + f.tz[cvt_flr(gz)];
+    if constexpr (LAYOUT == LAYOUT_CORNER8) {
+        r.q0 = __builtin_amdgcn_raw_buffer_load_b32(f.rsrc[ch], off, 0, 0);
+        r.q1 = __builtin_amdgcn_raw_buffer_load_b32(f.rsrc[ch], off + 4, 0, 0);
+    } else if constexpr (LAYOUT == LAYOUT_BRICK5) {
+        // R = 5: one load per z-slice, bytes off..off+6 (c000 c100 . . . c010
+        // c110) and the same 25 bytes on.  Each is a dword-ALIGNED 12-byte
+        // load from off & ~3 and two v_alignbyte_b32 that shift the slice
+        // down by off & 3: an 8-byte load at a byte-granular offset costs
+        // the L1 twice the tag lookups of a dword-aligned one, and a 12-byte
+        // one costs the same as 8 bytes (tools/tcp_calib.hip, DESIGN.md
+        // sec. 5.1): 0.264 -> 0.225 ms at 512^3, 0.195 -> 0.122 ms at 256^3.
+        // Narrow row loads (4 x u16 or u32 per tap) were 20 % slower than the
+        // byte-offset 8-byte loads: more instructions, more lookups.
+        const unsigned o1 = off + 25;
+        const auto s0 = __builtin_amdgcn_raw_buffer_load_b96(f.rsrc[ch], off & ~3u, 0, 0);
+        const auto s1 = __builtin_amdgcn_raw_buffer_load_b96(f.rsrc[ch], o1 & ~3u, 0, 0);
+        r.q0 = __builtin_amdgcn_alignbyte(s0[1], s0[0], off);
+        r.q1 = __builtin_amdgcn_alignbyte(s0[2], s0[1], off);
+        r.q2 = __builtin_amdgcn_alignbyte(s1[1], s1[0], o1);
+        r.q3 = __builtin_amdgcn_alignbyte(s1[2], s1[1], o1);
+    } else if constexpr (LAYOUT == LAYOUT_BRICK8) {
+        // R = 8: rows y and y+1 of a slice are 8 bytes apart, so one
+        // dword-aligned 16-byte load from off & ~3 holds both (bytes off,
+        // off+1, off+8, off+9); the z+1 slice is 64 bytes on.  Two loads per
+        // tap instead of four byte-offset u16 loads: 0.271 -> 0.235 ms at
+        // 512^3, 0.185 -> 0.119 ms at 128^3.
+        const unsigned o1 = off + 64;
+        const auto s0 = __builtin_amdgcn_raw_buffer_load_b128(f.rsrc[ch], off & ~3u, 0, 0);
+        const auto s1 = __builtin_amdgcn_raw_buffer_load_b128(f.rsrc[ch], o1 & ~3u, 0, 0);
+        r.q0 = __builtin_amdgcn_alignbyte(s0[1], s0[0], off);   // c000 c100 in bytes 0-1
+        r.q1 = __builtin_amdgcn_alignbyte(s0[3], s0[2], off);   // c010 c110
+        r.q2 = __builtin_amdgcn_alignbyte(s1[1], s1[0], o1);    // c001 c101
+        r.q3 = __builtin_amdgcn_alignbyte(s1[3], s1[2], o1);    // c011 c111
+    } else {
+        constexpr int R = LAYOUT == LAYOUT_BRICK8 ? 8 : 16;
+        r.q0 = __builtin_amdgcn_raw_buffer_load_b16(f.rsrc[ch], off, 0, 0);
+        r.q1 = __builtin_amdgcn_raw_buffer_load_b16(f.rsrc[ch], off + R, 0, 0);
+        r.q2 = __builtin_amdgcn_raw_buffer_load_b16(f.rsrc[ch], off + R * R, 0, 0);
+        r.q3 = __builtin_amdgcn_raw_buffer_load_b16(f.rsrc[ch], off + R * R + R, 0, 0);
+    }
+    return r;
+}
+template <int LAYOUT>
+__device__ __forceinline__ float tap_blend(const TapRaw& r)
+{
+    if constexpr (LAYOUT == LAYOUT_CORNER8) {
+        return blend(f2{ubyte<0>(r.q0), ubyte<0>(r.q1)}, f2{ubyte<1>(r.q0), ubyte<1>(r.q1)},
+                     f2{ubyte<2>(r.q0), ubyte<2>(r.q1)}, f2{ubyte<3>(r.q0), ubyte<3>(r.q1)}, r.wx, r.wy, r.wz);
+    } else if constexpr (LAYOUT == LAYOUT_BRICK5) {
+        return blend(f2{ubyte<0>(r.q0), ubyte<0>(r.q2)}, f2{ubyte<1>(r.q0), ubyte<1>(r.q2)},
+                     f2{ubyte<1>(r.q1), ubyte<1>(r.q3)}, f2{ubyte<2>(r.q1), ubyte<2>(r.q3)}, r.wx, r.wy, r.wz);
+    } else {
+        return blend(f2{ubyte<0>(r.q0), ubyte<0>(r.q2)}, f2{ubyte<1>(r.q0), ubyte<1>(r.q2)},
+                     f2{ubyte<0>(r.q1), ubyte<0>(r.q3)}, f2{ubyte<1>(r.q1), ubyte<1>(r.q3)}, r.wx, r.wy, r.wz);
+    }
+}
+// One trilinear tap of one channel from a fast layout, at padded texel
+// coordinate g (floor(g) = base texel + 1, fract(g) = weight).  Loads go
+// through a range-checked buffer descriptor: an offset outside the plane
+// reads 0 instead of faulting.
+template <int LAYOUT>
+__device__ __forceinline__ float tap_fast(const FastCtx& f, int ch, float gx, float gy, float gz)
+{
+    return tap_blend<LAYOUT>(tap_fetch<LAYOUT>(f, ch, gx, gy, gz));
+}
+
+template <int LAYOUT>
+__device__ __forceinline__ TapRaw tap_fetch_at(const MarchArgs& a, const FastCtx& f, int t, f2 pxy, float pz)
+{
+    const f2 gxy = __builtin_elementwise_fma(pxy, f2{a.tap_S[t][0], a.tap_S[t][1]}, f2{a.tap_T[t][0], a.tap_T[t][1]});
+    const float gz = fmaf(pz, a.tap_S[t][2], a.tap_T[t][2]);
+    return tap_fetch<LAYOUT>(f, t, gxy.x, gxy.y, gz);
+}
+
+// One trilinear tap from the planar layout with full wrap semantics.
+template <int WRAP>
+__device__ __forceinline__ float tap_planar(const uint8_t* __restrict__ pl, const MarchArgs& a, float gx,
+                                            float gy, float gz)
+{
+    const float wx = fract_(gx), wy = fract_(gy), wz = fract_(gz);
+    const int ix = cvt_flr(gx) - 1, iy = cvt_flr(gy) - 1, iz = cvt_flr(gz) - 1;
+    int i0, i1, j0, j1, k0, k1;
+    if constexpr (WRAP == WRAP_CLAMP) {
+        i0 = clampi(ix, 0, a.nx - 1); i1 = clampi(ix + 1, 0, a.nx - 1);
+        j0 = clampi(iy, 0, a.ny - 1); j1 = clampi(iy + 1, 0, a.ny - 1);
+        k0 = clampi(iz, 0, a.nz - 1); k1 = clampi(iz + 1, 0, a.nz - 1);
+    } else {
+        i0 = mirror_(ix, a.nx); i1 = mirror_(ix + 1, a.nx);
+        j0 = mirror_(iy, a.ny); j1 = mirror_(iy + 1, a.ny);
+        k0 = mirror_(iz, a.nz); k1 = mirror_(iz + 1, a.nz);
+    }
+    const int r00 = (k0 * a.ny + j0) * a.nx, r10 = (k0 * a.ny + j1) * a.nx;
+    const int r01 = (k1 * a.ny + j0) * a.nx, r11 = (k1 * a.ny + j1) * a.nx;
+    return blend(f2{ubyte<0>(pl[r00 + i0]), ubyte<0>(pl[r01 + i0])}, f2{ubyte<0>(pl[r00 + i1]), ubyte<0>(pl[r01 + i1])},
+                 f2{ubyte<0>(pl[r10 + i0]), ubyte<0>(pl[r11 + i0])}, f2{ubyte<0>(pl[r10 + i1]), ubyte<0>(pl[r11 + i1])},
+                 wx, wy, wz);
+}
+
+// Tap t at ray point P: padded texel coordinate g = fma(P, S_t, T_t).
+template <int LAYOUT, int WRAP>
+__device__ __forceinline__ float tap(const MarchArgs& a, const FastCtx& f, int t, f2 pxy, float pz)
+{
+    const f2 gxy = __builtin_elementwise_fma(pxy, f2{a.tap_S[t][0], a.tap_S[t][1]}, f2{a.tap_T[t][0], a.tap_T[t][1]});
+    const float gz = fmaf(pz, a.tap_S[t][2], a.tap_T[t][2]);
+    if constexpr (LAYOUT == LAYOUT_PLANAR)
+        return tap_planar<WRAP>(a.vol + (size_t)t * a.plane_stride, a, gxy.x, gxy.y, gz);
+    else
+        return tap_fast<LAYOUT>(f, t, gxy.x, gxy.y, gz);
+}
+
+// Per-ray state after ray setup (frag.glsl:36-55).
+struct Ray {
+    bool live;     // pixel exists (inside the target and the frame)
+    int n;         // steps (frag.glsl:46); -1 = not covered
+    f2 pxy;        // box-normalised ray point (frag.glsl:49-54)
+    float pz;
+    f2 sxy;        // step vector (frag.glsl:45, 54)
+    float sz;
+};
+
+__device__ __forceinline__ Ray setup_ray(const MarchArgs& a, int x, int orow)
+{
+    Ray r{};
+    r.n = -1;
+    const bool inside = x < a.width && orow < a.out_rows;
+    int y = 0;
+    if (inside) {
+        const int bl = orow / a.band_rows;
+        y = (a.band_first + bl * a.band_stride) * a.band_rows + (orow - bl * a.band_rows);
+    }
+    r.live = inside && y < a.height;
+    if (!r.live) return r;
+    const float fx = (float)x + 0.5f, fy = (float)y + 0.5f;
+    const float v0 = fmaf(fy, a.py[0], fmaf(fx, a.px[0], a.o[0]));
+    const float v1 = fmaf(fy, a.py[1], fmaf(fx, a.px[1], a.o[1]));
+    const float v2 = fmaf(fy, a.py[2], fmaf(fx, a.px[2], a.o[2]));
+    const float len = sqrtf(fmaf(v2, v2, fmaf(v1, v1, v0 * v0)));
+    const float d0 = v0 / len, d1 = v1 / len, d2 = v2 / len;
+    // IntersectAABB, frag.glsl:18-27
+    const float ta0 = (a.box_min[0] - a.org[0]) / d0, tb0 = (a.box_max[0] - a.org[0]) / d0;
+    const float ta1 = (a.box_min[1] - a.org[1]) / d1, tb1 = (a.box_max[1] - a.org[1]) / d1;
+    const float ta2 = (a.box_min[2] - a.org[2]) / d2, tb2 = (a.box_max[2] - a.org[2]) / d2;
+    const float tn = fmaxf(fmaxf(fminf(ta0, tb0), fminf(ta1, tb1)), fminf(ta2, tb2));
+    const float tf = fminf(fminf(fmaxf(ta0, tb0), fmaxf(ta1, tb1)), fmaxf(ta2, tb2));
+    if (!(tn <= tf)) return r;
+    const float pi0 = fmaf(d0, tn, a.org[0]), pi1 = fmaf(d1, tn, a.org[1]), pi2 = fmaf(d2, tn, a.org[2]);
+    // coverage: the front-face fragment survives clipping (0 <= z <= w)
+    const float zc = fmaf(a.r2[2], pi2, fmaf(a.r2[1], pi1, fmaf(a.r2[0], pi0, a.r2[3])));
+    const float wc = fmaf(a.r3[2], pi2, fmaf(a.r3[1], pi1, fmaf(a.r3[0], pi0, a.r3[3])));
+    if (!(wc > 0.0f && zc >= 0.0f && zc <= wc)) return r;
+    const float po0 = fmaf(d0, tf, a.org[0]), po1 = fmaf(d1, tf, a.org[1]), po2 = fmaf(d2, tf, a.org[2]);
+    const float e0 = po0 - pi0, e1 = po1 - pi1, e2 = po2 - pi2;
+    const float dist = sqrtf(fmaf(e2, e2, fmaf(e1, e1, e0 * e0)));
+    const float q = dist / a.step_size;                                   // :46
+    r.n = q >= (float)a.max_steps ? a.max_steps : (int)q;
+    r.pxy = f2{(pi0 - a.box_min[0]) / a.box_range[0], (pi1 - a.box_min[1]) / a.box_range[1]};   // :49-54
+    r.pz = (pi2 - a.box_min[2]) / a.box_range[2];
+    r.sxy = f2{(a.step_size * d0) / a.box_range[0], (a.step_size * d1) / a.box_range[1]};       // :45
+    r.sz = (a.step_size * d2) / a.box_range[2];
+    return r;
+}
+
+// Render-target store: grey g (frag.glsl:80), uncovered pixels keep the
+// clear colour (0,0,0,1) (VulkanRenderPass.cpp:17-24).
+__device__ __forceinline__ void store_pixel(const MarchArgs& a, int x, int orow, bool covered, float g)
+{
+    char* row = (char*)a.out + (long long)orow * a.pitch;
+    if (a.format == 0) {
+        g = covered ? g : 0.0f;
+        reinterpret_cast<float4*>(row)[x] = make_float4(g, g, g, 1.0f);
+    } else {
+        unsigned int q = 0;
+        if (covered) {
+            float c = fminf(fmaxf(g, 0.0f), 1.0f);
+            if (a.format == 2)
+                c = c <= 0.0031308f ? c * 12.92f : fmaf(1.055f, powf(c, 1.0f / 2.4f), -0.055f);
+            q = (unsigned int)rintf(c * 255.0f);
+        }
+        reinterpret_cast<unsigned int*>(row)[x] = q | (q << 8) | (q << 16) | 0xff000000u;
+    }
+}
+
+// One ray of the grid path: setup, the march (frag.glsl:57-75), the
+// epilogue (:76-80) and the store.  Returns the executed steps.
+// The brick layouts run software-pipelined: step i+1's loads are issued
+// before step i is blended, so a wave has two steps of gathers in flight.
+// This costs VGPRs (67-73, 6-7 waves/SIMD) and is still faster: at 512^3
+// brick5 0.334 -> 0.280 ms (before the aligned loads), brick8 unchanged.
+// Fetching two steps ahead spilled to scratch and was 2.6x slower.  CORNER8 (the cache-resident
+// layout, one load per tap) is not: 0.51 -> 0.56 ms at 3840x2160x256.
+// Forcing 6 or 8 waves/SIMD (amdgpu_waves_per_eu) was slower in every case,
+// with or without pipelining.
+#ifndef VR_PIPE
+#define VR_PIPE 1
+#endif
+template <int LAYOUT, int WRAP, bool EARLY>
+__device__ __forceinline__ unsigned march_pixel(const MarchArgs& a, const FastCtx& f, int x, int orow)
+{
+    const Ray r = setup_ray(a, x, orow);
+    if constexpr (VR_PIPE && LAYOUT != LAYOUT_PLANAR && LAYOUT != LAYOUT_CORNER8) {
+        f2 pxy = r.pxy;
+        float pz = r.pz;
+        float acc = 0.0f;
+        int i = 0;
+        if (r.n > 0) {
+            TapRaw c0 = tap_fetch_at<LAYOUT>(a, f, 0, pxy, pz), c1 = tap_fetch_at<LAYOUT>(a, f, 1, pxy, pz);
+            TapRaw c2 = tap_fetch_at<LAYOUT>(a, f, 2, pxy, pz), c3 = tap_fetch_at<LAYOUT>(a, f, 3, pxy, pz);
+            for (; i < r.n; ++i) {
+                const f2 cxy = pxy;
+                const float cz = pz;
+                pxy = pxy + r.sxy;                                                        // :74
+                pz = pz + r.sz;
+                // the last step re-fetches its own (in-box) point: no branch
+                const bool more = i + 1 < r.n;
+                const f2 qxy = more ? pxy : cxy;
+                const float qz = more ? pz : cz;
+                const TapRaw n0 = tap_fetch_at<LAYOUT>(a, f, 0, qxy, qz), n1 = tap_fetch_at<LAYOUT>(a, f, 1, qxy, qz);
+                const TapRaw n2 = tap_fetch_at<LAYOUT>(a, f, 2, qxy, qz), n3 = tap_fetch_at<LAYOUT>(a, f, 3, qxy, qz);
+                const float t0 = tap_blend<LAYOUT>(c0), t1 = tap_blend<LAYOUT>(c1);
+                const float t2 = tap_blend<LAYOUT>(c2), t3 = tap_blend<LAYOUT>(c3);
+                acc = acc + ((t0 * t1) * (t2 + t3)) * a.scale;                           // :71-73
+                c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+                if constexpr (EARLY) {
+                    if (acc > a.acc_limit) { ++i; break; }
+                }
+            }
+        }
+        if (r.live) {
+            const float at = acc * a.step_size;
+            store_pixel(a, x, orow, r.n >= 0, 1.0f - spec_expf(a.density * fminf(-at, 0.0f)));
+        }
+        return r.n > 0 ? (unsigned)i : 0u;
+    }
+    f2 pxy = r.pxy;
+    float pz = r.pz;
+    float acc = 0.0f;
+    int i = 0;
+    for (; i < r.n; ++i) {
+        const float t0 = tap<LAYOUT, WRAP>(a, f, 0, pxy, pz);
+        const float t1 = tap<LAYOUT, WRAP>(a, f, 1, pxy, pz);
+        const float t2 = tap<LAYOUT, WRAP>(a, f, 2, pxy, pz);
+        const float t3 = tap<LAYOUT, WRAP>(a, f, 3, pxy, pz);
+        acc = acc + ((t0 * t1) * (t2 + t3)) * a.scale;                               // :71-73
+        pxy = pxy + r.sxy;                                                            // :74
+        pz = pz + r.sz;
+        if constexpr (EARLY) {
+            if (acc > a.acc_limit) { ++i; break; }
+        }
+    }
+    if (r.live) {
+        const float at = acc * a.step_size;                                          // :76
+        store_pixel(a, x, orow, r.n >= 0, 1.0f - spec_expf(a.density * fminf(-at, 0.0f)));   // :79
+    }
+    return r.n > 0 ? (unsigned)i : 0u;
+}
+
+// Procedural medium (BASELINE configs 2/3, build-defined; spec in
+// oracle/vr_oracle.h vro_procedural): fBm Perlin x (1 - Worley F1).
+template <bool TABLE>
+__device__ __forceinline__ float proc_density(const ProcParams& p, const float4* wt, float scale, float px, float py,
+                                              float pz)
+{
+    const float qx = px * p.grid_scale, qy = py * p.grid_scale, qz = pz * p.grid_scale;
+    float f = p.freq0, amp = 1.0f, fbm = 0.0f;
+    for (int o = 0; o < p.octaves; ++o) {
+        float pn;
+        if constexpr (TABLE) pn = noise::perlin_gt(wt + p.wt_n * p.wt_n * p.wt_n, p.seed_fbm, qx * f, qy * f, qz * f);
+        else pn = noise::perlin(p.seed_fbm, qx * f, qy * f, qz * f);
+        fbm = fmaf(amp, pn, fbm);
+        f = f * p.lacunarity;
+        amp = amp * p.gain;
+    }
+    const float wf = p.worley_freq;
+    float f1;
+    if constexpr (TABLE) f1 = noise::cellular_table(wt, p.wt_lo, p.wt_n, qx * wf, qy * wf, qz * wf) + 1.0f;
+    else f1 = noise::cellular(p.seed_worley, qx * wf, qy * wf, qz * wf) + 1.0f;
+    return fmaxf(fbm * (1.0f - f1), 0.0f) * scale;
+}
+
+// Pixel value of the procedural march: single scatter, or frag.glsl:76-80.
+template <bool SHADOW>
+__device__ __forceinline__ float proc_epilogue(const MarchArgs& a, float acc, float rad)
+{
+    if constexpr (SHADOW) {
+        return rad;
+    } else {
+        const float at = acc * a.step_size;
+        return 1.0f - spec_expf(a.density * fminf(-at, 0.0f));
+    }
+}
+
+template <bool SHADOW, bool EARLY, bool TABLE>
+__device__ __forceinline__ unsigned march_pixel_proc(const MarchArgs& a, const float4* wt, int x, int orow)
+{
+    const Ray r = setup_ray(a, x, orow);
+    const ProcParams& p = a.proc;
+    float P0 = r.pxy.x, P1 = r.pxy.y, P2 = r.pz;
+    float acc = 0.0f, rad = 0.0f, tv = 1.0f;
+    int i = 0;
+    unsigned evals = 0;   // shadow density evaluations
+    for (; i < r.n; ++i) {
+        const float rho = proc_density<TABLE>(p, wt, a.scale, P0, P1, P2);
+        if constexpr (SHADOW) {
+            if (rho > 0.0f) {
+                float q0 = P0, q1 = P1, q2 = P2, sl = 0.0f;
+                for (int j = 0; j < p.shadow_steps; ++j) {
+                    q0 = q0 + p.lstep[0]; q1 = q1 + p.lstep[1]; q2 = q2 + p.lstep[2];
+                    if (q0 >= 0.0f && q0 <= 1.0f && q1 >= 0.0f && q1 <= 1.0f && q2 >= 0.0f && q2 <= 1.0f) {
+                        sl = sl + proc_density<TABLE>(p, wt, a.scale, q0, q1, q2);
+                        ++evals;
+                    }
+                }
+                const float tl = spec_expf(-(sl * p.od));
+                rad = fmaf((tv * (rho * p.od)), tl, rad);
+            }
+        }
+        acc = acc + rho;
+        if constexpr (SHADOW) tv = spec_expf(-(acc * p.od));
+        P0 = P0 + r.sxy.x; P1 = P1 + r.sxy.y; P2 = P2 + r.sz;
+        if constexpr (EARLY) {
+            if (acc > a.acc_limit) { ++i; break; }
+        }
+    }
+    if (r.live) store_pixel(a, x, orow, r.n >= 0, proc_epilogue<SHADOW>(a, acc, rad));
+    if (r.n <= 0) return 0u;
+    return p.count_evals ? (unsigned)i + evals : (unsigned)i;
+}
+
+// Shadow-ray compaction (config 3).  In march_pixel_proc a wave runs all
+// shadow_steps density evaluations whenever ANY lane has rho > 0, so most
+// lanes idle.  Here a wave instead deals the (lane, shadow step) pairs of the
+// lanes that need them over all 64 lanes: cnt lanes need cnt * S evaluations,
+// done in ceil(cnt * S / 64) rounds.  The results go through LDS and each lane
+// then sums its own S values in step order, so the arithmetic (and the
+// repeated-addition shadow positions) is exactly march_pixel_proc's.
+// Requires wave-uniform control flow: every lane of the wave calls it.
+constexpr int kMaxCompactShadow = 8;
+struct ShadowLds {
+    float p[64][3];                      // positions of the lanes that need shadow rays (compacted)
+    float d[64 * kMaxCompactShadow];     // densities, [compact lane][shadow step]
+};
+
+template <bool EARLY, bool TABLE>
+__device__ __forceinline__ unsigned march_pixel_proc_compact(const MarchArgs& a, const float4* wt, int x, int orow,
+                                                             bool valid,
+                                                             ShadowLds* sh, unsigned* shadow_evals)
+{
+    Ray r{};
+    r.n = -1;
+    if (valid) r = setup_ray(a, x, orow);
+    const ProcParams& p = a.proc;
+    const int S = p.shadow_steps;
+    const int lane = threadIdx.x & 63;
+    float P0 = r.pxy.x, P1 = r.pxy.y, P2 = r.pz;
+    float acc = 0.0f, rad = 0.0f, tv = 1.0f;
+    int i = 0;
+    bool act = r.n > 0;
+    unsigned evals = 0;
+    for (;;) {
+        act = act && i < r.n;
+        if (__ballot(act) == 0) break;
+        float rho = 0.0f;
+        if (act) rho = proc_density<TABLE>(p, wt, a.scale, P0, P1, P2);
+        const bool need = act && rho > 0.0f;
+        const unsigned long long m = __ballot(need);
+        if (m) {
+            const int cnt = __popcll(m);
+            const int k = __popcll(m & ((1ull << lane) - 1ull));   // compact index of this lane
+            if (need) { sh->p[k][0] = P0; sh->p[k][1] = P1; sh->p[k][2] = P2; }
+            __builtin_amdgcn_wave_barrier();
+            const int total = cnt * S;
+            for (int base = 0; base < total; base += 64) {
+                const int pid = base + lane;
+                if (pid < total) {
+                    const int kk = pid / S, j = pid - kk * S;
+                    float q0 = sh->p[kk][0], q1 = sh->p[kk][1], q2 = sh->p[kk][2];
+                    for (int jj = 0; jj <= j; ++jj) { q0 = q0 + p.lstep[0]; q1 = q1 + p.lstep[1]; q2 = q2 + p.lstep[2]; }
+                    float d = 0.0f;   // outside the box: contributes exactly +0
+                    if (q0 >= 0.0f && q0 <= 1.0f && q1 >= 0.0f && q1 <= 1.0f && q2 >= 0.0f && q2 <= 1.0f) {
+                        d = proc_density<TABLE>(p, wt, a.scale, q0, q1, q2);
+                        ++evals;
+                    }
+                    sh->d[kk * S + j] = d;
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (need) {
+                float sl = 0.0f;
+                for (int j = 0; j < S; ++j) sl = sl + sh->d[k * S + j];
+                const float tl = spec_expf(-(sl * p.od));
+                rad = fmaf((tv * (rho * p.od)), tl, rad);
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (act) {
+            acc = acc + rho;
+            tv = spec_expf(-(acc * p.od));
+            P0 = P0 + r.sxy.x; P1 = P1 + r.sxy.y; P2 = P2 + r.sz;
+            ++i;
+            if constexpr (EARLY) {
+                if (acc > a.acc_limit) act = false;
+            }
+        }
+    }
+    if (r.live) store_pixel(a, x, orow, r.n >= 0, rad);
+    *shadow_evals = evals;
+    return r.n > 0 ? (unsigned)i : 0u;
+}
+
+// Lane -> pixel inside an 8x8 wave tile.  Default row-major, so each 16-lane
+// TA group of a narrow load (tools/tcp_calib.hip) is an 8x2 strip; compact
+// 4x4 groups were measured no better for brick5 and 15 % slower for brick8's
+// u16 loads.  BRICK5's 12-byte loads are looked up per 4 lanes, and there 2x2
+// pixel quads (4x4 of them per tile) are 2.6 % faster at 512^3 than 4x1 rows
+// (neutral for the other layouts, 20 % slower for planar).
+template <int LAYOUT = 0>
+__device__ __forceinline__ int lane_x(int lane)
+{
+    if constexpr (LAYOUT == LAYOUT_BRICK5) return ((lane >> 2) & 3) * 2 + (lane & 1);
+    else return lane & 7;
+}
+template <int LAYOUT = 0>
+__device__ __forceinline__ int lane_y(int lane)
+{
+    if constexpr (LAYOUT == LAYOUT_BRICK5) return (lane >> 4) * 2 + ((lane >> 1) & 1);
+    else return lane >> 3;
+}
+
+__device__ __forceinline__ void add_steps(const MarchArgs& a, unsigned long long cnt)
+{
+    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+    if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(a.step_counter, cnt);
+}
+
+// Kernel prologue for the fast layouts: buffer descriptors (wave-uniform,
+// from kernargs only) and the per-axis offset tables, built in LDS by the
+// whole workgroup.  The tables are the only LDS use and are read-only after
+// the barrier.
+template <int LAYOUT>
+__device__ __forceinline__ FastCtx fast_prologue(const MarchArgs& a, unsigned* lds)
+{
+    FastCtx f{};
+    if constexpr (LAYOUT != LAYOUT_PLANAR) {
+        for (int c = 0; c < 4; ++c)
+            f.rsrc[c] = __builtin_amdgcn_make_buffer_rsrc((void*)(a.vol + (size_t)c * a.plane_stride), (short)0,
+                                                          (int)a.plane_stride, 0x00020000);
+        const int nx1 = a.nx + 1, ny1 = a.ny + 1, nz1 = a.nz + 1;
+        for (int i = threadIdx.x; i < nx1 + ny1 + nz1; i += kThreads) {
+            const int axis = i < nx1 ? 0 : i < nx1 + ny1 ? 1 : 2;
+            const int pos = axis == 0 ? i : axis == 1 ? i - nx1 : i - nx1 - ny1;
+            lds[i] = axis_offset(a.geom, LAYOUT, axis, pos);   // once per workgroup
+        }
+        __syncthreads();
+        f.tx = lds;
+        f.ty = lds + nx1;
+        f.tz = lds + nx1 + ny1;
+    }
+    return f;
+}
+
+// Static schedule: one 16x16 tile per workgroup, one 8x8 sub-tile per wave.
+// Tile rows are dealt to XCDs round-robin: XCD x (= blockIdx % 8 under the
+// observed dispatch, a speed-only assumption) walks tile rows x, x+8, ...
+template <int LAYOUT, int WRAP, bool EARLY>
+__global__ __launch_bounds__(kThreads) void march_grid(const MarchArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned lds[];
+    const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+    const int k = j / a.tiles_x, tx = j - k * a.tiles_x;
+    const int ty = xcd + 8 * k;
+    if (ty >= a.tiles_y) return;   // whole workgroup: uniform, before the barrier
+    const FastCtx f = fast_prologue<LAYOUT>(a, lds);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int x = tx * kTile + (wave & 1) * 8 + lane_x<LAYOUT>(lane);
+    const int orow = ty * kTile + (wave >> 1) * 8 + lane_y<LAYOUT>(lane);
+    const unsigned steps = march_pixel<LAYOUT, WRAP, EARLY>(a, f, x, orow);
+    if (a.step_counter) add_steps(a, steps);
+}
+
+// Strided schedule: wave g (of nw) renders 8x8 tiles g, g + nw, g + 2nw, ...
+// of the row-major tile grid.  Its tiles sit 1/T of the image apart, so the
+// per-wave (and per-SIMD) work evens out without atomics.
+template <int LAYOUT, int WRAP, bool EARLY>
+__global__ __launch_bounds__(kThreads) void march_strided(const MarchArgs a, int nw)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned lds[];
+    const FastCtx f = fast_prologue<LAYOUT>(a, lds);
+    const int lane = threadIdx.x & 63;
+    const int g = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+    const int tiles_x8 = (a.width + 7) >> 3, rows8 = (a.out_rows + 7) >> 3;
+    const int ntiles = tiles_x8 * rows8;
+    unsigned long long steps = 0;
+    for (int t = g; t < ntiles; t += nw) {
+        const int ty = t / tiles_x8, tx = t - ty * tiles_x8;
+        steps += march_pixel<LAYOUT, WRAP, EARLY>(a, f, tx * 8 + lane_x<LAYOUT>(lane), ty * 8 + lane_y<LAYOUT>(lane));
+    }
+    if (a.step_counter) add_steps(a, steps);
+}
+
+// Ring schedule: wave k renders the k-th 8x8 tile of square rings around the
+// tile (cx, cy) under the projected box centre, where rays are longest.  The
+// longest-running waves start first (longest-processing-time order), so no
+// long wave is left to run alone at the end.  Ring r >= 1 holds 8r tiles and
+// starts at wave (2r-1)^2; waves whose tile is off the target exit at once.
+__device__ __forceinline__ bool ring_tile(int k, int cx, int cy, int* tx, int* ty)
+{
+    if (k == 0) { *tx = cx; *ty = cy; return true; }
+    const int r = (int)((sqrtf((float)k) + 1.0f) * 0.5f);
+    const int j = k - (2 * r - 1) * (2 * r - 1), side = j / (2 * r), t = j - side * 2 * r;
+    if (side == 0) { *tx = cx - r + t; *ty = cy - r; }
+    else if (side == 1) { *tx = cx + r; *ty = cy - r + t; }
+    else if (side == 2) { *tx = cx + r - t; *ty = cy + r; }
+    else { *tx = cx - r; *ty = cy + r - t; }
+    return true;
+}
+
+template <int LAYOUT, int WRAP, bool EARLY>
+__global__ __launch_bounds__(kThreads) void march_rings(const MarchArgs a, int cx, int cy, int nw, int npos)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned lds[];
+    const FastCtx f = fast_prologue<LAYOUT>(a, lds);
+    const int lane = threadIdx.x & 63;
+    const int tiles_x8 = (a.width + 7) >> 3, rows8 = (a.out_rows + 7) >> 3;
+    unsigned long long steps = 0;
+    // wave g takes ring positions g, g + nw, ... (nw = all waves): fewer
+    // workgroups, so fewer LDS-table prologues, in the same inside-out order
+    for (int k = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6); k < npos; k += nw) {
+        int tx, ty;
+        ring_tile(k, cx, cy, &tx, &ty);
+        if (tx >= 0 && tx < tiles_x8 && ty >= 0 && ty < rows8)
+            steps += march_pixel<LAYOUT, WRAP, EARLY>(a, f, tx * 8 + lane_x<LAYOUT>(lane),
+                                                      ty * 8 + lane_y<LAYOUT>(lane));
+    }
+    if (a.step_counter) add_steps(a, steps);
+}
+
+// XCD-row schedule: one 8x8 tile per wave, 4 horizontally adjacent tiles per
+// workgroup.  8-px tile rows are dealt to XCDs round-robin: XCD x walks rows
+// x, x+8, ... (blockIdx % 8, speed-only).  Rows interleave, so the balance
+// holds, and a row's neighbours share one L2.
+template <int LAYOUT, int WRAP, bool EARLY>
+__global__ __launch_bounds__(kThreads) void march_xcdrows(const MarchArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned lds[];
+    const int tiles_x8 = (a.width + 7) >> 3, rows8 = (a.out_rows + 7) >> 3;
+    const int groups = (tiles_x8 + 3) >> 2;
+    const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+    const int k = j / groups, gx = j - k * groups;
+    const int ty = xcd + 8 * k;
+    if (ty >= rows8) return;   // whole workgroup, before the barrier
+    const FastCtx f = fast_prologue<LAYOUT>(a, lds);
+    const int lane = threadIdx.x & 63, tx = gx * 4 + (threadIdx.x >> 6);
+    unsigned long long steps = 0;
+    if (tx < tiles_x8) steps = march_pixel<LAYOUT, WRAP, EARLY>(a, f, tx * 8 + lane_x<LAYOUT>(lane), ty * 8 + lane_y<LAYOUT>(lane));
+    if (a.step_counter) add_steps(a, steps);
+}
+
+// Queue schedule: persistent waves pull 8x8 tiles from 8 queues, one per
+// XCD group (blockIdx % 8, speed-only).  Queue q owns the 16-row tile pairs
+// p = q, q+8, ..., walked column by column.  heads[] is zeroed by a memset
+// before every launch.  Every wave leaves once its queue is drained, so the
+// grid always completes.
+template <int LAYOUT, int WRAP, bool EARLY>
+__global__ __launch_bounds__(kThreads) void march_queue(const MarchArgs a, int* __restrict__ heads)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned lds[];
+    const FastCtx f = fast_prologue<LAYOUT>(a, lds);
+    const int q = blockIdx.x & 7, lane = threadIdx.x & 63;
+    const int tiles_x8 = (a.width + 7) >> 3, rows8 = (a.out_rows + 7) >> 3;
+    const int pairs = (rows8 + 1) >> 1;
+    const int per_pair = 2 * tiles_x8;
+    const int count = q < pairs ? ((pairs - q + 7) >> 3) * per_pair : 0;
+    unsigned long long steps = 0;
+    for (;;) {
+        int k = 0;
+        if (lane == 0) k = atomicAdd(&heads[q], 1);
+        k = __shfl(k, 0);
+        if (k >= count) break;
+        const int m = k / per_pair, rem = k - m * per_pair;
+        const int row8 = 2 * (q + 8 * m) + (rem & 1), tx = rem >> 1;
+        if (row8 >= rows8) continue;
+        steps += march_pixel<LAYOUT, WRAP, EARLY>(a, f, tx * 8 + lane_x<LAYOUT>(lane), row8 * 8 + lane_y<LAYOUT>(lane));
+    }
+    if (a.step_counter) add_steps(a, steps);
+}
+
+// Procedural medium: one 8x8 tile per wave (compute-bound; no volume), in
+// row order (cx < 0) or in rings around tile (cx, cy) (see march_rings).
+// Noise tables for the workgroup (dynamic LDS): the Worley cell table
+// (wt_n^3 float4) followed by the 16 Perlin gradient vectors, built before
+// any wave may leave.  Returns null when the tables are off (wt_n = 0).
+__device__ __forceinline__ const float4* worley_table(const ProcParams& p, float4* lds)
+{
+    if (p.wt_n <= 0) return nullptr;
+    const int n = p.wt_n, cells = n * n * n;
+    for (int i = threadIdx.x; i < cells; i += kThreads) {
+        const int ix = i % n, iy = (i / n) % n, iz = i / (n * n);
+        lds[i] = noise::cellular_cell(p.seed_worley, p.wt_lo + ix, p.wt_lo + iy, p.wt_lo + iz);
+    }
+    if (threadIdx.x < 16) lds[cells + threadIdx.x] = noise::grad_entry(threadIdx.x);
+    __syncthreads();
+    return lds;
+}
+
+template <bool SHADOW, bool EARLY, bool TABLE>
+__global__ __launch_bounds__(kThreads) void march_proc(const MarchArgs a, int cx, int cy)
+{
+    extern __shared__ float4 wt_lds[];
+    const float4* wt = worley_table(a.proc, wt_lds);
+    const int lane = threadIdx.x & 63;
+    const int t = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+    const int tiles_x8 = (a.width + 7) >> 3, rows8 = (a.out_rows + 7) >> 3;
+    unsigned long long steps = 0;
+    int tx, ty;
+    if (cx >= 0) {
+        ring_tile(t, cx, cy, &tx, &ty);
+    } else {
+        ty = t / tiles_x8;
+        tx = t - ty * tiles_x8;
+    }
+    if (tx >= 0 && tx < tiles_x8 && ty >= 0 && ty < rows8) {
+        steps = march_pixel_proc<SHADOW, EARLY, TABLE>(a, wt, tx * 8 + lane_x(lane), ty * 8 + lane_y(lane));
+    }
+    if (a.step_counter) add_steps(a, steps);
+}
+
+// ---- procedural, cost-sorted schedule ----
+// A ray's cost is its step count n (a3), known after the ray setup.  Pass 1
+// writes every pixel with n <= 0 and builds a histogram of n; pass 2 turns it
+// into descending-n offsets; pass 3 scatters the packed pixel ids (orow << 16
+// | x) in that order; the march then gives wave w the sorted pixels
+// [64w, 64w + 64).  Lanes of a wave share n (no loop divergence) and the
+// longest rays start first (longest-processing-time order, no tail).
+constexpr int kKeyBins = 1024;
+// Pixels per thread of the sort passes: fewer blocks -> fewer global atomics
+// on hot bins.  Measured 2/4/8/16: 16 is best (bin 21 us, scatter 11 us at
+// 1080p).  Wave-aggregated LDS increments (one atomic per distinct key) were
+// slower than the plain LDS atomics.
+constexpr int kSortPixelsPerThread = 16;
+__device__ __forceinline__ int cost_key(int n) { return n < kKeyBins - 1 ? n : kKeyBins - 1; }
+
+template <bool SHADOW>
+__global__ __launch_bounds__(256) void proc_bin(const MarchArgs a, unsigned* __restrict__ hist,
+                                                unsigned short* __restrict__ keys)
+{
+    __shared__ unsigned h[kKeyBins];
+    for (int i = threadIdx.x; i < kKeyBins; i += 256) h[i] = 0;
+    __syncthreads();
+    for (int it = 0; it < kSortPixelsPerThread; ++it) {
+        const unsigned pix = (blockIdx.x * kSortPixelsPerThread + it) * 256u + threadIdx.x;   // < 2^31 (host check)
+        const int orow = (int)(pix / (unsigned)a.width), x = (int)(pix - (unsigned)orow * (unsigned)a.width);
+        if (orow >= a.out_rows) break;
+        const Ray r = setup_ray(a, x, orow);
+        int key = 0;
+        if (r.n > 0) {
+            key = cost_key(r.n);
+            atomicAdd(&h[key], 1u);
+        } else if (r.live) {
+            store_pixel(a, x, orow, r.n >= 0, proc_epilogue<SHADOW>(a, 0.0f, 0.0f));   // 0 steps
+        }
+        keys[pix] = (unsigned short)key;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kKeyBins; i += 256)
+        if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+
+// hist[kKeyBins] -> cursor[kKeyBins] (start of each key, descending keys) and
+// total at cursor[kKeyBins].  One workgroup of kKeyBins threads.
+[[maybe_unused]] __global__ __launch_bounds__(kKeyBins) void proc_scan(const unsigned* __restrict__ hist, unsigned* __restrict__ cursor)
+{
+    __shared__ unsigned sc[kKeyBins];
+    const int t = threadIdx.x;
+    sc[t] = hist[kKeyBins - 1 - t];   // descending key order
+    __syncthreads();
+    for (int off = 1; off < kKeyBins; off <<= 1) {
+        const unsigned v = t >= off ? sc[t - off] : 0u;
+        __syncthreads();
+        sc[t] += v;
+        __syncthreads();
+    }
+    const int key = kKeyBins - 1 - t;
+    cursor[key] = sc[t] - hist[key];   // exclusive
+    if (t == kKeyBins - 1) cursor[kKeyBins] = sc[t];
+}
+
+[[maybe_unused]] __global__ __launch_bounds__(256) void proc_scatter(const MarchArgs a, const unsigned short* __restrict__ keys,
+                                                    unsigned* __restrict__ cursor, unsigned* __restrict__ order)
+{
+    __shared__ unsigned h[kKeyBins];
+    for (int i = threadIdx.x; i < kKeyBins; i += 256) h[i] = 0;
+    __syncthreads();
+    int key[kSortPixelsPerThread];
+    unsigned rank[kSortPixelsPerThread], packed[kSortPixelsPerThread];
+    for (int it = 0; it < kSortPixelsPerThread; ++it) {
+        key[it] = -1;
+        const unsigned pix = (blockIdx.x * kSortPixelsPerThread + it) * 256u + threadIdx.x;
+        const int orow = (int)(pix / (unsigned)a.width), x = (int)(pix - (unsigned)orow * (unsigned)a.width);
+        if (orow < a.out_rows) {
+            const int k = keys[pix];
+            if (k > 0) {
+                key[it] = k;
+                rank[it] = atomicAdd(&h[k], 1u);
+                packed[it] = ((unsigned)orow << 16) | (unsigned)x;
+            }
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kKeyBins; i += 256)
+        if (h[i]) h[i] = atomicAdd(&cursor[i], h[i]);   // block's base in the sorted list
+    __syncthreads();
+    for (int it = 0; it < kSortPixelsPerThread; ++it)
+        if (key[it] >= 0) order[h[key[it]] + rank[it]] = packed[it];
+}
+
+template <bool SHADOW, bool EARLY, bool TABLE>
+__global__ __launch_bounds__(kThreads) void march_proc_sorted(const MarchArgs a, const unsigned* __restrict__ order,
+                                                              const unsigned* __restrict__ total_ptr)
+{
+    extern __shared__ float4 wt_lds[];
+    const float4* wt = worley_table(a.proc, wt_lds);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const unsigned total = *total_ptr;
+    const unsigned base = (blockIdx.x * (kThreads / 64) + wave) * 64u;
+    if (base >= total) return;   // wave-uniform
+    const unsigned idx = base + lane;
+    const bool valid = idx < total;
+    int x = 0, orow = 0;
+    if (valid) {
+        const unsigned pk = order[idx];
+        x = (int)(pk & 0xffffu);
+        orow = (int)(pk >> 16);
+    }
+    unsigned long long steps;
+    if constexpr (SHADOW) {
+        __shared__ ShadowLds sh[kThreads / 64];
+        if (a.proc.shadow_steps <= kMaxCompactShadow) {
+            unsigned ev = 0;
+            steps = march_pixel_proc_compact<EARLY, TABLE>(a, wt, x, orow, valid, &sh[wave], &ev);
+            if (a.proc.count_evals) steps += ev;
+        } else {
+            steps = valid ? march_pixel_proc<true, EARLY, TABLE>(a, wt, x, orow) : 0u;
+        }
+    } else {
+        steps = valid ? march_pixel_proc<false, EARLY, TABLE>(a, wt, x, orow) : 0u;
+    }
+    if (a.step_counter) add_steps(a, steps);
+}
+
+template <int L, int W>
+hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStream_t s)
+{
+    const size_t lds = L == LAYOUT_PLANAR ? 0 : (size_t)(a.nx + a.ny + a.nz + 3) * sizeof(unsigned);
+    const dim3 block(kThreads);
+    if (sc.kind == SCHED_STRIDED) {
+        const int tiles = ((a.width + 7) >> 3) * ((a.out_rows + 7) >> 3);
+        const int tpw = sc.tiles_per_wave > 0 ? sc.tiles_per_wave : 1;
+        const int nw = (tiles + tpw - 1) / tpw;
+        const dim3 grid((nw + 3) / 4);
+        if (early)
+            hipLaunchKernelGGL((march_strided<L, W, true>), grid, block, lds, s, a, 4 * (int)grid.x);
+        else
+            hipLaunchKernelGGL((march_strided<L, W, false>), grid, block, lds, s, a, 4 * (int)grid.x);
+        return hipGetLastError();
+    }
+    if (sc.kind == SCHED_RINGS) {
+        const int tiles_x8 = (a.width + 7) >> 3, rows8 = (a.out_rows + 7) >> 3;
+        const int cx = min(max(sc.center_x >> 3, 0), tiles_x8 - 1), cy = min(max(sc.center_y >> 3, 0), rows8 - 1);
+        const int R = max(max(cx, tiles_x8 - 1 - cx), max(cy, rows8 - 1 - cy));
+        const int npos = (2 * R + 1) * (2 * R + 1);
+        const int tpw = sc.tiles_per_wave > 0 ? sc.tiles_per_wave : 1;
+        const int nw = (npos + tpw - 1) / tpw;
+        const dim3 grid((unsigned)((nw + 3) / 4));
+        if (early)
+            hipLaunchKernelGGL((march_rings<L, W, true>), grid, block, lds, s, a, cx, cy, 4 * (int)grid.x, npos);
+        else
+            hipLaunchKernelGGL((march_rings<L, W, false>), grid, block, lds, s, a, cx, cy, 4 * (int)grid.x, npos);
+        return hipGetLastError();
+    }
+    if (sc.kind == SCHED_XCDROWS) {
+        const int groups = (((a.width + 7) >> 3) + 3) >> 2, rows8 = (a.out_rows + 7) >> 3;
+        const dim3 grid(8 * ((rows8 + 7) / 8) * groups);
+        if (early)
+            hipLaunchKernelGGL((march_xcdrows<L, W, true>), grid, block, lds, s, a);
+        else
+            hipLaunchKernelGGL((march_xcdrows<L, W, false>), grid, block, lds, s, a);
+        return hipGetLastError();
+    }
+    if (sc.kind == SCHED_QUEUE) {
+        hipError_t e = hipMemsetAsync(sc.heads, 0, 32, s);
+        if (e != hipSuccess) return e;
+        const dim3 grid(256 * sc.waves_per_simd);
+        if (early)
+            hipLaunchKernelGGL((march_queue<L, W, true>), grid, block, lds, s, a, sc.heads);
+        else
+            hipLaunchKernelGGL((march_queue<L, W, false>), grid, block, lds, s, a, sc.heads);
+        return hipGetLastError();
+    }
+    const dim3 grid(a.num_blocks);
+    if (early)
+        hipLaunchKernelGGL((march_grid<L, W, true>), grid, block, lds, s, a);
+    else
+        hipLaunchKernelGGL((march_grid<L, W, false>), grid, block, lds, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace
+}  // namespace vr
