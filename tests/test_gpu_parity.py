@@ -524,3 +524,22 @@ def test_prepared_launchers_match_render(r, vol128):
     full = r.render(W, H, vr.FMT_RGBA8_UNORM)
     torch.cuda.synchronize()
     assert torch.equal(frame, full)
+
+
+def test_procedural_needs_no_volume(oracle):
+    """A context that never had a volume renders the procedural medium; with
+    the medium off it reports VR_ERR_NO_VOLUME."""
+    with vr.Renderer(0) as fresh:
+        osd, gsd = vr.reference_shader_data(1.0)
+        fresh.set_shader_data(osd, gsd)
+        fresh.set_march(vr.march_defaults(max_steps=32))
+        fresh.set_procedural()
+        p = oracle.procedural_from(fresh.procedural)
+        img = fresh.render(64, 64, vr.FMT_RGBA32F).cpu().numpy()
+        obj, glob = vr.shader_data_arrays(osd, gsd)
+        ref, _ = oracle.render_procedural(p, obj, glob, oracle.march(32), 64, 64, 0)
+        assert_exact(img, ref)
+        fresh.set_procedural(enabled=0)
+        with pytest.raises(VRError) as e:
+            fresh.render(64, 64, vr.FMT_RGBA32F)
+        assert e.value.status == 3   # VR_ERR_NO_VOLUME
