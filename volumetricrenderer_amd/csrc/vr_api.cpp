@@ -700,7 +700,7 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
         const int lo = (int)std::floor(std::min(0.0, G)) - 2, hi = (int)std::ceil(std::max(0.0, G)) + 2;
         const int n = hi - lo + 1;
         q.wt_lo = lo;
-        q.wt_n = (std::fabs(G) < 64.0 && (long long)n * n * n * 16 <= kMaxWorleyTableBytes) ? n : 0;
+        q.wt_n = (std::fabs(G) < 64.0 && (long long)n * n * n * 16 <= kMaxWorleyTableBytes) ? n : 0;   // + 8 KiB pairs
     }
     Plan pl{LAYOUT_PLANAR, WRAP_CLAMP, false};
     if (!c->proc.enabled) make_plan(c, &a, &pl);

@@ -25,7 +25,7 @@ hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_bu
     if (a.width <= 0 || a.out_rows <= 0) return hipSuccess;
     const bool shadow = a.proc.shadow_steps > 0;
     const size_t wt_bytes =
-        a.proc.wt_n > 0 ? ((size_t)a.proc.wt_n * a.proc.wt_n * a.proc.wt_n + 16) * sizeof(float4) : 0;
+        a.proc.wt_n > 0 ? ((size_t)a.proc.wt_n * a.proc.wt_n * a.proc.wt_n + 512) * sizeof(float4) : 0;
     if (sort_buf) {
         unsigned* hist = static_cast<unsigned*>(sort_buf);
         unsigned* cursor = hist + kKeyBins;            // kKeyBins + 1 entries

@@ -372,7 +372,7 @@ __device__ __forceinline__ float proc_density(const ProcParams& p, const float4*
     float f = p.freq0, amp = 1.0f, fbm = 0.0f;
     for (int o = 0; o < p.octaves; ++o) {
         float pn;
-        if constexpr (TABLE) pn = noise::perlin_gt(wt + p.wt_n * p.wt_n * p.wt_n, p.seed_fbm, qx * f, qy * f, qz * f);
+        if constexpr (TABLE) pn = noise::perlin_gp(wt + p.wt_n * p.wt_n * p.wt_n, p.seed_fbm, qx * f, qy * f, qz * f);
         else pn = noise::perlin(p.seed_fbm, qx * f, qy * f, qz * f);
         fbm = fmaf(amp, pn, fbm);
         f = f * p.lacunarity;
@@ -695,8 +695,9 @@ __global__ __launch_bounds__(kThreads) void march_queue(const MarchArgs a, int* 
 // Procedural medium: one 8x8 tile per wave (compute-bound; no volume), in
 // row order (cx < 0) or in rings around tile (cx, cy) (see march_rings).
 // Noise tables for the workgroup (dynamic LDS): the Worley cell table
-// (wt_n^3 float4) followed by the 16 Perlin gradient vectors, built before
-// any wave may leave.  Returns null when the tables are off (wt_n = 0).
+// (wt_n^3 float4) followed by the 256 Perlin gradient pairs (2 float4 each),
+// built before any wave may leave.  Returns null when the tables are off
+// (wt_n = 0).
 __device__ __forceinline__ const float4* worley_table(const ProcParams& p, float4* lds)
 {
     if (p.wt_n <= 0) return nullptr;
@@ -705,7 +706,7 @@ __device__ __forceinline__ const float4* worley_table(const ProcParams& p, float
         const int ix = i % n, iy = (i / n) % n, iz = i / (n * n);
         lds[i] = noise::cellular_cell(p.seed_worley, p.wt_lo + ix, p.wt_lo + iy, p.wt_lo + iz);
     }
-    if (threadIdx.x < 16) lds[cells + threadIdx.x] = noise::grad_entry(threadIdx.x);
+    noise::grad_pair_entry(threadIdx.x, lds + cells + 2 * threadIdx.x);   // 256 pairs, one per thread
     __syncthreads();
     return lds;
 }

@@ -100,6 +100,46 @@ __device__ inline float perlin_gt(const float4* __restrict__ gt, int32_t seed, f
     return 0.964921414852142333984375f * lerp(lerp(l00, l10, v), lerp(l01, l11, v), w);
 }
 
+// The same Perlin with the two x-neighbour corners of each (y, z) edge done
+// together in packed math: a 256-entry table of gradient PAIRS, entry
+// ka | kb << 4 = {gx_a, gx_b, gy_a, gy_b} {gz_a, gz_b, 0, 0} (32 B), so
+// one b128 + one b64 read yields register pairs that feed v_pk_mul /
+// v_pk_fma directly: 3 packed ops per corner pair.  A packed fma is two
+// IEEE fmas, so every value equals perlin_gt()'s.
+typedef float vr_pf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void grad_pair_entry(int e, float4* out)
+{
+    const float4 a = grad_entry(e & 15), b = grad_entry(e >> 4);
+    out[0] = make_float4(a.x, b.x, a.y, b.y);
+    out[1] = make_float4(a.z, b.z, 0.0f, 0.0f);
+}
+__device__ __forceinline__ float gdot_pair_lerp(const float4* __restrict__ gp, int32_t ha, int32_t hb, vr_pf2 fx,
+                                                float fy, float fz, float u)
+{
+    const float4* e = gp + 2 * ((ha & 15) | ((hb & 15) << 4));
+    const float4 g0 = e[0];
+    const float2 g1 = *reinterpret_cast<const float2*>(e + 1);
+    const vr_pf2 dz = vr_pf2{g1.x, g1.y} * vr_pf2{fz, fz};
+    const vr_pf2 dy = __builtin_elementwise_fma(vr_pf2{g0.z, g0.w}, vr_pf2{fy, fy}, dz);
+    const vr_pf2 d = __builtin_elementwise_fma(vr_pf2{g0.x, g0.y}, fx, dy);
+    return lerp(d.x, d.y, u);
+}
+__device__ inline float perlin_gp(const float4* __restrict__ gp, int32_t seed, float x, float y, float z)
+{
+    const float xs = floorf(x), ys = floorf(y), zs = floorf(z);
+    const int32_t x0 = wmul((int32_t)xs, kPX), y0 = wmul((int32_t)ys, kPY), z0 = wmul((int32_t)zs, kPZ);
+    const int32_t x1 = wadd(x0, kPX), y1 = wadd(y0, kPY), z1 = wadd(z0, kPZ);
+    const float xf0 = x - xs, yf0 = y - ys, zf0 = z - zs;
+    const float xf1 = xf0 - 1.0f, yf1 = yf0 - 1.0f, zf1 = zf0 - 1.0f;
+    const float u = quintic(xf0), v = quintic(yf0), w = quintic(zf0);
+    const vr_pf2 fx = {xf0, xf1};
+    const float l00 = gdot_pair_lerp(gp, hash(seed, x0, y0, z0), hash(seed, x1, y0, z0), fx, yf0, zf0, u);
+    const float l10 = gdot_pair_lerp(gp, hash(seed, x0, y1, z0), hash(seed, x1, y1, z0), fx, yf1, zf0, u);
+    const float l01 = gdot_pair_lerp(gp, hash(seed, x0, y0, z1), hash(seed, x1, y0, z1), fx, yf0, zf1, u);
+    const float l11 = gdot_pair_lerp(gp, hash(seed, x0, y1, z1), hash(seed, x1, y1, z1), fx, yf1, zf1, u);
+    return 0.964921414852142333984375f * lerp(lerp(l00, l10, v), lerp(l01, l11, v), w);
+}
+
 __device__ __forceinline__ float simplex_corner(int32_t seed, int32_t xp, int32_t yp, int32_t zp,
                                                 float x, float y, float z)
 {
