@@ -61,15 +61,14 @@ __device__ inline float perlin(int32_t seed, float x, float y, float z)
     return 0.964921414852142333984375f * lerp(lerp(l00, l10, v), lerp(l01, l11, v), w);
 }
 
-// Perlin with the gradient dot product from a 16-entry table (the LDS table
-// of the procedural march): entry k holds the (gx, gy, gz) in {-1, 0, 1} that
-// grad() selects for hash bits k = hash & 15, and the dot is
+// Perlin with the gradient dot product from a table (the LDS table of the
+// procedural march): for hash bits k = hash & 15, grad_entry(k) is the
+// (gx, gy, gz) in {-1, 0, 1} that grad() selects, and the dot is
 // fma(gx, fx, fma(gy, fy, gz * fz)).  Exactly one component is 0, so each
 // fma adds one exact term to an exact term: the value is grad()'s u + v,
 // correctly rounded once.  Only the sign of an exact zero can differ, and a
 // zero (of either sign) leaves every later sum, lerp and max unchanged, so
-// the rendered pixels are identical.  9 VALU ops + 1 LDS read per corner
-// instead of ~20.
+// the rendered pixels are identical.
 __device__ __forceinline__ float4 grad_entry(int k)
 {
     float g[3] = {0.0f, 0.0f, 0.0f};
@@ -80,32 +79,13 @@ __device__ __forceinline__ float4 grad_entry(int k)
     g[va] += (k & 2) ? -1.0f : 1.0f;
     return make_float4(g[0], g[1], g[2], 0.0f);
 }
-__device__ __forceinline__ float gdot(const float4* __restrict__ gt, int32_t h, float fx, float fy, float fz)
-{
-    const float4 g = gt[h & 15];
-    return fmaf(g.x, fx, fmaf(g.y, fy, g.z * fz));
-}
-__device__ inline float perlin_gt(const float4* __restrict__ gt, int32_t seed, float x, float y, float z)
-{
-    const float xs = floorf(x), ys = floorf(y), zs = floorf(z);
-    const int32_t x0 = wmul((int32_t)xs, kPX), y0 = wmul((int32_t)ys, kPY), z0 = wmul((int32_t)zs, kPZ);
-    const int32_t x1 = wadd(x0, kPX), y1 = wadd(y0, kPY), z1 = wadd(z0, kPZ);
-    const float xf0 = x - xs, yf0 = y - ys, zf0 = z - zs;
-    const float xf1 = xf0 - 1.0f, yf1 = yf0 - 1.0f, zf1 = zf0 - 1.0f;
-    const float u = quintic(xf0), v = quintic(yf0), w = quintic(zf0);
-    const float l00 = lerp(gdot(gt, hash(seed, x0, y0, z0), xf0, yf0, zf0), gdot(gt, hash(seed, x1, y0, z0), xf1, yf0, zf0), u);
-    const float l10 = lerp(gdot(gt, hash(seed, x0, y1, z0), xf0, yf1, zf0), gdot(gt, hash(seed, x1, y1, z0), xf1, yf1, zf0), u);
-    const float l01 = lerp(gdot(gt, hash(seed, x0, y0, z1), xf0, yf0, zf1), gdot(gt, hash(seed, x1, y0, z1), xf1, yf0, zf1), u);
-    const float l11 = lerp(gdot(gt, hash(seed, x0, y1, z1), xf0, yf1, zf1), gdot(gt, hash(seed, x1, y1, z1), xf1, yf1, zf1), u);
-    return 0.964921414852142333984375f * lerp(lerp(l00, l10, v), lerp(l01, l11, v), w);
-}
-
-// The same Perlin with the two x-neighbour corners of each (y, z) edge done
+// perlin_gp: the two x-neighbour corners of each (y, z) edge are done
 // together in packed math: a 256-entry table of gradient PAIRS, entry
 // ka | kb << 4 = {gx_a, gx_b, gy_a, gy_b} {gz_a, gz_b, 0, 0} (32 B), so
 // one b128 + one b64 read yields register pairs that feed v_pk_mul /
 // v_pk_fma directly: 3 packed ops per corner pair.  A packed fma is two
-// IEEE fmas, so every value equals perlin_gt()'s.
+// IEEE fmas.  Per octave 114 VALU + 8 LDS reads, against ~193 VALU for
+// perlin().
 typedef float vr_pf2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void grad_pair_entry(int e, float4* out)
 {
