@@ -97,6 +97,19 @@ class BandSharder:
         gather buffers and frames are double-buffered.  Each buffer of a
         parity is reused only after the stream order has retired its last
         reader.  Returns the last frame (rank 0) or band set."""
+        if self.world == 1 and hasattr(self.r, "prepare_render"):
+            # one rank: the frame is the render; launch it through a prepared
+            # launcher (the ctypes arguments are built once)
+            if getattr(self, "_launch1", None) is None:
+                self._launch1 = self.r.prepare_render(self.width, self.height, self.fmt, self.local)
+            for i in range(k):
+                ev = events[i] if events else None
+                if ev is not None:
+                    ev[0].record()
+                self._launch1()
+                if ev is not None:
+                    ev[1].record()
+            return self.frame_buf
         if self.world == 1 or (self.local.is_cuda and dist.get_backend(self.group) == "gloo"):
             out = None
             for i in range(k):
@@ -158,6 +171,7 @@ class BandSharder:
         return P["frame"][last] if self.rank == 0 else P["local"][last]
 
     def close(self):
+        self._launch1 = None
         self.local = None
         self.gathered = None
         self.frame_buf = None
