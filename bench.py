@@ -176,10 +176,10 @@ def main() -> int:
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    # HIP events around the march launch of every frame at N = 1; every 4th
-    # frame at N > 1, where a rank's frame is ~0.03 ms and two event records
-    # per frame are a visible share of the host time per frame
-    ev_every = 1 if world == 1 else 4
+    # HIP events around the march launch of every 4th frame: the sample of
+    # launch durations the roofline uses.  Two event records per frame cost a
+    # few microseconds of queue time between frames (and, at N > 1, host time)
+    ev_every = 4
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           if i % ev_every == 0 else None for i in range(args.steps)]
     t0 = time.perf_counter()
