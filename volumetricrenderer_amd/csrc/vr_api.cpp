@@ -195,6 +195,9 @@ vr_status make_plan(Ctx* c, MarchArgs* a, Plan* p)
 {
     const vr_march_params& m = c->march;
     tap_constants(c, a->tap_S, a->tap_T);
+    a->zero_offsets = 1;
+    for (int t = 0; t < 4; ++t)
+        for (int k = 0; k < 3; ++k) a->zero_offsets &= a->tap_T[t][k] == 0.5f;
     const bool exact = clamp_is_exact(c, a->tap_S, a->tap_T);
     if (!c->fast_layout) {
         p->layout = LAYOUT_PLANAR;

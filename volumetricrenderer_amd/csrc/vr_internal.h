@@ -95,6 +95,7 @@ struct MarchArgs {
     // tap t samples padded texel coordinate g = fma(P, tap_S, tap_T)
     // (= u*N + 0.5 with u = P*s_t + o_t, frag.glsl:66-69)
     float tap_S[4][3], tap_T[4][3];
+    int zero_offsets;            // every tap_T is exactly 0.5 (no MediaScroll offsets)
     // volume
     int nx, ny, nz;
     const uint8_t* vol;          // channel plane 0; plane c at vol + c*plane_stride

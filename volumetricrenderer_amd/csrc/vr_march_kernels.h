@@ -172,11 +172,31 @@ __device__ __forceinline__ float tap_fast(const FastCtx& f, int ch, float gx, fl
     return tap_blend<LAYOUT>(tap_fetch<LAYOUT>(f, ch, gx, gy, gz));
 }
 
-template <int LAYOUT>
+// Two CORNER8 taps blended together, one tap per packed-fp32 lane: every
+// stage (x, y, z lerps and the 1/255 scale) is one packed op for both taps,
+// where blend() needs scalar ops for its last stage.  Each lane runs
+// blend()'s exact op sequence, so {tA, tB} equal two blend() calls.
+__device__ __forceinline__ f2 blend_pair_c8(const TapRaw& A, const TapRaw& B)
+{
+    const f2 wx = {A.wx, B.wx}, wy = {A.wy, B.wy}, wz = {A.wz, B.wz};
+    const f2 x00 = lerp2(f2{ubyte<0>(A.q0), ubyte<0>(B.q0)}, f2{ubyte<1>(A.q0), ubyte<1>(B.q0)}, wx);
+    const f2 x10 = lerp2(f2{ubyte<2>(A.q0), ubyte<2>(B.q0)}, f2{ubyte<3>(A.q0), ubyte<3>(B.q0)}, wx);
+    const f2 x01 = lerp2(f2{ubyte<0>(A.q1), ubyte<0>(B.q1)}, f2{ubyte<1>(A.q1), ubyte<1>(B.q1)}, wx);
+    const f2 x11 = lerp2(f2{ubyte<2>(A.q1), ubyte<2>(B.q1)}, f2{ubyte<3>(A.q1), ubyte<3>(B.q1)}, wx);
+    const f2 y0 = lerp2(x00, x10, wy), y1 = lerp2(x01, x11, wy);
+    return lerp2(y0, y1, wz) * f2{1.0f / 255.0f, 1.0f / 255.0f};
+}
+
+// ZO: every tap offset T_t is 0.5 (no MediaScroll offset; the reference's
+// case), so T is the inline constant 0.5 instead of a kernel
+// argument.  An fma may read one scalar register, so with S and T both in
+// SGPRs each tap needed v_mov copies: 8 VALU ops per step.
+template <int LAYOUT, bool ZO = false>
 __device__ __forceinline__ TapRaw tap_fetch_at(const MarchArgs& a, const FastCtx& f, int t, f2 pxy, float pz)
 {
-    const f2 gxy = __builtin_elementwise_fma(pxy, f2{a.tap_S[t][0], a.tap_S[t][1]}, f2{a.tap_T[t][0], a.tap_T[t][1]});
-    const float gz = fmaf(pz, a.tap_S[t][2], a.tap_T[t][2]);
+    const f2 T = ZO ? f2{0.5f, 0.5f} : f2{a.tap_T[t][0], a.tap_T[t][1]};
+    const f2 gxy = __builtin_elementwise_fma(pxy, f2{a.tap_S[t][0], a.tap_S[t][1]}, T);
+    const float gz = fmaf(pz, a.tap_S[t][2], ZO ? 0.5f : a.tap_T[t][2]);
     return tap_fetch<LAYOUT>(f, t, gxy.x, gxy.y, gz);
 }
 
@@ -301,7 +321,7 @@ __device__ __forceinline__ void store_pixel(const MarchArgs& a, int x, int orow,
 #ifndef VR_PIPE
 #define VR_PIPE 1
 #endif
-template <int LAYOUT, int WRAP, bool EARLY>
+template <int LAYOUT, int WRAP, bool EARLY, bool ZO = false>
 __device__ __forceinline__ unsigned march_pixel(const MarchArgs& a, const FastCtx& f, int x, int orow)
 {
     const Ray r = setup_ray(a, x, orow);
@@ -311,8 +331,8 @@ __device__ __forceinline__ unsigned march_pixel(const MarchArgs& a, const FastCt
         float acc = 0.0f;
         int i = 0;
         if (r.n > 0) {
-            TapRaw c0 = tap_fetch_at<LAYOUT>(a, f, 0, pxy, pz), c1 = tap_fetch_at<LAYOUT>(a, f, 1, pxy, pz);
-            TapRaw c2 = tap_fetch_at<LAYOUT>(a, f, 2, pxy, pz), c3 = tap_fetch_at<LAYOUT>(a, f, 3, pxy, pz);
+            TapRaw c0 = tap_fetch_at<LAYOUT, ZO>(a, f, 0, pxy, pz), c1 = tap_fetch_at<LAYOUT, ZO>(a, f, 1, pxy, pz);
+            TapRaw c2 = tap_fetch_at<LAYOUT, ZO>(a, f, 2, pxy, pz), c3 = tap_fetch_at<LAYOUT, ZO>(a, f, 3, pxy, pz);
             for (; i < r.n; ++i) {
                 const f2 cxy = pxy;
                 const float cz = pz;
@@ -322,8 +342,8 @@ __device__ __forceinline__ unsigned march_pixel(const MarchArgs& a, const FastCt
                 const bool more = i + 1 < r.n;
                 const f2 qxy = more ? pxy : cxy;
                 const float qz = more ? pz : cz;
-                const TapRaw n0 = tap_fetch_at<LAYOUT>(a, f, 0, qxy, qz), n1 = tap_fetch_at<LAYOUT>(a, f, 1, qxy, qz);
-                const TapRaw n2 = tap_fetch_at<LAYOUT>(a, f, 2, qxy, qz), n3 = tap_fetch_at<LAYOUT>(a, f, 3, qxy, qz);
+                const TapRaw n0 = tap_fetch_at<LAYOUT, ZO>(a, f, 0, qxy, qz), n1 = tap_fetch_at<LAYOUT, ZO>(a, f, 1, qxy, qz);
+                const TapRaw n2 = tap_fetch_at<LAYOUT, ZO>(a, f, 2, qxy, qz), n3 = tap_fetch_at<LAYOUT, ZO>(a, f, 3, qxy, qz);
                 const float t0 = tap_blend<LAYOUT>(c0), t1 = tap_blend<LAYOUT>(c1);
                 const float t2 = tap_blend<LAYOUT>(c2), t3 = tap_blend<LAYOUT>(c3);
                 acc = acc + ((t0 * t1) * (t2 + t3)) * a.scale;                           // :71-73
@@ -344,10 +364,17 @@ __device__ __forceinline__ unsigned march_pixel(const MarchArgs& a, const FastCt
     float acc = 0.0f;
     int i = 0;
     for (; i < r.n; ++i) {
-        const float t0 = tap<LAYOUT, WRAP>(a, f, 0, pxy, pz);
-        const float t1 = tap<LAYOUT, WRAP>(a, f, 1, pxy, pz);
-        const float t2 = tap<LAYOUT, WRAP>(a, f, 2, pxy, pz);
-        const float t3 = tap<LAYOUT, WRAP>(a, f, 3, pxy, pz);
+        float t0, t1, t2, t3;
+        if constexpr (LAYOUT == LAYOUT_CORNER8) {
+            const f2 t01 = blend_pair_c8(tap_fetch_at<LAYOUT, ZO>(a, f, 0, pxy, pz), tap_fetch_at<LAYOUT, ZO>(a, f, 1, pxy, pz));
+            const f2 t23 = blend_pair_c8(tap_fetch_at<LAYOUT, ZO>(a, f, 2, pxy, pz), tap_fetch_at<LAYOUT, ZO>(a, f, 3, pxy, pz));
+            t0 = t01.x; t1 = t01.y; t2 = t23.x; t3 = t23.y;
+        } else {
+            t0 = tap<LAYOUT, WRAP>(a, f, 0, pxy, pz);
+            t1 = tap<LAYOUT, WRAP>(a, f, 1, pxy, pz);
+            t2 = tap<LAYOUT, WRAP>(a, f, 2, pxy, pz);
+            t3 = tap<LAYOUT, WRAP>(a, f, 3, pxy, pz);
+        }
         acc = acc + ((t0 * t1) * (t2 + t3)) * a.scale;                               // :71-73
         pxy = pxy + r.sxy;                                                            // :74
         pz = pz + r.sz;
@@ -622,7 +649,7 @@ __device__ __forceinline__ bool ring_tile(int k, int cx, int cy, int* tx, int* t
     return true;
 }
 
-template <int LAYOUT, int WRAP, bool EARLY>
+template <int LAYOUT, int WRAP, bool EARLY, bool ZO>
 __global__ __launch_bounds__(kThreads) void march_rings(const MarchArgs a, int cx, int cy, int nw, int npos)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned lds[];
@@ -636,7 +663,7 @@ __global__ __launch_bounds__(kThreads) void march_rings(const MarchArgs a, int c
         int tx, ty;
         ring_tile(k, cx, cy, &tx, &ty);
         if (tx >= 0 && tx < tiles_x8 && ty >= 0 && ty < rows8)
-            steps += march_pixel<LAYOUT, WRAP, EARLY>(a, f, tx * 8 + lane_x<LAYOUT>(lane),
+            steps += march_pixel<LAYOUT, WRAP, EARLY, ZO>(a, f, tx * 8 + lane_x<LAYOUT>(lane),
                                                       ty * 8 + lane_y<LAYOUT>(lane));
     }
     if (a.step_counter) add_steps(a, steps);
@@ -878,12 +905,16 @@ hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStre
         const int R = max(max(cx, tiles_x8 - 1 - cx), max(cy, rows8 - 1 - cy));
         const int npos = (2 * R + 1) * (2 * R + 1);
         const int tpw = sc.tiles_per_wave > 0 ? sc.tiles_per_wave : 1;
-        const int nw = (npos + tpw - 1) / tpw;
-        const dim3 grid((unsigned)((nw + 3) / 4));
-        if (early)
-            hipLaunchKernelGGL((march_rings<L, W, true>), grid, block, lds, s, a, cx, cy, 4 * (int)grid.x, npos);
+        const dim3 grid((unsigned)(((npos + tpw - 1) / tpw + 3) / 4));
+        const int nw = 4 * (int)grid.x;
+        if (early && a.zero_offsets)
+            hipLaunchKernelGGL((march_rings<L, W, true, true>), grid, block, lds, s, a, cx, cy, nw, npos);
+        else if (early)
+            hipLaunchKernelGGL((march_rings<L, W, true, false>), grid, block, lds, s, a, cx, cy, nw, npos);
+        else if (a.zero_offsets)
+            hipLaunchKernelGGL((march_rings<L, W, false, true>), grid, block, lds, s, a, cx, cy, nw, npos);
         else
-            hipLaunchKernelGGL((march_rings<L, W, false>), grid, block, lds, s, a, cx, cy, 4 * (int)grid.x, npos);
+            hipLaunchKernelGGL((march_rings<L, W, false, false>), grid, block, lds, s, a, cx, cy, nw, npos);
         return hipGetLastError();
     }
     if (sc.kind == SCHED_XCDROWS) {
