@@ -172,25 +172,6 @@ __device__ __forceinline__ float tap_fast(const FastCtx& f, int ch, float gx, fl
     return tap_blend<LAYOUT>(tap_fetch<LAYOUT>(f, ch, gx, gy, gz));
 }
 
-// Two CORNER8 taps blended together, one tap per packed-fp32 lane: every
-// stage (x, y, z lerps and the 1/255 scale) is one packed op for both taps,
-// where blend() needs scalar ops for its last stage.  Each lane runs
-// blend()'s exact op sequence, so {tA, tB} equal two blend() calls.
-__device__ __forceinline__ f2 blend_pair_c8(const TapRaw& A, const TapRaw& B)
-{
-    const f2 wx = {A.wx, B.wx}, wy = {A.wy, B.wy}, wz = {A.wz, B.wz};
-    const f2 x00 = lerp2(f2{ubyte<0>(A.q0), ubyte<0>(B.q0)}, f2{ubyte<1>(A.q0), ubyte<1>(B.q0)}, wx);
-    const f2 x10 = lerp2(f2{ubyte<2>(A.q0), ubyte<2>(B.q0)}, f2{ubyte<3>(A.q0), ubyte<3>(B.q0)}, wx);
-    const f2 x01 = lerp2(f2{ubyte<0>(A.q1), ubyte<0>(B.q1)}, f2{ubyte<1>(A.q1), ubyte<1>(B.q1)}, wx);
-    const f2 x11 = lerp2(f2{ubyte<2>(A.q1), ubyte<2>(B.q1)}, f2{ubyte<3>(A.q1), ubyte<3>(B.q1)}, wx);
-    const f2 y0 = lerp2(x00, x10, wy), y1 = lerp2(x01, x11, wy);
-    return lerp2(y0, y1, wz) * f2{1.0f / 255.0f, 1.0f / 255.0f};
-}
-
-// ZO: every tap offset T_t is 0.5 (no MediaScroll offset; the reference's
-// case), so T is the inline constant 0.5 instead of a kernel
-// argument.  An fma may read one scalar register, so with S and T both in
-// SGPRs each tap needed v_mov copies: 8 VALU ops per step.
 template <int LAYOUT, bool ZO = false>
 __device__ __forceinline__ TapRaw tap_fetch_at(const MarchArgs& a, const FastCtx& f, int t, f2 pxy, float pz)
 {
@@ -365,10 +346,11 @@ __device__ __forceinline__ unsigned march_pixel(const MarchArgs& a, const FastCt
     int i = 0;
     for (; i < r.n; ++i) {
         float t0, t1, t2, t3;
-        if constexpr (LAYOUT == LAYOUT_CORNER8) {
-            const f2 t01 = blend_pair_c8(tap_fetch_at<LAYOUT, ZO>(a, f, 0, pxy, pz), tap_fetch_at<LAYOUT, ZO>(a, f, 1, pxy, pz));
-            const f2 t23 = blend_pair_c8(tap_fetch_at<LAYOUT, ZO>(a, f, 2, pxy, pz), tap_fetch_at<LAYOUT, ZO>(a, f, 3, pxy, pz));
-            t0 = t01.x; t1 = t01.y; t2 = t23.x; t3 = t23.y;
+        if constexpr (LAYOUT != LAYOUT_PLANAR) {
+            t0 = tap_blend<LAYOUT>(tap_fetch_at<LAYOUT, ZO>(a, f, 0, pxy, pz));
+            t1 = tap_blend<LAYOUT>(tap_fetch_at<LAYOUT, ZO>(a, f, 1, pxy, pz));
+            t2 = tap_blend<LAYOUT>(tap_fetch_at<LAYOUT, ZO>(a, f, 2, pxy, pz));
+            t3 = tap_blend<LAYOUT>(tap_fetch_at<LAYOUT, ZO>(a, f, 3, pxy, pz));
         } else {
             t0 = tap<LAYOUT, WRAP>(a, f, 0, pxy, pz);
             t1 = tap<LAYOUT, WRAP>(a, f, 1, pxy, pz);
