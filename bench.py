@@ -102,7 +102,14 @@ def cpu_baseline(volume_host, osd, gsd, march, width, height, budget_s=10.0, pro
         if el >= budget_s or reps >= 2000:
             break
     mray = rows * width * march.max_steps / el / 1e6
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
+    except OSError:
+        pass
     return {"value": round(mray, 3), "unit": "Mray/s", "cores": threads, "kind": "port",
+            "host_cpu": model, "host_nproc": os.cpu_count(),
             "sample": f"{reps} band sets of every 8th 16-row band ({rows} rows of {height}) of the same "
                       f"{width}x{height}x{march.max_steps} frame and {'medium' if procedural else 'volume'}, "
                       f"{el:.1f} s; "
