@@ -748,6 +748,7 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
                 c->d_sort = nullptr;
                 c->sort_bytes = 0;
                 if (hipMalloc(&c->d_sort, need) != hipSuccess) return fail(VR_ERR_OOM, "vr_render: sort buffer");
+                HIP_TRY(hipMemset(c->d_sort, 0, need));   // the histogram starts at zero (proc_scan re-zeroes it)
                 c->sort_bytes = need;
             }
             sort_buf = c->d_sort;

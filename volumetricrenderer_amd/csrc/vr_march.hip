@@ -31,8 +31,8 @@ hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_bu
         unsigned* cursor = hist + kKeyBins;            // kKeyBins + 1 entries
         unsigned* order = hist + 2 * kKeyBins + 64;
         unsigned short* keys = reinterpret_cast<unsigned short*>(order + (size_t)a.width * a.out_rows);
-        hipError_t e = hipMemsetAsync(hist, 0, kKeyBins * sizeof(unsigned), s);
-        if (e != hipSuccess) return e;
+        // hist is all zero here: zeroed when the buffer was allocated, and by
+        // the previous frame's proc_scan after it read it
         const long long pixels = (long long)a.width * a.out_rows;
         const dim3 g1((unsigned)((pixels + 256 * kSortPixelsPerThread - 1) / (256 * kSortPixelsPerThread)));
         if (shadow) hipLaunchKernelGGL((proc_bin<true>), g1, dim3(256), 0, s, a, hist, keys);

@@ -785,11 +785,14 @@ __global__ __launch_bounds__(256) void proc_bin(const MarchArgs a, unsigned* __r
 
 // hist[kKeyBins] -> cursor[kKeyBins] (start of each key, descending keys) and
 // total at cursor[kKeyBins].  One workgroup of kKeyBins threads.
-[[maybe_unused]] __global__ __launch_bounds__(kKeyBins) void proc_scan(const unsigned* __restrict__ hist, unsigned* __restrict__ cursor)
+// It also zeroes the histogram for the next frame (the buffer is zeroed once
+// when allocated), which saves a memset launch per frame.
+[[maybe_unused]] __global__ __launch_bounds__(kKeyBins) void proc_scan(unsigned* __restrict__ hist, unsigned* __restrict__ cursor)
 {
     __shared__ unsigned sc[kKeyBins];
     const int t = threadIdx.x;
-    sc[t] = hist[kKeyBins - 1 - t];   // descending key order
+    const unsigned own = hist[kKeyBins - 1 - t];
+    sc[t] = own;   // descending key order
     __syncthreads();
     for (int off = 1; off < kKeyBins; off <<= 1) {
         const unsigned v = t >= off ? sc[t - off] : 0u;
@@ -798,8 +801,9 @@ __global__ __launch_bounds__(256) void proc_bin(const MarchArgs a, unsigned* __r
         __syncthreads();
     }
     const int key = kKeyBins - 1 - t;
-    cursor[key] = sc[t] - hist[key];   // exclusive
+    cursor[key] = sc[t] - own;   // exclusive
     if (t == kKeyBins - 1) cursor[kKeyBins] = sc[t];
+    hist[key] = 0u;              // each thread clears the bin it read
 }
 
 [[maybe_unused]] __global__ __launch_bounds__(256) void proc_scatter(const MarchArgs a, const unsigned short* __restrict__ keys,
