@@ -212,19 +212,24 @@ const char* vr_kernel_variant(void* ctx);
  * used only where clamp-to-edge equals mirrored repeat.  Otherwise the
  * planar, mirrored-repeat kernel runs.  Rebuilds the layout (synchronous). */
 vr_status vr_set_layout_preference(void* ctx, int pref);
-/* Tuning knobs: "layout" (as above); "schedule"
- * (-1 = auto, the default; 0 = one static 16x16 tile per workgroup, with
- * tile rows dealt to XCDs; 1 = persistent waves pulling 8x8 tiles from
- * per-XCD queues; 2 = each wave renders "tiles_per_wave" strided 8x8
- * tiles; 3 = 8-px tile rows dealt to XCDs; 4 = rings of 8x8 tiles around
- * the projected box centre, longest rays first -- the auto choice for the
- * volume; for the procedural medium auto is the cost-sorted schedule,
- * 0 = 8x8 tiles in row order, 4 = rings); "waves_per_simd" (1-8, queue schedule); "tiles_per_wave" (1-64,
- * strided and ring schedules; 0 = auto, the default: 2 for rings, 1 for
- * strided); "count" (0 = vr_target.step_counter sums executed
- * ray-steps, the default; 1 = it sums density evaluations, i.e. ray-steps
- * plus the procedural shadow samples -- the unit of the procedural
- * roofline).  vr_get_option returns -1 for an unknown name.               */
+/* Tuning knobs.
+ *   "layout"          as vr_set_layout_preference.
+ *   "schedule"        -1 = auto (the default); 0 = one static 16x16 tile per
+ *                     workgroup, tile rows dealt to XCDs; 1 = persistent waves
+ *                     pulling 8x8 tiles from per-XCD queues; 2 = each wave
+ *                     renders "tiles_per_wave" strided 8x8 tiles; 3 = 8-px
+ *                     tile rows dealt to XCDs; 4 = rings of 8x8 tiles around
+ *                     the projected box centre, longest rays first (auto for
+ *                     the volume).  Procedural medium: auto = cost-sorted
+ *                     pixels, 0 = 8x8 tiles in row order, 4 = rings.
+ *   "waves_per_simd"  1-8, queue schedule.
+ *   "tiles_per_wave"  1-64, strided and ring schedules; 0 = auto, the
+ *                     default: 2 for rings, 1 for strided.
+ *   "count"           0 = vr_target.step_counter sums executed ray-steps (the
+ *                     default); 1 = it sums density evaluations, i.e.
+ *                     ray-steps plus the procedural shadow samples -- the unit
+ *                     of the procedural roofline.
+ * vr_get_option returns -1 for an unknown name.                            */
 vr_status vr_set_option(void* ctx, const char* name, int value);
 int       vr_get_option(void* ctx, const char* name);
 
