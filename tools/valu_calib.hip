@@ -1,0 +1,168 @@
+// valu_calib.hip -- issue throughput of single VALU opcodes on gfx950, the cost
+// table behind the procedural kernel's instruction budget.
+// Each kernel runs ITER x 16 independent instances of one opcode per lane
+// (16 accumulators, so no dependent-latency stalls), at W waves per SIMD.
+// The shader clock is measured in-kernel (s_memtime against the 100 MHz
+// s_memrealtime), so the result is SIMD cycles per wave64 instruction.
+//   hipcc --offload-arch=gfx950 -O3 tools/valu_calib.hip -o tools/valu_calib
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+
+constexpr int ITER = 4096;
+
+#define R16(M) M(0) M(1) M(2) M(3) M(4) M(5) M(6) M(7) M(8) M(9) M(10) M(11) M(12) M(13) M(14) M(15)
+
+template <int OP>
+__device__ __forceinline__ void body(float (&f)[16], unsigned (&u)[16], float s)
+{
+#define FMA(i) asm volatile("v_fma_f32 %0, %0, %1, %1" : "+v"(f[i]) : "v"(s));
+#define MUL(i) asm volatile("v_mul_f32 %0, %0, %1" : "+v"(f[i]) : "v"(s));
+#define MULLO(i) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(u[i]) : "v"(u[(i + 1) & 15]));
+#define XOR(i) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(u[i]) : "v"(u[(i + 3) & 15]));
+#define CVT(i) asm volatile("v_cvt_i32_f32 %0, %1" : "=v"(u[i]) : "v"(f[i]));
+#define FLOOR(i) asm volatile("v_floor_f32 %0, %0" : "+v"(f[i]));
+#define EXP(i) asm volatile("v_exp_f32 %0, %0" : "+v"(f[i]));
+#define MIN3(i) asm volatile("v_min3_f32 %0, %0, %1, %1" : "+v"(f[i]) : "v"(s));
+#define FMAMIX(i) asm volatile("v_fma_f32 %0, %0, %1, %1\n\tv_mul_lo_u32 %2, %2, %3" : "+v"(f[i]), "+v"(u[i]) : "v"(s), "v"(u[(i + 1) & 15]));
+#define FMA3(i) asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(f[i]) : "v"(f[(i + 5) & 15]), "v"(s));
+#define FMAC(i) asm volatile("v_fmac_f32 %0, %1, %2" : "+v"(f[i]) : "v"(f[(i + 5) & 15]), "v"(s));
+#define ADD(i) asm volatile("v_add_f32 %0, %0, %1" : "+v"(f[i]) : "v"(f[(i + 5) & 15]));
+#define CND(i) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(u[i]) : "v"(u[(i + 5) & 15]));
+#define U24(i) asm volatile("v_mul_u32_u24 %0, %0, %1" : "+v"(u[i]) : "v"(u[(i + 1) & 15]));
+#define MAD24(i) asm volatile("v_mad_u32_u24 %0, %0, %1, %2" : "+v"(u[i]) : "v"(u[(i + 1) & 15]), "v"(u[(i + 2) & 15]));
+#define LSHLADD(i) asm volatile("v_lshl_add_u32 %0, %0, 3, %1" : "+v"(u[i]) : "v"(u[(i + 1) & 15]));
+#define MOV(i) asm volatile("v_mov_b32 %0, %1" : "=v"(u[i]) : "v"(u[(i + 1) & 15]));
+#define MULHI(i) asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(u[i]) : "v"(u[(i + 1) & 15]));
+#define CVTF(i) asm volatile("v_cvt_f32_i32 %0, %1" : "=v"(f[i]) : "v"(u[i]));
+#define FRACT(i) asm volatile("v_fract_f32 %0, %0" : "+v"(f[i]));
+    if constexpr (OP == 10) { R16(FMA3) }
+    if constexpr (OP == 11) { R16(FMAC) }
+    if constexpr (OP == 12) { R16(ADD) }
+    if constexpr (OP == 13) { R16(CND) }
+    if constexpr (OP == 14) { R16(U24) }
+    if constexpr (OP == 15) { R16(MAD24) }
+    if constexpr (OP == 16) { R16(LSHLADD) }
+    if constexpr (OP == 17) { R16(MOV) }
+    if constexpr (OP == 18) { R16(MULHI) }
+    if constexpr (OP == 19) { R16(CVTF) }
+    if constexpr (OP == 20) { R16(FRACT) }
+    if constexpr (OP == 21 || OP == 22 || OP == 23) {
+        for (int i = 0; i < 16; i += 2) {
+            float2 v = make_float2(f[i], f[i + 1]);
+            const float2 w = make_float2(f[(i + 4) & 15], f[(i + 5) & 15]);
+            if constexpr (OP == 21) asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(v) : "v"(w));
+            if constexpr (OP == 22) asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(v) : "v"(w));
+            if constexpr (OP == 23) asm volatile("v_pk_fma_f32 %0, %1, %0, %0" : "+v"(v) : "v"(w));
+            f[i] = v.x; f[i + 1] = v.y;
+        }
+    }
+    if constexpr (OP == 24) asm volatile("v_fma_f32 v64, v1, v2, v3\n\tv_fma_f32 v65, v1, v2, v3\n\tv_fma_f32 v66, v1, v2, v3\n\tv_fma_f32 v67, v1, v2, v3\n\tv_fma_f32 v68, v1, v2, v3\n\tv_fma_f32 v69, v1, v2, v3\n\tv_fma_f32 v70, v1, v2, v3\n\tv_fma_f32 v71, v1, v2, v3\n\tv_fma_f32 v72, v1, v2, v3\n\tv_fma_f32 v73, v1, v2, v3\n\tv_fma_f32 v74, v1, v2, v3\n\tv_fma_f32 v75, v1, v2, v3\n\tv_fma_f32 v76, v1, v2, v3\n\tv_fma_f32 v77, v1, v2, v3\n\tv_fma_f32 v78, v1, v2, v3\n\tv_fma_f32 v79, v1, v2, v3" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","v4","v5","v6","v8","v12","v13");
+    if constexpr (OP == 25) asm volatile("v_fma_f32 v64, v4, v8, v12\n\tv_fma_f32 v65, v4, v8, v12\n\tv_fma_f32 v66, v4, v8, v12\n\tv_fma_f32 v67, v4, v8, v12\n\tv_fma_f32 v68, v4, v8, v12\n\tv_fma_f32 v69, v4, v8, v12\n\tv_fma_f32 v70, v4, v8, v12\n\tv_fma_f32 v71, v4, v8, v12\n\tv_fma_f32 v72, v4, v8, v12\n\tv_fma_f32 v73, v4, v8, v12\n\tv_fma_f32 v74, v4, v8, v12\n\tv_fma_f32 v75, v4, v8, v12\n\tv_fma_f32 v76, v4, v8, v12\n\tv_fma_f32 v77, v4, v8, v12\n\tv_fma_f32 v78, v4, v8, v12\n\tv_fma_f32 v79, v4, v8, v12" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","v4","v5","v6","v8","v12","v13");
+    if constexpr (OP == 26) asm volatile("v_fma_f32 v64, v5, v5, v6\n\tv_fma_f32 v65, v5, v5, v6\n\tv_fma_f32 v66, v5, v5, v6\n\tv_fma_f32 v67, v5, v5, v6\n\tv_fma_f32 v68, v5, v5, v6\n\tv_fma_f32 v69, v5, v5, v6\n\tv_fma_f32 v70, v5, v5, v6\n\tv_fma_f32 v71, v5, v5, v6\n\tv_fma_f32 v72, v5, v5, v6\n\tv_fma_f32 v73, v5, v5, v6\n\tv_fma_f32 v74, v5, v5, v6\n\tv_fma_f32 v75, v5, v5, v6\n\tv_fma_f32 v76, v5, v5, v6\n\tv_fma_f32 v77, v5, v5, v6\n\tv_fma_f32 v78, v5, v5, v6\n\tv_fma_f32 v79, v5, v5, v6" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","v4","v5","v6","v8","v12","v13");
+    if constexpr (OP == 27) asm volatile("v_mul_f32 v64, v5, v5\n\tv_mul_f32 v65, v5, v5\n\tv_mul_f32 v66, v5, v5\n\tv_mul_f32 v67, v5, v5\n\tv_mul_f32 v68, v5, v5\n\tv_mul_f32 v69, v5, v5\n\tv_mul_f32 v70, v5, v5\n\tv_mul_f32 v71, v5, v5\n\tv_mul_f32 v72, v5, v5\n\tv_mul_f32 v73, v5, v5\n\tv_mul_f32 v74, v5, v5\n\tv_mul_f32 v75, v5, v5\n\tv_mul_f32 v76, v5, v5\n\tv_mul_f32 v77, v5, v5\n\tv_mul_f32 v78, v5, v5\n\tv_mul_f32 v79, v5, v5" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","v4","v5","v6","v8","v12","v13");
+    if constexpr (OP == 28) asm volatile("v_mul_f32 v64, v4, v8\n\tv_mul_f32 v65, v4, v8\n\tv_mul_f32 v66, v4, v8\n\tv_mul_f32 v67, v4, v8\n\tv_mul_f32 v68, v4, v8\n\tv_mul_f32 v69, v4, v8\n\tv_mul_f32 v70, v4, v8\n\tv_mul_f32 v71, v4, v8\n\tv_mul_f32 v72, v4, v8\n\tv_mul_f32 v73, v4, v8\n\tv_mul_f32 v74, v4, v8\n\tv_mul_f32 v75, v4, v8\n\tv_mul_f32 v76, v4, v8\n\tv_mul_f32 v77, v4, v8\n\tv_mul_f32 v78, v4, v8\n\tv_mul_f32 v79, v4, v8" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","v4","v5","v6","v8","v12","v13");
+    if constexpr (OP == 29) asm volatile("v_mul_f32 v64, v5, v6\n\tv_mul_f32 v65, v5, v6\n\tv_mul_f32 v66, v5, v6\n\tv_mul_f32 v67, v5, v6\n\tv_mul_f32 v68, v5, v6\n\tv_mul_f32 v69, v5, v6\n\tv_mul_f32 v70, v5, v6\n\tv_mul_f32 v71, v5, v6\n\tv_mul_f32 v72, v5, v6\n\tv_mul_f32 v73, v5, v6\n\tv_mul_f32 v74, v5, v6\n\tv_mul_f32 v75, v5, v6\n\tv_mul_f32 v76, v5, v6\n\tv_mul_f32 v77, v5, v6\n\tv_mul_f32 v78, v5, v6\n\tv_mul_f32 v79, v5, v6" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","v4","v5","v6","v8","v12","v13");
+    if constexpr (OP == 30) asm volatile("v_fma_f32 v64, v4, v8, v13\n\tv_fma_f32 v65, v4, v8, v13\n\tv_fma_f32 v66, v4, v8, v13\n\tv_fma_f32 v67, v4, v8, v13\n\tv_fma_f32 v68, v4, v8, v13\n\tv_fma_f32 v69, v4, v8, v13\n\tv_fma_f32 v70, v4, v8, v13\n\tv_fma_f32 v71, v4, v8, v13\n\tv_fma_f32 v72, v4, v8, v13\n\tv_fma_f32 v73, v4, v8, v13\n\tv_fma_f32 v74, v4, v8, v13\n\tv_fma_f32 v75, v4, v8, v13\n\tv_fma_f32 v76, v4, v8, v13\n\tv_fma_f32 v77, v4, v8, v13\n\tv_fma_f32 v78, v4, v8, v13\n\tv_fma_f32 v79, v4, v8, v13" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","v4","v5","v6","v8","v12","v13");
+    if constexpr (OP == 31) asm volatile("v_fma_f32 v64, v64, v2, v3\n\tv_fma_f32 v65, v65, v2, v3\n\tv_fma_f32 v66, v66, v2, v3\n\tv_fma_f32 v67, v67, v2, v3\n\tv_fma_f32 v68, v68, v2, v3\n\tv_fma_f32 v69, v69, v2, v3\n\tv_fma_f32 v70, v70, v2, v3\n\tv_fma_f32 v71, v71, v2, v3\n\tv_fma_f32 v72, v72, v2, v3\n\tv_fma_f32 v73, v73, v2, v3\n\tv_fma_f32 v74, v74, v2, v3\n\tv_fma_f32 v75, v75, v2, v3\n\tv_fma_f32 v76, v76, v2, v3\n\tv_fma_f32 v77, v77, v2, v3\n\tv_fma_f32 v78, v78, v2, v3\n\tv_fma_f32 v79, v79, v2, v3" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","v4","v5","v6","v8","v12","v13");
+    if constexpr (OP == 0) { R16(FMA) }
+    if constexpr (OP == 1) { R16(MUL) }
+    if constexpr (OP == 2) { R16(MULLO) }
+    if constexpr (OP == 3) { R16(XOR) }
+    if constexpr (OP == 4) { R16(CVT) }
+    if constexpr (OP == 5) { R16(FLOOR) }
+    if constexpr (OP == 6) { R16(EXP) }
+    if constexpr (OP == 7) { R16(MIN3) }
+    if constexpr (OP == 9) { R16(FMAMIX) }
+    if constexpr (OP == 8) {
+        // v_pk_fma_f32 on 8 register pairs (16 lanes of work per instruction pair)
+        for (int i = 0; i < 16; i += 2) {
+            float2 v = make_float2(f[i], f[i + 1]);
+            asm volatile("v_pk_fma_f32 %0, %0, %1, %1" : "+v"(v) : "v"(make_float2(s, s)));
+            f[i] = v.x; f[i + 1] = v.y;
+        }
+    }
+}
+
+template <int OP>
+__global__ __launch_bounds__(256) void k_op(float* out, unsigned long long* clk, float s)
+{
+    float f[16];
+    unsigned u[16];
+    for (int i = 0; i < 16; ++i) { f[i] = threadIdx.x * 0.001f + i; u[i] = threadIdx.x * 7u + i; }
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    for (int it = 0; it < ITER; ++it) body<OP>(f, u, s);
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    float acc = 0.0f;
+    for (int i = 0; i < 16; ++i) acc += f[i] + (float)u[i];
+    out[blockIdx.x * 256 + threadIdx.x] = acc;
+    if (threadIdx.x == 0 && blockIdx.x == 0) { clk[0] = t1 - t0; clk[1] = r1 - r0; }
+}
+
+template <int OP>
+void run(const char* name, double per_instr, int cus, float* out, unsigned long long* clk)
+{
+    for (int w : {2, 8}) {
+        const int blocks = cus * w;   // 4 waves per block = one per SIMD of a CU
+        hipEvent_t a, b;
+        hipEventCreate(&a); hipEventCreate(&b);
+        k_op<OP><<<blocks, 256>>>(out, clk, 1.0001f);
+        hipEventRecord(a);
+        k_op<OP><<<blocks, 256>>>(out, clk, 1.0001f);
+        hipEventRecord(b);
+        hipEventSynchronize(b);
+        float ms = 0;
+        hipEventElapsedTime(&ms, a, b);
+        unsigned long long h[2];
+        hipMemcpy(h, clk, sizeof h, hipMemcpyDeviceToHost);
+        const double mhz = h[1] ? 100.0 * (double)h[0] / (double)h[1] : 0.0;
+        const double instr_per_simd = (double)w * ITER * 16 * per_instr;
+        const double cyc = ms * 1e-3 * mhz * 1e6;
+        printf("%-10s waves/SIMD %d  %.3f ms  clock %.0f MHz  %.2f cycles per wave64 instr per SIMD\n", name, w, ms,
+               mhz, cyc / instr_per_simd);
+        hipEventDestroy(a); hipEventDestroy(b);
+    }
+}
+
+int main()
+{
+    int cus = 0;
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+    float* out;
+    unsigned long long* clk;
+    hipMalloc(&out, (size_t)cus * 8 * 256 * sizeof(float));
+    hipMalloc(&clk, 16);
+    run<0>("fma_f32", 1, cus, out, clk);
+    run<1>("mul_f32", 1, cus, out, clk);
+    run<2>("mul_lo_u32", 1, cus, out, clk);
+    run<3>("xor_b32", 1, cus, out, clk);
+    run<4>("cvt_i32", 1, cus, out, clk);
+    run<5>("floor_f32", 1, cus, out, clk);
+    run<6>("exp_f32", 1, cus, out, clk);
+    run<7>("min3_f32", 1, cus, out, clk);
+    run<8>("pk_fma_f32", 0.5, cus, out, clk);   // per pk instruction (8 per body)
+    run<9>("fma+mullo", 2, cus, out, clk);
+    run<10>("fma_3reg", 1, cus, out, clk);
+    run<11>("fmac_f32", 1, cus, out, clk);
+    run<12>("add_f32", 1, cus, out, clk);
+    run<13>("cndmask", 1, cus, out, clk);
+    run<14>("mul_u24", 1, cus, out, clk);
+    run<15>("mad_u24", 1, cus, out, clk);
+    run<16>("lshl_add", 1, cus, out, clk);
+    run<17>("mov_b32", 1, cus, out, clk);
+    run<18>("mul_hi_u32", 1, cus, out, clk);
+    run<19>("cvt_f32_i32", 1, cus, out, clk);
+    run<20>("fract_f32", 1, cus, out, clk);
+    run<21>("pk_mul_f32", 0.5, cus, out, clk);
+    run<22>("pk_add_f32", 0.5, cus, out, clk);
+    run<23>("pk_fma_3reg", 0.5, cus, out, clk);
+    run<24>("fma_banks_diff", 1, cus, out, clk);
+    run<25>("fma_banks_same", 1, cus, out, clk);
+    run<26>("fma_a_a_c", 1, cus, out, clk);
+    run<27>("mul_a_a", 1, cus, out, clk);
+    run<28>("mul_banks_same", 1, cus, out, clk);
+    run<29>("mul_banks_diff", 1, cus, out, clk);
+    run<30>("fma_2same_bank", 1, cus, out, clk);
+    run<31>("fma_dst_src", 1, cus, out, clk);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
+}

@@ -453,8 +453,11 @@ __device__ __forceinline__ unsigned march_pixel_proc(const MarchArgs& a, const f
 // Requires wave-uniform control flow: every lane of the wave calls it.
 constexpr int kMaxCompactShadow = 8;
 struct ShadowLds {
-    float p[64][3];                      // positions of the lanes that need shadow rays (compacted)
-    float d[64 * kMaxCompactShadow];     // densities, [compact lane][shadow step]
+    float p[64][3];                      // primary positions of the lanes that need shadow rays, [lane]
+    union {
+        unsigned code[64 * kMaxCompactShadow];   // dealt (lane << 3 | step) pairs, inside the box only
+        float d[64 * kMaxCompactShadow];         // then their densities, same slot
+    };
 };
 
 template <bool EARLY, bool TABLE>
@@ -481,29 +484,46 @@ __device__ __forceinline__ unsigned march_pixel_proc_compact(const MarchArgs& a,
         const bool need = act && rho > 0.0f;
         const unsigned long long m = __ballot(need);
         if (m) {
-            const int cnt = __popcll(m);
-            const int k = __popcll(m & ((1ull << lane) - 1ull));   // compact index of this lane
-            if (need) { sh->p[k][0] = P0; sh->p[k][1] = P1; sh->p[k][2] = P2; }
+            // The samples q_j = P + (j+1) lstep (sequential adds) that fall inside the box form
+            // one run j in [lo, lo+cnt): each coordinate moves monotonically, so its inside set
+            // along j is an interval, and so is their intersection.  Only those are dealt, so
+            // no lane of a round idles on an outside sample (they contribute exactly +0).
+            int lo = 0, cnt = 0;
+            if (need) {
+                float q0 = P0, q1 = P1, q2 = P2;
+                for (int j = 0; j < S; ++j) {
+                    q0 = q0 + p.lstep[0]; q1 = q1 + p.lstep[1]; q2 = q2 + p.lstep[2];
+                    const bool in = q0 >= 0.0f && q0 <= 1.0f && q1 >= 0.0f && q1 <= 1.0f && q2 >= 0.0f && q2 <= 1.0f;
+                    if (in && cnt == 0) lo = j;
+                    cnt += in ? 1 : 0;
+                }
+                sh->p[lane][0] = P0; sh->p[lane][1] = P1; sh->p[lane][2] = P2;
+            }
+            // Exclusive prefix of cnt (0..8, four bits) over the wave, by bit-plane ballots.
+            int off = 0, total = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const unsigned long long bb = __ballot((cnt >> b) & 1);
+                off += __popcll(bb & ((1ull << lane) - 1ull)) << b;
+                total += __popcll(bb) << b;
+            }
+            for (int c = 0; c < cnt; ++c) sh->code[off + c] = ((unsigned)lane << 3) | (unsigned)(lo + c);
             __builtin_amdgcn_wave_barrier();
-            const int total = cnt * S;
             for (int base = 0; base < total; base += 64) {
                 const int pid = base + lane;
                 if (pid < total) {
-                    const int kk = pid / S, j = pid - kk * S;
+                    const unsigned code = sh->code[pid];
+                    const int kk = (int)(code >> 3), j = (int)(code & 7u);
                     float q0 = sh->p[kk][0], q1 = sh->p[kk][1], q2 = sh->p[kk][2];
                     for (int jj = 0; jj <= j; ++jj) { q0 = q0 + p.lstep[0]; q1 = q1 + p.lstep[1]; q2 = q2 + p.lstep[2]; }
-                    float d = 0.0f;   // outside the box: contributes exactly +0
-                    if (q0 >= 0.0f && q0 <= 1.0f && q1 >= 0.0f && q1 <= 1.0f && q2 >= 0.0f && q2 <= 1.0f) {
-                        d = proc_density<TABLE>(p, wt, a.scale, q0, q1, q2);
-                        ++evals;
-                    }
-                    sh->d[kk * S + j] = d;
+                    sh->d[pid] = proc_density<TABLE>(p, wt, a.scale, q0, q1, q2);
+                    ++evals;
                 }
             }
             __builtin_amdgcn_wave_barrier();
             if (need) {
                 float sl = 0.0f;
-                for (int j = 0; j < S; ++j) sl = sl + sh->d[k * S + j];
+                for (int c = 0; c < cnt; ++c) sl = sl + sh->d[off + c];
                 const float tl = spec_expf(-(sl * p.od));
                 rad = fmaf((tv * (rho * p.od)), tl, rad);
             }
