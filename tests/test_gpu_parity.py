@@ -344,6 +344,8 @@ def test_procedural_config3_shadow(r, oracle, schedule, suffix):
                                 dict(shadow_steps=3, sun_dir=(0.0, 1.0, 0.0)),
                                 dict(shadow_steps=16, sun_dir=(-1.0, 0.5, 0.25)),
                                 dict(shadow_steps=21, sun_dir=(0.3, -1.0, 2.0)),     # > compaction limit
+                                dict(shadow_steps=8, sun_dir=(0.0, 0.0, -1.0)),      # in-box runs, zero components
+                                dict(shadow_steps=7, sun_dir=(-1.0, -1.0, 0.2), freq0=0.31),
                                 dict(shadow_steps=5, schedule=0),
                                 dict(worley_freq=0.1),                   # cell table too big: direct noise
                                 dict(worley_freq=-0.02, grid_scale=200.0, shadow_steps=4),

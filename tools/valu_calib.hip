@@ -65,6 +65,41 @@ __device__ __forceinline__ void body(float (&f)[16], unsigned (&u)[16], float s)
     if constexpr (OP == 29) asm volatile("v_mul_f32 v64, v5, v6\n\tv_mul_f32 v65, v5, v6\n\tv_mul_f32 v66, v5, v6\n\tv_mul_f32 v67, v5, v6\n\tv_mul_f32 v68, v5, v6\n\tv_mul_f32 v69, v5, v6\n\tv_mul_f32 v70, v5, v6\n\tv_mul_f32 v71, v5, v6\n\tv_mul_f32 v72, v5, v6\n\tv_mul_f32 v73, v5, v6\n\tv_mul_f32 v74, v5, v6\n\tv_mul_f32 v75, v5, v6\n\tv_mul_f32 v76, v5, v6\n\tv_mul_f32 v77, v5, v6\n\tv_mul_f32 v78, v5, v6\n\tv_mul_f32 v79, v5, v6" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","v4","v5","v6","v8","v12","v13");
     if constexpr (OP == 30) asm volatile("v_fma_f32 v64, v4, v8, v13\n\tv_fma_f32 v65, v4, v8, v13\n\tv_fma_f32 v66, v4, v8, v13\n\tv_fma_f32 v67, v4, v8, v13\n\tv_fma_f32 v68, v4, v8, v13\n\tv_fma_f32 v69, v4, v8, v13\n\tv_fma_f32 v70, v4, v8, v13\n\tv_fma_f32 v71, v4, v8, v13\n\tv_fma_f32 v72, v4, v8, v13\n\tv_fma_f32 v73, v4, v8, v13\n\tv_fma_f32 v74, v4, v8, v13\n\tv_fma_f32 v75, v4, v8, v13\n\tv_fma_f32 v76, v4, v8, v13\n\tv_fma_f32 v77, v4, v8, v13\n\tv_fma_f32 v78, v4, v8, v13\n\tv_fma_f32 v79, v4, v8, v13" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","v4","v5","v6","v8","v12","v13");
     if constexpr (OP == 31) asm volatile("v_fma_f32 v64, v64, v2, v3\n\tv_fma_f32 v65, v65, v2, v3\n\tv_fma_f32 v66, v66, v2, v3\n\tv_fma_f32 v67, v67, v2, v3\n\tv_fma_f32 v68, v68, v2, v3\n\tv_fma_f32 v69, v69, v2, v3\n\tv_fma_f32 v70, v70, v2, v3\n\tv_fma_f32 v71, v71, v2, v3\n\tv_fma_f32 v72, v72, v2, v3\n\tv_fma_f32 v73, v73, v2, v3\n\tv_fma_f32 v74, v74, v2, v3\n\tv_fma_f32 v75, v75, v2, v3\n\tv_fma_f32 v76, v76, v2, v3\n\tv_fma_f32 v77, v77, v2, v3\n\tv_fma_f32 v78, v78, v2, v3\n\tv_fma_f32 v79, v79, v2, v3" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","v4","v5","v6","v8","v12","v13");
+    if constexpr (OP == 32) asm volatile("v_fma_f32 v64, v5, v6, v6\n\tv_fma_f32 v65, v5, v6, v6\n\tv_fma_f32 v66, v5, v6, v6\n\tv_fma_f32 v67, v5, v6, v6\n\tv_fma_f32 v68, v5, v6, v6\n\tv_fma_f32 v69, v5, v6, v6\n\tv_fma_f32 v70, v5, v6, v6\n\tv_fma_f32 v71, v5, v6, v6\n\tv_fma_f32 v72, v5, v6, v6\n\tv_fma_f32 v73, v5, v6, v6\n\tv_fma_f32 v74, v5, v6, v6\n\tv_fma_f32 v75, v5, v6, v6\n\tv_fma_f32 v76, v5, v6, v6\n\tv_fma_f32 v77, v5, v6, v6\n\tv_fma_f32 v78, v5, v6, v6\n\tv_fma_f32 v79, v5, v6, v6" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","v4","v5","v6","v7","s40","s41","vcc");
+    if constexpr (OP == 33) asm volatile("v_min3_f32 v64, v1, v2, v3\n\tv_min3_f32 v65, v1, v2, v3\n\tv_min3_f32 v66, v1, v2, v3\n\tv_min3_f32 v67, v1, v2, v3\n\tv_min3_f32 v68, v1, v2, v3\n\tv_min3_f32 v69, v1, v2, v3\n\tv_min3_f32 v70, v1, v2, v3\n\tv_min3_f32 v71, v1, v2, v3\n\tv_min3_f32 v72, v1, v2, v3\n\tv_min3_f32 v73, v1, v2, v3\n\tv_min3_f32 v74, v1, v2, v3\n\tv_min3_f32 v75, v1, v2, v3\n\tv_min3_f32 v76, v1, v2, v3\n\tv_min3_f32 v77, v1, v2, v3\n\tv_min3_f32 v78, v1, v2, v3\n\tv_min3_f32 v79, v1, v2, v3" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","v4","v5","v6","v7","s40","s41","vcc");
+    if constexpr (OP == 34) asm volatile("v_bitop3_b32 v64, v1, v2, v3 bitop3:0x48\n\tv_bitop3_b32 v65, v1, v2, v3 bitop3:0x48\n\tv_bitop3_b32 v66, v1, v2, v3 bitop3:0x48\n\tv_bitop3_b32 v67, v1, v2, v3 bitop3:0x48\n\tv_bitop3_b32 v68, v1, v2, v3 bitop3:0x48\n\tv_bitop3_b32 v69, v1, v2, v3 bitop3:0x48\n\tv_bitop3_b32 v70, v1, v2, v3 bitop3:0x48\n\tv_bitop3_b32 v71, v1, v2, v3 bitop3:0x48\n\tv_bitop3_b32 v72, v1, v2, v3 bitop3:0x48\n\tv_bitop3_b32 v73, v1, v2, v3 bitop3:0x48\n\tv_bitop3_b32 v74, v1, v2, v3 bitop3:0x48\n\tv_bitop3_b32 v75, v1, v2, v3 bitop3:0x48\n\tv_bitop3_b32 v76, v1, v2, v3 bitop3:0x48\n\tv_bitop3_b32 v77, v1, v2, v3 bitop3:0x48\n\tv_bitop3_b32 v78, v1, v2, v3 bitop3:0x48\n\tv_bitop3_b32 v79, v1, v2, v3 bitop3:0x48" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","v4","v5","v6","v7","s40","s41","vcc");
+    if constexpr (OP == 35) asm volatile("v_and_or_b32 v64, v1, v2, v3\n\tv_and_or_b32 v65, v1, v2, v3\n\tv_and_or_b32 v66, v1, v2, v3\n\tv_and_or_b32 v67, v1, v2, v3\n\tv_and_or_b32 v68, v1, v2, v3\n\tv_and_or_b32 v69, v1, v2, v3\n\tv_and_or_b32 v70, v1, v2, v3\n\tv_and_or_b32 v71, v1, v2, v3\n\tv_and_or_b32 v72, v1, v2, v3\n\tv_and_or_b32 v73, v1, v2, v3\n\tv_and_or_b32 v74, v1, v2, v3\n\tv_and_or_b32 v75, v1, v2, v3\n\tv_and_or_b32 v76, v1, v2, v3\n\tv_and_or_b32 v77, v1, v2, v3\n\tv_and_or_b32 v78, v1, v2, v3\n\tv_and_or_b32 v79, v1, v2, v3" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","v4","v5","v6","v7","s40","s41","vcc");
+    if constexpr (OP == 36) asm volatile("v_add3_u32 v64, v1, v2, v3\n\tv_add3_u32 v65, v1, v2, v3\n\tv_add3_u32 v66, v1, v2, v3\n\tv_add3_u32 v67, v1, v2, v3\n\tv_add3_u32 v68, v1, v2, v3\n\tv_add3_u32 v69, v1, v2, v3\n\tv_add3_u32 v70, v1, v2, v3\n\tv_add3_u32 v71, v1, v2, v3\n\tv_add3_u32 v72, v1, v2, v3\n\tv_add3_u32 v73, v1, v2, v3\n\tv_add3_u32 v74, v1, v2, v3\n\tv_add3_u32 v75, v1, v2, v3\n\tv_add3_u32 v76, v1, v2, v3\n\tv_add3_u32 v77, v1, v2, v3\n\tv_add3_u32 v78, v1, v2, v3\n\tv_add3_u32 v79, v1, v2, v3" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","v4","v5","v6","v7","s40","s41","vcc");
+    if constexpr (OP == 37) asm volatile("v_lshl_or_b32 v64, v1, 4, v3\n\tv_lshl_or_b32 v65, v1, 4, v3\n\tv_lshl_or_b32 v66, v1, 4, v3\n\tv_lshl_or_b32 v67, v1, 4, v3\n\tv_lshl_or_b32 v68, v1, 4, v3\n\tv_lshl_or_b32 v69, v1, 4, v3\n\tv_lshl_or_b32 v70, v1, 4, v3\n\tv_lshl_or_b32 v71, v1, 4, v3\n\tv_lshl_or_b32 v72, v1, 4, v3\n\tv_lshl_or_b32 v73, v1, 4, v3\n\tv_lshl_or_b32 v74, v1, 4, v3\n\tv_lshl_or_b32 v75, v1, 4, v3\n\tv_lshl_or_b32 v76, v1, 4, v3\n\tv_lshl_or_b32 v77, v1, 4, v3\n\tv_lshl_or_b32 v78, v1, 4, v3\n\tv_lshl_or_b32 v79, v1, 4, v3" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","v4","v5","v6","v7","s40","s41","vcc");
+    if constexpr (OP == 38) asm volatile("v_bfe_u32 v64, v1, 15, 4\n\tv_bfe_u32 v65, v1, 15, 4\n\tv_bfe_u32 v66, v1, 15, 4\n\tv_bfe_u32 v67, v1, 15, 4\n\tv_bfe_u32 v68, v1, 15, 4\n\tv_bfe_u32 v69, v1, 15, 4\n\tv_bfe_u32 v70, v1, 15, 4\n\tv_bfe_u32 v71, v1, 15, 4\n\tv_bfe_u32 v72, v1, 15, 4\n\tv_bfe_u32 v73, v1, 15, 4\n\tv_bfe_u32 v74, v1, 15, 4\n\tv_bfe_u32 v75, v1, 15, 4\n\tv_bfe_u32 v76, v1, 15, 4\n\tv_bfe_u32 v77, v1, 15, 4\n\tv_bfe_u32 v78, v1, 15, 4\n\tv_bfe_u32 v79, v1, 15, 4" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","v4","v5","v6","v7","s40","s41","vcc");
+    if constexpr (OP == 39) asm volatile("v_alignbyte_b32 v64, v1, v2, v3\n\tv_alignbyte_b32 v65, v1, v2, v3\n\tv_alignbyte_b32 v66, v1, v2, v3\n\tv_alignbyte_b32 v67, v1, v2, v3\n\tv_alignbyte_b32 v68, v1, v2, v3\n\tv_alignbyte_b32 v69, v1, v2, v3\n\tv_alignbyte_b32 v70, v1, v2, v3\n\tv_alignbyte_b32 v71, v1, v2, v3\n\tv_alignbyte_b32 v72, v1, v2, v3\n\tv_alignbyte_b32 v73, v1, v2, v3\n\tv_alignbyte_b32 v74, v1, v2, v3\n\tv_alignbyte_b32 v75, v1, v2, v3\n\tv_alignbyte_b32 v76, v1, v2, v3\n\tv_alignbyte_b32 v77, v1, v2, v3\n\tv_alignbyte_b32 v78, v1, v2, v3\n\tv_alignbyte_b32 v79, v1, v2, v3" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","v4","v5","v6","v7","s40","s41","vcc");
+    if constexpr (OP == 40) asm volatile("v_cvt_flr_i32_f32 v64, v1\n\tv_cvt_flr_i32_f32 v65, v1\n\tv_cvt_flr_i32_f32 v66, v1\n\tv_cvt_flr_i32_f32 v67, v1\n\tv_cvt_flr_i32_f32 v68, v1\n\tv_cvt_flr_i32_f32 v69, v1\n\tv_cvt_flr_i32_f32 v70, v1\n\tv_cvt_flr_i32_f32 v71, v1\n\tv_cvt_flr_i32_f32 v72, v1\n\tv_cvt_flr_i32_f32 v73, v1\n\tv_cvt_flr_i32_f32 v74, v1\n\tv_cvt_flr_i32_f32 v75, v1\n\tv_cvt_flr_i32_f32 v76, v1\n\tv_cvt_flr_i32_f32 v77, v1\n\tv_cvt_flr_i32_f32 v78, v1\n\tv_cvt_flr_i32_f32 v79, v1" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","v4","v5","v6","v7","s40","s41","vcc");
+    if constexpr (OP == 41) asm volatile("v_cvt_f32_ubyte0 v64, v1\n\tv_cvt_f32_ubyte0 v65, v1\n\tv_cvt_f32_ubyte0 v66, v1\n\tv_cvt_f32_ubyte0 v67, v1\n\tv_cvt_f32_ubyte0 v68, v1\n\tv_cvt_f32_ubyte0 v69, v1\n\tv_cvt_f32_ubyte0 v70, v1\n\tv_cvt_f32_ubyte0 v71, v1\n\tv_cvt_f32_ubyte0 v72, v1\n\tv_cvt_f32_ubyte0 v73, v1\n\tv_cvt_f32_ubyte0 v74, v1\n\tv_cvt_f32_ubyte0 v75, v1\n\tv_cvt_f32_ubyte0 v76, v1\n\tv_cvt_f32_ubyte0 v77, v1\n\tv_cvt_f32_ubyte0 v78, v1\n\tv_cvt_f32_ubyte0 v79, v1" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","v4","v5","v6","v7","s40","s41","vcc");
+    if constexpr (OP == 42) asm volatile("v_max_f32 v64, v1, v2\n\tv_max_f32 v65, v1, v2\n\tv_max_f32 v66, v1, v2\n\tv_max_f32 v67, v1, v2\n\tv_max_f32 v68, v1, v2\n\tv_max_f32 v69, v1, v2\n\tv_max_f32 v70, v1, v2\n\tv_max_f32 v71, v1, v2\n\tv_max_f32 v72, v1, v2\n\tv_max_f32 v73, v1, v2\n\tv_max_f32 v74, v1, v2\n\tv_max_f32 v75, v1, v2\n\tv_max_f32 v76, v1, v2\n\tv_max_f32 v77, v1, v2\n\tv_max_f32 v78, v1, v2\n\tv_max_f32 v79, v1, v2" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","v4","v5","v6","v7","s40","s41","vcc");
+    if constexpr (OP == 43) asm volatile("v_rndne_f32 v64, v1\n\tv_rndne_f32 v65, v1\n\tv_rndne_f32 v66, v1\n\tv_rndne_f32 v67, v1\n\tv_rndne_f32 v68, v1\n\tv_rndne_f32 v69, v1\n\tv_rndne_f32 v70, v1\n\tv_rndne_f32 v71, v1\n\tv_rndne_f32 v72, v1\n\tv_rndne_f32 v73, v1\n\tv_rndne_f32 v74, v1\n\tv_rndne_f32 v75, v1\n\tv_rndne_f32 v76, v1\n\tv_rndne_f32 v77, v1\n\tv_rndne_f32 v78, v1\n\tv_rndne_f32 v79, v1" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","v4","v5","v6","v7","s40","s41","vcc");
+    if constexpr (OP == 44) asm volatile("v_cmp_lt_f32 vcc, v1, v64\n\tv_cmp_lt_f32 vcc, v1, v65\n\tv_cmp_lt_f32 vcc, v1, v66\n\tv_cmp_lt_f32 vcc, v1, v67\n\tv_cmp_lt_f32 vcc, v1, v68\n\tv_cmp_lt_f32 vcc, v1, v69\n\tv_cmp_lt_f32 vcc, v1, v70\n\tv_cmp_lt_f32 vcc, v1, v71\n\tv_cmp_lt_f32 vcc, v1, v72\n\tv_cmp_lt_f32 vcc, v1, v73\n\tv_cmp_lt_f32 vcc, v1, v74\n\tv_cmp_lt_f32 vcc, v1, v75\n\tv_cmp_lt_f32 vcc, v1, v76\n\tv_cmp_lt_f32 vcc, v1, v77\n\tv_cmp_lt_f32 vcc, v1, v78\n\tv_cmp_lt_f32 vcc, v1, v79" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","v4","v5","v6","v7","s40","s41","vcc");
+    if constexpr (OP == 45) asm volatile("v_cndmask_b32_e64 v64, v1, v2, s[40:41]\n\tv_cndmask_b32_e64 v65, v1, v2, s[40:41]\n\tv_cndmask_b32_e64 v66, v1, v2, s[40:41]\n\tv_cndmask_b32_e64 v67, v1, v2, s[40:41]\n\tv_cndmask_b32_e64 v68, v1, v2, s[40:41]\n\tv_cndmask_b32_e64 v69, v1, v2, s[40:41]\n\tv_cndmask_b32_e64 v70, v1, v2, s[40:41]\n\tv_cndmask_b32_e64 v71, v1, v2, s[40:41]\n\tv_cndmask_b32_e64 v72, v1, v2, s[40:41]\n\tv_cndmask_b32_e64 v73, v1, v2, s[40:41]\n\tv_cndmask_b32_e64 v74, v1, v2, s[40:41]\n\tv_cndmask_b32_e64 v75, v1, v2, s[40:41]\n\tv_cndmask_b32_e64 v76, v1, v2, s[40:41]\n\tv_cndmask_b32_e64 v77, v1, v2, s[40:41]\n\tv_cndmask_b32_e64 v78, v1, v2, s[40:41]\n\tv_cndmask_b32_e64 v79, v1, v2, s[40:41]" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","v4","v5","v6","v7","s40","s41","vcc");
+    if constexpr (OP == 46) asm volatile("v_lshrrev_b32 v64, 15, v1\n\tv_lshrrev_b32 v65, 15, v1\n\tv_lshrrev_b32 v66, 15, v1\n\tv_lshrrev_b32 v67, 15, v1\n\tv_lshrrev_b32 v68, 15, v1\n\tv_lshrrev_b32 v69, 15, v1\n\tv_lshrrev_b32 v70, 15, v1\n\tv_lshrrev_b32 v71, 15, v1\n\tv_lshrrev_b32 v72, 15, v1\n\tv_lshrrev_b32 v73, 15, v1\n\tv_lshrrev_b32 v74, 15, v1\n\tv_lshrrev_b32 v75, 15, v1\n\tv_lshrrev_b32 v76, 15, v1\n\tv_lshrrev_b32 v77, 15, v1\n\tv_lshrrev_b32 v78, 15, v1\n\tv_lshrrev_b32 v79, 15, v1" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","v4","v5","v6","v7","s40","s41","vcc");
+    if constexpr (OP == 47) asm volatile("v_add_u32 v64, v1, v2\n\tv_add_u32 v65, v1, v2\n\tv_add_u32 v66, v1, v2\n\tv_add_u32 v67, v1, v2\n\tv_add_u32 v68, v1, v2\n\tv_add_u32 v69, v1, v2\n\tv_add_u32 v70, v1, v2\n\tv_add_u32 v71, v1, v2\n\tv_add_u32 v72, v1, v2\n\tv_add_u32 v73, v1, v2\n\tv_add_u32 v74, v1, v2\n\tv_add_u32 v75, v1, v2\n\tv_add_u32 v76, v1, v2\n\tv_add_u32 v77, v1, v2\n\tv_add_u32 v78, v1, v2\n\tv_add_u32 v79, v1, v2" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","v4","v5","v6","v7","s40","s41","vcc");
+    if constexpr (OP == 48) asm volatile("v_fmamk_f32 v64, v1, 0x40c00000, v2\n\tv_fmamk_f32 v65, v1, 0x40c00000, v2\n\tv_fmamk_f32 v66, v1, 0x40c00000, v2\n\tv_fmamk_f32 v67, v1, 0x40c00000, v2\n\tv_fmamk_f32 v68, v1, 0x40c00000, v2\n\tv_fmamk_f32 v69, v1, 0x40c00000, v2\n\tv_fmamk_f32 v70, v1, 0x40c00000, v2\n\tv_fmamk_f32 v71, v1, 0x40c00000, v2\n\tv_fmamk_f32 v72, v1, 0x40c00000, v2\n\tv_fmamk_f32 v73, v1, 0x40c00000, v2\n\tv_fmamk_f32 v74, v1, 0x40c00000, v2\n\tv_fmamk_f32 v75, v1, 0x40c00000, v2\n\tv_fmamk_f32 v76, v1, 0x40c00000, v2\n\tv_fmamk_f32 v77, v1, 0x40c00000, v2\n\tv_fmamk_f32 v78, v1, 0x40c00000, v2\n\tv_fmamk_f32 v79, v1, 0x40c00000, v2" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","v4","v5","v6","v7","s40","s41","vcc");
+    if constexpr (OP == 49) asm volatile("v_mul_f32 v64, s40, v1\n\tv_mul_f32 v65, s40, v1\n\tv_mul_f32 v66, s40, v1\n\tv_mul_f32 v67, s40, v1\n\tv_mul_f32 v68, s40, v1\n\tv_mul_f32 v69, s40, v1\n\tv_mul_f32 v70, s40, v1\n\tv_mul_f32 v71, s40, v1\n\tv_mul_f32 v72, s40, v1\n\tv_mul_f32 v73, s40, v1\n\tv_mul_f32 v74, s40, v1\n\tv_mul_f32 v75, s40, v1\n\tv_mul_f32 v76, s40, v1\n\tv_mul_f32 v77, s40, v1\n\tv_mul_f32 v78, s40, v1\n\tv_mul_f32 v79, s40, v1" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","v4","v5","v6","v7","s40","s41","vcc");
+    if constexpr (OP == 51) asm volatile("v_pk_fma_f32 v[64:65], v[2:3], v[4:5], v[6:7]\n\tv_pk_fma_f32 v[66:67], v[2:3], v[4:5], v[6:7]\n\tv_pk_fma_f32 v[68:69], v[2:3], v[4:5], v[6:7]\n\tv_pk_fma_f32 v[70:71], v[2:3], v[4:5], v[6:7]\n\tv_pk_fma_f32 v[72:73], v[2:3], v[4:5], v[6:7]\n\tv_pk_fma_f32 v[74:75], v[2:3], v[4:5], v[6:7]\n\tv_pk_fma_f32 v[76:77], v[2:3], v[4:5], v[6:7]\n\tv_pk_fma_f32 v[78:79], v[2:3], v[4:5], v[6:7]" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","v4","v5","v6","v7","s40","s41","vcc");
+    if constexpr (OP == 52) asm volatile("v_mul_f32 v64, s40, v1\n\tv_mul_f32 v65, s41, v1\n\tv_mul_f32 v66, s42, v1\n\tv_mul_f32 v67, s43, v1\n\tv_mul_f32 v68, s44, v1\n\tv_mul_f32 v69, s45, v1\n\tv_mul_f32 v70, s46, v1\n\tv_mul_f32 v71, s47, v1\n\tv_mul_f32 v72, s40, v1\n\tv_mul_f32 v73, s41, v1\n\tv_mul_f32 v74, s42, v1\n\tv_mul_f32 v75, s43, v1\n\tv_mul_f32 v76, s44, v1\n\tv_mul_f32 v77, s45, v1\n\tv_mul_f32 v78, s46, v1\n\tv_mul_f32 v79, s47, v1" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
+    if constexpr (OP == 53) asm volatile("v_add_f32 v64, s40, v1\n\tv_add_f32 v65, s40, v1\n\tv_add_f32 v66, s40, v1\n\tv_add_f32 v67, s40, v1\n\tv_add_f32 v68, s40, v1\n\tv_add_f32 v69, s40, v1\n\tv_add_f32 v70, s40, v1\n\tv_add_f32 v71, s40, v1\n\tv_add_f32 v72, s40, v1\n\tv_add_f32 v73, s40, v1\n\tv_add_f32 v74, s40, v1\n\tv_add_f32 v75, s40, v1\n\tv_add_f32 v76, s40, v1\n\tv_add_f32 v77, s40, v1\n\tv_add_f32 v78, s40, v1\n\tv_add_f32 v79, s40, v1" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
+    if constexpr (OP == 54) asm volatile("v_xor_b32 v64, s40, v1\n\tv_xor_b32 v65, s40, v1\n\tv_xor_b32 v66, s40, v1\n\tv_xor_b32 v67, s40, v1\n\tv_xor_b32 v68, s40, v1\n\tv_xor_b32 v69, s40, v1\n\tv_xor_b32 v70, s40, v1\n\tv_xor_b32 v71, s40, v1\n\tv_xor_b32 v72, s40, v1\n\tv_xor_b32 v73, s40, v1\n\tv_xor_b32 v74, s40, v1\n\tv_xor_b32 v75, s40, v1\n\tv_xor_b32 v76, s40, v1\n\tv_xor_b32 v77, s40, v1\n\tv_xor_b32 v78, s40, v1\n\tv_xor_b32 v79, s40, v1" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
+    if constexpr (OP == 55) asm volatile("v_fma_f32 v64, s40, v1, v2\n\tv_fma_f32 v65, s40, v1, v2\n\tv_fma_f32 v66, s40, v1, v2\n\tv_fma_f32 v67, s40, v1, v2\n\tv_fma_f32 v68, s40, v1, v2\n\tv_fma_f32 v69, s40, v1, v2\n\tv_fma_f32 v70, s40, v1, v2\n\tv_fma_f32 v71, s40, v1, v2\n\tv_fma_f32 v72, s40, v1, v2\n\tv_fma_f32 v73, s40, v1, v2\n\tv_fma_f32 v74, s40, v1, v2\n\tv_fma_f32 v75, s40, v1, v2\n\tv_fma_f32 v76, s40, v1, v2\n\tv_fma_f32 v77, s40, v1, v2\n\tv_fma_f32 v78, s40, v1, v2\n\tv_fma_f32 v79, s40, v1, v2" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
+    if constexpr (OP == 56) asm volatile("v_mul_f32 v64, 0.5, v1\n\tv_mul_f32 v65, 0.5, v1\n\tv_mul_f32 v66, 0.5, v1\n\tv_mul_f32 v67, 0.5, v1\n\tv_mul_f32 v68, 0.5, v1\n\tv_mul_f32 v69, 0.5, v1\n\tv_mul_f32 v70, 0.5, v1\n\tv_mul_f32 v71, 0.5, v1\n\tv_mul_f32 v72, 0.5, v1\n\tv_mul_f32 v73, 0.5, v1\n\tv_mul_f32 v74, 0.5, v1\n\tv_mul_f32 v75, 0.5, v1\n\tv_mul_f32 v76, 0.5, v1\n\tv_mul_f32 v77, 0.5, v1\n\tv_mul_f32 v78, 0.5, v1\n\tv_mul_f32 v79, 0.5, v1" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
+    if constexpr (OP == 57) asm volatile("v_min_f32 v64, v1, v2\n\tv_min_f32 v65, v1, v2\n\tv_min_f32 v66, v1, v2\n\tv_min_f32 v67, v1, v2\n\tv_min_f32 v68, v1, v2\n\tv_min_f32 v69, v1, v2\n\tv_min_f32 v70, v1, v2\n\tv_min_f32 v71, v1, v2\n\tv_min_f32 v72, v1, v2\n\tv_min_f32 v73, v1, v2\n\tv_min_f32 v74, v1, v2\n\tv_min_f32 v75, v1, v2\n\tv_min_f32 v76, v1, v2\n\tv_min_f32 v77, v1, v2\n\tv_min_f32 v78, v1, v2\n\tv_min_f32 v79, v1, v2" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
+    if constexpr (OP == 58) asm volatile("v_sub_f32 v64, v1, v2\n\tv_sub_f32 v65, v1, v2\n\tv_sub_f32 v66, v1, v2\n\tv_sub_f32 v67, v1, v2\n\tv_sub_f32 v68, v1, v2\n\tv_sub_f32 v69, v1, v2\n\tv_sub_f32 v70, v1, v2\n\tv_sub_f32 v71, v1, v2\n\tv_sub_f32 v72, v1, v2\n\tv_sub_f32 v73, v1, v2\n\tv_sub_f32 v74, v1, v2\n\tv_sub_f32 v75, v1, v2\n\tv_sub_f32 v76, v1, v2\n\tv_sub_f32 v77, v1, v2\n\tv_sub_f32 v78, v1, v2\n\tv_sub_f32 v79, v1, v2" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
+    if constexpr (OP == 59) asm volatile("v_mul_f32 v64, v1, v2\n\tv_mul_f32 v65, v1, v2\n\tv_mul_f32 v66, v1, v2\n\tv_mul_f32 v67, v1, v2\n\tv_mul_f32 v68, v1, v2\n\tv_mul_f32 v69, v1, v2\n\tv_mul_f32 v70, v1, v2\n\tv_mul_f32 v71, v1, v2\n\tv_mul_f32 v72, v1, v2\n\tv_mul_f32 v73, v1, v2\n\tv_mul_f32 v74, v1, v2\n\tv_mul_f32 v75, v1, v2\n\tv_mul_f32 v76, v1, v2\n\tv_mul_f32 v77, v1, v2\n\tv_mul_f32 v78, v1, v2\n\tv_mul_f32 v79, v1, v2" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
+    if constexpr (OP == 60) asm volatile("v_cndmask_b32 v64, v1, v2, vcc\n\tv_cndmask_b32 v65, v1, v2, vcc\n\tv_cndmask_b32 v66, v1, v2, vcc\n\tv_cndmask_b32 v67, v1, v2, vcc\n\tv_cndmask_b32 v68, v1, v2, vcc\n\tv_cndmask_b32 v69, v1, v2, vcc\n\tv_cndmask_b32 v70, v1, v2, vcc\n\tv_cndmask_b32 v71, v1, v2, vcc\n\tv_cndmask_b32 v72, v1, v2, vcc\n\tv_cndmask_b32 v73, v1, v2, vcc\n\tv_cndmask_b32 v74, v1, v2, vcc\n\tv_cndmask_b32 v75, v1, v2, vcc\n\tv_cndmask_b32 v76, v1, v2, vcc\n\tv_cndmask_b32 v77, v1, v2, vcc\n\tv_cndmask_b32 v78, v1, v2, vcc\n\tv_cndmask_b32 v79, v1, v2, vcc" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
+    if constexpr (OP == 61) asm volatile("v_mul_f32_e64 v64, v1, s40\n\tv_mul_f32_e64 v65, v1, s40\n\tv_mul_f32_e64 v66, v1, s40\n\tv_mul_f32_e64 v67, v1, s40\n\tv_mul_f32_e64 v68, v1, s40\n\tv_mul_f32_e64 v69, v1, s40\n\tv_mul_f32_e64 v70, v1, s40\n\tv_mul_f32_e64 v71, v1, s40\n\tv_mul_f32_e64 v72, v1, s40\n\tv_mul_f32_e64 v73, v1, s40\n\tv_mul_f32_e64 v74, v1, s40\n\tv_mul_f32_e64 v75, v1, s40\n\tv_mul_f32_e64 v76, v1, s40\n\tv_mul_f32_e64 v77, v1, s40\n\tv_mul_f32_e64 v78, v1, s40\n\tv_mul_f32_e64 v79, v1, s40" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
+    if constexpr (OP == 62) asm volatile("v_mul_lo_u32 v64, v1, s40\n\tv_mul_lo_u32 v65, v1, s40\n\tv_mul_lo_u32 v66, v1, s40\n\tv_mul_lo_u32 v67, v1, s40\n\tv_mul_lo_u32 v68, v1, s40\n\tv_mul_lo_u32 v69, v1, s40\n\tv_mul_lo_u32 v70, v1, s40\n\tv_mul_lo_u32 v71, v1, s40\n\tv_mul_lo_u32 v72, v1, s40\n\tv_mul_lo_u32 v73, v1, s40\n\tv_mul_lo_u32 v74, v1, s40\n\tv_mul_lo_u32 v75, v1, s40\n\tv_mul_lo_u32 v76, v1, s40\n\tv_mul_lo_u32 v77, v1, s40\n\tv_mul_lo_u32 v78, v1, s40\n\tv_mul_lo_u32 v79, v1, s40" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
+    if constexpr (OP == 63) asm volatile("v_and_b32 v64, 15, v1\n\tv_and_b32 v65, 15, v1\n\tv_and_b32 v66, 15, v1\n\tv_and_b32 v67, 15, v1\n\tv_and_b32 v68, 15, v1\n\tv_and_b32 v69, 15, v1\n\tv_and_b32 v70, 15, v1\n\tv_and_b32 v71, 15, v1\n\tv_and_b32 v72, 15, v1\n\tv_and_b32 v73, 15, v1\n\tv_and_b32 v74, 15, v1\n\tv_and_b32 v75, 15, v1\n\tv_and_b32 v76, 15, v1\n\tv_and_b32 v77, 15, v1\n\tv_and_b32 v78, 15, v1\n\tv_and_b32 v79, 15, v1" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
+    if constexpr (OP == 64) asm volatile("v_or_b32 v64, v1, v2\n\tv_or_b32 v65, v1, v2\n\tv_or_b32 v66, v1, v2\n\tv_or_b32 v67, v1, v2\n\tv_or_b32 v68, v1, v2\n\tv_or_b32 v69, v1, v2\n\tv_or_b32 v70, v1, v2\n\tv_or_b32 v71, v1, v2\n\tv_or_b32 v72, v1, v2\n\tv_or_b32 v73, v1, v2\n\tv_or_b32 v74, v1, v2\n\tv_or_b32 v75, v1, v2\n\tv_or_b32 v76, v1, v2\n\tv_or_b32 v77, v1, v2\n\tv_or_b32 v78, v1, v2\n\tv_or_b32 v79, v1, v2" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
+    if constexpr (OP == 65) asm volatile("v_cmp_eq_u32 vcc, v1, v64\n\tv_cmp_eq_u32 vcc, v1, v65\n\tv_cmp_eq_u32 vcc, v1, v66\n\tv_cmp_eq_u32 vcc, v1, v67\n\tv_cmp_eq_u32 vcc, v1, v68\n\tv_cmp_eq_u32 vcc, v1, v69\n\tv_cmp_eq_u32 vcc, v1, v70\n\tv_cmp_eq_u32 vcc, v1, v71\n\tv_cmp_eq_u32 vcc, v1, v72\n\tv_cmp_eq_u32 vcc, v1, v73\n\tv_cmp_eq_u32 vcc, v1, v74\n\tv_cmp_eq_u32 vcc, v1, v75\n\tv_cmp_eq_u32 vcc, v1, v76\n\tv_cmp_eq_u32 vcc, v1, v77\n\tv_cmp_eq_u32 vcc, v1, v78\n\tv_cmp_eq_u32 vcc, v1, v79" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
+    if constexpr (OP == 66) asm volatile("v_max_i32 v64, v1, v2\n\tv_max_i32 v65, v1, v2\n\tv_max_i32 v66, v1, v2\n\tv_max_i32 v67, v1, v2\n\tv_max_i32 v68, v1, v2\n\tv_max_i32 v69, v1, v2\n\tv_max_i32 v70, v1, v2\n\tv_max_i32 v71, v1, v2\n\tv_max_i32 v72, v1, v2\n\tv_max_i32 v73, v1, v2\n\tv_max_i32 v74, v1, v2\n\tv_max_i32 v75, v1, v2\n\tv_max_i32 v76, v1, v2\n\tv_max_i32 v77, v1, v2\n\tv_max_i32 v78, v1, v2\n\tv_max_i32 v79, v1, v2" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
+    if constexpr (OP == 67) asm volatile("v_med3_f32 v64, v1, v2, v3\n\tv_med3_f32 v65, v1, v2, v3\n\tv_med3_f32 v66, v1, v2, v3\n\tv_med3_f32 v67, v1, v2, v3\n\tv_med3_f32 v68, v1, v2, v3\n\tv_med3_f32 v69, v1, v2, v3\n\tv_med3_f32 v70, v1, v2, v3\n\tv_med3_f32 v71, v1, v2, v3\n\tv_med3_f32 v72, v1, v2, v3\n\tv_med3_f32 v73, v1, v2, v3\n\tv_med3_f32 v74, v1, v2, v3\n\tv_med3_f32 v75, v1, v2, v3\n\tv_med3_f32 v76, v1, v2, v3\n\tv_med3_f32 v77, v1, v2, v3\n\tv_med3_f32 v78, v1, v2, v3\n\tv_med3_f32 v79, v1, v2, v3" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
     if constexpr (OP == 0) { R16(FMA) }
     if constexpr (OP == 1) { R16(MUL) }
     if constexpr (OP == 2) { R16(MULLO) }
@@ -164,5 +199,40 @@ int main()
     run<29>("mul_banks_diff", 1, cus, out, clk);
     run<30>("fma_2same_bank", 1, cus, out, clk);
     run<31>("fma_dst_src", 1, cus, out, clk);
+    run<32>("fma_a_c_c", 1, cus, out, clk);
+    run<33>("min3_diff", 1, cus, out, clk);
+    run<34>("bitop3", 1, cus, out, clk);
+    run<35>("and_or", 1, cus, out, clk);
+    run<36>("add3_u32", 1, cus, out, clk);
+    run<37>("lshl_or", 1, cus, out, clk);
+    run<38>("bfe_u32", 1, cus, out, clk);
+    run<39>("alignbyte", 1, cus, out, clk);
+    run<40>("cvt_flr_i32", 1, cus, out, clk);
+    run<41>("cvt_ubyte0", 1, cus, out, clk);
+    run<42>("max_f32", 1, cus, out, clk);
+    run<43>("rndne", 1, cus, out, clk);
+    run<44>("cmp_lt_f32", 1, cus, out, clk);
+    run<45>("cndmask_e64", 1, cus, out, clk);
+    run<46>("lshrrev", 1, cus, out, clk);
+    run<47>("add_u32", 1, cus, out, clk);
+    run<48>("fmamk", 1, cus, out, clk);
+    run<49>("mul_f32_sgpr", 1, cus, out, clk);
+    run<51>("pk_fma_banks", 0.5, cus, out, clk);
+    run<52>("mul_sgpr_each", 1, cus, out, clk);
+    run<53>("add_sgpr", 1, cus, out, clk);
+    run<54>("xor_sgpr", 1, cus, out, clk);
+    run<55>("fma_sgpr", 1, cus, out, clk);
+    run<56>("mul_inline", 1, cus, out, clk);
+    run<57>("min_f32", 1, cus, out, clk);
+    run<58>("sub_f32", 1, cus, out, clk);
+    run<59>("mul_vv", 1, cus, out, clk);
+    run<60>("cnd_vop2", 1, cus, out, clk);
+    run<61>("mul_sgpr_e64", 1, cus, out, clk);
+    run<62>("mullo_sgpr", 1, cus, out, clk);
+    run<63>("and_b32", 1, cus, out, clk);
+    run<64>("or_b32", 1, cus, out, clk);
+    run<65>("cmp_eq_u32", 1, cus, out, clk);
+    run<66>("max_i32", 1, cus, out, clk);
+    run<67>("med3", 1, cus, out, clk);
     return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
 }
