@@ -219,12 +219,18 @@ vr_status vr_set_layout_preference(void* ctx, int pref);
  *                     pulling 8x8 tiles from per-XCD queues; 2 = each wave
  *                     renders "tiles_per_wave" strided 8x8 tiles; 3 = 8-px
  *                     tile rows dealt to XCDs; 4 = rings of 8x8 tiles around
- *                     the projected box centre, longest rays first (auto for
- *                     the volume).  Procedural medium: auto = cost-sorted
- *                     pixels, 0 = 8x8 tiles in row order, 4 = rings.
+ *                     the projected box centre, longest rays first; 5 =
+ *                     regions: each XCD renders "wedges" contiguous angular
+ *                     wedges of tiles around the box centre with equal
+ *                     estimated work, inside-out (auto for the volume; the
+ *                     lists are rebuilt on the host when the geometry
+ *                     changes, at most every 32 renders for a moving camera).
+ *                     Procedural medium: auto = cost-sorted pixels, 0 = 8x8
+ *                     tiles in row order, 4 = rings.
  *   "waves_per_simd"  1-8, queue schedule.
- *   "tiles_per_wave"  1-64, strided and ring schedules; 0 = auto, the
- *                     default: 2 for rings, 1 for strided.
+ *   "tiles_per_wave"  1-64, strided, ring and region schedules; 0 = auto,
+ *                     the default: 2 for rings and regions, 1 for strided.
+ *   "wedges"          1-64, regions schedule: wedges per XCD (default 2).
  *   "count"           0 = vr_target.step_counter sums executed ray-steps (the
  *                     default); 1 = it sums density evaluations, i.e.
  *                     ray-steps plus the procedural shadow samples -- the unit

@@ -121,7 +121,7 @@ def test_every_layout_bitexact(r, oracle, vol128, layout, name):
 
 
 @pytest.mark.parametrize("schedule,wps", [(0, 4), (1, 1), (1, 3), (1, 8), (2, 1), (2, 3), (2, 16), (3, 1), (4, 1), (4, 2),
-                                          (4, 5)])
+                                          (4, 5), (5, 1), (5, 2), (5, 7)])
 def test_schedules_bitexact(r, oracle, vol128, schedule, wps):
     sched0, tpw0 = r.get_option("schedule"), r.get_option("tiles_per_wave")
     r.set_option("schedule", schedule)
@@ -445,11 +445,12 @@ def translated_shader_data(W, H, t):
 
 @pytest.mark.parametrize("t", [(0.9, -0.4, 0.2), (1.8, -1.8, 0.0), (0.0, 0.0, 3.5)])
 @pytest.mark.parametrize("layout", [2, 5])
-def test_ring_schedule_off_centre(r, oracle, vol128, t, layout):
+@pytest.mark.parametrize("schedule", [4, 5])
+def test_ring_schedule_off_centre(r, oracle, vol128, t, layout, schedule):
     W, H = 400, 240
     osd, gsd = translated_shader_data(W, H, t)
     r.set_layout_preference(layout)
-    r.set_option("schedule", 4)
+    r.set_option("schedule", schedule)
     try:
         for band in ({}, dict(band_rows=16, band_stride=2, band_first=1)):
             img, ref, c, s = render_both(r, oracle, vol128, W, H, osd, gsd, **band)
@@ -545,3 +546,36 @@ def test_procedural_needs_no_volume(oracle):
         with pytest.raises(VRError) as e:
             fresh.render(64, 64, vr.FMT_RGBA32F)
         assert e.value.status == 3   # VR_ERR_NO_VOLUME
+
+
+@pytest.mark.parametrize("wedges", [1, 3, 64])
+def test_regions_schedule_every_pixel_once(r, oracle, vol128, wedges):
+    """Regions schedule (5): the host-built per-XCD tile lists cover every
+    tile exactly once -- the output buffer is pre-filled with a sentinel --
+    and they are rebuilt when the geometry changes (camera, size, bands)."""
+    W, H = 328, 200
+    r.set_option("schedule", 5)
+    r.set_option("wedges", wedges)
+    try:
+        r.set_volume(vol128)
+        r.set_march(vr.march_defaults())
+        cases = [(W, H, vr.reference_shader_data(W / H), {}),
+                 (W, H, vr.reference_shader_data(W / H, 40.0, -25.0), {}),
+                 (W + 40, H - 8, vr.reference_shader_data(W / H, 40.0, -25.0), {}),
+                 (W, H, translated_shader_data(W, H, (1.1, -0.7, 0.3)), dict(band_rows=16, band_stride=3, band_first=1))]
+        for w, h, (osd, gsd), band in cases:
+            r.set_shader_data(osd, gsd)
+            out = r.alloc_target(w, h, vr.FMT_RGBA8_UNORM, band.get("band_rows", 0), band.get("band_stride", 1),
+                                 band.get("band_first", 0))
+            out.fill_(0x5A)
+            cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+            img = r.render(w, h, vr.FMT_RGBA8_UNORM, out=out, step_counter=cnt, **band)
+            torch.cuda.synchronize()
+            obj, glob = vr.shader_data_arrays(osd, gsd)
+            ref, steps = oracle.render(vol128, obj, glob, oracle.from_params(vr.march_defaults()), w, h,
+                                       vr.FMT_RGBA8_UNORM, **band)
+            assert_exact(img.cpu().numpy(), ref)
+            assert int(cnt.item()) == steps
+    finally:
+        r.set_option("schedule", -1)
+        r.set_option("wedges", 2)

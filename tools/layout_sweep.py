@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--sizes", default="128,512")
     ap.add_argument("--layouts", default="2,3,4,5,1")
     ap.add_argument("--variants", default="",
-                    help="comma list of layout:schedule:waves_per_simd, overrides --layouts")
+                    help="comma list of layout:schedule:waves_per_simd|tiles_per_wave[:wedges], overrides --layouts")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--frames", type=int, default=10)
     ap.add_argument("--width", type=int, default=1920)
@@ -43,11 +43,12 @@ def main():
         r.set_option("schedule", lay[1])
         if lay[1] == 1 and lay[2] > 0:
             r.set_option("waves_per_simd", lay[2])
-        if lay[1] in (2, 4) and lay[2] > 0:
-            r.set_option("tiles_per_wave", lay[2])
+        r.set_option("tiles_per_wave", lay[2] if lay[1] in (2, 4, 5) else 0)
+        if lay[1] == 5:
+            r.set_option("wedges", lay[3] if len(lay) > 3 else 1)
 
     def name(lay):
-        return f"{NAMES[lay[0]]}/{['static', 'queue', 'strided', 'xcdrows', 'rings'][lay[1]]}{lay[2] if lay[1] else ''}"
+        return f"{NAMES[lay[0]]}/{['static', 'queue', 'strided', 'xcdrows', 'rings', 'regions'][lay[1]]}{lay[2] if lay[1] else ''}{'w%d' % lay[3] if len(lay) > 3 else ''}"
     res = {}
     with vr.Renderer(0) as r:
         osd, gsd = vr.reference_shader_data(W / H)

@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--schedule", type=int, default=-1)
     ap.add_argument("--tpw", type=int, default=0)
     ap.add_argument("--frames", type=int, default=20)
+    ap.add_argument("--wedges", type=int, default=0, help="regions schedule: wedges per XCD")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--steps", type=int, default=128)
@@ -37,6 +38,8 @@ def main():
             r.set_layout_preference(a.layout)
         if a.schedule >= 0:
             r.set_option("schedule", a.schedule)
+        if a.wedges > 0:
+            r.set_option("wedges", a.wedges)
         if a.tpw > 0:
             r.set_option("tiles_per_wave", a.tpw)
         osd, gsd = vr.reference_shader_data(a.width / a.height)

@@ -14,6 +14,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <vector>
 
 #include "../../include/vr.h"
 #include "vr_internal.h"
@@ -45,7 +46,11 @@ vr_status fail(vr_status st, const char* fmt, ...)
 
 constexpr int kDefaultSchedule = -1;     // -1 auto, 0 static tiles, 1 persistent queue, 2 strided
 constexpr int kDefaultWavesPerSimd = 4;
-constexpr int kDefaultTilesPerWave = 0;   // 0 = auto: 2 for rings, 1 for strided (measured)
+constexpr int kDefaultTilesPerWave = 0;   // 0 = auto: 2 for rings and regions, 1 for strided (measured)
+constexpr int kDefaultWedges = 2;         // regions schedule: wedges per XCD (measured)
+// a moving camera reuses the current (still complete, maybe less balanced)
+// region lists for this many renders before they are rebuilt
+constexpr int kRegionRebuildInterval = 32;
 
 struct Ctx {
     int device = 0;
@@ -70,6 +75,20 @@ struct Ctx {
     int count = 0;                 // step_counter: 0 = executed ray-steps, 1 = density evaluations
     void* d_sort = nullptr;        // procedural cost-sort scratch (proc_sort_bytes), grown on demand
     size_t sort_bytes = 0;
+    // regions schedule (build_regions): per-XCD tile lists, double-buffered
+    // so a rebuild never waits for more than the render that last used the
+    // other buffer (2 frames in flight, VulkanRenderer.cpp:13)
+    int wedges = kDefaultWedges;   // wedges per XCD
+    struct RegionBuf {
+        unsigned* d = nullptr;     // device tile list
+        unsigned* h = nullptr;     // pinned staging copy
+        size_t cap = 0;            // entries
+        hipEvent_t used = nullptr; // recorded after every launch that reads d
+        TileMap map{};
+    } region[2];
+    int region_cur = -1;           // buffer of the current lists (-1 = none)
+    std::vector<float> region_key; // geometry the current lists were built for
+    long long renders_since_build = 0;
 };
 
 // Auto layout (measured): CORNER8 does one load per tap but
@@ -335,6 +354,12 @@ vr_status vr_destroy(void* p)
     free_volume(c);
     if (c->d_heads) (void)hipFree(c->d_heads);
     if (c->d_sort) (void)hipFree(c->d_sort);
+    for (auto& b : c->region) {
+        if (b.used) (void)hipEventSynchronize(b.used);
+        if (b.d) (void)hipFree(b.d);
+        if (b.h) (void)hipHostFree(b.h);
+        if (b.used) (void)hipEventDestroy(b.used);
+    }
     delete c;
     return VR_OK;
 }
@@ -565,9 +590,9 @@ vr_status vr_set_option(void* p, const char* name, int value)
     const std::string n(name);
     if (n == "layout") return vr_set_layout_preference(p, value);
     if (n == "schedule") {
-        if (value < -1 || value > 4)
+        if (value < -1 || value > 5)
             return fail(VR_ERR_INVALID, "vr_set_option: schedule is -1 (auto), 0 (static), 1 (queue), "
-                                        "2 (strided), 3 (xcd rows) or 4 (rings)");
+                                        "2 (strided), 3 (xcd rows), 4 (rings) or 5 (regions)");
         c->schedule = value;
         return VR_OK;
     }
@@ -580,6 +605,11 @@ vr_status vr_set_option(void* p, const char* name, int value)
         if (value < 0 || value > 64)
             return fail(VR_ERR_INVALID, "vr_set_option: tiles_per_wave in [1, 64], or 0 for auto");
         c->tiles_per_wave = value;
+        return VR_OK;
+    }
+    if (n == "wedges") {
+        if (value < 1 || value > 64) return fail(VR_ERR_INVALID, "vr_set_option: wedges in [1, 64]");
+        c->wedges = value;
         return VR_OK;
     }
     if (n == "count") {
@@ -600,6 +630,7 @@ int vr_get_option(void* p, const char* name)
     if (n == "waves_per_simd") return c->waves_per_simd;
     if (n == "tiles_per_wave") return c->tiles_per_wave;
     if (n == "count") return c->count;
+    if (n == "wedges") return c->wedges;
     return -1;
 }
 
@@ -648,6 +679,117 @@ void box_centre_pixel(const Ctx* c, const MarchArgs& a, int* px, int* prow)
     }
     *px = (int)std::min(std::max(sx, 0.0), (double)(a.width - 1));
     *prow = std::min(std::max(row, 0), std::max(a.out_rows - 1, 0));
+}
+
+// Regions schedule (SCHED_REGIONS): deal the 8x8 tiles of
+// the target to the 8 XCDs as contiguous angular wedges around the projected
+// box centre, `wedges` per XCD, with equal estimated work, so that the tiles
+// one L2 serves are mostly neighbours (their rays read the same bricks).  The
+// work estimate of a tile is the longest a3 step count of the rays through its
+// 4 corners (double, no clip test; one ray per tile corner of the frame).
+// Each XCD walks its tiles inside-out (Chebyshev ring, then angle), so its
+// longest rays start first; tiles without estimated work (background, or a
+// silhouette edge missing every corner) follow, dealt round-robin.  Every tile
+// is in exactly one list whatever the estimate, so a list built for an older
+// camera stays correct: a moving camera reuses it for kRegionRebuildInterval
+// renders.  Rebuilds go to the other of two buffers, after the render that
+// last read it (an event, not a device sync), uploaded on the render stream.
+vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow, hipStream_t stream)
+{
+    const int tw = (a.width + 7) >> 3, th = (a.out_rows + 7) >> 3;
+    std::vector<float> key = {(float)tw, (float)th, (float)a.width, (float)a.height, (float)a.out_rows,
+                              (float)a.band_rows, (float)a.band_stride, (float)a.band_first, (float)tpw,
+                              (float)c->wedges};
+    const size_t grid_part = key.size();   // the part a reused list must match
+    key.insert(key.end(), {(float)a.max_steps, a.step_size, (float)cpx, (float)cprow});
+    for (const float* v : {a.org, a.o, a.px, a.py, a.box_min, a.box_max}) key.insert(key.end(), v, v + 3);
+    ++c->renders_since_build;
+    if (c->region_cur >= 0) {
+        if (key == c->region_key) return VR_OK;
+        if (c->renders_since_build < kRegionRebuildInterval &&
+            std::equal(key.begin(), key.begin() + (long)grid_part, c->region_key.begin()))
+            return VR_OK;
+    }
+
+    // a3 step estimate of the ray through pixel-corner (fx, fy) of the packed target
+    auto steps_at = [&](double fx, int orow) {
+        const int bl = orow / a.band_rows;
+        const double fy = (double)((a.band_first + bl * a.band_stride) * a.band_rows + (orow - bl * a.band_rows));
+        double d[3], len = 0.0;
+        for (int k = 0; k < 3; ++k) {
+            d[k] = a.o[k] + fx * a.px[k] + fy * a.py[k];
+            len += d[k] * d[k];
+        }
+        len = std::sqrt(len);
+        double tn = -INFINITY, tf = INFINITY;
+        for (int k = 0; k < 3; ++k) {
+            const double ta = (a.box_min[k] - a.org[k]) * len / d[k], tb = (a.box_max[k] - a.org[k]) * len / d[k];
+            tn = std::max(tn, std::min(ta, tb));
+            tf = std::min(tf, std::max(ta, tb));
+        }
+        return (tn <= tf && std::isfinite(tf)) ? std::min((double)a.max_steps, (tf - tn) / a.step_size) : 0.0;
+    };
+    std::vector<double> corner((size_t)(tw + 1) * (th + 1));
+    for (int j = 0; j <= th; ++j) {
+        const int orow = std::min(j * 8, a.out_rows);   // the row a packed-row edge starts
+        for (int i = 0; i <= tw; ++i) corner[(size_t)j * (tw + 1) + i] = steps_at(std::min(i * 8, a.width), orow);
+    }
+    struct T { unsigned id; double cost, ang; int ring; };
+    std::vector<T> work, idle;
+    const double ccx = (cpx + 0.5) / 8.0, ccy = (cprow + 0.5) / 8.0;
+    const int ctx = cpx >> 3, cty = cprow >> 3;
+    for (int ty = 0; ty < th; ++ty)
+        for (int tx = 0; tx < tw; ++tx) {
+            const double* c0 = &corner[(size_t)ty * (tw + 1) + tx];
+            const double cost = std::max(std::max(c0[0], c0[1]), std::max(c0[tw + 1], c0[tw + 2]));
+            const T t{((unsigned)ty << 16) | (unsigned)tx, cost, std::atan2(ty + 0.5 - ccy, tx + 0.5 - ccx),
+                      std::max(std::abs(tx - ctx), std::abs(ty - cty))};
+            (cost >= 1.0 ? work : idle).push_back(t);
+        }
+    std::sort(work.begin(), work.end(), [](const T& u, const T& v) { return u.ang < v.ang; });
+    double total = 0.0;
+    for (const T& t : work) total += t.cost;
+    std::vector<std::vector<T>> xl(8);
+    const int K = 8 * c->wedges;
+    double run = 0.0;
+    for (const T& t : work) {   // wedge k = the k-th K-quantile of the work, dealt to XCD k % 8
+        xl[std::min(K - 1, (int)((run + 0.5 * t.cost) / total * K)) % 8].push_back(t);
+        run += t.cost;
+    }
+    auto inside_out = [](const T& u, const T& v) { return u.ring != v.ring ? u.ring < v.ring : u.ang < v.ang; };
+    for (auto& l : xl) std::sort(l.begin(), l.end(), inside_out);
+    std::sort(idle.begin(), idle.end(), inside_out);
+    for (size_t i = 0; i < idle.size(); ++i) xl[i % 8].push_back(idle[i]);
+
+    const size_t n = (size_t)tw * th;
+    const int b = c->region_cur < 0 ? 0 : c->region_cur ^ 1;
+    Ctx::RegionBuf& rb = c->region[b];
+    if (rb.used) HIP_TRY(hipEventSynchronize(rb.used));   // the last render that read this buffer
+    else HIP_TRY(hipEventCreateWithFlags(&rb.used, hipEventDisableTiming));
+    if (n > rb.cap) {
+        if (rb.d) (void)hipFree(rb.d);
+        if (rb.h) (void)hipHostFree(rb.h);
+        rb.d = rb.h = nullptr;
+        rb.cap = 0;
+        HIP_TRY(hipMalloc(&rb.d, n * sizeof(unsigned)));
+        HIP_TRY(hipHostMalloc(&rb.h, n * sizeof(unsigned), hipHostMallocDefault));
+        rb.cap = n;
+    }
+    TileMap m{};
+    size_t pos = 0, most = 0;
+    for (int x = 0; x < 8; ++x) {
+        m.off[x] = (int)pos;
+        for (const T& t : xl[x]) rb.h[pos++] = t.id;
+        most = std::max(most, xl[x].size());
+    }
+    m.off[8] = (int)pos;
+    m.nwx = std::max(1, (int)((most + tpw - 1) / tpw));
+    HIP_TRY(hipMemcpyAsync(rb.d, rb.h, n * sizeof(unsigned), hipMemcpyHostToDevice, stream));
+    rb.map = m;
+    c->region_cur = b;
+    c->region_key = key;
+    c->renders_since_build = 0;
+    return VR_OK;
 }
 
 vr_status vr_render(void* p, const vr_target* t, void* stream)
@@ -736,7 +878,7 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
         // schedule 0 = one 8x8 tile per wave in row order, 4 = in rings;
         // otherwise (auto) the cost-sorted schedule
         void* sort_buf = nullptr;
-        Schedule sc{c->schedule == SCHED_RINGS ? SCHED_RINGS : SCHED_STATIC, 0, 0, 1, 1, nullptr};
+        Schedule sc{c->schedule == SCHED_RINGS ? SCHED_RINGS : SCHED_STATIC, 0, 0, 1, 1, nullptr, nullptr, {}};
         if (sc.kind == SCHED_RINGS) box_centre_pixel(c, a, &sc.center_x, &sc.center_y);
         if (c->schedule != SCHED_STATIC && c->schedule != SCHED_RINGS && a.width < 65536 && a.out_rows < 65536 &&
             (long long)a.width * a.out_rows < (1ll << 31)) {
@@ -756,12 +898,20 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
         HIP_TRY(launch_march_procedural(a, m.early_out > 0.0f, sort_buf, sc, static_cast<hipStream_t>(stream)));
         return VR_OK;
     }
-    // auto schedule (measured): rings, longest rays first
-    const int kind = c->schedule >= 0 ? c->schedule : SCHED_RINGS;
-    const int tpw = c->tiles_per_wave > 0 ? c->tiles_per_wave : (kind == SCHED_RINGS ? 2 : 1);
-    Schedule sc{kind, 0, 0, tpw, c->waves_per_simd, c->d_heads};
-    if (kind == SCHED_RINGS) box_centre_pixel(c, a, &sc.center_x, &sc.center_y);
+    // auto schedule (measured): regions -- per-XCD angular
+    // wedges of the frame, each walked inside-out (longest rays first)
+    const int kind = c->schedule >= 0 ? c->schedule : SCHED_REGIONS;
+    const int tpw = c->tiles_per_wave > 0 ? c->tiles_per_wave : (kind == SCHED_RINGS || kind == SCHED_REGIONS ? 2 : 1);
+    Schedule sc{kind, 0, 0, tpw, c->waves_per_simd, c->d_heads, nullptr, {}};
+    if (kind == SCHED_RINGS || kind == SCHED_REGIONS) box_centre_pixel(c, a, &sc.center_x, &sc.center_y);
+    if (kind == SCHED_REGIONS) {
+        const vr_status st = build_regions(c, a, tpw, sc.center_x, sc.center_y, static_cast<hipStream_t>(stream));
+        if (st != VR_OK) return st;
+        sc.tiles = c->region[c->region_cur].d;
+        sc.map = c->region[c->region_cur].map;
+    }
     HIP_TRY(launch_march(a, pl.layout, pl.wrap, pl.early, sc, static_cast<hipStream_t>(stream)));
+    if (kind == SCHED_REGIONS) HIP_TRY(hipEventRecord(c->region[c->region_cur].used, static_cast<hipStream_t>(stream)));
     return VR_OK;
 }
 

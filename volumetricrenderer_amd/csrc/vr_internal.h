@@ -112,13 +112,24 @@ struct MarchArgs {
 };
 
 // How the march kernel maps tiles to waves.
-enum ScheduleKind : int { SCHED_STATIC = 0, SCHED_QUEUE = 1, SCHED_STRIDED = 2, SCHED_XCDROWS = 3, SCHED_RINGS = 4 };
+enum ScheduleKind : int {
+    SCHED_STATIC = 0, SCHED_QUEUE = 1, SCHED_STRIDED = 2, SCHED_XCDROWS = 3, SCHED_RINGS = 4, SCHED_REGIONS = 5
+};
+// Regions schedule: XCD x (blockIdx % 8) renders the 8x8 tiles
+// tiles[off[x] .. off[x+1]) (packed ty << 16 | tx), wave w of its nwx waves
+// the tiles w, w + nwx, ...  Built on the host (vr_api.cpp build_regions).
+struct TileMap {
+    int off[9];
+    int nwx;
+};
 struct Schedule {
     int kind;
     int center_x, center_y;   // rings: target pixel under the projected box centre
     int tiles_per_wave;    // strided: 8x8 tiles per wave
     int waves_per_simd;    // queue: persistent waves per SIMD (grid = 256 CUs x this)
     int* heads;            // queue: 8 device ints, zeroed before each launch
+    const unsigned* tiles; // regions: device tile lists
+    TileMap map;           // regions
 };
 
 // launchers (vr_march.hip / vr_volume.hip); return hipError_t

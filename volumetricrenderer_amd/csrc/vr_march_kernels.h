@@ -671,6 +671,33 @@ __global__ __launch_bounds__(kThreads) void march_rings(const MarchArgs a, int c
     if (a.step_counter) add_steps(a, steps);
 }
 
+// Regions schedule: each XCD renders one host-built list of 8x8 tiles, a few
+// contiguous angular wedges of the frame around the box centre with equal
+// estimated work, inside-out (vr_api.cpp build_regions).  Rays of neighbouring
+// tiles read the same 128-B bricks, so keeping neighbours on one XCD lets its
+// L2 serve them once: the lines the eight L2s fetch per 1080p frame at 512^3
+// drop from ~900 MB (ring positions dealt round-robin over XCDs) to ~620 MB
+// (DESIGN.md sec. 5.3).  XCD = blockIdx % 8 is a speed-only assumption.
+template <int LAYOUT, int WRAP, bool EARLY, bool ZO>
+__global__ __launch_bounds__(kThreads) void march_regions(const MarchArgs a, const unsigned* __restrict__ tiles,
+                                                         const TileMap m)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned lds[];
+    const int xcd = blockIdx.x & 7;
+    const int w = (int)(blockIdx.x >> 3) * (kThreads / 64) + (threadIdx.x >> 6);
+    const int begin = m.off[xcd], count = m.off[xcd + 1] - begin;
+    if ((int)(blockIdx.x >> 3) * (kThreads / 64) >= count) return;   // whole workgroup, before the barrier
+    const FastCtx f = fast_prologue<LAYOUT>(a, lds);
+    const int lane = threadIdx.x & 63;
+    unsigned long long steps = 0;
+    for (int k = w; w < m.nwx && k < count; k += m.nwx) {   // the grid rounds nwx up to whole workgroups
+        const unsigned t = tiles[begin + k];
+        const int tx = (int)(t & 0xffffu), ty = (int)(t >> 16);
+        steps += march_pixel<LAYOUT, WRAP, EARLY, ZO>(a, f, tx * 8 + lane_x<LAYOUT>(lane), ty * 8 + lane_y<LAYOUT>(lane));
+    }
+    if (a.step_counter) add_steps(a, steps);
+}
+
 // XCD-row schedule: one 8x8 tile per wave, 4 horizontally adjacent tiles per
 // workgroup.  8-px tile rows are dealt to XCDs round-robin: XCD x walks rows
 // x, x+8, ... (blockIdx % 8, speed-only).  Rows interleave, so the balance
@@ -921,6 +948,18 @@ hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStre
             hipLaunchKernelGGL((march_rings<L, W, false, true>), grid, block, lds, s, a, cx, cy, nw, npos);
         else
             hipLaunchKernelGGL((march_rings<L, W, false, false>), grid, block, lds, s, a, cx, cy, nw, npos);
+        return hipGetLastError();
+    }
+    if (sc.kind == SCHED_REGIONS) {
+        const dim3 grid((unsigned)(8 * ((sc.map.nwx + 3) / 4)));
+        if (early && a.zero_offsets)
+            hipLaunchKernelGGL((march_regions<L, W, true, true>), grid, block, lds, s, a, sc.tiles, sc.map);
+        else if (early)
+            hipLaunchKernelGGL((march_regions<L, W, true, false>), grid, block, lds, s, a, sc.tiles, sc.map);
+        else if (a.zero_offsets)
+            hipLaunchKernelGGL((march_regions<L, W, false, true>), grid, block, lds, s, a, sc.tiles, sc.map);
+        else
+            hipLaunchKernelGGL((march_regions<L, W, false, false>), grid, block, lds, s, a, sc.tiles, sc.map);
         return hipGetLastError();
     }
     if (sc.kind == SCHED_XCDROWS) {
