@@ -125,8 +125,13 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--schedule", type=int, default=-1, help="vr option 'schedule' (-1 = auto)")
+    ap.add_argument("--sharder", default="native", choices=["native", "torch"],
+                    help="N > 1: native = the C++ frame loop over this library's own RCCL communicator "
+                         "(libvr_shard.so; torch.distributed/gloo only carries its id and the barriers); "
+                         "torch = BandSharder over torch.distributed")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
-                    help="gloo: rehearse the N>1 path with several ranks on one GPU")
+                    help="torch sharder's backend; gloo: rehearse the N>1 path with several ranks on one GPU")
+    ap.add_argument("--pipeline1", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -134,9 +139,15 @@ def main() -> int:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     ndev = torch.cuda.device_count()
     dev = local % max(1, ndev)
+    # --pipeline1: the native frame loop with a one-rank communicator at N = 1
+    # (a rehearsal of the N > 1 host path on one GPU; not the default N = 1 line)
+    native = (world > 1 and args.sharder == "native") or args.pipeline1
+    if native and ndev < world:
+        raise SystemExit(f"--sharder native needs one GPU per rank ({world} ranks, {ndev} GPUs); "
+                         "use --sharder torch --backend gloo to rehearse on fewer GPUs")
     if world > 1:
         torch.cuda.set_device(dev)
-        if args.backend == "nccl":
+        if args.backend == "nccl" and not native:
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group("gloo")
@@ -173,29 +184,42 @@ def main() -> int:
         torch.cuda.synchronize()
         local_evals = int(counter.item())
         r.set_option("count", 0)
-    red_dev = "cuda" if args.backend == "nccl" else "cpu"
+    red_dev = "cuda" if args.backend == "nccl" and not native else "cpu"
     tot = torch.tensor([local_steps], dtype=torch.int64, device=red_dev)
     if world > 1:
         dist.all_reduce(tot)
     frame_steps = int(tot.item())
 
-    sharder.run_frames(args.warmup)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
     # HIP events around the march launch of every 4th frame: the sample of
     # launch durations the roofline uses.  Two event records per frame cost a
     # few microseconds of queue time between frames (and, at N > 1, host time)
     ev_every = 4
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          if i % ev_every == 0 else None for i in range(args.steps)]
-    t0 = time.perf_counter()
-    sharder.run_frames(args.steps, events=ev)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    kern_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev if e is not None]))
+    if native:
+        pipe = vrdist.RcclBandPipeline(r, W, H, fmt, band_rows=16, world=world, rank=rank)
+        pipe.run_frames(args.warmup)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        kern_ms = pipe.run_frames(args.steps, sample_every=ev_every)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+    else:
+        sharder.run_frames(args.warmup)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              if i % ev_every == 0 else None for i in range(args.steps)]
+        t0 = time.perf_counter()
+        sharder.run_frames(args.steps, events=ev)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        kern_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev if e is not None]))
     tt = torch.tensor([el, kern_ms], dtype=torch.float64, device=red_dev)
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -257,7 +281,9 @@ def main() -> int:
                        "baseline_config_index": cfg_idx, "width": W, "height": H, "max_steps": S,
                        "volume": f"{N}^3 RGBA8" if N else "procedural", "camera": "reference (TestMain.cpp:219-245)",
                        "kernel": r.kernel_variant, "parallelism": f"bands16x{world}",
-                       "collective": f"gather to rank 0 ({args.backend})" if world > 1 else None,
+                       "collective": (("RCCL grouped send/recv to rank 0, native frame loop (libvr_shard)" if native
+                                       else f"torch.distributed gather to rank 0 ({args.backend})")
+                                      if world > 1 else None),
                        "executed_steps_per_frame": frame_steps},
             "executed_steps_per_s": round(frame_steps * args.steps / el, 1),
             "kernel_ms_mean": round(kern_ms, 5),
@@ -273,6 +299,8 @@ def main() -> int:
             out["cpu_baseline"] = cpu_baseline(None if proc is not None else r.get_volume(), osd, gsd, march, W, H,
                                                args.cpu_budget, procedural=proc)
         print(json.dumps(out), flush=True)
+    if native:
+        pipe.close()
     sharder.close()
     r.close()
     if world > 1:

@@ -1,0 +1,74 @@
+/*
+ * vr_shard.h -- multi-GPU frame pipeline over RCCL (libvr_shard.so).
+ *
+ * pixels are independent, so a frame shards by screen
+ * rows over the GPUs of one node.  Band b of `band_rows` rows goes to rank
+ * b mod nranks (interleaved bands: the centred hexagonal silhouette makes
+ * contiguous strips 2.45x imbalanced at 8 ranks, interleaved bands 1.00-1.02).
+ * Each rank renders its packed band set with vr_render; one RCCL exchange
+ * per frame sends the sets to rank 0 over xGMI (grouped point-to-point
+ * sends/receives), and rank 0 scatters them into the frame with
+ * vr_assemble_bands.  The reference has no multi-GPU code at all (SURVEY.md
+ * sec. 2); this replaces its single-queue frame loop (VulkanRenderer.cpp:
+ * 142-230) for N GPUs and keeps its 2 frames in flight (:13): frame i's
+ * exchange and assembly run on a communication stream while frame i+1
+ * renders, with double-buffered band sets and frames.  The whole frame loop
+ * is native, so the host cost per frame is a few HIP/RCCL calls (strong
+ * scaling of a ~0.2 ms frame to 8 GPUs is host-bound from Python).
+ *
+ * One process per GPU.  The communicator is this library's own: rank 0 makes
+ * an id with vr_shard_unique_id, the caller broadcasts its bytes (e.g. over
+ * torch.distributed), and every rank calls vr_shard_create with it.
+ * Status codes are vr_status (vr.h); messages via vr_shard_last_error().
+ */
+#ifndef VR_SHARD_H
+#define VR_SHARD_H
+#include "vr.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VR_SHARD_ID_BYTES 128
+
+typedef struct vr_shard vr_shard;
+
+const char* vr_shard_last_error(void);
+
+/* A new communicator id (call on rank 0, then share the bytes). */
+vr_status vr_shard_unique_id(uint8_t id[VR_SHARD_ID_BYTES]);
+
+/* Collective over the nranks processes: joins the communicator on ctx's
+ * device and allocates the double-buffered band sets (every rank), gather
+ * buffers and frames (rank 0) for W x H frames of `format`.  The ctx keeps
+ * its volume, shader data and march constants; vr_shard_run renders with
+ * whatever they are when it is called. */
+vr_status vr_shard_create(void* ctx, const uint8_t id[VR_SHARD_ID_BYTES], int nranks, int rank,
+                          int width, int height, int format, int band_rows, vr_shard** out);
+vr_status vr_shard_destroy(vr_shard* sh);
+
+/* Render `frames` frames (collective: every rank, same count), 2 in flight.
+ * Asynchronous on `stream` (this rank's render stream): when it returns,
+ * the work is queued and `stream` is ordered after the last frame's exchange
+ * (and, on rank 0, its assembly).  If kernel_ms is not null, every
+ * `sample_every`-th render is bracketed by HIP events on `stream` and their
+ * mean duration is written there (this call then waits for that last
+ * sample). */
+vr_status vr_shard_run(vr_shard* sh, int frames, void* stream, int sample_every, float* kernel_ms);
+
+/* Rank 0: the last assembled frame (device pointer, tight rows) once
+ * `stream` of the last vr_shard_run has reached it.  Other ranks: their
+ * last band set. */
+vr_status vr_shard_frame(vr_shard* sh, void** pixels, size_t* row_pitch, int* rows);
+
+/* Copy what vr_shard_frame points at into a caller-owned device buffer
+ * (rows of `dst_pitch` bytes; 0 = tight), ordered on `stream`. */
+vr_status vr_shard_copy_frame(vr_shard* sh, void* dst, size_t dst_pitch, void* stream);
+
+/* This rank's rows (packed) and every rank's slot rows (rank 0's count). */
+vr_status vr_shard_rows(vr_shard* sh, int* my_rows, int* rows_per_rank);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VR_SHARD_H */

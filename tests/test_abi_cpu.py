@@ -10,8 +10,8 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def header_functions():
-    src = open(os.path.join(ROOT, "include", "vr.h")).read()
+def header_functions(header="vr.h"):
+    src = open(os.path.join(ROOT, "include", header)).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(vr_[a-z_0-9]+)\s*\(", src)))
 
@@ -24,6 +24,20 @@ def test_library_exports_every_declared_symbol():
     for name in declared:
         assert hasattr(lib, name), name
     assert sorted(declared) == _lib.exported_symbols()
+
+
+def test_shard_library_exports_every_declared_symbol():
+    """libvr_shard.so (multi-GPU frame loop, RCCL) loads without a GPU and
+    exports exactly what include/vr_shard.h declares."""
+    from volumetricrenderer_amd import _lib
+    lib = _lib.load_shard()
+    declared = header_functions("vr_shard.h")
+    assert len(declared) == 8
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert sorted(declared) == _lib.shard_exported_symbols()
+    with pytest.raises(_lib.VRError):
+        _lib.shard_call("vr_shard_create", None, None, 1, 0, 64, 64, 1, 16, ctypes.byref(ctypes.c_void_p()))
 
 
 def test_abi_struct_layouts():

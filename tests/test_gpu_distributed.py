@@ -65,3 +65,36 @@ def test_gloo_ranks_on_one_gpu_assemble_the_frame(world):
     for p in procs:
         p.join(timeout=60)
     assert all(r == ("ok", True) for r in res), res
+
+
+@pytest.mark.parametrize("fmt,band_rows", [(1, 16), (0, 8)])
+def test_rccl_pipeline_one_rank(fmt, band_rows):
+    """The native frame loop (libvr_shard.so) with a one-rank RCCL
+    communicator: render into the gather slot, (no peers), assemble, 2 frames
+    in flight.  The frame equals a plain render; the kernel-time sample is
+    positive.  Multi-rank RCCL needs one GPU per rank (the driver's run)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import volumetricrenderer_amd as vr
+    from volumetricrenderer_amd.distributed import RcclBandPipeline
+    W, H = 640, 360
+    with vr.Renderer(0) as r:
+        r.generate_volume(vr.volume_recipe_defaults(size=64))
+        osd, gsd = vr.reference_shader_data(W / H, 10.0, 20.0)
+        r.set_shader_data(osd, gsd)
+        r.set_march(vr.march_defaults())
+        pl = RcclBandPipeline(r, W, H, fmt, band_rows=band_rows, world=1, rank=0)
+        try:
+            assert pl.my_rows == pl.rows_per_rank == vr.band_rows_packed(H, band_rows, 1, 0) >= H
+            ms = pl.run_frames(5, sample_every=2)
+            assert ms > 0
+            got = pl.frame()
+            full = r.render(W, H, fmt)
+            torch.cuda.synchronize()
+            assert np.array_equal(got.cpu().numpy(), full.cpu().numpy())
+            pl.run_frames(4)
+            got2 = pl.frame()
+            torch.cuda.synchronize()
+            assert np.array_equal(got2.cpu().numpy(), full.cpu().numpy())
+        finally:
+            pl.close()

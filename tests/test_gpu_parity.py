@@ -579,3 +579,32 @@ def test_regions_schedule_every_pixel_once(r, oracle, vol128, wedges):
     finally:
         r.set_option("schedule", -1)
         r.set_option("wedges", 2)
+
+
+def test_regions_lists_across_streams(r, oracle, vol128):
+    """Region lists built (and uploaded) on one stream and used on another,
+    and rebuilt while both streams have queued renders: every frame exact."""
+    r.set_option("schedule", 5)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    try:
+        r.set_volume(vol128)
+        r.set_march(vr.march_defaults())
+        outs = []
+        for i, (w, h) in enumerate([(200, 120), (200, 120), (232, 120), (232, 120), (200, 136), (200, 120)]):
+            osd, gsd = vr.reference_shader_data(w / h, 15.0 * i, 5.0 * i)
+            r.set_shader_data(osd, gsd)
+            st = s1 if i % 2 == 0 else s2
+            out = r.alloc_target(w, h, vr.FMT_RGBA8_UNORM)
+            st.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(st):
+                out.fill_(0x33)
+                r.render(w, h, vr.FMT_RGBA8_UNORM, out=out, stream=st)
+            outs.append((w, h, osd, gsd, out))
+        torch.cuda.synchronize()
+        for w, h, osd, gsd, out in outs:
+            obj, glob = vr.shader_data_arrays(osd, gsd)
+            ref, _ = oracle.render(vol128, obj, glob, oracle.from_params(vr.march_defaults()), w, h,
+                                   vr.FMT_RGBA8_UNORM)
+            assert_exact(out.cpu().numpy(), ref)
+    finally:
+        r.set_option("schedule", -1)

@@ -41,5 +41,26 @@ def main():
         print("torch add_  host %.1f us/call, wall %.1f us/call" % per_call(lambda: x.add_(1)))
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and len(sys.argv) == 1:
     main()
+
+
+def gather_overhead():
+    """Host cost of one async torch.distributed gather on the RCCL backend
+    (world 1: the collective's host path, no peers)."""
+    import torch.distributed as dist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29533")
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    x = torch.zeros(1 << 20, dtype=torch.uint8, device="cuda")
+    g = [torch.empty_like(x)]
+
+    def one():
+        w = dist.gather(x, gather_list=g, dst=0, async_op=True)
+        w.wait()
+    print("gather+wait host %.1f us/call, wall %.1f us/call" % per_call(one, 1000))
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "gather":
+    gather_overhead()

@@ -164,3 +164,52 @@ def call(name: str, *args):
         return r
     check(r, name)
     return r
+
+
+# ---- libvr_shard.so: the multi-GPU frame pipeline (include/vr_shard.h) ----
+SHARD_LIB_PATH = os.environ.get("VR_SHARD_LIB") or os.path.join(HERE, "libvr_shard.so")
+SHARD_ID_BYTES = 128
+_SHARD_SIGS = {
+    "vr_shard_last_error": (ctypes.c_char_p, []),
+    "vr_shard_unique_id": (ctypes.c_int, [_vp]),
+    "vr_shard_create": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_int, ctypes.c_int, ctypes.POINTER(_vp)]),
+    "vr_shard_destroy": (ctypes.c_int, [_vp]),
+    "vr_shard_run": (ctypes.c_int, [_vp, ctypes.c_int, _vp, ctypes.c_int, c_float_p]),
+    "vr_shard_frame": (ctypes.c_int, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(ctypes.c_size_t), c_int_p]),
+    "vr_shard_copy_frame": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, _vp]),
+    "vr_shard_rows": (ctypes.c_int, [_vp, c_int_p, c_int_p]),
+}
+_shard_lib = None
+
+
+def load_shard() -> ctypes.CDLL:
+    """Open libvr_shard.so (libvr + RCCL).  Only the multi-GPU path loads it,
+    so single-GPU users never map RCCL.  Fails loudly if absent."""
+    global _shard_lib
+    if _shard_lib is not None:
+        return _shard_lib
+    load()   # libvr first: libvr_shard binds to the same copy
+    if not os.path.exists(SHARD_LIB_PATH):
+        raise ImportError(f"libvr_shard.so not built: {SHARD_LIB_PATH} is missing (run __graft_entry__.build())")
+    lib = ctypes.CDLL(SHARD_LIB_PATH)
+    for name, (res, args) in _SHARD_SIGS.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    _shard_lib = lib
+    return lib
+
+
+def shard_exported_symbols() -> list[str]:
+    return sorted(_SHARD_SIGS)
+
+
+def shard_call(name: str, *args):
+    """Call a vr_shard_* function, raising VRError on a non-zero status."""
+    lib = load_shard()
+    r = getattr(lib, name)(*args)
+    if r != VR_OK:
+        msg = lib.vr_shard_last_error()
+        raise VRError(r, name, msg.decode(errors="replace") if msg else "")
+    return r

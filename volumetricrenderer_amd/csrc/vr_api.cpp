@@ -51,6 +51,8 @@ constexpr int kDefaultWedges = 2;         // regions schedule: wedges per XCD (m
 // a moving camera reuses the current (still complete, maybe less balanced)
 // region lists for this many renders before they are rebuilt
 constexpr int kRegionRebuildInterval = 32;
+constexpr int kMaxRegionStreams = 4;
+constexpr int kRegionKeyLen = 32;
 
 struct Ctx {
     int device = 0;
@@ -83,11 +85,19 @@ struct Ctx {
         unsigned* d = nullptr;     // device tile list
         unsigned* h = nullptr;     // pinned staging copy
         size_t cap = 0;            // entries
-        hipEvent_t used = nullptr; // recorded after every launch that reads d
         TileMap map{};
+        // the streams that rendered with these lists; when the lists are
+        // retired an event is recorded on each, and the buffer is rewritten
+        // only after those events (kMaxRegionStreams; more -> device sync)
+        hipStream_t streams[kMaxRegionStreams] = {};
+        hipEvent_t retired[kMaxRegionStreams] = {};
+        int nstreams = 0;          // -1: more streams than tracked
+        int nretired = 0;
+        hipEvent_t uploaded = nullptr;   // the list upload (on streams[0]); other streams wait for it
+        hipStream_t upload_stream = nullptr;
     } region[2];
     int region_cur = -1;           // buffer of the current lists (-1 = none)
-    std::vector<float> region_key; // geometry the current lists were built for
+    float region_key[kRegionKeyLen] = {};   // geometry the current lists were built for
     long long renders_since_build = 0;
 };
 
@@ -354,11 +364,13 @@ vr_status vr_destroy(void* p)
     free_volume(c);
     if (c->d_heads) (void)hipFree(c->d_heads);
     if (c->d_sort) (void)hipFree(c->d_sort);
+    (void)hipDeviceSynchronize();   // queued renders may still read the region lists
     for (auto& b : c->region) {
-        if (b.used) (void)hipEventSynchronize(b.used);
         if (b.d) (void)hipFree(b.d);
         if (b.h) (void)hipHostFree(b.h);
-        if (b.used) (void)hipEventDestroy(b.used);
+        for (hipEvent_t e : b.retired)
+            if (e) (void)hipEventDestroy(e);
+        if (b.uploaded) (void)hipEventDestroy(b.uploaded);
     }
     delete c;
     return VR_OK;
@@ -692,23 +704,38 @@ void box_centre_pixel(const Ctx* c, const MarchArgs& a, int* px, int* prow)
 // silhouette edge missing every corner) follow, dealt round-robin.  Every tile
 // is in exactly one list whatever the estimate, so a list built for an older
 // camera stays correct: a moving camera reuses it for kRegionRebuildInterval
-// renders.  Rebuilds go to the other of two buffers, after the render that
-// last read it (an event, not a device sync), uploaded on the render stream.
+// renders.  Rebuilds go to the other of two buffers, once the renders that
+// last read it are done (events recorded when it was retired, on the streams
+// that used it; not a device sync), uploaded on the render stream.
+vr_status note_region_stream(Ctx::RegionBuf& rb, hipStream_t s)
+{
+    if (rb.nstreams < 0) return VR_OK;
+    for (int i = 0; i < rb.nstreams; ++i)
+        if (rb.streams[i] == s) return VR_OK;
+    if (s != rb.upload_stream) HIP_TRY(hipStreamWaitEvent(s, rb.uploaded, 0));   // first use on another stream
+    if (rb.nstreams == kMaxRegionStreams) rb.nstreams = -1;
+    else rb.streams[rb.nstreams++] = s;
+    return VR_OK;
+}
+
 vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow, hipStream_t stream)
 {
     const int tw = (a.width + 7) >> 3, th = (a.out_rows + 7) >> 3;
-    std::vector<float> key = {(float)tw, (float)th, (float)a.width, (float)a.height, (float)a.out_rows,
-                              (float)a.band_rows, (float)a.band_stride, (float)a.band_first, (float)tpw,
-                              (float)c->wedges};
-    const size_t grid_part = key.size();   // the part a reused list must match
-    key.insert(key.end(), {(float)a.max_steps, a.step_size, (float)cpx, (float)cprow});
-    for (const float* v : {a.org, a.o, a.px, a.py, a.box_min, a.box_max}) key.insert(key.end(), v, v + 3);
+    float key[kRegionKeyLen] = {(float)tw, (float)th, (float)a.width, (float)a.height, (float)a.out_rows,
+                                (float)a.band_rows, (float)a.band_stride, (float)a.band_first, (float)tpw,
+                                (float)c->wedges};
+    constexpr int grid_part = 10;   // the part a reused list must match
+    int kn = grid_part;
+    for (float v : {(float)a.max_steps, a.step_size, (float)cpx, (float)cprow}) key[kn++] = v;
+    for (const float* v : {a.org, a.o, a.px, a.py, a.box_min, a.box_max})
+        for (int k = 0; k < 3; ++k) key[kn++] = v[k];
     ++c->renders_since_build;
     if (c->region_cur >= 0) {
-        if (key == c->region_key) return VR_OK;
-        if (c->renders_since_build < kRegionRebuildInterval &&
-            std::equal(key.begin(), key.begin() + (long)grid_part, c->region_key.begin()))
-            return VR_OK;
+        if (std::memcmp(key, c->region_key, sizeof key) == 0 ||
+            (c->renders_since_build < kRegionRebuildInterval &&
+             std::memcmp(key, c->region_key, grid_part * sizeof(float)) == 0)) {
+            return note_region_stream(c->region[c->region_cur], stream);
+        }
     }
 
     // a3 step estimate of the ray through pixel-corner (fx, fy) of the packed target
@@ -762,10 +789,24 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     for (size_t i = 0; i < idle.size(); ++i) xl[i % 8].push_back(idle[i]);
 
     const size_t n = (size_t)tw * th;
+    if (c->region_cur >= 0) {   // retire the current lists in the stream order of their renders
+        Ctx::RegionBuf& old = c->region[c->region_cur];
+        old.nretired = 0;
+        if (old.nstreams < 0) {
+            HIP_TRY(hipDeviceSynchronize());
+        } else {
+            for (int i = 0; i < old.nstreams; ++i) {
+                if (!old.retired[i]) HIP_TRY(hipEventCreateWithFlags(&old.retired[i], hipEventDisableTiming));
+                HIP_TRY(hipEventRecord(old.retired[i], old.streams[i]));
+            }
+            old.nretired = old.nstreams;
+        }
+        old.nstreams = 0;
+    }
     const int b = c->region_cur < 0 ? 0 : c->region_cur ^ 1;
     Ctx::RegionBuf& rb = c->region[b];
-    if (rb.used) HIP_TRY(hipEventSynchronize(rb.used));   // the last render that read this buffer
-    else HIP_TRY(hipEventCreateWithFlags(&rb.used, hipEventDisableTiming));
+    for (int i = 0; i < rb.nretired; ++i) HIP_TRY(hipEventSynchronize(rb.retired[i]));   // its last renders
+    rb.nretired = 0;
     if (n > rb.cap) {
         if (rb.d) (void)hipFree(rb.d);
         if (rb.h) (void)hipHostFree(rb.h);
@@ -785,9 +826,15 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     m.off[8] = (int)pos;
     m.nwx = std::max(1, (int)((most + tpw - 1) / tpw));
     HIP_TRY(hipMemcpyAsync(rb.d, rb.h, n * sizeof(unsigned), hipMemcpyHostToDevice, stream));
+    if (!rb.uploaded) HIP_TRY(hipEventCreateWithFlags(&rb.uploaded, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(rb.uploaded, stream));
+    rb.upload_stream = stream;
     rb.map = m;
+    rb.nstreams = 0;
+    const vr_status st = note_region_stream(rb, stream);
+    if (st != VR_OK) return st;
     c->region_cur = b;
-    c->region_key = key;
+    std::memcpy(c->region_key, key, sizeof key);
     c->renders_since_build = 0;
     return VR_OK;
 }
@@ -911,7 +958,6 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
         sc.map = c->region[c->region_cur].map;
     }
     HIP_TRY(launch_march(a, pl.layout, pl.wrap, pl.early, sc, static_cast<hipStream_t>(stream)));
-    if (kind == SCHED_REGIONS) HIP_TRY(hipEventRecord(c->region[c->region_cur].used, static_cast<hipStream_t>(stream)));
     return VR_OK;
 }
 

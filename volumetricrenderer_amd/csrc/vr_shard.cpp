@@ -1,0 +1,298 @@
+// vr_shard.cpp -- the multi-GPU frame pipeline of include/vr_shard.h
+// (libvr_shard.so: libvr + RCCL).  SURVEY.md sec. 8e; DESIGN.md sec. 7.
+//
+// Per frame i (buffers of parity p = i & 1):
+//   render stream:  wait done[p] (frame i-2's exchange / assembly has read
+//                   the parity-p buffers) -> vr_render of this rank's bands
+//                   (rank 0 renders straight into its gather slot 0)
+//                   -> record rendered[p]
+//   comm stream:    wait rendered[p] -> grouped ncclSend (rank r > 0, its
+//                   packed rows) / ncclRecv x (N-1) (rank 0, into slots
+//                   1..N-1) -> rank 0: vr_assemble_bands into frame[p]
+//                   -> record done[p]
+// so frame i's exchange overlaps frame i+1's render (the reference's 2
+// frames in flight, VulkanRenderer.cpp:13).  No host synchronisation in the
+// loop: the host cost per frame is one render launch, one RCCL group and
+// (rank 0) one assembly launch.
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include "../../include/vr_shard.h"
+
+static_assert(sizeof(ncclUniqueId) == VR_SHARD_ID_BYTES, "ncclUniqueId size");
+
+namespace {
+
+thread_local std::string g_err;
+
+vr_status fail(vr_status st, const char* fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    std::vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return st;
+}
+
+#define HIP_TRY(expr)                                                                                     \
+    do {                                                                                                  \
+        hipError_t e_ = (expr);                                                                           \
+        if (e_ != hipSuccess)                                                                             \
+            return fail(e_ == hipErrorOutOfMemory ? VR_ERR_OOM : VR_ERR_HIP, "%s: %s (%s:%d)", #expr,     \
+                        hipGetErrorString(e_), __FILE__, __LINE__);                                       \
+    } while (0)
+#define NCCL_TRY(expr)                                                                                    \
+    do {                                                                                                  \
+        ncclResult_t r_ = (expr);                                                                         \
+        if (r_ != ncclSuccess)                                                                            \
+            return fail(VR_ERR_HIP, "%s: %s (%s:%d)", #expr, ncclGetErrorString(r_), __FILE__, __LINE__); \
+    } while (0)
+#define VR_TRY(expr)                                                                                      \
+    do {                                                                                                  \
+        vr_status s_ = (expr);                                                                            \
+        if (s_ != VR_OK) return fail(s_, "%s: %s", #expr, vr_last_error());                               \
+    } while (0)
+
+}  // namespace
+
+struct vr_shard {
+    void* ctx = nullptr;
+    int device = 0;
+    int nranks = 1, rank = 0;
+    int width = 0, height = 0, format = 0, band_rows = 0, bpp = 4;
+    size_t pitch = 0;                 // tight rows
+    int my_rows = 0, rows_per_rank = 0;
+    std::vector<int> rows_of;         // packed rows of every rank
+    ncclComm_t comm = nullptr;
+    hipStream_t comm_stream = nullptr;
+    uint8_t* local[2] = {};           // rank > 0: band sets
+    uint8_t* gathered[2] = {};        // rank 0: nranks slots of rows_per_rank rows
+    uint8_t* frame[2] = {};           // rank 0
+    hipEvent_t rendered[2] = {}, done[2] = {};
+    bool pending[2] = {};             // done[p] recorded and not yet waited on
+    int last = -1;                    // parity of the last frame
+    std::vector<hipEvent_t> timing;   // sampled render brackets (pairs)
+};
+
+namespace {
+
+void release(vr_shard* sh)
+{
+    if (sh->comm_stream) (void)hipStreamSynchronize(sh->comm_stream);
+    for (int p = 0; p < 2; ++p) {
+        if (sh->local[p]) (void)hipFree(sh->local[p]);
+        if (sh->gathered[p]) (void)hipFree(sh->gathered[p]);
+        if (sh->frame[p]) (void)hipFree(sh->frame[p]);
+        if (sh->rendered[p]) (void)hipEventDestroy(sh->rendered[p]);
+        if (sh->done[p]) (void)hipEventDestroy(sh->done[p]);
+    }
+    for (hipEvent_t e : sh->timing) (void)hipEventDestroy(e);
+    if (sh->comm) (void)ncclCommDestroy(sh->comm);
+    if (sh->comm_stream) (void)hipStreamDestroy(sh->comm_stream);
+    delete sh;
+}
+
+// The parity-p band set this rank renders into.
+uint8_t* render_buf(const vr_shard* sh, int p) { return sh->rank == 0 ? sh->gathered[p] : sh->local[p]; }
+
+vr_status one_frame(vr_shard* sh, int p, hipStream_t s, hipEvent_t t0, hipEvent_t t1)
+{
+    if (sh->pending[p]) HIP_TRY(hipStreamWaitEvent(s, sh->done[p], 0));
+    vr_target t{};
+    t.width = sh->width;
+    t.height = sh->height;
+    t.format = sh->format;
+    t.band_rows = sh->band_rows;
+    t.band_stride = sh->nranks;
+    t.band_first = sh->rank;
+    t.pixels = render_buf(sh, p);
+    t.row_pitch = sh->pitch;
+    if (t0) HIP_TRY(hipEventRecord(t0, s));
+    if (sh->my_rows > 0) VR_TRY(vr_render(sh->ctx, &t, s));
+    if (t1) HIP_TRY(hipEventRecord(t1, s));
+    HIP_TRY(hipEventRecord(sh->rendered[p], s));
+    HIP_TRY(hipStreamWaitEvent(sh->comm_stream, sh->rendered[p], 0));
+    if (sh->nranks > 1) {
+        NCCL_TRY(ncclGroupStart());
+        if (sh->rank == 0) {
+            for (int r = 1; r < sh->nranks; ++r)
+                if (sh->rows_of[r] > 0)
+                    NCCL_TRY(ncclRecv(sh->gathered[p] + (size_t)r * sh->rows_per_rank * sh->pitch,
+                                      (size_t)sh->rows_of[r] * sh->pitch, ncclUint8, r, sh->comm, sh->comm_stream));
+        } else if (sh->my_rows > 0) {
+            NCCL_TRY(ncclSend(sh->local[p], (size_t)sh->my_rows * sh->pitch, ncclUint8, 0, sh->comm,
+                              sh->comm_stream));
+        }
+        NCCL_TRY(ncclGroupEnd());
+    }
+    if (sh->rank == 0)
+        VR_TRY(vr_assemble_bands(sh->ctx, sh->gathered[p], (size_t)sh->rows_per_rank, sh->nranks, sh->width,
+                                 sh->height, sh->band_rows, sh->bpp, sh->frame[p], sh->comm_stream));
+    HIP_TRY(hipEventRecord(sh->done[p], sh->comm_stream));
+    sh->pending[p] = true;
+    sh->last = p;
+    return VR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* vr_shard_last_error(void) { return g_err.c_str(); }
+
+vr_status vr_shard_unique_id(uint8_t id[VR_SHARD_ID_BYTES])
+{
+    if (!id) return fail(VR_ERR_INVALID, "vr_shard_unique_id: null");
+    ncclUniqueId u;
+    NCCL_TRY(ncclGetUniqueId(&u));
+    std::memcpy(id, &u, sizeof u);
+    return VR_OK;
+}
+
+vr_status vr_shard_create(void* ctx, const uint8_t id[VR_SHARD_ID_BYTES], int nranks, int rank, int width,
+                          int height, int format, int band_rows, vr_shard** out)
+{
+    if (!ctx || !id || !out) return fail(VR_ERR_INVALID, "vr_shard_create: null argument");
+    *out = nullptr;
+    if (nranks < 1 || rank < 0 || rank >= nranks) return fail(VR_ERR_INVALID, "vr_shard_create: rank %d of %d", rank, nranks);
+    if (width <= 0 || height <= 0 || band_rows <= 0 || format < 0 || format > 2)
+        return fail(VR_ERR_INVALID, "vr_shard_create: bad frame %dx%d format %d bands %d", width, height, format, band_rows);
+    vr_shard* sh = new (std::nothrow) vr_shard();
+    if (!sh) return fail(VR_ERR_OOM, "vr_shard_create: host allocation");
+    sh->ctx = ctx;
+    sh->nranks = nranks;
+    sh->rank = rank;
+    sh->width = width;
+    sh->height = height;
+    sh->format = format;
+    sh->band_rows = band_rows;
+    sh->bpp = format == VR_FMT_RGBA32F ? 16 : 4;
+    sh->pitch = (size_t)width * sh->bpp;
+    for (int r = 0; r < nranks; ++r) sh->rows_of.push_back(vr_band_rows_packed(height, band_rows, nranks, r));
+    sh->my_rows = sh->rows_of[rank];
+    sh->rows_per_rank = sh->rows_of[0];   // band 0 is rank 0's: it has the most rows
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    vr_status st = VR_OK;
+    auto hip_ok = [&](hipError_t r, const char* what) {
+        if (st == VR_OK && r != hipSuccess)
+            st = fail(r == hipErrorOutOfMemory ? VR_ERR_OOM : VR_ERR_HIP, "vr_shard_create: %s: %s", what,
+                      hipGetErrorString(r));
+        return st == VR_OK;
+    };
+    hip_ok(e, "hipGetDevice");
+    sh->device = dev;
+    hip_ok(hipStreamCreateWithFlags(&sh->comm_stream, hipStreamNonBlocking), "comm stream");
+    for (int p = 0; p < 2 && st == VR_OK; ++p) {
+        hip_ok(hipEventCreateWithFlags(&sh->rendered[p], hipEventDisableTiming), "event");
+        hip_ok(hipEventCreateWithFlags(&sh->done[p], hipEventDisableTiming), "event");
+        if (rank == 0) {
+            hip_ok(hipMalloc(&sh->gathered[p], (size_t)nranks * sh->rows_per_rank * sh->pitch), "gather buffer");
+            hip_ok(hipMalloc(&sh->frame[p], (size_t)height * sh->pitch), "frame buffer");
+        } else {
+            hip_ok(hipMalloc(&sh->local[p], (size_t)std::max(sh->my_rows, 1) * sh->pitch), "band buffer");
+        }
+    }
+    if (st == VR_OK) {
+        ncclUniqueId u;
+        std::memcpy(&u, id, sizeof u);
+        const ncclResult_t r = ncclCommInitRank(&sh->comm, nranks, u, rank);
+        if (r != ncclSuccess) {
+            sh->comm = nullptr;
+            st = fail(VR_ERR_HIP, "vr_shard_create: ncclCommInitRank: %s", ncclGetErrorString(r));
+        }
+    }
+    if (st != VR_OK) {
+        const std::string msg = g_err;
+        release(sh);
+        g_err = msg;
+        return st;
+    }
+    *out = sh;
+    return VR_OK;
+}
+
+vr_status vr_shard_destroy(vr_shard* sh)
+{
+    if (sh) release(sh);
+    return VR_OK;
+}
+
+vr_status vr_shard_run(vr_shard* sh, int frames, void* stream, int sample_every, float* kernel_ms)
+{
+    if (!sh || frames < 0) return fail(VR_ERR_INVALID, "vr_shard_run: bad argument");
+    if (kernel_ms && sample_every <= 0) return fail(VR_ERR_INVALID, "vr_shard_run: sample_every must be > 0");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int nsamp = kernel_ms ? (frames + sample_every - 1) / sample_every : 0;
+    while ((int)sh->timing.size() < 2 * nsamp) {
+        hipEvent_t ev;
+        HIP_TRY(hipEventCreate(&ev));
+        sh->timing.push_back(ev);
+    }
+    int next = 0;
+    for (int i = 0; i < frames; ++i) {
+        const int p = sh->last < 0 ? 0 : sh->last ^ 1;
+        const bool samp = kernel_ms && i % sample_every == 0;
+        hipEvent_t t0 = samp ? sh->timing[2 * next] : nullptr, t1 = samp ? sh->timing[2 * next + 1] : nullptr;
+        if (samp) ++next;
+        const vr_status st = one_frame(sh, p, s, t0, t1);
+        if (st != VR_OK) return st;
+    }
+    if (sh->last >= 0) HIP_TRY(hipStreamWaitEvent(s, sh->done[sh->last], 0));   // the caller's stream sees the frame
+    if (kernel_ms) {
+        double sum = 0.0;
+        for (int k = 0; k < next; ++k) {
+            HIP_TRY(hipEventSynchronize(sh->timing[2 * k + 1]));
+            float ms = 0.0f;
+            HIP_TRY(hipEventElapsedTime(&ms, sh->timing[2 * k], sh->timing[2 * k + 1]));
+            sum += ms;
+        }
+        *kernel_ms = next ? (float)(sum / next) : 0.0f;
+    }
+    return VR_OK;
+}
+
+vr_status vr_shard_frame(vr_shard* sh, void** pixels, size_t* row_pitch, int* rows)
+{
+    if (!sh || !pixels) return fail(VR_ERR_INVALID, "vr_shard_frame: null argument");
+    if (sh->last < 0) return fail(VR_ERR_INVALID, "vr_shard_frame: no frame rendered yet");
+    *pixels = sh->rank == 0 ? sh->frame[sh->last] : sh->local[sh->last];
+    if (row_pitch) *row_pitch = sh->pitch;
+    if (rows) *rows = sh->rank == 0 ? sh->height : sh->my_rows;
+    return VR_OK;
+}
+
+vr_status vr_shard_copy_frame(vr_shard* sh, void* dst, size_t dst_pitch, void* stream)
+{
+    void* src = nullptr;
+    size_t pitch = 0;
+    int rows = 0;
+    const vr_status st = vr_shard_frame(sh, &src, &pitch, &rows);
+    if (st != VR_OK) return st;
+    if (!dst) return fail(VR_ERR_INVALID, "vr_shard_copy_frame: null dst");
+    if (dst_pitch == 0) dst_pitch = pitch;
+    if (dst_pitch < pitch) return fail(VR_ERR_INVALID, "vr_shard_copy_frame: dst_pitch %zu < %zu", dst_pitch, pitch);
+    HIP_TRY(hipMemcpy2DAsync(dst, dst_pitch, src, pitch, pitch, (size_t)rows, hipMemcpyDeviceToDevice,
+                             static_cast<hipStream_t>(stream)));
+    return VR_OK;
+}
+
+vr_status vr_shard_rows(vr_shard* sh, int* my_rows, int* rows_per_rank)
+{
+    if (!sh) return fail(VR_ERR_INVALID, "vr_shard_rows: null");
+    if (my_rows) *my_rows = sh->my_rows;
+    if (rows_per_rank) *rows_per_rank = sh->rows_per_rank;
+    return VR_OK;
+}
+
+}  // extern "C"

@@ -14,8 +14,12 @@ One process per GPU; the reference has no distributed code at all.
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 import torch.distributed as dist
+
+from . import _lib
 
 
 def rows_for_rank(height: int, band_rows: int, world: int, rank: int) -> int:
@@ -176,3 +180,58 @@ class BandSharder:
         self.gathered = None
         self.frame_buf = None
         self._pipe = None
+
+
+class RcclBandPipeline:
+    """The native multi-GPU frame loop (libvr_shard.so, include/vr_shard.h):
+    the same interleaved bands and gather to rank 0 as :class:`BandSharder`,
+    but the exchange is this library's own RCCL communicator (grouped
+    point-to-point sends/receives over xGMI) and the whole 2-in-flight frame
+    loop runs in C++, so the host cost per frame is a few HIP/RCCL calls.
+
+    `group` is any torch.distributed group (gloo is enough): it only carries
+    the communicator id from rank 0 and the barriers."""
+
+    def __init__(self, renderer, width: int, height: int, fmt: int, band_rows: int = 16, world: int = 1,
+                 rank: int = 0, group=None):
+        self.r = renderer
+        self.width, self.height, self.fmt = width, height, fmt
+        self.world, self.rank = world, rank
+        uid = (ctypes.c_uint8 * _lib.SHARD_ID_BYTES)()
+        if rank == 0:
+            _lib.shard_call("vr_shard_unique_id", uid)
+        if world > 1:
+            backend = dist.get_backend(group)
+            t = torch.tensor(bytearray(uid), dtype=torch.uint8,
+                             device="cuda" if backend == "nccl" else "cpu")
+            dist.broadcast(t, src=0, group=group)
+            ctypes.memmove(uid, bytes(t.cpu().tolist()), _lib.SHARD_ID_BYTES)
+        h = ctypes.c_void_p()
+        _lib.shard_call("vr_shard_create", renderer._ctx, uid, world, rank, width, height, fmt, band_rows,
+                        ctypes.byref(h))
+        self._h = h
+        mine, per = ctypes.c_int(), ctypes.c_int()
+        _lib.shard_call("vr_shard_rows", h, ctypes.byref(mine), ctypes.byref(per))
+        self.my_rows, self.rows_per_rank = mine.value, per.value
+
+    def run_frames(self, k: int, stream=None, sample_every: int = 0):
+        """Queue k frames (collective).  Returns the mean duration (ms) of the
+        sampled renders when sample_every > 0, else None."""
+        from .renderer import _stream_handle
+        ms = ctypes.c_float()
+        _lib.shard_call("vr_shard_run", self._h, k, _stream_handle(stream), sample_every,
+                        ctypes.byref(ms) if sample_every > 0 else None)
+        return ms.value if sample_every > 0 else None
+
+    def frame(self, stream=None) -> torch.Tensor:
+        """A copy of the last frame (rank 0) or band set (other ranks)."""
+        from .renderer import _stream_handle
+        rows = self.height if self.rank == 0 else self.my_rows
+        out = self.r.alloc_target(self.width, rows, self.fmt)
+        _lib.shard_call("vr_shard_copy_frame", self._h, ctypes.c_void_p(out.data_ptr()), 0, _stream_handle(stream))
+        return out
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.shard_call("vr_shard_destroy", self._h)
+            self._h = None
