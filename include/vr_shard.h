@@ -42,7 +42,10 @@ vr_status vr_shard_unique_id(uint8_t id[VR_SHARD_ID_BYTES]);
  * device and allocates the double-buffered band sets (every rank), gather
  * buffers and frames (rank 0) for W x H frames of `format`.  The ctx keeps
  * its volume, shader data and march constants; vr_shard_run renders with
- * whatever they are when it is called. */
+ * whatever they are when it is called.
+ * Loopback (id = NULL, rank 0): no communicator; this process renders every
+ * rank's band set into its gather slot and assembles the frame -- the
+ * N-rank data layout and assembly on one GPU (tests, rehearsals). */
 vr_status vr_shard_create(void* ctx, const uint8_t id[VR_SHARD_ID_BYTES], int nranks, int rank,
                           int width, int height, int format, int band_rows, vr_shard** out);
 vr_status vr_shard_destroy(vr_shard* sh);

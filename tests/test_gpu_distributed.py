@@ -98,3 +98,30 @@ def test_rccl_pipeline_one_rank(fmt, band_rows):
             assert np.array_equal(got2.cpu().numpy(), full.cpu().numpy())
         finally:
             pl.close()
+
+
+@pytest.mark.parametrize("world,band_rows,fmt", [(2, 16, 1), (3, 16, 0), (8, 16, 1), (5, 7, 1)])
+def test_native_pipeline_loopback_ranks(world, band_rows, fmt):
+    """The native frame loop's N-rank data layout (packed band sets in gather
+    slots of rank 0's row count, vr_assemble_bands) with every rank's bands
+    rendered by this one process: the frame equals a plain render."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import volumetricrenderer_amd as vr
+    from volumetricrenderer_amd.distributed import RcclBandPipeline
+    W, H = 500, 283
+    with vr.Renderer(0) as r:
+        r.generate_volume(vr.volume_recipe_defaults(size=64))
+        osd, gsd = vr.reference_shader_data(W / H, -30.0, 40.0)
+        r.set_shader_data(osd, gsd)
+        r.set_march(vr.march_defaults())
+        pl = RcclBandPipeline(r, W, H, fmt, band_rows=band_rows, world=world, rank=0, loopback=True)
+        try:
+            assert pl.rows_per_rank == vr.band_rows_packed(H, band_rows, world, 0)
+            pl.run_frames(3)
+            got = pl.frame()
+            full = r.render(W, H, fmt)
+            torch.cuda.synchronize()
+            assert np.array_equal(got.cpu().numpy(), full.cpu().numpy())
+        finally:
+            pl.close()

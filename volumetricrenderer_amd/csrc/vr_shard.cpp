@@ -81,6 +81,7 @@ struct vr_shard {
     hipEvent_t rendered[2] = {}, done[2] = {};
     bool pending[2] = {};             // done[p] recorded and not yet waited on
     int last = -1;                    // parity of the last frame
+    bool loopback = false;            // one process emulates all ranks (no RCCL)
     std::vector<hipEvent_t> timing;   // sampled render brackets (pairs)
 };
 
@@ -120,9 +121,15 @@ vr_status one_frame(vr_shard* sh, int p, hipStream_t s, hipEvent_t t0, hipEvent_
     if (t0) HIP_TRY(hipEventRecord(t0, s));
     if (sh->my_rows > 0) VR_TRY(vr_render(sh->ctx, &t, s));
     if (t1) HIP_TRY(hipEventRecord(t1, s));
+    if (sh->loopback)   // the other ranks' band sets, rendered here into their gather slots
+        for (int r = 1; r < sh->nranks; ++r) {
+            t.band_first = r;
+            t.pixels = sh->gathered[p] + (size_t)r * sh->rows_per_rank * sh->pitch;
+            if (sh->rows_of[r] > 0) VR_TRY(vr_render(sh->ctx, &t, s));
+        }
     HIP_TRY(hipEventRecord(sh->rendered[p], s));
     HIP_TRY(hipStreamWaitEvent(sh->comm_stream, sh->rendered[p], 0));
-    if (sh->nranks > 1) {
+    if (sh->nranks > 1 && !sh->loopback) {
         NCCL_TRY(ncclGroupStart());
         if (sh->rank == 0) {
             for (int r = 1; r < sh->nranks; ++r)
@@ -162,14 +169,17 @@ vr_status vr_shard_unique_id(uint8_t id[VR_SHARD_ID_BYTES])
 vr_status vr_shard_create(void* ctx, const uint8_t id[VR_SHARD_ID_BYTES], int nranks, int rank, int width,
                           int height, int format, int band_rows, vr_shard** out)
 {
-    if (!ctx || !id || !out) return fail(VR_ERR_INVALID, "vr_shard_create: null argument");
+    if (!ctx || !out) return fail(VR_ERR_INVALID, "vr_shard_create: null argument");
     *out = nullptr;
+    const bool loopback = !id && rank == 0;
+    if (!id && !loopback) return fail(VR_ERR_INVALID, "vr_shard_create: null id (loopback needs rank 0)");
     if (nranks < 1 || rank < 0 || rank >= nranks) return fail(VR_ERR_INVALID, "vr_shard_create: rank %d of %d", rank, nranks);
     if (width <= 0 || height <= 0 || band_rows <= 0 || format < 0 || format > 2)
         return fail(VR_ERR_INVALID, "vr_shard_create: bad frame %dx%d format %d bands %d", width, height, format, band_rows);
     vr_shard* sh = new (std::nothrow) vr_shard();
     if (!sh) return fail(VR_ERR_OOM, "vr_shard_create: host allocation");
     sh->ctx = ctx;
+    sh->loopback = loopback;
     sh->nranks = nranks;
     sh->rank = rank;
     sh->width = width;
@@ -203,7 +213,7 @@ vr_status vr_shard_create(void* ctx, const uint8_t id[VR_SHARD_ID_BYTES], int nr
             hip_ok(hipMalloc(&sh->local[p], (size_t)std::max(sh->my_rows, 1) * sh->pitch), "band buffer");
         }
     }
-    if (st == VR_OK) {
+    if (st == VR_OK && !loopback) {
         ncclUniqueId u;
         std::memcpy(&u, id, sizeof u);
         const ncclResult_t r = ncclCommInitRank(&sh->comm, nranks, u, rank);

@@ -193,14 +193,19 @@ class RcclBandPipeline:
     the communicator id from rank 0 and the barriers."""
 
     def __init__(self, renderer, width: int, height: int, fmt: int, band_rows: int = 16, world: int = 1,
-                 rank: int = 0, group=None):
+                 rank: int = 0, group=None, loopback: bool = False):
+        """loopback: one process renders all `world` ranks' band sets on its
+        GPU and assembles them (no communicator; tests and rehearsals)."""
         self.r = renderer
         self.width, self.height, self.fmt = width, height, fmt
         self.world, self.rank = world, rank
         uid = (ctypes.c_uint8 * _lib.SHARD_ID_BYTES)()
-        if rank == 0:
+        if loopback:
+            assert rank == 0
+            uid = None
+        elif rank == 0:
             _lib.shard_call("vr_shard_unique_id", uid)
-        if world > 1:
+        if world > 1 and not loopback:
             backend = dist.get_backend(group)
             t = torch.tensor(bytearray(uid), dtype=torch.uint8,
                              device="cuda" if backend == "nccl" else "cpu")
