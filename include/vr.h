@@ -208,7 +208,8 @@ const char* vr_kernel_variant(void* ctx);
 /* Choose the device volume layout: 0 = auto (default),
  * 1 = planar only, 2 = 4^3 apron bricks in 128-B lines ("brick5"),
  * 3 = 7^3 apron bricks of 512 B ("brick8"), 4 = 15^3 apron bricks of 4 KiB
- * ("brick16"), 5 = 8-corner footprint words ("corner8").  Layouts 2-5 are
+ * ("brick16"), 5 = 8-corner footprint words ("corner8"), 6 = 3^3 apron
+ * bricks of 64 B ("brick4").  Layouts 2-6 are
  * used only where clamp-to-edge equals mirrored repeat.  Otherwise the
  * planar, mirrored-repeat kernel runs.  Rebuilds the layout (synchronous). */
 vr_status vr_set_layout_preference(void* ctx, int pref);

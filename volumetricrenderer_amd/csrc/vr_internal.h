@@ -29,8 +29,10 @@ enum Layout : int {
     LAYOUT_BRICK16 = 4,   // B=15: 16^3 = 4 KiB bricks (1.21x bytes)
     LAYOUT_CORNER8 = 5,   // per base texel its 8 footprint bytes (u64) in 4^3
                           // position bricks of 512 B (8x bytes); 1 load per tap
+    LAYOUT_BRICK4 = 6,    // B=3: 3^3 texels + apron = 4^3 = 64 B (2.37x bytes);
+                          // a z-slice of a footprint is one dword-aligned 8-B load
 };
-constexpr int kNumLayouts = 6;
+constexpr int kNumLayouts = 7;
 
 enum Wrap : int { WRAP_CLAMP = 0, WRAP_MIRROR = 1 };
 
@@ -47,10 +49,11 @@ __host__ __device__ inline LayoutGeom layout_geom(int layout, int nx, int ny, in
     if (layout == LAYOUT_CORNER8) {
         g.B = 4; g.R = 4; g.brick = 512;
     } else {
-        g.B = layout == LAYOUT_BRICK5 ? 4 : layout == LAYOUT_BRICK8 ? 7 : 15;
+        g.B = layout == LAYOUT_BRICK4 ? 3 : layout == LAYOUT_BRICK5 ? 4 : layout == LAYOUT_BRICK8 ? 7 : 15;
         g.R = g.B + 1;
         const unsigned r3 = (unsigned)(g.R * g.R * g.R);
-        g.brick = (r3 + 127u) & ~127u;   // whole 128-B lines
+        // whole 128-B lines; BRICK4's 64-B bricks pair up in one line
+        g.brick = layout == LAYOUT_BRICK4 ? 64u : (r3 + 127u) & ~127u;
     }
     // padded base positions a in [0, N] -> bricks a / B in [0, N / B]
     g.nbx = nx / g.B + 1;

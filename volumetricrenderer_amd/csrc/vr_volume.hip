@@ -239,6 +239,7 @@ hipError_t launch_build_layout(int layout, const uint8_t* d_planar, int nx, int 
     const long long pb = (long long)layout_plane_bytes(layout, nx, ny, nz);
     const dim3 gr(grid_for(4 * elems)), b(kBlock);
     switch (layout) {
+    case LAYOUT_BRICK4: hipLaunchKernelGGL(k_build_layout<LAYOUT_BRICK4>, gr, b, 0, s, d_planar, nx, ny, nz, g, elems, pb, d_out); break;
     case LAYOUT_BRICK5: hipLaunchKernelGGL(k_build_layout<LAYOUT_BRICK5>, gr, b, 0, s, d_planar, nx, ny, nz, g, elems, pb, d_out); break;
     case LAYOUT_BRICK8: hipLaunchKernelGGL(k_build_layout<LAYOUT_BRICK8>, gr, b, 0, s, d_planar, nx, ny, nz, g, elems, pb, d_out); break;
     case LAYOUT_BRICK16: hipLaunchKernelGGL(k_build_layout<LAYOUT_BRICK16>, gr, b, 0, s, d_planar, nx, ny, nz, g, elems, pb, d_out); break;
