@@ -232,6 +232,11 @@ vr_status vr_set_layout_preference(void* ctx, int pref);
  *   "tiles_per_wave"  1-64, strided, ring and region schedules; 0 = auto,
  *                     the default: 2 for rings and regions, 1 for strided.
  *   "wedges"          1-64, regions schedule: wedges per XCD (default 2).
+ *   "split"           regions schedule, brick4/corner8 layouts: lanes per ray
+ *                     (1, 2, 4, 8; each lane marches every K-th step and the
+ *                     terms are summed in step order, bit-exact); 0 = auto,
+ *                     the default: 2 or 4 when the target has too few rays
+ *                     to fill the GPU (a 1/N share of a frame).
  *   "count"           0 = vr_target.step_counter sums executed ray-steps (the
  *                     default); 1 = it sums density evaluations, i.e.
  *                     ray-steps plus the procedural shadow samples -- the unit

@@ -609,3 +609,27 @@ def test_regions_lists_across_streams(r, oracle, vol128):
             assert_exact(out.cpu().numpy(), ref)
     finally:
         r.set_option("schedule", -1)
+
+
+@pytest.mark.parametrize("layout", [6, 5])
+@pytest.mark.parametrize("split", [2, 4, 8])
+def test_split_rays_bitexact(r, oracle, vol128, layout, split):
+    """Step-split rays (K lanes per ray, terms summed in step order): exact
+    against the oracle, step counts included, with bands, a rotated cube,
+    early-out and short rays (max_steps 7)."""
+    r.set_layout_preference(layout)
+    r.set_option("schedule", 5)
+    r.set_option("split", split)
+    try:
+        osd, gsd = vr.reference_shader_data(16 / 9, 25.0, -40.0)
+        for W, H, band, march in [(333, 187, {}, vr.march_defaults()),
+                                  (640, 360, dict(band_rows=16, band_stride=3, band_first=2), vr.march_defaults()),
+                                  (320, 180, {}, vr.march_defaults(max_steps=7)),
+                                  (320, 180, {}, vr.march_defaults(early_out=0.6, density=4.0))]:
+            img, ref, c, s = render_both(r, oracle, vol128, W, H, osd, gsd, march=march, **band)
+            assert_exact(img, ref)
+            assert c == s
+    finally:
+        r.set_option("split", 0)
+        r.set_option("schedule", -1)
+        r.set_layout_preference(0)

@@ -1,0 +1,56 @@
+"""Per-rank render time of the strong-scaled frame on ONE GPU: rank 0's band
+set (16-row bands, stride N) for N = 1, 2, 4, 8, against the whole frame / N.
+What a rank of bench.py --gpus N renders per frame, without the exchange.
+
+    python tools/band_scaling.py [--size 512] [--config grid512] [--tpw 0] [--schedule -1]
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import volumetricrenderer_amd as vr  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--size", type=int, default=512)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--steps", type=int, default=128)
+    ap.add_argument("--frames", type=int, default=20)
+    ap.add_argument("--variants", default="-1:0:0", help="comma list of schedule:tiles_per_wave:split")
+    a = ap.parse_args()
+    W, H = a.width, a.height
+    with vr.Renderer(0) as r:
+        r.generate_volume(vr.scaled_recipe(a.size))
+        osd, gsd = vr.reference_shader_data(1280 / 720)
+        r.set_shader_data(osd, gsd)
+        r.set_march(vr.march_defaults(max_steps=a.steps))
+        for var in a.variants.split(","):
+            sched, tpw, split = (int(v) for v in var.split(":"))
+            r.set_option("schedule", sched)
+            r.set_option("tiles_per_wave", tpw)
+            r.set_option("split", split)
+            base = None
+            for n in (1, 2, 4, 8):
+                band = dict(band_rows=16, band_stride=n, band_first=0)
+                out = r.alloc_target(W, H, 1, **band)
+                r.render(W, H, 1, out=out, **band)
+                ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.frames)]
+                for i in range(a.frames):
+                    ev[2 * i].record()
+                    r.render(W, H, 1, out=out, **band)
+                    ev[2 * i + 1].record()
+                torch.cuda.synchronize()
+                t = float(np.median([ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(a.frames)]))
+                base = base or t
+                print(f"schedule {sched} tpw {tpw} split {split} N={n}: rank-0 bands {t:.4f} ms, whole/N {base / n:.4f} ms, "
+                      f"efficiency {base / n / t:.2f}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -53,6 +53,11 @@ constexpr int kDefaultWedges = 2;         // regions schedule: wedges per XCD (m
 constexpr int kRegionRebuildInterval = 32;
 constexpr int kMaxRegionStreams = 4;
 constexpr int kRegionKeyLen = 32;
+// auto split: lanes per ray doubled (up to 4) while the frame's tiles with
+// work, times lanes per ray, stay under this many (measured on 1/N of the
+// 1080p frame, DESIGN.md sec. 7: K = 1, 2, 4, 4 at N = 1, 2, 4, 8)
+constexpr long long kSplitTargetUnits = 6000;
+constexpr int kMaxAutoSplit = 4;
 
 struct Ctx {
     int device = 0;
@@ -81,11 +86,13 @@ struct Ctx {
     // so a rebuild never waits for more than the render that last used the
     // other buffer (2 frames in flight, VulkanRenderer.cpp:13)
     int wedges = kDefaultWedges;   // wedges per XCD
+    int split = 0;                 // lanes per ray: 0 = auto, 1, 2, 4, 8
     struct RegionBuf {
         unsigned* d = nullptr;     // device tile list
         unsigned* h = nullptr;     // pinned staging copy
         size_t cap = 0;            // entries
         TileMap map{};
+        int nwork = 0;             // tiles with estimated work
         // the streams that rendered with these lists; when the lists are
         // retired an event is recorded on each, and the buffer is rewritten
         // only after those events (kMaxRegionStreams; more -> device sync)
@@ -622,6 +629,12 @@ vr_status vr_set_option(void* p, const char* name, int value)
         c->tiles_per_wave = value;
         return VR_OK;
     }
+    if (n == "split") {
+        if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8)
+            return fail(VR_ERR_INVALID, "vr_set_option: split is 0 (auto), 1, 2, 4 or 8");
+        c->split = value;
+        return VR_OK;
+    }
     if (n == "wedges") {
         if (value < 1 || value > 64) return fail(VR_ERR_INVALID, "vr_set_option: wedges in [1, 64]");
         c->wedges = value;
@@ -646,6 +659,7 @@ int vr_get_option(void* p, const char* name)
     if (n == "tiles_per_wave") return c->tiles_per_wave;
     if (n == "count") return c->count;
     if (n == "wedges") return c->wedges;
+    if (n == "split") return c->split;
     return -1;
 }
 
@@ -833,6 +847,7 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     HIP_TRY(hipEventRecord(rb.uploaded, stream));
     rb.upload_stream = stream;
     rb.map = m;
+    rb.nwork = (int)work.size();
     rb.nstreams = 0;
     const vr_status st = note_region_stream(rb, stream);
     if (st != VR_OK) return st;
@@ -928,7 +943,7 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
         // schedule 0 = one 8x8 tile per wave in row order, 4 = in rings;
         // otherwise (auto) the cost-sorted schedule
         void* sort_buf = nullptr;
-        Schedule sc{c->schedule == SCHED_RINGS ? SCHED_RINGS : SCHED_STATIC, 0, 0, 1, 1, nullptr, nullptr, {}};
+        Schedule sc{c->schedule == SCHED_RINGS ? SCHED_RINGS : SCHED_STATIC, 0, 0, 1, 1, nullptr, nullptr, {}, 1};
         if (sc.kind == SCHED_RINGS) box_centre_pixel(c, a, &sc.center_x, &sc.center_y);
         if (c->schedule != SCHED_STATIC && c->schedule != SCHED_RINGS && a.width < 65536 && a.out_rows < 65536 &&
             (long long)a.width * a.out_rows < (1ll << 31)) {
@@ -952,13 +967,30 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
     // wedges of the frame, each walked inside-out (longest rays first)
     const int kind = c->schedule >= 0 ? c->schedule : SCHED_REGIONS;
     const int tpw = c->tiles_per_wave > 0 ? c->tiles_per_wave : (kind == SCHED_RINGS || kind == SCHED_REGIONS ? 2 : 1);
-    Schedule sc{kind, 0, 0, tpw, c->waves_per_simd, c->d_heads, nullptr, {}};
+    Schedule sc{kind, 0, 0, tpw, c->waves_per_simd, c->d_heads, nullptr, {}, 1};
     if (kind == SCHED_RINGS || kind == SCHED_REGIONS) box_centre_pixel(c, a, &sc.center_x, &sc.center_y);
     if (kind == SCHED_REGIONS) {
         const vr_status st = build_regions(c, a, tpw, sc.center_x, sc.center_y, static_cast<hipStream_t>(stream));
         if (st != VR_OK) return st;
-        sc.tiles = c->region[c->region_cur].d;
-        sc.map = c->region[c->region_cur].map;
+        const Ctx::RegionBuf& rb = c->region[c->region_cur];
+        sc.tiles = rb.d;
+        sc.map = rb.map;
+        // step-split rays: K lanes per ray when the frame
+        // share is too small to fill the GPU with one-lane-per-ray waves
+        if (pl.layout == LAYOUT_BRICK4 || pl.layout == LAYOUT_CORNER8) {
+            int K = c->split;
+            if (K == 0) {
+                K = 1;
+                while (K < kMaxAutoSplit && (long long)rb.nwork * K < kSplitTargetUnits) K *= 2;
+            }
+            if (K > 1) {
+                const int ktpw = tpw;
+                int most = 0;
+                for (int x = 0; x < 8; ++x) most = std::max(most, rb.map.off[x + 1] - rb.map.off[x]);
+                sc.split = K;
+                sc.map.nwx = std::max(1, (most * K + ktpw - 1) / ktpw);
+            }
+        }
     }
     HIP_TRY(launch_march(a, pl.layout, pl.wrap, pl.early, sc, static_cast<hipStream_t>(stream)));
     return VR_OK;

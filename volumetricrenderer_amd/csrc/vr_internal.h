@@ -132,7 +132,8 @@ struct Schedule {
     int waves_per_simd;    // queue: persistent waves per SIMD (grid = 256 CUs x this)
     int* heads;            // queue: 8 device ints, zeroed before each launch
     const unsigned* tiles; // regions: device tile lists
-    TileMap map;           // regions
+    TileMap map;           // regions (nwx counts waves of split units)
+    int split;             // regions: lanes per ray (1, 2, 4, 8; BRICK4 / CORNER8 only)
 };
 
 // launchers (vr_march.hip / vr_volume.hip); return hipError_t

@@ -710,6 +710,110 @@ __global__ __launch_bounds__(kThreads) void march_regions(const MarchArgs a, con
     if (a.step_counter) add_steps(a, steps);
 }
 
+// ---- step-split rays (regions schedule) ----
+// A wave whose rays march alone on their SIMD waits ~110 dependent memory
+// round trips (the longest ray's steps): with a small share of the frame per
+// GPU (N GPUs strong-scaled) there are too few waves to hide that.  Here K
+// lanes share one ray: lane k computes the terms of steps k, k+K, k+2K, ...
+// and the K terms of each round are added to `acc` in step order, so the sum
+// is frag.glsl:71-73's sequential one, bit for bit.  A lane reaches its own
+// ray points by the same sequence of fp32 adds as the reference loop (k adds,
+// then K per round): P_i is never formed as P_0 + i*step.  The K lanes of a
+// ray share n, so they loop, shuffle and stop together.  Lanes beyond the
+// last step fetch the ray's entry point (in the box) and their terms are not
+// added.
+template <int LAYOUT, bool EARLY, bool ZO, int K>
+__device__ __forceinline__ unsigned march_pixel_split(const MarchArgs& a, const FastCtx& f, int x, int orow,
+                                                      int k, int ray_lane)
+{
+    constexpr int R = 64 / K;
+    const Ray r = setup_ray(a, x, orow);
+    const int n = r.n;
+    f2 pxy = r.pxy;
+    float pz = r.pz;
+    for (int j = 0; j < k; ++j) { pxy = pxy + r.sxy; pz = pz + r.sz; }   // this lane's first step
+    float acc = 0.0f;
+    int i = 0;
+    if (n > 0) {
+        const bool mine0 = k < n;
+        TapRaw c0 = tap_fetch_at<LAYOUT, ZO>(a, f, 0, mine0 ? pxy : r.pxy, mine0 ? pz : r.pz);
+        TapRaw c1 = tap_fetch_at<LAYOUT, ZO>(a, f, 1, mine0 ? pxy : r.pxy, mine0 ? pz : r.pz);
+        TapRaw c2 = tap_fetch_at<LAYOUT, ZO>(a, f, 2, mine0 ? pxy : r.pxy, mine0 ? pz : r.pz);
+        TapRaw c3 = tap_fetch_at<LAYOUT, ZO>(a, f, 3, mine0 ? pxy : r.pxy, mine0 ? pz : r.pz);
+        for (int base = 0; base < n; base += K) {
+            for (int j = 0; j < K; ++j) { pxy = pxy + r.sxy; pz = pz + r.sz; }   // step base + K + k
+            const bool mine = base + K + k < n;
+            const f2 qxy = mine ? pxy : r.pxy;
+            const float qz = mine ? pz : r.pz;
+            const TapRaw n0 = tap_fetch_at<LAYOUT, ZO>(a, f, 0, qxy, qz), n1 = tap_fetch_at<LAYOUT, ZO>(a, f, 1, qxy, qz);
+            const TapRaw n2 = tap_fetch_at<LAYOUT, ZO>(a, f, 2, qxy, qz), n3 = tap_fetch_at<LAYOUT, ZO>(a, f, 3, qxy, qz);
+            const float t0 = tap_blend<LAYOUT>(c0), t1 = tap_blend<LAYOUT>(c1);
+            const float t2 = tap_blend<LAYOUT>(c2), t3 = tap_blend<LAYOUT>(c3);
+            const float term = ((t0 * t1) * (t2 + t3)) * a.scale;                        // :71-73
+            bool stop = false;
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                const float tj = __shfl(term, ray_lane + j * R);
+                if (base + j < n && !stop) {
+                    acc = acc + tj;
+                    ++i;
+                    if constexpr (EARLY) stop = acc > a.acc_limit;
+                }
+            }
+            if constexpr (EARLY) {
+                if (stop) break;
+            }
+            c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+        }
+    }
+    if (r.live && k == 0) {
+        const float at = acc * a.step_size;
+        store_pixel(a, x, orow, n >= 0, 1.0f - spec_expf(a.density * fminf(-at, 0.0f)));
+    }
+    return (n > 0 && k == 0) ? (unsigned)i : 0u;
+}
+
+// Regions schedule with step-split rays: an 8x8 tile is K sub-blocks of 64/K
+// rays (8x8, 8x4, 4x4, 4x2 pixels), one per wave; wave w of its XCD's nwx
+// renders the units (tile, sub-block) w, w + nwx, ...  Lane = k * (64/K) + ray,
+// so 4 adjacent lanes are a 2x2 pixel quad at the same step offset.
+template <int LAYOUT, bool EARLY, bool ZO, int K>
+__global__ __launch_bounds__(kThreads) void march_regions_split(const MarchArgs a, const unsigned* __restrict__ tiles,
+                                                               const TileMap m)
+{
+    constexpr int R = 64 / K, SW = K >= 4 ? 4 : 8, SH = R / SW, NSX = 8 / SW;
+    extern __shared__ __attribute__((aligned(16))) unsigned lds[];
+    const int xcd = blockIdx.x & 7;
+    const int w = (int)(blockIdx.x >> 3) * (kThreads / 64) + (threadIdx.x >> 6);
+    const int begin = m.off[xcd], units = (m.off[xcd + 1] - begin) * K;
+    if ((int)(blockIdx.x >> 3) * (kThreads / 64) >= units) return;   // whole workgroup, before the barrier
+    const FastCtx f = fast_prologue<LAYOUT>(a, lds);
+    const int lane = threadIdx.x & 63, k = lane / R, rho = lane % R;
+    const int px = ((rho >> 2) % (SW / 2)) * 2 + (rho & 1), py = ((rho >> 2) / (SW / 2)) * 2 + ((rho >> 1) & 1);
+    unsigned long long steps = 0;
+    for (int u = w; w < m.nwx && u < units; u += m.nwx) {
+        const unsigned t = tiles[begin + u / K];
+        const int s = u % K;
+        const int x = (int)(t & 0xffffu) * 8 + (s % NSX) * SW + px, orow = (int)(t >> 16) * 8 + (s / NSX) * SH + py;
+        steps += march_pixel_split<LAYOUT, EARLY, ZO, K>(a, f, x, orow, k, rho);
+    }
+    if (a.step_counter) add_steps(a, steps);
+}
+
+template <int L, int K>
+void launch_regions_split(const MarchArgs& a, bool early, const Schedule& sc, dim3 grid, size_t lds, hipStream_t s)
+{
+    const dim3 block(kThreads);
+    if (early && a.zero_offsets)
+        hipLaunchKernelGGL((march_regions_split<L, true, true, K>), grid, block, lds, s, a, sc.tiles, sc.map);
+    else if (early)
+        hipLaunchKernelGGL((march_regions_split<L, true, false, K>), grid, block, lds, s, a, sc.tiles, sc.map);
+    else if (a.zero_offsets)
+        hipLaunchKernelGGL((march_regions_split<L, false, true, K>), grid, block, lds, s, a, sc.tiles, sc.map);
+    else
+        hipLaunchKernelGGL((march_regions_split<L, false, false, K>), grid, block, lds, s, a, sc.tiles, sc.map);
+}
+
 // XCD-row schedule: one 8x8 tile per wave, 4 horizontally adjacent tiles per
 // workgroup.  8-px tile rows are dealt to XCDs round-robin: XCD x walks rows
 // x, x+8, ... (blockIdx % 8, speed-only).  Rows interleave, so the balance
@@ -961,6 +1065,15 @@ hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStre
         else
             hipLaunchKernelGGL((march_rings<L, W, false, false>), grid, block, lds, s, a, cx, cy, nw, npos);
         return hipGetLastError();
+    }
+    if constexpr (L == LAYOUT_BRICK4 || L == LAYOUT_CORNER8) {
+        if (sc.kind == SCHED_REGIONS && sc.split > 1) {
+            const dim3 grid((unsigned)(8 * ((sc.map.nwx + 3) / 4)));
+            if (sc.split == 2) launch_regions_split<L, 2>(a, early, sc, grid, lds, s);
+            else if (sc.split == 4) launch_regions_split<L, 4>(a, early, sc, grid, lds, s);
+            else launch_regions_split<L, 8>(a, early, sc, grid, lds, s);
+            return hipGetLastError();
+        }
     }
     if (sc.kind == SCHED_REGIONS) {
         const dim3 grid((unsigned)(8 * ((sc.map.nwx + 3) / 4)));
