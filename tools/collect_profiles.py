@@ -1,0 +1,43 @@
+"""Copy a tools/round_profiles.sh run from gpurun_out/ into profiles/ (tracked):
+the bench line of each config -> profiles/r01_bench_<config>.json and the
+rocprofv3 --kernel-trace --stats summary of the same bench command ->
+profiles/r01_<config>_kernel_stats.csv, plus a check that the stats' mean
+march-kernel duration agrees with the bench's HIP-event mean.
+
+    python tools/collect_profiles.py [round-tag r01] [configs...]
+"""
+import csv
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+    configs = sys.argv[2:] or ["grid512", "grid128", "grid4k", "cloud", "cloud_shadow"]
+    out = os.path.join(ROOT, "profiles")
+    for c in configs:
+        log = os.path.join(ROOT, "gpurun_out", f"bench_{c}.log")
+        line = [ln for ln in open(log).read().splitlines() if ln.startswith("{")][-1]
+        bench = json.loads(line)
+        with open(os.path.join(out, f"{tag}_bench_{c}.json"), "w") as f:
+            f.write(line + "\n")
+        stats = os.path.join(ROOT, "gpurun_out", f"prof_{c}", "run_kernel_stats.csv")
+        if not os.path.exists(stats):   # rocprofv3 nests its output under host/pid dirs
+            for dp, _, fs in os.walk(os.path.join(ROOT, "gpurun_out", f"prof_{c}")):
+                for fn in fs:
+                    if fn.endswith("kernel_stats.csv"):
+                        stats = os.path.join(dp, fn)
+        shutil.copy(stats, os.path.join(out, f"{tag}_{c}_kernel_stats.csv"))
+        march = [r for r in csv.DictReader(open(stats)) if "march" in r["Name"]]
+        top = max(march, key=lambda r: float(r["TotalDurationNs"]))
+        print(f"{c:13s} bench {bench['value']:>14,.1f} {bench['unit']}  kernel(events) {bench['kernel_ms_mean']:.4f} ms  "
+              f"rocprof {top['Name'][:60]} avg {float(top['AverageNs']) / 1e6:.4f} ms x{top['Calls']}  "
+              f"roofline {bench['roofline']['frac']}")
+
+
+if __name__ == "__main__":
+    main()
