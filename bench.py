@@ -194,8 +194,22 @@ def main() -> int:
     # launch durations the roofline uses.  Two event records per frame cost a
     # few microseconds of queue time between frames (and, at N > 1, host time)
     ev_every = 4
+    pipe = None
     if native:
-        pipe = vrdist.RcclBandPipeline(r, W, H, fmt, band_rows=16, world=world, rank=rank)
+        try:
+            pipe = vrdist.RcclBandPipeline(r, W, H, fmt, band_rows=16, world=world, rank=rank)
+        except vr.VRError as e:   # every rank learns it below; then the Python path runs
+            print(f"rank {rank}: native frame loop unavailable ({e}); falling back to BandSharder over gloo",
+                  file=sys.stderr, flush=True)
+        ok = torch.tensor([1 if pipe is not None else 0], dtype=torch.int64)
+        if world > 1:
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok.item()) == 0:
+            if pipe is not None:
+                pipe.close()
+                pipe = None
+            native = False
+    if native:
         pipe.run_frames(args.warmup)
         torch.cuda.synchronize()
         if world > 1:

@@ -200,17 +200,26 @@ class RcclBandPipeline:
         self.width, self.height, self.fmt = width, height, fmt
         self.world, self.rank = world, rank
         uid = (ctypes.c_uint8 * _lib.SHARD_ID_BYTES)()
+        err = None
         if loopback:
             assert rank == 0
             uid = None
         elif rank == 0:
-            _lib.shard_call("vr_shard_unique_id", uid)
+            try:
+                _lib.shard_call("vr_shard_unique_id", uid)
+            except _lib.VRError as e:   # still broadcast, so no rank waits forever
+                err = e
         if world > 1 and not loopback:
             backend = dist.get_backend(group)
-            t = torch.tensor(bytearray(uid), dtype=torch.uint8,
+            t = torch.tensor([0 if err else 1] + list(bytearray(uid)), dtype=torch.uint8,
                              device="cuda" if backend == "nccl" else "cpu")
             dist.broadcast(t, src=0, group=group)
-            ctypes.memmove(uid, bytes(t.cpu().tolist()), _lib.SHARD_ID_BYTES)
+            got = t.cpu().tolist()
+            if not got[0]:
+                raise err or _lib.VRError(2, "vr_shard_unique_id", "failed on rank 0")
+            ctypes.memmove(uid, bytes(got[1:]), _lib.SHARD_ID_BYTES)
+        elif err:
+            raise err
         h = ctypes.c_void_p()
         _lib.shard_call("vr_shard_create", renderer._ctx, uid, world, rank, width, height, fmt, band_rows,
                         ctypes.byref(h))
