@@ -209,7 +209,10 @@ const char* vr_kernel_variant(void* ctx);
  * 1 = planar only, 2 = 4^3 apron bricks in 128-B lines ("brick5"),
  * 3 = 7^3 apron bricks of 512 B ("brick8"), 4 = 15^3 apron bricks of 4 KiB
  * ("brick16"), 5 = 8-corner footprint words ("corner8"), 6 = 3^3 apron
- * bricks of 64 B ("brick4").  Layouts 2-6 are
+ * bricks of 64 B ("brick4"), 7 = 4x16x2-texel bricks of 128 B whose
+ * rows run z-fastest, one 16-B load per tap ("zpair"), 8 = 4x4x8-texel
+ * bricks of 128 B ("brick448"), 9 = 4x8x8-texel bricks of 256 B
+ * ("brick488").  Layouts 2-9 are
  * used only where clamp-to-edge equals mirrored repeat.  Otherwise the
  * planar, mirrored-repeat kernel runs.  Rebuilds the layout (synchronous). */
 vr_status vr_set_layout_preference(void* ctx, int pref);
@@ -232,7 +235,7 @@ vr_status vr_set_layout_preference(void* ctx, int pref);
  *   "tiles_per_wave"  1-64, strided, ring and region schedules; 0 = auto,
  *                     the default: 2 for rings and regions, 1 for strided.
  *   "wedges"          1-64, regions schedule: wedges per XCD (default 2).
- *   "split"           regions schedule, brick4/corner8 layouts: lanes per ray
+ *   "split"           regions schedule, brick4/448/488/zpair/corner8: lanes per ray
  *                     (1, 2, 4, 8; each lane marches every K-th step and the
  *                     terms are summed in step order, bit-exact); 0 = auto,
  *                     the default: 2 or 4 when the target has too few rays

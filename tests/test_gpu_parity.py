@@ -101,7 +101,8 @@ def test_media_scroll_mirrored_repeat(r, oracle, vol128):
 
 
 @pytest.mark.parametrize("layout,name", [(1, "planar"), (2, "brick5"), (3, "brick8"), (4, "brick16"), (5, "corner8"),
-                                         (6, "brick4")])
+                                         (6, "brick4"), (7, "zpair"), (8, "brick448"),
+                                         (9, "brick488")])
 def test_every_layout_bitexact(r, oracle, vol128, layout, name):
     osd, gsd = vr.reference_shader_data(16 / 9, 20.0, -35.0)
     r.set_volume(vol128)
@@ -611,7 +612,7 @@ def test_regions_lists_across_streams(r, oracle, vol128):
         r.set_option("schedule", -1)
 
 
-@pytest.mark.parametrize("layout", [6, 5])
+@pytest.mark.parametrize("layout", [6, 7, 8, 9, 5])
 @pytest.mark.parametrize("split", [2, 4, 8])
 def test_split_rays_bitexact(r, oracle, vol128, layout, split):
     """Step-split rays (K lanes per ray, terms summed in step order): exact

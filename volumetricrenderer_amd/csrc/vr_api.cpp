@@ -261,6 +261,9 @@ const char* variant_name(const Plan& p)
         {"grid_brick16_clamp", "grid_brick16_clamp_early"},
         {"grid_corner8_clamp", "grid_corner8_clamp_early"},
         {"grid_brick4_clamp", "grid_brick4_clamp_early"},
+        {"grid_zpair_clamp", "grid_zpair_clamp_early"},
+        {"grid_brick448_clamp", "grid_brick448_clamp_early"},
+        {"grid_brick488_clamp", "grid_brick488_clamp_early"},
     };
     if (p.layout == LAYOUT_PLANAR && p.wrap == WRAP_MIRROR)
         return p.early ? "grid_planar_mirror_early" : "grid_planar_mirror";
@@ -977,7 +980,8 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
         sc.map = rb.map;
         // step-split rays: K lanes per ray when the frame
         // share is too small to fill the GPU with one-lane-per-ray waves
-        if (pl.layout == LAYOUT_BRICK4 || pl.layout == LAYOUT_CORNER8) {
+        if (pl.layout == LAYOUT_BRICK4 || pl.layout == LAYOUT_ZPAIR || pl.layout == LAYOUT_BRICK448 ||
+            pl.layout == LAYOUT_BRICK488 || pl.layout == LAYOUT_CORNER8) {
             int K = c->split;
             if (K == 0) {
                 K = 1;

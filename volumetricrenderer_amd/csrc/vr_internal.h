@@ -31,15 +31,25 @@ enum Layout : int {
                           // position bricks of 512 B (8x bytes); 1 load per tap
     LAYOUT_BRICK4 = 6,    // B=3: 3^3 texels + apron = 4^3 = 64 B (2.37x bytes);
                           // a z-slice of a footprint is one dword-aligned 8-B load
+    LAYOUT_ZPAIR = 7,     // 4x16x2 texels = 128 B (3x15x1 positions, 2.93x bytes),
+                          // 4-byte rows ordered z-fastest: rows (y,z) (y,z+1)
+                          // (y+1,z) (y+1,z+1) are 16 contiguous bytes, so a whole
+                          // footprint is one dword-aligned 16-B load
+    LAYOUT_BRICK448 = 8,  // 4x4x8 texels = 128 B (3x3x7 positions, 2.03x bytes);
+                          // BRICK4's in-brick order, so the same two 8-B loads
+    LAYOUT_BRICK488 = 9,  // 4x8x8 texels = 256 B (3x7x7 positions, 1.74x bytes);
+                          // slices 32 B apart
 };
-constexpr int kNumLayouts = 7;
+constexpr int kNumLayouts = 10;
 
 enum Wrap : int { WRAP_CLAMP = 0, WRAP_MIRROR = 1 };
 
 // Geometry of a fast layout for one channel (host and device).
 struct LayoutGeom {
-    int B;          // useful positions per brick edge
+    int B;          // useful positions per brick edge (cubic layouts)
     int R;          // stored edge of an apron brick, R = B + 1
+    int Ba[3];      // useful positions per brick along x, y, z
+    int Rn[3];      // stored texels per brick along x, y, z (in-brick order x fastest)
     unsigned brick; // bytes per brick
     int nbx, nby, nbz;
 };
@@ -48,6 +58,10 @@ __host__ __device__ inline LayoutGeom layout_geom(int layout, int nx, int ny, in
     LayoutGeom g{};
     if (layout == LAYOUT_CORNER8) {
         g.B = 4; g.R = 4; g.brick = 512;
+    } else if (layout == LAYOUT_ZPAIR) {
+        g.B = 3; g.R = 4; g.brick = 128;
+    } else if (layout == LAYOUT_BRICK448 || layout == LAYOUT_BRICK488) {
+        g.B = 3; g.R = 4; g.brick = layout == LAYOUT_BRICK448 ? 128u : 256u;
     } else {
         g.B = layout == LAYOUT_BRICK4 ? 3 : layout == LAYOUT_BRICK5 ? 4 : layout == LAYOUT_BRICK8 ? 7 : 15;
         g.R = g.B + 1;
@@ -55,20 +69,26 @@ __host__ __device__ inline LayoutGeom layout_geom(int layout, int nx, int ny, in
         // whole 128-B lines; BRICK4's 64-B bricks pair up in one line
         g.brick = layout == LAYOUT_BRICK4 ? 64u : (r3 + 127u) & ~127u;
     }
+    g.Ba[0] = g.Ba[1] = g.Ba[2] = g.B;
+    g.Rn[0] = g.Rn[1] = g.Rn[2] = g.R;
+    if (layout == LAYOUT_ZPAIR) { g.Ba[1] = 15; g.Ba[2] = 1; }
+    if (layout == LAYOUT_BRICK448) { g.Ba[2] = 7; g.Rn[2] = 8; }
+    if (layout == LAYOUT_BRICK488) { g.Ba[1] = g.Ba[2] = 7; g.Rn[1] = g.Rn[2] = 8; }
     // padded base positions a in [0, N] -> bricks a / B in [0, N / B]
-    g.nbx = nx / g.B + 1;
-    g.nby = ny / g.B + 1;
-    g.nbz = nz / g.B + 1;
+    g.nbx = nx / g.Ba[0] + 1;
+    g.nby = ny / g.Ba[1] + 1;
+    g.nbz = nz / g.Ba[2] + 1;
     return g;
 }
 // byte offset of padded position a along axis 0/1/2 inside one channel plane
 __host__ __device__ inline unsigned axis_offset(const LayoutGeom& g, int layout, int axis, int a)
 {
-    const unsigned q = (unsigned)(a / g.B), r = (unsigned)(a % g.B);
+    const unsigned q = (unsigned)(a / g.Ba[axis]), r = (unsigned)(a % g.Ba[axis]);
     const unsigned stride = axis == 0 ? g.brick : axis == 1 ? g.brick * (unsigned)g.nbx
                                                             : g.brick * (unsigned)g.nbx * (unsigned)g.nby;
     if (layout == LAYOUT_CORNER8) return q * stride + (r << (3 + 2 * axis));   // 8 B per position
-    return q * stride + r * (axis == 0 ? 1u : axis == 1 ? (unsigned)g.R : (unsigned)(g.R * g.R));
+    if (layout == LAYOUT_ZPAIR) return q * stride + (axis == 0 ? r : axis == 1 ? 8u * r : 0u);
+    return q * stride + r * (axis == 0 ? 1u : axis == 1 ? (unsigned)g.Rn[0] : (unsigned)(g.Rn[0] * g.Rn[1]));
 }
 
 // Procedural medium parameters (vr_procedural; BASELINE configs 2/3).

@@ -88,6 +88,9 @@ hipError_t launch_march(const MarchArgs& a, int layout, int wrap, bool early, co
     if (a.width <= 0 || a.out_rows <= 0) return hipSuccess;
     switch (layout) {
     case LAYOUT_BRICK4: return launch_lw<LAYOUT_BRICK4, WRAP_CLAMP>(a, early, sc, s);
+    case LAYOUT_BRICK448: return launch_lw<LAYOUT_BRICK448, WRAP_CLAMP>(a, early, sc, s);
+    case LAYOUT_BRICK488: return launch_lw<LAYOUT_BRICK488, WRAP_CLAMP>(a, early, sc, s);
+    case LAYOUT_ZPAIR: return launch_lw<LAYOUT_ZPAIR, WRAP_CLAMP>(a, early, sc, s);
     case LAYOUT_BRICK5: return launch_lw<LAYOUT_BRICK5, WRAP_CLAMP>(a, early, sc, s);
     case LAYOUT_BRICK8: return launch_lw<LAYOUT_BRICK8, WRAP_CLAMP>(a, early, sc, s);
     case LAYOUT_BRICK16: return launch_lw<LAYOUT_BRICK16, WRAP_CLAMP>(a, early, sc, s);

@@ -69,16 +69,24 @@ __global__ __launch_bounds__(kBlock) void k_build_layout(const uint8_t* __restri
             for (int k = 0; k < 8; ++k)
                 q |= (unsigned long long)src.at(a + (k & 1), b + ((k >> 1) & 1), c + (k >> 2)) << (8 * k);
             reinterpret_cast<unsigned long long*>(dst)[e] = q;
+        } else if constexpr (LAYOUT == LAYOUT_ZPAIR) {
+            // byte = x + 4 * (z + 2 * y): 4-byte rows, z fastest
+            const long long brick = e >> 7;
+            const int byte = (int)(e & 127);
+            const int bx = (int)(brick % g.nbx);
+            const long long t = brick / g.nbx;
+            const int by = (int)(t % g.nby), bz = (int)(t / g.nby);
+            dst[e] = src.at(3 * bx + (byte & 3), 15 * by + (byte >> 3), bz + ((byte >> 2) & 1));
         } else {
             const long long brick = e / g.brick;
             const int byte = (int)(e - brick * g.brick);
             unsigned int v = 0;
-            if (byte < g.R * g.R * g.R) {
-                const int u = byte % g.R, vv = (byte / g.R) % g.R, w = byte / (g.R * g.R);
+            if (byte < g.Rn[0] * g.Rn[1] * g.Rn[2]) {
+                const int u = byte % g.Rn[0], vv = (byte / g.Rn[0]) % g.Rn[1], w = byte / (g.Rn[0] * g.Rn[1]);
                 const int bx = (int)(brick % g.nbx);
                 const long long t = brick / g.nbx;
                 const int by = (int)(t % g.nby), bz = (int)(t / g.nby);
-                v = src.at(g.B * bx + u, g.B * by + vv, g.B * bz + w);
+                v = src.at(g.Ba[0] * bx + u, g.Ba[1] * by + vv, g.Ba[2] * bz + w);
             }
             dst[e] = (uint8_t)v;
         }
@@ -243,6 +251,9 @@ hipError_t launch_build_layout(int layout, const uint8_t* d_planar, int nx, int 
     case LAYOUT_BRICK5: hipLaunchKernelGGL(k_build_layout<LAYOUT_BRICK5>, gr, b, 0, s, d_planar, nx, ny, nz, g, elems, pb, d_out); break;
     case LAYOUT_BRICK8: hipLaunchKernelGGL(k_build_layout<LAYOUT_BRICK8>, gr, b, 0, s, d_planar, nx, ny, nz, g, elems, pb, d_out); break;
     case LAYOUT_BRICK16: hipLaunchKernelGGL(k_build_layout<LAYOUT_BRICK16>, gr, b, 0, s, d_planar, nx, ny, nz, g, elems, pb, d_out); break;
+    case LAYOUT_BRICK448: hipLaunchKernelGGL(k_build_layout<LAYOUT_BRICK448>, gr, b, 0, s, d_planar, nx, ny, nz, g, elems, pb, d_out); break;
+    case LAYOUT_BRICK488: hipLaunchKernelGGL(k_build_layout<LAYOUT_BRICK488>, gr, b, 0, s, d_planar, nx, ny, nz, g, elems, pb, d_out); break;
+    case LAYOUT_ZPAIR: hipLaunchKernelGGL(k_build_layout<LAYOUT_ZPAIR>, gr, b, 0, s, d_planar, nx, ny, nz, g, elems, pb, d_out); break;
     case LAYOUT_CORNER8: hipLaunchKernelGGL(k_build_layout<LAYOUT_CORNER8>, gr, b, 0, s, d_planar, nx, ny, nz, g, elems, pb, d_out); break;
     default: return hipErrorInvalidValue;
     }
