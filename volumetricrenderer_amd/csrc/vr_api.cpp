@@ -110,14 +110,14 @@ struct Ctx {
 
 // Auto layout (measured): CORNER8 does one load per tap but
 // stores 8 bytes per texel.  It wins while the volume fits the 256 MiB
-// Infinity Cache.  Past that it is HBM-bound, and BRICK4 (2.37x bytes, two
-// dword-aligned 8-byte loads per tap, each footprint inside one 64-B brick)
-// wins with the pipelined march: 1-6 % ahead of BRICK5 (2.0x bytes, two
-// 12-byte loads) at 200^3-512^3 although it fetches 16 % more.
+// Infinity Cache.  Past that it is HBM-bound, and BRICK488 (1.74x bytes, 3x7x7
+// positions per 4x8x8 brick, BRICK4's two dword-aligned 8-byte loads per tap)
+// wins with the pipelined march: 9-10 % ahead of BRICK4 (2.37x bytes) at
+// 384^3-512^3, level at 200^3, and 0.7 GiB smaller at 512^3.
 constexpr size_t kCorner8MaxBytes = 160ull << 20;
 int auto_layout(int nx, int ny, int nz)
 {
-    return 4 * layout_plane_bytes(LAYOUT_CORNER8, nx, ny, nz) <= kCorner8MaxBytes ? LAYOUT_CORNER8 : LAYOUT_BRICK4;
+    return 4 * layout_plane_bytes(LAYOUT_CORNER8, nx, ny, nz) <= kCorner8MaxBytes ? LAYOUT_CORNER8 : LAYOUT_BRICK488;
 }
 
 Ctx* as_ctx(void* p) { return static_cast<Ctx*>(p); }
