@@ -212,7 +212,9 @@ const char* vr_kernel_variant(void* ctx);
  * bricks of 64 B ("brick4"), 7 = 4x16x2-texel bricks of 128 B whose
  * rows run z-fastest, one 16-B load per tap ("zpair"), 8 = 4x4x8-texel
  * bricks of 128 B ("brick448"), 9 = 4x8x8-texel bricks of 256 B
- * ("brick488").  Layouts 2-9 are
+ * ("brick488"), 10 = 4x8x16-texel bricks of 512 B ("brick4816"),
+ * 11 = 4x16x16-texel bricks of 1 KiB ("brick41616"), 12 = 4x8x32-texel
+ * bricks of 1 KiB ("brick4832").  Layouts 2-12 are
  * used only where clamp-to-edge equals mirrored repeat.  Otherwise the
  * planar, mirrored-repeat kernel runs.  Rebuilds the layout (synchronous). */
 vr_status vr_set_layout_preference(void* ctx, int pref);

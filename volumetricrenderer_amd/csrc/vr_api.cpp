@@ -110,14 +110,15 @@ struct Ctx {
 
 // Auto layout (measured): CORNER8 does one load per tap but
 // stores 8 bytes per texel.  It wins while the volume fits the 256 MiB
-// Infinity Cache.  Past that it is HBM-bound, and BRICK488 (1.74x bytes, 3x7x7
-// positions per 4x8x8 brick, BRICK4's two dword-aligned 8-byte loads per tap)
-// wins with the pipelined march: 9-10 % ahead of BRICK4 (2.37x bytes) at
-// 384^3-512^3, level at 200^3, and 0.7 GiB smaller at 512^3.
+// Infinity Cache.  Past that it is HBM-bound, and BRICK4832 (1.53x bytes, 3x7x31
+// positions per 4x8x32 brick, BRICK4's two dword-aligned 8-byte loads per tap)
+// wins with the pipelined march: 2-5 % ahead of BRICK488 (1.74x) and 12-20 %
+// ahead of BRICK4 (2.37x) at 384^3-512^3, level at 200^3-256^3.  Taller bricks
+// in y (BRICK41616, slices 64 B apart) lose: a tap's z+1 slice leaves the line.
 constexpr size_t kCorner8MaxBytes = 160ull << 20;
 int auto_layout(int nx, int ny, int nz)
 {
-    return 4 * layout_plane_bytes(LAYOUT_CORNER8, nx, ny, nz) <= kCorner8MaxBytes ? LAYOUT_CORNER8 : LAYOUT_BRICK488;
+    return 4 * layout_plane_bytes(LAYOUT_CORNER8, nx, ny, nz) <= kCorner8MaxBytes ? LAYOUT_CORNER8 : LAYOUT_BRICK4832;
 }
 
 Ctx* as_ctx(void* p) { return static_cast<Ctx*>(p); }
@@ -264,6 +265,9 @@ const char* variant_name(const Plan& p)
         {"grid_zpair_clamp", "grid_zpair_clamp_early"},
         {"grid_brick448_clamp", "grid_brick448_clamp_early"},
         {"grid_brick488_clamp", "grid_brick488_clamp_early"},
+        {"grid_brick4816_clamp", "grid_brick4816_clamp_early"},
+        {"grid_brick41616_clamp", "grid_brick41616_clamp_early"},
+        {"grid_brick4832_clamp", "grid_brick4832_clamp_early"},
     };
     if (p.layout == LAYOUT_PLANAR && p.wrap == WRAP_MIRROR)
         return p.early ? "grid_planar_mirror_early" : "grid_planar_mirror";
@@ -980,8 +984,7 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
         sc.map = rb.map;
         // step-split rays: K lanes per ray when the frame
         // share is too small to fill the GPU with one-lane-per-ray waves
-        if (pl.layout == LAYOUT_BRICK4 || pl.layout == LAYOUT_ZPAIR || pl.layout == LAYOUT_BRICK448 ||
-            pl.layout == LAYOUT_BRICK488 || pl.layout == LAYOUT_CORNER8) {
+        if (is_b4_family(pl.layout) || pl.layout == LAYOUT_ZPAIR || pl.layout == LAYOUT_CORNER8) {
             int K = c->split;
             if (K == 0) {
                 K = 1;

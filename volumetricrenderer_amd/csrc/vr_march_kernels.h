@@ -126,13 +126,14 @@ __device__ __forceinline__ TapRaw tap_fetch(const FastCtx& f, int ch, float gx, 
         r.q1 = __builtin_amdgcn_alignbyte(s0[2], s0[1], off);
         r.q2 = __builtin_amdgcn_alignbyte(s1[1], s1[0], o1);
         r.q3 = __builtin_amdgcn_alignbyte(s1[2], s1[1], o1);
-    } else if constexpr (LAYOUT == LAYOUT_BRICK4 || LAYOUT == LAYOUT_BRICK448 || LAYOUT == LAYOUT_BRICK488) {
+    } else if constexpr (is_b4_family(LAYOUT)) {
         // R = 4: a slice's rows y and y+1 are the two dwords at off & ~3
         // (x = off & 3 <= 2), so one dword-aligned 8-byte load per z-slice,
         // the z+1 slice 16 bytes on (32 for BRICK488's 8-row slices): 2
         // dwords per lane and slice where BRICK5 needs 3.  q0/q2 = bytes x,
         // x+1 of row y, q1/q3 of row y+1.
-        constexpr unsigned kZ = LAYOUT == LAYOUT_BRICK488 ? 32u : 16u;
+        constexpr unsigned kZ = LAYOUT == LAYOUT_BRICK41616 ? 64u
+                             : LAYOUT == LAYOUT_BRICK488 || LAYOUT == LAYOUT_BRICK4816 || LAYOUT == LAYOUT_BRICK4832 ? 32u : 16u;
         const unsigned a0 = off & ~3u;
         const auto s0 = __builtin_amdgcn_raw_buffer_load_b64(f.rsrc[ch], a0, 0, 0);
         const auto s1 = __builtin_amdgcn_raw_buffer_load_b64(f.rsrc[ch], a0 + kZ, 0, 0);
@@ -575,13 +576,13 @@ __device__ __forceinline__ unsigned march_pixel_proc_compact(const MarchArgs& a,
 template <int LAYOUT = 0>
 __device__ __forceinline__ int lane_x(int lane)
 {
-    if constexpr (LAYOUT == LAYOUT_BRICK5 || LAYOUT == LAYOUT_BRICK4 || LAYOUT == LAYOUT_ZPAIR || LAYOUT == LAYOUT_BRICK448 || LAYOUT == LAYOUT_BRICK488) return ((lane >> 2) & 3) * 2 + (lane & 1);
+    if constexpr (LAYOUT == LAYOUT_BRICK5 || LAYOUT == LAYOUT_ZPAIR || is_b4_family(LAYOUT)) return ((lane >> 2) & 3) * 2 + (lane & 1);
     else return lane & 7;
 }
 template <int LAYOUT = 0>
 __device__ __forceinline__ int lane_y(int lane)
 {
-    if constexpr (LAYOUT == LAYOUT_BRICK5 || LAYOUT == LAYOUT_BRICK4 || LAYOUT == LAYOUT_ZPAIR || LAYOUT == LAYOUT_BRICK448 || LAYOUT == LAYOUT_BRICK488) return (lane >> 4) * 2 + ((lane >> 1) & 1);
+    if constexpr (LAYOUT == LAYOUT_BRICK5 || LAYOUT == LAYOUT_ZPAIR || is_b4_family(LAYOUT)) return (lane >> 4) * 2 + ((lane >> 1) & 1);
     else return lane >> 3;
 }
 
@@ -1076,7 +1077,7 @@ hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStre
             hipLaunchKernelGGL((march_rings<L, W, false, false>), grid, block, lds, s, a, cx, cy, nw, npos);
         return hipGetLastError();
     }
-    if constexpr (L == LAYOUT_BRICK4 || L == LAYOUT_ZPAIR || L == LAYOUT_BRICK448 || L == LAYOUT_BRICK488 || L == LAYOUT_CORNER8) {
+    if constexpr (is_b4_family(L) || L == LAYOUT_ZPAIR || L == LAYOUT_CORNER8) {
         if (sc.kind == SCHED_REGIONS && sc.split > 1) {
             const dim3 grid((unsigned)(8 * ((sc.map.nwx + 3) / 4)));
             if (sc.split == 2) launch_regions_split<L, 2>(a, early, sc, grid, lds, s);
