@@ -214,7 +214,8 @@ const char* vr_kernel_variant(void* ctx);
  * bricks of 128 B ("brick448"), 9 = 4x8x8-texel bricks of 256 B
  * ("brick488"), 10 = 4x8x16-texel bricks of 512 B ("brick4816"),
  * 11 = 4x16x16-texel bricks of 1 KiB ("brick41616"), 12 = 4x8x32-texel
- * bricks of 1 KiB ("brick4832").  Layouts 2-12 are
+ * bricks of 1 KiB ("brick4832"), 13 = 4x8x64-texel bricks of 2 KiB
+ * ("brick4864").  Layouts 2-13 are
  * used only where clamp-to-edge equals mirrored repeat.  Otherwise the
  * planar, mirrored-repeat kernel runs.  Rebuilds the layout (synchronous). */
 vr_status vr_set_layout_preference(void* ctx, int pref);

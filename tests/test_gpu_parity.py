@@ -103,7 +103,7 @@ def test_media_scroll_mirrored_repeat(r, oracle, vol128):
 @pytest.mark.parametrize("layout,name", [(1, "planar"), (2, "brick5"), (3, "brick8"), (4, "brick16"), (5, "corner8"),
                                          (6, "brick4"), (7, "zpair"), (8, "brick448"),
                                          (9, "brick488"), (10, "brick4816"), (11, "brick41616"),
-                                         (12, "brick4832")])
+                                         (12, "brick4832"), (13, "brick4864")])
 def test_every_layout_bitexact(r, oracle, vol128, layout, name):
     osd, gsd = vr.reference_shader_data(16 / 9, 20.0, -35.0)
     r.set_volume(vol128)

@@ -16,7 +16,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import volumetricrenderer_amd as vr  # noqa: E402
 
-NAMES = {1: "planar", 2: "brick5", 3: "brick8", 4: "brick16", 5: "corner8", 6: "brick4", 7: "zpair", 8: "brick448", 9: "brick488", 10: "brick4816", 11: "brick41616", 12: "brick4832"}
+NAMES = {1: "planar", 2: "brick5", 3: "brick8", 4: "brick16", 5: "corner8", 6: "brick4", 7: "zpair", 8: "brick448", 9: "brick488", 10: "brick4816", 11: "brick41616", 12: "brick4832", 13: "brick4864"}
 
 
 def main():
@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--steps", type=int, default=128)
+    ap.add_argument("--phi", type=float, default=0.0, help="camera orbit angles (deg), to check view dependence")
+    ap.add_argument("--theta", type=float, default=0.0)
     ap.add_argument("--no-check", action="store_true", help="skip the cross-layout image check (timing builds)")
     args = ap.parse_args()
     W, H, S = args.width, args.height, args.steps
@@ -51,7 +53,7 @@ def main():
         return f"{NAMES[lay[0]]}/{['static', 'queue', 'strided', 'xcdrows', 'rings', 'regions'][lay[1]]}{lay[2] if lay[1] else ''}{'w%d' % lay[3] if len(lay) > 3 else ''}"
     res = {}
     with vr.Renderer(0) as r:
-        osd, gsd = vr.reference_shader_data(W / H)
+        osd, gsd = vr.reference_shader_data(W / H, args.phi, args.theta)
         r.set_shader_data(osd, gsd)
         r.set_march(vr.march_defaults(max_steps=S))
         for n in [int(x) for x in args.sizes.split(",")]:

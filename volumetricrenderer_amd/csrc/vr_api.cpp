@@ -268,6 +268,7 @@ const char* variant_name(const Plan& p)
         {"grid_brick4816_clamp", "grid_brick4816_clamp_early"},
         {"grid_brick41616_clamp", "grid_brick41616_clamp_early"},
         {"grid_brick4832_clamp", "grid_brick4832_clamp_early"},
+        {"grid_brick4864_clamp", "grid_brick4864_clamp_early"},
     };
     if (p.layout == LAYOUT_PLANAR && p.wrap == WRAP_MIRROR)
         return p.early ? "grid_planar_mirror_early" : "grid_planar_mirror";

@@ -43,13 +43,15 @@ enum Layout : int {
     LAYOUT_BRICK41616 = 11,  // 4x16x16 texels = 1 KiB (3x15x15 positions, 1.52x
                              // bytes); slices 64 B apart
     LAYOUT_BRICK4832 = 12,   // 4x8x32 texels = 1 KiB (3x7x31 positions, 1.53x bytes)
+    LAYOUT_BRICK4864 = 13,   // 4x8x64 texels = 2 KiB (3x7x63 positions, 1.51x bytes)
 };
-constexpr int kNumLayouts = 13;
+constexpr int kNumLayouts = 14;
 // the layouts whose taps are BRICK4's two dword-aligned 8-B loads
 __host__ __device__ constexpr bool is_b4_family(int l)
 {
     return l == LAYOUT_BRICK4 || l == LAYOUT_BRICK448 || l == LAYOUT_BRICK488 || l == LAYOUT_BRICK4816 ||
-           l == LAYOUT_BRICK41616 || l == LAYOUT_BRICK4832;
+           l == LAYOUT_BRICK41616 || l == LAYOUT_BRICK4832 ||
+           l == LAYOUT_BRICK4864;
 }
 
 enum Wrap : int { WRAP_CLAMP = 0, WRAP_MIRROR = 1 };
@@ -71,10 +73,10 @@ __host__ __device__ inline LayoutGeom layout_geom(int layout, int nx, int ny, in
     } else if (layout == LAYOUT_ZPAIR) {
         g.B = 3; g.R = 4; g.brick = 128;
     } else if (layout == LAYOUT_BRICK448 || layout == LAYOUT_BRICK488 || layout == LAYOUT_BRICK4816 ||
-               layout == LAYOUT_BRICK41616 || layout == LAYOUT_BRICK4832) {
+               layout == LAYOUT_BRICK41616 || layout == LAYOUT_BRICK4832 || layout == LAYOUT_BRICK4864) {
         g.B = 3; g.R = 4;
         g.brick = layout == LAYOUT_BRICK448 ? 128u : layout == LAYOUT_BRICK488 ? 256u
-                : layout == LAYOUT_BRICK4816 ? 512u : 1024u;
+                : layout == LAYOUT_BRICK4816 ? 512u : layout == LAYOUT_BRICK4864 ? 2048u : 1024u;
     } else {
         g.B = layout == LAYOUT_BRICK4 ? 3 : layout == LAYOUT_BRICK5 ? 4 : layout == LAYOUT_BRICK8 ? 7 : 15;
         g.R = g.B + 1;
@@ -88,6 +90,7 @@ __host__ __device__ inline LayoutGeom layout_geom(int layout, int nx, int ny, in
     if (layout == LAYOUT_BRICK448) { g.Ba[2] = 7; g.Rn[2] = 8; }
     if (layout == LAYOUT_BRICK488) { g.Ba[1] = g.Ba[2] = 7; g.Rn[1] = g.Rn[2] = 8; }
     if (layout == LAYOUT_BRICK4816) { g.Ba[1] = 7; g.Rn[1] = 8; g.Ba[2] = 15; g.Rn[2] = 16; }
+    if (layout == LAYOUT_BRICK4864) { g.Ba[1] = 7; g.Rn[1] = 8; g.Ba[2] = 63; g.Rn[2] = 64; }
     if (layout == LAYOUT_BRICK4832) { g.Ba[1] = 7; g.Rn[1] = 8; g.Ba[2] = 31; g.Rn[2] = 32; }
     if (layout == LAYOUT_BRICK41616) { g.Ba[1] = g.Ba[2] = 15; g.Rn[1] = g.Rn[2] = 16; }
     // padded base positions a in [0, N] -> bricks a / B in [0, N / B]

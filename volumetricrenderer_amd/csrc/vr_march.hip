@@ -91,6 +91,7 @@ hipError_t launch_march(const MarchArgs& a, int layout, int wrap, bool early, co
     case LAYOUT_BRICK448: return launch_lw<LAYOUT_BRICK448, WRAP_CLAMP>(a, early, sc, s);
     case LAYOUT_BRICK488: return launch_lw<LAYOUT_BRICK488, WRAP_CLAMP>(a, early, sc, s);
     case LAYOUT_BRICK4816: return launch_lw<LAYOUT_BRICK4816, WRAP_CLAMP>(a, early, sc, s);
+    case LAYOUT_BRICK4864: return launch_lw<LAYOUT_BRICK4864, WRAP_CLAMP>(a, early, sc, s);
     case LAYOUT_BRICK4832: return launch_lw<LAYOUT_BRICK4832, WRAP_CLAMP>(a, early, sc, s);
     case LAYOUT_BRICK41616: return launch_lw<LAYOUT_BRICK41616, WRAP_CLAMP>(a, early, sc, s);
     case LAYOUT_ZPAIR: return launch_lw<LAYOUT_ZPAIR, WRAP_CLAMP>(a, early, sc, s);

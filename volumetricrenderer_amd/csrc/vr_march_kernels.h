@@ -133,7 +133,8 @@ __device__ __forceinline__ TapRaw tap_fetch(const FastCtx& f, int ch, float gx, 
         // dwords per lane and slice where BRICK5 needs 3.  q0/q2 = bytes x,
         // x+1 of row y, q1/q3 of row y+1.
         constexpr unsigned kZ = LAYOUT == LAYOUT_BRICK41616 ? 64u
-                             : LAYOUT == LAYOUT_BRICK488 || LAYOUT == LAYOUT_BRICK4816 || LAYOUT == LAYOUT_BRICK4832 ? 32u : 16u;
+                             : LAYOUT == LAYOUT_BRICK488 || LAYOUT == LAYOUT_BRICK4816 || LAYOUT == LAYOUT_BRICK4832 ||
+                                      LAYOUT == LAYOUT_BRICK4864 ? 32u : 16u;
         const unsigned a0 = off & ~3u;
         const auto s0 = __builtin_amdgcn_raw_buffer_load_b64(f.rsrc[ch], a0, 0, 0);
         const auto s1 = __builtin_amdgcn_raw_buffer_load_b64(f.rsrc[ch], a0 + kZ, 0, 0);
