@@ -22,7 +22,7 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--steps", type=int, default=128)
     ap.add_argument("--frames", type=int, default=20)
-    ap.add_argument("--variants", default="-1:0:0", help="comma list of schedule:tiles_per_wave:split")
+    ap.add_argument("--variants", default="-1:0:0", help="comma list of schedule:tiles_per_wave:split[:wedges]")
     a = ap.parse_args()
     W, H = a.width, a.height
     with vr.Renderer(0) as r:
@@ -31,10 +31,14 @@ def main():
         r.set_shader_data(osd, gsd)
         r.set_march(vr.march_defaults(max_steps=a.steps))
         for var in a.variants.split(","):
-            sched, tpw, split = (int(v) for v in var.split(":"))
+            vals = [int(v) for v in var.split(":")]
+            sched, tpw, split = vals[:3]
+            wedges = vals[3] if len(vals) > 3 else 0
             r.set_option("schedule", sched)
             r.set_option("tiles_per_wave", tpw)
             r.set_option("split", split)
+            if wedges:
+                r.set_option("wedges", wedges)
             base = None
             for n in (1, 2, 4, 8):
                 band = dict(band_rows=16, band_stride=n, band_first=0)
@@ -48,7 +52,7 @@ def main():
                 torch.cuda.synchronize()
                 t = float(np.median([ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(a.frames)]))
                 base = base or t
-                print(f"schedule {sched} tpw {tpw} split {split} N={n}: rank-0 bands {t:.4f} ms, whole/N {base / n:.4f} ms, "
+                print(f"schedule {sched} tpw {tpw} split {split} wedges {wedges} N={n}: rank-0 bands {t:.4f} ms, whole/N {base / n:.4f} ms, "
                       f"efficiency {base / n / t:.2f}", flush=True)
 
 

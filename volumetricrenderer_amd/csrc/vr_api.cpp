@@ -47,7 +47,7 @@ vr_status fail(vr_status st, const char* fmt, ...)
 constexpr int kDefaultSchedule = -1;     // -1 auto, 0 static tiles, 1 persistent queue, 2 strided
 constexpr int kDefaultWavesPerSimd = 4;
 constexpr int kDefaultTilesPerWave = 0;   // 0 = auto: 2 for rings and regions, 1 for strided (measured)
-constexpr int kDefaultWedges = 2;         // regions schedule: wedges per XCD (measured)
+constexpr int kDefaultWedges = 4;         // regions schedule: wedges per XCD (measured)
 // a moving camera reuses the current (still complete, maybe less balanced)
 // region lists for this many renders before they are rebuilt
 constexpr int kRegionRebuildInterval = 32;
