@@ -196,19 +196,15 @@ def main() -> int:
     ev_every = 4
     pipe = None
     if native:
+        # No silent fallback: a multi-GPU number must come from the path its
+        # label names.  If the native RCCL frame loop cannot be made, every
+        # rank fails (RcclBandPipeline agrees on success before the collective
+        # communicator init) and the bench exits non-zero.
         try:
             pipe = vrdist.RcclBandPipeline(r, W, H, fmt, band_rows=16, world=world, rank=rank)
-        except vr.VRError as e:   # every rank learns it below; then the Python path runs
-            print(f"rank {rank}: native frame loop unavailable ({e}); falling back to BandSharder over gloo",
-                  file=sys.stderr, flush=True)
-        ok = torch.tensor([1 if pipe is not None else 0], dtype=torch.int64)
-        if world > 1:
-            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        if int(ok.item()) == 0:
-            if pipe is not None:
-                pipe.close()
-                pipe = None
-            native = False
+        except vr.VRError as e:
+            print(f"rank {rank}: native RCCL frame loop unavailable: {e}", file=sys.stderr, flush=True)
+            raise SystemExit(3)
     if native:
         pipe.run_frames(args.warmup)
         torch.cuda.synchronize()
@@ -239,6 +235,15 @@ def main() -> int:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     el, kern_ms_max = float(tt[0]), float(tt[1])
 
+    collective_label = None
+    if world > 1:
+        if native:
+            collective_label = "RCCL grouped send/recv to rank 0 over xGMI, native frame loop (libvr_shard)"
+        else:
+            backend = dist.get_backend()   # what the process group really is, not what was asked for
+            collective_label = (f"torch.distributed gather to rank 0 ({backend}"
+                                + (", host-staged: band sets copied through host memory)" if backend == "gloo"
+                                   else ", device buffers)"))
     if rank == 0:
         ms_per_step = el / args.steps * 1e3
         value = W * H * S * args.steps / el / 1e6
@@ -295,9 +300,7 @@ def main() -> int:
                        "baseline_config_index": cfg_idx, "width": W, "height": H, "max_steps": S,
                        "volume": f"{N}^3 RGBA8" if N else "procedural", "camera": "reference (TestMain.cpp:219-245)",
                        "kernel": r.kernel_variant, "parallelism": f"bands16x{world}",
-                       "collective": (("RCCL grouped send/recv to rank 0, native frame loop (libvr_shard)" if native
-                                       else f"torch.distributed gather to rank 0 ({args.backend})")
-                                      if world > 1 else None),
+                       "collective": collective_label,
                        "executed_steps_per_frame": frame_steps},
             "executed_steps_per_s": round(frame_steps * args.steps / el, 1),
             "kernel_ms_mean": round(kern_ms, 5),

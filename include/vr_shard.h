@@ -48,6 +48,19 @@ vr_status vr_shard_unique_id(uint8_t id[VR_SHARD_ID_BYTES]);
  * N-rank data layout and assembly on one GPU (tests, rehearsals). */
 vr_status vr_shard_create(void* ctx, const uint8_t id[VR_SHARD_ID_BYTES], int nranks, int rank,
                           int width, int height, int format, int band_rows, vr_shard** out);
+/* The two halves of vr_shard_create, so that ranks can agree that every
+ * allocation succeeded before any of them enters the collective
+ * ncclCommInitRank (a rank that failed to allocate would otherwise leave its
+ * peers blocked in the init):
+ *   vr_shard_alloc   -- streams, events and buffers only (local, never
+ *                       blocks); the result behaves as loopback on rank 0
+ *                       until it is connected;
+ *   vr_shard_connect -- collective: joins the communicator with `id`.
+ * The caller agrees on success between the two (e.g. an all-reduce over a
+ * torch.distributed group) and destroys the shard on every rank otherwise. */
+vr_status vr_shard_alloc(void* ctx, int nranks, int rank, int width, int height, int format, int band_rows,
+                         vr_shard** out);
+vr_status vr_shard_connect(vr_shard* sh, const uint8_t id[VR_SHARD_ID_BYTES]);
 vr_status vr_shard_destroy(vr_shard* sh);
 
 /* Render `frames` frames (collective: every rank, same count), 2 in flight.

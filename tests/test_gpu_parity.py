@@ -557,6 +557,7 @@ def test_regions_schedule_every_pixel_once(r, oracle, vol128, wedges):
     tile exactly once -- the output buffer is pre-filled with a sentinel --
     and they are rebuilt when the geometry changes (camera, size, bands)."""
     W, H = 328, 200
+    wedges0 = r.get_option("wedges")
     r.set_option("schedule", 5)
     r.set_option("wedges", wedges)
     try:
@@ -581,7 +582,7 @@ def test_regions_schedule_every_pixel_once(r, oracle, vol128, wedges):
             assert int(cnt.item()) == steps
     finally:
         r.set_option("schedule", -1)
-        r.set_option("wedges", 2)
+        r.set_option("wedges", wedges0)
 
 
 def test_regions_lists_across_streams(r, oracle, vol128):
@@ -613,7 +614,7 @@ def test_regions_lists_across_streams(r, oracle, vol128):
         r.set_option("schedule", -1)
 
 
-@pytest.mark.parametrize("layout", [6, 7, 8, 9, 5])
+@pytest.mark.parametrize("layout", [6, 7, 8, 9, 10, 11, 12, 13, 5])
 @pytest.mark.parametrize("split", [2, 4, 8])
 def test_split_rays_bitexact(r, oracle, vol128, layout, split):
     """Step-split rays (K lanes per ray, terms summed in step order): exact
@@ -635,3 +636,88 @@ def test_split_rays_bitexact(r, oracle, vol128, layout, split):
         r.set_option("split", 0)
         r.set_option("schedule", -1)
         r.set_layout_preference(0)
+
+
+@pytest.mark.parametrize("layout", [12, 5])
+def test_auto_split_at_one_eighth_band_share(r, oracle, vol128, layout):
+    """The multi-GPU config-5 path: auto split (split=0) turns on for a 1/8
+    band share of a 1080p frame, with brick4832 (the auto
+    layout past the Infinity Cache) and corner8.  Exact, step counts too."""
+    r.set_layout_preference(layout)
+    r.set_option("schedule", 5)
+    r.set_option("split", 0)
+    try:
+        osd, gsd = vr.reference_shader_data(16 / 9)
+        for first in (0, 5):
+            img, ref, c, s = render_both(r, oracle, vol128, 1920, 1080, osd, gsd,
+                                         band_rows=16, band_stride=8, band_first=first)
+            assert_exact(img, ref)
+            assert c == s
+    finally:
+        r.set_option("schedule", -1)
+        r.set_layout_preference(0)
+
+
+# ---- BASELINE config 4: 3840x2160, 256 steps, 128^3 recipe volume ----
+
+@pytest.fixture(scope="module")
+def config4(r):
+    """The config-4 frame at its stated shape on the HIP path: the 128^3
+    reference-recipe volume generated on the GPU, reference camera (16:9),
+    max_steps 256 (frag.glsl:30,42,46: step 1/64, at most 221 steps)."""
+    r.generate_volume(vr.volume_recipe_defaults())
+    vol = r.get_volume()
+    osd, gsd = vr.reference_shader_data(16 / 9)
+    march = vr.march_defaults(max_steps=256)
+    return vol, osd, gsd, march
+
+
+@pytest.mark.parametrize("fmt", [0, 1])
+def test_config4_4k_256_bands(r, oracle, config4, fmt):
+    """3840x2160x256, RGBA32F and RGBA8: the whole GPU frame against the
+    oracle on three interleaved band subsets (every 24th 16-row band), and
+    the executed-step count of the whole frame (1.348e8)."""
+    vol, osd, gsd, march = config4
+    W, H = 3840, 2160
+    r.set_volume(vol)
+    r.set_shader_data(osd, gsd)
+    r.set_march(march)
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    img = r.render(W, H, fmt, step_counter=cnt).cpu().numpy()
+    steps = int(cnt.item())
+    assert 134_000_000 < steps < 135_600_000
+    obj, glob = vr.shader_data_arrays(osd, gsd)
+    for first in (0, 13, 23):
+        ref, _ = oracle.render(vol, obj, glob, oracle.from_params(march), W, H, fmt, band_rows=16,
+                               band_stride=24, band_first=first)
+        rows = [(first + (i // 16) * 24) * 16 + i % 16 for i in range(ref.shape[0])]
+        keep = [i for i, y in enumerate(rows) if y < H]
+        assert_exact(img[[rows[i] for i in keep]], ref[keep])
+    # the whole-frame step count equals the oracle's (a3 truncation, frag.glsl:46)
+    n = oracle.step_counts(obj, glob, oracle.from_params(march), W, H)
+    assert steps == int(n[n > 0].sum(dtype=np.int64))
+
+
+def test_config4_8_rank_loopback(r, config4):
+    """Config 4 through the native 8-rank frame loop in loopback (every rank's
+    interleaved band set rendered on this GPU into its gather slot, then
+    vr_assemble_bands): the assembled frame equals a plain render."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from volumetricrenderer_amd.distributed import RcclBandPipeline
+    vol, osd, gsd, march = config4
+    W, H = 3840, 2160
+    r.set_volume(vol)
+    r.set_shader_data(osd, gsd)
+    r.set_march(march)
+    for fmt in (1, 0):
+        pl = RcclBandPipeline(r, W, H, fmt, band_rows=16, world=8, rank=0, loopback=True)
+        try:
+            pl.run_frames(3)
+            got = pl.frame()
+            full = r.render(W, H, fmt)
+            torch.cuda.synchronize()
+            assert torch.equal(got, full)
+        finally:
+            pl.close()

@@ -174,6 +174,9 @@ _SHARD_SIGS = {
     "vr_shard_unique_id": (ctypes.c_int, [_vp]),
     "vr_shard_create": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_int, ctypes.c_int, ctypes.POINTER(_vp)]),
+    "vr_shard_alloc": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                      ctypes.c_int, ctypes.c_int, ctypes.POINTER(_vp)]),
+    "vr_shard_connect": (ctypes.c_int, [_vp, _vp]),
     "vr_shard_destroy": (ctypes.c_int, [_vp]),
     "vr_shard_run": (ctypes.c_int, [_vp, ctypes.c_int, _vp, ctypes.c_int, c_float_p]),
     "vr_shard_frame": (ctypes.c_int, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(ctypes.c_size_t), c_int_p]),

@@ -166,20 +166,18 @@ vr_status vr_shard_unique_id(uint8_t id[VR_SHARD_ID_BYTES])
     return VR_OK;
 }
 
-vr_status vr_shard_create(void* ctx, const uint8_t id[VR_SHARD_ID_BYTES], int nranks, int rank, int width,
-                          int height, int format, int band_rows, vr_shard** out)
+vr_status vr_shard_alloc(void* ctx, int nranks, int rank, int width, int height, int format, int band_rows,
+                         vr_shard** out)
 {
-    if (!ctx || !out) return fail(VR_ERR_INVALID, "vr_shard_create: null argument");
+    if (!ctx || !out) return fail(VR_ERR_INVALID, "vr_shard_alloc: null argument");
     *out = nullptr;
-    const bool loopback = !id && rank == 0;
-    if (!id && !loopback) return fail(VR_ERR_INVALID, "vr_shard_create: null id (loopback needs rank 0)");
-    if (nranks < 1 || rank < 0 || rank >= nranks) return fail(VR_ERR_INVALID, "vr_shard_create: rank %d of %d", rank, nranks);
+    if (nranks < 1 || rank < 0 || rank >= nranks) return fail(VR_ERR_INVALID, "vr_shard_alloc: rank %d of %d", rank, nranks);
     if (width <= 0 || height <= 0 || band_rows <= 0 || format < 0 || format > 2)
-        return fail(VR_ERR_INVALID, "vr_shard_create: bad frame %dx%d format %d bands %d", width, height, format, band_rows);
+        return fail(VR_ERR_INVALID, "vr_shard_alloc: bad frame %dx%d format %d bands %d", width, height, format, band_rows);
     vr_shard* sh = new (std::nothrow) vr_shard();
-    if (!sh) return fail(VR_ERR_OOM, "vr_shard_create: host allocation");
+    if (!sh) return fail(VR_ERR_OOM, "vr_shard_alloc: host allocation");
     sh->ctx = ctx;
-    sh->loopback = loopback;
+    sh->loopback = true;   // until vr_shard_connect joins a communicator
     sh->nranks = nranks;
     sh->rank = rank;
     sh->width = width;
@@ -196,7 +194,7 @@ vr_status vr_shard_create(void* ctx, const uint8_t id[VR_SHARD_ID_BYTES], int nr
     vr_status st = VR_OK;
     auto hip_ok = [&](hipError_t r, const char* what) {
         if (st == VR_OK && r != hipSuccess)
-            st = fail(r == hipErrorOutOfMemory ? VR_ERR_OOM : VR_ERR_HIP, "vr_shard_create: %s: %s", what,
+            st = fail(r == hipErrorOutOfMemory ? VR_ERR_OOM : VR_ERR_HIP, "vr_shard_alloc: %s: %s", what,
                       hipGetErrorString(r));
         return st == VR_OK;
     };
@@ -213,20 +211,49 @@ vr_status vr_shard_create(void* ctx, const uint8_t id[VR_SHARD_ID_BYTES], int nr
             hip_ok(hipMalloc(&sh->local[p], (size_t)std::max(sh->my_rows, 1) * sh->pitch), "band buffer");
         }
     }
-    if (st == VR_OK && !loopback) {
-        ncclUniqueId u;
-        std::memcpy(&u, id, sizeof u);
-        const ncclResult_t r = ncclCommInitRank(&sh->comm, nranks, u, rank);
-        if (r != ncclSuccess) {
-            sh->comm = nullptr;
-            st = fail(VR_ERR_HIP, "vr_shard_create: ncclCommInitRank: %s", ncclGetErrorString(r));
-        }
-    }
     if (st != VR_OK) {
         const std::string msg = g_err;
         release(sh);
         g_err = msg;
         return st;
+    }
+    *out = sh;
+    return VR_OK;
+}
+
+vr_status vr_shard_connect(vr_shard* sh, const uint8_t id[VR_SHARD_ID_BYTES])
+{
+    if (!sh || !id) return fail(VR_ERR_INVALID, "vr_shard_connect: null argument");
+    if (sh->comm) return fail(VR_ERR_INVALID, "vr_shard_connect: already connected");
+    if (sh->last >= 0) return fail(VR_ERR_INVALID, "vr_shard_connect: frames already rendered in loopback");
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof u);
+    const ncclResult_t r = ncclCommInitRank(&sh->comm, sh->nranks, u, sh->rank);
+    if (r != ncclSuccess) {
+        sh->comm = nullptr;
+        return fail(VR_ERR_HIP, "vr_shard_connect: ncclCommInitRank: %s", ncclGetErrorString(r));
+    }
+    sh->loopback = false;
+    return VR_OK;
+}
+
+vr_status vr_shard_create(void* ctx, const uint8_t id[VR_SHARD_ID_BYTES], int nranks, int rank, int width,
+                          int height, int format, int band_rows, vr_shard** out)
+{
+    if (!ctx || !out) return fail(VR_ERR_INVALID, "vr_shard_create: null argument");
+    *out = nullptr;
+    if (!id && rank != 0) return fail(VR_ERR_INVALID, "vr_shard_create: null id (loopback needs rank 0)");
+    vr_shard* sh = nullptr;
+    vr_status st = vr_shard_alloc(ctx, nranks, rank, width, height, format, band_rows, &sh);
+    if (st != VR_OK) return st;
+    if (id) {
+        st = vr_shard_connect(sh, id);
+        if (st != VR_OK) {
+            const std::string msg = g_err;
+            release(sh);
+            g_err = msg;
+            return st;
+        }
     }
     *out = sh;
     return VR_OK;
@@ -242,6 +269,8 @@ vr_status vr_shard_run(vr_shard* sh, int frames, void* stream, int sample_every,
 {
     if (!sh || frames < 0) return fail(VR_ERR_INVALID, "vr_shard_run: bad argument");
     if (kernel_ms && sample_every <= 0) return fail(VR_ERR_INVALID, "vr_shard_run: sample_every must be > 0");
+    if (sh->loopback && sh->rank != 0)
+        return fail(VR_ERR_INVALID, "vr_shard_run: rank %d is not connected (vr_shard_connect)", sh->rank);
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int nsamp = kernel_ms ? (frames + sample_every - 1) / sample_every : 0;
     while ((int)sh->timing.size() < 2 * nsamp) {

@@ -220,9 +220,32 @@ class RcclBandPipeline:
             ctypes.memmove(uid, bytes(got[1:]), _lib.SHARD_ID_BYTES)
         elif err:
             raise err
+        # Two phases, so that no rank enters the collective communicator init
+        # while a peer has failed to allocate (it would block there forever):
+        # allocate locally, agree over the torch group, then connect.
         h = ctypes.c_void_p()
-        _lib.shard_call("vr_shard_create", renderer._ctx, uid, world, rank, width, height, fmt, band_rows,
-                        ctypes.byref(h))
+        alloc_err = None
+        try:
+            _lib.shard_call("vr_shard_alloc", renderer._ctx, world, rank, width, height, fmt, band_rows,
+                            ctypes.byref(h))
+        except _lib.VRError as e:
+            alloc_err = e
+        if world > 1 and not loopback:
+            ok = torch.tensor([0 if alloc_err else 1], dtype=torch.int64,
+                              device="cuda" if dist.get_backend(group) == "nccl" else "cpu")
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+            if int(ok.item()) == 0:
+                if h:
+                    _lib.shard_call("vr_shard_destroy", h)
+                raise alloc_err or _lib.VRError(2, "vr_shard_alloc", "failed on another rank")
+        elif alloc_err:
+            raise alloc_err
+        if not loopback:
+            try:
+                _lib.shard_call("vr_shard_connect", h, uid)
+            except _lib.VRError:
+                _lib.shard_call("vr_shard_destroy", h)
+                raise
         self._h = h
         mine, per = ctypes.c_int(), ctypes.c_int()
         _lib.shard_call("vr_shard_rows", h, ctypes.byref(mine), ctypes.byref(per))

@@ -227,12 +227,36 @@ class Renderer:
             return torch.empty((rows, width, 4), dtype=torch.float32, device=dev)
         return torch.empty((rows, width, 4), dtype=torch.uint8, device=dev)
 
+    def _check_target(self, width: int, height: int, fmt: int, out: torch.Tensor, band_rows: int,
+                      band_stride: int, band_first: int, step_counter: torch.Tensor | None = None) -> None:
+        """The kernel writes band_rows_packed(...) rows of `width` pixels of
+        BYTES_PER_PIXEL[fmt] bytes through a raw pointer: refuse any tensor it
+        would write past, or that lives on another device."""
+        if fmt not in BYTES_PER_PIXEL:
+            raise ValueError(f"unknown format {fmt}")
+        if not isinstance(out, torch.Tensor) or not out.is_cuda or out.device.index != self.device:
+            raise ValueError(f"render target must be a tensor on cuda:{self.device}")
+        want_dtype = torch.float32 if fmt == FMT_RGBA32F else torch.uint8
+        if out.dtype != want_dtype:
+            raise ValueError(f"format {fmt} needs a {want_dtype} target, got {out.dtype}")
+        rows = band_rows_packed(height, band_rows, band_stride, band_first)
+        if out.dim() != 3 or out.shape[0] < rows or out.shape[1] != width or out.shape[2] != 4:
+            raise ValueError(f"render target must be shaped ({rows}, {width}, 4) (at least {rows} rows), "
+                             f"got {tuple(out.shape)}")
+        if out.stride(2) != 1 or out.stride(1) != 4 or out.stride(0) < 4 * width:
+            raise ValueError("render target rows must be contiguous RGBA pixels (strides (>=4*width, 4, 1))")
+        if step_counter is not None and (step_counter.dtype != torch.int64 or not step_counter.is_cuda
+                                         or step_counter.device.index != self.device
+                                         or step_counter.numel() < 1):
+            raise ValueError(f"step_counter must be an int64 tensor on cuda:{self.device}")
+
     def render(self, width: int, height: int, fmt: int = FMT_RGBA8_UNORM, out: torch.Tensor | None = None,
                band_rows: int = 0, band_stride: int = 1, band_first: int = 0, stream=None,
                step_counter: torch.Tensor | None = None) -> torch.Tensor:
         """Launch the march kernel (asynchronous on `stream`); returns `out`."""
         if out is None:
             out = self.alloc_target(width, height, fmt, band_rows, band_stride, band_first)
+        self._check_target(width, height, fmt, out, band_rows, band_stride, band_first, step_counter)
         t = Target(width=width, height=height, format=fmt, band_rows=band_rows, band_stride=band_stride,
                    band_first=band_first, pixels=out.data_ptr(), row_pitch=out.stride(0) * out.element_size(),
                    step_counter=step_counter.data_ptr() if step_counter is not None else None)
@@ -244,6 +268,7 @@ class Renderer:
         """A zero-argument launcher for one fixed render (target, bands,
         stream): the ctypes arguments are built once, so a frame loop pays
         only the call (host time per frame bounds multi-GPU strong scaling)."""
+        self._check_target(width, height, fmt, out, band_rows, band_stride, band_first)
         t = Target(width=width, height=height, format=fmt, band_rows=band_rows, band_stride=band_stride,
                    band_first=band_first, pixels=out.data_ptr(), row_pitch=out.stride(0) * out.element_size(),
                    step_counter=None)
@@ -253,12 +278,14 @@ class Renderer:
             st = fn(ctx, tref, sh)
             if st:
                 _lib.check(st, "vr_render")
-        launch.target = t   # keep the struct alive with the closure
+        launch.target = t   # keep the struct and the target tensor alive with the closure
+        launch.out = out
         return launch
 
     def prepare_assemble(self, gathered: torch.Tensor, nranks: int, width: int, height: int, band_rows: int,
                          frame: torch.Tensor, stream=None):
         """Zero-argument launcher for one fixed vr_assemble_bands call."""
+        self._check_assemble(gathered, nranks, width, height, band_rows, frame)
         bpp = gathered.element_size() * gathered.shape[-1]
         args = (self._ctx, ctypes.c_void_p(gathered.data_ptr()), gathered.shape[1], nranks, width, height, band_rows,
                 bpp, ctypes.c_void_p(frame.data_ptr()), _stream_handle(stream))
@@ -268,7 +295,18 @@ class Renderer:
             st = fn(*args)
             if st:
                 _lib.check(st, "vr_assemble_bands")
+        launch.keep = (gathered, frame)
         return launch
+
+    def _check_assemble(self, gathered: torch.Tensor, nranks: int, width: int, height: int, band_rows: int,
+                        frame: torch.Tensor) -> None:
+        for name, t in (("gathered", gathered), ("frame", frame)):
+            if not t.is_cuda or t.device.index != self.device or not t.is_contiguous():
+                raise ValueError(f"{name} must be a contiguous tensor on cuda:{self.device}")
+        if gathered.dim() != 4 or gathered.shape[0] < nranks or gathered.shape[2] != width or gathered.shape[3] != 4:
+            raise ValueError(f"gathered must be shaped (>= {nranks}, rows, {width}, 4), got {tuple(gathered.shape)}")
+        if frame.dtype != gathered.dtype or tuple(frame.shape) != (height, width, 4):
+            raise ValueError(f"frame must be a {gathered.dtype} tensor shaped ({height}, {width}, 4)")
 
     def assemble_bands(self, gathered: torch.Tensor, nranks: int, width: int, height: int, band_rows: int,
                        frame: torch.Tensor | None = None, stream=None) -> torch.Tensor:
@@ -277,6 +315,7 @@ class Renderer:
         rows_per_rank = gathered.shape[1]
         if frame is None:
             frame = torch.empty((height, width, gathered.shape[-1]), dtype=gathered.dtype, device=gathered.device)
+        self._check_assemble(gathered, nranks, width, height, band_rows, frame)
         call("vr_assemble_bands", self._ctx, ctypes.c_void_p(gathered.data_ptr()), rows_per_rank, nranks,
              width, height, band_rows, bpp, ctypes.c_void_p(frame.data_ptr()), _stream_handle(stream))
         return frame
