@@ -354,6 +354,11 @@ typedef struct {
     float org[3];   /* camera in box-local space  (frag.glsl:36)          */
     float o[3], px[3], py[3];  /* dir(x,y) = o + (x+.5) px + (y+.5) py    */
     float r2[4], r3[4];        /* rows 2,3 of P*V*M: clip z, clip w        */
+    /* cam_mode 1: CameraPosition is not the View eye; org/o/px/py are the
+     * eye's (the rasteriser's rays, vert.glsl:20) and cam is the box-local
+     * CameraPosition the fragment's ray starts from (frag.glsl:36-38).     */
+    int cam_mode;
+    float cam[3];
 } ray_basis;
 
 static int make_basis(const float* obj48, const float* glob36, int W, int H, ray_basis* b)
@@ -362,10 +367,24 @@ static int make_basis(const float* obj48, const float* glob36, int W, int H, ray
     for (int i = 0; i < 16; ++i) {
         M[i] = obj48[i]; V[i] = obj48[16 + i]; P[i] = obj48[32 + i]; L[i] = glob36[i];
     }
-    const double cam[3] = {glob36[16], glob36[17], glob36[18]};
+    const double cam_pos[3] = {glob36[16], glob36[17], glob36[18]};
     m4_mul_d(P, V, PV);
     m4_mul_d(PV, M, PVM);
     if (m4_inverse_d(PV, inv)) return 1;
+    /* the View eye, inverse(View) * (0,0,0,1): where the rasteriser's rays
+     * start.  Equal to CameraPosition up to float rounding in the reference
+     * (TestMain.cpp:225, :242): then the fragment's ray is the camera ray
+     * through the pixel centre (cam_mode 0).                                 */
+    double Vi[16];
+    if (m4_inverse_d(V, Vi) || Vi[15] == 0.0) return 1;
+    const double eye[3] = {Vi[12] / Vi[15], Vi[13] / Vi[15], Vi[14] / Vi[15]};
+    double err = 0.0, mag = 1.0;
+    for (int i = 0; i < 3; ++i) {
+        err = fmax(err, fabs(eye[i] - cam_pos[i]));
+        mag = fmax(mag, fabs(eye[i]));
+    }
+    b->cam_mode = err > 1e-6 * mag ? 1 : 0;
+    const double* cam = b->cam_mode ? eye : cam_pos;
     double D[3][3]; /* Dx, Dy, D0 (far plane, z_ndc = 1) in world space */
     for (int i = 0; i < 3; ++i) {
         D[0][i] = inv[0 * 4 + i] - cam[i] * inv[0 * 4 + 3];
@@ -383,6 +402,8 @@ static int make_basis(const float* obj48, const float* glob36, int W, int H, ray
         b->px[i] = (float)((Dl[0][i] * sx) * s);
         b->py[i] = (float)((Dl[1][i] * sy) * s);
         b->org[i] = (float)(((L[0 * 4 + i] * cam[0] + L[1 * 4 + i] * cam[1]) + L[2 * 4 + i] * cam[2]) + L[3 * 4 + i]);
+        b->cam[i] = (float)(((L[0 * 4 + i] * cam_pos[0] + L[1 * 4 + i] * cam_pos[1]) + L[2 * 4 + i] * cam_pos[2]) +
+                            L[3 * 4 + i]);
     }
     /* clip rows act on box-local points: P*V*M*inverse(W2L)... the reference
      * transforms local->world with Model (vert.glsl:20), so local == model
@@ -512,19 +533,39 @@ static inline int ray_setup(const ray_basis* b, const vro_march* m, const march_
     float tn = fmaxf(fmaxf(tlo[0], tlo[1]), tlo[2]);
     float tf = fminf(fminf(thi[0], thi[1]), thi[2]);
     if (!(tn <= tf)) return -1;
-    float pin[3], pout[3];                                                   /* :43-44 */
+    float pin[3], pout[3], c[3];                                             /* :43-44 */
     for (int a = 0; a < 3; ++a) {
         pin[a] = fmaf(d[a], tn, b->org[a]);
-        pout[a] = fmaf(d[a], tf, b->org[a]);
+        c[a] = b->org[a];
     }
     /* coverage: the front-face fragment survives clipping (0 <= z <= w)   */
     float zc = fmaf(b->r2[2], pin[2], fmaf(b->r2[1], pin[1], fmaf(b->r2[0], pin[0], b->r2[3])));
     float wc = fmaf(b->r3[2], pin[2], fmaf(b->r3[1], pin[1], fmaf(b->r3[0], pin[0], b->r3[3])));
     if (!(wc > 0.0f && zc >= 0.0f && zc <= wc)) return -1;
+    if (b->cam_mode) {
+        /* pin is the rasterised front-face point (vert.glsl:20); the
+         * fragment's ray leaves CameraPosition through it (frag.glsl:36-38)
+         * and IntersectAABB runs again from CameraPosition (:39).          */
+        float f[3];
+        for (int a = 0; a < 3; ++a) { c[a] = b->cam[a]; f[a] = pin[a] - c[a]; }
+        float fl = sqrtf(fmaf(f[2], f[2], fmaf(f[1], f[1], f[0] * f[0])));
+        for (int a = 0; a < 3; ++a) d[a] = f[a] / fl;
+        for (int a = 0; a < 3; ++a) {
+            float t0 = (m->box_min[a] - c[a]) / d[a];
+            float t1 = (m->box_max[a] - c[a]) / d[a];
+            tlo[a] = fminf(t0, t1);
+            thi[a] = fmaxf(t0, t1);
+        }
+        tn = fmaxf(fmaxf(tlo[0], tlo[1]), tlo[2]);
+        tf = fminf(fminf(thi[0], thi[1]), thi[2]);
+        for (int a = 0; a < 3; ++a) pin[a] = fmaf(d[a], tn, c[a]);
+    }
+    for (int a = 0; a < 3; ++a) pout[a] = fmaf(d[a], tf, c[a]);
     float dd[3] = {pout[0] - pin[0], pout[1] - pin[1], pout[2] - pin[2]};
     float dist = sqrtf(fmaf(dd[2], dd[2], fmaf(dd[1], dd[1], dd[0] * dd[0])));
     float q = dist / k->step_size;                                           /* :46 */
-    int n = q >= (float)m->max_steps ? m->max_steps : (int)q;
+    /* int(NaN) (a camera on the fragment) is undefined in GLSL: 0 here      */
+    int n = q >= (float)m->max_steps ? m->max_steps : q >= 0.0f ? (int)q : 0;
     for (int a = 0; a < 3; ++a) {                                            /* :45,49-54 */
         P[a] = (pin[a] - k->box_min[a]) / k->box_range[a];
         st[a] = (k->step_size * d[a]) / k->box_range[a];

@@ -253,9 +253,12 @@ def test_errors(oracle):
             rr.render(64, 64)
         assert e.value.status == 4  # VR_ERR_NO_CAMERA
         osd, gsd = vr.reference_shader_data(1.0)
-        gsd.camera_position[0] = 7.0  # not the View eye
-        with pytest.raises(VRError):
-            rr.set_shader_data(osd, gsd)
+        gsd.camera_position[0] = 7.0  # not the View eye: accepted (frag.glsl:36-38)
+        rr.set_shader_data(osd, gsd)
+        with pytest.raises(ValueError):   # a target the kernel would write past
+            rr.render(64, 64, vr.FMT_RGBA32F, out=torch.zeros((64, 64, 4), dtype=torch.uint8, device="cuda"))
+        with pytest.raises(ValueError):
+            rr.render(64, 64, vr.FMT_RGBA8_UNORM, out=torch.zeros((32, 64, 4), dtype=torch.uint8, device="cuda"))
         with pytest.raises(VRError):
             rr.set_march(vr.march_defaults(max_steps=0))
         with pytest.raises(ValueError):
@@ -721,3 +724,23 @@ def test_config4_8_rank_loopback(r, config4):
             assert torch.equal(got, full)
         finally:
             pl.close()
+
+
+@pytest.mark.parametrize("cam", [(4.0, 2.0, 2.5), (0.3, -0.2, 0.5), (-4.0, 1.0, 0.0), (3.0, 3.0, 3.0001)])
+@pytest.mark.parametrize("layout", [0, 1, 12])
+def test_camera_position_off_the_view_eye(r, oracle, vol128, cam, layout):
+    """CameraPosition != the View eye: the ray leaves CameraPosition through
+    the front-face point the View camera rasterises (frag.glsl:36-38,
+    vert.glsl:20).  Exact against the oracle (itself checked against the
+    float64 restatement in tests/test_oracle_independent.py), for the auto,
+    planar and brick4832 layouts."""
+    osd, gsd = vr.reference_shader_data(16 / 9, 20.0, 10.0)
+    gsd.camera_position[:] = list(cam)
+    r.set_layout_preference(layout)
+    try:
+        for W, H, band in [(320, 180, {}), (400, 225, dict(band_rows=16, band_stride=3, band_first=1))]:
+            img, ref, c, s = render_both(r, oracle, vol128, W, H, osd, gsd, **band)
+            assert_exact(img, ref)
+            assert c == s
+    finally:
+        r.set_layout_preference(0)

@@ -544,22 +544,6 @@ vr_status vr_set_shader_data(void* p, const vr_object_shader_data* osd, const vr
 {
     if (!p || !osd || !gsd) return fail(VR_ERR_INVALID, "vr_set_shader_data: null argument");
     Ctx* c = as_ctx(p);
-    // The fragment ray runs from CameraPosition through the rasterised point
-    // of the View eye's pixel ray (frag.glsl:36-38, vert.glsl:20).  Both agree
-    // only if CameraPosition is the View eye, as at TestMain.cpp:225 / :242.
-    {
-        double V[16], Vi[16];
-        for (int i = 0; i < 16; ++i) V[i] = osd->view[i];
-        if (!vr::invert4_d(V, Vi)) return fail(VR_ERR_INVALID, "vr_set_shader_data: View is singular");
-        double err = 0.0, mag = 1.0;
-        for (int i = 0; i < 3; ++i) {
-            const double e = Vi[12 + i] / Vi[15];   // eye = inverse(View) * (0,0,0,1)
-            err = std::fmax(err, std::fabs(e - (double)gsd->camera_position[i]));
-            mag = std::fmax(mag, std::fabs(e));
-        }
-        if (!(err <= 1e-4 * mag))
-            return fail(VR_ERR_INVALID, "vr_set_shader_data: CameraPosition differs from the View eye by %g", err);
-    }
     std::memcpy(c->obj, osd, sizeof(float) * 48);
     std::memcpy(c->glob, gsd, sizeof(float) * 36);
     RayBasis b;
@@ -889,6 +873,8 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
     std::memcpy(a.org, b.org, sizeof a.org); std::memcpy(a.o, b.o, sizeof a.o);
     std::memcpy(a.px, b.px, sizeof a.px); std::memcpy(a.py, b.py, sizeof a.py);
     std::memcpy(a.r2, b.r2, sizeof a.r2); std::memcpy(a.r3, b.r3, sizeof a.r3);
+    a.cam_mode = b.cam_mode;
+    std::memcpy(a.cam, b.cam, sizeof a.cam);
     const vr_march_params& m = c->march;
     a.step_size = (1.0f / (float)m.max_steps) * m.step_scale;   // frag.glsl:42
     for (int ax = 0; ax < 3; ++ax) {

@@ -144,10 +144,26 @@ bool make_ray_basis(const float* obj48, const float* glob36, int W, int H, RayBa
     for (int i = 0; i < 16; ++i) {
         M[i] = obj48[i]; V[i] = obj48[16 + i]; P[i] = obj48[32 + i]; L[i] = glob36[i];
     }
-    const double cam[3] = {glob36[16], glob36[17], glob36[18]};
+    const double cam_pos[3] = {glob36[16], glob36[17], glob36[18]};
     mul_d(P, V, PV);
     mul_d(PV, M, PVM);
     if (!inverse_d(PV, inv)) return false;
+    // The rasteriser's rays leave the View eye, inverse(View) * (0,0,0,1).  The
+    // fragment shader's ray leaves CameraPosition through the rasterised point
+    // (frag.glsl:36-38).  While the two agree to float rounding the ray is the
+    // camera ray through the pixel centre (cam_mode 0, the reference's case,
+    // TestMain.cpp:225 / :242); otherwise the kernel finds the front-face
+    // point along the eye's ray and turns towards it (cam_mode 1).
+    double Vi[16];
+    if (!inverse_d(V, Vi) || Vi[15] == 0.0) return false;
+    const double eye[3] = {Vi[12] / Vi[15], Vi[13] / Vi[15], Vi[14] / Vi[15]};
+    double err = 0.0, mag = 1.0;
+    for (int i = 0; i < 3; ++i) {
+        err = std::fmax(err, std::fabs(eye[i] - cam_pos[i]));
+        mag = std::fmax(mag, std::fabs(eye[i]));
+    }
+    b->cam_mode = err > 1e-6 * mag ? 1 : 0;
+    const double* cam = b->cam_mode ? eye : cam_pos;   // where the basis' rays start
     // Unprojected pixel ray minus the camera, scaled by the homogeneous w:
     // columns x, y and the far-plane point (z_ndc = 1) of inverse(P*V).
     double D[3][3];
@@ -167,6 +183,8 @@ bool make_ray_basis(const float* obj48, const float* glob36, int W, int H, RayBa
         b->px[i] = (float)((Dl[0][i] * sx) * s);
         b->py[i] = (float)((Dl[1][i] * sy) * s);
         b->org[i] = (float)(((L[0 * 4 + i] * cam[0] + L[1 * 4 + i] * cam[1]) + L[2 * 4 + i] * cam[2]) + L[3 * 4 + i]);
+        b->cam[i] = (float)(((L[0 * 4 + i] * cam_pos[0] + L[1 * 4 + i] * cam_pos[1]) + L[2 * 4 + i] * cam_pos[2]) +
+                            L[3 * 4 + i]);
     }
     // clip rows of P*V*M act on box-local points (vert.glsl:19)
     for (int c = 0; c < 4; ++c) {

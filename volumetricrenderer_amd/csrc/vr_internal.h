@@ -131,6 +131,8 @@ struct MarchArgs {
     // ray basis in box-local space: dir(x,y) = o + (x+.5)*px + (y+.5)*py
     float org[3], o[3], px[3], py[3];
     float r2[4], r3[4];          // rows 2/3 of P*V*M (coverage clip test)
+    int cam_mode;                // 1: org/o/px/py are the View eye's, the march starts at cam (RayBasis)
+    float cam[3];
     float box_min[3], box_max[3], box_range[3];
     float step_size, density, scale, acc_limit;
     int max_steps;
@@ -207,6 +209,13 @@ hipError_t launch_selftest_cell_inv(int variant, unsigned long long* d_bad, hipS
 // host camera math (vr_camera.cpp)
 struct RayBasis {
     float org[3], o[3], px[3], py[3], r2[4], r3[4];
+    // cam_mode 0: CameraPosition is the View eye (to float rounding): org is
+    // the camera, o/px/py its pixel-ray directions.  cam_mode 1: org and
+    // o/px/py are the View EYE's (they find the rasterised front-face point,
+    // vert.glsl:20), cam the box-local CameraPosition the march starts from
+    // (frag.glsl:36-38).  DESIGN.md sec. 3.1.
+    int cam_mode;
+    float cam[3];
 };
 bool invert4_d(const double* m, double* inv);
 bool make_ray_basis(const float* obj48, const float* glob36, int width, int height, RayBasis* b);

@@ -268,24 +268,41 @@ __device__ __forceinline__ Ray setup_ray(const MarchArgs& a, int x, int orow)
     const float v1 = fmaf(fy, a.py[1], fmaf(fx, a.px[1], a.o[1]));
     const float v2 = fmaf(fy, a.py[2], fmaf(fx, a.px[2], a.o[2]));
     const float len = sqrtf(fmaf(v2, v2, fmaf(v1, v1, v0 * v0)));
-    const float d0 = v0 / len, d1 = v1 / len, d2 = v2 / len;
+    float d0 = v0 / len, d1 = v1 / len, d2 = v2 / len;
     // IntersectAABB, frag.glsl:18-27
-    const float ta0 = (a.box_min[0] - a.org[0]) / d0, tb0 = (a.box_max[0] - a.org[0]) / d0;
-    const float ta1 = (a.box_min[1] - a.org[1]) / d1, tb1 = (a.box_max[1] - a.org[1]) / d1;
-    const float ta2 = (a.box_min[2] - a.org[2]) / d2, tb2 = (a.box_max[2] - a.org[2]) / d2;
-    const float tn = fmaxf(fmaxf(fminf(ta0, tb0), fminf(ta1, tb1)), fminf(ta2, tb2));
-    const float tf = fminf(fminf(fmaxf(ta0, tb0), fmaxf(ta1, tb1)), fmaxf(ta2, tb2));
+    float ta0 = (a.box_min[0] - a.org[0]) / d0, tb0 = (a.box_max[0] - a.org[0]) / d0;
+    float ta1 = (a.box_min[1] - a.org[1]) / d1, tb1 = (a.box_max[1] - a.org[1]) / d1;
+    float ta2 = (a.box_min[2] - a.org[2]) / d2, tb2 = (a.box_max[2] - a.org[2]) / d2;
+    float tn = fmaxf(fmaxf(fminf(ta0, tb0), fminf(ta1, tb1)), fminf(ta2, tb2));
+    float tf = fminf(fminf(fmaxf(ta0, tb0), fmaxf(ta1, tb1)), fmaxf(ta2, tb2));
     if (!(tn <= tf)) return r;
-    const float pi0 = fmaf(d0, tn, a.org[0]), pi1 = fmaf(d1, tn, a.org[1]), pi2 = fmaf(d2, tn, a.org[2]);
+    float pi0 = fmaf(d0, tn, a.org[0]), pi1 = fmaf(d1, tn, a.org[1]), pi2 = fmaf(d2, tn, a.org[2]);
     // coverage: the front-face fragment survives clipping (0 <= z <= w)
     const float zc = fmaf(a.r2[2], pi2, fmaf(a.r2[1], pi1, fmaf(a.r2[0], pi0, a.r2[3])));
     const float wc = fmaf(a.r3[2], pi2, fmaf(a.r3[1], pi1, fmaf(a.r3[0], pi0, a.r3[3])));
     if (!(wc > 0.0f && zc >= 0.0f && zc <= wc)) return r;
-    const float po0 = fmaf(d0, tf, a.org[0]), po1 = fmaf(d1, tf, a.org[1]), po2 = fmaf(d2, tf, a.org[2]);
+    float c0 = a.org[0], c1 = a.org[1], c2 = a.org[2];
+    if (a.cam_mode) {
+        // CameraPosition is not the View eye: pi is the rasterised front-face
+        // point (vert.glsl:20); the fragment's ray leaves CameraPosition through
+        // it (frag.glsl:36-38), and IntersectAABB runs again from there
+        c0 = a.cam[0]; c1 = a.cam[1]; c2 = a.cam[2];
+        const float f0 = pi0 - c0, f1 = pi1 - c1, f2 = pi2 - c2;
+        const float fl = sqrtf(fmaf(f2, f2, fmaf(f1, f1, f0 * f0)));
+        d0 = f0 / fl; d1 = f1 / fl; d2 = f2 / fl;
+        ta0 = (a.box_min[0] - c0) / d0; tb0 = (a.box_max[0] - c0) / d0;
+        ta1 = (a.box_min[1] - c1) / d1; tb1 = (a.box_max[1] - c1) / d1;
+        ta2 = (a.box_min[2] - c2) / d2; tb2 = (a.box_max[2] - c2) / d2;
+        tn = fmaxf(fmaxf(fminf(ta0, tb0), fminf(ta1, tb1)), fminf(ta2, tb2));
+        tf = fminf(fminf(fmaxf(ta0, tb0), fmaxf(ta1, tb1)), fmaxf(ta2, tb2));
+        pi0 = fmaf(d0, tn, c0); pi1 = fmaf(d1, tn, c1); pi2 = fmaf(d2, tn, c2);
+    }
+    const float po0 = fmaf(d0, tf, c0), po1 = fmaf(d1, tf, c1), po2 = fmaf(d2, tf, c2);
     const float e0 = po0 - pi0, e1 = po1 - pi1, e2 = po2 - pi2;
     const float dist = sqrtf(fmaf(e2, e2, fmaf(e1, e1, e0 * e0)));
     const float q = dist / a.step_size;                                   // :46
-    r.n = q >= (float)a.max_steps ? a.max_steps : (int)q;
+    // int(NaN) (a degenerate camera on the fragment) is undefined in GLSL: 0 here
+    r.n = q >= (float)a.max_steps ? a.max_steps : q >= 0.0f ? (int)q : 0;
     r.pxy = f2{(pi0 - a.box_min[0]) / a.box_range[0], (pi1 - a.box_min[1]) / a.box_range[1]};   // :49-54
     r.pz = (pi2 - a.box_min[2]) / a.box_range[2];
     r.sxy = f2{(a.step_size * d0) / a.box_range[0], (a.step_size * d1) / a.box_range[1]};       // :45
