@@ -744,3 +744,71 @@ def test_camera_position_off_the_view_eye(r, oracle, vol128, cam, layout):
             assert c == s
     finally:
         r.set_layout_preference(0)
+
+
+# ---- the clamp-to-edge proof (vr_api.cpp clamp_is_exact) under adversarial offsets ----
+
+def clamp_is_exact_py(march, glob, dims):
+    """Python replica of vr_api.cpp clamp_is_exact / tap_constants: may the
+    fast (clamp-to-edge) layouts stand in for MIRRORED_REPEAT this frame?"""
+    f32 = np.float32
+    slack = (march.max_steps + 16) * 1.2e-7
+    for t in range(4):
+        for a in range(3):
+            off = f32(glob[20 + a * 4 + t]) * f32(march.tap_weight[t])
+            S = f32(march.tap_scale[t]) * f32(dims[a])
+            T = off * f32(dims[a]) + f32(0.5)
+            s, o = float(S), float(T)
+            margin = abs(s) * slack + (dims[a] + 2.0) * 2.4e-7 + 1e-6
+            lo, hi = min(o, s + o) - margin, max(o, s + o) + margin
+            if not (lo >= 0.0 and hi < dims[a] + 1.0):
+                return False
+    return True
+
+
+def offset_for_T(T, N, w):
+    """A MediaScroll entry that makes the tap's padded offset T = off*N + 0.5 = T (float32)."""
+    f32 = np.float32
+    v = f32((T - 0.5) / N / w)
+    for _ in range(64):   # nudge to the float whose T rounds where asked
+        got = float(f32(v) * f32(w) * f32(N) + f32(0.5))
+        if got == np.float32(T):
+            break
+        v = np.nextafter(v, f32(np.inf) if got < T else f32(-np.inf), dtype=np.float32)
+    return float(v)
+
+
+@pytest.mark.parametrize("max_steps", [1, 300])
+@pytest.mark.parametrize("edge", ["low", "high"])
+def test_wrap_mode_switch_at_the_margin(r, oracle, vol128, max_steps, edge):
+    """Tap ranges g within ~1e-6 of 0 and of N+1, on both sides of
+    clamp_is_exact's margin: the fast layout runs exactly when the proof
+    holds, planar mirrored repeat otherwise, and the frame is exact either
+    way -- including offsets where rays entering through a face put taps a
+    hair outside [0, N+1), where clamp and mirror really differ."""
+    N = 128
+    base = vr.march_defaults(max_steps=max_steps)
+    slack = (max_steps + 16) * 1.2e-7
+    seen = set()
+    for t in (1, 3):
+        S = float(np.float32(base.tap_scale[t]) * np.float32(N))
+        margin = abs(S) * slack + (N + 2.0) * 2.4e-7 + 1e-6
+        for delta in (-3e-6, -1e-6, -1e-7, 1e-7, 1e-6, 3e-6, 2e-4):
+            # low edge: T just above/below margin; high edge: S + T just below/above N + 1 - margin
+            T = margin + delta if edge == "low" else (N + 1.0 - margin) - S + delta
+            # rays enter the box through the faces on the edge's side (P = 0 faces
+            # for the low edge: the camera rotated to local (-3,-3,3)), so taps at
+            # entry points sit right at the edge of the g-range
+            osd, gsd = vr.reference_shader_data(16 / 9, 180.0 if edge == "low" else 0.0, 5.0)
+            w = float(base.tap_weight[t])
+            for a in range(3):
+                gsd.media_scroll[a * 4 + t] = offset_for_T(T, N, w)
+            obj, glob = vr.shader_data_arrays(osd, gsd)
+            exact = clamp_is_exact_py(base, glob, (N, N, N))
+            img, ref, c, s = render_both(r, oracle, vol128, 256, 144, osd, gsd, march=base)
+            want = "grid_corner8_clamp" if exact else "grid_planar_mirror"
+            assert r.kernel_variant == want, (t, delta, exact)
+            assert_exact(img, ref)
+            assert c == s
+            seen.add(exact)
+    assert seen == {True, False}   # both sides of the margin were exercised
