@@ -106,3 +106,18 @@ hipError_t launch_march(const MarchArgs& a, int layout, int wrap, bool early, co
 }
 
 }  // namespace vr
+
+#ifdef VR_TIMELINE
+// timing experiments only (make timeline): copy / clear the per-wave records
+// of the regions kernels compiled in this translation unit
+extern "C" int vr_timeline_fetch(unsigned long long* host, int waves)
+{
+    waves = waves < vr::kTimelineWaves ? waves : vr::kTimelineWaves;
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(vr::g_timeline), (size_t)waves * 3 * sizeof(unsigned long long));
+}
+extern "C" int vr_timeline_clear()
+{
+    static unsigned long long zero[vr::kTimelineWaves][3];
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(vr::g_timeline), zero, sizeof(zero));
+}
+#endif

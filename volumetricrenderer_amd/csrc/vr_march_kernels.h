@@ -604,6 +604,25 @@ __device__ __forceinline__ int lane_y(int lane)
     else return lane >> 3;
 }
 
+#ifdef VR_TIMELINE
+// Timing experiments only (make timeline -> libvr_tl.so, tools/timeline.py):
+// per wave of a regions launch, {start, end} in s_memrealtime ticks (100 MHz),
+// the wave's XCD (blockIdx % 8) and its executed lane-steps.
+constexpr int kTimelineWaves = 1 << 16;
+__device__ unsigned long long g_timeline[kTimelineWaves][3];
+__device__ __forceinline__ void timeline_record(unsigned long long t_begin, unsigned long long steps)
+{
+    for (int off = 32; off > 0; off >>= 1) steps += __shfl_xor(steps, off);
+    const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+    const int wid = (int)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+    if ((threadIdx.x & 63) == 0 && wid < kTimelineWaves) {
+        g_timeline[wid][0] = t_begin;
+        g_timeline[wid][1] = t_end;
+        g_timeline[wid][2] = (steps << 8) | (blockIdx.x & 7);
+    }
+}
+#endif
+
 __device__ __forceinline__ void add_steps(const MarchArgs& a, unsigned long long cnt)
 {
     for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
@@ -728,6 +747,9 @@ __global__ __launch_bounds__(kThreads) void march_regions(const MarchArgs a, con
     const int w = (int)(blockIdx.x >> 3) * (kThreads / 64) + (threadIdx.x >> 6);
     const int begin = m.off[xcd], count = m.off[xcd + 1] - begin;
     if ((int)(blockIdx.x >> 3) * (kThreads / 64) >= count) return;   // whole workgroup, before the barrier
+#ifdef VR_TIMELINE
+    const unsigned long long t_begin = __builtin_amdgcn_s_memrealtime();
+#endif
     const FastCtx f = fast_prologue<LAYOUT>(a, lds);
     const int lane = threadIdx.x & 63;
     unsigned long long steps = 0;
@@ -736,6 +758,9 @@ __global__ __launch_bounds__(kThreads) void march_regions(const MarchArgs a, con
         const int tx = (int)(t & 0xffffu), ty = (int)(t >> 16);
         steps += march_pixel<LAYOUT, WRAP, EARLY, ZO>(a, f, tx * 8 + lane_x<LAYOUT>(lane), ty * 8 + lane_y<LAYOUT>(lane));
     }
+#ifdef VR_TIMELINE
+    timeline_record(t_begin, steps);
+#endif
     if (a.step_counter) add_steps(a, steps);
 }
 
@@ -817,6 +842,9 @@ __global__ __launch_bounds__(kThreads) void march_regions_split(const MarchArgs 
     const int begin = m.off[xcd], units = (m.off[xcd + 1] - begin) * K;
     if ((int)(blockIdx.x >> 3) * (kThreads / 64) >= units) return;   // whole workgroup, before the barrier
     const FastCtx f = fast_prologue<LAYOUT>(a, lds);
+#ifdef VR_TIMELINE
+    const unsigned long long t_begin = __builtin_amdgcn_s_memrealtime();
+#endif
     const int lane = threadIdx.x & 63, k = lane / R, rho = lane % R;
     const int px = ((rho >> 2) % (SW / 2)) * 2 + (rho & 1), py = ((rho >> 2) / (SW / 2)) * 2 + ((rho >> 1) & 1);
     unsigned long long steps = 0;
@@ -826,6 +854,9 @@ __global__ __launch_bounds__(kThreads) void march_regions_split(const MarchArgs 
         const int x = (int)(t & 0xffffu) * 8 + (s % NSX) * SW + px, orow = (int)(t >> 16) * 8 + (s / NSX) * SH + py;
         steps += march_pixel_split<LAYOUT, EARLY, ZO, K>(a, f, x, orow, k, rho);
     }
+#ifdef VR_TIMELINE
+    timeline_record(t_begin, steps);
+#endif
     if (a.step_counter) add_steps(a, steps);
 }
 
