@@ -46,8 +46,10 @@ BYTES_PER_STEP = 32        # 4 trilinear taps x 8 texels x 1 B (SURVEY.md sec. 8
 # fp32 FLOP per executed grid ray-step (FMA = 2): per tap, texel coordinate 3 fma (6),
 # 3 fractions (3), 7 lerps x (sub + fma) (21), x 1/255 (1) = 31; x 4 taps = 124;
 # combine t0*t1*(t2+t3)*scale + acc (5); advance the ray point (3).  (SURVEY.md 8d
-# estimates ~90.)
+# estimates ~90.)  The CORNERH layout stores each footprint row as {a, b - a}, so its
+# 4 x-lerp subtractions per tap are done once at layout build, not per step: 116.
 FLOP_PER_STEP = 132
+FLOP_PER_STEP_CORNERH = 132 - 16
 
 CONFIGS = {
     # name: (volume N or None = procedural, width, height, max_steps, shadow steps, BASELINE configs index)
@@ -248,19 +250,21 @@ def main() -> int:
         ms_per_step = el / args.steps * 1e3
         value = W * H * S * args.steps / el / 1e6
         gather = local_steps * BYTES_PER_STEP / (kern_ms * 1e-3) / 1e9
-        if proc is None and "corner8" not in r.kernel_variant:
+        variant = r.kernel_variant
+        if proc is None and "corner8" not in variant and "cornerh" not in variant:
             roofline = {"bound": "hbm", "achieved": round(gather, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(gather / HBM_PEAK_GBS, 4), "traffic": None,
                         "achieved_def": "32 B algorithmic gather per executed ray-step x steps per launch "
                                         "/ mean march-kernel duration (HIP events on its stream)"}
         elif proc is None:
-            # cache-resident volume (corner8 is auto only when it fits the
-            # Infinity Cache): the march is VALU-bound (VALUBusy ~100 %,
+            # cache-resident volume (cornerh / corner8 are auto only when they
+            # fit the Infinity Cache): the march is VALU-bound (VALUBusy ~100 %,
             # profiles/r01_pmc/c8_4k.json), so the roofline is fp32 VALU
-            tf = local_steps * FLOP_PER_STEP / (kern_ms * 1e-3) / 1e12
+            fps = FLOP_PER_STEP_CORNERH if "cornerh" in variant else FLOP_PER_STEP
+            tf = local_steps * fps / (kern_ms * 1e-3) / 1e12
             roofline = {"bound": "valu", "achieved": round(tf, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                         "frac": round(tf / FP32_PEAK_TFLOPS, 4), "traffic": None,
-                        "achieved_def": f"{FLOP_PER_STEP} algorithmic fp32 FLOP per executed ray-step x steps per "
+                        "achieved_def": f"{fps} algorithmic fp32 FLOP per executed ray-step x steps per "
                                         "launch / mean march-kernel duration (HIP events on its stream); the volume "
                                         "is cache-resident",
                         "gather_GBs": round(gather, 1)}

@@ -215,7 +215,9 @@ const char* vr_kernel_variant(void* ctx);
  * ("brick488"), 10 = 4x8x16-texel bricks of 512 B ("brick4816"),
  * 11 = 4x16x16-texel bricks of 1 KiB ("brick41616"), 12 = 4x8x32-texel
  * bricks of 1 KiB ("brick4832"), 13 = 4x8x64-texel bricks of 2 KiB
- * ("brick4864").  Layouts 2-13 are
+ * ("brick4864"), 14 = per position the f16 pairs {a, b - a} of the four
+ * footprint rows, one 16-B load and four v_fma_mix_f32 per tap ("cornerh";
+ * volumes below 2^24 positions).  Layouts 2-14 are
  * used only where clamp-to-edge equals mirrored repeat.  Otherwise the
  * planar, mirrored-repeat kernel runs.  Rebuilds the layout (synchronous). */
 vr_status vr_set_layout_preference(void* ctx, int pref);

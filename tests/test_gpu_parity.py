@@ -103,7 +103,7 @@ def test_media_scroll_mirrored_repeat(r, oracle, vol128):
 @pytest.mark.parametrize("layout,name", [(1, "planar"), (2, "brick5"), (3, "brick8"), (4, "brick16"), (5, "corner8"),
                                          (6, "brick4"), (7, "zpair"), (8, "brick448"),
                                          (9, "brick488"), (10, "brick4816"), (11, "brick41616"),
-                                         (12, "brick4832"), (13, "brick4864")])
+                                         (12, "brick4832"), (13, "brick4864"), (14, "cornerh")])
 def test_every_layout_bitexact(r, oracle, vol128, layout, name):
     osd, gsd = vr.reference_shader_data(16 / 9, 20.0, -35.0)
     r.set_volume(vol128)
@@ -617,7 +617,7 @@ def test_regions_lists_across_streams(r, oracle, vol128):
         r.set_option("schedule", -1)
 
 
-@pytest.mark.parametrize("layout", [6, 7, 8, 9, 10, 11, 12, 13, 5])
+@pytest.mark.parametrize("layout", [6, 7, 8, 9, 10, 11, 12, 13, 5, 14])
 @pytest.mark.parametrize("split", [2, 4, 8])
 def test_split_rays_bitexact(r, oracle, vol128, layout, split):
     """Step-split rays (K lanes per ray, terms summed in step order): exact
@@ -641,11 +641,12 @@ def test_split_rays_bitexact(r, oracle, vol128, layout, split):
         r.set_layout_preference(0)
 
 
-@pytest.mark.parametrize("layout", [12, 5])
+@pytest.mark.parametrize("layout", [12, 5, 14])
 def test_auto_split_at_one_eighth_band_share(r, oracle, vol128, layout):
     """The multi-GPU config-5 path: auto split (split=0) turns on for a 1/8
     band share of a 1080p frame, with brick4832 (the auto
-    layout past the Infinity Cache) and corner8.  Exact, step counts too."""
+    layout past the Infinity Cache), corner8 and cornerh (the auto layout for
+    cache-resident volumes).  Exact, step counts too."""
     r.set_layout_preference(layout)
     r.set_option("schedule", 5)
     r.set_option("split", 0)
@@ -806,7 +807,7 @@ def test_wrap_mode_switch_at_the_margin(r, oracle, vol128, max_steps, edge):
             obj, glob = vr.shader_data_arrays(osd, gsd)
             exact = clamp_is_exact_py(base, glob, (N, N, N))
             img, ref, c, s = render_both(r, oracle, vol128, 256, 144, osd, gsd, march=base)
-            want = "grid_corner8_clamp" if exact else "grid_planar_mirror"
+            want = "grid_cornerh_clamp" if exact else "grid_planar_mirror"
             assert r.kernel_variant == want, (t, delta, exact)
             assert_exact(img, ref)
             assert c == s

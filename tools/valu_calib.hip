@@ -100,6 +100,13 @@ __device__ __forceinline__ void body(float (&f)[16], unsigned (&u)[16], float s)
     if constexpr (OP == 65) asm volatile("v_cmp_eq_u32 vcc, v1, v64\n\tv_cmp_eq_u32 vcc, v1, v65\n\tv_cmp_eq_u32 vcc, v1, v66\n\tv_cmp_eq_u32 vcc, v1, v67\n\tv_cmp_eq_u32 vcc, v1, v68\n\tv_cmp_eq_u32 vcc, v1, v69\n\tv_cmp_eq_u32 vcc, v1, v70\n\tv_cmp_eq_u32 vcc, v1, v71\n\tv_cmp_eq_u32 vcc, v1, v72\n\tv_cmp_eq_u32 vcc, v1, v73\n\tv_cmp_eq_u32 vcc, v1, v74\n\tv_cmp_eq_u32 vcc, v1, v75\n\tv_cmp_eq_u32 vcc, v1, v76\n\tv_cmp_eq_u32 vcc, v1, v77\n\tv_cmp_eq_u32 vcc, v1, v78\n\tv_cmp_eq_u32 vcc, v1, v79" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
     if constexpr (OP == 66) asm volatile("v_max_i32 v64, v1, v2\n\tv_max_i32 v65, v1, v2\n\tv_max_i32 v66, v1, v2\n\tv_max_i32 v67, v1, v2\n\tv_max_i32 v68, v1, v2\n\tv_max_i32 v69, v1, v2\n\tv_max_i32 v70, v1, v2\n\tv_max_i32 v71, v1, v2\n\tv_max_i32 v72, v1, v2\n\tv_max_i32 v73, v1, v2\n\tv_max_i32 v74, v1, v2\n\tv_max_i32 v75, v1, v2\n\tv_max_i32 v76, v1, v2\n\tv_max_i32 v77, v1, v2\n\tv_max_i32 v78, v1, v2\n\tv_max_i32 v79, v1, v2" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
     if constexpr (OP == 67) asm volatile("v_med3_f32 v64, v1, v2, v3\n\tv_med3_f32 v65, v1, v2, v3\n\tv_med3_f32 v66, v1, v2, v3\n\tv_med3_f32 v67, v1, v2, v3\n\tv_med3_f32 v68, v1, v2, v3\n\tv_med3_f32 v69, v1, v2, v3\n\tv_med3_f32 v70, v1, v2, v3\n\tv_med3_f32 v71, v1, v2, v3\n\tv_med3_f32 v72, v1, v2, v3\n\tv_med3_f32 v73, v1, v2, v3\n\tv_med3_f32 v74, v1, v2, v3\n\tv_med3_f32 v75, v1, v2, v3\n\tv_med3_f32 v76, v1, v2, v3\n\tv_med3_f32 v77, v1, v2, v3\n\tv_med3_f32 v78, v1, v2, v3\n\tv_med3_f32 v79, v1, v2, v3" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
+    if constexpr (OP == 68) asm volatile("v_fma_mix_f32 v64, v1, v2, v3 op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v65, v1, v2, v3 op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v66, v1, v2, v3 op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v67, v1, v2, v3 op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v68, v1, v2, v3 op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v69, v1, v2, v3 op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v70, v1, v2, v3 op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v71, v1, v2, v3 op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v72, v1, v2, v3 op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v73, v1, v2, v3 op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v74, v1, v2, v3 op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v75, v1, v2, v3 op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v76, v1, v2, v3 op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v77, v1, v2, v3 op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v78, v1, v2, v3 op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v79, v1, v2, v3 op_sel_hi:[0,0,1]" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
+    if constexpr (OP == 69) asm volatile("v_lshlrev_b32 v64, 16, v1\n\tv_lshlrev_b32 v65, 16, v1\n\tv_lshlrev_b32 v66, 16, v1\n\tv_lshlrev_b32 v67, 16, v1\n\tv_lshlrev_b32 v68, 16, v1\n\tv_lshlrev_b32 v69, 16, v1\n\tv_lshlrev_b32 v70, 16, v1\n\tv_lshlrev_b32 v71, 16, v1\n\tv_lshlrev_b32 v72, 16, v1\n\tv_lshlrev_b32 v73, 16, v1\n\tv_lshlrev_b32 v74, 16, v1\n\tv_lshlrev_b32 v75, 16, v1\n\tv_lshlrev_b32 v76, 16, v1\n\tv_lshlrev_b32 v77, 16, v1\n\tv_lshlrev_b32 v78, 16, v1\n\tv_lshlrev_b32 v79, 16, v1" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
+    if constexpr (OP == 70) asm volatile("v_cvt_f32_bf16 v64, v1\n\tv_cvt_f32_bf16 v65, v1\n\tv_cvt_f32_bf16 v66, v1\n\tv_cvt_f32_bf16 v67, v1\n\tv_cvt_f32_bf16 v68, v1\n\tv_cvt_f32_bf16 v69, v1\n\tv_cvt_f32_bf16 v70, v1\n\tv_cvt_f32_bf16 v71, v1\n\tv_cvt_f32_bf16 v72, v1\n\tv_cvt_f32_bf16 v73, v1\n\tv_cvt_f32_bf16 v74, v1\n\tv_cvt_f32_bf16 v75, v1\n\tv_cvt_f32_bf16 v76, v1\n\tv_cvt_f32_bf16 v77, v1\n\tv_cvt_f32_bf16 v78, v1\n\tv_cvt_f32_bf16 v79, v1" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
+    if constexpr (OP == 71) asm volatile("v_perm_b32 v64, v1, v2, v3\n\tv_perm_b32 v65, v1, v2, v3\n\tv_perm_b32 v66, v1, v2, v3\n\tv_perm_b32 v67, v1, v2, v3\n\tv_perm_b32 v68, v1, v2, v3\n\tv_perm_b32 v69, v1, v2, v3\n\tv_perm_b32 v70, v1, v2, v3\n\tv_perm_b32 v71, v1, v2, v3\n\tv_perm_b32 v72, v1, v2, v3\n\tv_perm_b32 v73, v1, v2, v3\n\tv_perm_b32 v74, v1, v2, v3\n\tv_perm_b32 v75, v1, v2, v3\n\tv_perm_b32 v76, v1, v2, v3\n\tv_perm_b32 v77, v1, v2, v3\n\tv_perm_b32 v78, v1, v2, v3\n\tv_perm_b32 v79, v1, v2, v3" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
+    if constexpr (OP == 72) asm volatile("v_cvt_f32_ubyte1 v64, v1\n\tv_cvt_f32_ubyte1 v65, v1\n\tv_cvt_f32_ubyte1 v66, v1\n\tv_cvt_f32_ubyte1 v67, v1\n\tv_cvt_f32_ubyte1 v68, v1\n\tv_cvt_f32_ubyte1 v69, v1\n\tv_cvt_f32_ubyte1 v70, v1\n\tv_cvt_f32_ubyte1 v71, v1\n\tv_cvt_f32_ubyte1 v72, v1\n\tv_cvt_f32_ubyte1 v73, v1\n\tv_cvt_f32_ubyte1 v74, v1\n\tv_cvt_f32_ubyte1 v75, v1\n\tv_cvt_f32_ubyte1 v76, v1\n\tv_cvt_f32_ubyte1 v77, v1\n\tv_cvt_f32_ubyte1 v78, v1\n\tv_cvt_f32_ubyte1 v79, v1" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
+    if constexpr (OP == 73) asm volatile("v_and_b32 v64, v2, v1\n\tv_and_b32 v65, v2, v1\n\tv_and_b32 v66, v2, v1\n\tv_and_b32 v67, v2, v1\n\tv_and_b32 v68, v2, v1\n\tv_and_b32 v69, v2, v1\n\tv_and_b32 v70, v2, v1\n\tv_and_b32 v71, v2, v1\n\tv_and_b32 v72, v2, v1\n\tv_and_b32 v73, v2, v1\n\tv_and_b32 v74, v2, v1\n\tv_and_b32 v75, v2, v1\n\tv_and_b32 v76, v2, v1\n\tv_and_b32 v77, v2, v1\n\tv_and_b32 v78, v2, v1\n\tv_and_b32 v79, v2, v1" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
+    if constexpr (OP == 74) asm volatile("v_fma_mix_f32 v64, v1, v2, v3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v65, v1, v2, v3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v66, v1, v2, v3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v67, v1, v2, v3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v68, v1, v2, v3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v69, v1, v2, v3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v70, v1, v2, v3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v71, v1, v2, v3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v72, v1, v2, v3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v73, v1, v2, v3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v74, v1, v2, v3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v75, v1, v2, v3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v76, v1, v2, v3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v77, v1, v2, v3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v78, v1, v2, v3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v79, v1, v2, v3 op_sel:[0,0,1] op_sel_hi:[0,0,1]" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
     if constexpr (OP == 0) { R16(FMA) }
     if constexpr (OP == 1) { R16(MUL) }
     if constexpr (OP == 2) { R16(MULLO) }
@@ -228,6 +235,13 @@ int main()
     run<59>("mul_vv", 1, cus, out, clk);
     run<60>("cnd_vop2", 1, cus, out, clk);
     run<61>("mul_sgpr_e64", 1, cus, out, clk);
+    run<68>("fma_mix_f16c", 1, cus, out, clk);
+    run<69>("lshlrev_16", 1, cus, out, clk);
+    run<70>("cvt_f32_bf16", 1, cus, out, clk);
+    run<71>("perm_b32", 1, cus, out, clk);
+    run<72>("cvt_ubyte1", 1, cus, out, clk);
+    run<73>("and_b32", 1, cus, out, clk);
+    run<74>("fma_mix_hi", 1, cus, out, clk);
     run<62>("mullo_sgpr", 1, cus, out, clk);
     run<63>("and_b32", 1, cus, out, clk);
     run<64>("or_b32", 1, cus, out, clk);

@@ -108,9 +108,11 @@ struct Ctx {
     long long renders_since_build = 0;
 };
 
-// Auto layout (measured): CORNER8 does one load per tap but
-// stores 8 bytes per texel.  It wins while the volume fits the 256 MiB
-// Infinity Cache.  Past that it is HBM-bound, and BRICK4832 (1.53x bytes, 3x7x31
+// Auto layout (measured): CORNERH (16 B per texel: one load
+// and four v_fma_mix_f32 per tap, no byte conversions, arithmetic index) and
+// CORNER8 (8 B per texel, one load per tap) win while the volume fits the
+// 256 MiB Infinity Cache; CORNERH is 1.18x / 1.40x faster than CORNER8 at
+// 128^3 (1080p x 128 / 4K x 256).  Past that they are HBM-bound, and BRICK4832 (1.53x bytes, 3x7x31
 // positions per 4x8x32 brick, BRICK4's two dword-aligned 8-byte loads per tap)
 // wins with the pipelined march: 2-5 % ahead of BRICK488 (1.74x) and 12-20 %
 // ahead of BRICK4 (2.37x) at 384^3-512^3, level at 200^3-256^3.  Taller bricks
@@ -118,6 +120,9 @@ struct Ctx {
 constexpr size_t kCorner8MaxBytes = 160ull << 20;
 int auto_layout(int nx, int ny, int nz)
 {
+    if (4 * layout_plane_bytes(LAYOUT_CORNERH, nx, ny, nz) <= kCorner8MaxBytes &&
+        (long long)(nx + 1) * (ny + 1) * (nz + 1) <= kCornerHMaxPositions)
+        return LAYOUT_CORNERH;
     return 4 * layout_plane_bytes(LAYOUT_CORNER8, nx, ny, nz) <= kCorner8MaxBytes ? LAYOUT_CORNER8 : LAYOUT_BRICK4832;
 }
 
@@ -142,8 +147,11 @@ bool dims_ok(int nx, int ny, int nz)
 
 int wanted_fast_layout(const Ctx* c)
 {
-    const int want = c->layout_pref == 0 ? auto_layout(c->nx, c->ny, c->nz) : c->layout_pref;
+    int want = c->layout_pref == 0 ? auto_layout(c->nx, c->ny, c->nz) : c->layout_pref;
     if (want == LAYOUT_PLANAR) return 0;
+    // CORNERH's fp32 index is exact only below 2^24 positions
+    if (want == LAYOUT_CORNERH && (long long)(c->nx + 1) * (c->ny + 1) * (c->nz + 1) > kCornerHMaxPositions)
+        want = LAYOUT_CORNER8;
     // 32-bit offsets inside the kernels: fall back to PAD16 if too large
     // and LDS offset tables of (nx+ny+nz+3) words: fall back to planar
     if (layout_plane_bytes(want, c->nx, c->ny, c->nz) >= (1ull << 31)) return 0;
@@ -269,6 +277,7 @@ const char* variant_name(const Plan& p)
         {"grid_brick41616_clamp", "grid_brick41616_clamp_early"},
         {"grid_brick4832_clamp", "grid_brick4832_clamp_early"},
         {"grid_brick4864_clamp", "grid_brick4864_clamp_early"},
+        {"grid_cornerh_clamp", "grid_cornerh_clamp_early"},
     };
     if (p.layout == LAYOUT_PLANAR && p.wrap == WRAP_MIRROR)
         return p.early ? "grid_planar_mirror_early" : "grid_planar_mirror";
@@ -971,7 +980,8 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
         sc.map = rb.map;
         // step-split rays: K lanes per ray when the frame
         // share is too small to fill the GPU with one-lane-per-ray waves
-        if (is_b4_family(pl.layout) || pl.layout == LAYOUT_ZPAIR || pl.layout == LAYOUT_CORNER8) {
+        if (is_b4_family(pl.layout) || pl.layout == LAYOUT_ZPAIR || pl.layout == LAYOUT_CORNER8 ||
+            pl.layout == LAYOUT_CORNERH) {
             int K = c->split;
             if (K == 0) {
                 K = 1;

@@ -44,8 +44,14 @@ enum Layout : int {
                              // bytes); slices 64 B apart
     LAYOUT_BRICK4832 = 12,   // 4x8x32 texels = 1 KiB (3x7x31 positions, 1.53x bytes)
     LAYOUT_BRICK4864 = 13,   // 4x8x64 texels = 2 KiB (3x7x63 positions, 1.51x bytes)
+    LAYOUT_CORNERH = 14,     // per base position 16 B: for each footprint row (y,z)
+                             // the f16 pair {a, b - a} of its x-neighbours a, b, so
+                             // each x-lerp is one v_fma_mix_f32; x fastest, no
+                             // bricks: the index is computed in fp32 (16x bytes)
 };
-constexpr int kNumLayouts = 14;
+constexpr int kNumLayouts = 15;
+// CORNERH's fp32 index a + (nx+1)(b + (ny+1)c) is exact below 2^24 positions
+constexpr long long kCornerHMaxPositions = 1ll << 24;
 // the layouts whose taps are BRICK4's two dword-aligned 8-B loads
 __host__ __device__ constexpr bool is_b4_family(int l)
 {
@@ -70,6 +76,8 @@ __host__ __device__ inline LayoutGeom layout_geom(int layout, int nx, int ny, in
     LayoutGeom g{};
     if (layout == LAYOUT_CORNER8) {
         g.B = 4; g.R = 4; g.brick = 512;
+    } else if (layout == LAYOUT_CORNERH) {
+        g.B = 1; g.R = 1; g.brick = 16;
     } else if (layout == LAYOUT_ZPAIR) {
         g.B = 3; g.R = 4; g.brick = 128;
     } else if (layout == LAYOUT_BRICK448 || layout == LAYOUT_BRICK488 || layout == LAYOUT_BRICK4816 ||
@@ -179,7 +187,8 @@ struct Schedule {
 
 // launchers (vr_march.hip / vr_volume.hip); return hipError_t
 hipError_t launch_march(const MarchArgs& a, int layout, int wrap, bool early, const Schedule& sc, hipStream_t s);
-hipError_t launch_march_corner8(const MarchArgs& a, bool early, const Schedule& sc, hipStream_t s);   // vr_march_c8.hip
+hipError_t launch_march_corner8(const MarchArgs& a, int layout, bool early, const Schedule& sc,
+                                hipStream_t s);   // CORNER8 / CORNERH, vr_march_c8.hip
 // sort_buf (proc_sort_bytes) selects the cost-sorted schedule; null = 8x8
 // tiles, in rings when sc.kind == SCHED_RINGS, else in row order
 hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_buf, const Schedule& sc, hipStream_t s);

@@ -98,7 +98,8 @@ hipError_t launch_march(const MarchArgs& a, int layout, int wrap, bool early, co
     case LAYOUT_BRICK5: return launch_lw<LAYOUT_BRICK5, WRAP_CLAMP>(a, early, sc, s);
     case LAYOUT_BRICK8: return launch_lw<LAYOUT_BRICK8, WRAP_CLAMP>(a, early, sc, s);
     case LAYOUT_BRICK16: return launch_lw<LAYOUT_BRICK16, WRAP_CLAMP>(a, early, sc, s);
-    case LAYOUT_CORNER8: return launch_march_corner8(a, early, sc, s);   // vr_march_c8.hip
+    case LAYOUT_CORNER8:
+    case LAYOUT_CORNERH: return launch_march_corner8(a, layout, early, sc, s);   // vr_march_c8.hip
     default: break;
     }
     if (wrap == WRAP_CLAMP) return launch_lw<LAYOUT_PLANAR, WRAP_CLAMP>(a, early, sc, s);

@@ -1,4 +1,4 @@
-// vr_march_c8.hip -- the CORNER8 (cache-resident volume) instantiation of
+// vr_march_c8.hip -- the CORNER8 / CORNERH (cache-resident volume) instantiations of
 // the ray march.  A separate translation unit because it is built with
 // -fno-slp-vectorize: the SLP vectoriser packs pairs of scalar lerps into
 // v_pk_* ops whose operands then need v_mov pairs; for this VALU-bound
@@ -8,8 +8,9 @@
 
 namespace vr {
 
-hipError_t launch_march_corner8(const MarchArgs& a, bool early, const Schedule& sc, hipStream_t s)
+hipError_t launch_march_corner8(const MarchArgs& a, int layout, bool early, const Schedule& sc, hipStream_t s)
 {
+    if (layout == LAYOUT_CORNERH) return launch_lw<LAYOUT_CORNERH, WRAP_CLAMP>(a, early, sc, s);
     return launch_lw<LAYOUT_CORNER8, WRAP_CLAMP>(a, early, sc, s);
 }
 

@@ -91,7 +91,18 @@ struct FastCtx {
     const unsigned* tx;
     const unsigned* ty;
     const unsigned* tz;
+    float s1x16, s2x16;   // CORNERH: 16 (nx+1), 16 (nx+1)(ny+1) (byte strides of y, z)
 };
+
+// x-lerp of one CORNERH footprint row: fma(w, b - a, a) with the f16 pair
+// {a, b - a} of dword q (a low, b - a high), converted exactly inside the
+// one v_fma_mix_f32.  Equal to the spec's fmaf(w, b - a, a) bit for bit.
+__device__ __forceinline__ float mix_lerp(float w, unsigned q)
+{
+    float r;
+    asm("v_fma_mix_f32 %0, %1, %2, %2 op_sel:[0,1,0] op_sel_hi:[0,1,1]" : "=v"(r) : "v"(w), "v"(q));
+    return r;
+}
 
 // A fast-layout tap in two parts: fetch (issue the loads, keep the weights)
 // and blend.  The pipelined march issues step i+1's fetches before blending
@@ -104,6 +115,18 @@ template <int LAYOUT>
 __device__ __forceinline__ TapRaw tap_fetch(const FastCtx& f, int ch, float gx, float gy, float gz)
 {
     TapRaw r{};
+    if constexpr (LAYOUT == LAYOUT_CORNERH) {
+        // floor(g) in fp32 and the weight g - floor(g): exact and equal to
+        // v_fract_f32 because g >= 0 here (clamp_is_exact); the byte offset
+        // 16 (a + (nx+1) b + (nx+1)(ny+1) c) is an integer below 2^28 with at
+        // most 24 significant bits, so both fmas are exact
+        const float fx = floorf(gx), fy = floorf(gy), fz = floorf(gz);
+        r.wx = gx - fx; r.wy = gy - fy; r.wz = gz - fz;
+        const unsigned off = (unsigned)fmaf(fz, f.s2x16, fmaf(fy, f.s1x16, fx * 16.0f));
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(f.rsrc[ch], off, 0, 0);
+        r.q0 = v[0]; r.q1 = v[1]; r.q2 = v[2]; r.q3 = v[3];
+        return r;
+    }
     r.wx = fract_(gx); r.wy = fract_(gy); r.wz = fract_(gz);
     const unsigned off = f.tx[cvt_flr(gx)] + f.ty[cvt_flr(gy)] + f.tz[cvt_flr(gz)];
     if constexpr (LAYOUT == LAYOUT_CORNER8) {
@@ -175,7 +198,13 @@ __device__ __forceinline__ TapRaw tap_fetch(const FastCtx& f, int ch, float gx, 
 template <int LAYOUT>
 __device__ __forceinline__ float tap_blend(const TapRaw& r)
 {
-    if constexpr (LAYOUT == LAYOUT_CORNER8) {
+    if constexpr (LAYOUT == LAYOUT_CORNERH) {
+        // rows q0 (y0,z0) q1 (y1,z0) q2 (y0,z1) q3 (y1,z1): x-lerps, then y, then z
+        const float x00 = mix_lerp(r.wx, r.q0), x10 = mix_lerp(r.wx, r.q1);
+        const float x01 = mix_lerp(r.wx, r.q2), x11 = mix_lerp(r.wx, r.q3);
+        const float y0 = lerp_(x00, x10, r.wy), y1 = lerp_(x01, x11, r.wy);
+        return lerp_(y0, y1, r.wz) * (1.0f / 255.0f);
+    } else if constexpr (LAYOUT == LAYOUT_CORNER8) {
         return blend(f2{ubyte<0>(r.q0), ubyte<0>(r.q1)}, f2{ubyte<1>(r.q0), ubyte<1>(r.q1)},
                      f2{ubyte<2>(r.q0), ubyte<2>(r.q1)}, f2{ubyte<3>(r.q0), ubyte<3>(r.q1)}, r.wx, r.wy, r.wz);
     } else if constexpr (LAYOUT == LAYOUT_BRICK5) {
@@ -347,7 +376,7 @@ template <int LAYOUT, int WRAP, bool EARLY, bool ZO = false>
 __device__ __forceinline__ unsigned march_pixel(const MarchArgs& a, const FastCtx& f, int x, int orow)
 {
     const Ray r = setup_ray(a, x, orow);
-    if constexpr (VR_PIPE && LAYOUT != LAYOUT_PLANAR && LAYOUT != LAYOUT_CORNER8) {
+    if constexpr (VR_PIPE && LAYOUT != LAYOUT_PLANAR && LAYOUT != LAYOUT_CORNER8 && LAYOUT != LAYOUT_CORNERH) {
         f2 pxy = r.pxy;
         float pz = r.pz;
         float acc = 0.0f;
@@ -637,7 +666,14 @@ template <int LAYOUT>
 __device__ __forceinline__ FastCtx fast_prologue(const MarchArgs& a, unsigned* lds)
 {
     FastCtx f{};
-    if constexpr (LAYOUT != LAYOUT_PLANAR) {
+    if constexpr (LAYOUT == LAYOUT_CORNERH) {
+        // no offset tables: the index is arithmetic (tap_fetch)
+        for (int c = 0; c < 4; ++c)
+            f.rsrc[c] = __builtin_amdgcn_make_buffer_rsrc((void*)(a.vol + (size_t)c * a.plane_stride), (short)0,
+                                                          (int)a.plane_stride, 0x00020000);
+        f.s1x16 = (float)(16 * a.geom.nbx);
+        f.s2x16 = (float)(16 * a.geom.nbx) * (float)a.geom.nby;
+    } else if constexpr (LAYOUT != LAYOUT_PLANAR) {
         for (int c = 0; c < 4; ++c)
             f.rsrc[c] = __builtin_amdgcn_make_buffer_rsrc((void*)(a.vol + (size_t)c * a.plane_stride), (short)0,
                                                           (int)a.plane_stride, 0x00020000);
@@ -1095,7 +1131,7 @@ __global__ __launch_bounds__(kThreads) void march_proc_sorted(const MarchArgs a,
 template <int L, int W>
 hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStream_t s)
 {
-    const size_t lds = L == LAYOUT_PLANAR ? 0 : (size_t)(a.nx + a.ny + a.nz + 3) * sizeof(unsigned);
+    const size_t lds = L == LAYOUT_PLANAR || L == LAYOUT_CORNERH ? 0 : (size_t)(a.nx + a.ny + a.nz + 3) * sizeof(unsigned);
     const dim3 block(kThreads);
     if (sc.kind == SCHED_STRIDED) {
         const int tiles = ((a.width + 7) >> 3) * ((a.out_rows + 7) >> 3);
@@ -1126,7 +1162,7 @@ hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStre
             hipLaunchKernelGGL((march_rings<L, W, false, false>), grid, block, lds, s, a, cx, cy, nw, npos);
         return hipGetLastError();
     }
-    if constexpr (is_b4_family(L) || L == LAYOUT_ZPAIR || L == LAYOUT_CORNER8) {
+    if constexpr (is_b4_family(L) || L == LAYOUT_ZPAIR || L == LAYOUT_CORNER8 || L == LAYOUT_CORNERH) {
         if (sc.kind == SCHED_REGIONS && sc.split > 1) {
             const dim3 grid((unsigned)(8 * ((sc.map.nwx + 3) / 4)));
             if (sc.split == 2) launch_regions_split<L, 2>(a, early, sc, grid, lds, s);

@@ -69,6 +69,22 @@ __global__ __launch_bounds__(kBlock) void k_build_layout(const uint8_t* __restri
             for (int k = 0; k < 8; ++k)
                 q |= (unsigned long long)src.at(a + (k & 1), b + ((k >> 1) & 1), c + (k >> 2)) << (8 * k);
             reinterpret_cast<unsigned long long*>(dst)[e] = q;
+        } else if constexpr (LAYOUT == LAYOUT_CORNERH) {
+            // position (a, b, c), x fastest; dword k = footprint row (y, z) =
+            // (b + (k & 1), c + (k >> 1)): f16 a in the low half, f16 (b - a)
+            // in the high half (both exact: |values| <= 255)
+            const int a = (int)(e % g.nbx);
+            const long long t = e / g.nbx;
+            const int b = (int)(t % g.nby), c = (int)(t / g.nby);
+            unsigned w[4];
+            for (int k = 0; k < 4; ++k) {
+                const int y = b + (k & 1), z = c + (k >> 1);
+                const int va = (int)src.at(a, y, z), vb = (int)src.at(a + 1, y, z);
+                const _Float16 ha = (_Float16)(float)va, hd = (_Float16)(float)(vb - va);
+                w[k] = (unsigned)__builtin_bit_cast(unsigned short, ha) |
+                       ((unsigned)__builtin_bit_cast(unsigned short, hd) << 16);
+            }
+            reinterpret_cast<uint4*>(dst)[e] = make_uint4(w[0], w[1], w[2], w[3]);
         } else if constexpr (LAYOUT == LAYOUT_ZPAIR) {
             // byte = x + 4 * (z + 2 * y): 4-byte rows, z fastest
             const long long brick = e >> 7;
@@ -228,9 +244,9 @@ long long layout_elems(int layout, int nx, int ny, int nz)
 {
     const LayoutGeom g = layout_geom(layout, nx, ny, nz);
     const long long nb = (long long)g.nbx * g.nby * g.nbz;
-    return layout == LAYOUT_CORNER8 ? nb * 64 : nb * g.brick;
+    return layout == LAYOUT_CORNER8 ? nb * 64 : layout == LAYOUT_CORNERH ? nb : nb * g.brick;
 }
-int elem_bytes(int layout) { return layout == LAYOUT_CORNER8 ? 8 : 1; }
+int elem_bytes(int layout) { return layout == LAYOUT_CORNER8 ? 8 : layout == LAYOUT_CORNERH ? 16 : 1; }
 }  // namespace
 
 size_t layout_plane_bytes(int layout, int nx, int ny, int nz)
@@ -259,6 +275,7 @@ hipError_t launch_build_layout(int layout, const uint8_t* d_planar, int nx, int 
     case LAYOUT_BRICK41616: hipLaunchKernelGGL(k_build_layout<LAYOUT_BRICK41616>, gr, b, 0, s, d_planar, nx, ny, nz, g, elems, pb, d_out); break;
     case LAYOUT_ZPAIR: hipLaunchKernelGGL(k_build_layout<LAYOUT_ZPAIR>, gr, b, 0, s, d_planar, nx, ny, nz, g, elems, pb, d_out); break;
     case LAYOUT_CORNER8: hipLaunchKernelGGL(k_build_layout<LAYOUT_CORNER8>, gr, b, 0, s, d_planar, nx, ny, nz, g, elems, pb, d_out); break;
+    case LAYOUT_CORNERH: hipLaunchKernelGGL(k_build_layout<LAYOUT_CORNERH>, gr, b, 0, s, d_planar, nx, ny, nz, g, elems, pb, d_out); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
