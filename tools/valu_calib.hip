@@ -107,6 +107,18 @@ __device__ __forceinline__ void body(float (&f)[16], unsigned (&u)[16], float s)
     if constexpr (OP == 72) asm volatile("v_cvt_f32_ubyte1 v64, v1\n\tv_cvt_f32_ubyte1 v65, v1\n\tv_cvt_f32_ubyte1 v66, v1\n\tv_cvt_f32_ubyte1 v67, v1\n\tv_cvt_f32_ubyte1 v68, v1\n\tv_cvt_f32_ubyte1 v69, v1\n\tv_cvt_f32_ubyte1 v70, v1\n\tv_cvt_f32_ubyte1 v71, v1\n\tv_cvt_f32_ubyte1 v72, v1\n\tv_cvt_f32_ubyte1 v73, v1\n\tv_cvt_f32_ubyte1 v74, v1\n\tv_cvt_f32_ubyte1 v75, v1\n\tv_cvt_f32_ubyte1 v76, v1\n\tv_cvt_f32_ubyte1 v77, v1\n\tv_cvt_f32_ubyte1 v78, v1\n\tv_cvt_f32_ubyte1 v79, v1" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
     if constexpr (OP == 73) asm volatile("v_and_b32 v64, v2, v1\n\tv_and_b32 v65, v2, v1\n\tv_and_b32 v66, v2, v1\n\tv_and_b32 v67, v2, v1\n\tv_and_b32 v68, v2, v1\n\tv_and_b32 v69, v2, v1\n\tv_and_b32 v70, v2, v1\n\tv_and_b32 v71, v2, v1\n\tv_and_b32 v72, v2, v1\n\tv_and_b32 v73, v2, v1\n\tv_and_b32 v74, v2, v1\n\tv_and_b32 v75, v2, v1\n\tv_and_b32 v76, v2, v1\n\tv_and_b32 v77, v2, v1\n\tv_and_b32 v78, v2, v1\n\tv_and_b32 v79, v2, v1" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
     if constexpr (OP == 74) asm volatile("v_fma_mix_f32 v64, v1, v2, v3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v65, v1, v2, v3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v66, v1, v2, v3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v67, v1, v2, v3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v68, v1, v2, v3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v69, v1, v2, v3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v70, v1, v2, v3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v71, v1, v2, v3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v72, v1, v2, v3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v73, v1, v2, v3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v74, v1, v2, v3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v75, v1, v2, v3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v76, v1, v2, v3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v77, v1, v2, v3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v78, v1, v2, v3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\tv_fma_mix_f32 v79, v1, v2, v3 op_sel:[0,0,1] op_sel_hi:[0,0,1]" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
+    if constexpr (OP == 75) asm volatile("v_lshlrev_b32 v64, 4, v1\n\tv_lshlrev_b32 v65, 4, v1\n\tv_lshlrev_b32 v66, 4, v1\n\tv_lshlrev_b32 v67, 4, v1\n\tv_lshlrev_b32 v68, 4, v1\n\tv_lshlrev_b32 v69, 4, v1\n\tv_lshlrev_b32 v70, 4, v1\n\tv_lshlrev_b32 v71, 4, v1\n\tv_lshlrev_b32 v72, 4, v1\n\tv_lshlrev_b32 v73, 4, v1\n\tv_lshlrev_b32 v74, 4, v1\n\tv_lshlrev_b32 v75, 4, v1\n\tv_lshlrev_b32 v76, 4, v1\n\tv_lshlrev_b32 v77, 4, v1\n\tv_lshlrev_b32 v78, 4, v1\n\tv_lshlrev_b32 v79, 4, v1" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
+    if constexpr (OP == 76) asm volatile("v_lshlrev_b32 v64, v2, v1\n\tv_lshlrev_b32 v65, v2, v1\n\tv_lshlrev_b32 v66, v2, v1\n\tv_lshlrev_b32 v67, v2, v1\n\tv_lshlrev_b32 v68, v2, v1\n\tv_lshlrev_b32 v69, v2, v1\n\tv_lshlrev_b32 v70, v2, v1\n\tv_lshlrev_b32 v71, v2, v1\n\tv_lshlrev_b32 v72, v2, v1\n\tv_lshlrev_b32 v73, v2, v1\n\tv_lshlrev_b32 v74, v2, v1\n\tv_lshlrev_b32 v75, v2, v1\n\tv_lshlrev_b32 v76, v2, v1\n\tv_lshlrev_b32 v77, v2, v1\n\tv_lshlrev_b32 v78, v2, v1\n\tv_lshlrev_b32 v79, v2, v1" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
+    if constexpr (OP == 77) asm volatile("v_ashrrev_i32 v64, 4, v1\n\tv_ashrrev_i32 v65, 4, v1\n\tv_ashrrev_i32 v66, 4, v1\n\tv_ashrrev_i32 v67, 4, v1\n\tv_ashrrev_i32 v68, 4, v1\n\tv_ashrrev_i32 v69, 4, v1\n\tv_ashrrev_i32 v70, 4, v1\n\tv_ashrrev_i32 v71, 4, v1\n\tv_ashrrev_i32 v72, 4, v1\n\tv_ashrrev_i32 v73, 4, v1\n\tv_ashrrev_i32 v74, 4, v1\n\tv_ashrrev_i32 v75, 4, v1\n\tv_ashrrev_i32 v76, 4, v1\n\tv_ashrrev_i32 v77, 4, v1\n\tv_ashrrev_i32 v78, 4, v1\n\tv_ashrrev_i32 v79, 4, v1" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
+    if constexpr (OP == 78) asm volatile("v_cmp_lt_f32 vcc, v1, v64\n\tv_cndmask_b32 v64, v1, v2, vcc\n\tv_cmp_lt_f32 vcc, v1, v65\n\tv_cndmask_b32 v65, v1, v2, vcc\n\tv_cmp_lt_f32 vcc, v1, v66\n\tv_cndmask_b32 v66, v1, v2, vcc\n\tv_cmp_lt_f32 vcc, v1, v67\n\tv_cndmask_b32 v67, v1, v2, vcc\n\tv_cmp_lt_f32 vcc, v1, v68\n\tv_cndmask_b32 v68, v1, v2, vcc\n\tv_cmp_lt_f32 vcc, v1, v69\n\tv_cndmask_b32 v69, v1, v2, vcc\n\tv_cmp_lt_f32 vcc, v1, v70\n\tv_cndmask_b32 v70, v1, v2, vcc\n\tv_cmp_lt_f32 vcc, v1, v71\n\tv_cndmask_b32 v71, v1, v2, vcc\n\tv_cmp_lt_f32 vcc, v1, v72\n\tv_cndmask_b32 v72, v1, v2, vcc\n\tv_cmp_lt_f32 vcc, v1, v73\n\tv_cndmask_b32 v73, v1, v2, vcc\n\tv_cmp_lt_f32 vcc, v1, v74\n\tv_cndmask_b32 v74, v1, v2, vcc\n\tv_cmp_lt_f32 vcc, v1, v75\n\tv_cndmask_b32 v75, v1, v2, vcc\n\tv_cmp_lt_f32 vcc, v1, v76\n\tv_cndmask_b32 v76, v1, v2, vcc\n\tv_cmp_lt_f32 vcc, v1, v77\n\tv_cndmask_b32 v77, v1, v2, vcc\n\tv_cmp_lt_f32 vcc, v1, v78\n\tv_cndmask_b32 v78, v1, v2, vcc\n\tv_cmp_lt_f32 vcc, v1, v79\n\tv_cndmask_b32 v79, v1, v2, vcc" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
+    if constexpr (OP == 79) asm volatile("v_cmp_lt_f32 s[40:41], v1, v64\n\tv_cndmask_b32_e64 v64, v1, v2, s[40:41]\n\tv_cmp_lt_f32 s[40:41], v1, v65\n\tv_cndmask_b32_e64 v65, v1, v2, s[40:41]\n\tv_cmp_lt_f32 s[40:41], v1, v66\n\tv_cndmask_b32_e64 v66, v1, v2, s[40:41]\n\tv_cmp_lt_f32 s[40:41], v1, v67\n\tv_cndmask_b32_e64 v67, v1, v2, s[40:41]\n\tv_cmp_lt_f32 s[40:41], v1, v68\n\tv_cndmask_b32_e64 v68, v1, v2, s[40:41]\n\tv_cmp_lt_f32 s[40:41], v1, v69\n\tv_cndmask_b32_e64 v69, v1, v2, s[40:41]\n\tv_cmp_lt_f32 s[40:41], v1, v70\n\tv_cndmask_b32_e64 v70, v1, v2, s[40:41]\n\tv_cmp_lt_f32 s[40:41], v1, v71\n\tv_cndmask_b32_e64 v71, v1, v2, s[40:41]\n\tv_cmp_lt_f32 s[40:41], v1, v72\n\tv_cndmask_b32_e64 v72, v1, v2, s[40:41]\n\tv_cmp_lt_f32 s[40:41], v1, v73\n\tv_cndmask_b32_e64 v73, v1, v2, s[40:41]\n\tv_cmp_lt_f32 s[40:41], v1, v74\n\tv_cndmask_b32_e64 v74, v1, v2, s[40:41]\n\tv_cmp_lt_f32 s[40:41], v1, v75\n\tv_cndmask_b32_e64 v75, v1, v2, s[40:41]\n\tv_cmp_lt_f32 s[40:41], v1, v76\n\tv_cndmask_b32_e64 v76, v1, v2, s[40:41]\n\tv_cmp_lt_f32 s[40:41], v1, v77\n\tv_cndmask_b32_e64 v77, v1, v2, s[40:41]\n\tv_cmp_lt_f32 s[40:41], v1, v78\n\tv_cndmask_b32_e64 v78, v1, v2, s[40:41]\n\tv_cmp_lt_f32 s[40:41], v1, v79\n\tv_cndmask_b32_e64 v79, v1, v2, s[40:41]" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
+    if constexpr (OP == 80) asm volatile("v_sub_u32 v64, v1, v2\n\tv_sub_u32 v65, v1, v2\n\tv_sub_u32 v66, v1, v2\n\tv_sub_u32 v67, v1, v2\n\tv_sub_u32 v68, v1, v2\n\tv_sub_u32 v69, v1, v2\n\tv_sub_u32 v70, v1, v2\n\tv_sub_u32 v71, v1, v2\n\tv_sub_u32 v72, v1, v2\n\tv_sub_u32 v73, v1, v2\n\tv_sub_u32 v74, v1, v2\n\tv_sub_u32 v75, v1, v2\n\tv_sub_u32 v76, v1, v2\n\tv_sub_u32 v77, v1, v2\n\tv_sub_u32 v78, v1, v2\n\tv_sub_u32 v79, v1, v2" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
+    if constexpr (OP == 81) asm volatile("v_bfi_b32 v64, v1, v2, v3\n\tv_bfi_b32 v65, v1, v2, v3\n\tv_bfi_b32 v66, v1, v2, v3\n\tv_bfi_b32 v67, v1, v2, v3\n\tv_bfi_b32 v68, v1, v2, v3\n\tv_bfi_b32 v69, v1, v2, v3\n\tv_bfi_b32 v70, v1, v2, v3\n\tv_bfi_b32 v71, v1, v2, v3\n\tv_bfi_b32 v72, v1, v2, v3\n\tv_bfi_b32 v73, v1, v2, v3\n\tv_bfi_b32 v74, v1, v2, v3\n\tv_bfi_b32 v75, v1, v2, v3\n\tv_bfi_b32 v76, v1, v2, v3\n\tv_bfi_b32 v77, v1, v2, v3\n\tv_bfi_b32 v78, v1, v2, v3\n\tv_bfi_b32 v79, v1, v2, v3" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
+    if constexpr (OP == 82) asm volatile("v_mul_f32 v64, 0x3b808081, v1\n\tv_mul_f32 v65, 0x3b808081, v1\n\tv_mul_f32 v66, 0x3b808081, v1\n\tv_mul_f32 v67, 0x3b808081, v1\n\tv_mul_f32 v68, 0x3b808081, v1\n\tv_mul_f32 v69, 0x3b808081, v1\n\tv_mul_f32 v70, 0x3b808081, v1\n\tv_mul_f32 v71, 0x3b808081, v1\n\tv_mul_f32 v72, 0x3b808081, v1\n\tv_mul_f32 v73, 0x3b808081, v1\n\tv_mul_f32 v74, 0x3b808081, v1\n\tv_mul_f32 v75, 0x3b808081, v1\n\tv_mul_f32 v76, 0x3b808081, v1\n\tv_mul_f32 v77, 0x3b808081, v1\n\tv_mul_f32 v78, 0x3b808081, v1\n\tv_mul_f32 v79, 0x3b808081, v1" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
+    if constexpr (OP == 83) asm volatile("v_pk_add_f32 v[64:65], v[2:3], v[4:5]\n\tv_pk_add_f32 v[66:67], v[2:3], v[4:5]\n\tv_pk_add_f32 v[68:69], v[2:3], v[4:5]\n\tv_pk_add_f32 v[70:71], v[2:3], v[4:5]\n\tv_pk_add_f32 v[72:73], v[2:3], v[4:5]\n\tv_pk_add_f32 v[74:75], v[2:3], v[4:5]\n\tv_pk_add_f32 v[76:77], v[2:3], v[4:5]\n\tv_pk_add_f32 v[78:79], v[2:3], v[4:5]" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
+    if constexpr (OP == 84) asm volatile("v_xad_u32 v64, v1, v2, v3\n\tv_xad_u32 v65, v1, v2, v3\n\tv_xad_u32 v66, v1, v2, v3\n\tv_xad_u32 v67, v1, v2, v3\n\tv_xad_u32 v68, v1, v2, v3\n\tv_xad_u32 v69, v1, v2, v3\n\tv_xad_u32 v70, v1, v2, v3\n\tv_xad_u32 v71, v1, v2, v3\n\tv_xad_u32 v72, v1, v2, v3\n\tv_xad_u32 v73, v1, v2, v3\n\tv_xad_u32 v74, v1, v2, v3\n\tv_xad_u32 v75, v1, v2, v3\n\tv_xad_u32 v76, v1, v2, v3\n\tv_xad_u32 v77, v1, v2, v3\n\tv_xad_u32 v78, v1, v2, v3\n\tv_xad_u32 v79, v1, v2, v3" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
+    if constexpr (OP == 85) asm volatile("v_fmaak_f32 v64, v1, v2, 0x41200000\n\tv_fmaak_f32 v65, v1, v2, 0x41200000\n\tv_fmaak_f32 v66, v1, v2, 0x41200000\n\tv_fmaak_f32 v67, v1, v2, 0x41200000\n\tv_fmaak_f32 v68, v1, v2, 0x41200000\n\tv_fmaak_f32 v69, v1, v2, 0x41200000\n\tv_fmaak_f32 v70, v1, v2, 0x41200000\n\tv_fmaak_f32 v71, v1, v2, 0x41200000\n\tv_fmaak_f32 v72, v1, v2, 0x41200000\n\tv_fmaak_f32 v73, v1, v2, 0x41200000\n\tv_fmaak_f32 v74, v1, v2, 0x41200000\n\tv_fmaak_f32 v75, v1, v2, 0x41200000\n\tv_fmaak_f32 v76, v1, v2, 0x41200000\n\tv_fmaak_f32 v77, v1, v2, 0x41200000\n\tv_fmaak_f32 v78, v1, v2, 0x41200000\n\tv_fmaak_f32 v79, v1, v2, 0x41200000" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
+    if constexpr (OP == 86) asm volatile("v_cvt_u32_f32 v64, v1\n\tv_cvt_u32_f32 v65, v1\n\tv_cvt_u32_f32 v66, v1\n\tv_cvt_u32_f32 v67, v1\n\tv_cvt_u32_f32 v68, v1\n\tv_cvt_u32_f32 v69, v1\n\tv_cvt_u32_f32 v70, v1\n\tv_cvt_u32_f32 v71, v1\n\tv_cvt_u32_f32 v72, v1\n\tv_cvt_u32_f32 v73, v1\n\tv_cvt_u32_f32 v74, v1\n\tv_cvt_u32_f32 v75, v1\n\tv_cvt_u32_f32 v76, v1\n\tv_cvt_u32_f32 v77, v1\n\tv_cvt_u32_f32 v78, v1\n\tv_cvt_u32_f32 v79, v1" ::: "v64","v65","v66","v67","v68","v69","v70","v71","v72","v73","v74","v75","v76","v77","v78","v79", "v1","v2","v3","s40","s41","s42","s43","s44","s45","s46","s47","vcc");
     if constexpr (OP == 0) { R16(FMA) }
     if constexpr (OP == 1) { R16(MUL) }
     if constexpr (OP == 2) { R16(MULLO) }
@@ -242,6 +254,18 @@ int main()
     run<72>("cvt_ubyte1", 1, cus, out, clk);
     run<73>("and_b32", 1, cus, out, clk);
     run<74>("fma_mix_hi", 1, cus, out, clk);
+    run<75>("lshlrev_4", 1, cus, out, clk);
+    run<76>("lshlrev_vgpr", 1, cus, out, clk);
+    run<77>("ashrrev_4", 1, cus, out, clk);
+    run<78>("cmp+cnd_vcc", 2, cus, out, clk);
+    run<79>("cmp+cnd_sgpr", 2, cus, out, clk);
+    run<80>("sub_u32", 1, cus, out, clk);
+    run<81>("bfi_b32", 1, cus, out, clk);
+    run<82>("mul_literal", 1, cus, out, clk);
+    run<83>("pk_add_vv", 0.5, cus, out, clk);
+    run<84>("xad_u32", 1, cus, out, clk);
+    run<85>("fmaak_lit", 1, cus, out, clk);
+    run<86>("cvt_u32_f32", 1, cus, out, clk);
     run<62>("mullo_sgpr", 1, cus, out, clk);
     run<63>("and_b32", 1, cus, out, clk);
     run<64>("or_b32", 1, cus, out, clk);

@@ -337,6 +337,29 @@ vr_status vr_procedural_defaults(vr_procedural* p)
 
 constexpr long long kMaxWorleyTableBytes = 32 << 10;   // LDS per workgroup for the cell table
 
+// z pitch of the Worley cell table (entries): the smallest pz >= n*n for which
+// no two cells at most one apart on each axis share a ds_read_b128 bank slot
+// (index mod 16), fewest aliases among cells two apart.  The lanes of a sorted
+// wave sit in neighbouring cells; with pz = n*n (81 = 1 mod 16) cells
+// (x+1, y, z-1) and (x, y, z) collide.
+int worley_z_pitch(int n)
+{
+    int best = n * n, best_al = 1 << 30;
+    for (int pz = n * n; pz < n * n + 16; ++pz) {
+        int al1 = 0, al2 = 0;
+        for (int dz = -2; dz <= 2; ++dz)
+            for (int dy = -2; dy <= 2; ++dy)
+                for (int dx = -2; dx <= 2; ++dx) {
+                    if (!dx && !dy && !dz) continue;
+                    if (((dx + n * dy + pz * dz) % 16 + 16) % 16) continue;
+                    (std::abs(dx) <= 1 && std::abs(dy) <= 1 && std::abs(dz) <= 1 ? al1 : al2) += 1;
+                }
+        const int score = al1 * 1000 + al2;
+        if (score < best_al) { best_al = score; best = pz; }
+    }
+    return best;
+}
+
 vr_status vr_set_procedural(void* ctx, const vr_procedural* p)
 {
     if (!ctx || !p) return fail(VR_ERR_INVALID, "vr_set_procedural: null argument");
@@ -911,9 +934,13 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
         // 3x3x3 neighbourhood of rint() of those, with 2 cells of margin.
         const double G = (double)q.grid_scale * (double)q.worley_freq;
         const int lo = (int)std::floor(std::min(0.0, G)) - 2, hi = (int)std::ceil(std::max(0.0, G)) + 2;
-        const int n = hi - lo + 1;
+        const bool small = std::fabs(G) < 64.0;
+        int n = small ? hi - lo + 1 : 0;
+        q.wt_fixed = small && n <= 9;   // kernels' fixed geometry (noise::kWorleyN / kWorleyPz)
+        if (q.wt_fixed) n = 9;          // a superset of the cells needed
         q.wt_lo = lo;
-        q.wt_n = (std::fabs(G) < 64.0 && (long long)n * n * n * 16 <= kMaxWorleyTableBytes) ? n : 0;   // + 8 KiB pairs
+        q.wt_pz = q.wt_fixed ? 83 : small ? worley_z_pitch(n) : 0;
+        q.wt_n = (small && (long long)n * q.wt_pz * 16 <= kMaxWorleyTableBytes) ? n : 0;   // + 8 KiB pairs
     }
     Plan pl{LAYOUT_PLANAR, WRAP_CLAMP, false};
     if (!c->proc.enabled) make_plan(c, &a, &pl);
@@ -948,8 +975,9 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
         void* sort_buf = nullptr;
         Schedule sc{c->schedule == SCHED_RINGS ? SCHED_RINGS : SCHED_STATIC, 0, 0, 1, 1, nullptr, nullptr, {}, 1};
         if (sc.kind == SCHED_RINGS) box_centre_pixel(c, a, &sc.center_x, &sc.center_y);
+        // the sort passes enumerate whole 64x64 regions (vr_march_kernels.h sort_pixel)
         if (c->schedule != SCHED_STATIC && c->schedule != SCHED_RINGS && a.width < 65536 && a.out_rows < 65536 &&
-            (long long)a.width * a.out_rows < (1ll << 31)) {
+            (long long)((a.width + 63) / 64) * ((a.out_rows + 63) / 64) * 4096 < (1ll << 31)) {
             const size_t need = proc_sort_bytes(a.width, a.out_rows);
             if (need > c->sort_bytes) {
                 // the old buffer may still be read by queued work on another stream

@@ -131,6 +131,8 @@ struct ProcParams {
     float od;         // step_size * density
     int count_evals;  // step_counter counts density evaluations (incl. shadow samples)
     int wt_lo, wt_n;  // Worley cell table in LDS: cells [wt_lo, wt_lo + wt_n)^3; wt_n = 0: none
+    int wt_pz;        // its z pitch in entries (>= wt_n^2, padded against LDS bank aliasing)
+    int wt_fixed;     // 1: the fixed geometry wt_n = 9, wt_pz = 83 (noise::cellular_table9)
 };
 
 // Everything one launch of the march kernel needs.  Passed by value

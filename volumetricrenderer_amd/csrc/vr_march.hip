@@ -16,8 +16,11 @@ namespace vr {
 
 size_t proc_sort_bytes(int width, int out_rows)
 {
-    // hist, cursor (+ total), order (u32 per pixel), keys (u16 per pixel)
-    return (size_t)(2 * kKeyBins + 64) * sizeof(unsigned) + (size_t)width * (size_t)out_rows * 6u;
+    // hist, cursor (+ total), order (u32 per pixel), keys (u16 per enumerated
+    // position: whole 64x64 regions, kSortRegion)
+    const size_t regions = (size_t)((width + kSortRegion - 1) / kSortRegion) * ((out_rows + kSortRegion - 1) / kSortRegion);
+    return (size_t)(2 * kKeyBins + 64) * sizeof(unsigned) + (size_t)width * (size_t)out_rows * 4u +
+           regions * kSortRegion * kSortRegion * 2u;
 }
 
 hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_buf, const Schedule& sc, hipStream_t s)
@@ -25,7 +28,7 @@ hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_bu
     if (a.width <= 0 || a.out_rows <= 0) return hipSuccess;
     const bool shadow = a.proc.shadow_steps > 0;
     const size_t wt_bytes =
-        a.proc.wt_n > 0 ? ((size_t)a.proc.wt_n * a.proc.wt_n * a.proc.wt_n + 512) * sizeof(float4) : 0;
+        a.proc.wt_n > 0 ? ((size_t)a.proc.wt_n * a.proc.wt_pz + 512) * sizeof(float4) : 0;
     if (sort_buf) {
         unsigned* hist = static_cast<unsigned*>(sort_buf);
         unsigned* cursor = hist + kKeyBins;            // kKeyBins + 1 entries
@@ -34,7 +37,8 @@ hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_bu
         // hist is all zero here: zeroed when the buffer was allocated, and by
         // the previous frame's proc_scan after it read it
         const long long pixels = (long long)a.width * a.out_rows;
-        const dim3 g1((unsigned)((pixels + 256 * kSortPixelsPerThread - 1) / (256 * kSortPixelsPerThread)));
+        static_assert(kSortRegion * kSortRegion == 256 * kSortPixelsPerThread, "one 64x64 region per sort block");
+        const dim3 g1((unsigned)(((a.width + kSortRegion - 1) / kSortRegion) * ((a.out_rows + kSortRegion - 1) / kSortRegion)));
         if (shadow) hipLaunchKernelGGL((proc_bin<true>), g1, dim3(256), 0, s, a, hist, keys);
         else hipLaunchKernelGGL((proc_bin<false>), g1, dim3(256), 0, s, a, hist, keys);
         hipLaunchKernelGGL(proc_scan, dim3(1), dim3(kKeyBins), 0, s, hist, cursor);
@@ -42,18 +46,21 @@ hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_bu
         // the scatter advanced cursor[k] to the end of key k; total stays at cursor[kKeyBins]
         const dim3 g4((unsigned)((pixels + kThreads - 1) / kThreads));
         const unsigned* total = cursor + kKeyBins;
-        const int v = (shadow ? 4 : 0) | (early ? 2 : 0) | (wt_bytes ? 1 : 0);
+        // tables: 2 = the fixed 9-cell Worley geometry (compile-time offsets), 1 = runtime geometry
+        const int tm = wt_bytes ? (a.proc.wt_fixed ? 2 : 1) : 0;
+        const int v = (shadow ? 4 : 0) | (early ? 2 : 0);
 #define VR_PS(S, E, T) hipLaunchKernelGGL((march_proc_sorted<S, E, T>), g4, dim3(kThreads), wt_bytes, s, a, order, total)
+#define VR_PS3(S, E) \
+    if (tm == 2) VR_PS(S, E, 2); \
+    else if (tm == 1) VR_PS(S, E, 1); \
+    else VR_PS(S, E, 0)
         switch (v) {
-        case 0: VR_PS(false, false, false); break;
-        case 1: VR_PS(false, false, true); break;
-        case 2: VR_PS(false, true, false); break;
-        case 3: VR_PS(false, true, true); break;
-        case 4: VR_PS(true, false, false); break;
-        case 5: VR_PS(true, false, true); break;
-        case 6: VR_PS(true, true, false); break;
-        default: VR_PS(true, true, true); break;
+        case 0: VR_PS3(false, false); break;
+        case 2: VR_PS3(false, true); break;
+        case 4: VR_PS3(true, false); break;
+        default: VR_PS3(true, true); break;
         }
+#undef VR_PS3
 #undef VR_PS
         return hipGetLastError();
     }
@@ -67,17 +74,18 @@ hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_bu
         waves = (2ll * R + 1) * (2ll * R + 1);
     }
     const dim3 grid((unsigned)((waves + 3) / 4)), block(kThreads);
+    // the fixed geometry is also a valid runtime geometry (n = 9, pz = 83)
     const int v = (shadow ? 4 : 0) | (early ? 2 : 0) | (wt_bytes ? 1 : 0);
 #define VR_PT(S, E, T) hipLaunchKernelGGL((march_proc<S, E, T>), grid, block, wt_bytes, s, a, cx, cy)
     switch (v) {
-    case 0: VR_PT(false, false, false); break;
-    case 1: VR_PT(false, false, true); break;
-    case 2: VR_PT(false, true, false); break;
-    case 3: VR_PT(false, true, true); break;
-    case 4: VR_PT(true, false, false); break;
-    case 5: VR_PT(true, false, true); break;
-    case 6: VR_PT(true, true, false); break;
-    default: VR_PT(true, true, true); break;
+    case 0: VR_PT(false, false, 0); break;
+    case 1: VR_PT(false, false, 1); break;
+    case 2: VR_PT(false, true, 0); break;
+    case 3: VR_PT(false, true, 1); break;
+    case 4: VR_PT(true, false, 0); break;
+    case 5: VR_PT(true, false, 1); break;
+    case 6: VR_PT(true, true, 0); break;
+    default: VR_PT(true, true, 1); break;
     }
 #undef VR_PT
     return hipGetLastError();

@@ -443,25 +443,30 @@ __device__ __forceinline__ unsigned march_pixel(const MarchArgs& a, const FastCt
 
 // Procedural medium (BASELINE configs 2/3, build-defined; spec in
 // oracle/vr_oracle.h vro_procedural): fBm Perlin x (1 - Worley F1).
-template <bool TABLE>
+// TABLE: 0 = direct noise, 1 = LDS tables with runtime Worley geometry,
+// 2 = LDS tables with the fixed 9-cell geometry (noise::cellular_table9)
+template <int TABLE>
 __device__ __forceinline__ float proc_density(const ProcParams& p, const float4* wt, float scale, float px, float py,
                                               float pz)
 {
-    const float qx = px * p.grid_scale, qy = py * p.grid_scale, qz = pz * p.grid_scale;
-    float f = p.freq0, amp = 1.0f, fbm = 0.0f;
+    const float gs = noise::in_vgpr(p.grid_scale), lac = noise::in_vgpr(p.lacunarity), gain = noise::in_vgpr(p.gain);
+    const float qx = px * gs, qy = py * gs, qz = pz * gs;
+    float f = noise::in_vgpr(p.freq0), amp = 1.0f, fbm = 0.0f;
     for (int o = 0; o < p.octaves; ++o) {
         float pn;
-        if constexpr (TABLE) pn = noise::perlin_gp(wt + p.wt_n * p.wt_n * p.wt_n, p.seed_fbm, qx * f, qy * f, qz * f);
+        if constexpr (TABLE == 2) pn = noise::perlin_gp(wt + noise::kWorleyN * noise::kWorleyPz, p.seed_fbm, qx * f, qy * f, qz * f);
+        else if constexpr (TABLE == 1) pn = noise::perlin_gp(wt + p.wt_n * p.wt_pz, p.seed_fbm, qx * f, qy * f, qz * f);
         else pn = noise::perlin(p.seed_fbm, qx * f, qy * f, qz * f);
         fbm = fmaf(amp, pn, fbm);
-        f = f * p.lacunarity;
-        amp = amp * p.gain;
+        f = f * lac;
+        amp = amp * gain;
     }
-    const float wf = p.worley_freq;
+    const float wf = noise::in_vgpr(p.worley_freq);
     float f1;
-    if constexpr (TABLE) f1 = noise::cellular_table(wt, p.wt_lo, p.wt_n, qx * wf, qy * wf, qz * wf) + 1.0f;
+    if constexpr (TABLE == 2) f1 = noise::cellular_table9(wt, p.wt_lo, qx * wf, qy * wf, qz * wf) + 1.0f;
+    else if constexpr (TABLE == 1) f1 = noise::cellular_table(wt, p.wt_lo, p.wt_n, p.wt_pz, qx * wf, qy * wf, qz * wf) + 1.0f;
     else f1 = noise::cellular(p.seed_worley, qx * wf, qy * wf, qz * wf) + 1.0f;
-    return fmaxf(fbm * (1.0f - f1), 0.0f) * scale;
+    return fmaxf(fbm * (1.0f - f1), 0.0f) * noise::in_vgpr(scale);
 }
 
 // Pixel value of the procedural march: single scatter, or frag.glsl:76-80.
@@ -476,7 +481,7 @@ __device__ __forceinline__ float proc_epilogue(const MarchArgs& a, float acc, fl
     }
 }
 
-template <bool SHADOW, bool EARLY, bool TABLE>
+template <bool SHADOW, bool EARLY, int TABLE>
 __device__ __forceinline__ unsigned march_pixel_proc(const MarchArgs& a, const float4* wt, int x, int orow)
 {
     const Ray r = setup_ray(a, x, orow);
@@ -530,7 +535,7 @@ struct ShadowLds {
     };
 };
 
-template <bool EARLY, bool TABLE>
+template <bool EARLY, int TABLE>
 __device__ __forceinline__ unsigned march_pixel_proc_compact(const MarchArgs& a, const float4* wt, int x, int orow,
                                                              bool valid,
                                                              ShadowLds* sh, unsigned* shadow_evals)
@@ -966,24 +971,27 @@ __global__ __launch_bounds__(kThreads) void march_queue(const MarchArgs a, int* 
 // (wt_n^3 float4) followed by the 256 Perlin gradient pairs (2 float4 each),
 // built before any wave may leave.  Returns null when the tables are off
 // (wt_n = 0).
+template <int TABLE>
 __device__ __forceinline__ const float4* worley_table(const ProcParams& p, float4* lds)
 {
-    if (p.wt_n <= 0) return nullptr;
-    const int n = p.wt_n, cells = n * n * n;
-    for (int i = threadIdx.x; i < cells; i += kThreads) {
+    // TABLE > 0 only when the host sized the tables (wt_n > 0): the returned
+    // pointer is the LDS symbol itself, so table reads fold its address
+    if constexpr (TABLE == 0) return nullptr;
+    const int n = p.wt_n, cells = n * p.wt_pz;   // z pitch wt_pz >= n * n
+    for (int i = threadIdx.x; i < n * n * n; i += kThreads) {
         const int ix = i % n, iy = (i / n) % n, iz = i / (n * n);
-        lds[i] = noise::cellular_cell(p.seed_worley, p.wt_lo + ix, p.wt_lo + iy, p.wt_lo + iz);
+        lds[iz * p.wt_pz + iy * n + ix] = noise::cellular_cell(p.seed_worley, p.wt_lo + ix, p.wt_lo + iy, p.wt_lo + iz);
     }
-    noise::grad_pair_entry(threadIdx.x, lds + cells + 2 * threadIdx.x);   // 256 pairs, one per thread
+    noise::grad_pair_entry(threadIdx.x, lds + cells);   // 256 pairs, one per thread
     __syncthreads();
     return lds;
 }
 
-template <bool SHADOW, bool EARLY, bool TABLE>
+template <bool SHADOW, bool EARLY, int TABLE>
 __global__ __launch_bounds__(kThreads) void march_proc(const MarchArgs a, int cx, int cy)
 {
     extern __shared__ float4 wt_lds[];
-    const float4* wt = worley_table(a.proc, wt_lds);
+    const float4* wt = worley_table<TABLE>(a.proc, wt_lds);
     const int lane = threadIdx.x & 63;
     const int t = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
     const int tiles_x8 = (a.width + 7) >> 3, rows8 = (a.out_rows + 7) >> 3;
@@ -1015,6 +1023,29 @@ constexpr int kKeyBins = 1024;
 // slower than the plain LDS atomics.
 constexpr int kSortPixelsPerThread = 16;
 __device__ __forceinline__ int cost_key(int n) { return n < kKeyBins - 1 ? n : kKeyBins - 1; }
+// The sort passes enumerate pixels by 64x64 regions (one region per block of
+// 256 threads x 16 pixels), regions in row-major order.  A key's pixels then
+// come out region by region, so the 64 lanes of a sorted wave are one compact
+// segment of the n-contour instead of pixels from both sides of the ring
+// (row-major enumeration): neighbouring rays share Worley cells and Perlin
+// corners, so their LDS table reads broadcast instead of conflicting (config
+// 2: 9 % faster together with the fixed table geometry).  With shadow rays
+// (config 3) row-major order is kept: there compact waves are all-or-nothing
+// in shadow work, which the per-wave compaction balances worse (4 % slower).
+constexpr int kSortRegion = 64;
+__device__ __forceinline__ bool sort_pixel(const MarchArgs& a, unsigned idx, int* x, int* orow)
+{
+    if (a.proc.shadow_steps > 0) {
+        *orow = (int)(idx / (unsigned)a.width);
+        *x = (int)(idx - (unsigned)*orow * (unsigned)a.width);
+        return *orow < a.out_rows;
+    }
+    const unsigned rx = (unsigned)(a.width + kSortRegion - 1) / kSortRegion;
+    const unsigned reg = idx / (kSortRegion * kSortRegion), loc = idx % (kSortRegion * kSortRegion);
+    *x = (int)((reg % rx) * kSortRegion + loc % kSortRegion);
+    *orow = (int)((reg / rx) * kSortRegion + loc / kSortRegion);
+    return *x < a.width && *orow < a.out_rows;
+}
 
 template <bool SHADOW>
 __global__ __launch_bounds__(256) void proc_bin(const MarchArgs a, unsigned* __restrict__ hist,
@@ -1025,8 +1056,11 @@ __global__ __launch_bounds__(256) void proc_bin(const MarchArgs a, unsigned* __r
     __syncthreads();
     for (int it = 0; it < kSortPixelsPerThread; ++it) {
         const unsigned pix = (blockIdx.x * kSortPixelsPerThread + it) * 256u + threadIdx.x;   // < 2^31 (host check)
-        const int orow = (int)(pix / (unsigned)a.width), x = (int)(pix - (unsigned)orow * (unsigned)a.width);
-        if (orow >= a.out_rows) break;
+        int x, orow;
+        if (!sort_pixel(a, pix, &x, &orow)) {
+            keys[pix] = 0;
+            continue;
+        }
         const Ray r = setup_ray(a, x, orow);
         int key = 0;
         if (r.n > 0) {
@@ -1076,8 +1110,8 @@ __global__ __launch_bounds__(256) void proc_bin(const MarchArgs a, unsigned* __r
     for (int it = 0; it < kSortPixelsPerThread; ++it) {
         key[it] = -1;
         const unsigned pix = (blockIdx.x * kSortPixelsPerThread + it) * 256u + threadIdx.x;
-        const int orow = (int)(pix / (unsigned)a.width), x = (int)(pix - (unsigned)orow * (unsigned)a.width);
-        if (orow < a.out_rows) {
+        int x, orow;
+        if (sort_pixel(a, pix, &x, &orow)) {
             const int k = keys[pix];
             if (k > 0) {
                 key[it] = k;
@@ -1094,12 +1128,12 @@ __global__ __launch_bounds__(256) void proc_bin(const MarchArgs a, unsigned* __r
         if (key[it] >= 0) order[h[key[it]] + rank[it]] = packed[it];
 }
 
-template <bool SHADOW, bool EARLY, bool TABLE>
+template <bool SHADOW, bool EARLY, int TABLE>
 __global__ __launch_bounds__(kThreads) void march_proc_sorted(const MarchArgs a, const unsigned* __restrict__ order,
                                                               const unsigned* __restrict__ total_ptr)
 {
     extern __shared__ float4 wt_lds[];
-    const float4* wt = worley_table(a.proc, wt_lds);
+    const float4* wt = worley_table<TABLE>(a.proc, wt_lds);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const unsigned total = *total_ptr;
     const unsigned base = (blockIdx.x * (kThreads / 64) + wave) * 64u;

@@ -81,24 +81,46 @@ __device__ __forceinline__ float4 grad_entry(int k)
 }
 // perlin_gp: the two x-neighbour corners of each (y, z) edge are done
 // together in packed math: a 256-entry table of gradient PAIRS, entry
-// ka | kb << 4 = {gx_a, gx_b, gy_a, gy_b} {gz_a, gz_b, 0, 0} (32 B), so
-// one b128 + one b64 read yields register pairs that feed v_pk_mul /
-// v_pk_fma directly: 3 packed ops per corner pair.  A packed fma is two
-// IEEE fmas.  Per octave 114 VALU + 8 LDS reads, against ~193 VALU for
-// perlin().
+// e = ka | kb << 4.  Part 0 {gx_a, gx_b, gy_a, gy_b} is gp[e], part 1
+// {gz_a, gz_b, 0, 0} is gp[256 + e]: both at 16-B stride from one address
+// register (the second read takes a 4 KiB immediate offset), so a 16-lane
+// ds_read_b128 group spreads over 16 bank slots (e & 15), not the 8 of
+// interleaved 32-B entries.  One b128 + one b64 read yields register pairs
+// that feed v_pk_mul / v_pk_fma directly: 3 packed ops per corner pair.  A
+// packed fma is two IEEE fmas.  Per octave 114 VALU + 8 LDS reads, against
+// ~193 VALU for perlin().
 typedef float vr_pf2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void grad_pair_entry(int e, float4* out)
+// A loop-invariant value pinned to a VGPR.  gfx950 issues a VALU op that reads
+// an SGPR (kernel parameters, wave-uniform constants) at half rate, like the
+// 4-cycle ops (tools/valu_calib.hip), so values many VALU ops read in the
+// hot loops are copied to VGPRs once (the empty asm is hoisted).
+__device__ __forceinline__ float in_vgpr(float x) { asm("" : "+v"(x)); return x; }
+__device__ __forceinline__ uint32_t in_vgpr(uint32_t x) { asm("" : "+v"(x)); return x; }
+__device__ __forceinline__ void grad_pair_entry(int e, float4* gp)
 {
     const float4 a = grad_entry(e & 15), b = grad_entry(e >> 4);
-    out[0] = make_float4(a.x, b.x, a.y, b.y);
-    out[1] = make_float4(a.z, b.z, 0.0f, 0.0f);
+    gp[e] = make_float4(a.x, b.x, a.y, b.y);
+    gp[256 + e] = make_float4(a.z, b.z, 0.0f, 0.0f);
 }
-__device__ __forceinline__ float gdot_pair_lerp(const float4* __restrict__ gp, int32_t ha, int32_t hb, vr_pf2 fx,
+// Byte offset 16 e of the pair entry e = k_a | k_b << 4 of two corners with
+// hash inputs va, vb, where k = ((h >> 15) ^ h) & 15 and h = va * M (hash()).
+// The shifts are folded into the multiplier: h << 4 = va * (M << 4), and bits
+// 15..18 of h sit at 19..22 of that, so k_a << 4 = ((A >> 15) ^ A) & 0xf0 with
+// A = va * (M << 4); likewise k_b << 8 with M << 8.  Only right shifts, xor,
+// and, or: no 4-cycle left shifts (tools/valu_calib.hip).
+// The masks come in VGPRs (in_vgpr): as an SGPR or literal operand of the
+// 3-operand bitop3 they would halve its issue rate.
+__device__ __forceinline__ unsigned pair_offset(int32_t va, int32_t vb, uint32_t m0, uint32_t m1)
+{
+    const uint32_t A = (uint32_t)va * (0x27d4eb2du << 4), B = (uint32_t)vb * (0x27d4eb2du << 8);
+    return (((A >> 15) ^ A) & m0) | (((B >> 15) ^ B) & m1);
+}
+__device__ __forceinline__ float gdot_pair_lerp(const float4* __restrict__ gp, unsigned off16, vr_pf2 fx,
                                                 float fy, float fz, float u)
 {
-    const float4* e = gp + 2 * ((ha & 15) | ((hb & 15) << 4));
+    const float4* e = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(gp) + off16);
     const float4 g0 = e[0];
-    const float2 g1 = *reinterpret_cast<const float2*>(e + 1);
+    const float2 g1 = *reinterpret_cast<const float2*>(e + 256);
     const vr_pf2 dz = vr_pf2{g1.x, g1.y} * vr_pf2{fz, fz};
     const vr_pf2 dy = __builtin_elementwise_fma(vr_pf2{g0.z, g0.w}, vr_pf2{fy, fy}, dz);
     const vr_pf2 d = __builtin_elementwise_fma(vr_pf2{g0.x, g0.y}, fx, dy);
@@ -113,10 +135,13 @@ __device__ inline float perlin_gp(const float4* __restrict__ gp, int32_t seed, f
     const float xf1 = xf0 - 1.0f, yf1 = yf0 - 1.0f, zf1 = zf0 - 1.0f;
     const float u = quintic(xf0), v = quintic(yf0), w = quintic(zf0);
     const vr_pf2 fx = {xf0, xf1};
-    const float l00 = gdot_pair_lerp(gp, hash(seed, x0, y0, z0), hash(seed, x1, y0, z0), fx, yf0, zf0, u);
-    const float l10 = gdot_pair_lerp(gp, hash(seed, x0, y1, z0), hash(seed, x1, y1, z0), fx, yf1, zf0, u);
-    const float l01 = gdot_pair_lerp(gp, hash(seed, x0, y0, z1), hash(seed, x1, y0, z1), fx, yf0, zf1, u);
-    const float l11 = gdot_pair_lerp(gp, hash(seed, x0, y1, z1), hash(seed, x1, y1, z1), fx, yf1, zf1, u);
+    const int32_t s0 = seed ^ x0, s1 = seed ^ x1;   // hash inputs seed ^ x ^ y ^ z (hash())
+    const int32_t y0z0 = y0 ^ z0, y1z0 = y1 ^ z0, y0z1 = y0 ^ z1, y1z1 = y1 ^ z1;
+    const uint32_t m0 = in_vgpr(0xf0u), m1 = in_vgpr(0xf00u);
+    const float l00 = gdot_pair_lerp(gp, pair_offset(s0 ^ y0z0, s1 ^ y0z0, m0, m1), fx, yf0, zf0, u);
+    const float l10 = gdot_pair_lerp(gp, pair_offset(s0 ^ y1z0, s1 ^ y1z0, m0, m1), fx, yf1, zf0, u);
+    const float l01 = gdot_pair_lerp(gp, pair_offset(s0 ^ y0z1, s1 ^ y0z1, m0, m1), fx, yf0, zf1, u);
+    const float l11 = gdot_pair_lerp(gp, pair_offset(s0 ^ y1z1, s1 ^ y1z1, m0, m1), fx, yf1, zf1, u);
     return 0.964921414852142333984375f * lerp(lerp(l00, l10, v), lerp(l01, l11, v), w);
 }
 
@@ -219,17 +244,20 @@ __device__ inline float cellular(int32_t seed, float x, float y, float z)
 }
 
 // Cellular F1 from a table of per-cell feature-point data (the LDS table of
-// the procedural march; vr_march.hip).  Entry (ix, iy, iz) - lo holds
+// the procedural march; vr_march.hip).  Entry (ix, iy, iz) - lo (at
+// index iz * pz + iy * n + ix; the z pitch pz >= n * n is padded so that
+// lanes in neighbouring cells do not hit the same LDS bank slot) holds
 // {xd, yd, zd, inv} of cellular() for that integer cell, so each of the 27
 // cells costs one 16-byte LDS read and 7 VALU ops instead of the hash,
 // bit-field, sqrt and reciprocal.  The arithmetic per cell is cellular()'s,
 // op for op, and fminf is exact, so the result is bit-identical.  The caller
 // guarantees every cell rint(coord) - 1 .. + 1 lies in [lo, lo + n).
-__device__ inline float cellular_table(const float4* __restrict__ tab, int lo, int n, float x, float y, float z)
+__device__ inline float cellular_table(const float4* __restrict__ tab, int lo, int n, int pz, float x, float y,
+                                      float z)
 {
     const float xr = rintf(x), yr = rintf(y), zr = rintf(z);
     const int ix = (int)xr - 1 - lo, iy = (int)yr - 1 - lo, iz = (int)zr - 1 - lo;
-    const float4* t0 = tab + (iz * n + iy) * n + ix;
+    const float4* t0 = tab + iz * pz + iy * n + ix;
     float d0 = 3.402823466e+38f;
 #pragma unroll
     for (int xi = -1; xi <= 1; ++xi) {
@@ -240,10 +268,42 @@ __device__ inline float cellular_table(const float4* __restrict__ tab, int lo, i
 #pragma unroll
             for (int zi = -1; zi <= 1; ++zi) {
                 const float zcf = (zr + (float)zi) - z;
-                const float4 c = t0[((zi + 1) * n + (yi + 1)) * n + (xi + 1)];
+                const float4 c = t0[(zi + 1) * pz + (yi + 1) * n + (xi + 1)];
                 const float xd = fmaf(c.x, c.w, xcf);
                 const float yd = fmaf(c.y, c.w, ycf);
                 const float zd = fmaf(c.z, c.w, zcf);
+                d0 = fminf(d0, fmaf(zd, zd, fmaf(yd, yd, xd * xd)));
+            }
+        }
+    }
+    return d0 - 1.0f;
+}
+
+// cellular_table with the fixed geometry the host picks for tables of at most
+// 9 cells per axis (kWorleyN = 9, z pitch kWorleyPz = 83: no bank aliasing
+// between cells one apart): the base offset is computed in fp32 (small exact
+// integers, one conversion) and the 27 reads take immediate offsets.
+constexpr int kWorleyN = 9, kWorleyPz = 83;
+__device__ inline float cellular_table9(const float4* __restrict__ tab, int lo, float x, float y, float z)
+{
+    const float xr = rintf(x), yr = rintf(y), zr = rintf(z);
+    const float c = (float)(16 * (1 + lo) * (1 + kWorleyN + kWorleyPz));
+    const float fo = fmaf(zr, (float)(16 * kWorleyPz), fmaf(yr, (float)(16 * kWorleyN), fmaf(xr, 16.0f, -c)));
+    const float4* t0 = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(tab) + (int)fo);
+    float d0 = 3.402823466e+38f;
+#pragma unroll
+    for (int xi = -1; xi <= 1; ++xi) {
+        const float xcf = (xr + (float)xi) - x;
+#pragma unroll
+        for (int yi = -1; yi <= 1; ++yi) {
+            const float ycf = (yr + (float)yi) - y;
+#pragma unroll
+            for (int zi = -1; zi <= 1; ++zi) {
+                const float zcf = (zr + (float)zi) - z;
+                const float4 cc = t0[(zi + 1) * kWorleyPz + (yi + 1) * kWorleyN + (xi + 1)];
+                const float xd = fmaf(cc.x, cc.w, xcf);
+                const float yd = fmaf(cc.y, cc.w, ycf);
+                const float zd = fmaf(cc.z, cc.w, zcf);
                 d0 = fminf(d0, fmaf(zd, zd, fmaf(yd, yd, xd * xd)));
             }
         }
