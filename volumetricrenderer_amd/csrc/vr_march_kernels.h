@@ -528,7 +528,8 @@ __device__ __forceinline__ unsigned march_pixel_proc(const MarchArgs& a, const f
 // Requires wave-uniform control flow: every lane of the wave calls it.
 constexpr int kMaxCompactShadow = 8;
 struct ShadowLds {
-    float p[64][3];                      // primary positions of the lanes that need shadow rays, [lane]
+    float4 p[64];                        // primary positions of the lanes that need shadow rays, [lane]
+                                         // (one 16-B LDS access each way)
     union {
         unsigned code[64 * kMaxCompactShadow];   // dealt (lane << 3 | step) pairs, inside the box only
         float d[64 * kMaxCompactShadow];         // then their densities, same slot
@@ -572,7 +573,7 @@ __device__ __forceinline__ unsigned march_pixel_proc_compact(const MarchArgs& a,
                     if (in && cnt == 0) lo = j;
                     cnt += in ? 1 : 0;
                 }
-                sh->p[lane][0] = P0; sh->p[lane][1] = P1; sh->p[lane][2] = P2;
+                sh->p[lane] = make_float4(P0, P1, P2, 0.0f);
             }
             // Exclusive prefix of cnt (0..8, four bits) over the wave, by bit-plane ballots.
             int off = 0, total = 0;
@@ -589,7 +590,8 @@ __device__ __forceinline__ unsigned march_pixel_proc_compact(const MarchArgs& a,
                 if (pid < total) {
                     const unsigned code = sh->code[pid];
                     const int kk = (int)(code >> 3), j = (int)(code & 7u);
-                    float q0 = sh->p[kk][0], q1 = sh->p[kk][1], q2 = sh->p[kk][2];
+                    const float4 pk = sh->p[kk];
+                    float q0 = pk.x, q1 = pk.y, q2 = pk.z;
                     for (int jj = 0; jj <= j; ++jj) { q0 = q0 + p.lstep[0]; q1 = q1 + p.lstep[1]; q2 = q2 + p.lstep[2]; }
                     sh->d[pid] = proc_density<TABLE>(p, wt, a.scale, q0, q1, q2);
                     ++evals;
