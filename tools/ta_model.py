@@ -77,6 +77,8 @@ def main():
     ap.add_argument("--layout", default="brick4832")
     ap.add_argument("--quad", default="2x2")
     ap.add_argument("--tiles", type=int, default=0, help="model every K-th tile (0: all)")
+    ap.add_argument("--b32", action="store_true",
+                    help="4-B row loads (rows y, y+1 of each slice: 4 per tap), looked up per 16-lane group and line")
     args = ap.parse_args()
     n, p0, st = rays()
     tx8, ty8 = W // 8, (H + 7) // 8
@@ -118,8 +120,17 @@ def main():
         steps += a_.sum()
         for sc in (1, .8, .75, .7):
             g = np.clip(np.floor(P * sc * N + 0.5).astype(np.int64), 0, N)
-            for o in off(g[..., 0], g[..., 1], g[..., 2]):
+            offs = off(g[..., 0], g[..., 1], g[..., 2])
+            if args.b32:
+                offs = [o + d for o in offs for d in (0, 4)]   # rows y, y+1 of each slice
+            for o in offs:
                 ln = np.where(a_, o // 128, -1)
+                if args.b32:
+                    q = np.sort(ln.reshape(len(ln), 4, 16), axis=-1)
+                    new = np.concatenate([q[..., :1] >= 0, (q[..., 1:] != q[..., :-1]) & (q[..., 1:] >= 0)], -1)
+                    look += new.sum()
+                    insts += len(ln)
+                    continue
                 ln2 = np.where(a_ & ((o // 128) != ((o + span - 1) // 128)), (o + span - 1) // 128, -1)
                 q = np.sort(np.concatenate([ln.reshape(len(ln), 16, 4), ln2.reshape(len(ln), 16, 4)], -1), axis=-1)
                 new = np.concatenate([q[..., :1] >= 0, (q[..., 1:] != q[..., :-1]) & (q[..., 1:] >= 0)], -1)
@@ -136,7 +147,8 @@ def main():
             bbox_chunks += (rows * chunks).sum()
     print(f"  wave load instructions {insts}, lane-steps {steps}, "
           f"{insts * 64 / steps:.2f} lane loads/step (incl. idle lanes)")
-    print(f"  L1 lookups per instruction {look / insts:.2f} (min 16), per wave-step {look / insts * 8:.1f}")
+    per_step = insts / (steps / 64) if steps else 0
+    print(f"  L1 lookups per instruction {look / insts:.2f}, per wave-step {look / insts * (16 if args.b32 else 8):.1f}")
     print(f"  distinct 128-B lines per instruction (wave) {lines_w / insts:.2f}")
     print(f"  planar bbox 16-B chunks per tap-step {bbox_chunks / (insts / 2):.1f} "
           f"(= {bbox_chunks / (insts / 2) / 64:.2f} b128 wave loads)")
