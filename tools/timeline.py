@@ -31,10 +31,16 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--json", default="")
     ap.add_argument("--opt", action="append", default=[], help="extra vr_set_option name=value")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--steps", type=int, default=128)
+    ap.add_argument("--bands", type=int, default=1, help="render rank 0's 16-row bands of N (a 1/N frame share)")
     a = ap.parse_args()
     lib = _lib.load()
     lib.vr_timeline_fetch.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    W, H = 1920, 1080
+    lib.vr_timeline_fetch_c8.argtypes = [ctypes.c_void_p, ctypes.c_int]   # the CORNER8 / CORNERH unit
+    W, H = a.width, a.height
+    band = dict(band_rows=16, band_stride=a.bands, band_first=0) if a.bands > 1 else {}
     out_all = {}
     with vr.Renderer(0) as r:
         r.generate_volume(vr.scaled_recipe(a.size))
@@ -43,26 +49,28 @@ def main():
         for kv in a.opt:
             k, v = kv.split("=")
             r.set_option(k, int(v))
-        osd, gsd = vr.reference_shader_data(W / H)
+        osd, gsd = vr.reference_shader_data(1280 / 720)
         r.set_shader_data(osd, gsd)
-        r.set_march(vr.march_defaults(max_steps=128))
-        out = r.alloc_target(W, H, vr.FMT_RGBA8_UNORM)
+        r.set_march(vr.march_defaults(max_steps=a.steps))
+        out = r.alloc_target(W, H, vr.FMT_RGBA8_UNORM, **band)
         for _ in range(5):
-            r.render(W, H, vr.FMT_RGBA8_UNORM, out=out)
+            r.render(W, H, vr.FMT_RGBA8_UNORM, out=out, **band)
         torch.cuda.synchronize()
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         ev[0].record()
         for _ in range(20):
-            r.render(W, H, vr.FMT_RGBA8_UNORM, out=out)
+            r.render(W, H, vr.FMT_RGBA8_UNORM, out=out, **band)
         ev[1].record()
         torch.cuda.synchronize()
         print(json.dumps({"opts": a.opt, "split": a.split, "ms_per_frame_20": round(ev[0].elapsed_time(ev[1]) / 20, 4)}))
         for rep in range(a.reps):
-            assert lib.vr_timeline_clear() == 0
-            r.render(W, H, vr.FMT_RGBA8_UNORM, out=out)
+            assert lib.vr_timeline_clear() == 0 and lib.vr_timeline_clear_c8() == 0
+            r.render(W, H, vr.FMT_RGBA8_UNORM, out=out, **band)
             torch.cuda.synchronize()
             buf = np.zeros((1 << 16, 3), np.uint64)
             assert lib.vr_timeline_fetch(buf.ctypes.data, 1 << 16) == 0
+            if not (buf[:, 1] > 0).any():
+                assert lib.vr_timeline_fetch_c8(buf.ctypes.data, 1 << 16) == 0
             rec = buf[buf[:, 1] > 0]
             t0 = rec[:, 0].min()
             s = (rec[:, 0] - t0).astype(np.float64) / 100.0   # us

@@ -15,3 +15,17 @@ hipError_t launch_march_corner8(const MarchArgs& a, int layout, bool early, cons
 }
 
 }  // namespace vr
+
+#ifdef VR_TIMELINE
+// timing experiments only (make timeline): this translation unit's records
+extern "C" int vr_timeline_fetch_c8(unsigned long long* host, int waves)
+{
+    waves = waves < vr::kTimelineWaves ? waves : vr::kTimelineWaves;
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(vr::g_timeline), (size_t)waves * 3 * sizeof(unsigned long long));
+}
+extern "C" int vr_timeline_clear_c8()
+{
+    static unsigned long long zero[vr::kTimelineWaves][3];
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(vr::g_timeline), zero, sizeof(zero));
+}
+#endif
