@@ -1,6 +1,10 @@
 #!/bin/bash
 # Same-box A/B timing: bench.py with libvr.so vs another build (VR_LIB),
-# interleaved ROUNDS times per config.  Usage: LIBB=path CONFIGS="..." tools/ab.sh
+# interleaved ROUNDS times per config (boxes of the pool differ by ~5-10 %, so
+# compare builds inside one gpurun call).  Usage: LIBB=path CONFIGS="..." tools/ab.sh
+# A baseline build of an earlier commit, e.g.:
+#   git worktree add /tmp/base <commit> && make -C /tmp/base/volumetricrenderer_amd/csrc \
+#       OUT=$PWD/volumetricrenderer_amd/libvr_base.so OBJDIR=/tmp/base_obj $PWD/volumetricrenderer_amd/libvr_base.so
 set -u
 OUT=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out
 mkdir -p "$OUT"; export TMPDIR=/tmp
