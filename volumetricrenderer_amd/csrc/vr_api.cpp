@@ -53,11 +53,12 @@ constexpr int kDefaultWedges = 4;         // regions schedule: wedges per XCD (m
 constexpr int kRegionRebuildInterval = 32;
 constexpr int kMaxRegionStreams = 4;
 constexpr int kRegionKeyLen = 32;
-// auto split: lanes per ray doubled (up to 4) while the frame's tiles with
-// work, times lanes per ray, stay under this many (measured on 1/N of the
-// 1080p frame, DESIGN.md sec. 7: K = 1, 2, 4, 4 at N = 1, 2, 4, 8)
-constexpr long long kSplitTargetUnits = 6000;
-constexpr int kMaxAutoSplit = 4;
+// auto split (lanes per ray) from the frame share's tiles with work: K = 1 at
+// >= 6000, 2 at >= 1400, else 4.  Measured on 1/N of the 1080p frame at 512^3
+// (~7,500 tiles with work): K = 1, 2, 2, 4 at N = 1, 2, 4, 8.
+// K = 2 beats K = 1 by 17 % at N = 2 and K = 4 by 2-5 % at N = 4; at 4K x 256
+// (4x the tiles) it keeps K = 1 up to N = 4.
+constexpr long long kSplitOneLane = 6000, kSplitTwoLanes = 1400;
 
 struct Ctx {
     int device = 0;
@@ -1012,8 +1013,7 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
             pl.layout == LAYOUT_CORNERH) {
             int K = c->split;
             if (K == 0) {
-                K = 1;
-                while (K < kMaxAutoSplit && (long long)rb.nwork * K < kSplitTargetUnits) K *= 2;
+                K = rb.nwork >= kSplitOneLane ? 1 : rb.nwork >= kSplitTwoLanes ? 2 : 4;
             }
             if (K > 1) {
                 const int ktpw = tpw;
