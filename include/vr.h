@@ -121,8 +121,9 @@ typedef struct {
 /* A render target.  `pixels` is a DEVICE pointer that the caller owns.
  * With band_rows > 0 only bands b = band_first, band_first + band_stride, ...
  * are rendered.  Band b covers frame rows [b*band_rows, (b+1)*band_rows).
- * The bands are written packed and in order, from row 0 of `pixels`.  This
- * is how the frame is split across GPUs.  band_rows = 0 renders the whole
+ * The bands are written packed and in order, from row 0 of `pixels`; the
+ * rows of a last, partial band that lie past `height` are left untouched.
+ * This is how the frame is split across GPUs.  band_rows = 0 renders the whole
  * frame.  step_counter (device u64, may be NULL) has the executed ray-steps
  * added to it (the sum of n, frag.glsl:46).                                */
 typedef struct {

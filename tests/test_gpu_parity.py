@@ -373,6 +373,45 @@ def test_procedural_early_out_and_rgba8(r, oracle, shadow):
     assert c < c2   # the early-out really skipped steps
 
 
+def test_procedural_sort_reuse(r, oracle):
+    """The cost-sorted order is reused while the frame geometry is unchanged
+    (vr_api.cpp sort key) -- across medium changes -- and rebuilt when the
+    camera, band set or shadow flag changes.  Each render goes into a target
+    prefilled with garbage, so a reused order must still write every pixel
+    (the background fill).  Exact against the oracle every time."""
+    W, H = 160, 90
+    march = vr.march_defaults(max_steps=48)
+    cams = [vr.reference_shader_data(W / H, 20.0, 15.0), vr.reference_shader_data(W / H, -40.0, 5.0)]
+    seq = [(0, {}, dict(octaves=4)), (0, {}, dict(octaves=3, seed_fbm=7)), (1, {}, dict(octaves=4)),
+           (0, {}, dict(octaves=4, shadow_steps=8)), (0, {}, dict(octaves=2, shadow_steps=8)),
+           (0, dict(band_rows=16, band_stride=2, band_first=1), dict(octaves=4)),
+           (0, dict(band_rows=16, band_stride=2, band_first=1), dict(octaves=4, seed_fbm=11)),
+           (0, {}, dict(octaves=4))]
+    for cam, band, proc in seq:
+        osd, gsd = cams[cam]
+        r.set_shader_data(osd, gsd)
+        r.set_march(march)
+        r.set_procedural(**proc)
+        try:
+            out = r.alloc_target(W, H, vr.FMT_RGBA32F, **band)
+            out.fill_(123.0)
+            r.render(W, H, vr.FMT_RGBA32F, out=out, **band)
+            torch.cuda.synchronize()
+            p = oracle.procedural_from(r.procedural)
+        finally:
+            r.set_procedural(enabled=0)
+        obj, glob = vr.shader_data_arrays(osd, gsd)
+        ref, _ = oracle.render_procedural(p, obj, glob, oracle.from_params(march), W, H, 0, **band)
+        # packed rows that map past the frame (a partial last band) are not
+        # written (vr.h vr_target); compare the frame's rows
+        rows = np.arange(out.shape[0])
+        if band:
+            bl = rows // band["band_rows"]
+            rows = rows[(band["band_first"] + bl * band["band_stride"]) * band["band_rows"]
+                        + rows % band["band_rows"] < H]
+        assert_exact(out.cpu().numpy()[rows], ref[rows])
+
+
 @pytest.mark.parametrize("shadow", [0, 8])
 def test_procedural_bands(r, oracle, shadow):
     band = dict(band_rows=16, band_stride=3, band_first=1)

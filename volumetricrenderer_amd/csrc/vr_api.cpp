@@ -107,6 +107,9 @@ struct Ctx {
     int region_cur = -1;           // buffer of the current lists (-1 = none)
     float region_key[kRegionKeyLen] = {};   // geometry the current lists were built for
     long long renders_since_build = 0;
+    // procedural cost sort: the geometry whose order d_sort holds (n per pixel
+    // depends only on it, not on the medium), valid until the buffer changes
+    std::vector<float> sort_key;
 };
 
 // Auto layout (measured): CORNERH (16 B per texel: one load
@@ -986,13 +989,32 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
                 if (c->d_sort) (void)hipFree(c->d_sort);
                 c->d_sort = nullptr;
                 c->sort_bytes = 0;
+                c->sort_key.clear();
                 if (hipMalloc(&c->d_sort, need) != hipSuccess) return fail(VR_ERR_OOM, "vr_render: sort buffer");
                 HIP_TRY(hipMemset(c->d_sort, 0, need));   // the histogram starts at zero (proc_scan re-zeroes it)
                 c->sort_bytes = need;
             }
             sort_buf = c->d_sort;
         }
-        HIP_TRY(launch_march_procedural(a, m.early_out > 0.0f, sort_buf, sc, static_cast<hipStream_t>(stream)));
+        // The sorted order depends only on each pixel's step count n (a3),
+        // i.e. on the frame geometry below, not on the medium: a frame with
+        // the same geometry reuses it (like the region lists of the grid path)
+        bool reuse = false;
+        std::vector<float> key;
+        if (sort_buf) {
+            key = {(float)a.width, (float)a.height, (float)a.out_rows, (float)a.band_rows, (float)a.band_stride,
+                   (float)a.band_first, (float)a.max_steps, a.step_size, (float)a.cam_mode,
+                   (float)(a.proc.shadow_steps > 0)};
+            for (const float* v : {a.org, a.o, a.px, a.py, a.cam, a.box_min, a.box_max, a.box_range})
+                key.insert(key.end(), v, v + 3);
+            key.insert(key.end(), a.r2, a.r2 + 4);
+            key.insert(key.end(), a.r3, a.r3 + 4);
+            reuse = key.size() == c->sort_key.size() &&
+                    std::memcmp(key.data(), c->sort_key.data(), key.size() * sizeof(float)) == 0;
+        }
+        c->sort_key.clear();   // valid again only once this launch is queued
+        HIP_TRY(launch_march_procedural(a, m.early_out > 0.0f, sort_buf, reuse, sc, static_cast<hipStream_t>(stream)));
+        c->sort_key = key;
         return VR_OK;
     }
     // auto schedule (measured): regions -- per-XCD angular

@@ -193,7 +193,10 @@ hipError_t launch_march_corner8(const MarchArgs& a, int layout, bool early, cons
                                 hipStream_t s);   // CORNER8 / CORNERH, vr_march_c8.hip
 // sort_buf (proc_sort_bytes) selects the cost-sorted schedule; null = 8x8
 // tiles, in rings when sc.kind == SCHED_RINGS, else in row order
-hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_buf, const Schedule& sc, hipStream_t s);
+// reuse_sort: sort_buf holds the order of a frame with the same geometry
+// (vr_api.cpp sort key): skip the sort passes, write the background only
+hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_buf, bool reuse_sort, const Schedule& sc,
+                                   hipStream_t s);
 size_t proc_sort_bytes(int width, int out_rows);
 hipError_t launch_repack(const uint8_t* d_rgba, int nx, int ny, int nz, uint8_t* d_planar, hipStream_t s);
 // Build a fast layout from the planar planes.

@@ -23,7 +23,8 @@ size_t proc_sort_bytes(int width, int out_rows)
            regions * kSortRegion * kSortRegion * 2u;
 }
 
-hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_buf, const Schedule& sc, hipStream_t s)
+hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_buf, bool reuse_sort, const Schedule& sc,
+                                   hipStream_t s)
 {
     if (a.width <= 0 || a.out_rows <= 0) return hipSuccess;
     const bool shadow = a.proc.shadow_steps > 0;
@@ -39,10 +40,18 @@ hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_bu
         const long long pixels = (long long)a.width * a.out_rows;
         static_assert(kSortRegion * kSortRegion == 256 * kSortPixelsPerThread, "one 64x64 region per sort block");
         const dim3 g1((unsigned)(((a.width + kSortRegion - 1) / kSortRegion) * ((a.out_rows + kSortRegion - 1) / kSortRegion)));
-        if (shadow) hipLaunchKernelGGL((proc_bin<true>), g1, dim3(256), 0, s, a, hist, keys);
-        else hipLaunchKernelGGL((proc_bin<false>), g1, dim3(256), 0, s, a, hist, keys);
-        hipLaunchKernelGGL(proc_scan, dim3(1), dim3(kKeyBins), 0, s, hist, cursor);
-        hipLaunchKernelGGL(proc_scatter, g1, dim3(256), 0, s, a, keys, cursor, order);
+        if (reuse_sort) {
+            // same geometry as the frame that built keys / order / total: only
+            // the pixels without steps need writing before the march
+            const unsigned positions = g1.x * 256u * kSortPixelsPerThread;
+            hipLaunchKernelGGL(proc_fill_background, dim3((positions + 256 * 16 - 1) / (256 * 16)), dim3(256), 0, s, a,
+                               keys, positions);
+        } else {
+            if (shadow) hipLaunchKernelGGL((proc_bin<true>), g1, dim3(256), 0, s, a, hist, keys);
+            else hipLaunchKernelGGL((proc_bin<false>), g1, dim3(256), 0, s, a, hist, keys);
+            hipLaunchKernelGGL(proc_scan, dim3(1), dim3(kKeyBins), 0, s, hist, cursor);
+            hipLaunchKernelGGL(proc_scatter, g1, dim3(256), 0, s, a, keys, cursor, order);
+        }
         // the scatter advanced cursor[k] to the end of key k; total stays at cursor[kKeyBins]
         const dim3 g4((unsigned)((pixels + kThreads - 1) / kThreads));
         const unsigned* total = cursor + kKeyBins;

@@ -1082,6 +1082,22 @@ __global__ __launch_bounds__(256) void proc_bin(const MarchArgs a, unsigned* __r
 // total at cursor[kKeyBins].  One workgroup of kKeyBins threads.
 // It also zeroes the histogram for the next frame (the buffer is zeroed once
 // when allocated), which saves a memset launch per frame.
+// Background of a frame whose sorted order is reused (same geometry): the
+// pixels with no steps (key 0 in the bin pass) get (0,0,0,1), which is both
+// the clear colour and the epilogue of zero steps in every format, so this is
+// exactly what proc_bin stores for them.
+__global__ __launch_bounds__(256) void proc_fill_background(const MarchArgs a, const unsigned short* __restrict__ keys,
+                                                            unsigned positions)
+{
+    for (unsigned i = blockIdx.x * 256u + threadIdx.x; i < positions; i += gridDim.x * 256u) {
+        int x, orow;
+        if (!sort_pixel(a, i, &x, &orow) || keys[i] != 0) continue;
+        const int bl = orow / a.band_rows;
+        const int y = (a.band_first + bl * a.band_stride) * a.band_rows + (orow - bl * a.band_rows);
+        if (y < a.height) store_pixel(a, x, orow, false, 0.0f);
+    }
+}
+
 [[maybe_unused]] __global__ __launch_bounds__(kKeyBins) void proc_scan(unsigned* __restrict__ hist, unsigned* __restrict__ cursor)
 {
     __shared__ unsigned sc[kKeyBins];
