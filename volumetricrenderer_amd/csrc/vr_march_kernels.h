@@ -527,12 +527,17 @@ __device__ __forceinline__ unsigned march_pixel_proc(const MarchArgs& a, const f
 // repeated-addition shadow positions) is exactly march_pixel_proc's.
 // Requires wave-uniform control flow: every lane of the wave calls it.
 constexpr int kMaxCompactShadow = 8;
+// Dealt pair pid lives at slot pid + pid / 32: an owner lane writes (and later
+// reads) its run at off_k + c, and the offsets of neighbouring lanes step by
+// their run lengths (~8), which without the pad puts 32 lanes on 4 LDS banks.
+__device__ __forceinline__ int shadow_slot(int pid) { return pid + (pid >> 5); }
+constexpr int kShadowSlots = 64 * kMaxCompactShadow + 64 * kMaxCompactShadow / 32;
 struct ShadowLds {
     float4 p[64];                        // primary positions of the lanes that need shadow rays, [lane]
                                          // (one 16-B LDS access each way)
     union {
-        unsigned code[64 * kMaxCompactShadow];   // dealt (lane << 3 | step) pairs, inside the box only
-        float d[64 * kMaxCompactShadow];         // then their densities, same slot
+        unsigned code[kShadowSlots];   // dealt (lane << 3 | step) pairs, inside the box only
+        float d[kShadowSlots];         // then their densities, same slot
     };
 };
 
@@ -583,24 +588,24 @@ __device__ __forceinline__ unsigned march_pixel_proc_compact(const MarchArgs& a,
                 off += __popcll(bb & ((1ull << lane) - 1ull)) << b;
                 total += __popcll(bb) << b;
             }
-            for (int c = 0; c < cnt; ++c) sh->code[off + c] = ((unsigned)lane << 3) | (unsigned)(lo + c);
+            for (int c = 0; c < cnt; ++c) sh->code[shadow_slot(off + c)] = ((unsigned)lane << 3) | (unsigned)(lo + c);
             __builtin_amdgcn_wave_barrier();
             for (int base = 0; base < total; base += 64) {
                 const int pid = base + lane;
                 if (pid < total) {
-                    const unsigned code = sh->code[pid];
+                    const unsigned code = sh->code[shadow_slot(pid)];
                     const int kk = (int)(code >> 3), j = (int)(code & 7u);
                     const float4 pk = sh->p[kk];
                     float q0 = pk.x, q1 = pk.y, q2 = pk.z;
                     for (int jj = 0; jj <= j; ++jj) { q0 = q0 + p.lstep[0]; q1 = q1 + p.lstep[1]; q2 = q2 + p.lstep[2]; }
-                    sh->d[pid] = proc_density<TABLE>(p, wt, a.scale, q0, q1, q2);
+                    sh->d[shadow_slot(pid)] = proc_density<TABLE>(p, wt, a.scale, q0, q1, q2);
                     ++evals;
                 }
             }
             __builtin_amdgcn_wave_barrier();
             if (need) {
                 float sl = 0.0f;
-                for (int c = 0; c < cnt; ++c) sl = sl + sh->d[off + c];
+                for (int c = 0; c < cnt; ++c) sl = sl + sh->d[shadow_slot(off + c)];
                 const float tl = spec_expf(-(sl * p.od));
                 rad = fmaf((tv * (rho * p.od)), tl, rad);
             }
