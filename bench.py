@@ -119,6 +119,13 @@ def cpu_baseline(volume_host, osd, gsd, march, width, height, budget_s=10.0, pro
 
 
 def main() -> int:
+    # stdout carries exactly one JSON line (rank 0).  Libraries print to fd 1
+    # too -- RCCL its version banner at communicator init -- so fd 1 is
+    # pointed at stderr for the whole run and the JSON goes to a private
+    # duplicate of the original stdout.
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -208,16 +215,22 @@ def main() -> int:
             print(f"rank {rank}: native RCCL frame loop unavailable: {e}", file=sys.stderr, flush=True)
             raise SystemExit(3)
     if native:
+        # Bracket: host barrier (gloo) for the rendezvous, then the device-side
+        # RCCL barrier + synchronisation on both sides of the timed frames.  A
+        # gloo barrier across 8 processes costs a sizeable fraction of a
+        # millisecond -- several 1/8-frames -- so it stays outside the clock.
         pipe.run_frames(args.warmup)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
+        pipe.barrier(stream)
         t0 = time.perf_counter()
-        kern_ms = pipe.run_frames(args.steps, sample_every=ev_every)
+        kern_ms = pipe.run_frames(args.steps, stream=stream, sample_every=ev_every)
+        pipe.barrier(stream)
         torch.cuda.synchronize()
+        el = time.perf_counter() - t0
         if world > 1:
             dist.barrier()
-        el = time.perf_counter() - t0
     else:
         sharder.run_frames(args.warmup)
         if world > 1:
@@ -319,7 +332,7 @@ def main() -> int:
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(None if proc is not None else r.get_volume(), osd, gsd, march, W, H,
                                                args.cpu_budget, procedural=proc)
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
     if native:
         pipe.close()
     sharder.close()

@@ -72,6 +72,14 @@ vr_status vr_shard_destroy(vr_shard* sh);
  * sample). */
 vr_status vr_shard_run(vr_shard* sh, int frames, void* stream, int sample_every, float* kernel_ms);
 
+/* Collective barrier + synchronisation: returns once the work queued on
+ * `stream` and on the communication stream of EVERY rank before the call has
+ * finished (one 4-byte RCCL all-reduce over xGMI, ordered after `stream`,
+ * then a host wait).  Costs microseconds where a host-side gloo barrier
+ * across 8 processes costs a large fraction of a 1/8-frame; the bench
+ * brackets its timed frames with it.  Loopback: a stream synchronisation. */
+vr_status vr_shard_barrier(vr_shard* sh, void* stream);
+
 /* Rank 0: the last assembled frame (device pointer, tight rows) once
  * `stream` of the last vr_shard_run has reached it.  Other ranks: their
  * last band set. */

@@ -72,7 +72,7 @@ def test_rccl_pipeline_one_rank(fmt, band_rows):
     """The native frame loop (libvr_shard.so) with a one-rank RCCL
     communicator: render into the gather slot, (no peers), assemble, 2 frames
     in flight.  The frame equals a plain render; the kernel-time sample is
-    positive.  Multi-rank RCCL needs one GPU per rank (the driver's run)."""
+    positive; the RCCL barrier returns.  Multi-rank RCCL needs one GPU per rank (the driver's run)."""
     import sys
     sys.path.insert(0, ROOT)
     import volumetricrenderer_amd as vr
@@ -88,6 +88,7 @@ def test_rccl_pipeline_one_rank(fmt, band_rows):
             assert pl.my_rows == pl.rows_per_rank == vr.band_rows_packed(H, band_rows, 1, 0) >= H
             ms = pl.run_frames(5, sample_every=2)
             assert ms > 0
+            pl.barrier()   # one-rank RCCL all-reduce + host wait (the bench's bracket)
             got = pl.frame()
             full = r.render(W, H, fmt)
             torch.cuda.synchronize()
@@ -119,6 +120,7 @@ def test_native_pipeline_loopback_ranks(world, band_rows, fmt):
         try:
             assert pl.rows_per_rank == vr.band_rows_packed(H, band_rows, world, 0)
             pl.run_frames(3)
+            pl.barrier()   # loopback: a stream synchronisation
             got = pl.frame()
             full = r.render(W, H, fmt)
             torch.cuda.synchronize()

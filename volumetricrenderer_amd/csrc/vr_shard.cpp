@@ -79,6 +79,8 @@ struct vr_shard {
     uint8_t* gathered[2] = {};        // rank 0: nranks slots of rows_per_rank rows
     uint8_t* frame[2] = {};           // rank 0
     hipEvent_t rendered[2] = {}, done[2] = {};
+    hipEvent_t fence = nullptr;       // vr_shard_barrier: the caller's stream -> comm stream
+    int* token = nullptr;             // vr_shard_barrier: one int all-reduced over the ranks
     bool pending[2] = {};             // done[p] recorded and not yet waited on
     int last = -1;                    // parity of the last frame
     bool loopback = false;            // one process emulates all ranks (no RCCL)
@@ -98,6 +100,8 @@ void release(vr_shard* sh)
         if (sh->done[p]) (void)hipEventDestroy(sh->done[p]);
     }
     for (hipEvent_t e : sh->timing) (void)hipEventDestroy(e);
+    if (sh->fence) (void)hipEventDestroy(sh->fence);
+    if (sh->token) (void)hipFree(sh->token);
     if (sh->comm) (void)ncclCommDestroy(sh->comm);
     if (sh->comm_stream) (void)hipStreamDestroy(sh->comm_stream);
     delete sh;
@@ -201,6 +205,8 @@ vr_status vr_shard_alloc(void* ctx, int nranks, int rank, int width, int height,
     hip_ok(e, "hipGetDevice");
     sh->device = dev;
     hip_ok(hipStreamCreateWithFlags(&sh->comm_stream, hipStreamNonBlocking), "comm stream");
+    hip_ok(hipEventCreateWithFlags(&sh->fence, hipEventDisableTiming), "event");
+    hip_ok(hipMalloc(&sh->token, sizeof(int)), "barrier token");
     for (int p = 0; p < 2 && st == VR_OK; ++p) {
         hip_ok(hipEventCreateWithFlags(&sh->rendered[p], hipEventDisableTiming), "event");
         hip_ok(hipEventCreateWithFlags(&sh->done[p], hipEventDisableTiming), "event");
@@ -298,6 +304,23 @@ vr_status vr_shard_run(vr_shard* sh, int frames, void* stream, int sample_every,
         }
         *kernel_ms = next ? (float)(sum / next) : 0.0f;
     }
+    return VR_OK;
+}
+
+vr_status vr_shard_barrier(vr_shard* sh, void* stream)
+{
+    if (!sh) return fail(VR_ERR_INVALID, "vr_shard_barrier: null");
+    if (sh->loopback && sh->rank != 0)
+        return fail(VR_ERR_INVALID, "vr_shard_barrier: rank %d is not connected (vr_shard_connect)", sh->rank);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    HIP_TRY(hipEventRecord(sh->fence, s));
+    HIP_TRY(hipStreamWaitEvent(sh->comm_stream, sh->fence, 0));
+    // The all-reduce completes on a rank only once every rank's streams have
+    // reached it: a device-side barrier over xGMI, then the host waits for it.
+    if (sh->nranks > 1 && !sh->loopback)
+        NCCL_TRY(ncclAllReduce(sh->token, sh->token, 1, ncclInt32, ncclSum, sh->comm, sh->comm_stream));
+    HIP_TRY(hipStreamSynchronize(sh->comm_stream));
+    HIP_TRY(hipStreamSynchronize(s));
     return VR_OK;
 }
 

@@ -260,6 +260,13 @@ class RcclBandPipeline:
                         ctypes.byref(ms) if sample_every > 0 else None)
         return ms.value if sample_every > 0 else None
 
+    def barrier(self, stream=None):
+        """Collective: returns once every rank's queued frames (on `stream`
+        and the exchange stream) have finished -- a device-side RCCL barrier
+        plus a host wait (vr_shard_barrier)."""
+        from .renderer import _stream_handle
+        _lib.shard_call("vr_shard_barrier", self._h, _stream_handle(stream))
+
     def frame(self, stream=None) -> torch.Tensor:
         """A copy of the last frame (rank 0) or band set (other ranks)."""
         from .renderer import _stream_handle
