@@ -250,6 +250,11 @@ vr_status vr_set_layout_preference(void* ctx, int pref);
  *                     default); 1 = it sums density evaluations, i.e.
  *                     ray-steps plus the procedural shadow samples -- the unit
  *                     of the procedural roofline.
+ *   "lattice"         procedural medium, sorted schedule: 1 = the fBm reads its
+ *                     per-cell gradient-pair offsets from a lattice table in
+ *                     global memory (the default; built when the seed or the
+ *                     lattice range changes, at most 2^24 cells, 128 MiB);
+ *                     0 = it hashes every corner.  Results are identical.
  * vr_get_option returns -1 for an unknown name.                            */
 vr_status vr_set_option(void* ctx, const char* name, int value);
 int       vr_get_option(void* ctx, const char* name);

@@ -430,6 +430,27 @@ def test_procedural_1080p_config2_full_frame(r, oracle):
     assert c == s == 16737882
 
 
+@pytest.mark.parametrize("kw", [dict(), dict(freq0=-0.23, octaves=3), dict(lacunarity=-1.7, octaves=5, seed_fbm=5),
+                                dict(octaves=9), dict(shadow_steps=8)])
+def test_procedural_lattice_table(r, oracle, kw):
+    """The Perlin lattice table (vr_api.cpp ensure_lattice, option
+    "lattice"): exact against the oracle with it and without it, for negative
+    frequencies (cells below 0), alternating-sign lacunarity, a range too
+    large for the table (9 octaves: the per-octave hash path) and shadows."""
+    march = vr.march_defaults(max_steps=64)
+    try:
+        imgs = []
+        for lat in (1, 0):
+            r.set_option("lattice", lat)
+            img, ref, c, s, _ = render_proc_both(r, oracle, 112, 80, march, **kw)
+            assert_exact(img, ref)
+            assert c == s
+            imgs.append(img)
+        assert np.array_equal(imgs[0], imgs[1])
+    finally:
+        r.set_option("lattice", 1)
+
+
 def test_procedural_rejects_bad_parameters(r):
     with pytest.raises(VRError):
         r.set_procedural(octaves=17)

@@ -11,7 +11,7 @@ mkdir -p "$OUT"; export TMPDIR=/tmp
 for r in $(seq 1 ${ROUNDS:-3}); do
   for c in ${CONFIGS:-cloud}; do
     for lib in volumetricrenderer_amd/libvr.so $LIBB; do
-      VR_LIB=$lib timeout -k 10 300 python -u bench.py --config $c --steps ${STEPS:-40} > "$OUT/ab.log" 2>&1 || { tail "$OUT/ab.log"; exit 4; }
+      VR_LIB=$lib timeout -k 10 300 python -u bench.py --config $c --no-cpu-baseline --steps ${STEPS:-40} > "$OUT/ab.log" 2> "$OUT/ab.err" || { tail "$OUT/ab.err"; exit 4; }
       python -c "import json;j=json.loads(open('$OUT/ab.log').read().strip().split(chr(10))[-1]);print('$r $c $(basename $lib)', j['ms_per_step'], j['kernel_ms_mean'], j['roofline']['frac'])"
     done
   done

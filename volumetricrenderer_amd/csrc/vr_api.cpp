@@ -110,6 +110,12 @@ struct Ctx {
     // procedural cost sort: the geometry whose order d_sort holds (n per pixel
     // depends only on it, not on the medium), valid until the buffer changes
     std::vector<float> sort_key;
+    // Perlin lattice table of the procedural march (noise::perlin_lattice_entry),
+    // built when (seed, lo, n) changes; option "lattice" 0 turns it off
+    int lattice = 1;
+    uint2* d_lat = nullptr;
+    size_t lat_cap = 0;            // bytes allocated
+    long long lat_key[3] = {0, 0, -1};
 };
 
 // Auto layout (measured): CORNERH (16 B per texel: one load
@@ -419,6 +425,7 @@ vr_status vr_destroy(void* p)
     if (c->d_heads) (void)hipFree(c->d_heads);
     if (c->d_sort) (void)hipFree(c->d_sort);
     (void)hipDeviceSynchronize();   // queued renders may still read the region lists
+    if (c->d_lat) (void)hipFree(c->d_lat);
     for (auto& b : c->region) {
         if (b.d) (void)hipFree(b.d);
         if (b.h) (void)hipHostFree(b.h);
@@ -673,6 +680,11 @@ vr_status vr_set_option(void* p, const char* name, int value)
         c->count = value;
         return VR_OK;
     }
+    if (n == "lattice") {
+        if (value < 0 || value > 1) return fail(VR_ERR_INVALID, "vr_set_option: lattice is 0 or 1");
+        c->lattice = value;
+        return VR_OK;
+    }
     return fail(VR_ERR_INVALID, "vr_set_option: unknown option '%s'", name);
 }
 
@@ -688,6 +700,7 @@ int vr_get_option(void* p, const char* name)
     if (n == "count") return c->count;
     if (n == "wedges") return c->wedges;
     if (n == "split") return c->split;
+    if (n == "lattice") return c->lattice;
     return -1;
 }
 
@@ -885,6 +898,51 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     return VR_OK;
 }
 
+// Perlin lattice table (global memory) of the procedural march: the fBm's
+// octave o samples lattice coordinates P * grid_scale * f_o with P in the
+// box, [0, 1]^3 up to rounding; the table covers the cells of every octave,
+// with 2 cells of margin, when that is at most 2^24 cells (byte offsets
+// then stay exact in fp32; 128 MiB).  Built on `s` and waited for when the
+// seed or the range changes (a parameter change, not per frame).
+static vr_status ensure_lattice(Ctx* c, ProcParams* q, hipStream_t s)
+{
+    double lo_c = 0.0, hi_c = 0.0;
+    float f = q->freq0;
+    for (int o = 0; o < q->octaves; ++o) {
+        const double G = (double)q->grid_scale * (double)f;
+        lo_c = std::min(lo_c, G);
+        hi_c = std::max(hi_c, G);
+        f = f * q->lacunarity;
+    }
+    if (!(hi_c - lo_c < 1.0e4) || q->octaves <= 0) return VR_OK;
+    const long long lo = (long long)std::floor(lo_c) - 2, n = (long long)std::ceil(hi_c) + 2 - lo + 1;
+    if (n * n * n > (1ll << 24)) return VR_OK;
+    const size_t bytes = (size_t)(n * n * n) * sizeof(uint2);
+    if (!(c->lat_key[0] == q->seed_fbm && c->lat_key[1] == lo && c->lat_key[2] == n)) {
+        // renders queued on other streams may still read the old table
+        HIP_TRY(hipDeviceSynchronize());
+        c->lat_key[2] = -1;
+        if (bytes > c->lat_cap) {
+            if (c->d_lat) (void)hipFree(c->d_lat);
+            c->d_lat = nullptr;
+            c->lat_cap = 0;
+            if (hipMalloc(&c->d_lat, bytes) != hipSuccess) return fail(VR_ERR_OOM, "vr_render: lattice table");
+            c->lat_cap = bytes;
+        }
+        HIP_TRY(launch_perlin_lattice(c->d_lat, q->seed_fbm, (int)lo, (int)n, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        c->lat_key[0] = q->seed_fbm;
+        c->lat_key[1] = lo;
+        c->lat_key[2] = n;
+    }
+    q->lat = c->d_lat;
+    q->lat_bytes = (unsigned)bytes;
+    q->lat_c = (float)(8 * lo * (1 + n + n * n));
+    q->lat_sy = (float)(8 * n);
+    q->lat_sz = (float)(8 * n * n);
+    return VR_OK;
+}
+
 vr_status vr_render(void* p, const vr_target* t, void* stream)
 {
     if (!p || !t) return fail(VR_ERR_INVALID, "vr_render: null argument");
@@ -945,6 +1003,11 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
         q.wt_lo = lo;
         q.wt_pz = q.wt_fixed ? 83 : small ? worley_z_pitch(n) : 0;
         q.wt_n = (small && (long long)n * q.wt_pz * 16 <= kMaxWorleyTableBytes) ? n : 0;   // + 8 KiB pairs
+        q.lat = nullptr;
+        if (q.wt_fixed && q.wt_n > 0 && c->lattice && c->schedule != SCHED_STATIC && c->schedule != SCHED_RINGS) {
+            const vr_status st = ensure_lattice(c, &q, static_cast<hipStream_t>(stream));
+            if (st != VR_OK) return st;
+        }
     }
     Plan pl{LAYOUT_PLANAR, WRAP_CLAMP, false};
     if (!c->proc.enabled) make_plan(c, &a, &pl);

@@ -133,6 +133,12 @@ struct ProcParams {
     int wt_lo, wt_n;  // Worley cell table in LDS: cells [wt_lo, wt_lo + wt_n)^3; wt_n = 0: none
     int wt_pz;        // its z pitch in entries (>= wt_n^2, padded against LDS bank aliasing)
     int wt_fixed;     // 1: the fixed geometry wt_n = 9, wt_pz = 83 (noise::cellular_table9)
+    // Perlin lattice table (global, noise::perlin_lattice_entry): cells
+    // [lat_lo, lat_lo + lat_n)^3, entry (x, y, z) at byte offset
+    // 8 x + lat_sy y + lat_sz z - lat_c, all exact in fp32.  Null: none.
+    const uint2* lat;
+    unsigned lat_bytes;
+    float lat_c, lat_sy, lat_sz;
 };
 
 // Everything one launch of the march kernel needs.  Passed by value
@@ -205,6 +211,8 @@ hipError_t launch_build_layout(int layout, const uint8_t* d_planar, int nx, int 
 size_t layout_plane_bytes(int layout, int nx, int ny, int nz);
 hipError_t launch_unpack(const uint8_t* d_planar, int nx, int ny, int nz, uint8_t* d_rgba,
                          hipStream_t s);
+// Perlin lattice table: entry (x, y, z) - lo of n^3 = noise::perlin_lattice_entry(seed, x, y, z)
+hipError_t launch_perlin_lattice(uint2* d_out, int seed, int lo, int n, hipStream_t s);
 hipError_t launch_noise(int kind, float* d_out, int x0, int y0, int z0, int nx, int ny, int nz,
                         float freq, int32_t seed, float* d_partials, int* num_partials,
                         hipStream_t s);

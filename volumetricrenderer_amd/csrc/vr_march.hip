@@ -55,12 +55,14 @@ hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_bu
         // the scatter advanced cursor[k] to the end of key k; total stays at cursor[kKeyBins]
         const dim3 g4((unsigned)((pixels + kThreads - 1) / kThreads));
         const unsigned* total = cursor + kKeyBins;
-        // tables: 2 = the fixed 9-cell Worley geometry (compile-time offsets), 1 = runtime geometry
-        const int tm = wt_bytes ? (a.proc.wt_fixed ? 2 : 1) : 0;
+        // tables: 2 = the fixed 9-cell Worley geometry (compile-time offsets), 1 = runtime geometry,
+        // 3 = 2 + the Perlin lattice table
+        const int tm = wt_bytes ? (a.proc.wt_fixed ? (a.proc.lat ? 3 : 2) : 1) : 0;
         const int v = (shadow ? 4 : 0) | (early ? 2 : 0);
 #define VR_PS(S, E, T) hipLaunchKernelGGL((march_proc_sorted<S, E, T>), g4, dim3(kThreads), wt_bytes, s, a, order, total)
 #define VR_PS3(S, E) \
-    if (tm == 2) VR_PS(S, E, 2); \
+    if (tm == 3) VR_PS(S, E, 3); \
+    else if (tm == 2) VR_PS(S, E, 2); \
     else if (tm == 1) VR_PS(S, E, 1); \
     else VR_PS(S, E, 0)
         switch (v) {

@@ -444,7 +444,8 @@ __device__ __forceinline__ unsigned march_pixel(const MarchArgs& a, const FastCt
 // Procedural medium (BASELINE configs 2/3, build-defined; spec in
 // oracle/vr_oracle.h vro_procedural): fBm Perlin x (1 - Worley F1).
 // TABLE: 0 = direct noise, 1 = LDS tables with runtime Worley geometry,
-// 2 = LDS tables with the fixed 9-cell geometry (noise::cellular_table9)
+// 2 = LDS tables with the fixed 9-cell geometry (noise::cellular_table9),
+// 3 = 2 + the global Perlin lattice table (noise::perlin_lat)
 template <int TABLE>
 __device__ __forceinline__ float proc_density(const ProcParams& p, const float4* wt, float scale, float px, float py,
                                               float pz)
@@ -452,18 +453,41 @@ __device__ __forceinline__ float proc_density(const ProcParams& p, const float4*
     const float gs = noise::in_vgpr(p.grid_scale), lac = noise::in_vgpr(p.lacunarity), gain = noise::in_vgpr(p.gain);
     const float qx = px * gs, qy = py * gs, qz = pz * gs;
     float f = noise::in_vgpr(p.freq0), amp = 1.0f, fbm = 0.0f;
-    for (int o = 0; o < p.octaves; ++o) {
-        float pn;
-        if constexpr (TABLE == 2) pn = noise::perlin_gp(wt + noise::kWorleyN * noise::kWorleyPz, p.seed_fbm, qx * f, qy * f, qz * f);
-        else if constexpr (TABLE == 1) pn = noise::perlin_gp(wt + p.wt_n * p.wt_pz, p.seed_fbm, qx * f, qy * f, qz * f);
-        else pn = noise::perlin(p.seed_fbm, qx * f, qy * f, qz * f);
-        fbm = fmaf(amp, pn, fbm);
-        f = f * lac;
-        amp = amp * gain;
+    if constexpr (TABLE == 3) {
+        // the lattice word of octave o + 1 is loaded while octave o computes
+        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p.lat, (short)0, (int)p.lat_bytes, 0x00020000);
+        const float sy = noise::in_vgpr(p.lat_sy), sz = noise::in_vgpr(p.lat_sz), c = noise::in_vgpr(p.lat_c);
+        const float4* gp = wt + noise::kWorleyN * noise::kWorleyPz;
+        float x = qx * f, y = qy * f, z = qz * f;
+        float xs = floorf(x), ys = floorf(y), zs = floorf(z);
+        auto word = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (unsigned)fmaf(zs, sz, fmaf(ys, sy, fmaf(xs, 8.0f, -c))), 0, 0);
+        for (int o = 0; o < p.octaves; ++o) {
+            const uint2 w = make_uint2(word[0], word[1]);
+            const float cx = x, cy = y, cz = z, cxs = xs, cys = ys, czs = zs;
+            f = f * lac;
+            if (o + 1 < p.octaves) {
+                x = qx * f; y = qy * f; z = qz * f;
+                xs = floorf(x); ys = floorf(y); zs = floorf(z);
+                word = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (unsigned)fmaf(zs, sz, fmaf(ys, sy, fmaf(xs, 8.0f, -c))), 0, 0);
+            }
+            const float pn = noise::perlin_lat(gp, w, cx, cy, cz, cxs, cys, czs);
+            fbm = fmaf(amp, pn, fbm);
+            amp = amp * gain;
+        }
+    } else {
+        for (int o = 0; o < p.octaves; ++o) {
+            float pn;
+            if constexpr (TABLE == 2) pn = noise::perlin_gp(wt + noise::kWorleyN * noise::kWorleyPz, p.seed_fbm, qx * f, qy * f, qz * f);
+            else if constexpr (TABLE == 1) pn = noise::perlin_gp(wt + p.wt_n * p.wt_pz, p.seed_fbm, qx * f, qy * f, qz * f);
+            else pn = noise::perlin(p.seed_fbm, qx * f, qy * f, qz * f);
+            fbm = fmaf(amp, pn, fbm);
+            f = f * lac;
+            amp = amp * gain;
+        }
     }
     const float wf = noise::in_vgpr(p.worley_freq);
     float f1;
-    if constexpr (TABLE == 2) f1 = noise::cellular_table9(wt, p.wt_lo, qx * wf, qy * wf, qz * wf) + 1.0f;
+    if constexpr (TABLE >= 2) f1 = noise::cellular_table9(wt, p.wt_lo, qx * wf, qy * wf, qz * wf) + 1.0f;
     else if constexpr (TABLE == 1) f1 = noise::cellular_table(wt, p.wt_lo, p.wt_n, p.wt_pz, qx * wf, qy * wf, qz * wf) + 1.0f;
     else f1 = noise::cellular(p.seed_worley, qx * wf, qy * wf, qz * wf) + 1.0f;
     return fmaxf(fbm * (1.0f - f1), 0.0f) * noise::in_vgpr(scale);

@@ -145,6 +145,43 @@ __device__ inline float perlin_gp(const float4* __restrict__ gp, int32_t seed, f
     return 0.964921414852142333984375f * lerp(lerp(l00, l10, v), lerp(l01, l11, v), w);
 }
 
+// Perlin lattice table (the procedural march's global table, TABLE 3): for
+// every lattice cell (xs, ys, zs) the four byte offsets perlin_gp derives by
+// hashing for the cell's (y, z) edges -- (y0,z0), (y1,z0) in the low and high
+// 16 bits of .x, (y0,z1), (y1,z1) of .y.  The hash depends only on the seed
+// and the integer corners, and every octave of the fBm uses the same seed, so
+// one table serves all octaves.  Per octave the sample then costs one 8-byte
+// load and 4 mask/shift ops instead of 3 conversions, 11 multiplies, 14 xors
+// and the offset extraction.
+__device__ inline uint2 perlin_lattice_entry(int32_t seed, int ix, int iy, int iz)
+{
+    const int32_t x0 = wmul(ix, kPX), y0 = wmul(iy, kPY), z0 = wmul(iz, kPZ);
+    const int32_t x1 = wadd(x0, kPX), y1 = wadd(y0, kPY), z1 = wadd(z0, kPZ);
+    const int32_t s0 = seed ^ x0, s1 = seed ^ x1;
+    const int32_t y0z0 = y0 ^ z0, y1z0 = y1 ^ z0, y0z1 = y0 ^ z1, y1z1 = y1 ^ z1;
+    const unsigned o00 = pair_offset(s0 ^ y0z0, s1 ^ y0z0, 0xf0u, 0xf00u);
+    const unsigned o10 = pair_offset(s0 ^ y1z0, s1 ^ y1z0, 0xf0u, 0xf00u);
+    const unsigned o01 = pair_offset(s0 ^ y0z1, s1 ^ y0z1, 0xf0u, 0xf00u);
+    const unsigned o11 = pair_offset(s0 ^ y1z1, s1 ^ y1z1, 0xf0u, 0xf00u);
+    return make_uint2(o00 | (o10 << 16), o01 | (o11 << 16));
+}
+// perlin_gp with the edge offsets from the lattice table word w of cell
+// (xs, ys, zs) = floor(x, y, z): the same gradient pairs, fractions, fades and
+// lerps in the same order, so the value is perlin_gp's bit for bit.
+__device__ inline float perlin_lat(const float4* __restrict__ gp, uint2 w, float x, float y, float z, float xs,
+                                   float ys, float zs)
+{
+    const float xf0 = x - xs, yf0 = y - ys, zf0 = z - zs;
+    const float xf1 = xf0 - 1.0f, yf1 = yf0 - 1.0f, zf1 = zf0 - 1.0f;
+    const float u = quintic(xf0), v = quintic(yf0), w_ = quintic(zf0);
+    const vr_pf2 fx = {xf0, xf1};
+    const float l00 = gdot_pair_lerp(gp, w.x & 0xffffu, fx, yf0, zf0, u);
+    const float l10 = gdot_pair_lerp(gp, w.x >> 16, fx, yf1, zf0, u);
+    const float l01 = gdot_pair_lerp(gp, w.y & 0xffffu, fx, yf0, zf1, u);
+    const float l11 = gdot_pair_lerp(gp, w.y >> 16, fx, yf1, zf1, u);
+    return 0.964921414852142333984375f * lerp(lerp(l00, l10, v), lerp(l01, l11, v), w_);
+}
+
 __device__ __forceinline__ float simplex_corner(int32_t seed, int32_t xp, int32_t yp, int32_t zp,
                                                 float x, float y, float z)
 {
@@ -282,9 +319,23 @@ __device__ inline float cellular_table(const float4* __restrict__ tab, int lo, i
 // cellular_table with the fixed geometry the host picks for tables of at most
 // 9 cells per axis (kWorleyN = 9, z pitch kWorleyPz = 83: no bank aliasing
 // between cells one apart): the base offset is computed in fp32 (small exact
-// integers, one conversion) and the 27 reads take immediate offsets.
+// integers, one conversion) and the reads take immediate offsets.
+//
+// Pruned: feature points sit at distance kCellJitter (0.396) from their
+// cell's integer corner, so the 8 corners of the unit cube around the sample
+// (cells floor .. floor + 1 per axis, a subset of cellular()'s 27) usually
+// hold the minimum.  Each of the other 19 cells has one axis at distance
+// >= 1 + g_a from the sample (g_a = |coord - rint(coord)|) and the others
+// at >= g_b, so its point is at least sqrt(T + 1 + 2 min g) - jitter away
+// (T = sum g^2).  Only lanes whose cube minimum d does not beat that bound
+// evaluate all 27 cells; a wave with no such lane skips them.  fminf is exact
+// and order-free, and skipped cells are provably farther than d (margin
+// kPruneR - jitter = 5.6e-5 in distance, >> fp32 rounding of the distance
+// sums), so the result is bit-identical to cellular().  Modelled on config 2
+// (tools/worley_prune_model.py): 94 % of wave-steps need the cube only.
 constexpr int kWorleyN = 9, kWorleyPz = 83;
-__device__ inline float cellular_table9(const float4* __restrict__ tab, int lo, float x, float y, float z)
+constexpr float kPruneR = 0.3962f;
+__device__ inline float cellular_table9_full(const float4* __restrict__ tab, int lo, float x, float y, float z)
 {
     const float xr = rintf(x), yr = rintf(y), zr = rintf(z);
     const float c = (float)(16 * (1 + lo) * (1 + kWorleyN + kWorleyPz));
@@ -308,6 +359,37 @@ __device__ inline float cellular_table9(const float4* __restrict__ tab, int lo, 
             }
         }
     }
+    return d0;
+}
+__device__ inline float cellular_table9(const float4* __restrict__ tab, int lo, float x, float y, float z)
+{
+    const float xf = floorf(x), yf = floorf(y), zf = floorf(z);
+    // cellular()'s xcf = (integer cell coordinate) - x for the cube's two cells per axis
+    const float x0 = xf - x, x1 = (xf + 1.0f) - x;
+    const float y0 = yf - y, y1 = (yf + 1.0f) - y;
+    const float z0 = zf - z, z1 = (zf + 1.0f) - z;
+    const float c = (float)(16 * lo * (1 + kWorleyN + kWorleyPz));
+    const float fo = fmaf(zf, (float)(16 * kWorleyPz), fmaf(yf, (float)(16 * kWorleyN), fmaf(xf, 16.0f, -c)));
+    const float4* t0 = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(tab) + (int)fo);
+    float d0 = 3.402823466e+38f;
+#pragma unroll
+    for (int xi = 0; xi <= 1; ++xi) {
+#pragma unroll
+        for (int yi = 0; yi <= 1; ++yi) {
+#pragma unroll
+            for (int zi = 0; zi <= 1; ++zi) {
+                const float4 cc = t0[zi * kWorleyPz + yi * kWorleyN + xi];
+                const float xd = fmaf(cc.x, cc.w, xi ? x1 : x0);
+                const float yd = fmaf(cc.y, cc.w, yi ? y1 : y0);
+                const float zd = fmaf(cc.z, cc.w, zi ? z1 : z0);
+                d0 = fminf(d0, fmaf(zd, zd, fmaf(yd, yd, xd * xd)));
+            }
+        }
+    }
+    const float gx = fminf(-x0, x1), gy = fminf(-y0, y1), gz = fminf(-z0, z1);
+    const float bound = fmaf(2.0f, fminf(gx, fminf(gy, gz)), fmaf(gz, gz, fmaf(gy, gy, fmaf(gx, gx, 1.0f))));
+    const float e = __builtin_amdgcn_sqrtf(d0) + kPruneR;
+    if (e * e > bound) d0 = fminf(d0, cellular_table9_full(tab, lo, x, y, z));
     return d0 - 1.0f;
 }
 

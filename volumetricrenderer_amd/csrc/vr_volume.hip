@@ -422,6 +422,23 @@ hipError_t launch_noise(int kind, float* d_out, int x0, int y0, int z0, int nx, 
     return hipGetLastError();
 }
 
+__global__ __launch_bounds__(kBlock) void k_perlin_lattice(uint2* __restrict__ out, int seed, int lo, int n)
+{
+    const long long total = (long long)n * n * n;
+    for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < total; i += (long long)gridDim.x * kBlock) {
+        const int ix = (int)(i % n), iy = (int)((i / n) % n), iz = (int)(i / ((long long)n * n));
+        out[i] = noise::perlin_lattice_entry(seed, lo + ix, lo + iy, lo + iz);
+    }
+}
+
+hipError_t launch_perlin_lattice(uint2* d_out, int seed, int lo, int n, hipStream_t s)
+{
+    const long long total = (long long)n * n * n;
+    const long long blocks = std::min<long long>((total + kBlock - 1) / kBlock, 8192);
+    hipLaunchKernelGGL(k_perlin_lattice, dim3((unsigned)blocks), dim3(kBlock), 0, s, d_out, seed, lo, n);
+    return hipGetLastError();
+}
+
 hipError_t launch_minmax_reduce(const float* d_partials, int num_partials, float* d_minmax, hipStream_t s)
 {
     hipLaunchKernelGGL(k_minmax, dim3(1), dim3(kBlock), 0, s, reinterpret_cast<const float2*>(d_partials),
