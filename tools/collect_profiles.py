@@ -34,8 +34,17 @@ def main():
         shutil.copy(stats, os.path.join(out, f"{tag}_{c}_kernel_stats.csv"))
         march = [r for r in csv.DictReader(open(stats)) if "march" in r["Name"]]
         top = max(march, key=lambda r: float(r["TotalDurationNs"]))
+        # the timed launches only: the last `steps` dispatches of that kernel in the trace
+        timed = ""
+        trace = stats.replace("kernel_stats.csv", "kernel_trace.csv")
+        if os.path.exists(trace):
+            rows = [r for r in csv.DictReader(open(trace)) if r.get("Kernel_Name") == top["Name"]]
+            last = rows[-bench["steps"]:]
+            if last:
+                ms = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in last) / len(last) / 1e6
+                timed = f" (timed {len(last)}: {ms:.4f} ms)"
         print(f"{c:13s} bench {bench['value']:>14,.1f} {bench['unit']}  kernel(events) {bench['kernel_ms_mean']:.4f} ms  "
-              f"rocprof {top['Name'][:60]} avg {float(top['AverageNs']) / 1e6:.4f} ms x{top['Calls']}  "
+              f"rocprof {top['Name'][:60]} avg {float(top['AverageNs']) / 1e6:.4f} ms x{top['Calls']}{timed}  "
               f"roofline {bench['roofline']['frac']}")
 
 

@@ -5,10 +5,12 @@
 set -u
 OUT=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out
 mkdir -p "$OUT"; export TMPDIR=/tmp
+if [ -z "${SKIP_TESTS:-}" ]; then   # SKIP_TESTS=1: suite and smoke already run in an earlier call
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
 rc=$?; tail -1 "$OUT/pytest_gpu.log"; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { tail "$OUT/smoke.log"; exit 3; }
 tail -1 "$OUT/smoke.log"
+fi
 PMC_LIST="FETCH_SIZE
 WRITE_SIZE" timeout -k 10 400 bash tools/pmc.sh traffic512 --size 512 --frames 20 || exit 9
 python tools/traffic_json.py traffic512 grid512 profiles/traffic.json || exit 9

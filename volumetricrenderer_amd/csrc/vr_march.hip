@@ -40,26 +40,26 @@ hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_bu
         const long long pixels = (long long)a.width * a.out_rows;
         static_assert(kSortRegion * kSortRegion == 256 * kSortPixelsPerThread, "one 64x64 region per sort block");
         const dim3 g1((unsigned)(((a.width + kSortRegion - 1) / kSortRegion) * ((a.out_rows + kSortRegion - 1) / kSortRegion)));
-        if (reuse_sort) {
-            // same geometry as the frame that built keys / order / total: only
-            // the pixels without steps need writing before the march
-            const unsigned positions = g1.x * 256u * kSortPixelsPerThread;
-            hipLaunchKernelGGL(proc_fill_background, dim3((positions + 256 * 16 - 1) / (256 * 16)), dim3(256), 0, s, a,
-                               keys, positions);
-        } else {
+        // same geometry as the frame that built keys / order / total: only the
+        // pixels without steps need writing, by trailing blocks of the march
+        const unsigned positions = reuse_sort ? g1.x * 256u * kSortPixelsPerThread : 0u;
+        if (!reuse_sort) {
             if (shadow) hipLaunchKernelGGL((proc_bin<true>), g1, dim3(256), 0, s, a, hist, keys);
             else hipLaunchKernelGGL((proc_bin<false>), g1, dim3(256), 0, s, a, hist, keys);
             hipLaunchKernelGGL(proc_scan, dim3(1), dim3(kKeyBins), 0, s, hist, cursor);
             hipLaunchKernelGGL(proc_scatter, g1, dim3(256), 0, s, a, keys, cursor, order);
         }
         // the scatter advanced cursor[k] to the end of key k; total stays at cursor[kKeyBins]
-        const dim3 g4((unsigned)((pixels + kThreads - 1) / kThreads));
+        const unsigned march_blocks = (unsigned)((pixels + kThreads - 1) / kThreads);
+        const dim3 g4(march_blocks + (positions + kThreads * 16 - 1) / (kThreads * 16));
         const unsigned* total = cursor + kKeyBins;
         // tables: 2 = the fixed 9-cell Worley geometry (compile-time offsets), 1 = runtime geometry,
         // 3 = 2 + the Perlin lattice table
         const int tm = wt_bytes ? (a.proc.wt_fixed ? (a.proc.lat ? 3 : 2) : 1) : 0;
         const int v = (shadow ? 4 : 0) | (early ? 2 : 0);
-#define VR_PS(S, E, T) hipLaunchKernelGGL((march_proc_sorted<S, E, T>), g4, dim3(kThreads), wt_bytes, s, a, order, total)
+#define VR_PS(S, E, T) \
+    hipLaunchKernelGGL((march_proc_sorted<S, E, T>), g4, dim3(kThreads), wt_bytes, s, a, order, total, keys, positions, \
+                       march_blocks)
 #define VR_PS3(S, E) \
     if (tm == 3) VR_PS(S, E, 3); \
     else if (tm == 2) VR_PS(S, E, 2); \

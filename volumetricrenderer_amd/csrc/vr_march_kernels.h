@@ -1115,10 +1115,11 @@ __global__ __launch_bounds__(256) void proc_bin(const MarchArgs a, unsigned* __r
 // pixels with no steps (key 0 in the bin pass) get (0,0,0,1), which is both
 // the clear colour and the epilogue of zero steps in every format, so this is
 // exactly what proc_bin stores for them.
-__global__ __launch_bounds__(256) void proc_fill_background(const MarchArgs a, const unsigned short* __restrict__ keys,
-                                                            unsigned positions)
+// Run by the trailing blocks of march_proc_sorted (one launch per reused frame).
+__device__ __forceinline__ void proc_fill_background(const MarchArgs& a, const unsigned short* __restrict__ keys,
+                                                     unsigned positions, unsigned block, unsigned blocks)
 {
-    for (unsigned i = blockIdx.x * 256u + threadIdx.x; i < positions; i += gridDim.x * 256u) {
+    for (unsigned i = block * kThreads + threadIdx.x; i < positions; i += blocks * kThreads) {
         int x, orow;
         if (!sort_pixel(a, i, &x, &orow) || keys[i] != 0) continue;
         const int bl = orow / a.band_rows;
@@ -1177,8 +1178,16 @@ __global__ __launch_bounds__(256) void proc_fill_background(const MarchArgs a, c
 
 template <bool SHADOW, bool EARLY, int TABLE>
 __global__ __launch_bounds__(kThreads) void march_proc_sorted(const MarchArgs a, const unsigned* __restrict__ order,
-                                                              const unsigned* __restrict__ total_ptr)
+                                                              const unsigned* __restrict__ total_ptr,
+                                                              const unsigned short* __restrict__ keys,
+                                                              unsigned fill_positions, unsigned fill_first)
 {
+    // A reused sort order (vr_render): blocks from fill_first on write the
+    // pixels without steps instead of marching, so a frame is one launch
+    if (blockIdx.x >= fill_first) {
+        proc_fill_background(a, keys, fill_positions, blockIdx.x - fill_first, gridDim.x - fill_first);
+        return;
+    }
     extern __shared__ float4 wt_lds[];
     const float4* wt = worley_table<TABLE>(a.proc, wt_lds);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
