@@ -163,7 +163,10 @@ vr_status vr_noise_grid(void* ctx, int kind, void* d_out, int x0, int y0, int z0
 /* Exhaustive device self-test of an arithmetic shortcut against its IEEE
  * definition; *failures = number of mismatching inputs (synchronous).
  * "cell_inv" (the cellular cell-point magnitude that the noise kernels use)
- * and the candidates "cell_inv_a", "cell_inv_b", "cell_inv_c".           */
+ * and the candidates "cell_inv_a", "cell_inv_b", "cell_inv_c";
+ * "worley_prune": the procedural march's pruned Worley F1 against the full
+ * 27-cell one on 2^23 points per seed (uniform, and at the bound's edge
+ * cases: rint and floor switches, feature points, near ties).            */
 vr_status vr_selftest(void* ctx, const char* name, long long* failures);
 
 /* ---- uniforms: replaces UniformBuffer<T>::Update x2 (TestMain.cpp:248-249,

@@ -496,6 +496,15 @@ def test_cellular_inv_shortcut_exhaustive(r):
         r.selftest("nope")
 
 
+def test_worley_pruning_bit_exact(r):
+    """The pruned Worley F1 of the procedural march (8-cell cube, the other
+    19 cells only when the distance bound needs them) equals the full
+    27-cell cellular() bit for bit on 2^23 points per seed, including points
+    a few ulps around the rint / floor switches, at feature points and
+    between two of them (vr_selftest "worley_prune")."""
+    assert r.selftest("worley_prune") == 0
+
+
 def translated_shader_data(W, H, t):
     """Reference camera with Model = translate(t) and W2L = its inverse, so the
     projected box centre leaves the screen centre (ring schedule centring)."""

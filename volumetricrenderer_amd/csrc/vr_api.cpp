@@ -520,9 +520,9 @@ vr_status vr_noise_grid(void* p, int kind, void* d_out, int x0, int y0, int z0, 
 vr_status vr_selftest(void* p, const char* name, long long* failures)
 {
     if (!p || !name || !failures) return fail(VR_ERR_INVALID, "vr_selftest: null argument");
-    static const char* const kNames[] = {"cell_inv_a", "cell_inv_b", "cell_inv_c", "cell_inv"};
+    static const char* const kNames[] = {"cell_inv_a", "cell_inv_b", "cell_inv_c", "cell_inv", "worley_prune"};
     int variant = -1;
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 5; ++i)
         if (std::strcmp(name, kNames[i]) == 0) variant = i;
     if (variant < 0) return fail(VR_ERR_INVALID, "vr_selftest: unknown test '%s'", name);
     Ctx* c = as_ctx(p);
@@ -531,7 +531,12 @@ vr_status vr_selftest(void* p, const char* name, long long* failures)
     HIP_TRY(hipMalloc(&d, sizeof *d));
     unsigned long long h = 0;
     hipError_t e = hipMemset(d, 0, sizeof *d);
-    if (e == hipSuccess) e = launch_selftest_cell_inv(variant, d, nullptr);
+    if (variant == 4) {   // three seeds, the recipe's Worley seed among them
+        for (int seed : {2, 1337, -987654321})
+            if (e == hipSuccess) e = launch_selftest_worley(seed, d, nullptr);
+    } else if (e == hipSuccess) {
+        e = launch_selftest_cell_inv(variant, d, nullptr);
+    }
     if (e == hipSuccess) e = hipMemcpy(&h, d, sizeof h, hipMemcpyDeviceToHost);
     (void)hipFree(d);
     if (e != hipSuccess) return fail(VR_ERR_HIP, "vr_selftest: %s", hipGetErrorString(e));

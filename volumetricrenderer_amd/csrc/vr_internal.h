@@ -227,6 +227,8 @@ hipError_t launch_assemble(const uint8_t* d_gathered, size_t rows_per_rank, int 
 int noise_partials_needed(int nx, int ny, int nz);
 // variant 0..2 = noise::cell_inv_a..c, 3 = the sequence cellular() uses
 hipError_t launch_selftest_cell_inv(int variant, unsigned long long* d_bad, hipStream_t s);
+// noise::cellular_table9 (pruned) vs noise::cellular on 2^23 points per seed
+hipError_t launch_selftest_worley(int seed, unsigned long long* d_bad, hipStream_t s);
 
 // host camera math (vr_camera.cpp)
 struct RayBasis {

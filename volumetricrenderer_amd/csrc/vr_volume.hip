@@ -493,6 +493,68 @@ __global__ __launch_bounds__(256) void k_selftest_cell_inv(int variant, unsigned
 }
 }  // namespace
 
+// Worley pruning (noise::cellular_table9) against the unpruned cellular():
+// bit-equal F1 on points drawn uniformly and at the edge cases of the bound
+// -- coordinates a few ulps around half-integers (the rint switch) and
+// integers (the floor switch), and points next to a feature point (F1 ~ 0)
+// or between two (near ties).  The table is the march's, cells [0, 9)^3
+// with z pitch 83; points keep rint +- 1 inside it.
+constexpr int kWorleyTestBlocks = 2048, kWorleyTestPerThread = 16;
+__global__ __launch_bounds__(256) void k_selftest_worley(int seed, unsigned long long* __restrict__ bad)
+{
+    __shared__ float4 tab[noise::kWorleyN * noise::kWorleyPz];
+    for (int i = threadIdx.x; i < noise::kWorleyN * noise::kWorleyN * noise::kWorleyN; i += 256) {
+        const int ix = i % noise::kWorleyN, iy = (i / noise::kWorleyN) % noise::kWorleyN, iz = i / (noise::kWorleyN * noise::kWorleyN);
+        tab[iz * noise::kWorleyPz + iy * noise::kWorleyN + ix] = noise::cellular_cell(seed, ix, iy, iz);
+    }
+    __syncthreads();
+    unsigned miss = 0;
+    for (int j = 0; j < kWorleyTestPerThread; ++j) {
+        const unsigned id = (blockIdx.x * 256u + threadIdx.x) * kWorleyTestPerThread + (unsigned)j;
+        unsigned h = id * 0x9E3779B1u + 0x85EBCA77u;
+        auto next = [&h]() { h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12; h *= 0x297A2D39u; h ^= h >> 15; return h; };
+        auto unit = [&]() { return (float)(next() >> 8) * (1.0f / 16777216.0f); };   // [0, 1)
+        float c[3];
+        const unsigned kind = id % 5u;
+        for (int a = 0; a < 3; ++a) c[a] = 1.0f + 6.0f * unit();   // [1, 7)
+        if (kind == 1 || kind == 2) {
+            // a few ulps around k + 0.5 (rint) or k (floor) on a random subset of axes
+            for (int a = 0; a < 3; ++a) {
+                if (next() & 1u) continue;
+                const float k = (float)(1 + (int)(next() % 6u)) + (kind == 1 ? 0.5f : 0.0f);
+                const int ulps = (int)(next() % 7u) - 3;
+                c[a] = __int_as_float(__float_as_int(k) + ulps);
+            }
+        } else if (kind == 3 || kind == 4) {
+            // next to a feature point (3), or between two neighbouring ones (4)
+            const int cx = 2 + (int)(next() % 5u), cy = 2 + (int)(next() % 5u), cz = 2 + (int)(next() % 5u);
+            const float4 f = tab[cz * noise::kWorleyPz + cy * noise::kWorleyN + cx];
+            float p[3] = {fmaf(f.x, f.w, (float)cx), fmaf(f.y, f.w, (float)cy), fmaf(f.z, f.w, (float)cz)};
+            if (kind == 4) {
+                const int a = (int)(next() % 3u);
+                const int dx = a == 0, dy = a == 1, dz = a == 2;
+                const float4 g = tab[(cz + dz) * noise::kWorleyPz + (cy + dy) * noise::kWorleyN + cx + dx];
+                const float q[3] = {fmaf(g.x, g.w, (float)(cx + dx)), fmaf(g.y, g.w, (float)(cy + dy)), fmaf(g.z, g.w, (float)(cz + dz))};
+                for (int b = 0; b < 3; ++b) p[b] = 0.5f * (p[b] + q[b]);
+            }
+            const float r = kind == 3 ? 1e-3f : 1e-5f;
+            for (int b = 0; b < 3; ++b) c[b] = fminf(fmaxf(p[b] + r * (2.0f * unit() - 1.0f), 0.51f), 7.49f);
+        }
+        const float got = noise::cellular_table9(tab, 0, c[0], c[1], c[2]);
+        const float want = noise::cellular(seed, c[0], c[1], c[2]);
+        miss += __float_as_uint(got) != __float_as_uint(want);
+    }
+    unsigned long long cnt = miss;
+    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+    if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(bad, cnt);
+}
+
+hipError_t launch_selftest_worley(int seed, unsigned long long* d_bad, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_selftest_worley, dim3(kWorleyTestBlocks), dim3(256), 0, s, seed, d_bad);
+    return hipGetLastError();
+}
+
 hipError_t launch_selftest_cell_inv(int variant, unsigned long long* d_bad, hipStream_t s)
 {
     constexpr unsigned kCount = (3u * 1023u * 1023u - 3u) / 8u + 1u;
