@@ -206,7 +206,7 @@ vr_status vr_shard_alloc(void* ctx, int nranks, int rank, int width, int height,
     sh->device = dev;
     hip_ok(hipStreamCreateWithFlags(&sh->comm_stream, hipStreamNonBlocking), "comm stream");
     hip_ok(hipEventCreateWithFlags(&sh->fence, hipEventDisableTiming), "event");
-    hip_ok(hipMalloc(&sh->token, sizeof(int)), "barrier token");
+    if (hip_ok(hipMalloc(&sh->token, sizeof(int)), "barrier token")) hip_ok(hipMemset(sh->token, 0, sizeof(int)), "barrier token");
     for (int p = 0; p < 2 && st == VR_OK; ++p) {
         hip_ok(hipEventCreateWithFlags(&sh->rendered[p], hipEventDisableTiming), "event");
         hip_ok(hipEventCreateWithFlags(&sh->done[p], hipEventDisableTiming), "event");
