@@ -80,6 +80,16 @@ vr_status vr_shard_run(vr_shard* sh, int frames, void* stream, int sample_every,
  * brackets its timed frames with it.  Loopback: a stream synchronisation. */
 vr_status vr_shard_barrier(vr_shard* sh, void* stream);
 
+/* Collective, once per volume (SURVEY.md sec. 8e collective 1): rank 0's
+ * RGBA8 volume (device pointer, nz x ny x nx x 4 bytes, x fastest; ignored on
+ * the other ranks) goes to every rank with one ncclBroadcast over xGMI, and
+ * every rank's ctx installs it as vr_set_volume_device would.  All ranks
+ * name the same extent; they agree on it and on every receive buffer (one
+ * all-reduce) before the broadcast, so a failure on one rank fails all of
+ * them instead of leaving peers blocked.  Synchronous: returns once this
+ * rank's ctx holds the volume.  Loopback: vr_set_volume_device. */
+vr_status vr_shard_share_volume(vr_shard* sh, const void* d_rgba8, int nx, int ny, int nz, void* stream);
+
 /* Rank 0: the last assembled frame (device pointer, tight rows) once
  * `stream` of the last vr_shard_run has reached it.  Other ranks: their
  * last band set. */

@@ -32,12 +32,14 @@ def test_shard_library_exports_every_declared_symbol():
     from volumetricrenderer_amd import _lib
     lib = _lib.load_shard()
     declared = header_functions("vr_shard.h")
-    assert len(declared) == 11
+    assert len(declared) == 12
     for name in declared:
         assert hasattr(lib, name), name
     assert sorted(declared) == _lib.shard_exported_symbols()
     with pytest.raises(_lib.VRError):
         _lib.shard_call("vr_shard_create", None, None, 1, 0, 64, 64, 1, 16, ctypes.byref(ctypes.c_void_p()))
+    with pytest.raises(_lib.VRError):   # argument check only, no GPU
+        _lib.shard_call("vr_shard_share_volume", None, None, 8, 8, 8, None)
 
 
 def test_abi_struct_layouts():

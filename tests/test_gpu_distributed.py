@@ -20,20 +20,27 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, share=False):
     import sys
     sys.path.insert(0, ROOT)
     import torch.distributed as dist
 
     import volumetricrenderer_amd as vr
-    from volumetricrenderer_amd.distributed import BandSharder
+    from volumetricrenderer_amd.distributed import BandSharder, share_volume
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         torch.cuda.set_device(0)
         W, H = 640, 360
         with vr.Renderer(0) as r:
-            r.generate_volume(vr.volume_recipe_defaults(size=64))
+            if share:   # only rank 0 makes the volume; the others receive it (SURVEY.md 8e collective 1)
+                vol = None
+                if rank == 0:
+                    r.generate_volume(vr.volume_recipe_defaults(size=64))
+                    vol = r.get_volume()
+                share_volume(r, vol, rank=rank)
+            else:
+                r.generate_volume(vr.volume_recipe_defaults(size=64))
             osd, gsd = vr.reference_shader_data(W / H, 10.0, 20.0)
             r.set_shader_data(osd, gsd)
             r.set_march(vr.march_defaults())
@@ -52,13 +59,15 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gloo_ranks_on_one_gpu_assemble_the_frame(world):
+@pytest.mark.parametrize("world,share", [(2, False), (3, False), (3, True)])
+def test_gloo_ranks_on_one_gpu_assemble_the_frame(world, share):
+    """share=True: the volume exists only on rank 0 and reaches the others
+    through distributed.share_volume before the frame."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(rk, world, port, q)) for rk in range(world)]
+    procs = [ctx.Process(target=_worker, args=(rk, world, port, q, share)) for rk in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in procs]
@@ -125,5 +134,45 @@ def test_native_pipeline_loopback_ranks(world, band_rows, fmt):
             full = r.render(W, H, fmt)
             torch.cuda.synchronize()
             assert np.array_equal(got.cpu().numpy(), full.cpu().numpy())
+        finally:
+            pl.close()
+
+
+@pytest.mark.parametrize("world,loopback", [(1, False), (4, True)])
+def test_native_share_volume(world, loopback):
+    """vr_shard_share_volume: rank 0's device volume installed through the
+    native pipeline -- over a one-rank RCCL communicator (the agreement
+    all-reduce and the in-place broadcast run for real) or in loopback.  The
+    renderer started without a volume; afterwards it holds exactly those
+    bytes and the pipeline's frame equals a plain render of them by a second
+    renderer."""
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import vr_oracle as oracle
+
+    import volumetricrenderer_amd as vr
+    from volumetricrenderer_amd.distributed import RcclBandPipeline
+    W, H = 400, 240
+    vol = oracle.build_volume(40)
+    osd, gsd = vr.reference_shader_data(W / H, 15.0, -25.0)
+    with vr.Renderer(0) as r, vr.Renderer(0) as ref:
+        r.set_shader_data(osd, gsd)
+        r.set_march(vr.march_defaults())
+        pl = RcclBandPipeline(r, W, H, vr.FMT_RGBA32F, band_rows=16, world=world, rank=0, loopback=loopback)
+        try:
+            pl.share_volume(torch.from_numpy(vol).cuda())
+            assert np.array_equal(r.get_volume(), vol)
+            pl.run_frames(2)
+            pl.barrier()
+            got = pl.frame()
+            ref.set_volume(vol)
+            ref.set_shader_data(osd, gsd)
+            ref.set_march(vr.march_defaults())
+            full = ref.render(W, H, vr.FMT_RGBA32F)
+            torch.cuda.synchronize()
+            assert np.array_equal(got.cpu().numpy(), full.cpu().numpy())
+            with pytest.raises(ValueError):   # not RGBA8
+                pl.share_volume(torch.zeros((4, 4, 4, 3), dtype=torch.uint8, device="cuda"))
         finally:
             pl.close()

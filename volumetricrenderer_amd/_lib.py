@@ -183,6 +183,7 @@ _SHARD_SIGS = {
     "vr_shard_copy_frame": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, _vp]),
     "vr_shard_rows": (ctypes.c_int, [_vp, c_int_p, c_int_p]),
     "vr_shard_barrier": (ctypes.c_int, [_vp, _vp]),
+    "vr_shard_share_volume": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp]),
 }
 _shard_lib = None
 

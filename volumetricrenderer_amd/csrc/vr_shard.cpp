@@ -80,7 +80,8 @@ struct vr_shard {
     uint8_t* frame[2] = {};           // rank 0
     hipEvent_t rendered[2] = {}, done[2] = {};
     hipEvent_t fence = nullptr;       // vr_shard_barrier: the caller's stream -> comm stream
-    int* token = nullptr;             // vr_shard_barrier: one int all-reduced over the ranks
+    int* token = nullptr;             // [0]: vr_shard_barrier's all-reduced int; [1..7]:
+                                      // vr_shard_share_volume's agreement vector
     bool pending[2] = {};             // done[p] recorded and not yet waited on
     int last = -1;                    // parity of the last frame
     bool loopback = false;            // one process emulates all ranks (no RCCL)
@@ -206,7 +207,8 @@ vr_status vr_shard_alloc(void* ctx, int nranks, int rank, int width, int height,
     sh->device = dev;
     hip_ok(hipStreamCreateWithFlags(&sh->comm_stream, hipStreamNonBlocking), "comm stream");
     hip_ok(hipEventCreateWithFlags(&sh->fence, hipEventDisableTiming), "event");
-    if (hip_ok(hipMalloc(&sh->token, sizeof(int)), "barrier token")) hip_ok(hipMemset(sh->token, 0, sizeof(int)), "barrier token");
+    if (hip_ok(hipMalloc(&sh->token, 8 * sizeof(int)), "barrier token"))
+        hip_ok(hipMemset(sh->token, 0, 8 * sizeof(int)), "barrier token");
     for (int p = 0; p < 2 && st == VR_OK; ++p) {
         hip_ok(hipEventCreateWithFlags(&sh->rendered[p], hipEventDisableTiming), "event");
         hip_ok(hipEventCreateWithFlags(&sh->done[p], hipEventDisableTiming), "event");
@@ -322,6 +324,76 @@ vr_status vr_shard_barrier(vr_shard* sh, void* stream)
     HIP_TRY(hipStreamSynchronize(sh->comm_stream));
     HIP_TRY(hipStreamSynchronize(s));
     return VR_OK;
+}
+
+// SURVEY.md sec. 8e collective (1): the volume, once, from rank 0 to every
+// rank over xGMI (the reference uploads it once per process, Texture3D,
+// VulkanTexture.cpp:111-156).  The ranks first agree -- one all-reduce (max)
+// of {failed, nx, ny, nz, -nx, -ny, -nz} -- that every receive buffer exists
+// and every rank named the same extent, so no rank enters the broadcast
+// alone; then one ncclBroadcast of the RGBA8 bytes and, on every rank,
+// vr_set_volume_device (repack + fast layout), ordered on `stream`.
+vr_status vr_shard_share_volume(vr_shard* sh, const void* d_rgba8, int nx, int ny, int nz, void* stream)
+{
+    if (!sh) return fail(VR_ERR_INVALID, "vr_shard_share_volume: null shard");
+    if (sh->loopback && sh->rank != 0)
+        return fail(VR_ERR_INVALID, "vr_shard_share_volume: rank %d is not connected (vr_shard_connect)", sh->rank);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    HIP_TRY(hipSetDevice(sh->device));
+    if (sh->loopback) {   // one process holds every rank's work: nothing to send
+        if (!d_rgba8) return fail(VR_ERR_INVALID, "vr_shard_share_volume: rank 0 needs the volume");
+        VR_TRY(vr_set_volume_device(sh->ctx, d_rgba8, nx, ny, nz, stream));
+        HIP_TRY(hipStreamSynchronize(s));
+        return VR_OK;
+    }
+    int failed = (nx <= 0 || ny <= 0 || nz <= 0 || (sh->rank == 0 && !d_rgba8)) ? 1 : 0;
+    const size_t bytes = failed ? 0 : (size_t)nx * ny * nz * 4;
+    uint8_t* buf = nullptr;
+    if (!failed && sh->rank != 0 && hipMalloc(&buf, bytes) != hipSuccess) {
+        buf = nullptr;
+        failed = 1;
+    }
+    const int agree[7] = {failed, nx, ny, nz, -nx, -ny, -nz};
+    int got[7] = {};
+    hipError_t he = hipMemcpyAsync(sh->token + 1, agree, sizeof agree, hipMemcpyHostToDevice, sh->comm_stream);
+    ncclResult_t nr = ncclSuccess;
+    if (he == hipSuccess)
+        nr = ncclAllReduce(sh->token + 1, sh->token + 1, 7, ncclInt32, ncclMax, sh->comm, sh->comm_stream);
+    if (he == hipSuccess && nr == ncclSuccess)
+        he = hipMemcpyAsync(got, sh->token + 1, sizeof got, hipMemcpyDeviceToHost, sh->comm_stream);
+    if (he == hipSuccess) he = hipStreamSynchronize(sh->comm_stream);
+    if (he != hipSuccess || nr != ncclSuccess) {
+        if (buf) (void)hipFree(buf);
+        if (nr != ncclSuccess) return fail(VR_ERR_HIP, "vr_shard_share_volume: agreement: %s", ncclGetErrorString(nr));
+        return fail(VR_ERR_HIP, "vr_shard_share_volume: agreement: %s", hipGetErrorString(he));
+    }
+    if (got[0] || got[1] != -got[4] || got[2] != -got[5] || got[3] != -got[6]) {
+        if (buf) (void)hipFree(buf);
+        if (failed) return fail(VR_ERR_INVALID, "vr_shard_share_volume: rank %d: bad extent, no volume or no memory", sh->rank);
+        if (got[0]) return fail(VR_ERR_INVALID, "vr_shard_share_volume: failed on another rank");
+        return fail(VR_ERR_INVALID, "vr_shard_share_volume: ranks named different extents");
+    }
+    void* data = sh->rank == 0 ? const_cast<void*>(d_rgba8) : buf;
+    // the broadcast after the caller's stream (rank 0 may have produced the volume
+    // on it), the install after the broadcast
+    he = hipEventRecord(sh->fence, s);
+    if (he == hipSuccess) he = hipStreamWaitEvent(sh->comm_stream, sh->fence, 0);
+    if (he == hipSuccess) {
+        nr = ncclBroadcast(data, data, bytes, ncclUint8, 0, sh->comm, sh->comm_stream);
+        if (nr == ncclSuccess) {
+            he = hipEventRecord(sh->fence, sh->comm_stream);
+            if (he == hipSuccess) he = hipStreamWaitEvent(s, sh->fence, 0);
+        }
+    }
+    vr_status st = VR_OK;
+    if (nr != ncclSuccess) st = fail(VR_ERR_HIP, "vr_shard_share_volume: ncclBroadcast: %s", ncclGetErrorString(nr));
+    else if (he != hipSuccess) st = fail(VR_ERR_HIP, "vr_shard_share_volume: %s", hipGetErrorString(he));
+    else if (vr_set_volume_device(sh->ctx, data, nx, ny, nz, stream) != VR_OK)
+        st = fail(VR_ERR_HIP, "vr_shard_share_volume: vr_set_volume_device: %s", vr_last_error());
+    (void)hipStreamSynchronize(sh->comm_stream);
+    (void)hipStreamSynchronize(s);
+    if (buf) (void)hipFree(buf);
+    return st;
 }
 
 vr_status vr_shard_frame(vr_shard* sh, void** pixels, size_t* row_pitch, int* rows)

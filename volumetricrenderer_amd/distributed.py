@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import ctypes
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -25,6 +26,36 @@ from . import _lib
 def rows_for_rank(height: int, band_rows: int, world: int, rank: int) -> int:
     nb = (height + band_rows - 1) // band_rows
     return len(range(rank, nb, world)) * band_rows
+
+
+def share_volume(renderer, vol=None, rank: int = 0, group=None):
+    """Collective (collective 1): rank 0's RGBA8 volume
+    (nz, ny, nx, 4; numpy or tensor, ignored elsewhere) reaches every rank of
+    the torch.distributed group once, and each rank's `renderer` installs it
+    (``set_volume``).  The shape goes first, so the other ranks need nothing
+    but the call.  Over gloo the bytes travel as a CPU tensor, over nccl
+    (RCCL) as a device tensor.  Returns the volume as this rank received it."""
+    world = dist.get_world_size(group)
+    dev = "cuda" if dist.get_backend(group) == "nccl" else "cpu"
+    shape = torch.zeros(4, dtype=torch.int64, device=dev)
+    if rank == 0:
+        if vol is None:
+            raise ValueError("share_volume: rank 0 needs the volume")
+        t = vol if isinstance(vol, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(vol, dtype=np.uint8))
+        if t.dtype != torch.uint8 or t.dim() != 4 or t.shape[3] != 4:
+            raise ValueError("share_volume: the volume must be uint8 shaped (nz, ny, nx, 4)")
+        shape.copy_(torch.tensor(list(t.shape), dtype=torch.int64))
+    if world > 1:
+        dist.broadcast(shape, src=0, group=group)
+    dims = [int(v) for v in shape.tolist()]
+    if rank == 0:
+        data = t.to(dev).contiguous()
+    else:
+        data = torch.empty(dims, dtype=torch.uint8, device=dev)
+    if world > 1:
+        dist.broadcast(data, src=0, group=group)
+    renderer.set_volume(data if data.is_cuda else data.numpy())
+    return data
 
 
 class BandSharder:
@@ -198,7 +229,7 @@ class RcclBandPipeline:
         GPU and assembles them (no communicator; tests and rehearsals)."""
         self.r = renderer
         self.width, self.height, self.fmt = width, height, fmt
-        self.world, self.rank = world, rank
+        self.world, self.rank, self.group, self.loopback = world, rank, group, loopback
         uid = (ctypes.c_uint8 * _lib.SHARD_ID_BYTES)()
         err = None
         if loopback:
@@ -259,6 +290,28 @@ class RcclBandPipeline:
         _lib.shard_call("vr_shard_run", self._h, k, _stream_handle(stream), sample_every,
                         ctypes.byref(ms) if sample_every > 0 else None)
         return ms.value if sample_every > 0 else None
+
+    def share_volume(self, vol=None, stream=None) -> None:
+        """Collective, once per volume: rank 0's RGBA8 volume (a contiguous
+        uint8 CUDA tensor (nz, ny, nx, 4); ignored on other ranks) is
+        broadcast over this pipeline's own RCCL communicator and installed
+        in every rank's renderer (vr_shard_share_volume).  The extent goes
+        to the other ranks over the torch group first."""
+        from .renderer import _stream_handle
+        dims = torch.zeros(3, dtype=torch.int64)
+        if self.rank == 0:
+            if vol is None or not isinstance(vol, torch.Tensor) or not vol.is_cuda:
+                raise ValueError("share_volume: rank 0 needs the volume as a CUDA tensor")
+            if vol.dtype != torch.uint8 or vol.dim() != 4 or vol.shape[3] != 4 or not vol.is_contiguous():
+                raise ValueError("share_volume: the volume must be a contiguous uint8 tensor (nz, ny, nx, 4)")
+            dims = torch.tensor([vol.shape[2], vol.shape[1], vol.shape[0]], dtype=torch.int64)
+        if self.world > 1 and not self.loopback:
+            t = dims.to("cuda" if dist.get_backend(self.group) == "nccl" else "cpu")
+            dist.broadcast(t, src=0, group=self.group)
+            dims = t.cpu()
+        nx, ny, nz = (int(v) for v in dims.tolist())
+        ptr = ctypes.c_void_p(vol.data_ptr()) if self.rank == 0 else None
+        _lib.shard_call("vr_shard_share_volume", self._h, ptr, nx, ny, nz, _stream_handle(stream))
 
     def barrier(self, stream=None):
         """Collective: returns once every rank's queued frames (on `stream`
