@@ -1,0 +1,9 @@
+# Final check of a session: the whole GPU suite (verbose), smoke, the default bench line
+set -u
+OUT=$GRAFT_REPO_ROOT/gpurun_out; mkdir -p $OUT; export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo tests fail; tail -30 $OUT/pytest_gpu.log; exit 1; }
+tail -1 $OUT/pytest_gpu.log
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail $OUT/smoke.log; exit 3; }
+tail -1 $OUT/smoke.log
+timeout -k 10 300 python -u bench.py > $OUT/bench.log 2>&1 || { tail $OUT/bench.log; exit 4; }
+tail -1 $OUT/bench.log | cut -c1-300
