@@ -882,3 +882,26 @@ def test_wrap_mode_switch_at_the_margin(r, oracle, vol128, max_steps, edge):
             assert c == s
             seen.add(exact)
     assert seen == {True, False}   # both sides of the margin were exercised
+
+
+@pytest.mark.parametrize("W,H", [(1, 1), (1, 7), (9, 1), (2, 3), (8, 8), (65, 1)])
+@pytest.mark.parametrize("layout", [0, 12, 1])
+def test_tiny_and_ragged_frames(r, oracle, vol128, W, H, layout):
+    """Frames of one pixel, one row, one column and sizes around the 8x8 wave
+    tile, through the auto (cornerh), brick4832 and planar paths with the auto
+    (regions) schedule: exact, step counts too."""
+    r.set_layout_preference(layout)
+    try:
+        img, ref, c, s = render_both(r, oracle, vol128, W, H)
+        assert_exact(img, ref)
+        assert c == s
+    finally:
+        r.set_layout_preference(0)
+
+
+@pytest.mark.parametrize("W,H,shadow", [(1, 1, 0), (5, 3, 8), (1, 9, 8), (70, 2, 0)])
+def test_tiny_frames_procedural(r, oracle, W, H, shadow):
+    """The cost-sorted procedural path on frames smaller than one wave."""
+    img, ref, c, s, _ = render_proc_both(r, oracle, W, H, vr.march_defaults(), shadow_steps=shadow)
+    assert_exact(img, ref)
+    assert c == s

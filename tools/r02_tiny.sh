@@ -1,0 +1,6 @@
+set -u
+OUT=$GRAFT_REPO_ROOT/gpurun_out; mkdir -p $OUT; export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 120 --timeout-method thread -k "tiny" > $OUT/pytest_tiny.log 2>&1 || { echo tiny fail; tail -40 $OUT/pytest_tiny.log; exit 1; }
+tail -2 $OUT/pytest_tiny.log
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo tests fail; tail -30 $OUT/pytest_gpu.log; exit 1; }
+tail -1 $OUT/pytest_gpu.log
