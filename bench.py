@@ -61,17 +61,27 @@ CONFIGS = {
 }
 
 
-def flop_per_density(octaves: int) -> int:
+def flop_per_density(octaves: int, cells_per_eval: float | None = None) -> float:
     """Algorithmic fp32 FLOP of one procedural density evaluation, counted on
-    the minimal per-sample form (FMA = 2; add, sub, mul, min, max, floor,
-    rint = 1; integer hashing, table reads and int<->float conversions not
-    counted).  Per Perlin octave 67: floor 3, fraction subs 6, quintic 3 x 7,
-    8 gradient dots x 1 (u + v), 7 lerps x 3, scale 1, coordinate scale 3,
-    fbm fma 2, parameter updates 2.  Worley F1 346: rint 3, per-axis cell
-    offsets 18, per cell 12 (3 fma + squared distance 5 + min) x 27, final 1;
-    the cell's feature-point normalisation (hash, sqrt, divide) is per cell,
-    not per sample, and is not counted.  The rest 11."""
-    return 67 * octaves + 346 + 11
+    the algorithm the kernel runs (FMA = 2; add, sub, mul, min, max, floor,
+    rint, sqrt = 1; integer hashing, table reads and int<->float conversions
+    not counted).  Per Perlin octave 67: floor 3, fraction subs 6, quintic
+    3 x 7, 8 gradient dots x 1 (u + v), 7 lerps x 3, scale 1, coordinate scale
+    3, fbm fma 2, parameter updates 2.  Worley F1 (noise::cellular_table9,
+    pruned): setup 9 (floor 3, the cube's cell offsets 6), 12 per cell
+    computed (3 fma, squared distance 5, min) x cells_per_eval -- measured per
+    launch with vr option "count" = 2: 8 for the unit cube, 35 when a sample
+    also runs the 27-cell block --, the bound test 15 (3 min, T + 1 + 2 min g
+    5 fma/min, sqrt, add, square, compare), the full block's own setup 12
+    (rint 3, offsets 9) for the fraction (cells - 8) / 27 of samples that run
+    it, final 1; the cell's feature-point normalisation is per cell, not per
+    sample (LDS table), and is not counted.  The rest 11.
+    cells_per_eval None: the unpruned 27-cell F1 (round 2's count, 625 FLOP
+    at 4 octaves), kept as a secondary figure."""
+    if cells_per_eval is None:
+        return 67 * octaves + 346 + 11
+    full = max(0.0, (cells_per_eval - 8.0) / 27.0)
+    return 67 * octaves + 9 + 12 * cells_per_eval + 15 + 12 * full + 1 + 11
 
 
 def cpu_baseline(volume_host, osd, gsd, march, width, height, budget_s=10.0, procedural=None):
@@ -141,6 +151,9 @@ def main() -> int:
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch sharder's backend; gloo: rehearse the N>1 path with several ranks on one GPU")
     ap.add_argument("--pipeline1", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--spin", action="store_true",
+                    help="moving camera: every frame gets new shader data, phi += 1.6 deg (the reference's "
+                         "held A/D key, TestMain.cpp:171-184, :222-224); N = 1 only")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -151,6 +164,8 @@ def main() -> int:
     # --pipeline1: the native frame loop with a one-rank communicator at N = 1
     # (a rehearsal of the N > 1 host path on one GPU; not the default N = 1 line)
     native = (world > 1 and args.sharder == "native") or args.pipeline1
+    if args.spin and (world > 1 or args.pipeline1):
+        raise SystemExit("--spin: one GPU, one process (the shard loop renders a fixed camera)")
     if native and ndev < world:
         raise SystemExit(f"--sharder native needs one GPU per rank ({world} ranks, {ndev} GPUs); "
                          "use --sharder torch --backend gloo to rehearse on fewer GPUs")
@@ -186,12 +201,18 @@ def main() -> int:
     torch.cuda.synchronize()
     local_steps = int(counter.item())
     local_evals = local_steps
+    local_cells = None
     if proc is not None:
         r.set_option("count", 1)
         counter.zero_()
         sharder.render_local(step_counter=counter)
         torch.cuda.synchronize()
         local_evals = int(counter.item())
+        r.set_option("count", 2)   # Worley cells the pruned evaluations computed
+        counter.zero_()
+        sharder.render_local(step_counter=counter)
+        torch.cuda.synchronize()
+        local_cells = int(counter.item())
         r.set_option("count", 0)
     red_dev = "cuda" if args.backend == "nccl" and not native else "cpu"
     tot = torch.tensor([local_steps], dtype=torch.int64, device=red_dev)
@@ -231,6 +252,42 @@ def main() -> int:
         el = time.perf_counter() - t0
         if world > 1:
             dist.barrier()
+    elif args.spin:
+        # a spinning camera: new shader data before every frame, so the frame
+        # pays the region-list reuse / rebuild (grid) or the cost sort
+        # (procedural) that a static camera skips.  The shader data of every
+        # frame is made before the clock starts (host math, TestMain.cpp:219-245).
+        SPIN_DEG = 1.6
+        sd = [vr.reference_shader_data(1280.0 / 720.0, SPIN_DEG * i, 0.0) for i in range(args.warmup + args.steps)]
+        launch = r.prepare_render(W, H, fmt, sharder.local)
+        for i in range(args.warmup):
+            r.set_shader_data(*sd[i])
+            launch()
+        torch.cuda.synchronize()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              if i % ev_every == 0 else None for i in range(args.steps)]
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            r.set_shader_data(*sd[args.warmup + i])
+            if ev[i] is not None:
+                ev[i][0].record()
+            launch()
+            if ev[i] is not None:
+                ev[i][1].record()
+        host_el = time.perf_counter() - t0
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        kern_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev if e is not None]))
+        # the executed steps of the sampled frames (untimed): the roofline's unit
+        sampled = []
+        for i in range(args.steps):
+            if ev[i] is not None:
+                r.set_shader_data(*sd[args.warmup + i])
+                counter.zero_()
+                sharder.render_local(step_counter=counter)
+                torch.cuda.synchronize()
+                sampled.append(int(counter.item()))
+        local_steps = frame_steps = int(round(float(np.mean(sampled))))
     else:
         sharder.run_frames(args.warmup)
         if world > 1:
@@ -282,13 +339,21 @@ def main() -> int:
                                         "is cache-resident",
                         "gather_GBs": round(gather, 1)}
         else:
-            fpd = flop_per_density(proc.octaves)
+            cpe = local_cells / max(1, local_evals)
+            fpd = flop_per_density(proc.octaves, cpe)
+            fpd27 = flop_per_density(proc.octaves)
             achieved = local_evals * fpd / (kern_ms * 1e-3) / 1e12
+            a27 = local_evals * fpd27 / (kern_ms * 1e-3) / 1e12
             roofline = {"bound": "valu", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS,
                         "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None,
-                        "achieved_def": f"{fpd} algorithmic fp32 FLOP per density evaluation x "
+                        "achieved_def": f"{fpd:.1f} algorithmic fp32 FLOP per density evaluation (Perlin "
+                                        f"{67 * proc.octaves} + pruned Worley at {cpe:.3f} cells per evaluation, "
+                                        "measured with vr option count=2, + bound test, setup, rest) x "
                                         f"{local_evals} evaluations per launch / mean march-kernel duration "
-                                        "(HIP events on its stream); no volume is read"}
+                                        "(HIP events on its stream); no volume is read",
+                        "worley_cells_per_eval": round(cpe, 4),
+                        "flop_per_eval_27cell": fpd27,
+                        "frac_27cell": round(a27 / FP32_PEAK_TFLOPS, 4)}
         traffic = None
         tfile = os.path.join(ROOT, "profiles", "traffic.json")
         if os.path.exists(tfile):
@@ -315,12 +380,16 @@ def main() -> int:
                                     else f"{args.config}: procedural {proc.octaves}-octave Perlin-Worley cloud, "
                                          f"{W}x{H}, {S} steps, shadow {shadow} steps, RGBA8 out"),
                        "baseline_config_index": cfg_idx, "width": W, "height": H, "max_steps": S,
-                       "volume": f"{N}^3 RGBA8" if N else "procedural", "camera": "reference (TestMain.cpp:219-245)",
+                       "volume": f"{N}^3 RGBA8" if N else "procedural",
+                       "camera": ("reference (TestMain.cpp:219-245), spinning: phi += 1.6 deg per frame, new shader "
+                                  "data every frame (TestMain.cpp:171-184)" if args.spin
+                                  else "reference (TestMain.cpp:219-245)"),
                        "kernel": r.kernel_variant, "parallelism": f"bands16x{world}",
                        "collective": collective_label,
                        "executed_steps_per_frame": frame_steps},
             "executed_steps_per_s": round(frame_steps * args.steps / el, 1),
             "kernel_ms_mean": round(kern_ms, 5),
+            **({"host_ms_per_frame": round(host_el / args.steps * 1e3, 4)} if args.spin else {}),
             "kernel_ms_mean_max_rank": round(kern_ms_max, 5),
             "roofline": dict(roofline, traffic=traffic,
                              **({"traffic_GBs": round(traffic / (kern_ms * 1e-3) / 1e9, 1),

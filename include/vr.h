@@ -35,7 +35,9 @@ typedef enum {
     VR_ERR_NO_VOLUME = 3,   /* vr_render before vr_set_volume/generate     */
     VR_ERR_NO_CAMERA = 4,   /* vr_render before vr_set_shader_data         */
     VR_ERR_OOM = 5,         /* device allocation failed                    */
-    VR_ERR_NO_DEVICE = 6    /* no HIP device / bad device index            */
+    VR_ERR_NO_DEVICE = 6,   /* no HIP device / bad device index            */
+    VR_ERR_TIMEOUT = 7,     /* a collective (vr_shard.h) missed its deadline; communicator aborted */
+    VR_ERR_COMM = 8         /* communicator error (RCCL, vr_shard.h); communicator aborted */
 } vr_status;
 
 typedef enum {
@@ -150,6 +152,9 @@ vr_status vr_set_volume_device(void* ctx, const void* d_rgba8, int nx, int ny, i
 /* read the volume back as RGBA8 (host); for tests and tools             */
 vr_status vr_get_volume(void* ctx, uint8_t* rgba8_out);
 vr_status vr_volume_dims(void* ctx, int* nx, int* ny, int* nz);
+/* 1 if vr_set_volume / vr_set_volume_device accept an nx x ny x nz extent
+ * (the device layouts index a plane with 32-bit offsets), else 0          */
+int       vr_volume_extent_ok(int nx, int ny, int nz);
 
 /* ---- volume generation on the GPU: replaces the host start-up loops of
  *      TestMain.cpp:43-92.  Synchronous.             */

@@ -102,6 +102,23 @@ vr_status vr_shard_copy_frame(vr_shard* sh, void* dst, size_t dst_pitch, void* s
 /* This rank's rows (packed) and every rank's slot rows (rank 0's count). */
 vr_status vr_shard_rows(vr_shard* sh, int* my_rows, int* rows_per_rank);
 
+/* Failure handling.  The communicator is non-blocking: every host wait on a
+ * collective (vr_shard_connect's init, vr_shard_barrier, vr_shard_share_volume,
+ * the sampled renders of vr_shard_run) polls the stream and the
+ * communicator's asynchronous error against a deadline -- `seconds`, default
+ * the environment's VR_SHARD_TIMEOUT_S or 120.  On an error or at the
+ * deadline the communicator is aborted (ncclCommAbort) and the call returns
+ * VR_ERR_COMM or VR_ERR_TIMEOUT: a rank whose peer died fails with a message
+ * instead of waiting forever.  Every later collective on the shard fails at
+ * once (vr_shard_aborted = 1); vr_shard_destroy still frees it. */
+vr_status vr_shard_set_timeout(vr_shard* sh, double seconds);
+int       vr_shard_aborted(vr_shard* sh);
+/* Self-test of the deadline loop on the host (no GPU, no RCCL): mode 0 a
+ * state that completes after 5 polls, 1 one that fails at the 3rd, 2 one that
+ * never completes.  Returns 0 done, 1 failed, 2 deadline (-1 bad mode) and
+ * the number of polls. */
+int       vr_shard_poll_selftest(int mode, double timeout_s, int* polls);
+
 #ifdef __cplusplus
 }
 #endif

@@ -685,6 +685,42 @@ float vro_procedural_density(const vro_procedural* p, float scale, float px, flo
     return fmaxf(fbm * (1.0f - f1), 0.0f) * scale;
 }
 
+/* Worley cells the device computes for this evaluation (vr option "count" =
+ * 2; test infrastructure, mirrors noise::cellular_table9's pruning decision):
+ * the 8 cells of the unit cube around the sample, and all 27 of
+ * vro_cellular3's block again when the cube's minimum does not provably hold
+ * F1: sqrt(d_cube) + 0.3962 squared > T + 1 + 2 min g.  The device's square
+ * root is v_sqrt_f32 and this one is correctly rounded, so a sample whose
+ * test sits within an ulp of the bound may count differently (tests allow for
+ * it). */
+int vro_worley_cells(const vro_procedural* p, float px, float py, float pz)
+{
+    const float wf = p->worley_freq;
+    const float x = (px * p->grid_scale) * wf, y = (py * p->grid_scale) * wf, z = (pz * p->grid_scale) * wf;
+    const float jitter = 0.39614353f;
+    const float xf = floorf(x), yf = floorf(y), zf = floorf(z);
+    const float c0[3] = {xf - x, yf - y, zf - z}, c1[3] = {(xf + 1.0f) - x, (yf + 1.0f) - y, (zf + 1.0f) - z};
+    float d0 = FLT_MAX;
+    for (int xi = 0; xi <= 1; ++xi)
+        for (int yi = 0; yi <= 1; ++yi)
+            for (int zi = 0; zi <= 1; ++zi) {
+                const int32_t h = hash_primes_hb(p->seed_worley, wmul((int32_t)xf + xi, PRIME_X),
+                                                 wmul((int32_t)yf + yi, PRIME_Y), wmul((int32_t)zf + zi, PRIME_Z));
+                float xd = (float)(h & 0x3ff) - 511.5f;
+                float yd = (float)((h >> 10) & 0x3ff) - 511.5f;
+                float zd = (float)((h >> 20) & 0x3ff) - 511.5f;
+                const float inv = jitter / sqrtf(fmaf(zd, zd, fmaf(yd, yd, xd * xd)));
+                xd = fmaf(xd, inv, xi ? c1[0] : c0[0]);
+                yd = fmaf(yd, inv, yi ? c1[1] : c0[1]);
+                zd = fmaf(zd, inv, zi ? c1[2] : c0[2]);
+                d0 = fminf(d0, fmaf(zd, zd, fmaf(yd, yd, xd * xd)));
+            }
+    const float gx = fminf(-c0[0], c1[0]), gy = fminf(-c0[1], c1[1]), gz = fminf(-c0[2], c1[2]);
+    const float bound = fmaf(2.0f, fminf(gx, fminf(gy, gz)), fmaf(gz, gz, fmaf(gy, gy, fmaf(gx, gx, 1.0f))));
+    const float e = sqrtf(d0) + 0.3962f;
+    return e * e > bound ? 35 : 8;
+}
+
 static inline int inside01(const float q[3])
 {
     return q[0] >= 0.0f && q[0] <= 1.0f && q[1] >= 0.0f && q[1] <= 1.0f && q[2] >= 0.0f && q[2] <= 1.0f;
@@ -693,7 +729,7 @@ static inline int inside01(const float q[3])
 int vro_render_procedural(const vro_procedural* p, const float* obj48, const float* glob36, const vro_march* m,
                           int width, int height, int format, void* out, size_t pitch,
                           int band_rows, int band_stride, int band_first, int64_t* steps_out,
-                          int64_t* evals_out, int threads)
+                          int64_t* evals_out, int64_t* cells_out, int threads)
 {
     ray_basis b;
     march_consts k;
@@ -709,13 +745,14 @@ int vro_render_procedural(const vro_procedural* p, const float* obj48, const flo
     int nsel = 0;
     for (int bb = band_first; bb < nbands; bb += band_stride) nsel++;
     const int out_rows = nsel * band_rows;
-    int64_t total = 0, shadow_total = 0;
+    int64_t total = 0, shadow_total = 0, cells_total = 0;
+    const int count_cells = cells_out != NULL;
 #ifdef _OPENMP
     if (threads > 0) omp_set_num_threads(threads);
 #else
     (void)threads;
 #endif
-#pragma omp parallel for schedule(dynamic, 1) reduction(+ : total, shadow_total)
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : total, shadow_total, cells_total)
     for (int orow = 0; orow < out_rows; ++orow) {
         const int sel = orow / band_rows, r = orow % band_rows;
         const int y = (band_first + sel * band_stride) * band_rows + r;
@@ -729,12 +766,14 @@ int vro_render_procedural(const vro_procedural* p, const float* obj48, const flo
             int i = 0;
             for (; i < n; ++i) {
                 const float rho = vro_procedural_density(p, m->scale, P[0], P[1], P[2]);
+                if (count_cells) cells_total += vro_worley_cells(p, P[0], P[1], P[2]);
                 if (p->shadow_steps > 0 && rho > 0.0f) {
                     float q[3] = {P[0], P[1], P[2]}, sl = 0.0f;
                     for (int j = 0; j < p->shadow_steps; ++j) {
                         q[0] = q[0] + lstep[0]; q[1] = q[1] + lstep[1]; q[2] = q[2] + lstep[2];
                         if (inside01(q)) {
                             sl = sl + vro_procedural_density(p, m->scale, q[0], q[1], q[2]);
+                            if (count_cells) cells_total += vro_worley_cells(p, q[0], q[1], q[2]);
                             ++shadow;
                         }
                     }
@@ -760,5 +799,6 @@ int vro_render_procedural(const vro_procedural* p, const float* obj48, const flo
     }
     if (steps_out) *steps_out = total;
     if (evals_out) *evals_out = total + shadow_total;
+    if (cells_out) *cells_out = cells_total;
     return 0;
 }

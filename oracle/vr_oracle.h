@@ -122,8 +122,11 @@ float vro_procedural_density(const vro_procedural* p, float scale, float px, flo
 int vro_render_procedural(const vro_procedural* p, const float* obj48, const float* glob36, const vro_march* m,
                           int width, int height, int format, void* out, size_t pitch,
                           int band_rows, int band_stride, int band_first, int64_t* steps_out,
-                          int64_t* evals_out, int threads);
-/* evals_out (nullable): density evaluations = executed steps + shadow samples. */
+                          int64_t* evals_out, int64_t* cells_out, int threads);
+/* evals_out (nullable): density evaluations = executed steps + shadow samples.
+ * cells_out (nullable): the Worley cells the device's pruned evaluation
+ * computes, summed (vro_worley_cells; vr option "count" = 2).              */
+int vro_worley_cells(const vro_procedural* p, float px, float py, float pz);
 
 /* Per-pixel step count n (frag.glsl:46) and coverage, for KAT tests.
  * n_out[y*width+x] = -1 for uncovered pixels.                              */

@@ -74,7 +74,8 @@ def lib() -> ctypes.CDLL:
                                             ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, ctypes.c_size_t,
                                             ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                             ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
-                                            ctypes.c_int]
+                                            ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
+        L.vro_worley_cells.argtypes = [ctypes.POINTER(Procedural), ctypes.c_float, ctypes.c_float, ctypes.c_float]
         L.vro_procedural_density.argtypes = [ctypes.POINTER(Procedural), ctypes.c_float, ctypes.c_float,
                                              ctypes.c_float, ctypes.c_float]
         L.vro_procedural_density.restype = ctypes.c_float
@@ -182,9 +183,10 @@ def procedural_from(p) -> Procedural:
 
 
 def render_procedural(p: Procedural, obj, glob, m: March, width, height, fmt=FMT_RGBA32F, band_rows=0,
-                      band_stride=1, band_first=0, threads=0, with_evals=False):
+                      band_stride=1, band_first=0, threads=0, with_evals=False, with_cells=False):
     """BASELINE configs 2/3 with the CPU restatement -> (image, executed steps)
-    or, with_evals, (image, steps, density evaluations)."""
+    or, with_evals, (image, steps, density evaluations); with_cells appends the
+    Worley cells the device's pruned evaluation computes (vr "count" = 2)."""
     if band_rows > 0:
         nb = (height + band_rows - 1) // band_rows
         rows = len(range(band_first, nb, band_stride)) * band_rows
@@ -192,13 +194,14 @@ def render_procedural(p: Procedural, obj, glob, m: March, width, height, fmt=FMT
         rows = height
     dt = np.float32 if fmt == FMT_RGBA32F else np.uint8
     out = np.zeros((rows, width, 4), dt)
-    steps, evals = ctypes.c_int64(), ctypes.c_int64()
+    steps, evals, cells = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
     obj = np.ascontiguousarray(obj, np.float32)
     glob = np.ascontiguousarray(glob, np.float32)
     rc = lib().vro_render_procedural(ctypes.byref(p), obj.ctypes.data_as(_fp), glob.ctypes.data_as(_fp),
                                      ctypes.byref(m), width, height, fmt, out.ctypes.data_as(_vp), out.strides[0],
                                      band_rows, band_stride, band_first, ctypes.byref(steps), ctypes.byref(evals),
-                                     threads)
+                                     ctypes.byref(cells) if with_cells else None, threads)
     if rc != 0:
         raise ValueError(f"vro_render_procedural failed ({rc})")
-    return (out, steps.value, evals.value) if with_evals else (out, steps.value)
+    res = (out, steps.value) + ((evals.value,) if with_evals else ()) + ((cells.value,) if with_cells else ())
+    return res

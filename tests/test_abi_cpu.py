@@ -32,7 +32,7 @@ def test_shard_library_exports_every_declared_symbol():
     from volumetricrenderer_amd import _lib
     lib = _lib.load_shard()
     declared = header_functions("vr_shard.h")
-    assert len(declared) == 12
+    assert len(declared) == 15
     for name in declared:
         assert hasattr(lib, name), name
     assert sorted(declared) == _lib.shard_exported_symbols()
@@ -40,6 +40,34 @@ def test_shard_library_exports_every_declared_symbol():
         _lib.shard_call("vr_shard_create", None, None, 1, 0, 64, 64, 1, 16, ctypes.byref(ctypes.c_void_p()))
     with pytest.raises(_lib.VRError):   # argument check only, no GPU
         _lib.shard_call("vr_shard_share_volume", None, None, 8, 8, 8, None)
+
+
+def test_shard_deadline_loop_selftest():
+    """The deadline logic every collective wait of libvr_shard uses
+    (poll_until), run on the host with stub states: a state that settles, one
+    that fails, one that never settles (returns at the deadline, does not
+    hang).  Verdict r02 #6: a failing peer must give rc != 0, not a hang."""
+    import time
+    from volumetricrenderer_amd import _lib
+    n = ctypes.c_int()
+    assert _lib.shard_call("vr_shard_poll_selftest", 0, 5.0, ctypes.byref(n)) == 0 and n.value == 5
+    assert _lib.shard_call("vr_shard_poll_selftest", 1, 5.0, ctypes.byref(n)) == 1 and n.value == 3
+    t0 = time.perf_counter()
+    assert _lib.shard_call("vr_shard_poll_selftest", 2, 0.05, ctypes.byref(n)) == 2
+    el = time.perf_counter() - t0
+    assert 0.05 <= el < 2.0 and n.value >= 2
+    assert _lib.shard_call("vr_shard_poll_selftest", 3, 0.05, ctypes.byref(n)) == -1
+    with pytest.raises(_lib.VRError):
+        _lib.shard_call("vr_shard_set_timeout", None, 1.0)
+    assert _lib.shard_call("vr_shard_aborted", None) == 0
+    assert _lib.STATUS_NAMES[7] == "VR_ERR_TIMEOUT" and _lib.STATUS_NAMES[8] == "VR_ERR_COMM"
+
+
+def test_volume_extent_ok():
+    from volumetricrenderer_amd import _lib
+    ok = lambda *d: _lib.call("vr_volume_extent_ok", *d)  # noqa: E731
+    assert ok(1, 1, 1) == 1 and ok(512, 512, 512) == 1
+    assert ok(0, 4, 4) == 0 and ok(4, -1, 4) == 0 and ok(2000, 2000, 2000) == 0
 
 
 def test_abi_struct_layouts():

@@ -98,6 +98,48 @@ def test_share_volume_from_rank0(world):
     assert all(r[0] == "ok" and r[1] for r in res), res
 
 
+def _bad_share_worker(rank, world, port, which, q):
+    """Rank 0 passes a bad volume: every rank must raise, none may hang in
+    the broadcast (the check used to come before it)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    from volumetricrenderer_amd.distributed import RcclBandPipeline, share_volume
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=__import__("datetime").timedelta(seconds=60))
+    try:
+        bad = np.zeros((4, 4, 4, 3), dtype=np.uint8)   # three channels: not RGBA8
+        try:
+            if which == "torch":
+                share_volume(None, bad if rank == 0 else None)   # rank from the group
+            else:
+                # the pipeline's Python side only; the bad volume is caught before any library call
+                p = RcclBandPipeline.__new__(RcclBandPipeline)
+                p.world, p.rank, p.group, p.loopback, p._h = world, rank, None, False, None
+                p.share_volume(torch.from_numpy(bad) if rank == 0 else None)
+            q.put(("no-raise", rank))
+        except ValueError as e:
+            q.put(("raised", rank, str(e)))
+    except Exception as e:  # pragma: no cover - surfaced by the assertion below
+        q.put(("err", rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("which", ["torch", "pipeline"])
+def test_share_volume_bad_input_raises_on_every_rank(which):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bad_share_worker, args=(rk, 2, port, which, q)) for rk in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert sorted(r[1] for r in res) == [0, 1], res
+    assert all(r[0] == "raised" for r in res), res
+
+
 def _worker(rank, world, port, W, H, q):
     import sys
     sys.path.insert(0, ROOT)

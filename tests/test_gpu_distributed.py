@@ -110,6 +110,41 @@ def test_rccl_pipeline_one_rank(fmt, band_rows):
             pl.close()
 
 
+def test_rccl_pipeline_deadline_aborts():
+    """The failure path of the native frame loop (verdict r02 #6): with a
+    deadline far shorter than the queued work, the barrier's host wait gives
+    up, aborts the (one-rank, non-blocking) communicator and raises
+    VR_ERR_TIMEOUT instead of waiting; every later collective on the shard
+    fails at once with VR_ERR_COMM, and the shard can still be closed."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import volumetricrenderer_amd as vr
+    from volumetricrenderer_amd.distributed import RcclBandPipeline
+    W, H = 3840, 2160
+    with vr.Renderer(0) as r:
+        r.generate_volume(vr.volume_recipe_defaults(size=128))
+        osd, gsd = vr.reference_shader_data(W / H)
+        r.set_shader_data(osd, gsd)
+        r.set_march(vr.march_defaults(max_steps=256))
+        pl = RcclBandPipeline(r, W, H, vr.FMT_RGBA32F, band_rows=16, world=1, rank=0, timeout_s=30.0)
+        try:
+            pl.run_frames(2)
+            pl.barrier()            # within the deadline: fine
+            assert not pl.aborted
+            pl.set_timeout(1e-6)    # ~20 frames of 4K x 256 take milliseconds
+            pl.run_frames(20)
+            with pytest.raises(vr.VRError) as e:
+                pl.barrier()
+            assert e.value.status == 7, e.value   # VR_ERR_TIMEOUT
+            assert pl.aborted
+            with pytest.raises(vr.VRError) as e2:
+                pl.run_frames(1)
+            assert e2.value.status == 8, e2.value  # VR_ERR_COMM
+            torch.cuda.synchronize()
+        finally:
+            pl.close()
+
+
 @pytest.mark.parametrize("world,band_rows,fmt", [(2, 16, 1), (3, 16, 0), (8, 16, 1), (5, 7, 1)])
 def test_native_pipeline_loopback_ranks(world, band_rows, fmt):
     """The native frame loop's N-rank data layout (packed band sets in gather

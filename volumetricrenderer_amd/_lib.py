@@ -28,6 +28,7 @@ VR_OK = 0
 STATUS_NAMES = {
     0: "VR_OK", 1: "VR_ERR_INVALID", 2: "VR_ERR_HIP", 3: "VR_ERR_NO_VOLUME",
     4: "VR_ERR_NO_CAMERA", 5: "VR_ERR_OOM", 6: "VR_ERR_NO_DEVICE",
+    7: "VR_ERR_TIMEOUT", 8: "VR_ERR_COMM",
 }
 FMT_RGBA32F, FMT_RGBA8_UNORM, FMT_RGBA8_SRGB = 0, 1, 2
 BYTES_PER_PIXEL = {FMT_RGBA32F: 16, FMT_RGBA8_UNORM: 4, FMT_RGBA8_SRGB: 4}
@@ -97,6 +98,7 @@ _SIGS = {
     "vr_set_volume_device": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp]),
     "vr_get_volume": (ctypes.c_int, [_vp, _vp]),
     "vr_volume_dims": (ctypes.c_int, [_vp, c_int_p, c_int_p, c_int_p]),
+    "vr_volume_extent_ok": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "vr_volume_recipe_defaults": (ctypes.c_int, [ctypes.POINTER(VolumeRecipe)]),
     "vr_generate_volume": (ctypes.c_int, [_vp, ctypes.POINTER(VolumeRecipe), _vp]),
     "vr_noise_grid": (ctypes.c_int, [_vp, ctypes.c_int, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -122,7 +124,7 @@ _SIGS = {
     "vr_get_option": (ctypes.c_int, [_vp, ctypes.c_char_p]),
 }
 # functions whose int return is a value, not a vr_status
-_VALUE_RETURNS = {"vr_abi_version", "vr_band_rows_packed", "vr_get_option"}
+_VALUE_RETURNS = {"vr_abi_version", "vr_band_rows_packed", "vr_get_option", "vr_volume_extent_ok"}
 
 _lib = None
 
@@ -184,7 +186,12 @@ _SHARD_SIGS = {
     "vr_shard_rows": (ctypes.c_int, [_vp, c_int_p, c_int_p]),
     "vr_shard_barrier": (ctypes.c_int, [_vp, _vp]),
     "vr_shard_share_volume": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp]),
+    "vr_shard_set_timeout": (ctypes.c_int, [_vp, ctypes.c_double]),
+    "vr_shard_aborted": (ctypes.c_int, [_vp]),
+    "vr_shard_poll_selftest": (ctypes.c_int, [ctypes.c_int, ctypes.c_double, c_int_p]),
 }
+# shard functions whose int return is a value, not a vr_status
+_SHARD_VALUE_RETURNS = {"vr_shard_aborted", "vr_shard_poll_selftest"}
 _shard_lib = None
 
 
@@ -214,6 +221,8 @@ def shard_call(name: str, *args):
     """Call a vr_shard_* function, raising VRError on a non-zero status."""
     lib = load_shard()
     r = getattr(lib, name)(*args)
+    if name in _SHARD_VALUE_RETURNS:
+        return r
     if r != VR_OK:
         msg = lib.vr_shard_last_error()
         raise VRError(r, name, msg.decode(errors="replace") if msg else "")

@@ -80,7 +80,8 @@ struct Ctx {
     int tiles_per_wave = kDefaultTilesPerWave;
     int* d_heads = nullptr;        // 8 queue heads (+ padding), zeroed per launch
     vr_procedural proc{};          // procedural medium (configs 2/3), off by default
-    int count = 0;                 // step_counter: 0 = executed ray-steps, 1 = density evaluations
+    int count = 0;                 // step_counter: 0 = executed ray-steps, 1 = density evaluations,
+                                   // 2 = Worley cells computed (procedural)
     void* d_sort = nullptr;        // procedural cost-sort scratch (proc_sort_bytes), grown on demand
     size_t sort_bytes = 0;
     // regions schedule (build_regions): per-XCD tile lists, double-buffered
@@ -465,6 +466,8 @@ vr_status vr_set_volume_device(void* p, const void* d_rgba8, int nx, int ny, int
     return install_volume(c, static_cast<const uint8_t*>(d_rgba8), nx, ny, nz, static_cast<hipStream_t>(stream));
 }
 
+int vr_volume_extent_ok(int nx, int ny, int nz) { return dims_ok(nx, ny, nz) ? 1 : 0; }
+
 vr_status vr_volume_dims(void* p, int* nx, int* ny, int* nz)
 {
     if (!p || !nx || !ny || !nz) return fail(VR_ERR_INVALID, "vr_volume_dims: null argument");
@@ -681,7 +684,8 @@ vr_status vr_set_option(void* p, const char* name, int value)
         return VR_OK;
     }
     if (n == "count") {
-        if (value < 0 || value > 1) return fail(VR_ERR_INVALID, "vr_set_option: count is 0 (steps) or 1 (evals)");
+        if (value < 0 || value > 2)
+            return fail(VR_ERR_INVALID, "vr_set_option: count is 0 (steps), 1 (evals) or 2 (Worley cells)");
         c->count = value;
         return VR_OK;
     }

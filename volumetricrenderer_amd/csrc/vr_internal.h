@@ -129,7 +129,8 @@ struct ProcParams {
     int shadow_steps;
     float lstep[3];   // (step_size * sun_dir) / box_range
     float od;         // step_size * density
-    int count_evals;  // step_counter counts density evaluations (incl. shadow samples)
+    int count_evals;  // step_counter counts: 0 ray-steps, 1 density evaluations (incl. shadow
+                      // samples), 2 Worley cells computed (8 or 35 per evaluation when pruned, else 27)
     int wt_lo, wt_n;  // Worley cell table in LDS: cells [wt_lo, wt_lo + wt_n)^3; wt_n = 0: none
     int wt_pz;        // its z pitch in entries (>= wt_n^2, padded against LDS bank aliasing)
     int wt_fixed;     // 1: the fixed geometry wt_n = 9, wt_pz = 83 (noise::cellular_table9)

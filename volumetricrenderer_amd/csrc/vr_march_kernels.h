@@ -450,9 +450,12 @@ __device__ __forceinline__ unsigned march_pixel(const MarchArgs& a, const FastCt
 // TABLE: 0 = direct noise, 1 = LDS tables with runtime Worley geometry,
 // 2 = LDS tables with the fixed 9-cell geometry (noise::cellular_table9),
 // 3 = 2 + the global Perlin lattice table (noise::perlin_lat)
+// `cells` accumulates the Worley cells this evaluation computed (8, or 35 when
+// the pruned lane also ran the 27-cell block; 27 without the pruned table) --
+// vr option "count" = 2, the algorithmic work of the roofline (bench.py)
 template <int TABLE>
 __device__ __forceinline__ float proc_density(const ProcParams& p, const float4* wt, float scale, float px, float py,
-                                              float pz)
+                                              float pz, unsigned& cells)
 {
     const float gs = noise::in_vgpr(p.grid_scale), lac = noise::in_vgpr(p.lacunarity), gain = noise::in_vgpr(p.gain);
     const float qx = px * gs, qy = py * gs, qz = pz * gs;
@@ -491,9 +494,15 @@ __device__ __forceinline__ float proc_density(const ProcParams& p, const float4*
     }
     const float wf = noise::in_vgpr(p.worley_freq);
     float f1;
-    if constexpr (TABLE >= 2) f1 = noise::cellular_table9(wt, p.wt_lo, qx * wf, qy * wf, qz * wf) + 1.0f;
-    else if constexpr (TABLE == 1) f1 = noise::cellular_table(wt, p.wt_lo, p.wt_n, p.wt_pz, qx * wf, qy * wf, qz * wf) + 1.0f;
-    else f1 = noise::cellular(p.seed_worley, qx * wf, qy * wf, qz * wf) + 1.0f;
+    if constexpr (TABLE >= 2) {
+        bool full;
+        f1 = noise::cellular_table9(wt, p.wt_lo, qx * wf, qy * wf, qz * wf, full) + 1.0f;
+        if (p.count_evals == 2) cells += full ? 35u : 8u;
+    } else {
+        if constexpr (TABLE == 1) f1 = noise::cellular_table(wt, p.wt_lo, p.wt_n, p.wt_pz, qx * wf, qy * wf, qz * wf) + 1.0f;
+        else f1 = noise::cellular(p.seed_worley, qx * wf, qy * wf, qz * wf) + 1.0f;
+        if (p.count_evals == 2) cells += 27u;
+    }
     return fmaxf(fbm * (1.0f - f1), 0.0f) * noise::in_vgpr(scale);
 }
 
@@ -518,15 +527,16 @@ __device__ __forceinline__ unsigned march_pixel_proc(const MarchArgs& a, const f
     float acc = 0.0f, rad = 0.0f, tv = 1.0f;
     int i = 0;
     unsigned evals = 0;   // shadow density evaluations
+    unsigned cells = 0;   // Worley cells computed (count mode 2)
     for (; i < r.n; ++i) {
-        const float rho = proc_density<TABLE>(p, wt, a.scale, P0, P1, P2);
+        const float rho = proc_density<TABLE>(p, wt, a.scale, P0, P1, P2, cells);
         if constexpr (SHADOW) {
             if (rho > 0.0f) {
                 float q0 = P0, q1 = P1, q2 = P2, sl = 0.0f;
                 for (int j = 0; j < p.shadow_steps; ++j) {
                     q0 = q0 + p.lstep[0]; q1 = q1 + p.lstep[1]; q2 = q2 + p.lstep[2];
                     if (q0 >= 0.0f && q0 <= 1.0f && q1 >= 0.0f && q1 <= 1.0f && q2 >= 0.0f && q2 <= 1.0f) {
-                        sl = sl + proc_density<TABLE>(p, wt, a.scale, q0, q1, q2);
+                        sl = sl + proc_density<TABLE>(p, wt, a.scale, q0, q1, q2, cells);
                         ++evals;
                     }
                 }
@@ -543,6 +553,7 @@ __device__ __forceinline__ unsigned march_pixel_proc(const MarchArgs& a, const f
     }
     if (r.live) store_pixel(a, x, orow, r.n >= 0, proc_epilogue<SHADOW>(a, acc, rad));
     if (r.n <= 0) return 0u;
+    if (p.count_evals == 2) return cells;
     return p.count_evals ? (unsigned)i + evals : (unsigned)i;
 }
 
@@ -587,11 +598,12 @@ __device__ __forceinline__ unsigned march_pixel_proc_compact(const MarchArgs& a,
     int i = 0;
     bool act = r.n > 0;
     unsigned evals = 0;
+    unsigned cells = 0;   // Worley cells this lane computed (count mode 2), primary and dealt
     for (;;) {
         act = act && i < r.n;
         if (__ballot(act) == 0) break;
         float rho = 0.0f;
-        if (act) rho = proc_density<TABLE>(p, wt, a.scale, P0, P1, P2);
+        if (act) rho = proc_density<TABLE>(p, wt, a.scale, P0, P1, P2, cells);
         const bool need = act && rho > 0.0f;
         const unsigned long long m = __ballot(need);
         if (m) {
@@ -629,7 +641,7 @@ __device__ __forceinline__ unsigned march_pixel_proc_compact(const MarchArgs& a,
                     const float4 pk = sh->p[kk];
                     float q0 = pk.x, q1 = pk.y, q2 = pk.z;
                     for (int jj = 0; jj <= j; ++jj) { q0 = q0 + l0; q1 = q1 + l1; q2 = q2 + l2; }
-                    sh->d[shadow_slot(pid)] = proc_density<TABLE>(p, wt, a.scale, q0, q1, q2);
+                    sh->d[shadow_slot(pid)] = proc_density<TABLE>(p, wt, a.scale, q0, q1, q2, cells);
                     ++evals;
                 }
             }
@@ -653,6 +665,10 @@ __device__ __forceinline__ unsigned march_pixel_proc_compact(const MarchArgs& a,
         }
     }
     if (r.live) store_pixel(a, x, orow, r.n >= 0, rad);
+    if (p.count_evals == 2) {   // every lane's cells, also those a lane computed for another's shadow ray
+        *shadow_evals = 0;
+        return cells;
+    }
     *shadow_evals = evals;
     return r.n > 0 ? (unsigned)i : 0u;
 }

@@ -14,12 +14,24 @@
 // frames in flight, VulkanRenderer.cpp:13).  No host synchronisation in the
 // loop: the host cost per frame is one render launch, one RCCL group and
 // (rank 0) one assembly launch.
+//
+// Failure handling: the communicator is non-blocking (ncclConfig_t.blocking
+// = 0).  Every host wait on a collective -- the init, the barrier, the volume
+// agreement and broadcast -- polls the stream and ncclCommGetAsyncError
+// against a deadline (vr_shard_set_timeout; VR_SHARD_TIMEOUT_S; default
+// 120 s).  On an asynchronous error or at the deadline the communicator is
+// aborted (ncclCommAbort) and the call returns VR_ERR_COMM / VR_ERR_TIMEOUT,
+// so a rank whose peer died fails with a message instead of hanging; every
+// later collective call on that shard fails at once.
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <hip/hip_runtime.h>
@@ -51,17 +63,57 @@ vr_status fail(vr_status st, const char* fmt, ...)
             return fail(e_ == hipErrorOutOfMemory ? VR_ERR_OOM : VR_ERR_HIP, "%s: %s (%s:%d)", #expr,     \
                         hipGetErrorString(e_), __FILE__, __LINE__);                                       \
     } while (0)
+// a non-blocking communicator may answer ncclInProgress: settle() then
+// waits (with the deadline) until the call has taken effect
 #define NCCL_TRY(expr)                                                                                    \
     do {                                                                                                  \
         ncclResult_t r_ = (expr);                                                                         \
-        if (r_ != ncclSuccess)                                                                            \
-            return fail(VR_ERR_HIP, "%s: %s (%s:%d)", #expr, ncclGetErrorString(r_), __FILE__, __LINE__); \
+        if (r_ == ncclInProgress) {                                                                       \
+            const vr_status s2_ = settle(sh, #expr);                                                      \
+            if (s2_ != VR_OK) return s2_;                                                                 \
+        } else if (r_ != ncclSuccess) {                                                                   \
+            abort_comm(sh);                                                                               \
+            return fail(VR_ERR_COMM, "%s: %s (%s:%d)", #expr, ncclGetErrorString(r_), __FILE__, __LINE__); \
+        }                                                                                                 \
+    } while (0)
+// a shard helper that has already set the message
+#define SH_TRY(expr)                  \
+    do {                              \
+        vr_status t_ = (expr);        \
+        if (t_ != VR_OK) return t_;   \
     } while (0)
 #define VR_TRY(expr)                                                                                      \
     do {                                                                                                  \
         vr_status s_ = (expr);                                                                            \
         if (s_ != VR_OK) return fail(s_, "%s: %s", #expr, vr_last_error());                               \
     } while (0)
+
+// Poll `state()` -- 0 done, 1 pending, 2 failed -- until it is not pending or
+// `timeout_s` has passed: 0 done, 1 failed, 2 timed out.  Spins for the first
+// 2 ms (a barrier at the end of a timed window costs microseconds), then
+// sleeps 50 us between polls.  Shared by the collective waits and the CPU
+// self-test of the deadline logic (vr_shard_poll_selftest).
+template <class State>
+int poll_until(State state, double timeout_s)
+{
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    for (;;) {
+        const int st = state();
+        if (st == 0) return 0;
+        if (st == 2) return 1;
+        const double el = std::chrono::duration<double>(clk::now() - t0).count();
+        if (el > timeout_s) return 2;
+        if (el > 2e-3) std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+}
+
+double default_timeout()
+{
+    const char* e = std::getenv("VR_SHARD_TIMEOUT_S");
+    const double v = e ? std::atof(e) : 0.0;
+    return v > 0.0 ? v : 120.0;
+}
 
 }  // namespace
 
@@ -86,9 +138,88 @@ struct vr_shard {
     int last = -1;                    // parity of the last frame
     bool loopback = false;            // one process emulates all ranks (no RCCL)
     std::vector<hipEvent_t> timing;   // sampled render brackets (pairs)
+    double timeout_s = 120.0;         // deadline of every host wait on a collective
+    bool aborted = false;             // the communicator was aborted (error or deadline)
 };
 
 namespace {
+
+void abort_comm(vr_shard* sh)
+{
+    if (sh && sh->comm) {
+        (void)ncclCommAbort(sh->comm);
+        sh->comm = nullptr;
+        sh->aborted = true;
+    }
+}
+
+// the communicator's asynchronous state: 0 ok, 1 in progress, 2 failed
+int comm_state(vr_shard* sh)
+{
+    if (!sh->comm) return sh->aborted ? 2 : 0;
+    ncclResult_t r = ncclSuccess;
+    if (ncclCommGetAsyncError(sh->comm, &r) != ncclSuccess) return 2;
+    return r == ncclSuccess ? 0 : r == ncclInProgress ? 1 : 2;
+}
+
+vr_status deadline_fail(vr_shard* sh, int res, const char* what)
+{
+    ncclResult_t r = ncclSuccess;
+    if (sh->comm) (void)ncclCommGetAsyncError(sh->comm, &r);
+    abort_comm(sh);
+    if (res == 2)
+        return fail(VR_ERR_TIMEOUT, "%s: no completion within %.3g s (a peer rank failed or stalled); communicator aborted",
+                    what, sh->timeout_s);
+    return fail(VR_ERR_COMM, "%s: communicator error: %s; communicator aborted", what, ncclGetErrorString(r));
+}
+
+// A non-blocking NCCL call returned ncclInProgress: wait until it has taken effect.
+vr_status settle(vr_shard* sh, const char* what)
+{
+    const int res = poll_until([&] { return comm_state(sh); }, sh->timeout_s);
+    return res == 0 ? VR_OK : deadline_fail(sh, res, what);
+}
+
+// Host wait for stream `s` (which may hold collectives), with the deadline and
+// the communicator's error state.
+vr_status wait_stream(vr_shard* sh, hipStream_t s, const char* what)
+{
+    hipError_t he = hipSuccess;
+    const int res = poll_until([&] {
+        const int c = comm_state(sh);
+        if (c == 2) return 2;
+        he = hipStreamQuery(s);
+        if (he == hipSuccess) return 0;
+        return he == hipErrorNotReady ? 1 : 2;
+    }, sh->timeout_s);
+    if (res == 0) return VR_OK;
+    if (res == 1 && he != hipSuccess && he != hipErrorNotReady) {
+        abort_comm(sh);
+        return fail(VR_ERR_HIP, "%s: %s; communicator aborted", what, hipGetErrorString(he));
+    }
+    return deadline_fail(sh, res, what);
+}
+
+vr_status wait_event(vr_shard* sh, hipEvent_t e, const char* what)
+{
+    hipError_t he = hipSuccess;
+    const int res = poll_until([&] {
+        if (comm_state(sh) == 2) return 2;
+        he = hipEventQuery(e);
+        if (he == hipSuccess) return 0;
+        return he == hipErrorNotReady ? 1 : 2;
+    }, sh->timeout_s);
+    if (res == 0) return VR_OK;
+    if (res == 1 && he != hipSuccess && he != hipErrorNotReady)
+        return fail(VR_ERR_HIP, "%s: %s", what, hipGetErrorString(he));
+    return deadline_fail(sh, res, what);
+}
+
+vr_status check_usable(vr_shard* sh, const char* what)
+{
+    if (sh->aborted) return fail(VR_ERR_COMM, "%s: the communicator was aborted by an earlier error or deadline", what);
+    return VR_OK;
+}
 
 void release(vr_shard* sh)
 {
@@ -103,7 +234,7 @@ void release(vr_shard* sh)
     for (hipEvent_t e : sh->timing) (void)hipEventDestroy(e);
     if (sh->fence) (void)hipEventDestroy(sh->fence);
     if (sh->token) (void)hipFree(sh->token);
-    if (sh->comm) (void)ncclCommDestroy(sh->comm);
+    if (sh->comm) (void)ncclCommDestroy(sh->comm);   // an aborted communicator is already gone
     if (sh->comm_stream) (void)hipStreamDestroy(sh->comm_stream);
     delete sh;
 }
@@ -166,7 +297,8 @@ vr_status vr_shard_unique_id(uint8_t id[VR_SHARD_ID_BYTES])
 {
     if (!id) return fail(VR_ERR_INVALID, "vr_shard_unique_id: null");
     ncclUniqueId u;
-    NCCL_TRY(ncclGetUniqueId(&u));
+    const ncclResult_t r = ncclGetUniqueId(&u);
+    if (r != ncclSuccess) return fail(VR_ERR_COMM, "ncclGetUniqueId: %s", ncclGetErrorString(r));
     std::memcpy(id, &u, sizeof u);
     return VR_OK;
 }
@@ -183,6 +315,7 @@ vr_status vr_shard_alloc(void* ctx, int nranks, int rank, int width, int height,
     if (!sh) return fail(VR_ERR_OOM, "vr_shard_alloc: host allocation");
     sh->ctx = ctx;
     sh->loopback = true;   // until vr_shard_connect joins a communicator
+    sh->timeout_s = default_timeout();
     sh->nranks = nranks;
     sh->rank = rank;
     sh->width = width;
@@ -234,13 +367,20 @@ vr_status vr_shard_connect(vr_shard* sh, const uint8_t id[VR_SHARD_ID_BYTES])
     if (!sh || !id) return fail(VR_ERR_INVALID, "vr_shard_connect: null argument");
     if (sh->comm) return fail(VR_ERR_INVALID, "vr_shard_connect: already connected");
     if (sh->last >= 0) return fail(VR_ERR_INVALID, "vr_shard_connect: frames already rendered in loopback");
+    if (sh->aborted) return fail(VR_ERR_COMM, "vr_shard_connect: communicator already aborted");
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof u);
-    const ncclResult_t r = ncclCommInitRank(&sh->comm, sh->nranks, u, sh->rank);
-    if (r != ncclSuccess) {
+    // non-blocking: the init returns at once and completes as the peers join;
+    // a peer that never joins ends in the deadline, not in a hang
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    const ncclResult_t r = ncclCommInitRankConfig(&sh->comm, sh->nranks, u, sh->rank, &cfg);
+    if (r != ncclSuccess && r != ncclInProgress) {
         sh->comm = nullptr;
-        return fail(VR_ERR_HIP, "vr_shard_connect: ncclCommInitRank: %s", ncclGetErrorString(r));
+        return fail(VR_ERR_COMM, "vr_shard_connect: ncclCommInitRankConfig: %s", ncclGetErrorString(r));
     }
+    const vr_status st = settle(sh, "vr_shard_connect: ncclCommInitRankConfig");
+    if (st != VR_OK) return st;
     sh->loopback = false;
     return VR_OK;
 }
@@ -279,6 +419,7 @@ vr_status vr_shard_run(vr_shard* sh, int frames, void* stream, int sample_every,
     if (kernel_ms && sample_every <= 0) return fail(VR_ERR_INVALID, "vr_shard_run: sample_every must be > 0");
     if (sh->loopback && sh->rank != 0)
         return fail(VR_ERR_INVALID, "vr_shard_run: rank %d is not connected (vr_shard_connect)", sh->rank);
+    SH_TRY(check_usable(sh, "vr_shard_run"));
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int nsamp = kernel_ms ? (frames + sample_every - 1) / sample_every : 0;
     while ((int)sh->timing.size() < 2 * nsamp) {
@@ -299,7 +440,7 @@ vr_status vr_shard_run(vr_shard* sh, int frames, void* stream, int sample_every,
     if (kernel_ms) {
         double sum = 0.0;
         for (int k = 0; k < next; ++k) {
-            HIP_TRY(hipEventSynchronize(sh->timing[2 * k + 1]));
+            SH_TRY(wait_event(sh, sh->timing[2 * k + 1], "vr_shard_run: sampled render"));
             float ms = 0.0f;
             HIP_TRY(hipEventElapsedTime(&ms, sh->timing[2 * k], sh->timing[2 * k + 1]));
             sum += ms;
@@ -314,6 +455,7 @@ vr_status vr_shard_barrier(vr_shard* sh, void* stream)
     if (!sh) return fail(VR_ERR_INVALID, "vr_shard_barrier: null");
     if (sh->loopback && sh->rank != 0)
         return fail(VR_ERR_INVALID, "vr_shard_barrier: rank %d is not connected (vr_shard_connect)", sh->rank);
+    SH_TRY(check_usable(sh, "vr_shard_barrier"));
     hipStream_t s = static_cast<hipStream_t>(stream);
     HIP_TRY(hipEventRecord(sh->fence, s));
     HIP_TRY(hipStreamWaitEvent(sh->comm_stream, sh->fence, 0));
@@ -321,8 +463,8 @@ vr_status vr_shard_barrier(vr_shard* sh, void* stream)
     // reached it: a device-side barrier over xGMI, then the host waits for it.
     if (sh->nranks > 1 && !sh->loopback)
         NCCL_TRY(ncclAllReduce(sh->token, sh->token, 1, ncclInt32, ncclSum, sh->comm, sh->comm_stream));
-    HIP_TRY(hipStreamSynchronize(sh->comm_stream));
-    HIP_TRY(hipStreamSynchronize(s));
+    SH_TRY(wait_stream(sh, sh->comm_stream, "vr_shard_barrier"));
+    SH_TRY(wait_stream(sh, s, "vr_shard_barrier"));
     return VR_OK;
 }
 
@@ -338,15 +480,21 @@ vr_status vr_shard_share_volume(vr_shard* sh, const void* d_rgba8, int nx, int n
     if (!sh) return fail(VR_ERR_INVALID, "vr_shard_share_volume: null shard");
     if (sh->loopback && sh->rank != 0)
         return fail(VR_ERR_INVALID, "vr_shard_share_volume: rank %d is not connected (vr_shard_connect)", sh->rank);
+    SH_TRY(check_usable(sh, "vr_shard_share_volume"));
     hipStream_t s = static_cast<hipStream_t>(stream);
-    HIP_TRY(hipSetDevice(sh->device));
     if (sh->loopback) {   // one process holds every rank's work: nothing to send
+        HIP_TRY(hipSetDevice(sh->device));
         if (!d_rgba8) return fail(VR_ERR_INVALID, "vr_shard_share_volume: rank 0 needs the volume");
         VR_TRY(vr_set_volume_device(sh->ctx, d_rgba8, nx, ny, nz, stream));
         HIP_TRY(hipStreamSynchronize(s));
         return VR_OK;
     }
-    int failed = (nx <= 0 || ny <= 0 || nz <= 0 || (sh->rank == 0 && !d_rgba8)) ? 1 : 0;
+    // Every local failure before the broadcast -- the device, the extent (the
+    // same test vr_set_volume_device applies), rank 0's missing volume, the
+    // receive buffer -- is folded into `failed` and still takes part in the
+    // agreement all-reduce, so no rank returns while its peers wait in it.
+    int failed = hipSetDevice(sh->device) != hipSuccess ? 1 : 0;
+    if (!vr_volume_extent_ok(nx, ny, nz) || (sh->rank == 0 && !d_rgba8)) failed = 1;
     const size_t bytes = failed ? 0 : (size_t)nx * ny * nz * 4;
     uint8_t* buf = nullptr;
     if (!failed && sh->rank != 0 && hipMalloc(&buf, bytes) != hipSuccess) {
@@ -357,19 +505,26 @@ vr_status vr_shard_share_volume(vr_shard* sh, const void* d_rgba8, int nx, int n
     int got[7] = {};
     hipError_t he = hipMemcpyAsync(sh->token + 1, agree, sizeof agree, hipMemcpyHostToDevice, sh->comm_stream);
     ncclResult_t nr = ncclSuccess;
-    if (he == hipSuccess)
+    if (he == hipSuccess) {
         nr = ncclAllReduce(sh->token + 1, sh->token + 1, 7, ncclInt32, ncclMax, sh->comm, sh->comm_stream);
+        if (nr == ncclInProgress) nr = settle(sh, "vr_shard_share_volume: agreement") == VR_OK ? ncclSuccess : ncclInternalError;
+    }
     if (he == hipSuccess && nr == ncclSuccess)
         he = hipMemcpyAsync(got, sh->token + 1, sizeof got, hipMemcpyDeviceToHost, sh->comm_stream);
-    if (he == hipSuccess) he = hipStreamSynchronize(sh->comm_stream);
-    if (he != hipSuccess || nr != ncclSuccess) {
+    vr_status st = VR_OK;
+    if (he == hipSuccess && nr == ncclSuccess) st = wait_stream(sh, sh->comm_stream, "vr_shard_share_volume: agreement");
+    if (he != hipSuccess || nr != ncclSuccess || st != VR_OK) {
         if (buf) (void)hipFree(buf);
-        if (nr != ncclSuccess) return fail(VR_ERR_HIP, "vr_shard_share_volume: agreement: %s", ncclGetErrorString(nr));
+        if (st != VR_OK) return st;
+        if (nr != ncclSuccess) {
+            if (!sh->aborted) abort_comm(sh);
+            return fail(VR_ERR_COMM, "vr_shard_share_volume: agreement: %s", ncclGetErrorString(nr));
+        }
         return fail(VR_ERR_HIP, "vr_shard_share_volume: agreement: %s", hipGetErrorString(he));
     }
     if (got[0] || got[1] != -got[4] || got[2] != -got[5] || got[3] != -got[6]) {
         if (buf) (void)hipFree(buf);
-        if (failed) return fail(VR_ERR_INVALID, "vr_shard_share_volume: rank %d: bad extent, no volume or no memory", sh->rank);
+        if (failed) return fail(VR_ERR_INVALID, "vr_shard_share_volume: rank %d: bad extent, no volume, no device or no memory", sh->rank);
         if (got[0]) return fail(VR_ERR_INVALID, "vr_shard_share_volume: failed on another rank");
         return fail(VR_ERR_INVALID, "vr_shard_share_volume: ranks named different extents");
     }
@@ -380,20 +535,52 @@ vr_status vr_shard_share_volume(vr_shard* sh, const void* d_rgba8, int nx, int n
     if (he == hipSuccess) he = hipStreamWaitEvent(sh->comm_stream, sh->fence, 0);
     if (he == hipSuccess) {
         nr = ncclBroadcast(data, data, bytes, ncclUint8, 0, sh->comm, sh->comm_stream);
+        if (nr == ncclInProgress) nr = settle(sh, "vr_shard_share_volume: broadcast") == VR_OK ? ncclSuccess : ncclInternalError;
         if (nr == ncclSuccess) {
             he = hipEventRecord(sh->fence, sh->comm_stream);
             if (he == hipSuccess) he = hipStreamWaitEvent(s, sh->fence, 0);
         }
     }
-    vr_status st = VR_OK;
-    if (nr != ncclSuccess) st = fail(VR_ERR_HIP, "vr_shard_share_volume: ncclBroadcast: %s", ncclGetErrorString(nr));
-    else if (he != hipSuccess) st = fail(VR_ERR_HIP, "vr_shard_share_volume: %s", hipGetErrorString(he));
-    else if (vr_set_volume_device(sh->ctx, data, nx, ny, nz, stream) != VR_OK)
+    if (nr != ncclSuccess) {
+        if (!sh->aborted) abort_comm(sh);
+        st = fail(VR_ERR_COMM, "vr_shard_share_volume: ncclBroadcast: %s", ncclGetErrorString(nr));
+    } else if (he != hipSuccess) {
+        st = fail(VR_ERR_HIP, "vr_shard_share_volume: %s", hipGetErrorString(he));
+    } else if (vr_set_volume_device(sh->ctx, data, nx, ny, nz, stream) != VR_OK) {
         st = fail(VR_ERR_HIP, "vr_shard_share_volume: vr_set_volume_device: %s", vr_last_error());
-    (void)hipStreamSynchronize(sh->comm_stream);
-    (void)hipStreamSynchronize(s);
-    if (buf) (void)hipFree(buf);
+    }
+    // the broadcast must be finished (or the communicator aborted) before buf goes
+    const vr_status w1 = wait_stream(sh, sh->comm_stream, "vr_shard_share_volume: broadcast");
+    const vr_status w2 = w1 == VR_OK ? wait_stream(sh, s, "vr_shard_share_volume: install") : w1;
+    if (st == VR_OK) st = w2;
+    if (buf && !sh->aborted) (void)hipFree(buf);   // an aborted broadcast may still own it: leak, not corrupt
     return st;
+}
+
+vr_status vr_shard_set_timeout(vr_shard* sh, double seconds)
+{
+    if (!sh || !(seconds > 0.0)) return fail(VR_ERR_INVALID, "vr_shard_set_timeout: need a shard and seconds > 0");
+    sh->timeout_s = seconds;
+    return VR_OK;
+}
+
+int vr_shard_aborted(vr_shard* sh) { return sh && sh->aborted ? 1 : 0; }
+
+// CPU self-test of the deadline logic (no HIP, no RCCL): mode 0 -- the state
+// settles after a few polls; 1 -- it reports an error; 2 -- it never settles
+// (the deadline).  Returns poll_until's 0 / 1 / 2, or -1 for a bad mode.
+int vr_shard_poll_selftest(int mode, double timeout_s, int* polls)
+{
+    if (mode < 0 || mode > 2) return -1;
+    int n = 0;
+    const int res = poll_until([&] {
+        ++n;
+        if (mode == 0) return n >= 5 ? 0 : 1;
+        if (mode == 1) return n >= 3 ? 2 : 1;
+        return 1;
+    }, timeout_s);
+    if (polls) *polls = n;
+    return res;
 }
 
 vr_status vr_shard_frame(vr_shard* sh, void** pixels, size_t* row_pitch, int* rows)

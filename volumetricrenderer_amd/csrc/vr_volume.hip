@@ -394,7 +394,9 @@ hipError_t launch_noise(int kind, float* d_out, int x0, int y0, int z0, int nx, 
 {
     const int g = grid_for((long long)nx * ny * nz);
     *num_partials = g;
-    if ((long long)nx * ny * nz >= (1ll << 32)) return hipErrorInvalidValue;
+    // k_noise strides a 32-bit index by gridDim * kBlock (<= 4096 * kBlock): a
+    // total within one stride of 2^32 would wrap it and loop forever
+    if ((long long)nx * ny * nz > (1ll << 32) - 4096ll * kBlock) return hipErrorInvalidValue;
     // cellular: the cell range the grid's coordinates (start + i) * freq can
     // reach, +-1 neighbour and a cell of margin for rint (cellular_table)
     int lo = 0, n = 0;
@@ -540,7 +542,8 @@ __global__ __launch_bounds__(256) void k_selftest_worley(int seed, unsigned long
             const float r = kind == 3 ? 1e-3f : 1e-5f;
             for (int b = 0; b < 3; ++b) c[b] = fminf(fmaxf(p[b] + r * (2.0f * unit() - 1.0f), 0.51f), 7.49f);
         }
-        const float got = noise::cellular_table9(tab, 0, c[0], c[1], c[2]);
+        bool full;
+        const float got = noise::cellular_table9(tab, 0, c[0], c[1], c[2], full);
         const float want = noise::cellular(seed, c[0], c[1], c[2]);
         miss += __float_as_uint(got) != __float_as_uint(want);
     }

@@ -28,26 +28,37 @@ def rows_for_rank(height: int, band_rows: int, world: int, rank: int) -> int:
     return len(range(rank, nb, world)) * band_rows
 
 
-def share_volume(renderer, vol=None, rank: int = 0, group=None):
+def share_volume(renderer, vol=None, rank: int | None = None, group=None):
     """Collective (collective 1): rank 0's RGBA8 volume
     (nz, ny, nx, 4; numpy or tensor, ignored elsewhere) reaches every rank of
     the torch.distributed group once, and each rank's `renderer` installs it
     (``set_volume``).  The shape goes first, so the other ranks need nothing
     but the call.  Over gloo the bytes travel as a CPU tensor, over nccl
-    (RCCL) as a device tensor.  Returns the volume as this rank received it."""
+    (RCCL) as a device tensor.  Returns the volume as this rank received it.
+
+    `rank` defaults to this process's rank in `group`.  A bad volume on rank 0
+    is announced with a shape of -1s, so every rank raises together instead of
+    the others waiting in the broadcast."""
     world = dist.get_world_size(group)
+    if rank is None:
+        rank = dist.get_rank(group)
     dev = "cuda" if dist.get_backend(group) == "nccl" else "cpu"
-    shape = torch.zeros(4, dtype=torch.int64, device=dev)
+    shape = torch.full((4,), -1, dtype=torch.int64, device=dev)
+    bad = None
     if rank == 0:
         if vol is None:
-            raise ValueError("share_volume: rank 0 needs the volume")
-        t = vol if isinstance(vol, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(vol, dtype=np.uint8))
-        if t.dtype != torch.uint8 or t.dim() != 4 or t.shape[3] != 4:
-            raise ValueError("share_volume: the volume must be uint8 shaped (nz, ny, nx, 4)")
-        shape.copy_(torch.tensor(list(t.shape), dtype=torch.int64))
+            bad = "share_volume: rank 0 needs the volume"
+        else:
+            t = vol if isinstance(vol, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(vol, dtype=np.uint8))
+            if t.dtype != torch.uint8 or t.dim() != 4 or t.shape[3] != 4 or min(t.shape) <= 0:
+                bad = "share_volume: the volume must be uint8 shaped (nz, ny, nx, 4)"
+            else:
+                shape.copy_(torch.tensor(list(t.shape), dtype=torch.int64))
     if world > 1:
         dist.broadcast(shape, src=0, group=group)
     dims = [int(v) for v in shape.tolist()]
+    if bad or min(dims) <= 0:
+        raise ValueError(bad or "share_volume: rank 0 had no valid volume")
     if rank == 0:
         data = t.to(dev).contiguous()
     else:
@@ -224,9 +235,13 @@ class RcclBandPipeline:
     the communicator id from rank 0 and the barriers."""
 
     def __init__(self, renderer, width: int, height: int, fmt: int, band_rows: int = 16, world: int = 1,
-                 rank: int = 0, group=None, loopback: bool = False):
+                 rank: int = 0, group=None, loopback: bool = False, timeout_s: float | None = None):
         """loopback: one process renders all `world` ranks' band sets on its
-        GPU and assembles them (no communicator; tests and rehearsals)."""
+        GPU and assembles them (no communicator; tests and rehearsals).
+        timeout_s: deadline of every host wait on a collective, from the
+        communicator init on (vr_shard_set_timeout; default VR_SHARD_TIMEOUT_S
+        or 120 s).  A rank whose peer fails gets VRError VR_ERR_TIMEOUT /
+        VR_ERR_COMM instead of hanging."""
         self.r = renderer
         self.width, self.height, self.fmt = width, height, fmt
         self.world, self.rank, self.group, self.loopback = world, rank, group, loopback
@@ -271,6 +286,8 @@ class RcclBandPipeline:
                 raise alloc_err or _lib.VRError(2, "vr_shard_alloc", "failed on another rank")
         elif alloc_err:
             raise alloc_err
+        if timeout_s is not None:
+            _lib.shard_call("vr_shard_set_timeout", h, float(timeout_s))
         if not loopback:
             try:
                 _lib.shard_call("vr_shard_connect", h, uid)
@@ -281,6 +298,15 @@ class RcclBandPipeline:
         mine, per = ctypes.c_int(), ctypes.c_int()
         _lib.shard_call("vr_shard_rows", h, ctypes.byref(mine), ctypes.byref(per))
         self.my_rows, self.rows_per_rank = mine.value, per.value
+
+    def set_timeout(self, seconds: float) -> None:
+        """Deadline (s) of every later host wait on a collective."""
+        _lib.shard_call("vr_shard_set_timeout", self._h, float(seconds))
+
+    @property
+    def aborted(self) -> bool:
+        """True once an error or a missed deadline aborted the communicator."""
+        return bool(_lib.shard_call("vr_shard_aborted", self._h))
 
     def run_frames(self, k: int, stream=None, sample_every: int = 0):
         """Queue k frames (collective).  Returns the mean duration (ms) of the
@@ -298,18 +324,24 @@ class RcclBandPipeline:
         in every rank's renderer (vr_shard_share_volume).  The extent goes
         to the other ranks over the torch group first."""
         from .renderer import _stream_handle
-        dims = torch.zeros(3, dtype=torch.int64)
+        # -1s announce a bad volume on rank 0: every rank raises after the
+        # broadcast, none is left waiting in it
+        dims = torch.full((3,), -1, dtype=torch.int64)
+        bad = None
         if self.rank == 0:
             if vol is None or not isinstance(vol, torch.Tensor) or not vol.is_cuda:
-                raise ValueError("share_volume: rank 0 needs the volume as a CUDA tensor")
-            if vol.dtype != torch.uint8 or vol.dim() != 4 or vol.shape[3] != 4 or not vol.is_contiguous():
-                raise ValueError("share_volume: the volume must be a contiguous uint8 tensor (nz, ny, nx, 4)")
-            dims = torch.tensor([vol.shape[2], vol.shape[1], vol.shape[0]], dtype=torch.int64)
+                bad = "share_volume: rank 0 needs the volume as a CUDA tensor"
+            elif vol.dtype != torch.uint8 or vol.dim() != 4 or vol.shape[3] != 4 or not vol.is_contiguous():
+                bad = "share_volume: the volume must be a contiguous uint8 tensor (nz, ny, nx, 4)"
+            else:
+                dims = torch.tensor([vol.shape[2], vol.shape[1], vol.shape[0]], dtype=torch.int64)
         if self.world > 1 and not self.loopback:
             t = dims.to("cuda" if dist.get_backend(self.group) == "nccl" else "cpu")
             dist.broadcast(t, src=0, group=self.group)
             dims = t.cpu()
         nx, ny, nz = (int(v) for v in dims.tolist())
+        if bad or min(nx, ny, nz) <= 0:
+            raise ValueError(bad or "share_volume: rank 0 had no valid volume")
         ptr = ctypes.c_void_p(vol.data_ptr()) if self.rank == 0 else None
         _lib.shard_call("vr_shard_share_volume", self._h, ptr, nx, ny, nz, _stream_handle(stream))
 
