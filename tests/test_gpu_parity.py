@@ -165,7 +165,7 @@ def test_media_scroll_mirrored_repeat(r, oracle, vol128):
 @pytest.mark.parametrize("layout,name", [(1, "planar"), (2, "brick5"), (3, "brick8"), (4, "brick16"), (5, "corner8"),
                                          (6, "brick4"), (7, "zpair"), (8, "brick448"),
                                          (9, "brick488"), (10, "brick4816"), (11, "brick41616"),
-                                         (12, "brick4832"), (13, "brick4864"), (14, "cornerh")])
+                                         (12, "brick4832"), (13, "brick4864"), (14, "cornerh"), (15, "col48")])
 def test_every_layout_bitexact(r, oracle, vol128, layout, name):
     osd, gsd = vr.reference_shader_data(16 / 9, 20.0, -35.0)
     r.set_volume(vol128)
@@ -182,6 +182,50 @@ def test_every_layout_bitexact(r, oracle, vol128, layout, name):
             img, ref, c, s = render_both(r, oracle, vol, 160, 90, osd, gsd)
             assert_exact(img, ref)
     finally:
+        r.set_layout_preference(0)
+
+
+@pytest.mark.parametrize("cap", [32, 12, 0])
+def test_slab_march_bitexact(r, oracle, vol128, cap):
+    """The LDS-slab march (COL48 + option slab, vr_march_slab.hip): per step a
+    wave fills its box of 64-B chunks per channel into LDS and reads its taps
+    there; a channel whose box exceeds slab_cap chunks reads straight from the
+    layout.  cap 32 = the full slab, 12 = a mix of slab and fallback channels,
+    0 = every channel falls back.  Bit-exact vs the oracle with step counts:
+    the reference view and rotated views at 128^3, odd extents, a 200^3
+    random volume on a small frame (big boxes), early-out, MediaScroll offsets
+    inside the clamp-exact range (the non-zero-offset kernel)."""
+    r.set_volume(vol128)
+    r.set_layout_preference(15)
+    r.set_option("slab", 1)
+    r.set_option("slab_cap", cap)
+    try:
+        for (W, H, phi, theta) in [(480, 270, 0.0, 0.0), (320, 180, 20.0, -35.0), (200, 120, -75.0, 60.0)]:
+            osd, gsd = vr.reference_shader_data(W / H, phi, theta)
+            img, ref, c, s = render_both(r, oracle, vol128, W, H, osd, gsd)
+            assert r.kernel_variant == "grid_col48_slab_clamp"
+            assert_exact(img, ref)
+            assert c == s
+        rng = np.random.default_rng(cap + 5)
+        osd, gsd = vr.reference_shader_data(16 / 9, 10.0, 25.0)
+        for dims in [(13, 22, 9), (61, 17, 45), (200, 200, 200)]:
+            vol = rng.integers(0, 256, size=dims + (4,), dtype=np.uint8)
+            img, ref, c, s = render_both(r, oracle, vol, 96, 54, osd, gsd)
+            assert_exact(img, ref)
+            assert c == s
+        # early-out, and small per-tap offsets (stays clamp-exact: the plain T path)
+        vol = rng.integers(0, 256, size=(40, 40, 40, 4), dtype=np.uint8)
+        osd, gsd = vr.reference_shader_data(16 / 9, 30.0, 5.0)
+        gsd.media_scroll[1 * 4 + 1] = 0.01
+        gsd.media_scroll[2 * 4 + 2] = -0.02
+        m = vr.march_defaults(early_out=0.6)
+        img, ref, c, s = render_both(r, oracle, vol, 160, 90, osd, gsd, march=m)
+        assert r.kernel_variant == "grid_col48_slab_clamp_early"
+        assert_exact(img, ref)
+        assert c == s
+    finally:
+        r.set_option("slab", 0)
+        r.set_option("slab_cap", 32)
         r.set_layout_preference(0)
 
 
@@ -558,8 +602,8 @@ def test_procedural_worley_cell_count(r, oracle, shadow):
     The oracle mirrors the pruning decision with a correctly rounded square
     root where the device uses v_sqrt_f32, so a sample whose test sits within
     an ulp of the bound may count 27 cells differently: the bar is 1e-5 of
-    the total.  Both schedules (sorted, with the shadow compaction, and plain
-    tiles) must agree with each other exactly."""
+    the total.  The plain-tile schedule (schedule 0) evaluates F1 from the
+    unpruned cell table: exactly 27 cells per evaluation."""
     W, H = 160, 96
     m = vr.march_defaults(max_steps=128)
     osd, gsd = vr.reference_shader_data(W / H, -15.0, 25.0)
@@ -588,8 +632,7 @@ def test_procedural_worley_cell_count(r, oracle, shadow):
                                                       with_evals=True, with_cells=True)
     assert got[0][1] == got[1][1] == evals
     cells_sorted, cells_tiles = got[0][0], got[1][0]
-    # the plain-tile schedule evaluates without the shadow compaction: same samples, same decisions
-    assert cells_sorted == cells_tiles
+    assert cells_tiles == 27 * evals
     assert abs(cells_sorted - cells) <= max(27, 1e-5 * cells), (cells_sorted, cells)
     assert 8 * evals <= cells <= 35 * evals
     assert cells < 12 * evals   # pruning keeps the mean far below 27 cells per sample

@@ -59,6 +59,26 @@ __global__ __launch_bounds__(256) void k_reg(const unsigned char* __restrict__ b
     out[blockIdx.x * 256 + threadIdx.x] = acc;
 }
 
+// CORNERH's tap load at config 4 (4K x 256 at 128^3): the four lanes of a
+// 2x2 quad read the same 16 B, neighbouring quads neighbouring 16-B pieces.
+// LEAD = 1: only the quad leaders load (the quad-dedup idea of verdict r02
+// #5), the other lanes are masked off.
+template <int LEAD>
+__global__ __launch_bounds__(256) void k_quad(const unsigned char* __restrict__ buf, unsigned* __restrict__ out)
+{
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const unsigned wave = blockIdx.x * 4u + (unsigned)w;
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)buf, (short)0, (int)kWindow, 0x00020000);
+    unsigned acc = 0;
+    for (int it = 0; it < ITER; ++it) {
+        if (!LEAD || (lane & 3) == 0) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (unsigned)(lane >> 2) * 16u, base_of(wave, it), 0);
+            acc += v[0] ^ v[1] ^ v[2] ^ v[3];
+        }
+    }
+    out[blockIdx.x * 256 + threadIdx.x] = acc;
+}
+
 // the shipped march's b64 tap load: lanes of a 2x2 pixel quad 0-1 texels
 // apart inside 4x8x32 bricks (brick4832), quads of a tile 2 texels apart
 __global__ __launch_bounds__(256) void k_b64(const unsigned char* __restrict__ buf, unsigned* __restrict__ out)
@@ -91,6 +111,8 @@ int main()
         DMA(64, 0); DMA(64, 1); DMA(32, 1); DMA(24, 1); DMA(16, 1); DMA(8, 1); DMA(4, 1);
         REG(64, 0); REG(64, 1); REG(24, 1); REG(8, 1);
         hipLaunchKernelGGL(k_b64, g, b, 0, 0, buf, out);
+        hipLaunchKernelGGL(k_quad<0>, g, b, 0, 0, buf, out);
+        hipLaunchKernelGGL(k_quad<1>, g, b, 0, 0, buf, out);
     }
     if (hipDeviceSynchronize() != hipSuccess) return 2;
     std::printf("lds_dma_calib done: %u blocks x 4 waves x %d loads per kernel\n", g.x, ITER);

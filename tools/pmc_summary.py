@@ -32,6 +32,19 @@ def derived(c):
         d["l1_miss_ratio"] = c["TCP_TCC_READ_REQ_sum"] / max(1.0, c["TCP_TOTAL_CACHE_ACCESSES_sum"])
     if "FETCH_SIZE" in c:
         d["fetch_MB_x2"] = c["FETCH_SIZE"] * 1024 * 2 / 1e6   # gfx950: FETCH_SIZE under-counts 2x
+    cyc = c.get("GRBM_GUI_ACTIVE", 0) / 8
+    if cyc:
+        for k, n in (("TA_TA_BUSY_sum", "ta_busy"), ("TD_TD_BUSY_sum", "td_busy")):
+            if k in c:
+                d[n] = c[k] / (256 * cyc)   # 256 CUs
+    vm = c.get("SQ_INSTS_VMEM_RD", 0)
+    if vm:
+        for k, n in (("TA_TA_BUSY_sum", "ta_cycles_per_vmem_inst"), ("TD_TD_BUSY_sum", "td_cycles_per_vmem_inst"),
+                     ("TCP_TOTAL_CACHE_ACCESSES_sum", "l1_lookups_per_vmem_inst")):
+            if k in c:
+                d[n] = c[k] / vm
+    if "SQ_LDS_BANK_CONFLICT" in c and c.get("SQ_INSTS_LDS"):
+        d["lds_conflict_cycles_per_lds_inst"] = c["SQ_LDS_BANK_CONFLICT"] / c["SQ_INSTS_LDS"]
     if "TCC_EA0_RDREQ_sum" in c:
         d["ea_rdreq_MB_64B"] = c["TCC_EA0_RDREQ_sum"] * 64 / 1e6
     return d

@@ -14,3 +14,6 @@ for c in ${CONFIGS:-grid512 cloud cloud_shadow}; do
     python -c "import json;j=json.loads(open('$OUT/bench_$n.json').read());print('$n', j['ms_per_step'], j['kernel_ms_mean'], j.get('host_ms_per_frame'), j['roofline']['frac'], j['roofline'].get('worley_cells_per_eval'), j['roofline'].get('frac_27cell'))"
   done
 done
+if [ -n "${AB:-}" ]; then
+  ROUNDS=${ROUNDS:-3} CONFIGS="$AB" LIBB=volumetricrenderer_amd/libvr_base.so bash tools/ab.sh | tee $OUT/ab.txt
+fi

@@ -89,6 +89,8 @@ struct Ctx {
     // other buffer (2 frames in flight, VulkanRenderer.cpp:13)
     int wedges = kDefaultWedges;   // wedges per XCD
     int split = 0;                 // lanes per ray: 0 = auto, 1, 2, 4, 8
+    int slab = 0;                  // COL48 + regions: the LDS slab march (vr_march_slab.hip)
+    int slab_cap = kSlabMaxChunks; // its chunks per channel (<= kSlabMaxChunks; smaller forces the fallback)
     struct RegionBuf {
         unsigned* d = nullptr;     // device tile list
         unsigned* h = nullptr;     // pinned staging copy
@@ -289,6 +291,7 @@ const char* variant_name(const Plan& p)
         {"grid_brick4832_clamp", "grid_brick4832_clamp_early"},
         {"grid_brick4864_clamp", "grid_brick4864_clamp_early"},
         {"grid_cornerh_clamp", "grid_cornerh_clamp_early"},
+        {"grid_col48_clamp", "grid_col48_clamp_early"},
     };
     if (p.layout == LAYOUT_PLANAR && p.wrap == WRAP_MIRROR)
         return p.early ? "grid_planar_mirror_early" : "grid_planar_mirror";
@@ -683,6 +686,17 @@ vr_status vr_set_option(void* p, const char* name, int value)
         c->wedges = value;
         return VR_OK;
     }
+    if (n == "slab") {
+        if (value < 0 || value > 1) return fail(VR_ERR_INVALID, "vr_set_option: slab is 0 or 1");
+        c->slab = value;
+        return VR_OK;
+    }
+    if (n == "slab_cap") {
+        if (value < 0 || value > kSlabMaxChunks)
+            return fail(VR_ERR_INVALID, "vr_set_option: slab_cap in [0, %d]", kSlabMaxChunks);
+        c->slab_cap = value;
+        return VR_OK;
+    }
     if (n == "count") {
         if (value < 0 || value > 2)
             return fail(VR_ERR_INVALID, "vr_set_option: count is 0 (steps), 1 (evals) or 2 (Worley cells)");
@@ -710,6 +724,8 @@ int vr_get_option(void* p, const char* name)
     if (n == "wedges") return c->wedges;
     if (n == "split") return c->split;
     if (n == "lattice") return c->lattice;
+    if (n == "slab") return c->slab;
+    if (n == "slab_cap") return c->slab_cap;
     return -1;
 }
 
@@ -726,6 +742,9 @@ const char* vr_kernel_variant(void* p)
     MarchArgs a{};
     Plan pl{};
     make_plan(c, &a, &pl);
+    const int kind = c->schedule >= 0 ? c->schedule : SCHED_REGIONS;
+    if (pl.layout == LAYOUT_COL48 && c->slab && kind == SCHED_REGIONS && c->split <= 1)
+        return pl.early ? "grid_col48_slab_clamp_early" : "grid_col48_slab_clamp";
     return variant_name(pl);
 }
 
@@ -1049,7 +1068,7 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
         // schedule 0 = one 8x8 tile per wave in row order, 4 = in rings;
         // otherwise (auto) the cost-sorted schedule
         void* sort_buf = nullptr;
-        Schedule sc{c->schedule == SCHED_RINGS ? SCHED_RINGS : SCHED_STATIC, 0, 0, 1, 1, nullptr, nullptr, {}, 1};
+        Schedule sc{c->schedule == SCHED_RINGS ? SCHED_RINGS : SCHED_STATIC, 0, 0, 1, 1, nullptr, nullptr, {}, 1, 0};
         if (sc.kind == SCHED_RINGS) box_centre_pixel(c, a, &sc.center_x, &sc.center_y);
         // the sort passes enumerate whole 64x64 regions (vr_march_kernels.h sort_pixel)
         if (c->schedule != SCHED_STATIC && c->schedule != SCHED_RINGS && a.width < 65536 && a.out_rows < 65536 &&
@@ -1093,7 +1112,9 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
     // wedges of the frame, each walked inside-out (longest rays first)
     const int kind = c->schedule >= 0 ? c->schedule : SCHED_REGIONS;
     const int tpw = c->tiles_per_wave > 0 ? c->tiles_per_wave : (kind == SCHED_RINGS || kind == SCHED_REGIONS ? 2 : 1);
-    Schedule sc{kind, 0, 0, tpw, c->waves_per_simd, c->d_heads, nullptr, {}, 1};
+    Schedule sc{kind, 0, 0, tpw, c->waves_per_simd, c->d_heads, nullptr, {}, 1, 0};
+    sc.slab = pl.layout == LAYOUT_COL48 && c->slab;
+    a.slab_cap = c->slab_cap;
     if (kind == SCHED_RINGS || kind == SCHED_REGIONS) box_centre_pixel(c, a, &sc.center_x, &sc.center_y);
     if (kind == SCHED_REGIONS) {
         const vr_status st = build_regions(c, a, tpw, sc.center_x, sc.center_y, static_cast<hipStream_t>(stream));
@@ -1106,6 +1127,7 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
         if (is_b4_family(pl.layout) || pl.layout == LAYOUT_ZPAIR || pl.layout == LAYOUT_CORNER8 ||
             pl.layout == LAYOUT_CORNERH) {
             int K = c->split;
+            if (sc.slab) K = K == 0 ? 1 : K;   // the slab march has one lane per ray; split > 1 uses the plain march
             if (K == 0) {
                 K = rb.nwork >= kSplitOneLane ? 1 : rb.nwork >= kSplitTwoLanes ? 2 : 4;
             }

@@ -48,8 +48,13 @@ enum Layout : int {
                              // the f16 pair {a, b - a} of its x-neighbours a, b, so
                              // each x-lerp is one v_fma_mix_f32; x fastest, no
                              // bricks: the index is computed in fp32 (16x bytes)
+    LAYOUT_COL48 = 15,       // columns of 4x8 texels (3x7 positions) through the whole
+                             // z extent, slices 32 B apart (1.52x bytes): BRICK4832
+                             // without z bricks, so any run of slices of a column is
+                             // contiguous -- the fill unit of the LDS slab march
+                             // (vr_march_slab.hip); also a plain BRICK4-family layout
 };
-constexpr int kNumLayouts = 15;
+constexpr int kNumLayouts = 16;
 // CORNERH's fp32 index a + (nx+1)(b + (ny+1)c) is exact below 2^24 positions
 constexpr long long kCornerHMaxPositions = 1ll << 24;
 // the layouts whose taps are BRICK4's two dword-aligned 8-B loads
@@ -57,7 +62,7 @@ __host__ __device__ constexpr bool is_b4_family(int l)
 {
     return l == LAYOUT_BRICK4 || l == LAYOUT_BRICK448 || l == LAYOUT_BRICK488 || l == LAYOUT_BRICK4816 ||
            l == LAYOUT_BRICK41616 || l == LAYOUT_BRICK4832 ||
-           l == LAYOUT_BRICK4864;
+           l == LAYOUT_BRICK4864 || l == LAYOUT_COL48;
 }
 
 enum Wrap : int { WRAP_CLAMP = 0, WRAP_MIRROR = 1 };
@@ -80,6 +85,11 @@ __host__ __device__ inline LayoutGeom layout_geom(int layout, int nx, int ny, in
         g.B = 1; g.R = 1; g.brick = 16;
     } else if (layout == LAYOUT_ZPAIR) {
         g.B = 3; g.R = 4; g.brick = 128;
+    } else if (layout == LAYOUT_COL48) {
+        // slices c and c + 1 for every padded position c in [0, nz]: nz + 2
+        // slices, rounded up to an even count (64-B chunks of two slices)
+        g.B = 3; g.R = 4;
+        g.brick = 32u * (unsigned)((nz + 3) & ~1);
     } else if (layout == LAYOUT_BRICK448 || layout == LAYOUT_BRICK488 || layout == LAYOUT_BRICK4816 ||
                layout == LAYOUT_BRICK41616 || layout == LAYOUT_BRICK4832 || layout == LAYOUT_BRICK4864) {
         g.B = 3; g.R = 4;
@@ -101,6 +111,7 @@ __host__ __device__ inline LayoutGeom layout_geom(int layout, int nx, int ny, in
     if (layout == LAYOUT_BRICK4864) { g.Ba[1] = 7; g.Rn[1] = 8; g.Ba[2] = 63; g.Rn[2] = 64; }
     if (layout == LAYOUT_BRICK4832) { g.Ba[1] = 7; g.Rn[1] = 8; g.Ba[2] = 31; g.Rn[2] = 32; }
     if (layout == LAYOUT_BRICK41616) { g.Ba[1] = g.Ba[2] = 15; g.Rn[1] = g.Rn[2] = 16; }
+    if (layout == LAYOUT_COL48) { g.Ba[1] = 7; g.Rn[1] = 8; g.Ba[2] = nz + 1; g.Rn[2] = (nz + 3) & ~1; }
     // padded base positions a in [0, N] -> bricks a / B in [0, N / B]
     g.nbx = nx / g.Ba[0] + 1;
     g.nby = ny / g.Ba[1] + 1;
@@ -170,6 +181,7 @@ struct MarchArgs {
     int format;
     unsigned long long* step_counter;
     ProcParams proc;
+    int slab_cap;                // LDS slab march (COL48): chunks per channel the slab holds
 };
 
 // How the march kernel maps tiles to waves.
@@ -192,12 +204,15 @@ struct Schedule {
     const unsigned* tiles; // regions: device tile lists
     TileMap map;           // regions (nwx counts waves of split units)
     int split;             // regions: lanes per ray (1, 2, 4, 8; BRICK4 / CORNER8 only)
+    int slab;              // regions + COL48: the LDS slab march (vr_march_slab.hip)
 };
 
 // launchers (vr_march.hip / vr_volume.hip); return hipError_t
 hipError_t launch_march(const MarchArgs& a, int layout, int wrap, bool early, const Schedule& sc, hipStream_t s);
 hipError_t launch_march_corner8(const MarchArgs& a, int layout, bool early, const Schedule& sc,
                                 hipStream_t s);   // CORNER8 / CORNERH, vr_march_c8.hip
+hipError_t launch_march_slab(const MarchArgs& a, bool early, const Schedule& sc, hipStream_t s);   // vr_march_slab.hip
+constexpr int kSlabMaxChunks = 32;   // per channel and wave (64 B each): 8 KiB of LDS per wave
 // sort_buf (proc_sort_bytes) selects the cost-sorted schedule; null = 8x8
 // tiles, in rings when sc.kind == SCHED_RINGS, else in row order
 // reuse_sort: sort_buf holds the order of a frame with the same geometry

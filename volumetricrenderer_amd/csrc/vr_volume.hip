@@ -370,6 +370,7 @@ hipError_t launch_build_layout(int layout, const uint8_t* d_planar, int nx, int 
     case LAYOUT_BRICK4816: hipLaunchKernelGGL(k_build_layout<LAYOUT_BRICK4816>, gr, b, 0, s, d_planar, nx, ny, nz, g, elems, pb, d_out); break;
     case LAYOUT_BRICK4864: hipLaunchKernelGGL(k_build_layout<LAYOUT_BRICK4864>, gr, b, 0, s, d_planar, nx, ny, nz, g, elems, pb, d_out); break;
     case LAYOUT_BRICK4832: hipLaunchKernelGGL(k_build_layout<LAYOUT_BRICK4832>, gr, b, 0, s, d_planar, nx, ny, nz, g, elems, pb, d_out); break;
+    case LAYOUT_COL48: hipLaunchKernelGGL(k_build_layout<LAYOUT_COL48>, gr, b, 0, s, d_planar, nx, ny, nz, g, elems, pb, d_out); break;
     case LAYOUT_BRICK41616: hipLaunchKernelGGL(k_build_layout<LAYOUT_BRICK41616>, gr, b, 0, s, d_planar, nx, ny, nz, g, elems, pb, d_out); break;
     case LAYOUT_ZPAIR: hipLaunchKernelGGL(k_build_layout<LAYOUT_ZPAIR>, gr, b, 0, s, d_planar, nx, ny, nz, g, elems, pb, d_out); break;
     case LAYOUT_CORNER8: hipLaunchKernelGGL(k_build_layout<LAYOUT_CORNER8>, gr, b, 0, s, d_planar, nx, ny, nz, g, elems, pb, d_out); break;
