@@ -860,12 +860,13 @@ def test_split_rays_bitexact(r, oracle, vol128, layout, split):
         r.set_layout_preference(0)
 
 
-@pytest.mark.parametrize("layout", [12, 5, 14])
+@pytest.mark.parametrize("layout", [15, 12, 5, 14])
 def test_auto_split_at_one_eighth_band_share(r, oracle, vol128, layout):
     """The multi-GPU config-5 path: auto split (split=0) turns on for a 1/8
-    band share of a 1080p frame, with brick4832 (the auto
-    layout past the Infinity Cache), corner8 and cornerh (the auto layout for
-    cache-resident volumes).  Exact, step counts too."""
+    band share of a 1080p frame, with col48 (the auto
+    layout past the Infinity Cache since round 3), brick4832 (before it),
+    corner8 and cornerh (the auto layout for cache-resident volumes).  Exact,
+    step counts too."""
     r.set_layout_preference(layout)
     r.set_option("schedule", 5)
     r.set_option("split", 0)

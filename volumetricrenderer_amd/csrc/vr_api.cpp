@@ -130,13 +130,17 @@ struct Ctx {
 // wins with the pipelined march: 2-5 % ahead of BRICK488 (1.74x) and 12-20 %
 // ahead of BRICK4 (2.37x) at 384^3-512^3, level at 200^3-256^3.  Taller bricks
 // in y (BRICK41616, slices 64 B apart) lose: a tap's z+1 slice leaves the line.
+// COL48 (round 3) drops the z bricks altogether, and is the auto choice.
 constexpr size_t kCorner8MaxBytes = 160ull << 20;
 int auto_layout(int nx, int ny, int nz)
 {
     if (4 * layout_plane_bytes(LAYOUT_CORNERH, nx, ny, nz) <= kCorner8MaxBytes &&
         (long long)(nx + 1) * (ny + 1) * (nz + 1) <= kCornerHMaxPositions)
         return LAYOUT_CORNERH;
-    return 4 * layout_plane_bytes(LAYOUT_CORNER8, nx, ny, nz) <= kCorner8MaxBytes ? LAYOUT_CORNER8 : LAYOUT_BRICK4832;
+    // COL48 = BRICK4832 without z bricks (columns of 3 x 7 positions through the
+    // whole z extent): 2-4 % faster at 512^3 in round 3's same-box A/B
+    // (profiles/r03/slab_ab_grid512.txt, 0.160-0.163 vs 0.164-0.170 ms).
+    return 4 * layout_plane_bytes(LAYOUT_CORNER8, nx, ny, nz) <= kCorner8MaxBytes ? LAYOUT_CORNER8 : LAYOUT_COL48;
 }
 
 Ctx* as_ctx(void* p) { return static_cast<Ctx*>(p); }

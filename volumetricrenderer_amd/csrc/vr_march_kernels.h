@@ -565,18 +565,17 @@ __device__ __forceinline__ unsigned march_pixel_proc(const MarchArgs& a, const f
 // then sums its own S values in step order, so the arithmetic (and the
 // repeated-addition shadow positions) is exactly march_pixel_proc's.
 // Requires wave-uniform control flow: every lane of the wave calls it.
-//
-// The pairs are dealt STEP-major: all owners' shadow step 0, then step 1, ...
-// in lane order inside a step.  Neighbouring lanes of a round then evaluate
-// neighbouring rays at the same shadow step -- points a fraction of a texel
-// apart that share their Perlin lattice cells and Worley cells, so their
-// gradient-pair and cell-table reads broadcast instead of conflicting.  Dealt
-// owner-major (round 2), a round's lanes held one ray's consecutive shadow
-// steps, a lattice cell or more apart at the finer octaves, and the
-// ds_read_b128s of a 16-lane group scattered over the 256-entry pair table:
-// 2.6 bank-conflict cycles per LDS instruction (profiles/r02/pmc_cloud_shadow_final.json).
+// The pairs are dealt owner-major (a lane's run of steps is contiguous).  A
+// step-major deal -- all owners' step 0, then step 1, ..., so that a round's
+// neighbouring lanes evaluate neighbouring rays at one shadow step and share
+// lattice cells -- was 3 % slower at config 3 (two S-step ballot loops per
+// event instead of four bit-plane ballots; profiles/r03/ab_shadow_dealing.txt).
 constexpr int kMaxCompactShadow = 8;
-constexpr int kShadowSlots = 64 * kMaxCompactShadow;
+// Dealt pair pid lives at slot pid + pid / 32: an owner lane writes (and later
+// reads) its run at off_k + c, and the offsets of neighbouring lanes step by
+// their run lengths (~8), which without the pad puts 32 lanes on 4 LDS banks.
+__device__ __forceinline__ int shadow_slot(int pid) { return pid + (pid >> 5); }
+constexpr int kShadowSlots = 64 * kMaxCompactShadow + 64 * kMaxCompactShadow / 32;
 struct ShadowLds {
     float4 p[64];                        // primary positions of the lanes that need shadow rays, [lane]
                                          // (one 16-B LDS access each way)
@@ -629,40 +628,32 @@ __device__ __forceinline__ unsigned march_pixel_proc_compact(const MarchArgs& a,
                 }
                 sh->p[lane] = make_float4(P0, P1, P2, 0.0f);
             }
-            // Step-major deal: slot of (lane, step j) = base_j + (owners of step j
-            // below this lane), base_j = owners of the steps before j.  The
-            // step masks are wave-uniform (SGPRs); the same loop order writes
-            // and reads, so each lane sums its values in step order.
-            int total = 0;
-            for (int j = 0; j < S; ++j) {
-                const bool mine = need && j >= lo && j < lo + cnt;
-                const unsigned long long mj = __ballot(mine);
-                if (mine) sh->code[total + __popcll(mj & ((1ull << lane) - 1ull))] = ((unsigned)lane << 3) | (unsigned)j;
-                total += __popcll(mj);
+            // Exclusive prefix of cnt (0..8, four bits) over the wave, by bit-plane ballots.
+            int off = 0, total = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const unsigned long long bb = __ballot((cnt >> b) & 1);
+                off += __popcll(bb & ((1ull << lane) - 1ull)) << b;
+                total += __popcll(bb) << b;
             }
+            for (int c = 0; c < cnt; ++c) sh->code[shadow_slot(off + c)] = ((unsigned)lane << 3) | (unsigned)(lo + c);
             __builtin_amdgcn_wave_barrier();
             for (int base = 0; base < total; base += 64) {
                 const int pid = base + lane;
                 if (pid < total) {
-                    const unsigned code = sh->code[pid];
+                    const unsigned code = sh->code[shadow_slot(pid)];
                     const int kk = (int)(code >> 3), j = (int)(code & 7u);
                     const float4 pk = sh->p[kk];
                     float q0 = pk.x, q1 = pk.y, q2 = pk.z;
                     for (int jj = 0; jj <= j; ++jj) { q0 = q0 + l0; q1 = q1 + l1; q2 = q2 + l2; }
-                    sh->d[pid] = proc_density<TABLE>(p, wt, a.scale, q0, q1, q2, cells);
+                    sh->d[shadow_slot(pid)] = proc_density<TABLE>(p, wt, a.scale, q0, q1, q2, cells);
                     ++evals;
                 }
             }
             __builtin_amdgcn_wave_barrier();
-            float sl = 0.0f;
-            int at = 0;
-            for (int j = 0; j < S; ++j) {
-                const bool mine = need && j >= lo && j < lo + cnt;
-                const unsigned long long mj = __ballot(mine);
-                if (mine) sl = sl + sh->d[at + __popcll(mj & ((1ull << lane) - 1ull))];
-                at += __popcll(mj);
-            }
             if (need) {
+                float sl = 0.0f;
+                for (int c = 0; c < cnt; ++c) sl = sl + sh->d[shadow_slot(off + c)];
                 const float tl = spec_expf(-(sl * p.od));
                 rad = fmaf((tv * (rho * p.od)), tl, rad);
             }

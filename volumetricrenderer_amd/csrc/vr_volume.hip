@@ -121,8 +121,13 @@ __global__ __launch_bounds__(kBlock) void k_build_layout(const uint8_t* __restri
 // kernel before it (a 1-B store and 8 scattered planar reads per thread,
 // 64-bit decode) took 4.0 ms at 512^3.
 constexpr int kBrickStageBytes = 16 * 1024;
+//
+// zseg > 0 (COL48, whose columns run through the whole z extent): a workgroup
+// builds segment blockIdx.y -- slices [zseg * seg, zseg * (seg + 1)) -- of a
+// run of columns; a column's segment is contiguous, the run's columns sit a
+// column (g.brick bytes) apart.
 __global__ __launch_bounds__(kBlock) void k_build_bricks(const uint8_t* __restrict__ planar, int nx, int ny, int nz,
-                                                         LayoutGeom g, int run, long long plane_bytes,
+                                                         LayoutGeom g, int run, long long plane_bytes, int zseg,
                                                          uint8_t* __restrict__ out)
 {
     __shared__ uint8_t st[kBrickStageBytes];
@@ -131,8 +136,9 @@ __global__ __launch_bounds__(kBlock) void k_build_bricks(const uint8_t* __restri
     const int runs_x = (g.nbx + run - 1) / run;
     const int rx = (int)blockIdx.x % runs_x, by = (int)blockIdx.x / runs_x, bz = (int)blockIdx.y;
     const int bx0 = rx * run, nb = min(run, g.nbx - bx0);
-    const int rn0 = g.Rn[0], rn1 = g.Rn[1], rn2 = g.Rn[2];
-    const int x0 = g.Ba[0] * bx0 - 1, y0 = g.Ba[1] * by - 1, z0 = g.Ba[2] * bz - 1;
+    const int rn0 = g.Rn[0], rn1 = g.Rn[1], rn2 = zseg > 0 ? min(zseg, g.Rn[2] - zseg * bz) : g.Rn[2];
+    // slice w of a COL48 column holds padded z position w (texel w - 1)
+    const int x0 = g.Ba[0] * bx0 - 1, y0 = g.Ba[1] * by - 1, z0 = zseg > 0 ? zseg * bz - 1 : g.Ba[2] * bz - 1;
     const int xe = x0 + g.Ba[0] * (nb - 1) + rn0;    // one past the last staged x
     const int rows = rn1 * rn2;
     // stage: rows (v, w) of the source box, x fastest over the whole workgroup.
@@ -161,12 +167,16 @@ __global__ __launch_bounds__(kBlock) void k_build_bricks(const uint8_t* __restri
         }
     }
     __syncthreads();
-    // write: the run's bricks are contiguous, brick by brick in-brick order x fastest
-    const unsigned used = (unsigned)(rn0 * rn1 * rn2), per_brick = g.brick / 16u;
-    uint4* __restrict__ dst = reinterpret_cast<uint4*>(out + (long long)ch * plane_bytes +
-                                                       ((long long)(bz * g.nby + by) * g.nbx + bx0) * g.brick);
+    // write: the run's bricks are contiguous, brick by brick in-brick order x
+    // fastest (COL48: each column's segment is contiguous, columns g.brick apart)
+    const unsigned used = (unsigned)(rn0 * rn1 * rn2);
+    const unsigned per_brick = zseg > 0 ? used / 16u : g.brick / 16u;   // COL48: 32 B per slice
+    uint8_t* __restrict__ dst0 = out + (long long)ch * plane_bytes +
+                                 (zseg > 0 ? ((long long)by * g.nbx + bx0) * g.brick + (long long)bz * rn0 * rn1 * zseg
+                                           : ((long long)(bz * g.nby + by) * g.nbx + bx0) * g.brick);
     for (unsigned c = threadIdx.x; c < (unsigned)nb * per_brick; c += kBlock) {
         const unsigned j = c / per_brick, b0 = (c - j * per_brick) * 16u;
+        uint4* __restrict__ dst = reinterpret_cast<uint4*>(dst0 + (long long)j * g.brick) - j * per_brick;
         unsigned u = b0 % (unsigned)rn0, v = (b0 / (unsigned)rn0) % (unsigned)rn1, w = b0 / (unsigned)(rn0 * rn1);
         const unsigned xb = j * (unsigned)g.Ba[0] + (unsigned)(x0 - xa);
         unsigned word[4] = {0u, 0u, 0u, 0u};
@@ -350,6 +360,16 @@ hipError_t launch_build_layout(int layout, const uint8_t* d_planar, int nx, int 
     const long long pb = (long long)layout_plane_bytes(layout, nx, ny, nz);
     const dim3 gr(grid_for(4 * elems)), b(kBlock);
     const long long rows = (long long)g.Rn[1] * g.Rn[2];
+    if (layout == LAYOUT_COL48) {
+        // columns in z segments of 32 slices (1 KiB of a column: BRICK4832's stage)
+        constexpr int kSeg = 32;
+        const long long srows = (long long)g.Rn[1] * kSeg;
+        const int run = (int)std::min<long long>(g.nbx, (kBrickStageBytes / srows - g.Rn[0] - 7) / g.Ba[0] + 1);
+        const int runs_x = (g.nbx + run - 1) / run;
+        const dim3 gb((unsigned)(runs_x * g.nby), (unsigned)((g.Rn[2] + kSeg - 1) / kSeg), 4);   // last segment partial
+        hipLaunchKernelGGL(k_build_bricks, gb, b, 0, s, d_planar, nx, ny, nz, g, run, pb, kSeg, d_out);
+        return hipGetLastError();
+    }
     if (layout != LAYOUT_CORNER8 && layout != LAYOUT_CORNERH && layout != LAYOUT_ZPAIR && g.brick % 16u == 0 &&
         rows * (g.Ba[0] + g.Rn[0] + 8) <= kBrickStageBytes) {
         // bricks per workgroup: the longest run whose source box (+ up to 7
@@ -357,7 +377,7 @@ hipError_t launch_build_layout(int layout, const uint8_t* d_planar, int nx, int 
         const int run = (int)std::min<long long>(g.nbx, (kBrickStageBytes / rows - g.Rn[0] - 7) / g.Ba[0] + 1);
         const int runs_x = (g.nbx + run - 1) / run;
         const dim3 gb((unsigned)(runs_x * g.nby), (unsigned)g.nbz, 4);
-        hipLaunchKernelGGL(k_build_bricks, gb, b, 0, s, d_planar, nx, ny, nz, g, run, pb, d_out);
+        hipLaunchKernelGGL(k_build_bricks, gb, b, 0, s, d_planar, nx, ny, nz, g, run, pb, 0, d_out);
         return hipGetLastError();
     }
     switch (layout) {
