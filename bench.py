@@ -153,6 +153,7 @@ def main() -> int:
     ap.add_argument("--pipeline1", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--layout", type=int, default=0, help="vr layout preference (0 = auto; 15 = COL48)")
     ap.add_argument("--slab", action="store_true", help="COL48 layout + the LDS-slab march (vr_march_slab.hip)")
+    ap.add_argument("--opt", action="append", default=[], help="vr option NAME=VALUE (experiments)")
     ap.add_argument("--spin", action="store_true",
                     help="moving camera: every frame gets new shader data, phi += 1.6 deg (the reference's "
                          "held A/D key, TestMain.cpp:171-184, :222-224); N = 1 only")
@@ -190,6 +191,9 @@ def main() -> int:
         r.generate_volume(vr.scaled_recipe(N))
     osd, gsd = vr.reference_shader_data(1280.0 / 720.0)
     r.set_option("schedule", args.schedule)
+    for o in args.opt:
+        k, v = o.split("=")
+        r.set_option(k, int(v))
     if args.slab:
         args.layout = 15
         r.set_option("slab", 1)

@@ -452,6 +452,23 @@ def test_procedural_config3_shadow(r, oracle, schedule, suffix):
     assert img[..., 0].max() > 0.0
 
 
+def test_procedural_shadow_region_enumeration(r, oracle):
+    """Config 3 with the 64x64-region sort enumeration (option "proc_enum",
+    a round-3 experiment; row-major is the default with shadow rays) stays
+    bit-exact, with early-out and short shadow runs too."""
+    r.set_option("proc_enum", 1)
+    try:
+        for W, H, m, kw in [(128, 72, vr.march_defaults(max_steps=128), dict(shadow_steps=8)),
+                            (96, 64, vr.march_defaults(max_steps=96, density=400.0, early_out=0.01),
+                             dict(shadow_steps=5, sun_dir=(-1.0, 0.5, 0.25)))]:
+            img, ref, c, s, var = render_proc_both(r, oracle, W, H, m, **kw)
+            assert var == "procedural_shadow"
+            assert_exact(img, ref)
+            assert c == s > 0
+    finally:
+        r.set_option("proc_enum", 0)
+
+
 @pytest.mark.parametrize("kw", [dict(octaves=1, seed_fbm=11), dict(octaves=6, gain=0.6, worley_freq=0.05),
                                 dict(shadow_steps=3, sun_dir=(0.0, 1.0, 0.0)),
                                 dict(shadow_steps=16, sun_dir=(-1.0, 0.5, 0.25)),

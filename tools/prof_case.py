@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--proc", action="store_true", help="procedural medium (config 2)")
     ap.add_argument("--shadow", type=int, default=0, help="procedural shadow steps (config 3: 8)")
     ap.add_argument("--slab", type=int, default=-1, help="LDS slab march (COL48): 1 on, 0 off")
+    ap.add_argument("--proc-enum", type=int, default=-1, help="procedural sort: 1 region enumeration with shadows")
     ap.add_argument("--slab-cap", type=int, default=-1)
     a = ap.parse_args()
     with vr.Renderer(0) as r:
@@ -42,6 +43,8 @@ def main():
             r.set_option("schedule", a.schedule)
         if a.slab >= 0:
             r.set_option("slab", a.slab)
+        if a.proc_enum >= 0:
+            r.set_option("proc_enum", a.proc_enum)
         if a.slab_cap >= 0:
             r.set_option("slab_cap", a.slab_cap)
         if a.wedges > 0:

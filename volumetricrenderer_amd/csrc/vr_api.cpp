@@ -90,6 +90,7 @@ struct Ctx {
     int wedges = kDefaultWedges;   // wedges per XCD
     int split = 0;                 // lanes per ray: 0 = auto, 1, 2, 4, 8
     int slab = 0;                  // COL48 + regions: the LDS slab march (vr_march_slab.hip)
+    int proc_enum = 0;             // procedural sort: 1 = 64x64-region enumeration with shadow rays too
     int slab_cap = kSlabMaxChunks; // its chunks per channel (<= kSlabMaxChunks; smaller forces the fallback)
     struct RegionBuf {
         unsigned* d = nullptr;     // device tile list
@@ -690,6 +691,11 @@ vr_status vr_set_option(void* p, const char* name, int value)
         c->wedges = value;
         return VR_OK;
     }
+    if (n == "proc_enum") {
+        if (value < 0 || value > 1) return fail(VR_ERR_INVALID, "vr_set_option: proc_enum is 0 or 1");
+        c->proc_enum = value;
+        return VR_OK;
+    }
     if (n == "slab") {
         if (value < 0 || value > 1) return fail(VR_ERR_INVALID, "vr_set_option: slab is 0 or 1");
         c->slab = value;
@@ -729,6 +735,7 @@ int vr_get_option(void* p, const char* name)
     if (n == "split") return c->split;
     if (n == "lattice") return c->lattice;
     if (n == "slab") return c->slab;
+    if (n == "proc_enum") return c->proc_enum;
     if (n == "slab_cap") return c->slab_cap;
     return -1;
 }
@@ -1023,6 +1030,7 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
         for (int ax = 0; ax < 3; ++ax) q.lstep[ax] = (a.step_size * c->proc.sun_dir[ax]) / a.box_range[ax];
         q.od = a.step_size * m.density;
         q.count_evals = c->count;
+        q.enum_regions = c->proc_enum;
         // Worley cell table (LDS): box points P in [0,1]^3 give cellular
         // coordinates in [0, G] per axis, G = grid_scale * worley_freq; the
         // 3x3x3 neighbourhood of rint() of those, with 2 cells of margin.
@@ -1099,7 +1107,7 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
         if (sort_buf) {
             key = {(float)a.width, (float)a.height, (float)a.out_rows, (float)a.band_rows, (float)a.band_stride,
                    (float)a.band_first, (float)a.max_steps, a.step_size, (float)a.cam_mode,
-                   (float)(a.proc.shadow_steps > 0)};
+                   (float)(a.proc.shadow_steps > 0), (float)a.proc.enum_regions};
             for (const float* v : {a.org, a.o, a.px, a.py, a.cam, a.box_min, a.box_max, a.box_range})
                 key.insert(key.end(), v, v + 3);
             key.insert(key.end(), a.r2, a.r2 + 4);

@@ -145,6 +145,7 @@ struct ProcParams {
     int wt_lo, wt_n;  // Worley cell table in LDS: cells [wt_lo, wt_lo + wt_n)^3; wt_n = 0: none
     int wt_pz;        // its z pitch in entries (>= wt_n^2, padded against LDS bank aliasing)
     int wt_fixed;     // 1: the fixed geometry wt_n = 9, wt_pz = 83 (noise::cellular_table9)
+    int enum_regions; // sort passes: 1 = 64x64-region enumeration also with shadow rays
     // Perlin lattice table (global, noise::perlin_lattice_entry): cells
     // [lat_lo, lat_lo + lat_n)^3, entry (x, y, z) at byte offset
     // 8 x + lat_sy y + lat_sz z - lat_c, all exact in fp32.  Null: none.

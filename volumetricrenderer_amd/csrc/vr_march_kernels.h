@@ -568,8 +568,11 @@ __device__ __forceinline__ unsigned march_pixel_proc(const MarchArgs& a, const f
 // The pairs are dealt owner-major (a lane's run of steps is contiguous).  A
 // step-major deal -- all owners' step 0, then step 1, ..., so that a round's
 // neighbouring lanes evaluate neighbouring rays at one shadow step and share
-// lattice cells -- was 3 % slower at config 3 (two S-step ballot loops per
-// event instead of four bit-plane ballots; profiles/r03/ab_shadow_dealing.txt).
+// lattice cells -- cut the bank conflicts from 2.6 to 2.2 cycles per LDS
+// instruction (1.4 together with the 64x64-region enumeration, option
+// "proc_enum") and the VALU count by 2-6 %, yet ran 2-5 % slower
+// (profiles/r03/ab_config3_deal_enum.txt, pmc_config3_deal_enum.txt): the
+// conflicts are not on config 3's critical path.  Removed after measuring.
 constexpr int kMaxCompactShadow = 8;
 // Dealt pair pid lives at slot pid + pid / 32: an owner lane writes (and later
 // reads) its run at off_k + c, and the offsets of neighbouring lanes step by
@@ -1099,7 +1102,7 @@ __device__ __forceinline__ int cost_key(int n) { return n < kKeyBins - 1 ? n : k
 constexpr int kSortRegion = 64;
 __device__ __forceinline__ bool sort_pixel(const MarchArgs& a, unsigned idx, int* x, int* orow)
 {
-    if (a.proc.shadow_steps > 0) {
+    if (a.proc.shadow_steps > 0 && !a.proc.enum_regions) {
         *orow = (int)(idx / (unsigned)a.width);
         *x = (int)(idx - (unsigned)*orow * (unsigned)a.width);
         return *orow < a.out_rows;
