@@ -42,6 +42,7 @@ from volumetricrenderer_amd import distributed as vrdist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: fp32 vector peak
+TA_PEAK_GLOOKUPS = 256 * 2.4   # L1 tag lookups: 1 per CU-cycle at 2.4 GHz (tools/tcp_calib.hip)
 BYTES_PER_STEP = 32        # 4 trilinear taps x 8 texels x 1 B
 # fp32 FLOP per executed grid ray-step (FMA = 2): per tap, texel coordinate 3 fma (6),
 # 3 fractions (3), 7 lerps x (sub + fma) (21), x 1/255 (1) = 31; x 4 taps = 124;
@@ -366,12 +367,24 @@ def main() -> int:
                         "flop_per_eval_27cell": fpd27,
                         "frac_27cell": round(a27 / FP32_PEAK_TFLOPS, 4)}
         traffic = None
+        ta = None
         tfile = os.path.join(ROOT, "profiles", "traffic.json")
         if os.path.exists(tfile):
             with open(tfile) as f:
                 tj = json.load(f)
             if tj.get("config") == args.config and tj.get("kernel") == r.kernel_variant and world == 1:
                 traffic = tj.get("hbm_bytes_per_launch")
+                lookups = tj.get("l1_lookups_per_launch")
+                if lookups:
+                    # the unit that binds config 5: the texture
+                    # address pipe, ~1 cycle per L1 lookup (quad x distinct 128-B line)
+                    rate = lookups / (kern_ms * 1e-3) / 1e9
+                    ta = {"achieved": round(rate, 1), "peak": TA_PEAK_GLOOKUPS, "unit": "G L1 lookups/s",
+                          "frac": round(rate / TA_PEAK_GLOOKUPS, 4), "lookups_per_launch": lookups,
+                          "ta_busy_pmc": tj.get("ta_busy"),
+                          "def": "PMC TCP_TOTAL_CACHE_ACCESSES_sum per launch (profiles/traffic.json) / the mean "
+                                 "march-kernel duration; peak = 256 CUs x 1 lookup/cycle x 2.4 GHz "
+                                 "(tools/tcp_calib.hip)"}
         out = {
             "metric": "Mray/s (= W*H*steps/s) at 1080p x 128 steps" if (W, H, S) == (1920, 1080, 128)
                       else f"Mray/s (= W*H*steps/s) at {W}x{H} x {S} steps",
@@ -407,7 +420,8 @@ def main() -> int:
                                  "traffic_frac": round(traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                                  "traffic_def": "PMC HBM bytes per launch (profiles/traffic.json) / the same "
                                                 "mean kernel duration: the bytes the kernel really moves"}
-                                if traffic else {})),
+                                if traffic else {}),
+                             **({"ta_lookup": ta} if ta else {})),
         }
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(None if proc is not None else r.get_volume(), osd, gsd, march, W, H,

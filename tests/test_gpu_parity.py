@@ -185,6 +185,42 @@ def test_every_layout_bitexact(r, oracle, vol128, layout, name):
         r.set_layout_preference(0)
 
 
+@pytest.mark.parametrize("layout", [15, 12, 14, 7])
+def test_split_long_tiles_bitexact(r, oracle, vol128, layout):
+    """split_long (march_regions_mixed): the tiles costing >= split_long % of
+    the longest are marched as two 8x4 halves with two lanes per ray, the rest
+    with one.  split = 1 forces the one-lane frame the mix applies to on these
+    small targets.  1 % splits every tile with work, 100 % only the longest;
+    bit-exact with exact step counts, with and without early-out, and with a
+    banded target (packed rows)."""
+    r.set_volume(vol128)
+    r.set_layout_preference(layout)
+    r.set_option("split", 1)
+    try:
+        for pct in (1, 60, 100):
+            r.set_option("split_long", pct)
+            assert r.get_option("split_long") == pct
+            for (W, H, phi, theta) in [(480, 270, 0.0, 0.0), (203, 117, 35.0, -20.0)]:
+                osd, gsd = vr.reference_shader_data(W / H, phi, theta)
+                img, ref, c, s = render_both(r, oracle, vol128, W, H, osd, gsd)
+                assert_exact(img, ref)
+                assert c == s
+        r.set_option("split_long", 50)
+        osd, gsd = vr.reference_shader_data(16 / 9, -40.0, 15.0)
+        m = vr.march_defaults(early_out=0.5)
+        img, ref, c, s = render_both(r, oracle, vol128, 320, 180, osd, gsd, march=m)
+        assert_exact(img, ref)
+        assert c == s
+        img, ref, c, s = render_both(r, oracle, vol128, 320, 180, osd, gsd, band_rows=16, band_stride=3,
+                                     band_first=1)
+        assert_exact(img, ref)
+        assert c == s
+    finally:
+        r.set_option("split_long", 0)
+        r.set_option("split", 0)
+        r.set_layout_preference(0)
+
+
 @pytest.mark.parametrize("cap", [32, 12, 0])
 def test_slab_march_bitexact(r, oracle, vol128, cap):
     """The LDS-slab march (COL48 + option slab, vr_march_slab.hip): per step a

@@ -52,7 +52,7 @@ constexpr int kDefaultWedges = 4;         // regions schedule: wedges per XCD (m
 // region lists for this many renders before they are rebuilt
 constexpr int kRegionRebuildInterval = 32;
 constexpr int kMaxRegionStreams = 4;
-constexpr int kRegionKeyLen = 32;
+constexpr int kRegionKeyLen = 34;
 // auto split (lanes per ray) from the frame share's tiles with work: K = 1 at
 // >= 6000, 2 at >= 1400, else 4.  Measured on 1/N of the 1080p frame at 512^3
 // (~7,500 tiles with work): K = 1, 2, 2, 4 at N = 1, 2, 4, 8.
@@ -92,12 +92,14 @@ struct Ctx {
     int slab = 0;                  // COL48 + regions: the LDS slab march (vr_march_slab.hip)
     int proc_enum = 0;             // procedural sort: 1 = 64x64-region enumeration with shadow rays too
     int slab_cap = kSlabMaxChunks; // its chunks per channel (<= kSlabMaxChunks; smaller forces the fallback)
+    int split_long = 0;            // regions: tiles costing >= this % of the longest split in two halves (0 = off)
     struct RegionBuf {
         unsigned* d = nullptr;     // device tile list
         unsigned* h = nullptr;     // pinned staging copy
         size_t cap = 0;            // entries
         TileMap map{};
         int nwork = 0;             // tiles with estimated work
+        bool mixed = false;        // the lists hold split halves of the longest tiles (bit 31)
         // the streams that rendered with these lists; when the lists are
         // retired an event is recorded on each, and the buffer is rewritten
         // only after those events (kMaxRegionStreams; more -> device sync)
@@ -707,6 +709,11 @@ vr_status vr_set_option(void* p, const char* name, int value)
         c->slab_cap = value;
         return VR_OK;
     }
+    if (n == "split_long") {
+        if (value < 0 || value > 100) return fail(VR_ERR_INVALID, "vr_set_option: split_long in [0, 100] (percent)");
+        c->split_long = value;
+        return VR_OK;
+    }
     if (n == "count") {
         if (value < 0 || value > 2)
             return fail(VR_ERR_INVALID, "vr_set_option: count is 0 (steps), 1 (evals) or 2 (Worley cells)");
@@ -737,6 +744,7 @@ int vr_get_option(void* p, const char* name)
     if (n == "slab") return c->slab;
     if (n == "proc_enum") return c->proc_enum;
     if (n == "slab_cap") return c->slab_cap;
+    if (n == "split_long") return c->split_long;
     return -1;
 }
 
@@ -815,13 +823,13 @@ vr_status note_region_stream(Ctx::RegionBuf& rb, hipStream_t s)
     return VR_OK;
 }
 
-vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow, hipStream_t stream)
+vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow, bool mixable, hipStream_t stream)
 {
     const int tw = (a.width + 7) >> 3, th = (a.out_rows + 7) >> 3;
     float key[kRegionKeyLen] = {(float)tw, (float)th, (float)a.width, (float)a.height, (float)a.out_rows,
                                 (float)a.band_rows, (float)a.band_stride, (float)a.band_first, (float)tpw,
-                                (float)c->wedges};
-    constexpr int grid_part = 10;   // the part a reused list must match
+                                (float)c->wedges, (float)(mixable ? c->split_long : 0), (float)c->split};
+    constexpr int grid_part = 12;   // the part a reused list must match
     int kn = grid_part;
     for (float v : {(float)a.max_steps, a.step_size, (float)cpx, (float)cprow}) key[kn++] = v;
     for (const float* v : {a.org, a.o, a.px, a.py, a.box_min, a.box_max})
@@ -885,7 +893,17 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     std::sort(idle.begin(), idle.end(), inside_out);
     for (size_t i = 0; i < idle.size(); ++i) xl[i % 8].push_back(idle[i]);
 
-    const size_t n = (size_t)tw * th;
+    // split_long: the tiles costing >= split_long % of the longest go in as two
+    // halves marched two lanes per ray (march_regions_mixed), only where the
+    // rest of the frame runs one lane per ray
+    double most_cost = 0.0;
+    for (const T& t : work) most_cost = std::max(most_cost, t.cost);
+    const double split_at = std::max(1.0, most_cost * c->split_long / 100.0);
+    const bool mixed = mixable && c->split_long > 0 && th < 16384 &&
+                       (c->split == 1 || (c->split == 0 && (long long)work.size() >= kSplitOneLane));
+    size_t n = (size_t)tw * th;
+    if (mixed)
+        for (const T& t : work) n += t.cost >= split_at;
     if (c->region_cur >= 0) {   // retire the current lists in the stream order of their renders
         Ctx::RegionBuf& old = c->region[c->region_cur];
         old.nretired = 0;
@@ -917,8 +935,15 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     size_t pos = 0, most = 0;
     for (int x = 0; x < 8; ++x) {
         m.off[x] = (int)pos;
-        for (const T& t : xl[x]) rb.h[pos++] = t.id;
-        most = std::max(most, xl[x].size());
+        for (const T& t : xl[x]) {
+            if (mixed && t.cost >= split_at) {
+                rb.h[pos++] = t.id | 0x80000000u;
+                rb.h[pos++] = t.id | 0xc0000000u;
+            } else {
+                rb.h[pos++] = t.id;
+            }
+        }
+        most = std::max(most, pos - (size_t)m.off[x]);
     }
     m.off[8] = (int)pos;
     m.nwx = std::max(1, (int)((most + tpw - 1) / tpw));
@@ -928,6 +953,7 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     rb.upload_stream = stream;
     rb.map = m;
     rb.nwork = (int)work.size();
+    rb.mixed = mixed;
     rb.nstreams = 0;
     const vr_status st = note_region_stream(rb, stream);
     if (st != VR_OK) return st;
@@ -1080,7 +1106,7 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
         // schedule 0 = one 8x8 tile per wave in row order, 4 = in rings;
         // otherwise (auto) the cost-sorted schedule
         void* sort_buf = nullptr;
-        Schedule sc{c->schedule == SCHED_RINGS ? SCHED_RINGS : SCHED_STATIC, 0, 0, 1, 1, nullptr, nullptr, {}, 1, 0};
+        Schedule sc{c->schedule == SCHED_RINGS ? SCHED_RINGS : SCHED_STATIC, 0, 0, 1, 1, nullptr, nullptr, {}, 1, 0, 0};
         if (sc.kind == SCHED_RINGS) box_centre_pixel(c, a, &sc.center_x, &sc.center_y);
         // the sort passes enumerate whole 64x64 regions (vr_march_kernels.h sort_pixel)
         if (c->schedule != SCHED_STATIC && c->schedule != SCHED_RINGS && a.width < 65536 && a.out_rows < 65536 &&
@@ -1124,20 +1150,23 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
     // wedges of the frame, each walked inside-out (longest rays first)
     const int kind = c->schedule >= 0 ? c->schedule : SCHED_REGIONS;
     const int tpw = c->tiles_per_wave > 0 ? c->tiles_per_wave : (kind == SCHED_RINGS || kind == SCHED_REGIONS ? 2 : 1);
-    Schedule sc{kind, 0, 0, tpw, c->waves_per_simd, c->d_heads, nullptr, {}, 1, 0};
+    Schedule sc{kind, 0, 0, tpw, c->waves_per_simd, c->d_heads, nullptr, {}, 1, 0, 0};
     sc.slab = pl.layout == LAYOUT_COL48 && c->slab;
     a.slab_cap = c->slab_cap;
     if (kind == SCHED_RINGS || kind == SCHED_REGIONS) box_centre_pixel(c, a, &sc.center_x, &sc.center_y);
     if (kind == SCHED_REGIONS) {
-        const vr_status st = build_regions(c, a, tpw, sc.center_x, sc.center_y, static_cast<hipStream_t>(stream));
+        const bool splittable = is_b4_family(pl.layout) || pl.layout == LAYOUT_ZPAIR || pl.layout == LAYOUT_CORNER8 ||
+                                pl.layout == LAYOUT_CORNERH;
+        const vr_status st = build_regions(c, a, tpw, sc.center_x, sc.center_y, splittable && !sc.slab,
+                                           static_cast<hipStream_t>(stream));
         if (st != VR_OK) return st;
         const Ctx::RegionBuf& rb = c->region[c->region_cur];
         sc.tiles = rb.d;
         sc.map = rb.map;
+        sc.mixed = rb.mixed;
         // step-split rays: K lanes per ray when the frame
         // share is too small to fill the GPU with one-lane-per-ray waves
-        if (is_b4_family(pl.layout) || pl.layout == LAYOUT_ZPAIR || pl.layout == LAYOUT_CORNER8 ||
-            pl.layout == LAYOUT_CORNERH) {
+        if (splittable && !rb.mixed) {
             int K = c->split;
             if (sc.slab) K = K == 0 ? 1 : K;   // the slab march has one lane per ray; split > 1 uses the plain march
             if (K == 0) {

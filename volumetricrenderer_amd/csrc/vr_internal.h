@@ -206,6 +206,7 @@ struct Schedule {
     TileMap map;           // regions (nwx counts waves of split units)
     int split;             // regions: lanes per ray (1, 2, 4, 8; BRICK4 / CORNER8 only)
     int slab;              // regions + COL48: the LDS slab march (vr_march_slab.hip)
+    int mixed;             // regions: the list holds split halves of the longest tiles (march_regions_mixed)
 };
 
 // launchers (vr_march.hip / vr_volume.hip); return hipError_t
