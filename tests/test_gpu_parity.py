@@ -121,31 +121,42 @@ def test_spinning_camera_frames(r, oracle, vol128, layout):
         r.set_layout_preference(0)
 
 
-def test_spinning_camera_procedural(r, oracle):
+@pytest.mark.parametrize("shadow", [0, 8])
+def test_spinning_camera_procedural(r, oracle, shadow):
     """The procedural march under a moving camera: every frame has new
-    geometry, so the cost sort (bin, scan, scatter) runs again each frame
-    instead of being reused; frames 1, 33 and 40 of a 1.6-degree spin equal
-    the oracle bit for bit."""
+    geometry.  With sort_reuse = 31 the cost sort (bin, scan, scatter) is built
+    at frame 1 and again at frame 33; frames in between march the stale order
+    of an older camera and, in the trailing blocks, the pixels it left out
+    (vr_render SORT_STALE).  Frames 1, 2, 32, 33 and 40 of a 1.6-degree spin
+    equal the oracle bit for bit, step counts included; by frame 32 the cube
+    has turned ~50 degrees, so many pixels changed coverage.  With sort_reuse
+    0 (the default) every frame sorts again."""
     W, H = 160, 96
     m = vr.march_defaults(max_steps=64)
     r.set_march(m)
-    r.set_procedural()
+    r.set_procedural(shadow_steps=shadow)
     p = oracle.procedural_from(r.procedural)
     keep = {}
     try:
-        for i in range(1, 41):
-            osd, gsd = vr.reference_shader_data(W / H, SPIN_DEG * i, 0.0)
-            r.set_shader_data(osd, gsd)
-            img = r.render(W, H, 0)
-            if i in (1, 33, 40):
-                keep[i] = (img, osd, gsd)
+        for reuse in (31, 0):
+            r.set_option("sort_reuse", reuse)
+            assert r.get_option("sort_reuse") == reuse
+            for i in range(1, 41):
+                osd, gsd = vr.reference_shader_data(W / H, SPIN_DEG * i, 0.0)
+                r.set_shader_data(osd, gsd)
+                cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+                img = r.render(W, H, 0, step_counter=cnt)
+                if i in (1, 2, 32, 33, 40) and (reuse or i == 2):
+                    keep[(reuse, i)] = (img, cnt, osd, gsd)
         torch.cuda.synchronize()
     finally:
+        r.set_option("sort_reuse", 0)
         r.set_procedural(enabled=0)
-    for i, (img, osd, gsd) in keep.items():
+    for (reuse, i), (img, cnt, osd, gsd) in keep.items():
         obj, glob = vr.shader_data_arrays(osd, gsd)
-        ref, _ = oracle.render_procedural(p, obj, glob, oracle.from_params(m), W, H, 0)
+        ref, steps = oracle.render_procedural(p, obj, glob, oracle.from_params(m), W, H, 0)
         assert_exact(img.cpu().numpy(), ref)
+        assert int(cnt.item()) == steps, (reuse, i)
 
 
 def test_media_scroll_mirrored_repeat(r, oracle, vol128):

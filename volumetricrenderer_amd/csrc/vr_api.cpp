@@ -51,6 +51,12 @@ constexpr int kDefaultWedges = 4;         // regions schedule: wedges per XCD (m
 // a moving camera reuses the current (still complete, maybe less balanced)
 // region lists for this many renders before they are rebuilt
 constexpr int kRegionRebuildInterval = 32;
+// Procedural cost sort under a moving camera: with option sort_reuse = R > 0 a
+// frame with the same target and march settings but another camera marches the
+// order built for an older one, for R renders after the build (vr_render; the
+// march then also checks the pixels the old order left out, so every frame
+// stays exact).
+constexpr size_t kSortKeyGridPart = 11;   // leading sort-key entries a stale order must match
 constexpr int kMaxRegionStreams = 4;
 constexpr int kRegionKeyLen = 34;
 // auto split (lanes per ray) from the frame share's tiles with work: K = 1 at
@@ -116,6 +122,8 @@ struct Ctx {
     // procedural cost sort: the geometry whose order d_sort holds (n per pixel
     // depends only on it, not on the medium), valid until the buffer changes
     std::vector<float> sort_key;
+    long long renders_since_sort = 0;   // renders with a stale order since it was built
+    int sort_reuse = 0;                 // option "sort_reuse": renders a stale order serves (0 = sort every changed frame)
     // Perlin lattice table of the procedural march (noise::perlin_lattice_entry),
     // built when (seed, lo, n) changes; option "lattice" 0 turns it off
     int lattice = 1;
@@ -714,6 +722,11 @@ vr_status vr_set_option(void* p, const char* name, int value)
         c->split_long = value;
         return VR_OK;
     }
+    if (n == "sort_reuse") {
+        if (value < 0 || value > 64) return fail(VR_ERR_INVALID, "vr_set_option: sort_reuse in [0, 64] renders");
+        c->sort_reuse = value;
+        return VR_OK;
+    }
     if (n == "count") {
         if (value < 0 || value > 2)
             return fail(VR_ERR_INVALID, "vr_set_option: count is 0 (steps), 1 (evals) or 2 (Worley cells)");
@@ -745,6 +758,7 @@ int vr_get_option(void* p, const char* name)
     if (n == "proc_enum") return c->proc_enum;
     if (n == "slab_cap") return c->slab_cap;
     if (n == "split_long") return c->split_long;
+    if (n == "sort_reuse") return c->sort_reuse;
     return -1;
 }
 
@@ -1128,7 +1142,7 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
         // The sorted order depends only on each pixel's step count n (a3),
         // i.e. on the frame geometry below, not on the medium: a frame with
         // the same geometry reuses it (like the region lists of the grid path)
-        bool reuse = false;
+        int reuse = SORT_BUILD;
         std::vector<float> key;
         if (sort_buf) {
             key = {(float)a.width, (float)a.height, (float)a.out_rows, (float)a.band_rows, (float)a.band_stride,
@@ -1138,12 +1152,18 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
                 key.insert(key.end(), v, v + 3);
             key.insert(key.end(), a.r2, a.r2 + 4);
             key.insert(key.end(), a.r3, a.r3 + 4);
-            reuse = key.size() == c->sort_key.size() &&
-                    std::memcmp(key.data(), c->sort_key.data(), key.size() * sizeof(float)) == 0;
+            const bool same_size = key.size() == c->sort_key.size();
+            if (same_size && std::memcmp(key.data(), c->sort_key.data(), key.size() * sizeof(float)) == 0)
+                reuse = SORT_REUSE;
+            else if (same_size && c->renders_since_sort < c->sort_reuse &&
+                     std::memcmp(key.data(), c->sort_key.data(), kSortKeyGridPart * sizeof(float)) == 0)
+                reuse = SORT_STALE;
         }
+        std::vector<float> built = reuse == SORT_BUILD ? key : c->sort_key;
         c->sort_key.clear();   // valid again only once this launch is queued
         HIP_TRY(launch_march_procedural(a, m.early_out > 0.0f, sort_buf, reuse, sc, static_cast<hipStream_t>(stream)));
-        c->sort_key = key;
+        c->sort_key = std::move(built);
+        c->renders_since_sort = reuse == SORT_STALE ? c->renders_since_sort + 1 : 0;
         return VR_OK;
     }
     // auto schedule (measured): regions -- per-XCD angular

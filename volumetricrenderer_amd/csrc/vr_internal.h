@@ -217,9 +217,12 @@ hipError_t launch_march_slab(const MarchArgs& a, bool early, const Schedule& sc,
 constexpr int kSlabMaxChunks = 32;   // per channel and wave (64 B each): 8 KiB of LDS per wave
 // sort_buf (proc_sort_bytes) selects the cost-sorted schedule; null = 8x8
 // tiles, in rings when sc.kind == SCHED_RINGS, else in row order
-// reuse_sort: sort_buf holds the order of a frame with the same geometry
-// (vr_api.cpp sort key): skip the sort passes, write the background only
-hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_buf, bool reuse_sort, const Schedule& sc,
+// reuse_sort (vr_api.cpp sort key): SORT_BUILD = sort this frame; SORT_REUSE =
+// sort_buf holds the order of a frame with the same geometry (skip the sort
+// passes, write the background only); SORT_STALE = the order of an older camera
+// with the same target (skip the sort passes, march the pixels it left out too)
+enum { SORT_BUILD = 0, SORT_REUSE = 1, SORT_STALE = 2 };
+hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_buf, int reuse_sort, const Schedule& sc,
                                    hipStream_t s);
 size_t proc_sort_bytes(int width, int out_rows);
 hipError_t launch_repack(const uint8_t* d_rgba, int nx, int ny, int nz, uint8_t* d_planar, hipStream_t s);

@@ -23,7 +23,7 @@ size_t proc_sort_bytes(int width, int out_rows)
            regions * kSortRegion * kSortRegion * 2u;
 }
 
-hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_buf, bool reuse_sort, const Schedule& sc,
+hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_buf, int reuse_sort, const Schedule& sc,
                                    hipStream_t s)
 {
     if (a.width <= 0 || a.out_rows <= 0) return hipSuccess;
@@ -42,8 +42,8 @@ hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_bu
         const dim3 g1((unsigned)(((a.width + kSortRegion - 1) / kSortRegion) * ((a.out_rows + kSortRegion - 1) / kSortRegion)));
         // same geometry as the frame that built keys / order / total: only the
         // pixels without steps need writing, by trailing blocks of the march
-        const unsigned positions = reuse_sort ? g1.x * 256u * kSortPixelsPerThread : 0u;
-        if (!reuse_sort) {
+        const unsigned positions = reuse_sort != SORT_BUILD ? g1.x * 256u * kSortPixelsPerThread : 0u;
+        if (reuse_sort == SORT_BUILD) {
             if (shadow) hipLaunchKernelGGL((proc_bin<true>), g1, dim3(256), 0, s, a, hist, keys);
             else hipLaunchKernelGGL((proc_bin<false>), g1, dim3(256), 0, s, a, hist, keys);
             hipLaunchKernelGGL(proc_scan, dim3(1), dim3(kKeyBins), 0, s, hist, cursor);
@@ -59,7 +59,7 @@ hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_bu
         const int v = (shadow ? 4 : 0) | (early ? 2 : 0);
 #define VR_PS(S, E, T) \
     hipLaunchKernelGGL((march_proc_sorted<S, E, T>), g4, dim3(kThreads), wt_bytes, s, a, order, total, keys, positions, \
-                       march_blocks)
+                       march_blocks, reuse_sort == SORT_STALE)
 #define VR_PS3(S, E) \
     if (tm == 3) VR_PS(S, E, 3); \
     else if (tm == 2) VR_PS(S, E, 2); \

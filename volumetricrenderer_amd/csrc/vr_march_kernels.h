@@ -1254,15 +1254,29 @@ template <bool SHADOW, bool EARLY, int TABLE>
 __global__ __launch_bounds__(kThreads) void march_proc_sorted(const MarchArgs a, const unsigned* __restrict__ order,
                                                               const unsigned* __restrict__ total_ptr,
                                                               const unsigned short* __restrict__ keys,
-                                                              unsigned fill_positions, unsigned fill_first)
+                                                              unsigned fill_positions, unsigned fill_first, int stale)
 {
+    extern __shared__ float4 wt_lds[];
     // A reused sort order (vr_render): blocks from fill_first on write the
-    // pixels without steps instead of marching, so a frame is one launch
+    // pixels without steps instead of marching, so a frame is one launch.
+    // A stale order (an older camera, same target): the pixels it left out
+    // may have steps now, so those blocks march them (unsorted; a 1.6-degree
+    // turn moves only the silhouette) -- every pixel is still written once.
     if (blockIdx.x >= fill_first) {
-        proc_fill_background(a, keys, fill_positions, blockIdx.x - fill_first, gridDim.x - fill_first);
+        if (!stale) {
+            proc_fill_background(a, keys, fill_positions, blockIdx.x - fill_first, gridDim.x - fill_first);
+            return;
+        }
+        const float4* wt = worley_table<TABLE>(a.proc, wt_lds);
+        unsigned long long steps = 0;
+        const unsigned blocks = gridDim.x - fill_first;
+        for (unsigned i = (blockIdx.x - fill_first) * kThreads + threadIdx.x; i < fill_positions; i += blocks * kThreads) {
+            int x, orow;
+            if (sort_pixel(a, i, &x, &orow) && keys[i] == 0) steps += march_pixel_proc<SHADOW, EARLY, TABLE>(a, wt, x, orow);
+        }
+        if (a.step_counter) add_steps(a, steps);
         return;
     }
-    extern __shared__ float4 wt_lds[];
     const float4* wt = worley_table<TABLE>(a.proc, wt_lds);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const unsigned total = *total_ptr;
