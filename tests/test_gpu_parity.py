@@ -232,6 +232,36 @@ def test_split_long_tiles_bitexact(r, oracle, vol128, layout):
         r.set_layout_preference(0)
 
 
+@pytest.mark.parametrize("layout", [15, 12, 14])
+def test_region_workgroups_and_supertiles_bitexact(r, oracle, vol128, layout):
+    """Regions schedule with 8 or 16 waves per workgroup (wg_waves) and the
+    list ordered per tile or by 4x4 blocks of tiles (supertile; 2x2 is the
+    default every other test runs): only the order and
+    the grouping of tiles change, so every frame is bit-exact, step counts
+    included; also a banded target and early-out."""
+    r.set_volume(vol128)
+    r.set_layout_preference(layout)
+    try:
+        for wg, st in [(4, 1), (8, 1), (16, 1), (4, 4), (8, 2), (16, 4)]:
+            r.set_option("wg_waves", wg)
+            r.set_option("supertile", st)
+            assert (r.get_option("wg_waves"), r.get_option("supertile")) == (wg, st)
+            for (W, H, phi, theta) in [(480, 270, 0.0, 0.0), (203, 117, 35.0, -20.0)]:
+                osd, gsd = vr.reference_shader_data(W / H, phi, theta)
+                img, ref, c, s = render_both(r, oracle, vol128, W, H, osd, gsd)
+                assert_exact(img, ref)
+                assert c == s
+        osd, gsd = vr.reference_shader_data(16 / 9, -40.0, 15.0)
+        img, ref, c, s = render_both(r, oracle, vol128, 320, 180, osd, gsd, march=vr.march_defaults(early_out=0.5),
+                                     band_rows=16, band_stride=3, band_first=1)
+        assert_exact(img, ref)
+        assert c == s
+    finally:
+        r.set_option("wg_waves", 4)
+        r.set_option("supertile", 2)
+        r.set_layout_preference(0)
+
+
 @pytest.mark.parametrize("cap", [32, 12, 0])
 def test_slab_march_bitexact(r, oracle, vol128, cap):
     """The LDS-slab march (COL48 + option slab, vr_march_slab.hip): per step a

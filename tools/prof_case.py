@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--slab", type=int, default=-1, help="LDS slab march (COL48): 1 on, 0 off")
     ap.add_argument("--proc-enum", type=int, default=-1, help="procedural sort: 1 region enumeration with shadows")
     ap.add_argument("--slab-cap", type=int, default=-1)
+    ap.add_argument("--opt", action="append", default=[], help="vr option NAME=VALUE")
     a = ap.parse_args()
     with vr.Renderer(0) as r:
         if a.proc:
@@ -51,6 +52,9 @@ def main():
             r.set_option("wedges", a.wedges)
         if a.tpw > 0:
             r.set_option("tiles_per_wave", a.tpw)
+        for o in a.opt:
+            k, v = o.split("=")
+            r.set_option(k, int(v))
         osd, gsd = vr.reference_shader_data(a.width / a.height)
         r.set_shader_data(osd, gsd)
         r.set_march(vr.march_defaults(max_steps=a.steps))

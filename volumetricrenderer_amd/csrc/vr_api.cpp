@@ -58,7 +58,7 @@ constexpr int kRegionRebuildInterval = 32;
 // stays exact).
 constexpr size_t kSortKeyGridPart = 11;   // leading sort-key entries a stale order must match
 constexpr int kMaxRegionStreams = 4;
-constexpr int kRegionKeyLen = 34;
+constexpr int kRegionKeyLen = 35;
 // auto split (lanes per ray) from the frame share's tiles with work: K = 1 at
 // >= 6000, 2 at >= 1400, else 4.  Measured on 1/N of the 1080p frame at 512^3
 // (~7,500 tiles with work): K = 1, 2, 2, 4 at N = 1, 2, 4, 8.
@@ -99,6 +99,8 @@ struct Ctx {
     int proc_enum = 0;             // procedural sort: 1 = 64x64-region enumeration with shadow rays too
     int slab_cap = kSlabMaxChunks; // its chunks per channel (<= kSlabMaxChunks; smaller forces the fallback)
     int split_long = 0;            // regions: tiles costing >= this % of the longest split in two halves (0 = off)
+    int wg_waves = 4;              // regions: waves per workgroup (4, 8, 16)
+    int supertile = 2;             // regions: list order by S x S blocks of tiles (1 = per tile; 2 measured 1 % faster)
     struct RegionBuf {
         unsigned* d = nullptr;     // device tile list
         unsigned* h = nullptr;     // pinned staging copy
@@ -722,6 +724,16 @@ vr_status vr_set_option(void* p, const char* name, int value)
         c->split_long = value;
         return VR_OK;
     }
+    if (n == "wg_waves") {
+        if (value != 4 && value != 8 && value != 16) return fail(VR_ERR_INVALID, "vr_set_option: wg_waves is 4, 8 or 16");
+        c->wg_waves = value;
+        return VR_OK;
+    }
+    if (n == "supertile") {
+        if (value != 1 && value != 2 && value != 4) return fail(VR_ERR_INVALID, "vr_set_option: supertile is 1, 2 or 4");
+        c->supertile = value;
+        return VR_OK;
+    }
     if (n == "sort_reuse") {
         if (value < 0 || value > 64) return fail(VR_ERR_INVALID, "vr_set_option: sort_reuse in [0, 64] renders");
         c->sort_reuse = value;
@@ -759,6 +771,8 @@ int vr_get_option(void* p, const char* name)
     if (n == "slab_cap") return c->slab_cap;
     if (n == "split_long") return c->split_long;
     if (n == "sort_reuse") return c->sort_reuse;
+    if (n == "wg_waves") return c->wg_waves;
+    if (n == "supertile") return c->supertile;
     return -1;
 }
 
@@ -842,8 +856,9 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     const int tw = (a.width + 7) >> 3, th = (a.out_rows + 7) >> 3;
     float key[kRegionKeyLen] = {(float)tw, (float)th, (float)a.width, (float)a.height, (float)a.out_rows,
                                 (float)a.band_rows, (float)a.band_stride, (float)a.band_first, (float)tpw,
-                                (float)c->wedges, (float)(mixable ? c->split_long : 0), (float)c->split};
-    constexpr int grid_part = 12;   // the part a reused list must match
+                                (float)c->wedges, (float)(mixable ? c->split_long : 0), (float)c->split,
+                                (float)c->supertile};
+    constexpr int grid_part = 13;   // the part a reused list must match
     int kn = grid_part;
     for (float v : {(float)a.max_steps, a.step_size, (float)cpx, (float)cprow}) key[kn++] = v;
     for (const float* v : {a.org, a.o, a.px, a.py, a.box_min, a.box_max})
@@ -880,19 +895,25 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
         const int orow = std::min(j * 8, a.out_rows);   // the row a packed-row edge starts
         for (int i = 0; i <= tw; ++i) corner[(size_t)j * (tw + 1) + i] = steps_at(std::min(i * 8, a.width), orow);
     }
-    struct T { unsigned id; double cost, ang; int ring; };
+    // supertile S: tiles are ordered by S x S blocks (angle and ring of the
+    // block, then row-major inside it), so consecutive entries -- the waves of
+    // one workgroup, on one CU -- are a compact block sharing the CU's L1
+    struct T { unsigned id; double cost, ang; int ring, sub; };
     std::vector<T> work, idle;
+    const int S = c->supertile;
     const double ccx = (cpx + 0.5) / 8.0, ccy = (cprow + 0.5) / 8.0;
-    const int ctx = cpx >> 3, cty = cprow >> 3;
+    const int ctx = (cpx >> 3) / S, cty = (cprow >> 3) / S;
     for (int ty = 0; ty < th; ++ty)
         for (int tx = 0; tx < tw; ++tx) {
             const double* c0 = &corner[(size_t)ty * (tw + 1) + tx];
             const double cost = std::max(std::max(c0[0], c0[1]), std::max(c0[tw + 1], c0[tw + 2]));
-            const T t{((unsigned)ty << 16) | (unsigned)tx, cost, std::atan2(ty + 0.5 - ccy, tx + 0.5 - ccx),
-                      std::max(std::abs(tx - ctx), std::abs(ty - cty))};
+            const int sx = tx / S, sy = ty / S;
+            const T t{((unsigned)ty << 16) | (unsigned)tx, cost,
+                      std::atan2(sy * S + 0.5 * S - ccy, sx * S + 0.5 * S - ccx),
+                      std::max(std::abs(sx - ctx), std::abs(sy - cty)), (ty % S) * S + tx % S};
             (cost >= 1.0 ? work : idle).push_back(t);
         }
-    std::sort(work.begin(), work.end(), [](const T& u, const T& v) { return u.ang < v.ang; });
+    std::sort(work.begin(), work.end(), [](const T& u, const T& v) { return u.ang != v.ang ? u.ang < v.ang : u.sub < v.sub; });
     double total = 0.0;
     for (const T& t : work) total += t.cost;
     std::vector<std::vector<T>> xl(8);
@@ -902,7 +923,9 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
         xl[std::min(K - 1, (int)((run + 0.5 * t.cost) / total * K)) % 8].push_back(t);
         run += t.cost;
     }
-    auto inside_out = [](const T& u, const T& v) { return u.ring != v.ring ? u.ring < v.ring : u.ang < v.ang; };
+    auto inside_out = [](const T& u, const T& v) {
+        return u.ring != v.ring ? u.ring < v.ring : u.ang != v.ang ? u.ang < v.ang : u.sub < v.sub;
+    };
     for (auto& l : xl) std::sort(l.begin(), l.end(), inside_out);
     std::sort(idle.begin(), idle.end(), inside_out);
     for (size_t i = 0; i < idle.size(); ++i) xl[i % 8].push_back(idle[i]);
@@ -1120,7 +1143,7 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
         // schedule 0 = one 8x8 tile per wave in row order, 4 = in rings;
         // otherwise (auto) the cost-sorted schedule
         void* sort_buf = nullptr;
-        Schedule sc{c->schedule == SCHED_RINGS ? SCHED_RINGS : SCHED_STATIC, 0, 0, 1, 1, nullptr, nullptr, {}, 1, 0, 0};
+        Schedule sc{c->schedule == SCHED_RINGS ? SCHED_RINGS : SCHED_STATIC, 0, 0, 1, 1, nullptr, nullptr, {}, 1, 0, 0, 4};
         if (sc.kind == SCHED_RINGS) box_centre_pixel(c, a, &sc.center_x, &sc.center_y);
         // the sort passes enumerate whole 64x64 regions (vr_march_kernels.h sort_pixel)
         if (c->schedule != SCHED_STATIC && c->schedule != SCHED_RINGS && a.width < 65536 && a.out_rows < 65536 &&
@@ -1170,7 +1193,7 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
     // wedges of the frame, each walked inside-out (longest rays first)
     const int kind = c->schedule >= 0 ? c->schedule : SCHED_REGIONS;
     const int tpw = c->tiles_per_wave > 0 ? c->tiles_per_wave : (kind == SCHED_RINGS || kind == SCHED_REGIONS ? 2 : 1);
-    Schedule sc{kind, 0, 0, tpw, c->waves_per_simd, c->d_heads, nullptr, {}, 1, 0, 0};
+    Schedule sc{kind, 0, 0, tpw, c->waves_per_simd, c->d_heads, nullptr, {}, 1, 0, 0, c->wg_waves};
     sc.slab = pl.layout == LAYOUT_COL48 && c->slab;
     a.slab_cap = c->slab_cap;
     if (kind == SCHED_RINGS || kind == SCHED_REGIONS) box_centre_pixel(c, a, &sc.center_x, &sc.center_y);

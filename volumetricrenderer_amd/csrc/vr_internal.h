@@ -207,6 +207,7 @@ struct Schedule {
     int split;             // regions: lanes per ray (1, 2, 4, 8; BRICK4 / CORNER8 only)
     int slab;              // regions + COL48: the LDS slab march (vr_march_slab.hip)
     int mixed;             // regions: the list holds split halves of the longest tiles (march_regions_mixed)
+    int wg_waves;          // regions (one lane per ray): waves per workgroup, 4 (default), 8 or 16
 };
 
 // launchers (vr_march.hip / vr_volume.hip); return hipError_t

@@ -710,7 +710,7 @@ __device__ __forceinline__ void timeline_record(unsigned long long t_begin, unsi
 {
     for (int off = 32; off > 0; off >>= 1) steps += __shfl_xor(steps, off);
     const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
-    const int wid = (int)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+    const int wid = (int)blockIdx.x * (int)(blockDim.x >> 6) + (threadIdx.x >> 6);
     if ((threadIdx.x & 63) == 0 && wid < kTimelineWaves) {
         g_timeline[wid][0] = t_begin;
         g_timeline[wid][1] = t_end;
@@ -750,7 +750,7 @@ __device__ __forceinline__ FastCtx fast_prologue(const MarchArgs& a, unsigned* l
             f.rsrc[c] = __builtin_amdgcn_make_buffer_rsrc((void*)(a.vol + (size_t)c * a.plane_stride), (short)0,
                                                           (int)a.plane_stride, 0x00020000);
         const int nx1 = a.nx + 1, ny1 = a.ny + 1, nz1 = a.nz + 1;
-        for (int i = threadIdx.x; i < nx1 + ny1 + nz1; i += kThreads) {
+        for (int i = threadIdx.x; i < nx1 + ny1 + nz1; i += (int)blockDim.x) {
             const int axis = i < nx1 ? 0 : i < nx1 + ny1 ? 1 : 2;
             const int pos = axis == 0 ? i : axis == 1 ? i - nx1 : i - nx1 - ny1;
             lds[i] = axis_offset(a.geom, LAYOUT, axis, pos);   // once per workgroup
@@ -846,15 +846,17 @@ __global__ __launch_bounds__(kThreads) void march_rings(const MarchArgs a, int c
 // L2 serve them once: the lines the eight L2s fetch per 1080p frame at 512^3
 // drop from ~900 MB (ring positions dealt round-robin over XCDs) to ~620 MB
 // (DESIGN.md sec. 5.3).  XCD = blockIdx % 8 is a speed-only assumption.
-template <int LAYOUT, int WRAP, bool EARLY, bool ZO>
-__global__ __launch_bounds__(kThreads) void march_regions(const MarchArgs a, const unsigned* __restrict__ tiles,
+// WGW waves per workgroup (option wg_waves): the waves of one workgroup run on
+// one CU and share its L1, and they render consecutive list entries.
+template <int LAYOUT, int WRAP, bool EARLY, bool ZO, int WGW = kThreads / 64>
+__global__ __launch_bounds__(64 * WGW) void march_regions(const MarchArgs a, const unsigned* __restrict__ tiles,
                                                          const TileMap m)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned lds[];
     const int xcd = blockIdx.x & 7;
-    const int w = (int)(blockIdx.x >> 3) * (kThreads / 64) + (threadIdx.x >> 6);
+    const int w = (int)(blockIdx.x >> 3) * WGW + (threadIdx.x >> 6);
     const int begin = m.off[xcd], count = m.off[xcd + 1] - begin;
-    if ((int)(blockIdx.x >> 3) * (kThreads / 64) >= count) return;   // whole workgroup, before the barrier
+    if ((int)(blockIdx.x >> 3) * WGW >= count) return;   // whole workgroup, before the barrier
 #ifdef VR_TIMELINE
     const unsigned long long t_begin = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -1358,6 +1360,20 @@ hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStre
                 hipLaunchKernelGGL((march_regions_mixed<L, false, true>), grid, block, lds, s, a, sc.tiles, sc.map);
             else
                 hipLaunchKernelGGL((march_regions_mixed<L, false, false>), grid, block, lds, s, a, sc.tiles, sc.map);
+            return hipGetLastError();
+        }
+    }
+    if constexpr (L == LAYOUT_COL48 || L == LAYOUT_BRICK4832 || L == LAYOUT_CORNERH) {
+        if (sc.kind == SCHED_REGIONS && (sc.wg_waves == 8 || sc.wg_waves == 16)) {
+            const int g = sc.wg_waves;
+            const dim3 grid((unsigned)(8 * ((sc.map.nwx + g - 1) / g))), blk(64 * g);
+#define VR_RW(G) \
+    if (early && a.zero_offsets) hipLaunchKernelGGL((march_regions<L, W, true, true, G>), grid, blk, lds, s, a, sc.tiles, sc.map); \
+    else if (early) hipLaunchKernelGGL((march_regions<L, W, true, false, G>), grid, blk, lds, s, a, sc.tiles, sc.map); \
+    else if (a.zero_offsets) hipLaunchKernelGGL((march_regions<L, W, false, true, G>), grid, blk, lds, s, a, sc.tiles, sc.map); \
+    else hipLaunchKernelGGL((march_regions<L, W, false, false, G>), grid, blk, lds, s, a, sc.tiles, sc.map)
+            if (g == 8) { VR_RW(8); } else { VR_RW(16); }
+#undef VR_RW
             return hipGetLastError();
         }
     }
