@@ -43,9 +43,16 @@ typedef enum {
 typedef enum {
     VR_FMT_RGBA32F = 0,      /* 16 B/pixel, linear                          */
     VR_FMT_RGBA8_UNORM = 1,  /* 4 B/pixel, linear, round-to-nearest-even    */
-    VR_FMT_RGBA8_SRGB = 2    /* 4 B/pixel, sRGB-encoded on store, as the
+    VR_FMT_RGBA8_SRGB = 2,   /* 4 B/pixel, sRGB-encoded on store, as the
                                 reference's swapchain format
                                 (VulkanSwapchain.cpp:181-191)               */
+    /* Grey targets: frag.glsl:79-80 writes vec4(vec3(c), 1.0), so one channel
+     * holds the whole pixel.  The value is the RGBA format's R (bit for bit);
+     * G = B = R and A = 1 (255) are implied.  The multi-GPU band sets travel
+     * in these (vr_shard.h), and vr_assemble_frame expands them.           */
+    VR_FMT_R8_UNORM = 3,     /* 1 B/pixel: VR_FMT_RGBA8_UNORM's R           */
+    VR_FMT_R8_SRGB = 4,      /* 1 B/pixel: VR_FMT_RGBA8_SRGB's R            */
+    VR_FMT_R32F = 5          /* 4 B/pixel: VR_FMT_RGBA32F's R               */
 } vr_format;
 
 /* Replaces the binding-0 UBO `ObjectShaderData` (TestMain.cpp:27-32,
@@ -204,10 +211,19 @@ vr_status vr_render(void* ctx, const vr_target* target, void* stream);
  *      gathered into one device buffer, d_gathered = [rank][packed rows].
  *      Each rank's set holds `rows_per_rank` rows.  This call scatters them
  *      into the full frame.  Rank r rendered with band_stride = nranks and
- *      band_first = r.  The layout matches vr_render's packed output.      */
+ *      band_first = r.  The layout matches vr_render's packed output.
+ *      bytes_per_pixel: 1, 4 or 16 (the target format's pixel size).      */
 vr_status vr_assemble_bands(void* ctx, const void* d_gathered, size_t rows_per_rank,
                             int nranks, int width, int height, int band_rows,
                             int bytes_per_pixel, void* d_frame, void* stream);
+/* The same scatter between formats: band sets gathered in `gathered_format`
+ * into a frame in `frame_format`.  Equal formats copy (vr_assemble_bands);
+ * a grey set expands into its RGBA format: R8_UNORM -> RGBA8_UNORM,
+ * R8_SRGB -> RGBA8_SRGB, R32F -> RGBA32F (G = B = R, A = 255 / 1.0), so the
+ * gather moves a quarter of the bytes.  Other pairs are VR_ERR_INVALID.   */
+vr_status vr_assemble_frame(void* ctx, const void* d_gathered, int gathered_format, size_t rows_per_rank,
+                            int nranks, int width, int height, int band_rows, int frame_format,
+                            void* d_frame, void* stream);
 /* rows that vr_render writes for a band set (for sizing buffers)          */
 int vr_band_rows_packed(int height, int band_rows, int band_stride, int band_first);
 
@@ -226,7 +242,8 @@ const char* vr_kernel_variant(void* ctx);
  * bricks of 1 KiB ("brick4832"), 13 = 4x8x64-texel bricks of 2 KiB
  * ("brick4864"), 14 = per position the f16 pairs {a, b - a} of the four
  * footprint rows, one 16-B load and four v_fma_mix_f32 per tap ("cornerh";
- * volumes below 2^24 positions).  Layouts 2-14 are
+ * volumes below 2^24 positions), 15 = columns of 4x8 texels through the
+ * whole z extent, slices 32 B apart ("col48"; auto above 160 MiB).  Layouts 2-15 are
  * used only where clamp-to-edge equals mirrored repeat.  Otherwise the
  * planar, mirrored-repeat kernel runs.  Rebuilds the layout (synchronous). */
 vr_status vr_set_layout_preference(void* ctx, int pref);
@@ -248,7 +265,18 @@ vr_status vr_set_layout_preference(void* ctx, int pref);
  *   "waves_per_simd"  1-8, queue schedule.
  *   "tiles_per_wave"  1-64, strided, ring and region schedules; 0 = auto,
  *                     the default: 2 for rings and regions, 1 for strided.
- *   "wedges"          1-64, regions schedule: wedges per XCD (default 2).
+ *   "wedges"          1-64, regions schedule: wedges per XCD (default 4).
+ *   "supertile"       1, 2, 4, regions schedule: the tile lists are ordered by
+ *                     S x S blocks of 8x8 tiles (default 2), so a workgroup's
+ *                     waves render one block.
+ *   "wg_waves"        4 (default), 8, 16: waves per workgroup of the regions
+ *                     march (col48, brick4832, cornerh).
+ *   "split_long"      0-100 (percent, default 0 = off), regions schedule with
+ *                     one lane per ray: tiles whose estimated work is at least
+ *                     this share of the longest are marched as two halves with
+ *                     two lanes per ray.
+ *   "slab"            0/1, col48 + regions: the per-wave LDS slab march
+ *                     (default 0); "slab_cap" 0-32 chunks per channel.
  *   "split"           regions schedule, brick4/448/488/zpair/corner8: lanes per ray
  *                     (1, 2, 4, 8; each lane marches every K-th step and the
  *                     terms are summed in step order, bit-exact); 0 = auto,
@@ -257,7 +285,12 @@ vr_status vr_set_layout_preference(void* ctx, int pref);
  *   "count"           0 = vr_target.step_counter sums executed ray-steps (the
  *                     default); 1 = it sums density evaluations, i.e.
  *                     ray-steps plus the procedural shadow samples -- the unit
- *                     of the procedural roofline.
+ *                     of the procedural roofline; 2 = the Worley cells those
+ *                     evaluations computed.
+ *   "sort_reuse"      0-64, procedural sorted schedule: renders that may march
+ *                     the cost order of an older camera (default 0).
+ *   "proc_enum"       0/1, procedural sort with shadow rays: enumerate
+ *                     64x64 regions (default 0, row-major).
  *   "lattice"         procedural medium, sorted schedule: 1 = the fBm reads its
  *                     per-cell gradient-pair offsets from a lattice table in
  *                     global memory (the default; built when the seed or the

@@ -8,7 +8,10 @@
  * Each rank renders its packed band set with vr_render; one RCCL exchange
  * per frame sends the sets to rank 0 over xGMI (grouped point-to-point
  * sends/receives), and rank 0 scatters them into the frame with
- * vr_assemble_bands.  The reference has no multi-GPU code at all (SURVEY.md
+ * vr_assemble_frame.  The band sets travel in the grey format of the frame's
+ * (vr.h VR_FMT_R8_UNORM / R8_SRGB / R32F: the shader's pixel is
+ * vec4(vec3(c), 1), frag.glsl:79-80), a quarter of the RGBA bytes, and the
+ * assembly expands them.  The reference has no multi-GPU code at all (SURVEY.md
  * sec. 2); this replaces its single-queue frame loop (VulkanRenderer.cpp:
  * 142-230) for N GPUs and keeps its 2 frames in flight (:13): frame i's
  * exchange and assembly run on a communication stream while frame i+1
@@ -90,9 +93,10 @@ vr_status vr_shard_barrier(vr_shard* sh, void* stream);
  * rank's ctx holds the volume.  Loopback: vr_set_volume_device. */
 vr_status vr_shard_share_volume(vr_shard* sh, const void* d_rgba8, int nx, int ny, int nz, void* stream);
 
-/* Rank 0: the last assembled frame (device pointer, tight rows) once
- * `stream` of the last vr_shard_run has reached it.  Other ranks: their
- * last band set. */
+/* Rank 0: the last assembled frame (device pointer, tight rows, the shard's
+ * format) once `stream` of the last vr_shard_run has reached it.  Other ranks:
+ * their last band set, in the grey format of the frame's (1 B per pixel, or
+ * 4 B for VR_FMT_RGBA32F frames). */
 vr_status vr_shard_frame(vr_shard* sh, void** pixels, size_t* row_pitch, int* rows);
 
 /* Copy what vr_shard_frame points at into a caller-owned device buffer

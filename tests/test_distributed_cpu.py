@@ -19,7 +19,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 class OracleRenderer:
-    """CPU stand-in for volumetricrenderer_amd.Renderer (test only)."""
+    """CPU stand-in for volumetricrenderer_amd.Renderer (test only).  Grey
+    formats 3-5 are the R channel of the RGBA formats 1, 2, 0."""
+
+    RGBA_OF = {3: 1, 4: 2, 5: 0}
 
     def __init__(self, oracle, vol, obj, glob, march):
         self.o, self.vol, self.obj, self.glob, self.m = oracle, vol, obj, glob, march
@@ -27,21 +30,28 @@ class OracleRenderer:
     def alloc_target(self, width, height, fmt, band_rows=0, band_stride=1, band_first=0):
         from volumetricrenderer_amd.distributed import rows_for_rank
         rows = rows_for_rank(height, band_rows, band_stride, band_first) if band_rows else height
-        return torch.zeros((rows, width, 4), dtype=torch.float32 if fmt == 0 else torch.uint8)
+        shape = (rows, width) if fmt in self.RGBA_OF else (rows, width, 4)
+        return torch.zeros(shape, dtype=torch.float32 if fmt in (0, 5) else torch.uint8)
 
     def render(self, width, height, fmt, out=None, band_rows=0, band_stride=1, band_first=0, step_counter=None):
-        img, _ = self.o.render(self.vol, self.obj, self.glob, self.m, width, height, fmt, band_rows=band_rows,
-                               band_stride=band_stride, band_first=band_first)
+        img, _ = self.o.render(self.vol, self.obj, self.glob, self.m, width, height, self.RGBA_OF.get(fmt, fmt),
+                               band_rows=band_rows, band_stride=band_stride, band_first=band_first)
+        if fmt in self.RGBA_OF:
+            img = np.ascontiguousarray(img[..., 0])
         out[: img.shape[0]].copy_(torch.from_numpy(img))
         return out
 
     def set_volume(self, vol):
         self.vol = np.ascontiguousarray(vol, dtype=np.uint8)
 
-    def assemble_bands(self, gathered, nranks, width, height, band_rows, frame=None):
+    def assemble_frame(self, gathered, gfmt, nranks, width, height, band_rows, ffmt, frame=None):
         for y in range(height):
             b, r = divmod(y, band_rows)
-            frame[y] = gathered[b % nranks, (b // nranks) * band_rows + r]
+            row = gathered[b % nranks, (b // nranks) * band_rows + r]
+            if gfmt != ffmt:   # grey -> RGBA: G = B = R, A = 1 / 255
+                alpha = 1.0 if ffmt == 0 else 255
+                row = torch.stack([row, row, row, torch.full_like(row, alpha)], dim=-1)
+            frame[y] = row
         return frame
 
 
@@ -140,7 +150,7 @@ def test_share_volume_bad_input_raises_on_every_rank(which):
     assert all(r[0] == "raised" for r in res), res
 
 
-def _worker(rank, world, port, W, H, q):
+def _worker(rank, world, port, W, H, fmt, q):
     import sys
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -153,10 +163,11 @@ def _worker(rank, world, port, W, H, q):
         vol = np.random.default_rng(7).integers(0, 256, size=(24, 20, 28, 4), dtype=np.uint8)
         obj, glob = oracle.reference_shader_data(W / H, 25.0, -10.0)
         r = OracleRenderer(oracle, vol, obj, glob, oracle.march(64))
-        sh = BandSharder(r, W, H, 0, band_rows=16, world=world, rank=rank)
+        sh = BandSharder(r, W, H, fmt, band_rows=16, world=world, rank=rank)
+        assert sh.gfmt == {0: 5, 1: 3, 2: 4}[fmt]   # grey band sets travel
         frame = sh.run_frames(3)
         if rank == 0:
-            ref, _ = oracle.render(vol, obj, glob, oracle.march(64), W, H, 0)
+            ref, _ = oracle.render(vol, obj, glob, oracle.march(64), W, H, fmt)
             q.put(("ok", bool(np.array_equal(frame.numpy(), ref)), int(sh.my_rows)))
         else:
             q.put(("ok", True, int(sh.my_rows)))
@@ -166,12 +177,14 @@ def _worker(rank, world, port, W, H, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,W,H", [(2, 96, 72), (3, 64, 100)])
-def test_band_shard_gather_matches_full_frame(world, W, H):
+@pytest.mark.parametrize("world,W,H,fmt", [(2, 96, 72, 0), (3, 64, 100, 0), (2, 80, 48, 1)])
+def test_band_shard_gather_matches_full_frame(world, W, H, fmt):
+    """Grey band sets (one value per pixel) gathered over gloo and expanded
+    on rank 0 equal one full-frame oracle render, RGBA32F and RGBA8."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(rk, world, port, W, H, q)) for rk in range(world)]
+    procs = [ctx.Process(target=_worker, args=(rk, world, port, W, H, fmt, q)) for rk in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in procs]

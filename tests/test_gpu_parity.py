@@ -393,6 +393,49 @@ def test_band_sharding_and_assembly(r, oracle, vol128):
     assert_exact(frame.cpu().numpy(), full.cpu().numpy())
 
 
+@pytest.mark.parametrize("fmt", [vr.FMT_RGBA32F, vr.FMT_RGBA8_UNORM, vr.FMT_RGBA8_SRGB] if torch.cuda.is_available()
+                         else [])
+def test_grey_targets_and_expanding_assembly(r, oracle, vol128, fmt):
+    """Grey targets (include/vr.h formats 3-5) hold the R channel of the RGBA
+    format bit for bit, for the grid and the procedural march, whole frames
+    and band sets; grey band sets of 3 ranks, gathered and expanded by
+    vr_assemble_frame, equal the RGBA frame (G = B = R, A = 1 / 255).  Widths
+    320 and 203 take the 4-pixel and the per-pixel expansion."""
+    g = vr.GREY_OF[fmt]
+    r.set_volume(vol128)
+    try:
+        for proc in (False, True):
+            if proc:
+                r.set_procedural()
+            for W, H in [(320, 200), (203, 117)]:
+                osd, gsd = vr.reference_shader_data(W / H, 15.0, 5.0)
+                r.set_shader_data(osd, gsd)
+                r.set_march(vr.march_defaults(max_steps=64))
+                full = r.render(W, H, fmt)
+                grey = r.render(W, H, g)
+                torch.cuda.synchronize()
+                assert tuple(grey.shape) == (H, W)
+                assert torch.equal(grey, full[..., 0])
+                if not proc:
+                    obj, glob = vr.shader_data_arrays(osd, gsd)
+                    ref, _ = oracle.render(vol128, obj, glob, oracle.march(64), W, H, fmt)
+                    assert_exact(grey.cpu().numpy(), np.ascontiguousarray(ref[..., 0]))
+                br, n = 16, 3
+                gathered = torch.zeros((n, vr.band_rows_packed(H, br, n, 0), W), dtype=grey.dtype, device="cuda")
+                for k in range(n):
+                    rows = vr.band_rows_packed(H, br, n, k)
+                    r.render(W, H, g, out=gathered[k, :rows], band_rows=br, band_stride=n, band_first=k)
+                frame = r.assemble_frame(gathered, g, n, W, H, br, fmt)
+                same = r.assemble_frame(gathered, g, n, W, H, br, g)   # equal formats: a plain scatter
+                torch.cuda.synchronize()
+                assert_exact(frame.cpu().numpy(), full.cpu().numpy())
+                assert torch.equal(same, grey)
+        with pytest.raises(ValueError):
+            r.assemble_frame(gathered, g, n, W, H, br, vr.GREY_OF[(fmt + 1) % 3])
+    finally:
+        r.set_procedural(enabled=0)
+
+
 def test_volume_generator_matches_oracle(r, oracle):
     for literal in (True, False):
         rec = vr.volume_recipe_defaults(size=48, literal_overwrite=int(literal))

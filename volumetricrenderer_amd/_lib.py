@@ -31,7 +31,13 @@ STATUS_NAMES = {
     7: "VR_ERR_TIMEOUT", 8: "VR_ERR_COMM",
 }
 FMT_RGBA32F, FMT_RGBA8_UNORM, FMT_RGBA8_SRGB = 0, 1, 2
-BYTES_PER_PIXEL = {FMT_RGBA32F: 16, FMT_RGBA8_UNORM: 4, FMT_RGBA8_SRGB: 4}
+# grey targets (include/vr.h): the R channel of the RGBA format, 1 value per pixel
+FMT_R8_UNORM, FMT_R8_SRGB, FMT_R32F = 3, 4, 5
+BYTES_PER_PIXEL = {FMT_RGBA32F: 16, FMT_RGBA8_UNORM: 4, FMT_RGBA8_SRGB: 4, FMT_R8_UNORM: 1, FMT_R8_SRGB: 1,
+                   FMT_R32F: 4}
+CHANNELS = {FMT_RGBA32F: 4, FMT_RGBA8_UNORM: 4, FMT_RGBA8_SRGB: 4, FMT_R8_UNORM: 1, FMT_R8_SRGB: 1, FMT_R32F: 1}
+GREY_OF = {FMT_RGBA32F: FMT_R32F, FMT_RGBA8_UNORM: FMT_R8_UNORM, FMT_RGBA8_SRGB: FMT_R8_SRGB}
+FLOAT_FORMATS = (FMT_RGBA32F, FMT_R32F)
 
 c_float_p = ctypes.POINTER(ctypes.c_float)
 c_int_p = ctypes.POINTER(ctypes.c_int)
@@ -116,6 +122,8 @@ _SIGS = {
     "vr_set_march": (ctypes.c_int, [_vp, ctypes.POINTER(MarchParams)]),
     "vr_render": (ctypes.c_int, [_vp, ctypes.POINTER(Target), _vp]),
     "vr_assemble_bands": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, _vp]),
+    "vr_assemble_frame": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, _vp]),
     "vr_band_rows_packed": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "vr_kernel_variant": (ctypes.c_char_p, [_vp]),

@@ -1053,9 +1053,9 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
         return fail(VR_ERR_NO_VOLUME, "vr_render: no volume (vr_set_volume / vr_generate_volume)");
     if (!c->has_camera) return fail(VR_ERR_NO_CAMERA, "vr_render: no shader data (vr_set_shader_data)");
     if (t->width <= 0 || t->height <= 0) return fail(VR_ERR_INVALID, "vr_render: bad size %dx%d", t->width, t->height);
-    if (t->format < 0 || t->format > 2) return fail(VR_ERR_INVALID, "vr_render: bad format %d", t->format);
+    if (t->format < 0 || t->format > 5) return fail(VR_ERR_INVALID, "vr_render: bad format %d", t->format);
     if (!t->pixels) return fail(VR_ERR_INVALID, "vr_render: pixels is null");
-    const int bpp = t->format == VR_FMT_RGBA32F ? 16 : 4;
+    const int bpp = format_bytes(t->format);
     const size_t pitch = t->row_pitch ? t->row_pitch : (size_t)t->width * bpp;
     if (pitch < (size_t)t->width * bpp || pitch % bpp != 0 || ((uintptr_t)t->pixels % bpp) != 0)
         return fail(VR_ERR_INVALID, "vr_render: pitch/alignment (pitch %zu, bpp %d)", pitch, bpp);
@@ -1228,11 +1228,37 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
     return VR_OK;
 }
 
+vr_status vr_assemble_frame(void* p, const void* d_gathered, int gathered_format, size_t rows_per_rank, int nranks,
+                            int width, int height, int band_rows, int frame_format, void* d_frame, void* stream)
+{
+    if (!p || !d_gathered || !d_frame) return fail(VR_ERR_INVALID, "vr_assemble_frame: null argument");
+    if (gathered_format < 0 || gathered_format > 5 || frame_format < 0 || frame_format > 5)
+        return fail(VR_ERR_INVALID, "vr_assemble_frame: bad format %d -> %d", gathered_format, frame_format);
+    if (gathered_format != frame_format && grey_of(frame_format) != gathered_format)
+        return fail(VR_ERR_INVALID, "vr_assemble_frame: format %d does not expand into %d", gathered_format,
+                    frame_format);
+    if (gathered_format == frame_format)
+        return vr_assemble_bands(p, d_gathered, rows_per_rank, nranks, width, height, band_rows,
+                                 format_bytes(frame_format), d_frame, stream);
+    if (nranks <= 0 || width <= 0 || height <= 0 || band_rows <= 0)
+        return fail(VR_ERR_INVALID, "vr_assemble_frame: bad geometry");
+    for (int r = 0; r < nranks; ++r)
+        if ((size_t)band_rows_packed(height, band_rows, nranks, r) > rows_per_rank)
+            return fail(VR_ERR_INVALID, "vr_assemble_frame: rows_per_rank %zu too small for rank %d", rows_per_rank, r);
+    Ctx* c = as_ctx(p);
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(launch_assemble_grey(static_cast<const uint8_t*>(d_gathered), rows_per_rank, nranks, width, height,
+                                 band_rows, frame_format == VR_FMT_RGBA32F, static_cast<uint8_t*>(d_frame),
+                                 static_cast<hipStream_t>(stream)));
+    return VR_OK;
+}
+
 vr_status vr_assemble_bands(void* p, const void* d_gathered, size_t rows_per_rank, int nranks, int width,
                             int height, int band_rows, int bytes_per_pixel, void* d_frame, void* stream)
 {
     if (!p || !d_gathered || !d_frame) return fail(VR_ERR_INVALID, "vr_assemble_bands: null argument");
-    if (nranks <= 0 || width <= 0 || height <= 0 || band_rows <= 0 || (bytes_per_pixel != 4 && bytes_per_pixel != 16))
+    if (nranks <= 0 || width <= 0 || height <= 0 || band_rows <= 0 ||
+        (bytes_per_pixel != 1 && bytes_per_pixel != 4 && bytes_per_pixel != 16))
         return fail(VR_ERR_INVALID, "vr_assemble_bands: bad geometry");
     for (int r = 0; r < nranks; ++r)
         if ((size_t)band_rows_packed(height, band_rows, nranks, r) > rows_per_rank)

@@ -212,6 +212,12 @@ struct Schedule {
 
 // launchers (vr_march.hip / vr_volume.hip); return hipError_t
 hipError_t launch_march(const MarchArgs& a, int layout, int wrap, bool early, const Schedule& sc, hipStream_t s);
+// bytes per pixel of a vr_format (include/vr.h), and the grey format of an RGBA one
+__host__ __device__ constexpr int format_bytes(int f) { return f == 0 ? 16 : f <= 2 ? 4 : f <= 4 ? 1 : 4; }
+__host__ __device__ constexpr int grey_of(int f) { return f == 0 ? 5 : f == 1 ? 3 : f == 2 ? 4 : -1; }
+// grey band sets (1 B or fp32 per pixel) -> RGBA frame rows (vr_assemble_frame)
+hipError_t launch_assemble_grey(const uint8_t* d_gathered, size_t rows_per_rank, int nranks, int width, int height,
+                                int band_rows, bool f32, uint8_t* d_frame, hipStream_t s);
 hipError_t launch_march_corner8(const MarchArgs& a, int layout, bool early, const Schedule& sc,
                                 hipStream_t s);   // CORNER8 / CORNERH, vr_march_c8.hip
 hipError_t launch_march_slab(const MarchArgs& a, bool early, const Schedule& sc, hipStream_t s);   // vr_march_slab.hip

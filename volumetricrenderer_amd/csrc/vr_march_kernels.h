@@ -344,22 +344,25 @@ __device__ __forceinline__ Ray setup_ray(const MarchArgs& a, int x, int orow)
 }
 
 // Render-target store: grey g (frag.glsl:80), uncovered pixels keep the
-// clear colour (0,0,0,1) (VulkanRenderPass.cpp:17-24).
+// clear colour (0,0,0,1) (VulkanRenderPass.cpp:17-24).  Formats 3-5 store the
+// R channel only (include/vr.h grey targets).
 __device__ __forceinline__ void store_pixel(const MarchArgs& a, int x, int orow, bool covered, float g)
 {
     char* row = (char*)a.out + (long long)orow * a.pitch;
-    if (a.format == 0) {
+    if (a.format == 0 || a.format == 5) {
         g = covered ? g : 0.0f;
-        reinterpret_cast<float4*>(row)[x] = make_float4(g, g, g, 1.0f);
+        if (a.format == 0) reinterpret_cast<float4*>(row)[x] = make_float4(g, g, g, 1.0f);
+        else reinterpret_cast<float*>(row)[x] = g;
     } else {
         unsigned int q = 0;
         if (covered) {
             float c = fminf(fmaxf(g, 0.0f), 1.0f);
-            if (a.format == 2)
+            if (a.format == 2 || a.format == 4)
                 c = c <= 0.0031308f ? c * 12.92f : fmaf(1.055f, powf(c, 1.0f / 2.4f), -0.055f);
             q = (unsigned int)rintf(c * 255.0f);
         }
-        reinterpret_cast<unsigned int*>(row)[x] = q | (q << 8) | (q << 16) | 0xff000000u;
+        if (a.format <= 2) reinterpret_cast<unsigned int*>(row)[x] = q | (q << 8) | (q << 16) | 0xff000000u;
+        else reinterpret_cast<unsigned char*>(row)[x] = (unsigned char)q;
     }
 }
 

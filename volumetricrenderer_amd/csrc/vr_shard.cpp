@@ -8,8 +8,12 @@
 //                   -> record rendered[p]
 //   comm stream:    wait rendered[p] -> grouped ncclSend (rank r > 0, its
 //                   packed rows) / ncclRecv x (N-1) (rank 0, into slots
-//                   1..N-1) -> rank 0: vr_assemble_bands into frame[p]
+//                   1..N-1) -> rank 0: vr_assemble_frame into frame[p]
 //                   -> record done[p]
+// The band sets are rendered in the grey format of the frame's (include/vr.h
+// VR_FMT_R8_* / R32F: the pixel is vec4(vec3(c), 1), frag.glsl:79-80), so the
+// exchange moves 1 B (or 4 B) per pixel instead of 4 B (16 B), and rank 0's
+// assembly expands them into the RGBA frame.
 // so frame i's exchange overlaps frame i+1's render (the reference's 2
 // frames in flight, VulkanRenderer.cpp:13).  No host synchronisation in the
 // loop: the host cost per frame is one render launch, one RCCL group and
@@ -122,13 +126,15 @@ struct vr_shard {
     int device = 0;
     int nranks = 1, rank = 0;
     int width = 0, height = 0, format = 0, band_rows = 0, bpp = 4;
-    size_t pitch = 0;                 // tight rows
+    size_t pitch = 0;                 // tight frame rows (format)
+    int gformat = 3;                  // grey format of the band sets (exchanged)
+    size_t gpitch = 0;                // tight band-set rows
     int my_rows = 0, rows_per_rank = 0;
     std::vector<int> rows_of;         // packed rows of every rank
     ncclComm_t comm = nullptr;
     hipStream_t comm_stream = nullptr;
-    uint8_t* local[2] = {};           // rank > 0: band sets
-    uint8_t* gathered[2] = {};        // rank 0: nranks slots of rows_per_rank rows
+    uint8_t* local[2] = {};           // rank > 0: band sets (gformat)
+    uint8_t* gathered[2] = {};        // rank 0: nranks slots of rows_per_rank rows (gformat)
     uint8_t* frame[2] = {};           // rank 0
     hipEvent_t rendered[2] = {}, done[2] = {};
     hipEvent_t fence = nullptr;       // vr_shard_barrier: the caller's stream -> comm stream
@@ -248,19 +254,19 @@ vr_status one_frame(vr_shard* sh, int p, hipStream_t s, hipEvent_t t0, hipEvent_
     vr_target t{};
     t.width = sh->width;
     t.height = sh->height;
-    t.format = sh->format;
+    t.format = sh->gformat;
     t.band_rows = sh->band_rows;
     t.band_stride = sh->nranks;
     t.band_first = sh->rank;
     t.pixels = render_buf(sh, p);
-    t.row_pitch = sh->pitch;
+    t.row_pitch = sh->gpitch;
     if (t0) HIP_TRY(hipEventRecord(t0, s));
     if (sh->my_rows > 0) VR_TRY(vr_render(sh->ctx, &t, s));
     if (t1) HIP_TRY(hipEventRecord(t1, s));
     if (sh->loopback)   // the other ranks' band sets, rendered here into their gather slots
         for (int r = 1; r < sh->nranks; ++r) {
             t.band_first = r;
-            t.pixels = sh->gathered[p] + (size_t)r * sh->rows_per_rank * sh->pitch;
+            t.pixels = sh->gathered[p] + (size_t)r * sh->rows_per_rank * sh->gpitch;
             if (sh->rows_of[r] > 0) VR_TRY(vr_render(sh->ctx, &t, s));
         }
     HIP_TRY(hipEventRecord(sh->rendered[p], s));
@@ -270,17 +276,17 @@ vr_status one_frame(vr_shard* sh, int p, hipStream_t s, hipEvent_t t0, hipEvent_
         if (sh->rank == 0) {
             for (int r = 1; r < sh->nranks; ++r)
                 if (sh->rows_of[r] > 0)
-                    NCCL_TRY(ncclRecv(sh->gathered[p] + (size_t)r * sh->rows_per_rank * sh->pitch,
-                                      (size_t)sh->rows_of[r] * sh->pitch, ncclUint8, r, sh->comm, sh->comm_stream));
+                    NCCL_TRY(ncclRecv(sh->gathered[p] + (size_t)r * sh->rows_per_rank * sh->gpitch,
+                                      (size_t)sh->rows_of[r] * sh->gpitch, ncclUint8, r, sh->comm, sh->comm_stream));
         } else if (sh->my_rows > 0) {
-            NCCL_TRY(ncclSend(sh->local[p], (size_t)sh->my_rows * sh->pitch, ncclUint8, 0, sh->comm,
+            NCCL_TRY(ncclSend(sh->local[p], (size_t)sh->my_rows * sh->gpitch, ncclUint8, 0, sh->comm,
                               sh->comm_stream));
         }
         NCCL_TRY(ncclGroupEnd());
     }
     if (sh->rank == 0)
-        VR_TRY(vr_assemble_bands(sh->ctx, sh->gathered[p], (size_t)sh->rows_per_rank, sh->nranks, sh->width,
-                                 sh->height, sh->band_rows, sh->bpp, sh->frame[p], sh->comm_stream));
+        VR_TRY(vr_assemble_frame(sh->ctx, sh->gathered[p], sh->gformat, (size_t)sh->rows_per_rank, sh->nranks,
+                                 sh->width, sh->height, sh->band_rows, sh->format, sh->frame[p], sh->comm_stream));
     HIP_TRY(hipEventRecord(sh->done[p], sh->comm_stream));
     sh->pending[p] = true;
     sh->last = p;
@@ -324,6 +330,8 @@ vr_status vr_shard_alloc(void* ctx, int nranks, int rank, int width, int height,
     sh->band_rows = band_rows;
     sh->bpp = format == VR_FMT_RGBA32F ? 16 : 4;
     sh->pitch = (size_t)width * sh->bpp;
+    sh->gformat = format == VR_FMT_RGBA32F ? VR_FMT_R32F : format == VR_FMT_RGBA8_SRGB ? VR_FMT_R8_SRGB : VR_FMT_R8_UNORM;
+    sh->gpitch = (size_t)width * (format == VR_FMT_RGBA32F ? 4 : 1);
     for (int r = 0; r < nranks; ++r) sh->rows_of.push_back(vr_band_rows_packed(height, band_rows, nranks, r));
     sh->my_rows = sh->rows_of[rank];
     sh->rows_per_rank = sh->rows_of[0];   // band 0 is rank 0's: it has the most rows
@@ -346,10 +354,10 @@ vr_status vr_shard_alloc(void* ctx, int nranks, int rank, int width, int height,
         hip_ok(hipEventCreateWithFlags(&sh->rendered[p], hipEventDisableTiming), "event");
         hip_ok(hipEventCreateWithFlags(&sh->done[p], hipEventDisableTiming), "event");
         if (rank == 0) {
-            hip_ok(hipMalloc(&sh->gathered[p], (size_t)nranks * sh->rows_per_rank * sh->pitch), "gather buffer");
+            hip_ok(hipMalloc(&sh->gathered[p], (size_t)nranks * sh->rows_per_rank * sh->gpitch), "gather buffer");
             hip_ok(hipMalloc(&sh->frame[p], (size_t)height * sh->pitch), "frame buffer");
         } else {
-            hip_ok(hipMalloc(&sh->local[p], (size_t)std::max(sh->my_rows, 1) * sh->pitch), "band buffer");
+            hip_ok(hipMalloc(&sh->local[p], (size_t)std::max(sh->my_rows, 1) * sh->gpitch), "band buffer");
         }
     }
     if (st != VR_OK) {
@@ -588,7 +596,7 @@ vr_status vr_shard_frame(vr_shard* sh, void** pixels, size_t* row_pitch, int* ro
     if (!sh || !pixels) return fail(VR_ERR_INVALID, "vr_shard_frame: null argument");
     if (sh->last < 0) return fail(VR_ERR_INVALID, "vr_shard_frame: no frame rendered yet");
     *pixels = sh->rank == 0 ? sh->frame[sh->last] : sh->local[sh->last];
-    if (row_pitch) *row_pitch = sh->pitch;
+    if (row_pitch) *row_pitch = sh->rank == 0 ? sh->pitch : sh->gpitch;
     if (rows) *rows = sh->rank == 0 ? sh->height : sh->my_rows;
     return VR_OK;
 }

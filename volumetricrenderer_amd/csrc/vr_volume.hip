@@ -318,6 +318,52 @@ __global__ __launch_bounds__(kBlock) void k_assemble(const T* __restrict__ src, 
     }
 }
 
+// Grey band sets -> RGBA frame (vr_assemble_frame): element e of frame row y
+// comes from the same place k_assemble reads, expanded.  P pixels per element:
+// u8 x 4 (uchar4 -> 4 RGBA8 words, rows of a multiple of 4 pixels), u8 x 1,
+// or fp32 x 1 (-> float4).
+template <typename S, typename D>
+__device__ __forceinline__ D grey_expand(S v);
+template <>
+__device__ __forceinline__ uint4 grey_expand<unsigned int, uint4>(unsigned int v)
+{
+    uint4 o;
+    unsigned q = v & 0xffu;
+    o.x = q * 0x010101u | 0xff000000u;
+    q = (v >> 8) & 0xffu;
+    o.y = q * 0x010101u | 0xff000000u;
+    q = (v >> 16) & 0xffu;
+    o.z = q * 0x010101u | 0xff000000u;
+    q = v >> 24;
+    o.w = q * 0x010101u | 0xff000000u;
+    return o;
+}
+template <>
+__device__ __forceinline__ unsigned int grey_expand<unsigned char, unsigned int>(unsigned char v)
+{
+    return (unsigned)v * 0x010101u | 0xff000000u;
+}
+template <>
+__device__ __forceinline__ float4 grey_expand<float, float4>(float v)
+{
+    return make_float4(v, v, v, 1.0f);
+}
+template <typename S, typename D>
+__global__ __launch_bounds__(kBlock) void k_assemble_grey(const S* __restrict__ src, long long rows_per_rank,
+                                                          int nranks, int row_elems, int height, int band_rows,
+                                                          D* __restrict__ dst)
+{
+    const long long total = (long long)height * row_elems;
+    for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < total;
+         i += (long long)gridDim.x * kBlock) {
+        const int y = (int)(i / row_elems), e = (int)(i % row_elems);
+        const int b = y / band_rows, r = y - b * band_rows;
+        const int rank = b % nranks, lb = b / nranks;
+        const long long srow = (long long)rank * rows_per_rank + (long long)lb * band_rows + r;
+        dst[i] = grey_expand<S, D>(src[srow * row_elems + e]);
+    }
+}
+
 int grid_for(long long n)
 {
     long long g = (n + kBlock - 1) / kBlock;
@@ -486,11 +532,36 @@ hipError_t launch_assemble(const uint8_t* d_gathered, size_t rows_per_rank, int 
         hipLaunchKernelGGL(k_assemble<uint4>, dim3(grid_for((long long)height * elems)), dim3(kBlock), 0, s,
                            reinterpret_cast<const uint4*>(d_gathered), (long long)rows_per_rank, nranks, elems,
                            height, band_rows, reinterpret_cast<uint4*>(d_frame));
-    } else {
+    } else if (row_bytes % 4 == 0) {
         const int elems = (int)(row_bytes / 4);
         hipLaunchKernelGGL(k_assemble<unsigned int>, dim3(grid_for((long long)height * elems)), dim3(kBlock), 0,
                            s, reinterpret_cast<const unsigned int*>(d_gathered), (long long)rows_per_rank, nranks,
                            elems, height, band_rows, reinterpret_cast<unsigned int*>(d_frame));
+    } else {   // 1-byte pixels, rows of any width
+        const int elems = (int)row_bytes;
+        hipLaunchKernelGGL(k_assemble<unsigned char>, dim3(grid_for((long long)height * elems)), dim3(kBlock), 0,
+                           s, d_gathered, (long long)rows_per_rank, nranks, elems, height, band_rows, d_frame);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_assemble_grey(const uint8_t* d_gathered, size_t rows_per_rank, int nranks, int width, int height,
+                                int band_rows, bool f32, uint8_t* d_frame, hipStream_t s)
+{
+    const dim3 blk(kBlock);
+    if (f32) {
+        hipLaunchKernelGGL((k_assemble_grey<float, float4>), dim3(grid_for((long long)height * width)), blk, 0, s,
+                           reinterpret_cast<const float*>(d_gathered), (long long)rows_per_rank, nranks, width, height,
+                           band_rows, reinterpret_cast<float4*>(d_frame));
+    } else if (width % 4 == 0) {
+        const int elems = width / 4;
+        hipLaunchKernelGGL((k_assemble_grey<unsigned int, uint4>), dim3(grid_for((long long)height * elems)), blk, 0,
+                           s, reinterpret_cast<const unsigned int*>(d_gathered), (long long)rows_per_rank, nranks,
+                           elems, height, band_rows, reinterpret_cast<uint4*>(d_frame));
+    } else {
+        hipLaunchKernelGGL((k_assemble_grey<unsigned char, unsigned int>), dim3(grid_for((long long)height * width)),
+                           blk, 0, s, d_gathered, (long long)rows_per_rank, nranks, width, height, band_rows,
+                           reinterpret_cast<unsigned int*>(d_frame));
     }
     return hipGetLastError();
 }

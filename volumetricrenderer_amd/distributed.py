@@ -8,7 +8,9 @@ Interleaved 16-row bands, where band b goes to rank b mod N, are balanced to
 within 1-2 %.  The only exchange is one gather per frame.  Each rank's packed
 band set goes to rank 0, over RCCL (torch.distributed "nccl") on GPUs or gloo
 in the CPU tests.  Rank 0 then scatters the sets into the frame with
-vr_assemble_bands.
+vr_assemble_frame.  The sets travel in the frame format's grey form (one value
+per pixel: the shader writes vec4(vec3(c), 1), frag.glsl:79-80), a quarter of
+the RGBA bytes; the assembly expands them.
 
 One process per GPU; the reference has no distributed code at all.
 """
@@ -72,9 +74,12 @@ def share_volume(renderer, vol=None, rank: int | None = None, group=None):
 class BandSharder:
     """Renders this rank's bands of a W x H frame and gathers them on rank 0.
 
-    `renderer` provides ``alloc_target``, ``render`` and ``assemble_bands``.
+    `renderer` provides ``alloc_target``, ``render`` and ``assemble_frame``
+    (or only ``assemble_bands``: then the band sets keep the frame format).
     That is :class:`volumetricrenderer_amd.Renderer`, or a CPU stand-in in
-    the gloo tests.
+    the gloo tests.  With several ranks the band sets are grey
+    (``GREY_OF[fmt]``); :meth:`frame` returns rank 0's RGBA frame and the
+    other ranks' grey band sets.
     """
 
     def __init__(self, renderer, width: int, height: int, fmt: int, band_rows: int = 16, world: int = 1,
@@ -83,17 +88,19 @@ class BandSharder:
         self.width, self.height, self.fmt = width, height, fmt
         self.world, self.rank, self.group = world, rank, group
         self.band_rows = band_rows if world > 1 else 0
+        grey = world > 1 and hasattr(renderer, "assemble_frame") and fmt in _lib.GREY_OF
+        self.gfmt = _lib.GREY_OF[fmt] if grey else fmt   # format of the band sets (exchanged)
         if world > 1:
             self.my_rows = rows_for_rank(height, band_rows, world, rank)
             # every rank's buffer has rank 0's row count (the most rows), so
             # the gather moves equal-sized messages
             self.rows_per_rank = rows_for_rank(height, band_rows, world, 0)
-            buf = renderer.alloc_target(width, height, fmt, band_rows, world, 0)
+            buf = renderer.alloc_target(width, height, self.gfmt, band_rows, world, 0)
             assert buf.shape[0] == self.rows_per_rank
             self.local = buf
             if rank == 0:
                 self.gathered = torch.empty((world,) + tuple(buf.shape), dtype=buf.dtype, device=buf.device)
-                self.frame_buf = torch.empty((height, width, buf.shape[-1]), dtype=buf.dtype, device=buf.device)
+                self.frame_buf = renderer.alloc_target(width, height, fmt)
         else:
             self.my_rows = height
             self.rows_per_rank = height
@@ -105,7 +112,7 @@ class BandSharder:
         if events is not None:
             events[0].record()
         if self.world > 1:
-            self.r.render(self.width, self.height, self.fmt, out=self.local[: self.my_rows],
+            self.r.render(self.width, self.height, self.gfmt, out=self.local[: self.my_rows],
                           band_rows=self.band_rows, band_stride=self.world, band_first=self.rank,
                           step_counter=step_counter)
         else:
@@ -131,10 +138,16 @@ class BandSharder:
             gl = list(self.gathered.unbind(0)) if self.rank == 0 else None
             dist.gather(self.local, gather_list=gl, dst=0, group=self.group)
         if self.rank == 0:
-            self.r.assemble_bands(self.gathered, self.world, self.width, self.height, self.band_rows,
-                                  frame=self.frame_buf)
+            self._assemble(self.gathered, self.frame_buf)
             return self.frame_buf
         return self.local
+
+    def _assemble(self, gathered, frame):
+        if hasattr(self.r, "assemble_frame"):
+            self.r.assemble_frame(gathered, self.gfmt, self.world, self.width, self.height, self.band_rows,
+                                  self.fmt, frame=frame)
+        else:
+            self.r.assemble_bands(gathered, self.world, self.width, self.height, self.band_rows, frame=frame)
 
     def run_frames(self, k: int, events=None):
         """Render k frames with two in flight, mirroring the reference's
@@ -174,11 +187,12 @@ class BandSharder:
                                    else [None, None])
             if hasattr(self.r, "prepare_render"):
                 self._pipe["render"] = [
-                    self.r.prepare_render(self.width, self.height, self.fmt, loc[: self.my_rows],
+                    self.r.prepare_render(self.width, self.height, self.gfmt, loc[: self.my_rows],
                                           band_rows=self.band_rows, band_stride=self.world, band_first=self.rank)
                     for loc in self._pipe["local"]]
                 self._pipe["assemble"] = ([
-                    self.r.prepare_assemble(g, self.world, self.width, self.height, self.band_rows, fr)
+                    self.r.prepare_assemble_frame(g, self.gfmt, self.world, self.width, self.height, self.band_rows,
+                                                  self.fmt, fr)
                     for g, fr in zip(self._pipe["gathered"], self._pipe["frame"])] if self.rank == 0
                     else [None, None])
         P = self._pipe
@@ -191,8 +205,7 @@ class BandSharder:
                 if "assemble" in P:
                     P["assemble"][par]()
                 else:
-                    self.r.assemble_bands(P["gathered"][par], self.world, self.width, self.height,
-                                          self.band_rows, frame=P["frame"][par])
+                    self._assemble(P["gathered"][par], P["frame"][par])
 
         last = None
         for i in range(k):
@@ -204,7 +217,7 @@ class BandSharder:
             if "render" in P:
                 P["render"][par]()
             else:
-                self.r.render(self.width, self.height, self.fmt, out=loc[: self.my_rows],
+                self.r.render(self.width, self.height, self.gfmt, out=loc[: self.my_rows],
                               band_rows=self.band_rows, band_stride=self.world, band_first=self.rank)
             if ev is not None:
                 ev[1].record()
@@ -353,10 +366,10 @@ class RcclBandPipeline:
         _lib.shard_call("vr_shard_barrier", self._h, _stream_handle(stream))
 
     def frame(self, stream=None) -> torch.Tensor:
-        """A copy of the last frame (rank 0) or band set (other ranks)."""
+        """A copy of the last frame (rank 0) or grey band set (other ranks)."""
         from .renderer import _stream_handle
         rows = self.height if self.rank == 0 else self.my_rows
-        out = self.r.alloc_target(self.width, rows, self.fmt)
+        out = self.r.alloc_target(self.width, rows, self.fmt if self.rank == 0 else _lib.GREY_OF[self.fmt])
         _lib.shard_call("vr_shard_copy_frame", self._h, ctypes.c_void_p(out.data_ptr()), 0, _stream_handle(stream))
         return out
 

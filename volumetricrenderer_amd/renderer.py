@@ -30,8 +30,8 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import (BYTES_PER_PIXEL, FMT_RGBA8_SRGB, FMT_RGBA8_UNORM, FMT_RGBA32F,  # noqa: F401
-                   GlobalShaderData, MarchParams, ObjectShaderData, Procedural, Target, VolumeRecipe, VRError,
+from ._lib import (BYTES_PER_PIXEL, CHANNELS, FLOAT_FORMATS, FMT_RGBA8_SRGB, FMT_RGBA8_UNORM, FMT_RGBA32F,  # noqa: F401
+                   GREY_OF, GlobalShaderData, MarchParams, ObjectShaderData, Procedural, Target, VolumeRecipe, VRError,
                    call)
 
 _lib.load()  # fail at import if the HIP library is missing
@@ -221,11 +221,13 @@ class Renderer:
     # -- the hot path ------------------------------------------------------
     def alloc_target(self, width: int, height: int, fmt: int = FMT_RGBA8_UNORM, band_rows: int = 0,
                      band_stride: int = 1, band_first: int = 0) -> torch.Tensor:
+        """(rows, width, 4) for the RGBA formats, (rows, width) for the grey ones."""
         rows = band_rows_packed(height, band_rows, band_stride, band_first)
         dev = torch.device("cuda", self.device)
-        if fmt == FMT_RGBA32F:
-            return torch.empty((rows, width, 4), dtype=torch.float32, device=dev)
-        return torch.empty((rows, width, 4), dtype=torch.uint8, device=dev)
+        if fmt not in BYTES_PER_PIXEL:
+            raise ValueError(f"unknown format {fmt}")
+        shape = (rows, width, 4) if CHANNELS[fmt] == 4 else (rows, width)
+        return torch.empty(shape, dtype=torch.float32 if fmt in FLOAT_FORMATS else torch.uint8, device=dev)
 
     def _check_target(self, width: int, height: int, fmt: int, out: torch.Tensor, band_rows: int,
                       band_stride: int, band_first: int, step_counter: torch.Tensor | None = None) -> None:
@@ -236,15 +238,22 @@ class Renderer:
             raise ValueError(f"unknown format {fmt}")
         if not isinstance(out, torch.Tensor) or not out.is_cuda or out.device.index != self.device:
             raise ValueError(f"render target must be a tensor on cuda:{self.device}")
-        want_dtype = torch.float32 if fmt == FMT_RGBA32F else torch.uint8
+        want_dtype = torch.float32 if fmt in FLOAT_FORMATS else torch.uint8
         if out.dtype != want_dtype:
             raise ValueError(f"format {fmt} needs a {want_dtype} target, got {out.dtype}")
         rows = band_rows_packed(height, band_rows, band_stride, band_first)
-        if out.dim() != 3 or out.shape[0] < rows or out.shape[1] != width or out.shape[2] != 4:
-            raise ValueError(f"render target must be shaped ({rows}, {width}, 4) (at least {rows} rows), "
-                             f"got {tuple(out.shape)}")
-        if out.stride(2) != 1 or out.stride(1) != 4 or out.stride(0) < 4 * width:
-            raise ValueError("render target rows must be contiguous RGBA pixels (strides (>=4*width, 4, 1))")
+        if CHANNELS[fmt] == 4:
+            if out.dim() != 3 or out.shape[0] < rows or out.shape[1] != width or out.shape[2] != 4:
+                raise ValueError(f"render target must be shaped ({rows}, {width}, 4) (at least {rows} rows), "
+                                 f"got {tuple(out.shape)}")
+            if out.stride(2) != 1 or out.stride(1) != 4 or out.stride(0) < 4 * width:
+                raise ValueError("render target rows must be contiguous RGBA pixels (strides (>=4*width, 4, 1))")
+        else:
+            if out.dim() != 2 or out.shape[0] < rows or out.shape[1] != width:
+                raise ValueError(f"grey render target must be shaped ({rows}, {width}) (at least {rows} rows), "
+                                 f"got {tuple(out.shape)}")
+            if out.stride(1) != 1 or out.stride(0) < width:
+                raise ValueError("grey render target rows must be contiguous (strides (>=width, 1))")
         if step_counter is not None and (step_counter.dtype != torch.int64 or not step_counter.is_cuda
                                          or step_counter.device.index != self.device
                                          or step_counter.numel() < 1):
@@ -295,6 +304,52 @@ class Renderer:
             st = fn(*args)
             if st:
                 _lib.check(st, "vr_assemble_bands")
+        launch.keep = (gathered, frame)
+        return launch
+
+    def _check_assemble_frame(self, gathered: torch.Tensor, gfmt: int, nranks: int, width: int, height: int,
+                              frame: torch.Tensor, ffmt: int) -> None:
+        for name, t in (("gathered", gathered), ("frame", frame)):
+            if not t.is_cuda or t.device.index != self.device or not t.is_contiguous():
+                raise ValueError(f"{name} must be a contiguous tensor on cuda:{self.device}")
+        if gfmt != ffmt and GREY_OF.get(ffmt) != gfmt:
+            raise ValueError(f"band sets in format {gfmt} do not expand into format {ffmt}")
+        gshape = (width, 4) if CHANNELS[gfmt] == 4 else (width,)
+        gdtype = torch.float32 if gfmt in FLOAT_FORMATS else torch.uint8
+        if gathered.dim() != 2 + len(gshape) or gathered.shape[0] < nranks or tuple(gathered.shape[2:]) != gshape \
+                or gathered.dtype != gdtype:
+            raise ValueError(f"gathered must be a {gdtype} tensor shaped (>= {nranks}, rows, {gshape}), "
+                             f"got {gathered.dtype} {tuple(gathered.shape)}")
+        fdtype = torch.float32 if ffmt in FLOAT_FORMATS else torch.uint8
+        fshape = (height, width, 4) if CHANNELS[ffmt] == 4 else (height, width)
+        if frame.dtype != fdtype or tuple(frame.shape) != fshape:
+            raise ValueError(f"frame must be a {fdtype} tensor shaped {fshape}")
+
+    def assemble_frame(self, gathered: torch.Tensor, gathered_fmt: int, nranks: int, width: int, height: int,
+                       band_rows: int, frame_fmt: int, frame: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+        """vr_assemble_frame: [rank][packed rows] band sets in `gathered_fmt`
+        (e.g. grey) scattered and expanded into a `frame_fmt` frame."""
+        if frame is None:
+            shape = (height, width, 4) if CHANNELS[frame_fmt] == 4 else (height, width)
+            frame = torch.empty(shape, dtype=torch.float32 if frame_fmt in FLOAT_FORMATS else torch.uint8,
+                                device=gathered.device)
+        self._check_assemble_frame(gathered, gathered_fmt, nranks, width, height, frame, frame_fmt)
+        call("vr_assemble_frame", self._ctx, ctypes.c_void_p(gathered.data_ptr()), gathered_fmt, gathered.shape[1],
+             nranks, width, height, band_rows, frame_fmt, ctypes.c_void_p(frame.data_ptr()), _stream_handle(stream))
+        return frame
+
+    def prepare_assemble_frame(self, gathered: torch.Tensor, gathered_fmt: int, nranks: int, width: int, height: int,
+                               band_rows: int, frame_fmt: int, frame: torch.Tensor, stream=None):
+        """Zero-argument launcher for one fixed vr_assemble_frame call."""
+        self._check_assemble_frame(gathered, gathered_fmt, nranks, width, height, frame, frame_fmt)
+        args = (self._ctx, ctypes.c_void_p(gathered.data_ptr()), gathered_fmt, gathered.shape[1], nranks, width,
+                height, band_rows, frame_fmt, ctypes.c_void_p(frame.data_ptr()), _stream_handle(stream))
+        fn = _lib.load().vr_assemble_frame
+
+        def launch():
+            st = fn(*args)
+            if st:
+                _lib.check(st, "vr_assemble_frame")
         launch.keep = (gathered, frame)
         return launch
 
