@@ -199,16 +199,18 @@ def test_every_layout_bitexact(r, oracle, vol128, layout, name):
 @pytest.mark.parametrize("layout", [15, 12, 14, 7])
 def test_split_long_tiles_bitexact(r, oracle, vol128, layout):
     """split_long (march_regions_mixed): the tiles costing >= split_long % of
-    the longest are marched as two 8x4 halves with two lanes per ray, the rest
-    with one.  split = 1 forces the one-lane frame the mix applies to on these
-    small targets.  1 % splits every tile with work, 100 % only the longest;
-    bit-exact with exact step counts, with and without early-out, and with a
-    banded target (packed rows)."""
+    the longest are marched as KS sub-blocks with KS lanes per ray, the rest
+    with one.  split = 1 gives KS = 2 (halves), split = 2 / 4 KS = 2 / 4.
+    1 % splits every tile with work, 100 % only the longest; bit-exact with
+    exact step counts, with and without early-out, and with a banded target
+    (packed rows).  Layout 7 (zpair) has no mixed kernel: the option must
+    leave it on its plain / split path."""
     r.set_volume(vol128)
     r.set_layout_preference(layout)
     r.set_option("split", 1)
     try:
-        for pct in (1, 60, 100):
+        for split, pct in [(1, 1), (1, 60), (1, 100), (2, 50), (4, 1), (4, 70)]:
+            r.set_option("split", split)   # 1: long tiles in halves (KS = 2); 2, 4: KS = the split K
             r.set_option("split_long", pct)
             assert r.get_option("split_long") == pct
             for (W, H, phi, theta) in [(480, 270, 0.0, 0.0), (203, 117, 35.0, -20.0)]:

@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--steps", type=int, default=128)
     ap.add_argument("--frames", type=int, default=20)
     ap.add_argument("--variants", default="-1:0:0", help="comma list of schedule:tiles_per_wave:split[:wedges]")
+    ap.add_argument("--opt", action="append", default=[], help="vr option NAME=VALUE, set first")
+    ap.add_argument("--ns", default="1,2,4,8")
     a = ap.parse_args()
     W, H = a.width, a.height
     with vr.Renderer(0) as r:
@@ -30,6 +32,9 @@ def main():
         osd, gsd = vr.reference_shader_data(1280 / 720)
         r.set_shader_data(osd, gsd)
         r.set_march(vr.march_defaults(max_steps=a.steps))
+        for o in a.opt:
+            k, v = o.split("=")
+            r.set_option(k, int(v))
         for var in a.variants.split(","):
             vals = [int(v) for v in var.split(":")]
             sched, tpw, split = vals[:3]
@@ -40,7 +45,7 @@ def main():
             if wedges:
                 r.set_option("wedges", wedges)
             base = None
-            for n in (1, 2, 4, 8):
+            for n in [int(v) for v in a.ns.split(",")]:
                 band = dict(band_rows=16, band_stride=n, band_first=0)
                 out = r.alloc_target(W, H, 1, **band)
                 r.render(W, H, 1, out=out, **band)
@@ -52,7 +57,7 @@ def main():
                 torch.cuda.synchronize()
                 t = float(np.median([ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(a.frames)]))
                 base = base or t
-                print(f"schedule {sched} tpw {tpw} split {split} wedges {wedges} N={n}: rank-0 bands {t:.4f} ms, whole/N {base / n:.4f} ms, "
+                print(f"{' '.join(a.opt)} schedule {sched} tpw {tpw} split {split} wedges {wedges} N={n}: rank-0 bands {t:.4f} ms, whole/N {base / n:.4f} ms, "
                       f"efficiency {base / n / t:.2f}", flush=True)
 
 

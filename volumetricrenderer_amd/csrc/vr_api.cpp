@@ -107,7 +107,7 @@ struct Ctx {
         size_t cap = 0;            // entries
         TileMap map{};
         int nwork = 0;             // tiles with estimated work
-        bool mixed = false;        // the lists hold split halves of the longest tiles (bit 31)
+        int mixed = 0;             // the lists hold this many sub-blocks (2, 4) of the longest tiles (bit 31)
         // the streams that rendered with these lists; when the lists are
         // retired an event is recorded on each, and the buffer is rewritten
         // only after those events (kMaxRegionStreams; more -> device sync)
@@ -851,6 +851,13 @@ vr_status note_region_stream(Ctx::RegionBuf& rb, hipStream_t s)
     return VR_OK;
 }
 
+// lanes per ray of a regions frame: option split, or auto from the tiles with work
+static int auto_split(const Ctx* c, long long nwork)
+{
+    if (c->split > 0) return c->split;
+    return nwork >= kSplitOneLane ? 1 : nwork >= kSplitTwoLanes ? 2 : 4;
+}
+
 vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow, bool mixable, hipStream_t stream)
 {
     const int tw = (a.width + 7) >> 3, th = (a.out_rows + 7) >> 3;
@@ -930,17 +937,19 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     std::sort(idle.begin(), idle.end(), inside_out);
     for (size_t i = 0; i < idle.size(); ++i) xl[i % 8].push_back(idle[i]);
 
-    // split_long: the tiles costing >= split_long % of the longest go in as two
-    // halves marched two lanes per ray (march_regions_mixed), only where the
-    // rest of the frame runs one lane per ray
+    // split_long: the tiles costing >= split_long % of the longest go in as KS
+    // sub-blocks marched KS lanes per ray (march_regions_mixed), the rest with
+    // one lane per ray.  KS = the frame's split K (auto_split), or 2 where that
+    // is 1.
     double most_cost = 0.0;
     for (const T& t : work) most_cost = std::max(most_cost, t.cost);
     const double split_at = std::max(1.0, most_cost * c->split_long / 100.0);
-    const bool mixed = mixable && c->split_long > 0 && th < 16384 &&
-                       (c->split == 1 || (c->split == 0 && (long long)work.size() >= kSplitOneLane));
+    const int kall = auto_split(c, (long long)work.size());
+    const int ks = kall > 1 ? kall : 2;
+    const int mixed = mixable && c->split_long > 0 && th < 8192 && ks <= 4 ? ks : 0;
     size_t n = (size_t)tw * th;
     if (mixed)
-        for (const T& t : work) n += t.cost >= split_at;
+        for (const T& t : work) n += (size_t)(t.cost >= split_at) * (size_t)(ks - 1);
     if (c->region_cur >= 0) {   // retire the current lists in the stream order of their renders
         Ctx::RegionBuf& old = c->region[c->region_cur];
         old.nretired = 0;
@@ -974,8 +983,7 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
         m.off[x] = (int)pos;
         for (const T& t : xl[x]) {
             if (mixed && t.cost >= split_at) {
-                rb.h[pos++] = t.id | 0x80000000u;
-                rb.h[pos++] = t.id | 0xc0000000u;
+                for (int s = 0; s < mixed; ++s) rb.h[pos++] = t.id | 0x80000000u | ((unsigned)s << 29);
             } else {
                 rb.h[pos++] = t.id;
             }
@@ -1200,7 +1208,9 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
     if (kind == SCHED_REGIONS) {
         const bool splittable = is_b4_family(pl.layout) || pl.layout == LAYOUT_ZPAIR || pl.layout == LAYOUT_CORNER8 ||
                                 pl.layout == LAYOUT_CORNERH;
-        const vr_status st = build_regions(c, a, tpw, sc.center_x, sc.center_y, splittable && !sc.slab,
+        const bool mixable = !sc.slab && (pl.layout == LAYOUT_COL48 || pl.layout == LAYOUT_BRICK4832 ||
+                                          pl.layout == LAYOUT_CORNERH);   // march_regions_mixed instances
+        const vr_status st = build_regions(c, a, tpw, sc.center_x, sc.center_y, mixable,
                                            static_cast<hipStream_t>(stream));
         if (st != VR_OK) return st;
         const Ctx::RegionBuf& rb = c->region[c->region_cur];
@@ -1212,9 +1222,7 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
         if (splittable && !rb.mixed) {
             int K = c->split;
             if (sc.slab) K = K == 0 ? 1 : K;   // the slab march has one lane per ray; split > 1 uses the plain march
-            if (K == 0) {
-                K = rb.nwork >= kSplitOneLane ? 1 : rb.nwork >= kSplitTwoLanes ? 2 : 4;
-            }
+            if (K == 0) K = auto_split(c, rb.nwork);
             if (K > 1) {
                 const int ktpw = tpw;
                 int most = 0;

@@ -206,7 +206,7 @@ struct Schedule {
     TileMap map;           // regions (nwx counts waves of split units)
     int split;             // regions: lanes per ray (1, 2, 4, 8; BRICK4 / CORNER8 only)
     int slab;              // regions + COL48: the LDS slab march (vr_march_slab.hip)
-    int mixed;             // regions: the list holds split halves of the longest tiles (march_regions_mixed)
+    int mixed;             // regions: 2 or 4 = the list holds that many sub-blocks of each longest tile (march_regions_mixed)
     int wg_waves;          // regions (one lane per ray): waves per workgroup, 4 (default), 8 or 16
 };
 
