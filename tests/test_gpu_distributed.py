@@ -145,16 +145,18 @@ def test_rccl_pipeline_deadline_aborts():
             pl.close()
 
 
-@pytest.mark.parametrize("world,band_rows,fmt", [(2, 16, 1), (3, 16, 0), (8, 16, 1), (5, 7, 1)])
-def test_native_pipeline_loopback_ranks(world, band_rows, fmt):
-    """The native frame loop's N-rank data layout (packed band sets in gather
-    slots of rank 0's row count, vr_assemble_bands) with every rank's bands
-    rendered by this one process: the frame equals a plain render."""
+@pytest.mark.parametrize("world,band_rows,fmt,W", [(2, 16, 1, 500), (3, 16, 0, 500), (8, 16, 1, 500), (5, 7, 1, 500),
+                                                   (3, 16, 2, 499), (4, 16, 0, 499)])
+def test_native_pipeline_loopback_ranks(world, band_rows, fmt, W):
+    """The native frame loop's N-rank data layout (grey band sets in gather
+    slots of rank 0's row count, expanded by vr_assemble_frame) with every
+    rank's bands rendered by this one process: the frame equals a plain
+    render.  Width 499 takes the per-pixel expansion, 500 the 4-pixel one."""
     import sys
     sys.path.insert(0, ROOT)
     import volumetricrenderer_amd as vr
     from volumetricrenderer_amd.distributed import RcclBandPipeline
-    W, H = 500, 283
+    H = 283
     with vr.Renderer(0) as r:
         r.generate_volume(vr.volume_recipe_defaults(size=64))
         osd, gsd = vr.reference_shader_data(W / H, -30.0, 40.0)
