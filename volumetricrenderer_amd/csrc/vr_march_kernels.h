@@ -577,6 +577,9 @@ __device__ __forceinline__ unsigned march_pixel_proc(const MarchArgs& a, const f
 // (profiles/r03/ab_config3_deal_enum.txt, pmc_config3_deal_enum.txt): the
 // conflicts are not on config 3's critical path.  Removed after measuring.
 constexpr int kMaxCompactShadow = 8;
+// Distance from the box faces beyond which the shadow-run fast path needs no
+// per-sample test: 8 sequential adds drift < 8 * 6e-8 from the exact segment.
+constexpr float kShadowInMargin = 1.0e-6f;
 // Dealt pair pid lives at slot pid + pid / 32: an owner lane writes (and later
 // reads) its run at off_k + c, and the offsets of neighbouring lanes step by
 // their run lengths (~8), which without the pad puts 32 lanes on 4 LDS banks.
@@ -623,16 +626,32 @@ __device__ __forceinline__ unsigned march_pixel_proc_compact(const MarchArgs& a,
             // along j is an interval, and so is their intersection.  Only those are dealt, so
             // no lane of a round idles on an outside sample (they contribute exactly +0).
             int lo = 0, cnt = 0;
+            // Fast path: the shadow samples lie on the segment from P + L to
+            // P + S L (convex), and the sequential adds drift from it by at most
+            // S half-ulps (< 6e-8 each below 2).  When both ends are inside the
+            // box by kShadowInMargin, every sample is: the run is j = 0..S-1.
+            bool slow = false;
             if (need) {
-                float q0 = P0, q1 = P1, q2 = P2;
-                for (int j = 0; j < S; ++j) {
-                    q0 = q0 + l0; q1 = q1 + l1; q2 = q2 + l2;
-                    // the box test as min3 / max3 (q is never NaN): 4 ops, not 6 compares
-                    const bool in = fminf(fminf(q0, q1), q2) >= 0.0f && fmaxf(fmaxf(q0, q1), q2) <= 1.0f;
-                    if (in && cnt == 0) lo = j;
-                    cnt += in ? 1 : 0;
-                }
+                const float fs = (float)S;
+                const float a0 = fmaf(fs, l0, P0), a1 = fmaf(fs, l1, P1), a2 = fmaf(fs, l2, P2);
+                const float b0 = P0 + l0, b1 = P1 + l1, b2 = P2 + l2;
+                const float lo3 = fminf(fminf(fminf(a0, a1), a2), fminf(fminf(b0, b1), b2));
+                const float hi3 = fmaxf(fmaxf(fmaxf(a0, a1), a2), fmaxf(fmaxf(b0, b1), b2));
+                slow = !(lo3 >= kShadowInMargin && hi3 <= 1.0f - kShadowInMargin);
+                cnt = slow ? 0 : S;
                 sh->p[lane] = make_float4(P0, P1, P2, 0.0f);
+            }
+            if (__ballot(slow)) {
+                if (slow) {
+                    float q0 = P0, q1 = P1, q2 = P2;
+                    for (int j = 0; j < S; ++j) {
+                        q0 = q0 + l0; q1 = q1 + l1; q2 = q2 + l2;
+                        // the box test as min3 / max3 (q is never NaN): 4 ops, not 6 compares
+                        const bool in = fminf(fminf(q0, q1), q2) >= 0.0f && fmaxf(fmaxf(q0, q1), q2) <= 1.0f;
+                        if (in && cnt == 0) lo = j;
+                        cnt += in ? 1 : 0;
+                    }
+                }
             }
             // Exclusive prefix of cnt (0..8, four bits) over the wave, by bit-plane ballots.
             int off = 0, total = 0;
