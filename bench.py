@@ -314,6 +314,26 @@ def main() -> int:
             dist.barrier()
         el = time.perf_counter() - t0
         kern_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev if e is not None]))
+    # A uniform channel (the recipe's constant G) is a constant tap with no
+    # loads ("_u" kernels).  For comparison, the same K
+    # frames with every channel loaded, timed after the main window (N = 1).
+    all_loaded = None
+    if world == 1 and not native and not args.spin and "_u" in r.kernel_variant:
+        skipped_variant = r.kernel_variant
+        r.set_option("uniform_skip", 0)
+        sharder.run_frames(args.warmup)
+        torch.cuda.synchronize()
+        ev2 = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               if i % ev_every == 0 else None for i in range(args.steps)]
+        t1 = time.perf_counter()
+        sharder.run_frames(args.steps, events=ev2)
+        torch.cuda.synchronize()
+        el2 = time.perf_counter() - t1
+        all_loaded = {"kernel": r.kernel_variant, "ms_per_step": round(el2 / args.steps * 1e3, 4),
+                      "kernel_ms_mean": round(float(np.mean([e[0].elapsed_time(e[1]) for e in ev2 if e is not None])), 5),
+                      "value": round(W * H * S * args.steps / el2 / 1e6, 3)}
+        r.set_option("uniform_skip", 1)
+        assert r.kernel_variant == skipped_variant
     tt = torch.tensor([el, kern_ms], dtype=torch.float64, device=red_dev)
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -331,24 +351,32 @@ def main() -> int:
     if rank == 0:
         ms_per_step = el / args.steps * 1e3
         value = W * H * S * args.steps / el / 1e6
-        gather = local_steps * BYTES_PER_STEP / (kern_ms * 1e-3) / 1e9
         variant = r.kernel_variant
+        # bytes a step must gather: 8 per tap whose channel is not uniform
+        umask = r.get_option("uniform_mask") if proc is None and "_u" in variant else 0
+        taps_loaded = 4 - bin(max(umask, 0)).count("1")
+        bytes_per_step = 8 * taps_loaded
+        gather = local_steps * bytes_per_step / (kern_ms * 1e-3) / 1e9
+        gather32 = local_steps * BYTES_PER_STEP / (kern_ms * 1e-3) / 1e9
         if proc is None and "corner8" not in variant and "cornerh" not in variant:
             roofline = {"bound": "hbm", "achieved": round(gather, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(gather / HBM_PEAK_GBS, 4), "traffic": None,
-                        "achieved_def": "32 B algorithmic gather per executed ray-step x steps per launch "
-                                        "/ mean march-kernel duration (HIP events on its stream)"}
+                        "achieved_def": f"{bytes_per_step} B algorithmic gather per executed ray-step (8 B per tap "
+                                        f"of a non-uniform channel; {4 - taps_loaded} uniform) x steps per launch "
+                                        "/ mean march-kernel duration (HIP events on its stream)",
+                        **({"frac_32B": round(gather32 / HBM_PEAK_GBS, 4)} if taps_loaded < 4 else {})}
         elif proc is None:
             # cache-resident volume (cornerh / corner8 are auto only when they
             # fit the Infinity Cache): the march is VALU-bound (VALUBusy ~100 %,
             # profiles/r01_pmc/c8_4k.json), so the roofline is fp32 VALU
             fps = FLOP_PER_STEP_CORNERH if "cornerh" in variant else FLOP_PER_STEP
+            fps -= (27 if "cornerh" in variant else 31) * (4 - taps_loaded)   # a uniform tap is a constant
             tf = local_steps * fps / (kern_ms * 1e-3) / 1e12
             roofline = {"bound": "valu", "achieved": round(tf, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                         "frac": round(tf / FP32_PEAK_TFLOPS, 4), "traffic": None,
-                        "achieved_def": f"{fps} algorithmic fp32 FLOP per executed ray-step x steps per "
-                                        "launch / mean march-kernel duration (HIP events on its stream); the volume "
-                                        "is cache-resident",
+                        "achieved_def": f"{fps} algorithmic fp32 FLOP per executed ray-step ({taps_loaded} "
+                                        "sampled taps) x steps per launch / mean march-kernel duration (HIP events "
+                                        "on its stream); the volume is cache-resident",
                         "gather_GBs": round(gather, 1)}
         else:
             cpe = local_cells / max(1, local_evals)
@@ -414,6 +442,7 @@ def main() -> int:
             "executed_steps_per_s": round(frame_steps * args.steps / el, 1),
             "kernel_ms_mean": round(kern_ms, 5),
             **({"host_ms_per_frame": round(host_el / args.steps * 1e3, 4)} if args.spin else {}),
+            **({"all_channels_loaded": all_loaded} if all_loaded else {}),
             "kernel_ms_mean_max_rank": round(kern_ms_max, 5),
             "roofline": dict(roofline, traffic=traffic,
                              **({"traffic_GBs": round(traffic / (kern_ms * 1e-3) / 1e9, 1),

@@ -72,7 +72,7 @@ def test_config1_perlin_cube_256_32(r, oracle):
 
 def test_reference_frame_1080p_128(r, oracle, vol128):
     img, ref, c, s = render_both(r, oracle, vol128, 1920, 1080)
-    assert r.kernel_variant.endswith("_clamp")
+    assert "_clamp" in r.kernel_variant   # the fast clamp path, not planar mirror
     assert_exact(img, ref)
     assert c == s
     assert 16_700_000 < s < 16_780_000  # 1.674e7 executed steps
@@ -183,7 +183,10 @@ def test_every_layout_bitexact(r, oracle, vol128, layout, name):
     r.set_layout_preference(layout)
     try:
         img, ref, c, s = render_both(r, oracle, vol128, 480, 270, osd, gsd)
-        assert r.kernel_variant == f"grid_{name}_clamp"
+        # the recipe's constant G (uniform_mask 2) skips its loads in the three regions kernels
+        um = r.get_option("uniform_mask")
+        suffix = "_uG" if um == 2 and name in ("col48", "brick4832", "cornerh") else ""
+        assert r.kernel_variant == f"grid_{name}_clamp{suffix}"
         assert_exact(img, ref)
         assert c == s
         # odd, non-power-of-two extents exercise the brick edges
@@ -232,6 +235,57 @@ def test_split_long_tiles_bitexact(r, oracle, vol128, layout):
         r.set_option("split_long", 0)
         r.set_option("split", 0)
         r.set_layout_preference(0)
+
+
+@pytest.mark.parametrize("layout", [15, 12, 14])
+def test_uniform_channel_skip_bitexact(r, oracle, layout):
+    """A channel whose texels are all equal (the reference recipe's G,
+    TestMain.cpp:60/76) is detected at install (vr_get_option "uniform_mask")
+    and its tap becomes the constant v/255 with no load -- exact, because the
+    spec's lerps of equal values return them.  Bit-exact with step counts for
+    each single uniform channel, with uniform_skip on and off, for the one-lane
+    march and the step-split march (split 2 and 4, banded), and for two uniform
+    channels (the general kernel)."""
+    rng = np.random.default_rng(layout)
+    base = rng.integers(0, 256, size=(40, 44, 36, 4), dtype=np.uint8)
+    r.set_layout_preference(layout)
+    try:
+        for mask in (1, 2, 4, 8, 2 | 8):
+            vol = base.copy()
+            for ch in range(4):
+                if mask >> ch & 1:
+                    vol[..., ch] = 17 + 40 * ch
+            r.set_volume(vol)
+            assert r.get_option("uniform_mask") == mask
+            osd, gsd = vr.reference_shader_data(16 / 9, 20.0, -15.0)
+            for skip in (1, 0):
+                r.set_option("uniform_skip", skip)
+                img, ref, c, s = render_both(r, oracle, vol, 320, 180, osd, gsd)
+                assert_exact(img, ref)
+                assert c == s
+                single = mask in (1, 2, 4, 8)
+                assert r.kernel_variant.endswith("_u" + "RGBA"[(mask & -mask).bit_length() - 1]) == (skip and single)
+            for split in (2, 4):
+                r.set_option("split", split)
+                img, ref, c, s = render_both(r, oracle, vol, 320, 180, osd, gsd, band_rows=16, band_stride=3,
+                                             band_first=1)
+                assert_exact(img, ref)
+                assert c == s
+            r.set_option("split", 0)
+    finally:
+        r.set_option("uniform_skip", 1)
+        r.set_option("split", 0)
+        r.set_layout_preference(0)
+
+
+def test_reference_recipe_green_channel_is_uniform(r):
+    """The recipe replicates TestMain.cpp:60 (the f=.03 grid written into
+    noiseOutput1), so noiseOutput2 stays zero and G is one constant byte
+    (SURVEY.md sec. 8 a8): the install finds channel G (bit 1) uniform."""
+    r.generate_volume(vr.volume_recipe_defaults(size=48))
+    assert r.get_option("uniform_mask") == 2
+    r.generate_volume(vr.volume_recipe_defaults(size=48, literal_overwrite=0))
+    assert r.get_option("uniform_mask") == 0
 
 
 @pytest.mark.parametrize("layout", [15, 12, 14])

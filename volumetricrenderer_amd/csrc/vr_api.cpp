@@ -71,6 +71,9 @@ struct Ctx {
     // volume (channel planes; see vr_internal.h Layout)
     int nx = 0, ny = 0, nz = 0;
     uint8_t* d_planar = nullptr;   // canonical planes (LAYOUT_PLANAR)
+    int uniform_mask = 0;          // channels whose every texel is uniform_val[c] (install_volume)
+    uint8_t uniform_val[4] = {};
+    int uniform_skip = 1;          // option "uniform_skip": 0 = load uniform channels anyway
     uint8_t* d_fast = nullptr;     // one fast layout, built from d_planar
     int fast_layout = 0;           // which one (0 = none)
     size_t fast_plane_bytes = 0;
@@ -163,6 +166,7 @@ void free_volume(Ctx* c)
     if (c->d_planar) (void)hipFree(c->d_planar);
     if (c->d_fast) (void)hipFree(c->d_fast);
     c->d_planar = c->d_fast = nullptr;
+    c->uniform_mask = 0;
     c->fast_layout = 0;
     c->fast_plane_bytes = 0;
     c->nx = c->ny = c->nz = 0;
@@ -215,6 +219,23 @@ vr_status install_volume(Ctx* c, const uint8_t* d_rgba, int nx, int ny, int nz, 
     HIP_TRY(hipMalloc(&c->d_planar, 4 * total));
     HIP_TRY(launch_repack(d_rgba, nx, ny, nz, c->d_planar, s));
     c->nx = nx; c->ny = ny; c->nz = nz;
+    // uniform channels: per-plane byte min / max, once per volume (synchronous)
+    unsigned* d_mm = nullptr;
+    HIP_TRY(hipMalloc(&d_mm, 8 * sizeof(unsigned)));
+    unsigned mm[8];
+    hipError_t e = hipMemsetAsync(d_mm, 0xff, 4 * sizeof(unsigned), s);
+    if (e == hipSuccess) e = hipMemsetAsync(d_mm + 4, 0, 4 * sizeof(unsigned), s);
+    if (e == hipSuccess) e = launch_plane_minmax(c->d_planar, (long long)total, d_mm, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(mm, d_mm, sizeof mm, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    (void)hipFree(d_mm);
+    HIP_TRY(e);
+    c->uniform_mask = 0;
+    for (int ch = 0; ch < 4; ++ch)
+        if (mm[ch] == mm[4 + ch]) {
+            c->uniform_mask |= 1 << ch;
+            c->uniform_val[ch] = (uint8_t)mm[ch];
+        }
     return ensure_fast_layout(c, s);
 }
 
@@ -734,6 +755,11 @@ vr_status vr_set_option(void* p, const char* name, int value)
         c->supertile = value;
         return VR_OK;
     }
+    if (n == "uniform_skip") {
+        if (value < 0 || value > 1) return fail(VR_ERR_INVALID, "vr_set_option: uniform_skip is 0 or 1");
+        c->uniform_skip = value;
+        return VR_OK;
+    }
     if (n == "sort_reuse") {
         if (value < 0 || value > 64) return fail(VR_ERR_INVALID, "vr_set_option: sort_reuse in [0, 64] renders");
         c->sort_reuse = value;
@@ -772,6 +798,8 @@ int vr_get_option(void* p, const char* name)
     if (n == "split_long") return c->split_long;
     if (n == "sort_reuse") return c->sort_reuse;
     if (n == "wg_waves") return c->wg_waves;
+    if (n == "uniform_skip") return c->uniform_skip;
+    if (n == "uniform_mask") return c->d_planar ? c->uniform_mask : -1;   // read-only
     if (n == "supertile") return c->supertile;
     return -1;
 }
@@ -792,6 +820,18 @@ const char* vr_kernel_variant(void* p)
     const int kind = c->schedule >= 0 ? c->schedule : SCHED_REGIONS;
     if (pl.layout == LAYOUT_COL48 && c->slab && kind == SCHED_REGIONS && c->split <= 1)
         return pl.early ? "grid_col48_slab_clamp_early" : "grid_col48_slab_clamp";
+    const int um = c->uniform_skip ? c->uniform_mask : 0;
+    if (kind == SCHED_REGIONS && !pl.early && a.zero_offsets && c->wg_waves == 4 && c->split_long == 0 &&
+        (um == 1 || um == 2 || um == 4 || um == 8)) {
+        // one uniform channel, no loads for it (launch_lw): "_u" + the channel
+        static std::string named[kNumLayouts][4];
+        const int ch = um == 1 ? 0 : um == 2 ? 1 : um == 4 ? 2 : 3;
+        if (pl.layout == LAYOUT_COL48 || pl.layout == LAYOUT_BRICK4832 || pl.layout == LAYOUT_CORNERH) {
+            std::string& n = named[pl.layout][ch];
+            if (n.empty()) n = std::string(variant_name(pl)) + "_u" + "RGBA"[ch];
+            return n.c_str();
+        }
+    }
     return variant_name(pl);
 }
 
@@ -1123,6 +1163,10 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
     Plan pl{LAYOUT_PLANAR, WRAP_CLAMP, false};
     if (!c->proc.enabled) make_plan(c, &a, &pl);
     a.nx = c->nx; a.ny = c->ny; a.nz = c->nz;
+    if (!c->proc.enabled && c->uniform_skip) {
+        a.umask = c->uniform_mask;
+        for (int ch = 0; ch < 4; ++ch) a.uval[ch] = (float)c->uniform_val[ch] * (1.0f / 255.0f);   // blend()'s scale
+    }
     if (pl.layout != LAYOUT_PLANAR) {
         a.vol = c->d_fast;
         a.plane_stride = (unsigned)c->fast_plane_bytes;

@@ -169,6 +169,12 @@ struct MarchArgs {
     // (= u*N + 0.5 with u = P*s_t + o_t, frag.glsl:66-69)
     float tap_S[4][3], tap_T[4][3];
     int zero_offsets;            // every tap_T is exactly 0.5 (no MediaScroll offsets)
+    // uniform channels (vr_api.cpp install_volume: min == max over the plane):
+    // bit t set = every texel of channel t is v_t, so tap t is exactly
+    // uval[t] = v_t * (1/255) (the spec's lerps of equal values return them,
+    // DESIGN.md sec. 3.2) and the march needs no load for it
+    int umask;
+    float uval[4];
     // volume
     int nx, ny, nz;
     const uint8_t* vol;          // channel plane 0; plane c at vol + c*plane_stride
@@ -212,6 +218,9 @@ struct Schedule {
 
 // launchers (vr_march.hip / vr_volume.hip); return hipError_t
 hipError_t launch_march(const MarchArgs& a, int layout, int wrap, bool early, const Schedule& sc, hipStream_t s);
+// per-plane byte min (mm[0..3]) and max (mm[4..7]) of the planar volume; mm
+// must hold 0xffffffff x 4 then 0 x 4 (atomicMin / atomicMax)
+hipError_t launch_plane_minmax(const uint8_t* d_planar, long long total, unsigned* mm, hipStream_t s);
 // bytes per pixel of a vr_format (include/vr.h), and the grey format of an RGBA one
 __host__ __device__ constexpr int format_bytes(int f) { return f == 0 ? 16 : f <= 2 ? 4 : f <= 4 ? 1 : 4; }
 __host__ __device__ constexpr int grey_of(int f) { return f == 0 ? 5 : f == 1 ? 3 : f == 2 ? 4 : -1; }

@@ -379,18 +379,36 @@ __device__ __forceinline__ void store_pixel(const MarchArgs& a, int x, int orow,
 #ifndef VR_PIPE
 #define VR_PIPE 1
 #endif
-template <int LAYOUT, int WRAP, bool EARLY, bool ZO = false>
+// Taps of a march with uniform channels UM (MarchArgs.umask): a uniform
+// channel's tap is the constant uv[T], with no load.
+template <int UM, int T, int LAYOUT, bool ZO>
+__device__ __forceinline__ TapRaw fetch_u(const MarchArgs& a, const FastCtx& f, f2 pxy, float pz)
+{
+    if constexpr ((UM >> T) & 1) return TapRaw{};
+    else return tap_fetch_at<LAYOUT, ZO>(a, f, T, pxy, pz);
+}
+template <int UM, int T, int LAYOUT>
+__device__ __forceinline__ float blend_u(const TapRaw& c, const float* uv)
+{
+    if constexpr ((UM >> T) & 1) return uv[T];
+    else return tap_blend<LAYOUT>(c);
+}
+template <int LAYOUT, int WRAP, bool EARLY, bool ZO = false, int UM = 0>
 __device__ __forceinline__ unsigned march_pixel(const MarchArgs& a, const FastCtx& f, int x, int orow)
 {
     const Ray r = setup_ray(a, x, orow);
+    float uv[4] = {};
+    if constexpr (UM != 0)
+        for (int t = 0; t < 4; ++t)
+            if ((UM >> t) & 1) uv[t] = noise::in_vgpr(a.uval[t]);
     if constexpr (VR_PIPE && LAYOUT != LAYOUT_PLANAR && LAYOUT != LAYOUT_CORNER8 && LAYOUT != LAYOUT_CORNERH) {
         f2 pxy = r.pxy;
         float pz = r.pz;
         float acc = 0.0f;
         int i = 0;
         if (r.n > 0) {
-            TapRaw c0 = tap_fetch_at<LAYOUT, ZO>(a, f, 0, pxy, pz), c1 = tap_fetch_at<LAYOUT, ZO>(a, f, 1, pxy, pz);
-            TapRaw c2 = tap_fetch_at<LAYOUT, ZO>(a, f, 2, pxy, pz), c3 = tap_fetch_at<LAYOUT, ZO>(a, f, 3, pxy, pz);
+            TapRaw c0 = fetch_u<UM, 0, LAYOUT, ZO>(a, f, pxy, pz), c1 = fetch_u<UM, 1, LAYOUT, ZO>(a, f, pxy, pz);
+            TapRaw c2 = fetch_u<UM, 2, LAYOUT, ZO>(a, f, pxy, pz), c3 = fetch_u<UM, 3, LAYOUT, ZO>(a, f, pxy, pz);
             for (; i < r.n; ++i) {
                 const f2 cxy = pxy;
                 const float cz = pz;
@@ -400,10 +418,10 @@ __device__ __forceinline__ unsigned march_pixel(const MarchArgs& a, const FastCt
                 const bool more = i + 1 < r.n;
                 const f2 qxy = more ? pxy : cxy;
                 const float qz = more ? pz : cz;
-                const TapRaw n0 = tap_fetch_at<LAYOUT, ZO>(a, f, 0, qxy, qz), n1 = tap_fetch_at<LAYOUT, ZO>(a, f, 1, qxy, qz);
-                const TapRaw n2 = tap_fetch_at<LAYOUT, ZO>(a, f, 2, qxy, qz), n3 = tap_fetch_at<LAYOUT, ZO>(a, f, 3, qxy, qz);
-                const float t0 = tap_blend<LAYOUT>(c0), t1 = tap_blend<LAYOUT>(c1);
-                const float t2 = tap_blend<LAYOUT>(c2), t3 = tap_blend<LAYOUT>(c3);
+                const TapRaw n0 = fetch_u<UM, 0, LAYOUT, ZO>(a, f, qxy, qz), n1 = fetch_u<UM, 1, LAYOUT, ZO>(a, f, qxy, qz);
+                const TapRaw n2 = fetch_u<UM, 2, LAYOUT, ZO>(a, f, qxy, qz), n3 = fetch_u<UM, 3, LAYOUT, ZO>(a, f, qxy, qz);
+                const float t0 = blend_u<UM, 0, LAYOUT>(c0, uv), t1 = blend_u<UM, 1, LAYOUT>(c1, uv);
+                const float t2 = blend_u<UM, 2, LAYOUT>(c2, uv), t3 = blend_u<UM, 3, LAYOUT>(c3, uv);
                 acc = acc + ((t0 * t1) * (t2 + t3)) * a.scale;                           // :71-73
                 c0 = n0; c1 = n1; c2 = n2; c3 = n3;
                 if constexpr (EARLY) {
@@ -424,10 +442,10 @@ __device__ __forceinline__ unsigned march_pixel(const MarchArgs& a, const FastCt
     for (; i < r.n; ++i) {
         float t0, t1, t2, t3;
         if constexpr (LAYOUT != LAYOUT_PLANAR) {
-            t0 = tap_blend<LAYOUT>(tap_fetch_at<LAYOUT, ZO>(a, f, 0, pxy, pz));
-            t1 = tap_blend<LAYOUT>(tap_fetch_at<LAYOUT, ZO>(a, f, 1, pxy, pz));
-            t2 = tap_blend<LAYOUT>(tap_fetch_at<LAYOUT, ZO>(a, f, 2, pxy, pz));
-            t3 = tap_blend<LAYOUT>(tap_fetch_at<LAYOUT, ZO>(a, f, 3, pxy, pz));
+            t0 = blend_u<UM, 0, LAYOUT>(fetch_u<UM, 0, LAYOUT, ZO>(a, f, pxy, pz), uv);
+            t1 = blend_u<UM, 1, LAYOUT>(fetch_u<UM, 1, LAYOUT, ZO>(a, f, pxy, pz), uv);
+            t2 = blend_u<UM, 2, LAYOUT>(fetch_u<UM, 2, LAYOUT, ZO>(a, f, pxy, pz), uv);
+            t3 = blend_u<UM, 3, LAYOUT>(fetch_u<UM, 3, LAYOUT, ZO>(a, f, pxy, pz), uv);
         } else {
             t0 = tap<LAYOUT, WRAP>(a, f, 0, pxy, pz);
             t1 = tap<LAYOUT, WRAP>(a, f, 1, pxy, pz);
@@ -870,7 +888,7 @@ __global__ __launch_bounds__(kThreads) void march_rings(const MarchArgs a, int c
 // (DESIGN.md sec. 5.3).  XCD = blockIdx % 8 is a speed-only assumption.
 // WGW waves per workgroup (option wg_waves): the waves of one workgroup run on
 // one CU and share its L1, and they render consecutive list entries.
-template <int LAYOUT, int WRAP, bool EARLY, bool ZO, int WGW = kThreads / 64>
+template <int LAYOUT, int WRAP, bool EARLY, bool ZO, int WGW = kThreads / 64, int UM = 0>
 __global__ __launch_bounds__(64 * WGW) void march_regions(const MarchArgs a, const unsigned* __restrict__ tiles,
                                                          const TileMap m)
 {
@@ -888,7 +906,8 @@ __global__ __launch_bounds__(64 * WGW) void march_regions(const MarchArgs a, con
     for (int k = w; w < m.nwx && k < count; k += m.nwx) {   // the grid rounds nwx up to whole workgroups
         const unsigned t = tiles[begin + k];
         const int tx = (int)(t & 0xffffu), ty = (int)(t >> 16);
-        steps += march_pixel<LAYOUT, WRAP, EARLY, ZO>(a, f, tx * 8 + lane_x<LAYOUT>(lane), ty * 8 + lane_y<LAYOUT>(lane));
+        steps += march_pixel<LAYOUT, WRAP, EARLY, ZO, UM>(a, f, tx * 8 + lane_x<LAYOUT>(lane),
+                                                          ty * 8 + lane_y<LAYOUT>(lane));
     }
 #ifdef VR_TIMELINE
     timeline_record(t_begin, steps);
@@ -908,12 +927,16 @@ __global__ __launch_bounds__(64 * WGW) void march_regions(const MarchArgs a, con
 // ray share n, so they loop, shuffle and stop together.  Lanes beyond the
 // last step fetch the ray's entry point (in the box) and their terms are not
 // added.
-template <int LAYOUT, bool EARLY, bool ZO, int K>
+template <int LAYOUT, bool EARLY, bool ZO, int K, int UM = 0>
 __device__ __forceinline__ unsigned march_pixel_split(const MarchArgs& a, const FastCtx& f, int x, int orow,
                                                       int k, int ray_lane)
 {
     constexpr int R = 64 / K;
     const Ray r = setup_ray(a, x, orow);
+    float uv[4] = {};
+    if constexpr (UM != 0)
+        for (int t = 0; t < 4; ++t)
+            if ((UM >> t) & 1) uv[t] = noise::in_vgpr(a.uval[t]);
     const int n = r.n;
     f2 pxy = r.pxy;
     float pz = r.pz;
@@ -922,19 +945,19 @@ __device__ __forceinline__ unsigned march_pixel_split(const MarchArgs& a, const 
     int i = 0;
     if (n > 0) {
         const bool mine0 = k < n;
-        TapRaw c0 = tap_fetch_at<LAYOUT, ZO>(a, f, 0, mine0 ? pxy : r.pxy, mine0 ? pz : r.pz);
-        TapRaw c1 = tap_fetch_at<LAYOUT, ZO>(a, f, 1, mine0 ? pxy : r.pxy, mine0 ? pz : r.pz);
-        TapRaw c2 = tap_fetch_at<LAYOUT, ZO>(a, f, 2, mine0 ? pxy : r.pxy, mine0 ? pz : r.pz);
-        TapRaw c3 = tap_fetch_at<LAYOUT, ZO>(a, f, 3, mine0 ? pxy : r.pxy, mine0 ? pz : r.pz);
+        TapRaw c0 = fetch_u<UM, 0, LAYOUT, ZO>(a, f, mine0 ? pxy : r.pxy, mine0 ? pz : r.pz);
+        TapRaw c1 = fetch_u<UM, 1, LAYOUT, ZO>(a, f, mine0 ? pxy : r.pxy, mine0 ? pz : r.pz);
+        TapRaw c2 = fetch_u<UM, 2, LAYOUT, ZO>(a, f, mine0 ? pxy : r.pxy, mine0 ? pz : r.pz);
+        TapRaw c3 = fetch_u<UM, 3, LAYOUT, ZO>(a, f, mine0 ? pxy : r.pxy, mine0 ? pz : r.pz);
         for (int base = 0; base < n; base += K) {
             for (int j = 0; j < K; ++j) { pxy = pxy + r.sxy; pz = pz + r.sz; }   // step base + K + k
             const bool mine = base + K + k < n;
             const f2 qxy = mine ? pxy : r.pxy;
             const float qz = mine ? pz : r.pz;
-            const TapRaw n0 = tap_fetch_at<LAYOUT, ZO>(a, f, 0, qxy, qz), n1 = tap_fetch_at<LAYOUT, ZO>(a, f, 1, qxy, qz);
-            const TapRaw n2 = tap_fetch_at<LAYOUT, ZO>(a, f, 2, qxy, qz), n3 = tap_fetch_at<LAYOUT, ZO>(a, f, 3, qxy, qz);
-            const float t0 = tap_blend<LAYOUT>(c0), t1 = tap_blend<LAYOUT>(c1);
-            const float t2 = tap_blend<LAYOUT>(c2), t3 = tap_blend<LAYOUT>(c3);
+            const TapRaw n0 = fetch_u<UM, 0, LAYOUT, ZO>(a, f, qxy, qz), n1 = fetch_u<UM, 1, LAYOUT, ZO>(a, f, qxy, qz);
+            const TapRaw n2 = fetch_u<UM, 2, LAYOUT, ZO>(a, f, qxy, qz), n3 = fetch_u<UM, 3, LAYOUT, ZO>(a, f, qxy, qz);
+            const float t0 = blend_u<UM, 0, LAYOUT>(c0, uv), t1 = blend_u<UM, 1, LAYOUT>(c1, uv);
+            const float t2 = blend_u<UM, 2, LAYOUT>(c2, uv), t3 = blend_u<UM, 3, LAYOUT>(c3, uv);
             const float term = ((t0 * t1) * (t2 + t3)) * a.scale;                        // :71-73
             bool stop = false;
 #pragma unroll
@@ -963,7 +986,7 @@ __device__ __forceinline__ unsigned march_pixel_split(const MarchArgs& a, const 
 // rays (8x8, 8x4, 4x4, 4x2 pixels), one per wave; wave w of its XCD's nwx
 // renders the units (tile, sub-block) w, w + nwx, ...  Lane = k * (64/K) + ray,
 // so 4 adjacent lanes are a 2x2 pixel quad at the same step offset.
-template <int LAYOUT, bool EARLY, bool ZO, int K>
+template <int LAYOUT, bool EARLY, bool ZO, int K, int UM = 0>
 __global__ __launch_bounds__(kThreads) void march_regions_split(const MarchArgs a, const unsigned* __restrict__ tiles,
                                                                const TileMap m)
 {
@@ -984,7 +1007,7 @@ __global__ __launch_bounds__(kThreads) void march_regions_split(const MarchArgs 
         const unsigned t = tiles[begin + u / K];
         const int s = u % K;
         const int x = (int)(t & 0xffffu) * 8 + (s % NSX) * SW + px, orow = (int)(t >> 16) * 8 + (s / NSX) * SH + py;
-        steps += march_pixel_split<LAYOUT, EARLY, ZO, K>(a, f, x, orow, k, rho);
+        steps += march_pixel_split<LAYOUT, EARLY, ZO, K, UM>(a, f, x, orow, k, rho);
     }
 #ifdef VR_TIMELINE
     timeline_record(t_begin, steps);
@@ -1037,6 +1060,18 @@ template <int L, int K>
 void launch_regions_split(const MarchArgs& a, bool early, const Schedule& sc, dim3 grid, size_t lds, hipStream_t s)
 {
     const dim3 block(kThreads);
+    if constexpr (L == LAYOUT_COL48 || L == LAYOUT_BRICK4832 || L == LAYOUT_CORNERH) {
+        const int um = a.umask;   // one uniform channel: no loads for it (march_regions' launcher)
+        if (!early && a.zero_offsets && (um == 1 || um == 2 || um == 4 || um == 8)) {
+#define VR_UMS(U) hipLaunchKernelGGL((march_regions_split<L, false, true, K, U>), grid, block, lds, s, a, sc.tiles, sc.map)
+            if (um == 1) VR_UMS(1);
+            else if (um == 2) VR_UMS(2);
+            else if (um == 4) VR_UMS(4);
+            else VR_UMS(8);
+#undef VR_UMS
+            return;
+        }
+    }
     if (early && a.zero_offsets)
         hipLaunchKernelGGL((march_regions_split<L, true, true, K>), grid, block, lds, s, a, sc.tiles, sc.map);
     else if (early)
@@ -1400,6 +1435,21 @@ hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStre
     else hipLaunchKernelGGL((march_regions<L, W, false, false, G>), grid, blk, lds, s, a, sc.tiles, sc.map)
             if (g == 8) { VR_RW(8); } else { VR_RW(16); }
 #undef VR_RW
+            return hipGetLastError();
+        }
+    }
+    if constexpr (L == LAYOUT_COL48 || L == LAYOUT_BRICK4832 || L == LAYOUT_CORNERH) {
+        // one uniform channel (the reference recipe's G, TestMain.cpp:60/76):
+        // its loads are skipped; other masks run the general kernel (exact too)
+        const int um = a.umask;
+        if (sc.kind == SCHED_REGIONS && !early && a.zero_offsets && (um == 1 || um == 2 || um == 4 || um == 8)) {
+            const dim3 grid((unsigned)(8 * ((sc.map.nwx + 3) / 4)));
+#define VR_UM(U) hipLaunchKernelGGL((march_regions<L, W, false, true, kThreads / 64, U>), grid, block, lds, s, a, sc.tiles, sc.map)
+            if (um == 1) VR_UM(1);
+            else if (um == 2) VR_UM(2);
+            else if (um == 4) VR_UM(4);
+            else VR_UM(8);
+#undef VR_UM
             return hipGetLastError();
         }
     }

@@ -374,6 +374,49 @@ int grid_for(long long n)
 
 }  // namespace
 
+// Byte min / max of each plane (blockIdx.y = plane): grid-stride bytes, a
+// wave reduction, one atomicMin / atomicMax per wave.
+__global__ __launch_bounds__(kBlock) void k_plane_minmax(const uint8_t* __restrict__ planes, long long total,
+                                                         unsigned* __restrict__ mm)
+{
+    const uint8_t* pl = planes + (size_t)blockIdx.y * (size_t)total;
+    unsigned lo = 255u, hi = 0u;
+    // the 4-byte-aligned body as words, the rest as bytes
+    const long long mis = (long long)((4u - (unsigned)((uintptr_t)pl & 3u)) & 3u);
+    const long long head = mis < total ? mis : total;
+    const long long words = (total - head) / 4;
+    const unsigned* w = reinterpret_cast<const unsigned*>(pl + head);
+    const long long stride = (long long)gridDim.x * kBlock;
+    for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < words; i += stride) {
+        const unsigned v = w[i];
+        const unsigned b0 = v & 0xffu, b1 = (v >> 8) & 0xffu, b2 = (v >> 16) & 0xffu, b3 = v >> 24;
+        lo = min(lo, min(min(b0, b1), min(b2, b3)));
+        hi = max(hi, max(max(b0, b1), max(b2, b3)));
+    }
+    const long long tail0 = head + words * 4;
+    for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < head + (total - tail0); i += stride) {
+        const unsigned b = i < head ? pl[i] : pl[tail0 + (i - head)];
+        lo = min(lo, b);
+        hi = max(hi, b);
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        lo = min(lo, (unsigned)__shfl_xor((int)lo, off));
+        hi = max(hi, (unsigned)__shfl_xor((int)hi, off));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMin(&mm[blockIdx.y], lo);
+        atomicMax(&mm[4 + blockIdx.y], hi);
+    }
+}
+
+hipError_t launch_plane_minmax(const uint8_t* d_planar, long long total, unsigned* mm, hipStream_t s)
+{
+    long long g = (total / 4 + kBlock - 1) / kBlock;
+    g = g < 1 ? 1 : g > 1024 ? 1024 : g;
+    hipLaunchKernelGGL(k_plane_minmax, dim3((unsigned)g, 4), dim3(kBlock), 0, s, d_planar, total, mm);
+    return hipGetLastError();
+}
+
 hipError_t launch_repack(const uint8_t* d_rgba, int nx, int ny, int nz, uint8_t* d_planar, hipStream_t s)
 {
     const long long total = (long long)nx * ny * nz;
