@@ -33,9 +33,9 @@ def main():
                         stats = os.path.join(dp, fn)
         shutil.copy(stats, os.path.join(out, f"{tag}_{c}_kernel_stats.csv"))
         march = [r for r in csv.DictReader(open(stats)) if "march" in r["Name"]]
-        # a "_u<channel>" bench kernel (uniform channel skipped) is the march_regions
+        # a "_u<channel>" bench kernel (uniform channel skipped) is the march_regions_u
         # instance whose last template argument is that channel's bit; the bench's
-        # all-channels comparison run adds the ", 0>" instance to the same trace
+        # all-channels comparison run adds plain march_regions to the same trace
         variant = bench["config"].get("kernel", "")
         if "_u" in variant:
             bit = {"R": 1, "G": 2, "B": 4, "A": 8}[variant[-1]]

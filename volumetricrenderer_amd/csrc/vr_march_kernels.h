@@ -888,11 +888,10 @@ __global__ __launch_bounds__(kThreads) void march_rings(const MarchArgs a, int c
 // (DESIGN.md sec. 5.3).  XCD = blockIdx % 8 is a speed-only assumption.
 // WGW waves per workgroup (option wg_waves): the waves of one workgroup run on
 // one CU and share its L1, and they render consecutive list entries.
-template <int LAYOUT, int WRAP, bool EARLY, bool ZO, int WGW = kThreads / 64, int UM = 0>
-__global__ __launch_bounds__(64 * WGW) void march_regions(const MarchArgs a, const unsigned* __restrict__ tiles,
-                                                         const TileMap m)
+template <int LAYOUT, int WRAP, bool EARLY, bool ZO, int WGW, int UM>
+__device__ __forceinline__ void regions_body(const MarchArgs& a, const unsigned* __restrict__ tiles, const TileMap& m,
+                                             unsigned* lds)
 {
-    extern __shared__ __attribute__((aligned(16))) unsigned lds[];
     const int xcd = blockIdx.x & 7;
     const int w = (int)(blockIdx.x >> 3) * WGW + (threadIdx.x >> 6);
     const int begin = m.off[xcd], count = m.off[xcd + 1] - begin;
@@ -913,6 +912,24 @@ __global__ __launch_bounds__(64 * WGW) void march_regions(const MarchArgs a, con
     timeline_record(t_begin, steps);
 #endif
     if (a.step_counter) add_steps(a, steps);
+}
+template <int LAYOUT, int WRAP, bool EARLY, bool ZO, int WGW = kThreads / 64>
+__global__ __launch_bounds__(64 * WGW) void march_regions(const MarchArgs a, const unsigned* __restrict__ tiles,
+                                                         const TileMap m)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned lds[];
+    regions_body<LAYOUT, WRAP, EARLY, ZO, WGW, 0>(a, tiles, m, lds);
+}
+// with uniform channels UM (march_pixel's fetch_u / blend_u)
+#ifndef VR_UM_ATTR
+#define VR_UM_ATTR
+#endif
+template <int LAYOUT, int WRAP, bool EARLY, bool ZO, int UM>
+__global__ __launch_bounds__(kThreads) VR_UM_ATTR void march_regions_u(const MarchArgs a, const unsigned* __restrict__ tiles,
+                                                                      const TileMap m)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned lds[];
+    regions_body<LAYOUT, WRAP, EARLY, ZO, kThreads / 64, UM>(a, tiles, m, lds);
 }
 
 // ---- step-split rays (regions schedule) ----
@@ -1444,7 +1461,7 @@ hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStre
         const int um = a.umask;
         if (sc.kind == SCHED_REGIONS && !early && a.zero_offsets && (um == 1 || um == 2 || um == 4 || um == 8)) {
             const dim3 grid((unsigned)(8 * ((sc.map.nwx + 3) / 4)));
-#define VR_UM(U) hipLaunchKernelGGL((march_regions<L, W, false, true, kThreads / 64, U>), grid, block, lds, s, a, sc.tiles, sc.map)
+#define VR_UM(U) hipLaunchKernelGGL((march_regions_u<L, W, false, true, U>), grid, block, lds, s, a, sc.tiles, sc.map)
             if (um == 1) VR_UM(1);
             else if (um == 2) VR_UM(2);
             else if (um == 4) VR_UM(4);
