@@ -278,6 +278,25 @@ def test_uniform_channel_skip_bitexact(r, oracle, layout):
         r.set_layout_preference(0)
 
 
+@pytest.mark.parametrize("dims", [(13, 22, 9), (7, 5, 3), (64, 64, 64)])
+def test_uniform_detection_edges(r, dims):
+    """k_plane_minmax on planes that start off a 4-byte boundary (odd texel
+    counts) and tiny ones: a channel is uniform only if every byte is, so a
+    single different byte at the first or the last texel of the plane clears
+    its bit."""
+    rng = np.random.default_rng(sum(dims))
+    for ch in range(4):
+        vol = rng.integers(0, 256, size=tuple(reversed(dims)) + (4,), dtype=np.uint8)
+        vol[..., ch] = 200
+        r.set_volume(vol)
+        assert r.get_option("uniform_mask") == 1 << ch
+        for idx in ((0, 0, 0), (-1, -1, -1)):
+            v2 = vol.copy()
+            v2[idx + (ch,)] = 201
+            r.set_volume(v2)
+            assert r.get_option("uniform_mask") == 0, (ch, idx)
+
+
 def test_reference_recipe_green_channel_is_uniform(r):
     """The recipe replicates TestMain.cpp:60 (the f=.03 grid written into
     noiseOutput1), so noiseOutput2 stays zero and G is one constant byte
