@@ -14,7 +14,10 @@
  *
  * Threading: one vr_ctx per device and host thread.  Calls on one vr_ctx are
  * not reentrant.  vr_render is asynchronous on the given stream.  It does not
- * allocate or synchronise, so a caller may capture it in a hipGraph.
+ * allocate or synchronise, so a caller may capture it in a hipGraph -- except
+ * that the first vr_render after a volume install waits (host) for that
+ * install's uniform-channel scan (a few microseconds of GPU work queued with
+ * the install).
  */
 #ifndef VR_H
 #define VR_H
@@ -287,6 +290,11 @@ vr_status vr_set_layout_preference(void* ctx, int pref);
  *                     ray-steps plus the procedural shadow samples -- the unit
  *                     of the procedural roofline; 2 = the Worley cells those
  *                     evaluations computed.
+ *   "uniform_skip"    1 (default) = a channel whose texels all hold one byte value
+ *                     (found when the volume is installed; the reference recipe's
+ *                     G, TestMain.cpp:60) is sampled as the exact constant v/255
+ *                     with no loads; 0 = every channel is loaded.
+ *   "uniform_mask"    read-only (vr_get_option): bit c set = channel c uniform.
  *   "sort_reuse"      0-64, procedural sorted schedule: renders that may march
  *                     the cost order of an older camera (default 0).
  *   "proc_enum"       0/1, procedural sort with shadow rays: enumerate

@@ -73,6 +73,13 @@ struct Ctx {
     uint8_t* d_planar = nullptr;   // canonical planes (LAYOUT_PLANAR)
     int uniform_mask = 0;          // channels whose every texel is uniform_val[c] (install_volume)
     uint8_t uniform_val[4] = {};
+    // the install's per-plane min / max scan, read back asynchronously and
+    // resolved at first use (resolve_uniform): no host wait inside the install,
+    // so a collective volume share keeps its deadline (vr_shard.cpp)
+    unsigned* d_mm = nullptr;      // device [min x 4, max x 4]
+    unsigned* h_mm = nullptr;      // pinned copy
+    hipEvent_t mm_ready = nullptr;
+    bool mm_pending = false;
     int uniform_skip = 1;          // option "uniform_skip": 0 = load uniform channels anyway
     uint8_t* d_fast = nullptr;     // one fast layout, built from d_planar
     int fast_layout = 0;           // which one (0 = none)
@@ -163,6 +170,8 @@ Ctx* as_ctx(void* p) { return static_cast<Ctx*>(p); }
 
 void free_volume(Ctx* c)
 {
+    if (c->mm_pending) (void)hipEventSynchronize(c->mm_ready);   // the scan still reads d_planar
+    c->mm_pending = false;
     if (c->d_planar) (void)hipFree(c->d_planar);
     if (c->d_fast) (void)hipFree(c->d_fast);
     c->d_planar = c->d_fast = nullptr;
@@ -219,24 +228,34 @@ vr_status install_volume(Ctx* c, const uint8_t* d_rgba, int nx, int ny, int nz, 
     HIP_TRY(hipMalloc(&c->d_planar, 4 * total));
     HIP_TRY(launch_repack(d_rgba, nx, ny, nz, c->d_planar, s));
     c->nx = nx; c->ny = ny; c->nz = nz;
-    // uniform channels: per-plane byte min / max, once per volume (synchronous)
-    unsigned* d_mm = nullptr;
-    HIP_TRY(hipMalloc(&d_mm, 8 * sizeof(unsigned)));
-    unsigned mm[8];
-    hipError_t e = hipMemsetAsync(d_mm, 0xff, 4 * sizeof(unsigned), s);
-    if (e == hipSuccess) e = hipMemsetAsync(d_mm + 4, 0, 4 * sizeof(unsigned), s);
-    if (e == hipSuccess) e = launch_plane_minmax(c->d_planar, (long long)total, d_mm, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(mm, d_mm, sizeof mm, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-    (void)hipFree(d_mm);
-    HIP_TRY(e);
+    // uniform channels: per-plane byte min / max, once per volume, on `s`;
+    // read back into pinned memory and resolved at first use
+    if (!c->d_mm) HIP_TRY(hipMalloc(&c->d_mm, 8 * sizeof(unsigned)));
+    if (!c->h_mm) HIP_TRY(hipHostMalloc(&c->h_mm, 8 * sizeof(unsigned), hipHostMallocDefault));
+    if (!c->mm_ready) HIP_TRY(hipEventCreateWithFlags(&c->mm_ready, hipEventDisableTiming));
+    HIP_TRY(hipMemsetAsync(c->d_mm, 0xff, 4 * sizeof(unsigned), s));
+    HIP_TRY(hipMemsetAsync(c->d_mm + 4, 0, 4 * sizeof(unsigned), s));
+    HIP_TRY(launch_plane_minmax(c->d_planar, (long long)total, c->d_mm, s));
+    HIP_TRY(hipMemcpyAsync(c->h_mm, c->d_mm, 8 * sizeof(unsigned), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipEventRecord(c->mm_ready, s));
+    c->mm_pending = true;
+    return ensure_fast_layout(c, s);
+}
+
+// The uniform channels of the installed volume: waits (once per volume) for
+// the install's scan.  vr_render, vr_kernel_variant and vr_get_option call it.
+vr_status resolve_uniform(Ctx* c)
+{
+    if (!c->mm_pending) return VR_OK;
+    HIP_TRY(hipEventSynchronize(c->mm_ready));
+    c->mm_pending = false;
     c->uniform_mask = 0;
     for (int ch = 0; ch < 4; ++ch)
-        if (mm[ch] == mm[4 + ch]) {
+        if (c->h_mm[ch] == c->h_mm[4 + ch]) {
             c->uniform_mask |= 1 << ch;
-            c->uniform_val[ch] = (uint8_t)mm[ch];
+            c->uniform_val[ch] = (uint8_t)c->h_mm[ch];
         }
-    return ensure_fast_layout(c, s);
+    return VR_OK;
 }
 
 // Tap constants of spec v2: tap t samples padded texel
@@ -468,6 +487,9 @@ vr_status vr_destroy(void* p)
     if (c->d_sort) (void)hipFree(c->d_sort);
     (void)hipDeviceSynchronize();   // queued renders may still read the region lists
     if (c->d_lat) (void)hipFree(c->d_lat);
+    if (c->d_mm) (void)hipFree(c->d_mm);
+    if (c->h_mm) (void)hipHostFree(c->h_mm);
+    if (c->mm_ready) (void)hipEventDestroy(c->mm_ready);
     for (auto& b : c->region) {
         if (b.d) (void)hipFree(b.d);
         if (b.h) (void)hipHostFree(b.h);
@@ -782,7 +804,7 @@ vr_status vr_set_option(void* p, const char* name, int value)
 int vr_get_option(void* p, const char* name)
 {
     if (!p || !name) return -1;
-    const Ctx* c = as_ctx(p);
+    Ctx* c = as_ctx(p);
     const std::string n(name);
     if (n == "layout") return c->fast_layout ? c->fast_layout : LAYOUT_PLANAR;
     if (n == "schedule") return c->schedule;
@@ -799,7 +821,10 @@ int vr_get_option(void* p, const char* name)
     if (n == "sort_reuse") return c->sort_reuse;
     if (n == "wg_waves") return c->wg_waves;
     if (n == "uniform_skip") return c->uniform_skip;
-    if (n == "uniform_mask") return c->d_planar ? c->uniform_mask : -1;   // read-only
+    if (n == "uniform_mask") {   // read-only
+        if (!c->d_planar || resolve_uniform(c) != VR_OK) return -1;
+        return c->uniform_mask;
+    }
     if (n == "supertile") return c->supertile;
     return -1;
 }
@@ -814,6 +839,7 @@ const char* vr_kernel_variant(void* p)
         return c->proc.shadow_steps > 0 ? "procedural_shadow" : "procedural";
     }
     if (!c->d_planar || !c->has_camera) return "none";
+    if (resolve_uniform(c) != VR_OK) return "none";
     MarchArgs a{};
     Plan pl{};
     make_plan(c, &a, &pl);
@@ -1164,6 +1190,8 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
     if (!c->proc.enabled) make_plan(c, &a, &pl);
     a.nx = c->nx; a.ny = c->ny; a.nz = c->nz;
     if (!c->proc.enabled && c->uniform_skip) {
+        const vr_status us = resolve_uniform(c);
+        if (us != VR_OK) return us;
         a.umask = c->uniform_mask;
         for (int ch = 0; ch < 4; ++ch) a.uval[ch] = (float)c->uniform_val[ch] * (1.0f / 255.0f);   // blend()'s scale
     }
