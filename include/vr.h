@@ -246,7 +246,8 @@ const char* vr_kernel_variant(void* ctx);
  * ("brick4864"), 14 = per position the f16 pairs {a, b - a} of the four
  * footprint rows, one 16-B load and four v_fma_mix_f32 per tap ("cornerh";
  * volumes below 2^24 positions), 15 = columns of 4x8 texels through the
- * whole z extent, slices 32 B apart ("col48"; auto above 160 MiB).  Layouts 2-15 are
+ * whole z extent, slices 32 B apart ("col48"; auto above 160 MiB), 16 = col48
+ * for channels 0-2 and zpair for channel 3 ("col48z").  Layouts 2-16 are
  * used only where clamp-to-edge equals mirrored repeat.  Otherwise the
  * planar, mirrored-repeat kernel runs.  Rebuilds the layout (synchronous). */
 vr_status vr_set_layout_preference(void* ctx, int pref);

@@ -176,7 +176,8 @@ def test_media_scroll_mirrored_repeat(r, oracle, vol128):
 @pytest.mark.parametrize("layout,name", [(1, "planar"), (2, "brick5"), (3, "brick8"), (4, "brick16"), (5, "corner8"),
                                          (6, "brick4"), (7, "zpair"), (8, "brick448"),
                                          (9, "brick488"), (10, "brick4816"), (11, "brick41616"),
-                                         (12, "brick4832"), (13, "brick4864"), (14, "cornerh"), (15, "col48")])
+                                         (12, "brick4832"), (13, "brick4864"), (14, "cornerh"), (15, "col48"),
+                                         (16, "col48z")])
 def test_every_layout_bitexact(r, oracle, vol128, layout, name):
     osd, gsd = vr.reference_shader_data(16 / 9, 20.0, -35.0)
     r.set_volume(vol128)
@@ -185,7 +186,7 @@ def test_every_layout_bitexact(r, oracle, vol128, layout, name):
         img, ref, c, s = render_both(r, oracle, vol128, 480, 270, osd, gsd)
         # the recipe's constant G (uniform_mask 2) skips its loads in the three regions kernels
         um = r.get_option("uniform_mask")
-        suffix = "_uG" if um == 2 and name in ("col48", "brick4832", "cornerh") else ""
+        suffix = "_uG" if um == 2 and name in ("col48", "brick4832", "cornerh", "col48z") else ""
         assert r.kernel_variant == f"grid_{name}_clamp{suffix}"
         assert_exact(img, ref)
         assert c == s
@@ -237,7 +238,7 @@ def test_split_long_tiles_bitexact(r, oracle, vol128, layout):
         r.set_layout_preference(0)
 
 
-@pytest.mark.parametrize("layout", [15, 12, 14])
+@pytest.mark.parametrize("layout", [15, 12, 14, 16])
 def test_uniform_channel_skip_bitexact(r, oracle, layout):
     """A channel whose texels are all equal (the reference recipe's G,
     TestMain.cpp:60/76) is detected at install (vr_get_option "uniform_mask")

@@ -16,7 +16,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import volumetricrenderer_amd as vr  # noqa: E402
 
-NAMES = {1: "planar", 2: "brick5", 3: "brick8", 4: "brick16", 5: "corner8", 6: "brick4", 7: "zpair", 8: "brick448", 9: "brick488", 10: "brick4816", 11: "brick41616", 12: "brick4832", 13: "brick4864", 14: "cornerh", 15: "col48"}
+NAMES = {1: "planar", 2: "brick5", 3: "brick8", 4: "brick16", 5: "corner8", 6: "brick4", 7: "zpair", 8: "brick448", 9: "brick488", 10: "brick4816", 11: "brick41616", 12: "brick4832", 13: "brick4864", 14: "cornerh", 15: "col48", 16: "col48z"}
 
 
 def main():

@@ -198,6 +198,7 @@ int wanted_fast_layout(const Ctx* c)
     // 32-bit offsets inside the kernels: fall back to PAD16 if too large
     // and LDS offset tables of (nx+ny+nz+3) words: fall back to planar
     if (layout_plane_bytes(want, c->nx, c->ny, c->nz) >= (1ull << 31)) return 0;
+    if (want == LAYOUT_COL48Z && layout_plane_bytes(LAYOUT_ZPAIR, c->nx, c->ny, c->nz) >= (1ull << 31)) return 0;
     if ((size_t)(c->nx + c->ny + c->nz + 3) * 4 > 48 * 1024) return 0;
     return want;
 }
@@ -213,7 +214,7 @@ vr_status ensure_fast_layout(Ctx* c, hipStream_t s)
     c->fast_plane_bytes = 0;
     if (!want) return VR_OK;
     const size_t pb = layout_plane_bytes(want, c->nx, c->ny, c->nz);
-    HIP_TRY(hipMalloc(&c->d_fast, 4 * pb));
+    HIP_TRY(hipMalloc(&c->d_fast, layout_total_bytes(want, c->nx, c->ny, c->nz)));
     HIP_TRY(launch_build_layout(want, c->d_planar, c->nx, c->ny, c->nz, c->d_fast, s));
     c->fast_layout = want;
     c->fast_plane_bytes = pb;
@@ -349,6 +350,7 @@ const char* variant_name(const Plan& p)
         {"grid_brick4864_clamp", "grid_brick4864_clamp_early"},
         {"grid_cornerh_clamp", "grid_cornerh_clamp_early"},
         {"grid_col48_clamp", "grid_col48_clamp_early"},
+        {"grid_col48z_clamp", "grid_col48z_clamp_early"},
     };
     if (p.layout == LAYOUT_PLANAR && p.wrap == WRAP_MIRROR)
         return p.early ? "grid_planar_mirror_early" : "grid_planar_mirror";
@@ -852,7 +854,8 @@ const char* vr_kernel_variant(void* p)
         // one uniform channel, no loads for it (launch_lw): "_u" + the channel
         static std::string named[kNumLayouts][4];
         const int ch = um == 1 ? 0 : um == 2 ? 1 : um == 4 ? 2 : 3;
-        if (pl.layout == LAYOUT_COL48 || pl.layout == LAYOUT_BRICK4832 || pl.layout == LAYOUT_CORNERH) {
+        if (pl.layout == LAYOUT_COL48 || pl.layout == LAYOUT_BRICK4832 || pl.layout == LAYOUT_CORNERH ||
+            pl.layout == LAYOUT_COL48Z) {
             std::string& n = named[pl.layout][ch];
             if (n.empty()) n = std::string(variant_name(pl)) + "_u" + "RGBA"[ch];
             return n.c_str();
@@ -1199,6 +1202,10 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
         a.vol = c->d_fast;
         a.plane_stride = (unsigned)c->fast_plane_bytes;
         a.geom = layout_geom(pl.layout, c->nx, c->ny, c->nz);
+        if (pl.layout == LAYOUT_COL48Z) {
+            a.geom3 = layout_geom(LAYOUT_ZPAIR, c->nx, c->ny, c->nz);
+            a.plane3_bytes = (unsigned)layout_plane_bytes(LAYOUT_ZPAIR, c->nx, c->ny, c->nz);
+        }
     } else {
         a.vol = c->d_planar;
         a.plane_stride = (unsigned)((size_t)c->nx * c->ny * c->nz);
@@ -1279,7 +1286,7 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
     if (kind == SCHED_RINGS || kind == SCHED_REGIONS) box_centre_pixel(c, a, &sc.center_x, &sc.center_y);
     if (kind == SCHED_REGIONS) {
         const bool splittable = is_b4_family(pl.layout) || pl.layout == LAYOUT_ZPAIR || pl.layout == LAYOUT_CORNER8 ||
-                                pl.layout == LAYOUT_CORNERH;
+                                pl.layout == LAYOUT_CORNERH || pl.layout == LAYOUT_COL48Z;
         const bool mixable = !sc.slab && (pl.layout == LAYOUT_COL48 || pl.layout == LAYOUT_BRICK4832 ||
                                           pl.layout == LAYOUT_CORNERH);   // march_regions_mixed instances
         const vr_status st = build_regions(c, a, tpw, sc.center_x, sc.center_y, mixable,

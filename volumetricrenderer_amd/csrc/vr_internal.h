@@ -53,8 +53,11 @@ enum Layout : int {
                              // without z bricks, so any run of slices of a column is
                              // contiguous -- the fill unit of the LDS slab march
                              // (vr_march_slab.hip); also a plain BRICK4-family layout
+    LAYOUT_COL48Z = 16,      // channels 0-2 as COL48, channel 3 as ZPAIR (one 16-B load per
+                             // tap): the reference's smallest-scale tap (A at 0.7,
+                             // frag.glsl:69) trades 1.9x its bytes for half its loads
 };
-constexpr int kNumLayouts = 16;
+constexpr int kNumLayouts = 17;
 // CORNERH's fp32 index a + (nx+1)(b + (ny+1)c) is exact below 2^24 positions
 constexpr long long kCornerHMaxPositions = 1ll << 24;
 // the layouts whose taps are BRICK4's two dword-aligned 8-B loads
@@ -85,7 +88,7 @@ __host__ __device__ inline LayoutGeom layout_geom(int layout, int nx, int ny, in
         g.B = 1; g.R = 1; g.brick = 16;
     } else if (layout == LAYOUT_ZPAIR) {
         g.B = 3; g.R = 4; g.brick = 128;
-    } else if (layout == LAYOUT_COL48) {
+    } else if (layout == LAYOUT_COL48 || layout == LAYOUT_COL48Z) {
         // slices c and c + 1 for every padded position c in [0, nz]: nz + 2
         // slices, rounded up to an even count (64-B chunks of two slices)
         g.B = 3; g.R = 4;
@@ -111,7 +114,7 @@ __host__ __device__ inline LayoutGeom layout_geom(int layout, int nx, int ny, in
     if (layout == LAYOUT_BRICK4864) { g.Ba[1] = 7; g.Rn[1] = 8; g.Ba[2] = 63; g.Rn[2] = 64; }
     if (layout == LAYOUT_BRICK4832) { g.Ba[1] = 7; g.Rn[1] = 8; g.Ba[2] = 31; g.Rn[2] = 32; }
     if (layout == LAYOUT_BRICK41616) { g.Ba[1] = g.Ba[2] = 15; g.Rn[1] = g.Rn[2] = 16; }
-    if (layout == LAYOUT_COL48) { g.Ba[1] = 7; g.Rn[1] = 8; g.Ba[2] = nz + 1; g.Rn[2] = (nz + 3) & ~1; }
+    if (layout == LAYOUT_COL48 || layout == LAYOUT_COL48Z) { g.Ba[1] = 7; g.Rn[1] = 8; g.Ba[2] = nz + 1; g.Rn[2] = (nz + 3) & ~1; }
     // padded base positions a in [0, N] -> bricks a / B in [0, N / B]
     g.nbx = nx / g.Ba[0] + 1;
     g.nby = ny / g.Ba[1] + 1;
@@ -175,6 +178,9 @@ struct MarchArgs {
     // DESIGN.md sec. 3.2) and the march needs no load for it
     int umask;
     float uval[4];
+    // COL48Z: channel 3's ZPAIR plane (geometry, bytes) after the three COL48 planes
+    LayoutGeom geom3;
+    unsigned plane3_bytes;
     // volume
     int nx, ny, nz;
     const uint8_t* vol;          // channel plane 0; plane c at vol + c*plane_stride
@@ -246,6 +252,8 @@ hipError_t launch_repack(const uint8_t* d_rgba, int nx, int ny, int nz, uint8_t*
 hipError_t launch_build_layout(int layout, const uint8_t* d_planar, int nx, int ny, int nz, uint8_t* d_out,
                                hipStream_t s);
 size_t layout_plane_bytes(int layout, int nx, int ny, int nz);
+// bytes of all four planes of a fast layout (COL48Z's planes differ in size)
+size_t layout_total_bytes(int layout, int nx, int ny, int nz);
 hipError_t launch_unpack(const uint8_t* d_planar, int nx, int ny, int nz, uint8_t* d_rgba,
                          hipStream_t s);
 // Perlin lattice table: entry (x, y, z) - lo of n^3 = noise::perlin_lattice_entry(seed, x, y, z)

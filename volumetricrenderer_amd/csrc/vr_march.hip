@@ -116,6 +116,7 @@ hipError_t launch_march(const MarchArgs& a, int layout, int wrap, bool early, co
     case LAYOUT_COL48:
         if (sc.kind == SCHED_REGIONS && sc.slab && sc.split <= 1) return launch_march_slab(a, early, sc, s);
         return launch_lw<LAYOUT_COL48, WRAP_CLAMP>(a, early, sc, s);
+    case LAYOUT_COL48Z: return launch_lw<LAYOUT_COL48Z, WRAP_CLAMP>(a, early, sc, s);
     case LAYOUT_ZPAIR: return launch_lw<LAYOUT_ZPAIR, WRAP_CLAMP>(a, early, sc, s);
     case LAYOUT_BRICK5: return launch_lw<LAYOUT_BRICK5, WRAP_CLAMP>(a, early, sc, s);
     case LAYOUT_BRICK8: return launch_lw<LAYOUT_BRICK8, WRAP_CLAMP>(a, early, sc, s);

@@ -91,6 +91,9 @@ struct FastCtx {
     const unsigned* tx;
     const unsigned* ty;
     const unsigned* tz;
+    const unsigned* tx3;   // COL48Z: channel 3's ZPAIR offset tables (a second set in LDS)
+    const unsigned* ty3;
+    const unsigned* tz3;
     float s1x16, s2x16;   // CORNERH: 16 (nx+1), 16 (nx+1)(ny+1) (byte strides of y, z)
     // CORNERH: the z tap constants and the sample scale pinned to VGPRs (an fp32
     // op reading an SGPR issues at ~4.1 instead of ~2.2 cycles, sec. 5.5)
@@ -381,16 +384,29 @@ __device__ __forceinline__ void store_pixel(const MarchArgs& a, int x, int orow,
 #endif
 // Taps of a march with uniform channels UM (MarchArgs.umask): a uniform
 // channel's tap is the constant uv[T], with no load.
+// COL48Z: taps 0-2 are COL48's, tap 3 ZPAIR's (its own tables and plane).
 template <int UM, int T, int LAYOUT, bool ZO>
 __device__ __forceinline__ TapRaw fetch_u(const MarchArgs& a, const FastCtx& f, f2 pxy, float pz)
 {
-    if constexpr ((UM >> T) & 1) return TapRaw{};
-    else return tap_fetch_at<LAYOUT, ZO>(a, f, T, pxy, pz);
+    if constexpr ((UM >> T) & 1) {
+        return TapRaw{};
+    } else if constexpr (LAYOUT == LAYOUT_COL48Z) {
+        if constexpr (T == 3) {
+            FastCtx g = f;
+            g.tx = f.tx3; g.ty = f.ty3; g.tz = f.tz3;
+            return tap_fetch_at<LAYOUT_ZPAIR, ZO>(a, g, T, pxy, pz);
+        } else {
+            return tap_fetch_at<LAYOUT_COL48, ZO>(a, f, T, pxy, pz);
+        }
+    } else {
+        return tap_fetch_at<LAYOUT, ZO>(a, f, T, pxy, pz);
+    }
 }
 template <int UM, int T, int LAYOUT>
 __device__ __forceinline__ float blend_u(const TapRaw& c, const float* uv)
 {
     if constexpr ((UM >> T) & 1) return uv[T];
+    else if constexpr (LAYOUT == LAYOUT_COL48Z) return tap_blend<T == 3 ? LAYOUT_ZPAIR : LAYOUT_COL48>(c);
     else return tap_blend<LAYOUT>(c);
 }
 template <int LAYOUT, int WRAP, bool EARLY, bool ZO = false, int UM = 0>
@@ -730,13 +746,13 @@ __device__ __forceinline__ unsigned march_pixel_proc_compact(const MarchArgs& a,
 template <int LAYOUT = 0>
 __device__ __forceinline__ int lane_x(int lane)
 {
-    if constexpr (LAYOUT == LAYOUT_BRICK5 || LAYOUT == LAYOUT_ZPAIR || is_b4_family(LAYOUT)) return ((lane >> 2) & 3) * 2 + (lane & 1);
+    if constexpr (LAYOUT == LAYOUT_BRICK5 || LAYOUT == LAYOUT_ZPAIR || LAYOUT == LAYOUT_COL48Z || is_b4_family(LAYOUT)) return ((lane >> 2) & 3) * 2 + (lane & 1);
     else return lane & 7;
 }
 template <int LAYOUT = 0>
 __device__ __forceinline__ int lane_y(int lane)
 {
-    if constexpr (LAYOUT == LAYOUT_BRICK5 || LAYOUT == LAYOUT_ZPAIR || is_b4_family(LAYOUT)) return (lane >> 4) * 2 + ((lane >> 1) & 1);
+    if constexpr (LAYOUT == LAYOUT_BRICK5 || LAYOUT == LAYOUT_ZPAIR || LAYOUT == LAYOUT_COL48Z || is_b4_family(LAYOUT)) return (lane >> 4) * 2 + ((lane >> 1) & 1);
     else return lane >> 3;
 }
 
@@ -785,6 +801,24 @@ __device__ __forceinline__ FastCtx fast_prologue(const MarchArgs& a, unsigned* l
             f.oz[c] = noise::in_vgpr(a.tap_T[c][2]);
         }
         f.scale = noise::in_vgpr(a.scale);
+    } else if constexpr (LAYOUT == LAYOUT_COL48Z) {
+        for (int c = 0; c < 4; ++c)
+            f.rsrc[c] = __builtin_amdgcn_make_buffer_rsrc((void*)(a.vol + (size_t)c * a.plane_stride), (short)0,
+                                                          (int)(c < 3 ? a.plane_stride : a.plane3_bytes), 0x00020000);
+        const int nx1 = a.nx + 1, ny1 = a.ny + 1, nz1 = a.nz + 1, n3 = nx1 + ny1 + nz1;
+        for (int i = threadIdx.x; i < 2 * n3; i += (int)blockDim.x) {
+            const int set = i >= n3, j = i - set * n3;
+            const int axis = j < nx1 ? 0 : j < nx1 + ny1 ? 1 : 2;
+            const int pos = axis == 0 ? j : axis == 1 ? j - nx1 : j - nx1 - ny1;
+            lds[i] = set ? axis_offset(a.geom3, LAYOUT_ZPAIR, axis, pos) : axis_offset(a.geom, LAYOUT_COL48, axis, pos);
+        }
+        __syncthreads();
+        f.tx = lds;
+        f.ty = lds + nx1;
+        f.tz = lds + nx1 + ny1;
+        f.tx3 = lds + n3;
+        f.ty3 = lds + n3 + nx1;
+        f.tz3 = lds + n3 + nx1 + ny1;
     } else if constexpr (LAYOUT != LAYOUT_PLANAR) {
         for (int c = 0; c < 4; ++c)
             f.rsrc[c] = __builtin_amdgcn_make_buffer_rsrc((void*)(a.vol + (size_t)c * a.plane_stride), (short)0,
@@ -1077,7 +1111,7 @@ template <int L, int K>
 void launch_regions_split(const MarchArgs& a, bool early, const Schedule& sc, dim3 grid, size_t lds, hipStream_t s)
 {
     const dim3 block(kThreads);
-    if constexpr (L == LAYOUT_COL48 || L == LAYOUT_BRICK4832 || L == LAYOUT_CORNERH) {
+    if constexpr (L == LAYOUT_COL48 || L == LAYOUT_BRICK4832 || L == LAYOUT_CORNERH || L == LAYOUT_COL48Z) {
         const int um = a.umask;   // one uniform channel: no loads for it (march_regions' launcher)
         if (!early && a.zero_offsets && (um == 1 || um == 2 || um == 4 || um == 8)) {
 #define VR_UMS(U) hipLaunchKernelGGL((march_regions_split<L, false, true, K, U>), grid, block, lds, s, a, sc.tiles, sc.map)
@@ -1388,7 +1422,8 @@ __global__ __launch_bounds__(kThreads) void march_proc_sorted(const MarchArgs a,
 template <int L, int W>
 hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStream_t s)
 {
-    const size_t lds = L == LAYOUT_PLANAR || L == LAYOUT_CORNERH ? 0 : (size_t)(a.nx + a.ny + a.nz + 3) * sizeof(unsigned);
+    const size_t lds = L == LAYOUT_PLANAR || L == LAYOUT_CORNERH ? 0
+                     : (size_t)(a.nx + a.ny + a.nz + 3) * sizeof(unsigned) * (L == LAYOUT_COL48Z ? 2 : 1);
     const dim3 block(kThreads);
     if (sc.kind == SCHED_STRIDED) {
         const int tiles = ((a.width + 7) >> 3) * ((a.out_rows + 7) >> 3);
@@ -1419,7 +1454,8 @@ hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStre
             hipLaunchKernelGGL((march_rings<L, W, false, false>), grid, block, lds, s, a, cx, cy, nw, npos);
         return hipGetLastError();
     }
-    if constexpr (is_b4_family(L) || L == LAYOUT_ZPAIR || L == LAYOUT_CORNER8 || L == LAYOUT_CORNERH) {
+    if constexpr (is_b4_family(L) || L == LAYOUT_ZPAIR || L == LAYOUT_CORNER8 || L == LAYOUT_CORNERH ||
+                  L == LAYOUT_COL48Z) {
         if (sc.kind == SCHED_REGIONS && sc.split > 1) {
             const dim3 grid((unsigned)(8 * ((sc.map.nwx + 3) / 4)));
             if (sc.split == 2) launch_regions_split<L, 2>(a, early, sc, grid, lds, s);
@@ -1455,7 +1491,7 @@ hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStre
             return hipGetLastError();
         }
     }
-    if constexpr (L == LAYOUT_COL48 || L == LAYOUT_BRICK4832 || L == LAYOUT_CORNERH) {
+    if constexpr (L == LAYOUT_COL48 || L == LAYOUT_BRICK4832 || L == LAYOUT_CORNERH || L == LAYOUT_COL48Z) {
         // one uniform channel (the reference recipe's G, TestMain.cpp:60/76):
         // its loads are skipped; other masks run the general kernel (exact too)
         const int um = a.umask;
@@ -1469,6 +1505,13 @@ hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStre
 #undef VR_UM
             return hipGetLastError();
         }
+#ifdef VR_UM_EXPERIMENT
+        if (sc.kind == SCHED_REGIONS && !early && a.zero_offsets && um == 10) {   // G and A (timing experiment)
+            const dim3 grid((unsigned)(8 * ((sc.map.nwx + 3) / 4)));
+            hipLaunchKernelGGL((march_regions_u<L, W, false, true, 10>), grid, block, lds, s, a, sc.tiles, sc.map);
+            return hipGetLastError();
+        }
+#endif
     }
     if (sc.kind == SCHED_REGIONS) {
         const dim3 grid((unsigned)(8 * ((sc.map.nwx + 3) / 4)));

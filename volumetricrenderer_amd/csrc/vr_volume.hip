@@ -52,10 +52,10 @@ struct PlaneSrc {
 template <int LAYOUT>
 __global__ __launch_bounds__(kBlock) void k_build_layout(const uint8_t* __restrict__ planar, int nx, int ny,
                                                          int nz, LayoutGeom g, long long plane_elems,
-                                                         long long plane_bytes, uint8_t* __restrict__ out)
+                                                         long long plane_bytes, uint8_t* __restrict__ out, int nch = 4)
 {
     const long long total_planar = (long long)nx * ny * nz;
-    for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < 4 * plane_elems;
+    for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < nch * plane_elems;
          i += (long long)gridDim.x * kBlock) {
         const int ch = (int)(i / plane_elems);
         const long long e = i - ch * plane_elems;
@@ -441,6 +441,13 @@ size_t layout_plane_bytes(int layout, int nx, int ny, int nz)
     return (b + 255) & ~(size_t)255;
 }
 
+size_t layout_total_bytes(int layout, int nx, int ny, int nz)
+{
+    if (layout == LAYOUT_COL48Z)   // three COL48 planes, then channel 3's ZPAIR plane
+        return 3 * layout_plane_bytes(LAYOUT_COL48, nx, ny, nz) + layout_plane_bytes(LAYOUT_ZPAIR, nx, ny, nz);
+    return 4 * layout_plane_bytes(layout, nx, ny, nz);
+}
+
 hipError_t launch_build_layout(int layout, const uint8_t* d_planar, int nx, int ny, int nz, uint8_t* d_out,
                                hipStream_t s)
 {
@@ -449,14 +456,22 @@ hipError_t launch_build_layout(int layout, const uint8_t* d_planar, int nx, int 
     const long long pb = (long long)layout_plane_bytes(layout, nx, ny, nz);
     const dim3 gr(grid_for(4 * elems)), b(kBlock);
     const long long rows = (long long)g.Rn[1] * g.Rn[2];
-    if (layout == LAYOUT_COL48) {
+    if (layout == LAYOUT_COL48 || layout == LAYOUT_COL48Z) {
+        const int nch = layout == LAYOUT_COL48Z ? 3 : 4;   // COL48Z: channel 3 is ZPAIR's, below
         // columns in z segments of 32 slices (1 KiB of a column: BRICK4832's stage)
         constexpr int kSeg = 32;
         const long long srows = (long long)g.Rn[1] * kSeg;
         const int run = (int)std::min<long long>(g.nbx, (kBrickStageBytes / srows - g.Rn[0] - 7) / g.Ba[0] + 1);
         const int runs_x = (g.nbx + run - 1) / run;
-        const dim3 gb((unsigned)(runs_x * g.nby), (unsigned)((g.Rn[2] + kSeg - 1) / kSeg), 4);   // last segment partial
+        const dim3 gb((unsigned)(runs_x * g.nby), (unsigned)((g.Rn[2] + kSeg - 1) / kSeg), nch);   // last segment partial
         hipLaunchKernelGGL(k_build_bricks, gb, b, 0, s, d_planar, nx, ny, nz, g, run, pb, kSeg, d_out);
+        if (layout == LAYOUT_COL48Z) {
+            const LayoutGeom gz = layout_geom(LAYOUT_ZPAIR, nx, ny, nz);
+            const long long ez = layout_elems(LAYOUT_ZPAIR, nx, ny, nz);
+            hipLaunchKernelGGL(k_build_layout<LAYOUT_ZPAIR>, dim3(grid_for(ez)), b, 0, s,
+                               d_planar + 3 * (long long)nx * ny * nz, nx, ny, nz, gz, ez,
+                               (long long)layout_plane_bytes(LAYOUT_ZPAIR, nx, ny, nz), d_out + 3 * pb, 1);
+        }
         return hipGetLastError();
     }
     if (layout != LAYOUT_CORNER8 && layout != LAYOUT_CORNERH && layout != LAYOUT_ZPAIR && g.brick % 16u == 0 &&
