@@ -296,6 +296,8 @@ vr_status vr_set_layout_preference(void* ctx, int pref);
  *                     G, TestMain.cpp:60) is sampled as the exact constant v/255
  *                     with no loads; 0 = every channel is loaded.
  *   "uniform_mask"    read-only (vr_get_option): bit c set = channel c uniform.
+ *   "region_work_tiles" read-only: 8x8 tiles with estimated work in the current
+ *                     region lists (what the auto split K is chosen from).
  *   "sort_reuse"      0-64, procedural sorted schedule: renders that may march
  *                     the cost order of an older camera (default 0).
  *   "proc_enum"       0/1, procedural sort with shadow rays: enumerate

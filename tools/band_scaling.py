@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--variants", default="-1:0:0", help="comma list of schedule:tiles_per_wave:split[:wedges]")
     ap.add_argument("--opt", action="append", default=[], help="vr option NAME=VALUE, set first")
     ap.add_argument("--ns", default="1,2,4,8")
+    ap.add_argument("--band-rows", type=int, default=16)
+    ap.add_argument("--all-ranks", action="store_true", help="time every rank's band set, report the slowest")
     a = ap.parse_args()
     W, H = a.width, a.height
     with vr.Renderer(0) as r:
@@ -46,16 +48,23 @@ def main():
                 r.set_option("wedges", wedges)
             base = None
             for n in [int(v) for v in a.ns.split(",")]:
-                band = dict(band_rows=16, band_stride=n, band_first=0)
-                out = r.alloc_target(W, H, 1, **band)
-                r.render(W, H, 1, out=out, **band)
-                ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.frames)]
-                for i in range(a.frames):
-                    ev[2 * i].record()
+                ts = []
+                for first in (range(n) if a.all_ranks else (0,)):
+                    band = dict(band_rows=a.band_rows, band_stride=n, band_first=first)
+                    out = r.alloc_target(W, H, 1, **band)
                     r.render(W, H, 1, out=out, **band)
-                    ev[2 * i + 1].record()
-                torch.cuda.synchronize()
-                t = float(np.median([ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(a.frames)]))
+                    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.frames)]
+                    for i in range(a.frames):
+                        ev[2 * i].record()
+                        r.render(W, H, 1, out=out, **band)
+                        ev[2 * i + 1].record()
+                    torch.cuda.synchronize()
+                    ts.append(float(np.median([ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(a.frames)])))
+                    if a.all_ranks:
+                        print(f"    N={n} rank {first}: region_work_tiles {r.get_option('region_work_tiles')}", flush=True)
+                t = max(ts)
+                if a.all_ranks:
+                    print(f"  N={n} band_rows {a.band_rows}: per-rank ms " + " ".join(f"{v:.4f}" for v in ts), flush=True)
                 base = base or t
                 print(f"{' '.join(a.opt)} schedule {sched} tpw {tpw} split {split} wedges {wedges} N={n}: rank-0 bands {t:.4f} ms, whole/N {base / n:.4f} ms, "
                       f"efficiency {base / n / t:.2f}", flush=True)

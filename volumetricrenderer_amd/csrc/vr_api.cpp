@@ -823,6 +823,8 @@ int vr_get_option(void* p, const char* name)
     if (n == "sort_reuse") return c->sort_reuse;
     if (n == "wg_waves") return c->wg_waves;
     if (n == "uniform_skip") return c->uniform_skip;
+    if (n == "region_work_tiles")   // read-only: tiles with estimated work in the current region lists
+        return c->region_cur >= 0 ? c->region[c->region_cur].nwork : -1;
     if (n == "uniform_mask") {   // read-only
         if (!c->d_planar || resolve_uniform(c) != VR_OK) return -1;
         return c->uniform_mask;
