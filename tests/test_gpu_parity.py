@@ -665,6 +665,72 @@ def test_procedural_shadow_region_enumeration(r, oracle):
         r.set_option("proc_enum", 0)
 
 
+DEFER_CASES = [
+    (128, 72, dict(max_steps=128), dict(shadow_steps=8), {}),
+    (96, 64, dict(max_steps=96, density=400.0, early_out=0.01), dict(shadow_steps=5, sun_dir=(-1.0, 0.5, 0.25)), {}),
+    (96, 64, dict(max_steps=48, density=3.0), dict(shadow_steps=21, sun_dir=(0.3, -1.0, 2.0)), {}),
+    (96, 64, dict(max_steps=48, density=3.0), dict(shadow_steps=8, sun_dir=(0.0, 0.0, -1.0)), {}),
+    (96, 64, dict(max_steps=48, density=3.0), dict(shadow_steps=1, octaves=6, gain=0.6), {}),
+    (200, 150, dict(max_steps=64), dict(shadow_steps=8), dict(band_rows=16, band_stride=3, band_first=1)),
+    (1, 1, dict(max_steps=64), dict(shadow_steps=8), {}),
+    (67, 9, dict(max_steps=64), dict(shadow_steps=8), {}),
+]
+
+
+@pytest.mark.parametrize("case", range(len(DEFER_CASES)))
+def test_procedural_shadow_deferred(r, oracle, case):
+    """Deferred shadow rays (option "shadow_defer": primary march appends
+    (P, coefficient) entries, one thread per entry sums its sun samples, a
+    resolve pass folds them per ray in step order): bit-exact against the
+    oracle and equal to the in-wave compaction, with step counts (count 0),
+    density evaluations (count 1) and Worley cells (count 2); shadow runs
+    longer than the compaction's limit, early-out, zero sun components, bands
+    and frames smaller than a wave."""
+    W, H, m, kw, band = DEFER_CASES[case]
+    march = vr.march_defaults(**m)
+    imgs, counts = [], []
+    try:
+        for defer in (1, 0):
+            r.set_option("shadow_defer", defer)
+            img, ref, c, s, var = render_proc_both(r, oracle, W, H, march, band=band, **kw)
+            assert var == "procedural_shadow"
+            assert_exact(img, ref)
+            assert c == s
+            imgs.append(img)
+            cc = []
+            for cm in (1, 2):
+                r.set_option("count", cm)
+                img2, _, c2, _, _ = render_proc_both(r, oracle, W, H, march, band=band, **kw)
+                cc.append(c2)
+                assert np.array_equal(img2, img)
+            r.set_option("count", 0)
+            counts.append(cc)
+    finally:
+        r.set_option("shadow_defer", 0)
+        r.set_option("count", 0)
+    assert np.array_equal(imgs[0], imgs[1])
+    assert counts[0] == counts[1]
+
+
+def test_procedural_shadow_deferred_stale_and_reuse(r, oracle):
+    """The deferred passes with a reused sort order (background fill blocks)
+    and a stale one (option sort_reuse: leftover pixels marched inline by the
+    trailing blocks), over a spinning camera: exact every frame."""
+    W, H = 160, 90
+    march = vr.march_defaults(max_steps=64)
+    r.set_option("shadow_defer", 1)
+    r.set_option("sort_reuse", 2)
+    try:
+        for k, phi in enumerate([20.0, 20.0, 21.6, 23.2, 24.8, 24.8]):
+            osd, gsd = vr.reference_shader_data(W / H, phi, 15.0)
+            img, ref, c, s, _ = render_proc_both(r, oracle, W, H, march, osd=osd, gsd=gsd, shadow_steps=8)
+            assert_exact(img, ref)
+            assert c == s, k
+    finally:
+        r.set_option("shadow_defer", 0)
+        r.set_option("sort_reuse", 0)
+
+
 @pytest.mark.parametrize("kw", [dict(octaves=1, seed_fbm=11), dict(octaves=6, gain=0.6, worley_freq=0.05),
                                 dict(shadow_steps=3, sun_dir=(0.0, 1.0, 0.0)),
                                 dict(shadow_steps=16, sun_dir=(-1.0, 0.5, 0.25)),

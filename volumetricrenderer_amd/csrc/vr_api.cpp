@@ -100,6 +100,11 @@ struct Ctx {
                                    // 2 = Worley cells computed (procedural)
     void* d_sort = nullptr;        // procedural cost-sort scratch (proc_sort_bytes), grown on demand
     size_t sort_bytes = 0;
+    // deferred shadow rays (option "shadow_defer", vr_internal.h ShadowDefer):
+    // counter, per-wave step counts and records, entries; grown on demand
+    int shadow_defer = 0;
+    void* d_defer = nullptr;
+    size_t defer_bytes = 0;
     // regions schedule (build_regions): per-XCD tile lists, double-buffered
     // so a rebuild never waits for more than the render that last used the
     // other buffer (2 frames in flight, VulkanRenderer.cpp:13)
@@ -487,6 +492,7 @@ vr_status vr_destroy(void* p)
     free_volume(c);
     if (c->d_heads) (void)hipFree(c->d_heads);
     if (c->d_sort) (void)hipFree(c->d_sort);
+    if (c->d_defer) (void)hipFree(c->d_defer);
     (void)hipDeviceSynchronize();   // queued renders may still read the region lists
     if (c->d_lat) (void)hipFree(c->d_lat);
     if (c->d_mm) (void)hipFree(c->d_mm);
@@ -753,6 +759,11 @@ vr_status vr_set_option(void* p, const char* name, int value)
         c->proc_enum = value;
         return VR_OK;
     }
+    if (n == "shadow_defer") {
+        if (value < 0 || value > 1) return fail(VR_ERR_INVALID, "vr_set_option: shadow_defer is 0 or 1");
+        c->shadow_defer = value;
+        return VR_OK;
+    }
     if (n == "slab") {
         if (value < 0 || value > 1) return fail(VR_ERR_INVALID, "vr_set_option: slab is 0 or 1");
         c->slab = value;
@@ -818,6 +829,7 @@ int vr_get_option(void* p, const char* name)
     if (n == "lattice") return c->lattice;
     if (n == "slab") return c->slab;
     if (n == "proc_enum") return c->proc_enum;
+    if (n == "shadow_defer") return c->shadow_defer;
     if (n == "slab_cap") return c->slab_cap;
     if (n == "split_long") return c->split_long;
     if (n == "sort_reuse") return c->sort_reuse;
@@ -1124,6 +1136,48 @@ static vr_status ensure_lattice(Ctx* c, ProcParams* q, hipStream_t s)
     return VR_OK;
 }
 
+// Scratch of the deferred shadow passes (ShadowDefer) for this frame shape:
+// [chunk count | per-wave step counts, entry counts, first chunks | chunk map |
+// per-wave step records | per-wave entry regions].  A sorted wave marches at
+// most max_steps wave-steps and appends at most 64 entries per step, so its
+// region of 64 * max_steps entries cannot overflow (4.2 GB at 1080p x 128 on a
+// 288 GB device).
+constexpr size_t kMaxDeferBytes = 32ull << 30;
+static vr_status ensure_defer(Ctx* c, const MarchArgs& a, ShadowDefer* d)
+{
+    const size_t pixels = (size_t)a.width * (size_t)a.out_rows;
+    const size_t waves = (pixels + 255) / 256 * 4;   // the sorted march: 256-thread blocks of 4 waves
+    const size_t stride = (size_t)std::max(a.max_steps, 1);
+    auto up = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    const size_t off_ws = 256, off_wc = up(off_ws + waves * 4), off_wk = up(off_wc + waves * 4);
+    const size_t off_map = up(off_wk + waves * 4);
+    const size_t off_rec = up(off_map + waves * stride * sizeof(uint4));   // <= stride chunks per wave
+    const size_t off_ent = up(off_rec + waves * stride * sizeof(uint4));
+    const size_t need = off_ent + waves * 64 * stride * sizeof(float4);
+    if (waves * stride >= (1ull << 32) || need > kMaxDeferBytes)
+        return fail(VR_ERR_INVALID, "vr_render: shadow_defer scratch for %zu pixels x %d steps exceeds %zu GiB",
+                    pixels, a.max_steps, kMaxDeferBytes >> 30);
+    if (need > c->defer_bytes) {
+        HIP_TRY(hipDeviceSynchronize());   // queued work on another stream may still read the old one
+        if (c->d_defer) (void)hipFree(c->d_defer);
+        c->d_defer = nullptr;
+        c->defer_bytes = 0;
+        if (hipMalloc(&c->d_defer, need) != hipSuccess) return fail(VR_ERR_OOM, "vr_render: shadow_defer scratch");
+        c->defer_bytes = need;
+    }
+    char* b = static_cast<char*>(c->d_defer);
+    d->count = reinterpret_cast<unsigned*>(b);
+    d->wsteps = reinterpret_cast<unsigned*>(b + off_ws);
+    d->wcount = reinterpret_cast<unsigned*>(b + off_wc);
+    d->wchunk = reinterpret_cast<unsigned*>(b + off_wk);
+    d->map = reinterpret_cast<uint4*>(b + off_map);
+    d->rec = reinterpret_cast<uint4*>(b + off_rec);
+    d->ent = reinterpret_cast<float4*>(b + off_ent);
+    d->rec_stride = (unsigned)stride;
+    d->waves = (unsigned)waves;
+    return VR_OK;
+}
+
 vr_status vr_render(void* p, const vr_target* t, void* stream)
 {
     if (!p || !t) return fail(VR_ERR_INVALID, "vr_render: null argument");
@@ -1172,7 +1226,9 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
         for (int ax = 0; ax < 3; ++ax) q.lstep[ax] = (a.step_size * c->proc.sun_dir[ax]) / a.box_range[ax];
         q.od = a.step_size * m.density;
         q.count_evals = c->count;
-        q.enum_regions = c->proc_enum;
+        // deferred shadow rays need the sorted schedule and the fixed-geometry tables (checked below);
+        // they march the waves in 64x64-region order, like config 2
+        q.enum_regions = c->proc_enum || (c->shadow_defer && q.shadow_steps > 0);
         // Worley cell table (LDS): box points P in [0,1]^3 give cellular
         // coordinates in [0, G] per axis, G = grid_scale * worley_freq; the
         // 3x3x3 neighbourhood of rint() of those, with 2 cells of margin.
@@ -1271,9 +1327,17 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
                      std::memcmp(key.data(), c->sort_key.data(), kSortKeyGridPart * sizeof(float)) == 0)
                 reuse = SORT_STALE;
         }
+        ShadowDefer defer{};
+        const bool use_defer = sort_buf && c->shadow_defer && a.proc.shadow_steps > 0 && a.proc.wt_fixed &&
+                               a.proc.wt_n > 0;
+        if (use_defer) {
+            const vr_status st = ensure_defer(c, a, &defer);
+            if (st != VR_OK) return st;
+        }
         std::vector<float> built = reuse == SORT_BUILD ? key : c->sort_key;
         c->sort_key.clear();   // valid again only once this launch is queued
-        HIP_TRY(launch_march_procedural(a, m.early_out > 0.0f, sort_buf, reuse, sc, static_cast<hipStream_t>(stream)));
+        HIP_TRY(launch_march_procedural(a, m.early_out > 0.0f, sort_buf, reuse, sc, static_cast<hipStream_t>(stream),
+                                        use_defer ? &defer : nullptr));
         c->sort_key = std::move(built);
         c->renders_since_sort = reuse == SORT_STALE ? c->renders_since_sort + 1 : 0;
         return VR_OK;

@@ -222,6 +222,19 @@ struct Schedule {
     int wg_waves;          // regions (one lane per ray): waves per workgroup, 4 (default), 8 or 16
 };
 
+// Deferred shadow rays (vr_march_kernels.h march_proc_defer): device scratch
+struct ShadowDefer {
+    unsigned* count;      // [0]: chunks of 64 entries this frame (written by proc_shadow_scan)
+    unsigned* wsteps;     // per sorted wave: wave-steps marched
+    unsigned* wcount;     // per sorted wave: entries appended (dense in the wave's own region)
+    unsigned* wchunk;     // per sorted wave: its first chunk (exclusive prefix of ceil(wcount / 64))
+    uint4* map;           // per chunk: {wave, chunk of the wave, entries in it, 0}
+    uint4* rec;           // per sorted wave, rec_stride per wave: {wave-local first entry, lane mask lo, hi, 0}
+    float4* ent;          // entries (P, coef), region of wave w at w * 64 * rec_stride; pass 2 rewrites .xy as (coef, tl)
+    unsigned rec_stride;  // wave-steps per wave: max_steps bounds them
+    unsigned waves;       // sorted waves the scratch holds
+};
+
 // launchers (vr_march.hip / vr_volume.hip); return hipError_t
 hipError_t launch_march(const MarchArgs& a, int layout, int wrap, bool early, const Schedule& sc, hipStream_t s);
 // per-plane byte min (mm[0..3]) and max (mm[4..7]) of the planar volume; mm
@@ -245,7 +258,9 @@ constexpr int kSlabMaxChunks = 32;   // per channel and wave (64 B each): 8 KiB 
 // with the same target (skip the sort passes, march the pixels it left out too)
 enum { SORT_BUILD = 0, SORT_REUSE = 1, SORT_STALE = 2 };
 hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_buf, int reuse_sort, const Schedule& sc,
-                                   hipStream_t s);
+                                   hipStream_t s, const ShadowDefer* defer = nullptr);
+// blocks of the deferred shadow pass (proc_shadow_eval): a grid-stride loop over the chunks
+constexpr unsigned kShadowEvalBlocks = 256 * 6;
 size_t proc_sort_bytes(int width, int out_rows);
 hipError_t launch_repack(const uint8_t* d_rgba, int nx, int ny, int nz, uint8_t* d_planar, hipStream_t s);
 // Build a fast layout from the planar planes.

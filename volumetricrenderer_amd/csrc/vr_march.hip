@@ -24,7 +24,7 @@ size_t proc_sort_bytes(int width, int out_rows)
 }
 
 hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_buf, int reuse_sort, const Schedule& sc,
-                                   hipStream_t s)
+                                   hipStream_t s, const ShadowDefer* defer)
 {
     if (a.width <= 0 || a.out_rows <= 0) return hipSuccess;
     const bool shadow = a.proc.shadow_steps > 0;
@@ -56,6 +56,26 @@ hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_bu
         // tables: 2 = the fixed 9-cell Worley geometry (compile-time offsets), 1 = runtime geometry,
         // 3 = 2 + the Perlin lattice table
         const int tm = wt_bytes ? (a.proc.wt_fixed ? (a.proc.lat ? 3 : 2) : 1) : 0;
+        if (shadow && defer && tm >= 2) {   // deferred shadow rays: three passes (vr_march_kernels.h)
+            const ShadowDefer d = *defer;
+            const bool stale = reuse_sort == SORT_STALE;
+#define VR_PD(E, T)                                                                                                  \
+    do {                                                                                                             \
+        hipLaunchKernelGGL((march_proc_defer<E, T>), g4, dim3(kThreads), wt_bytes, s, a, order, total, keys,        \
+                           positions, march_blocks, stale, d);                                                       \
+        hipLaunchKernelGGL(proc_shadow_scan, dim3(1), dim3(kScanThreads), 0, s, total, d);                          \
+        hipLaunchKernelGGL(proc_shadow_map, dim3((d.waves + 3) / 4), dim3(kThreads), 0, s, total, d);               \
+        hipLaunchKernelGGL((proc_shadow_eval<T>), dim3(kShadowEvalBlocks), dim3(kThreads), wt_bytes, s, a, d);      \
+    } while (0)
+            if (tm == 3) {
+                if (early) VR_PD(true, 3); else VR_PD(false, 3);
+            } else {
+                if (early) VR_PD(true, 2); else VR_PD(false, 2);
+            }
+#undef VR_PD
+            hipLaunchKernelGGL(proc_shadow_resolve, dim3(march_blocks), dim3(kThreads), 0, s, a, order, total, d);
+            return hipGetLastError();
+        }
         const int v = (shadow ? 4 : 0) | (early ? 2 : 0);
 #define VR_PS(S, E, T) \
     hipLaunchKernelGGL((march_proc_sorted<S, E, T>), g4, dim3(kThreads), wt_bytes, s, a, order, total, keys, positions, \

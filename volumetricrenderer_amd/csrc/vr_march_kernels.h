@@ -1419,6 +1419,223 @@ __global__ __launch_bounds__(kThreads) void march_proc_sorted(const MarchArgs a,
     if (a.step_counter) add_steps(a, steps);
 }
 
+// ---- deferred shadow rays (config 3; vr option "shadow_defer") ----
+// The compaction above deals a wave's shadow samples over its own lanes at
+// every primary step, so each step ends in a partial round (lane use ~0.85)
+// and pays the dealing (box scan, ballot prefix, LDS round trips).  Deferred,
+// the frame runs in passes instead:
+//  1. march_proc_defer: the primary march of the sorted waves (config 2's loop,
+//     64x64-region enumeration).  At a step with rho > 0 a lane appends the
+//     entry (P, tv * (rho * od)) -- its ray point and the coefficient the
+//     single-scatter term multiplies by the sun transmittance -- to its wave's
+//     own region (a running count, no atomics: one device-scope counter for
+//     all waves saturates at ~88 adds/us, MI355X_MICROARCH.md, and ran the
+//     frame at 3.7 ms), and the wave records {first entry, lane mask} per step.
+//  2. proc_shadow_scan / proc_shadow_map: the waves' entries in chunks of 64,
+//     numbered across the frame: chunk -> (wave, chunk of the wave, count).
+//  3. proc_shadow_eval: one lane per entry walks the S sun samples
+//     P + (j+1) L (sequential adds) and sums the in-box densities in step
+//     order, tl = exp(-(sl * od)); it rewrites the entry as (coef, tl).  Lanes
+//     are busy whatever the owner rays (one partial chunk per wave).
+//  4. proc_shadow_resolve: the sorted waves again; a lane folds
+//     rad = fma(coef, tl, rad) over its entries in step order and stores the
+//     pixel.
+// Every value is computed by the same ops in the same order as
+// march_pixel_proc<true>, so the frame stays bit-exact.
+// (struct ShadowDefer: vr_internal.h)
+__device__ __forceinline__ float4* defer_region(const ShadowDefer& d, unsigned w)
+{
+    return d.ent + (size_t)w * 64u * d.rec_stride;
+}
+
+template <bool EARLY, int TABLE>
+__global__ __launch_bounds__(kThreads) void march_proc_defer(const MarchArgs a, const unsigned* __restrict__ order,
+                                                             const unsigned* __restrict__ total_ptr,
+                                                             const unsigned short* __restrict__ keys,
+                                                             unsigned fill_positions, unsigned fill_first, int stale,
+                                                             ShadowDefer d)
+{
+    extern __shared__ float4 wt_lds[];
+    if (blockIdx.x >= fill_first) {   // as march_proc_sorted: background, or a stale order's leftovers
+        if (!stale) {
+            proc_fill_background(a, keys, fill_positions, blockIdx.x - fill_first, gridDim.x - fill_first);
+            return;
+        }
+        const float4* wt = worley_table<TABLE>(a.proc, wt_lds);
+        unsigned long long steps = 0;
+        const unsigned blocks = gridDim.x - fill_first;
+        for (unsigned i = (blockIdx.x - fill_first) * kThreads + threadIdx.x; i < fill_positions; i += blocks * kThreads) {
+            int x, orow;
+            if (sort_pixel(a, i, &x, &orow) && keys[i] == 0) steps += march_pixel_proc<true, EARLY, TABLE>(a, wt, x, orow);
+        }
+        if (a.step_counter) add_steps(a, steps);
+        return;
+    }
+    const float4* wt = worley_table<TABLE>(a.proc, wt_lds);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const unsigned total = *total_ptr;
+    const unsigned wid = blockIdx.x * (kThreads / 64) + wave;
+    const unsigned base = wid * 64u;
+    if (base >= total) return;   // wave-uniform
+    const unsigned idx = base + lane;
+    Ray r{};
+    r.n = -1;
+    if (idx < total) {
+        const unsigned pk = order[idx];
+        r = setup_ray(a, (int)(pk & 0xffffu), (int)(pk >> 16));
+    }
+    const ProcParams& p = a.proc;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    uint4* rec = d.rec + (size_t)wid * d.rec_stride;
+    float4* ent = defer_region(d, wid);
+    float P0 = r.pxy.x, P1 = r.pxy.y, P2 = r.pz;
+    float acc = 0.0f, tv = 1.0f;
+    int i = 0;
+    bool act = r.n > 0;
+    unsigned cells = 0, s = 0, b = 0;   // b: entries the wave appended so far (wave-uniform)
+    for (;;) {
+        act = act && i < r.n;
+        if (__ballot(act) == 0) break;
+        float rho = 0.0f;
+        if (act) rho = proc_density<TABLE>(p, wt, a.scale, P0, P1, P2, cells);
+        const bool need = act && rho > 0.0f;
+        const unsigned long long m = __ballot(need);
+        if (need) ent[b + (unsigned)__popcll(m & lt)] = make_float4(P0, P1, P2, tv * (rho * p.od));
+        if (lane == 0) rec[s] = make_uint4(b, (unsigned)m, (unsigned)(m >> 32), 0u);
+        b += (unsigned)__popcll(m);
+        ++s;
+        if (act) {
+            acc = acc + rho;
+            tv = spec_expf(-(acc * p.od));
+            P0 = P0 + r.sxy.x; P1 = P1 + r.sxy.y; P2 = P2 + r.sz;
+            ++i;
+            if constexpr (EARLY) {
+                if (acc > a.acc_limit) act = false;
+            }
+        }
+    }
+    if (lane == 0) {
+        d.wsteps[wid] = s;
+        d.wcount[wid] = b;
+    }
+    if (a.step_counter) add_steps(a, p.count_evals == 2 ? cells : r.n > 0 ? (unsigned)i : 0u);
+}
+
+// Exclusive prefix of the waves' chunk counts (one workgroup; waves past the
+// frame's sorted total count 0) and the frame's chunk total in count[0].
+constexpr int kScanThreads = 1024;
+[[maybe_unused]] __global__ __launch_bounds__(kScanThreads) void proc_shadow_scan(const unsigned* __restrict__ total_ptr,
+                                                                                  ShadowDefer d)
+{
+    __shared__ unsigned sc[kScanThreads];
+    const int t = threadIdx.x;
+    const unsigned nw = min((*total_ptr + 63u) / 64u, d.waves);
+    const unsigned per = (nw + kScanThreads - 1) / kScanThreads;
+    const unsigned w0 = min((unsigned)t * per, nw), w1 = min(w0 + per, nw);
+    unsigned own = 0;
+    for (unsigned w = w0; w < w1; ++w) own += (d.wcount[w] + 63u) / 64u;
+    sc[t] = own;
+    __syncthreads();
+    for (int off = 1; off < kScanThreads; off <<= 1) {
+        const unsigned v = t >= off ? sc[t - off] : 0u;
+        __syncthreads();
+        sc[t] += v;
+        __syncthreads();
+    }
+    unsigned c = sc[t] - own;
+    for (unsigned w = w0; w < w1; ++w) {
+        d.wchunk[w] = c;
+        c += (d.wcount[w] + 63u) / 64u;
+    }
+    if (t == kScanThreads - 1) d.count[0] = sc[t];
+}
+
+// chunk -> (wave, chunk of the wave, entries): one wave per sorted wave.
+[[maybe_unused]] __global__ __launch_bounds__(kThreads) void proc_shadow_map(const unsigned* __restrict__ total_ptr,
+                                                                             ShadowDefer d)
+{
+    const unsigned w = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+    const unsigned lane = threadIdx.x & 63;
+    if (w >= min((*total_ptr + 63u) / 64u, d.waves)) return;
+    const unsigned n = d.wcount[w], c0 = d.wchunk[w];
+    for (unsigned k = lane; k * 64u < n; k += 64u) d.map[c0 + k] = make_uint4(w, k, min(64u, n - k * 64u), 0u);
+}
+
+template <int TABLE>
+__global__ __launch_bounds__(kThreads) void proc_shadow_eval(const MarchArgs a, ShadowDefer d)
+{
+    extern __shared__ float4 wt_lds[];
+    const float4* wt = worley_table<TABLE>(a.proc, wt_lds);
+    const ProcParams& p = a.proc;
+    const unsigned chunks = *d.count;
+    const int S = p.shadow_steps;
+    const unsigned lane = threadIdx.x & 63;
+    const float l0 = noise::in_vgpr(p.lstep[0]), l1 = noise::in_vgpr(p.lstep[1]), l2 = noise::in_vgpr(p.lstep[2]);
+    unsigned evals = 0, cells = 0;
+    for (unsigned c = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6); c < chunks; c += gridDim.x * (kThreads / 64)) {
+        const uint4 mc = d.map[c];   // wave-uniform
+        if (lane >= mc.z) continue;
+        float4* e = defer_region(d, mc.x) + mc.y * 64u + lane;
+        const float4 en = *e;
+        float q0 = en.x, q1 = en.y, q2 = en.z, sl = 0.0f;
+        for (int j = 0; j < S; ++j) {
+            q0 = q0 + l0; q1 = q1 + l1; q2 = q2 + l2;
+            // march_pixel_proc's box test as min3 / max3 (q is never NaN)
+            if (fminf(fminf(q0, q1), q2) >= 0.0f && fmaxf(fmaxf(q0, q1), q2) <= 1.0f) {
+                sl = sl + proc_density<TABLE>(p, wt, a.scale, q0, q1, q2, cells);
+                ++evals;
+            }
+        }
+        const float tl = spec_expf(-(sl * p.od));
+        *reinterpret_cast<float2*>(e) = make_float2(en.w, tl);
+    }
+    if (a.step_counter) add_steps(a, p.count_evals == 2 ? cells : p.count_evals ? evals : 0u);
+}
+
+// Loads of entries in flight per lane in the resolve pass (the fold itself is
+// a serial fma chain; the loads are independent).  The step records are
+// wave-uniform (scalar loads); each batch costs two dependent round trips.
+constexpr int kResolveBatch = 32;
+[[maybe_unused]] __global__ __launch_bounds__(kThreads) void proc_shadow_resolve(const MarchArgs a, const unsigned* __restrict__ order,
+                                                                const unsigned* __restrict__ total_ptr, ShadowDefer d)
+{
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const unsigned total = *total_ptr;
+    const unsigned wid = __builtin_amdgcn_readfirstlane(blockIdx.x * (kThreads / 64) + wave);
+    const unsigned base = wid * 64u;
+    if (base >= total) return;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    const uint4* rec = d.rec + (size_t)wid * d.rec_stride;
+    const float4* ent = defer_region(d, wid);
+    const unsigned ns = d.wsteps[wid];
+    float rad = 0.0f;
+    for (unsigned s0 = 0; s0 < ns; s0 += kResolveBatch) {
+        float2 v[kResolveBatch];
+        bool h[kResolveBatch];
+#pragma unroll
+        for (int k = 0; k < kResolveBatch; ++k) {
+            h[k] = false;
+            v[k] = make_float2(0.0f, 0.0f);
+            if (s0 + k < ns) {
+                const uint4 rc = rec[s0 + k];
+                const unsigned long long m = ((unsigned long long)rc.z << 32) | rc.y;
+                h[k] = (m >> lane) & 1ull;
+                if (h[k]) v[k] = *reinterpret_cast<const float2*>(ent + rc.x + (unsigned)__popcll(m & lt));
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kResolveBatch; ++k)
+            if (h[k]) rad = fmaf(v[k].x, v[k].y, rad);
+    }
+    const unsigned idx = base + lane;
+    if (idx < total) {
+        const unsigned pk = order[idx];
+        const int x = (int)(pk & 0xffffu), orow = (int)(pk >> 16);
+        const Ray r = setup_ray(a, x, orow);
+        if (r.live) store_pixel(a, x, orow, r.n >= 0, rad);
+    }
+}
+
 template <int L, int W>
 hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStream_t s)
 {
