@@ -301,7 +301,16 @@ vr_status vr_set_layout_preference(void* ctx, int pref);
  *   "sort_reuse"      0-64, procedural sorted schedule: renders that may march
  *                     the cost order of an older camera (default 0).
  *   "proc_enum"       0/1, procedural sort with shadow rays: enumerate
- *                     64x64 regions (default 0, row-major).
+ *                     64x64 regions (default 0, row-major; the deferred
+ *                     shadow passes always enumerate regions).
+ *   "shadow_defer"    procedural medium with shadow rays, sorted schedule:
+ *                     1 (default) = the primary march appends its
+ *                     shadow-ray origins, one pass evaluates them all and a
+ *                     resolve pass folds them per ray in step order
+ *                     (device scratch of 16 B x 64 x max_steps per 64 rays,
+ *                     e.g. 4.2 GB at 1080p x 128, kept by the context);
+ *                     0 = each wave deals its own shadow samples at every
+ *                     step (at most 8 shadow steps).  Results are identical.
  *   "lattice"         procedural medium, sorted schedule: 1 = the fBm reads its
  *                     per-cell gradient-pair offsets from a lattice table in
  *                     global memory (the default; built when the seed or the

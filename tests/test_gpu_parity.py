@@ -706,7 +706,7 @@ def test_procedural_shadow_deferred(r, oracle, case):
             r.set_option("count", 0)
             counts.append(cc)
     finally:
-        r.set_option("shadow_defer", 0)
+        r.set_option("shadow_defer", 1)   # the default
         r.set_option("count", 0)
     assert np.array_equal(imgs[0], imgs[1])
     assert counts[0] == counts[1]
@@ -727,7 +727,7 @@ def test_procedural_shadow_deferred_stale_and_reuse(r, oracle):
             assert_exact(img, ref)
             assert c == s, k
     finally:
-        r.set_option("shadow_defer", 0)
+        r.set_option("shadow_defer", 1)
         r.set_option("sort_reuse", 0)
 
 

@@ -102,7 +102,7 @@ struct Ctx {
     size_t sort_bytes = 0;
     // deferred shadow rays (option "shadow_defer", vr_internal.h ShadowDefer):
     // counter, per-wave step counts and records, entries; grown on demand
-    int shadow_defer = 0;
+    int shadow_defer = 1;          // measured 1.25 -> 0.99 ms at config 3
     void* d_defer = nullptr;
     size_t defer_bytes = 0;
     // regions schedule (build_regions): per-XCD tile lists, double-buffered

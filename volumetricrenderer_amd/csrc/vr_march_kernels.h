@@ -1592,9 +1592,10 @@ __global__ __launch_bounds__(kThreads) void proc_shadow_eval(const MarchArgs a, 
     if (a.step_counter) add_steps(a, p.count_evals == 2 ? cells : p.count_evals ? evals : 0u);
 }
 
-// Loads of entries in flight per lane in the resolve pass (the fold itself is
-// a serial fma chain; the loads are independent).  The step records are
-// wave-uniform (scalar loads); each batch costs two dependent round trips.
+// Steps folded per batch in the resolve pass: lanes 0..31 load the batch's
+// step records with one vector load, v_readlane hands each record to the
+// wave, and every lane issues its entry loads back to back (the fold itself is
+// a serial fma chain; the loads are independent): two round trips per batch.
 constexpr int kResolveBatch = 32;
 [[maybe_unused]] __global__ __launch_bounds__(kThreads) void proc_shadow_resolve(const MarchArgs a, const unsigned* __restrict__ order,
                                                                 const unsigned* __restrict__ total_ptr, ShadowDefer d)
@@ -1610,18 +1611,19 @@ constexpr int kResolveBatch = 32;
     const unsigned ns = d.wsteps[wid];
     float rad = 0.0f;
     for (unsigned s0 = 0; s0 < ns; s0 += kResolveBatch) {
+        uint4 rc = make_uint4(0u, 0u, 0u, 0u);
+        if (lane < kResolveBatch && s0 + lane < ns) rc = rec[s0 + lane];
         float2 v[kResolveBatch];
         bool h[kResolveBatch];
 #pragma unroll
         for (int k = 0; k < kResolveBatch; ++k) {
-            h[k] = false;
+            // (readlane returns int: widen the low word unsigned, not sign-extended)
+            const unsigned bk = (unsigned)__builtin_amdgcn_readlane(rc.x, k);
+            const unsigned long long m = ((unsigned long long)(unsigned)__builtin_amdgcn_readlane(rc.z, k) << 32) |
+                                         (unsigned long long)(unsigned)__builtin_amdgcn_readlane(rc.y, k);
+            h[k] = (m >> lane) & 1ull;
             v[k] = make_float2(0.0f, 0.0f);
-            if (s0 + k < ns) {
-                const uint4 rc = rec[s0 + k];
-                const unsigned long long m = ((unsigned long long)rc.z << 32) | rc.y;
-                h[k] = (m >> lane) & 1ull;
-                if (h[k]) v[k] = *reinterpret_cast<const float2*>(ent + rc.x + (unsigned)__popcll(m & lt));
-            }
+            if (h[k]) v[k] = *reinterpret_cast<const float2*>(ent + bk + (unsigned)__popcll(m & lt));
         }
 #pragma unroll
         for (int k = 0; k < kResolveBatch; ++k)
