@@ -51,6 +51,8 @@ def derived(c):
 
 
 if __name__ == "__main__":
-    for tag in sys.argv[1:]:
-        c = load(tag)
-        print(tag, json.dumps({k: round(v, 4) for k, v in {**c, **derived(c)}.items()}, indent=0))
+    # TAG or TAG:KERNEL (substring of the kernel name; default "march")
+    for arg in sys.argv[1:]:
+        tag, _, kern = arg.partition(":")
+        c = load(tag, kern or "march")
+        print(arg, json.dumps({k: round(v, 4) for k, v in {**c, **derived(c)}.items()}, indent=0))
