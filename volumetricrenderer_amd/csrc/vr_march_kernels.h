@@ -743,16 +743,23 @@ __device__ __forceinline__ unsigned march_pixel_proc_compact(const MarchArgs& a,
 // u16 loads.  BRICK5's 12-byte loads are looked up per 4 lanes, and there 2x2
 // pixel quads (4x4 of them per tile) are 2.6 % faster at 512^3 than 4x1 rows
 // (neutral for the other layouts, 20 % slower for planar).
+#ifndef VR_LANEMAP
+#define VR_LANEMAP 0   // timing experiments: COL48 lanes 1 = 4x1 row quads, 2 = 1x4 column quads
+#endif
 template <int LAYOUT = 0>
 __device__ __forceinline__ int lane_x(int lane)
 {
-    if constexpr (LAYOUT == LAYOUT_BRICK5 || LAYOUT == LAYOUT_ZPAIR || LAYOUT == LAYOUT_COL48Z || is_b4_family(LAYOUT)) return ((lane >> 2) & 3) * 2 + (lane & 1);
+    if constexpr (LAYOUT == LAYOUT_COL48 && VR_LANEMAP == 1) return lane & 7;
+    else if constexpr (LAYOUT == LAYOUT_COL48 && VR_LANEMAP == 2) return lane >> 3;
+    else if constexpr (LAYOUT == LAYOUT_BRICK5 || LAYOUT == LAYOUT_ZPAIR || LAYOUT == LAYOUT_COL48Z || is_b4_family(LAYOUT)) return ((lane >> 2) & 3) * 2 + (lane & 1);
     else return lane & 7;
 }
 template <int LAYOUT = 0>
 __device__ __forceinline__ int lane_y(int lane)
 {
-    if constexpr (LAYOUT == LAYOUT_BRICK5 || LAYOUT == LAYOUT_ZPAIR || LAYOUT == LAYOUT_COL48Z || is_b4_family(LAYOUT)) return (lane >> 4) * 2 + ((lane >> 1) & 1);
+    if constexpr (LAYOUT == LAYOUT_COL48 && VR_LANEMAP == 1) return lane >> 3;
+    else if constexpr (LAYOUT == LAYOUT_COL48 && VR_LANEMAP == 2) return lane & 7;
+    else if constexpr (LAYOUT == LAYOUT_BRICK5 || LAYOUT == LAYOUT_ZPAIR || LAYOUT == LAYOUT_COL48Z || is_b4_family(LAYOUT)) return (lane >> 4) * 2 + ((lane >> 1) & 1);
     else return lane >> 3;
 }
 
