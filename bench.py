@@ -379,6 +379,7 @@ def main() -> int:
                                         "on its stream); the volume is cache-resident",
                         "gather_GBs": round(gather, 1)}
         else:
+            defer = shadow > 0 and r.get_option("shadow_defer") == 1
             cpe = local_cells / max(1, local_evals)
             fpd = flop_per_density(proc.octaves, cpe)
             fpd27 = flop_per_density(proc.octaves)
@@ -390,7 +391,10 @@ def main() -> int:
                                         f"{67 * proc.octaves} + pruned Worley at {cpe:.3f} cells per evaluation, "
                                         "measured with vr option count=2, + bound test, setup, rest) x "
                                         f"{local_evals} evaluations per launch / mean march-kernel duration "
-                                        "(HIP events on its stream); no volume is read",
+                                        "(HIP events on its stream); no volume is read" +
+                                        ("; with deferred shadow rays (vr option shadow_defer = 1) the frame is "
+                                         "five launches -- primary march, scan, chunk map, shadow pass, resolve "
+                                         "-- and the events bracket all of them" if defer else ""),
                         "worley_cells_per_eval": round(cpe, 4),
                         "flop_per_eval_27cell": fpd27,
                         "frac_27cell": round(a27 / FP32_PEAK_TFLOPS, 4)}
@@ -436,7 +440,9 @@ def main() -> int:
                        "camera": ("reference (TestMain.cpp:219-245), spinning: phi += 1.6 deg per frame, new shader "
                                   "data every frame (TestMain.cpp:171-184)" if args.spin
                                   else "reference (TestMain.cpp:219-245)"),
-                       "kernel": r.kernel_variant, "parallelism": f"bands16x{world}",
+                       "kernel": r.kernel_variant + ("_deferred" if proc is not None and shadow > 0
+                                                      and r.get_option("shadow_defer") == 1 else ""),
+                       "parallelism": f"bands16x{world}",
                        "collective": collective_label,
                        "executed_steps_per_frame": frame_steps},
             "executed_steps_per_s": round(frame_steps * args.steps / el, 1),

@@ -40,6 +40,19 @@ def main():
         if "_u" in variant:
             bit = {"R": 1, "G": 2, "B": 4, "A": 8}[variant[-1]]
             march = [r for r in march if f", {bit}>(" in r["Name"]] or march
+        if variant.endswith("_deferred"):
+            # deferred shadow rays: a frame is five launches; their mean durations add up
+            # to what the bench's events bracket
+            passes = [r for r in csv.DictReader(open(stats))
+                      if any(k in r["Name"] for k in ("march_proc_defer", "proc_shadow_scan", "proc_shadow_map",
+                                                       "proc_shadow_eval", "proc_shadow_resolve"))]
+            parts = ", ".join(f"{r['Name'].split('(')[0].split('::')[-1]} {float(r['AverageNs']) / 1e6:.4f}"
+                              for r in passes)
+            tot = sum(float(r["AverageNs"]) for r in passes) / 1e6
+            print(f"{c:13s} bench {bench['value']:>14,.1f} {bench['unit']}  kernel(events) "
+                  f"{bench['kernel_ms_mean']:.4f} ms  rocprof passes sum {tot:.4f} ms ({parts})  "
+                  f"roofline {bench['roofline']['frac']}")
+            continue
         top = max(march, key=lambda r: float(r["TotalDurationNs"]))
         # the timed launches only: the last `steps` dispatches of that kernel in the trace
         timed = ""
