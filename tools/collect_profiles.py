@@ -46,7 +46,7 @@ def main():
             passes = [r for r in csv.DictReader(open(stats))
                       if any(k in r["Name"] for k in ("march_proc_defer", "proc_shadow_scan", "proc_shadow_map",
                                                        "proc_shadow_eval", "proc_shadow_resolve"))]
-            parts = ", ".join(f"{r['Name'].split('(')[0].split('::')[-1]} {float(r['AverageNs']) / 1e6:.4f}"
+            parts = ", ".join(f"{r['Name'].split('namespace)::')[-1].split('(')[0]} {float(r['AverageNs']) / 1e6:.4f}"
                               for r in passes)
             tot = sum(float(r["AverageNs"]) for r in passes) / 1e6
             print(f"{c:13s} bench {bench['value']:>14,.1f} {bench['unit']}  kernel(events) "
