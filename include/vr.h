@@ -17,7 +17,11 @@
  * allocate or synchronise, so a caller may capture it in a hipGraph -- except
  * that the first vr_render after a volume install waits (host) for that
  * install's uniform-channel scan (a few microseconds of GPU work queued with
- * the install).
+ * the install), and the first procedural render of a
+ * larger target allocates the context's cost-sort scratch (with shadow rays
+ * also the deferred-shadow scratch, option "shadow_defer") after a device
+ * synchronisation.  That scratch belongs to the context: renders of one
+ * vr_ctx on different streams must not overlap (order them with events).
  */
 #ifndef VR_H
 #define VR_H
