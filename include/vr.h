@@ -315,6 +315,8 @@ vr_status vr_set_layout_preference(void* ctx, int pref);
  *                     e.g. 4.2 GB at 1080p x 128, kept by the context);
  *                     0 = each wave deals its own shadow samples at every
  *                     step (at most 8 shadow steps).  Results are identical.
+ *                     "shadow_blocks" 0-65536: workgroups of the deferred
+ *                     shadow pass (0 = auto, 3/8 of the sorted waves).
  *   "lattice"         procedural medium, sorted schedule: 1 = the fBm reads its
  *                     per-cell gradient-pair offsets from a lattice table in
  *                     global memory (the default; built when the seed or the

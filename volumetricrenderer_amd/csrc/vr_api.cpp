@@ -102,6 +102,7 @@ struct Ctx {
     size_t sort_bytes = 0;
     // deferred shadow rays (option "shadow_defer", vr_internal.h ShadowDefer):
     // counter, per-wave step counts and records, entries; grown on demand
+    int shadow_blocks = 0;         // option "shadow_blocks": workgroups of the deferred shadow pass (0 = auto)
     int shadow_defer = 1;          // measured 1.25 -> 0.99 ms at config 3
     void* d_defer = nullptr;
     size_t defer_bytes = 0;
@@ -759,6 +760,11 @@ vr_status vr_set_option(void* p, const char* name, int value)
         c->proc_enum = value;
         return VR_OK;
     }
+    if (n == "shadow_blocks") {
+        if (value < 0 || value > 65536) return fail(VR_ERR_INVALID, "vr_set_option: shadow_blocks in [0, 65536]");
+        c->shadow_blocks = value;
+        return VR_OK;
+    }
     if (n == "shadow_defer") {
         if (value < 0 || value > 1) return fail(VR_ERR_INVALID, "vr_set_option: shadow_defer is 0 or 1");
         c->shadow_defer = value;
@@ -830,6 +836,7 @@ int vr_get_option(void* p, const char* name)
     if (n == "slab") return c->slab;
     if (n == "proc_enum") return c->proc_enum;
     if (n == "shadow_defer") return c->shadow_defer;
+    if (n == "shadow_blocks") return c->shadow_blocks;
     if (n == "slab_cap") return c->slab_cap;
     if (n == "split_long") return c->split_long;
     if (n == "sort_reuse") return c->sort_reuse;
@@ -1175,6 +1182,12 @@ static vr_status ensure_defer(Ctx* c, const MarchArgs& a, ShadowDefer* d)
     d->ent = reinterpret_cast<float4*>(b + off_ent);
     d->rec_stride = (unsigned)stride;
     d->waves = (unsigned)waves;
+    // the shadow pass's grid: ~2-3 chunks per wave rather than one persistent
+    // round (1,536 workgroups at 6 per CU), so the hardware dispatcher balances
+    // the tail -- 3/8 of the sorted waves measured 0.90-0.91 ms against 0.98 at
+    // config 3 (profiles/r03/ab_shadow_blocks_*.txt)
+    d->eval_blocks = c->shadow_blocks ? (unsigned)c->shadow_blocks
+                                      : (unsigned)std::max<size_t>(kShadowEvalBlocks, waves * 3 / 8);
     return VR_OK;
 }
 

@@ -233,6 +233,7 @@ struct ShadowDefer {
     float4* ent;          // entries (P, coef), region of wave w at w * 64 * rec_stride; pass 2 rewrites .xy as (coef, tl)
     unsigned rec_stride;  // wave-steps per wave: max_steps bounds them
     unsigned waves;       // sorted waves the scratch holds
+    unsigned eval_blocks; // workgroups of the shadow pass (0 = kShadowEvalBlocks)
 };
 
 // launchers (vr_march.hip / vr_volume.hip); return hipError_t
@@ -259,7 +260,8 @@ constexpr int kSlabMaxChunks = 32;   // per channel and wave (64 B each): 8 KiB 
 enum { SORT_BUILD = 0, SORT_REUSE = 1, SORT_STALE = 2 };
 hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_buf, int reuse_sort, const Schedule& sc,
                                    hipStream_t s, const ShadowDefer* defer = nullptr);
-// blocks of the deferred shadow pass (proc_shadow_eval): a grid-stride loop over the chunks
+// blocks of the deferred shadow pass (proc_shadow_eval), at least: a grid-stride loop over
+// the chunks (vr_api.cpp ensure_defer sizes the grid from the frame)
 constexpr unsigned kShadowEvalBlocks = 256 * 6;
 size_t proc_sort_bytes(int width, int out_rows);
 hipError_t launch_repack(const uint8_t* d_rgba, int nx, int ny, int nz, uint8_t* d_planar, hipStream_t s);

@@ -65,7 +65,7 @@ hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_bu
                            positions, march_blocks, stale, d);                                                       \
         hipLaunchKernelGGL(proc_shadow_scan, dim3(1), dim3(kScanThreads), 0, s, total, d);                          \
         hipLaunchKernelGGL(proc_shadow_map, dim3((d.waves + 3) / 4), dim3(kThreads), 0, s, total, d);               \
-        hipLaunchKernelGGL((proc_shadow_eval<T>), dim3(kShadowEvalBlocks), dim3(kThreads), wt_bytes, s, a, d);      \
+        hipLaunchKernelGGL((proc_shadow_eval<T>), dim3(d.eval_blocks ? d.eval_blocks : kShadowEvalBlocks), dim3(kThreads), wt_bytes, s, a, d); \
     } while (0)
             if (tm == 3) {
                 if (early) VR_PD(true, 3); else VR_PD(false, 3);
