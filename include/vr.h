@@ -317,6 +317,9 @@ vr_status vr_set_layout_preference(void* ctx, int pref);
  *                     step (at most 8 shadow steps).  Results are identical.
  *                     "shadow_blocks" 0-65536: workgroups of the deferred
  *                     shadow pass (0 = auto, 3/8 of the sorted waves).
+ *                     "shadow_defer_mib": the largest scratch the deferred
+ *                     passes may allocate (default 32768); a frame that needs
+ *                     more, or whose allocation fails, takes the in-wave path.
  *   "lattice"         procedural medium, sorted schedule: 1 = the fBm reads its
  *                     per-cell gradient-pair offsets from a lattice table in
  *                     global memory (the default; built when the seed or the

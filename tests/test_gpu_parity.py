@@ -712,6 +712,26 @@ def test_procedural_shadow_deferred(r, oracle, case):
     assert counts[0] == counts[1]
 
 
+def test_procedural_shadow_deferred_scratch_limit(r, oracle):
+    """A frame whose deferred-shadow scratch would exceed option
+    shadow_defer_mib takes the in-wave path instead of failing: same frame,
+    exact, with a 1 MiB limit and with the default."""
+    W, H = 128, 72
+    march = vr.march_defaults(max_steps=128)
+    assert r.get_option("shadow_defer_mib") == 32768
+    imgs = []
+    try:
+        for mib in (1, 32768):
+            r.set_option("shadow_defer_mib", mib)
+            img, ref, c, s, _ = render_proc_both(r, oracle, W, H, march, shadow_steps=8)
+            assert_exact(img, ref)
+            assert c == s
+            imgs.append(img)
+    finally:
+        r.set_option("shadow_defer_mib", 32768)
+    assert np.array_equal(imgs[0], imgs[1])
+
+
 def test_procedural_shadow_deferred_stale_and_reuse(r, oracle):
     """The deferred passes with a reused sort order (background fill blocks)
     and a stale one (option sort_reuse: leftover pixels marched inline by the

@@ -58,6 +58,8 @@ constexpr int kRegionRebuildInterval = 32;
 // stays exact).
 constexpr size_t kSortKeyGridPart = 11;   // leading sort-key entries a stale order must match
 constexpr int kMaxRegionStreams = 4;
+// largest deferred-shadow scratch (option "shadow_defer_mib"): 32 GiB of the 288 GB device
+constexpr int kMaxDeferMiB = 32 << 10;
 constexpr int kRegionKeyLen = 35;
 // auto split (lanes per ray) from the frame share's tiles with work: K = 1 at
 // >= 6000, 2 at >= 1400, else 4.  Measured on 1/N of the 1080p frame at 512^3
@@ -102,6 +104,7 @@ struct Ctx {
     size_t sort_bytes = 0;
     // deferred shadow rays (option "shadow_defer", vr_internal.h ShadowDefer):
     // counter, per-wave step counts and records, entries; grown on demand
+    int shadow_defer_mib = kMaxDeferMiB;   // largest deferred-shadow scratch; a frame needing more compacts in-wave
     int shadow_blocks = 0;         // option "shadow_blocks": workgroups of the deferred shadow pass (0 = auto)
     int shadow_defer = 1;          // measured 1.25 -> 0.99 ms at config 3
     void* d_defer = nullptr;
@@ -760,6 +763,11 @@ vr_status vr_set_option(void* p, const char* name, int value)
         c->proc_enum = value;
         return VR_OK;
     }
+    if (n == "shadow_defer_mib") {
+        if (value < 0) return fail(VR_ERR_INVALID, "vr_set_option: shadow_defer_mib >= 0");
+        c->shadow_defer_mib = value;
+        return VR_OK;
+    }
     if (n == "shadow_blocks") {
         if (value < 0 || value > 65536) return fail(VR_ERR_INVALID, "vr_set_option: shadow_blocks in [0, 65536]");
         c->shadow_blocks = value;
@@ -837,6 +845,7 @@ int vr_get_option(void* p, const char* name)
     if (n == "proc_enum") return c->proc_enum;
     if (n == "shadow_defer") return c->shadow_defer;
     if (n == "shadow_blocks") return c->shadow_blocks;
+    if (n == "shadow_defer_mib") return c->shadow_defer_mib;
     if (n == "slab_cap") return c->slab_cap;
     if (n == "split_long") return c->split_long;
     if (n == "sort_reuse") return c->sort_reuse;
@@ -1149,9 +1158,12 @@ static vr_status ensure_lattice(Ctx* c, ProcParams* q, hipStream_t s)
 // most max_steps wave-steps and appends at most 64 entries per step, so its
 // region of 64 * max_steps entries cannot overflow (4.2 GB at 1080p x 128 on a
 // 288 GB device).
-constexpr size_t kMaxDeferBytes = 32ull << 30;
-static vr_status ensure_defer(Ctx* c, const MarchArgs& a, ShadowDefer* d)
+// *ok = false (and VR_OK): the frame needs more scratch than shadow_defer_mib, or
+// the allocation failed -- the render then takes the in-wave compaction (or the
+// per-lane shadow loop), which needs none.
+static vr_status ensure_defer(Ctx* c, const MarchArgs& a, ShadowDefer* d, bool* ok)
 {
+    *ok = false;
     const size_t pixels = (size_t)a.width * (size_t)a.out_rows;
     const size_t waves = (pixels + 255) / 256 * 4;   // the sorted march: 256-thread blocks of 4 waves
     const size_t stride = (size_t)std::max(a.max_steps, 1);
@@ -1161,17 +1173,19 @@ static vr_status ensure_defer(Ctx* c, const MarchArgs& a, ShadowDefer* d)
     const size_t off_rec = up(off_map + waves * stride * sizeof(uint4));   // <= stride chunks per wave
     const size_t off_ent = up(off_rec + waves * stride * sizeof(uint4));
     const size_t need = off_ent + waves * 64 * stride * sizeof(float4);
-    if (waves * stride >= (1ull << 32) || need > kMaxDeferBytes)
-        return fail(VR_ERR_INVALID, "vr_render: shadow_defer scratch for %zu pixels x %d steps exceeds %zu GiB",
-                    pixels, a.max_steps, kMaxDeferBytes >> 30);
+    if (waves * stride >= (1ull << 32) || need > ((size_t)c->shadow_defer_mib << 20)) return VR_OK;
     if (need > c->defer_bytes) {
         HIP_TRY(hipDeviceSynchronize());   // queued work on another stream may still read the old one
         if (c->d_defer) (void)hipFree(c->d_defer);
         c->d_defer = nullptr;
         c->defer_bytes = 0;
-        if (hipMalloc(&c->d_defer, need) != hipSuccess) return fail(VR_ERR_OOM, "vr_render: shadow_defer scratch");
+        if (hipMalloc(&c->d_defer, need) != hipSuccess) {
+            (void)hipGetLastError();   // clear the sticky allocation error
+            return VR_OK;
+        }
         c->defer_bytes = need;
     }
+    *ok = true;
     char* b = static_cast<char*>(c->d_defer);
     d->count = reinterpret_cast<unsigned*>(b);
     d->wsteps = reinterpret_cast<unsigned*>(b + off_ws);
@@ -1341,10 +1355,10 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
                 reuse = SORT_STALE;
         }
         ShadowDefer defer{};
-        const bool use_defer = sort_buf && c->shadow_defer && a.proc.shadow_steps > 0 && a.proc.wt_fixed &&
-                               a.proc.wt_n > 0;
+        bool use_defer = sort_buf && c->shadow_defer && a.proc.shadow_steps > 0 && a.proc.wt_fixed &&
+                         a.proc.wt_n > 0;
         if (use_defer) {
-            const vr_status st = ensure_defer(c, a, &defer);
+            const vr_status st = ensure_defer(c, a, &defer, &use_defer);
             if (st != VR_OK) return st;
         }
         std::vector<float> built = reuse == SORT_BUILD ? key : c->sort_key;
