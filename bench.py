@@ -85,6 +85,59 @@ def flop_per_density(octaves: int, cells_per_eval: float | None = None) -> float
     return 67 * octaves + 9 + 12 * cells_per_eval + 15 + 12 * full + 1 + 11
 
 
+def roofline_of(r, proc, shadow, variant, local_steps, local_evals, local_cells, kern_ms):
+    """The roofline object of one config's march: HBM
+    gather bytes for a grid past the Infinity Cache, fp32 VALU for the
+    cache-resident grid and the procedural medium."""
+    # bytes a step must gather: 8 per tap whose channel is not uniform
+    umask = r.get_option("uniform_mask") if proc is None and "_u" in variant else 0
+    taps_loaded = 4 - bin(max(umask, 0)).count("1")
+    bytes_per_step = 8 * taps_loaded
+    gather = local_steps * bytes_per_step / (kern_ms * 1e-3) / 1e9
+    gather32 = local_steps * BYTES_PER_STEP / (kern_ms * 1e-3) / 1e9
+    if proc is None and "corner8" not in variant and "cornerh" not in variant:
+        roofline = {"bound": "hbm", "achieved": round(gather, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(gather / HBM_PEAK_GBS, 4), "traffic": None,
+                    "achieved_def": f"{bytes_per_step} B algorithmic gather per executed ray-step (8 B per tap "
+                                    f"of a non-uniform channel; {4 - taps_loaded} uniform) x steps per launch "
+                                    "/ mean march-kernel duration (HIP events on its stream)",
+                    **({"frac_32B": round(gather32 / HBM_PEAK_GBS, 4)} if taps_loaded < 4 else {})}
+    elif proc is None:
+        # cache-resident volume (cornerh / corner8 are auto only when they
+        # fit the Infinity Cache): the march is VALU-bound (VALUBusy ~100 %,
+        # profiles/r01_pmc/c8_4k.json), so the roofline is fp32 VALU
+        fps = FLOP_PER_STEP_CORNERH if "cornerh" in variant else FLOP_PER_STEP
+        fps -= (27 if "cornerh" in variant else 31) * (4 - taps_loaded)   # a uniform tap is a constant
+        tf = local_steps * fps / (kern_ms * 1e-3) / 1e12
+        roofline = {"bound": "valu", "achieved": round(tf, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(tf / FP32_PEAK_TFLOPS, 4), "traffic": None,
+                    "achieved_def": f"{fps} algorithmic fp32 FLOP per executed ray-step ({taps_loaded} "
+                                    "sampled taps) x steps per launch / mean march-kernel duration (HIP events "
+                                    "on its stream); the volume is cache-resident",
+                    "gather_GBs": round(gather, 1)}
+    else:
+        defer = shadow > 0 and r.get_option("shadow_defer") == 1
+        cpe = local_cells / max(1, local_evals)
+        fpd = flop_per_density(proc.octaves, cpe)
+        fpd27 = flop_per_density(proc.octaves)
+        achieved = local_evals * fpd / (kern_ms * 1e-3) / 1e12
+        a27 = local_evals * fpd27 / (kern_ms * 1e-3) / 1e12
+        roofline = {"bound": "valu", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None,
+                    "achieved_def": f"{fpd:.1f} algorithmic fp32 FLOP per density evaluation (Perlin "
+                                    f"{67 * proc.octaves} + pruned Worley at {cpe:.3f} cells per evaluation, "
+                                    "measured with vr option count=2, + bound test, setup, rest) x "
+                                    f"{local_evals} evaluations per launch / mean march-kernel duration "
+                                    "(HIP events on its stream); no volume is read" +
+                                    ("; with deferred shadow rays (vr option shadow_defer = 1) the frame is "
+                                     "five launches -- primary march, scan, chunk map, shadow pass, resolve "
+                                     "-- and the events bracket all of them" if defer else ""),
+                    "worley_cells_per_eval": round(cpe, 4),
+                    "flop_per_eval_27cell": fpd27,
+                    "frac_27cell": round(a27 / FP32_PEAK_TFLOPS, 4)}
+    return roofline
+
+
 def cpu_baseline(volume_host, osd, gsd, march, width, height, budget_s=10.0, procedural=None):
     """Time the oracle on the same frame (all cores it is allowed), ~budget_s."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -129,6 +182,71 @@ def cpu_baseline(volume_host, osd, gsd, march, width, height, budget_s=10.0, pro
                       f"executed steps/s {steps / el:.4g}"}
 
 
+def other_config(name, steps, warmup):
+    """Time one more BASELINE config on this GPU in the same process, after the
+    headline window (verdict r03 #6): ms/frame, kernel ms (HIP events on its
+    stream, every 4th frame), the roofline object.  Returns the result and the
+    arguments of its CPU baseline."""
+    N, W, H, S, shadow, cfg_idx = CONFIGS[name]
+    fmt = vr.FMT_RGBA8_UNORM
+    with vr.Renderer(0) as r:
+        proc = None
+        if N is None:
+            r.set_procedural(shadow_steps=shadow)
+            proc = r.procedural
+        else:
+            r.generate_volume(vr.scaled_recipe(N))
+        osd, gsd = vr.reference_shader_data(1280.0 / 720.0)
+        r.set_shader_data(osd, gsd)
+        march = vr.march_defaults(max_steps=S)
+        r.set_march(march)
+        out = r.alloc_target(W, H, fmt)
+        counter = torch.zeros(1, dtype=torch.int64, device="cuda")
+
+        def units(mode):
+            r.set_option("count", mode)
+            counter.zero_()
+            r.render(W, H, fmt, out=out, step_counter=counter)
+            torch.cuda.synchronize()
+            return int(counter.item())
+
+        nsteps = units(0)
+        evals, cells = (units(1), units(2)) if proc is not None else (nsteps, None)
+        r.set_option("count", 0)
+        launch = r.prepare_render(W, H, fmt, out)
+        for _ in range(warmup):
+            launch()
+        torch.cuda.synchronize()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if i % 4 == 0 else None
+              for i in range(steps)]
+        t0 = time.perf_counter()
+        for i in range(steps):
+            if ev[i] is not None:
+                ev[i][0].record()
+            launch()
+            if ev[i] is not None:
+                ev[i][1].record()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        kern_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev if e is not None]))
+        variant = r.kernel_variant
+        defer = proc is not None and shadow > 0 and r.get_option("shadow_defer_last") == 1
+        res = {"metric": f"Mray/s (= W*H*steps/s) at {W}x{H} x {S} steps",
+               "value": round(W * H * S * steps / el / 1e6, 3), "unit": "Mray/s", "steps": steps,
+               "ms_per_step": round(el / steps * 1e3, 4), "kernel_ms_mean": round(kern_ms, 5),
+               "config": {"workload": (f"{name}: {N}^3 RGBA8 grid, {W}x{H}, {S} steps, RGBA8 out" if proc is None
+                                       else f"{name}: procedural {proc.octaves}-octave Perlin-Worley cloud, "
+                                            f"{W}x{H}, {S} steps, shadow {shadow} steps, RGBA8 out"),
+                          "baseline_config_index": cfg_idx,
+                          "kernel": variant + ("_deferred" if defer else ""),
+                          "executed_steps_per_frame": nsteps},
+               "roofline": roofline_of(r, proc, shadow, variant, nsteps, evals, cells, kern_ms)}
+        if defer:
+            res["shadow_defer_scratch_MB"] = round(r.get_option("shadow_defer_kib") / 1024.0, 1)
+        vol = r.get_volume() if proc is None else None
+    return res, (vol, osd, gsd, march, W, H, proc)
+
+
 def main() -> int:
     # stdout carries exactly one JSON line (rank 0).  Libraries print to fd 1
     # too -- RCCL its version banner at communicator init -- so fd 1 is
@@ -144,6 +262,9 @@ def main() -> int:
     ap.add_argument("--config", default="grid512", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--cpu-budget-other", type=float, default=3.0, help="CPU baseline budget of each other config")
+    ap.add_argument("--no-other-configs", action="store_true",
+                    help="N = 1, default config: skip timing configs 2, 3, 4 after the headline window")
     ap.add_argument("--schedule", type=int, default=-1, help="vr option 'schedule' (-1 = auto)")
     ap.add_argument("--sharder", default="native", choices=["native", "torch"],
                     help="N > 1: native = the C++ frame loop over this library's own RCCL communicator "
@@ -334,6 +455,14 @@ def main() -> int:
                       "value": round(W * H * S * args.steps / el2 / 1e6, 3)}
         r.set_option("uniform_skip", 1)
         assert r.kernel_variant == skipped_variant
+    # the other BASELINE configs, timed in this process after the headline
+    # window (N = 1 only; a multi-GPU run keeps to the headline)
+    others, other_cpu = {}, {}
+    if world == 1 and not native and not args.spin and args.config == "grid512" and not args.no_other_configs:
+        for name in ("grid4k", "cloud", "cloud_shadow"):
+            others[name], other_cpu[name] = other_config(name, args.steps, args.warmup)
+    # the measured HBM roofline of this box: a 16-B-per-lane streaming copy
+    copy_best, copy_med = (r.measure_copy_bandwidth(2 << 30, 10) if rank == 0 else (None, None))
     tt = torch.tensor([el, kern_ms], dtype=torch.float64, device=red_dev)
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -352,52 +481,13 @@ def main() -> int:
         ms_per_step = el / args.steps * 1e3
         value = W * H * S * args.steps / el / 1e6
         variant = r.kernel_variant
-        # bytes a step must gather: 8 per tap whose channel is not uniform
-        umask = r.get_option("uniform_mask") if proc is None and "_u" in variant else 0
-        taps_loaded = 4 - bin(max(umask, 0)).count("1")
-        bytes_per_step = 8 * taps_loaded
-        gather = local_steps * bytes_per_step / (kern_ms * 1e-3) / 1e9
-        gather32 = local_steps * BYTES_PER_STEP / (kern_ms * 1e-3) / 1e9
-        if proc is None and "corner8" not in variant and "cornerh" not in variant:
-            roofline = {"bound": "hbm", "achieved": round(gather, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(gather / HBM_PEAK_GBS, 4), "traffic": None,
-                        "achieved_def": f"{bytes_per_step} B algorithmic gather per executed ray-step (8 B per tap "
-                                        f"of a non-uniform channel; {4 - taps_loaded} uniform) x steps per launch "
-                                        "/ mean march-kernel duration (HIP events on its stream)",
-                        **({"frac_32B": round(gather32 / HBM_PEAK_GBS, 4)} if taps_loaded < 4 else {})}
-        elif proc is None:
-            # cache-resident volume (cornerh / corner8 are auto only when they
-            # fit the Infinity Cache): the march is VALU-bound (VALUBusy ~100 %,
-            # profiles/r01_pmc/c8_4k.json), so the roofline is fp32 VALU
-            fps = FLOP_PER_STEP_CORNERH if "cornerh" in variant else FLOP_PER_STEP
-            fps -= (27 if "cornerh" in variant else 31) * (4 - taps_loaded)   # a uniform tap is a constant
-            tf = local_steps * fps / (kern_ms * 1e-3) / 1e12
-            roofline = {"bound": "valu", "achieved": round(tf, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                        "frac": round(tf / FP32_PEAK_TFLOPS, 4), "traffic": None,
-                        "achieved_def": f"{fps} algorithmic fp32 FLOP per executed ray-step ({taps_loaded} "
-                                        "sampled taps) x steps per launch / mean march-kernel duration (HIP events "
-                                        "on its stream); the volume is cache-resident",
-                        "gather_GBs": round(gather, 1)}
-        else:
-            defer = shadow > 0 and r.get_option("shadow_defer") == 1
-            cpe = local_cells / max(1, local_evals)
-            fpd = flop_per_density(proc.octaves, cpe)
-            fpd27 = flop_per_density(proc.octaves)
-            achieved = local_evals * fpd / (kern_ms * 1e-3) / 1e12
-            a27 = local_evals * fpd27 / (kern_ms * 1e-3) / 1e12
-            roofline = {"bound": "valu", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS,
-                        "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None,
-                        "achieved_def": f"{fpd:.1f} algorithmic fp32 FLOP per density evaluation (Perlin "
-                                        f"{67 * proc.octaves} + pruned Worley at {cpe:.3f} cells per evaluation, "
-                                        "measured with vr option count=2, + bound test, setup, rest) x "
-                                        f"{local_evals} evaluations per launch / mean march-kernel duration "
-                                        "(HIP events on its stream); no volume is read" +
-                                        ("; with deferred shadow rays (vr option shadow_defer = 1) the frame is "
-                                         "five launches -- primary march, scan, chunk map, shadow pass, resolve "
-                                         "-- and the events bracket all of them" if defer else ""),
-                        "worley_cells_per_eval": round(cpe, 4),
-                        "flop_per_eval_27cell": fpd27,
-                        "frac_27cell": round(a27 / FP32_PEAK_TFLOPS, 4)}
+        roofline = roofline_of(r, proc, shadow, variant, local_steps, local_evals, local_cells, kern_ms)
+        if roofline["bound"] == "hbm":
+            roofline.update({"peak_measured": round(copy_best, 1),
+                             "frac_measured": round(roofline["achieved"] / copy_best, 4),
+                             "peak_measured_def": "best of 10 timed 16-B-per-lane grid-stride copies of 2 GiB on this "
+                                                  "GPU (vr_measure_copy_bandwidth; read + written bytes / time; "
+                                                  f"median {copy_med:.0f} GB/s)"})
         traffic = None
         ta = None
         tfile = os.path.join(ROOT, "profiles", "traffic.json")
@@ -458,9 +548,14 @@ def main() -> int:
                                 if traffic else {}),
                              **({"ta_lookup": ta} if ta else {})),
         }
+        if others:
+            out["other_configs"] = others
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(None if proc is not None else r.get_volume(), osd, gsd, march, W, H,
                                                args.cpu_budget, procedural=proc)
+            for name, (vol_o, osd_o, gsd_o, march_o, W_o, H_o, proc_o) in other_cpu.items():
+                others[name]["cpu_baseline"] = cpu_baseline(vol_o, osd_o, gsd_o, march_o, W_o, H_o,
+                                                            args.cpu_budget_other, procedural=proc_o)
         print(json.dumps(out), file=json_out, flush=True)
     if native:
         pipe.close()

@@ -310,16 +310,29 @@ vr_status vr_set_layout_preference(void* ctx, int pref);
  *   "shadow_defer"    procedural medium with shadow rays, sorted schedule:
  *                     1 (default) = the primary march appends its
  *                     shadow-ray origins, one pass evaluates them all and a
- *                     resolve pass folds them per ray in step order
- *                     (device scratch of 16 B x 64 x max_steps per 64 rays,
- *                     e.g. 4.2 GB at 1080p x 128, kept by the context);
+ *                     resolve pass folds them per ray in step order;
  *                     0 = each wave deals its own shadow samples at every
  *                     step (at most 8 shadow steps).  Results are identical.
+ *                     The deferred passes keep a device scratch sized from
+ *                     the frame: ~16 B per executed ray-step x 5/4 (0.35 GB at
+ *                     1080p x 128, ~2.7 GB at 3840 x 2160 x 256), grown when a
+ *                     frame needs more (a wave past it marches its shadow rays
+ *                     in place, exactly); setting "shadow_defer" 0 or
+ *                     "shadow_defer_mib" 0 frees it (after a device sync).
  *                     "shadow_blocks" 0-65536: workgroups of the deferred
  *                     shadow pass (0 = auto, 3/8 of the sorted waves).
  *                     "shadow_defer_mib": the largest scratch the deferred
- *                     passes may allocate (default 32768); a frame that needs
- *                     more, or whose allocation fails, takes the in-wave path.
+ *                     passes may allocate (default 4096); "shadow_defer_entries"
+ *                     a fixed entry capacity (tests; 0 = from the frame).
+ *                     Read-only: "shadow_defer_kib" the scratch held now,
+ *                     "shadow_defer_last" 1 if the last procedural render ran
+ *                     the deferred passes.
+ *   "lat"             regions schedule, col48 / brick4832 / cornerh: the
+ *                     latency-mode march for small frame shares ("split" lanes
+ *                     per ray, 2-4 rounds of loads in flight; bit-exact):
+ *                     0 = off, 2/3/4 = on with that depth, -1 = auto (on when
+ *                     the target's tiles with work are too few to fill the GPU,
+ *                     e.g. a 1/8 multi-GPU share).
  *   "lattice"         procedural medium, sorted schedule: 1 = the fBm reads its
  *                     per-cell gradient-pair offsets from a lattice table in
  *                     global memory (the default; built when the seed or the
@@ -328,6 +341,14 @@ vr_status vr_set_layout_preference(void* ctx, int pref);
  * vr_get_option returns -1 for an unknown name.                            */
 vr_status vr_set_option(void* ctx, const char* name, int value);
 int       vr_get_option(void* ctx, const char* name);
+
+/* ---- measurement: the device's streaming-copy bandwidth, the measured HBM
+ *      roofline the bench reports next to the 8 TB/s spec.  A float4 (16 B per
+ *      lane) grid-stride copy of `bytes` between two fresh device buffers,
+ *      `reps` times on `stream`, each timed with HIP events; *gbs_best and
+ *      *gbs_median = (read + written bytes) / time, GB/s.  Synchronous.      */
+vr_status vr_measure_copy_bandwidth(void* ctx, size_t bytes, int reps, void* stream, double* gbs_best,
+                                    double* gbs_median);
 
 #ifdef __cplusplus
 }

@@ -89,35 +89,51 @@ def test_rotated_cube(r, oracle, vol128, phi, theta):
 SPIN_DEG = 1.6   # TestMain.cpp:171-184, :222-224: 100 deg/s held key x 0.016 s per frame
 
 
-@pytest.mark.parametrize("layout", [0, 12])
-def test_spinning_camera_frames(r, oracle, vol128, layout):
+@pytest.mark.parametrize("layout", [0, 12, 15])
+@pytest.mark.parametrize("gpu,interval", [(1, 32), (0, 32), (1, 1), (1, 7)])
+def test_spinning_camera_frames(r, oracle, vol128, layout, gpu, interval):
     """A moving camera (verdict r02 #3): 40 consecutive frames, each with new
     shader data (phi += 1.6 deg, the reference's held A/D key).  The region
-    lists of the first frame are reused while the camera moves and rebuilt
-    after kRegionRebuildInterval (32) renders (vr_api.cpp build_regions), so
-    frames 1, 33 and 40 cover a reused list, the rebuild and the list after
-    it; each is checked bit-exactly against the oracle, with its step count.
-    Layout 0 = auto (cornerh at 128^3), 12 = brick4832 (the config-5 layout)."""
+    lists of the first frame (built on the host: a new target) are reused while
+    the camera moves and rebuilt every `interval` renders -- on the GPU
+    (vr_regions.hip, option region_gpu 1, the default) or on the host -- so
+    frames 1, 33 and 40 cover a reused list, a rebuild and the lists after it;
+    each is checked bit-exactly against the oracle, with its step count (a
+    tile listed twice would count its steps twice; one left out keeps the
+    target's garbage).  Layout 0 = auto (cornerh at 128^3), 12 = brick4832,
+    15 = col48 (the config-5 layout)."""
     W, H = 320, 180
     r.set_volume(vol128)
     r.set_layout_preference(layout)
     r.set_march(vr.march_defaults())
+    r.set_option("region_gpu", gpu)
+    r.set_option("region_interval", interval)
     keep = {1: None, 33: None, 40: None}
     try:
+        builds0 = r.get_option("region_gpu_builds")
         for i in range(1, 41):
             osd, gsd = vr.reference_shader_data(W / H, SPIN_DEG * i, 0.0)
             r.set_shader_data(osd, gsd)
             cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
-            img = r.render(W, H, 0, step_counter=cnt)
+            img = r.alloc_target(W, H, 0)
+            img.fill_(float("nan"))
+            r.render(W, H, 0, out=img, step_counter=cnt)
             if i in keep:
                 keep[i] = (img, cnt, osd, gsd)
         torch.cuda.synchronize()
+        builds = r.get_option("region_gpu_builds") - builds0
+        if gpu:
+            assert builds >= 39 // interval - 1, builds
+        else:
+            assert builds == 0
         for i, (img, cnt, osd, gsd) in keep.items():
             obj, glob = vr.shader_data_arrays(osd, gsd)
             ref, steps = oracle.render(vol128, obj, glob, oracle.from_params(vr.march_defaults()), W, H, 0)
             assert_exact(img.cpu().numpy(), ref)
             assert int(cnt.item()) == steps, i
     finally:
+        r.set_option("region_gpu", 1)
+        r.set_option("region_interval", 32)
         r.set_layout_preference(0)
 
 
@@ -713,23 +729,86 @@ def test_procedural_shadow_deferred(r, oracle, case):
 
 
 def test_procedural_shadow_deferred_scratch_limit(r, oracle):
-    """A frame whose deferred-shadow scratch would exceed option
-    shadow_defer_mib takes the in-wave path instead of failing: same frame,
-    exact, with a 1 MiB limit and with the default."""
+    """The deferred-shadow scratch is sized from the frame (vr_api.cpp
+    ensure_defer): sorted wave w owns the entry range proc_scan lays out from
+    the cost histogram, and a wave past the capacity marches its shadow rays in
+    place.  Exact with a capacity of 4096 entries (most waves in place), with
+    the frame-sized scratch, and with shadow_defer_mib 0 (no scratch: the
+    in-wave compaction) -- the same frame every time."""
     W, H = 128, 72
     march = vr.march_defaults(max_steps=128)
-    assert r.get_option("shadow_defer_mib") == 32768
+    assert r.get_option("shadow_defer_mib") == 4096
     imgs = []
     try:
-        for mib in (1, 32768):
+        for ents, mib in ((4096, 4096), (0, 4096), (0, 0)):
+            r.set_option("shadow_defer_entries", ents)
             r.set_option("shadow_defer_mib", mib)
             img, ref, c, s, _ = render_proc_both(r, oracle, W, H, march, shadow_steps=8)
             assert_exact(img, ref)
             assert c == s
+            assert r.get_option("shadow_defer_last") == (1 if mib else 0)
+            kib = r.get_option("shadow_defer_kib")
+            assert (0 < kib < 4096) if mib else kib == 0
             imgs.append(img)
     finally:
-        r.set_option("shadow_defer_mib", 32768)
-    assert np.array_equal(imgs[0], imgs[1])
+        r.set_option("shadow_defer_entries", 0)
+        r.set_option("shadow_defer_mib", 4096)
+    assert np.array_equal(imgs[0], imgs[1]) and np.array_equal(imgs[0], imgs[2])
+
+
+def proc_frame_bands(r, oracle, W, H, march, firsts, stride=24, fmt=0, **proc):
+    """A whole procedural frame on the GPU against the oracle on interleaved
+    16-row band subsets, and its executed-step count against the oracle's
+    geometry (frag.glsl:46).  Returns the GPU frame."""
+    osd, gsd = vr.reference_shader_data(16 / 9)
+    r.set_shader_data(osd, gsd)
+    r.set_march(march)
+    r.set_procedural(**proc)
+    p = oracle.procedural_from(r.procedural)
+    try:
+        cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+        img = r.render(W, H, fmt, step_counter=cnt).cpu().numpy()
+        defer = r.get_option("shadow_defer_last")
+        kib = r.get_option("shadow_defer_kib")
+    finally:
+        r.set_procedural(enabled=0)
+    obj, glob = vr.shader_data_arrays(osd, gsd)
+    for first in firsts:
+        ref, _ = oracle.render_procedural(p, obj, glob, oracle.from_params(march), W, H, fmt, band_rows=16,
+                                          band_stride=stride, band_first=first)
+        rows = [(first + (i // 16) * stride) * 16 + i % 16 for i in range(ref.shape[0])]
+        keep = [i for i, y in enumerate(rows) if y < H]
+        assert_exact(img[[rows[i] for i in keep]], ref[keep])
+    n = oracle.step_counts(obj, glob, oracle.from_params(march), W, H)
+    assert int(cnt.item()) == int(n[n > 0].sum(dtype=np.int64))
+    return img, defer, kib
+
+
+def test_config3_full_frame_bands(r, oracle):
+    """BASELINE config 3 at its full shape: the whole 1920x1080x128 frame with
+    8-step shadow rays, on the deferred passes (12,150 shadow workgroups),
+    against the oracle on three interleaved band subsets, with the whole-frame
+    step count.  Rendered twice: the second frame runs with the scratch sized
+    from the first one's need, <= 0.4 GB (the old per-wave worst case took
+    4.2 GB)."""
+    march = vr.march_defaults(max_steps=128)
+    for rep in range(2):
+        img, defer, kib = proc_frame_bands(r, oracle, 1920, 1080, march, (0, 11, 17) if rep else (5,),
+                                           shadow_steps=8)
+        assert defer == 1
+        assert 0 < kib <= 400 * 1024, kib
+        assert img[..., 0].max() > 0.05
+
+
+def test_config3_4k_256_deferred(r, oracle):
+    """Config 3's medium at config 4's shape (3840x2160, 256 steps): the frame
+    takes the deferred path (its worst-case scratch would have been ~68 GB),
+    exact against the oracle on band subsets, with the whole-frame step
+    count."""
+    march = vr.march_defaults(max_steps=256)
+    img, defer, kib = proc_frame_bands(r, oracle, 3840, 2160, march, (3, 40), stride=48, shadow_steps=8)
+    assert defer == 1
+    assert 0 < kib <= 4096 * 1024
 
 
 def test_procedural_shadow_deferred_stale_and_reuse(r, oracle):
@@ -1154,6 +1233,50 @@ def test_split_rays_bitexact(r, oracle, vol128, layout, split):
             assert_exact(img, ref)
             assert c == s
     finally:
+        r.set_option("split", 0)
+        r.set_option("schedule", -1)
+        r.set_layout_preference(0)
+
+
+@pytest.mark.parametrize("layout", [15, 12, 14])
+@pytest.mark.parametrize("split,lat", [(1, 2), (1, 4), (2, 3), (4, 2), (4, 3), (4, 4), (8, 3)])
+def test_latency_march_bitexact(r, oracle, vol128, layout, split, lat):
+    """The latency-mode march for small frame shares (vr_march_lat.hip: K =
+    split lanes per ray, `lat` rounds of loads in flight):
+    exact against the oracle with step counts -- the recipe volume (G uniform:
+    the _uG kernel), a rotated cube, bands, short rays (fewer steps than the
+    pipeline's rounds), early-out, a random volume (every channel loaded) and
+    per-tap MediaScroll offsets inside the clamp-exact range."""
+    r.set_layout_preference(layout)
+    r.set_option("schedule", 5)
+    r.set_option("split", split)
+    r.set_option("lat", lat)
+    try:
+        osd, gsd = vr.reference_shader_data(16 / 9, 25.0, -40.0)
+        for W, H, band, march in [(333, 187, {}, vr.march_defaults()),
+                                  (640, 360, dict(band_rows=16, band_stride=3, band_first=2), vr.march_defaults()),
+                                  (320, 180, {}, vr.march_defaults(max_steps=7)),
+                                  (320, 180, {}, vr.march_defaults(max_steps=2)),
+                                  (320, 180, {}, vr.march_defaults(early_out=0.6, density=4.0))]:
+            img, ref, c, s = render_both(r, oracle, vol128, W, H, osd, gsd, march=march, **band)
+            assert r.kernel_variant.endswith(f"_lat{lat}")
+            assert_exact(img, ref)
+            assert c == s
+        rng = np.random.default_rng(split * 10 + lat)
+        vol = rng.integers(0, 256, size=(40, 52, 36, 4), dtype=np.uint8)
+        osd, gsd = vr.reference_shader_data(16 / 9, 30.0, 5.0)
+        img, ref, c, s = render_both(r, oracle, vol, 200, 112, osd, gsd)
+        assert_exact(img, ref)
+        assert c == s
+        gsd.media_scroll[1 * 4 + 1] = 0.01
+        gsd.media_scroll[2 * 4 + 2] = -0.02
+        for m in (vr.march_defaults(), vr.march_defaults(early_out=0.6)):
+            img, ref, c, s = render_both(r, oracle, vol, 160, 90, osd, gsd, march=m)
+            assert "_lat" in r.kernel_variant
+            assert_exact(img, ref)
+            assert c == s
+    finally:
+        r.set_option("lat", 0)
         r.set_option("split", 0)
         r.set_option("schedule", -1)
         r.set_layout_preference(0)

@@ -130,6 +130,8 @@ _SIGS = {
     "vr_set_layout_preference": (ctypes.c_int, [_vp, ctypes.c_int]),
     "vr_set_option": (ctypes.c_int, [_vp, ctypes.c_char_p, ctypes.c_int]),
     "vr_get_option": (ctypes.c_int, [_vp, ctypes.c_char_p]),
+    "vr_measure_copy_bandwidth": (ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.c_int, _vp,
+                                                 ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
 }
 # functions whose int return is a value, not a vr_status
 _VALUE_RETURNS = {"vr_abi_version", "vr_band_rows_packed", "vr_get_option", "vr_volume_extent_ok"}

@@ -58,8 +58,13 @@ constexpr int kRegionRebuildInterval = 32;
 // stays exact).
 constexpr size_t kSortKeyGridPart = 11;   // leading sort-key entries a stale order must match
 constexpr int kMaxRegionStreams = 4;
-// largest deferred-shadow scratch (option "shadow_defer_mib"): 32 GiB of the 288 GB device
-constexpr int kMaxDeferMiB = 32 << 10;
+// largest deferred-shadow scratch (option "shadow_defer_mib"): the scratch is
+// sized from the frame (ensure_defer: ~0.35 GB at 1080p x 128, ~2.7 GB at
+// 3840 x 2160 x 256); a frame needing more marches its last waves' shadow rays
+// in place
+constexpr int kMaxDeferMiB = 4 << 10;
+// retired deferred scratch buffers kept before a device sync frees them
+constexpr size_t kMaxDeferRetired = 4;
 constexpr int kRegionKeyLen = 35;
 // auto split (lanes per ray) from the frame share's tiles with work: K = 1 at
 // >= 6000, 2 at >= 1400, else 4.  Measured on 1/N of the 1080p frame at 512^3
@@ -100,7 +105,7 @@ struct Ctx {
     vr_procedural proc{};          // procedural medium (configs 2/3), off by default
     int count = 0;                 // step_counter: 0 = executed ray-steps, 1 = density evaluations,
                                    // 2 = Worley cells computed (procedural)
-    void* d_sort = nullptr;        // procedural cost-sort scratch (proc_sort_bytes), grown on demand
+    void* d_sort = nullptr;        // procedural cost-sort scratch (sort_layout), grown on demand
     size_t sort_bytes = 0;
     // deferred shadow rays (option "shadow_defer", vr_internal.h ShadowDefer):
     // counter, per-wave step counts and records, entries; grown on demand
@@ -109,6 +114,19 @@ struct Ctx {
     int shadow_defer = 1;          // measured 1.25 -> 0.99 ms at config 3
     void* d_defer = nullptr;
     size_t defer_bytes = 0;
+    unsigned long long defer_ent_cap = 0;   // entries / step records / waves the current scratch holds
+    unsigned defer_rec_cap = 0, defer_waves = 0;
+    // entries / step records per pixel-step (per wave-step) of the frame: 5/4 of
+    // the largest need seen (proc_scan -> need_host); 1/12 and 1/8 until one is
+    double want_ent = 0.0, want_rec = 0.0;
+    double need_pixsteps = 0.0, need_wavesteps = 0.0;   // of the frame whose need is pending
+    unsigned defer_entries = 0;    // option "shadow_defer_entries": entry capacity override (tests; 0 = sized from the frame)
+    int defer_last = 0;            // the last procedural render ran the deferred passes
+    std::vector<void*> defer_retired;   // outgrown scratch buffers: queued frames may still use them
+    unsigned long long* h_need = nullptr;   // host-mapped [entries, records] written by the last sorting frame
+    unsigned long long* d_need = nullptr;   // its device address
+    hipEvent_t need_ev = nullptr;
+    bool need_pending = false;
     // regions schedule (build_regions): per-XCD tile lists, double-buffered
     // so a rebuild never waits for more than the render that last used the
     // other buffer (2 frames in flight, VulkanRenderer.cpp:13)
@@ -120,11 +138,22 @@ struct Ctx {
     int split_long = 0;            // regions: tiles costing >= this % of the longest split in two halves (0 = off)
     int wg_waves = 4;              // regions: waves per workgroup (4, 8, 16)
     int supertile = 2;             // regions: list order by S x S blocks of tiles (1 = per tile; 2 measured 1 % faster)
+    int lat = 0;                   // regions: latency-mode march, rounds of loads in flight (0 = off, -1 = auto, 2-4)
+    int region_interval = kRegionRebuildInterval;   // option "region_interval": renders a moved camera reuses the lists
+    int region_gpu = 1;            // option "region_gpu": 1 = a moved camera's lists are rebuilt on the GPU
+    void* d_rg = nullptr;          // GPU list build scratch (region_build_bytes), zeroed when allocated
+    size_t rg_bytes = 0;
+    int* h_rghdr = nullptr;        // host-mapped copy of the last GPU build's header (kRegionHeader ints)
+    hipEvent_t rg_ev = nullptr;    // recorded after that build
+    bool rg_pending = false;
+    int rg_buf = -1;               // the region buffer it built
+    long long gpu_builds = 0;      // read-only option "region_gpu_builds"
     struct RegionBuf {
-        unsigned* d = nullptr;     // device tile list
-        unsigned* h = nullptr;     // pinned staging copy
+        unsigned* d = nullptr;     // device: kRegionHeader ints (off[9], tiles with work, longest, tiles), then the list
+        unsigned* h = nullptr;     // pinned staging copy (host builds)
         size_t cap = 0;            // entries
-        TileMap map{};
+        TileMap map{};             // host copy: nwx (and off[] for host builds)
+        int most = 0;              // the longest per-XCD list (sizes the launch)
         int nwork = 0;             // tiles with estimated work
         int mixed = 0;             // the lists hold this many sub-blocks (2, 4) of the longest tiles (bit 31)
         // the streams that rendered with these lists; when the lists are
@@ -370,6 +399,8 @@ const char* variant_name(const Plan& p)
 
 extern "C" {
 
+static vr_status release_defer(Ctx* c);
+
 const char* vr_last_error(void) { return g_err.c_str(); }
 int vr_abi_version(void) { return VR_ABI_VERSION; }
 
@@ -496,9 +527,15 @@ vr_status vr_destroy(void* p)
     free_volume(c);
     if (c->d_heads) (void)hipFree(c->d_heads);
     if (c->d_sort) (void)hipFree(c->d_sort);
+    (void)hipDeviceSynchronize();   // queued renders may still read the region lists and the scratch
     if (c->d_defer) (void)hipFree(c->d_defer);
-    (void)hipDeviceSynchronize();   // queued renders may still read the region lists
+    for (void* q : c->defer_retired) (void)hipFree(q);
+    if (c->h_need) (void)hipHostFree(c->h_need);
+    if (c->need_ev) (void)hipEventDestroy(c->need_ev);
     if (c->d_lat) (void)hipFree(c->d_lat);
+    if (c->d_rg) (void)hipFree(c->d_rg);
+    if (c->h_rghdr) (void)hipHostFree(c->h_rghdr);
+    if (c->rg_ev) (void)hipEventDestroy(c->rg_ev);
     if (c->d_mm) (void)hipFree(c->d_mm);
     if (c->h_mm) (void)hipHostFree(c->h_mm);
     if (c->mm_ready) (void)hipEventDestroy(c->mm_ready);
@@ -619,6 +656,46 @@ vr_status vr_selftest(void* p, const char* name, long long* failures)
     (void)hipFree(d);
     if (e != hipSuccess) return fail(VR_ERR_HIP, "vr_selftest: %s", hipGetErrorString(e));
     *failures = (long long)h;
+    return VR_OK;
+}
+
+vr_status vr_measure_copy_bandwidth(void* p, size_t bytes, int reps, void* stream, double* gbs_best, double* gbs_median)
+{
+    if (!p || !gbs_best || reps <= 0 || bytes < 16) return fail(VR_ERR_INVALID, "vr_measure_copy_bandwidth: bad argument");
+    Ctx* c = as_ctx(p);
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    bytes &= ~(size_t)15;
+    void *src = nullptr, *dst = nullptr;
+    std::vector<hipEvent_t> ev(2 * (size_t)reps + 2, nullptr);
+    hipError_t e = hipMalloc(&src, bytes);
+    if (e == hipSuccess) e = hipMalloc(&dst, bytes);
+    if (e == hipSuccess) e = hipMemsetAsync(src, 0x5a, bytes, s);
+    for (auto& v : ev)
+        if (e == hipSuccess) e = hipEventCreate(&v);
+    if (e == hipSuccess) e = launch_stream_copy(src, dst, bytes, s);   // warm-up (page mapping, clocks)
+    for (int i = 0; i < reps && e == hipSuccess; ++i) {
+        e = hipEventRecord(ev[2 * i], s);
+        if (e == hipSuccess) e = launch_stream_copy(src, dst, bytes, s);
+        if (e == hipSuccess) e = hipEventRecord(ev[2 * i + 1], s);
+    }
+    std::vector<double> gbs;
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    for (int i = 0; i < reps && e == hipSuccess; ++i) {
+        float ms = 0.0f;
+        e = hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]);
+        if (e == hipSuccess && ms > 0.0f) gbs.push_back(2.0 * (double)bytes / (ms * 1e-3) / 1e9);
+    }
+    for (auto& v : ev)
+        if (v) (void)hipEventDestroy(v);
+    if (src) (void)hipFree(src);
+    if (dst) (void)hipFree(dst);
+    if (e != hipSuccess) return fail(e == hipErrorOutOfMemory ? VR_ERR_OOM : VR_ERR_HIP, "vr_measure_copy_bandwidth: %s",
+                                     hipGetErrorString(e));
+    if (gbs.empty()) return fail(VR_ERR_HIP, "vr_measure_copy_bandwidth: no timing");
+    std::sort(gbs.begin(), gbs.end());
+    *gbs_best = gbs.back();
+    if (gbs_median) *gbs_median = gbs[gbs.size() / 2];
     return VR_OK;
 }
 
@@ -766,7 +843,12 @@ vr_status vr_set_option(void* p, const char* name, int value)
     if (n == "shadow_defer_mib") {
         if (value < 0) return fail(VR_ERR_INVALID, "vr_set_option: shadow_defer_mib >= 0");
         c->shadow_defer_mib = value;
-        return VR_OK;
+        return value == 0 ? release_defer(c) : VR_OK;
+    }
+    if (n == "shadow_defer_entries") {
+        if (value < 0) return fail(VR_ERR_INVALID, "vr_set_option: shadow_defer_entries >= 0");
+        c->defer_entries = (unsigned)value;
+        return release_defer(c);
     }
     if (n == "shadow_blocks") {
         if (value < 0 || value > 65536) return fail(VR_ERR_INVALID, "vr_set_option: shadow_blocks in [0, 65536]");
@@ -776,7 +858,7 @@ vr_status vr_set_option(void* p, const char* name, int value)
     if (n == "shadow_defer") {
         if (value < 0 || value > 1) return fail(VR_ERR_INVALID, "vr_set_option: shadow_defer is 0 or 1");
         c->shadow_defer = value;
-        return VR_OK;
+        return value == 0 ? release_defer(c) : VR_OK;
     }
     if (n == "slab") {
         if (value < 0 || value > 1) return fail(VR_ERR_INVALID, "vr_set_option: slab is 0 or 1");
@@ -802,6 +884,22 @@ vr_status vr_set_option(void* p, const char* name, int value)
     if (n == "supertile") {
         if (value != 1 && value != 2 && value != 4) return fail(VR_ERR_INVALID, "vr_set_option: supertile is 1, 2 or 4");
         c->supertile = value;
+        return VR_OK;
+    }
+    if (n == "region_interval") {
+        if (value < 1 || value > 1 << 20) return fail(VR_ERR_INVALID, "vr_set_option: region_interval in [1, 2^20]");
+        c->region_interval = value;
+        return VR_OK;
+    }
+    if (n == "region_gpu") {
+        if (value < 0 || value > 1) return fail(VR_ERR_INVALID, "vr_set_option: region_gpu is 0 or 1");
+        c->region_gpu = value;
+        return VR_OK;
+    }
+    if (n == "lat") {
+        if (value != -1 && value != 0 && value != 2 && value != 3 && value != 4)
+            return fail(VR_ERR_INVALID, "vr_set_option: lat is -1 (auto), 0 (off), 2, 3 or 4 (rounds in flight)");
+        c->lat = value;
         return VR_OK;
     }
     if (n == "uniform_skip") {
@@ -846,6 +944,10 @@ int vr_get_option(void* p, const char* name)
     if (n == "shadow_defer") return c->shadow_defer;
     if (n == "shadow_blocks") return c->shadow_blocks;
     if (n == "shadow_defer_mib") return c->shadow_defer_mib;
+    if (n == "shadow_defer_entries") return (int)c->defer_entries;
+    if (n == "shadow_defer_last") return c->defer_last;   // read-only
+    if (n == "shadow_defer_kib")                          // read-only: the scratch held now, KiB
+        return (int)std::min<size_t>((c->defer_bytes + 1023) / 1024, 0x7fffffff);
     if (n == "slab_cap") return c->slab_cap;
     if (n == "split_long") return c->split_long;
     if (n == "sort_reuse") return c->sort_reuse;
@@ -858,6 +960,10 @@ int vr_get_option(void* p, const char* name)
         return c->uniform_mask;
     }
     if (n == "supertile") return c->supertile;
+    if (n == "lat") return c->lat;
+    if (n == "region_interval") return c->region_interval;
+    if (n == "region_gpu") return c->region_gpu;
+    if (n == "region_gpu_builds") return (int)std::min<long long>(c->gpu_builds, 0x7fffffff);   // read-only
     return -1;
 }
 
@@ -879,19 +985,33 @@ const char* vr_kernel_variant(void* p)
     if (pl.layout == LAYOUT_COL48 && c->slab && kind == SCHED_REGIONS && c->split <= 1)
         return pl.early ? "grid_col48_slab_clamp_early" : "grid_col48_slab_clamp";
     const int um = c->uniform_skip ? c->uniform_mask : 0;
+    int ch = -1;   // one uniform channel, no loads for it (launch_lw / launch_lat_kd): "_u" + the channel
     if (kind == SCHED_REGIONS && !pl.early && a.zero_offsets && c->wg_waves == 4 && c->split_long == 0 &&
-        (um == 1 || um == 2 || um == 4 || um == 8)) {
-        // one uniform channel, no loads for it (launch_lw): "_u" + the channel
-        static std::string named[kNumLayouts][4];
-        const int ch = um == 1 ? 0 : um == 2 ? 1 : um == 4 ? 2 : 3;
-        if (pl.layout == LAYOUT_COL48 || pl.layout == LAYOUT_BRICK4832 || pl.layout == LAYOUT_CORNERH ||
-            pl.layout == LAYOUT_COL48Z) {
-            std::string& n = named[pl.layout][ch];
-            if (n.empty()) n = std::string(variant_name(pl)) + "_u" + "RGBA"[ch];
-            return n.c_str();
-        }
-    }
-    return variant_name(pl);
+        (um == 1 || um == 2 || um == 4 || um == 8) &&
+        (pl.layout == LAYOUT_COL48 || pl.layout == LAYOUT_BRICK4832 || pl.layout == LAYOUT_CORNERH ||
+         pl.layout == LAYOUT_COL48Z))
+        ch = um == 1 ? 0 : um == 2 ? 1 : um == 4 ? 2 : 3;
+    // the latency-mode march (small frame shares, vr_march_lat.hip) when it is forced on
+    const int lat = kind == SCHED_REGIONS && c->lat > 0 && lat_supported(pl.layout) ? c->lat : 0;
+    if (ch < 0 && lat == 0) return variant_name(pl);
+    // built once, thread-safe (a function-local static): every layout x early x channel x depth
+    struct Names {
+        std::string n[kNumLayouts][2][5][5];
+    };
+    static const Names table = [] {
+        Names t;
+        for (int l = 1; l < kNumLayouts; ++l)
+            for (int e = 0; e < 2; ++e)
+                for (int u = 0; u < 5; ++u)
+                    for (int d = 0; d < 5; ++d) {
+                        std::string v = variant_name(Plan{l, WRAP_CLAMP, e == 1});
+                        if (u > 0) v += std::string("_u") + "RGBA"[u - 1];
+                        if (d > 0) v += "_lat" + std::to_string(d);
+                        t.n[l][e][u][d] = v;
+                    }
+        return t;
+    }();
+    return table.n[pl.layout][pl.early ? 1 : 0][ch + 1][lat].c_str();
 }
 
 // Target pixel (x, packed output row) under the projected box centre: the
@@ -957,6 +1077,71 @@ static int auto_split(const Ctx* c, long long nwork)
     return nwork >= kSplitOneLane ? 1 : nwork >= kSplitTwoLanes ? 2 : 4;
 }
 
+// The lists of the GPU build that last completed (host-mapped header, read
+// once its event is done -- never waited for): tiles with work and the longest
+// list, which size the next launches of the same target.
+static void poll_region_header(Ctx* c)
+{
+    if (!c->rg_pending) return;
+    const hipError_t q = hipEventQuery(c->rg_ev);
+    if (q == hipErrorNotReady) {
+        (void)hipGetLastError();   // not an error: the build is still queued
+        return;
+    }
+    c->rg_pending = false;
+    if (q != hipSuccess) return;
+    Ctx::RegionBuf& rb = c->region[c->rg_buf];
+    rb.nwork = c->h_rghdr[9];
+    rb.most = c->h_rghdr[10];
+}
+
+// Retire the current lists (events on the streams that rendered with them) and
+// pick the other buffer for new ones, sized for n entries.  host_staging: the
+// host will rewrite the pinned staging copy, so it waits for the renders that
+// last used this buffer; otherwise (a GPU build) `stream` waits for them.
+static vr_status next_region_buf(Ctx* c, size_t n, bool host_staging, hipStream_t stream, int* out)
+{
+    if (c->region_cur >= 0) {   // retire the current lists in the stream order of their renders
+        Ctx::RegionBuf& old = c->region[c->region_cur];
+        old.nretired = 0;
+        if (old.nstreams < 0) {
+            HIP_TRY(hipDeviceSynchronize());
+        } else {
+            for (int i = 0; i < old.nstreams; ++i) {
+                if (!old.retired[i]) HIP_TRY(hipEventCreateWithFlags(&old.retired[i], hipEventDisableTiming));
+                HIP_TRY(hipEventRecord(old.retired[i], old.streams[i]));
+            }
+            old.nretired = old.nstreams;
+        }
+        old.nstreams = 0;
+    }
+    const int b = c->region_cur < 0 ? 0 : c->region_cur ^ 1;
+    Ctx::RegionBuf& rb = c->region[b];
+    if (c->rg_pending && c->rg_buf == b) {   // a GPU build into this buffer is still queued
+        HIP_TRY(hipEventSynchronize(c->rg_ev));
+        poll_region_header(c);
+    }
+    for (int i = 0; i < rb.nretired; ++i) {   // its last renders
+        if (host_staging || rb.d == nullptr) HIP_TRY(hipEventSynchronize(rb.retired[i]));
+        else HIP_TRY(hipStreamWaitEvent(stream, rb.retired[i], 0));
+    }
+    rb.nretired = 0;
+    if (n > rb.cap) {
+        if (rb.d) {
+            HIP_TRY(hipStreamSynchronize(stream));   // the stream may have queued work on the old list
+            (void)hipFree(rb.d);
+        }
+        if (rb.h) (void)hipHostFree(rb.h);
+        rb.d = rb.h = nullptr;
+        rb.cap = 0;
+        HIP_TRY(hipMalloc(&rb.d, (n + kRegionHeader) * sizeof(unsigned)));
+        HIP_TRY(hipHostMalloc(&rb.h, (n + kRegionHeader) * sizeof(unsigned), hipHostMallocDefault));
+        rb.cap = n;
+    }
+    *out = b;
+    return VR_OK;
+}
+
 vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow, bool mixable, hipStream_t stream)
 {
     const int tw = (a.width + 7) >> 3, th = (a.out_rows + 7) >> 3;
@@ -970,12 +1155,73 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     for (const float* v : {a.org, a.o, a.px, a.py, a.box_min, a.box_max})
         for (int k = 0; k < 3; ++k) key[kn++] = v[k];
     ++c->renders_since_build;
-    if (c->region_cur >= 0) {
-        if (std::memcmp(key, c->region_key, sizeof key) == 0 ||
-            (c->renders_since_build < kRegionRebuildInterval &&
-             std::memcmp(key, c->region_key, grid_part * sizeof(float)) == 0)) {
-            return note_region_stream(c->region[c->region_cur], stream);
+    poll_region_header(c);
+    const bool same_grid = c->region_cur >= 0 && std::memcmp(key, c->region_key, grid_part * sizeof(float)) == 0;
+    if (same_grid && (std::memcmp(key, c->region_key, sizeof key) == 0 || c->renders_since_build < c->region_interval))
+        return note_region_stream(c->region[c->region_cur], stream);
+
+    const int S = c->supertile;
+    // a moved camera over the same target (no split_long sub-blocks): the
+    // lists come from the GPU build on the render stream (vr_regions.hip) --
+    // no host loop, no host wait; tiles with work and the longest list are
+    // the last completed build's (they size the launch, not the result)
+    if (same_grid && c->region_gpu && !(mixable && c->split_long > 0) && th < 65536 && tw < 65536) {
+        const size_t n = (size_t)tw * th;
+        const Ctx::RegionBuf& cur = c->region[c->region_cur];
+        const int nwork = cur.nwork, most = cur.most;
+        const size_t need = region_build_bytes((int)n);
+        if (need > c->rg_bytes) {
+            if (c->d_rg) {
+                HIP_TRY(hipStreamSynchronize(stream));
+                (void)hipFree(c->d_rg);
+            }
+            c->d_rg = nullptr;
+            c->rg_bytes = 0;
+            HIP_TRY(hipMalloc(&c->d_rg, need));
+            HIP_TRY(hipMemsetAsync(c->d_rg, 0, need, stream));   // the build's counters start at zero
+            c->rg_bytes = need;
         }
+        if (!c->h_rghdr) {
+            HIP_TRY(hipHostMalloc(&c->h_rghdr, kRegionHeader * sizeof(int), hipHostMallocMapped));
+            HIP_TRY(hipEventCreateWithFlags(&c->rg_ev, hipEventDisableTiming));
+        }
+        int b = 0;
+        const vr_status st0 = next_region_buf(c, n, false, stream, &b);
+        if (st0 != VR_OK) return st0;
+        Ctx::RegionBuf& rb = c->region[b];
+        RegionBuild g{};
+        g.tw = tw; g.th = th; g.width = a.width; g.out_rows = a.out_rows;
+        g.band_rows = a.band_rows; g.band_stride = a.band_stride; g.band_first = a.band_first;
+        g.max_steps = a.max_steps; g.step_size = a.step_size;
+        for (int k = 0; k < 3; ++k) {
+            g.org[k] = a.org[k]; g.o[k] = a.o[k]; g.px[k] = a.px[k]; g.py[k] = a.py[k];
+            g.box_min[k] = a.box_min[k]; g.box_max[k] = a.box_max[k];
+        }
+        g.ccx = (cpx + 0.5) / 8.0; g.ccy = (cprow + 0.5) / 8.0;
+        g.ctx = (cpx >> 3) / S; g.cty = (cprow >> 3) / S;
+        g.supertile = S; g.wedges = c->wedges;
+        int* dev_hdr = nullptr;
+        HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&dev_hdr), c->h_rghdr, 0));
+        HIP_TRY(launch_region_build(g, c->d_rg, rb.d + kRegionHeader, reinterpret_cast<int*>(rb.d), dev_hdr, stream));
+        HIP_TRY(hipEventRecord(c->rg_ev, stream));
+        c->rg_pending = true;
+        c->rg_buf = b;
+        ++c->gpu_builds;
+        if (!rb.uploaded) HIP_TRY(hipEventCreateWithFlags(&rb.uploaded, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(rb.uploaded, stream));
+        rb.upload_stream = stream;
+        rb.nwork = nwork;
+        rb.most = most;
+        rb.map = TileMap{};
+        rb.map.nwx = std::max(1, (most + tpw - 1) / tpw);
+        rb.mixed = 0;
+        rb.nstreams = 0;
+        const vr_status st = note_region_stream(rb, stream);
+        if (st != VR_OK) return st;
+        c->region_cur = b;
+        std::memcpy(c->region_key, key, sizeof key);
+        c->renders_since_build = 0;
+        return VR_OK;
     }
 
     // a3 step estimate of the ray through pixel-corner (fx, fy) of the packed target
@@ -1006,7 +1252,6 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     // one workgroup, on one CU -- are a compact block sharing the CU's L1
     struct T { unsigned id; double cost, ang; int ring, sub; };
     std::vector<T> work, idle;
-    const int S = c->supertile;
     const double ccx = (cpx + 0.5) / 8.0, ccy = (cprow + 0.5) / 8.0;
     const int ctx = (cpx >> 3) / S, cty = (cprow >> 3) / S;
     for (int ty = 0; ty < th; ++ty)
@@ -1049,53 +1294,37 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     size_t n = (size_t)tw * th;
     if (mixed)
         for (const T& t : work) n += (size_t)(t.cost >= split_at) * (size_t)(ks - 1);
-    if (c->region_cur >= 0) {   // retire the current lists in the stream order of their renders
-        Ctx::RegionBuf& old = c->region[c->region_cur];
-        old.nretired = 0;
-        if (old.nstreams < 0) {
-            HIP_TRY(hipDeviceSynchronize());
-        } else {
-            for (int i = 0; i < old.nstreams; ++i) {
-                if (!old.retired[i]) HIP_TRY(hipEventCreateWithFlags(&old.retired[i], hipEventDisableTiming));
-                HIP_TRY(hipEventRecord(old.retired[i], old.streams[i]));
-            }
-            old.nretired = old.nstreams;
-        }
-        old.nstreams = 0;
-    }
-    const int b = c->region_cur < 0 ? 0 : c->region_cur ^ 1;
+    int b = 0;
+    const vr_status st0 = next_region_buf(c, n, true, stream, &b);
+    if (st0 != VR_OK) return st0;
     Ctx::RegionBuf& rb = c->region[b];
-    for (int i = 0; i < rb.nretired; ++i) HIP_TRY(hipEventSynchronize(rb.retired[i]));   // its last renders
-    rb.nretired = 0;
-    if (n > rb.cap) {
-        if (rb.d) (void)hipFree(rb.d);
-        if (rb.h) (void)hipHostFree(rb.h);
-        rb.d = rb.h = nullptr;
-        rb.cap = 0;
-        HIP_TRY(hipMalloc(&rb.d, n * sizeof(unsigned)));
-        HIP_TRY(hipHostMalloc(&rb.h, n * sizeof(unsigned), hipHostMallocDefault));
-        rb.cap = n;
-    }
     TileMap m{};
     size_t pos = 0, most = 0;
+    unsigned* list = rb.h + kRegionHeader;
     for (int x = 0; x < 8; ++x) {
         m.off[x] = (int)pos;
         for (const T& t : xl[x]) {
             if (mixed && t.cost >= split_at) {
-                for (int s = 0; s < mixed; ++s) rb.h[pos++] = t.id | 0x80000000u | ((unsigned)s << 29);
+                for (int q = 0; q < mixed; ++q) list[pos++] = t.id | 0x80000000u | ((unsigned)q << 29);
             } else {
-                rb.h[pos++] = t.id;
+                list[pos++] = t.id;
             }
         }
         most = std::max(most, pos - (size_t)m.off[x]);
     }
     m.off[8] = (int)pos;
     m.nwx = std::max(1, (int)((most + tpw - 1) / tpw));
-    HIP_TRY(hipMemcpyAsync(rb.d, rb.h, n * sizeof(unsigned), hipMemcpyHostToDevice, stream));
+    int* hdr = reinterpret_cast<int*>(rb.h);
+    for (int x = 0; x < 9; ++x) hdr[x] = m.off[x];
+    hdr[9] = (int)work.size();
+    hdr[10] = (int)most;
+    hdr[11] = (int)pos;
+    HIP_TRY(hipMemcpyAsync(rb.d, rb.h, (n + kRegionHeader) * sizeof(unsigned), hipMemcpyHostToDevice, stream));
     if (!rb.uploaded) HIP_TRY(hipEventCreateWithFlags(&rb.uploaded, hipEventDisableTiming));
     HIP_TRY(hipEventRecord(rb.uploaded, stream));
     rb.upload_stream = stream;
     rb.map = m;
+    rb.most = (int)most;
     rb.nwork = (int)work.size();
     rb.mixed = mixed;
     rb.nstreams = 0;
@@ -1133,6 +1362,9 @@ static vr_status ensure_lattice(Ctx* c, ProcParams* q, hipStream_t s)
         c->lat_key[2] = -1;
         if (bytes > c->lat_cap) {
             if (c->d_lat) (void)hipFree(c->d_lat);
+    if (c->d_rg) (void)hipFree(c->d_rg);
+    if (c->h_rghdr) (void)hipHostFree(c->h_rghdr);
+    if (c->rg_ev) (void)hipEventDestroy(c->rg_ev);
             c->d_lat = nullptr;
             c->lat_cap = 0;
             if (hipMalloc(&c->d_lat, bytes) != hipSuccess) return fail(VR_ERR_OOM, "vr_render: lattice table");
@@ -1152,56 +1384,142 @@ static vr_status ensure_lattice(Ctx* c, ProcParams* q, hipStream_t s)
     return VR_OK;
 }
 
-// Scratch of the deferred shadow passes (ShadowDefer) for this frame shape:
+// Scratch of the deferred shadow passes (ShadowDefer), sized from the frame:
 // [chunk count | per-wave step counts, entry counts, first chunks | chunk map |
-// per-wave step records | per-wave entry regions].  A sorted wave marches at
-// most max_steps wave-steps and appends at most 64 entries per step, so its
-// region of 64 * max_steps entries cannot overflow (4.2 GB at 1080p x 128 on a
-// 288 GB device).
-// *ok = false (and VR_OK): the frame needs more scratch than shadow_defer_mib, or
-// the allocation failed -- the render then takes the in-wave compaction (or the
-// per-lane shadow loop), which needs none.
-static vr_status ensure_defer(Ctx* c, const MarchArgs& a, ShadowDefer* d, bool* ok)
+// step records | entries].  Sorted wave w owns the entries [went[w],
+// went[w+1]) and step records [wrec[w], wrec[w+1]) that proc_scan lays out
+// from the cost histogram (the sum of its lanes' step-count bounds), so a
+// frame needs about its executed lane-steps of entries: 16.7 M (0.27 GB) at
+// 1080p x 128 where the old per-wave worst case (64 x max_steps) took 4.2 GB.
+// The capacity follows the largest need seen (written by every sorting frame
+// into host-mapped memory, read once its event has completed: no host wait),
+// x 5/4; before one is known it starts at pixels x max_steps / 16 entries.
+// A wave beyond the capacity marches its shadow rays in place, so a frame
+// larger than the scratch is still exact, and the next one gets more.
+// Growing keeps the outgrown buffer until a later device sync (queued frames
+// on other streams may still use it): vr_render never waits for the device.
+// *ok = false (and VR_OK): no usable scratch (shadow_defer_mib too small, or
+// the allocation failed) -- the render then takes the in-wave compaction.
+static vr_status release_defer(Ctx* c)
+{
+    if (!c->d_defer && c->defer_retired.empty()) return VR_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipDeviceSynchronize());   // an option change, not a frame: queued renders may use the scratch
+    if (c->d_defer) (void)hipFree(c->d_defer);
+    for (void* q : c->defer_retired) (void)hipFree(q);
+    c->defer_retired.clear();
+    c->d_defer = nullptr;
+    c->defer_bytes = 0;
+    c->defer_ent_cap = 0;
+    c->defer_rec_cap = 0;
+    c->defer_waves = 0;
+    c->want_ent = c->want_rec = 0.0;
+    return VR_OK;
+}
+
+static vr_status ensure_defer(Ctx* c, const MarchArgs& a, void* sort_buf, ShadowDefer* d, bool* ok)
 {
     *ok = false;
-    const size_t pixels = (size_t)a.width * (size_t)a.out_rows;
-    const size_t waves = (pixels + 255) / 256 * 4;   // the sorted march: 256-thread blocks of 4 waves
-    const size_t stride = (size_t)std::max(a.max_steps, 1);
-    auto up = [](size_t v) { return (v + 255) & ~(size_t)255; };
-    const size_t off_ws = 256, off_wc = up(off_ws + waves * 4), off_wk = up(off_wc + waves * 4);
-    const size_t off_map = up(off_wk + waves * 4);
-    const size_t off_rec = up(off_map + waves * stride * sizeof(uint4));   // <= stride chunks per wave
-    const size_t off_ent = up(off_rec + waves * stride * sizeof(uint4));
-    const size_t need = off_ent + waves * 64 * stride * sizeof(float4);
-    if (waves * stride >= (1ull << 32) || need > ((size_t)c->shadow_defer_mib << 20)) return VR_OK;
-    if (need > c->defer_bytes) {
-        HIP_TRY(hipDeviceSynchronize());   // queued work on another stream may still read the old one
-        if (c->d_defer) (void)hipFree(c->d_defer);
-        c->d_defer = nullptr;
-        c->defer_bytes = 0;
-        if (hipMalloc(&c->d_defer, need) != hipSuccess) {
-            (void)hipGetLastError();   // clear the sticky allocation error
-            return VR_OK;
-        }
-        c->defer_bytes = need;
+    if (c->shadow_defer_mib == 0) return VR_OK;
+    const SortLayout L = sort_layout(a.width, a.out_rows);
+    const unsigned long long pixels = (unsigned long long)a.width * (unsigned long long)a.out_rows;
+    if (!c->h_need) {
+        HIP_TRY(hipHostMalloc(&c->h_need, 2 * sizeof(unsigned long long), hipHostMallocMapped));
+        HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->d_need), c->h_need, 0));
+        HIP_TRY(hipEventCreateWithFlags(&c->need_ev, hipEventDisableTiming));
     }
+    if (c->need_pending) {   // the last sorting frame's need, if it has run
+        const hipError_t q = hipEventQuery(c->need_ev);
+        if (q == hipSuccess) {
+            c->need_pending = false;
+            c->want_ent = std::max(c->want_ent, 1.25 * (double)c->h_need[0] / c->need_pixsteps);
+            c->want_rec = std::max(c->want_rec, 1.25 * (double)c->h_need[1] / c->need_wavesteps);
+        } else if (q == hipErrorNotReady) {
+            (void)hipGetLastError();   // not an error: the frame is still queued
+        } else {
+            return fail(VR_ERR_HIP, "vr_render: need event: %s", hipGetErrorString(q));
+        }
+    }
+    const unsigned long long steps = (unsigned long long)std::max(a.max_steps, 1);
+    constexpr unsigned long long kMaxCap = 0xffff0000ull;   // entry / record indices stay 32-bit
+    const double pixsteps = (double)pixels * (double)steps, wavesteps = (double)L.waves * (double)steps;
+    unsigned long long ent = (unsigned long long)std::min(4.0e9, pixsteps * std::max(c->want_ent, 1.0 / 12.0));
+    unsigned long long rec = (unsigned long long)std::min(4.0e9, wavesteps * std::max(c->want_rec, 0.125));
+    ent = std::max(ent, 4096ull);
+    rec = std::max(rec, 1024ull);
+    if (c->defer_entries) ent = c->defer_entries;   // test override
+    auto up = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    struct Off { size_t ws, wc, wk, map, rec, ent, bytes; };
+    auto layout = [&](unsigned long long e, unsigned long long r, unsigned w) {
+        Off o{};
+        o.ws = 256;
+        o.wc = up(o.ws + (size_t)w * 4);
+        o.wk = up(o.wc + (size_t)w * 4);
+        o.map = up(o.wk + (size_t)w * 4);
+        o.rec = up(o.map + (size_t)(e / 64 + w) * sizeof(uint4));
+        o.ent = up(o.rec + (size_t)r * sizeof(uint4));
+        o.bytes = o.ent + (size_t)e * sizeof(float4);
+        return o;
+    };
+    const unsigned waves = std::max(L.waves, c->defer_waves);
+    const bool fits = c->d_defer && L.waves <= c->defer_waves && rec <= c->defer_rec_cap &&
+                      (c->defer_entries ? ent == c->defer_ent_cap : ent <= c->defer_ent_cap);
+    if (!fits) {
+        if (c->d_defer && !c->defer_entries) {   // grow by at least 1/4: a slowly growing need reallocates rarely
+            ent = std::max(ent, c->defer_ent_cap + c->defer_ent_cap / 4);
+            rec = std::max(rec, (unsigned long long)c->defer_rec_cap + c->defer_rec_cap / 4);
+        }
+        ent = std::min(ent, kMaxCap);
+        rec = std::min(rec, kMaxCap);
+        const size_t limit = (size_t)c->shadow_defer_mib << 20;
+        if (layout(ent, rec, waves).bytes > limit) {   // fewer entries: the last waves march in place
+            const size_t base = layout(0, rec, waves).bytes + 256;
+            ent = base < limit ? (limit - base) / (sizeof(float4) + sizeof(uint4) / 64 + 1) : 0;
+        }
+        void* nb = nullptr;
+        const Off o = layout(ent, rec, waves);
+        if (ent < 4096 || o.bytes > limit || hipMalloc(&nb, o.bytes) != hipSuccess) {
+            (void)hipGetLastError();   // clear an allocation error; keep what there is
+            if (!c->d_defer || L.waves > c->defer_waves) return VR_OK;
+        } else {
+            if (c->d_defer) {
+                c->defer_retired.push_back(c->d_defer);
+                if (c->defer_retired.size() > kMaxDeferRetired) {   // rare: a device sync frees them
+                    HIP_TRY(hipDeviceSynchronize());
+                    for (void* q : c->defer_retired) (void)hipFree(q);
+                    c->defer_retired.clear();
+                }
+            }
+            c->d_defer = nb;
+            c->defer_bytes = o.bytes;
+            c->defer_ent_cap = ent;
+            c->defer_rec_cap = (unsigned)rec;
+            c->defer_waves = waves;
+        }
+    }
+    const Off o = layout(c->defer_ent_cap, c->defer_rec_cap, c->defer_waves);
     *ok = true;
     char* b = static_cast<char*>(c->d_defer);
+    char* sb = static_cast<char*>(sort_buf);
     d->count = reinterpret_cast<unsigned*>(b);
-    d->wsteps = reinterpret_cast<unsigned*>(b + off_ws);
-    d->wcount = reinterpret_cast<unsigned*>(b + off_wc);
-    d->wchunk = reinterpret_cast<unsigned*>(b + off_wk);
-    d->map = reinterpret_cast<uint4*>(b + off_map);
-    d->rec = reinterpret_cast<uint4*>(b + off_rec);
-    d->ent = reinterpret_cast<float4*>(b + off_ent);
-    d->rec_stride = (unsigned)stride;
-    d->waves = (unsigned)waves;
+    d->wsteps = reinterpret_cast<unsigned*>(b + o.ws);
+    d->wcount = reinterpret_cast<unsigned*>(b + o.wc);
+    d->wchunk = reinterpret_cast<unsigned*>(b + o.wk);
+    d->map = reinterpret_cast<uint4*>(b + o.map);
+    d->rec = reinterpret_cast<uint4*>(b + o.rec);
+    d->ent = reinterpret_cast<float4*>(b + o.ent);
+    d->went = reinterpret_cast<const unsigned long long*>(sb + L.went);
+    d->wrec = reinterpret_cast<const unsigned*>(sb + L.wrec);
+    d->ent_cap = c->defer_ent_cap;
+    d->rec_cap = c->defer_rec_cap;
+    d->map_cap = (unsigned)(c->defer_ent_cap / 64 + c->defer_waves);
+    d->waves = L.waves;
     // the shadow pass's grid: ~2-3 chunks per wave rather than one persistent
     // round (1,536 workgroups at 6 per CU), so the hardware dispatcher balances
     // the tail -- 3/8 of the sorted waves measured 0.90-0.91 ms against 0.98 at
     // config 3 (profiles/r03/ab_shadow_blocks_*.txt)
     d->eval_blocks = c->shadow_blocks ? (unsigned)c->shadow_blocks
-                                      : (unsigned)std::max<size_t>(kShadowEvalBlocks, waves * 3 / 8);
+                                      : (unsigned)std::max<size_t>(kShadowEvalBlocks, (size_t)L.waves * 3 / 8);
     return VR_OK;
 }
 
@@ -1315,12 +1633,12 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
         // schedule 0 = one 8x8 tile per wave in row order, 4 = in rings;
         // otherwise (auto) the cost-sorted schedule
         void* sort_buf = nullptr;
-        Schedule sc{c->schedule == SCHED_RINGS ? SCHED_RINGS : SCHED_STATIC, 0, 0, 1, 1, nullptr, nullptr, {}, 1, 0, 0, 4};
+        Schedule sc{c->schedule == SCHED_RINGS ? SCHED_RINGS : SCHED_STATIC, 0, 0, 1, 1, nullptr, nullptr, {}, 1, 0, 0, 4, 0, nullptr};
         if (sc.kind == SCHED_RINGS) box_centre_pixel(c, a, &sc.center_x, &sc.center_y);
         // the sort passes enumerate whole 64x64 regions (vr_march_kernels.h sort_pixel)
         if (c->schedule != SCHED_STATIC && c->schedule != SCHED_RINGS && a.width < 65536 && a.out_rows < 65536 &&
             (long long)((a.width + 63) / 64) * ((a.out_rows + 63) / 64) * 4096 < (1ll << 31)) {
-            const size_t need = proc_sort_bytes(a.width, a.out_rows);
+            const size_t need = sort_layout(a.width, a.out_rows).bytes;
             if (need > c->sort_bytes) {
                 // the old buffer may still be read by queued work on another stream
                 HIP_TRY(hipDeviceSynchronize());
@@ -1357,14 +1675,24 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
         ShadowDefer defer{};
         bool use_defer = sort_buf && c->shadow_defer && a.proc.shadow_steps > 0 && a.proc.wt_fixed &&
                          a.proc.wt_n > 0;
+        // a stale order's keys do not bound the new step counts: no deferred ranges
+        if (reuse == SORT_STALE) use_defer = false;
         if (use_defer) {
-            const vr_status st = ensure_defer(c, a, &defer, &use_defer);
+            const vr_status st = ensure_defer(c, a, sort_buf, &defer, &use_defer);
             if (st != VR_OK) return st;
         }
         std::vector<float> built = reuse == SORT_BUILD ? key : c->sort_key;
         c->sort_key.clear();   // valid again only once this launch is queued
+        const bool report = use_defer && reuse == SORT_BUILD;   // proc_scan writes the frame's need
         HIP_TRY(launch_march_procedural(a, m.early_out > 0.0f, sort_buf, reuse, sc, static_cast<hipStream_t>(stream),
-                                        use_defer ? &defer : nullptr));
+                                        use_defer ? &defer : nullptr, report ? c->d_need : nullptr));
+        if (report) {
+            HIP_TRY(hipEventRecord(c->need_ev, static_cast<hipStream_t>(stream)));
+            c->need_pending = true;
+            c->need_pixsteps = (double)a.width * (double)a.out_rows * (double)std::max(a.max_steps, 1);
+            c->need_wavesteps = (double)sort_layout(a.width, a.out_rows).waves * (double)std::max(a.max_steps, 1);
+        }
+        c->defer_last = use_defer ? 1 : 0;
         c->sort_key = std::move(built);
         c->renders_since_sort = reuse == SORT_STALE ? c->renders_since_sort + 1 : 0;
         return VR_OK;
@@ -1373,7 +1701,7 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
     // wedges of the frame, each walked inside-out (longest rays first)
     const int kind = c->schedule >= 0 ? c->schedule : SCHED_REGIONS;
     const int tpw = c->tiles_per_wave > 0 ? c->tiles_per_wave : (kind == SCHED_RINGS || kind == SCHED_REGIONS ? 2 : 1);
-    Schedule sc{kind, 0, 0, tpw, c->waves_per_simd, c->d_heads, nullptr, {}, 1, 0, 0, c->wg_waves};
+    Schedule sc{kind, 0, 0, tpw, c->waves_per_simd, c->d_heads, nullptr, {}, 1, 0, 0, c->wg_waves, 0, nullptr};
     sc.slab = pl.layout == LAYOUT_COL48 && c->slab;
     a.slab_cap = c->slab_cap;
     if (kind == SCHED_RINGS || kind == SCHED_REGIONS) box_centre_pixel(c, a, &sc.center_x, &sc.center_y);
@@ -1386,19 +1714,26 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
                                            static_cast<hipStream_t>(stream));
         if (st != VR_OK) return st;
         const Ctx::RegionBuf& rb = c->region[c->region_cur];
-        sc.tiles = rb.d;
+        sc.tiles = rb.d + kRegionHeader;
+        sc.hdr = reinterpret_cast<const int*>(rb.d);
         sc.map = rb.map;
         sc.mixed = rb.mixed;
         // step-split rays: K lanes per ray when the frame
         // share is too small to fill the GPU with one-lane-per-ray waves
-        if (splittable && !rb.mixed) {
+        if (c->lat > 0 && lat_supported(pl.layout) && !sc.slab && !rb.mixed) {
+            // latency-mode march (vr_march_lat.hip): K lanes per ray, c->lat rounds of loads in flight
+            const int K = c->split > 0 ? c->split : auto_split(c, rb.nwork);
+            const int most = rb.most;
+            sc.lat = c->lat;
+            sc.split = K;
+            sc.map.nwx = std::max(1, (most * K + tpw - 1) / tpw);
+        } else if (splittable && !rb.mixed) {
             int K = c->split;
             if (sc.slab) K = K == 0 ? 1 : K;   // the slab march has one lane per ray; split > 1 uses the plain march
             if (K == 0) K = auto_split(c, rb.nwork);
             if (K > 1) {
                 const int ktpw = tpw;
-                int most = 0;
-                for (int x = 0; x < 8; ++x) most = std::max(most, rb.map.off[x + 1] - rb.map.off[x]);
+                const int most = rb.most;
                 sc.split = K;
                 sc.map.nwx = std::max(1, (most * K + ktpw - 1) / ktpw);
             }

@@ -208,6 +208,25 @@ struct TileMap {
     int off[9];
     int nwx;
 };
+// The regions schedule's lists in device memory: a header of kRegionHeader
+// ints -- off[0..8] (XCD x renders list entries [off[x], off[x+1])), tiles
+// with estimated work, the longest list, tiles -- then the entries.  Built on
+// the host (vr_api.cpp build_regions) or, for a moving camera, on the GPU
+// (vr_regions.hip launch_region_build, the same dealing).
+constexpr int kRegionHeader = 16;
+struct RegionBuild {
+    int tw, th, width, out_rows, band_rows, band_stride, band_first, max_steps;
+    float step_size;
+    float org[3], o[3], px[3], py[3], box_min[3], box_max[3];
+    double ccx, ccy;       // box-centre tile (fractional), S x S block of it
+    int ctx, cty;
+    int supertile, wedges;
+};
+size_t region_build_bytes(int ntiles);
+// h_hdr (optional, host-mapped): a copy of the header, for sizing later launches
+hipError_t launch_region_build(const RegionBuild& b, void* scratch, unsigned* d_list, int* d_hdr, int* h_hdr,
+                               hipStream_t s);
+
 struct Schedule {
     int kind;
     int center_x, center_y;   // rings: target pixel under the projected box centre
@@ -220,21 +239,47 @@ struct Schedule {
     int slab;              // regions + COL48: the LDS slab march (vr_march_slab.hip)
     int mixed;             // regions: 2 or 4 = the list holds that many sub-blocks of each longest tile (march_regions_mixed)
     int wg_waves;          // regions (one lane per ray): waves per workgroup, 4 (default), 8 or 16
+    int lat;               // regions: latency-mode march (vr_march_lat.hip), rounds of loads in flight (0 = off)
+    const int* hdr;        // regions: the lists' device header (kRegionHeader; off[x] per XCD)
 };
 
-// Deferred shadow rays (vr_march_kernels.h march_proc_defer): device scratch
+// Cost-sort scratch of the procedural march (vr_march.hip launch_march_procedural),
+// byte offsets for a target of width x out_rows: the key histogram, the bin
+// cursors, the sorted order, the keys per enumerated position, and for the
+// deferred shadow passes the per-sorted-wave first entry / first step record
+// (proc_scan; waves + 1 entries each) and the frame's totals (need[0] entries,
+// need[1] step records).
+struct SortLayout {
+    size_t hist, cursor, order, keys, went, wrec, need, bytes;
+    unsigned waves;   // sorted waves a frame can have: ceil(pixels / 64)
+};
+SortLayout sort_layout(int width, int out_rows);
+
+// Deferred shadow rays (vr_march_kernels.h march_proc_defer): device scratch,
+// sized from the frame (vr_api.cpp ensure_defer).  Sorted wave w appends at most
+// went[w + 1] - went[w] entries (the sum of its lanes' step counts, bounded by
+// their cost keys) and marches at most wrec[w + 1] - wrec[w] wave-steps (its
+// first lane's key); proc_scan computes both prefixes from the cost histogram.
+// A wave whose range lies beyond the capacities marches its shadow rays in
+// place (march_pixel_proc) and is skipped by the later passes, so any capacity
+// gives the exact frame.
 struct ShadowDefer {
     unsigned* count;      // [0]: chunks of 64 entries this frame (written by proc_shadow_scan)
-    unsigned* wsteps;     // per sorted wave: wave-steps marched
-    unsigned* wcount;     // per sorted wave: entries appended (dense in the wave's own region)
+    unsigned* wsteps;     // per sorted wave: wave-steps marched; kDeferInPlace = its shadow rays were marched in place
+    unsigned* wcount;     // per sorted wave: entries appended (dense from went[w])
     unsigned* wchunk;     // per sorted wave: its first chunk (exclusive prefix of ceil(wcount / 64))
-    uint4* map;           // per chunk: {wave, chunk of the wave, entries in it, 0}
-    uint4* rec;           // per sorted wave, rec_stride per wave: {wave-local first entry, lane mask lo, hi, 0}
-    float4* ent;          // entries (P, coef), region of wave w at w * 64 * rec_stride; pass 2 rewrites .xy as (coef, tl)
-    unsigned rec_stride;  // wave-steps per wave: max_steps bounds them
-    unsigned waves;       // sorted waves the scratch holds
-    unsigned eval_blocks; // workgroups of the shadow pass (0 = kShadowEvalBlocks)
+    uint4* map;           // per chunk: {index of its first entry, 0, entries in it, 0}
+    uint4* rec;           // step records {wave-local first entry, lane mask lo, hi, 0}, wave w's from wrec[w]
+    float4* ent;          // entries (P, coef), wave w's from went[w]; pass 2 rewrites .xy as (coef, tl)
+    const unsigned long long* went;   // sort buffer (SortLayout::went)
+    const unsigned* wrec;             // sort buffer (SortLayout::wrec)
+    unsigned long long ent_cap;       // entries the scratch holds (< 2^32)
+    unsigned rec_cap;                 // step records it holds
+    unsigned map_cap;                 // chunk map entries (ent_cap / 64 + waves)
+    unsigned waves;                   // sorted waves the per-wave arrays hold
+    unsigned eval_blocks;             // workgroups of the shadow pass (0 = kShadowEvalBlocks)
 };
+constexpr unsigned kDeferInPlace = 0xffffffffu;
 
 // launchers (vr_march.hip / vr_volume.hip); return hipError_t
 hipError_t launch_march(const MarchArgs& a, int layout, int wrap, bool early, const Schedule& sc, hipStream_t s);
@@ -249,21 +294,27 @@ hipError_t launch_assemble_grey(const uint8_t* d_gathered, size_t rows_per_rank,
                                 int band_rows, bool f32, uint8_t* d_frame, hipStream_t s);
 hipError_t launch_march_corner8(const MarchArgs& a, int layout, bool early, const Schedule& sc,
                                 hipStream_t s);   // CORNER8 / CORNERH, vr_march_c8.hip
+// latency-mode march for small frame shares (vr_march_lat.hip): sc.split lanes per
+// ray, sc.lat rounds of loads in flight; lat_supported(layout) says which layouts
+hipError_t launch_march_lat(const MarchArgs& a, int layout, bool early, const Schedule& sc, hipStream_t s);
+bool lat_supported(int layout);
 hipError_t launch_march_slab(const MarchArgs& a, bool early, const Schedule& sc, hipStream_t s);   // vr_march_slab.hip
 constexpr int kSlabMaxChunks = 32;   // per channel and wave (64 B each): 8 KiB of LDS per wave
-// sort_buf (proc_sort_bytes) selects the cost-sorted schedule; null = 8x8
+// sort_buf (sort_layout) selects the cost-sorted schedule; null = 8x8
 // tiles, in rings when sc.kind == SCHED_RINGS, else in row order
 // reuse_sort (vr_api.cpp sort key): SORT_BUILD = sort this frame; SORT_REUSE =
 // sort_buf holds the order of a frame with the same geometry (skip the sort
 // passes, write the background only); SORT_STALE = the order of an older camera
 // with the same target (skip the sort passes, march the pixels it left out too)
 enum { SORT_BUILD = 0, SORT_REUSE = 1, SORT_STALE = 2 };
+// need_host (optional, host-mapped, 2 entries): a frame that sorts with shadow rays
+// writes there the deferred scratch it needs (entries, step records; ensure_defer)
 hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_buf, int reuse_sort, const Schedule& sc,
-                                   hipStream_t s, const ShadowDefer* defer = nullptr);
+                                   hipStream_t s, const ShadowDefer* defer = nullptr,
+                                   unsigned long long* need_host = nullptr);
 // blocks of the deferred shadow pass (proc_shadow_eval), at least: a grid-stride loop over
 // the chunks (vr_api.cpp ensure_defer sizes the grid from the frame)
 constexpr unsigned kShadowEvalBlocks = 256 * 6;
-size_t proc_sort_bytes(int width, int out_rows);
 hipError_t launch_repack(const uint8_t* d_rgba, int nx, int ny, int nz, uint8_t* d_planar, hipStream_t s);
 // Build a fast layout from the planar planes.
 hipError_t launch_build_layout(int layout, const uint8_t* d_planar, int nx, int ny, int nz, uint8_t* d_out,
@@ -287,6 +338,8 @@ hipError_t launch_assemble(const uint8_t* d_gathered, size_t rows_per_rank, int 
                            int width, int height, int band_rows, int bpp, uint8_t* d_frame,
                            hipStream_t s);
 int noise_partials_needed(int nx, int ny, int nz);
+// 16-B-per-lane grid-stride copy of `bytes` (a multiple of 16): the measured HBM roofline
+hipError_t launch_stream_copy(const void* src, void* dst, size_t bytes, hipStream_t s);
 // variant 0..2 = noise::cell_inv_a..c, 3 = the sequence cellular() uses
 hipError_t launch_selftest_cell_inv(int variant, unsigned long long* d_bad, hipStream_t s);
 // noise::cellular_table9 (pruned) vs noise::cellular on 2^23 points per seed

@@ -14,27 +14,41 @@
 
 namespace vr {
 
-size_t proc_sort_bytes(int width, int out_rows)
+SortLayout sort_layout(int width, int out_rows)
 {
     // hist, cursor (+ total), order (u32 per pixel), keys (u16 per enumerated
-    // position: whole 64x64 regions, kSortRegion)
+    // position: whole 64x64 regions, kSortRegion), then the deferred shadow
+    // passes' per-wave prefixes (proc_scan) and the frame's totals
+    auto up = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    SortLayout L{};
+    const size_t pixels = (size_t)width * (size_t)out_rows;
     const size_t regions = (size_t)((width + kSortRegion - 1) / kSortRegion) * ((out_rows + kSortRegion - 1) / kSortRegion);
-    return (size_t)(2 * kKeyBins + 64) * sizeof(unsigned) + (size_t)width * (size_t)out_rows * 4u +
-           regions * kSortRegion * kSortRegion * 2u;
+    L.waves = (unsigned)((pixels + 63) / 64);
+    L.hist = 0;
+    L.cursor = kKeyBins * sizeof(unsigned);
+    L.order = (size_t)(2 * kKeyBins + 64) * sizeof(unsigned);
+    L.keys = L.order + pixels * 4u;
+    L.went = up(L.keys + regions * kSortRegion * kSortRegion * 2u);
+    L.wrec = up(L.went + ((size_t)L.waves + 1) * sizeof(unsigned long long));
+    L.need = up(L.wrec + ((size_t)L.waves + 1) * sizeof(unsigned));
+    L.bytes = L.need + 2 * sizeof(unsigned long long);
+    return L;
 }
 
 hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_buf, int reuse_sort, const Schedule& sc,
-                                   hipStream_t s, const ShadowDefer* defer)
+                                   hipStream_t s, const ShadowDefer* defer, unsigned long long* need_host)
 {
     if (a.width <= 0 || a.out_rows <= 0) return hipSuccess;
     const bool shadow = a.proc.shadow_steps > 0;
     const size_t wt_bytes =
         a.proc.wt_n > 0 ? ((size_t)a.proc.wt_n * a.proc.wt_pz + 512) * sizeof(float4) : 0;
     if (sort_buf) {
-        unsigned* hist = static_cast<unsigned*>(sort_buf);
-        unsigned* cursor = hist + kKeyBins;            // kKeyBins + 1 entries
-        unsigned* order = hist + 2 * kKeyBins + 64;
-        unsigned short* keys = reinterpret_cast<unsigned short*>(order + (size_t)a.width * a.out_rows);
+        const SortLayout L = sort_layout(a.width, a.out_rows);
+        char* sb = static_cast<char*>(sort_buf);
+        unsigned* hist = reinterpret_cast<unsigned*>(sb + L.hist);
+        unsigned* cursor = reinterpret_cast<unsigned*>(sb + L.cursor);   // kKeyBins + 1 entries
+        unsigned* order = reinterpret_cast<unsigned*>(sb + L.order);
+        unsigned short* keys = reinterpret_cast<unsigned short*>(sb + L.keys);
         // hist is all zero here: zeroed when the buffer was allocated, and by
         // the previous frame's proc_scan after it read it
         const long long pixels = (long long)a.width * a.out_rows;
@@ -46,7 +60,16 @@ hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_bu
         if (reuse_sort == SORT_BUILD) {
             if (shadow) hipLaunchKernelGGL((proc_bin<true>), g1, dim3(256), 0, s, a, hist, keys);
             else hipLaunchKernelGGL((proc_bin<false>), g1, dim3(256), 0, s, a, hist, keys);
-            hipLaunchKernelGGL(proc_scan, dim3(1), dim3(kKeyBins), 0, s, hist, cursor);
+            // with shadow rays proc_scan also lays out the deferred passes' per-wave ranges
+            ScanOut so{};
+            if (shadow) {
+                so.went = reinterpret_cast<unsigned long long*>(sb + L.went);
+                so.wrec = reinterpret_cast<unsigned*>(sb + L.wrec);
+                so.need = reinterpret_cast<unsigned long long*>(sb + L.need);
+                so.need_host = need_host;
+                so.max_steps = a.max_steps;
+            }
+            hipLaunchKernelGGL(proc_scan, dim3(1), dim3(kKeyBins), 0, s, hist, cursor, so);
             hipLaunchKernelGGL(proc_scatter, g1, dim3(256), 0, s, a, keys, cursor, order);
         }
         // the scatter advanced cursor[k] to the end of key k; total stays at cursor[kKeyBins]
@@ -125,6 +148,8 @@ hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_bu
 hipError_t launch_march(const MarchArgs& a, int layout, int wrap, bool early, const Schedule& sc, hipStream_t s)
 {
     if (a.width <= 0 || a.out_rows <= 0) return hipSuccess;
+    if (sc.kind == SCHED_REGIONS && sc.lat > 0 && lat_supported(layout))
+        return launch_march_lat(a, layout, early, sc, s);   // vr_march_lat.hip
     switch (layout) {
     case LAYOUT_BRICK4: return launch_lw<LAYOUT_BRICK4, WRAP_CLAMP>(a, early, sc, s);
     case LAYOUT_BRICK448: return launch_lw<LAYOUT_BRICK448, WRAP_CLAMP>(a, early, sc, s);

@@ -930,12 +930,12 @@ __global__ __launch_bounds__(kThreads) void march_rings(const MarchArgs a, int c
 // WGW waves per workgroup (option wg_waves): the waves of one workgroup run on
 // one CU and share its L1, and they render consecutive list entries.
 template <int LAYOUT, int WRAP, bool EARLY, bool ZO, int WGW, int UM>
-__device__ __forceinline__ void regions_body(const MarchArgs& a, const unsigned* __restrict__ tiles, const TileMap& m,
+__device__ __forceinline__ void regions_body(const MarchArgs& a, const unsigned* __restrict__ tiles, const int* __restrict__ hdr, int nwx,
                                              unsigned* lds)
 {
     const int xcd = blockIdx.x & 7;
     const int w = (int)(blockIdx.x >> 3) * WGW + (threadIdx.x >> 6);
-    const int begin = m.off[xcd], count = m.off[xcd + 1] - begin;
+    const int begin = hdr[xcd], count = hdr[xcd + 1] - begin;
     if ((int)(blockIdx.x >> 3) * WGW >= count) return;   // whole workgroup, before the barrier
 #ifdef VR_TIMELINE
     const unsigned long long t_begin = __builtin_amdgcn_s_memrealtime();
@@ -943,7 +943,7 @@ __device__ __forceinline__ void regions_body(const MarchArgs& a, const unsigned*
     const FastCtx f = fast_prologue<LAYOUT>(a, lds);
     const int lane = threadIdx.x & 63;
     unsigned long long steps = 0;
-    for (int k = w; w < m.nwx && k < count; k += m.nwx) {   // the grid rounds nwx up to whole workgroups
+    for (int k = w; w < nwx && k < count; k += nwx) {   // the grid rounds nwx up to whole workgroups
         const unsigned t = tiles[begin + k];
         const int tx = (int)(t & 0xffffu), ty = (int)(t >> 16);
         steps += march_pixel<LAYOUT, WRAP, EARLY, ZO, UM>(a, f, tx * 8 + lane_x<LAYOUT>(lane),
@@ -956,10 +956,10 @@ __device__ __forceinline__ void regions_body(const MarchArgs& a, const unsigned*
 }
 template <int LAYOUT, int WRAP, bool EARLY, bool ZO, int WGW = kThreads / 64>
 __global__ __launch_bounds__(64 * WGW) void march_regions(const MarchArgs a, const unsigned* __restrict__ tiles,
-                                                         const TileMap m)
+                                                         const int* __restrict__ hdr, int nwx)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned lds[];
-    regions_body<LAYOUT, WRAP, EARLY, ZO, WGW, 0>(a, tiles, m, lds);
+    regions_body<LAYOUT, WRAP, EARLY, ZO, WGW, 0>(a, tiles, hdr, nwx, lds);
 }
 // with uniform channels UM (march_pixel's fetch_u / blend_u)
 #ifndef VR_UM_ATTR
@@ -967,10 +967,10 @@ __global__ __launch_bounds__(64 * WGW) void march_regions(const MarchArgs a, con
 #endif
 template <int LAYOUT, int WRAP, bool EARLY, bool ZO, int UM>
 __global__ __launch_bounds__(kThreads) VR_UM_ATTR void march_regions_u(const MarchArgs a, const unsigned* __restrict__ tiles,
-                                                                      const TileMap m)
+                                                                      const int* __restrict__ hdr, int nwx)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned lds[];
-    regions_body<LAYOUT, WRAP, EARLY, ZO, kThreads / 64, UM>(a, tiles, m, lds);
+    regions_body<LAYOUT, WRAP, EARLY, ZO, kThreads / 64, UM>(a, tiles, hdr, nwx, lds);
 }
 
 // ---- step-split rays (regions schedule) ----
@@ -1046,13 +1046,13 @@ __device__ __forceinline__ unsigned march_pixel_split(const MarchArgs& a, const 
 // so 4 adjacent lanes are a 2x2 pixel quad at the same step offset.
 template <int LAYOUT, bool EARLY, bool ZO, int K, int UM = 0>
 __global__ __launch_bounds__(kThreads) void march_regions_split(const MarchArgs a, const unsigned* __restrict__ tiles,
-                                                               const TileMap m)
+                                                               const int* __restrict__ hdr, int nwx)
 {
     constexpr int R = 64 / K, SW = K >= 4 ? 4 : 8, SH = R / SW, NSX = 8 / SW;
     extern __shared__ __attribute__((aligned(16))) unsigned lds[];
     const int xcd = blockIdx.x & 7;
     const int w = (int)(blockIdx.x >> 3) * (kThreads / 64) + (threadIdx.x >> 6);
-    const int begin = m.off[xcd], units = (m.off[xcd + 1] - begin) * K;
+    const int begin = hdr[xcd], units = (hdr[xcd + 1] - begin) * K;
     if ((int)(blockIdx.x >> 3) * (kThreads / 64) >= units) return;   // whole workgroup, before the barrier
     const FastCtx f = fast_prologue<LAYOUT>(a, lds);
 #ifdef VR_TIMELINE
@@ -1061,7 +1061,7 @@ __global__ __launch_bounds__(kThreads) void march_regions_split(const MarchArgs 
     const int lane = threadIdx.x & 63, k = lane / R, rho = lane % R;
     const int px = ((rho >> 2) % (SW / 2)) * 2 + (rho & 1), py = ((rho >> 2) / (SW / 2)) * 2 + ((rho >> 1) & 1);
     unsigned long long steps = 0;
-    for (int u = w; w < m.nwx && u < units; u += m.nwx) {
+    for (int u = w; w < nwx && u < units; u += nwx) {
         const unsigned t = tiles[begin + u / K];
         const int s = u % K;
         const int x = (int)(t & 0xffffu) * 8 + (s % NSX) * SW + px, orow = (int)(t >> 16) * 8 + (s / NSX) * SH + py;
@@ -1082,13 +1082,13 @@ __global__ __launch_bounds__(kThreads) void march_regions_split(const MarchArgs 
 // split's lane overhead on every tile.
 template <int LAYOUT, bool EARLY, bool ZO, int KS>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void march_regions_mixed(const MarchArgs a, const unsigned* __restrict__ tiles,
-                                                               const TileMap m)
+                                                               const int* __restrict__ hdr, int nwx)
 {
     constexpr int R = 64 / KS, SW = KS >= 4 ? 4 : 8, SH = R / SW, NSX = 8 / SW;
     extern __shared__ __attribute__((aligned(16))) unsigned lds[];
     const int xcd = blockIdx.x & 7;
     const int w = (int)(blockIdx.x >> 3) * (kThreads / 64) + (threadIdx.x >> 6);
-    const int begin = m.off[xcd], count = m.off[xcd + 1] - begin;
+    const int begin = hdr[xcd], count = hdr[xcd + 1] - begin;
     if ((int)(blockIdx.x >> 3) * (kThreads / 64) >= count) return;   // whole workgroup, before the barrier
 #ifdef VR_TIMELINE
     const unsigned long long t_begin = __builtin_amdgcn_s_memrealtime();
@@ -1097,7 +1097,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     const int lane = threadIdx.x & 63, k = lane / R, rho = lane % R;
     const int px = ((rho >> 2) % (SW / 2)) * 2 + (rho & 1), py = ((rho >> 2) / (SW / 2)) * 2 + ((rho >> 1) & 1);
     unsigned long long steps = 0;
-    for (int u = w; w < m.nwx && u < count; u += m.nwx) {
+    for (int u = w; w < nwx && u < count; u += nwx) {
         const unsigned t = tiles[begin + u];
         const int tx = (int)(t & 0xffffu), ty = (int)((t >> 16) & 0x1fffu);
         if (t >> 31) {
@@ -1121,7 +1121,7 @@ void launch_regions_split(const MarchArgs& a, bool early, const Schedule& sc, di
     if constexpr (L == LAYOUT_COL48 || L == LAYOUT_BRICK4832 || L == LAYOUT_CORNERH || L == LAYOUT_COL48Z) {
         const int um = a.umask;   // one uniform channel: no loads for it (march_regions' launcher)
         if (!early && a.zero_offsets && (um == 1 || um == 2 || um == 4 || um == 8)) {
-#define VR_UMS(U) hipLaunchKernelGGL((march_regions_split<L, false, true, K, U>), grid, block, lds, s, a, sc.tiles, sc.map)
+#define VR_UMS(U) hipLaunchKernelGGL((march_regions_split<L, false, true, K, U>), grid, block, lds, s, a, sc.tiles, sc.hdr, sc.map.nwx)
             if (um == 1) VR_UMS(1);
             else if (um == 2) VR_UMS(2);
             else if (um == 4) VR_UMS(4);
@@ -1131,13 +1131,13 @@ void launch_regions_split(const MarchArgs& a, bool early, const Schedule& sc, di
         }
     }
     if (early && a.zero_offsets)
-        hipLaunchKernelGGL((march_regions_split<L, true, true, K>), grid, block, lds, s, a, sc.tiles, sc.map);
+        hipLaunchKernelGGL((march_regions_split<L, true, true, K>), grid, block, lds, s, a, sc.tiles, sc.hdr, sc.map.nwx);
     else if (early)
-        hipLaunchKernelGGL((march_regions_split<L, true, false, K>), grid, block, lds, s, a, sc.tiles, sc.map);
+        hipLaunchKernelGGL((march_regions_split<L, true, false, K>), grid, block, lds, s, a, sc.tiles, sc.hdr, sc.map.nwx);
     else if (a.zero_offsets)
-        hipLaunchKernelGGL((march_regions_split<L, false, true, K>), grid, block, lds, s, a, sc.tiles, sc.map);
+        hipLaunchKernelGGL((march_regions_split<L, false, true, K>), grid, block, lds, s, a, sc.tiles, sc.hdr, sc.map.nwx);
     else
-        hipLaunchKernelGGL((march_regions_split<L, false, false, K>), grid, block, lds, s, a, sc.tiles, sc.map);
+        hipLaunchKernelGGL((march_regions_split<L, false, false, K>), grid, block, lds, s, a, sc.tiles, sc.hdr, sc.map.nwx);
 }
 
 // XCD-row schedule: one 8x8 tile per wave, 4 horizontally adjacent tiles per
@@ -1322,9 +1322,28 @@ __device__ __forceinline__ void proc_fill_background(const MarchArgs& a, const u
     }
 }
 
-[[maybe_unused]] __global__ __launch_bounds__(kKeyBins) void proc_scan(unsigned* __restrict__ hist, unsigned* __restrict__ cursor)
+// With shadow rays (config 3) it also lays out the deferred passes' scratch
+// (ScanOut; went = null: not needed).  Sorted wave w covers the sorted
+// positions [64w, 64w + 64), whose keys bound their step counts (key = n below
+// kKeyBins - 1, the last key holds every n >= kKeyBins - 1, bounded by
+// max_steps).  Its lanes append at most one entry per step, so its entries fit
+// the sum of its lanes' bounds, and it marches at most its first (largest)
+// key's bound of wave-steps.  went / wrec are the exclusive prefixes of those
+// two bounds over the waves -- the thread of a key writes the waves whose
+// first position falls in its key's range -- and need[] their totals, which the
+// host sizes the scratch from (vr_api.cpp ensure_defer).
+struct ScanOut {
+    unsigned long long* went;        // [waves + 1]: first entry of sorted wave w
+    unsigned* wrec;                  // [waves + 1]: first step record (saturated at 2^32 - 1)
+    unsigned long long* need;        // [0] entries, [1] step records of the frame
+    unsigned long long* need_host;   // the same, host-mapped (optional)
+    int max_steps;
+};
+[[maybe_unused]] __global__ __launch_bounds__(kKeyBins) void proc_scan(unsigned* __restrict__ hist, unsigned* __restrict__ cursor,
+                                                                       ScanOut so)
 {
     __shared__ unsigned sc[kKeyBins];
+    __shared__ unsigned long long ce[kKeyBins], cr[kKeyBins];
     const int t = threadIdx.x;
     const unsigned own = hist[kKeyBins - 1 - t];
     sc[t] = own;   // descending key order
@@ -1336,9 +1355,41 @@ __device__ __forceinline__ void proc_fill_background(const MarchArgs& a, const u
         __syncthreads();
     }
     const int key = kKeyBins - 1 - t;
-    cursor[key] = sc[t] - own;   // exclusive
-    if (t == kKeyBins - 1) cursor[kKeyBins] = sc[t];
+    const unsigned start = sc[t] - own, end = sc[t];
+    cursor[key] = start;   // exclusive
+    if (t == kKeyBins - 1) cursor[kKeyBins] = end;
     hist[key] = 0u;              // each thread clears the bin it read
+    if (!so.went) return;        // kernel-uniform
+    const unsigned long long val = key < kKeyBins - 1 ? (unsigned long long)key
+                                                      : (unsigned long long)max(so.max_steps, key);
+    const unsigned ws0 = (start + 63u) / 64u, ws1 = (end + 63u) / 64u;   // waves whose first position has this key
+    const unsigned long long e_own = (unsigned long long)own * val, r_own = (unsigned long long)(ws1 - ws0) * val;
+    ce[t] = e_own;
+    cr[t] = r_own;
+    __syncthreads();
+    for (int off = 1; off < kKeyBins; off <<= 1) {
+        const unsigned long long ve = t >= off ? ce[t - off] : 0ull, vr = t >= off ? cr[t - off] : 0ull;
+        __syncthreads();
+        ce[t] += ve;
+        cr[t] += vr;
+        __syncthreads();
+    }
+    const unsigned long long e0 = ce[t] - e_own, r0 = cr[t] - r_own;
+    for (unsigned w = ws0; w < ws1; ++w) {
+        so.went[w] = e0 + (unsigned long long)(64u * w - start) * val;
+        const unsigned long long rw = r0 + (unsigned long long)(w - ws0) * val;
+        so.wrec[w] = rw < 0xffffffffull ? (unsigned)rw : 0xffffffffu;
+    }
+    if (t == kKeyBins - 1) {   // key 0 holds no pixel: its start is the frame's end
+        so.went[ws1] = ce[t];
+        so.wrec[ws1] = cr[t] < 0xffffffffull ? (unsigned)cr[t] : 0xffffffffu;
+        so.need[0] = ce[t];
+        so.need[1] = cr[t];
+        if (so.need_host) {
+            so.need_host[0] = ce[t];
+            so.need_host[1] = cr[t];
+        }
+    }
 }
 
 [[maybe_unused]] __global__ __launch_bounds__(256) void proc_scatter(const MarchArgs a, const unsigned short* __restrict__ keys,
@@ -1450,11 +1501,6 @@ __global__ __launch_bounds__(kThreads) void march_proc_sorted(const MarchArgs a,
 // Every value is computed by the same ops in the same order as
 // march_pixel_proc<true>, so the frame stays bit-exact.
 // (struct ShadowDefer: vr_internal.h)
-__device__ __forceinline__ float4* defer_region(const ShadowDefer& d, unsigned w)
-{
-    return d.ent + (size_t)w * 64u * d.rec_stride;
-}
-
 template <bool EARLY, int TABLE>
 __global__ __launch_bounds__(kThreads) void march_proc_defer(const MarchArgs a, const unsigned* __restrict__ order,
                                                              const unsigned* __restrict__ total_ptr,
@@ -1485,6 +1531,24 @@ __global__ __launch_bounds__(kThreads) void march_proc_defer(const MarchArgs a, 
     const unsigned base = wid * 64u;
     if (base >= total) return;   // wave-uniform
     const unsigned idx = base + lane;
+    // the wave's ranges of entries and step records (proc_scan); past the
+    // scratch (a frame larger than the one it was sized for) the wave marches
+    // its shadow rays in place, and the later passes skip it
+    const unsigned long long eb = d.went[wid];
+    const unsigned rb = d.wrec[wid];
+    if (d.went[wid + 1] > d.ent_cap || d.wrec[wid + 1] > d.rec_cap) {   // wave-uniform
+        unsigned steps = 0;
+        if (idx < total) {
+            const unsigned pk = order[idx];
+            steps = march_pixel_proc<true, EARLY, TABLE>(a, wt, (int)(pk & 0xffffu), (int)(pk >> 16));
+        }
+        if (lane == 0) {
+            d.wsteps[wid] = kDeferInPlace;
+            d.wcount[wid] = 0;
+        }
+        if (a.step_counter) add_steps(a, steps);
+        return;
+    }
     Ray r{};
     r.n = -1;
     if (idx < total) {
@@ -1493,8 +1557,8 @@ __global__ __launch_bounds__(kThreads) void march_proc_defer(const MarchArgs a, 
     }
     const ProcParams& p = a.proc;
     const unsigned long long lt = (1ull << lane) - 1ull;
-    uint4* rec = d.rec + (size_t)wid * d.rec_stride;
-    float4* ent = defer_region(d, wid);
+    uint4* rec = d.rec + rb;
+    float4* ent = d.ent + eb;
     float P0 = r.pxy.x, P1 = r.pxy.y, P2 = r.pz;
     float acc = 0.0f, tv = 1.0f;
     int i = 0;
@@ -1565,7 +1629,8 @@ constexpr int kScanThreads = 1024;
     const unsigned lane = threadIdx.x & 63;
     if (w >= min((*total_ptr + 63u) / 64u, d.waves)) return;
     const unsigned n = d.wcount[w], c0 = d.wchunk[w];
-    for (unsigned k = lane; k * 64u < n; k += 64u) d.map[c0 + k] = make_uint4(w, k, min(64u, n - k * 64u), 0u);
+    const unsigned e0 = (unsigned)d.went[w];   // < ent_cap < 2^32 for a wave with entries
+    for (unsigned k = lane; k * 64u < n; k += 64u) d.map[c0 + k] = make_uint4(e0 + k * 64u, 0u, min(64u, n - k * 64u), 0u);
 }
 
 template <int TABLE>
@@ -1582,7 +1647,7 @@ __global__ __launch_bounds__(kThreads) void proc_shadow_eval(const MarchArgs a, 
     for (unsigned c = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6); c < chunks; c += gridDim.x * (kThreads / 64)) {
         const uint4 mc = d.map[c];   // wave-uniform
         if (lane >= mc.z) continue;
-        float4* e = defer_region(d, mc.x) + mc.y * 64u + lane;
+        float4* e = d.ent + mc.x + lane;
         const float4 en = *e;
         float q0 = en.x, q1 = en.y, q2 = en.z, sl = 0.0f;
         for (int j = 0; j < S; ++j) {
@@ -1612,10 +1677,11 @@ constexpr int kResolveBatch = 32;
     const unsigned wid = __builtin_amdgcn_readfirstlane(blockIdx.x * (kThreads / 64) + wave);
     const unsigned base = wid * 64u;
     if (base >= total) return;
-    const unsigned long long lt = (1ull << lane) - 1ull;
-    const uint4* rec = d.rec + (size_t)wid * d.rec_stride;
-    const float4* ent = defer_region(d, wid);
     const unsigned ns = d.wsteps[wid];
+    if (ns == kDeferInPlace) return;   // the primary pass stored this wave's pixels
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    const uint4* rec = d.rec + d.wrec[wid];
+    const float4* ent = d.ent + d.went[wid];
     float rad = 0.0f;
     for (unsigned s0 = 0; s0 < ns; s0 += kResolveBatch) {
         uint4 rc = make_uint4(0u, 0u, 0u, 0u);
@@ -1693,10 +1759,10 @@ hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStre
             if (sc.kind == SCHED_REGIONS && (sc.mixed == 2 || sc.mixed == 4)) {
                 const dim3 grid((unsigned)(8 * ((sc.map.nwx + 3) / 4)));
 #define VR_MX(KS) \
-    if (early && a.zero_offsets) hipLaunchKernelGGL((march_regions_mixed<L, true, true, KS>), grid, block, lds, s, a, sc.tiles, sc.map); \
-    else if (early) hipLaunchKernelGGL((march_regions_mixed<L, true, false, KS>), grid, block, lds, s, a, sc.tiles, sc.map); \
-    else if (a.zero_offsets) hipLaunchKernelGGL((march_regions_mixed<L, false, true, KS>), grid, block, lds, s, a, sc.tiles, sc.map); \
-    else hipLaunchKernelGGL((march_regions_mixed<L, false, false, KS>), grid, block, lds, s, a, sc.tiles, sc.map)
+    if (early && a.zero_offsets) hipLaunchKernelGGL((march_regions_mixed<L, true, true, KS>), grid, block, lds, s, a, sc.tiles, sc.hdr, sc.map.nwx); \
+    else if (early) hipLaunchKernelGGL((march_regions_mixed<L, true, false, KS>), grid, block, lds, s, a, sc.tiles, sc.hdr, sc.map.nwx); \
+    else if (a.zero_offsets) hipLaunchKernelGGL((march_regions_mixed<L, false, true, KS>), grid, block, lds, s, a, sc.tiles, sc.hdr, sc.map.nwx); \
+    else hipLaunchKernelGGL((march_regions_mixed<L, false, false, KS>), grid, block, lds, s, a, sc.tiles, sc.hdr, sc.map.nwx)
                 if (sc.mixed == 2) { VR_MX(2); } else { VR_MX(4); }
 #undef VR_MX
                 return hipGetLastError();
@@ -1708,10 +1774,10 @@ hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStre
             const int g = sc.wg_waves;
             const dim3 grid((unsigned)(8 * ((sc.map.nwx + g - 1) / g))), blk(64 * g);
 #define VR_RW(G) \
-    if (early && a.zero_offsets) hipLaunchKernelGGL((march_regions<L, W, true, true, G>), grid, blk, lds, s, a, sc.tiles, sc.map); \
-    else if (early) hipLaunchKernelGGL((march_regions<L, W, true, false, G>), grid, blk, lds, s, a, sc.tiles, sc.map); \
-    else if (a.zero_offsets) hipLaunchKernelGGL((march_regions<L, W, false, true, G>), grid, blk, lds, s, a, sc.tiles, sc.map); \
-    else hipLaunchKernelGGL((march_regions<L, W, false, false, G>), grid, blk, lds, s, a, sc.tiles, sc.map)
+    if (early && a.zero_offsets) hipLaunchKernelGGL((march_regions<L, W, true, true, G>), grid, blk, lds, s, a, sc.tiles, sc.hdr, sc.map.nwx); \
+    else if (early) hipLaunchKernelGGL((march_regions<L, W, true, false, G>), grid, blk, lds, s, a, sc.tiles, sc.hdr, sc.map.nwx); \
+    else if (a.zero_offsets) hipLaunchKernelGGL((march_regions<L, W, false, true, G>), grid, blk, lds, s, a, sc.tiles, sc.hdr, sc.map.nwx); \
+    else hipLaunchKernelGGL((march_regions<L, W, false, false, G>), grid, blk, lds, s, a, sc.tiles, sc.hdr, sc.map.nwx)
             if (g == 8) { VR_RW(8); } else { VR_RW(16); }
 #undef VR_RW
             return hipGetLastError();
@@ -1723,7 +1789,7 @@ hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStre
         const int um = a.umask;
         if (sc.kind == SCHED_REGIONS && !early && a.zero_offsets && (um == 1 || um == 2 || um == 4 || um == 8)) {
             const dim3 grid((unsigned)(8 * ((sc.map.nwx + 3) / 4)));
-#define VR_UM(U) hipLaunchKernelGGL((march_regions_u<L, W, false, true, U>), grid, block, lds, s, a, sc.tiles, sc.map)
+#define VR_UM(U) hipLaunchKernelGGL((march_regions_u<L, W, false, true, U>), grid, block, lds, s, a, sc.tiles, sc.hdr, sc.map.nwx)
             if (um == 1) VR_UM(1);
             else if (um == 2) VR_UM(2);
             else if (um == 4) VR_UM(4);
@@ -1734,7 +1800,7 @@ hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStre
 #ifdef VR_UM_EXPERIMENT
         if (sc.kind == SCHED_REGIONS && !early && a.zero_offsets && um == 10) {   // G and A (timing experiment)
             const dim3 grid((unsigned)(8 * ((sc.map.nwx + 3) / 4)));
-            hipLaunchKernelGGL((march_regions_u<L, W, false, true, 10>), grid, block, lds, s, a, sc.tiles, sc.map);
+            hipLaunchKernelGGL((march_regions_u<L, W, false, true, 10>), grid, block, lds, s, a, sc.tiles, sc.hdr, sc.map.nwx);
             return hipGetLastError();
         }
 #endif
@@ -1742,13 +1808,13 @@ hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStre
     if (sc.kind == SCHED_REGIONS) {
         const dim3 grid((unsigned)(8 * ((sc.map.nwx + 3) / 4)));
         if (early && a.zero_offsets)
-            hipLaunchKernelGGL((march_regions<L, W, true, true>), grid, block, lds, s, a, sc.tiles, sc.map);
+            hipLaunchKernelGGL((march_regions<L, W, true, true>), grid, block, lds, s, a, sc.tiles, sc.hdr, sc.map.nwx);
         else if (early)
-            hipLaunchKernelGGL((march_regions<L, W, true, false>), grid, block, lds, s, a, sc.tiles, sc.map);
+            hipLaunchKernelGGL((march_regions<L, W, true, false>), grid, block, lds, s, a, sc.tiles, sc.hdr, sc.map.nwx);
         else if (a.zero_offsets)
-            hipLaunchKernelGGL((march_regions<L, W, false, true>), grid, block, lds, s, a, sc.tiles, sc.map);
+            hipLaunchKernelGGL((march_regions<L, W, false, true>), grid, block, lds, s, a, sc.tiles, sc.hdr, sc.map.nwx);
         else
-            hipLaunchKernelGGL((march_regions<L, W, false, false>), grid, block, lds, s, a, sc.tiles, sc.map);
+            hipLaunchKernelGGL((march_regions<L, W, false, false>), grid, block, lds, s, a, sc.tiles, sc.hdr, sc.map.nwx);
         return hipGetLastError();
     }
     if (sc.kind == SCHED_XCDROWS) {

@@ -206,12 +206,12 @@ __device__ __forceinline__ unsigned march_pixel_slab(const MarchArgs& a, const _
 // {a / 3, a % 3} and {b / 7, 4 (b % 7)} as float2.
 template <bool EARLY, bool ZO>
 __global__ __launch_bounds__(kThreads) void march_regions_slab(const MarchArgs a, const unsigned* __restrict__ tiles,
-                                                              const TileMap m)
+                                                              const int* __restrict__ hdr, int nwx)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     const int xcd = blockIdx.x & 7;
     const int w = (int)(blockIdx.x >> 3) * kSlabWaves + (threadIdx.x >> 6);
-    const int begin = m.off[xcd], count = m.off[xcd + 1] - begin;
+    const int begin = hdr[xcd], count = hdr[xcd + 1] - begin;
     if ((int)(blockIdx.x >> 3) * kSlabWaves >= count) return;   // whole workgroup, before the barrier
     float2* tx2 = reinterpret_cast<float2*>(lds_raw + kSlabWaves * kSlabWaveBytes);
     float2* ty2 = tx2 + (a.nx + 1);
@@ -230,7 +230,7 @@ __global__ __launch_bounds__(kThreads) void march_regions_slab(const MarchArgs a
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     unsigned char* slab = lds_raw + wave * kSlabWaveBytes;
     unsigned long long steps = 0;
-    for (int k = w; w < m.nwx && k < count; k += m.nwx) {   // the grid rounds nwx up to whole workgroups
+    for (int k = w; w < nwx && k < count; k += nwx) {   // the grid rounds nwx up to whole workgroups
         const unsigned t = tiles[begin + k];
         const int tx = (int)(t & 0xffffu), ty = (int)(t >> 16);
         steps += march_pixel_slab<EARLY, ZO>(a, rsrc, tx2, ty2, slab, 0u, tx * 8 + lane_x<LAYOUT_COL48>(lane),
@@ -248,13 +248,13 @@ hipError_t launch_march_slab(const MarchArgs& a, bool early, const Schedule& sc,
     const dim3 grid((unsigned)(8 * ((sc.map.nwx + 3) / 4))), block(kThreads);
     const size_t lds = slab_lds_bytes(a.nx, a.ny);
     if (early && a.zero_offsets)
-        hipLaunchKernelGGL((march_regions_slab<true, true>), grid, block, lds, s, a, sc.tiles, sc.map);
+        hipLaunchKernelGGL((march_regions_slab<true, true>), grid, block, lds, s, a, sc.tiles, sc.hdr, sc.map.nwx);
     else if (early)
-        hipLaunchKernelGGL((march_regions_slab<true, false>), grid, block, lds, s, a, sc.tiles, sc.map);
+        hipLaunchKernelGGL((march_regions_slab<true, false>), grid, block, lds, s, a, sc.tiles, sc.hdr, sc.map.nwx);
     else if (a.zero_offsets)
-        hipLaunchKernelGGL((march_regions_slab<false, true>), grid, block, lds, s, a, sc.tiles, sc.map);
+        hipLaunchKernelGGL((march_regions_slab<false, true>), grid, block, lds, s, a, sc.tiles, sc.hdr, sc.map.nwx);
     else
-        hipLaunchKernelGGL((march_regions_slab<false, false>), grid, block, lds, s, a, sc.tiles, sc.map);
+        hipLaunchKernelGGL((march_regions_slab<false, false>), grid, block, lds, s, a, sc.tiles, sc.hdr, sc.map.nwx);
     return hipGetLastError();
 }
 

@@ -1,0 +1,222 @@
+// vr_regions.hip -- the regions schedule's tile lists built on the GPU, for a
+// moving camera (verdict r03 #2).
+//
+// build_regions (vr_api.cpp) deals the 8x8 tiles of the target to the 8 XCDs
+// as contiguous angular wedges around the projected box centre with equal
+// estimated work, each XCD walking its tiles inside-out (longest rays first).
+// On the host that is ~33 k corner slab tests and three sorts, 1-2 ms per
+// rebuild at 1080p, which a camera that moves every frame (the reference's held
+// A/D/W/S key, TestMain.cpp:171-184) cannot pay per frame.  Here the same lists
+// come from four kernels and one device radix sort on the render stream:
+//   1. rg_tiles: per tile, the a3 step estimate of the rays through its 4
+//      corners (double, as the host), the angle of its S x S block around the
+//      centre quantised to kAngleBins bins, the Chebyshev ring of the block,
+//      the tile's place in its block; the work of each angle bin (fixed point,
+//      so the sums do not depend on the atomic order);
+//   2. rg_wedges: one workgroup scans the bins' work and cuts it into
+//      8 x wedges equal quantiles; wedge k goes to XCD k % 8 (as the host
+//      cuts tiles sorted by angle);
+//   3. rg_keys: the sort key of a tile -- XCD, idle flag (tiles without
+//      estimated work go after the XCD's work, dealt round-robin), ring, angle
+//      bin, place in block -- and the per-XCD counts;
+//   4. hipcub::DeviceRadixSort::SortPairs: keys -> the concatenated lists;
+//   5. rg_header: the per-XCD offsets, tiles with work and the longest list,
+//      into the list buffer's header (and host-mapped memory, which the host
+//      reads later to size the next launches -- no host wait).
+// The lists only order work: every tile is in exactly one list whatever the
+// estimate, so a frame is exact with any lists (tests/test_gpu_parity.py).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <cmath>
+
+#include "vr_internal.h"
+
+namespace vr {
+namespace {
+
+constexpr int kAngleBins = 4096;
+constexpr int kWedgeThreads = 1024;
+constexpr double kCostScale = 1024.0;   // fixed point of the per-bin work sums
+
+struct RgScratch {
+    unsigned* keys_in;
+    unsigned* keys_out;
+    unsigned* vals_in;
+    unsigned long long* bin_cost;   // [kAngleBins], zeroed by rg_wedges after use
+    unsigned char* bin_xcd;         // [kAngleBins]
+    unsigned* counts;               // [8] per XCD, [8] tiles with work; zeroed by rg_header after use
+    void* sort_tmp;
+    size_t sort_bytes;
+};
+
+__device__ double steps_at(const RegionBuild& b, double fx, int orow)
+{
+    const int bl = orow / b.band_rows;
+    const double fy = (double)((b.band_first + bl * b.band_stride) * b.band_rows + (orow - bl * b.band_rows));
+    double d[3], len = 0.0;
+    for (int k = 0; k < 3; ++k) {
+        d[k] = (double)b.o[k] + fx * (double)b.px[k] + fy * (double)b.py[k];
+        len += d[k] * d[k];
+    }
+    len = sqrt(len);
+    double tn = -INFINITY, tf = INFINITY;
+    for (int k = 0; k < 3; ++k) {
+        const double ta = ((double)b.box_min[k] - (double)b.org[k]) * len / d[k];
+        const double tb = ((double)b.box_max[k] - (double)b.org[k]) * len / d[k];
+        tn = fmax(tn, fmin(ta, tb));
+        tf = fmin(tf, fmax(ta, tb));
+    }
+    return (tn <= tf && isfinite(tf)) ? fmin((double)b.max_steps, (tf - tn) / (double)b.step_size) : 0.0;
+}
+
+// 1. per tile: work estimate, angle bin, ring, place in block
+__global__ __launch_bounds__(256) void rg_tiles(const RegionBuild b, RgScratch s)
+{
+    const int i = (int)(blockIdx.x * 256 + threadIdx.x);
+    if (i >= b.tw * b.th) return;
+    const int ty = i / b.tw, tx = i - ty * b.tw;
+    const int x0 = min(tx * 8, b.width), x1 = min(tx * 8 + 8, b.width);
+    const int r0 = min(ty * 8, b.out_rows), r1 = min(ty * 8 + 8, b.out_rows);
+    const double cost = fmax(fmax(steps_at(b, x0, r0), steps_at(b, x1, r0)), fmax(steps_at(b, x0, r1), steps_at(b, x1, r1)));
+    const int S = b.supertile;
+    const int sx = tx / S, sy = ty / S;
+    const double ang = atan2(sy * S + 0.5 * S - b.ccy, sx * S + 0.5 * S - b.ccx);
+    int abin = (int)((ang + M_PI) * (kAngleBins / (2.0 * M_PI)));
+    abin = min(max(abin, 0), kAngleBins - 1);
+    const int ring = min(max(abs(sx - b.ctx), abs(sy - b.cty)), 2047);
+    const int sub = (ty % S) * S + tx % S;
+    const bool work = cost >= 1.0;
+    if (work) {
+        atomicAdd(&s.bin_cost[abin], (unsigned long long)(cost * kCostScale));
+        atomicAdd(&s.counts[8], 1u);
+    }
+    s.keys_in[i] = (work ? 0u : 1u) << 27 | (unsigned)ring << 16 | (unsigned)abin << 4 | (unsigned)sub;
+    s.vals_in[i] = ((unsigned)ty << 16) | (unsigned)tx;
+}
+
+// 2. the bins' work in angle order, cut into K = 8 x wedges equal quantiles
+__global__ __launch_bounds__(kWedgeThreads) void rg_wedges(const RegionBuild b, RgScratch s)
+{
+    constexpr int kPer = kAngleBins / kWedgeThreads;
+    __shared__ unsigned long long sc[kWedgeThreads];
+    const int t = threadIdx.x;
+    unsigned long long c[kPer], own = 0;
+    for (int j = 0; j < kPer; ++j) {
+        c[j] = s.bin_cost[t * kPer + j];
+        s.bin_cost[t * kPer + j] = 0ull;   // zero for the next build
+        own += c[j];
+    }
+    sc[t] = own;
+    __syncthreads();
+    for (int off = 1; off < kWedgeThreads; off <<= 1) {
+        const unsigned long long v = t >= off ? sc[t - off] : 0ull;
+        __syncthreads();
+        sc[t] += v;
+        __syncthreads();
+    }
+    const double total = (double)sc[kWedgeThreads - 1];
+    double run = (double)(sc[t] - own);
+    const int K = 8 * b.wedges;
+    for (int j = 0; j < kPer; ++j) {
+        const int k = total > 0.0 ? min(K - 1, (int)((run + 0.5 * (double)c[j]) / total * K)) : 0;
+        s.bin_xcd[t * kPer + j] = (unsigned char)(k % 8);
+        run += (double)c[j];
+    }
+}
+
+// 3. the sort key: XCD | idle | ring | angle bin | place in block
+__global__ __launch_bounds__(256) void rg_keys(const RegionBuild b, RgScratch s)
+{
+    const int i = (int)(blockIdx.x * 256 + threadIdx.x);
+    if (i >= b.tw * b.th) return;
+    const unsigned k = s.keys_in[i];
+    const bool idle = (k >> 27) & 1u;
+    const unsigned xcd = idle ? (unsigned)(i % 8) : (unsigned)s.bin_xcd[(k >> 4) & (kAngleBins - 1)];
+    s.keys_in[i] = xcd << 28 | k;
+    atomicAdd(&s.counts[xcd], 1u);
+}
+
+// 5. header: off[0..8], tiles with work, longest list; counters zeroed
+__global__ __launch_bounds__(64) void rg_header(RgScratch s, int* hdr, int* hdr_host, int n)
+{
+    if (threadIdx.x != 0) return;
+    int pos = 0, most = 0;
+    for (int x = 0; x < 8; ++x) {
+        hdr[x] = pos;
+        const int cnt = (int)s.counts[x];
+        most = max(most, cnt);
+        pos += cnt;
+        s.counts[x] = 0u;
+    }
+    hdr[8] = pos;   // == n
+    hdr[9] = (int)s.counts[8];
+    hdr[10] = most;
+    hdr[11] = n;
+    s.counts[8] = 0u;
+    if (hdr_host)
+        for (int j = 0; j < kRegionHeader; ++j) hdr_host[j] = hdr[j];
+}
+
+RgScratch carve(void* scratch, int n, size_t sort_bytes)
+{
+    auto up = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    char* p = static_cast<char*>(scratch);
+    RgScratch s{};
+    size_t o = 0;
+    s.bin_cost = reinterpret_cast<unsigned long long*>(p + o);
+    o = up(o + kAngleBins * sizeof(unsigned long long));
+    s.counts = reinterpret_cast<unsigned*>(p + o);
+    o = up(o + 16 * sizeof(unsigned));
+    s.bin_xcd = reinterpret_cast<unsigned char*>(p + o);
+    o = up(o + kAngleBins);
+    s.keys_in = reinterpret_cast<unsigned*>(p + o);
+    o = up(o + (size_t)n * 4);
+    s.keys_out = reinterpret_cast<unsigned*>(p + o);
+    o = up(o + (size_t)n * 4);
+    s.vals_in = reinterpret_cast<unsigned*>(p + o);
+    o = up(o + (size_t)n * 4);
+    s.sort_tmp = p + o;
+    s.sort_bytes = sort_bytes;
+    return s;
+}
+
+size_t sort_temp_bytes(int n)
+{
+    size_t bytes = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const unsigned*)nullptr, (unsigned*)nullptr,
+                                             (const unsigned*)nullptr, (unsigned*)nullptr, n, 0, 31, nullptr);
+    return bytes;
+}
+
+}  // namespace
+
+// Scratch of a build over n tiles.  The per-bin sums and the counters must be
+// zero when the first build starts (the caller zeroes a new scratch); every
+// build leaves them zero for the next.
+size_t region_build_bytes(int n)
+{
+    return 256 + (size_t)kAngleBins * 8 + 256 + kAngleBins + 256 + 3 * ((size_t)n * 4 + 256) + sort_temp_bytes(n) + 256;
+}
+
+hipError_t launch_region_build(const RegionBuild& b, void* scratch, unsigned* d_list, int* d_hdr, int* h_hdr,
+                               hipStream_t st)
+{
+    const int n = b.tw * b.th;
+    if (n <= 0) return hipSuccess;
+    const size_t sb = sort_temp_bytes(n);
+    RgScratch s = carve(scratch, n, sb);
+    const dim3 grid((unsigned)((n + 255) / 256));
+    hipLaunchKernelGGL(rg_tiles, grid, dim3(256), 0, st, b, s);
+    hipLaunchKernelGGL(rg_wedges, dim3(1), dim3(kWedgeThreads), 0, st, b, s);
+    hipLaunchKernelGGL(rg_keys, grid, dim3(256), 0, st, b, s);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    size_t bytes = s.sort_bytes;
+    e = hipcub::DeviceRadixSort::SortPairs(s.sort_tmp, bytes, s.keys_in, s.keys_out, s.vals_in, d_list, n, 0, 31, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(rg_header, dim3(1), dim3(64), 0, st, s, d_hdr, h_hdr, n);
+    return hipGetLastError();
+}
+
+}  // namespace vr

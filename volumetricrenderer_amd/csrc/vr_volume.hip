@@ -581,6 +581,31 @@ hipError_t launch_pack_recipe(const float* d_g1, const float* d_g2, const float*
     return hipGetLastError();
 }
 
+// Streaming copy for the measured HBM roofline (vr_measure_copy_bandwidth):
+// 16 B per lane, four independent loads in flight per lane, grid-stride.
+__global__ __launch_bounds__(256) void k_stream_copy(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                     long long n)
+{
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < n; i += 4 * stride) {
+        const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+        dst[i] = a;
+        dst[i + stride] = b;
+        dst[i + 2 * stride] = c;
+        dst[i + 3 * stride] = d;
+    }
+    for (; i < n; i += stride) dst[i] = src[i];
+}
+
+hipError_t launch_stream_copy(const void* src, void* dst, size_t bytes, hipStream_t s)
+{
+    // 8 workgroups of 256 lanes per CU (256 CUs): every CU keeps ~32 KiB of loads in flight
+    hipLaunchKernelGGL(k_stream_copy, dim3(2048), dim3(256), 0, s, static_cast<const uint4*>(src),
+                       static_cast<uint4*>(dst), (long long)(bytes / 16));
+    return hipGetLastError();
+}
+
 hipError_t launch_assemble(const uint8_t* d_gathered, size_t rows_per_rank, int nranks, int width, int height,
                            int band_rows, int bpp, uint8_t* d_frame, hipStream_t s)
 {

@@ -218,6 +218,14 @@ class Renderer:
     def kernel_variant(self) -> str:
         return _lib.load().vr_kernel_variant(self._ctx).decode()
 
+    def measure_copy_bandwidth(self, nbytes: int = 2 << 30, reps: int = 10, stream=None) -> tuple[float, float]:
+        """(best, median) GB/s of the device's 16-B-per-lane streaming copy
+        (read + written bytes): the measured HBM roofline (vr.h)."""
+        best, med = ctypes.c_double(), ctypes.c_double()
+        _lib.call("vr_measure_copy_bandwidth", self._ctx, nbytes, reps, _stream_handle(stream), ctypes.byref(best),
+                  ctypes.byref(med))
+        return best.value, med.value
+
     # -- the hot path ------------------------------------------------------
     def alloc_target(self, width: int, height: int, fmt: int = FMT_RGBA8_UNORM, band_rows: int = 0,
                      band_stride: int = 1, band_first: int = 0) -> torch.Tensor:
