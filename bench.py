@@ -278,7 +278,8 @@ def main() -> int:
     ap.add_argument("--opt", action="append", default=[], help="vr option NAME=VALUE (experiments)")
     ap.add_argument("--spin", action="store_true",
                     help="moving camera: every frame gets new shader data, phi += 1.6 deg (the reference's "
-                         "held A/D key, TestMain.cpp:171-184, :222-224); N = 1 only")
+                         "held A/D key, TestMain.cpp:171-184, :222-224), queued natively (vr_render_sequence "
+                         "at N = 1, vr_shard_run_frames at N > 1)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -289,8 +290,6 @@ def main() -> int:
     # --pipeline1: the native frame loop with a one-rank communicator at N = 1
     # (a rehearsal of the N > 1 host path on one GPU; not the default N = 1 line)
     native = (world > 1 and args.sharder == "native") or args.pipeline1
-    if args.spin and (world > 1 or args.pipeline1):
-        raise SystemExit("--spin: one GPU, one process (the shard loop renders a fixed camera)")
     if native and ndev < world:
         raise SystemExit(f"--sharder native needs one GPU per rank ({world} ranks, {ndev} GPUs); "
                          "use --sharder torch --backend gloo to rehearse on fewer GPUs")
@@ -368,38 +367,46 @@ def main() -> int:
         except vr.VRError as e:
             print(f"rank {rank}: native RCCL frame loop unavailable: {e}", file=sys.stderr, flush=True)
             raise SystemExit(3)
+    # a spinning camera: new shader data before every frame (phi += 1.6 deg, the
+    # reference's held A/D key), so the frame pays the region-list reuse / GPU
+    # rebuild (grid) or the cost sort (procedural) that a static camera skips.
+    # The shader data of every frame is made before the clock starts (host
+    # math, TestMain.cpp:219-245); the frames are queued natively.
+    SPIN_DEG = 1.6
+    sd = ([vr.reference_shader_data(1280.0 / 720.0, SPIN_DEG * i, 0.0) for i in range(args.warmup + args.steps)]
+          if args.spin else None)
     if native:
         # Bracket: host barrier (gloo) for the rendezvous, then the device-side
         # RCCL barrier + synchronisation on both sides of the timed frames.  A
         # gloo barrier across 8 processes costs a sizeable fraction of a
         # millisecond -- several 1/8-frames -- so it stays outside the clock.
-        pipe.run_frames(args.warmup)
+        pipe.run_frames(args.warmup, cameras=sd[:args.warmup] if sd else None)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         pipe.barrier(stream)
         t0 = time.perf_counter()
-        kern_ms = pipe.run_frames(args.steps, stream=stream, sample_every=ev_every)
+        kern_ms = pipe.run_frames(args.steps, stream=stream, sample_every=ev_every,
+                                  cameras=sd[args.warmup:] if sd else None)
+        host_el = pipe.host_ms * args.steps * 1e-3
         pipe.barrier(stream)
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
         if world > 1:
             dist.barrier()
     elif args.spin:
-        # a spinning camera: new shader data before every frame, so the frame
-        # pays the region-list reuse / rebuild (grid) or the cost sort
-        # (procedural) that a static camera skips.  The shader data of every
-        # frame is made before the clock starts (host math, TestMain.cpp:219-245).
-        SPIN_DEG = 1.6
-        sd = [vr.reference_shader_data(1280.0 / 720.0, SPIN_DEG * i, 0.0) for i in range(args.warmup + args.steps)]
-        launch = r.prepare_render(W, H, fmt, sharder.local)
-        for i in range(args.warmup):
-            r.set_shader_data(*sd[i])
-            launch()
+        r.render_sequence(W, H, fmt, sharder.local, sd[:args.warmup])
         torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        r.render_sequence(W, H, fmt, sharder.local, sd[args.warmup:])
+        host_el = time.perf_counter() - t0
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        # kernel time of every 4th frame: the same frames replayed (untimed),
+        # events around each render
+        launch = r.prepare_render(W, H, fmt, sharder.local)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               if i % ev_every == 0 else None for i in range(args.steps)]
-        t0 = time.perf_counter()
         for i in range(args.steps):
             r.set_shader_data(*sd[args.warmup + i])
             if ev[i] is not None:
@@ -407,9 +414,7 @@ def main() -> int:
             launch()
             if ev[i] is not None:
                 ev[i][1].record()
-        host_el = time.perf_counter() - t0
         torch.cuda.synchronize()
-        el = time.perf_counter() - t0
         kern_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev if e is not None]))
         # the executed steps of the sampled frames (untimed): the roofline's unit
         sampled = []
@@ -537,7 +542,9 @@ def main() -> int:
                        "executed_steps_per_frame": frame_steps},
             "executed_steps_per_s": round(frame_steps * args.steps / el, 1),
             "kernel_ms_mean": round(kern_ms, 5),
-            **({"host_ms_per_frame": round(host_el / args.steps * 1e3, 4)} if args.spin else {}),
+            **({"host_ms_per_frame": round(host_el / args.steps * 1e3, 4)} if args.spin or native else {}),
+            **({"region_lists": {"gpu_builds": r.get_option("region_gpu_builds"),
+                                 "interval": r.get_option("region_interval")}} if args.spin and proc is None else {}),
             **({"all_channels_loaded": all_loaded} if all_loaded else {}),
             "kernel_ms_mean_max_rank": round(kern_ms_max, 5),
             "roofline": dict(roofline, traffic=traffic,

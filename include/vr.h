@@ -213,6 +213,12 @@ vr_status vr_set_march(void* ctx, const vr_march_params* m);
 
  *      stream = hipStream_t (NULL = default stream).                       */
 vr_status vr_render(void* ctx, const vr_target* target, void* stream);
+/* The frame loop of TestMain.cpp:173-256 with a moving camera: `frames`
+ * renders into `target`, frame i with shader data (osd[i], gsd[i]) -- the
+ * per-frame UBO updates of :219-249 -- all queued on `stream` without a host
+ * wait.  The ctx keeps the last frame's shader data.                       */
+vr_status vr_render_sequence(void* ctx, const vr_target* target, int frames, const vr_object_shader_data* osd,
+                             const vr_global_shader_data* gsd, void* stream);
 
 /* ---- multi-GPU frame assembly.  The band sets of `nranks` ranks are
  *      gathered into one device buffer, d_gathered = [rank][packed rows].

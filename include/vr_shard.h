@@ -74,6 +74,15 @@ vr_status vr_shard_destroy(vr_shard* sh);
  * mean duration is written there (this call then waits for that last
  * sample). */
 vr_status vr_shard_run(vr_shard* sh, int frames, void* stream, int sample_every, float* kernel_ms);
+/* vr_shard_run with a moving camera (the reference's held A/D/W/S key,
+ * TestMain.cpp:171-184, and its per-frame UBO updates, :219-249): frame i
+ * renders with shader data (osd[i], gsd[i]) -- every rank passes the same
+ * arrays -- set on the ctx before its render; osd = gsd = NULL keeps the ctx's.
+ * host_ms (optional): host time per frame spent queueing the frames (before
+ * any wait for the sampled renders), ms. */
+vr_status vr_shard_run_frames(vr_shard* sh, int frames, const vr_object_shader_data* osd,
+                              const vr_global_shader_data* gsd, void* stream, int sample_every, float* kernel_ms,
+                              double* host_ms);
 
 /* Collective barrier + synchronisation: returns once the work queued on
  * `stream` and on the communication stream of EVERY rank before the call has

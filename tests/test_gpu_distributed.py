@@ -145,6 +145,38 @@ def test_rccl_pipeline_deadline_aborts():
             pl.close()
 
 
+def test_rccl_init_deadline_when_a_peer_never_joins():
+    """A 2-rank communicator whose rank 1 never joins (it died before the
+    collective init): rank 0's non-blocking ncclCommInitRankConfig gives up at
+    the deadline with VR_ERR_TIMEOUT and the communicator aborted, instead of
+    waiting forever (the init deadline, untested until now)."""
+    import ctypes
+    import sys
+    import time
+    sys.path.insert(0, ROOT)
+    import volumetricrenderer_amd as vr
+    from volumetricrenderer_amd import _lib
+    with vr.Renderer(0) as r:
+        h = ctypes.c_void_p()
+        _lib.shard_call("vr_shard_alloc", r._ctx, 2, 0, 64, 64, 1, 16, ctypes.byref(h))
+        try:
+            _lib.shard_call("vr_shard_set_timeout", h, 3.0)
+            uid = (ctypes.c_uint8 * _lib.SHARD_ID_BYTES)()
+            _lib.shard_call("vr_shard_unique_id", uid)
+            t0 = time.perf_counter()
+            with pytest.raises(vr.VRError) as e:
+                _lib.shard_call("vr_shard_connect", h, uid)
+            el = time.perf_counter() - t0
+            assert e.value.status == 7, e.value   # VR_ERR_TIMEOUT
+            assert 2.5 < el < 30.0, el
+            assert _lib.shard_call("vr_shard_aborted", h) == 1
+            with pytest.raises(vr.VRError) as e2:   # every later collective fails at once
+                _lib.shard_call("vr_shard_barrier", h, None)
+            assert e2.value.status in (2, 8), e2.value
+        finally:
+            _lib.shard_call("vr_shard_destroy", h)
+
+
 @pytest.mark.parametrize("world,band_rows,fmt,W", [(2, 16, 1, 500), (3, 16, 0, 500), (8, 16, 1, 500), (5, 7, 1, 500),
                                                    (3, 16, 2, 499), (4, 16, 0, 499)])
 def test_native_pipeline_loopback_ranks(world, band_rows, fmt, W):
@@ -213,3 +245,66 @@ def test_native_share_volume(world, loopback):
                 pl.share_volume(torch.zeros((4, 4, 4, 3), dtype=torch.uint8, device="cuda"))
         finally:
             pl.close()
+
+
+SPIN_DEG = 1.6   # TestMain.cpp:171-184, :222-224: the held A/D key, 100 deg/s x 0.016 s
+
+
+@pytest.mark.parametrize("fmt", [0, 1])
+def test_native_loopback_spinning_8_ranks(oracle, fmt):
+    """A moving camera through the native 8-rank frame loop (loopback: this
+    process renders every rank's interleaved band set): 40 frames, frame i
+    with its own shader data (vr_shard_run_frames, phi += 1.6 deg), 2 in
+    flight.  Frames 1, 33 and 40, assembled on rank 0, equal the oracle's
+    whole frame bit for bit (RGBA32F and RGBA8)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import volumetricrenderer_amd as vr
+    from volumetricrenderer_amd.distributed import RcclBandPipeline
+    W, H = 320, 180
+    vol = oracle.build_volume(128)
+    with vr.Renderer(0) as r:
+        r.set_volume(vol)
+        cams = [vr.reference_shader_data(W / H, SPIN_DEG * i, 0.0) for i in range(1, 41)]
+        r.set_shader_data(*cams[0])
+        r.set_march(vr.march_defaults())
+        pl = RcclBandPipeline(r, W, H, fmt, band_rows=16, world=8, rank=0, loopback=True)
+        got, done = {}, 0
+        try:
+            for stop in (1, 33, 40):
+                pl.run_frames(stop - done, cameras=cams[done:stop])
+                assert pl.host_ms >= 0.0
+                done = stop
+                got[stop] = pl.frame()
+            torch.cuda.synchronize()
+        finally:
+            pl.close()
+    for i, img in got.items():
+        obj, glob = vr.shader_data_arrays(*cams[i - 1])
+        ref, _ = oracle.render(vol, obj, glob, oracle.from_params(vr.march_defaults()), W, H, fmt)
+        assert np.array_equal(img.cpu().numpy(), ref), i
+
+
+def test_render_sequence_spinning(oracle):
+    """vr_render_sequence, the one-GPU frame loop with a moving camera: 33
+    frames queued in one native call (with GPU-rebuilt region lists every 8
+    renders); the target holds frame 33, equal to the oracle's."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import volumetricrenderer_amd as vr
+    W, H = 320, 180
+    vol = oracle.build_volume(128)
+    with vr.Renderer(0) as r:
+        r.set_volume(vol)
+        r.set_march(vr.march_defaults())
+        r.set_option("region_interval", 8)
+        cams = [vr.reference_shader_data(W / H, SPIN_DEG * i, 0.0) for i in range(1, 34)]
+        r.set_shader_data(*cams[0])
+        out = r.alloc_target(W, H, 0)
+        r.render(W, H, 0, out=out)   # the first lists: a host build
+        r.render_sequence(W, H, 0, out, cams)
+        torch.cuda.synchronize()
+        assert r.get_option("region_gpu_builds") >= 3
+        obj, glob = vr.shader_data_arrays(*cams[-1])
+        ref, _ = oracle.render(vol, obj, glob, oracle.from_params(vr.march_defaults()), W, H, 0)
+        assert np.array_equal(out.cpu().numpy(), ref)

@@ -49,6 +49,17 @@ def assert_exact(img, ref):
                           f"{img[tuple(bad[0])]} vs {ref[tuple(bad[0])]}"
 
 
+# layouts measured slower than the auto ones, built only with VR_EXPERIMENTS
+# (make EXPERIMENTS=1; vr_internal.h layout_built)
+EXPERIMENTAL_LAYOUTS = {2, 3, 4, 6, 7, 8, 9, 10, 11, 13, 16}
+
+
+def need_experiments(r, what):
+    """Skip unless the library was built with the measured-slower variants."""
+    if r.get_option("experiments") != 1:
+        pytest.skip(f"{what}: built only with VR_EXPERIMENTS (make EXPERIMENTS=1)")
+
+
 def perlin_cube_volume(oracle, n=128):
     """BASELINE config 1 volume: single-octave Perlin (f=.19, seed 3),
     normalised and inverted as TestMain.cpp:64-78, in all four channels."""
@@ -154,7 +165,7 @@ def test_spinning_camera_procedural(r, oracle, shadow):
     p = oracle.procedural_from(r.procedural)
     keep = {}
     try:
-        for reuse in (31, 0):
+        for reuse in ((31, 0) if r.get_option("experiments") == 1 else (0,)):   # sort_reuse: VR_EXPERIMENTS
             r.set_option("sort_reuse", reuse)
             assert r.get_option("sort_reuse") == reuse
             for i in range(1, 41):
@@ -195,6 +206,8 @@ def test_media_scroll_mirrored_repeat(r, oracle, vol128):
                                          (12, "brick4832"), (13, "brick4864"), (14, "cornerh"), (15, "col48"),
                                          (16, "col48z")])
 def test_every_layout_bitexact(r, oracle, vol128, layout, name):
+    if layout in EXPERIMENTAL_LAYOUTS:
+        need_experiments(r, name)
     osd, gsd = vr.reference_shader_data(16 / 9, 20.0, -35.0)
     r.set_volume(vol128)
     r.set_layout_preference(layout)
@@ -225,6 +238,7 @@ def test_split_long_tiles_bitexact(r, oracle, vol128, layout):
     exact step counts, with and without early-out, and with a banded target
     (packed rows).  Layout 7 (zpair) has no mixed kernel: the option must
     leave it on its plain / split path."""
+    need_experiments(r, "split_long")
     r.set_volume(vol128)
     r.set_layout_preference(layout)
     r.set_option("split", 1)
@@ -263,6 +277,8 @@ def test_uniform_channel_skip_bitexact(r, oracle, layout):
     each single uniform channel, with uniform_skip on and off, for the one-lane
     march and the step-split march (split 2 and 4, banded), and for two uniform
     channels (the general kernel)."""
+    if layout in EXPERIMENTAL_LAYOUTS:
+        need_experiments(r, "col48z")
     rng = np.random.default_rng(layout)
     base = rng.integers(0, 256, size=(40, 44, 36, 4), dtype=np.uint8)
     r.set_layout_preference(layout)
@@ -334,7 +350,10 @@ def test_region_workgroups_and_supertiles_bitexact(r, oracle, vol128, layout):
     r.set_volume(vol128)
     r.set_layout_preference(layout)
     try:
+        exp = r.get_option("experiments") == 1   # 8 / 16-wave workgroups: VR_EXPERIMENTS only
         for wg, st in [(4, 1), (8, 1), (16, 1), (4, 4), (8, 2), (16, 4)]:
+            if wg != 4 and not exp:
+                continue
             r.set_option("wg_waves", wg)
             r.set_option("supertile", st)
             assert (r.get_option("wg_waves"), r.get_option("supertile")) == (wg, st)
@@ -364,6 +383,7 @@ def test_slab_march_bitexact(r, oracle, vol128, cap):
     the reference view and rotated views at 128^3, odd extents, a 200^3
     random volume on a small frame (big boxes), early-out, MediaScroll offsets
     inside the clamp-exact range (the non-zero-offset kernel)."""
+    need_experiments(r, "slab")
     r.set_volume(vol128)
     r.set_layout_preference(15)
     r.set_option("slab", 1)
@@ -401,6 +421,8 @@ def test_slab_march_bitexact(r, oracle, vol128, cap):
 @pytest.mark.parametrize("schedule,wps", [(0, 4), (1, 1), (1, 3), (1, 8), (2, 1), (2, 3), (2, 16), (3, 1), (4, 1), (4, 2),
                                           (4, 5), (5, 1), (5, 2), (5, 7)])
 def test_schedules_bitexact(r, oracle, vol128, schedule, wps):
+    if schedule in (1, 2, 3):   # queue, strided, XCD rows: measured slower
+        need_experiments(r, f"schedule {schedule}")
     sched0, tpw0 = r.get_option("schedule"), r.get_option("tiles_per_wave")
     r.set_option("schedule", schedule)
     r.set_option("waves_per_simd" if schedule == 1 else "tiles_per_wave", wps)
@@ -668,6 +690,7 @@ def test_procedural_shadow_region_enumeration(r, oracle):
     """Config 3 with the 64x64-region sort enumeration (option "proc_enum",
     a round-3 experiment; row-major is the default with shadow rays) stays
     bit-exact, with early-out and short shadow runs too."""
+    need_experiments(r, "proc_enum")
     r.set_option("proc_enum", 1)
     try:
         for W, H, m, kw in [(128, 72, vr.march_defaults(max_steps=128), dict(shadow_steps=8)),
@@ -706,8 +729,9 @@ def test_procedural_shadow_deferred(r, oracle, case):
     march = vr.march_defaults(**m)
     imgs, counts = [], []
     try:
-        for defer in (1, 0):
+        for defer, cache in ((1, 0), (0, 0), (1, 1), (1, 2)):   # shadow pass: register Worley cube / 8 lanes per entry
             r.set_option("shadow_defer", defer)
+            r.set_option("shadow_cache", cache)
             img, ref, c, s, var = render_proc_both(r, oracle, W, H, march, band=band, **kw)
             assert var == "procedural_shadow"
             assert_exact(img, ref)
@@ -723,9 +747,11 @@ def test_procedural_shadow_deferred(r, oracle, case):
             counts.append(cc)
     finally:
         r.set_option("shadow_defer", 1)   # the default
+        r.set_option("shadow_cache", 0)
         r.set_option("count", 0)
-    assert np.array_equal(imgs[0], imgs[1])
-    assert counts[0] == counts[1]
+    for k in range(1, len(imgs)):
+        assert np.array_equal(imgs[0], imgs[k]), k
+        assert counts[0] == counts[k], k
 
 
 def test_procedural_shadow_deferred_scratch_limit(r, oracle):
@@ -818,6 +844,7 @@ def test_procedural_shadow_deferred_stale_and_reuse(r, oracle):
     W, H = 160, 90
     march = vr.march_defaults(max_steps=64)
     r.set_option("shadow_defer", 1)
+    need_experiments(r, "sort_reuse")
     r.set_option("sort_reuse", 2)
     try:
         for k, phi in enumerate([20.0, 20.0, 21.6, 23.2, 24.8, 24.8]):
@@ -1047,7 +1074,7 @@ def translated_shader_data(W, H, t):
 
 
 @pytest.mark.parametrize("t", [(0.9, -0.4, 0.2), (1.8, -1.8, 0.0), (0.0, 0.0, 3.5)])
-@pytest.mark.parametrize("layout", [2, 5])
+@pytest.mark.parametrize("layout", [15, 5])
 @pytest.mark.parametrize("schedule", [4, 5])
 def test_ring_schedule_off_centre(r, oracle, vol128, t, layout, schedule):
     W, H = 400, 240
@@ -1214,12 +1241,14 @@ def test_regions_lists_across_streams(r, oracle, vol128):
         r.set_option("schedule", -1)
 
 
-@pytest.mark.parametrize("layout", [6, 7, 8, 9, 10, 11, 12, 13, 5, 14])
+@pytest.mark.parametrize("layout", [6, 7, 8, 9, 10, 11, 12, 13, 5, 14, 15])
 @pytest.mark.parametrize("split", [2, 4, 8])
 def test_split_rays_bitexact(r, oracle, vol128, layout, split):
     """Step-split rays (K lanes per ray, terms summed in step order): exact
     against the oracle, step counts included, with bands, a rotated cube,
     early-out and short rays (max_steps 7)."""
+    if layout in EXPERIMENTAL_LAYOUTS:
+        need_experiments(r, f"layout {layout}")
     r.set_layout_preference(layout)
     r.set_option("schedule", 5)
     r.set_option("split", split)

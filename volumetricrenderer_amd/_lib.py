@@ -121,6 +121,8 @@ _SIGS = {
     "vr_set_procedural": (ctypes.c_int, [_vp, ctypes.POINTER(Procedural)]),
     "vr_set_march": (ctypes.c_int, [_vp, ctypes.POINTER(MarchParams)]),
     "vr_render": (ctypes.c_int, [_vp, ctypes.POINTER(Target), _vp]),
+    "vr_render_sequence": (ctypes.c_int, [_vp, ctypes.POINTER(Target), ctypes.c_int, ctypes.POINTER(ObjectShaderData),
+                                          ctypes.POINTER(GlobalShaderData), _vp]),
     "vr_assemble_bands": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, _vp]),
     "vr_assemble_frame": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
@@ -191,6 +193,9 @@ _SHARD_SIGS = {
     "vr_shard_connect": (ctypes.c_int, [_vp, _vp]),
     "vr_shard_destroy": (ctypes.c_int, [_vp]),
     "vr_shard_run": (ctypes.c_int, [_vp, ctypes.c_int, _vp, ctypes.c_int, c_float_p]),
+    "vr_shard_run_frames": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(ObjectShaderData),
+                                           ctypes.POINTER(GlobalShaderData), _vp, ctypes.c_int, c_float_p,
+                                           ctypes.POINTER(ctypes.c_double)]),
     "vr_shard_frame": (ctypes.c_int, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(ctypes.c_size_t), c_int_p]),
     "vr_shard_copy_frame": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, _vp]),
     "vr_shard_rows": (ctypes.c_int, [_vp, c_int_p, c_int_p]),

@@ -112,6 +112,7 @@ struct Ctx {
     int shadow_defer_mib = kMaxDeferMiB;   // largest deferred-shadow scratch; a frame needing more compacts in-wave
     int shadow_blocks = 0;         // option "shadow_blocks": workgroups of the deferred shadow pass (0 = auto)
     int shadow_defer = 1;          // measured 1.25 -> 0.99 ms at config 3
+    int shadow_cache = 0;          // deferred shadow pass: Worley cube cached in registers per lane
     void* d_defer = nullptr;
     size_t defer_bytes = 0;
     unsigned long long defer_ent_cap = 0;   // entries / step records / waves the current scratch holds
@@ -792,6 +793,9 @@ int vr_band_rows_packed(int height, int band_rows, int band_stride, int band_fir
 vr_status vr_set_layout_preference(void* p, int pref)
 {
     if (!p || pref < 0 || pref >= kNumLayouts) return fail(VR_ERR_INVALID, "vr_set_layout_preference: bad argument");
+    if (pref > 0 && !layout_built(pref))
+        return fail(VR_ERR_INVALID, "vr_set_layout_preference: layout %d is built only with VR_EXPERIMENTS "
+                                    "(make EXPERIMENTS=1; measured slower, DESIGN.md sec. 4)", pref);
     Ctx* c = as_ctx(p);
     HIP_TRY(hipSetDevice(c->device));
     c->layout_pref = pref;
@@ -805,6 +809,15 @@ vr_status vr_set_option(void* p, const char* name, int value)
     if (!p || !name) return fail(VR_ERR_INVALID, "vr_set_option: null argument");
     Ctx* c = as_ctx(p);
     const std::string n(name);
+    // variants measured slower than the defaults (vr_internal.h VR_EXPERIMENTS)
+    const bool experimental = (n == "schedule" && (value == SCHED_QUEUE || value == SCHED_STRIDED ||
+                                                   value == SCHED_XCDROWS)) ||
+                              (n == "wg_waves" && value != 4) || (n == "split_long" && value != 0) ||
+                              (n == "slab" && value != 0) || (n == "sort_reuse" && value != 0) ||
+                              (n == "proc_enum" && value != 0);
+    if (experimental && !VR_EXPERIMENTS)
+        return fail(VR_ERR_INVALID, "vr_set_option: %s = %d is built only with VR_EXPERIMENTS (make EXPERIMENTS=1; "
+                                    "measured slower, DESIGN.md)", name, value);
     if (n == "layout") return vr_set_layout_preference(p, value);
     if (n == "schedule") {
         if (value < -1 || value > 5)
@@ -849,6 +862,13 @@ vr_status vr_set_option(void* p, const char* name, int value)
         if (value < 0) return fail(VR_ERR_INVALID, "vr_set_option: shadow_defer_entries >= 0");
         c->defer_entries = (unsigned)value;
         return release_defer(c);
+    }
+    if (n == "shadow_cache") {
+        if (value < 0 || value > 2)
+            return fail(VR_ERR_INVALID, "vr_set_option: shadow_cache is 0 (lane per entry), 1 (+ register Worley cube) "
+                                        "or 2 (8 lanes per entry)");
+        c->shadow_cache = value;
+        return VR_OK;
     }
     if (n == "shadow_blocks") {
         if (value < 0 || value > 65536) return fail(VR_ERR_INVALID, "vr_set_option: shadow_blocks in [0, 65536]");
@@ -943,6 +963,7 @@ int vr_get_option(void* p, const char* name)
     if (n == "proc_enum") return c->proc_enum;
     if (n == "shadow_defer") return c->shadow_defer;
     if (n == "shadow_blocks") return c->shadow_blocks;
+    if (n == "shadow_cache") return c->shadow_cache;
     if (n == "shadow_defer_mib") return c->shadow_defer_mib;
     if (n == "shadow_defer_entries") return (int)c->defer_entries;
     if (n == "shadow_defer_last") return c->defer_last;   // read-only
@@ -961,6 +982,7 @@ int vr_get_option(void* p, const char* name)
     }
     if (n == "supertile") return c->supertile;
     if (n == "lat") return c->lat;
+    if (n == "experiments") return VR_EXPERIMENTS;   // read-only: the measured-slower variants are built
     if (n == "region_interval") return c->region_interval;
     if (n == "region_gpu") return c->region_gpu;
     if (n == "region_gpu_builds") return (int)std::min<long long>(c->gpu_builds, 0x7fffffff);   // read-only
@@ -1202,6 +1224,8 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
         g.supertile = S; g.wedges = c->wedges;
         int* dev_hdr = nullptr;
         HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&dev_hdr), c->h_rghdr, 0));
+        // one build scratch per context: a build on another stream waits for the last one
+        if (c->gpu_builds > 0) HIP_TRY(hipStreamWaitEvent(stream, c->rg_ev, 0));
         HIP_TRY(launch_region_build(g, c->d_rg, rb.d + kRegionHeader, reinterpret_cast<int*>(rb.d), dev_hdr, stream));
         HIP_TRY(hipEventRecord(c->rg_ev, stream));
         c->rg_pending = true;
@@ -1518,6 +1542,7 @@ static vr_status ensure_defer(Ctx* c, const MarchArgs& a, void* sort_buf, Shadow
     // round (1,536 workgroups at 6 per CU), so the hardware dispatcher balances
     // the tail -- 3/8 of the sorted waves measured 0.90-0.91 ms against 0.98 at
     // config 3 (profiles/r03/ab_shadow_blocks_*.txt)
+    d->worley_cache = c->shadow_cache;
     d->eval_blocks = c->shadow_blocks ? (unsigned)c->shadow_blocks
                                       : (unsigned)std::max<size_t>(kShadowEvalBlocks, (size_t)L.waves * 3 / 8);
     return VR_OK;
@@ -1740,6 +1765,19 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
         }
     }
     HIP_TRY(launch_march(a, pl.layout, pl.wrap, pl.early, sc, static_cast<hipStream_t>(stream)));
+    return VR_OK;
+}
+
+vr_status vr_render_sequence(void* p, const vr_target* t, int frames, const vr_object_shader_data* osd,
+                             const vr_global_shader_data* gsd, void* stream)
+{
+    if (!p || !t || frames < 0 || (frames > 0 && (!osd || !gsd)))
+        return fail(VR_ERR_INVALID, "vr_render_sequence: bad argument");
+    for (int i = 0; i < frames; ++i) {
+        vr_status st = vr_set_shader_data(p, &osd[i], &gsd[i]);
+        if (st == VR_OK) st = vr_render(p, t, stream);
+        if (st != VR_OK) return st;
+    }
     return VR_OK;
 }
 

@@ -68,6 +68,21 @@ __host__ __device__ constexpr bool is_b4_family(int l)
            l == LAYOUT_BRICK4864 || l == LAYOUT_COL48;
 }
 
+// Variants measured slower than the defaults and kept as the record of that
+// (DESIGN.md sec. 4, 5.1-5.4): the layouts other than the auto ones, the
+// queue / strided / XCD-row schedules, split_long, 8- and 16-wave workgroups,
+// the LDS slab, and the procedural sort_reuse / proc_enum options.  They are
+// compiled only with VR_EXPERIMENTS=1 (make EXPERIMENTS=1); the default
+// library refuses their options.
+#ifndef VR_EXPERIMENTS
+#define VR_EXPERIMENTS 0
+#endif
+__host__ __device__ constexpr bool layout_built(int l)
+{
+    return VR_EXPERIMENTS || l == LAYOUT_PLANAR || l == LAYOUT_CORNER8 || l == LAYOUT_CORNERH || l == LAYOUT_COL48 ||
+           l == LAYOUT_BRICK4832;
+}
+
 enum Wrap : int { WRAP_CLAMP = 0, WRAP_MIRROR = 1 };
 
 // Geometry of a fast layout for one channel (host and device).
@@ -278,6 +293,7 @@ struct ShadowDefer {
     unsigned map_cap;                 // chunk map entries (ent_cap / 64 + waves)
     unsigned waves;                   // sorted waves the per-wave arrays hold
     unsigned eval_blocks;             // workgroups of the shadow pass (0 = kShadowEvalBlocks)
+    int worley_cache;                 // shadow pass: keep each lane's Worley cube in registers (option shadow_cache)
 };
 constexpr unsigned kDeferInPlace = 0xffffffffu;
 

@@ -88,7 +88,9 @@ hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_bu
                            positions, march_blocks, stale, d);                                                       \
         hipLaunchKernelGGL(proc_shadow_scan, dim3(1), dim3(kScanThreads), 0, s, total, d);                          \
         hipLaunchKernelGGL(proc_shadow_map, dim3((d.waves + 3) / 4), dim3(kThreads), 0, s, total, d);               \
-        hipLaunchKernelGGL((proc_shadow_eval<T>), dim3(d.eval_blocks ? d.eval_blocks : kShadowEvalBlocks), dim3(kThreads), wt_bytes, s, a, d); \
+        if (d.worley_cache == 2) hipLaunchKernelGGL((proc_shadow_eval8<T>), dim3(d.eval_blocks ? d.eval_blocks : kShadowEvalBlocks), dim3(kThreads), wt_bytes, s, a, d); \
+        else if (d.worley_cache) hipLaunchKernelGGL((proc_shadow_eval<T, true>), dim3(d.eval_blocks ? d.eval_blocks : kShadowEvalBlocks), dim3(kThreads), wt_bytes, s, a, d); \
+        else hipLaunchKernelGGL((proc_shadow_eval<T, false>), dim3(d.eval_blocks ? d.eval_blocks : kShadowEvalBlocks), dim3(kThreads), wt_bytes, s, a, d); \
     } while (0)
             if (tm == 3) {
                 if (early) VR_PD(true, 3); else VR_PD(false, 3);
@@ -151,21 +153,25 @@ hipError_t launch_march(const MarchArgs& a, int layout, int wrap, bool early, co
     if (sc.kind == SCHED_REGIONS && sc.lat > 0 && lat_supported(layout))
         return launch_march_lat(a, layout, early, sc, s);   // vr_march_lat.hip
     switch (layout) {
+    case LAYOUT_BRICK4832: return launch_lw<LAYOUT_BRICK4832, WRAP_CLAMP>(a, early, sc, s);
+    case LAYOUT_COL48:
+#if VR_EXPERIMENTS
+        if (sc.kind == SCHED_REGIONS && sc.slab && sc.split <= 1) return launch_march_slab(a, early, sc, s);
+#endif
+        return launch_lw<LAYOUT_COL48, WRAP_CLAMP>(a, early, sc, s);
+#if VR_EXPERIMENTS
     case LAYOUT_BRICK4: return launch_lw<LAYOUT_BRICK4, WRAP_CLAMP>(a, early, sc, s);
     case LAYOUT_BRICK448: return launch_lw<LAYOUT_BRICK448, WRAP_CLAMP>(a, early, sc, s);
     case LAYOUT_BRICK488: return launch_lw<LAYOUT_BRICK488, WRAP_CLAMP>(a, early, sc, s);
     case LAYOUT_BRICK4816: return launch_lw<LAYOUT_BRICK4816, WRAP_CLAMP>(a, early, sc, s);
     case LAYOUT_BRICK4864: return launch_lw<LAYOUT_BRICK4864, WRAP_CLAMP>(a, early, sc, s);
-    case LAYOUT_BRICK4832: return launch_lw<LAYOUT_BRICK4832, WRAP_CLAMP>(a, early, sc, s);
     case LAYOUT_BRICK41616: return launch_lw<LAYOUT_BRICK41616, WRAP_CLAMP>(a, early, sc, s);
-    case LAYOUT_COL48:
-        if (sc.kind == SCHED_REGIONS && sc.slab && sc.split <= 1) return launch_march_slab(a, early, sc, s);
-        return launch_lw<LAYOUT_COL48, WRAP_CLAMP>(a, early, sc, s);
     case LAYOUT_COL48Z: return launch_lw<LAYOUT_COL48Z, WRAP_CLAMP>(a, early, sc, s);
     case LAYOUT_ZPAIR: return launch_lw<LAYOUT_ZPAIR, WRAP_CLAMP>(a, early, sc, s);
     case LAYOUT_BRICK5: return launch_lw<LAYOUT_BRICK5, WRAP_CLAMP>(a, early, sc, s);
     case LAYOUT_BRICK8: return launch_lw<LAYOUT_BRICK8, WRAP_CLAMP>(a, early, sc, s);
     case LAYOUT_BRICK16: return launch_lw<LAYOUT_BRICK16, WRAP_CLAMP>(a, early, sc, s);
+#endif
     case LAYOUT_CORNER8:
     case LAYOUT_CORNERH: return launch_march_corner8(a, layout, early, sc, s);   // vr_march_c8.hip
     default: break;

@@ -490,9 +490,11 @@ __device__ __forceinline__ unsigned march_pixel(const MarchArgs& a, const FastCt
 // `cells` accumulates the Worley cells this evaluation computed (8, or 35 when
 // the pruned lane also ran the 27-cell block; 27 without the pruned table) --
 // vr option "count" = 2, the algorithmic work of the roofline (bench.py)
-template <int TABLE>
+// WC: the Worley cube comes from the lane's register cache *wc
+// (noise::cellular_table9_cached; the deferred shadow pass)
+template <int TABLE, bool WC = false>
 __device__ __forceinline__ float proc_density(const ProcParams& p, const float4* wt, float scale, float px, float py,
-                                              float pz, unsigned& cells)
+                                              float pz, unsigned& cells, noise::WorleyCube* wc = nullptr)
 {
     const float gs = noise::in_vgpr(p.grid_scale), lac = noise::in_vgpr(p.lacunarity), gain = noise::in_vgpr(p.gain);
     const float qx = px * gs, qy = py * gs, qz = pz * gs;
@@ -533,7 +535,8 @@ __device__ __forceinline__ float proc_density(const ProcParams& p, const float4*
     float f1;
     if constexpr (TABLE >= 2) {
         bool full;
-        f1 = noise::cellular_table9(wt, p.wt_lo, qx * wf, qy * wf, qz * wf, full) + 1.0f;
+        if constexpr (WC) f1 = noise::cellular_table9_cached(wt, p.wt_lo, qx * wf, qy * wf, qz * wf, full, *wc) + 1.0f;
+        else f1 = noise::cellular_table9(wt, p.wt_lo, qx * wf, qy * wf, qz * wf, full) + 1.0f;
         if (p.count_evals == 2) cells += full ? 35u : 8u;
     } else {
         if constexpr (TABLE == 1) f1 = noise::cellular_table(wt, p.wt_lo, p.wt_n, p.wt_pz, qx * wf, qy * wf, qz * wf) + 1.0f;
@@ -963,7 +966,11 @@ __global__ __launch_bounds__(64 * WGW) void march_regions(const MarchArgs a, con
 }
 // with uniform channels UM (march_pixel's fetch_u / blend_u)
 #ifndef VR_UM_ATTR
+#ifdef VR_UM_WAVES   // timing experiments: the _u kernels built for this many waves per SIMD
+#define VR_UM_ATTR __attribute__((amdgpu_waves_per_eu(VR_UM_WAVES)))
+#else
 #define VR_UM_ATTR
+#endif
 #endif
 template <int LAYOUT, int WRAP, bool EARLY, bool ZO, int UM>
 __global__ __launch_bounds__(kThreads) VR_UM_ATTR void march_regions_u(const MarchArgs a, const unsigned* __restrict__ tiles,
@@ -1633,9 +1640,10 @@ constexpr int kScanThreads = 1024;
     for (unsigned k = lane; k * 64u < n; k += 64u) d.map[c0 + k] = make_uint4(e0 + k * 64u, 0u, min(64u, n - k * 64u), 0u);
 }
 
-template <int TABLE>
+template <int TABLE, bool WC>
 __global__ __launch_bounds__(kThreads) void proc_shadow_eval(const MarchArgs a, ShadowDefer d)
 {
+    noise::WorleyCube wc;   // WC: the lane's Worley cube, kept across its samples (and entries)
     extern __shared__ float4 wt_lds[];
     const float4* wt = worley_table<TABLE>(a.proc, wt_lds);
     const ProcParams& p = a.proc;
@@ -1654,12 +1662,59 @@ __global__ __launch_bounds__(kThreads) void proc_shadow_eval(const MarchArgs a, 
             q0 = q0 + l0; q1 = q1 + l1; q2 = q2 + l2;
             // march_pixel_proc's box test as min3 / max3 (q is never NaN)
             if (fminf(fminf(q0, q1), q2) >= 0.0f && fmaxf(fmaxf(q0, q1), q2) <= 1.0f) {
-                sl = sl + proc_density<TABLE>(p, wt, a.scale, q0, q1, q2, cells);
+                sl = sl + proc_density<TABLE, WC>(p, wt, a.scale, q0, q1, q2, cells, &wc);
                 ++evals;
             }
         }
         const float tl = spec_expf(-(sl * p.od));
         *reinterpret_cast<float2*>(e) = make_float2(en.w, tl);
+    }
+    if (a.step_counter) add_steps(a, p.count_evals == 2 ? cells : p.count_evals ? evals : 0u);
+}
+
+// The shadow pass with 8 lanes per entry (option shadow_cache = 2): lane j of
+// an entry's group of 8 evaluates the sun samples j, j + 8, ... of its ray
+// (reached by the same sequential adds, P + (s+1) L), and the group sums them
+// in sample order through __shfl, so sl is the per-lane loop's, bit for bit
+// (an out-of-box sample adds +0, which leaves sl >= +0 unchanged).  The 8
+// lanes of a group sample one sun ray a few texels apart, so their Worley
+// cube and Perlin corners mostly coincide: their LDS table reads broadcast
+// instead of spreading over 64 rays' cells (bank conflicts, verdict r03 #5).
+template <int TABLE>
+__global__ __launch_bounds__(kThreads) void proc_shadow_eval8(const MarchArgs a, ShadowDefer d)
+{
+    extern __shared__ float4 wt_lds[];
+    const float4* wt = worley_table<TABLE>(a.proc, wt_lds);
+    const ProcParams& p = a.proc;
+    const unsigned units = *d.count * 8u;   // 8 entries per unit
+    const int S = p.shadow_steps;
+    const unsigned lane = threadIdx.x & 63, g = lane >> 3, j = lane & 7;
+    const float l0 = noise::in_vgpr(p.lstep[0]), l1 = noise::in_vgpr(p.lstep[1]), l2 = noise::in_vgpr(p.lstep[2]);
+    unsigned evals = 0, cells = 0;
+    for (unsigned u = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6); u < units; u += gridDim.x * (kThreads / 64)) {
+        const uint4 mc = d.map[u >> 3];   // wave-uniform
+        const unsigned k = (u & 7u) * 8u + g;   // the group's entry within the chunk
+        const bool has = k < mc.z;
+        float4* e = d.ent + mc.x + k;
+        float4 en = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (has) en = *e;
+        float q0 = en.x, q1 = en.y, q2 = en.z, sl = 0.0f;
+        for (unsigned t = 0; t <= j; ++t) { q0 = q0 + l0; q1 = q1 + l1; q2 = q2 + l2; }   // sample j
+        for (int r = 0; r < S; r += 8) {
+            float v = 0.0f;
+            // march_pixel_proc's box test as min3 / max3 (q is never NaN)
+            if (has && r + (int)j < S && fminf(fminf(q0, q1), q2) >= 0.0f && fmaxf(fmaxf(q0, q1), q2) <= 1.0f) {
+                v = proc_density<TABLE>(p, wt, a.scale, q0, q1, q2, cells);
+                ++evals;
+            }
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {   // the group's samples r .. r + 7, in order
+                const float vt = __shfl(v, (int)(g * 8u) + t);
+                if (r + t < S) sl = sl + vt;
+            }
+            for (int t = 0; t < 8; ++t) { q0 = q0 + l0; q1 = q1 + l1; q2 = q2 + l2; }   // sample j + r + 8
+        }
+        if (has && j == 0) *reinterpret_cast<float2*>(e) = make_float2(en.w, spec_expf(-(sl * p.od)));
     }
     if (a.step_counter) add_steps(a, p.count_evals == 2 ? cells : p.count_evals ? evals : 0u);
 }
@@ -1717,6 +1772,7 @@ hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStre
     const size_t lds = L == LAYOUT_PLANAR || L == LAYOUT_CORNERH ? 0
                      : (size_t)(a.nx + a.ny + a.nz + 3) * sizeof(unsigned) * (L == LAYOUT_COL48Z ? 2 : 1);
     const dim3 block(kThreads);
+#if VR_EXPERIMENTS
     if (sc.kind == SCHED_STRIDED) {
         const int tiles = ((a.width + 7) >> 3) * ((a.out_rows + 7) >> 3);
         const int tpw = sc.tiles_per_wave > 0 ? sc.tiles_per_wave : 1;
@@ -1728,6 +1784,7 @@ hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStre
             hipLaunchKernelGGL((march_strided<L, W, false>), grid, block, lds, s, a, 4 * (int)grid.x);
         return hipGetLastError();
     }
+#endif
     if (sc.kind == SCHED_RINGS) {
         const int tiles_x8 = (a.width + 7) >> 3, rows8 = (a.out_rows + 7) >> 3;
         const int cx = min(max(sc.center_x >> 3, 0), tiles_x8 - 1), cy = min(max(sc.center_y >> 3, 0), rows8 - 1);
@@ -1755,6 +1812,7 @@ hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStre
             else launch_regions_split<L, 8>(a, early, sc, grid, lds, s);
             return hipGetLastError();
         }
+#if VR_EXPERIMENTS
         if constexpr (L == LAYOUT_COL48 || L == LAYOUT_BRICK4832 || L == LAYOUT_CORNERH) {
             if (sc.kind == SCHED_REGIONS && (sc.mixed == 2 || sc.mixed == 4)) {
                 const dim3 grid((unsigned)(8 * ((sc.map.nwx + 3) / 4)));
@@ -1768,7 +1826,9 @@ hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStre
                 return hipGetLastError();
             }
         }
+#endif
     }
+#if VR_EXPERIMENTS
     if constexpr (L == LAYOUT_COL48 || L == LAYOUT_BRICK4832 || L == LAYOUT_CORNERH) {
         if (sc.kind == SCHED_REGIONS && (sc.wg_waves == 8 || sc.wg_waves == 16)) {
             const int g = sc.wg_waves;
@@ -1783,6 +1843,7 @@ hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStre
             return hipGetLastError();
         }
     }
+#endif
     if constexpr (L == LAYOUT_COL48 || L == LAYOUT_BRICK4832 || L == LAYOUT_CORNERH || L == LAYOUT_COL48Z) {
         // one uniform channel (the reference recipe's G, TestMain.cpp:60/76):
         // its loads are skipped; other masks run the general kernel (exact too)
@@ -1817,6 +1878,7 @@ hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStre
             hipLaunchKernelGGL((march_regions<L, W, false, false>), grid, block, lds, s, a, sc.tiles, sc.hdr, sc.map.nwx);
         return hipGetLastError();
     }
+#if VR_EXPERIMENTS
     if (sc.kind == SCHED_XCDROWS) {
         const int groups = (((a.width + 7) >> 3) + 3) >> 2, rows8 = (a.out_rows + 7) >> 3;
         const dim3 grid(8 * ((rows8 + 7) / 8) * groups);
@@ -1836,6 +1898,7 @@ hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStre
             hipLaunchKernelGGL((march_queue<L, W, false>), grid, block, lds, s, a, sc.heads);
         return hipGetLastError();
     }
+#endif
     const dim3 grid(a.num_blocks);
     if (early)
         hipLaunchKernelGGL((march_grid<L, W, true>), grid, block, lds, s, a);

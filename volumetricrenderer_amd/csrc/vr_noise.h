@@ -396,6 +396,54 @@ __device__ inline float cellular_table9(const float4* __restrict__ tab, int lo, 
     return d0 - 1.0f;
 }
 
+// cellular_table9 for a lane that evaluates a run of nearby samples (the
+// deferred shadow pass: a sun ray's samples are ~2 texels apart, Worley cells
+// at f = .03 ~33): the unit cube's 8 table entries stay in registers while
+// the cube's base cell is unchanged (key = its table offset), so the LDS is
+// read only when a sample crosses a cell face.  The same entries, the same
+// ops: bit-identical to cellular_table9.
+struct WorleyCube {
+    int fo = -1;   // byte offset of the cached cube's base entry (-1: none)
+    float4 c[8];
+};
+__device__ inline float cellular_table9_cached(const float4* __restrict__ tab, int lo, float x, float y, float z,
+                                               bool& full, WorleyCube& wc)
+{
+    const float xf = floorf(x), yf = floorf(y), zf = floorf(z);
+    const float x0 = xf - x, x1 = (xf + 1.0f) - x;
+    const float y0 = yf - y, y1 = (yf + 1.0f) - y;
+    const float z0 = zf - z, z1 = (zf + 1.0f) - z;
+    const float c = (float)(16 * lo * (1 + kWorleyN + kWorleyPz));
+    const int fo = (int)fmaf(zf, (float)(16 * kWorleyPz), fmaf(yf, (float)(16 * kWorleyN), fmaf(xf, 16.0f, -c)));
+    if (fo != wc.fo) {
+        wc.fo = fo;
+        const float4* t0 = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(tab) + fo);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) wc.c[k] = t0[(k & 1) * kWorleyPz + ((k >> 1) & 1) * kWorleyN + (k >> 2)];
+    }
+    float d0 = 3.402823466e+38f;
+#pragma unroll
+    for (int xi = 0; xi <= 1; ++xi) {
+#pragma unroll
+        for (int yi = 0; yi <= 1; ++yi) {
+#pragma unroll
+            for (int zi = 0; zi <= 1; ++zi) {
+                const float4 cc = wc.c[xi * 4 + yi * 2 + zi];
+                const float xd = fmaf(cc.x, cc.w, xi ? x1 : x0);
+                const float yd = fmaf(cc.y, cc.w, yi ? y1 : y0);
+                const float zd = fmaf(cc.z, cc.w, zi ? z1 : z0);
+                d0 = fminf(d0, fmaf(zd, zd, fmaf(yd, yd, xd * xd)));
+            }
+        }
+    }
+    const float gx = fminf(-x0, x1), gy = fminf(-y0, y1), gz = fminf(-z0, z1);
+    const float bound = fmaf(2.0f, fminf(gx, fminf(gy, gz)), fmaf(gz, gz, fmaf(gy, gy, fmaf(gx, gx, 1.0f))));
+    const float e = __builtin_amdgcn_sqrtf(d0) + kPruneR;
+    full = e * e > bound;
+    if (full) d0 = fminf(d0, cellular_table9_full(tab, lo, x, y, z));
+    return d0 - 1.0f;
+}
+
 // One table entry: cellular()'s feature-point data for integer cell (ix, iy, iz).
 __device__ inline float4 cellular_cell(int32_t seed, int ix, int iy, int iz)
 {

@@ -216,8 +216,10 @@ vr_status wait_event(vr_shard* sh, hipEvent_t e, const char* what)
         return he == hipErrorNotReady ? 1 : 2;
     }, sh->timeout_s);
     if (res == 0) return VR_OK;
-    if (res == 1 && he != hipSuccess && he != hipErrorNotReady)
-        return fail(VR_ERR_HIP, "%s: %s", what, hipGetErrorString(he));
+    if (res == 1 && he != hipSuccess && he != hipErrorNotReady) {
+        abort_comm(sh);   // as wait_stream: every later collective fails at once
+        return fail(VR_ERR_HIP, "%s: %s; communicator aborted", what, hipGetErrorString(he));
+    }
     return deadline_fail(sh, res, what);
 }
 
@@ -423,7 +425,14 @@ vr_status vr_shard_destroy(vr_shard* sh)
 
 vr_status vr_shard_run(vr_shard* sh, int frames, void* stream, int sample_every, float* kernel_ms)
 {
-    if (!sh || frames < 0) return fail(VR_ERR_INVALID, "vr_shard_run: bad argument");
+    return vr_shard_run_frames(sh, frames, nullptr, nullptr, stream, sample_every, kernel_ms, nullptr);
+}
+
+vr_status vr_shard_run_frames(vr_shard* sh, int frames, const vr_object_shader_data* osd,
+                              const vr_global_shader_data* gsd, void* stream, int sample_every, float* kernel_ms,
+                              double* host_ms)
+{
+    if (!sh || frames < 0 || (!osd) != (!gsd)) return fail(VR_ERR_INVALID, "vr_shard_run: bad argument");
     if (kernel_ms && sample_every <= 0) return fail(VR_ERR_INVALID, "vr_shard_run: sample_every must be > 0");
     if (sh->loopback && sh->rank != 0)
         return fail(VR_ERR_INVALID, "vr_shard_run: rank %d is not connected (vr_shard_connect)", sh->rank);
@@ -436,15 +445,20 @@ vr_status vr_shard_run(vr_shard* sh, int frames, void* stream, int sample_every,
         sh->timing.push_back(ev);
     }
     int next = 0;
+    const auto h0 = std::chrono::steady_clock::now();
     for (int i = 0; i < frames; ++i) {
         const int p = sh->last < 0 ? 0 : sh->last ^ 1;
         const bool samp = kernel_ms && i % sample_every == 0;
         hipEvent_t t0 = samp ? sh->timing[2 * next] : nullptr, t1 = samp ? sh->timing[2 * next + 1] : nullptr;
         if (samp) ++next;
+        if (osd) VR_TRY(vr_set_shader_data(sh->ctx, &osd[i], &gsd[i]));   // this frame's camera
         const vr_status st = one_frame(sh, p, s, t0, t1);
         if (st != VR_OK) return st;
     }
     if (sh->last >= 0) HIP_TRY(hipStreamWaitEvent(s, sh->done[sh->last], 0));   // the caller's stream sees the frame
+    if (host_ms)
+        *host_ms = frames ? std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count() / frames
+                          : 0.0;
     if (kernel_ms) {
         double sum = 0.0;
         for (int k = 0; k < next; ++k) {
@@ -513,16 +527,20 @@ vr_status vr_shard_share_volume(vr_shard* sh, const void* d_rgba8, int nx, int n
     int got[7] = {};
     hipError_t he = hipMemcpyAsync(sh->token + 1, agree, sizeof agree, hipMemcpyHostToDevice, sh->comm_stream);
     ncclResult_t nr = ncclSuccess;
+    vr_status st = VR_OK;   // a settle()/wait failure keeps its own status and message (VR_ERR_TIMEOUT / _COMM)
     if (he == hipSuccess) {
         nr = ncclAllReduce(sh->token + 1, sh->token + 1, 7, ncclInt32, ncclMax, sh->comm, sh->comm_stream);
-        if (nr == ncclInProgress) nr = settle(sh, "vr_shard_share_volume: agreement") == VR_OK ? ncclSuccess : ncclInternalError;
+        if (nr == ncclInProgress) {
+            st = settle(sh, "vr_shard_share_volume: agreement");
+            nr = ncclSuccess;
+        }
     }
-    if (he == hipSuccess && nr == ncclSuccess)
+    if (he == hipSuccess && nr == ncclSuccess && st == VR_OK)
         he = hipMemcpyAsync(got, sh->token + 1, sizeof got, hipMemcpyDeviceToHost, sh->comm_stream);
-    vr_status st = VR_OK;
-    if (he == hipSuccess && nr == ncclSuccess) st = wait_stream(sh, sh->comm_stream, "vr_shard_share_volume: agreement");
+    if (he == hipSuccess && nr == ncclSuccess && st == VR_OK)
+        st = wait_stream(sh, sh->comm_stream, "vr_shard_share_volume: agreement");
     if (he != hipSuccess || nr != ncclSuccess || st != VR_OK) {
-        if (buf) (void)hipFree(buf);
+        if (buf && !sh->aborted) (void)hipFree(buf);
         if (st != VR_OK) return st;
         if (nr != ncclSuccess) {
             if (!sh->aborted) abort_comm(sh);
@@ -543,13 +561,18 @@ vr_status vr_shard_share_volume(vr_shard* sh, const void* d_rgba8, int nx, int n
     if (he == hipSuccess) he = hipStreamWaitEvent(sh->comm_stream, sh->fence, 0);
     if (he == hipSuccess) {
         nr = ncclBroadcast(data, data, bytes, ncclUint8, 0, sh->comm, sh->comm_stream);
-        if (nr == ncclInProgress) nr = settle(sh, "vr_shard_share_volume: broadcast") == VR_OK ? ncclSuccess : ncclInternalError;
-        if (nr == ncclSuccess) {
+        if (nr == ncclInProgress) {
+            st = settle(sh, "vr_shard_share_volume: broadcast");   // keeps its status and message
+            nr = ncclSuccess;
+        }
+        if (nr == ncclSuccess && st == VR_OK) {
             he = hipEventRecord(sh->fence, sh->comm_stream);
             if (he == hipSuccess) he = hipStreamWaitEvent(s, sh->fence, 0);
         }
     }
-    if (nr != ncclSuccess) {
+    if (st != VR_OK) {
+        // settle() aborted the communicator and set the message
+    } else if (nr != ncclSuccess) {
         if (!sh->aborted) abort_comm(sh);
         st = fail(VR_ERR_COMM, "vr_shard_share_volume: ncclBroadcast: %s", ncclGetErrorString(nr));
     } else if (he != hipSuccess) {
@@ -557,10 +580,14 @@ vr_status vr_shard_share_volume(vr_shard* sh, const void* d_rgba8, int nx, int n
     } else if (vr_set_volume_device(sh->ctx, data, nx, ny, nz, stream) != VR_OK) {
         st = fail(VR_ERR_HIP, "vr_shard_share_volume: vr_set_volume_device: %s", vr_last_error());
     }
-    // the broadcast must be finished (or the communicator aborted) before buf goes
-    const vr_status w1 = wait_stream(sh, sh->comm_stream, "vr_shard_share_volume: broadcast");
-    const vr_status w2 = w1 == VR_OK ? wait_stream(sh, s, "vr_shard_share_volume: install") : w1;
-    if (st == VR_OK) st = w2;
+    // the broadcast must be finished (or the communicator aborted) before buf
+    // goes; after an abort the waits are skipped, so they cannot overwrite the
+    // message of the real cause
+    if (!sh->aborted) {
+        const vr_status w1 = wait_stream(sh, sh->comm_stream, "vr_shard_share_volume: broadcast");
+        const vr_status w2 = w1 == VR_OK ? wait_stream(sh, s, "vr_shard_share_volume: install") : w1;
+        if (st == VR_OK) st = w2;
+    }
     if (buf && !sh->aborted) (void)hipFree(buf);   // an aborted broadcast may still own it: leak, not corrupt
     return st;
 }

@@ -321,13 +321,27 @@ class RcclBandPipeline:
         """True once an error or a missed deadline aborted the communicator."""
         return bool(_lib.shard_call("vr_shard_aborted", self._h))
 
-    def run_frames(self, k: int, stream=None, sample_every: int = 0):
+    def run_frames(self, k: int, stream=None, sample_every: int = 0, cameras=None):
         """Queue k frames (collective).  Returns the mean duration (ms) of the
-        sampled renders when sample_every > 0, else None."""
+        sampled renders when sample_every > 0, else None.  cameras: k
+        (ObjectShaderData, GlobalShaderData) pairs, one per frame (a moving
+        camera, vr_shard_run_frames; every rank passes the same); after the
+        call self.host_ms is the host time per frame spent queueing them."""
         from .renderer import _stream_handle
         ms = ctypes.c_float()
-        _lib.shard_call("vr_shard_run", self._h, k, _stream_handle(stream), sample_every,
-                        ctypes.byref(ms) if sample_every > 0 else None)
+        host = ctypes.c_double()
+        if cameras is None:
+            _lib.shard_call("vr_shard_run_frames", self._h, k, None, None, _stream_handle(stream), sample_every,
+                            ctypes.byref(ms) if sample_every > 0 else None, ctypes.byref(host))
+        else:
+            cams = list(cameras)
+            if len(cams) != k:
+                raise ValueError(f"run_frames: {k} frames need {k} cameras, got {len(cams)}")
+            osd = (_lib.ObjectShaderData * max(1, k))(*[c[0] for c in cams])
+            gsd = (_lib.GlobalShaderData * max(1, k))(*[c[1] for c in cams])
+            _lib.shard_call("vr_shard_run_frames", self._h, k, osd, gsd, _stream_handle(stream), sample_every,
+                            ctypes.byref(ms) if sample_every > 0 else None, ctypes.byref(host))
+        self.host_ms = host.value
         return ms.value if sample_every > 0 else None
 
     def share_volume(self, vol=None, stream=None) -> None:

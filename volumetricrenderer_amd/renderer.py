@@ -280,6 +280,21 @@ class Renderer:
         call("vr_render", self._ctx, ctypes.byref(t), _stream_handle(stream))
         return out
 
+    def render_sequence(self, width: int, height: int, fmt: int, out: torch.Tensor, cameras, band_rows: int = 0,
+                        band_stride: int = 1, band_first: int = 0, stream=None) -> torch.Tensor:
+        """The reference's frame loop with a moving camera (TestMain.cpp:173-256):
+        one render per (ObjectShaderData, GlobalShaderData) of `cameras`, all
+        into `out`, queued natively (vr_render_sequence) without host waits."""
+        self._check_target(width, height, fmt, out, band_rows, band_stride, band_first)
+        cams = list(cameras)
+        osd = (ObjectShaderData * max(1, len(cams)))(*[c[0] for c in cams])
+        gsd = (GlobalShaderData * max(1, len(cams)))(*[c[1] for c in cams])
+        t = Target(width=width, height=height, format=fmt, band_rows=band_rows, band_stride=band_stride,
+                   band_first=band_first, pixels=out.data_ptr(), row_pitch=out.stride(0) * out.element_size(),
+                   step_counter=None)
+        call("vr_render_sequence", self._ctx, ctypes.byref(t), len(cams), osd, gsd, _stream_handle(stream))
+        return out
+
     def prepare_render(self, width: int, height: int, fmt: int, out: torch.Tensor, band_rows: int = 0,
                        band_stride: int = 1, band_first: int = 0, stream=None):
         """A zero-argument launcher for one fixed render (target, bands,
