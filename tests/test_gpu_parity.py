@@ -1398,6 +1398,49 @@ def test_config4_8_rank_loopback(r, config4):
             pl.close()
 
 
+def test_region_lists_outlive_destroyed_streams(r, oracle, vol128):
+    """Region lists rendered on streams the caller destroys afterwards (the
+    native loop's own render streams, gone at close()): later rebuilds -- on
+    the GPU and on the host, every render -- must not touch those streams.
+    vr_render records each stream's 'lists used' event right after its
+    launch, never later on a remembered stream handle (round 4: recording on
+    a destroyed stream aborted the process inside the HIP runtime)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from volumetricrenderer_amd.distributed import RcclBandPipeline
+    W, H = 320, 180
+    r.set_volume(vol128)
+    r.set_march(vr.march_defaults())
+    r.set_option("region_interval", 1)
+    try:
+        for gpu in (1, 0):
+            r.set_option("region_gpu", gpu)
+            osd, gsd = vr.reference_shader_data(W / H, 3.0, 0.0)
+            r.set_shader_data(osd, gsd)
+            r.render(W, H, 0)   # lists for the full target on the default stream
+            pl = RcclBandPipeline(r, W, H, 0, band_rows=16, world=2, rank=0, loopback=True)
+            try:
+                pl.run_frames(2)   # rank 0's and rank 1's lists, on the loop's streams
+                pl.frame()
+            finally:
+                pl.close()
+            torch.cuda.synchronize()
+            for i in range(1, 5):   # spinning: a rebuild every render retires the loop's lists
+                osd, gsd = vr.reference_shader_data(W / H, 3.0 + SPIN_DEG * i, 0.0)
+                r.set_shader_data(osd, gsd)
+                cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+                img = r.render(W, H, 0, step_counter=cnt)
+            torch.cuda.synchronize()
+            obj, glob = vr.shader_data_arrays(osd, gsd)
+            ref, steps = oracle.render(vol128, obj, glob, oracle.from_params(vr.march_defaults()), W, H, 0)
+            assert_exact(img.cpu().numpy(), ref)
+            assert int(cnt.item()) == steps
+    finally:
+        r.set_option("region_gpu", 1)
+        r.set_option("region_interval", 32)
+
+
 @pytest.mark.parametrize("cam", [(4.0, 2.0, 2.5), (0.3, -0.2, 0.5), (-4.0, 1.0, 0.0), (3.0, 3.0, 3.0001)])
 @pytest.mark.parametrize("layout", [0, 1, 12])
 def test_camera_position_off_the_view_eye(r, oracle, vol128, cam, layout):

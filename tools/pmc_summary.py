@@ -23,7 +23,7 @@ def derived(c):
     if "SQ_ACTIVE_INST_VALU" in c and "GRBM_GUI_ACTIVE" in c:
         # quad-cycles of VALU issue over all SIMDs vs SIMD quad-cycles available
         d["valu_busy"] = c["SQ_ACTIVE_INST_VALU"] / (1024 * c["GRBM_GUI_ACTIVE"] / 8 / 4)
-    for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+    for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_LDS"):
         if k in c and "SQ_WAVE_CYCLES" in c:
             d[k + "_frac"] = c[k] / c["SQ_WAVE_CYCLES"]
     if "TCC_HIT_sum" in c:
@@ -43,6 +43,8 @@ def derived(c):
                      ("TCP_TOTAL_CACHE_ACCESSES_sum", "l1_lookups_per_vmem_inst")):
             if k in c:
                 d[n] = c[k] / vm
+    if "SQ_ACTIVE_INST_LDS" in c and cyc:
+        d["lds_issue_busy_per_cu"] = c["SQ_ACTIVE_INST_LDS"] / (256 * cyc)   # LDS issue cycles per CU cycle
     if "SQ_LDS_BANK_CONFLICT" in c and c.get("SQ_INSTS_LDS"):
         d["lds_conflict_cycles_per_lds_inst"] = c["SQ_LDS_BANK_CONFLICT"] / c["SQ_INSTS_LDS"]
     if "TCC_EA0_RDREQ_sum" in c:

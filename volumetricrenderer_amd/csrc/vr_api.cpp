@@ -157,17 +157,20 @@ struct Ctx {
         int most = 0;              // the longest per-XCD list (sizes the launch)
         int nwork = 0;             // tiles with estimated work
         int mixed = 0;             // the lists hold this many sub-blocks (2, 4) of the longest tiles (bit 31)
-        // the streams that rendered with these lists; when the lists are
-        // retired an event is recorded on each, and the buffer is rewritten
-        // only after those events (kMaxRegionStreams; more -> device sync)
+        // the streams that rendered with these lists and, per stream, an event
+        // recorded after each of its renders; the buffer is rewritten only
+        // after those events (kMaxRegionStreams; more -> device sync).  The
+        // events are recorded at render time, never later on a remembered
+        // stream: the caller may have destroyed that stream since.
         hipStream_t streams[kMaxRegionStreams] = {};
-        hipEvent_t retired[kMaxRegionStreams] = {};
+        hipEvent_t used[kMaxRegionStreams] = {};
         int nstreams = 0;          // -1: more streams than tracked
-        int nretired = 0;
+        int nretired = 0;          // events of the renders before the lists were retired
         hipEvent_t uploaded = nullptr;   // the list upload (on streams[0]); other streams wait for it
         hipStream_t upload_stream = nullptr;
     } region[2];
     int region_cur = -1;           // buffer of the current lists (-1 = none)
+    int region_slot = -1;          // the render stream's event slot in it (note_region_stream)
     float region_key[kRegionKeyLen] = {};   // geometry the current lists were built for
     long long renders_since_build = 0;
     // procedural cost sort: the geometry whose order d_sort holds (n per pixel
@@ -543,7 +546,7 @@ vr_status vr_destroy(void* p)
     for (auto& b : c->region) {
         if (b.d) (void)hipFree(b.d);
         if (b.h) (void)hipHostFree(b.h);
-        for (hipEvent_t e : b.retired)
+        for (hipEvent_t e : b.used)
             if (e) (void)hipEventDestroy(e);
         if (b.uploaded) (void)hipEventDestroy(b.uploaded);
     }
@@ -1079,16 +1082,43 @@ void box_centre_pixel(const Ctx* c, const MarchArgs& a, int* px, int* prow)
 // is in exactly one list whatever the estimate, so a list built for an older
 // camera stays correct: a moving camera reuses it for kRegionRebuildInterval
 // renders.  Rebuilds go to the other of two buffers, once the renders that
-// last read it are done (events recorded when it was retired, on the streams
-// that used it; not a device sync), uploaded on the render stream.
-vr_status note_region_stream(Ctx::RegionBuf& rb, hipStream_t s)
+// last read it are done (per stream, an event recorded after each render; not
+// a device sync), uploaded on the render stream.
+//
+// `s` waits for `ev` unless it has already completed (an event recorded on a
+// stream the caller has destroyed since is complete: no wait is queued for it)
+static vr_status stream_wait_pending(hipStream_t s, hipEvent_t ev)
 {
+    const hipError_t q = hipEventQuery(ev);
+    if (q == hipSuccess) return VR_OK;
+    if (q != hipErrorNotReady) return fail(VR_ERR_HIP, "vr_render: event query: %s", hipGetErrorString(q));
+    (void)hipGetLastError();   // not an error: still queued
+    HIP_TRY(hipStreamWaitEvent(s, ev, 0));
+    return VR_OK;
+}
+
+// The render stream s uses the lists: *slot = the stream's event slot (-1:
+// untracked, more streams than kMaxRegionStreams), recorded after the launch
+vr_status note_region_stream(Ctx::RegionBuf& rb, hipStream_t s, int* slot)
+{
+    *slot = -1;
     if (rb.nstreams < 0) return VR_OK;
     for (int i = 0; i < rb.nstreams; ++i)
-        if (rb.streams[i] == s) return VR_OK;
-    if (s != rb.upload_stream) HIP_TRY(hipStreamWaitEvent(s, rb.uploaded, 0));   // first use on another stream
-    if (rb.nstreams == kMaxRegionStreams) rb.nstreams = -1;
-    else rb.streams[rb.nstreams++] = s;
+        if (rb.streams[i] == s) {
+            *slot = i;
+            return VR_OK;
+        }
+    if (s != rb.upload_stream) {   // first use on another stream
+        const vr_status st = stream_wait_pending(s, rb.uploaded);
+        if (st != VR_OK) return st;
+    }
+    if (rb.nstreams == kMaxRegionStreams) {
+        rb.nstreams = -1;
+        return VR_OK;
+    }
+    if (!rb.used[rb.nstreams]) HIP_TRY(hipEventCreateWithFlags(&rb.used[rb.nstreams], hipEventDisableTiming));
+    *slot = rb.nstreams;
+    rb.streams[rb.nstreams++] = s;
     return VR_OK;
 }
 
@@ -1126,15 +1156,8 @@ static vr_status next_region_buf(Ctx* c, size_t n, bool host_staging, hipStream_
     if (c->region_cur >= 0) {   // retire the current lists in the stream order of their renders
         Ctx::RegionBuf& old = c->region[c->region_cur];
         old.nretired = 0;
-        if (old.nstreams < 0) {
-            HIP_TRY(hipDeviceSynchronize());
-        } else {
-            for (int i = 0; i < old.nstreams; ++i) {
-                if (!old.retired[i]) HIP_TRY(hipEventCreateWithFlags(&old.retired[i], hipEventDisableTiming));
-                HIP_TRY(hipEventRecord(old.retired[i], old.streams[i]));
-            }
-            old.nretired = old.nstreams;
-        }
+        if (old.nstreams < 0) HIP_TRY(hipDeviceSynchronize());
+        else old.nretired = old.nstreams;   // their events were recorded after each render
         old.nstreams = 0;
     }
     const int b = c->region_cur < 0 ? 0 : c->region_cur ^ 1;
@@ -1144,8 +1167,12 @@ static vr_status next_region_buf(Ctx* c, size_t n, bool host_staging, hipStream_
         poll_region_header(c);
     }
     for (int i = 0; i < rb.nretired; ++i) {   // its last renders
-        if (host_staging || rb.d == nullptr) HIP_TRY(hipEventSynchronize(rb.retired[i]));
-        else HIP_TRY(hipStreamWaitEvent(stream, rb.retired[i], 0));
+        if (host_staging || rb.d == nullptr) {
+            HIP_TRY(hipEventSynchronize(rb.used[i]));
+        } else {
+            const vr_status st = stream_wait_pending(stream, rb.used[i]);
+            if (st != VR_OK) return st;
+        }
     }
     rb.nretired = 0;
     if (n > rb.cap) {
@@ -1180,7 +1207,7 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     poll_region_header(c);
     const bool same_grid = c->region_cur >= 0 && std::memcmp(key, c->region_key, grid_part * sizeof(float)) == 0;
     if (same_grid && (std::memcmp(key, c->region_key, sizeof key) == 0 || c->renders_since_build < c->region_interval))
-        return note_region_stream(c->region[c->region_cur], stream);
+        return note_region_stream(c->region[c->region_cur], stream, &c->region_slot);
 
     const int S = c->supertile;
     // a moved camera over the same target (no split_long sub-blocks): the
@@ -1225,7 +1252,10 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
         int* dev_hdr = nullptr;
         HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&dev_hdr), c->h_rghdr, 0));
         // one build scratch per context: a build on another stream waits for the last one
-        if (c->gpu_builds > 0) HIP_TRY(hipStreamWaitEvent(stream, c->rg_ev, 0));
+        if (c->gpu_builds > 0) {
+            const vr_status sw = stream_wait_pending(stream, c->rg_ev);
+            if (sw != VR_OK) return sw;
+        }
         HIP_TRY(launch_region_build(g, c->d_rg, rb.d + kRegionHeader, reinterpret_cast<int*>(rb.d), dev_hdr, stream));
         HIP_TRY(hipEventRecord(c->rg_ev, stream));
         c->rg_pending = true;
@@ -1240,7 +1270,7 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
         rb.map.nwx = std::max(1, (most + tpw - 1) / tpw);
         rb.mixed = 0;
         rb.nstreams = 0;
-        const vr_status st = note_region_stream(rb, stream);
+        const vr_status st = note_region_stream(rb, stream, &c->region_slot);
         if (st != VR_OK) return st;
         c->region_cur = b;
         std::memcpy(c->region_key, key, sizeof key);
@@ -1352,7 +1382,7 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     rb.nwork = (int)work.size();
     rb.mixed = mixed;
     rb.nstreams = 0;
-    const vr_status st = note_region_stream(rb, stream);
+    const vr_status st = note_region_stream(rb, stream, &c->region_slot);
     if (st != VR_OK) return st;
     c->region_cur = b;
     std::memcpy(c->region_key, key, sizeof key);
@@ -1765,6 +1795,8 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
         }
     }
     HIP_TRY(launch_march(a, pl.layout, pl.wrap, pl.early, sc, static_cast<hipStream_t>(stream)));
+    if (kind == SCHED_REGIONS && c->region_slot >= 0)   // the lists' last use on this stream
+        HIP_TRY(hipEventRecord(c->region[c->region_cur].used[c->region_slot], static_cast<hipStream_t>(stream)));
     return VR_OK;
 }
 
