@@ -229,41 +229,67 @@ def test_every_layout_bitexact(r, oracle, vol128, layout, name):
         r.set_layout_preference(0)
 
 
-@pytest.mark.parametrize("layout", [15, 12, 14, 7])
+@pytest.mark.parametrize("layout", [15, 12, 14, 1])
 def test_split_long_tiles_bitexact(r, oracle, vol128, layout):
-    """split_long (march_regions_mixed): the tiles costing >= split_long % of
-    the longest are marched as KS sub-blocks with KS lanes per ray, the rest
-    with one.  split = 1 gives KS = 2 (halves), split = 2 / 4 KS = 2 / 4.
-    1 % splits every tile with work, 100 % only the longest; bit-exact with
-    exact step counts, with and without early-out, and with a banded target
-    (packed rows).  Layout 7 (zpair) has no mixed kernel: the option must
-    leave it on its plain / split path."""
-    need_experiments(r, "split_long")
+    """split_long (round 4): the tiles costing >= split_long % of the longest
+    get their own per-XCD lists, marched in a second launch on the context's
+    side stream with split_long_k lanes per ray, while the rest keep the
+    frame's split K.  1 % puts every tile with work in the long launch, 100 %
+    only the longest; bit-exact with exact step counts (both launches add to
+    one counter), with early-out, a banded target (packed rows), the
+    latency-mode march for the long launch, and GPU-built lists (a moving
+    camera).  Layout 1 (planar) cannot split: the option leaves it on one
+    launch."""
     r.set_volume(vol128)
     r.set_layout_preference(layout)
-    r.set_option("split", 1)
     try:
-        for split, pct in [(1, 1), (1, 60), (1, 100), (2, 50), (4, 1), (4, 70)]:
-            r.set_option("split", split)   # 1: long tiles in halves (KS = 2); 2, 4: KS = the split K
+        for split, pct, kl in [(1, 1, 2), (1, 60, 4), (1, 100, 8), (2, 50, 4), (4, 1, 8), (1, 70, 8)]:
+            r.set_option("split", split)
             r.set_option("split_long", pct)
-            assert r.get_option("split_long") == pct
+            r.set_option("split_long_k", kl)
+            assert r.get_option("split_long") == pct and r.get_option("split_long_k") == kl
             for (W, H, phi, theta) in [(480, 270, 0.0, 0.0), (203, 117, 35.0, -20.0)]:
                 osd, gsd = vr.reference_shader_data(W / H, phi, theta)
                 img, ref, c, s = render_both(r, oracle, vol128, W, H, osd, gsd)
                 assert_exact(img, ref)
                 assert c == s
+                if layout != 1 and pct < 100:
+                    assert r.get_option("region_long_tiles") > 0
+        r.set_option("split", 0)
         r.set_option("split_long", 50)
         osd, gsd = vr.reference_shader_data(16 / 9, -40.0, 15.0)
         m = vr.march_defaults(early_out=0.5)
         img, ref, c, s = render_both(r, oracle, vol128, 320, 180, osd, gsd, march=m)
         assert_exact(img, ref)
         assert c == s
-        img, ref, c, s = render_both(r, oracle, vol128, 320, 180, osd, gsd, band_rows=16, band_stride=3,
-                                     band_first=1)
-        assert_exact(img, ref)
-        assert c == s
+        for lat in (0, 3):   # the long launch on the latency-mode march
+            r.set_option("lat", lat)
+            img, ref, c, s = render_both(r, oracle, vol128, 320, 180, osd, gsd, band_rows=16, band_stride=3,
+                                         band_first=1)
+            assert_exact(img, ref)
+            assert c == s
+        r.set_option("lat", 0)
+        # a moving camera: GPU-built long / short lists, rebuilt every render
+        r.set_option("region_interval", 1)
+        W, H = 320, 180
+        r.set_march(vr.march_defaults())
+        for i in range(1, 6):
+            osd, gsd = vr.reference_shader_data(W / H, SPIN_DEG * i, 0.0)
+            r.set_shader_data(osd, gsd)
+            cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+            img = r.alloc_target(W, H, 0)
+            img.fill_(float("nan"))
+            r.render(W, H, 0, out=img, step_counter=cnt)
+        torch.cuda.synchronize()
+        obj, glob = vr.shader_data_arrays(osd, gsd)
+        ref, steps = oracle.render(vol128, obj, glob, oracle.from_params(vr.march_defaults()), W, H, 0)
+        assert_exact(img.cpu().numpy(), ref)
+        assert int(cnt.item()) == steps
     finally:
+        r.set_option("region_interval", 32)
+        r.set_option("lat", 0)
         r.set_option("split_long", 0)
+        r.set_option("split_long_k", 4)
         r.set_option("split", 0)
         r.set_layout_preference(0)
 

@@ -136,7 +136,10 @@ struct Ctx {
     int slab = 0;                  // COL48 + regions: the LDS slab march (vr_march_slab.hip)
     int proc_enum = 0;             // procedural sort: 1 = 64x64-region enumeration with shadow rays too
     int slab_cap = kSlabMaxChunks; // its chunks per channel (<= kSlabMaxChunks; smaller forces the fallback)
-    int split_long = 0;            // regions: tiles costing >= this % of the longest split in two halves (0 = off)
+    int split_long = 0;            // regions: tiles costing >= this % of the longest get their own launch (0 = off)
+    int split_long_k = 4;          // lanes per ray of that launch (2, 4, 8)
+    hipStream_t side_stream = nullptr;   // split_long: the long tiles' launch (forked from the render stream)
+    hipEvent_t fork_ev = nullptr, join_ev = nullptr;
     int wg_waves = 4;              // regions: waves per workgroup (4, 8, 16)
     int supertile = 2;             // regions: list order by S x S blocks of tiles (1 = per tile; 2 measured 1 % faster)
     int lat = 0;                   // regions: latency-mode march, rounds of loads in flight (0 = off, -1 = auto, 2-4)
@@ -156,7 +159,9 @@ struct Ctx {
         TileMap map{};             // host copy: nwx (and off[] for host builds)
         int most = 0;              // the longest per-XCD list (sizes the launch)
         int nwork = 0;             // tiles with estimated work
-        int mixed = 0;             // the lists hold this many sub-blocks (2, 4) of the longest tiles (bit 31)
+        int longs = 0;             // 1: split_long lists (launched on their own, even when empty)
+        int most_long = 0;         // the longest per-XCD long list
+        int nlong = 0;             // long tiles
         // the streams that rendered with these lists and, per stream, an event
         // recorded after each of its renders; the buffer is rewritten only
         // after those events (kMaxRegionStreams; more -> device sync).  The
@@ -540,6 +545,9 @@ vr_status vr_destroy(void* p)
     if (c->d_rg) (void)hipFree(c->d_rg);
     if (c->h_rghdr) (void)hipHostFree(c->h_rghdr);
     if (c->rg_ev) (void)hipEventDestroy(c->rg_ev);
+    if (c->side_stream) (void)hipStreamDestroy(c->side_stream);
+    if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
+    if (c->join_ev) (void)hipEventDestroy(c->join_ev);
     if (c->d_mm) (void)hipFree(c->d_mm);
     if (c->h_mm) (void)hipHostFree(c->h_mm);
     if (c->mm_ready) (void)hipEventDestroy(c->mm_ready);
@@ -815,7 +823,7 @@ vr_status vr_set_option(void* p, const char* name, int value)
     // variants measured slower than the defaults (vr_internal.h VR_EXPERIMENTS)
     const bool experimental = (n == "schedule" && (value == SCHED_QUEUE || value == SCHED_STRIDED ||
                                                    value == SCHED_XCDROWS)) ||
-                              (n == "wg_waves" && value != 4) || (n == "split_long" && value != 0) ||
+                              (n == "wg_waves" && value != 4) ||
                               (n == "slab" && value != 0) || (n == "sort_reuse" && value != 0) ||
                               (n == "proc_enum" && value != 0);
     if (experimental && !VR_EXPERIMENTS)
@@ -892,6 +900,11 @@ vr_status vr_set_option(void* p, const char* name, int value)
         if (value < 0 || value > kSlabMaxChunks)
             return fail(VR_ERR_INVALID, "vr_set_option: slab_cap in [0, %d]", kSlabMaxChunks);
         c->slab_cap = value;
+        return VR_OK;
+    }
+    if (n == "split_long_k") {
+        if (value != 2 && value != 4 && value != 8) return fail(VR_ERR_INVALID, "vr_set_option: split_long_k is 2, 4 or 8");
+        c->split_long_k = value;
         return VR_OK;
     }
     if (n == "split_long") {
@@ -974,6 +987,8 @@ int vr_get_option(void* p, const char* name)
         return (int)std::min<size_t>((c->defer_bytes + 1023) / 1024, 0x7fffffff);
     if (n == "slab_cap") return c->slab_cap;
     if (n == "split_long") return c->split_long;
+    if (n == "split_long_k") return c->split_long_k;
+    if (n == "region_long_tiles") return c->region_cur >= 0 ? c->region[c->region_cur].nlong : 0;
     if (n == "sort_reuse") return c->sort_reuse;
     if (n == "wg_waves") return c->wg_waves;
     if (n == "uniform_skip") return c->uniform_skip;
@@ -1145,6 +1160,8 @@ static void poll_region_header(Ctx* c)
     Ctx::RegionBuf& rb = c->region[c->rg_buf];
     rb.nwork = c->h_rghdr[9];
     rb.most = c->h_rghdr[10];
+    rb.most_long = c->h_rghdr[12];
+    rb.nlong = c->h_rghdr[13];
 }
 
 // Retire the current lists (events on the streams that rendered with them) and
@@ -1191,13 +1208,12 @@ static vr_status next_region_buf(Ctx* c, size_t n, bool host_staging, hipStream_
     return VR_OK;
 }
 
-vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow, bool mixable, hipStream_t stream)
+vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow, int long_pct, hipStream_t stream)
 {
     const int tw = (a.width + 7) >> 3, th = (a.out_rows + 7) >> 3;
     float key[kRegionKeyLen] = {(float)tw, (float)th, (float)a.width, (float)a.height, (float)a.out_rows,
                                 (float)a.band_rows, (float)a.band_stride, (float)a.band_first, (float)tpw,
-                                (float)c->wedges, (float)(mixable ? c->split_long : 0), (float)c->split,
-                                (float)c->supertile};
+                                (float)c->wedges, (float)long_pct, (float)c->split, (float)c->supertile};
     constexpr int grid_part = 13;   // the part a reused list must match
     int kn = grid_part;
     for (float v : {(float)a.max_steps, a.step_size, (float)cpx, (float)cprow}) key[kn++] = v;
@@ -1210,14 +1226,14 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
         return note_region_stream(c->region[c->region_cur], stream, &c->region_slot);
 
     const int S = c->supertile;
-    // a moved camera over the same target (no split_long sub-blocks): the
-    // lists come from the GPU build on the render stream (vr_regions.hip) --
-    // no host loop, no host wait; tiles with work and the longest list are
-    // the last completed build's (they size the launch, not the result)
-    if (same_grid && c->region_gpu && !(mixable && c->split_long > 0) && th < 65536 && tw < 65536) {
+    // a moved camera over the same target: the lists come from the GPU build
+    // on the render stream (vr_regions.hip) -- no host loop, no host wait;
+    // tiles with work and the longest lists are the last completed build's
+    // (they size the launches, not the result)
+    if (same_grid && c->region_gpu && th < 65536 && tw < 65536) {
         const size_t n = (size_t)tw * th;
         const Ctx::RegionBuf& cur = c->region[c->region_cur];
-        const int nwork = cur.nwork, most = cur.most;
+        const int nwork = cur.nwork, most = cur.most, most_long = cur.most_long, nlong = cur.nlong;
         const size_t need = region_build_bytes((int)n);
         if (need > c->rg_bytes) {
             if (c->d_rg) {
@@ -1248,7 +1264,7 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
         }
         g.ccx = (cpx + 0.5) / 8.0; g.ccy = (cprow + 0.5) / 8.0;
         g.ctx = (cpx >> 3) / S; g.cty = (cprow >> 3) / S;
-        g.supertile = S; g.wedges = c->wedges;
+        g.supertile = S; g.wedges = c->wedges; g.long_pct = long_pct;
         int* dev_hdr = nullptr;
         HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&dev_hdr), c->h_rghdr, 0));
         // one build scratch per context: a build on another stream waits for the last one
@@ -1268,7 +1284,9 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
         rb.most = most;
         rb.map = TileMap{};
         rb.map.nwx = std::max(1, (most + tpw - 1) / tpw);
-        rb.mixed = 0;
+        rb.longs = long_pct > 0 ? 1 : 0;
+        rb.most_long = most_long;
+        rb.nlong = nlong;
         rb.nstreams = 0;
         const vr_status st = note_region_stream(rb, stream, &c->region_slot);
         if (st != VR_OK) return st;
@@ -1335,44 +1353,45 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     std::sort(idle.begin(), idle.end(), inside_out);
     for (size_t i = 0; i < idle.size(); ++i) xl[i % 8].push_back(idle[i]);
 
-    // split_long: the tiles costing >= split_long % of the longest go in as KS
-    // sub-blocks marched KS lanes per ray (march_regions_mixed), the rest with
-    // one lane per ray.  KS = the frame's split K (auto_split), or 2 where that
-    // is 1.
+    // split_long: the tiles costing >= long_pct % of the longest form their own
+    // per-XCD lists (first in the buffer, same inside-out order), launched
+    // separately with split_long_k lanes per ray (vr_render)
     double most_cost = 0.0;
     for (const T& t : work) most_cost = std::max(most_cost, t.cost);
-    const double split_at = std::max(1.0, most_cost * c->split_long / 100.0);
-    const int kall = auto_split(c, (long long)work.size());
-    const int ks = kall > 1 ? kall : 2;
-    const int mixed = mixable && c->split_long > 0 && th < 8192 && ks <= 4 ? ks : 0;
-    size_t n = (size_t)tw * th;
-    if (mixed)
-        for (const T& t : work) n += (size_t)(t.cost >= split_at) * (size_t)(ks - 1);
+    const double split_at = std::max(1.0, most_cost * long_pct / 100.0);
+    const size_t n = (size_t)tw * th;
     int b = 0;
     const vr_status st0 = next_region_buf(c, n, true, stream, &b);
     if (st0 != VR_OK) return st0;
     Ctx::RegionBuf& rb = c->region[b];
-    TileMap m{};
-    size_t pos = 0, most = 0;
+    int* hdr = reinterpret_cast<int*>(rb.h);
+    std::memset(hdr, 0, kRegionHeader * sizeof(int));
     unsigned* list = rb.h + kRegionHeader;
-    for (int x = 0; x < 8; ++x) {
+    size_t pos = 0, most_long = 0, most = 0;
+    for (int x = 0; x < 8; ++x) {   // the long lists
+        hdr[kRegionLongHdr + x] = (int)pos;
+        if (long_pct > 0)
+            for (const T& t : xl[x])
+                if (t.cost >= split_at) list[pos++] = t.id;
+        most_long = std::max(most_long, pos - (size_t)hdr[kRegionLongHdr + x]);
+    }
+    hdr[kRegionLongHdr + 8] = (int)pos;
+    const size_t nlong = pos;
+    TileMap m{};
+    for (int x = 0; x < 8; ++x) {   // the rest
         m.off[x] = (int)pos;
-        for (const T& t : xl[x]) {
-            if (mixed && t.cost >= split_at) {
-                for (int q = 0; q < mixed; ++q) list[pos++] = t.id | 0x80000000u | ((unsigned)q << 29);
-            } else {
-                list[pos++] = t.id;
-            }
-        }
+        for (const T& t : xl[x])
+            if (long_pct == 0 || t.cost < split_at) list[pos++] = t.id;
         most = std::max(most, pos - (size_t)m.off[x]);
     }
     m.off[8] = (int)pos;
     m.nwx = std::max(1, (int)((most + tpw - 1) / tpw));
-    int* hdr = reinterpret_cast<int*>(rb.h);
     for (int x = 0; x < 9; ++x) hdr[x] = m.off[x];
     hdr[9] = (int)work.size();
     hdr[10] = (int)most;
     hdr[11] = (int)pos;
+    hdr[12] = (int)most_long;
+    hdr[13] = (int)nlong;
     HIP_TRY(hipMemcpyAsync(rb.d, rb.h, (n + kRegionHeader) * sizeof(unsigned), hipMemcpyHostToDevice, stream));
     if (!rb.uploaded) HIP_TRY(hipEventCreateWithFlags(&rb.uploaded, hipEventDisableTiming));
     HIP_TRY(hipEventRecord(rb.uploaded, stream));
@@ -1380,7 +1399,9 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     rb.map = m;
     rb.most = (int)most;
     rb.nwork = (int)work.size();
-    rb.mixed = mixed;
+    rb.longs = long_pct > 0 ? 1 : 0;
+    rb.most_long = (int)most_long;
+    rb.nlong = (int)nlong;
     rb.nstreams = 0;
     const vr_status st = note_region_stream(rb, stream, &c->region_slot);
     if (st != VR_OK) return st;
@@ -1416,9 +1437,6 @@ static vr_status ensure_lattice(Ctx* c, ProcParams* q, hipStream_t s)
         c->lat_key[2] = -1;
         if (bytes > c->lat_cap) {
             if (c->d_lat) (void)hipFree(c->d_lat);
-    if (c->d_rg) (void)hipFree(c->d_rg);
-    if (c->h_rghdr) (void)hipHostFree(c->h_rghdr);
-    if (c->rg_ev) (void)hipEventDestroy(c->rg_ev);
             c->d_lat = nullptr;
             c->lat_cap = 0;
             if (hipMalloc(&c->d_lat, bytes) != hipSuccess) return fail(VR_ERR_OOM, "vr_render: lattice table");
@@ -1688,7 +1706,7 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
         // schedule 0 = one 8x8 tile per wave in row order, 4 = in rings;
         // otherwise (auto) the cost-sorted schedule
         void* sort_buf = nullptr;
-        Schedule sc{c->schedule == SCHED_RINGS ? SCHED_RINGS : SCHED_STATIC, 0, 0, 1, 1, nullptr, nullptr, {}, 1, 0, 0, 4, 0, nullptr};
+        Schedule sc{c->schedule == SCHED_RINGS ? SCHED_RINGS : SCHED_STATIC, 0, 0, 1, 1, nullptr, nullptr, {}, 1, 0, 4, 0, nullptr};
         if (sc.kind == SCHED_RINGS) box_centre_pixel(c, a, &sc.center_x, &sc.center_y);
         // the sort passes enumerate whole 64x64 regions (vr_march_kernels.h sort_pixel)
         if (c->schedule != SCHED_STATIC && c->schedule != SCHED_RINGS && a.width < 65536 && a.out_rows < 65536 &&
@@ -1756,33 +1774,46 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
     // wedges of the frame, each walked inside-out (longest rays first)
     const int kind = c->schedule >= 0 ? c->schedule : SCHED_REGIONS;
     const int tpw = c->tiles_per_wave > 0 ? c->tiles_per_wave : (kind == SCHED_RINGS || kind == SCHED_REGIONS ? 2 : 1);
-    Schedule sc{kind, 0, 0, tpw, c->waves_per_simd, c->d_heads, nullptr, {}, 1, 0, 0, c->wg_waves, 0, nullptr};
+    Schedule sc{kind, 0, 0, tpw, c->waves_per_simd, c->d_heads, nullptr, {}, 1, 0, c->wg_waves, 0, nullptr};
+    Schedule lsc = sc;   // split_long: the long tiles' launch
+    bool two = false;
     sc.slab = pl.layout == LAYOUT_COL48 && c->slab;
     a.slab_cap = c->slab_cap;
     if (kind == SCHED_RINGS || kind == SCHED_REGIONS) box_centre_pixel(c, a, &sc.center_x, &sc.center_y);
     if (kind == SCHED_REGIONS) {
         const bool splittable = is_b4_family(pl.layout) || pl.layout == LAYOUT_ZPAIR || pl.layout == LAYOUT_CORNER8 ||
                                 pl.layout == LAYOUT_CORNERH || pl.layout == LAYOUT_COL48Z;
-        const bool mixable = !sc.slab && (pl.layout == LAYOUT_COL48 || pl.layout == LAYOUT_BRICK4832 ||
-                                          pl.layout == LAYOUT_CORNERH);   // march_regions_mixed instances
-        const vr_status st = build_regions(c, a, tpw, sc.center_x, sc.center_y, mixable,
+        // split_long: the long tiles in their own lists and launch (below)
+        const int long_pct = splittable && !sc.slab && c->split_long > 0 ? c->split_long : 0;
+        const vr_status st = build_regions(c, a, tpw, sc.center_x, sc.center_y, long_pct,
                                            static_cast<hipStream_t>(stream));
         if (st != VR_OK) return st;
         const Ctx::RegionBuf& rb = c->region[c->region_cur];
         sc.tiles = rb.d + kRegionHeader;
         sc.hdr = reinterpret_cast<const int*>(rb.d);
         sc.map = rb.map;
-        sc.mixed = rb.mixed;
+        const bool lat_ok = c->lat > 0 && lat_supported(pl.layout) && !sc.slab;
+        if (rb.longs) {
+            // the long tiles: split_long_k lanes per ray, launched whatever the
+            // last known count (a GPU-built list may hold long tiles the host
+            // has not seen yet; the kernels stride over whatever the header says)
+            lsc = sc;
+            lsc.hdr = sc.hdr + kRegionLongHdr;
+            lsc.split = c->split_long_k;
+            lsc.lat = lat_ok ? c->lat : 0;
+            lsc.map.nwx = std::max(1, (rb.most_long * lsc.split + tpw - 1) / tpw);
+            two = true;
+        }
         // step-split rays: K lanes per ray when the frame
         // share is too small to fill the GPU with one-lane-per-ray waves
-        if (c->lat > 0 && lat_supported(pl.layout) && !sc.slab && !rb.mixed) {
+        if (lat_ok && !two) {
             // latency-mode march (vr_march_lat.hip): K lanes per ray, c->lat rounds of loads in flight
             const int K = c->split > 0 ? c->split : auto_split(c, rb.nwork);
             const int most = rb.most;
             sc.lat = c->lat;
             sc.split = K;
             sc.map.nwx = std::max(1, (most * K + tpw - 1) / tpw);
-        } else if (splittable && !rb.mixed) {
+        } else if (splittable) {
             int K = c->split;
             if (sc.slab) K = K == 0 ? 1 : K;   // the slab march has one lane per ray; split > 1 uses the plain march
             if (K == 0) K = auto_split(c, rb.nwork);
@@ -1793,6 +1824,27 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
                 sc.map.nwx = std::max(1, (most * K + ktpw - 1) / ktpw);
             }
         }
+    }
+    if (two) {
+        // long tiles on the context's side stream, forked from and joined back
+        // into the render stream (capturable into a hipGraph); launched first
+        // so that their waves start first
+        const hipStream_t s = static_cast<hipStream_t>(stream);
+        if (!c->side_stream) {
+            int lo = 0, hi = 0;
+            HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+            HIP_TRY(hipStreamCreateWithPriority(&c->side_stream, hipStreamNonBlocking, hi));
+            HIP_TRY(hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming));
+        }
+        HIP_TRY(hipEventRecord(c->fork_ev, s));
+        HIP_TRY(hipStreamWaitEvent(c->side_stream, c->fork_ev, 0));
+        HIP_TRY(launch_march(a, pl.layout, pl.wrap, pl.early, lsc, c->side_stream));
+        HIP_TRY(launch_march(a, pl.layout, pl.wrap, pl.early, sc, s));
+        HIP_TRY(hipEventRecord(c->join_ev, c->side_stream));
+        HIP_TRY(hipStreamWaitEvent(s, c->join_ev, 0));
+        if (c->region_slot >= 0) HIP_TRY(hipEventRecord(c->region[c->region_cur].used[c->region_slot], s));
+        return VR_OK;
     }
     HIP_TRY(launch_march(a, pl.layout, pl.wrap, pl.early, sc, static_cast<hipStream_t>(stream)));
     if (kind == SCHED_REGIONS && c->region_slot >= 0)   // the lists' last use on this stream

@@ -224,11 +224,19 @@ struct TileMap {
     int nwx;
 };
 // The regions schedule's lists in device memory: a header of kRegionHeader
-// ints -- off[0..8] (XCD x renders list entries [off[x], off[x+1])), tiles
-// with estimated work, the longest list, tiles -- then the entries.  Built on
-// the host (vr_api.cpp build_regions) or, for a moving camera, on the GPU
-// (vr_regions.hip launch_region_build, the same dealing).
-constexpr int kRegionHeader = 16;
+// ints, then the entries.  Two sets of per-XCD lists: the long tiles (option
+// split_long: estimated cost >= that % of the frame's longest; marched with
+// split_long_k lanes per ray in their own launch) and the rest.  The header:
+//   [0..8]   off[]: XCD x renders the (short) entries [off[x], off[x+1])
+//   [9]      tiles with estimated work    [10] the longest short list
+//   [11]     entries                       [12] the longest long list
+//   [13]     long tiles
+//   [16..24] the long lists' off[] (empty without split_long)
+// Long lists come first in the entries.  Built on the host (vr_api.cpp
+// build_regions) or, for a moving camera, on the GPU (vr_regions.hip
+// launch_region_build, the same dealing).
+constexpr int kRegionHeader = 32;
+constexpr int kRegionLongHdr = 16;   // the long lists' off[] in the header
 struct RegionBuild {
     int tw, th, width, out_rows, band_rows, band_stride, band_first, max_steps;
     float step_size;
@@ -236,6 +244,7 @@ struct RegionBuild {
     double ccx, ccy;       // box-centre tile (fractional), S x S block of it
     int ctx, cty;
     int supertile, wedges;
+    int long_pct;          // split_long: tiles costing >= this % of the longest are long (0 = none)
 };
 size_t region_build_bytes(int ntiles);
 // h_hdr (optional, host-mapped): a copy of the header, for sizing later launches
@@ -252,7 +261,6 @@ struct Schedule {
     TileMap map;           // regions (nwx counts waves of split units)
     int split;             // regions: lanes per ray (1, 2, 4, 8; BRICK4 / CORNER8 only)
     int slab;              // regions + COL48: the LDS slab march (vr_march_slab.hip)
-    int mixed;             // regions: 2 or 4 = the list holds that many sub-blocks of each longest tile (march_regions_mixed)
     int wg_waves;          // regions (one lane per ray): waves per workgroup, 4 (default), 8 or 16
     int lat;               // regions: latency-mode march (vr_march_lat.hip), rounds of loads in flight (0 = off)
     const int* hdr;        // regions: the lists' device header (kRegionHeader; off[x] per XCD)

@@ -1080,47 +1080,6 @@ __global__ __launch_bounds__(kThreads) void march_regions_split(const MarchArgs 
     if (a.step_counter) add_steps(a, steps);
 }
 
-// Regions schedule with the longest tiles split (vr_set_option "split_long"):
-// a list entry with bit 31 set is sub-block (bits 29-30) of a tile marched
-// with KS lanes per ray (march_pixel_split; the sub-blocks of
-// march_regions_split); the other tiles keep one lane per ray.  For a small
-// frame share (N GPUs) the launch ends with its longest rays' dependent
-// memory round trips: split those without paying the
-// split's lane overhead on every tile.
-template <int LAYOUT, bool EARLY, bool ZO, int KS>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void march_regions_mixed(const MarchArgs a, const unsigned* __restrict__ tiles,
-                                                               const int* __restrict__ hdr, int nwx)
-{
-    constexpr int R = 64 / KS, SW = KS >= 4 ? 4 : 8, SH = R / SW, NSX = 8 / SW;
-    extern __shared__ __attribute__((aligned(16))) unsigned lds[];
-    const int xcd = blockIdx.x & 7;
-    const int w = (int)(blockIdx.x >> 3) * (kThreads / 64) + (threadIdx.x >> 6);
-    const int begin = hdr[xcd], count = hdr[xcd + 1] - begin;
-    if ((int)(blockIdx.x >> 3) * (kThreads / 64) >= count) return;   // whole workgroup, before the barrier
-#ifdef VR_TIMELINE
-    const unsigned long long t_begin = __builtin_amdgcn_s_memrealtime();
-#endif
-    const FastCtx f = fast_prologue<LAYOUT>(a, lds);
-    const int lane = threadIdx.x & 63, k = lane / R, rho = lane % R;
-    const int px = ((rho >> 2) % (SW / 2)) * 2 + (rho & 1), py = ((rho >> 2) / (SW / 2)) * 2 + ((rho >> 1) & 1);
-    unsigned long long steps = 0;
-    for (int u = w; w < nwx && u < count; u += nwx) {
-        const unsigned t = tiles[begin + u];
-        const int tx = (int)(t & 0xffffu), ty = (int)((t >> 16) & 0x1fffu);
-        if (t >> 31) {
-            const int s = (int)((t >> 29) & 3u);
-            steps += march_pixel_split<LAYOUT, EARLY, ZO, KS>(a, f, tx * 8 + (s % NSX) * SW + px,
-                                                              ty * 8 + (s / NSX) * SH + py, k, rho);
-        } else
-            steps += march_pixel<LAYOUT, WRAP_CLAMP, EARLY, ZO>(a, f, tx * 8 + lane_x<LAYOUT>(lane),
-                                                                ty * 8 + lane_y<LAYOUT>(lane));
-    }
-#ifdef VR_TIMELINE
-    timeline_record(t_begin, steps);
-#endif
-    if (a.step_counter) add_steps(a, steps);
-}
-
 template <int L, int K>
 void launch_regions_split(const MarchArgs& a, bool early, const Schedule& sc, dim3 grid, size_t lds, hipStream_t s)
 {
@@ -1812,21 +1771,6 @@ hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStre
             else launch_regions_split<L, 8>(a, early, sc, grid, lds, s);
             return hipGetLastError();
         }
-#if VR_EXPERIMENTS
-        if constexpr (L == LAYOUT_COL48 || L == LAYOUT_BRICK4832 || L == LAYOUT_CORNERH) {
-            if (sc.kind == SCHED_REGIONS && (sc.mixed == 2 || sc.mixed == 4)) {
-                const dim3 grid((unsigned)(8 * ((sc.map.nwx + 3) / 4)));
-#define VR_MX(KS) \
-    if (early && a.zero_offsets) hipLaunchKernelGGL((march_regions_mixed<L, true, true, KS>), grid, block, lds, s, a, sc.tiles, sc.hdr, sc.map.nwx); \
-    else if (early) hipLaunchKernelGGL((march_regions_mixed<L, true, false, KS>), grid, block, lds, s, a, sc.tiles, sc.hdr, sc.map.nwx); \
-    else if (a.zero_offsets) hipLaunchKernelGGL((march_regions_mixed<L, false, true, KS>), grid, block, lds, s, a, sc.tiles, sc.hdr, sc.map.nwx); \
-    else hipLaunchKernelGGL((march_regions_mixed<L, false, false, KS>), grid, block, lds, s, a, sc.tiles, sc.hdr, sc.map.nwx)
-                if (sc.mixed == 2) { VR_MX(2); } else { VR_MX(4); }
-#undef VR_MX
-                return hipGetLastError();
-            }
-        }
-#endif
     }
 #if VR_EXPERIMENTS
     if constexpr (L == LAYOUT_COL48 || L == LAYOUT_BRICK4832 || L == LAYOUT_CORNERH) {
