@@ -285,10 +285,16 @@ vr_status vr_set_layout_preference(void* ctx, int pref);
  *                     waves render one block.
  *   "wg_waves"        4 (default), 8, 16: waves per workgroup of the regions
  *                     march (col48, brick4832, cornerh).
- *   "split_long"      0-100 (percent, default 0 = off), regions schedule with
- *                     one lane per ray: tiles whose estimated work is at least
- *                     this share of the longest are marched as two halves with
- *                     two lanes per ray.
+ *   "segment"         0 (off, the default) or 4-4096 steps, regions schedule
+ *                     (col48, brick4832, cornerh): tiles whose estimated work
+ *                     is at least 2L steps are marched as segments of L steps,
+ *                     one wave each, and a resolve pass adds each ray's stored
+ *                     terms in step order (bit-exact).  For small frame shares
+ *                     (N GPUs), whose time is their longest rays.  Scratch:
+ *                     segmented tiles x max_steps x 256 bytes, at most 1 GiB
+ *                     per context (grown inside vr_render, with a device sync,
+ *                     when a frame needs more).  Read-only
+ *                     "region_segment_tiles": segmented tiles of the lists.
  *   "slab"            0/1, col48 + regions: the per-wave LDS slab march
  *                     (default 0); "slab_cap" 0-32 chunks per channel.
  *   "split"           regions schedule, brick4/448/488/zpair/corner8: lanes per ray

@@ -230,67 +230,50 @@ def test_every_layout_bitexact(r, oracle, vol128, layout, name):
 
 
 @pytest.mark.parametrize("layout", [15, 12, 14, 1])
-def test_split_long_tiles_bitexact(r, oracle, vol128, layout):
-    """split_long (round 4): the tiles costing >= split_long % of the longest
-    get their own per-XCD lists, marched in a second launch on the context's
-    side stream with split_long_k lanes per ray, while the rest keep the
-    frame's split K.  1 % puts every tile with work in the long launch, 100 %
-    only the longest; bit-exact with exact step counts (both launches add to
-    one counter), with early-out, a banded target (packed rows), the
-    latency-mode march for the long launch, and GPU-built lists (a moving
-    camera).  Layout 1 (planar) cannot split: the option leaves it on one
-    launch."""
-    r.set_volume(vol128)
+@pytest.mark.parametrize("seg", [4, 16, 48])
+def test_ray_segments_bitexact(r, oracle, vol128, layout, seg):
+    """Ray segments (option segment = L): the tiles
+    estimated at >= 2L steps are marched as segments of L steps whose terms
+    seg_resolve adds in step order -- exact against the oracle, step counts
+    included: the recipe volume (G uniform: the _uG kernel), a rotated cube,
+    bands, short rays (max_steps 7 < L), early-out (the sum stops at the same
+    step), 300 steps (up to 75 segments), lists reused for a larger
+    max_steps (the terms scratch grows), a random volume (every channel
+    loaded) and per-tap MediaScroll offsets.  Layout 1 (planar) has no
+    segmented kernel: the option leaves it on its plain path."""
     r.set_layout_preference(layout)
+    r.set_option("schedule", 5)
+    r.set_option("segment", seg)
+    assert r.get_option("segment") == seg
     try:
-        for split, pct, kl in [(1, 1, 2), (1, 60, 4), (1, 100, 8), (2, 50, 4), (4, 1, 8), (1, 70, 8)]:
-            r.set_option("split", split)
-            r.set_option("split_long", pct)
-            r.set_option("split_long_k", kl)
-            assert r.get_option("split_long") == pct and r.get_option("split_long_k") == kl
-            for (W, H, phi, theta) in [(480, 270, 0.0, 0.0), (203, 117, 35.0, -20.0)]:
-                osd, gsd = vr.reference_shader_data(W / H, phi, theta)
-                img, ref, c, s = render_both(r, oracle, vol128, W, H, osd, gsd)
-                assert_exact(img, ref)
-                assert c == s
-                if layout != 1 and pct < 100:
-                    assert r.get_option("region_long_tiles") > 0
-        r.set_option("split", 0)
-        r.set_option("split_long", 50)
-        osd, gsd = vr.reference_shader_data(16 / 9, -40.0, 15.0)
-        m = vr.march_defaults(early_out=0.5)
-        img, ref, c, s = render_both(r, oracle, vol128, 320, 180, osd, gsd, march=m)
-        assert_exact(img, ref)
-        assert c == s
-        for lat in (0, 3):   # the long launch on the latency-mode march
-            r.set_option("lat", lat)
-            img, ref, c, s = render_both(r, oracle, vol128, 320, 180, osd, gsd, band_rows=16, band_stride=3,
-                                         band_first=1)
+        osd, gsd = vr.reference_shader_data(16 / 9, 25.0, -40.0)
+        for W, H, band, march in [(333, 187, {}, vr.march_defaults()),
+                                  (640, 360, dict(band_rows=16, band_stride=3, band_first=2), vr.march_defaults()),
+                                  (320, 180, {}, vr.march_defaults(max_steps=7)),
+                                  (320, 180, {}, vr.march_defaults(early_out=0.6, density=4.0)),
+                                  (320, 180, {}, vr.march_defaults(max_steps=300)),
+                                  (320, 180, {}, vr.march_defaults(max_steps=128))]:
+            img, ref, c, s = render_both(r, oracle, vol128, W, H, osd, gsd, march=march, **band)
             assert_exact(img, ref)
             assert c == s
-        r.set_option("lat", 0)
-        # a moving camera: GPU-built long / short lists, rebuilt every render
-        r.set_option("region_interval", 1)
-        W, H = 320, 180
-        r.set_march(vr.march_defaults())
-        for i in range(1, 6):
-            osd, gsd = vr.reference_shader_data(W / H, SPIN_DEG * i, 0.0)
-            r.set_shader_data(osd, gsd)
-            cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
-            img = r.alloc_target(W, H, 0)
-            img.fill_(float("nan"))
-            r.render(W, H, 0, out=img, step_counter=cnt)
-        torch.cuda.synchronize()
-        obj, glob = vr.shader_data_arrays(osd, gsd)
-        ref, steps = oracle.render(vol128, obj, glob, oracle.from_params(vr.march_defaults()), W, H, 0)
-        assert_exact(img.cpu().numpy(), ref)
-        assert int(cnt.item()) == steps
+            if layout != 1 and march.max_steps >= 2 * seg:
+                assert r.get_option("region_segment_tiles") > 0
+        assert layout != 1 or r.get_option("region_segment_tiles") == 0
+        rng = np.random.default_rng(seg + layout)
+        vol = rng.integers(0, 256, size=(40, 52, 36, 4), dtype=np.uint8)
+        osd, gsd = vr.reference_shader_data(16 / 9, 30.0, 5.0)
+        img, ref, c, s = render_both(r, oracle, vol, 200, 112, osd, gsd)
+        assert_exact(img, ref)
+        assert c == s
+        gsd.media_scroll[1 * 4 + 1] = 0.01
+        gsd.media_scroll[2 * 4 + 2] = -0.02
+        for m in (vr.march_defaults(), vr.march_defaults(early_out=0.6)):
+            img, ref, c, s = render_both(r, oracle, vol, 160, 90, osd, gsd, march=m)
+            assert_exact(img, ref)
+            assert c == s
     finally:
-        r.set_option("region_interval", 32)
-        r.set_option("lat", 0)
-        r.set_option("split_long", 0)
-        r.set_option("split_long_k", 4)
-        r.set_option("split", 0)
+        r.set_option("segment", 0)
+        r.set_option("schedule", -1)
         r.set_layout_preference(0)
 
 
@@ -1338,15 +1321,18 @@ def test_latency_march_bitexact(r, oracle, vol128, layout, split, lat):
 
 
 @pytest.mark.parametrize("layout", [15, 12, 5, 14])
-def test_auto_split_at_one_eighth_band_share(r, oracle, vol128, layout):
+@pytest.mark.parametrize("seg", [0, 24])
+def test_auto_split_at_one_eighth_band_share(r, oracle, vol128, layout, seg):
     """The multi-GPU config-5 path: auto split (split=0) turns on for a 1/8
     band share of a 1080p frame, with col48 (the auto
     layout past the Infinity Cache since round 3), brick4832 (before it),
-    corner8 and cornerh (the auto layout for cache-resident volumes).  Exact,
+    corner8 and cornerh (the auto layout for cache-resident volumes); and ray
+    segments of 24 steps on that share (sec. 7.1; corner8 has none).  Exact,
     step counts too."""
     r.set_layout_preference(layout)
     r.set_option("schedule", 5)
     r.set_option("split", 0)
+    r.set_option("segment", seg)
     try:
         osd, gsd = vr.reference_shader_data(16 / 9)
         for first in (0, 5):
@@ -1354,7 +1340,10 @@ def test_auto_split_at_one_eighth_band_share(r, oracle, vol128, layout):
                                          band_rows=16, band_stride=8, band_first=first)
             assert_exact(img, ref)
             assert c == s
+            if seg and layout != 5:
+                assert r.get_option("region_segment_tiles") > 0
     finally:
+        r.set_option("segment", 0)
         r.set_option("schedule", -1)
         r.set_layout_preference(0)
 
@@ -1428,9 +1417,9 @@ def test_region_lists_outlive_destroyed_streams(r, oracle, vol128):
     """Region lists rendered on streams the caller destroys afterwards (the
     native loop's own render streams, gone at close()): later rebuilds -- on
     the GPU and on the host, every render -- must not touch those streams.
-    vr_render records each stream's 'lists used' event right after its
-    launch, never later on a remembered stream handle (round 4: recording on
-    a destroyed stream aborted the process inside the HIP runtime)."""
+    Lists retire with an event recorded on the retiring render's own stream
+    when that is the only stream that used them, and with a device sync
+    otherwise: never with an event recorded on a remembered stream handle."""
     import os
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))

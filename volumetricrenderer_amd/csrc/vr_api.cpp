@@ -63,6 +63,7 @@ constexpr int kMaxRegionStreams = 4;
 // 3840 x 2160 x 256); a frame needing more marches its last waves' shadow rays
 // in place
 constexpr int kMaxDeferMiB = 4 << 10;
+constexpr size_t kMaxTermsBytes = (size_t)1 << 30;   // ray segments: the terms scratch (slots x max_steps x 64 floats)
 // retired deferred scratch buffers kept before a device sync frees them
 constexpr size_t kMaxDeferRetired = 4;
 constexpr int kRegionKeyLen = 35;
@@ -136,10 +137,9 @@ struct Ctx {
     int slab = 0;                  // COL48 + regions: the LDS slab march (vr_march_slab.hip)
     int proc_enum = 0;             // procedural sort: 1 = 64x64-region enumeration with shadow rays too
     int slab_cap = kSlabMaxChunks; // its chunks per channel (<= kSlabMaxChunks; smaller forces the fallback)
-    int split_long = 0;            // regions: tiles costing >= this % of the longest get their own launch (0 = off)
-    int split_long_k = 4;          // lanes per ray of that launch (2, 4, 8)
-    hipStream_t side_stream = nullptr;   // split_long: the long tiles' launch (forked from the render stream)
-    hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+    int segment = 0;               // regions: ray segments of L steps for the long tiles (0 = off)
+    float* d_terms = nullptr;      // segments: the per-step terms (SegArgs.terms)
+    size_t terms_bytes = 0;
     int wg_waves = 4;              // regions: waves per workgroup (4, 8, 16)
     int supertile = 2;             // regions: list order by S x S blocks of tiles (1 = per tile; 2 measured 1 % faster)
     int lat = 0;                   // regions: latency-mode march, rounds of loads in flight (0 = off, -1 = auto, 2-4)
@@ -159,23 +159,23 @@ struct Ctx {
         TileMap map{};             // host copy: nwx (and off[] for host builds)
         int most = 0;              // the longest per-XCD list (sizes the launch)
         int nwork = 0;             // tiles with estimated work
-        int longs = 0;             // 1: split_long lists (launched on their own, even when empty)
-        int most_long = 0;         // the longest per-XCD long list
-        int nlong = 0;             // long tiles
-        // the streams that rendered with these lists and, per stream, an event
-        // recorded after each of its renders; the buffer is rewritten only
-        // after those events (kMaxRegionStreams; more -> device sync).  The
-        // events are recorded at render time, never later on a remembered
-        // stream: the caller may have destroyed that stream since.
+        int seg_len = 0;           // segments: steps per segment the lists were built for (0 = none)
+        int nseg_tiles = 0;        // segmented tiles (slots of SegArgs.info)
+        int icap = 0;              // info entries before the list
+        // the streams that rendered with these lists.  When the lists are
+        // retired by a render on their only stream, an event is recorded on
+        // it and the buffer is rewritten only after that event; lists that
+        // another stream used retire with a device sync instead: an event is
+        // never recorded on a remembered stream, which the caller may have
+        // destroyed since (kMaxRegionStreams; more -> device sync too)
         hipStream_t streams[kMaxRegionStreams] = {};
-        hipEvent_t used[kMaxRegionStreams] = {};
+        hipEvent_t used = nullptr;
         int nstreams = 0;          // -1: more streams than tracked
-        int nretired = 0;          // events of the renders before the lists were retired
+        int nretired = 0;          // 1: `used` marks the end of the renders before the lists were retired
         hipEvent_t uploaded = nullptr;   // the list upload (on streams[0]); other streams wait for it
         hipStream_t upload_stream = nullptr;
     } region[2];
     int region_cur = -1;           // buffer of the current lists (-1 = none)
-    int region_slot = -1;          // the render stream's event slot in it (note_region_stream)
     float region_key[kRegionKeyLen] = {};   // geometry the current lists were built for
     long long renders_since_build = 0;
     // procedural cost sort: the geometry whose order d_sort holds (n per pixel
@@ -545,17 +545,14 @@ vr_status vr_destroy(void* p)
     if (c->d_rg) (void)hipFree(c->d_rg);
     if (c->h_rghdr) (void)hipHostFree(c->h_rghdr);
     if (c->rg_ev) (void)hipEventDestroy(c->rg_ev);
-    if (c->side_stream) (void)hipStreamDestroy(c->side_stream);
-    if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
-    if (c->join_ev) (void)hipEventDestroy(c->join_ev);
+    if (c->d_terms) (void)hipFree(c->d_terms);
     if (c->d_mm) (void)hipFree(c->d_mm);
     if (c->h_mm) (void)hipHostFree(c->h_mm);
     if (c->mm_ready) (void)hipEventDestroy(c->mm_ready);
     for (auto& b : c->region) {
         if (b.d) (void)hipFree(b.d);
         if (b.h) (void)hipHostFree(b.h);
-        for (hipEvent_t e : b.used)
-            if (e) (void)hipEventDestroy(e);
+        if (b.used) (void)hipEventDestroy(b.used);
         if (b.uploaded) (void)hipEventDestroy(b.uploaded);
     }
     delete c;
@@ -902,14 +899,10 @@ vr_status vr_set_option(void* p, const char* name, int value)
         c->slab_cap = value;
         return VR_OK;
     }
-    if (n == "split_long_k") {
-        if (value != 2 && value != 4 && value != 8) return fail(VR_ERR_INVALID, "vr_set_option: split_long_k is 2, 4 or 8");
-        c->split_long_k = value;
-        return VR_OK;
-    }
-    if (n == "split_long") {
-        if (value < 0 || value > 100) return fail(VR_ERR_INVALID, "vr_set_option: split_long in [0, 100] (percent)");
-        c->split_long = value;
+    if (n == "segment") {
+        if (value != 0 && (value < 4 || value > 4096))
+            return fail(VR_ERR_INVALID, "vr_set_option: segment is 0 (off) or 4-4096 steps");
+        c->segment = value;
         return VR_OK;
     }
     if (n == "wg_waves") {
@@ -986,9 +979,8 @@ int vr_get_option(void* p, const char* name)
     if (n == "shadow_defer_kib")                          // read-only: the scratch held now, KiB
         return (int)std::min<size_t>((c->defer_bytes + 1023) / 1024, 0x7fffffff);
     if (n == "slab_cap") return c->slab_cap;
-    if (n == "split_long") return c->split_long;
-    if (n == "split_long_k") return c->split_long_k;
-    if (n == "region_long_tiles") return c->region_cur >= 0 ? c->region[c->region_cur].nlong : 0;
+    if (n == "segment") return c->segment;
+    if (n == "region_segment_tiles") return c->region_cur >= 0 ? c->region[c->region_cur].nseg_tiles : 0;
     if (n == "sort_reuse") return c->sort_reuse;
     if (n == "wg_waves") return c->wg_waves;
     if (n == "uniform_skip") return c->uniform_skip;
@@ -1026,7 +1018,7 @@ const char* vr_kernel_variant(void* p)
         return pl.early ? "grid_col48_slab_clamp_early" : "grid_col48_slab_clamp";
     const int um = c->uniform_skip ? c->uniform_mask : 0;
     int ch = -1;   // one uniform channel, no loads for it (launch_lw / launch_lat_kd): "_u" + the channel
-    if (kind == SCHED_REGIONS && !pl.early && a.zero_offsets && c->wg_waves == 4 && c->split_long == 0 &&
+    if (kind == SCHED_REGIONS && !pl.early && a.zero_offsets && c->wg_waves == 4 &&
         (um == 1 || um == 2 || um == 4 || um == 8) &&
         (pl.layout == LAYOUT_COL48 || pl.layout == LAYOUT_BRICK4832 || pl.layout == LAYOUT_CORNERH ||
          pl.layout == LAYOUT_COL48Z))
@@ -1097,8 +1089,9 @@ void box_centre_pixel(const Ctx* c, const MarchArgs& a, int* px, int* prow)
 // is in exactly one list whatever the estimate, so a list built for an older
 // camera stays correct: a moving camera reuses it for kRegionRebuildInterval
 // renders.  Rebuilds go to the other of two buffers, once the renders that
-// last read it are done (per stream, an event recorded after each render; not
-// a device sync), uploaded on the render stream.
+// last read it are done (an event recorded when it was retired, on its one
+// render stream; a device sync if several streams used it), uploaded on the
+// render stream.
 //
 // `s` waits for `ev` unless it has already completed (an event recorded on a
 // stream the caller has destroyed since is complete: no wait is queued for it)
@@ -1112,28 +1105,18 @@ static vr_status stream_wait_pending(hipStream_t s, hipEvent_t ev)
     return VR_OK;
 }
 
-// The render stream s uses the lists: *slot = the stream's event slot (-1:
-// untracked, more streams than kMaxRegionStreams), recorded after the launch
-vr_status note_region_stream(Ctx::RegionBuf& rb, hipStream_t s, int* slot)
+// The render stream s uses the lists
+vr_status note_region_stream(Ctx::RegionBuf& rb, hipStream_t s)
 {
-    *slot = -1;
     if (rb.nstreams < 0) return VR_OK;
     for (int i = 0; i < rb.nstreams; ++i)
-        if (rb.streams[i] == s) {
-            *slot = i;
-            return VR_OK;
-        }
+        if (rb.streams[i] == s) return VR_OK;
     if (s != rb.upload_stream) {   // first use on another stream
         const vr_status st = stream_wait_pending(s, rb.uploaded);
         if (st != VR_OK) return st;
     }
-    if (rb.nstreams == kMaxRegionStreams) {
-        rb.nstreams = -1;
-        return VR_OK;
-    }
-    if (!rb.used[rb.nstreams]) HIP_TRY(hipEventCreateWithFlags(&rb.used[rb.nstreams], hipEventDisableTiming));
-    *slot = rb.nstreams;
-    rb.streams[rb.nstreams++] = s;
+    if (rb.nstreams == kMaxRegionStreams) rb.nstreams = -1;
+    else rb.streams[rb.nstreams++] = s;
     return VR_OK;
 }
 
@@ -1160,8 +1143,6 @@ static void poll_region_header(Ctx* c)
     Ctx::RegionBuf& rb = c->region[c->rg_buf];
     rb.nwork = c->h_rghdr[9];
     rb.most = c->h_rghdr[10];
-    rb.most_long = c->h_rghdr[12];
-    rb.nlong = c->h_rghdr[13];
 }
 
 // Retire the current lists (events on the streams that rendered with them) and
@@ -1173,8 +1154,13 @@ static vr_status next_region_buf(Ctx* c, size_t n, bool host_staging, hipStream_
     if (c->region_cur >= 0) {   // retire the current lists in the stream order of their renders
         Ctx::RegionBuf& old = c->region[c->region_cur];
         old.nretired = 0;
-        if (old.nstreams < 0) HIP_TRY(hipDeviceSynchronize());
-        else old.nretired = old.nstreams;   // their events were recorded after each render
+        if (old.nstreams == 1 && old.streams[0] == stream) {   // the usual case: one stream, this one
+            if (!old.used) HIP_TRY(hipEventCreateWithFlags(&old.used, hipEventDisableTiming));
+            HIP_TRY(hipEventRecord(old.used, stream));
+            old.nretired = 1;
+        } else if (old.nstreams != 0) {
+            HIP_TRY(hipDeviceSynchronize());
+        }
         old.nstreams = 0;
     }
     const int b = c->region_cur < 0 ? 0 : c->region_cur ^ 1;
@@ -1183,11 +1169,11 @@ static vr_status next_region_buf(Ctx* c, size_t n, bool host_staging, hipStream_
         HIP_TRY(hipEventSynchronize(c->rg_ev));
         poll_region_header(c);
     }
-    for (int i = 0; i < rb.nretired; ++i) {   // its last renders
+    if (rb.nretired) {   // its last renders
         if (host_staging || rb.d == nullptr) {
-            HIP_TRY(hipEventSynchronize(rb.used[i]));
+            HIP_TRY(hipEventSynchronize(rb.used));
         } else {
-            const vr_status st = stream_wait_pending(stream, rb.used[i]);
+            const vr_status st = stream_wait_pending(stream, rb.used);
             if (st != VR_OK) return st;
         }
     }
@@ -1208,12 +1194,12 @@ static vr_status next_region_buf(Ctx* c, size_t n, bool host_staging, hipStream_
     return VR_OK;
 }
 
-vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow, int long_pct, hipStream_t stream)
+vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow, int seg_len, hipStream_t stream)
 {
     const int tw = (a.width + 7) >> 3, th = (a.out_rows + 7) >> 3;
     float key[kRegionKeyLen] = {(float)tw, (float)th, (float)a.width, (float)a.height, (float)a.out_rows,
                                 (float)a.band_rows, (float)a.band_stride, (float)a.band_first, (float)tpw,
-                                (float)c->wedges, (float)long_pct, (float)c->split, (float)c->supertile};
+                                (float)c->wedges, (float)seg_len, (float)c->split, (float)c->supertile};
     constexpr int grid_part = 13;   // the part a reused list must match
     int kn = grid_part;
     for (float v : {(float)a.max_steps, a.step_size, (float)cpx, (float)cprow}) key[kn++] = v;
@@ -1223,17 +1209,17 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     poll_region_header(c);
     const bool same_grid = c->region_cur >= 0 && std::memcmp(key, c->region_key, grid_part * sizeof(float)) == 0;
     if (same_grid && (std::memcmp(key, c->region_key, sizeof key) == 0 || c->renders_since_build < c->region_interval))
-        return note_region_stream(c->region[c->region_cur], stream, &c->region_slot);
+        return note_region_stream(c->region[c->region_cur], stream);
 
     const int S = c->supertile;
-    // a moved camera over the same target: the lists come from the GPU build
-    // on the render stream (vr_regions.hip) -- no host loop, no host wait;
-    // tiles with work and the longest lists are the last completed build's
-    // (they size the launches, not the result)
-    if (same_grid && c->region_gpu && th < 65536 && tw < 65536) {
+    // a moved camera over the same target (no segments): the lists come from
+    // the GPU build on the render stream (vr_regions.hip) -- no host loop, no
+    // host wait; tiles with work and the longest list are the last completed
+    // build's (they size the launch, not the result)
+    if (same_grid && c->region_gpu && seg_len == 0 && th < 65536 && tw < 65536) {
         const size_t n = (size_t)tw * th;
         const Ctx::RegionBuf& cur = c->region[c->region_cur];
-        const int nwork = cur.nwork, most = cur.most, most_long = cur.most_long, nlong = cur.nlong;
+        const int nwork = cur.nwork, most = cur.most;
         const size_t need = region_build_bytes((int)n);
         if (need > c->rg_bytes) {
             if (c->d_rg) {
@@ -1264,7 +1250,7 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
         }
         g.ccx = (cpx + 0.5) / 8.0; g.ccy = (cprow + 0.5) / 8.0;
         g.ctx = (cpx >> 3) / S; g.cty = (cprow >> 3) / S;
-        g.supertile = S; g.wedges = c->wedges; g.long_pct = long_pct;
+        g.supertile = S; g.wedges = c->wedges;
         int* dev_hdr = nullptr;
         HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&dev_hdr), c->h_rghdr, 0));
         // one build scratch per context: a build on another stream waits for the last one
@@ -1284,11 +1270,11 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
         rb.most = most;
         rb.map = TileMap{};
         rb.map.nwx = std::max(1, (most + tpw - 1) / tpw);
-        rb.longs = long_pct > 0 ? 1 : 0;
-        rb.most_long = most_long;
-        rb.nlong = nlong;
+        rb.seg_len = 0;
+        rb.nseg_tiles = 0;
+        rb.icap = 0;
         rb.nstreams = 0;
-        const vr_status st = note_region_stream(rb, stream, &c->region_slot);
+        const vr_status st = note_region_stream(rb, stream);
         if (st != VR_OK) return st;
         c->region_cur = b;
         std::memcpy(c->region_key, key, sizeof key);
@@ -1353,35 +1339,56 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     std::sort(idle.begin(), idle.end(), inside_out);
     for (size_t i = 0; i < idle.size(); ++i) xl[i % 8].push_back(idle[i]);
 
-    // split_long: the tiles costing >= long_pct % of the longest form their own
-    // per-XCD lists (first in the buffer, same inside-out order), launched
-    // separately with split_long_k lanes per ray (vr_render)
-    double most_cost = 0.0;
-    for (const T& t : work) most_cost = std::max(most_cost, t.cost);
-    const double split_at = std::max(1.0, most_cost * long_pct / 100.0);
-    const size_t n = (size_t)tw * th;
+    // segments (option "segment", L steps): a tile with work estimated at
+    // >= 2L steps is marched as round(cost / L) segments (at most 127; as many
+    // tiles as kMaxTermsBytes of terms hold at this max_steps), segment-major
+    // (the first segments of an XCD's long tiles, then the second, ...) ahead
+    // of its whole tiles; the info of XCD x's segmented tiles is contiguous
+    const int L = seg_len;
+    const size_t slot_bytes = (size_t)std::max(a.max_steps, 1) * 64 * sizeof(float);
+    const int slot_cap = L > 0 ? (int)std::min<size_t>(kMaxTermsBytes / slot_bytes, (size_t)1 << 24) : 0;
+    struct SegT { unsigned id; int nseg; };
+    std::vector<std::vector<SegT>> segx(8);
+    std::vector<std::vector<unsigned>> wholex(8);
+    int nslots = 0;
+    size_t nent = 0;
+    for (int x = 0; x < 8; ++x)
+        for (const T& t : xl[x]) {
+            const int ns = L > 0 && t.cost >= 2.0 * L ? (int)std::min(127.0, std::floor(t.cost / L + 0.5)) : 1;
+            if (ns >= 2 && nslots < slot_cap) {
+                segx[x].push_back({t.id, ns});
+                ++nslots;
+                nent += (size_t)ns;
+            } else {
+                wholex[x].push_back(t.id);
+                ++nent;
+            }
+        }
+    const size_t n = 2 * (size_t)nslots + nent;   // words after the header
     int b = 0;
     const vr_status st0 = next_region_buf(c, n, true, stream, &b);
     if (st0 != VR_OK) return st0;
     Ctx::RegionBuf& rb = c->region[b];
     int* hdr = reinterpret_cast<int*>(rb.h);
     std::memset(hdr, 0, kRegionHeader * sizeof(int));
-    unsigned* list = rb.h + kRegionHeader;
-    size_t pos = 0, most_long = 0, most = 0;
-    for (int x = 0; x < 8; ++x) {   // the long lists
-        hdr[kRegionLongHdr + x] = (int)pos;
-        if (long_pct > 0)
-            for (const T& t : xl[x])
-                if (t.cost >= split_at) list[pos++] = t.id;
-        most_long = std::max(most_long, pos - (size_t)hdr[kRegionLongHdr + x]);
-    }
-    hdr[kRegionLongHdr + 8] = (int)pos;
-    const size_t nlong = pos;
+    unsigned* info = rb.h + kRegionHeader;
+    unsigned* list = info + 2 * (size_t)nslots;
     TileMap m{};
-    for (int x = 0; x < 8; ++x) {   // the rest
+    size_t pos = 0, most = 0;
+    int slot = 0;
+    for (int x = 0; x < 8; ++x) {
         m.off[x] = (int)pos;
-        for (const T& t : xl[x])
-            if (long_pct == 0 || t.cost < split_at) list[pos++] = t.id;
+        int maxns = 0;
+        for (const SegT& q : segx[x]) maxns = std::max(maxns, q.nseg);
+        for (int sg = 0; sg < maxns; ++sg)
+            for (size_t j = 0; j < segx[x].size(); ++j)
+                if (sg < segx[x][j].nseg) list[pos++] = 0x80000000u | ((unsigned)sg << 24) | (unsigned)(slot + (int)j);
+        for (const SegT& q : segx[x]) {
+            info[2 * slot] = q.id;
+            info[2 * slot + 1] = (unsigned)q.nseg;
+            ++slot;
+        }
+        for (unsigned id : wholex[x]) list[pos++] = id;
         most = std::max(most, pos - (size_t)m.off[x]);
     }
     m.off[8] = (int)pos;
@@ -1390,8 +1397,7 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     hdr[9] = (int)work.size();
     hdr[10] = (int)most;
     hdr[11] = (int)pos;
-    hdr[12] = (int)most_long;
-    hdr[13] = (int)nlong;
+    hdr[kRegionSegTiles] = nslots;
     HIP_TRY(hipMemcpyAsync(rb.d, rb.h, (n + kRegionHeader) * sizeof(unsigned), hipMemcpyHostToDevice, stream));
     if (!rb.uploaded) HIP_TRY(hipEventCreateWithFlags(&rb.uploaded, hipEventDisableTiming));
     HIP_TRY(hipEventRecord(rb.uploaded, stream));
@@ -1399,11 +1405,11 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     rb.map = m;
     rb.most = (int)most;
     rb.nwork = (int)work.size();
-    rb.longs = long_pct > 0 ? 1 : 0;
-    rb.most_long = (int)most_long;
-    rb.nlong = (int)nlong;
+    rb.seg_len = L;
+    rb.nseg_tiles = nslots;
+    rb.icap = nslots;
     rb.nstreams = 0;
-    const vr_status st = note_region_stream(rb, stream, &c->region_slot);
+    const vr_status st = note_region_stream(rb, stream);
     if (st != VR_OK) return st;
     c->region_cur = b;
     std::memcpy(c->region_key, key, sizeof key);
@@ -1775,45 +1781,56 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
     const int kind = c->schedule >= 0 ? c->schedule : SCHED_REGIONS;
     const int tpw = c->tiles_per_wave > 0 ? c->tiles_per_wave : (kind == SCHED_RINGS || kind == SCHED_REGIONS ? 2 : 1);
     Schedule sc{kind, 0, 0, tpw, c->waves_per_simd, c->d_heads, nullptr, {}, 1, 0, c->wg_waves, 0, nullptr};
-    Schedule lsc = sc;   // split_long: the long tiles' launch
-    bool two = false;
     sc.slab = pl.layout == LAYOUT_COL48 && c->slab;
     a.slab_cap = c->slab_cap;
     if (kind == SCHED_RINGS || kind == SCHED_REGIONS) box_centre_pixel(c, a, &sc.center_x, &sc.center_y);
     if (kind == SCHED_REGIONS) {
         const bool splittable = is_b4_family(pl.layout) || pl.layout == LAYOUT_ZPAIR || pl.layout == LAYOUT_CORNER8 ||
                                 pl.layout == LAYOUT_CORNERH || pl.layout == LAYOUT_COL48Z;
-        // split_long: the long tiles in their own lists and launch (below)
-        const int long_pct = splittable && !sc.slab && c->split_long > 0 ? c->split_long : 0;
-        const vr_status st = build_regions(c, a, tpw, sc.center_x, sc.center_y, long_pct,
+        // ray segments for the long tiles (march_regions_seg instances)
+        const bool segable = !sc.slab && (pl.layout == LAYOUT_COL48 || pl.layout == LAYOUT_BRICK4832 ||
+                                          pl.layout == LAYOUT_CORNERH);
+        const int seg_len = segable ? c->segment : 0;
+        const vr_status st = build_regions(c, a, tpw, sc.center_x, sc.center_y, seg_len,
                                            static_cast<hipStream_t>(stream));
         if (st != VR_OK) return st;
         const Ctx::RegionBuf& rb = c->region[c->region_cur];
-        sc.tiles = rb.d + kRegionHeader;
+        sc.tiles = rb.d + kRegionHeader + 2 * (size_t)rb.icap;
         sc.hdr = reinterpret_cast<const int*>(rb.d);
         sc.map = rb.map;
-        const bool lat_ok = c->lat > 0 && lat_supported(pl.layout) && !sc.slab;
-        if (rb.longs) {
-            // the long tiles: split_long_k lanes per ray, launched whatever the
-            // last known count (a GPU-built list may hold long tiles the host
-            // has not seen yet; the kernels stride over whatever the header says)
-            lsc = sc;
-            lsc.hdr = sc.hdr + kRegionLongHdr;
-            lsc.split = c->split_long_k;
-            lsc.lat = lat_ok ? c->lat : 0;
-            lsc.map.nwx = std::max(1, (rb.most_long * lsc.split + tpw - 1) / tpw);
-            two = true;
-        }
-        // step-split rays: K lanes per ray when the frame
-        // share is too small to fill the GPU with one-lane-per-ray waves
-        if (lat_ok && !two) {
-            // latency-mode march (vr_march_lat.hip): K lanes per ray, c->lat rounds of loads in flight
+        if (rb.seg_len > 0) {
+            // segmented lists (one lane per ray): the terms scratch must hold
+            // every segmented tile's rays at this frame's max_steps
+            const size_t need = (size_t)rb.nseg_tiles * (size_t)std::max(a.max_steps, 1) * 64 * sizeof(float);
+            if (need > c->terms_bytes) {
+                if (c->d_terms) {
+                    HIP_TRY(hipDeviceSynchronize());   // growth only: queued frames may use the old scratch
+                    (void)hipFree(c->d_terms);
+                }
+                c->d_terms = nullptr;
+                c->terms_bytes = 0;
+                const size_t want = std::max(need, std::min(need + need / 4, kMaxTermsBytes));
+                if (hipMalloc(&c->d_terms, want) != hipSuccess) {
+                    (void)hipGetLastError();
+                    return fail(VR_ERR_OOM, "vr_render: segment terms (%zu bytes)", want);
+                }
+                c->terms_bytes = want;
+            }
+            sc.seg.terms = c->d_terms;
+            sc.seg.info = reinterpret_cast<const uint2*>(rb.d + kRegionHeader);
+            sc.seg.len = rb.seg_len;
+            sc.seg_tiles = rb.nseg_tiles;
+        } else if (c->lat > 0 && lat_supported(pl.layout) && !sc.slab) {
+            // step-split rays on the latency-mode march
+            // (vr_march_lat.hip): K lanes per ray, c->lat rounds of loads in flight
             const int K = c->split > 0 ? c->split : auto_split(c, rb.nwork);
             const int most = rb.most;
             sc.lat = c->lat;
             sc.split = K;
             sc.map.nwx = std::max(1, (most * K + tpw - 1) / tpw);
         } else if (splittable) {
+            // step-split rays: K lanes per ray when the frame
+            // share is too small to fill the GPU with one-lane-per-ray waves
             int K = c->split;
             if (sc.slab) K = K == 0 ? 1 : K;   // the slab march has one lane per ray; split > 1 uses the plain march
             if (K == 0) K = auto_split(c, rb.nwork);
@@ -1825,30 +1842,7 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
             }
         }
     }
-    if (two) {
-        // long tiles on the context's side stream, forked from and joined back
-        // into the render stream (capturable into a hipGraph); launched first
-        // so that their waves start first
-        const hipStream_t s = static_cast<hipStream_t>(stream);
-        if (!c->side_stream) {
-            int lo = 0, hi = 0;
-            HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-            HIP_TRY(hipStreamCreateWithPriority(&c->side_stream, hipStreamNonBlocking, hi));
-            HIP_TRY(hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
-            HIP_TRY(hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming));
-        }
-        HIP_TRY(hipEventRecord(c->fork_ev, s));
-        HIP_TRY(hipStreamWaitEvent(c->side_stream, c->fork_ev, 0));
-        HIP_TRY(launch_march(a, pl.layout, pl.wrap, pl.early, lsc, c->side_stream));
-        HIP_TRY(launch_march(a, pl.layout, pl.wrap, pl.early, sc, s));
-        HIP_TRY(hipEventRecord(c->join_ev, c->side_stream));
-        HIP_TRY(hipStreamWaitEvent(s, c->join_ev, 0));
-        if (c->region_slot >= 0) HIP_TRY(hipEventRecord(c->region[c->region_cur].used[c->region_slot], s));
-        return VR_OK;
-    }
     HIP_TRY(launch_march(a, pl.layout, pl.wrap, pl.early, sc, static_cast<hipStream_t>(stream)));
-    if (kind == SCHED_REGIONS && c->region_slot >= 0)   // the lists' last use on this stream
-        HIP_TRY(hipEventRecord(c->region[c->region_cur].used[c->region_slot], static_cast<hipStream_t>(stream)));
     return VR_OK;
 }
 

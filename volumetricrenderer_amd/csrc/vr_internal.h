@@ -224,19 +224,21 @@ struct TileMap {
     int nwx;
 };
 // The regions schedule's lists in device memory: a header of kRegionHeader
-// ints, then the entries.  Two sets of per-XCD lists: the long tiles (option
-// split_long: estimated cost >= that % of the frame's longest; marched with
-// split_long_k lanes per ray in their own launch) and the rest.  The header:
-//   [0..8]   off[]: XCD x renders the (short) entries [off[x], off[x+1])
-//   [9]      tiles with estimated work    [10] the longest short list
-//   [11]     entries                       [12] the longest long list
-//   [13]     long tiles
-//   [16..24] the long lists' off[] (empty without split_long)
-// Long lists come first in the entries.  Built on the host (vr_api.cpp
-// build_regions) or, for a moving camera, on the GPU (vr_regions.hip
-// launch_region_build, the same dealing).
-constexpr int kRegionHeader = 32;
-constexpr int kRegionLongHdr = 16;   // the long lists' off[] in the header
+// ints, the segmented tiles' info (SegArgs.info, `icap` uint2 entries; option
+// "segment"), then the list entries.  The header:
+//   [0..8]   off[]: XCD x renders the entries [off[x], off[x+1])
+//   [9]      tiles with estimated work    [10] the longest list
+//   [11]     entries                       [12] segmented tiles (kRegionSegTiles)
+// Built on the host (vr_api.cpp build_regions) or, for a moving camera, on
+// the GPU (vr_regions.hip launch_region_build, the same dealing; no segments).
+constexpr int kRegionHeader = 16;
+constexpr int kRegionSegTiles = 12;
+// Ray segments (vr_march_kernels.h march_regions_seg / seg_resolve)
+struct SegArgs {
+    float* terms;          // [slot][max_steps][64]: each ray's per-step terms
+    const uint2* info;     // [slot]: {tile (ty << 16 | tx), segments}
+    int len;               // L, steps per segment (0 = no segments)
+};
 struct RegionBuild {
     int tw, th, width, out_rows, band_rows, band_stride, band_first, max_steps;
     float step_size;
@@ -244,7 +246,6 @@ struct RegionBuild {
     double ccx, ccy;       // box-centre tile (fractional), S x S block of it
     int ctx, cty;
     int supertile, wedges;
-    int long_pct;          // split_long: tiles costing >= this % of the longest are long (0 = none)
 };
 size_t region_build_bytes(int ntiles);
 // h_hdr (optional, host-mapped): a copy of the header, for sizing later launches
@@ -264,6 +265,8 @@ struct Schedule {
     int wg_waves;          // regions (one lane per ray): waves per workgroup, 4 (default), 8 or 16
     int lat;               // regions: latency-mode march (vr_march_lat.hip), rounds of loads in flight (0 = off)
     const int* hdr;        // regions: the lists' device header (kRegionHeader; off[x] per XCD)
+    SegArgs seg = {};      // regions: ray segments of the long tiles (seg.len 0 = none)
+    int seg_tiles = 0;     // regions: segmented tiles (the resolve pass's waves)
 };
 
 // Cost-sort scratch of the procedural march (vr_march.hip launch_march_procedural),

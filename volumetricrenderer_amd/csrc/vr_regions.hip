@@ -16,13 +16,12 @@
 //   2. rg_wedges: one workgroup scans the bins' work and cuts it into
 //      8 x wedges equal quantiles; wedge k goes to XCD k % 8 (as the host
 //      cuts tiles sorted by angle);
-//   3. rg_keys: the sort key of a tile -- short flag (option split_long:
-//      the long tiles' lists come first), XCD, idle flag (tiles without
+//   3. rg_keys: the sort key of a tile -- XCD, idle flag (tiles without
 //      estimated work go after the XCD's work, dealt round-robin), ring, angle
 //      bin, place in block -- and the per-XCD counts;
 //   4. hipcub::DeviceRadixSort::SortPairs: keys -> the concatenated lists;
-//   5. rg_header: the per-XCD offsets (long lists, then the rest), tiles with
-//      work, the longest lists, into the list buffer's header (and host-mapped memory, which the host
+//   5. rg_header: the per-XCD offsets, tiles with work and the longest list,
+//      into the list buffer's header (and host-mapped memory, which the host
 //      reads later to size the next launches -- no host wait).
 // The lists only order work: every tile is in exactly one list whatever the
 // estimate, so a frame is exact with any lists (tests/test_gpu_parity.py).
@@ -44,12 +43,9 @@ struct RgScratch {
     unsigned* keys_in;
     unsigned* keys_out;
     unsigned* vals_in;
-    float* cost;                    // [n] per tile
     unsigned long long* bin_cost;   // [kAngleBins], zeroed by rg_wedges after use
     unsigned char* bin_xcd;         // [kAngleBins]
-    // [0..7] short tiles per XCD, [8] tiles with work, [9] the longest tile's
-    // cost (fixed point), [16..23] long tiles per XCD; zeroed by rg_header after use
-    unsigned* counts;
+    unsigned* counts;               // [8] per XCD, [8] tiles with work; zeroed by rg_header after use
     void* sort_tmp;
     size_t sort_bytes;
 };
@@ -91,11 +87,9 @@ __global__ __launch_bounds__(256) void rg_tiles(const RegionBuild b, RgScratch s
     const int ring = min(max(abs(sx - b.ctx), abs(sy - b.cty)), 2047);
     const int sub = (ty % S) * S + tx % S;
     const bool work = cost >= 1.0;
-    s.cost[i] = (float)cost;
     if (work) {
         atomicAdd(&s.bin_cost[abin], (unsigned long long)(cost * kCostScale));
         atomicAdd(&s.counts[8], 1u);
-        atomicMax(&s.counts[9], (unsigned)fmin(cost * kCostScale, 4294967295.0));
     }
     s.keys_in[i] = (work ? 0u : 1u) << 27 | (unsigned)ring << 16 | (unsigned)abin << 4 | (unsigned)sub;
     s.vals_in[i] = ((unsigned)ty << 16) | (unsigned)tx;
@@ -131,7 +125,7 @@ __global__ __launch_bounds__(kWedgeThreads) void rg_wedges(const RegionBuild b, 
     }
 }
 
-// 3. the sort key: short | XCD | idle | ring | angle bin | place in block
+// 3. the sort key: XCD | idle | ring | angle bin | place in block
 __global__ __launch_bounds__(256) void rg_keys(const RegionBuild b, RgScratch s)
 {
     const int i = (int)(blockIdx.x * 256 + threadIdx.x);
@@ -139,40 +133,27 @@ __global__ __launch_bounds__(256) void rg_keys(const RegionBuild b, RgScratch s)
     const unsigned k = s.keys_in[i];
     const bool idle = (k >> 27) & 1u;
     const unsigned xcd = idle ? (unsigned)(i % 8) : (unsigned)s.bin_xcd[(k >> 4) & (kAngleBins - 1)];
-    // long: cost >= long_pct % of the longest (as the host build, on the float cost)
-    const double most = (double)s.counts[9] / kCostScale;
-    const bool lng = b.long_pct > 0 && !idle && (double)s.cost[i] >= fmax(1.0, most * b.long_pct / 100.0);
-    s.keys_in[i] = (lng ? 0u : 1u) << 31 | xcd << 28 | k;
-    atomicAdd(&s.counts[lng ? 16 + xcd : xcd], 1u);
+    s.keys_in[i] = xcd << 28 | k;
+    atomicAdd(&s.counts[xcd], 1u);
 }
 
-// 5. header (vr_internal.h kRegionHeader): the long lists' offsets, then the
-// short lists', tiles with work, the longest lists; counters zeroed
+// 5. header: off[0..8], tiles with work, longest list; counters zeroed
 __global__ __launch_bounds__(64) void rg_header(RgScratch s, int* hdr, int* hdr_host, int n)
 {
     if (threadIdx.x != 0) return;
-    int pos = 0, most_long = 0, most = 0;
-    for (int x = 0; x < 8; ++x) {
-        hdr[kRegionLongHdr + x] = pos;
-        const int cnt = (int)s.counts[16 + x];
-        most_long = max(most_long, cnt);
-        pos += cnt;
-    }
-    hdr[kRegionLongHdr + 8] = pos;
-    const int nlong = pos;
+    int pos = 0, most = 0;
     for (int x = 0; x < 8; ++x) {
         hdr[x] = pos;
         const int cnt = (int)s.counts[x];
         most = max(most, cnt);
         pos += cnt;
+        s.counts[x] = 0u;
     }
     hdr[8] = pos;   // == n
     hdr[9] = (int)s.counts[8];
     hdr[10] = most;
     hdr[11] = n;
-    hdr[12] = most_long;
-    hdr[13] = nlong;
-    for (int j = 0; j < 32; ++j) s.counts[j] = 0u;
+    s.counts[8] = 0u;
     if (hdr_host)
         for (int j = 0; j < kRegionHeader; ++j) hdr_host[j] = hdr[j];
 }
@@ -186,9 +167,7 @@ RgScratch carve(void* scratch, int n, size_t sort_bytes)
     s.bin_cost = reinterpret_cast<unsigned long long*>(p + o);
     o = up(o + kAngleBins * sizeof(unsigned long long));
     s.counts = reinterpret_cast<unsigned*>(p + o);
-    o = up(o + 32 * sizeof(unsigned));
-    s.cost = reinterpret_cast<float*>(p + o);
-    o = up(o + (size_t)n * 4);
+    o = up(o + 16 * sizeof(unsigned));
     s.bin_xcd = reinterpret_cast<unsigned char*>(p + o);
     o = up(o + kAngleBins);
     s.keys_in = reinterpret_cast<unsigned*>(p + o);
@@ -206,7 +185,7 @@ size_t sort_temp_bytes(int n)
 {
     size_t bytes = 0;
     (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const unsigned*)nullptr, (unsigned*)nullptr,
-                                             (const unsigned*)nullptr, (unsigned*)nullptr, n, 0, 32, nullptr);
+                                             (const unsigned*)nullptr, (unsigned*)nullptr, n, 0, 31, nullptr);
     return bytes;
 }
 
@@ -217,8 +196,7 @@ size_t sort_temp_bytes(int n)
 // build leaves them zero for the next.
 size_t region_build_bytes(int n)
 {
-    return 256 + (size_t)kAngleBins * 8 + 256 + 32 * 4 + 256 + kAngleBins + 256 + 4 * ((size_t)n * 4 + 256) +
-           sort_temp_bytes(n) + 256;
+    return 256 + (size_t)kAngleBins * 8 + 256 + kAngleBins + 256 + 3 * ((size_t)n * 4 + 256) + sort_temp_bytes(n) + 256;
 }
 
 hipError_t launch_region_build(const RegionBuild& b, void* scratch, unsigned* d_list, int* d_hdr, int* h_hdr,
@@ -235,7 +213,7 @@ hipError_t launch_region_build(const RegionBuild& b, void* scratch, unsigned* d_
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     size_t bytes = s.sort_bytes;
-    e = hipcub::DeviceRadixSort::SortPairs(s.sort_tmp, bytes, s.keys_in, s.keys_out, s.vals_in, d_list, n, 0, 32, st);
+    e = hipcub::DeviceRadixSort::SortPairs(s.sort_tmp, bytes, s.keys_in, s.keys_out, s.vals_in, d_list, n, 0, 31, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(rg_header, dim3(1), dim3(64), 0, st, s, d_hdr, h_hdr, n);
     return hipGetLastError();
