@@ -245,20 +245,26 @@ def test_ray_segments_bitexact(r, oracle, vol128, layout, seg):
     r.set_option("schedule", 5)
     r.set_option("segment", seg)
     assert r.get_option("segment") == seg
+    r.set_option("region_interval", 1)   # new lists for every new frame geometry
     try:
         osd, gsd = vr.reference_shader_data(16 / 9, 25.0, -40.0)
         for W, H, band, march in [(333, 187, {}, vr.march_defaults()),
                                   (640, 360, dict(band_rows=16, band_stride=3, band_first=2), vr.march_defaults()),
                                   (320, 180, {}, vr.march_defaults(max_steps=7)),
                                   (320, 180, {}, vr.march_defaults(early_out=0.6, density=4.0)),
-                                  (320, 180, {}, vr.march_defaults(max_steps=300)),
-                                  (320, 180, {}, vr.march_defaults(max_steps=128))]:
+                                  (320, 180, {}, vr.march_defaults(max_steps=300))]:
             img, ref, c, s = render_both(r, oracle, vol128, W, H, osd, gsd, march=march, **band)
             assert_exact(img, ref)
             assert c == s
             if layout != 1 and march.max_steps >= 2 * seg:
                 assert r.get_option("region_segment_tiles") > 0
         assert layout != 1 or r.get_option("region_segment_tiles") == 0
+        # lists built at 64 steps, reused (interval 32) at 300: the terms scratch grows
+        r.set_option("region_interval", 32)
+        for ms in (64, 300):
+            img, ref, c, s = render_both(r, oracle, vol128, 300, 200, osd, gsd, march=vr.march_defaults(max_steps=ms))
+            assert_exact(img, ref)
+            assert c == s
         rng = np.random.default_rng(seg + layout)
         vol = rng.integers(0, 256, size=(40, 52, 36, 4), dtype=np.uint8)
         osd, gsd = vr.reference_shader_data(16 / 9, 30.0, 5.0)
@@ -272,6 +278,7 @@ def test_ray_segments_bitexact(r, oracle, vol128, layout, seg):
             assert_exact(img, ref)
             assert c == s
     finally:
+        r.set_option("region_interval", 32)
         r.set_option("segment", 0)
         r.set_option("schedule", -1)
         r.set_layout_preference(0)
