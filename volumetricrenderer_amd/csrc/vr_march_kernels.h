@@ -1073,8 +1073,9 @@ __global__ __launch_bounds__(kThreads) void march_regions_seg(const MarchArgs a,
 }
 
 // The segmented tiles' rays: each lane adds its ray's stored terms in step
-// order (8 loads in flight), with march_pixel's early-out and step count,
-// then the epilogue (:76-80) and the store.  One wave per tile.
+// order (kSegBatch loads in flight), with march_pixel's early-out and step
+// count, then the epilogue (:76-80) and the store.  One wave per tile.
+constexpr int kSegBatch = 32;
 template <int LAYOUT, bool EARLY>
 __global__ __launch_bounds__(256) void seg_resolve(const MarchArgs a, const int* __restrict__ hdr, SegArgs sg)
 {
@@ -1088,12 +1089,16 @@ __global__ __launch_bounds__(256) void seg_resolve(const MarchArgs a, const int*
     float acc = 0.0f;
     int i = 0;
     bool stop = false;
-    for (int b = 0; b < r.n && !stop; b += 8) {
-        float v[8];
+    // the wave's longest ray: batches of kSegBatch loads, all in flight
+    // before the first add (a batch costs one memory round trip)
+    int nmax = r.n;
+    for (int off = 32; off > 0; off >>= 1) nmax = max(nmax, __shfl_xor(nmax, off));
+    for (int b = 0; b < nmax && !stop; b += kSegBatch) {
+        float v[kSegBatch];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = b + j < r.n ? tp[(size_t)(b + j) * 64] : 0.0f;
+        for (int j = 0; j < kSegBatch; ++j) v[j] = b + j < r.n ? tp[(size_t)(b + j) * 64] : 0.0f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
+        for (int j = 0; j < kSegBatch; ++j) {
             if (b + j < r.n && !stop) {
                 acc = acc + v[j];
                 ++i;
