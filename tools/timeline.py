@@ -75,8 +75,10 @@ def main():
             t0 = rec[:, 0].min()
             s = (rec[:, 0] - t0).astype(np.float64) / 100.0   # us
             e = (rec[:, 1] - t0).astype(np.float64) / 100.0
-            steps = (rec[:, 2] >> np.uint64(8)).astype(np.int64)
+            steps = (rec[:, 2] >> np.uint64(24)).astype(np.int64)
             xcd = (rec[:, 2] & np.uint64(255)).astype(np.int64)
+            hw = ((rec[:, 2] >> np.uint64(8)) & np.uint64(0xfff)).astype(np.int64)   # HW_ID [15:4]
+            simd = xcd * 4096 + hw   # one SIMD of one CU of one XCD
             span = e.max()
             dur = e - s
             grid = np.linspace(0, span, 41)
@@ -95,6 +97,24 @@ def main():
                 "xcd_steps": [int(steps[xcd == x].sum()) for x in range(8)],
                 "us_per_step_longest": round(dur.max() / max(1, steps[dur.argmax()] / 64), 3),
             }
+            # per SIMD: waves, the busy span (first start to last end) and the
+            # summed lane-steps; the SIMD of the longest wave and the busiest ones
+            ids, inv = np.unique(simd, return_inverse=True)
+            nw = np.bincount(inv)
+            sstep = np.bincount(inv, weights=steps)
+            send = np.zeros(len(ids)); np.maximum.at(send, inv, e)
+            lw = int(dur.argmax())
+            mates = (inv == inv[lw])
+            res.update({
+                "simds_used": int(len(ids)),
+                "waves_per_simd_p50_max": [int(np.median(nw)), int(nw.max())],
+                "simd_steps_p50_p99_max": [int(np.median(sstep)), int(np.percentile(sstep, 99)), int(sstep.max())],
+                "simd_end_p50_p99_max_us": [round(float(np.median(send)), 2), round(float(np.percentile(send, 99)), 2),
+                                            round(float(send.max()), 2)],
+                "longest_wave_simd": {"waves": int(mates.sum()), "steps_per_lane": [round(float(v) / 64, 1) for v in steps[mates]],
+                                      "start_end_us": [[round(float(a_), 2), round(float(b_), 2)] for a_, b_ in zip(s[mates], e[mates])]},
+                "slowest_simd_steps_rank": int((sstep > sstep[inv[int(e.argmax())]]).sum()),
+            })
             print(json.dumps(res))
             out_all[f"rep{rep}"] = res
     if a.json:

@@ -769,7 +769,8 @@ __device__ __forceinline__ int lane_y(int lane)
 #ifdef VR_TIMELINE
 // Timing experiments only (make timeline -> libvr_tl.so, tools/timeline.py):
 // per wave of a regions launch, {start, end} in s_memrealtime ticks (100 MHz),
-// the wave's XCD (blockIdx % 8) and its executed lane-steps.
+// the wave's XCD (blockIdx % 8), its SIMD / CU / SE (HW_ID) and its executed
+// lane-steps.
 constexpr int kTimelineWaves = 1 << 16;
 __device__ unsigned long long g_timeline[kTimelineWaves][3];
 __device__ __forceinline__ void timeline_record(unsigned long long t_begin, unsigned long long steps)
@@ -780,7 +781,9 @@ __device__ __forceinline__ void timeline_record(unsigned long long t_begin, unsi
     if ((threadIdx.x & 63) == 0 && wid < kTimelineWaves) {
         g_timeline[wid][0] = t_begin;
         g_timeline[wid][1] = t_end;
-        g_timeline[wid][2] = (steps << 8) | (blockIdx.x & 7);
+        // HW_ID (hwreg 4): wave slot [3:0], SIMD [5:4], pipe [7:6], CU [11:8], SH [12], SE [15:13]
+        const unsigned hw = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+        g_timeline[wid][2] = (steps << 24) | ((unsigned long long)((hw >> 4) & 0xfffu) << 8) | (blockIdx.x & 7);
     }
 }
 #endif
