@@ -240,7 +240,9 @@ def test_ray_segments_bitexact(r, oracle, vol128, layout, seg):
     step), 300 steps (up to 75 segments), lists reused for a larger
     max_steps (the terms scratch grows), a random volume (every channel
     loaded) and per-tap MediaScroll offsets.  Layout 1 (planar) has no
-    segmented kernel: the option leaves it on its plain path."""
+    segmented kernel: the option leaves it on its plain path.  Measured
+    slower than step-split rays: built only with VR_EXPERIMENTS."""
+    need_experiments(r, "segment")
     r.set_layout_preference(layout)
     r.set_option("schedule", 5)
     r.set_option("segment", seg)
@@ -1291,7 +1293,9 @@ def test_latency_march_bitexact(r, oracle, vol128, layout, split, lat):
     exact against the oracle with step counts -- the recipe volume (G uniform:
     the _uG kernel), a rotated cube, bands, short rays (fewer steps than the
     pipeline's rounds), early-out, a random volume (every channel loaded) and
-    per-tap MediaScroll offsets inside the clamp-exact range."""
+    per-tap MediaScroll offsets inside the clamp-exact range.  Measured
+    slower than the split march: built only with VR_EXPERIMENTS."""
+    need_experiments(r, "lat")
     r.set_layout_preference(layout)
     r.set_option("schedule", 5)
     r.set_option("split", split)
@@ -1336,6 +1340,8 @@ def test_auto_split_at_one_eighth_band_share(r, oracle, vol128, layout, seg):
     corner8 and cornerh (the auto layout for cache-resident volumes); and ray
     segments of 24 steps on that share (sec. 7.1; corner8 has none).  Exact,
     step counts too."""
+    if seg:
+        need_experiments(r, "segment")
     r.set_layout_preference(layout)
     r.set_option("schedule", 5)
     r.set_option("split", 0)

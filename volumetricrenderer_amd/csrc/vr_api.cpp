@@ -820,7 +820,8 @@ vr_status vr_set_option(void* p, const char* name, int value)
     // variants measured slower than the defaults (vr_internal.h VR_EXPERIMENTS)
     const bool experimental = (n == "schedule" && (value == SCHED_QUEUE || value == SCHED_STRIDED ||
                                                    value == SCHED_XCDROWS)) ||
-                              (n == "wg_waves" && value != 4) ||
+                              (n == "wg_waves" && value != 4) || (n == "lat" && value != 0) ||
+                              (n == "segment" && value != 0) ||
                               (n == "slab" && value != 0) || (n == "sort_reuse" && value != 0) ||
                               (n == "proc_enum" && value != 0);
     if (experimental && !VR_EXPERIMENTS)
@@ -999,6 +1000,8 @@ int vr_get_option(void* p, const char* name)
     return -1;
 }
 
+static bool lat_on(const Ctx* c, int layout);
+
 const char* vr_kernel_variant(void* p)
 {
     if (!p) return "none";
@@ -1024,7 +1027,7 @@ const char* vr_kernel_variant(void* p)
          pl.layout == LAYOUT_COL48Z))
         ch = um == 1 ? 0 : um == 2 ? 1 : um == 4 ? 2 : 3;
     // the latency-mode march (small frame shares, vr_march_lat.hip) when it is forced on
-    const int lat = kind == SCHED_REGIONS && c->lat > 0 && lat_supported(pl.layout) ? c->lat : 0;
+    const int lat = kind == SCHED_REGIONS && lat_on(c, pl.layout) ? c->lat : 0;
     if (ch < 0 && lat == 0) return variant_name(pl);
     // built once, thread-safe (a function-local static): every layout x early x channel x depth
     struct Names {
@@ -1118,6 +1121,18 @@ vr_status note_region_stream(Ctx::RegionBuf& rb, hipStream_t s)
     if (rb.nstreams == kMaxRegionStreams) rb.nstreams = -1;
     else rb.streams[rb.nstreams++] = s;
     return VR_OK;
+}
+
+// the latency-mode march (vr_march_lat.hip, built with VR_EXPERIMENTS) for this layout
+static bool lat_on(const Ctx* c, int layout)
+{
+#if VR_EXPERIMENTS
+    return c->lat > 0 && lat_supported(layout);
+#else
+    (void)c;
+    (void)layout;
+    return false;
+#endif
 }
 
 // lanes per ray of a regions frame: option split, or auto from the tiles with work
@@ -1820,7 +1835,7 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
             sc.seg.info = reinterpret_cast<const uint2*>(rb.d + kRegionHeader);
             sc.seg.len = rb.seg_len;
             sc.seg_tiles = rb.nseg_tiles;
-        } else if (c->lat > 0 && lat_supported(pl.layout) && !sc.slab) {
+        } else if (lat_on(c, pl.layout) && !sc.slab) {
             // step-split rays on the latency-mode march
             // (vr_march_lat.hip): K lanes per ray, c->lat rounds of loads in flight
             const int K = c->split > 0 ? c->split : auto_split(c, rb.nwork);

@@ -983,6 +983,7 @@ __global__ __launch_bounds__(kThreads) VR_UM_ATTR void march_regions_u(const Mar
     regions_body<LAYOUT, WRAP, EARLY, ZO, kThreads / 64, UM>(a, tiles, hdr, nwx, lds);
 }
 
+#if VR_EXPERIMENTS   // measured slower than step-split rays
 // ---- ray segments (regions schedule, option "segment") ----
 // With a small frame share (N GPUs) a launch ends with its longest rays: a
 // wave marching a 200-step ray alone on its SIMD issues ~100 VALU ops per
@@ -1143,6 +1144,8 @@ void launch_regions_seg(const MarchArgs& a, bool early, const Schedule& sc, size
         else hipLaunchKernelGGL((seg_resolve<L, false>), rgrid, dim3(256), 0, s, a, sc.hdr, sc.seg);
     }
 }
+
+#endif   // VR_EXPERIMENTS
 
 // ---- step-split rays (regions schedule) ----
 // A wave whose rays march alone on their SIMD waits ~110 dependent memory
@@ -1926,12 +1929,14 @@ hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStre
             hipLaunchKernelGGL((march_rings<L, W, false, false>), grid, block, lds, s, a, cx, cy, nw, npos);
         return hipGetLastError();
     }
+#if VR_EXPERIMENTS
     if constexpr (L == LAYOUT_COL48 || L == LAYOUT_BRICK4832 || L == LAYOUT_CORNERH) {
         if (sc.kind == SCHED_REGIONS && sc.seg.len > 0) {
             launch_regions_seg<L, W>(a, early, sc, lds, s);
             return hipGetLastError();
         }
     }
+#endif
     if constexpr (is_b4_family(L) || L == LAYOUT_ZPAIR || L == LAYOUT_CORNER8 || L == LAYOUT_CORNERH ||
                   L == LAYOUT_COL48Z) {
         if (sc.kind == SCHED_REGIONS && sc.split > 1) {
