@@ -8,7 +8,7 @@ mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1 VR_LIB=$PWD/volumetricrenderer_amd/libvr_tl.so
 run() { timeout -k 10 120 python3 -u tools/timeline.py --reps 2 "$@"; }
 { run --bands 8 --split 4 && run --bands 8 --split 4 --opt tiles_per_wave=1 && run --bands 8 --split 1 \
-  && run --bands 8 --split 1 --opt segment=16 && run --bands 1 --split 1; } > gpurun_out/r04_timeline.txt 2>&1
+  && run --bands 1 --split 1; } > gpurun_out/r04_timeline.txt 2>&1
 rc=$?
 grep -E '^\{"opts' gpurun_out/r04_timeline.txt
 exit $rc
