@@ -159,7 +159,6 @@ struct Ctx {
         TileMap map{};             // host copy: nwx (and off[] for host builds)
         int most = 0;              // the longest per-XCD list (sizes the launch)
         int nwork = 0;             // tiles with estimated work
-        int xwork[8] = {}, xtiles[8] = {};   // per XCD: tiles with work, tiles (sizes the split launch)
         int seg_len = 0;           // segments: steps per segment the lists were built for (0 = none)
         int nseg_tiles = 0;        // segmented tiles (slots of SegArgs.info)
         int icap = 0;              // info entries before the list
@@ -1159,10 +1158,6 @@ static void poll_region_header(Ctx* c)
     Ctx::RegionBuf& rb = c->region[c->rg_buf];
     rb.nwork = c->h_rghdr[9];
     rb.most = c->h_rghdr[10];
-    for (int x = 0; x < 8; ++x) {
-        rb.xwork[x] = c->h_rghdr[kRegionWorkHdr + x];
-        rb.xtiles[x] = c->h_rghdr[x + 1] - c->h_rghdr[x];
-    }
 }
 
 // Retire the current lists (events on the streams that rendered with them) and
@@ -1240,11 +1235,6 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
         const size_t n = (size_t)tw * th;
         const Ctx::RegionBuf& cur = c->region[c->region_cur];
         const int nwork = cur.nwork, most = cur.most;
-        int xwork[8], xtiles[8];
-        for (int x = 0; x < 8; ++x) {
-            xwork[x] = cur.xwork[x];
-            xtiles[x] = cur.xtiles[x];
-        }
         const size_t need = region_build_bytes((int)n);
         if (need > c->rg_bytes) {
             if (c->d_rg) {
@@ -1295,10 +1285,6 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
         rb.most = most;
         rb.map = TileMap{};
         rb.map.nwx = std::max(1, (most + tpw - 1) / tpw);
-        for (int x = 0; x < 8; ++x) {
-            rb.xwork[x] = xwork[x];
-            rb.xtiles[x] = xtiles[x];
-        }
         rb.seg_len = 0;
         rb.nseg_tiles = 0;
         rb.icap = 0;
@@ -1379,7 +1365,6 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     struct SegT { unsigned id; int nseg; };
     std::vector<std::vector<SegT>> segx(8);
     std::vector<std::vector<unsigned>> wholex(8);
-    size_t nworkx[8] = {};   // whole tiles with work: they start each XCD's whole tiles
     int nslots = 0;
     size_t nent = 0;
     for (int x = 0; x < 8; ++x)
@@ -1391,7 +1376,6 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
                 nent += (size_t)ns;
             } else {
                 wholex[x].push_back(t.id);
-                nworkx[x] += t.cost >= 1.0 ? 1 : 0;
                 ++nent;
             }
         }
@@ -1421,9 +1405,6 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
         }
         for (unsigned id : wholex[x]) list[pos++] = id;
         most = std::max(most, pos - (size_t)m.off[x]);
-        hdr[kRegionWorkHdr + x] = (int)nworkx[x];
-        rb.xwork[x] = (int)nworkx[x];
-        rb.xtiles[x] = (int)(pos - (size_t)m.off[x]);
     }
     m.off[8] = (int)pos;
     m.nwx = std::max(1, (int)((most + tpw - 1) / tpw));
@@ -1869,12 +1850,10 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
             if (sc.slab) K = K == 0 ? 1 : K;   // the slab march has one lane per ray; split > 1 uses the plain march
             if (K == 0) K = auto_split(c, rb.nwork);
             if (K > 1) {
-                // a tile with work is K units, an idle one a single unit (vr_march_kernels.h
-                // march_regions_split): the longest XCD's units size the grid
-                int most = 1;
-                for (int x = 0; x < 8; ++x) most = std::max(most, rb.xwork[x] * K + (rb.xtiles[x] - rb.xwork[x]));
+                const int ktpw = tpw;
+                const int most = rb.most;
                 sc.split = K;
-                sc.map.nwx = std::max(1, (most + tpw - 1) / tpw);
+                sc.map.nwx = std::max(1, (most * K + ktpw - 1) / ktpw);
             }
         }
     }

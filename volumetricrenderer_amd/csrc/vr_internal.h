@@ -229,13 +229,10 @@ struct TileMap {
 //   [0..8]   off[]: XCD x renders the entries [off[x], off[x+1])
 //   [9]      tiles with estimated work    [10] the longest list
 //   [11]     entries                       [12] segmented tiles (kRegionSegTiles)
-//   [16..23] per XCD: the tiles with estimated work that start its list
-//            (kRegionWorkHdr; the split march gives an idle tile one wave)
 // Built on the host (vr_api.cpp build_regions) or, for a moving camera, on
 // the GPU (vr_regions.hip launch_region_build, the same dealing; no segments).
-constexpr int kRegionHeader = 32;
+constexpr int kRegionHeader = 16;
 constexpr int kRegionSegTiles = 12;
-constexpr int kRegionWorkHdr = 16;
 // Ray segments (vr_march_kernels.h march_regions_seg / seg_resolve)
 struct SegArgs {
     float* terms;          // [slot][max_steps][64]: each ray's per-step terms

@@ -1216,24 +1216,17 @@ __device__ __forceinline__ unsigned march_pixel_split(const MarchArgs& a, const 
 
 // Regions schedule with step-split rays: an 8x8 tile is K sub-blocks of 64/K
 // rays (8x8, 8x4, 4x4, 4x2 pixels), one per wave; wave w of its XCD's nwx
-// renders the units w, w + nwx, ...  Lane = k * (64/K) + ray, so 4 adjacent
-// lanes are a 2x2 pixel quad at the same step offset.  A tile with estimated
-// work is K units (one sub-block each); an idle tile (background, the tail of
-// each XCD's list, hdr[kRegionWorkHdr + x] tiles in) is one unit that renders
-// its K sub-blocks in turn: at a 1/8 share of config 5 three tiles in four are
-// idle, and as K units each they were 63 % of the launch's waves
-// (DESIGN.md sec. 7.1).
+// renders the units (tile, sub-block) w, w + nwx, ...  Lane = k * (64/K) + ray,
+// so 4 adjacent lanes are a 2x2 pixel quad at the same step offset.
 template <int LAYOUT, bool EARLY, bool ZO, int K, int UM = 0>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void march_regions_split(const MarchArgs a, const unsigned* __restrict__ tiles,
+__global__ __launch_bounds__(kThreads) void march_regions_split(const MarchArgs a, const unsigned* __restrict__ tiles,
                                                                const int* __restrict__ hdr, int nwx)
 {
     constexpr int R = 64 / K, SW = K >= 4 ? 4 : 8, SH = R / SW, NSX = 8 / SW;
     extern __shared__ __attribute__((aligned(16))) unsigned lds[];
     const int xcd = blockIdx.x & 7;
     const int w = (int)(blockIdx.x >> 3) * (kThreads / 64) + (threadIdx.x >> 6);
-    const int begin = hdr[xcd], ntiles = hdr[xcd + 1] - begin;
-    const int nwork = min(max(hdr[kRegionWorkHdr + xcd], 0), ntiles), wunits = nwork * K;
-    const int units = wunits + (ntiles - nwork);
+    const int begin = hdr[xcd], units = (hdr[xcd + 1] - begin) * K;
     if ((int)(blockIdx.x >> 3) * (kThreads / 64) >= units) return;   // whole workgroup, before the barrier
     const FastCtx f = fast_prologue<LAYOUT>(a, lds);
 #ifdef VR_TIMELINE
@@ -1243,15 +1236,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     const int px = ((rho >> 2) % (SW / 2)) * 2 + (rho & 1), py = ((rho >> 2) / (SW / 2)) * 2 + ((rho >> 1) & 1);
     unsigned long long steps = 0;
     for (int u = w; w < nwx && u < units; u += nwx) {
-        // a work tile's sub-block u % K, or all K sub-blocks of an idle tile
-        const bool idle = u >= wunits;
-        const int ti = idle ? nwork + (u - wunits) : u / K;
-        const int s_lo = idle ? 0 : u % K, s_hi = idle ? K : s_lo + 1;
-        const unsigned t = tiles[begin + ti];
-        for (int s = s_lo; s < s_hi; ++s) {
-            const int x = (int)(t & 0xffffu) * 8 + (s % NSX) * SW + px, orow = (int)(t >> 16) * 8 + (s / NSX) * SH + py;
-            steps += march_pixel_split<LAYOUT, EARLY, ZO, K, UM>(a, f, x, orow, k, rho);
-        }
+        const unsigned t = tiles[begin + u / K];
+        const int s = u % K;
+        const int x = (int)(t & 0xffffu) * 8 + (s % NSX) * SW + px, orow = (int)(t >> 16) * 8 + (s / NSX) * SH + py;
+        steps += march_pixel_split<LAYOUT, EARLY, ZO, K, UM>(a, f, x, orow, k, rho);
     }
 #ifdef VR_TIMELINE
     timeline_record(t_begin, steps);

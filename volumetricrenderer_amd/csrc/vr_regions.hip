@@ -45,9 +45,7 @@ struct RgScratch {
     unsigned* vals_in;
     unsigned long long* bin_cost;   // [kAngleBins], zeroed by rg_wedges after use
     unsigned char* bin_xcd;         // [kAngleBins]
-    // [0..7] tiles per XCD, [8] tiles with work, [16..23] tiles with work per
-    // XCD; zeroed by rg_header after use
-    unsigned* counts;
+    unsigned* counts;               // [8] per XCD, [8] tiles with work; zeroed by rg_header after use
     void* sort_tmp;
     size_t sort_bytes;
 };
@@ -137,7 +135,6 @@ __global__ __launch_bounds__(256) void rg_keys(const RegionBuild b, RgScratch s)
     const unsigned xcd = idle ? (unsigned)(i % 8) : (unsigned)s.bin_xcd[(k >> 4) & (kAngleBins - 1)];
     s.keys_in[i] = xcd << 28 | k;
     atomicAdd(&s.counts[xcd], 1u);
-    if (!idle) atomicAdd(&s.counts[16 + xcd], 1u);
 }
 
 // 5. header: off[0..8], tiles with work, longest list; counters zeroed
@@ -156,11 +153,6 @@ __global__ __launch_bounds__(64) void rg_header(RgScratch s, int* hdr, int* hdr_
     hdr[9] = (int)s.counts[8];
     hdr[10] = most;
     hdr[11] = n;
-    hdr[kRegionSegTiles] = 0;
-    for (int x = 0; x < 8; ++x) {
-        hdr[kRegionWorkHdr + x] = (int)s.counts[16 + x];
-        s.counts[16 + x] = 0u;
-    }
     s.counts[8] = 0u;
     if (hdr_host)
         for (int j = 0; j < kRegionHeader; ++j) hdr_host[j] = hdr[j];
@@ -175,7 +167,7 @@ RgScratch carve(void* scratch, int n, size_t sort_bytes)
     s.bin_cost = reinterpret_cast<unsigned long long*>(p + o);
     o = up(o + kAngleBins * sizeof(unsigned long long));
     s.counts = reinterpret_cast<unsigned*>(p + o);
-    o = up(o + 32 * sizeof(unsigned));
+    o = up(o + 16 * sizeof(unsigned));
     s.bin_xcd = reinterpret_cast<unsigned char*>(p + o);
     o = up(o + kAngleBins);
     s.keys_in = reinterpret_cast<unsigned*>(p + o);
