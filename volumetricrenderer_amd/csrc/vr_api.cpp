@@ -152,6 +152,7 @@ struct Ctx {
     bool rg_pending = false;
     int rg_buf = -1;               // the region buffer it built
     long long gpu_builds = 0;      // read-only option "region_gpu_builds"
+    bool rg_preloaded = false;     // region_build_preload done
     struct RegionBuf {
         unsigned* d = nullptr;     // device: kRegionHeader ints (off[9], tiles with work, longest, tiles), then the list
         unsigned* h = nullptr;     // pinned staging copy (host builds)
@@ -1297,6 +1298,12 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
         return VR_OK;
     }
 
+    // a host build (a new target or band set) is already the slow path: load the
+    // GPU build's code object here, not at the first GPU rebuild mid-sequence
+    if (c->region_gpu && !c->rg_preloaded) {
+        HIP_TRY(region_build_preload());
+        c->rg_preloaded = true;
+    }
     // a3 step estimate of the ray through pixel-corner (fx, fy) of the packed target
     auto steps_at = [&](double fx, int orow) {
         const int bl = orow / a.band_rows;

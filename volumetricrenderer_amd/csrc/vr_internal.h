@@ -248,6 +248,7 @@ struct RegionBuild {
     int supertile, wedges;
 };
 size_t region_build_bytes(int ntiles);
+hipError_t region_build_preload();   // load the build's code object (first host build, once)
 // h_hdr (optional, host-mapped): a copy of the header, for sizing later launches
 hipError_t launch_region_build(const RegionBuild& b, void* scratch, unsigned* d_list, int* d_hdr, int* h_hdr,
                                hipStream_t s);

@@ -191,6 +191,16 @@ size_t sort_temp_bytes(int n)
 
 }  // namespace
 
+// Load this translation unit's code object (the build kernels and hipCUB's
+// sort kernels) now: HIP loads a code object at the first launch of one of
+// its kernels, ~20 ms, which would otherwise land in the middle of a moving
+// camera's frame sequence (the first GPU rebuild, region_interval renders in).
+hipError_t region_build_preload()
+{
+    hipFuncAttributes fa;
+    return hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&rg_tiles));
+}
+
 // Scratch of a build over n tiles.  The per-bin sums and the counters must be
 // zero when the first build starts (the caller zeroes a new scratch); every
 // build leaves them zero for the next.

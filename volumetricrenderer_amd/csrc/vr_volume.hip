@@ -582,27 +582,33 @@ hipError_t launch_pack_recipe(const float* d_g1, const float* d_g2, const float*
 }
 
 // Streaming copy for the measured HBM roofline (vr_measure_copy_bandwidth):
-// 16 B per lane, four independent loads in flight per lane, grid-stride.
+// 16 B per lane, one pass over the buffer -- each workgroup copies its own
+// 4 x 256 x 16 B = 16 KiB (four independent loads per lane, issued before
+// the stores), the grid as large as the buffer: the float4 copy of
+// MI355X_MICROARCH.md's measured HBM rate.  (A persistent 2,048-workgroup
+// grid-stride loop read 4.6-4.7 TB/s.)
+constexpr int kCopyPerLane = 4;
 __global__ __launch_bounds__(256) void k_stream_copy(const uint4* __restrict__ src, uint4* __restrict__ dst,
                                                      long long n)
 {
-    const long long stride = (long long)gridDim.x * blockDim.x;
-    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    for (; i + 3 * stride < n; i += 4 * stride) {
-        const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
-        dst[i] = a;
-        dst[i + stride] = b;
-        dst[i + 2 * stride] = c;
-        dst[i + 3 * stride] = d;
-    }
-    for (; i < n; i += stride) dst[i] = src[i];
+    const long long base = (long long)blockIdx.x * (256 * kCopyPerLane) + threadIdx.x;
+    uint4 v[kCopyPerLane];
+#pragma unroll
+    for (int k = 0; k < kCopyPerLane; ++k)
+        if (base + k * 256 < n) v[k] = src[base + k * 256];
+#pragma unroll
+    for (int k = 0; k < kCopyPerLane; ++k)
+        if (base + k * 256 < n) dst[base + k * 256] = v[k];
 }
 
 hipError_t launch_stream_copy(const void* src, void* dst, size_t bytes, hipStream_t s)
 {
-    // 8 workgroups of 256 lanes per CU (256 CUs): every CU keeps ~32 KiB of loads in flight
-    hipLaunchKernelGGL(k_stream_copy, dim3(2048), dim3(256), 0, s, static_cast<const uint4*>(src),
-                       static_cast<uint4*>(dst), (long long)(bytes / 16));
+    const long long n = (long long)(bytes / 16);
+    const long long blocks = (n + 256 * kCopyPerLane - 1) / (256 * kCopyPerLane);
+    if (blocks <= 0) return hipSuccess;
+    if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_stream_copy, dim3((unsigned)blocks), dim3(256), 0, s, static_cast<const uint4*>(src),
+                       static_cast<uint4*>(dst), n);
     return hipGetLastError();
 }
 
