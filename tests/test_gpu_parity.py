@@ -1361,6 +1361,27 @@ def test_auto_split_at_one_eighth_band_share(r, oracle, vol128, layout, seg):
         r.set_layout_preference(0)
 
 
+@pytest.mark.parametrize("order", [1, 2])
+@pytest.mark.parametrize("layout", [15, 14])
+def test_region_order_bitexact(r, oracle, vol128, layout, order):
+    """Option region_order: each XCD's list by estimated
+    cost, longest tile (1) or longest S x S block (2) first, instead of
+    inside-out.  The lists only order the work: full frame and a 1/8 band
+    share stay exact, step counts included."""
+    r.set_layout_preference(layout)
+    r.set_option("region_order", order)
+    assert r.get_option("region_order") == order
+    try:
+        osd, gsd = vr.reference_shader_data(16 / 9, 20.0, -15.0)
+        for W, H, band in [(640, 360, {}), (1920, 1080, dict(band_rows=16, band_stride=8, band_first=3))]:
+            img, ref, c, s = render_both(r, oracle, vol128, W, H, osd, gsd, **band)
+            assert_exact(img, ref)
+            assert c == s
+    finally:
+        r.set_option("region_order", 0)
+        r.set_layout_preference(0)
+
+
 # ---- BASELINE config 4: 3840x2160, 256 steps, 128^3 recipe volume ----
 
 @pytest.fixture(scope="module")

@@ -138,6 +138,7 @@ struct Ctx {
     int proc_enum = 0;             // procedural sort: 1 = 64x64-region enumeration with shadow rays too
     int slab_cap = kSlabMaxChunks; // its chunks per channel (<= kSlabMaxChunks; smaller forces the fallback)
     int segment = 0;               // regions: ray segments of L steps for the long tiles (0 = off)
+    int region_order = 0;          // regions: 0 = each XCD inside-out (ring, angle); 1 = by estimated cost, longest first
     float* d_terms = nullptr;      // segments: the per-step terms (SegArgs.terms)
     size_t terms_bytes = 0;
     int wg_waves = 4;              // regions: waves per workgroup (4, 8, 16)
@@ -901,6 +902,13 @@ vr_status vr_set_option(void* p, const char* name, int value)
         c->slab_cap = value;
         return VR_OK;
     }
+    if (n == "region_order") {
+        if (value < 0 || value > 2)
+            return fail(VR_ERR_INVALID, "vr_set_option: region_order is 0 (inside-out), 1 (longest tile first) or "
+                                        "2 (longest block first)");
+        c->region_order = value;
+        return VR_OK;
+    }
     if (n == "segment") {
         if (value != 0 && (value < 4 || value > 4096))
             return fail(VR_ERR_INVALID, "vr_set_option: segment is 0 (off) or 4-4096 steps");
@@ -982,6 +990,7 @@ int vr_get_option(void* p, const char* name)
         return (int)std::min<size_t>((c->defer_bytes + 1023) / 1024, 0x7fffffff);
     if (n == "slab_cap") return c->slab_cap;
     if (n == "segment") return c->segment;
+    if (n == "region_order") return c->region_order;
     if (n == "region_segment_tiles") return c->region_cur >= 0 ? c->region[c->region_cur].nseg_tiles : 0;
     if (n == "sort_reuse") return c->sort_reuse;
     if (n == "wg_waves") return c->wg_waves;
@@ -1215,7 +1224,7 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     const int tw = (a.width + 7) >> 3, th = (a.out_rows + 7) >> 3;
     float key[kRegionKeyLen] = {(float)tw, (float)th, (float)a.width, (float)a.height, (float)a.out_rows,
                                 (float)a.band_rows, (float)a.band_stride, (float)a.band_first, (float)tpw,
-                                (float)c->wedges, (float)seg_len, (float)c->split, (float)c->supertile};
+                                (float)c->wedges, (float)(seg_len + 65536 * c->region_order), (float)c->split, (float)c->supertile};
     constexpr int grid_part = 13;   // the part a reused list must match
     int kn = grid_part;
     for (float v : {(float)a.max_steps, a.step_size, (float)cpx, (float)cprow}) key[kn++] = v;
@@ -1232,7 +1241,7 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     // the GPU build on the render stream (vr_regions.hip) -- no host loop, no
     // host wait; tiles with work and the longest list are the last completed
     // build's (they size the launch, not the result)
-    if (same_grid && c->region_gpu && seg_len == 0 && th < 65536 && tw < 65536) {
+    if (same_grid && c->region_gpu && seg_len == 0 && c->region_order == 0 && th < 65536 && tw < 65536) {
         const size_t n = (size_t)tw * th;
         const Ctx::RegionBuf& cur = c->region[c->region_cur];
         const int nwork = cur.nwork, most = cur.most;
@@ -1357,7 +1366,27 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     auto inside_out = [](const T& u, const T& v) {
         return u.ring != v.ring ? u.ring < v.ring : u.ang != v.ang ? u.ang < v.ang : u.sub < v.sub;
     };
-    for (auto& l : xl) std::sort(l.begin(), l.end(), inside_out);
+    if (c->region_order == 1) {   // longest estimated work first (LPT), inside-out among equals
+        for (auto& l : xl)
+            std::stable_sort(l.begin(), l.end(), [&](const T& u, const T& v) {
+                return u.cost != v.cost ? u.cost > v.cost : inside_out(u, v);
+            });
+    } else if (c->region_order == 2) {   // S x S blocks by their longest tile, a block's tiles together
+        const int bw = (tw + S - 1) / S;
+        std::vector<double> bmax((size_t)bw * ((th + S - 1) / S), 0.0);
+        auto bidx = [&](const T& t) { return (size_t)((t.id >> 16) / S) * bw + (size_t)((t.id & 0xffffu) / S); };
+        for (const auto& l : xl)
+            for (const T& t : l) bmax[bidx(t)] = std::max(bmax[bidx(t)], t.cost);
+        for (auto& l : xl)
+            std::stable_sort(l.begin(), l.end(), [&](const T& u, const T& v) {
+                const double cu = bmax[bidx(u)], cv = bmax[bidx(v)];
+                if (cu != cv) return cu > cv;
+                if (bidx(u) != bidx(v)) return bidx(u) < bidx(v);
+                return u.sub < v.sub;
+            });
+    } else {
+        for (auto& l : xl) std::sort(l.begin(), l.end(), inside_out);
+    }
     std::sort(idle.begin(), idle.end(), inside_out);
     for (size_t i = 0; i < idle.size(); ++i) xl[i % 8].push_back(idle[i]);
 
