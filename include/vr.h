@@ -283,6 +283,10 @@ vr_status vr_set_layout_preference(void* ctx, int pref);
  *   "supertile"       1, 2, 4, regions schedule: the tile lists are ordered by
  *                     S x S blocks of 8x8 tiles (default 2), so a workgroup's
  *                     waves render one block.
+ *   "region_order"    regions schedule, each XCD's list: 2 (default) = S x S
+ *                     blocks by their longest estimated tile, longest first;
+ *                     1 = tiles by estimate, longest first; 0 = inside-out
+ *                     (ring around the projected box centre, then angle).
  *   "wg_waves"        4 (default), 8, 16: waves per workgroup of the regions
  *                     march (col48, brick4832, cornerh).
  *   "segment"         0 (off, the default) or 4-4096 steps, regions schedule

@@ -1361,13 +1361,14 @@ def test_auto_split_at_one_eighth_band_share(r, oracle, vol128, layout, seg):
         r.set_layout_preference(0)
 
 
-@pytest.mark.parametrize("order", [1, 2])
+@pytest.mark.parametrize("order", [0, 1, 2])
 @pytest.mark.parametrize("layout", [15, 14])
 def test_region_order_bitexact(r, oracle, vol128, layout, order):
-    """Option region_order: each XCD's list by estimated
-    cost, longest tile (1) or longest S x S block (2) first, instead of
-    inside-out.  The lists only order the work: full frame and a 1/8 band
-    share stay exact, step counts included."""
+    """Option region_order: each XCD's list inside-out
+    (0), longest tile first (1) or longest S x S block first (2, the
+    default).  The lists only order the work: full frame, a 1/8 band share
+    and GPU-rebuilt lists under a moving camera stay exact, step counts
+    included."""
     r.set_layout_preference(layout)
     r.set_option("region_order", order)
     assert r.get_option("region_order") == order
@@ -1377,8 +1378,17 @@ def test_region_order_bitexact(r, oracle, vol128, layout, order):
             img, ref, c, s = render_both(r, oracle, vol128, W, H, osd, gsd, **band)
             assert_exact(img, ref)
             assert c == s
+        r.set_option("region_interval", 1)   # GPU rebuilds every render
+        builds0 = r.get_option("region_gpu_builds")
+        for i in range(1, 5):
+            osd, gsd = vr.reference_shader_data(16 / 9, 20.0 + SPIN_DEG * i, -15.0)
+            img, ref, c, s = render_both(r, oracle, vol128, 640, 360, osd, gsd)
+            assert_exact(img, ref)
+            assert c == s
+        assert r.get_option("region_gpu_builds") - builds0 >= 3
     finally:
-        r.set_option("region_order", 0)
+        r.set_option("region_interval", 32)
+        r.set_option("region_order", 2)
         r.set_layout_preference(0)
 
 

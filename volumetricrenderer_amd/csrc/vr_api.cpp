@@ -138,7 +138,9 @@ struct Ctx {
     int proc_enum = 0;             // procedural sort: 1 = 64x64-region enumeration with shadow rays too
     int slab_cap = kSlabMaxChunks; // its chunks per channel (<= kSlabMaxChunks; smaller forces the fallback)
     int segment = 0;               // regions: ray segments of L steps for the long tiles (0 = off)
-    int region_order = 0;          // regions: 0 = each XCD inside-out (ring, angle); 1 = by estimated cost, longest first
+    // regions: each XCD's list 0 = inside-out (ring, angle); 1 = longest tile first;
+    // 2 = longest S x S block first (the default since round 4)
+    int region_order = 2;
     float* d_terms = nullptr;      // segments: the per-step terms (SegArgs.terms)
     size_t terms_bytes = 0;
     int wg_waves = 4;              // regions: waves per workgroup (4, 8, 16)
@@ -1241,7 +1243,7 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     // the GPU build on the render stream (vr_regions.hip) -- no host loop, no
     // host wait; tiles with work and the longest list are the last completed
     // build's (they size the launch, not the result)
-    if (same_grid && c->region_gpu && seg_len == 0 && c->region_order == 0 && th < 65536 && tw < 65536) {
+    if (same_grid && c->region_gpu && seg_len == 0 && th < 65536 && tw < 65536) {
         const size_t n = (size_t)tw * th;
         const Ctx::RegionBuf& cur = c->region[c->region_cur];
         const int nwork = cur.nwork, most = cur.most;
@@ -1275,7 +1277,7 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
         }
         g.ccx = (cpx + 0.5) / 8.0; g.ccy = (cprow + 0.5) / 8.0;
         g.ctx = (cpx >> 3) / S; g.cty = (cprow >> 3) / S;
-        g.supertile = S; g.wedges = c->wedges;
+        g.supertile = S; g.wedges = c->wedges; g.order = c->region_order;
         int* dev_hdr = nullptr;
         HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&dev_hdr), c->h_rghdr, 0));
         // one build scratch per context: a build on another stream waits for the last one

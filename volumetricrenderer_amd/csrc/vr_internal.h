@@ -246,6 +246,7 @@ struct RegionBuild {
     double ccx, ccy;       // box-centre tile (fractional), S x S block of it
     int ctx, cty;
     int supertile, wedges;
+    int order;             // option region_order: 0 inside-out, 1 longest tile first, 2 longest S x S block first
 };
 size_t region_build_bytes(int ntiles);
 hipError_t region_build_preload();   // load the build's code object (first host build, once)

@@ -40,6 +40,7 @@ constexpr int kWedgeThreads = 1024;
 constexpr double kCostScale = 1024.0;   // fixed point of the per-bin work sums
 
 struct RgScratch {
+    unsigned* bmax;                 // [blocks] region_order 1/2: the longest tile of each S x S block (x16 fixed point)
     unsigned* keys_in;
     unsigned* keys_out;
     unsigned* vals_in;
@@ -90,6 +91,10 @@ __global__ __launch_bounds__(256) void rg_tiles(const RegionBuild b, RgScratch s
     if (work) {
         atomicAdd(&s.bin_cost[abin], (unsigned long long)(cost * kCostScale));
         atomicAdd(&s.counts[8], 1u);
+        if (b.order != 0) {   // order 1: the tile's own cost (its block slot is its own tile index)
+            const int bw = (b.tw + S - 1) / S;
+            atomicMax(&s.bmax[b.order == 2 ? sy * bw + sx : i], (unsigned)fmin(cost * 16.0, 4294967295.0));
+        }
     }
     s.keys_in[i] = (work ? 0u : 1u) << 27 | (unsigned)ring << 16 | (unsigned)abin << 4 | (unsigned)sub;
     s.vals_in[i] = ((unsigned)ty << 16) | (unsigned)tx;
@@ -125,14 +130,25 @@ __global__ __launch_bounds__(kWedgeThreads) void rg_wedges(const RegionBuild b, 
     }
 }
 
-// 3. the sort key: XCD | idle | ring | angle bin | place in block
+// 3. the sort key: XCD | idle | ring | angle bin | place in block.  With
+// region_order 1 / 2 a work tile's key is XCD | 0 | the inverted cost of the
+// tile / of its S x S block (10 bits, relative to max_steps) | its block (13
+// bits; equal costs of far-apart blocks may interleave: order only) | place
+// in block -- the host build's longest-first order, quantised
 __global__ __launch_bounds__(256) void rg_keys(const RegionBuild b, RgScratch s)
 {
     const int i = (int)(blockIdx.x * 256 + threadIdx.x);
     if (i >= b.tw * b.th) return;
-    const unsigned k = s.keys_in[i];
+    unsigned k = s.keys_in[i];
     const bool idle = (k >> 27) & 1u;
     const unsigned xcd = idle ? (unsigned)(i % 8) : (unsigned)s.bin_xcd[(k >> 4) & (kAngleBins - 1)];
+    if (b.order != 0 && !idle) {
+        const int S = b.supertile, ty = i / b.tw, tx = i - ty * b.tw;
+        const int bw = (b.tw + S - 1) / S, blk = (ty / S) * bw + tx / S;
+        const double c = (double)s.bmax[b.order == 2 ? blk : i] / 16.0;
+        const unsigned q = (unsigned)fmin(1023.0, c * 1023.0 / (double)max(b.max_steps, 1));
+        k = (1023u - q) << 17 | ((unsigned)blk & 0x1fffu) << 4 | (k & 0xfu);
+    }
     s.keys_in[i] = xcd << 28 | k;
     atomicAdd(&s.counts[xcd], 1u);
 }
@@ -164,6 +180,8 @@ RgScratch carve(void* scratch, int n, size_t sort_bytes)
     char* p = static_cast<char*>(scratch);
     RgScratch s{};
     size_t o = 0;
+    s.bmax = reinterpret_cast<unsigned*>(p + o);
+    o = up(o + (size_t)n * 4);
     s.bin_cost = reinterpret_cast<unsigned long long*>(p + o);
     o = up(o + kAngleBins * sizeof(unsigned long long));
     s.counts = reinterpret_cast<unsigned*>(p + o);
@@ -206,7 +224,7 @@ hipError_t region_build_preload()
 // build leaves them zero for the next.
 size_t region_build_bytes(int n)
 {
-    return 256 + (size_t)kAngleBins * 8 + 256 + kAngleBins + 256 + 3 * ((size_t)n * 4 + 256) + sort_temp_bytes(n) + 256;
+    return 256 + (size_t)kAngleBins * 8 + 256 + kAngleBins + 256 + 4 * ((size_t)n * 4 + 256) + sort_temp_bytes(n) + 256;
 }
 
 hipError_t launch_region_build(const RegionBuild& b, void* scratch, unsigned* d_list, int* d_hdr, int* h_hdr,
@@ -217,6 +235,10 @@ hipError_t launch_region_build(const RegionBuild& b, void* scratch, unsigned* d_
     const size_t sb = sort_temp_bytes(n);
     RgScratch s = carve(scratch, n, sb);
     const dim3 grid((unsigned)((n + 255) / 256));
+    if (b.order != 0) {   // the per-block maxima start at zero
+        const hipError_t z = hipMemsetAsync(s.bmax, 0, (size_t)n * 4, st);
+        if (z != hipSuccess) return z;
+    }
     hipLaunchKernelGGL(rg_tiles, grid, dim3(256), 0, st, b, s);
     hipLaunchKernelGGL(rg_wedges, dim3(1), dim3(kWedgeThreads), 0, st, b, s);
     hipLaunchKernelGGL(rg_keys, grid, dim3(256), 0, st, b, s);
