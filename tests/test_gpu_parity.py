@@ -1374,9 +1374,12 @@ def test_region_order_bitexact(r, oracle, vol128, layout, order):
     assert r.get_option("region_order") == order
     try:
         osd, gsd = vr.reference_shader_data(16 / 9, 20.0, -15.0)
+        # band_first 3 of 8 holds the partial last band (frame rows 1072-1079):
+        # its rows past the frame are left untouched (vr.h), so they are not compared
         for W, H, band in [(640, 360, {}), (1920, 1080, dict(band_rows=16, band_stride=8, band_first=3))]:
             img, ref, c, s = render_both(r, oracle, vol128, W, H, osd, gsd, **band)
-            assert_exact(img, ref)
+            rows = sum(min(16, H - b * 16) for b in range(3, (H + 15) // 16, 8)) if band else H
+            assert_exact(img[:rows], ref[:rows])
             assert c == s
         r.set_option("region_interval", 1)   # GPU rebuilds every render
         builds0 = r.get_option("region_gpu_builds")
