@@ -289,7 +289,8 @@ vr_status vr_set_layout_preference(void* ctx, int pref);
  *                     (ring around the projected box centre, then angle).
  *   "wg_waves"        4 (default), 8, 16: waves per workgroup of the regions
  *                     march (col48, brick4832, cornerh).
- *   "segment"         0 (off, the default) or 4-4096 steps, regions schedule
+ *   "segment"         VR_EXPERIMENTS builds only (measured slower, DESIGN.md
+ *                     sec. 7.1).  0 (off, the default) or 4-4096 steps, regions schedule
  *                     (col48, brick4832, cornerh): tiles whose estimated work
  *                     is at least 2L steps are marched as segments of L steps,
  *                     one wave each, and a resolve pass adds each ray's stored
@@ -343,12 +344,11 @@ vr_status vr_set_layout_preference(void* ctx, int pref);
  *                     Read-only: "shadow_defer_kib" the scratch held now,
  *                     "shadow_defer_last" 1 if the last procedural render ran
  *                     the deferred passes.
- *   "lat"             regions schedule, col48 / brick4832 / cornerh: the
- *                     latency-mode march for small frame shares ("split" lanes
- *                     per ray, 2-4 rounds of loads in flight; bit-exact):
- *                     0 = off, 2/3/4 = on with that depth, -1 = auto (on when
- *                     the target's tiles with work are too few to fill the GPU,
- *                     e.g. a 1/8 multi-GPU share).
+ *   "lat"             VR_EXPERIMENTS builds only (measured slower, DESIGN.md
+ *                     sec. 7.1): regions schedule, col48 / brick4832 / cornerh,
+ *                     the latency-mode march ("split" lanes per ray, 2-4
+ *                     rounds of loads in flight; bit-exact): 0 = off (the only
+ *                     value the default library accepts), 2/3/4 = that depth.
  *   "lattice"         procedural medium, sorted schedule: 1 = the fBm reads its
  *                     per-cell gradient-pair offsets from a lattice table in
  *                     global memory (the default; built when the seed or the

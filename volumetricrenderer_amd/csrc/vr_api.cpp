@@ -145,7 +145,7 @@ struct Ctx {
     size_t terms_bytes = 0;
     int wg_waves = 4;              // regions: waves per workgroup (4, 8, 16)
     int supertile = 2;             // regions: list order by S x S blocks of tiles (1 = per tile; 2 measured 1 % faster)
-    int lat = 0;                   // regions: latency-mode march, rounds of loads in flight (0 = off, -1 = auto, 2-4)
+    int lat = 0;                   // regions: latency-mode march, rounds of loads in flight (0 = off, 2-4; VR_EXPERIMENTS)
     int region_interval = kRegionRebuildInterval;   // option "region_interval": renders a moved camera reuses the lists
     int region_gpu = 1;            // option "region_gpu": 1 = a moved camera's lists are rebuilt on the GPU
     void* d_rg = nullptr;          // GPU list build scratch (region_build_bytes), zeroed when allocated
@@ -938,8 +938,8 @@ vr_status vr_set_option(void* p, const char* name, int value)
         return VR_OK;
     }
     if (n == "lat") {
-        if (value != -1 && value != 0 && value != 2 && value != 3 && value != 4)
-            return fail(VR_ERR_INVALID, "vr_set_option: lat is -1 (auto), 0 (off), 2, 3 or 4 (rounds in flight)");
+        if (value != 0 && value != 2 && value != 3 && value != 4)
+            return fail(VR_ERR_INVALID, "vr_set_option: lat is 0 (off), 2, 3 or 4 (rounds in flight)");
         c->lat = value;
         return VR_OK;
     }
