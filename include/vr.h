@@ -278,8 +278,9 @@ vr_status vr_set_layout_preference(void* ctx, int pref);
  *                     tiles in row order, 4 = rings.
  *   "waves_per_simd"  1-8, queue schedule.
  *   "tiles_per_wave"  1-64, strided, ring and region schedules; 0 = auto,
- *                     the default: 2 for rings and regions, 1 for strided.
- *   "wedges"          1-64, regions schedule: wedges per XCD (default 4).
+ *                     the default: 2 for rings, 3 for regions on the col48
+ *                     layout and 2 on the others, 1 for strided.
+ *   "wedges"          1-64, regions schedule: wedges per XCD (default 8).
  *   "supertile"       1, 2, 4, regions schedule: the tile lists are ordered by
  *                     S x S blocks of 8x8 tiles (default 2), so a workgroup's
  *                     waves render one block.

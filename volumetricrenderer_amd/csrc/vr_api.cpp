@@ -47,7 +47,7 @@ vr_status fail(vr_status st, const char* fmt, ...)
 constexpr int kDefaultSchedule = -1;     // -1 auto, 0 static tiles, 1 persistent queue, 2 strided
 constexpr int kDefaultWavesPerSimd = 4;
 constexpr int kDefaultTilesPerWave = 0;   // 0 = auto: 2 for rings and regions, 1 for strided (measured)
-constexpr int kDefaultWedges = 4;         // regions schedule: wedges per XCD (measured)
+constexpr int kDefaultWedges = 8;         // regions schedule: wedges per XCD (measured; 4 until round 4)
 // a moving camera reuses the current (still complete, maybe less balanced)
 // region lists for this many renders before they are rebuilt
 constexpr int kRegionRebuildInterval = 32;
@@ -1832,7 +1832,12 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
     // auto schedule (measured): regions -- per-XCD angular
     // wedges of the frame, each walked inside-out (longest rays first)
     const int kind = c->schedule >= 0 ? c->schedule : SCHED_REGIONS;
-    const int tpw = c->tiles_per_wave > 0 ? c->tiles_per_wave : (kind == SCHED_RINGS || kind == SCHED_REGIONS ? 2 : 1);
+    // tiles per wave, auto: rings 2; regions 3 for COL48 (the streamed 512^3
+    // layout: 0.1216 -> 0.1176 ms with 8 wedges, profiles/r04/r04_tpw_c5.txt)
+    // and 2 for the others (config 4 level); strided 1
+    const int tpw = c->tiles_per_wave > 0 ? c->tiles_per_wave
+                    : kind == SCHED_REGIONS ? (pl.layout == LAYOUT_COL48 ? 3 : 2)
+                    : kind == SCHED_RINGS ? 2 : 1;
     Schedule sc{kind, 0, 0, tpw, c->waves_per_simd, c->d_heads, nullptr, {}, 1, 0, c->wg_waves, 0, nullptr};
     sc.slab = pl.layout == LAYOUT_COL48 && c->slab;
     a.slab_cap = c->slab_cap;
