@@ -1395,29 +1395,6 @@ def test_region_order_bitexact(r, oracle, vol128, layout, order):
         r.set_layout_preference(0)
 
 
-@pytest.mark.parametrize("split", [2, 4, 8])
-@pytest.mark.parametrize("layout", [15, 14])
-def test_split_unit_order_bitexact(r, oracle, vol128, layout, split):
-    """Option unit_order 1: the split march takes its units sub-block-major
-    (tile u % count, sub-block u / count), so a tile's K sub-blocks land on
-    different workgroups.  Exact, step counts too, on a 1/8 band share and a
-    rotated small frame."""
-    r.set_layout_preference(layout)
-    r.set_option("split", split)
-    r.set_option("unit_order", 1)
-    try:
-        for W, H, band, osd_args in [(1920, 1080, dict(band_rows=16, band_stride=8, band_first=5), (16 / 9,)),
-                                     (333, 187, {}, (16 / 9, 25.0, -40.0))]:
-            osd, gsd = vr.reference_shader_data(*osd_args)
-            img, ref, c, s = render_both(r, oracle, vol128, W, H, osd, gsd, **band)
-            assert_exact(img, ref)
-            assert c == s
-    finally:
-        r.set_option("unit_order", 0)
-        r.set_option("split", 0)
-        r.set_layout_preference(0)
-
-
 # ---- BASELINE config 4: 3840x2160, 256 steps, 128^3 recipe volume ----
 
 @pytest.fixture(scope="module")

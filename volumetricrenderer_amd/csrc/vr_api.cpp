@@ -141,7 +141,6 @@ struct Ctx {
     // regions: each XCD's list 0 = inside-out (ring, angle); 1 = longest tile first;
     // 2 = longest S x S block first (the default since round 4)
     int region_order = 2;
-    int unit_order = 0;            // split march: 0 tile-major units, 1 sub-block-major (option "unit_order")
     float* d_terms = nullptr;      // segments: the per-step terms (SegArgs.terms)
     size_t terms_bytes = 0;
     int wg_waves = 4;              // regions: waves per workgroup (4, 8, 16)
@@ -905,11 +904,6 @@ vr_status vr_set_option(void* p, const char* name, int value)
         c->slab_cap = value;
         return VR_OK;
     }
-    if (n == "unit_order") {
-        if (value < 0 || value > 1) return fail(VR_ERR_INVALID, "vr_set_option: unit_order is 0 or 1");
-        c->unit_order = value;
-        return VR_OK;
-    }
     if (n == "region_order") {
         if (value < 0 || value > 2)
             return fail(VR_ERR_INVALID, "vr_set_option: region_order is 0 (inside-out), 1 (longest tile first) or "
@@ -999,7 +993,6 @@ int vr_get_option(void* p, const char* name)
     if (n == "slab_cap") return c->slab_cap;
     if (n == "segment") return c->segment;
     if (n == "region_order") return c->region_order;
-    if (n == "unit_order") return c->unit_order;
     if (n == "region_segment_tiles") return c->region_cur >= 0 ? c->region[c->region_cur].nseg_tiles : 0;
     if (n == "sort_reuse") return c->sort_reuse;
     if (n == "wg_waves") return c->wg_waves;
@@ -1848,7 +1841,6 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
     Schedule sc{kind, 0, 0, tpw, c->waves_per_simd, c->d_heads, nullptr, {}, 1, 0, c->wg_waves, 0, nullptr};
     sc.slab = pl.layout == LAYOUT_COL48 && c->slab;
     a.slab_cap = c->slab_cap;
-    a.unit_order = c->unit_order;
     if (kind == SCHED_RINGS || kind == SCHED_REGIONS) box_centre_pixel(c, a, &sc.center_x, &sc.center_y);
     if (kind == SCHED_REGIONS) {
         const bool splittable = is_b4_family(pl.layout) || pl.layout == LAYOUT_ZPAIR || pl.layout == LAYOUT_CORNER8 ||

@@ -210,7 +210,6 @@ struct MarchArgs {
     unsigned long long* step_counter;
     ProcParams proc;
     int slab_cap;                // LDS slab march (COL48): chunks per channel the slab holds
-    int unit_order;              // split march: 0 = a tile's K sub-blocks are consecutive units, 1 = sub-block-major
 };
 
 // How the march kernel maps tiles to waves.

@@ -1235,13 +1235,9 @@ __global__ __launch_bounds__(kThreads) void march_regions_split(const MarchArgs 
     const int lane = threadIdx.x & 63, k = lane / R, rho = lane % R;
     const int px = ((rho >> 2) % (SW / 2)) * 2 + (rho & 1), py = ((rho >> 2) / (SW / 2)) * 2 + ((rho >> 1) & 1);
     unsigned long long steps = 0;
-    const int count = units / K;
     for (int u = w; w < nwx && u < units; u += nwx) {
-        // unit_order 0: tile u / K, sub-block u % K (a tile's sub-blocks on
-        // neighbouring waves of one workgroup); 1: tile u % count, sub-block
-        // u / count (the sub-blocks of one tile on different workgroups)
-        const int ti = a.unit_order ? u % count : u / K, s = a.unit_order ? u / count : u % K;
-        const unsigned t = tiles[begin + ti];
+        const unsigned t = tiles[begin + u / K];
+        const int s = u % K;
         const int x = (int)(t & 0xffffu) * 8 + (s % NSX) * SW + px, orow = (int)(t >> 16) * 8 + (s / NSX) * SH + py;
         steps += march_pixel_split<LAYOUT, EARLY, ZO, K, UM>(a, f, x, orow, k, rho);
     }
