@@ -308,3 +308,40 @@ def test_render_sequence_spinning(oracle):
         obj, glob = vr.shader_data_arrays(*cams[-1])
         ref, _ = oracle.render(vol, obj, glob, oracle.from_params(vr.march_defaults()), W, H, 0)
         assert np.array_equal(out.cpu().numpy(), ref)
+
+
+def test_one_rank_frames_in_flight(oracle):
+    """BandSharder at world 1 (the bench's N = 1 frame loop): grid frames
+    alternate two streams and two targets (two frames in flight); each
+    target's frame equals the oracle's, and the caller's stream waits for
+    both.  The procedural medium keeps one stream (its scratch is the
+    context's): its frames are exact as well."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import volumetricrenderer_amd as vr
+    from volumetricrenderer_amd.distributed import BandSharder
+    W, H = 320, 180
+    vol = oracle.build_volume(128)
+    with vr.Renderer(0) as r:
+        r.set_volume(vol)
+        osd, gsd = vr.reference_shader_data(W / H, 10.0, 5.0)
+        r.set_shader_data(osd, gsd)
+        r.set_march(vr.march_defaults())
+        sh = BandSharder(r, W, H, 0)
+        obj, glob = vr.shader_data_arrays(osd, gsd)
+        ref, _ = oracle.render(vol, obj, glob, oracle.from_params(vr.march_defaults()), W, H, 0)
+        for k in (1, 4, 5):
+            frame = sh.run_frames(k)
+            torch.cuda.current_stream().synchronize()   # the caller's stream joined both
+            assert np.array_equal(frame.cpu().numpy(), ref), k
+        assert len(sh._targets2) == 2 and all(np.array_equal(t.cpu().numpy(), ref) for t in sh._targets2)
+        m = vr.march_defaults(max_steps=32)
+        r.set_march(m)
+        r.set_procedural(shadow_steps=4)
+        p = oracle.procedural_from(r.procedural)
+        sh2 = BandSharder(r, W, H, 0)
+        frame = sh2.run_frames(3)
+        torch.cuda.synchronize()
+        ref2, _ = oracle.render_procedural(p, obj, glob, oracle.from_params(m), W, H, 0)
+        assert np.array_equal(frame.cpu().numpy(), ref2)
+        assert getattr(sh2, "_launch2", None) is None

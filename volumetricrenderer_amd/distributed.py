@@ -156,9 +156,40 @@ class BandSharder:
         gather buffers and frames are double-buffered.  Each buffer of a
         parity is reused only after the stream order has retired its last
         reader.  Returns the last frame (rank 0) or band set."""
+        proc = getattr(self.r, "procedural", None)
+        if self.world == 1 and hasattr(self.r, "prepare_render") and (proc is None or not proc.enabled):
+            # one rank, grid medium: the frame is the render.  Two frames in
+            # flight here too: consecutive frames alternate between two
+            # streams and two targets, so frame i+1's waves fill the SIMDs
+            # while frame i's last, longest rays finish (7 % more frames/s at
+            # config 5, profiles/r04/inflight_ab.txt).  The grid render's only
+            # shared state is the read-only region lists; the procedural
+            # medium's cost-sort and shadow scratch belong to the context and
+            # serve one frame at a time, so it keeps one stream (below).
+            # Both streams start after the caller's stream and the caller's
+            # stream waits for both.  The launchers are prepared once.
+            if getattr(self, "_launch2", None) is None:
+                self._streams2 = [torch.cuda.Stream(self.local.device), torch.cuda.Stream(self.local.device)]
+                self._targets2 = [self.local, torch.empty_like(self.local)]
+                self._launch2 = [self.r.prepare_render(self.width, self.height, self.fmt, self._targets2[j],
+                                                       stream=self._streams2[j]) for j in range(2)]
+            cur = torch.cuda.current_stream(self.local.device)
+            for st in self._streams2:
+                st.wait_stream(cur)
+            for i in range(k):
+                j = i % 2
+                ev = events[i] if events else None
+                if ev is not None:
+                    ev[0].record(self._streams2[j])
+                self._launch2[j]()
+                if ev is not None:
+                    ev[1].record(self._streams2[j])
+            for st in self._streams2:
+                cur.wait_stream(st)
+            self.frame_buf = self._targets2[(k - 1) % 2] if k > 0 else self.frame_buf
+            return self.frame_buf
         if self.world == 1 and hasattr(self.r, "prepare_render"):
-            # one rank: the frame is the render; launch it through a prepared
-            # launcher (the ctypes arguments are built once)
+            # one rank, procedural medium: one stream, a prepared launcher
             if getattr(self, "_launch1", None) is None:
                 self._launch1 = self.r.prepare_render(self.width, self.height, self.fmt, self.local)
             for i in range(k):
