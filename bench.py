@@ -276,6 +276,9 @@ def main() -> int:
     ap.add_argument("--layout", type=int, default=0, help="vr layout preference (0 = auto; 15 = COL48)")
     ap.add_argument("--slab", action="store_true", help="COL48 layout + the LDS-slab march (vr_march_slab.hip)")
     ap.add_argument("--opt", action="append", default=[], help="vr option NAME=VALUE (experiments)")
+    ap.add_argument("--inflight", type=int, default=1, choices=[1, 2],
+                    help="N = 1, grid medium: 2 = consecutive frames alternate two streams and targets (throughput "
+                         "mode; per-launch kernel times then overlap the next frame)")
     ap.add_argument("--spin", action="store_true",
                     help="moving camera: every frame gets new shader data, phi += 1.6 deg (the reference's "
                          "held A/D key, TestMain.cpp:171-184, :222-224), queued natively (vr_render_sequence "
@@ -324,7 +327,7 @@ def main() -> int:
     march = vr.march_defaults(max_steps=S)
     r.set_march(march)
     fmt = vr.FMT_RGBA8_UNORM
-    sharder = vrdist.BandSharder(r, W, H, fmt, band_rows=16, world=world, rank=rank)
+    sharder = vrdist.BandSharder(r, W, H, fmt, band_rows=16, world=world, rank=rank, inflight=args.inflight)
     stream = torch.cuda.current_stream()
 
     # executed ray-steps per launch (this rank's bands), one untimed pass
@@ -546,7 +549,7 @@ def main() -> int:
                                   else "reference (TestMain.cpp:219-245)"),
                        "kernel": r.kernel_variant + ("_deferred" if proc is not None and shadow > 0
                                                       and r.get_option("shadow_defer") == 1 else ""),
-                       "parallelism": f"bands16x{world}",
+                       "parallelism": f"bands16x{world}" + (", 2 frames in flight" if args.inflight == 2 else ""),
                        "collective": collective_label,
                        "executed_steps_per_frame": frame_steps},
             "executed_steps_per_s": round(frame_steps * args.steps / el, 1),

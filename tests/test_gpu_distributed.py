@@ -311,10 +311,10 @@ def test_render_sequence_spinning(oracle):
 
 
 def test_one_rank_frames_in_flight(oracle):
-    """BandSharder at world 1 (the bench's N = 1 frame loop): grid frames
-    alternate two streams and two targets (two frames in flight); each
-    target's frame equals the oracle's, and the caller's stream waits for
-    both.  The procedural medium keeps one stream (its scratch is the
+    """BandSharder at world 1 with inflight=2 (bench.py --inflight 2): grid
+    frames alternate two streams and two targets (two frames in flight);
+    each target's frame equals the oracle's, and the caller's stream waits
+    for both.  The procedural medium keeps one stream (its scratch is the
     context's): its frames are exact as well."""
     import sys
     sys.path.insert(0, ROOT)
@@ -327,7 +327,7 @@ def test_one_rank_frames_in_flight(oracle):
         osd, gsd = vr.reference_shader_data(W / H, 10.0, 5.0)
         r.set_shader_data(osd, gsd)
         r.set_march(vr.march_defaults())
-        sh = BandSharder(r, W, H, 0)
+        sh = BandSharder(r, W, H, 0, inflight=2)
         obj, glob = vr.shader_data_arrays(osd, gsd)
         ref, _ = oracle.render(vol, obj, glob, oracle.from_params(vr.march_defaults()), W, H, 0)
         for k in (1, 4, 5):
@@ -339,7 +339,7 @@ def test_one_rank_frames_in_flight(oracle):
         r.set_march(m)
         r.set_procedural(shadow_steps=4)
         p = oracle.procedural_from(r.procedural)
-        sh2 = BandSharder(r, W, H, 0)
+        sh2 = BandSharder(r, W, H, 0, inflight=2)
         frame = sh2.run_frames(3)
         torch.cuda.synchronize()
         ref2, _ = oracle.render_procedural(p, obj, glob, oracle.from_params(m), W, H, 0)

@@ -83,8 +83,9 @@ class BandSharder:
     """
 
     def __init__(self, renderer, width: int, height: int, fmt: int, band_rows: int = 16, world: int = 1,
-                 rank: int = 0, group=None):
+                 rank: int = 0, group=None, inflight: int = 1):
         self.r = renderer
+        self.inflight = inflight   # world 1, grid medium: 2 = frames alternate two streams (run_frames)
         self.width, self.height, self.fmt = width, height, fmt
         self.world, self.rank, self.group = world, rank, group
         self.band_rows = band_rows if world > 1 else 0
@@ -157,17 +158,19 @@ class BandSharder:
         parity is reused only after the stream order has retired its last
         reader.  Returns the last frame (rank 0) or band set."""
         proc = getattr(self.r, "procedural", None)
-        if self.world == 1 and hasattr(self.r, "prepare_render") and (proc is None or not proc.enabled):
-            # one rank, grid medium: the frame is the render.  Two frames in
-            # flight here too: consecutive frames alternate between two
-            # streams and two targets, so frame i+1's waves fill the SIMDs
-            # while frame i's last, longest rays finish (7 % more frames/s at
-            # config 5, profiles/r04/inflight_ab.txt).  The grid render's only
-            # shared state is the read-only region lists; the procedural
-            # medium's cost-sort and shadow scratch belong to the context and
-            # serve one frame at a time, so it keeps one stream (below).
-            # Both streams start after the caller's stream and the caller's
-            # stream waits for both.  The launchers are prepared once.
+        if (self.world == 1 and self.inflight == 2 and hasattr(self.r, "prepare_render") and
+                (proc is None or not proc.enabled)):
+            # one rank, grid medium, inflight 2 (throughput mode): consecutive
+            # frames alternate between two streams and two targets, so frame
+            # i+1's waves fill the SIMDs while frame i's last, longest rays
+            # finish (3-7 % more frames/s at config 5,
+            # profiles/r04/inflight_ab.txt; each launch then overlaps the next,
+            # so per-launch kernel times no longer measure one frame, and the
+            # default stays one stream).  The grid render's only shared state
+            # is the read-only region lists; the procedural medium's cost-sort
+            # and shadow scratch belong to the context and serve one frame at a
+            # time, so it keeps one stream (below).  Both streams start after
+            # the caller's stream and the caller's stream waits for both.
             if getattr(self, "_launch2", None) is None:
                 self._streams2 = [torch.cuda.Stream(self.local.device), torch.cuda.Stream(self.local.device)]
                 self._targets2 = [self.local, torch.empty_like(self.local)]
@@ -189,7 +192,7 @@ class BandSharder:
             self.frame_buf = self._targets2[(k - 1) % 2] if k > 0 else self.frame_buf
             return self.frame_buf
         if self.world == 1 and hasattr(self.r, "prepare_render"):
-            # one rank, procedural medium: one stream, a prepared launcher
+            # one rank: one stream, a prepared launcher (ctypes arguments built once)
             if getattr(self, "_launch1", None) is None:
                 self._launch1 = self.r.prepare_render(self.width, self.height, self.fmt, self.local)
             for i in range(k):
