@@ -70,8 +70,9 @@ __host__ __device__ constexpr bool is_b4_family(int l)
 
 // Variants measured slower than the defaults and kept as the record of that
 // (DESIGN.md sec. 4, 5.1-5.4): the layouts other than the auto ones, the
-// queue / strided / XCD-row schedules, split_long, 8- and 16-wave workgroups,
-// the LDS slab, and the procedural sort_reuse / proc_enum options.  They are
+// queue / strided / XCD-row schedules, 8- and 16-wave workgroups, the LDS
+// slab, the latency-mode march (lat), ray segments (segment), and the
+// procedural sort_reuse / proc_enum options.  They are
 // compiled only with VR_EXPERIMENTS=1 (make EXPERIMENTS=1); the default
 // library refuses their options.
 #ifndef VR_EXPERIMENTS
