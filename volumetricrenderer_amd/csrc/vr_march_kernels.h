@@ -1766,8 +1766,15 @@ constexpr int kScanThreads = 1024;
     for (unsigned k = lane; k * 64u < n; k += 64u) d.map[c0 + k] = make_uint4(e0 + k * 64u, 0u, min(64u, n - k * 64u), 0u);
 }
 
+#ifndef VR_SHADOW_ATTR
+#ifdef VR_SHADOW_WAVES   // timing experiments: the shadow pass built for this many waves per SIMD
+#define VR_SHADOW_ATTR __attribute__((amdgpu_waves_per_eu(VR_SHADOW_WAVES)))
+#else
+#define VR_SHADOW_ATTR
+#endif
+#endif
 template <int TABLE, bool WC>
-__global__ __launch_bounds__(kThreads) void proc_shadow_eval(const MarchArgs a, ShadowDefer d)
+__global__ __launch_bounds__(kThreads) VR_SHADOW_ATTR void proc_shadow_eval(const MarchArgs a, ShadowDefer d)
 {
     noise::WorleyCube wc;   // WC: the lane's Worley cube, kept across its samples (and entries)
     extern __shared__ float4 wt_lds[];
