@@ -279,6 +279,9 @@ def main() -> int:
     ap.add_argument("--inflight", type=int, default=1, choices=[1, 2],
                     help="N = 1, grid medium: 2 = consecutive frames alternate two streams and targets (throughput "
                          "mode; per-launch kernel times then overlap the next frame)")
+    ap.add_argument("--render-streams", type=int, default=2, choices=[1, 2],
+                    help="N > 1 (native loop): 2 = consecutive frames render on two alternating streams and overlap "
+                         "(vr_shard_set_render_streams; the default), 1 = one render stream")
     ap.add_argument("--spin", action="store_true",
                     help="moving camera: every frame gets new shader data, phi += 1.6 deg (the reference's "
                          "held A/D key, TestMain.cpp:171-184, :222-224), queued natively (vr_render_sequence "
@@ -366,7 +369,8 @@ def main() -> int:
         # rank fails (RcclBandPipeline agrees on success before the collective
         # communicator init) and the bench exits non-zero.
         try:
-            pipe = vrdist.RcclBandPipeline(r, W, H, fmt, band_rows=16, world=world, rank=rank)
+            pipe = vrdist.RcclBandPipeline(r, W, H, fmt, band_rows=16, world=world, rank=rank,
+                                           render_streams=args.render_streams)
         except vr.VRError as e:
             print(f"rank {rank}: native RCCL frame loop unavailable: {e}", file=sys.stderr, flush=True)
             raise SystemExit(3)
@@ -472,14 +476,39 @@ def main() -> int:
                       "value": round(W * H * S * args.steps / el2 / 1e6, 3)}
         r.set_option("uniform_skip", 1)
         assert r.kernel_variant == skipped_variant
+    # The same K frames with two in flight (consecutive frames on two
+    # alternating streams and targets, the reference's 2 frames in flight,
+    # VulkanRenderer.cpp:13), timed after the main window under the same clock
+    # (N = 1).  Launches then overlap, so their durations no longer measure a
+    # frame: the headline keeps one stream, whose per-launch time the roofline
+    # and the rocprof profile use.
+    inflight2 = None
+    if world == 1 and not native and not args.spin and proc is None and args.inflight == 1:
+        sh2 = vrdist.BandSharder(r, W, H, fmt, band_rows=16, world=1, rank=0, inflight=2)
+        sh2.run_frames(args.warmup)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        sh2.run_frames(args.steps)
+        torch.cuda.synchronize()
+        el3 = time.perf_counter() - t1
+        inflight2 = {"ms_per_step": round(el3 / args.steps * 1e3, 4),
+                     "value": round(W * H * S * args.steps / el3 / 1e6, 3),
+                     "def": "the same frames, consecutive frames alternating two streams and two targets "
+                            "(bench.py --inflight 2), wall time per frame"}
+        sh2.close()
     # the other BASELINE configs, timed in this process after the headline
     # window (N = 1 only; a multi-GPU run keeps to the headline)
     others, other_cpu = {}, {}
     if world == 1 and not native and not args.spin and args.config == "grid512" and not args.no_other_configs:
         for name in ("grid4k", "cloud", "cloud_shadow"):
             others[name], other_cpu[name] = other_config(name, args.steps, args.warmup)
-    # the measured HBM roofline of this box: a 16-B-per-lane streaming copy
-    copy_best, copy_med = (r.measure_copy_bandwidth(2 << 30, 10) if rank == 0 else (None, None))
+    # the measured HBM roofline of this box: one-pass 16-B-per-lane streams of
+    # 2 GiB (past the 256 MiB Infinity Cache), read-only and copy, 4 / 8 / 16
+    # loads in flight per lane; the larger rate is the denominator
+    bw = {}
+    if rank == 0:
+        for kind in ("read", "copy"):
+            bw[kind] = r.measure_bandwidth(kind, 0, 2 << 30, 10)
     tt = torch.tensor([el, kern_ms], dtype=torch.float64, device=red_dev)
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -498,13 +527,27 @@ def main() -> int:
         ms_per_step = el / args.steps * 1e3
         value = W * H * S * args.steps / el / 1e6
         variant = r.kernel_variant
-        roofline = roofline_of(r, proc, shadow, variant, local_steps, local_evals, local_cells, kern_ms)
+        # two render streams (native loop, N > 1): a launch overlaps the next, so
+        # its duration is not a frame's -- the roofline takes the wall time per frame
+        overlap = native and args.render_streams == 2
+        roof_ms = ms_per_step if overlap else kern_ms
+        roofline = roofline_of(r, proc, shadow, variant, local_steps, local_evals, local_cells, roof_ms)
+        if overlap:
+            roofline["achieved_def"] += ("; renders overlap (two render streams, vr_shard_set_render_streams), so "
+                                         "the time is the wall time per frame of the timed window, not a launch's "
+                                         "duration (kernel_ms_mean: the overlapping launches' mean)")
         if roofline["bound"] == "hbm":
-            roofline.update({"peak_measured": round(copy_best, 1),
-                             "frac_measured": round(roofline["achieved"] / copy_best, 4),
-                             "peak_measured_def": "best of 10 timed 16-B-per-lane grid-stride copies of 2 GiB on this "
-                                                  "GPU (vr_measure_copy_bandwidth; read + written bytes / time; "
-                                                  f"median {copy_med:.0f} GB/s)"})
+            pk_kind = max(bw, key=lambda k: bw[k][0])
+            pk = bw[pk_kind][0]
+            roofline.update({"peak_measured": round(pk, 1), "peak_measured_kind": pk_kind,
+                             "frac_measured": round(roofline["achieved"] / pk, 4),
+                             "peak_read": round(bw["read"][0], 1), "peak_copy": round(bw["copy"][0], 1),
+                             "peak_measured_def": "the larger of a read-only stream (loads folded into a register, "
+                                                  "bytes read / time) and a float4 copy (read + written bytes / time): "
+                                                  "best of 10 one-pass 16-B-per-lane sweeps of 2 GiB at each of 4, 8 "
+                                                  "and 16 loads in flight per lane, on this GPU (vr_measure_bandwidth; "
+                                                  + ", ".join(f"{k} best {v[0]:.0f} GB/s at {v[2]} loads per lane, "
+                                                              f"median {v[1]:.0f}" for k, v in bw.items()) + ")"})
         traffic = None
         ta = None
         tfile = os.path.join(ROOT, "profiles", "traffic.json")
@@ -549,7 +592,9 @@ def main() -> int:
                                   else "reference (TestMain.cpp:219-245)"),
                        "kernel": r.kernel_variant + ("_deferred" if proc is not None and shadow > 0
                                                       and r.get_option("shadow_defer") == 1 else ""),
-                       "parallelism": f"bands16x{world}" + (", 2 frames in flight" if args.inflight == 2 else ""),
+                       "parallelism": f"bands16x{world}" + (", 2 frames in flight" if args.inflight == 2 else "")
+                                      + (f", {args.render_streams} render stream{'s' if args.render_streams > 1 else ''}"
+                                         if native else ""),
                        "collective": collective_label,
                        "executed_steps_per_frame": frame_steps},
             "executed_steps_per_s": round(frame_steps * args.steps / el, 1),
@@ -562,6 +607,7 @@ def main() -> int:
             **({"region_lists": {"gpu_builds": r.get_option("region_gpu_builds"),
                                  "interval": r.get_option("region_interval")}} if args.spin and proc is None else {}),
             **({"all_channels_loaded": all_loaded} if all_loaded else {}),
+            **({"frames_in_flight_2": inflight2} if inflight2 else {}),
             "kernel_ms_mean_max_rank": round(kern_ms_max, 5),
             "roofline": dict(roofline, traffic=traffic,
                              **({"traffic_GBs": round(traffic / (kern_ms * 1e-3) / 1e9, 1),

@@ -359,11 +359,23 @@ vr_status vr_set_layout_preference(void* ctx, int pref);
 vr_status vr_set_option(void* ctx, const char* name, int value);
 int       vr_get_option(void* ctx, const char* name);
 
-/* ---- measurement: the device's streaming-copy bandwidth, the measured HBM
- *      roofline the bench reports next to the 8 TB/s spec.  A float4 (16 B per
- *      lane) grid-stride copy of `bytes` between two fresh device buffers,
- *      `reps` times on `stream`, each timed with HIP events; *gbs_best and
- *      *gbs_median = (read + written bytes) / time, GB/s.  Synchronous.      */
+/* ---- measurement: the device's streaming bandwidth, the measured HBM
+ *      roofline the bench reports next to the 8 TB/s spec.
+ *      vr_measure_bandwidth: one pass of 16 B per lane over `bytes`, the grid
+ *      as large as the buffer, `loads_per_lane` (4, 8 or 16) independent loads
+ *      in flight per lane, 0 = each of 4, 8, 16 (the best is reported), `reps`
+ *      times on `stream`, each timed with HIP events.
+ *        kind VR_BW_COPY: float4 copy between two fresh buffers; bytes moved
+ *                         = read + written (2 x bytes);
+ *        kind VR_BW_READ: loads only, folded into a register, nothing stored;
+ *                         bytes moved = bytes (the ray march is ~98 % reads).
+ *      *gbs_best and *gbs_median in GB/s; *loads_best (may be NULL) = the
+ *      loads per lane of the best rep.  Synchronous.
+ *      vr_measure_copy_bandwidth = kind VR_BW_COPY at 4 loads per lane.     */
+#define VR_BW_COPY 0
+#define VR_BW_READ 1
+vr_status vr_measure_bandwidth(void* ctx, int kind, int loads_per_lane, size_t bytes, int reps, void* stream,
+                               double* gbs_best, double* gbs_median, int* loads_best);
 vr_status vr_measure_copy_bandwidth(void* ctx, size_t bytes, int reps, void* stream, double* gbs_best,
                                     double* gbs_median);
 

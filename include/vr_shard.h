@@ -67,12 +67,16 @@ vr_status vr_shard_connect(vr_shard* sh, const uint8_t id[VR_SHARD_ID_BYTES]);
 vr_status vr_shard_destroy(vr_shard* sh);
 
 /* Render `frames` frames (collective: every rank, same count), 2 in flight.
- * Asynchronous on `stream` (this rank's render stream): when it returns,
- * the work is queued and `stream` is ordered after the last frame's exchange
- * (and, on rank 0, its assembly).  If kernel_ms is not null, every
- * `sample_every`-th render is bracketed by HIP events on `stream` and their
- * mean duration is written there (this call then waits for that last
- * sample). */
+ * Asynchronous on `stream`: the frames start after the work queued on it,
+ * and when the call returns the work is queued and `stream` is ordered after
+ * the last frame's exchange (and, on rank 0, its assembly).  By default the
+ * renders alternate between two streams of the shard, one per buffer parity
+ * (vr_shard_set_render_streams): frame i+1's render waits only for frame
+ * i-1's exchange, never for frame i's render, so consecutive renders overlap.
+ * If kernel_ms is not null, every `sample_every`-th render is bracketed by
+ * HIP events on its render stream and their mean duration is written there
+ * (this call then waits for that last sample; overlapping renders make it
+ * longer than the frame period). */
 vr_status vr_shard_run(vr_shard* sh, int frames, void* stream, int sample_every, float* kernel_ms);
 /* vr_shard_run with a moving camera (the reference's held A/D/W/S key,
  * TestMain.cpp:171-184, and its per-frame UBO updates, :219-249): frame i
@@ -125,6 +129,18 @@ vr_status vr_shard_rows(vr_shard* sh, int* my_rows, int* rows_per_rank);
  * instead of waiting forever.  Every later collective on the shard fails at
  * once (vr_shard_aborted = 1); vr_shard_destroy still frees it. */
 vr_status vr_shard_set_timeout(vr_shard* sh, double seconds);
+/* Render streams of vr_shard_run: 2 (the default) = two streams of the shard,
+ * alternating by buffer parity, renders of consecutive frames overlap;
+ * 1 = every render on the caller's stream, after the previous one.  Results
+ * are identical.  Switching waits (host) for the frames in flight. */
+vr_status vr_shard_set_render_streams(vr_shard* sh, int n);
+int       vr_shard_get_render_streams(vr_shard* sh);
+/* Per-rank rehearsal on one GPU (an unconnected shard, any rank): 1 = each
+ * frame renders only this rank's band set, on the same streams and buffers
+ * as the N-rank loop, with no exchange (rank 0 still assembles, from its own
+ * set and whatever the other slots hold).  The frame period and host cost of
+ * one rank without its peers (tools/band_scaling.py --native). */
+vr_status vr_shard_set_solo(vr_shard* sh, int on);
 int       vr_shard_aborted(vr_shard* sh);
 /* Self-test of the deadline loop on the host (no GPU, no RCCL): mode 0 a
  * state that completes after 5 polls, 1 one that fails at the 3rd, 2 one that

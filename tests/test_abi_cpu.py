@@ -32,7 +32,7 @@ def test_shard_library_exports_every_declared_symbol():
     from volumetricrenderer_amd import _lib
     lib = _lib.load_shard()
     declared = header_functions("vr_shard.h")
-    assert len(declared) == 16
+    assert len(declared) == 19
     for name in declared:
         assert hasattr(lib, name), name
     assert sorted(declared) == _lib.shard_exported_symbols()
@@ -40,6 +40,12 @@ def test_shard_library_exports_every_declared_symbol():
         _lib.shard_call("vr_shard_create", None, None, 1, 0, 64, 64, 1, 16, ctypes.byref(ctypes.c_void_p()))
     with pytest.raises(_lib.VRError):   # argument check only, no GPU
         _lib.shard_call("vr_shard_share_volume", None, None, 8, 8, 8, None)
+    for bad in (0, 3):   # render streams: 1 or 2
+        with pytest.raises(_lib.VRError):
+            _lib.shard_call("vr_shard_set_render_streams", None, bad)
+    with pytest.raises(_lib.VRError):
+        _lib.shard_call("vr_shard_set_solo", None, 1)
+    assert _lib.shard_call("vr_shard_get_render_streams", None) == 0
 
 
 def test_shard_deadline_loop_selftest():

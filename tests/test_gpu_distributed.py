@@ -177,13 +177,15 @@ def test_rccl_init_deadline_when_a_peer_never_joins():
             _lib.shard_call("vr_shard_destroy", h)
 
 
+@pytest.mark.parametrize("render_streams", [1, 2])
 @pytest.mark.parametrize("world,band_rows,fmt,W", [(2, 16, 1, 500), (3, 16, 0, 500), (8, 16, 1, 500), (5, 7, 1, 500),
                                                    (3, 16, 2, 499), (4, 16, 0, 499)])
-def test_native_pipeline_loopback_ranks(world, band_rows, fmt, W):
+def test_native_pipeline_loopback_ranks(world, band_rows, fmt, W, render_streams):
     """The native frame loop's N-rank data layout (grey band sets in gather
     slots of rank 0's row count, expanded by vr_assemble_frame) with every
     rank's bands rendered by this one process: the frame equals a plain
-    render.  Width 499 takes the per-pixel expansion, 500 the 4-pixel one."""
+    render.  Width 499 takes the per-pixel expansion, 500 the 4-pixel one.
+    With 1 render stream and with 2 (consecutive frames overlap)."""
     import sys
     sys.path.insert(0, ROOT)
     import volumetricrenderer_amd as vr
@@ -194,8 +196,10 @@ def test_native_pipeline_loopback_ranks(world, band_rows, fmt, W):
         osd, gsd = vr.reference_shader_data(W / H, -30.0, 40.0)
         r.set_shader_data(osd, gsd)
         r.set_march(vr.march_defaults())
-        pl = RcclBandPipeline(r, W, H, fmt, band_rows=band_rows, world=world, rank=0, loopback=True)
+        pl = RcclBandPipeline(r, W, H, fmt, band_rows=band_rows, world=world, rank=0, loopback=True,
+                              render_streams=render_streams)
         try:
+            assert pl.render_streams == render_streams
             assert pl.rows_per_rank == vr.band_rows_packed(H, band_rows, world, 0)
             pl.run_frames(3)
             pl.barrier()   # loopback: a stream synchronisation
@@ -250,13 +254,14 @@ def test_native_share_volume(world, loopback):
 SPIN_DEG = 1.6   # TestMain.cpp:171-184, :222-224: the held A/D key, 100 deg/s x 0.016 s
 
 
-@pytest.mark.parametrize("fmt", [0, 1])
-def test_native_loopback_spinning_8_ranks(oracle, fmt):
+@pytest.mark.parametrize("fmt,render_streams", [(0, 2), (1, 2), (1, 1)])
+def test_native_loopback_spinning_8_ranks(oracle, fmt, render_streams):
     """A moving camera through the native 8-rank frame loop (loopback: this
     process renders every rank's interleaved band set): 40 frames, frame i
     with its own shader data (vr_shard_run_frames, phi += 1.6 deg), 2 in
-    flight.  Frames 1, 33 and 40, assembled on rank 0, equal the oracle's
-    whole frame bit for bit (RGBA32F and RGBA8)."""
+    flight, on two alternating render streams (the default) or one.  Frames
+    1, 33 and 40, assembled on rank 0, equal the oracle's whole frame bit for
+    bit (RGBA32F and RGBA8)."""
     import sys
     sys.path.insert(0, ROOT)
     import volumetricrenderer_amd as vr
@@ -268,7 +273,8 @@ def test_native_loopback_spinning_8_ranks(oracle, fmt):
         cams = [vr.reference_shader_data(W / H, SPIN_DEG * i, 0.0) for i in range(1, 41)]
         r.set_shader_data(*cams[0])
         r.set_march(vr.march_defaults())
-        pl = RcclBandPipeline(r, W, H, fmt, band_rows=16, world=8, rank=0, loopback=True)
+        pl = RcclBandPipeline(r, W, H, fmt, band_rows=16, world=8, rank=0, loopback=True,
+                              render_streams=render_streams)
         got, done = {}, 0
         try:
             for stop in (1, 33, 40):
@@ -283,6 +289,54 @@ def test_native_loopback_spinning_8_ranks(oracle, fmt):
         obj, glob = vr.shader_data_arrays(*cams[i - 1])
         ref, _ = oracle.render(vol, obj, glob, oracle.from_params(vr.march_defaults()), W, H, fmt)
         assert np.array_equal(img.cpu().numpy(), ref), i
+
+
+def band_set_of(frame, rank, world, band_rows):
+    """The packed rows of `rank`'s interleaved bands in a whole frame (vr.h)."""
+    H = frame.shape[0]
+    rows = [y for b in range(rank, (H + band_rows - 1) // band_rows, world)
+            for y in range(b * band_rows, min(H, (b + 1) * band_rows))]
+    return frame[rows]
+
+
+@pytest.mark.parametrize("render_streams,interval", [(2, 3), (2, 32), (1, 3)])
+def test_native_solo_rank_spinning(oracle, render_streams, interval):
+    """One rank of a 4-rank frame loop rehearsed alone (vr_shard_set_solo:
+    its band set only, no exchange) with a moving camera: 24 frames with their
+    own shader data on two alternating render streams, the region lists
+    rebuilt on the GPU every `interval` renders while the previous frame is
+    still in flight on the other stream (per-stream retire events).  The band
+    set of frames 1, 7, 20 and 24 equals the rows of the oracle's frame."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import volumetricrenderer_amd as vr
+    from volumetricrenderer_amd.distributed import RcclBandPipeline
+    W, H, world, rank = 320, 180, 4, 2
+    vol = oracle.build_volume(128)
+    with vr.Renderer(0) as r:
+        r.set_volume(vol)
+        r.set_option("region_interval", interval)
+        cams = [vr.reference_shader_data(W / H, SPIN_DEG * i, 0.5 * i) for i in range(1, 25)]
+        r.set_shader_data(*cams[0])
+        r.set_march(vr.march_defaults())
+        pl = RcclBandPipeline(r, W, H, 1, band_rows=16, world=world, rank=rank, loopback=True, solo=True,
+                              render_streams=render_streams)
+        got, done = {}, 0
+        try:
+            for stop in (1, 7, 20, 24):
+                pl.run_frames(stop - done, cameras=cams[done:stop])
+                done = stop
+                got[stop] = pl.frame()
+            torch.cuda.synchronize()
+            builds = r.get_option("region_gpu_builds")
+        finally:
+            pl.close()
+    assert builds >= (24 // interval) - 1, builds
+    for i, img in got.items():
+        obj, glob = vr.shader_data_arrays(*cams[i - 1])
+        ref, _ = oracle.render(vol, obj, glob, oracle.from_params(vr.march_defaults()), W, H, 1)
+        want = band_set_of(ref, rank, world, 16)[..., 0]
+        assert img.shape == want.shape and np.array_equal(img.cpu().numpy(), want), i
 
 
 def test_render_sequence_spinning(oracle):
@@ -345,3 +399,44 @@ def test_one_rank_frames_in_flight(oracle):
         ref2, _ = oracle.render_procedural(p, obj, glob, oracle.from_params(m), W, H, 0)
         assert np.array_equal(frame.cpu().numpy(), ref2)
         assert getattr(sh2, "_launch2", None) is None
+
+
+def test_frames_in_flight_then_one_stream_paths(oracle):
+    """after an inflight=2 run of an even number of frames, the
+    one-stream paths of the SAME sharder -- frame() and a procedural
+    run_frames -- must return what they just rendered, not the other
+    in-flight target.  Each path's frame is checked against the oracle after
+    the camera changed, so a stale buffer shows."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import volumetricrenderer_amd as vr
+    from volumetricrenderer_amd.distributed import BandSharder
+    W, H = 320, 180
+    vol = oracle.build_volume(96)
+    cams = [vr.reference_shader_data(W / H, a, 5.0) for a in (10.0, 40.0, 70.0)]
+    with vr.Renderer(0) as r:
+        r.set_volume(vol)
+        r.set_march(vr.march_defaults())
+        sh = BandSharder(r, W, H, 0, inflight=2)
+
+        def ref(c):
+            obj, glob = vr.shader_data_arrays(*c)
+            return oracle.render(vol, obj, glob, oracle.from_params(vr.march_defaults()), W, H, 0)[0]
+        r.set_shader_data(*cams[0])
+        f = sh.run_frames(4)
+        torch.cuda.current_stream().synchronize()
+        assert np.array_equal(f.cpu().numpy(), ref(cams[0]))
+        r.set_shader_data(*cams[1])
+        f = sh.frame()
+        torch.cuda.synchronize()
+        assert np.array_equal(f.cpu().numpy(), ref(cams[1]))
+        m = vr.march_defaults(max_steps=32)
+        r.set_march(m)
+        r.set_procedural(shadow_steps=0)
+        r.set_shader_data(*cams[2])
+        f = sh.run_frames(2)
+        torch.cuda.synchronize()
+        obj, glob = vr.shader_data_arrays(*cams[2])
+        want, _ = oracle.render_procedural(oracle.procedural_from(r.procedural), obj, glob, oracle.from_params(m),
+                                           W, H, 0)
+        assert np.array_equal(f.cpu().numpy(), want)

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-3 final evidence in one call: the whole GPU suite, smoke(), then
-# tools/r03_round.sh (PMC traffic of the default kernel, bench + rocprofv3 per
+# tools/archive/r03_round.sh (PMC traffic of the default kernel, bench + rocprofv3 per
 # config, spinning-camera lines).
 set -u
 OUT=$GRAFT_REPO_ROOT/gpurun_out; mkdir -p $OUT; export TMPDIR=/tmp
@@ -8,4 +8,4 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 tail -1 $OUT/pytest_gpu_final.log
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo "smoke fail"; tail -20 $OUT/smoke.log; exit 2; }
 tail -2 $OUT/smoke.log
-bash tools/r03_round.sh
+bash tools/archive/r03_round.sh

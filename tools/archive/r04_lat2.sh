@@ -10,4 +10,4 @@ timeout -k 10 300 python -u tools/band_scaling.py --all-ranks --variants="$V" > 
 grep "rank-0" gpurun_out/r04_lat_c5.txt
 timeout -k 10 300 python -u tools/band_scaling.py --all-ranks --size 128 --width 3840 --height 2160 --steps 256 --variants="$V" > gpurun_out/r04_lat_c4.txt 2>&1 || { tail gpurun_out/r04_lat_c4.txt; exit 1; }
 grep "rank-0" gpurun_out/r04_lat_c4.txt
-bash tools/r04_abort.sh
+bash tools/archive/r04_abort.sh

@@ -3,6 +3,14 @@ set (16-row bands, stride N) for N = 1, 2, 4, 8, against the whole frame / N.
 What a rank of bench.py --gpus N renders per frame, without the exchange.
 
     python tools/band_scaling.py [--size 512] [--config grid512] [--tpw 0] [--schedule -1]
+
+--native: the frame STREAM of each rank instead of one launch -- the native
+frame loop (libvr_shard, vr_shard_run_frames) in its solo rehearsal
+(vr_shard_set_solo: this rank's band set only, no exchange), `--frames`
+frames queued at once, timed with events on the caller's stream from before
+the first render to after the last; ms per frame and the loop's host ms per
+frame, with 1 and 2 render streams (vr_shard_set_render_streams), `--rounds`
+interleaved rounds.
 """
 import argparse
 import os
@@ -27,7 +35,12 @@ def main():
     ap.add_argument("--ns", default="1,2,4,8")
     ap.add_argument("--band-rows", type=int, default=16)
     ap.add_argument("--all-ranks", action="store_true", help="time every rank's band set, report the slowest")
+    ap.add_argument("--native", action="store_true", help="per-rank frame streams through the native loop (solo)")
+    ap.add_argument("--streams", default="1,2", help="--native: render streams to compare")
+    ap.add_argument("--rounds", type=int, default=3, help="--native: interleaved rounds")
     a = ap.parse_args()
+    if a.native:
+        return native(a)
     W, H = a.width, a.height
     with vr.Renderer(0) as r:
         r.generate_volume(vr.scaled_recipe(a.size))
@@ -73,6 +86,62 @@ def main():
                 base = base or t
                 print(f"{' '.join(a.opt)} schedule {sched} tpw {tpw} split {split} wedges {wedges} lat {lat} seg {seg} N={n}: rank-0 bands {t:.4f} ms, whole/N {base / n:.4f} ms, "
                       f"efficiency {base / n / t:.2f}", flush=True)
+
+
+def native(a):
+    """Per-rank frame streams of the native loop (solo rehearsal), 1 vs 2 render streams."""
+    from volumetricrenderer_amd.distributed import RcclBandPipeline
+    W, H = a.width, a.height
+    with vr.Renderer(0) as r:
+        r.generate_volume(vr.scaled_recipe(a.size))
+        osd, gsd = vr.reference_shader_data(1280 / 720)
+        r.set_shader_data(osd, gsd)
+        r.set_march(vr.march_defaults(max_steps=a.steps))
+        for o in a.opt:
+            k, v = o.split("=")
+            r.set_option(k, int(v))
+        print(f"native frame streams: {a.size}^3, {W}x{H}x{a.steps}, {a.frames} frames per timing, "
+              f"variant {r.kernel_variant} {' '.join(a.opt)}", flush=True)
+        streams = [int(v) for v in a.streams.split(",")]
+        base = {}
+        for n in [int(v) for v in a.ns.split(",")]:
+            res = {ns: [] for ns in streams}   # per stream count: per round, the slowest rank's ms/frame
+            host = {ns: [] for ns in streams}
+            pipes = {}
+            for first in (range(n) if a.all_ranks else (0,)):
+                for ns in streams:
+                    p = RcclBandPipeline(r, W, H, vr.FMT_RGBA8_UNORM, band_rows=a.band_rows, world=n, rank=first,
+                                         loopback=True, solo=True, render_streams=ns)
+                    p.run_frames(8)   # region lists, code objects
+                    p.barrier()
+                    pipes[(first, ns)] = p
+            for _ in range(a.rounds):
+                for ns in streams:
+                    worst, hmax = 0.0, 0.0
+                    for first in (range(n) if a.all_ranks else (0,)):
+                        p = pipes[(first, ns)]
+                        p.run_frames(4)
+                        p.barrier()
+                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        e0.record()
+                        p.run_frames(a.frames)
+                        e1.record()
+                        torch.cuda.synchronize()
+                        worst = max(worst, e0.elapsed_time(e1) / a.frames)
+                        hmax = max(hmax, p.host_ms)
+                    res[ns].append(worst)
+                    host[ns].append(hmax)
+            for p in pipes.values():
+                p.close()
+            for ns in streams:
+                t = float(np.median(res[ns]))
+                if n == 1:
+                    base[ns] = t
+                b = base.get(ns)
+                eff = f", efficiency {b / n / t:.2f} (vs N=1, same streams)" if b else ""
+                print(f"N={n} render_streams {ns}: slowest rank {t:.4f} ms/frame (rounds "
+                      + " ".join(f"{v:.4f}" for v in res[ns]) + f"), host {max(host[ns]):.4f} ms/frame{eff}",
+                      flush=True)
 
 
 if __name__ == "__main__":

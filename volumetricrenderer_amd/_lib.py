@@ -134,6 +134,9 @@ _SIGS = {
     "vr_get_option": (ctypes.c_int, [_vp, ctypes.c_char_p]),
     "vr_measure_copy_bandwidth": (ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.c_int, _vp,
                                                  ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
+    "vr_measure_bandwidth": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int, _vp,
+                                            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                            ctypes.POINTER(ctypes.c_int)]),
 }
 # functions whose int return is a value, not a vr_status
 _VALUE_RETURNS = {"vr_abi_version", "vr_band_rows_packed", "vr_get_option", "vr_volume_extent_ok"}
@@ -203,10 +206,13 @@ _SHARD_SIGS = {
     "vr_shard_share_volume": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp]),
     "vr_shard_set_timeout": (ctypes.c_int, [_vp, ctypes.c_double]),
     "vr_shard_aborted": (ctypes.c_int, [_vp]),
+    "vr_shard_set_render_streams": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "vr_shard_get_render_streams": (ctypes.c_int, [_vp]),
+    "vr_shard_set_solo": (ctypes.c_int, [_vp, ctypes.c_int]),
     "vr_shard_poll_selftest": (ctypes.c_int, [ctypes.c_int, ctypes.c_double, c_int_p]),
 }
 # shard functions whose int return is a value, not a vr_status
-_SHARD_VALUE_RETURNS = {"vr_shard_aborted", "vr_shard_poll_selftest"}
+_SHARD_VALUE_RETURNS = {"vr_shard_aborted", "vr_shard_poll_selftest", "vr_shard_get_render_streams"}
 _shard_lib = None
 
 

@@ -125,6 +125,12 @@ struct Ctx {
     unsigned defer_entries = 0;    // option "shadow_defer_entries": entry capacity override (tests; 0 = sized from the frame)
     int defer_last = 0;            // the last procedural render ran the deferred passes
     std::vector<void*> defer_retired;   // outgrown scratch buffers: queued frames may still use them
+    // the procedural scratch (d_sort, d_defer, d_lat) serves one frame at a
+    // time: a procedural render on another stream than the last one waits
+    // for it (frames in flight on alternating streams, vr_shard.cpp)
+    hipEvent_t proc_ev = nullptr;
+    hipStream_t proc_stream = nullptr;
+    bool proc_pending = false;
     unsigned long long* h_need = nullptr;   // host-mapped [entries, records] written by the last sorting frame
     unsigned long long* d_need = nullptr;   // its device address
     hipEvent_t need_ev = nullptr;
@@ -166,20 +172,26 @@ struct Ctx {
         int seg_len = 0;           // segments: steps per segment the lists were built for (0 = none)
         int nseg_tiles = 0;        // segmented tiles (slots of SegArgs.info)
         int icap = 0;              // info entries before the list
-        // the streams that rendered with these lists.  When the lists are
-        // retired by a render on their only stream, an event is recorded on
-        // it and the buffer is rewritten only after that event; lists that
-        // another stream used retire with a device sync instead: an event is
-        // never recorded on a remembered stream, which the caller may have
-        // destroyed since (kMaxRegionStreams; more -> device sync too)
+        // the streams that rendered with these lists, and per stream an event
+        // that follows its last render with them.  One stream: the event is
+        // recorded when the lists are retired by a render on it.  Several
+        // streams (frames in flight on alternating streams, vr_shard.cpp): each
+        // render records its stream's event, so a retire waits for every
+        // stream's last render without a host sync.  An event is never
+        // recorded on a remembered stream, which the caller may have destroyed
+        // since: a stream whose last render has no event, other than the
+        // retiring one, retires with a device sync (kMaxRegionStreams; more ->
+        // device sync too).
         hipStream_t streams[kMaxRegionStreams] = {};
-        hipEvent_t used = nullptr;
+        hipEvent_t used[kMaxRegionStreams] = {};
+        bool evented[kMaxRegionStreams] = {};   // used[i] follows stream i's last render
         int nstreams = 0;          // -1: more streams than tracked
-        int nretired = 0;          // 1: `used` marks the end of the renders before the lists were retired
+        int nretired = 0;          // used[0 .. nretired) mark the end of the renders before the lists were retired
         hipEvent_t uploaded = nullptr;   // the list upload (on streams[0]); other streams wait for it
         hipStream_t upload_stream = nullptr;
     } region[2];
     int region_cur = -1;           // buffer of the current lists (-1 = none)
+    int region_slot = -1;          // the last render stream's slot in them (note_region_stream)
     float region_key[kRegionKeyLen] = {};   // geometry the current lists were built for
     long long renders_since_build = 0;
     // procedural cost sort: the geometry whose order d_sort holds (n per pixel
@@ -549,6 +561,7 @@ vr_status vr_destroy(void* p)
     if (c->d_rg) (void)hipFree(c->d_rg);
     if (c->h_rghdr) (void)hipHostFree(c->h_rghdr);
     if (c->rg_ev) (void)hipEventDestroy(c->rg_ev);
+    if (c->proc_ev) (void)hipEventDestroy(c->proc_ev);
     if (c->d_terms) (void)hipFree(c->d_terms);
     if (c->d_mm) (void)hipFree(c->d_mm);
     if (c->h_mm) (void)hipHostFree(c->h_mm);
@@ -556,7 +569,8 @@ vr_status vr_destroy(void* p)
     for (auto& b : c->region) {
         if (b.d) (void)hipFree(b.d);
         if (b.h) (void)hipHostFree(b.h);
-        if (b.used) (void)hipEventDestroy(b.used);
+        for (hipEvent_t e : b.used)
+            if (e) (void)hipEventDestroy(e);
         if (b.uploaded) (void)hipEventDestroy(b.uploaded);
     }
     delete c;
@@ -672,44 +686,68 @@ vr_status vr_selftest(void* p, const char* name, long long* failures)
     return VR_OK;
 }
 
-vr_status vr_measure_copy_bandwidth(void* p, size_t bytes, int reps, void* stream, double* gbs_best, double* gbs_median)
+vr_status vr_measure_bandwidth(void* p, int kind, int loads_per_lane, size_t bytes, int reps, void* stream,
+                               double* gbs_best, double* gbs_median, int* loads_best)
 {
-    if (!p || !gbs_best || reps <= 0 || bytes < 16) return fail(VR_ERR_INVALID, "vr_measure_copy_bandwidth: bad argument");
+    if (!p || !gbs_best || reps <= 0 || bytes < 16 || (kind != VR_BW_COPY && kind != VR_BW_READ) ||
+        (loads_per_lane != 0 && loads_per_lane != 4 && loads_per_lane != 8 && loads_per_lane != 16))
+        return fail(VR_ERR_INVALID, "vr_measure_bandwidth: bad argument");
     Ctx* c = as_ctx(p);
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t s = static_cast<hipStream_t>(stream);
     bytes &= ~(size_t)15;
+    const std::vector<int> pls = loads_per_lane ? std::vector<int>{loads_per_lane} : std::vector<int>{4, 8, 16};
+    const size_t dst_bytes = kind == VR_BW_COPY ? bytes : 1024;   // a read's 1 KiB sink is never written
+    const size_t nev = 2 * (size_t)reps * pls.size();
     void *src = nullptr, *dst = nullptr;
-    std::vector<hipEvent_t> ev(2 * (size_t)reps + 2, nullptr);
+    std::vector<hipEvent_t> ev(nev, nullptr);
     hipError_t e = hipMalloc(&src, bytes);
-    if (e == hipSuccess) e = hipMalloc(&dst, bytes);
+    if (e == hipSuccess) e = hipMalloc(&dst, dst_bytes);
     if (e == hipSuccess) e = hipMemsetAsync(src, 0x5a, bytes, s);
     for (auto& v : ev)
         if (e == hipSuccess) e = hipEventCreate(&v);
-    if (e == hipSuccess) e = launch_stream_copy(src, dst, bytes, s);   // warm-up (page mapping, clocks)
-    for (int i = 0; i < reps && e == hipSuccess; ++i) {
-        e = hipEventRecord(ev[2 * i], s);
-        if (e == hipSuccess) e = launch_stream_copy(src, dst, bytes, s);
-        if (e == hipSuccess) e = hipEventRecord(ev[2 * i + 1], s);
-    }
-    std::vector<double> gbs;
+    // warm-up (page mapping, clocks), then the timed reps, interleaved over the widths
+    for (int pl : pls)
+        if (e == hipSuccess) e = launch_stream_bw(kind, pl, src, dst, bytes, s);
+    for (int i = 0; i < reps && e == hipSuccess; ++i)
+        for (size_t j = 0; j < pls.size() && e == hipSuccess; ++j) {
+            const size_t k = 2 * (i * pls.size() + j);
+            e = hipEventRecord(ev[k], s);
+            if (e == hipSuccess) e = launch_stream_bw(kind, pls[j], src, dst, bytes, s);
+            if (e == hipSuccess) e = hipEventRecord(ev[k + 1], s);
+        }
+    std::vector<std::pair<double, int>> gbs;
     if (e == hipSuccess) e = hipStreamSynchronize(s);
-    for (int i = 0; i < reps && e == hipSuccess; ++i) {
-        float ms = 0.0f;
-        e = hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]);
-        if (e == hipSuccess && ms > 0.0f) gbs.push_back(2.0 * (double)bytes / (ms * 1e-3) / 1e9);
-    }
+    const double moved = (kind == VR_BW_COPY ? 2.0 : 1.0) * (double)bytes;
+    for (int i = 0; i < reps && e == hipSuccess; ++i)
+        for (size_t j = 0; j < pls.size() && e == hipSuccess; ++j) {
+            const size_t k = 2 * (i * pls.size() + j);
+            float ms = 0.0f;
+            e = hipEventElapsedTime(&ms, ev[k], ev[k + 1]);
+            if (e == hipSuccess && ms > 0.0f) gbs.push_back({moved / (ms * 1e-3) / 1e9, pls[j]});
+        }
     for (auto& v : ev)
         if (v) (void)hipEventDestroy(v);
     if (src) (void)hipFree(src);
     if (dst) (void)hipFree(dst);
-    if (e != hipSuccess) return fail(e == hipErrorOutOfMemory ? VR_ERR_OOM : VR_ERR_HIP, "vr_measure_copy_bandwidth: %s",
+    if (e != hipSuccess) return fail(e == hipErrorOutOfMemory ? VR_ERR_OOM : VR_ERR_HIP, "vr_measure_bandwidth: %s",
                                      hipGetErrorString(e));
-    if (gbs.empty()) return fail(VR_ERR_HIP, "vr_measure_copy_bandwidth: no timing");
+    if (gbs.empty()) return fail(VR_ERR_HIP, "vr_measure_bandwidth: no timing");
     std::sort(gbs.begin(), gbs.end());
-    *gbs_best = gbs.back();
-    if (gbs_median) *gbs_median = gbs[gbs.size() / 2];
+    *gbs_best = gbs.back().first;
+    if (loads_best) *loads_best = gbs.back().second;
+    if (gbs_median) {   // the median rep of the best width
+        std::vector<double> w;
+        for (const auto& g : gbs)
+            if (g.second == gbs.back().second) w.push_back(g.first);
+        *gbs_median = w[w.size() / 2];
+    }
     return VR_OK;
+}
+
+vr_status vr_measure_copy_bandwidth(void* p, size_t bytes, int reps, void* stream, double* gbs_best, double* gbs_median)
+{
+    return vr_measure_bandwidth(p, VR_BW_COPY, 4, bytes, reps, stream, gbs_best, gbs_median, nullptr);
 }
 
 vr_status vr_generate_volume(void* p, const vr_volume_recipe* r, void* stream)
@@ -1120,18 +1158,47 @@ static vr_status stream_wait_pending(hipStream_t s, hipEvent_t ev)
     return VR_OK;
 }
 
-// The render stream s uses the lists
-vr_status note_region_stream(Ctx::RegionBuf& rb, hipStream_t s)
+// The render stream s uses the lists: *slot = its index in rb.streams (-1:
+// untracked, more streams than kMaxRegionStreams)
+vr_status note_region_stream(Ctx::RegionBuf& rb, hipStream_t s, int* slot)
 {
+    *slot = -1;
     if (rb.nstreams < 0) return VR_OK;
     for (int i = 0; i < rb.nstreams; ++i)
-        if (rb.streams[i] == s) return VR_OK;
+        if (rb.streams[i] == s) {
+            *slot = i;
+            return VR_OK;
+        }
     if (s != rb.upload_stream) {   // first use on another stream
         const vr_status st = stream_wait_pending(s, rb.uploaded);
         if (st != VR_OK) return st;
     }
-    if (rb.nstreams == kMaxRegionStreams) rb.nstreams = -1;
-    else rb.streams[rb.nstreams++] = s;
+    if (rb.nstreams == kMaxRegionStreams) {
+        rb.nstreams = -1;
+        return VR_OK;
+    }
+    if (!rb.used[rb.nstreams]) HIP_TRY(hipEventCreateWithFlags(&rb.used[rb.nstreams], hipEventDisableTiming));
+    rb.evented[rb.nstreams] = false;
+    *slot = rb.nstreams;
+    rb.streams[rb.nstreams++] = s;
+    return VR_OK;
+}
+
+// After a regions launch on stream s (slot c->region_slot of the current
+// lists): with several streams on the lists, record the stream's event so a
+// retire can wait for it; with one, its last render stays uncovered until
+// the retire records on it
+vr_status note_region_render(Ctx* c, hipStream_t s)
+{
+    if (c->region_cur < 0 || c->region_slot < 0) return VR_OK;
+    Ctx::RegionBuf& rb = c->region[c->region_cur];
+    if (c->region_slot >= rb.nstreams) return VR_OK;
+    if (rb.nstreams >= 2) {
+        HIP_TRY(hipEventRecord(rb.used[c->region_slot], s));
+        rb.evented[c->region_slot] = true;
+    } else {
+        rb.evented[c->region_slot] = false;
+    }
     return VR_OK;
 }
 
@@ -1181,14 +1248,18 @@ static vr_status next_region_buf(Ctx* c, size_t n, bool host_staging, hipStream_
     if (c->region_cur >= 0) {   // retire the current lists in the stream order of their renders
         Ctx::RegionBuf& old = c->region[c->region_cur];
         old.nretired = 0;
-        if (old.nstreams == 1 && old.streams[0] == stream) {   // the usual case: one stream, this one
-            if (!old.used) HIP_TRY(hipEventCreateWithFlags(&old.used, hipEventDisableTiming));
-            HIP_TRY(hipEventRecord(old.used, stream));
-            old.nretired = 1;
-        } else if (old.nstreams != 0) {
+        bool sync = old.nstreams < 0;
+        for (int i = 0; i < old.nstreams && !sync; ++i)
+            if (!old.evented[i] && old.streams[i] != stream) sync = true;   // an uncovered render elsewhere
+        if (sync) {
             HIP_TRY(hipDeviceSynchronize());
+        } else {
+            for (int i = 0; i < old.nstreams; ++i)
+                if (!old.evented[i]) HIP_TRY(hipEventRecord(old.used[i], stream));   // this stream: its order covers them
+            old.nretired = old.nstreams;
         }
         old.nstreams = 0;
+        c->region_slot = -1;
     }
     const int b = c->region_cur < 0 ? 0 : c->region_cur ^ 1;
     Ctx::RegionBuf& rb = c->region[b];
@@ -1196,11 +1267,11 @@ static vr_status next_region_buf(Ctx* c, size_t n, bool host_staging, hipStream_
         HIP_TRY(hipEventSynchronize(c->rg_ev));
         poll_region_header(c);
     }
-    if (rb.nretired) {   // its last renders
+    for (int i = 0; i < rb.nretired; ++i) {   // its last renders, per stream
         if (host_staging || rb.d == nullptr) {
-            HIP_TRY(hipEventSynchronize(rb.used));
+            HIP_TRY(hipEventSynchronize(rb.used[i]));
         } else {
-            const vr_status st = stream_wait_pending(stream, rb.used);
+            const vr_status st = stream_wait_pending(stream, rb.used[i]);
             if (st != VR_OK) return st;
         }
     }
@@ -1236,7 +1307,7 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     poll_region_header(c);
     const bool same_grid = c->region_cur >= 0 && std::memcmp(key, c->region_key, grid_part * sizeof(float)) == 0;
     if (same_grid && (std::memcmp(key, c->region_key, sizeof key) == 0 || c->renders_since_build < c->region_interval))
-        return note_region_stream(c->region[c->region_cur], stream);
+        return note_region_stream(c->region[c->region_cur], stream, &c->region_slot);
 
     const int S = c->supertile;
     // a moved camera over the same target (no segments): the lists come from
@@ -1301,7 +1372,7 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
         rb.nseg_tiles = 0;
         rb.icap = 0;
         rb.nstreams = 0;
-        const vr_status st = note_region_stream(rb, stream);
+        const vr_status st = note_region_stream(rb, stream, &c->region_slot);
         if (st != VR_OK) return st;
         c->region_cur = b;
         std::memcpy(c->region_key, key, sizeof key);
@@ -1462,7 +1533,7 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     rb.nseg_tiles = nslots;
     rb.icap = nslots;
     rb.nstreams = 0;
-    const vr_status st = note_region_stream(rb, stream);
+    const vr_status st = note_region_stream(rb, stream, &c->region_slot);
     if (st != VR_OK) return st;
     c->region_cur = b;
     std::memcpy(c->region_key, key, sizeof key);
@@ -1816,8 +1887,16 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
         std::vector<float> built = reuse == SORT_BUILD ? key : c->sort_key;
         c->sort_key.clear();   // valid again only once this launch is queued
         const bool report = use_defer && reuse == SORT_BUILD;   // proc_scan writes the frame's need
+        if (c->proc_pending && c->proc_stream != static_cast<hipStream_t>(stream)) {
+            const vr_status sw = stream_wait_pending(static_cast<hipStream_t>(stream), c->proc_ev);
+            if (sw != VR_OK) return sw;
+        }
         HIP_TRY(launch_march_procedural(a, m.early_out > 0.0f, sort_buf, reuse, sc, static_cast<hipStream_t>(stream),
                                         use_defer ? &defer : nullptr, report ? c->d_need : nullptr));
+        if (!c->proc_ev) HIP_TRY(hipEventCreateWithFlags(&c->proc_ev, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(c->proc_ev, static_cast<hipStream_t>(stream)));
+        c->proc_stream = static_cast<hipStream_t>(stream);
+        c->proc_pending = true;
         if (report) {
             HIP_TRY(hipEventRecord(c->need_ev, static_cast<hipStream_t>(stream)));
             c->need_pending = true;
@@ -1901,6 +1980,7 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
         }
     }
     HIP_TRY(launch_march(a, pl.layout, pl.wrap, pl.early, sc, static_cast<hipStream_t>(stream)));
+    if (kind == SCHED_REGIONS) return note_region_render(c, static_cast<hipStream_t>(stream));
     return VR_OK;
 }
 

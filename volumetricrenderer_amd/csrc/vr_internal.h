@@ -370,6 +370,9 @@ hipError_t launch_assemble(const uint8_t* d_gathered, size_t rows_per_rank, int 
 int noise_partials_needed(int nx, int ny, int nz);
 // 16-B-per-lane grid-stride copy of `bytes` (a multiple of 16): the measured HBM roofline
 hipError_t launch_stream_copy(const void* src, void* dst, size_t bytes, hipStream_t s);
+// kind 0 = that copy, 1 = a read-only stream (loads folded into a register);
+// loads_per_lane 4, 8 or 16 in flight per lane; dst of a read is a 1 KiB sink
+hipError_t launch_stream_bw(int kind, int loads_per_lane, const void* src, void* dst, size_t bytes, hipStream_t s);
 // variant 0..2 = noise::cell_inv_a..c, 3 = the sequence cellular() uses
 hipError_t launch_selftest_cell_inv(int variant, unsigned long long* d_bad, hipStream_t s);
 // noise::cellular_table9 (pruned) vs noise::cellular on 2^23 points per seed

@@ -2,7 +2,7 @@
 // (libvr_shard.so: libvr + RCCL).  SURVEY.md sec. 8e; DESIGN.md sec. 7.
 //
 // Per frame i (buffers of parity p = i & 1):
-//   render stream:  wait done[p] (frame i-2's exchange / assembly has read
+//   render stream p: wait done[p] (frame i-2's exchange / assembly has read
 //                   the parity-p buffers) -> vr_render of this rank's bands
 //                   (rank 0 renders straight into its gather slot 0)
 //                   -> record rendered[p]
@@ -14,10 +14,15 @@
 // VR_FMT_R8_* / R32F: the pixel is vec4(vec3(c), 1), frag.glsl:79-80), so the
 // exchange moves 1 B (or 4 B) per pixel instead of 4 B (16 B), and rank 0's
 // assembly expands them into the RGBA frame.
-// so frame i's exchange overlaps frame i+1's render (the reference's 2
-// frames in flight, VulkanRenderer.cpp:13).  No host synchronisation in the
-// loop: the host cost per frame is one render launch, one RCCL group and
-// (rank 0) one assembly launch.
+// Two render streams, one per parity (vr_shard_set_render_streams; 1 = the
+// caller's stream renders every frame): frame i+1's render waits only for
+// done[p^1], never for frame i's render, so its waves fill the SIMDs while
+// frame i's longest rays finish, and frame i's exchange overlaps frame i+1's
+// render -- the reference's 2 frames in flight (VulkanRenderer.cpp:13,
+// :142-172).  Each vr_render captures its frame's shader data in its launch
+// arguments, so frames in flight with different cameras stay exact.  No host
+// synchronisation in the loop: the host cost per frame is one render launch,
+// one RCCL group and (rank 0) one assembly launch.
 //
 // Failure handling: the communicator is non-blocking (ncclConfig_t.blocking
 // = 0).  Every host wait on a collective -- the init, the barrier, the volume
@@ -133,6 +138,8 @@ struct vr_shard {
     std::vector<int> rows_of;         // packed rows of every rank
     ncclComm_t comm = nullptr;
     hipStream_t comm_stream = nullptr;
+    hipStream_t render_stream[2] = {};   // one per parity (render_streams == 2)
+    int render_streams = 2;           // 1: every frame renders on the caller's stream
     uint8_t* local[2] = {};           // rank > 0: band sets (gformat)
     uint8_t* gathered[2] = {};        // rank 0: nranks slots of rows_per_rank rows (gformat)
     uint8_t* frame[2] = {};           // rank 0
@@ -143,6 +150,7 @@ struct vr_shard {
     bool pending[2] = {};             // done[p] recorded and not yet waited on
     int last = -1;                    // parity of the last frame
     bool loopback = false;            // one process emulates all ranks (no RCCL)
+    bool solo = false;                // loopback rehearsal of one rank: its own band set only, no exchange
     std::vector<hipEvent_t> timing;   // sampled render brackets (pairs)
     double timeout_s = 120.0;         // deadline of every host wait on a collective
     bool aborted = false;             // the communicator was aborted (error or deadline)
@@ -231,6 +239,8 @@ vr_status check_usable(vr_shard* sh, const char* what)
 
 void release(vr_shard* sh)
 {
+    for (hipStream_t rs : sh->render_stream)
+        if (rs) (void)hipStreamSynchronize(rs);
     if (sh->comm_stream) (void)hipStreamSynchronize(sh->comm_stream);
     for (int p = 0; p < 2; ++p) {
         if (sh->local[p]) (void)hipFree(sh->local[p]);
@@ -244,6 +254,8 @@ void release(vr_shard* sh)
     if (sh->token) (void)hipFree(sh->token);
     if (sh->comm) (void)ncclCommDestroy(sh->comm);   // an aborted communicator is already gone
     if (sh->comm_stream) (void)hipStreamDestroy(sh->comm_stream);
+    for (hipStream_t rs : sh->render_stream)
+        if (rs) (void)hipStreamDestroy(rs);
     delete sh;
 }
 
@@ -265,7 +277,7 @@ vr_status one_frame(vr_shard* sh, int p, hipStream_t s, hipEvent_t t0, hipEvent_
     if (t0) HIP_TRY(hipEventRecord(t0, s));
     if (sh->my_rows > 0) VR_TRY(vr_render(sh->ctx, &t, s));
     if (t1) HIP_TRY(hipEventRecord(t1, s));
-    if (sh->loopback)   // the other ranks' band sets, rendered here into their gather slots
+    if (sh->loopback && !sh->solo)   // the other ranks' band sets, rendered here into their gather slots
         for (int r = 1; r < sh->nranks; ++r) {
             t.band_first = r;
             t.pixels = sh->gathered[p] + (size_t)r * sh->rows_per_rank * sh->gpitch;
@@ -349,6 +361,7 @@ vr_status vr_shard_alloc(void* ctx, int nranks, int rank, int width, int height,
     hip_ok(e, "hipGetDevice");
     sh->device = dev;
     hip_ok(hipStreamCreateWithFlags(&sh->comm_stream, hipStreamNonBlocking), "comm stream");
+    for (hipStream_t& rs : sh->render_stream) hip_ok(hipStreamCreateWithFlags(&rs, hipStreamNonBlocking), "render stream");
     hip_ok(hipEventCreateWithFlags(&sh->fence, hipEventDisableTiming), "event");
     if (hip_ok(hipMalloc(&sh->token, 8 * sizeof(int)), "barrier token"))
         hip_ok(hipMemset(sh->token, 0, 8 * sizeof(int)), "barrier token");
@@ -378,6 +391,7 @@ vr_status vr_shard_connect(vr_shard* sh, const uint8_t id[VR_SHARD_ID_BYTES])
     if (sh->comm) return fail(VR_ERR_INVALID, "vr_shard_connect: already connected");
     if (sh->last >= 0) return fail(VR_ERR_INVALID, "vr_shard_connect: frames already rendered in loopback");
     if (sh->aborted) return fail(VR_ERR_COMM, "vr_shard_connect: communicator already aborted");
+    if (sh->solo) return fail(VR_ERR_INVALID, "vr_shard_connect: a solo rehearsal shard does not connect");
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof u);
     // non-blocking: the init returns at once and completes as the peers join;
@@ -434,7 +448,7 @@ vr_status vr_shard_run_frames(vr_shard* sh, int frames, const vr_object_shader_d
 {
     if (!sh || frames < 0 || (!osd) != (!gsd)) return fail(VR_ERR_INVALID, "vr_shard_run: bad argument");
     if (kernel_ms && sample_every <= 0) return fail(VR_ERR_INVALID, "vr_shard_run: sample_every must be > 0");
-    if (sh->loopback && sh->rank != 0)
+    if (sh->loopback && sh->rank != 0 && !sh->solo)
         return fail(VR_ERR_INVALID, "vr_shard_run: rank %d is not connected (vr_shard_connect)", sh->rank);
     SH_TRY(check_usable(sh, "vr_shard_run"));
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -446,13 +460,18 @@ vr_status vr_shard_run_frames(vr_shard* sh, int frames, const vr_object_shader_d
     }
     int next = 0;
     const auto h0 = std::chrono::steady_clock::now();
+    const bool two = sh->render_streams == 2;
+    if (two && frames > 0) {   // the render streams start after the caller's queued work (e.g. the volume)
+        HIP_TRY(hipEventRecord(sh->fence, s));
+        for (hipStream_t rs : sh->render_stream) HIP_TRY(hipStreamWaitEvent(rs, sh->fence, 0));
+    }
     for (int i = 0; i < frames; ++i) {
         const int p = sh->last < 0 ? 0 : sh->last ^ 1;
         const bool samp = kernel_ms && i % sample_every == 0;
         hipEvent_t t0 = samp ? sh->timing[2 * next] : nullptr, t1 = samp ? sh->timing[2 * next + 1] : nullptr;
         if (samp) ++next;
         if (osd) VR_TRY(vr_set_shader_data(sh->ctx, &osd[i], &gsd[i]));   // this frame's camera
-        const vr_status st = one_frame(sh, p, s, t0, t1);
+        const vr_status st = one_frame(sh, p, two ? sh->render_stream[p] : s, t0, t1);
         if (st != VR_OK) return st;
     }
     if (sh->last >= 0) HIP_TRY(hipStreamWaitEvent(s, sh->done[sh->last], 0));   // the caller's stream sees the frame
@@ -475,7 +494,7 @@ vr_status vr_shard_run_frames(vr_shard* sh, int frames, const vr_object_shader_d
 vr_status vr_shard_barrier(vr_shard* sh, void* stream)
 {
     if (!sh) return fail(VR_ERR_INVALID, "vr_shard_barrier: null");
-    if (sh->loopback && sh->rank != 0)
+    if (sh->loopback && sh->rank != 0 && !sh->solo)
         return fail(VR_ERR_INVALID, "vr_shard_barrier: rank %d is not connected (vr_shard_connect)", sh->rank);
     SH_TRY(check_usable(sh, "vr_shard_barrier"));
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -590,6 +609,29 @@ vr_status vr_shard_share_volume(vr_shard* sh, const void* d_rgba8, int nx, int n
     }
     if (buf && !sh->aborted) (void)hipFree(buf);   // an aborted broadcast may still own it: leak, not corrupt
     return st;
+}
+
+vr_status vr_shard_set_render_streams(vr_shard* sh, int n)
+{
+    if (!sh || (n != 1 && n != 2)) return fail(VR_ERR_INVALID, "vr_shard_set_render_streams: need a shard and n = 1 or 2");
+    if (n != sh->render_streams && sh->last >= 0) {
+        // frames of the old arrangement may still be in flight: the next
+        // frame's stream must see them (each parity's done[] covers its render)
+        for (int p = 0; p < 2; ++p)
+            if (sh->pending[p]) SH_TRY(wait_event(sh, sh->done[p], "vr_shard_set_render_streams"));
+    }
+    sh->render_streams = n;
+    return VR_OK;
+}
+
+int vr_shard_get_render_streams(vr_shard* sh) { return sh ? sh->render_streams : 0; }
+
+vr_status vr_shard_set_solo(vr_shard* sh, int on)
+{
+    if (!sh) return fail(VR_ERR_INVALID, "vr_shard_set_solo: null");
+    if (!sh->loopback) return fail(VR_ERR_INVALID, "vr_shard_set_solo: only an unconnected (loopback) shard rehearses alone");
+    sh->solo = on != 0;
+    return VR_OK;
 }
 
 vr_status vr_shard_set_timeout(vr_shard* sh, double seconds)

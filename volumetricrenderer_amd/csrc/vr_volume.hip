@@ -581,35 +581,76 @@ hipError_t launch_pack_recipe(const float* d_g1, const float* d_g2, const float*
     return hipGetLastError();
 }
 
-// Streaming copy for the measured HBM roofline (vr_measure_copy_bandwidth):
-// 16 B per lane, one pass over the buffer -- each workgroup copies its own
-// 4 x 256 x 16 B = 16 KiB (four independent loads per lane, issued before
-// the stores), the grid as large as the buffer: the float4 copy of
-// MI355X_MICROARCH.md's measured HBM rate.  (A persistent 2,048-workgroup
-// grid-stride loop read 4.6-4.7 TB/s.)
-constexpr int kCopyPerLane = 4;
+// Streaming kernels for the measured HBM roofline (vr_measure_bandwidth):
+// 16 B per lane, one pass over the buffer, the grid as large as the buffer
+// (each workgroup owns PL x 256 x 16 B; a persistent 2,048-workgroup
+// grid-stride loop read 4.6-4.7 TB/s).  PL independent loads per lane are
+// issued before anything consumes them.
+//  * copy: the float4 copy of MI355X_MICROARCH.md's measured HBM rate
+//    (counted as 2 x bytes moved);
+//  * read: loads only, folded into one register per lane (xor), which is
+//    stored only if it equals a value the 0x5a fill never produces -- every
+//    lane's loads stay live, nothing is written.  The ray march is 98 % reads
+//    (profiles/traffic.json), so this is its roofline denominator.
+template <int PL>
 __global__ __launch_bounds__(256) void k_stream_copy(const uint4* __restrict__ src, uint4* __restrict__ dst,
                                                      long long n)
 {
-    const long long base = (long long)blockIdx.x * (256 * kCopyPerLane) + threadIdx.x;
-    uint4 v[kCopyPerLane];
+    const long long base = (long long)blockIdx.x * (256 * PL) + threadIdx.x;
+    uint4 v[PL];
 #pragma unroll
-    for (int k = 0; k < kCopyPerLane; ++k)
+    for (int k = 0; k < PL; ++k)
         if (base + k * 256 < n) v[k] = src[base + k * 256];
 #pragma unroll
-    for (int k = 0; k < kCopyPerLane; ++k)
+    for (int k = 0; k < PL; ++k)
         if (base + k * 256 < n) dst[base + k * 256] = v[k];
+}
+
+constexpr unsigned kReadSinkMagic = 0x9e3779b9u;
+
+template <int PL>
+__global__ __launch_bounds__(256) void k_stream_read(const uint4* __restrict__ src, unsigned* __restrict__ sink,
+                                                     long long n)
+{
+    const long long base = (long long)blockIdx.x * (256 * PL) + threadIdx.x;
+    uint4 v[PL];
+#pragma unroll
+    for (int k = 0; k < PL; ++k) v[k] = base + k * 256 < n ? src[base + k * 256] : make_uint4(0u, 0u, 0u, 0u);
+    unsigned x = 0u;
+#pragma unroll
+    for (int k = 0; k < PL; ++k) x ^= (v[k].x ^ v[k].y) ^ (v[k].z ^ v[k].w);
+    if (x == kReadSinkMagic) sink[threadIdx.x] = x;   // never taken for the 0x5a fill
+}
+
+template <int PL>
+static hipError_t launch_stream_pl(int kind, const void* src, void* dst, long long n, hipStream_t s)
+{
+    const long long blocks = (n + 256 * PL - 1) / (256 * PL);
+    if (blocks <= 0) return hipSuccess;
+    if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
+    if (kind == 0)
+        hipLaunchKernelGGL(k_stream_copy<PL>, dim3((unsigned)blocks), dim3(256), 0, s, static_cast<const uint4*>(src),
+                           static_cast<uint4*>(dst), n);
+    else
+        hipLaunchKernelGGL(k_stream_read<PL>, dim3((unsigned)blocks), dim3(256), 0, s, static_cast<const uint4*>(src),
+                           static_cast<unsigned*>(dst), n);
+    return hipGetLastError();
+}
+
+hipError_t launch_stream_bw(int kind, int loads_per_lane, const void* src, void* dst, size_t bytes, hipStream_t s)
+{
+    const long long n = (long long)(bytes / 16);
+    switch (loads_per_lane) {
+    case 4: return launch_stream_pl<4>(kind, src, dst, n, s);
+    case 8: return launch_stream_pl<8>(kind, src, dst, n, s);
+    case 16: return launch_stream_pl<16>(kind, src, dst, n, s);
+    default: return hipErrorInvalidValue;
+    }
 }
 
 hipError_t launch_stream_copy(const void* src, void* dst, size_t bytes, hipStream_t s)
 {
-    const long long n = (long long)(bytes / 16);
-    const long long blocks = (n + 256 * kCopyPerLane - 1) / (256 * kCopyPerLane);
-    if (blocks <= 0) return hipSuccess;
-    if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_stream_copy, dim3((unsigned)blocks), dim3(256), 0, s, static_cast<const uint4*>(src),
-                       static_cast<uint4*>(dst), n);
-    return hipGetLastError();
+    return launch_stream_bw(0, 4, src, dst, bytes, s);
 }
 
 hipError_t launch_assemble(const uint8_t* d_gathered, size_t rows_per_rank, int nranks, int width, int height,

@@ -189,8 +189,10 @@ class BandSharder:
                     ev[1].record(self._streams2[j])
             for st in self._streams2:
                 cur.wait_stream(st)
-            self.frame_buf = self._targets2[(k - 1) % 2] if k > 0 else self.frame_buf
-            return self.frame_buf
+            # the last target, without moving self.frame_buf: the one-stream
+            # paths (frame(), the procedural medium) render into self.local and
+            # return self.frame_buf, which must stay that buffer
+            return self._targets2[(k - 1) % 2] if k > 0 else self.frame_buf
         if self.world == 1 and hasattr(self.r, "prepare_render"):
             # one rank: one stream, a prepared launcher (ctypes arguments built once)
             if getattr(self, "_launch1", None) is None:
@@ -282,9 +284,16 @@ class RcclBandPipeline:
     the communicator id from rank 0 and the barriers."""
 
     def __init__(self, renderer, width: int, height: int, fmt: int, band_rows: int = 16, world: int = 1,
-                 rank: int = 0, group=None, loopback: bool = False, timeout_s: float | None = None):
+                 rank: int = 0, group=None, loopback: bool = False, timeout_s: float | None = None,
+                 render_streams: int = 2, solo: bool = False):
         """loopback: one process renders all `world` ranks' band sets on its
         GPU and assembles them (no communicator; tests and rehearsals).
+        solo (loopback only, any rank): each frame renders only this rank's
+        band set, without an exchange -- one rank's frame period on one GPU
+        (vr_shard_set_solo; tools/band_scaling.py --native).
+        render_streams: 2 (default) = consecutive frames render on two
+        alternating streams and overlap; 1 = on the caller's stream, in turn
+        (vr_shard_set_render_streams).
         timeout_s: deadline of every host wait on a collective, from the
         communicator init on (vr_shard_set_timeout; default VR_SHARD_TIMEOUT_S
         or 120 s).  A rank whose peer fails gets VRError VR_ERR_TIMEOUT /
@@ -292,10 +301,13 @@ class RcclBandPipeline:
         self.r = renderer
         self.width, self.height, self.fmt = width, height, fmt
         self.world, self.rank, self.group, self.loopback = world, rank, group, loopback
+        if solo and not loopback:
+            raise ValueError("RcclBandPipeline: solo is a loopback rehearsal")
         uid = (ctypes.c_uint8 * _lib.SHARD_ID_BYTES)()
         err = None
         if loopback:
-            assert rank == 0
+            if rank != 0 and not solo:
+                raise ValueError("RcclBandPipeline: a loopback pipeline of rank > 0 needs solo=True")
             uid = None
         elif rank == 0:
             try:
@@ -335,6 +347,13 @@ class RcclBandPipeline:
             raise alloc_err
         if timeout_s is not None:
             _lib.shard_call("vr_shard_set_timeout", h, float(timeout_s))
+        try:
+            _lib.shard_call("vr_shard_set_render_streams", h, int(render_streams))
+            if solo:
+                _lib.shard_call("vr_shard_set_solo", h, 1)
+        except _lib.VRError:
+            _lib.shard_call("vr_shard_destroy", h)
+            raise
         if not loopback:
             try:
                 _lib.shard_call("vr_shard_connect", h, uid)
@@ -345,6 +364,14 @@ class RcclBandPipeline:
         mine, per = ctypes.c_int(), ctypes.c_int()
         _lib.shard_call("vr_shard_rows", h, ctypes.byref(mine), ctypes.byref(per))
         self.my_rows, self.rows_per_rank = mine.value, per.value
+
+    @property
+    def render_streams(self) -> int:
+        return _lib.shard_call("vr_shard_get_render_streams", self._h)
+
+    @render_streams.setter
+    def render_streams(self, n: int) -> None:
+        _lib.shard_call("vr_shard_set_render_streams", self._h, int(n))
 
     def set_timeout(self, seconds: float) -> None:
         """Deadline (s) of every later host wait on a collective."""

@@ -226,6 +226,18 @@ class Renderer:
                   ctypes.byref(med))
         return best.value, med.value
 
+    def measure_bandwidth(self, kind: str = "read", loads_per_lane: int = 0, nbytes: int = 2 << 30, reps: int = 10,
+                          stream=None) -> tuple[float, float, int]:
+        """(best, median GB/s, loads per lane of the best) of a one-pass 16-B-per-lane
+        stream over `nbytes` (vr_measure_bandwidth): kind "read" (loads only, bytes
+        read / time) or "copy" (read + written bytes / time); loads_per_lane 4, 8,
+        16, or 0 = each of them."""
+        k = {"copy": 0, "read": 1}[kind]
+        best, med, pl = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
+        _lib.call("vr_measure_bandwidth", self._ctx, k, int(loads_per_lane), nbytes, reps, _stream_handle(stream),
+                  ctypes.byref(best), ctypes.byref(med), ctypes.byref(pl))
+        return best.value, med.value, pl.value
+
     # -- the hot path ------------------------------------------------------
     def alloc_target(self, width: int, height: int, fmt: int = FMT_RGBA8_UNORM, band_rows: int = 0,
                      band_stride: int = 1, band_first: int = 0) -> torch.Tensor:
