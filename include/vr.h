@@ -156,6 +156,10 @@ vr_status   vr_create(int device, void** out_ctx);
 vr_status   vr_destroy(void* ctx);
 const char* vr_last_error(void);
 int         vr_abi_version(void);
+/* Hash of the sources this library was built from (tools/build_id.py; a
+ * "-exp" suffix for the VR_EXPERIMENTS build): the tests and smoke() check
+ * that the prebuilt library matches the checked-out code.  Static string.  */
+const char* vr_build_id(void);
 
 /* ---- volume: replaces vkc::Texture3D(unsigned char*, VkExtent3D)
  *      (VulkanTexture.h:55-60, VulkanTexture.cpp:111-156).  RGBA8 UNORM,

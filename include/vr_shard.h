@@ -37,6 +37,8 @@ extern "C" {
 typedef struct vr_shard vr_shard;
 
 const char* vr_shard_last_error(void);
+/* vr_build_id of the sources libvr_shard.so was built from (vr.h).       */
+const char* vr_shard_build_id(void);
 
 /* A new communicator id (call on rank 0, then share the bytes). */
 vr_status vr_shard_unique_id(uint8_t id[VR_SHARD_ID_BYTES]);

@@ -1612,3 +1612,42 @@ def test_tiny_frames_procedural(r, oracle, W, H, shadow):
     img, ref, c, s, _ = render_proc_both(r, oracle, W, H, vr.march_defaults(), shadow_steps=shadow)
     assert_exact(img, ref)
     assert c == s
+
+
+@pytest.mark.parametrize("kind,status", [(1, 2), (2, 5)])
+def test_exception_never_crosses_the_abi(oracle, vol128, kind, status):
+    """Verdict r04 #5: a C++ exception inside an entry point's host path
+    (option inject_throw: std::runtime_error / std::bad_alloc thrown inside
+    vr_render) comes back as a vr_status -- VR_ERR_HIP / VR_ERR_OOM with the
+    message in vr_last_error -- instead of terminating the process; the same
+    context then renders exactly again.  The native frame loop passes the
+    status through (loopback, 2 ranks) and runs on afterwards."""
+    from volumetricrenderer_amd.distributed import RcclBandPipeline
+    W, H = 200, 120
+    with vr.Renderer(0) as rr:
+        img, ref, cnt, steps = render_both(rr, oracle, vol128, W, H)
+        assert_exact(img, ref)
+        rr.set_option("inject_throw", kind)
+        with pytest.raises(VRError) as e:
+            rr.render(W, H, 0)
+        assert e.value.status == status, e.value
+        assert "vr_render" in str(e.value)
+        again = rr.render(W, H, 0)
+        torch.cuda.synchronize()
+        assert_exact(again.cpu().numpy(), ref)
+        pl = RcclBandPipeline(rr, W, H, 0, band_rows=16, world=2, rank=0, loopback=True)
+        try:
+            pl.run_frames(2)
+            rr.set_option("inject_throw", kind)
+            with pytest.raises(VRError) as e2:
+                pl.run_frames(2)
+            assert e2.value.status == status, e2.value
+            pl.run_frames(3)
+            pl.barrier()
+            got = pl.frame()
+            torch.cuda.synchronize()
+            assert_exact(got.cpu().numpy(), ref)
+        finally:
+            pl.close()
+    with vr.Renderer(0) as r2, pytest.raises(VRError):
+        r2.set_option("inject_throw", 3)

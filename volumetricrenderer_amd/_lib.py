@@ -100,6 +100,7 @@ _SIGS = {
     "vr_destroy": (ctypes.c_int, [_vp]),
     "vr_last_error": (ctypes.c_char_p, []),
     "vr_abi_version": (ctypes.c_int, []),
+    "vr_build_id": (ctypes.c_char_p, []),
     "vr_set_volume": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "vr_set_volume_device": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp]),
     "vr_get_volume": (ctypes.c_int, [_vp, _vp]),
@@ -188,6 +189,7 @@ SHARD_LIB_PATH = os.environ.get("VR_SHARD_LIB") or os.path.join(HERE, "libvr_sha
 SHARD_ID_BYTES = 128
 _SHARD_SIGS = {
     "vr_shard_last_error": (ctypes.c_char_p, []),
+    "vr_shard_build_id": (ctypes.c_char_p, []),
     "vr_shard_unique_id": (ctypes.c_int, [_vp]),
     "vr_shard_create": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_int, ctypes.c_int, ctypes.POINTER(_vp)]),

@@ -12,7 +12,9 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <exception>
 #include <new>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -34,6 +36,24 @@ vr_status fail(vr_status st, const char* fmt, ...)
     va_end(ap);
     g_err = buf;
     return st;
+}
+
+// Every extern "C" entry is a function-try-block ending in caught_exception:
+// no C++ exception crosses the ABI (vr.h).  A host-side std::bad_alloc (the
+// region-list build's vectors, a grown scratch) becomes VR_ERR_OOM, anything
+// else VR_ERR_HIP, with the message in vr_last_error().  Called inside a
+// catch handler: `throw;` rethrows the exception being handled.
+vr_status caught_exception(const char* fn) noexcept
+{
+    try {
+        throw;
+    } catch (const std::bad_alloc&) {
+        return fail(VR_ERR_OOM, "%s: host allocation failed (std::bad_alloc)", fn);
+    } catch (const std::exception& e) {
+        return fail(VR_ERR_HIP, "%s: unexpected exception: %s", fn, e.what());
+    } catch (...) {
+        return fail(VR_ERR_HIP, "%s: unexpected exception", fn);
+    }
 }
 
 #define HIP_TRY(expr)                                                                        \
@@ -202,6 +222,9 @@ struct Ctx {
     // Perlin lattice table of the procedural march (noise::perlin_lattice_entry),
     // built when (seed, lo, n) changes; option "lattice" 0 turns it off
     int lattice = 1;
+    // option "inject_throw" (tests of the exception guard): the next vr_render
+    // throws std::runtime_error (1) or std::bad_alloc (2) in its host path
+    int inject_throw = 0;
     uint2* d_lat = nullptr;
     size_t lat_cap = 0;            // bytes allocated
     long long lat_key[3] = {0, 0, -1};
@@ -430,7 +453,7 @@ const char* vr_last_error(void) { return g_err.c_str(); }
 int vr_abi_version(void) { return VR_ABI_VERSION; }
 
 vr_status vr_march_defaults(vr_march_params* m)
-{
+try {
     if (!m) return fail(VR_ERR_INVALID, "vr_march_defaults: null");
     std::memset(m, 0, sizeof *m);
     m->max_steps = 128;        // frag.glsl:30
@@ -442,20 +465,24 @@ vr_status vr_march_defaults(vr_march_params* m)
     for (int t = 0; t < 4; ++t) { m->tap_scale[t] = ts[t]; m->tap_weight[t] = tw[t]; }
     m->early_out = 0.0f;
     return VR_OK;
+} catch (...) {
+    return caught_exception("vr_march_defaults");
 }
 
 vr_status vr_volume_recipe_defaults(vr_volume_recipe* r)
-{
+try {
     if (!r) return fail(VR_ERR_INVALID, "vr_volume_recipe_defaults: null");
     r->size = 128;  // TestMain.cpp:51
     const float f[4] = {0.01f, 0.03f, 0.19f, 0.15f};  // :59-62
     for (int k = 0; k < 4; ++k) { r->freq[k] = f[k]; r->seed[k] = k + 1; }
     r->literal_overwrite = 1;
     return VR_OK;
+} catch (...) {
+    return caught_exception("vr_volume_recipe_defaults");
 }
 
 vr_status vr_procedural_defaults(vr_procedural* p)
-{
+try {
     if (!p) return fail(VR_ERR_INVALID, "vr_procedural_defaults: null");
     std::memset(p, 0, sizeof *p);
     p->enabled = 0;
@@ -471,6 +498,8 @@ vr_status vr_procedural_defaults(vr_procedural* p)
     const double n = std::sqrt(1.0 + 1.0 + 4.0);
     p->sun_dir[0] = (float)(1.0 / n); p->sun_dir[1] = (float)(1.0 / n); p->sun_dir[2] = (float)(2.0 / n);
     return VR_OK;
+} catch (...) {
+    return caught_exception("vr_procedural_defaults");
 }
 
 constexpr long long kMaxWorleyTableBytes = 32 << 10;   // LDS per workgroup for the cell table
@@ -499,7 +528,7 @@ int worley_z_pitch(int n)
 }
 
 vr_status vr_set_procedural(void* ctx, const vr_procedural* p)
-{
+try {
     if (!ctx || !p) return fail(VR_ERR_INVALID, "vr_set_procedural: null argument");
     if (p->enabled) {
         if (p->octaves < 0 || p->octaves > 16) return fail(VR_ERR_INVALID, "vr_set_procedural: octaves in [0,16]");
@@ -522,10 +551,12 @@ vr_status vr_set_procedural(void* ctx, const vr_procedural* p)
         for (int a = 0; a < 3; ++a) c->proc.sun_dir[a] = (float)((double)p->sun_dir[a] / l);
     }
     return VR_OK;
+} catch (...) {
+    return caught_exception("vr_set_procedural");
 }
 
 vr_status vr_create(int device, void** out)
-{
+try {
     if (!out) return fail(VR_ERR_INVALID, "vr_create: out is null");
     *out = nullptr;
     int n = 0;
@@ -542,10 +573,12 @@ vr_status vr_create(int device, void** out)
     }
     *out = c;
     return VR_OK;
+} catch (...) {
+    return caught_exception("vr_create");
 }
 
 vr_status vr_destroy(void* p)
-{
+try {
     if (!p) return VR_OK;
     Ctx* c = as_ctx(p);
     (void)hipSetDevice(c->device);
@@ -575,10 +608,12 @@ vr_status vr_destroy(void* p)
     }
     delete c;
     return VR_OK;
+} catch (...) {
+    return caught_exception("vr_destroy");
 }
 
 vr_status vr_set_volume(void* p, const uint8_t* rgba8, int nx, int ny, int nz)
-{
+try {
     if (!p || !rgba8) return fail(VR_ERR_INVALID, "vr_set_volume: null argument");  // VulkanTexture.cpp:121-124
     if (!dims_ok(nx, ny, nz)) return fail(VR_ERR_INVALID, "vr_set_volume: bad extent %dx%dx%d", nx, ny, nz);
     Ctx* c = as_ctx(p);
@@ -594,29 +629,35 @@ vr_status vr_set_volume(void* p, const uint8_t* rgba8, int nx, int ny, int nz)
     if (st != VR_OK) return st;
     if (e != hipSuccess) return fail(VR_ERR_HIP, "vr_set_volume: %s", hipGetErrorString(e));
     return VR_OK;
+} catch (...) {
+    return caught_exception("vr_set_volume");
 }
 
 vr_status vr_set_volume_device(void* p, const void* d_rgba8, int nx, int ny, int nz, void* stream)
-{
+try {
     if (!p || !d_rgba8) return fail(VR_ERR_INVALID, "vr_set_volume_device: null argument");
     if (!dims_ok(nx, ny, nz)) return fail(VR_ERR_INVALID, "vr_set_volume_device: bad extent %dx%dx%d", nx, ny, nz);
     Ctx* c = as_ctx(p);
     HIP_TRY(hipSetDevice(c->device));
     return install_volume(c, static_cast<const uint8_t*>(d_rgba8), nx, ny, nz, static_cast<hipStream_t>(stream));
+} catch (...) {
+    return caught_exception("vr_set_volume_device");
 }
 
 int vr_volume_extent_ok(int nx, int ny, int nz) { return dims_ok(nx, ny, nz) ? 1 : 0; }
 
 vr_status vr_volume_dims(void* p, int* nx, int* ny, int* nz)
-{
+try {
     if (!p || !nx || !ny || !nz) return fail(VR_ERR_INVALID, "vr_volume_dims: null argument");
     Ctx* c = as_ctx(p);
     *nx = c->nx; *ny = c->ny; *nz = c->nz;
     return VR_OK;
+} catch (...) {
+    return caught_exception("vr_volume_dims");
 }
 
 vr_status vr_get_volume(void* p, uint8_t* out)
-{
+try {
     if (!p || !out) return fail(VR_ERR_INVALID, "vr_get_volume: null argument");
     Ctx* c = as_ctx(p);
     if (!c->d_planar) return fail(VR_ERR_NO_VOLUME, "vr_get_volume: no volume set");
@@ -629,11 +670,13 @@ vr_status vr_get_volume(void* p, uint8_t* out)
     (void)hipFree(staging);
     if (e != hipSuccess) return fail(VR_ERR_HIP, "vr_get_volume: %s", hipGetErrorString(e));
     return VR_OK;
+} catch (...) {
+    return caught_exception("vr_get_volume");
 }
 
 vr_status vr_noise_grid(void* p, int kind, void* d_out, int x0, int y0, int z0, int nx, int ny, int nz,
                         float freq, int32_t seed, float* out_min, float* out_max, void* stream)
-{
+try {
     if (!p) return fail(VR_ERR_INVALID, "vr_noise_grid: null ctx");
     if (kind < 0 || kind > 2) return fail(VR_ERR_INVALID, "vr_noise_grid: kind %d", kind);
     if (nx <= 0 || ny <= 0 || nz <= 0) return fail(VR_ERR_INVALID, "vr_noise_grid: bad extent");
@@ -657,10 +700,12 @@ vr_status vr_noise_grid(void* p, int kind, void* d_out, int x0, int y0, int z0, 
     if (out_min) *out_min = h[0];
     if (out_max) *out_max = h[1];
     return VR_OK;
+} catch (...) {
+    return caught_exception("vr_noise_grid");
 }
 
 vr_status vr_selftest(void* p, const char* name, long long* failures)
-{
+try {
     if (!p || !name || !failures) return fail(VR_ERR_INVALID, "vr_selftest: null argument");
     static const char* const kNames[] = {"cell_inv_a", "cell_inv_b", "cell_inv_c", "cell_inv", "worley_prune"};
     int variant = -1;
@@ -684,11 +729,13 @@ vr_status vr_selftest(void* p, const char* name, long long* failures)
     if (e != hipSuccess) return fail(VR_ERR_HIP, "vr_selftest: %s", hipGetErrorString(e));
     *failures = (long long)h;
     return VR_OK;
+} catch (...) {
+    return caught_exception("vr_selftest");
 }
 
 vr_status vr_measure_bandwidth(void* p, int kind, int loads_per_lane, size_t bytes, int reps, void* stream,
                                double* gbs_best, double* gbs_median, int* loads_best)
-{
+try {
     if (!p || !gbs_best || reps <= 0 || bytes < 16 || (kind != VR_BW_COPY && kind != VR_BW_READ) ||
         (loads_per_lane != 0 && loads_per_lane != 4 && loads_per_lane != 8 && loads_per_lane != 16))
         return fail(VR_ERR_INVALID, "vr_measure_bandwidth: bad argument");
@@ -743,15 +790,19 @@ vr_status vr_measure_bandwidth(void* p, int kind, int loads_per_lane, size_t byt
         *gbs_median = w[w.size() / 2];
     }
     return VR_OK;
+} catch (...) {
+    return caught_exception("vr_measure_bandwidth");
 }
 
 vr_status vr_measure_copy_bandwidth(void* p, size_t bytes, int reps, void* stream, double* gbs_best, double* gbs_median)
-{
+try {
     return vr_measure_bandwidth(p, VR_BW_COPY, 4, bytes, reps, stream, gbs_best, gbs_median, nullptr);
+} catch (...) {
+    return caught_exception("vr_measure_copy_bandwidth");
 }
 
 vr_status vr_generate_volume(void* p, const vr_volume_recipe* r, void* stream)
-{
+try {
     if (!p || !r) return fail(VR_ERR_INVALID, "vr_generate_volume: null argument");
     const int N = r->size;
     if (!dims_ok(N, N, N)) return fail(VR_ERR_INVALID, "vr_generate_volume: bad size %d", N);
@@ -792,10 +843,12 @@ vr_status vr_generate_volume(void* p, const vr_volume_recipe* r, void* stream)
         return fail(e == hipErrorOutOfMemory ? VR_ERR_OOM : VR_ERR_HIP, "vr_generate_volume: %s", hipGetErrorString(e));
     }
     return VR_OK;
+} catch (...) {
+    return caught_exception("vr_generate_volume");
 }
 
 vr_status vr_set_shader_data(void* p, const vr_object_shader_data* osd, const vr_global_shader_data* gsd)
-{
+try {
     if (!p || !osd || !gsd) return fail(VR_ERR_INVALID, "vr_set_shader_data: null argument");
     Ctx* c = as_ctx(p);
     std::memcpy(c->obj, osd, sizeof(float) * 48);
@@ -807,20 +860,24 @@ vr_status vr_set_shader_data(void* p, const vr_object_shader_data* osd, const vr
     }
     c->has_camera = true;
     return VR_OK;
+} catch (...) {
+    return caught_exception("vr_set_shader_data");
 }
 
 vr_status vr_reference_shader_data(float aspect, float phi_deg, float theta_deg, float frame_time,
                                    vr_object_shader_data* osd, vr_global_shader_data* gsd)
-{
+try {
     if (!osd || !gsd) return fail(VR_ERR_INVALID, "vr_reference_shader_data: null argument");
     if (!(aspect > 0.0f)) return fail(VR_ERR_INVALID, "vr_reference_shader_data: aspect must be > 0");
     reference_shader_data(aspect, phi_deg, theta_deg, frame_time, reinterpret_cast<float*>(osd),
                           reinterpret_cast<float*>(gsd));
     return VR_OK;
+} catch (...) {
+    return caught_exception("vr_reference_shader_data");
 }
 
 vr_status vr_set_march(void* p, const vr_march_params* m)
-{
+try {
     if (!p || !m) return fail(VR_ERR_INVALID, "vr_set_march: null argument");
     if (m->max_steps <= 0) return fail(VR_ERR_INVALID, "vr_set_march: max_steps must be > 0");
     if (!(m->step_scale > 0.0f) || !std::isfinite(m->step_scale))
@@ -833,15 +890,20 @@ vr_status vr_set_march(void* p, const vr_march_params* m)
     if (m->reserved[0] || m->reserved[1] || m->reserved[2]) return fail(VR_ERR_INVALID, "vr_set_march: reserved must be 0");
     as_ctx(p)->march = *m;
     return VR_OK;
+} catch (...) {
+    return caught_exception("vr_set_march");
 }
 
 int vr_band_rows_packed(int height, int band_rows, int band_stride, int band_first)
-{
+try {
     return band_rows_packed(height, band_rows, band_stride, band_first);
+} catch (...) {
+    (void)caught_exception("vr_band_rows_packed");
+    return -1;
 }
 
 vr_status vr_set_layout_preference(void* p, int pref)
-{
+try {
     if (!p || pref < 0 || pref >= kNumLayouts) return fail(VR_ERR_INVALID, "vr_set_layout_preference: bad argument");
     if (pref > 0 && !layout_built(pref))
         return fail(VR_ERR_INVALID, "vr_set_layout_preference: layout %d is built only with VR_EXPERIMENTS "
@@ -852,10 +914,12 @@ vr_status vr_set_layout_preference(void* p, int pref)
     vr_status st = ensure_fast_layout(c, nullptr);
     if (st == VR_OK && hipDeviceSynchronize() != hipSuccess) return fail(VR_ERR_HIP, "vr_set_layout_preference: sync");
     return st;
+} catch (...) {
+    return caught_exception("vr_set_layout_preference");
 }
 
 vr_status vr_set_option(void* p, const char* name, int value)
-{
+try {
     if (!p || !name) return fail(VR_ERR_INVALID, "vr_set_option: null argument");
     Ctx* c = as_ctx(p);
     const std::string n(name);
@@ -870,6 +934,12 @@ vr_status vr_set_option(void* p, const char* name, int value)
         return fail(VR_ERR_INVALID, "vr_set_option: %s = %d is built only with VR_EXPERIMENTS (make EXPERIMENTS=1; "
                                     "measured slower, DESIGN.md)", name, value);
     if (n == "layout") return vr_set_layout_preference(p, value);
+    if (n == "inject_throw") {   // test hook: the next vr_render throws in its host path
+        if (value < 0 || value > 2)
+            return fail(VR_ERR_INVALID, "vr_set_option: inject_throw is 0, 1 (std::runtime_error) or 2 (std::bad_alloc)");
+        c->inject_throw = value;
+        return VR_OK;
+    }
     if (n == "schedule") {
         if (value < -1 || value > 5)
             return fail(VR_ERR_INVALID, "vr_set_option: schedule is -1 (auto), 0 (static), 1 (queue), "
@@ -1003,10 +1073,12 @@ vr_status vr_set_option(void* p, const char* name, int value)
         return VR_OK;
     }
     return fail(VR_ERR_INVALID, "vr_set_option: unknown option '%s'", name);
+} catch (...) {
+    return caught_exception("vr_set_option");
 }
 
 int vr_get_option(void* p, const char* name)
-{
+try {
     if (!p || !name) return -1;
     Ctx* c = as_ctx(p);
     const std::string n(name);
@@ -1048,12 +1120,15 @@ int vr_get_option(void* p, const char* name)
     if (n == "region_gpu") return c->region_gpu;
     if (n == "region_gpu_builds") return (int)std::min<long long>(c->gpu_builds, 0x7fffffff);   // read-only
     return -1;
+} catch (...) {
+    (void)caught_exception("vr_get_option");
+    return -1;
 }
 
 static bool lat_on(const Ctx* c, int layout);
 
 const char* vr_kernel_variant(void* p)
-{
+try {
     if (!p) return "none";
     Ctx* c = as_ctx(p);
     if (c->proc.enabled) {
@@ -1097,6 +1172,9 @@ const char* vr_kernel_variant(void* p)
         return t;
     }();
     return table.n[pl.layout][pl.early ? 1 : 0][ch + 1][lat].c_str();
+} catch (...) {
+    (void)caught_exception("vr_kernel_variant");
+    return "error";
 }
 
 // Target pixel (x, packed output row) under the projected box centre: the
@@ -1727,7 +1805,7 @@ static vr_status ensure_defer(Ctx* c, const MarchArgs& a, void* sort_buf, Shadow
 }
 
 vr_status vr_render(void* p, const vr_target* t, void* stream)
-{
+try {
     if (!p || !t) return fail(VR_ERR_INVALID, "vr_render: null argument");
     Ctx* c = as_ctx(p);
     if (!c->d_planar && !c->proc.enabled)
@@ -1743,6 +1821,12 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
     if (t->band_rows < 0 || (t->band_rows > 0 && (t->band_stride <= 0 || t->band_first < 0)))
         return fail(VR_ERR_INVALID, "vr_render: bad band selection");
 
+    if (c->inject_throw) {
+        const int k = c->inject_throw;
+        c->inject_throw = 0;
+        if (k == 2) throw std::bad_alloc();
+        throw std::runtime_error("injected by vr option inject_throw");
+    }
     MarchArgs a{};
     RayBasis b;
     if (!make_ray_basis(c->obj, c->glob, t->width, t->height, &b))
@@ -1982,11 +2066,13 @@ vr_status vr_render(void* p, const vr_target* t, void* stream)
     HIP_TRY(launch_march(a, pl.layout, pl.wrap, pl.early, sc, static_cast<hipStream_t>(stream)));
     if (kind == SCHED_REGIONS) return note_region_render(c, static_cast<hipStream_t>(stream));
     return VR_OK;
+} catch (...) {
+    return caught_exception("vr_render");
 }
 
 vr_status vr_render_sequence(void* p, const vr_target* t, int frames, const vr_object_shader_data* osd,
                              const vr_global_shader_data* gsd, void* stream)
-{
+try {
     if (!p || !t || frames < 0 || (frames > 0 && (!osd || !gsd)))
         return fail(VR_ERR_INVALID, "vr_render_sequence: bad argument");
     for (int i = 0; i < frames; ++i) {
@@ -1995,11 +2081,13 @@ vr_status vr_render_sequence(void* p, const vr_target* t, int frames, const vr_o
         if (st != VR_OK) return st;
     }
     return VR_OK;
+} catch (...) {
+    return caught_exception("vr_render_sequence");
 }
 
 vr_status vr_assemble_frame(void* p, const void* d_gathered, int gathered_format, size_t rows_per_rank, int nranks,
                             int width, int height, int band_rows, int frame_format, void* d_frame, void* stream)
-{
+try {
     if (!p || !d_gathered || !d_frame) return fail(VR_ERR_INVALID, "vr_assemble_frame: null argument");
     if (gathered_format < 0 || gathered_format > 5 || frame_format < 0 || frame_format > 5)
         return fail(VR_ERR_INVALID, "vr_assemble_frame: bad format %d -> %d", gathered_format, frame_format);
@@ -2020,11 +2108,13 @@ vr_status vr_assemble_frame(void* p, const void* d_gathered, int gathered_format
                                  band_rows, frame_format == VR_FMT_RGBA32F, static_cast<uint8_t*>(d_frame),
                                  static_cast<hipStream_t>(stream)));
     return VR_OK;
+} catch (...) {
+    return caught_exception("vr_assemble_frame");
 }
 
 vr_status vr_assemble_bands(void* p, const void* d_gathered, size_t rows_per_rank, int nranks, int width,
                             int height, int band_rows, int bytes_per_pixel, void* d_frame, void* stream)
-{
+try {
     if (!p || !d_gathered || !d_frame) return fail(VR_ERR_INVALID, "vr_assemble_bands: null argument");
     if (nranks <= 0 || width <= 0 || height <= 0 || band_rows <= 0 ||
         (bytes_per_pixel != 1 && bytes_per_pixel != 4 && bytes_per_pixel != 16))
@@ -2038,6 +2128,8 @@ vr_status vr_assemble_bands(void* p, const void* d_gathered, size_t rows_per_ran
                             band_rows, bytes_per_pixel, static_cast<uint8_t*>(d_frame),
                             static_cast<hipStream_t>(stream)));
     return VR_OK;
+} catch (...) {
+    return caught_exception("vr_assemble_bands");
 }
 
 }  // extern "C"

@@ -38,6 +38,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <new>
 #include <string>
 #include <thread>
@@ -63,6 +64,23 @@ vr_status fail(vr_status st, const char* fmt, ...)
     va_end(ap);
     g_err = buf;
     return st;
+}
+
+// Every extern "C" entry is a function-try-block ending in caught_exception:
+// no C++ exception crosses the ABI (a std::bad_alloc -> VR_ERR_OOM, anything
+// else VR_ERR_HIP, the message in vr_shard_last_error()).  Called inside a
+// catch handler: `throw;` rethrows the exception being handled.
+vr_status caught_exception(const char* fn) noexcept
+{
+    try {
+        throw;
+    } catch (const std::bad_alloc&) {
+        return fail(VR_ERR_OOM, "%s: host allocation failed (std::bad_alloc)", fn);
+    } catch (const std::exception& e) {
+        return fail(VR_ERR_HIP, "%s: unexpected exception: %s", fn, e.what());
+    } catch (...) {
+        return fail(VR_ERR_HIP, "%s: unexpected exception", fn);
+    }
 }
 
 #define HIP_TRY(expr)                                                                                     \
@@ -314,18 +332,20 @@ extern "C" {
 const char* vr_shard_last_error(void) { return g_err.c_str(); }
 
 vr_status vr_shard_unique_id(uint8_t id[VR_SHARD_ID_BYTES])
-{
+try {
     if (!id) return fail(VR_ERR_INVALID, "vr_shard_unique_id: null");
     ncclUniqueId u;
     const ncclResult_t r = ncclGetUniqueId(&u);
     if (r != ncclSuccess) return fail(VR_ERR_COMM, "ncclGetUniqueId: %s", ncclGetErrorString(r));
     std::memcpy(id, &u, sizeof u);
     return VR_OK;
+} catch (...) {
+    return caught_exception("vr_shard_unique_id");
 }
 
 vr_status vr_shard_alloc(void* ctx, int nranks, int rank, int width, int height, int format, int band_rows,
                          vr_shard** out)
-{
+try {
     if (!ctx || !out) return fail(VR_ERR_INVALID, "vr_shard_alloc: null argument");
     *out = nullptr;
     if (nranks < 1 || rank < 0 || rank >= nranks) return fail(VR_ERR_INVALID, "vr_shard_alloc: rank %d of %d", rank, nranks);
@@ -383,10 +403,12 @@ vr_status vr_shard_alloc(void* ctx, int nranks, int rank, int width, int height,
     }
     *out = sh;
     return VR_OK;
+} catch (...) {
+    return caught_exception("vr_shard_alloc");
 }
 
 vr_status vr_shard_connect(vr_shard* sh, const uint8_t id[VR_SHARD_ID_BYTES])
-{
+try {
     if (!sh || !id) return fail(VR_ERR_INVALID, "vr_shard_connect: null argument");
     if (sh->comm) return fail(VR_ERR_INVALID, "vr_shard_connect: already connected");
     if (sh->last >= 0) return fail(VR_ERR_INVALID, "vr_shard_connect: frames already rendered in loopback");
@@ -407,11 +429,13 @@ vr_status vr_shard_connect(vr_shard* sh, const uint8_t id[VR_SHARD_ID_BYTES])
     if (st != VR_OK) return st;
     sh->loopback = false;
     return VR_OK;
+} catch (...) {
+    return caught_exception("vr_shard_connect");
 }
 
 vr_status vr_shard_create(void* ctx, const uint8_t id[VR_SHARD_ID_BYTES], int nranks, int rank, int width,
                           int height, int format, int band_rows, vr_shard** out)
-{
+try {
     if (!ctx || !out) return fail(VR_ERR_INVALID, "vr_shard_create: null argument");
     *out = nullptr;
     if (!id && rank != 0) return fail(VR_ERR_INVALID, "vr_shard_create: null id (loopback needs rank 0)");
@@ -429,23 +453,29 @@ vr_status vr_shard_create(void* ctx, const uint8_t id[VR_SHARD_ID_BYTES], int nr
     }
     *out = sh;
     return VR_OK;
+} catch (...) {
+    return caught_exception("vr_shard_create");
 }
 
 vr_status vr_shard_destroy(vr_shard* sh)
-{
+try {
     if (sh) release(sh);
     return VR_OK;
+} catch (...) {
+    return caught_exception("vr_shard_destroy");
 }
 
 vr_status vr_shard_run(vr_shard* sh, int frames, void* stream, int sample_every, float* kernel_ms)
-{
+try {
     return vr_shard_run_frames(sh, frames, nullptr, nullptr, stream, sample_every, kernel_ms, nullptr);
+} catch (...) {
+    return caught_exception("vr_shard_run");
 }
 
 vr_status vr_shard_run_frames(vr_shard* sh, int frames, const vr_object_shader_data* osd,
                               const vr_global_shader_data* gsd, void* stream, int sample_every, float* kernel_ms,
                               double* host_ms)
-{
+try {
     if (!sh || frames < 0 || (!osd) != (!gsd)) return fail(VR_ERR_INVALID, "vr_shard_run: bad argument");
     if (kernel_ms && sample_every <= 0) return fail(VR_ERR_INVALID, "vr_shard_run: sample_every must be > 0");
     if (sh->loopback && sh->rank != 0 && !sh->solo)
@@ -489,10 +519,12 @@ vr_status vr_shard_run_frames(vr_shard* sh, int frames, const vr_object_shader_d
         *kernel_ms = next ? (float)(sum / next) : 0.0f;
     }
     return VR_OK;
+} catch (...) {
+    return caught_exception("vr_shard_run_frames");
 }
 
 vr_status vr_shard_barrier(vr_shard* sh, void* stream)
-{
+try {
     if (!sh) return fail(VR_ERR_INVALID, "vr_shard_barrier: null");
     if (sh->loopback && sh->rank != 0 && !sh->solo)
         return fail(VR_ERR_INVALID, "vr_shard_barrier: rank %d is not connected (vr_shard_connect)", sh->rank);
@@ -507,6 +539,8 @@ vr_status vr_shard_barrier(vr_shard* sh, void* stream)
     SH_TRY(wait_stream(sh, sh->comm_stream, "vr_shard_barrier"));
     SH_TRY(wait_stream(sh, s, "vr_shard_barrier"));
     return VR_OK;
+} catch (...) {
+    return caught_exception("vr_shard_barrier");
 }
 
 // SURVEY.md sec. 8e collective (1): the volume, once, from rank 0 to every
@@ -517,7 +551,7 @@ vr_status vr_shard_barrier(vr_shard* sh, void* stream)
 // alone; then one ncclBroadcast of the RGBA8 bytes and, on every rank,
 // vr_set_volume_device (repack + fast layout), ordered on `stream`.
 vr_status vr_shard_share_volume(vr_shard* sh, const void* d_rgba8, int nx, int ny, int nz, void* stream)
-{
+try {
     if (!sh) return fail(VR_ERR_INVALID, "vr_shard_share_volume: null shard");
     if (sh->loopback && sh->rank != 0)
         return fail(VR_ERR_INVALID, "vr_shard_share_volume: rank %d is not connected (vr_shard_connect)", sh->rank);
@@ -609,10 +643,12 @@ vr_status vr_shard_share_volume(vr_shard* sh, const void* d_rgba8, int nx, int n
     }
     if (buf && !sh->aborted) (void)hipFree(buf);   // an aborted broadcast may still own it: leak, not corrupt
     return st;
+} catch (...) {
+    return caught_exception("vr_shard_share_volume");
 }
 
 vr_status vr_shard_set_render_streams(vr_shard* sh, int n)
-{
+try {
     if (!sh || (n != 1 && n != 2)) return fail(VR_ERR_INVALID, "vr_shard_set_render_streams: need a shard and n = 1 or 2");
     if (n != sh->render_streams && sh->last >= 0) {
         // frames of the old arrangement may still be in flight: the next
@@ -622,23 +658,29 @@ vr_status vr_shard_set_render_streams(vr_shard* sh, int n)
     }
     sh->render_streams = n;
     return VR_OK;
+} catch (...) {
+    return caught_exception("vr_shard_set_render_streams");
 }
 
 int vr_shard_get_render_streams(vr_shard* sh) { return sh ? sh->render_streams : 0; }
 
 vr_status vr_shard_set_solo(vr_shard* sh, int on)
-{
+try {
     if (!sh) return fail(VR_ERR_INVALID, "vr_shard_set_solo: null");
     if (!sh->loopback) return fail(VR_ERR_INVALID, "vr_shard_set_solo: only an unconnected (loopback) shard rehearses alone");
     sh->solo = on != 0;
     return VR_OK;
+} catch (...) {
+    return caught_exception("vr_shard_set_solo");
 }
 
 vr_status vr_shard_set_timeout(vr_shard* sh, double seconds)
-{
+try {
     if (!sh || !(seconds > 0.0)) return fail(VR_ERR_INVALID, "vr_shard_set_timeout: need a shard and seconds > 0");
     sh->timeout_s = seconds;
     return VR_OK;
+} catch (...) {
+    return caught_exception("vr_shard_set_timeout");
 }
 
 int vr_shard_aborted(vr_shard* sh) { return sh && sh->aborted ? 1 : 0; }
@@ -647,7 +689,7 @@ int vr_shard_aborted(vr_shard* sh) { return sh && sh->aborted ? 1 : 0; }
 // settles after a few polls; 1 -- it reports an error; 2 -- it never settles
 // (the deadline).  Returns poll_until's 0 / 1 / 2, or -1 for a bad mode.
 int vr_shard_poll_selftest(int mode, double timeout_s, int* polls)
-{
+try {
     if (mode < 0 || mode > 2) return -1;
     int n = 0;
     const int res = poll_until([&] {
@@ -658,20 +700,25 @@ int vr_shard_poll_selftest(int mode, double timeout_s, int* polls)
     }, timeout_s);
     if (polls) *polls = n;
     return res;
+} catch (...) {
+    (void)caught_exception("vr_shard_poll_selftest");
+    return -1;
 }
 
 vr_status vr_shard_frame(vr_shard* sh, void** pixels, size_t* row_pitch, int* rows)
-{
+try {
     if (!sh || !pixels) return fail(VR_ERR_INVALID, "vr_shard_frame: null argument");
     if (sh->last < 0) return fail(VR_ERR_INVALID, "vr_shard_frame: no frame rendered yet");
     *pixels = sh->rank == 0 ? sh->frame[sh->last] : sh->local[sh->last];
     if (row_pitch) *row_pitch = sh->rank == 0 ? sh->pitch : sh->gpitch;
     if (rows) *rows = sh->rank == 0 ? sh->height : sh->my_rows;
     return VR_OK;
+} catch (...) {
+    return caught_exception("vr_shard_frame");
 }
 
 vr_status vr_shard_copy_frame(vr_shard* sh, void* dst, size_t dst_pitch, void* stream)
-{
+try {
     void* src = nullptr;
     size_t pitch = 0;
     int rows = 0;
@@ -683,14 +730,18 @@ vr_status vr_shard_copy_frame(vr_shard* sh, void* dst, size_t dst_pitch, void* s
     HIP_TRY(hipMemcpy2DAsync(dst, dst_pitch, src, pitch, pitch, (size_t)rows, hipMemcpyDeviceToDevice,
                              static_cast<hipStream_t>(stream)));
     return VR_OK;
+} catch (...) {
+    return caught_exception("vr_shard_copy_frame");
 }
 
 vr_status vr_shard_rows(vr_shard* sh, int* my_rows, int* rows_per_rank)
-{
+try {
     if (!sh) return fail(VR_ERR_INVALID, "vr_shard_rows: null");
     if (my_rows) *my_rows = sh->my_rows;
     if (rows_per_rank) *rows_per_rank = sh->rows_per_rank;
     return VR_OK;
+} catch (...) {
+    return caught_exception("vr_shard_rows");
 }
 
 }  // extern "C"
