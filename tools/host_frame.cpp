@@ -36,6 +36,11 @@ __global__ void k_empty(Big b, int* out)
     if (b.v[0] == 12345.0f && threadIdx.x == 0) out[0] = 1;
 }
 
+__global__ void k_small(float v, int* out)
+{
+    if (v == 12345.0f && threadIdx.x == 0) out[0] = 1;
+}
+
 // median over batches of the host microseconds per call of f, 8 calls per batch
 double per_call_us(int batches, const std::function<void()>& f, const std::function<void()>& sync)
 {
@@ -86,10 +91,29 @@ int main(int argc, char** argv)
     std::printf("variant %s\n", vr_kernel_variant(ctx));
 
     const double t_empty = per_call_us(nb, [&] { hipLaunchKernelGGL(k_empty, dim3(1), dim3(64), 0, s, big, d_out); }, sync);
+    const double t_small = per_call_us(nb, [&] { hipLaunchKernelGGL(k_small, dim3(1), dim3(64), 0, s, 1.0f, d_out); }, sync);
+    const double t_bigg = per_call_us(nb, [&] { hipLaunchKernelGGL(k_empty, dim3(9000), dim3(256), 0, s, big, d_out); }, sync);
     const double t_rec = per_call_us(nb, [&] { (void)hipEventRecord(e, s); }, sync);
+    hipEvent_t ef;
+    CHECK(hipEventCreateWithFlags(&ef, hipEventDisableTiming | hipEventDisableSystemFence));
+    const double t_recf = per_call_us(nb, [&] { (void)hipEventRecord(ef, s); }, sync);
     const double t_wait = per_call_us(nb, [&] { (void)hipStreamWaitEvent(s2, e, 0); }, sync);
-    std::printf("hipLaunchKernel (480-B args) %.2f us, hipEventRecord %.2f, hipStreamWaitEvent %.2f\n", t_empty, t_rec,
-                t_wait);
+    uint32_t* flag = nullptr;
+    CHECK(hipMalloc(&flag, 64));
+    CHECK(hipMemset(flag, 0, 64));
+    uint32_t val = 0;
+    const double t_wv = per_call_us(nb, [&] { (void)hipStreamWriteValue32(s, flag, ++val, 0); }, sync);
+    const double t_wtv = per_call_us(nb, [&] { (void)hipStreamWaitValue32(s2, flag, 1, hipStreamWaitValueGte, 0xffffffffu); }, sync);
+    void* pinned = nullptr;
+    CHECK(hipHostMalloc(&pinned, 4096, hipHostMallocDefault));
+    const double t_cp = per_call_us(nb, [&] { (void)hipMemcpyAsync(d_out, pinned, 512, hipMemcpyHostToDevice, s); }, sync);
+    int dev = 0;
+    const double t_setdev = per_call_us(nb, [&] { (void)hipSetDevice(0); }, sync);
+    const double t_getdev = per_call_us(nb, [&] { (void)hipGetDevice(&dev); }, sync);
+    std::printf("hipLaunchKernel: 480-B args 1 block %.2f us, 4-B args %.2f, 480-B args 9000 blocks %.2f; "
+                "hipEventRecord %.2f (no system fence %.2f), hipStreamWaitEvent %.2f, hipStreamWriteValue32 %.2f, "
+                "hipStreamWaitValue32 %.2f, hipMemcpyAsync 512 B H2D %.2f, hipSetDevice %.2f, hipGetDevice %.2f\n",
+                t_empty, t_small, t_bigg, t_rec, t_recf, t_wait, t_wv, t_wtv, t_cp, t_setdev, t_getdev);
 
     for (int n : {1, 8}) {
         vr_target t{};
@@ -106,9 +130,9 @@ int main(int argc, char** argv)
         // the same render captured in a hipGraph, replayed
         hipGraph_t g;
         hipGraphExec_t ge;
-        CHECK(hipStreamBeginCapture(s2, hipStreamCaptureModeThreadLocal));
-        CHECK(vr_render(ctx, &t, s2));
-        CHECK(hipStreamEndCapture(s2, &g));
+        CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
+        CHECK(vr_render(ctx, &t, s));
+        CHECK(hipStreamEndCapture(s, &g));
         CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
         const double t_g = per_call_us(nb, [&] { CHECK(hipGraphLaunch(ge, s)); }, sync);
         std::printf("N=%d band set: vr_render %.2f us, hipGraphLaunch of it %.2f us\n", n, t_r, t_g);

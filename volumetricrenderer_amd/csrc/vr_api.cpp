@@ -144,7 +144,15 @@ struct Ctx {
     double need_pixsteps = 0.0, need_wavesteps = 0.0;   // of the frame whose need is pending
     unsigned defer_entries = 0;    // option "shadow_defer_entries": entry capacity override (tests; 0 = sized from the frame)
     int defer_last = 0;            // the last procedural render ran the deferred passes
-    std::vector<void*> defer_retired;   // outgrown scratch buffers: queued frames may still use them
+    // outgrown scratch buffers: queued frames may still use them.  Each gets an
+    // event recorded on the render stream of the frame that outgrew it, after
+    // that stream has waited for the last procedural render (proc_ev), and is
+    // freed by a later ensure_defer once the event has completed
+    struct Retired {
+        void* p;
+        hipEvent_t ev;             // nullptr until recorded
+    };
+    std::vector<Retired> defer_retired;
     // the procedural scratch (d_sort, d_defer, d_lat) serves one frame at a
     // time: a procedural render on another stream than the last one waits
     // for it (frames in flight on alternating streams, vr_shard.cpp)
@@ -192,21 +200,20 @@ struct Ctx {
         int seg_len = 0;           // segments: steps per segment the lists were built for (0 = none)
         int nseg_tiles = 0;        // segmented tiles (slots of SegArgs.info)
         int icap = 0;              // info entries before the list
-        // the streams that rendered with these lists, and per stream an event
-        // that follows its last render with them.  One stream: the event is
-        // recorded when the lists are retired by a render on it.  Several
-        // streams (frames in flight on alternating streams, vr_shard.cpp): each
-        // render records its stream's event, so a retire waits for every
-        // stream's last render without a host sync.  An event is never
-        // recorded on a remembered stream, which the caller may have destroyed
-        // since: a stream whose last render has no event, other than the
-        // retiring one, retires with a device sync (kMaxRegionStreams; more ->
-        // device sync too).
+        // The streams that rendered with these lists, and per stream an event
+        // recorded after its FIRST render with them (one event per stream and
+        // build, never one per render).  These lists are rewritten two builds
+        // later; by then every stream that used them has either rendered with
+        // the newer lists -- and the newer lists' first-render event on that
+        // stream follows all its renders with these -- or it is the rebuilding
+        // stream itself, whose order covers them.  A stream that is neither
+        // costs a device sync (as do more than kMaxRegionStreams streams).  An
+        // event is never recorded on a remembered stream, which the caller may
+        // have destroyed since (r04's abort), only on the rendering one.
         hipStream_t streams[kMaxRegionStreams] = {};
         hipEvent_t used[kMaxRegionStreams] = {};
-        bool evented[kMaxRegionStreams] = {};   // used[i] follows stream i's last render
+        bool first_rec[kMaxRegionStreams] = {};   // used[i] recorded after stream i's first render
         int nstreams = 0;          // -1: more streams than tracked
-        int nretired = 0;          // used[0 .. nretired) mark the end of the renders before the lists were retired
         hipEvent_t uploaded = nullptr;   // the list upload (on streams[0]); other streams wait for it
         hipStream_t upload_stream = nullptr;
     } region[2];
@@ -587,7 +594,10 @@ try {
     if (c->d_sort) (void)hipFree(c->d_sort);
     (void)hipDeviceSynchronize();   // queued renders may still read the region lists and the scratch
     if (c->d_defer) (void)hipFree(c->d_defer);
-    for (void* q : c->defer_retired) (void)hipFree(q);
+    for (const auto& q : c->defer_retired) {
+        (void)hipFree(q.p);
+        if (q.ev) (void)hipEventDestroy(q.ev);
+    }
     if (c->h_need) (void)hipHostFree(c->h_need);
     if (c->need_ev) (void)hipEventDestroy(c->need_ev);
     if (c->d_lat) (void)hipFree(c->d_lat);
@@ -1256,27 +1266,21 @@ vr_status note_region_stream(Ctx::RegionBuf& rb, hipStream_t s, int* slot)
         return VR_OK;
     }
     if (!rb.used[rb.nstreams]) HIP_TRY(hipEventCreateWithFlags(&rb.used[rb.nstreams], hipEventDisableTiming));
-    rb.evented[rb.nstreams] = false;
+    rb.first_rec[rb.nstreams] = false;
     *slot = rb.nstreams;
     rb.streams[rb.nstreams++] = s;
     return VR_OK;
 }
 
 // After a regions launch on stream s (slot c->region_slot of the current
-// lists): with several streams on the lists, record the stream's event so a
-// retire can wait for it; with one, its last render stays uncovered until
-// the retire records on it
+// lists): the stream's first render with these lists records its event
 vr_status note_region_render(Ctx* c, hipStream_t s)
 {
     if (c->region_cur < 0 || c->region_slot < 0) return VR_OK;
     Ctx::RegionBuf& rb = c->region[c->region_cur];
-    if (c->region_slot >= rb.nstreams) return VR_OK;
-    if (rb.nstreams >= 2) {
-        HIP_TRY(hipEventRecord(rb.used[c->region_slot], s));
-        rb.evented[c->region_slot] = true;
-    } else {
-        rb.evented[c->region_slot] = false;
-    }
+    if (c->region_slot >= rb.nstreams || rb.first_rec[c->region_slot]) return VR_OK;
+    HIP_TRY(hipEventRecord(rb.used[c->region_slot], s));
+    rb.first_rec[c->region_slot] = true;
     return VR_OK;
 }
 
@@ -1317,43 +1321,38 @@ static void poll_region_header(Ctx* c)
     rb.most = c->h_rghdr[10];
 }
 
-// Retire the current lists (events on the streams that rendered with them) and
-// pick the other buffer for new ones, sized for n entries.  host_staging: the
-// host will rewrite the pinned staging copy, so it waits for the renders that
-// last used this buffer; otherwise (a GPU build) `stream` waits for them.
+// Pick the buffer for new lists, sized for n entries: the one the current
+// lists replaced (two builds old), once the renders that used it are done --
+// the new lists are written on `stream` (GPU build, or the upload of a host
+// build), so `stream` waits for the other streams' renders (RegionBuf);
+// host_staging: the host also rewrites that buffer's pinned staging copy,
+// once its last upload has run.
 static vr_status next_region_buf(Ctx* c, size_t n, bool host_staging, hipStream_t stream, int* out)
 {
-    if (c->region_cur >= 0) {   // retire the current lists in the stream order of their renders
-        Ctx::RegionBuf& old = c->region[c->region_cur];
-        old.nretired = 0;
-        bool sync = old.nstreams < 0;
-        for (int i = 0; i < old.nstreams && !sync; ++i)
-            if (!old.evented[i] && old.streams[i] != stream) sync = true;   // an uncovered render elsewhere
-        if (sync) {
-            HIP_TRY(hipDeviceSynchronize());
-        } else {
-            for (int i = 0; i < old.nstreams; ++i)
-                if (!old.evented[i]) HIP_TRY(hipEventRecord(old.used[i], stream));   // this stream: its order covers them
-            old.nretired = old.nstreams;
-        }
-        old.nstreams = 0;
-        c->region_slot = -1;
-    }
+    c->region_slot = -1;
     const int b = c->region_cur < 0 ? 0 : c->region_cur ^ 1;
     Ctx::RegionBuf& rb = c->region[b];
     if (c->rg_pending && c->rg_buf == b) {   // a GPU build into this buffer is still queued
         HIP_TRY(hipEventSynchronize(c->rg_ev));
         poll_region_header(c);
     }
-    for (int i = 0; i < rb.nretired; ++i) {   // its last renders, per stream
-        if (host_staging || rb.d == nullptr) {
-            HIP_TRY(hipEventSynchronize(rb.used[i]));
+    if (host_staging && rb.uploaded && rb.h) HIP_TRY(hipEventSynchronize(rb.uploaded));   // the staging copy is free
+    const Ctx::RegionBuf* newer = c->region_cur >= 0 ? &c->region[c->region_cur] : nullptr;
+    bool sync = rb.nstreams < 0;
+    for (int i = 0; i < rb.nstreams && !sync; ++i) {
+        if (rb.streams[i] == stream) continue;   // this stream's order covers its renders
+        int j = -1;
+        for (int k = 0; newer && k < newer->nstreams; ++k)
+            if (newer->streams[k] == rb.streams[i] && newer->first_rec[k]) j = k;
+        if (j < 0) {
+            sync = true;   // a stream that never rendered with the newer lists
         } else {
-            const vr_status st = stream_wait_pending(stream, rb.used[i]);
+            const vr_status st = stream_wait_pending(stream, newer->used[j]);
             if (st != VR_OK) return st;
         }
     }
-    rb.nretired = 0;
+    if (sync) HIP_TRY(hipDeviceSynchronize());
+    rb.nstreams = 0;
     if (n > rb.cap) {
         if (rb.d) {
             HIP_TRY(hipStreamSynchronize(stream));   // the stream may have queued work on the old list
@@ -1399,13 +1398,14 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
         const size_t need = region_build_bytes((int)n);
         if (need > c->rg_bytes) {
             if (c->d_rg) {
+                // the last build may have been queued on another stream
+                if (c->rg_pending) HIP_TRY(hipEventSynchronize(c->rg_ev));
                 HIP_TRY(hipStreamSynchronize(stream));
                 (void)hipFree(c->d_rg);
             }
             c->d_rg = nullptr;
             c->rg_bytes = 0;
-            HIP_TRY(hipMalloc(&c->d_rg, need));
-            HIP_TRY(hipMemsetAsync(c->d_rg, 0, need, stream));   // the build's counters start at zero
+            HIP_TRY(hipMalloc(&c->d_rg, need));   // every build zeroes its own counters (launch_region_build)
             c->rg_bytes = need;
         }
         if (!c->h_rghdr) {
@@ -1676,8 +1676,9 @@ static vr_status ensure_lattice(Ctx* c, ProcParams* q, hipStream_t s)
 // x 5/4; before one is known it starts at pixels x max_steps / 16 entries.
 // A wave beyond the capacity marches its shadow rays in place, so a frame
 // larger than the scratch is still exact, and the next one gets more.
-// Growing keeps the outgrown buffer until a later device sync (queued frames
-// on other streams may still use it): vr_render never waits for the device.
+// Growing keeps the outgrown buffer until the frames queued before the growth
+// have run (an event, Ctx::Retired; queued frames on other streams may still
+// use it): vr_render never waits for the device.
 // *ok = false (and VR_OK): no usable scratch (shadow_defer_mib too small, or
 // the allocation failed) -- the render then takes the in-wave compaction.
 static vr_status release_defer(Ctx* c)
@@ -1686,7 +1687,10 @@ static vr_status release_defer(Ctx* c)
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipDeviceSynchronize());   // an option change, not a frame: queued renders may use the scratch
     if (c->d_defer) (void)hipFree(c->d_defer);
-    for (void* q : c->defer_retired) (void)hipFree(q);
+    for (const auto& q : c->defer_retired) {
+        (void)hipFree(q.p);
+        if (q.ev) (void)hipEventDestroy(q.ev);
+    }
     c->defer_retired.clear();
     c->d_defer = nullptr;
     c->defer_bytes = 0;
@@ -1700,6 +1704,19 @@ static vr_status release_defer(Ctx* c)
 static vr_status ensure_defer(Ctx* c, const MarchArgs& a, void* sort_buf, ShadowDefer* d, bool* ok)
 {
     *ok = false;
+    // free the outgrown buffers whose frames have run
+    for (size_t i = 0; i < c->defer_retired.size();) {
+        Ctx::Retired& q = c->defer_retired[i];
+        const hipError_t st = q.ev ? hipEventQuery(q.ev) : hipErrorNotReady;
+        if (st == hipSuccess) {
+            (void)hipFree(q.p);
+            (void)hipEventDestroy(q.ev);
+            c->defer_retired.erase(c->defer_retired.begin() + (long)i);
+        } else {
+            if (q.ev) (void)hipGetLastError();   // not an error: still queued
+            ++i;
+        }
+    }
     if (c->shadow_defer_mib == 0) return VR_OK;
     const SortLayout L = sort_layout(a.width, a.out_rows);
     const unsigned long long pixels = (unsigned long long)a.width * (unsigned long long)a.out_rows;
@@ -1763,11 +1780,14 @@ static vr_status ensure_defer(Ctx* c, const MarchArgs& a, void* sort_buf, Shadow
             if (!c->d_defer || L.waves > c->defer_waves) return VR_OK;
         } else {
             if (c->d_defer) {
-                c->defer_retired.push_back(c->d_defer);
+                c->defer_retired.push_back({c->d_defer, nullptr});   // its event: vr_render, before the launch
                 if (c->defer_retired.size() > kMaxDeferRetired) {   // rare: a device sync frees them
                     HIP_TRY(hipDeviceSynchronize());
-                    for (void* q : c->defer_retired) (void)hipFree(q);
-                    c->defer_retired.clear();
+                    for (const auto& q : c->defer_retired) {
+                        (void)hipFree(q.p);
+                        if (q.ev) (void)hipEventDestroy(q.ev);
+                    }
+                    c->defer_retired.clear();   // the device is idle: the old scratch too
                 }
             }
             c->d_defer = nb;
@@ -1975,6 +1995,13 @@ try {
             const vr_status sw = stream_wait_pending(static_cast<hipStream_t>(stream), c->proc_ev);
             if (sw != VR_OK) return sw;
         }
+        // a scratch this frame outgrew: free once every earlier frame has run
+        // (this stream now follows the last procedural render)
+        for (auto& q : c->defer_retired)
+            if (!q.ev) {
+                HIP_TRY(hipEventCreateWithFlags(&q.ev, hipEventDisableTiming));
+                HIP_TRY(hipEventRecord(q.ev, static_cast<hipStream_t>(stream)));
+            }
         HIP_TRY(launch_march_procedural(a, m.early_out > 0.0f, sort_buf, reuse, sc, static_cast<hipStream_t>(stream),
                                         use_defer ? &defer : nullptr, report ? c->d_need : nullptr));
         if (!c->proc_ev) HIP_TRY(hipEventCreateWithFlags(&c->proc_ev, hipEventDisableTiming));

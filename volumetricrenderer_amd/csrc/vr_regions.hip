@@ -219,9 +219,9 @@ hipError_t region_build_preload()
     return hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&rg_tiles));
 }
 
-// Scratch of a build over n tiles.  The per-bin sums and the counters must be
-// zero when the first build starts (the caller zeroes a new scratch); every
-// build leaves them zero for the next.
+// Scratch of a build over n tiles.  Every build zeroes its per-block maxima,
+// per-bin sums and counters first (one memset), so a build that failed
+// part-way cannot leave the next one wrong offsets.
 size_t region_build_bytes(int n)
 {
     return 256 + (size_t)kAngleBins * 8 + 256 + kAngleBins + 256 + 4 * ((size_t)n * 4 + 256) + sort_temp_bytes(n) + 256;
@@ -235,8 +235,9 @@ hipError_t launch_region_build(const RegionBuild& b, void* scratch, unsigned* d_
     const size_t sb = sort_temp_bytes(n);
     RgScratch s = carve(scratch, n, sb);
     const dim3 grid((unsigned)((n + 255) / 256));
-    if (b.order != 0) {   // the per-block maxima start at zero
-        const hipError_t z = hipMemsetAsync(s.bmax, 0, (size_t)n * 4, st);
+    {   // the per-block maxima, per-bin sums and counters start at zero
+        const size_t zb = static_cast<size_t>(reinterpret_cast<char*>(s.counts + 16) - static_cast<char*>(scratch));
+        const hipError_t z = hipMemsetAsync(scratch, 0, zb, st);
         if (z != hipSuccess) return z;
     }
     hipLaunchKernelGGL(rg_tiles, grid, dim3(256), 0, st, b, s);
