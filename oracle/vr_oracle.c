@@ -284,8 +284,50 @@ static void m4_perspective(float fovy, float aspect, float zn, float zf, float* 
     o[11] = -1.0f;
     o[14] = -(zf * zn) / (zf - zn);
 }
-/* glm::inverse (cofactor form) in double precision, used only for W2L. */
-static int m4_inverse_d(const double* m, double* inv);
+/* glm::inverse of a mat4 in float (glm/detail/func_matrix.inl,
+ * compute_inverse<4,4>; the scalar path, no GLM_FORCE_INTRINSICS in
+ * VulkanHeader.h:9-11), op for op, each fp32 op rounded on its own
+ * (-ffp-contract=off): 18 cofactors a*b - c*d; columns
+ * Inv_c = (Vec_a*Fac_x - Vec_b*Fac_y) + Vec_d*Fac_z with the SignA/SignB
+ * flips; det = (x + y) + (z + w) of m[0] * row 0; out = inv * (1/det). */
+static void m4_inverse_glm(const float* mm, float* out)
+{
+#define M(c, r) mm[(c) * 4 + (r)]
+    const float c00 = M(2, 2) * M(3, 3) - M(3, 2) * M(2, 3);
+    const float c02 = M(1, 2) * M(3, 3) - M(3, 2) * M(1, 3);
+    const float c03 = M(1, 2) * M(2, 3) - M(2, 2) * M(1, 3);
+    const float c04 = M(2, 1) * M(3, 3) - M(3, 1) * M(2, 3);
+    const float c06 = M(1, 1) * M(3, 3) - M(3, 1) * M(1, 3);
+    const float c07 = M(1, 1) * M(2, 3) - M(2, 1) * M(1, 3);
+    const float c08 = M(2, 1) * M(3, 2) - M(3, 1) * M(2, 2);
+    const float c10 = M(1, 1) * M(3, 2) - M(3, 1) * M(1, 2);
+    const float c11 = M(1, 1) * M(2, 2) - M(2, 1) * M(1, 2);
+    const float c12 = M(2, 0) * M(3, 3) - M(3, 0) * M(2, 3);
+    const float c14 = M(1, 0) * M(3, 3) - M(3, 0) * M(1, 3);
+    const float c15 = M(1, 0) * M(2, 3) - M(2, 0) * M(1, 3);
+    const float c16 = M(2, 0) * M(3, 2) - M(3, 0) * M(2, 2);
+    const float c18 = M(1, 0) * M(3, 2) - M(3, 0) * M(1, 2);
+    const float c19 = M(1, 0) * M(2, 2) - M(2, 0) * M(1, 2);
+    const float c20 = M(2, 0) * M(3, 1) - M(3, 0) * M(2, 1);
+    const float c22 = M(1, 0) * M(3, 1) - M(3, 0) * M(1, 1);
+    const float c23 = M(1, 0) * M(2, 1) - M(2, 0) * M(1, 1);
+    const float f0[4] = {c00, c00, c02, c03}, f1[4] = {c04, c04, c06, c07}, f2[4] = {c08, c08, c10, c11};
+    const float f3[4] = {c12, c12, c14, c15}, f4[4] = {c16, c16, c18, c19}, f5[4] = {c20, c20, c22, c23};
+    const float v0[4] = {M(1, 0), M(0, 0), M(0, 0), M(0, 0)}, v1[4] = {M(1, 1), M(0, 1), M(0, 1), M(0, 1)};
+    const float v2[4] = {M(1, 2), M(0, 2), M(0, 2), M(0, 2)}, v3[4] = {M(1, 3), M(0, 3), M(0, 3), M(0, 3)};
+    const float sa[4] = {1.0f, -1.0f, 1.0f, -1.0f}, sb[4] = {-1.0f, 1.0f, -1.0f, 1.0f};
+    float inv[16];
+    for (int i = 0; i < 4; ++i) {
+        inv[0 * 4 + i] = ((v1[i] * f0[i] - v2[i] * f1[i]) + v3[i] * f2[i]) * sa[i];
+        inv[1 * 4 + i] = ((v0[i] * f0[i] - v2[i] * f3[i]) + v3[i] * f4[i]) * sb[i];
+        inv[2 * 4 + i] = ((v0[i] * f1[i] - v1[i] * f3[i]) + v3[i] * f5[i]) * sa[i];
+        inv[3 * 4 + i] = ((v0[i] * f2[i] - v1[i] * f4[i]) + v2[i] * f5[i]) * sb[i];
+    }
+    const float dot = (M(0, 0) * inv[0] + M(0, 1) * inv[4]) + (M(0, 2) * inv[8] + M(0, 3) * inv[12]);
+    const float one_over = 1.0f / dot;
+    for (int i = 0; i < 16; ++i) out[i] = inv[i] * one_over;
+#undef M
+}
 
 void vro_reference_shader_data(float aspect, float phi_deg, float theta_deg,
                                float frame_time, float* obj48, float* glob36)
@@ -302,10 +344,7 @@ void vro_reference_shader_data(float aspect, float phi_deg, float theta_deg,
     memcpy(obj48, model, 64);
     memcpy(obj48 + 16, view, 64);
     memcpy(obj48 + 32, proj, 64);
-    double md[16], wd[16];
-    for (int i = 0; i < 16; ++i) md[i] = model[i];
-    m4_inverse_d(md, wd);                                          /* :230 */
-    for (int i = 0; i < 16; ++i) glob36[i] = (float)wd[i];
+    m4_inverse_glm(model, glob36);                                 /* :230 glm::inverse(Model), float */
     glob36[16] = 3.0f; glob36[17] = 3.0f; glob36[18] = 3.0f; glob36[19] = 0.0f;  /* :242 */
     float* ms = glob36 + 20;                                       /* :233-238 */
     memset(ms, 0, 16 * sizeof(float));
@@ -317,6 +356,7 @@ void vro_reference_shader_data(float aspect, float phi_deg, float theta_deg,
  * pixel-centre ray, affine in the pixel coordinates.  Computed in double with
  * a fixed operation order; the product's host code restates the same.
  * ==================================================================== */
+/* 4x4 inverse by cofactors in double (the ray basis, not a glm call) */
 static int m4_inverse_d(const double* m, double* inv)
 {
     double t[16];

@@ -74,6 +74,61 @@ void m4_perspective(float fovy, float aspect, float zn, float zf, float* o)
     o[14] = -(zf * zn) / (zf - zn);
 }
 
+// glm::inverse of a mat4 in float (glm/detail/func_matrix.inl,
+// compute_inverse<4, 4, T, Q>; the scalar path -- the reference defines no
+// GLM_FORCE_INTRINSICS, VulkanHeader.h:9-11), operation for operation: the
+// 18 2x2 cofactors a*b - c*d, the four Inv columns (Vec*Fac - Vec*Fac) +
+// Vec*Fac, the sign flips, the determinant (x + y) + (z + w) of column 0 of
+// m times row 0 of the adjugate, and each element times 1/det.  Each fp32
+// operation rounds on its own (-ffp-contract=off).  The W2L of TestMain.cpp:230.
+void inverse_glm(const float* mm, float* out)
+{
+    auto m = [mm](int c, int r) { return mm[c * 4 + r]; };
+    const float c00 = m(2, 2) * m(3, 3) - m(3, 2) * m(2, 3);
+    const float c02 = m(1, 2) * m(3, 3) - m(3, 2) * m(1, 3);
+    const float c03 = m(1, 2) * m(2, 3) - m(2, 2) * m(1, 3);
+    const float c04 = m(2, 1) * m(3, 3) - m(3, 1) * m(2, 3);
+    const float c06 = m(1, 1) * m(3, 3) - m(3, 1) * m(1, 3);
+    const float c07 = m(1, 1) * m(2, 3) - m(2, 1) * m(1, 3);
+    const float c08 = m(2, 1) * m(3, 2) - m(3, 1) * m(2, 2);
+    const float c10 = m(1, 1) * m(3, 2) - m(3, 1) * m(1, 2);
+    const float c11 = m(1, 1) * m(2, 2) - m(2, 1) * m(1, 2);
+    const float c12 = m(2, 0) * m(3, 3) - m(3, 0) * m(2, 3);
+    const float c14 = m(1, 0) * m(3, 3) - m(3, 0) * m(1, 3);
+    const float c15 = m(1, 0) * m(2, 3) - m(2, 0) * m(1, 3);
+    const float c16 = m(2, 0) * m(3, 2) - m(3, 0) * m(2, 2);
+    const float c18 = m(1, 0) * m(3, 2) - m(3, 0) * m(1, 2);
+    const float c19 = m(1, 0) * m(2, 2) - m(2, 0) * m(1, 2);
+    const float c20 = m(2, 0) * m(3, 1) - m(3, 0) * m(2, 1);
+    const float c22 = m(1, 0) * m(3, 1) - m(3, 0) * m(1, 1);
+    const float c23 = m(1, 0) * m(2, 1) - m(2, 0) * m(1, 1);
+    const float fac[6][4] = {{c00, c00, c02, c03}, {c04, c04, c06, c07}, {c08, c08, c10, c11},
+                             {c12, c12, c14, c15}, {c16, c16, c18, c19}, {c20, c20, c22, c23}};
+    float vec[4][4];   // Vec0..Vec3: (m[1][k], m[0][k], m[0][k], m[0][k])
+    for (int k = 0; k < 4; ++k) {
+        vec[k][0] = m(1, k);
+        vec[k][1] = vec[k][2] = vec[k][3] = m(0, k);
+    }
+    // Inv0 = Vec1*Fac0 - Vec2*Fac1 + Vec3*Fac2, Inv1 = Vec0*Fac0 - Vec2*Fac3 + Vec3*Fac4,
+    // Inv2 = Vec0*Fac1 - Vec1*Fac3 + Vec3*Fac5, Inv3 = Vec0*Fac2 - Vec1*Fac4 + Vec2*Fac5
+    static const int kv[4][3] = {{1, 2, 3}, {0, 2, 3}, {0, 1, 3}, {0, 1, 2}};
+    static const int kf[4][3] = {{0, 1, 2}, {0, 3, 4}, {1, 3, 5}, {2, 4, 5}};
+    float inv[16];
+    for (int col = 0; col < 4; ++col)
+        for (int i = 0; i < 4; ++i) {
+            const float t = (vec[kv[col][0]][i] * fac[kf[col][0]][i] - vec[kv[col][1]][i] * fac[kf[col][1]][i]) +
+                            vec[kv[col][2]][i] * fac[kf[col][2]][i];
+            // SignA (+,-,+,-) on columns 0 and 2, SignB (-,+,-,+) on 1 and 3
+            const bool neg = ((col & 1) == 0) ? (i & 1) : !(i & 1);
+            inv[col * 4 + i] = neg ? -t : t;
+        }
+    const float d0 = m(0, 0) * inv[0 * 4 + 0], d1 = m(0, 1) * inv[1 * 4 + 0];
+    const float d2 = m(0, 2) * inv[2 * 4 + 0], d3 = m(0, 3) * inv[3 * 4 + 0];
+    const float det = (d0 + d1) + (d2 + d3);
+    const float one_over = 1.0f / det;
+    for (int i = 0; i < 16; ++i) out[i] = inv[i] * one_over;
+}
+
 // 4x4 inverse by cofactors, double precision (fixed evaluation order).
 bool inverse_d(const double* m, double* inv)
 {
@@ -128,10 +183,7 @@ void reference_shader_data(float aspect, float phi_deg, float theta_deg, float f
     std::memcpy(obj48, model, 64);
     std::memcpy(obj48 + 16, view, 64);
     std::memcpy(obj48 + 32, proj, 64);
-    double md[16], wd[16];
-    for (int i = 0; i < 16; ++i) md[i] = model[i];
-    inverse_d(md, wd);                                            // :230 glm::inverse(Model)
-    for (int i = 0; i < 16; ++i) glob36[i] = (float)wd[i];
+    inverse_glm(model, glob36);                                   // :230 glm::inverse(Model), in float
     glob36[16] = 3.0f; glob36[17] = 3.0f; glob36[18] = 3.0f; glob36[19] = 0.0f;   // :242
     float* ms = glob36 + 20;                                      // :233-238
     std::memset(ms, 0, 16 * sizeof(float));
