@@ -492,46 +492,108 @@ __device__ __forceinline__ unsigned march_pixel(const MarchArgs& a, const FastCt
 // vr option "count" = 2, the algorithmic work of the roofline (bench.py)
 // WC: the Worley cube comes from the lane's register cache *wc
 // (noise::cellular_table9_cached; the deferred shadow pass)
-template <int TABLE, bool WC = false>
-__device__ __forceinline__ float proc_density(const ProcParams& p, const float4* wt, float scale, float px, float py,
-                                              float pz, unsigned& cells, noise::WorleyCube* wc = nullptr)
+// The loop-invariant operands of proc_density, pinned to VGPRs ONCE, before
+// a kernel's step / sample loops: a VALU op reading an SGPR issues at half
+// rate, and an in_vgpr() inside the density is re-done
+// (v_mov from the SGPR) at every evaluation -- the round-4 shadow pass spent
+// 7 of its ~44 per-sample instructions outside the octaves on those copies.
+#ifndef VR_PROC_ATTR
+#ifdef VR_PROC_WAVES   // timing experiments: the primary procedural marches built for this many waves per SIMD
+#define VR_PROC_ATTR __attribute__((amdgpu_waves_per_eu(VR_PROC_WAVES)))
+#else
+#define VR_PROC_ATTR
+#endif
+#endif
+struct DensityK {
+    float gs, lac, gain, f0, wf, scale;
+    float lat_sy, lat_sz, lat_c;   // TABLE 3: the lattice table's byte-offset fma constants
+};
+template <int TABLE>
+__device__ __forceinline__ DensityK density_k(const ProcParams& p, float scale)
 {
-    const float gs = noise::in_vgpr(p.grid_scale), lac = noise::in_vgpr(p.lacunarity), gain = noise::in_vgpr(p.gain);
-    const float qx = px * gs, qy = py * gs, qz = pz * gs;
-    float f = noise::in_vgpr(p.freq0), amp = 1.0f, fbm = 0.0f;
+    DensityK k;
+    k.gs = noise::in_vgpr(p.grid_scale);
+    k.lac = noise::in_vgpr(p.lacunarity);
+    k.gain = noise::in_vgpr(p.gain);
+    k.f0 = noise::in_vgpr(p.freq0);
+    k.wf = noise::in_vgpr(p.worley_freq);
+    k.scale = noise::in_vgpr(scale);
     if constexpr (TABLE == 3) {
-        // the lattice word of octave o + 1 is loaded while octave o computes
-        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p.lat, (short)0, (int)p.lat_bytes, 0x00020000);
-        const float sy = noise::in_vgpr(p.lat_sy), sz = noise::in_vgpr(p.lat_sz), c = noise::in_vgpr(p.lat_c);
-        const float4* gp = wt + noise::kWorleyN * noise::kWorleyPz;
-        float x = qx * f, y = qy * f, z = qz * f;
-        float xs = floorf(x), ys = floorf(y), zs = floorf(z);
-        auto word = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (unsigned)fmaf(zs, sz, fmaf(ys, sy, fmaf(xs, 8.0f, -c))), 0, 0);
-        for (int o = 0; o < p.octaves; ++o) {
-            const uint2 w = make_uint2(word[0], word[1]);
-            const float cx = x, cy = y, cz = z, cxs = xs, cys = ys, czs = zs;
-            f = f * lac;
-            if (o + 1 < p.octaves) {
-                x = qx * f; y = qy * f; z = qz * f;
-                xs = floorf(x); ys = floorf(y); zs = floorf(z);
-                word = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (unsigned)fmaf(zs, sz, fmaf(ys, sy, fmaf(xs, 8.0f, -c))), 0, 0);
-            }
-            const float pn = noise::perlin_lat(gp, w, cx, cy, cz, cxs, cys, czs);
-            fbm = fmaf(amp, pn, fbm);
-            amp = amp * gain;
-        }
+        k.lat_sy = noise::in_vgpr(p.lat_sy);
+        k.lat_sz = noise::in_vgpr(p.lat_sz);
+        k.lat_c = noise::in_vgpr(p.lat_c);
     } else {
+        k.lat_sy = k.lat_sz = k.lat_c = 0.0f;
+    }
+    return k;
+}
+
+// fBm over the lattice table (TABLE 3): the lattice word of octave o + 1 is
+// loaded while octave o computes.  OCT > 0: exactly OCT octaves, fully
+// unrolled (no loop-carried register copies, no loop control; the recipe's 4,
+// vr_procedural_defaults); OCT = 0: p.octaves, a loop.  The same operations in
+// the same order either way.
+#ifndef VR_FBM_UNROLL_BY
+#define VR_FBM_UNROLL_BY 1
+#endif
+#ifndef VR_FBM_UNROLL
+#define VR_FBM_UNROLL 0   // timing experiments: the unrolled 4-octave path (VGPRs 75 -> 104 in the shadow pass)
+#endif
+template <int OCT>
+__device__ __forceinline__ float fbm_lat(const ProcParams& p, const DensityK& k, const float4* gp, float qx, float qy,
+                                         float qz)
+{
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p.lat, (short)0, (int)p.lat_bytes, 0x00020000);
+    float f = k.f0, amp = 1.0f, fbm = 0.0f;
+    float x = qx * f, y = qy * f, z = qz * f;
+    float xs = floorf(x), ys = floorf(y), zs = floorf(z);
+    auto word = __builtin_amdgcn_raw_buffer_load_b64(
+        rsrc, (unsigned)fmaf(zs, k.lat_sz, fmaf(ys, k.lat_sy, fmaf(xs, 8.0f, -k.lat_c))), 0, 0);
+    const int n = OCT > 0 ? OCT : p.octaves;
+#pragma unroll VR_FBM_UNROLL_BY
+    for (int o = 0; o < (OCT > 0 ? OCT : n); ++o) {
+        const uint2 w = make_uint2(word[0], word[1]);
+        const float cx = x, cy = y, cz = z, cxs = xs, cys = ys, czs = zs;
+        f = f * k.lac;
+        if (o + 1 < n) {
+            x = qx * f; y = qy * f; z = qz * f;
+            xs = floorf(x); ys = floorf(y); zs = floorf(z);
+            word = __builtin_amdgcn_raw_buffer_load_b64(
+                rsrc, (unsigned)fmaf(zs, k.lat_sz, fmaf(ys, k.lat_sy, fmaf(xs, 8.0f, -k.lat_c))), 0, 0);
+        }
+        const float pn = noise::perlin_lat(gp, w, cx, cy, cz, cxs, cys, czs);
+        fbm = fmaf(amp, pn, fbm);
+        amp = amp * k.gain;
+    }
+    return fbm;
+}
+
+template <int TABLE, bool WC = false>
+__device__ __forceinline__ float proc_density(const ProcParams& p, const DensityK& k, const float4* wt, float px,
+                                              float py, float pz, unsigned& cells, noise::WorleyCube* wc = nullptr)
+{
+    const float qx = px * k.gs, qy = py * k.gs, qz = pz * k.gs;
+    float fbm = 0.0f;
+    if constexpr (TABLE == 3) {
+        const float4* gp = wt + noise::kWorleyN * noise::kWorleyPz;
+#if VR_FBM_UNROLL
+        fbm = p.octaves == VR_FBM_UNROLL ? fbm_lat<VR_FBM_UNROLL>(p, k, gp, qx, qy, qz) : fbm_lat<0>(p, k, gp, qx, qy, qz);
+#else
+        fbm = fbm_lat<0>(p, k, gp, qx, qy, qz);
+#endif
+    } else {
+        float f = k.f0, amp = 1.0f;
         for (int o = 0; o < p.octaves; ++o) {
             float pn;
             if constexpr (TABLE == 2) pn = noise::perlin_gp(wt + noise::kWorleyN * noise::kWorleyPz, p.seed_fbm, qx * f, qy * f, qz * f);
             else if constexpr (TABLE == 1) pn = noise::perlin_gp(wt + p.wt_n * p.wt_pz, p.seed_fbm, qx * f, qy * f, qz * f);
             else pn = noise::perlin(p.seed_fbm, qx * f, qy * f, qz * f);
             fbm = fmaf(amp, pn, fbm);
-            f = f * lac;
-            amp = amp * gain;
+            f = f * k.lac;
+            amp = amp * k.gain;
         }
     }
-    const float wf = noise::in_vgpr(p.worley_freq);
+    const float wf = k.wf;
     float f1;
     if constexpr (TABLE >= 2) {
         bool full;
@@ -543,7 +605,7 @@ __device__ __forceinline__ float proc_density(const ProcParams& p, const float4*
         else f1 = noise::cellular(p.seed_worley, qx * wf, qy * wf, qz * wf) + 1.0f;
         if (p.count_evals == 2) cells += 27u;
     }
-    return fmaxf(fbm * (1.0f - f1), 0.0f) * noise::in_vgpr(scale);
+    return fmaxf(fbm * (1.0f - f1), 0.0f) * k.scale;
 }
 
 // Pixel value of the procedural march: single scatter, or frag.glsl:76-80.
@@ -568,15 +630,16 @@ __device__ __forceinline__ unsigned march_pixel_proc(const MarchArgs& a, const f
     int i = 0;
     unsigned evals = 0;   // shadow density evaluations
     unsigned cells = 0;   // Worley cells computed (count mode 2)
+    const DensityK dk = density_k<TABLE>(p, a.scale);
     for (; i < r.n; ++i) {
-        const float rho = proc_density<TABLE>(p, wt, a.scale, P0, P1, P2, cells);
+        const float rho = proc_density<TABLE>(p, dk, wt, P0, P1, P2, cells);
         if constexpr (SHADOW) {
             if (rho > 0.0f) {
                 float q0 = P0, q1 = P1, q2 = P2, sl = 0.0f;
                 for (int j = 0; j < p.shadow_steps; ++j) {
                     q0 = q0 + p.lstep[0]; q1 = q1 + p.lstep[1]; q2 = q2 + p.lstep[2];
                     if (q0 >= 0.0f && q0 <= 1.0f && q1 >= 0.0f && q1 <= 1.0f && q2 >= 0.0f && q2 <= 1.0f) {
-                        sl = sl + proc_density<TABLE>(p, wt, a.scale, q0, q1, q2, cells);
+                        sl = sl + proc_density<TABLE>(p, dk, wt, q0, q1, q2, cells);
                         ++evals;
                     }
                 }
@@ -650,11 +713,12 @@ __device__ __forceinline__ unsigned march_pixel_proc_compact(const MarchArgs& a,
     bool act = r.n > 0;
     unsigned evals = 0;
     unsigned cells = 0;   // Worley cells this lane computed (count mode 2), primary and dealt
+    const DensityK dk = density_k<TABLE>(p, a.scale);
     for (;;) {
         act = act && i < r.n;
         if (__ballot(act) == 0) break;
         float rho = 0.0f;
-        if (act) rho = proc_density<TABLE>(p, wt, a.scale, P0, P1, P2, cells);
+        if (act) rho = proc_density<TABLE>(p, dk, wt, P0, P1, P2, cells);
         const bool need = act && rho > 0.0f;
         const unsigned long long m = __ballot(need);
         if (m) {
@@ -708,7 +772,7 @@ __device__ __forceinline__ unsigned march_pixel_proc_compact(const MarchArgs& a,
                     const float4 pk = sh->p[kk];
                     float q0 = pk.x, q1 = pk.y, q2 = pk.z;
                     for (int jj = 0; jj <= j; ++jj) { q0 = q0 + l0; q1 = q1 + l1; q2 = q2 + l2; }
-                    sh->d[shadow_slot(pid)] = proc_density<TABLE>(p, wt, a.scale, q0, q1, q2, cells);
+                    sh->d[shadow_slot(pid)] = proc_density<TABLE>(p, dk, wt, q0, q1, q2, cells);
                     ++evals;
                 }
             }
@@ -1555,7 +1619,7 @@ struct ScanOut {
 }
 
 template <bool SHADOW, bool EARLY, int TABLE>
-__global__ __launch_bounds__(kThreads) void march_proc_sorted(const MarchArgs a, const unsigned* __restrict__ order,
+__global__ __launch_bounds__(kThreads) VR_PROC_ATTR void march_proc_sorted(const MarchArgs a, const unsigned* __restrict__ order,
                                                               const unsigned* __restrict__ total_ptr,
                                                               const unsigned short* __restrict__ keys,
                                                               unsigned fill_positions, unsigned fill_first, int stale)
@@ -1635,7 +1699,7 @@ __global__ __launch_bounds__(kThreads) void march_proc_sorted(const MarchArgs a,
 // march_pixel_proc<true>, so the frame stays bit-exact.
 // (struct ShadowDefer: vr_internal.h)
 template <bool EARLY, int TABLE>
-__global__ __launch_bounds__(kThreads) void march_proc_defer(const MarchArgs a, const unsigned* __restrict__ order,
+__global__ __launch_bounds__(kThreads) VR_PROC_ATTR void march_proc_defer(const MarchArgs a, const unsigned* __restrict__ order,
                                                              const unsigned* __restrict__ total_ptr,
                                                              const unsigned short* __restrict__ keys,
                                                              unsigned fill_positions, unsigned fill_first, int stale,
@@ -1697,11 +1761,12 @@ __global__ __launch_bounds__(kThreads) void march_proc_defer(const MarchArgs a, 
     int i = 0;
     bool act = r.n > 0;
     unsigned cells = 0, s = 0, b = 0;   // b: entries the wave appended so far (wave-uniform)
+    const DensityK dk = density_k<TABLE>(p, a.scale);
     for (;;) {
         act = act && i < r.n;
         if (__ballot(act) == 0) break;
         float rho = 0.0f;
-        if (act) rho = proc_density<TABLE>(p, wt, a.scale, P0, P1, P2, cells);
+        if (act) rho = proc_density<TABLE>(p, dk, wt, P0, P1, P2, cells);
         const bool need = act && rho > 0.0f;
         const unsigned long long m = __ballot(need);
         if (need) ent[b + (unsigned)__popcll(m & lt)] = make_float4(P0, P1, P2, tv * (rho * p.od));
@@ -1785,6 +1850,7 @@ __global__ __launch_bounds__(kThreads) VR_SHADOW_ATTR void proc_shadow_eval(cons
     const unsigned lane = threadIdx.x & 63;
     const float l0 = noise::in_vgpr(p.lstep[0]), l1 = noise::in_vgpr(p.lstep[1]), l2 = noise::in_vgpr(p.lstep[2]);
     unsigned evals = 0, cells = 0;
+    const DensityK dk = density_k<TABLE>(p, a.scale);
     for (unsigned c = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6); c < chunks; c += gridDim.x * (kThreads / 64)) {
         const uint4 mc = d.map[c];   // wave-uniform
         if (lane >= mc.z) continue;
@@ -1795,7 +1861,7 @@ __global__ __launch_bounds__(kThreads) VR_SHADOW_ATTR void proc_shadow_eval(cons
             q0 = q0 + l0; q1 = q1 + l1; q2 = q2 + l2;
             // march_pixel_proc's box test as min3 / max3 (q is never NaN)
             if (fminf(fminf(q0, q1), q2) >= 0.0f && fmaxf(fmaxf(q0, q1), q2) <= 1.0f) {
-                sl = sl + proc_density<TABLE, WC>(p, wt, a.scale, q0, q1, q2, cells, &wc);
+                sl = sl + proc_density<TABLE, WC>(p, dk, wt, q0, q1, q2, cells, &wc);
                 ++evals;
             }
         }
@@ -1824,6 +1890,7 @@ __global__ __launch_bounds__(kThreads) void proc_shadow_eval8(const MarchArgs a,
     const unsigned lane = threadIdx.x & 63, g = lane >> 3, j = lane & 7;
     const float l0 = noise::in_vgpr(p.lstep[0]), l1 = noise::in_vgpr(p.lstep[1]), l2 = noise::in_vgpr(p.lstep[2]);
     unsigned evals = 0, cells = 0;
+    const DensityK dk = density_k<TABLE>(p, a.scale);
     for (unsigned u = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6); u < units; u += gridDim.x * (kThreads / 64)) {
         const uint4 mc = d.map[u >> 3];   // wave-uniform
         const unsigned k = (u & 7u) * 8u + g;   // the group's entry within the chunk
@@ -1837,7 +1904,7 @@ __global__ __launch_bounds__(kThreads) void proc_shadow_eval8(const MarchArgs a,
             float v = 0.0f;
             // march_pixel_proc's box test as min3 / max3 (q is never NaN)
             if (has && r + (int)j < S && fminf(fminf(q0, q1), q2) >= 0.0f && fmaxf(fmaxf(q0, q1), q2) <= 1.0f) {
-                v = proc_density<TABLE>(p, wt, a.scale, q0, q1, q2, cells);
+                v = proc_density<TABLE>(p, dk, wt, q0, q1, q2, cells);
                 ++evals;
             }
 #pragma unroll
