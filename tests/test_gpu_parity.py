@@ -1651,3 +1651,52 @@ def test_exception_never_crosses_the_abi(oracle, vol128, kind, status):
             pl.close()
     with vr.Renderer(0) as r2, pytest.raises(VRError):
         r2.set_option("inject_throw", 3)
+
+
+def test_launch_cache_hits_and_invalidation(oracle, vol128):
+    """The grid launch cache (option launch_cache): repeated renders of an
+    unchanged frame on the same stream and target reuse the cached kernel
+    arguments (the hit counter moves), and every change that alters the
+    launch -- camera, march constants, another target or band set, an option
+    -- is seen: each frame equals the oracle's, bit for bit, alternating two
+    targets on two streams as the multi-GPU loop does."""
+    W, H = 256, 144
+    with vr.Renderer(0) as rr:
+        rr.set_volume(vol128)
+        cams = [vr.reference_shader_data(W / H, a, 0.5 * a) for a in (0.0, 25.0)]
+        m2 = vr.march_defaults(max_steps=64)
+        assert rr.get_option("launch_cache") == 1
+        outs = [rr.alloc_target(W, H, 0), rr.alloc_target(W, H, 0)]
+        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+
+        def ref(cam, m, **band):
+            obj, glob = vr.shader_data_arrays(*cam)
+            return oracle.render(vol128, obj, glob, oracle.from_params(m), W, H, 0, **band)[0]
+        for cam, m in ((cams[0], vr.march_defaults()), (cams[1], vr.march_defaults()), (cams[1], m2)):
+            rr.set_shader_data(*cam)
+            rr.set_march(m)
+            h0 = rr.get_option("launch_cache_hits")
+            for i in range(6):
+                with torch.cuda.stream(streams[i % 2]):
+                    rr.render(W, H, 0, out=outs[i % 2])
+            torch.cuda.synchronize()
+            assert rr.get_option("launch_cache_hits") - h0 >= 4
+            want = ref(cam, m)
+            for o in outs:
+                assert_exact(o.cpu().numpy(), want)
+        # a band set on the same buffers, then the whole frame again
+        band = dict(band_rows=16, band_stride=3, band_first=1)
+        b = rr.render(W, H, 0, **band)
+        torch.cuda.synchronize()
+        assert_exact(b.cpu().numpy(), ref(cams[1], m2, **band))
+        rr.set_option("uniform_skip", 0)
+        rr.render(W, H, 0, out=outs[0])
+        torch.cuda.synchronize()
+        assert_exact(outs[0].cpu().numpy(), ref(cams[1], m2))
+        rr.set_option("launch_cache", 0)
+        h1 = rr.get_option("launch_cache_hits")
+        rr.render(W, H, 0, out=outs[1])
+        rr.render(W, H, 0, out=outs[1])
+        torch.cuda.synchronize()
+        assert rr.get_option("launch_cache_hits") == h1
+        assert_exact(outs[1].cpu().numpy(), ref(cams[1], m2))

@@ -72,6 +72,19 @@ def brick_offset(layout):
     return off
 
 
+def generic_b4(Ry, Rz):
+    """A BRICK4-family geometry of 4-B rows (3 x positions), Ry rows per slice
+    and Rz slices per brick (the bricks overlap by one position per axis)."""
+    By, Bz, brick = Ry - 1, Rz - 1, 4 * Ry * Rz
+    nbx, nby = N // 3 + 1, N // By + 1
+
+    def off(a, b, c):
+        o = (a // 3) * brick + (b // By) * brick * nbx + (c // Bz) * brick * nbx * nby \
+            + (b % By) * 4 + (c % Bz) * 4 * Ry
+        return o, o + 4 * Ry
+    return off, (4 * Ry * Rz) / (3 * By * Bz)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--layout", default="brick4832")
@@ -101,7 +114,12 @@ def main():
     keep = nn.max(1) > 0
     nn, P0, ST = nn[keep], p0[Y, X][keep], st[Y, X][keep]
     print(f"{args.layout} quad {args.quad}: {keep.sum()} tiles with rays, {nn.sum()} executed steps")
-    if args.layout.startswith("r8_"):
+    if args.layout.startswith("b4_"):   # b4_<Ry>_<Rz>: tools/ta_model.py --search
+        _, ry, rz = args.layout.split("_")
+        off, ratio = generic_b4(int(ry), int(rz))
+        print(f"  bytes {ratio:.3f}x the volume")
+        span = 8
+    elif args.layout.startswith("r8_"):
         _, ry, rz = args.layout.split("_")
         off = brick8_offset(int(ry), int(rz))
         span = 16

@@ -94,6 +94,11 @@ constexpr int kRegionKeyLen = 35;
 // (4x the tiles) it keeps K = 1 up to N = 4.
 constexpr long long kSplitOneLane = 6000, kSplitTwoLanes = 1400;
 
+struct Plan {
+    int layout, wrap;
+    bool early;
+};
+
 struct Ctx {
     int device = 0;
     // volume (channel planes; see vr_internal.h Layout)
@@ -232,6 +237,28 @@ struct Ctx {
     // option "inject_throw" (tests of the exception guard): the next vr_render
     // throws std::runtime_error (1) or std::bad_alloc (2) in its host path
     int inject_throw = 0;
+    // Launch cache of the grid march (option "launch_cache", default 1): the
+    // last few renders' kernel arguments keyed by target and stream, valid
+    // while `gen` is unchanged -- every call that can change a grid launch
+    // (shader data, march constants, volume, options, a region-list build or
+    // a GPU build's sizing) bumps it.  A repeated render of an unchanged frame
+    // (the static camera of a frame stream; the two parities of the multi-GPU
+    // loop) then skips the basis, plan and list bookkeeping and only launches.
+    unsigned long long gen = 1;
+    int launch_cache = 1;
+    struct Cached {
+        bool valid = false;
+        unsigned long long gen = 0;
+        vr_target t{};
+        hipStream_t stream = nullptr;
+        MarchArgs a{};
+        Plan pl{};
+        Schedule sc{};
+        int kind = 0;
+        int slot = -1;   // the stream's slot in the region lists (note_region_render)
+    } lc[4];
+    int lc_next = 0;
+    long long lc_hits = 0;         // read-only option "launch_cache_hits"
     uint2* d_lat = nullptr;
     size_t lat_cap = 0;            // bytes allocated
     long long lat_key[3] = {0, 0, -1};
@@ -263,6 +290,7 @@ Ctx* as_ctx(void* p) { return static_cast<Ctx*>(p); }
 
 void free_volume(Ctx* c)
 {
+    ++c->gen;
     if (c->mm_pending) (void)hipEventSynchronize(c->mm_ready);   // the scan still reads d_planar
     c->mm_pending = false;
     if (c->d_planar) (void)hipFree(c->d_planar);
@@ -317,6 +345,7 @@ vr_status ensure_fast_layout(Ctx* c, hipStream_t s)
 // Allocate the planes and repack from a device RGBA8 buffer.
 vr_status install_volume(Ctx* c, const uint8_t* d_rgba, int nx, int ny, int nz, hipStream_t s)
 {
+    ++c->gen;
     free_volume(c);
     const size_t total = (size_t)nx * ny * nz;
     HIP_TRY(hipMalloc(&c->d_planar, 4 * total));
@@ -343,6 +372,7 @@ vr_status resolve_uniform(Ctx* c)
     if (!c->mm_pending) return VR_OK;
     HIP_TRY(hipEventSynchronize(c->mm_ready));
     c->mm_pending = false;
+    ++c->gen;
     c->uniform_mask = 0;
     for (int ch = 0; ch < 4; ++ch)
         if (c->h_mm[ch] == c->h_mm[4 + ch]) {
@@ -396,11 +426,6 @@ int band_rows_packed(int height, int band_rows, int band_stride, int band_first)
     const int nsel = (nb - 1 - band_first) / band_stride + 1;
     return nsel * band_rows;
 }
-
-struct Plan {
-    int layout, wrap;
-    bool early;
-};
 
 vr_status make_plan(Ctx* c, MarchArgs* a, Plan* p)
 {
@@ -551,6 +576,7 @@ try {
             return fail(VR_ERR_INVALID, "vr_set_procedural: parameters must be finite");
     }
     Ctx* c = as_ctx(ctx);
+    ++c->gen;
     c->proc = *p;
     if (p->enabled && p->shadow_steps > 0) {   // normalise in double, round once
         const double l = std::sqrt((double)p->sun_dir[0] * p->sun_dir[0] + (double)p->sun_dir[1] * p->sun_dir[1] +
@@ -627,6 +653,7 @@ try {
     if (!p || !rgba8) return fail(VR_ERR_INVALID, "vr_set_volume: null argument");  // VulkanTexture.cpp:121-124
     if (!dims_ok(nx, ny, nz)) return fail(VR_ERR_INVALID, "vr_set_volume: bad extent %dx%dx%d", nx, ny, nz);
     Ctx* c = as_ctx(p);
+    ++c->gen;
     HIP_TRY(hipSetDevice(c->device));
     const size_t bytes = (size_t)nx * ny * nz * 4;
     uint8_t* staging = nullptr;
@@ -648,6 +675,7 @@ try {
     if (!p || !d_rgba8) return fail(VR_ERR_INVALID, "vr_set_volume_device: null argument");
     if (!dims_ok(nx, ny, nz)) return fail(VR_ERR_INVALID, "vr_set_volume_device: bad extent %dx%dx%d", nx, ny, nz);
     Ctx* c = as_ctx(p);
+    ++c->gen;
     HIP_TRY(hipSetDevice(c->device));
     return install_volume(c, static_cast<const uint8_t*>(d_rgba8), nx, ny, nz, static_cast<hipStream_t>(stream));
 } catch (...) {
@@ -861,6 +889,7 @@ vr_status vr_set_shader_data(void* p, const vr_object_shader_data* osd, const vr
 try {
     if (!p || !osd || !gsd) return fail(VR_ERR_INVALID, "vr_set_shader_data: null argument");
     Ctx* c = as_ctx(p);
+    ++c->gen;
     std::memcpy(c->obj, osd, sizeof(float) * 48);
     std::memcpy(c->glob, gsd, sizeof(float) * 36);
     RayBasis b;
@@ -899,6 +928,7 @@ try {
         if (!(m->box_max[a] != m->box_min[a])) return fail(VR_ERR_INVALID, "vr_set_march: empty box on axis %d", a);
     if (m->reserved[0] || m->reserved[1] || m->reserved[2]) return fail(VR_ERR_INVALID, "vr_set_march: reserved must be 0");
     as_ctx(p)->march = *m;
+    ++as_ctx(p)->gen;
     return VR_OK;
 } catch (...) {
     return caught_exception("vr_set_march");
@@ -919,6 +949,7 @@ try {
         return fail(VR_ERR_INVALID, "vr_set_layout_preference: layout %d is built only with VR_EXPERIMENTS "
                                     "(make EXPERIMENTS=1; measured slower, DESIGN.md sec. 4)", pref);
     Ctx* c = as_ctx(p);
+    ++c->gen;
     HIP_TRY(hipSetDevice(c->device));
     c->layout_pref = pref;
     vr_status st = ensure_fast_layout(c, nullptr);
@@ -932,6 +963,7 @@ vr_status vr_set_option(void* p, const char* name, int value)
 try {
     if (!p || !name) return fail(VR_ERR_INVALID, "vr_set_option: null argument");
     Ctx* c = as_ctx(p);
+    ++c->gen;
     const std::string n(name);
     // variants measured slower than the defaults (vr_internal.h VR_EXPERIMENTS)
     const bool experimental = (n == "schedule" && (value == SCHED_QUEUE || value == SCHED_STRIDED ||
@@ -944,6 +976,11 @@ try {
         return fail(VR_ERR_INVALID, "vr_set_option: %s = %d is built only with VR_EXPERIMENTS (make EXPERIMENTS=1; "
                                     "measured slower, DESIGN.md)", name, value);
     if (n == "layout") return vr_set_layout_preference(p, value);
+    if (n == "launch_cache") {
+        if (value < 0 || value > 1) return fail(VR_ERR_INVALID, "vr_set_option: launch_cache is 0 or 1");
+        c->launch_cache = value;
+        return VR_OK;
+    }
     if (n == "inject_throw") {   // test hook: the next vr_render throws in its host path
         if (value < 0 || value > 2)
             return fail(VR_ERR_INVALID, "vr_set_option: inject_throw is 0, 1 (std::runtime_error) or 2 (std::bad_alloc)");
@@ -1125,6 +1162,8 @@ try {
     }
     if (n == "supertile") return c->supertile;
     if (n == "lat") return c->lat;
+    if (n == "launch_cache") return c->launch_cache;
+    if (n == "launch_cache_hits") return (int)std::min<long long>(c->lc_hits, 0x7fffffff);
     if (n == "experiments") return VR_EXPERIMENTS;   // read-only: the measured-slower variants are built
     if (n == "region_interval") return c->region_interval;
     if (n == "region_gpu") return c->region_gpu;
@@ -1315,6 +1354,7 @@ static void poll_region_header(Ctx* c)
         return;
     }
     c->rg_pending = false;
+    ++c->gen;   // the next launches are sized from the completed build
     if (q != hipSuccess) return;
     Ctx::RegionBuf& rb = c->region[c->rg_buf];
     rb.nwork = c->h_rghdr[9];
@@ -1455,6 +1495,7 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
         c->region_cur = b;
         std::memcpy(c->region_key, key, sizeof key);
         c->renders_since_build = 0;
+        ++c->gen;   // new lists: cached launches point at the old ones
         return VR_OK;
     }
 
@@ -1616,6 +1657,7 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     c->region_cur = b;
     std::memcpy(c->region_key, key, sizeof key);
     c->renders_since_build = 0;
+    ++c->gen;   // new lists: cached launches point at the old ones
     return VR_OK;
 }
 
@@ -1846,6 +1888,20 @@ try {
         c->inject_throw = 0;
         if (k == 2) throw std::bad_alloc();
         throw std::runtime_error("injected by vr option inject_throw");
+    }
+    // an unchanged grid frame on this stream and target: launch the cached arguments
+    const hipStream_t hs = static_cast<hipStream_t>(stream);
+    if (!c->proc.enabled && c->launch_cache && !c->mm_pending && !c->rg_pending) {
+        for (const Ctx::Cached& e : c->lc)
+            if (e.valid && e.gen == c->gen && e.stream == hs && std::memcmp(&e.t, t, sizeof *t) == 0) {
+                HIP_TRY(hipSetDevice(c->device));
+                ++c->renders_since_build;
+                ++c->lc_hits;
+                HIP_TRY(launch_march(e.a, e.pl.layout, e.pl.wrap, e.pl.early, e.sc, hs));
+                if (e.kind != SCHED_REGIONS) return VR_OK;
+                c->region_slot = e.slot;
+                return note_region_render(c, hs);
+            }
     }
     MarchArgs a{};
     RayBasis b;
@@ -2090,8 +2146,21 @@ try {
             }
         }
     }
-    HIP_TRY(launch_march(a, pl.layout, pl.wrap, pl.early, sc, static_cast<hipStream_t>(stream)));
-    if (kind == SCHED_REGIONS) return note_region_render(c, static_cast<hipStream_t>(stream));
+    HIP_TRY(launch_march(a, pl.layout, pl.wrap, pl.early, sc, hs));
+    if (c->launch_cache && sc.seg_tiles == 0 && sc.lat == 0) {   // remember it (not the experiments' scratch paths)
+        Ctx::Cached& e = c->lc[c->lc_next];
+        c->lc_next = (c->lc_next + 1) % (int)(sizeof c->lc / sizeof c->lc[0]);
+        e.valid = true;
+        e.gen = c->gen;
+        e.t = *t;
+        e.stream = hs;
+        e.a = a;
+        e.pl = pl;
+        e.sc = sc;
+        e.kind = kind;
+        e.slot = c->region_slot;
+    }
+    if (kind == SCHED_REGIONS) return note_region_render(c, hs);
     return VR_OK;
 } catch (...) {
     return caught_exception("vr_render");
