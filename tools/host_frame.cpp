@@ -126,6 +126,9 @@ int main(int argc, char** argv)
         t.pixels = d_frame;
         CHECK(vr_render(ctx, &t, s));   // region lists
         sync();
+        CHECK(vr_set_option(ctx, "launch_cache", 0));
+        const double t_r0 = per_call_us(nb, [&] { CHECK(vr_render(ctx, &t, s)); }, sync);
+        CHECK(vr_set_option(ctx, "launch_cache", 1));
         const double t_r = per_call_us(nb, [&] { CHECK(vr_render(ctx, &t, s)); }, sync);
         // the same render captured in a hipGraph, replayed
         hipGraph_t g;
@@ -135,13 +138,17 @@ int main(int argc, char** argv)
         CHECK(hipStreamEndCapture(s, &g));
         CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
         const double t_g = per_call_us(nb, [&] { CHECK(hipGraphLaunch(ge, s)); }, sync);
-        std::printf("N=%d band set: vr_render %.2f us, hipGraphLaunch of it %.2f us\n", n, t_r, t_g);
+        std::printf("N=%d band set: vr_render %.2f us (launch cache off: %.2f), hipGraphLaunch of it %.2f us\n", n, t_r,
+                    t_r0, t_g);
         (void)hipGraphExecDestroy(ge);
         (void)hipGraphDestroy(g);
     }
+    for (int lc : {1, 0})
     for (int n : {1, 8})
         for (int rank : {0, 1})
             for (int rs : {1, 2}) {
+                if (lc == 0 && (n == 1 || rs == 1)) continue;
+                CHECK(vr_set_option(ctx, "launch_cache", lc));
                 if (n == 1 && rank == 1) continue;
                 vr_shard* sh = nullptr;
                 CHECK(vr_shard_alloc(ctx, n, rank, W, H, VR_FMT_RGBA8_UNORM, 16, &sh));
@@ -157,8 +164,8 @@ int main(int argc, char** argv)
                     sync();
                 }
                 std::sort(hv.begin(), hv.end());
-                std::printf("solo loop N=%d rank %d, %d render stream(s): host %.2f us per frame\n", n, rank, rs,
-                            hv[hv.size() / 2]);
+                std::printf("solo loop N=%d rank %d, %d render stream(s)%s: host %.2f us per frame\n", n, rank, rs,
+                            lc ? "" : ", launch cache off", hv[hv.size() / 2]);
                 CHECK(vr_shard_destroy(sh));
             }
     vr_destroy(ctx);
