@@ -142,9 +142,16 @@ typedef struct {
  * This is how the frame is split across GPUs.  band_rows = 0 renders the whole
  * frame.  step_counter (device u64, may be NULL) has the executed ray-steps
  * added to it (the sum of n, frag.glsl:46).                                */
+/* OR'ed into vr_target.format with band_rows > 0: each band is written at its
+ * own frame rows of `pixels` (a whole-frame buffer, `height` rows) instead of
+ * packed from row 0 -- rank 0 of the multi-GPU loop renders its bands straight
+ * into the frame (vr_shard.h), and the assembly skips them
+ * (vr_assemble_frame_ranks).                                               */
+#define VR_TARGET_BANDS_IN_PLACE 0x100
+
 typedef struct {
     int32_t   width, height;
-    int32_t   format;        /* vr_format */
+    int32_t   format;        /* vr_format, optionally | VR_TARGET_BANDS_IN_PLACE */
     int32_t   band_rows, band_stride, band_first;
     void*     pixels;
     size_t    row_pitch;     /* bytes; 0 = tightly packed                  */
@@ -241,6 +248,12 @@ vr_status vr_assemble_bands(void* ctx, const void* d_gathered, size_t rows_per_r
 vr_status vr_assemble_frame(void* ctx, const void* d_gathered, int gathered_format, size_t rows_per_rank,
                             int nranks, int width, int height, int band_rows, int frame_format,
                             void* d_frame, void* stream);
+/* vr_assemble_frame for the ranks first_rank .. nranks-1 only: the rows of
+ * ranks below first_rank are left untouched (rendered in place, with
+ * VR_TARGET_BANDS_IN_PLACE); their gather slots are not read.             */
+vr_status vr_assemble_frame_ranks(void* ctx, const void* d_gathered, int gathered_format, size_t rows_per_rank,
+                                  int nranks, int first_rank, int width, int height, int band_rows,
+                                  int frame_format, void* d_frame, void* stream);
 /* rows that vr_render writes for a band set (for sizing buffers)          */
 int vr_band_rows_packed(int height, int band_rows, int band_stride, int band_first);
 

@@ -1700,3 +1700,63 @@ def test_launch_cache_hits_and_invalidation(oracle, vol128):
         torch.cuda.synchronize()
         assert rr.get_option("launch_cache_hits") == h1
         assert_exact(outs[1].cpu().numpy(), ref(cams[1], m2))
+
+
+@pytest.mark.parametrize("fmt", [0, 1, 2])
+def test_bands_in_place_and_partial_assembly(oracle, vol128, fmt):
+    """VR_TARGET_BANDS_IN_PLACE (vr.h): band sets rendered at their own frame
+    rows of a whole-frame buffer -- every rank's set in turn -- give the plain
+    whole-frame render bit for bit, and a set leaves the other rows as they
+    were (NaN / 0xAB prefill).  vr_assemble_frame_ranks(first_rank = 1) fills
+    the other ranks' rows from grey gather slots and leaves rank 0's rows
+    untouched (the multi-GPU loop's rank 0, vr_shard.cpp)."""
+    import ctypes
+    from volumetricrenderer_amd import _lib
+    W, H, N, B = 301, 170, 3, 16
+    with vr.Renderer(0) as rr:
+        rr.set_volume(vol128)
+        rr.set_shader_data(*vr.reference_shader_data(W / H, 20.0, -10.0))
+        rr.set_march(vr.march_defaults())
+        full = rr.render(W, H, fmt)
+        frame = rr.alloc_target(W, H, fmt)
+        if frame.dtype == torch.float32:
+            frame.fill_(float("nan"))
+        else:
+            frame.fill_(0xAB)
+        pitch = frame.stride(0) * frame.element_size()
+
+        def in_place(first):
+            t = _lib.Target(width=W, height=H, format=fmt | _lib.TARGET_BANDS_IN_PLACE, band_rows=B, band_stride=N,
+                            band_first=first, pixels=frame.data_ptr(), row_pitch=pitch, step_counter=None)
+            _lib.call("vr_render", rr._ctx, ctypes.byref(t), None)
+        in_place(1)
+        torch.cuda.synchronize()
+        got, want = frame.cpu().numpy(), full.cpu().numpy()
+        rows1 = [y for y in range(H) if (y // B) % N == 1]
+        other = [y for y in range(H) if (y // B) % N != 1]
+        assert np.array_equal(got[rows1], want[rows1])
+        if fmt == 0:
+            assert np.isnan(got[other]).all()
+        else:
+            assert (got[other] == 0xAB).all()
+        in_place(0)
+        in_place(2)
+        torch.cuda.synchronize()
+        assert np.array_equal(frame.cpu().numpy(), want)
+        # rank 0 in place, ranks 1..N-1 as grey sets in gather slots
+        g = {0: 5, 1: 3, 2: 4}[fmt]
+        rpr = vr.band_rows_packed(H, B, N, 0)
+        gathered = torch.zeros((N, rpr) + tuple(rr.alloc_target(W, 1, g).shape[1:]), dtype=rr.alloc_target(W, 1, g).dtype,
+                               device="cuda")
+        for r in range(1, N):
+            rr.render(W, H, g, out=gathered[r][: vr.band_rows_packed(H, B, N, r)], band_rows=B, band_stride=N,
+                      band_first=r)
+        if frame.dtype == torch.float32:
+            frame.fill_(float("nan"))
+        else:
+            frame.fill_(0xAB)
+        in_place(0)
+        _lib.call("vr_assemble_frame_ranks", rr._ctx, ctypes.c_void_p(gathered.data_ptr()), g, rpr, N, 1, W, H, B, fmt,
+                  ctypes.c_void_p(frame.data_ptr()), None)
+        torch.cuda.synchronize()
+        assert np.array_equal(frame.cpu().numpy(), want)

@@ -38,6 +38,8 @@ BYTES_PER_PIXEL = {FMT_RGBA32F: 16, FMT_RGBA8_UNORM: 4, FMT_RGBA8_SRGB: 4, FMT_R
 CHANNELS = {FMT_RGBA32F: 4, FMT_RGBA8_UNORM: 4, FMT_RGBA8_SRGB: 4, FMT_R8_UNORM: 1, FMT_R8_SRGB: 1, FMT_R32F: 1}
 GREY_OF = {FMT_RGBA32F: FMT_R32F, FMT_RGBA8_UNORM: FMT_R8_UNORM, FMT_RGBA8_SRGB: FMT_R8_SRGB}
 FLOAT_FORMATS = (FMT_RGBA32F, FMT_R32F)
+# OR'ed into a target's format: bands written at their frame rows (include/vr.h)
+TARGET_BANDS_IN_PLACE = 0x100
 
 c_float_p = ctypes.POINTER(ctypes.c_float)
 c_int_p = ctypes.POINTER(ctypes.c_int)
@@ -128,6 +130,8 @@ _SIGS = {
                                          ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, _vp]),
     "vr_assemble_frame": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, _vp]),
+    "vr_assemble_frame_ranks": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                                               ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, _vp]),
     "vr_band_rows_packed": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "vr_kernel_variant": (ctypes.c_char_p, [_vp]),
     "vr_set_layout_preference": (ctypes.c_int, [_vp, ctypes.c_int]),

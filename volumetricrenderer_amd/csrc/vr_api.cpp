@@ -1874,9 +1874,11 @@ try {
         return fail(VR_ERR_NO_VOLUME, "vr_render: no volume (vr_set_volume / vr_generate_volume)");
     if (!c->has_camera) return fail(VR_ERR_NO_CAMERA, "vr_render: no shader data (vr_set_shader_data)");
     if (t->width <= 0 || t->height <= 0) return fail(VR_ERR_INVALID, "vr_render: bad size %dx%d", t->width, t->height);
-    if (t->format < 0 || t->format > 5) return fail(VR_ERR_INVALID, "vr_render: bad format %d", t->format);
+    const int tfmt = t->format & ~VR_TARGET_BANDS_IN_PLACE;
+    const bool in_place = (t->format & VR_TARGET_BANDS_IN_PLACE) != 0;
+    if (tfmt < 0 || tfmt > 5) return fail(VR_ERR_INVALID, "vr_render: bad format %d", t->format);
     if (!t->pixels) return fail(VR_ERR_INVALID, "vr_render: pixels is null");
-    const int bpp = format_bytes(t->format);
+    const int bpp = format_bytes(tfmt);
     const size_t pitch = t->row_pitch ? t->row_pitch : (size_t)t->width * bpp;
     if (pitch < (size_t)t->width * bpp || pitch % bpp != 0 || ((uintptr_t)t->pixels % bpp) != 0)
         return fail(VR_ERR_INVALID, "vr_render: pitch/alignment (pitch %zu, bpp %d)", pitch, bpp);
@@ -1989,7 +1991,8 @@ try {
     a.num_blocks = 8 * ((a.tiles_y + 7) / 8) * a.tiles_x;
     a.out = t->pixels;
     a.pitch = (long long)pitch;
-    a.format = t->format;
+    a.format = tfmt;
+    a.bands_in_place = in_place && t->band_rows > 0 ? 1 : 0;
     a.step_counter = reinterpret_cast<unsigned long long*>(t->step_counter);
     HIP_TRY(hipSetDevice(c->device));
     if (c->proc.enabled) {
@@ -2184,28 +2187,51 @@ try {
 vr_status vr_assemble_frame(void* p, const void* d_gathered, int gathered_format, size_t rows_per_rank, int nranks,
                             int width, int height, int band_rows, int frame_format, void* d_frame, void* stream)
 try {
+    return vr_assemble_frame_ranks(p, d_gathered, gathered_format, rows_per_rank, nranks, 0, width, height, band_rows,
+                                   frame_format, d_frame, stream);
+} catch (...) {
+    return caught_exception("vr_assemble_frame");
+}
+
+vr_status vr_assemble_frame_ranks(void* p, const void* d_gathered, int gathered_format, size_t rows_per_rank,
+                                  int nranks, int first_rank, int width, int height, int band_rows, int frame_format,
+                                  void* d_frame, void* stream)
+try {
     if (!p || !d_gathered || !d_frame) return fail(VR_ERR_INVALID, "vr_assemble_frame: null argument");
+    if (first_rank < 0 || first_rank > nranks) return fail(VR_ERR_INVALID, "vr_assemble_frame: first_rank %d", first_rank);
+    if (first_rank == nranks) return VR_OK;   // every rank's rows are in place
     if (gathered_format < 0 || gathered_format > 5 || frame_format < 0 || frame_format > 5)
         return fail(VR_ERR_INVALID, "vr_assemble_frame: bad format %d -> %d", gathered_format, frame_format);
     if (gathered_format != frame_format && grey_of(frame_format) != gathered_format)
         return fail(VR_ERR_INVALID, "vr_assemble_frame: format %d does not expand into %d", gathered_format,
                     frame_format);
-    if (gathered_format == frame_format)
-        return vr_assemble_bands(p, d_gathered, rows_per_rank, nranks, width, height, band_rows,
-                                 format_bytes(frame_format), d_frame, stream);
+    if (gathered_format == frame_format) {
+        const int bpp = format_bytes(frame_format);
+        if (nranks <= 0 || width <= 0 || height <= 0 || band_rows <= 0)
+            return fail(VR_ERR_INVALID, "vr_assemble_frame: bad geometry");
+        for (int r = first_rank; r < nranks; ++r)
+            if ((size_t)band_rows_packed(height, band_rows, nranks, r) > rows_per_rank)
+                return fail(VR_ERR_INVALID, "vr_assemble_frame: rows_per_rank %zu too small for rank %d", rows_per_rank, r);
+        Ctx* c = as_ctx(p);
+        HIP_TRY(hipSetDevice(c->device));
+        HIP_TRY(launch_assemble(static_cast<const uint8_t*>(d_gathered), rows_per_rank, nranks, width, height,
+                                band_rows, bpp, first_rank, static_cast<uint8_t*>(d_frame),
+                                static_cast<hipStream_t>(stream)));
+        return VR_OK;
+    }
     if (nranks <= 0 || width <= 0 || height <= 0 || band_rows <= 0)
         return fail(VR_ERR_INVALID, "vr_assemble_frame: bad geometry");
-    for (int r = 0; r < nranks; ++r)
+    for (int r = first_rank; r < nranks; ++r)
         if ((size_t)band_rows_packed(height, band_rows, nranks, r) > rows_per_rank)
             return fail(VR_ERR_INVALID, "vr_assemble_frame: rows_per_rank %zu too small for rank %d", rows_per_rank, r);
     Ctx* c = as_ctx(p);
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(launch_assemble_grey(static_cast<const uint8_t*>(d_gathered), rows_per_rank, nranks, width, height,
-                                 band_rows, frame_format == VR_FMT_RGBA32F, static_cast<uint8_t*>(d_frame),
+                                 band_rows, frame_format == VR_FMT_RGBA32F, first_rank, static_cast<uint8_t*>(d_frame),
                                  static_cast<hipStream_t>(stream)));
     return VR_OK;
 } catch (...) {
-    return caught_exception("vr_assemble_frame");
+    return caught_exception("vr_assemble_frame_ranks");
 }
 
 vr_status vr_assemble_bands(void* p, const void* d_gathered, size_t rows_per_rank, int nranks, int width,
@@ -2221,7 +2247,7 @@ try {
     Ctx* c = as_ctx(p);
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(launch_assemble(static_cast<const uint8_t*>(d_gathered), rows_per_rank, nranks, width, height,
-                            band_rows, bytes_per_pixel, static_cast<uint8_t*>(d_frame),
+                            band_rows, bytes_per_pixel, 0, static_cast<uint8_t*>(d_frame),
                             static_cast<hipStream_t>(stream)));
     return VR_OK;
 } catch (...) {

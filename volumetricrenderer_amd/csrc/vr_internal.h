@@ -208,6 +208,7 @@ struct MarchArgs {
     void* out;
     long long pitch;
     int format;
+    int bands_in_place;          // vr.h VR_TARGET_BANDS_IN_PLACE: packed row orow is stored at its frame row
     unsigned long long* step_counter;
     ProcParams proc;
     int slab_cap;                // LDS slab march (COL48): chunks per channel the slab holds
@@ -321,7 +322,7 @@ __host__ __device__ constexpr int format_bytes(int f) { return f == 0 ? 16 : f <
 __host__ __device__ constexpr int grey_of(int f) { return f == 0 ? 5 : f == 1 ? 3 : f == 2 ? 4 : -1; }
 // grey band sets (1 B or fp32 per pixel) -> RGBA frame rows (vr_assemble_frame)
 hipError_t launch_assemble_grey(const uint8_t* d_gathered, size_t rows_per_rank, int nranks, int width, int height,
-                                int band_rows, bool f32, uint8_t* d_frame, hipStream_t s);
+                                int band_rows, bool f32, int first_rank, uint8_t* d_frame, hipStream_t s);
 hipError_t launch_march_corner8(const MarchArgs& a, int layout, bool early, const Schedule& sc,
                                 hipStream_t s);   // CORNER8 / CORNERH, vr_march_c8.hip
 // latency-mode march for small frame shares (vr_march_lat.hip): sc.split lanes per
@@ -365,7 +366,7 @@ hipError_t launch_pack_recipe(const float* d_g1, const float* d_g2, const float*
                               const float* d_g4, const float* d_minmax, long long total,
                               uint8_t* d_rgba, hipStream_t s);
 hipError_t launch_assemble(const uint8_t* d_gathered, size_t rows_per_rank, int nranks,
-                           int width, int height, int band_rows, int bpp, uint8_t* d_frame,
+                           int width, int height, int band_rows, int bpp, int first_rank, uint8_t* d_frame,
                            hipStream_t s);
 int noise_partials_needed(int nx, int ny, int nz);
 // 16-B-per-lane grid-stride copy of `bytes` (a multiple of 16): the measured HBM roofline

@@ -351,7 +351,12 @@ __device__ __forceinline__ Ray setup_ray(const MarchArgs& a, int x, int orow)
 // R channel only (include/vr.h grey targets).
 __device__ __forceinline__ void store_pixel(const MarchArgs& a, int x, int orow, bool covered, float g)
 {
-    char* row = (char*)a.out + (long long)orow * a.pitch;
+    int trow = orow;
+    if (a.bands_in_place) {   // the band's frame row (vr.h VR_TARGET_BANDS_IN_PLACE)
+        const int bl = orow / a.band_rows;
+        trow = (a.band_first + bl * a.band_stride) * a.band_rows + (orow - bl * a.band_rows);
+    }
+    char* row = (char*)a.out + (long long)trow * a.pitch;
     if (a.format == 0 || a.format == 5) {
         g = covered ? g : 0.0f;
         if (a.format == 0) reinterpret_cast<float4*>(row)[x] = make_float4(g, g, g, 1.0f);

@@ -162,6 +162,7 @@ struct vr_shard {
     uint8_t* gathered[2] = {};        // rank 0: nranks slots of rows_per_rank rows (gformat)
     uint8_t* frame[2] = {};           // rank 0
     hipEvent_t rendered[2] = {}, done[2] = {};
+    hipEvent_t tail[2] = {};          // rank 0: the end of the render streams' frames (vr_shard_run_frames)
     hipEvent_t fence = nullptr;       // vr_shard_barrier: the caller's stream -> comm stream
     int* token = nullptr;             // [0]: vr_shard_barrier's all-reduced int; [1..7]:
                                       // vr_shard_share_volume's agreement vector
@@ -266,6 +267,7 @@ void release(vr_shard* sh)
         if (sh->frame[p]) (void)hipFree(sh->frame[p]);
         if (sh->rendered[p]) (void)hipEventDestroy(sh->rendered[p]);
         if (sh->done[p]) (void)hipEventDestroy(sh->done[p]);
+        if (sh->tail[p]) (void)hipEventDestroy(sh->tail[p]);
     }
     for (hipEvent_t e : sh->timing) (void)hipEventDestroy(e);
     if (sh->fence) (void)hipEventDestroy(sh->fence);
@@ -277,35 +279,54 @@ void release(vr_shard* sh)
     delete sh;
 }
 
-// The parity-p band set this rank renders into.
-uint8_t* render_buf(const vr_shard* sh, int p) { return sh->rank == 0 ? sh->gathered[p] : sh->local[p]; }
+// Rank 0 renders its bands straight into the frame (vr.h
+// VR_TARGET_BANDS_IN_PLACE), so its render and the exchange + assembly of the
+// other ranks' rows share no buffer: neither waits for the other, and the
+// frame needs no event per frame on rank 0 (host time: an event record costs
+// ~2.7 us, a frame of the 1/8 share ~20 us; profiles/r05/host_frame*).  The
+// run's end joins the streams (vr_shard_run_frames).  Other ranks (and
+// loopback, which renders the other ranks' sets here) order render ->
+// exchange -> the next render of the parity with rendered[p] / done[p].
+bool others_here(const vr_shard* sh) { return sh->loopback && !sh->solo; }
 
 vr_status one_frame(vr_shard* sh, int p, hipStream_t s, hipEvent_t t0, hipEvent_t t1)
 {
-    if (sh->pending[p]) HIP_TRY(hipStreamWaitEvent(s, sh->done[p], 0));
+    const bool r0 = sh->rank == 0, here = others_here(sh);
+    if ((!r0 || here) && sh->pending[p]) HIP_TRY(hipStreamWaitEvent(s, sh->done[p], 0));
     vr_target t{};
     t.width = sh->width;
     t.height = sh->height;
-    t.format = sh->gformat;
     t.band_rows = sh->band_rows;
     t.band_stride = sh->nranks;
     t.band_first = sh->rank;
-    t.pixels = render_buf(sh, p);
-    t.row_pitch = sh->gpitch;
+    if (r0) {   // in place: the frame's own rows, the frame's format
+        t.format = sh->format | VR_TARGET_BANDS_IN_PLACE;
+        t.pixels = sh->frame[p];
+        t.row_pitch = sh->pitch;
+    } else {
+        t.format = sh->gformat;
+        t.pixels = sh->local[p];
+        t.row_pitch = sh->gpitch;
+    }
     if (t0) HIP_TRY(hipEventRecord(t0, s));
     if (sh->my_rows > 0) VR_TRY(vr_render(sh->ctx, &t, s));
     if (t1) HIP_TRY(hipEventRecord(t1, s));
-    if (sh->loopback && !sh->solo)   // the other ranks' band sets, rendered here into their gather slots
+    if (here) {   // the other ranks' band sets, rendered here into their gather slots
+        t.format = sh->gformat;
+        t.row_pitch = sh->gpitch;
         for (int r = 1; r < sh->nranks; ++r) {
             t.band_first = r;
             t.pixels = sh->gathered[p] + (size_t)r * sh->rows_per_rank * sh->gpitch;
             if (sh->rows_of[r] > 0) VR_TRY(vr_render(sh->ctx, &t, s));
         }
-    HIP_TRY(hipEventRecord(sh->rendered[p], s));
-    HIP_TRY(hipStreamWaitEvent(sh->comm_stream, sh->rendered[p], 0));
+    }
+    if (!r0 || here) {
+        HIP_TRY(hipEventRecord(sh->rendered[p], s));
+        HIP_TRY(hipStreamWaitEvent(sh->comm_stream, sh->rendered[p], 0));
+    }
     if (sh->nranks > 1 && !sh->loopback) {
         NCCL_TRY(ncclGroupStart());
-        if (sh->rank == 0) {
+        if (r0) {
             for (int r = 1; r < sh->nranks; ++r)
                 if (sh->rows_of[r] > 0)
                     NCCL_TRY(ncclRecv(sh->gathered[p] + (size_t)r * sh->rows_per_rank * sh->gpitch,
@@ -316,11 +337,14 @@ vr_status one_frame(vr_shard* sh, int p, hipStream_t s, hipEvent_t t0, hipEvent_
         }
         NCCL_TRY(ncclGroupEnd());
     }
-    if (sh->rank == 0)
-        VR_TRY(vr_assemble_frame(sh->ctx, sh->gathered[p], sh->gformat, (size_t)sh->rows_per_rank, sh->nranks,
-                                 sh->width, sh->height, sh->band_rows, sh->format, sh->frame[p], sh->comm_stream));
-    HIP_TRY(hipEventRecord(sh->done[p], sh->comm_stream));
-    sh->pending[p] = true;
+    if (r0 && sh->nranks > 1)   // (a solo rehearsal expands whatever its slots hold: the same work)
+        VR_TRY(vr_assemble_frame_ranks(sh->ctx, sh->gathered[p], sh->gformat, (size_t)sh->rows_per_rank, sh->nranks,
+                                       1, sh->width, sh->height, sh->band_rows, sh->format, sh->frame[p],
+                                       sh->comm_stream));
+    if (!r0 || here) {
+        HIP_TRY(hipEventRecord(sh->done[p], sh->comm_stream));
+        sh->pending[p] = true;
+    }
     sh->last = p;
     return VR_OK;
 }
@@ -388,6 +412,7 @@ try {
     for (int p = 0; p < 2 && st == VR_OK; ++p) {
         hip_ok(hipEventCreateWithFlags(&sh->rendered[p], hipEventDisableTiming), "event");
         hip_ok(hipEventCreateWithFlags(&sh->done[p], hipEventDisableTiming), "event");
+        hip_ok(hipEventCreateWithFlags(&sh->tail[p], hipEventDisableTiming), "event");
         if (rank == 0) {
             hip_ok(hipMalloc(&sh->gathered[p], (size_t)nranks * sh->rows_per_rank * sh->gpitch), "gather buffer");
             hip_ok(hipMalloc(&sh->frame[p], (size_t)height * sh->pitch), "frame buffer");
@@ -504,7 +529,21 @@ try {
         const vr_status st = one_frame(sh, p, two ? sh->render_stream[p] : s, t0, t1);
         if (st != VR_OK) return st;
     }
-    if (sh->last >= 0) HIP_TRY(hipStreamWaitEvent(s, sh->done[sh->last], 0));   // the caller's stream sees the frame
+    if (sh->last >= 0 && frames > 0) {   // the caller's stream sees the frame
+        if (sh->rank == 0 && !others_here(sh)) {
+            // rank 0 recorded no event per frame: join the exchange / assembly
+            // stream and the render streams now (the render streams' frames
+            // are the rank's own rows of the frames)
+            HIP_TRY(hipEventRecord(sh->done[sh->last], sh->comm_stream));
+            sh->pending[sh->last] = true;
+            if (two)
+                for (int q = 0; q < 2; ++q) {
+                    HIP_TRY(hipEventRecord(sh->tail[q], sh->render_stream[q]));
+                    HIP_TRY(hipStreamWaitEvent(s, sh->tail[q], 0));
+                }
+        }
+        HIP_TRY(hipStreamWaitEvent(s, sh->done[sh->last], 0));
+    }
     if (host_ms)
         *host_ms = frames ? std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count() / frames
                           : 0.0;

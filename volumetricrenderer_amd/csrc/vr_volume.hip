@@ -301,11 +301,13 @@ __global__ __launch_bounds__(kBlock) void k_pack_recipe(const float* __restrict_
 }
 
 // frame row y lives in band b = y / band_rows, rendered by rank b % nranks as
-// its (b / nranks)-th band.  16-byte chunks when rows allow it.
+// its (b / nranks)-th band.  16-byte chunks when rows allow it.  Rows of ranks
+// below first_rank are left as they are (rendered in place into the frame,
+// vr.h VR_TARGET_BANDS_IN_PLACE).
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_assemble(const T* __restrict__ src, long long rows_per_rank,
                                                      int nranks, int row_elems, int height, int band_rows,
-                                                     T* __restrict__ dst)
+                                                     int first_rank, T* __restrict__ dst)
 {
     const long long total = (long long)height * row_elems;
     for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < total;
@@ -313,6 +315,7 @@ __global__ __launch_bounds__(kBlock) void k_assemble(const T* __restrict__ src, 
         const int y = (int)(i / row_elems), e = (int)(i % row_elems);
         const int b = y / band_rows, r = y - b * band_rows;
         const int rank = b % nranks, lb = b / nranks;
+        if (rank < first_rank) continue;
         const long long srow = (long long)rank * rows_per_rank + (long long)lb * band_rows + r;
         dst[i] = src[srow * row_elems + e];
     }
@@ -351,7 +354,7 @@ __device__ __forceinline__ float4 grey_expand<float, float4>(float v)
 template <typename S, typename D>
 __global__ __launch_bounds__(kBlock) void k_assemble_grey(const S* __restrict__ src, long long rows_per_rank,
                                                           int nranks, int row_elems, int height, int band_rows,
-                                                          D* __restrict__ dst)
+                                                          int first_rank, D* __restrict__ dst)
 {
     const long long total = (long long)height * row_elems;
     for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < total;
@@ -359,6 +362,7 @@ __global__ __launch_bounds__(kBlock) void k_assemble_grey(const S* __restrict__ 
         const int y = (int)(i / row_elems), e = (int)(i % row_elems);
         const int b = y / band_rows, r = y - b * band_rows;
         const int rank = b % nranks, lb = b / nranks;
+        if (rank < first_rank) continue;
         const long long srow = (long long)rank * rows_per_rank + (long long)lb * band_rows + r;
         dst[i] = grey_expand<S, D>(src[srow * row_elems + e]);
     }
@@ -654,43 +658,44 @@ hipError_t launch_stream_copy(const void* src, void* dst, size_t bytes, hipStrea
 }
 
 hipError_t launch_assemble(const uint8_t* d_gathered, size_t rows_per_rank, int nranks, int width, int height,
-                           int band_rows, int bpp, uint8_t* d_frame, hipStream_t s)
+                           int band_rows, int bpp, int first_rank, uint8_t* d_frame, hipStream_t s)
 {
     const long long row_bytes = (long long)width * bpp;
     if (row_bytes % 16 == 0) {
         const int elems = (int)(row_bytes / 16);
         hipLaunchKernelGGL(k_assemble<uint4>, dim3(grid_for((long long)height * elems)), dim3(kBlock), 0, s,
                            reinterpret_cast<const uint4*>(d_gathered), (long long)rows_per_rank, nranks, elems,
-                           height, band_rows, reinterpret_cast<uint4*>(d_frame));
+                           height, band_rows, first_rank, reinterpret_cast<uint4*>(d_frame));
     } else if (row_bytes % 4 == 0) {
         const int elems = (int)(row_bytes / 4);
         hipLaunchKernelGGL(k_assemble<unsigned int>, dim3(grid_for((long long)height * elems)), dim3(kBlock), 0,
                            s, reinterpret_cast<const unsigned int*>(d_gathered), (long long)rows_per_rank, nranks,
-                           elems, height, band_rows, reinterpret_cast<unsigned int*>(d_frame));
+                           elems, height, band_rows, first_rank, reinterpret_cast<unsigned int*>(d_frame));
     } else {   // 1-byte pixels, rows of any width
         const int elems = (int)row_bytes;
         hipLaunchKernelGGL(k_assemble<unsigned char>, dim3(grid_for((long long)height * elems)), dim3(kBlock), 0,
-                           s, d_gathered, (long long)rows_per_rank, nranks, elems, height, band_rows, d_frame);
+                           s, d_gathered, (long long)rows_per_rank, nranks, elems, height, band_rows, first_rank,
+                           d_frame);
     }
     return hipGetLastError();
 }
 
 hipError_t launch_assemble_grey(const uint8_t* d_gathered, size_t rows_per_rank, int nranks, int width, int height,
-                                int band_rows, bool f32, uint8_t* d_frame, hipStream_t s)
+                                int band_rows, bool f32, int first_rank, uint8_t* d_frame, hipStream_t s)
 {
     const dim3 blk(kBlock);
     if (f32) {
         hipLaunchKernelGGL((k_assemble_grey<float, float4>), dim3(grid_for((long long)height * width)), blk, 0, s,
                            reinterpret_cast<const float*>(d_gathered), (long long)rows_per_rank, nranks, width, height,
-                           band_rows, reinterpret_cast<float4*>(d_frame));
+                           band_rows, first_rank, reinterpret_cast<float4*>(d_frame));
     } else if (width % 4 == 0) {
         const int elems = width / 4;
         hipLaunchKernelGGL((k_assemble_grey<unsigned int, uint4>), dim3(grid_for((long long)height * elems)), blk, 0,
                            s, reinterpret_cast<const unsigned int*>(d_gathered), (long long)rows_per_rank, nranks,
-                           elems, height, band_rows, reinterpret_cast<uint4*>(d_frame));
+                           elems, height, band_rows, first_rank, reinterpret_cast<uint4*>(d_frame));
     } else {
         hipLaunchKernelGGL((k_assemble_grey<unsigned char, unsigned int>), dim3(grid_for((long long)height * width)),
-                           blk, 0, s, d_gathered, (long long)rows_per_rank, nranks, width, height, band_rows,
+                           blk, 0, s, d_gathered, (long long)rows_per_rank, nranks, width, height, band_rows, first_rank,
                            reinterpret_cast<unsigned int*>(d_frame));
     }
     return hipGetLastError();
