@@ -93,6 +93,17 @@ int main(int argc, char** argv)
     const double t_empty = per_call_us(nb, [&] { hipLaunchKernelGGL(k_empty, dim3(1), dim3(64), 0, s, big, d_out); }, sync);
     const double t_small = per_call_us(nb, [&] { hipLaunchKernelGGL(k_small, dim3(1), dim3(64), 0, s, 1.0f, d_out); }, sync);
     const double t_bigg = per_call_us(nb, [&] { hipLaunchKernelGGL(k_empty, dim3(9000), dim3(256), 0, s, big, d_out); }, sync);
+    // the same kernel through hipModuleLaunchKernel with its arguments as one buffer
+    hipFunction_t fn = nullptr;
+    CHECK(hipGetFuncBySymbol(&fn, reinterpret_cast<const void*>(&k_empty)));
+    struct {
+        Big b;
+        int* out;
+    } argbuf{big, d_out};
+    size_t argsz = sizeof argbuf;
+    void* extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &argbuf, HIP_LAUNCH_PARAM_BUFFER_SIZE, &argsz, HIP_LAUNCH_PARAM_END};
+    const double t_mod = per_call_us(nb, [&] { (void)hipModuleLaunchKernel(fn, 1, 1, 1, 64, 1, 1, 0, s, nullptr, extra); }, sync);
+    std::printf("hipModuleLaunchKernel (480-B arg buffer) %.2f us\n", t_mod);
     const double t_rec = per_call_us(nb, [&] { (void)hipEventRecord(e, s); }, sync);
     hipEvent_t ef;
     CHECK(hipEventCreateWithFlags(&ef, hipEventDisableTiming | hipEventDisableSystemFence));
