@@ -1,0 +1,124 @@
+"""Per-evaluation VALU mix of the procedural density (verdict r04 #3), from a
+hipcc -S device assembly file: the octave loop (8 LDS reads + the lattice
+load), the rest of one sample (fractions, Worley cube, combine), and the
+27-cell Worley block that (cells - 8) / 27 of the samples also run.  Each
+region's opcodes are classed by tools/isa_hist.py (flop / int / conv / sel /
+move) and costed with the calibrated gfx950 issue cycles (tools/isa_cost.py).
+
+    python tools/proc_isa_report.py FILE.s [KERNEL_SUBSTRING ...] [--octaves 4] [--cells 8.68]
+
+With PMC numbers (SQ_INSTS_VALU per launch, density evaluations per launch,
+GRBM_GUI_ACTIVE) it also gives the measured wave-instructions per 64
+evaluations and the model's VALU issue utilisation (instructions per SIMD
+cycle x calibrated cycles per instruction): --pmc INSTS,EVALS,GUI_ACTIVE.
+"""
+import argparse
+import collections
+import re
+import sys
+
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.abspath(__file__)))
+from isa_cost import cost  # noqa: E402
+from isa_hist import classify, kernel_body  # noqa: E402
+
+
+def loops(body):
+    labels = {m.group(1): i for i, l in enumerate(body) if (m := re.match(r"^(\.LBB\S+):", l))}
+    out = []
+    for i, l in enumerate(body):
+        m = re.search(r"s_cbranch_\w+\s+(\.LBB\S+)|s_branch\s+(\.LBB\S+)", l)
+        if m:
+            tgt = m.group(1) or m.group(2)
+            if tgt in labels and labels[tgt] < i:
+                out.append((labels[tgt], i))
+    return out
+
+
+def instrs(body, lines):
+    for i in sorted(lines):
+        x = body[i].strip()
+        if x and not x.startswith((".", ";")) and not x.endswith(":"):
+            yield x
+
+
+def count(body, lines):
+    n = collections.Counter()
+    for x in instrs(body, lines):
+        op = x.split()[0]
+        if op.startswith("ds_"):
+            n["LDS"] += 1
+        elif op.startswith(("buffer_", "global_")):
+            n["VMEM"] += 1
+        elif op.startswith("v_"):
+            n["VALU"] += 1
+    return n
+
+
+def mix(body, lines):
+    cls, cyc, ops = collections.Counter(), collections.Counter(), collections.Counter()
+    for x in instrs(body, lines):
+        op = re.sub(r"_e(32|64|64_dpp|32_dpp|_sdwa)$", "", x.split()[0])
+        if op.startswith("v_"):
+            c = classify(op)
+            cls[c] += 1
+            cyc[c] += cost(x)[0]
+            ops[op] += 1
+    return cls, cyc, ops
+
+
+def report(path, want, octaves, cells, pmc):
+    body = kernel_body(path, want)
+    ls = loops(body)
+    regions = [(a, b, count(body, range(a, b + 1))) for a, b in ls]
+    oct_ = max((r for r in regions if r[2]["LDS"] == 8 and r[2]["VMEM"] == 1), key=lambda r: r[2]["VALU"])
+    samp = min((r for r in regions if r[2]["LDS"] == 16 and r[0] <= oct_[0] and r[1] >= oct_[1]),
+               key=lambda r: r[1] - r[0])
+    full = min((r for r in regions if r[2]["LDS"] == 43 and r[0] <= samp[0] and r[1] >= samp[1]),
+               key=lambda r: r[1] - r[0])
+    L_oct = set(range(oct_[0], oct_[1] + 1))
+    L_rest = set(range(samp[0], samp[1] + 1)) - L_oct
+    L_full = set(range(full[0], full[1] + 1)) - set(range(samp[0], samp[1] + 1))
+    p_full = max(0.0, (cells - 8.0) / 27.0)
+    parts = [("octave x %d" % octaves, L_oct, octaves), ("rest of the sample", L_rest, 1.0),
+             ("27-cell block x %.3f" % p_full, L_full, p_full)]
+    tot_cls, tot_cyc = collections.Counter(), collections.Counter()
+    print(f"{body[0].split(':')[0]}")
+    for name, L, w in parts:
+        cls, cyc, ops = mix(body, L)
+        print(f"  {name:24s} per pass: {sum(cls.values()):4d} VALU, {sum(cyc.values()):7.1f} issue cycles; "
+              + ", ".join(f"{k} {cls[k]}" for k in ("flop", "int", "conv", "sel", "move")))
+        if name.startswith("octave") or name.startswith("rest"):
+            print("      " + ", ".join(f"{op} {k}" for op, k in ops.most_common(12)))
+        for k in cls:
+            tot_cls[k] += w * cls[k]
+            tot_cyc[k] += w * cyc[k]
+    n, c = sum(tot_cls.values()), sum(tot_cyc.values())
+    print(f"  per density evaluation (static, all lanes active): {n:.1f} VALU, {c:.1f} issue cycles "
+          f"({c / n:.2f} per instruction)")
+    for k in ("flop", "int", "conv", "sel", "move"):
+        print(f"    {k:5s} {tot_cls[k]:6.1f} instr ({tot_cls[k] / n:5.1%}), {tot_cyc[k]:7.1f} cycles ({tot_cyc[k] / c:5.1%})")
+    if pmc:
+        insts, evals, gui = pmc
+        per64 = insts / evals * 64
+        cyc_xcd = gui / 8
+        ipc = insts / (1024 * cyc_xcd)
+        print(f"  PMC: {per64:.1f} wave-instructions per 64 evaluations (static {n:.1f}: lane use {n / per64:.2f}); "
+              f"{ipc:.3f} VALU instructions per SIMD-cycle; x {c / n:.2f} calibrated cycles = VALU issue "
+              f"utilisation {ipc * c / n:.2f}")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("asm")
+    ap.add_argument("kernels", nargs="*", default=["march_proc_sortedILb0ELb0ELi3", "proc_shadow_evalILi3ELb0"])
+    ap.add_argument("--octaves", type=int, default=4)
+    ap.add_argument("--cells", type=float, default=8.68)
+    ap.add_argument("--pmc", default=None, help="INSTS,EVALS,GUI_ACTIVE (one kernel)")
+    a = ap.parse_args()
+    pmc = tuple(float(v) for v in a.pmc.split(",")) if a.pmc else None
+    for k in a.kernels:
+        report(a.asm, k, a.octaves, a.cells, pmc)
+
+
+if __name__ == "__main__":
+    main()

@@ -538,6 +538,9 @@ __device__ __forceinline__ DensityK density_k(const ProcParams& p, float scale)
 // unrolled (no loop-carried register copies, no loop control; the recipe's 4,
 // vr_procedural_defaults); OCT = 0: p.octaves, a loop.  The same operations in
 // the same order either way.
+#ifndef VR_FBM_FENCE
+#define VR_FBM_FENCE 1
+#endif
 #ifndef VR_FBM_UNROLL_BY
 #define VR_FBM_UNROLL_BY 1
 #endif
@@ -555,8 +558,7 @@ __device__ __forceinline__ float fbm_lat(const ProcParams& p, const DensityK& k,
     auto word = __builtin_amdgcn_raw_buffer_load_b64(
         rsrc, (unsigned)fmaf(zs, k.lat_sz, fmaf(ys, k.lat_sy, fmaf(xs, 8.0f, -k.lat_c))), 0, 0);
     const int n = OCT > 0 ? OCT : p.octaves;
-#pragma unroll VR_FBM_UNROLL_BY
-    for (int o = 0; o < (OCT > 0 ? OCT : n); ++o) {
+    auto octave = [&](int o) {
         const uint2 w = make_uint2(word[0], word[1]);
         const float cx = x, cy = y, cz = z, cxs = xs, cys = ys, czs = zs;
         f = f * k.lac;
@@ -569,6 +571,21 @@ __device__ __forceinline__ float fbm_lat(const ProcParams& p, const DensityK& k,
         const float pn = noise::perlin_lat(gp, w, cx, cy, cz, cxs, cys, czs);
         fbm = fmaf(amp, pn, fbm);
         amp = amp * k.gain;
+    };
+    if constexpr (OCT > 0) {
+#pragma unroll
+        for (int o = 0; o < OCT; ++o) {
+            octave(o);
+#if VR_FBM_FENCE
+            // keep each octave's instructions in their own block, so that the
+            // scheduler does not hoist later octaves' loads and LDS reads (and
+            // their registers) into earlier ones
+            __builtin_amdgcn_sched_barrier(0);
+#endif
+        }
+    } else {
+#pragma unroll VR_FBM_UNROLL_BY
+        for (int o = 0; o < n; ++o) octave(o);
     }
     return fbm;
 }
