@@ -19,12 +19,13 @@
 
 namespace {
 
-#define CHECK(x)                                                                  \
-    do {                                                                          \
-        if ((x) != 0) {                                                           \
-            std::fprintf(stderr, "%s failed at %s:%d\n", #x, __FILE__, __LINE__); \
-            std::exit(1);                                                         \
-        }                                                                         \
+#define CHECK(x)                                                                                        \
+    do {                                                                                                \
+        if ((x) != 0) {                                                                                 \
+            std::fprintf(stderr, "%s failed at %s:%d (%s | %s)\n", #x, __FILE__, __LINE__, vr_last_error(), \
+                         vr_shard_last_error());                                                        \
+            std::exit(1);                                                                               \
+        }                                                                                               \
     } while (0)
 
 struct Big {
@@ -102,8 +103,13 @@ int main(int argc, char** argv)
     } argbuf{big, d_out};
     size_t argsz = sizeof argbuf;
     void* extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &argbuf, HIP_LAUNCH_PARAM_BUFFER_SIZE, &argsz, HIP_LAUNCH_PARAM_END};
-    const double t_mod = per_call_us(nb, [&] { (void)hipModuleLaunchKernel(fn, 1, 1, 1, 64, 1, 1, 0, s, nullptr, extra); }, sync);
-    std::printf("hipModuleLaunchKernel (480-B arg buffer) %.2f us\n", t_mod);
+    hipError_t me = hipSuccess;
+    const double t_mod = per_call_us(nb, [&] {
+        const hipError_t r = hipModuleLaunchKernel(fn, 1, 1, 1, 64, 1, 1, 0, s, nullptr, extra);
+        if (r != hipSuccess) me = r;
+    }, sync);
+    (void)hipGetLastError();
+    std::printf("hipModuleLaunchKernel (480-B arg buffer) %.2f us (%s)\n", t_mod, hipGetErrorString(me));
     const double t_rec = per_call_us(nb, [&] { (void)hipEventRecord(e, s); }, sync);
     hipEvent_t ef;
     CHECK(hipEventCreateWithFlags(&ef, hipEventDisableTiming | hipEventDisableSystemFence));
@@ -126,6 +132,8 @@ int main(int argc, char** argv)
                 "hipStreamWaitValue32 %.2f, hipMemcpyAsync 512 B H2D %.2f, hipSetDevice %.2f, hipGetDevice %.2f\n",
                 t_empty, t_small, t_bigg, t_rec, t_recf, t_wait, t_wv, t_wtv, t_cp, t_setdev, t_getdev);
 
+    (void)hipGetLastError();
+    CHECK(hipDeviceSynchronize());
     for (int n : {1, 8}) {
         vr_target t{};
         t.width = W;
