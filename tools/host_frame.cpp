@@ -110,6 +110,29 @@ int main(int argc, char** argv)
     }, sync);
     (void)hipGetLastError();
     std::printf("hipModuleLaunchKernel (480-B arg buffer) %.2f us (%s)\n", t_mod, hipGetErrorString(me));
+    // a launch that records an event at its end (hipExtLaunchKernel's stopEvent)
+    hipEvent_t es;
+    CHECK(hipEventCreateWithFlags(&es, hipEventDisableTiming));
+    void* kargs[] = {&big, &d_out};
+    hipError_t xe = hipSuccess;
+    const double t_ext = per_call_us(nb, [&] {
+        const hipError_t r = hipExtLaunchKernel(reinterpret_cast<const void*>(&k_empty), dim3(1), dim3(64), kargs, 0, s,
+                                                nullptr, es, 0);
+        if (r != hipSuccess) xe = r;
+    }, sync);
+    (void)hipGetLastError();
+    const double t_ext_wait = per_call_us(nb, [&] {
+        (void)hipExtLaunchKernel(reinterpret_cast<const void*>(&k_empty), dim3(1), dim3(64), kargs, 0, s, nullptr, es, 0);
+        (void)hipStreamWaitEvent(s2, es, 0);
+    }, sync);
+    const double t_plain_rec_wait = per_call_us(nb, [&] {
+        hipLaunchKernelGGL(k_empty, dim3(1), dim3(64), 0, s, big, d_out);
+        (void)hipEventRecord(es, s);
+        (void)hipStreamWaitEvent(s2, es, 0);
+    }, sync);
+    std::printf("hipExtLaunchKernel with stopEvent %.2f us (%s); + hipStreamWaitEvent on it %.2f; plain launch + "
+                "hipEventRecord + hipStreamWaitEvent %.2f\n", t_ext, hipGetErrorString(xe), t_ext_wait,
+                t_plain_rec_wait);
     const double t_rec = per_call_us(nb, [&] { (void)hipEventRecord(e, s); }, sync);
     hipEvent_t ef;
     CHECK(hipEventCreateWithFlags(&ef, hipEventDisableTiming | hipEventDisableSystemFence));

@@ -160,6 +160,8 @@ def load(path: str | None = None) -> ctypes.CDLL:
                           "or `make -C volumetricrenderer_amd/csrc`)")
     lib = ctypes.CDLL(p)
     for name, (res, args) in _SIGS.items():
+        if os.environ.get("VR_LIB") and not hasattr(lib, name):
+            continue   # an older build for a timing A/B (VR_LIB) may lack newer entry points
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args
