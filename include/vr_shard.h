@@ -143,6 +143,12 @@ int       vr_shard_get_render_streams(vr_shard* sh);
  * set and whatever the other slots hold).  The frame period and host cost of
  * one rank without its peers (tools/band_scaling.py --native). */
 vr_status vr_shard_set_solo(vr_shard* sh, int on);
+/* Host threads of vr_shard_run: 1 (default) = the caller's thread issues
+ * every frame; 2 = a worker thread issues each frame's exchange half (wait
+ * for the render, RCCL send / receive, rank 0's assembly) while the caller's
+ * thread issues the renders, so the host time per frame is the longer half
+ * instead of the sum.  Results are identical.                             */
+vr_status vr_shard_set_host_threads(vr_shard* sh, int n);
 int       vr_shard_aborted(vr_shard* sh);
 /* Self-test of the deadline loop on the host (no GPU, no RCCL): mode 0 a
  * state that completes after 5 polls, 1 one that fails at the 3rd, 2 one that

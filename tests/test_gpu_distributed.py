@@ -254,8 +254,8 @@ def test_native_share_volume(world, loopback):
 SPIN_DEG = 1.6   # TestMain.cpp:171-184, :222-224: the held A/D key, 100 deg/s x 0.016 s
 
 
-@pytest.mark.parametrize("fmt,render_streams", [(0, 2), (1, 2), (1, 1)])
-def test_native_loopback_spinning_8_ranks(oracle, fmt, render_streams):
+@pytest.mark.parametrize("fmt,render_streams,threads", [(0, 2, 1), (1, 2, 1), (1, 1, 1), (1, 2, 2)])
+def test_native_loopback_spinning_8_ranks(oracle, fmt, render_streams, threads):
     """A moving camera through the native 8-rank frame loop (loopback: this
     process renders every rank's interleaved band set): 40 frames, frame i
     with its own shader data (vr_shard_run_frames, phi += 1.6 deg), 2 in
@@ -274,7 +274,7 @@ def test_native_loopback_spinning_8_ranks(oracle, fmt, render_streams):
         r.set_shader_data(*cams[0])
         r.set_march(vr.march_defaults())
         pl = RcclBandPipeline(r, W, H, fmt, band_rows=16, world=8, rank=0, loopback=True,
-                              render_streams=render_streams)
+                              render_streams=render_streams, host_threads=threads)
         got, done = {}, 0
         try:
             for stop in (1, 33, 40):
@@ -299,8 +299,8 @@ def band_set_of(frame, rank, world, band_rows):
     return frame[rows]
 
 
-@pytest.mark.parametrize("render_streams,interval", [(2, 3), (2, 32), (1, 3)])
-def test_native_solo_rank_spinning(oracle, render_streams, interval):
+@pytest.mark.parametrize("render_streams,interval,threads", [(2, 3, 1), (2, 32, 1), (1, 3, 1), (2, 3, 2)])
+def test_native_solo_rank_spinning(oracle, render_streams, interval, threads):
     """One rank of a 4-rank frame loop rehearsed alone (vr_shard_set_solo:
     its band set only, no exchange) with a moving camera: 24 frames with their
     own shader data on two alternating render streams, the region lists
@@ -320,7 +320,7 @@ def test_native_solo_rank_spinning(oracle, render_streams, interval):
         r.set_shader_data(*cams[0])
         r.set_march(vr.march_defaults())
         pl = RcclBandPipeline(r, W, H, 1, band_rows=16, world=world, rank=rank, loopback=True, solo=True,
-                              render_streams=render_streams)
+                              render_streams=render_streams, host_threads=threads)
         got, done = {}, 0
         try:
             for stop in (1, 7, 20, 24):

@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--native", action="store_true", help="per-rank frame streams through the native loop (solo)")
     ap.add_argument("--streams", default="1,2", help="--native: render streams to compare")
     ap.add_argument("--rounds", type=int, default=3, help="--native: interleaved rounds")
+    ap.add_argument("--threads", type=int, default=1, help="--native: host threads of the frame loop (1 or 2)")
     a = ap.parse_args()
     if a.native:
         return native(a)
@@ -101,6 +102,7 @@ def native(a):
             k, v = o.split("=")
             r.set_option(k, int(v))
         print(f"native frame streams: {a.size}^3, {W}x{H}x{a.steps}, {a.frames} frames per timing, "
+              f"{a.threads} host thread(s), "
               f"variant {r.kernel_variant} {' '.join(a.opt)}", flush=True)
         streams = [int(v) for v in a.streams.split(",")]
         base = {}
@@ -111,7 +113,7 @@ def native(a):
             for first in (range(n) if a.all_ranks else (0,)):
                 for ns in streams:
                     p = RcclBandPipeline(r, W, H, vr.FMT_RGBA8_UNORM, band_rows=a.band_rows, world=n, rank=first,
-                                         loopback=True, solo=True, render_streams=ns)
+                                         loopback=True, solo=True, render_streams=ns, host_threads=a.threads)
                     p.run_frames(8)   # region lists, code objects
                     p.barrier()
                     pipes[(first, ns)] = p

@@ -185,17 +185,20 @@ int main(int argc, char** argv)
         (void)hipGraphExecDestroy(ge);
         (void)hipGraphDestroy(g);
     }
+    for (int th : {1, 2})
     for (int lc : {1, 0})
     for (int n : {1, 8})
         for (int rank : {0, 1})
             for (int rs : {1, 2}) {
-                if (lc == 0 && (n == 1 || rs == 1)) continue;
+                if (lc == 0 && (n == 1 || rs == 1 || th == 2)) continue;
+                if (th == 2 && (n == 1 || rs == 1)) continue;
                 CHECK(vr_set_option(ctx, "launch_cache", lc));
                 if (n == 1 && rank == 1) continue;
                 vr_shard* sh = nullptr;
                 CHECK(vr_shard_alloc(ctx, n, rank, W, H, VR_FMT_RGBA8_UNORM, 16, &sh));
                 CHECK(vr_shard_set_solo(sh, 1));
                 CHECK(vr_shard_set_render_streams(sh, rs));
+                CHECK(vr_shard_set_host_threads(sh, th));
                 CHECK(vr_shard_run(sh, 8, s, 0, nullptr));
                 sync();
                 std::vector<double> hv;
@@ -206,8 +209,8 @@ int main(int argc, char** argv)
                     sync();
                 }
                 std::sort(hv.begin(), hv.end());
-                std::printf("solo loop N=%d rank %d, %d render stream(s)%s: host %.2f us per frame\n", n, rank, rs,
-                            lc ? "" : ", launch cache off", hv[hv.size() / 2]);
+                std::printf("solo loop N=%d rank %d, %d render stream(s)%s, %d host thread(s): host %.2f us per frame\n", n,
+                            rank, rs, lc ? "" : ", launch cache off", th, hv[hv.size() / 2]);
                 CHECK(vr_shard_destroy(sh));
             }
     vr_destroy(ctx);

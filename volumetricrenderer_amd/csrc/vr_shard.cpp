@@ -41,6 +41,7 @@
 #include <exception>
 #include <new>
 #include <string>
+#include <atomic>
 #include <thread>
 #include <vector>
 
@@ -158,6 +159,7 @@ struct vr_shard {
     hipStream_t comm_stream = nullptr;
     hipStream_t render_stream[2] = {};   // one per parity (render_streams == 2)
     int render_streams = 2;           // 1: every frame renders on the caller's stream
+    int host_threads = 1;             // 2: a second host thread issues the exchange half of every frame
     uint8_t* local[2] = {};           // rank > 0: band sets (gformat)
     uint8_t* gathered[2] = {};        // rank 0: nranks slots of rows_per_rank rows (gformat)
     uint8_t* frame[2] = {};           // rank 0
@@ -289,7 +291,10 @@ void release(vr_shard* sh)
 // exchange -> the next render of the parity with rendered[p] / done[p].
 bool others_here(const vr_shard* sh) { return sh->loopback && !sh->solo; }
 
-vr_status one_frame(vr_shard* sh, int p, hipStream_t s, hipEvent_t t0, hipEvent_t t1)
+// The render-stream half of frame (parity p): wait for the exchange that last
+// read the parity's buffers (not rank 0, which renders in place), render, and
+// (not rank 0) mark the render for the exchange.
+vr_status render_half(vr_shard* sh, int p, hipStream_t s, hipEvent_t t0, hipEvent_t t1)
 {
     const bool r0 = sh->rank == 0, here = others_here(sh);
     if ((!r0 || here) && sh->pending[p]) HIP_TRY(hipStreamWaitEvent(s, sh->done[p], 0));
@@ -320,10 +325,17 @@ vr_status one_frame(vr_shard* sh, int p, hipStream_t s, hipEvent_t t0, hipEvent_
             if (sh->rows_of[r] > 0) VR_TRY(vr_render(sh->ctx, &t, s));
         }
     }
-    if (!r0 || here) {
-        HIP_TRY(hipEventRecord(sh->rendered[p], s));
-        HIP_TRY(hipStreamWaitEvent(sh->comm_stream, sh->rendered[p], 0));
-    }
+    if (!r0 || here) HIP_TRY(hipEventRecord(sh->rendered[p], s));
+    return VR_OK;
+}
+
+// The communication-stream half: the exchange of the band sets (rank 0 receives
+// into its gather slots, the others send), rank 0's assembly of the other
+// ranks' rows, and (not rank 0) the mark that frees the parity's buffers.
+vr_status comm_half(vr_shard* sh, int p)
+{
+    const bool r0 = sh->rank == 0, here = others_here(sh);
+    if (!r0 || here) HIP_TRY(hipStreamWaitEvent(sh->comm_stream, sh->rendered[p], 0));
     if (sh->nranks > 1 && !sh->loopback) {
         NCCL_TRY(ncclGroupStart());
         if (r0) {
@@ -345,8 +357,30 @@ vr_status one_frame(vr_shard* sh, int p, hipStream_t s, hipEvent_t t0, hipEvent_
         HIP_TRY(hipEventRecord(sh->done[p], sh->comm_stream));
         sh->pending[p] = true;
     }
+    return VR_OK;
+}
+
+vr_status one_frame(vr_shard* sh, int p, hipStream_t s, hipEvent_t t0, hipEvent_t t1)
+{
+    SH_TRY(render_half(sh, p, s, t0, t1));
+    SH_TRY(comm_half(sh, p));
     sh->last = p;
     return VR_OK;
+}
+
+// Spin (then yield) until `ready()` or `stop`; false at the deadline.
+template <class F>
+bool wait_host(F ready, const std::atomic<bool>& stop, double timeout_s)
+{
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int k = 0;; ++k) {
+        if (ready()) return true;
+        if (stop.load(std::memory_order_acquire)) return false;
+        if ((k & 1023) == 1023) {
+            if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s) return false;
+            std::this_thread::yield();
+        }
+    }
 }
 
 }  // namespace
@@ -520,14 +554,71 @@ try {
         HIP_TRY(hipEventRecord(sh->fence, s));
         for (hipStream_t rs : sh->render_stream) HIP_TRY(hipStreamWaitEvent(rs, sh->fence, 0));
     }
-    for (int i = 0; i < frames; ++i) {
-        const int p = sh->last < 0 ? 0 : sh->last ^ 1;
-        const bool samp = kernel_ms && i % sample_every == 0;
-        hipEvent_t t0 = samp ? sh->timing[2 * next] : nullptr, t1 = samp ? sh->timing[2 * next + 1] : nullptr;
-        if (samp) ++next;
-        if (osd) VR_TRY(vr_set_shader_data(sh->ctx, &osd[i], &gsd[i]));   // this frame's camera
-        const vr_status st = one_frame(sh, p, two ? sh->render_stream[p] : s, t0, t1);
-        if (st != VR_OK) return st;
+    if (sh->host_threads == 2 && frames > 1) {
+        // Two host threads: this one issues the render halves, a worker the
+        // exchange halves, so a frame's host time is the longer half, not the
+        // sum (an event record or a launch costs ~3-5 us).
+        // Frame i's exchange is issued after its render (rendered[p] recorded);
+        // frame i's render after frame i-2's exchange (done[p] recorded, and
+        // rendered[p] no longer awaited).
+        const int p0 = sh->last < 0 ? 0 : sh->last ^ 1;
+        std::atomic<int> rdone{0}, cdone{0};
+        std::atomic<bool> stop{false};
+        vr_status wst = VR_OK;
+        std::string werr;
+        std::thread worker([&] {
+            if (hipSetDevice(sh->device) != hipSuccess) {
+                wst = fail(VR_ERR_HIP, "vr_shard_run: worker hipSetDevice");
+            } else {
+                for (int i = 0; i < frames; ++i) {
+                    if (!wait_host([&] { return rdone.load(std::memory_order_acquire) > i; }, stop, sh->timeout_s)) {
+                        if (!stop.load()) wst = fail(VR_ERR_TIMEOUT, "vr_shard_run: render thread stalled");
+                        break;
+                    }
+                    wst = comm_half(sh, (p0 + i) & 1);
+                    if (wst != VR_OK) break;
+                    cdone.store(i + 1, std::memory_order_release);
+                }
+            }
+            if (wst != VR_OK) {
+                werr = g_err;
+                stop.store(true, std::memory_order_release);
+            }
+        });
+        vr_status mst = VR_OK;
+        for (int i = 0; i < frames && mst == VR_OK; ++i) {
+            if (i >= 2 && !wait_host([&] { return cdone.load(std::memory_order_acquire) >= i - 1; }, stop, sh->timeout_s))
+                break;   // the worker failed (its status is reported) or stalled
+            const int p = (p0 + i) & 1;
+            const bool samp = kernel_ms && i % sample_every == 0;
+            hipEvent_t t0 = samp ? sh->timing[2 * next] : nullptr, t1 = samp ? sh->timing[2 * next + 1] : nullptr;
+            if (samp) ++next;
+            if (osd) {
+                mst = vr_set_shader_data(sh->ctx, &osd[i], &gsd[i]);
+                if (mst != VR_OK) mst = fail(mst, "vr_set_shader_data: %s", vr_last_error());
+            }
+            if (mst == VR_OK) mst = render_half(sh, p, two ? sh->render_stream[p] : s, t0, t1);
+            if (mst == VR_OK) rdone.store(i + 1, std::memory_order_release);
+        }
+        if (mst != VR_OK) stop.store(true, std::memory_order_release);
+        worker.join();
+        if (mst != VR_OK) return mst;
+        if (wst != VR_OK) {
+            g_err = werr;
+            return wst;
+        }
+        if (cdone.load() != frames) return fail(VR_ERR_TIMEOUT, "vr_shard_run: render thread stalled");
+        sh->last = (p0 + frames - 1) & 1;
+    } else {
+        for (int i = 0; i < frames; ++i) {
+            const int p = sh->last < 0 ? 0 : sh->last ^ 1;
+            const bool samp = kernel_ms && i % sample_every == 0;
+            hipEvent_t t0 = samp ? sh->timing[2 * next] : nullptr, t1 = samp ? sh->timing[2 * next + 1] : nullptr;
+            if (samp) ++next;
+            if (osd) VR_TRY(vr_set_shader_data(sh->ctx, &osd[i], &gsd[i]));   // this frame's camera
+            const vr_status st = one_frame(sh, p, two ? sh->render_stream[p] : s, t0, t1);
+            if (st != VR_OK) return st;
+        }
     }
     if (sh->last >= 0 && frames > 0) {   // the caller's stream sees the frame
         if (sh->rank == 0 && !others_here(sh)) {
@@ -702,6 +793,15 @@ try {
 }
 
 int vr_shard_get_render_streams(vr_shard* sh) { return sh ? sh->render_streams : 0; }
+
+vr_status vr_shard_set_host_threads(vr_shard* sh, int n)
+try {
+    if (!sh || (n != 1 && n != 2)) return fail(VR_ERR_INVALID, "vr_shard_set_host_threads: need a shard and n = 1 or 2");
+    sh->host_threads = n;
+    return VR_OK;
+} catch (...) {
+    return caught_exception("vr_shard_set_host_threads");
+}
 
 vr_status vr_shard_set_solo(vr_shard* sh, int on)
 try {

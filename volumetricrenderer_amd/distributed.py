@@ -285,7 +285,7 @@ class RcclBandPipeline:
 
     def __init__(self, renderer, width: int, height: int, fmt: int, band_rows: int = 16, world: int = 1,
                  rank: int = 0, group=None, loopback: bool = False, timeout_s: float | None = None,
-                 render_streams: int = 2, solo: bool = False):
+                 render_streams: int = 2, solo: bool = False, host_threads: int = 1):
         """loopback: one process renders all `world` ranks' band sets on its
         GPU and assembles them (no communicator; tests and rehearsals).
         solo (loopback only, any rank): each frame renders only this rank's
@@ -294,6 +294,8 @@ class RcclBandPipeline:
         render_streams: 2 (default) = consecutive frames render on two
         alternating streams and overlap; 1 = on the caller's stream, in turn
         (vr_shard_set_render_streams).
+        host_threads: 2 = a worker thread issues every frame's exchange half
+        (vr_shard_set_host_threads).
         timeout_s: deadline of every host wait on a collective, from the
         communicator init on (vr_shard_set_timeout; default VR_SHARD_TIMEOUT_S
         or 120 s).  A rank whose peer fails gets VRError VR_ERR_TIMEOUT /
@@ -349,6 +351,7 @@ class RcclBandPipeline:
             _lib.shard_call("vr_shard_set_timeout", h, float(timeout_s))
         try:
             _lib.shard_call("vr_shard_set_render_streams", h, int(render_streams))
+            _lib.shard_call("vr_shard_set_host_threads", h, int(host_threads))
             if solo:
                 _lib.shard_call("vr_shard_set_solo", h, 1)
         except _lib.VRError:
