@@ -39,6 +39,9 @@ def main():
     ap.add_argument("--streams", default="1,2", help="--native: render streams to compare")
     ap.add_argument("--rounds", type=int, default=3, help="--native: interleaved rounds")
     ap.add_argument("--threads", type=int, default=1, help="--native: host threads of the frame loop (1 or 2)")
+    ap.add_argument("--gate-ms", type=float, default=0.0,
+                    help="--native: hold the stream with a spin kernel of this many ms while the host queues the "
+                         "frames, so the timing is the GPU's alone (not the host's)")
     a = ap.parse_args()
     if a.native:
         return native(a)
@@ -102,7 +105,7 @@ def native(a):
             k, v = o.split("=")
             r.set_option(k, int(v))
         print(f"native frame streams: {a.size}^3, {W}x{H}x{a.steps}, {a.frames} frames per timing, "
-              f"{a.threads} host thread(s), "
+              f"{a.threads} host thread(s), gate {a.gate_ms} ms, "
               f"variant {r.kernel_variant} {' '.join(a.opt)}", flush=True)
         streams = [int(v) for v in a.streams.split(",")]
         base = {}
@@ -125,6 +128,8 @@ def native(a):
                         p.run_frames(4)
                         p.barrier()
                         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        if a.gate_ms > 0:   # ~2.1 GHz shader clock under this load
+                            torch.cuda._sleep(int(a.gate_ms * 1e-3 * 2.1e9))
                         e0.record()
                         p.run_frames(a.frames)
                         e1.record()

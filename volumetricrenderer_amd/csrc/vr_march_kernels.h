@@ -502,8 +502,11 @@ __device__ __forceinline__ unsigned march_pixel(const MarchArgs& a, const FastCt
 // rate, and an in_vgpr() inside the density is re-done
 // (v_mov from the SGPR) at every evaluation -- the round-4 shadow pass spent
 // 7 of its ~44 per-sample instructions outside the octaves on those copies.
+#ifndef VR_PROC_WAVES   // the primary procedural marches (unrolled fBm) held to 4 waves per SIMD (<= 128 VGPRs)
+#define VR_PROC_WAVES 4
+#endif
 #ifndef VR_PROC_ATTR
-#ifdef VR_PROC_WAVES   // timing experiments: the primary procedural marches built for this many waves per SIMD
+#if VR_PROC_WAVES > 0
 #define VR_PROC_ATTR __attribute__((amdgpu_waves_per_eu(VR_PROC_WAVES)))
 #else
 #define VR_PROC_ATTR
@@ -539,13 +542,17 @@ __device__ __forceinline__ DensityK density_k(const ProcParams& p, float scale)
 // vr_procedural_defaults); OCT = 0: p.octaves, a loop.  The same operations in
 // the same order either way.
 #ifndef VR_FBM_FENCE
-#define VR_FBM_FENCE 1
+#define VR_FBM_FENCE 0
 #endif
 #ifndef VR_FBM_UNROLL_BY
 #define VR_FBM_UNROLL_BY 1
 #endif
 #ifndef VR_FBM_UNROLL
-#define VR_FBM_UNROLL 0   // timing experiments: the unrolled 4-octave path (VGPRs 75 -> 104 in the shadow pass)
+// the primary marches' fBm with the recipe's 4 octaves unrolled (no
+// loop-carried register copies): config 2 -4 % at 4 waves per SIMD
+// (VR_PROC_WAVES), profiles/r05/ab_proc_diet_*.txt; the shadow pass keeps the
+// loop (unrolled it needs 104 VGPRs, and was level or slower)
+#define VR_FBM_UNROLL 4
 #endif
 template <int OCT>
 __device__ __forceinline__ float fbm_lat(const ProcParams& p, const DensityK& k, const float4* gp, float qx, float qy,
@@ -590,7 +597,7 @@ __device__ __forceinline__ float fbm_lat(const ProcParams& p, const DensityK& k,
     return fbm;
 }
 
-template <int TABLE, bool WC = false>
+template <int TABLE, bool WC = false, bool UNROLL = false>
 __device__ __forceinline__ float proc_density(const ProcParams& p, const DensityK& k, const float4* wt, float px,
                                               float py, float pz, unsigned& cells, noise::WorleyCube* wc = nullptr)
 {
@@ -599,7 +606,10 @@ __device__ __forceinline__ float proc_density(const ProcParams& p, const Density
     if constexpr (TABLE == 3) {
         const float4* gp = wt + noise::kWorleyN * noise::kWorleyPz;
 #if VR_FBM_UNROLL
-        fbm = p.octaves == VR_FBM_UNROLL ? fbm_lat<VR_FBM_UNROLL>(p, k, gp, qx, qy, qz) : fbm_lat<0>(p, k, gp, qx, qy, qz);
+        if constexpr (UNROLL)
+            fbm = p.octaves == VR_FBM_UNROLL ? fbm_lat<VR_FBM_UNROLL>(p, k, gp, qx, qy, qz) : fbm_lat<0>(p, k, gp, qx, qy, qz);
+        else
+            fbm = fbm_lat<0>(p, k, gp, qx, qy, qz);
 #else
         fbm = fbm_lat<0>(p, k, gp, qx, qy, qz);
 #endif
@@ -654,7 +664,7 @@ __device__ __forceinline__ unsigned march_pixel_proc(const MarchArgs& a, const f
     unsigned cells = 0;   // Worley cells computed (count mode 2)
     const DensityK dk = density_k<TABLE>(p, a.scale);
     for (; i < r.n; ++i) {
-        const float rho = proc_density<TABLE>(p, dk, wt, P0, P1, P2, cells);
+        const float rho = proc_density<TABLE, false, true>(p, dk, wt, P0, P1, P2, cells);
         if constexpr (SHADOW) {
             if (rho > 0.0f) {
                 float q0 = P0, q1 = P1, q2 = P2, sl = 0.0f;
@@ -740,7 +750,7 @@ __device__ __forceinline__ unsigned march_pixel_proc_compact(const MarchArgs& a,
         act = act && i < r.n;
         if (__ballot(act) == 0) break;
         float rho = 0.0f;
-        if (act) rho = proc_density<TABLE>(p, dk, wt, P0, P1, P2, cells);
+        if (act) rho = proc_density<TABLE, false, true>(p, dk, wt, P0, P1, P2, cells);
         const bool need = act && rho > 0.0f;
         const unsigned long long m = __ballot(need);
         if (m) {
@@ -1788,7 +1798,7 @@ __global__ __launch_bounds__(kThreads) VR_PROC_ATTR void march_proc_defer(const 
         act = act && i < r.n;
         if (__ballot(act) == 0) break;
         float rho = 0.0f;
-        if (act) rho = proc_density<TABLE>(p, dk, wt, P0, P1, P2, cells);
+        if (act) rho = proc_density<TABLE, false, true>(p, dk, wt, P0, P1, P2, cells);
         const bool need = act && rho > 0.0f;
         const unsigned long long m = __ballot(need);
         if (need) ent[b + (unsigned)__popcll(m & lt)] = make_float4(P0, P1, P2, tv * (rho * p.od));
@@ -1872,7 +1882,6 @@ __global__ __launch_bounds__(kThreads) VR_SHADOW_ATTR void proc_shadow_eval(cons
     const unsigned lane = threadIdx.x & 63;
     const float l0 = noise::in_vgpr(p.lstep[0]), l1 = noise::in_vgpr(p.lstep[1]), l2 = noise::in_vgpr(p.lstep[2]);
     unsigned evals = 0, cells = 0;
-    const DensityK dk = density_k<TABLE>(p, a.scale);
     for (unsigned c = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6); c < chunks; c += gridDim.x * (kThreads / 64)) {
         const uint4 mc = d.map[c];   // wave-uniform
         if (lane >= mc.z) continue;
@@ -1883,6 +1892,10 @@ __global__ __launch_bounds__(kThreads) VR_SHADOW_ATTR void proc_shadow_eval(cons
             q0 = q0 + l0; q1 = q1 + l1; q2 = q2 + l2;
             // march_pixel_proc's box test as min3 / max3 (q is never NaN)
             if (fminf(fminf(q0, q1), q2) >= 0.0f && fmaxf(fmaxf(q0, q1), q2) <= 1.0f) {
+                // the operands pinned per sample, as before round 5: hoisted out
+                // of the loops they take the pass from 75 to 86 VGPRs (6 -> 5
+                // waves per SIMD) and it ran 0.4 % slower (profiles/r05)
+                const DensityK dk = density_k<TABLE>(p, a.scale);
                 sl = sl + proc_density<TABLE, WC>(p, dk, wt, q0, q1, q2, cells, &wc);
                 ++evals;
             }
