@@ -76,8 +76,8 @@ def test_gloo_ranks_on_one_gpu_assemble_the_frame(world, share):
     assert all(r == ("ok", True) for r in res), res
 
 
-@pytest.mark.parametrize("fmt,band_rows", [(1, 16), (0, 8)])
-def test_rccl_pipeline_one_rank(fmt, band_rows):
+@pytest.mark.parametrize("fmt,band_rows,on_render", [(1, 16, False), (0, 8, False), (1, 16, True)])
+def test_rccl_pipeline_one_rank(fmt, band_rows, on_render):
     """The native frame loop (libvr_shard.so) with a one-rank RCCL
     communicator: render into the gather slot, (no peers), assemble, 2 frames
     in flight.  The frame equals a plain render; the kernel-time sample is
@@ -92,7 +92,7 @@ def test_rccl_pipeline_one_rank(fmt, band_rows):
         osd, gsd = vr.reference_shader_data(W / H, 10.0, 20.0)
         r.set_shader_data(osd, gsd)
         r.set_march(vr.march_defaults())
-        pl = RcclBandPipeline(r, W, H, fmt, band_rows=band_rows, world=1, rank=0)
+        pl = RcclBandPipeline(r, W, H, fmt, band_rows=band_rows, world=1, rank=0, exchange_on_render=on_render)
         try:
             assert pl.my_rows == pl.rows_per_rank == vr.band_rows_packed(H, band_rows, 1, 0) >= H
             ms = pl.run_frames(5, sample_every=2)
@@ -254,8 +254,9 @@ def test_native_share_volume(world, loopback):
 SPIN_DEG = 1.6   # TestMain.cpp:171-184, :222-224: the held A/D key, 100 deg/s x 0.016 s
 
 
-@pytest.mark.parametrize("fmt,render_streams,threads", [(0, 2, 1), (1, 2, 1), (1, 1, 1), (1, 2, 2)])
-def test_native_loopback_spinning_8_ranks(oracle, fmt, render_streams, threads):
+@pytest.mark.parametrize("fmt,render_streams,threads,on_render", [(0, 2, 1, False), (1, 2, 1, False), (1, 1, 1, False),
+                                                                  (1, 2, 2, False), (0, 2, 1, True)])
+def test_native_loopback_spinning_8_ranks(oracle, fmt, render_streams, threads, on_render):
     """A moving camera through the native 8-rank frame loop (loopback: this
     process renders every rank's interleaved band set): 40 frames, frame i
     with its own shader data (vr_shard_run_frames, phi += 1.6 deg), 2 in
@@ -274,7 +275,7 @@ def test_native_loopback_spinning_8_ranks(oracle, fmt, render_streams, threads):
         r.set_shader_data(*cams[0])
         r.set_march(vr.march_defaults())
         pl = RcclBandPipeline(r, W, H, fmt, band_rows=16, world=8, rank=0, loopback=True,
-                              render_streams=render_streams, host_threads=threads)
+                              render_streams=render_streams, host_threads=threads, exchange_on_render=on_render)
         got, done = {}, 0
         try:
             for stop in (1, 33, 40):
@@ -299,8 +300,10 @@ def band_set_of(frame, rank, world, band_rows):
     return frame[rows]
 
 
-@pytest.mark.parametrize("render_streams,interval,threads", [(2, 3, 1), (2, 32, 1), (1, 3, 1), (2, 3, 2)])
-def test_native_solo_rank_spinning(oracle, render_streams, interval, threads):
+@pytest.mark.parametrize("render_streams,interval,threads,on_render", [(2, 3, 1, False), (2, 32, 1, False),
+                                                                       (1, 3, 1, False), (2, 3, 2, False),
+                                                                       (2, 3, 1, True)])
+def test_native_solo_rank_spinning(oracle, render_streams, interval, threads, on_render):
     """One rank of a 4-rank frame loop rehearsed alone (vr_shard_set_solo:
     its band set only, no exchange) with a moving camera: 24 frames with their
     own shader data on two alternating render streams, the region lists
@@ -320,7 +323,7 @@ def test_native_solo_rank_spinning(oracle, render_streams, interval, threads):
         r.set_shader_data(*cams[0])
         r.set_march(vr.march_defaults())
         pl = RcclBandPipeline(r, W, H, 1, band_rows=16, world=world, rank=rank, loopback=True, solo=True,
-                              render_streams=render_streams, host_threads=threads)
+                              render_streams=render_streams, host_threads=threads, exchange_on_render=on_render)
         got, done = {}, 0
         try:
             for stop in (1, 7, 20, 24):

@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--streams", default="1,2", help="--native: render streams to compare")
     ap.add_argument("--rounds", type=int, default=3, help="--native: interleaved rounds")
     ap.add_argument("--threads", type=int, default=1, help="--native: host threads of the frame loop (1 or 2)")
+    ap.add_argument("--on-render", action="store_true",
+                    help="--native: the exchange on the render streams (vr_shard_set_exchange_streams 1)")
     ap.add_argument("--gate-ms", type=float, default=0.0,
                     help="--native: hold the stream with a spin kernel of this many ms while the host queues the "
                          "frames, so the timing is the GPU's alone (not the host's)")
@@ -105,7 +107,8 @@ def native(a):
             k, v = o.split("=")
             r.set_option(k, int(v))
         print(f"native frame streams: {a.size}^3, {W}x{H}x{a.steps}, {a.frames} frames per timing, "
-              f"{a.threads} host thread(s), gate {a.gate_ms} ms, "
+              f"{a.threads} host thread(s), gate {a.gate_ms} ms, exchange on {'render' if a.on_render else 'comm'} "
+              "streams, "
               f"variant {r.kernel_variant} {' '.join(a.opt)}", flush=True)
         streams = [int(v) for v in a.streams.split(",")]
         base = {}
@@ -116,7 +119,8 @@ def native(a):
             for first in (range(n) if a.all_ranks else (0,)):
                 for ns in streams:
                     p = RcclBandPipeline(r, W, H, vr.FMT_RGBA8_UNORM, band_rows=a.band_rows, world=n, rank=first,
-                                         loopback=True, solo=True, render_streams=ns, host_threads=a.threads)
+                                         loopback=True, solo=True, render_streams=ns, host_threads=a.threads,
+                                         exchange_on_render=a.on_render)
                     p.run_frames(8)   # region lists, code objects
                     p.barrier()
                     pipes[(first, ns)] = p

@@ -218,6 +218,7 @@ _SHARD_SIGS = {
     "vr_shard_get_render_streams": (ctypes.c_int, [_vp]),
     "vr_shard_set_solo": (ctypes.c_int, [_vp, ctypes.c_int]),
     "vr_shard_set_host_threads": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "vr_shard_set_exchange_streams": (ctypes.c_int, [_vp, ctypes.c_int]),
     "vr_shard_poll_selftest": (ctypes.c_int, [ctypes.c_int, ctypes.c_double, c_int_p]),
 }
 # shard functions whose int return is a value, not a vr_status

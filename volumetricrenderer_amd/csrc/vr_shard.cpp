@@ -160,6 +160,12 @@ struct vr_shard {
     hipStream_t render_stream[2] = {};   // one per parity (render_streams == 2)
     int render_streams = 2;           // 1: every frame renders on the caller's stream
     int host_threads = 1;             // 2: a second host thread issues the exchange half of every frame
+    // exchange on the render streams (vr_shard_set_exchange_streams): frame i's
+    // exchange (and rank 0's assembly) follows its render on render_stream[p],
+    // over a communicator of its own per parity (comm for p = 0, comm2 for
+    // p = 1, split from comm at the first such run), with no events at all
+    bool on_render = false;
+    ncclComm_t comm2 = nullptr;
     uint8_t* local[2] = {};           // rank > 0: band sets (gformat)
     uint8_t* gathered[2] = {};        // rank 0: nranks slots of rows_per_rank rows (gformat)
     uint8_t* frame[2] = {};           // rank 0
@@ -181,6 +187,10 @@ namespace {
 
 void abort_comm(vr_shard* sh)
 {
+    if (sh && sh->comm2) {
+        (void)ncclCommAbort(sh->comm2);
+        sh->comm2 = nullptr;
+    }
     if (sh && sh->comm) {
         (void)ncclCommAbort(sh->comm);
         sh->comm = nullptr;
@@ -188,13 +198,19 @@ void abort_comm(vr_shard* sh)
     }
 }
 
-// the communicator's asynchronous state: 0 ok, 1 in progress, 2 failed
+// the communicators' asynchronous state: 0 ok, 1 in progress, 2 failed
 int comm_state(vr_shard* sh)
 {
     if (!sh->comm) return sh->aborted ? 2 : 0;
-    ncclResult_t r = ncclSuccess;
-    if (ncclCommGetAsyncError(sh->comm, &r) != ncclSuccess) return 2;
-    return r == ncclSuccess ? 0 : r == ncclInProgress ? 1 : 2;
+    int st = 0;
+    for (ncclComm_t c : {sh->comm, sh->comm2}) {
+        if (!c) continue;
+        ncclResult_t r = ncclSuccess;
+        if (ncclCommGetAsyncError(c, &r) != ncclSuccess) return 2;
+        if (r != ncclSuccess && r != ncclInProgress) return 2;
+        if (r == ncclInProgress) st = 1;
+    }
+    return st;
 }
 
 vr_status deadline_fail(vr_shard* sh, int res, const char* what)
@@ -274,6 +290,7 @@ void release(vr_shard* sh)
     for (hipEvent_t e : sh->timing) (void)hipEventDestroy(e);
     if (sh->fence) (void)hipEventDestroy(sh->fence);
     if (sh->token) (void)hipFree(sh->token);
+    if (sh->comm2) (void)ncclCommDestroy(sh->comm2);
     if (sh->comm) (void)ncclCommDestroy(sh->comm);   // an aborted communicator is already gone
     if (sh->comm_stream) (void)hipStreamDestroy(sh->comm_stream);
     for (hipStream_t rs : sh->render_stream)
@@ -364,6 +381,61 @@ vr_status one_frame(vr_shard* sh, int p, hipStream_t s, hipEvent_t t0, hipEvent_
 {
     SH_TRY(render_half(sh, p, s, t0, t1));
     SH_TRY(comm_half(sh, p));
+    sh->last = p;
+    return VR_OK;
+}
+
+// Frame (parity p) with its exchange on the render stream rs = render_stream[p]
+// (vr_shard_set_exchange_streams): render -> send / receive over the parity's
+// communicator -> (rank 0) assembly, in rs's order.  The next frame of the
+// parity follows in the same order, so no event is recorded or waited for;
+// the other parity's frame overlaps on the other stream and communicator.
+vr_status one_frame_on_render(vr_shard* sh, int p, hipStream_t rs, hipEvent_t t0, hipEvent_t t1)
+{
+    const bool r0 = sh->rank == 0, here = others_here(sh);
+    vr_target t{};
+    t.width = sh->width;
+    t.height = sh->height;
+    t.band_rows = sh->band_rows;
+    t.band_stride = sh->nranks;
+    t.band_first = sh->rank;
+    if (r0) {
+        t.format = sh->format | VR_TARGET_BANDS_IN_PLACE;
+        t.pixels = sh->frame[p];
+        t.row_pitch = sh->pitch;
+    } else {
+        t.format = sh->gformat;
+        t.pixels = sh->local[p];
+        t.row_pitch = sh->gpitch;
+    }
+    if (t0) HIP_TRY(hipEventRecord(t0, rs));
+    if (sh->my_rows > 0) VR_TRY(vr_render(sh->ctx, &t, rs));
+    if (t1) HIP_TRY(hipEventRecord(t1, rs));
+    if (here) {
+        t.format = sh->gformat;
+        t.row_pitch = sh->gpitch;
+        for (int r = 1; r < sh->nranks; ++r) {
+            t.band_first = r;
+            t.pixels = sh->gathered[p] + (size_t)r * sh->rows_per_rank * sh->gpitch;
+            if (sh->rows_of[r] > 0) VR_TRY(vr_render(sh->ctx, &t, rs));
+        }
+    }
+    if (sh->nranks > 1 && !sh->loopback) {
+        ncclComm_t c = p == 0 ? sh->comm : sh->comm2;
+        NCCL_TRY(ncclGroupStart());
+        if (r0) {
+            for (int r = 1; r < sh->nranks; ++r)
+                if (sh->rows_of[r] > 0)
+                    NCCL_TRY(ncclRecv(sh->gathered[p] + (size_t)r * sh->rows_per_rank * sh->gpitch,
+                                      (size_t)sh->rows_of[r] * sh->gpitch, ncclUint8, r, c, rs));
+        } else if (sh->my_rows > 0) {
+            NCCL_TRY(ncclSend(sh->local[p], (size_t)sh->my_rows * sh->gpitch, ncclUint8, 0, c, rs));
+        }
+        NCCL_TRY(ncclGroupEnd());
+    }
+    if (r0 && sh->nranks > 1)
+        VR_TRY(vr_assemble_frame_ranks(sh->ctx, sh->gathered[p], sh->gformat, (size_t)sh->rows_per_rank, sh->nranks,
+                                       1, sh->width, sh->height, sh->band_rows, sh->format, sh->frame[p], rs));
     sh->last = p;
     return VR_OK;
 }
@@ -554,7 +626,45 @@ try {
         HIP_TRY(hipEventRecord(sh->fence, s));
         for (hipStream_t rs : sh->render_stream) HIP_TRY(hipStreamWaitEvent(rs, sh->fence, 0));
     }
-    if (sh->host_threads == 2 && frames > 1) {
+    const bool on_render = sh->on_render && two;
+    if (on_render && frames > 0) {
+        // the parity-1 communicator, once, split from the first (collective:
+        // every rank runs its first such frames together)
+        if (!sh->loopback && sh->nranks > 1 && !sh->comm2) {
+            ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+            cfg.blocking = 0;
+            const ncclResult_t r = ncclCommSplit(sh->comm, 0, sh->rank, &sh->comm2, &cfg);
+            if (r != ncclSuccess && r != ncclInProgress) {
+                sh->comm2 = nullptr;
+                abort_comm(sh);
+                return fail(VR_ERR_COMM, "vr_shard_run: ncclCommSplit: %s; communicator aborted", ncclGetErrorString(r));
+            }
+            SH_TRY(settle(sh, "vr_shard_run: ncclCommSplit"));
+        }
+        // the parities' buffers were last used by frames of the comm-stream
+        // path, if any: their exchanges must be done
+        for (int q = 0; q < 2; ++q)
+            if (sh->pending[q]) {
+                for (hipStream_t rs : sh->render_stream) HIP_TRY(hipStreamWaitEvent(rs, sh->done[q], 0));
+                sh->pending[q] = false;
+            }
+        for (int i = 0; i < frames; ++i) {
+            const int p = sh->last < 0 ? 0 : sh->last ^ 1;
+            const bool samp = kernel_ms && i % sample_every == 0;
+            hipEvent_t t0 = samp ? sh->timing[2 * next] : nullptr, t1 = samp ? sh->timing[2 * next + 1] : nullptr;
+            if (samp) ++next;
+            if (osd) VR_TRY(vr_set_shader_data(sh->ctx, &osd[i], &gsd[i]));   // this frame's camera
+            SH_TRY(one_frame_on_render(sh, p, sh->render_stream[p], t0, t1));
+        }
+        // join: the caller's stream after both render streams' last frames
+        for (int q = 0; q < 2; ++q) {
+            HIP_TRY(hipEventRecord(sh->tail[q], sh->render_stream[q]));
+            HIP_TRY(hipStreamWaitEvent(s, sh->tail[q], 0));
+            // a later comm-stream frame of parity q waits for this one
+            HIP_TRY(hipEventRecord(sh->done[q], sh->render_stream[q]));
+            sh->pending[q] = true;
+        }
+    } else if (sh->host_threads == 2 && frames > 1) {
         // Two host threads: this one issues the render halves, a worker the
         // exchange halves, so a frame's host time is the longer half, not the
         // sum (an event record or a launch costs ~3-5 us).
@@ -620,7 +730,7 @@ try {
             if (st != VR_OK) return st;
         }
     }
-    if (sh->last >= 0 && frames > 0) {   // the caller's stream sees the frame
+    if (sh->last >= 0 && frames > 0 && !on_render) {   // the caller's stream sees the frame
         if (sh->rank == 0 && !others_here(sh)) {
             // rank 0 recorded no event per frame: join the exchange / assembly
             // stream and the render streams now (the render streams' frames
@@ -793,6 +903,16 @@ try {
 }
 
 int vr_shard_get_render_streams(vr_shard* sh) { return sh ? sh->render_streams : 0; }
+
+vr_status vr_shard_set_exchange_streams(vr_shard* sh, int on_render)
+try {
+    if (!sh || on_render < 0 || on_render > 1)
+        return fail(VR_ERR_INVALID, "vr_shard_set_exchange_streams: need a shard and 0 or 1");
+    sh->on_render = on_render == 1;
+    return VR_OK;
+} catch (...) {
+    return caught_exception("vr_shard_set_exchange_streams");
+}
 
 vr_status vr_shard_set_host_threads(vr_shard* sh, int n)
 try {
