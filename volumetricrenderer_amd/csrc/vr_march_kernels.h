@@ -512,6 +512,14 @@ __device__ __forceinline__ unsigned march_pixel(const MarchArgs& a, const FastCt
 #define VR_PROC_ATTR
 #endif
 #endif
+// the deferred-shadow primary march (config 3): its own unroll / occupancy
+// switches, for A/B runs (defaults: those of the other primary marches)
+#ifndef VR_DEFER_UNROLL
+#define VR_DEFER_UNROLL 1
+#endif
+#ifndef VR_DEFER_ATTR
+#define VR_DEFER_ATTR VR_PROC_ATTR
+#endif
 struct DensityK {
     float gs, lac, gain, f0, wf, scale;
     float lat_sy, lat_sz, lat_c;   // TABLE 3: the lattice table's byte-offset fma constants
@@ -1731,7 +1739,7 @@ __global__ __launch_bounds__(kThreads) VR_PROC_ATTR void march_proc_sorted(const
 // march_pixel_proc<true>, so the frame stays bit-exact.
 // (struct ShadowDefer: vr_internal.h)
 template <bool EARLY, int TABLE>
-__global__ __launch_bounds__(kThreads) VR_PROC_ATTR void march_proc_defer(const MarchArgs a, const unsigned* __restrict__ order,
+__global__ __launch_bounds__(kThreads) VR_DEFER_ATTR void march_proc_defer(const MarchArgs a, const unsigned* __restrict__ order,
                                                              const unsigned* __restrict__ total_ptr,
                                                              const unsigned short* __restrict__ keys,
                                                              unsigned fill_positions, unsigned fill_first, int stale,
@@ -1798,7 +1806,7 @@ __global__ __launch_bounds__(kThreads) VR_PROC_ATTR void march_proc_defer(const 
         act = act && i < r.n;
         if (__ballot(act) == 0) break;
         float rho = 0.0f;
-        if (act) rho = proc_density<TABLE, false, true>(p, dk, wt, P0, P1, P2, cells);
+        if (act) rho = proc_density<TABLE, false, (VR_DEFER_UNROLL != 0)>(p, dk, wt, P0, P1, P2, cells);
         const bool need = act && rho > 0.0f;
         const unsigned long long m = __ballot(need);
         if (need) ent[b + (unsigned)__popcll(m & lt)] = make_float4(P0, P1, P2, tv * (rho * p.od));
