@@ -114,6 +114,7 @@ def native(a):
         base = {}
         for n in [int(v) for v in a.ns.split(",")]:
             res = {ns: [] for ns in streams}   # per stream count: per round, the slowest rank's ms/frame
+            per_rank = {ns: {} for ns in streams}   # per stream count, rank: ms/frame per round
             host = {ns: [] for ns in streams}
             pipes = {}
             for first in (range(n) if a.all_ranks else (0,)):
@@ -139,6 +140,7 @@ def native(a):
                         e1.record()
                         torch.cuda.synchronize()
                         worst = max(worst, e0.elapsed_time(e1) / a.frames)
+                        per_rank[ns].setdefault(first, []).append(e0.elapsed_time(e1) / a.frames)
                         hmax = max(hmax, p.host_ms)
                     res[ns].append(worst)
                     host[ns].append(hmax)
@@ -153,6 +155,9 @@ def native(a):
                 print(f"N={n} render_streams {ns}: slowest rank {t:.4f} ms/frame (rounds "
                       + " ".join(f"{v:.4f}" for v in res[ns]) + f"), host {max(host[ns]):.4f} ms/frame{eff}",
                       flush=True)
+                if a.all_ranks and n > 1:
+                    print("  per rank (median ms/frame): " + " ".join(
+                        f"{k}:{float(np.median(v)):.4f}" for k, v in sorted(per_rank[ns].items())), flush=True)
 
 
 if __name__ == "__main__":

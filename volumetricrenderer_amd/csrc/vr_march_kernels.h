@@ -512,13 +512,14 @@ __device__ __forceinline__ unsigned march_pixel(const MarchArgs& a, const FastCt
 #define VR_PROC_ATTR
 #endif
 #endif
-// the deferred-shadow primary march (config 3): its own unroll / occupancy
-// switches, for A/B runs (defaults: those of the other primary marches)
+// the deferred-shadow primary march (config 3): the unrolled fBm without the
+// occupancy cap -- 0.905 ms vs 0.937 capped at 4 waves and 0.910 for round 4's
+// build (profiles/r05/ab_defer.txt)
 #ifndef VR_DEFER_UNROLL
 #define VR_DEFER_UNROLL 1
 #endif
 #ifndef VR_DEFER_ATTR
-#define VR_DEFER_ATTR VR_PROC_ATTR
+#define VR_DEFER_ATTR
 #endif
 struct DensityK {
     float gs, lac, gain, f0, wf, scale;

@@ -304,20 +304,34 @@ __global__ __launch_bounds__(kBlock) void k_pack_recipe(const float* __restrict_
 // its (b / nranks)-th band.  16-byte chunks when rows allow it.  Rows of ranks
 // below first_rank are left as they are (rendered in place into the frame,
 // vr.h VR_TARGET_BANDS_IN_PLACE).
+// Row q (from rank first_rank's slot on) of the gathered band sets -> its
+// frame row y: rank r's slot holds its bands lb = 0, 1, ... packed, and band
+// lb of rank r is frame band lb * nranks + r.  False for slot rows past the
+// frame (a rank with fewer rows than the slot).  Block-uniform: the divisions
+// are scalar, once per row.
+__device__ __forceinline__ bool assembled_row(long long q, long long rows_per_rank, int nranks, int band_rows,
+                                              int first_rank, int height, long long& y)
+{
+    const long long r = first_rank + q / rows_per_rank, lr = q % rows_per_rank;
+    const long long lb = lr / band_rows, rr = lr - lb * band_rows;
+    y = (lb * nranks + r) * band_rows + rr;
+    return y < height;
+}
+
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_assemble(const T* __restrict__ src, long long rows_per_rank,
                                                      int nranks, int row_elems, int height, int band_rows,
                                                      int first_rank, T* __restrict__ dst)
 {
-    const long long total = (long long)height * row_elems;
-    for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < total;
-         i += (long long)gridDim.x * kBlock) {
-        const int y = (int)(i / row_elems), e = (int)(i % row_elems);
-        const int b = y / band_rows, r = y - b * band_rows;
-        const int rank = b % nranks, lb = b / nranks;
-        if (rank < first_rank) continue;
-        const long long srow = (long long)rank * rows_per_rank + (long long)lb * band_rows + r;
-        dst[i] = src[srow * row_elems + e];
+    // one gathered row per blockIdx.y (its frame row from block-uniform
+    // scalar arithmetic: no per-element division), elements across x
+    const long long rows = (long long)(nranks - first_rank) * rows_per_rank;
+    const int e = blockIdx.x * kBlock + threadIdx.x;
+    for (long long q = blockIdx.y; q < rows; q += gridDim.y) {
+        long long y;
+        if (!assembled_row(q, rows_per_rank, nranks, band_rows, first_rank, height, y) || e >= row_elems) continue;
+        const long long sr = (long long)first_rank * rows_per_rank + q;
+        dst[y * row_elems + e] = src[sr * row_elems + e];
     }
 }
 
@@ -356,16 +370,22 @@ __global__ __launch_bounds__(kBlock) void k_assemble_grey(const S* __restrict__ 
                                                           int nranks, int row_elems, int height, int band_rows,
                                                           int first_rank, D* __restrict__ dst)
 {
-    const long long total = (long long)height * row_elems;
-    for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < total;
-         i += (long long)gridDim.x * kBlock) {
-        const int y = (int)(i / row_elems), e = (int)(i % row_elems);
-        const int b = y / band_rows, r = y - b * band_rows;
-        const int rank = b % nranks, lb = b / nranks;
-        if (rank < first_rank) continue;
-        const long long srow = (long long)rank * rows_per_rank + (long long)lb * band_rows + r;
-        dst[i] = grey_expand<S, D>(src[srow * row_elems + e]);
+    const long long rows = (long long)(nranks - first_rank) * rows_per_rank;
+    const int e = blockIdx.x * kBlock + threadIdx.x;
+    for (long long q = blockIdx.y; q < rows; q += gridDim.y) {
+        long long y;
+        if (!assembled_row(q, rows_per_rank, nranks, band_rows, first_rank, height, y) || e >= row_elems) continue;
+        const long long sr = (long long)first_rank * rows_per_rank + q;
+        dst[y * row_elems + e] = grey_expand<S, D>(src[sr * row_elems + e]);
     }
+}
+
+// rows x elements grid of the assembly kernels: one row per blockIdx.y
+// (grid-stride past 65535 rows), ceil(elems / kBlock) blocks across
+dim3 grid_rows(size_t rows_per_rank, int nranks, int first_rank, long long elems)
+{
+    const long long rows = (long long)(nranks - first_rank) * (long long)rows_per_rank;
+    return dim3((unsigned)((elems + kBlock - 1) / kBlock), (unsigned)std::max(1LL, std::min(rows, 65535LL)));
 }
 
 int grid_for(long long n)
@@ -663,17 +683,17 @@ hipError_t launch_assemble(const uint8_t* d_gathered, size_t rows_per_rank, int 
     const long long row_bytes = (long long)width * bpp;
     if (row_bytes % 16 == 0) {
         const int elems = (int)(row_bytes / 16);
-        hipLaunchKernelGGL(k_assemble<uint4>, dim3(grid_for((long long)height * elems)), dim3(kBlock), 0, s,
+        hipLaunchKernelGGL(k_assemble<uint4>, grid_rows(rows_per_rank, nranks, first_rank, elems), dim3(kBlock), 0, s,
                            reinterpret_cast<const uint4*>(d_gathered), (long long)rows_per_rank, nranks, elems,
                            height, band_rows, first_rank, reinterpret_cast<uint4*>(d_frame));
     } else if (row_bytes % 4 == 0) {
         const int elems = (int)(row_bytes / 4);
-        hipLaunchKernelGGL(k_assemble<unsigned int>, dim3(grid_for((long long)height * elems)), dim3(kBlock), 0,
+        hipLaunchKernelGGL(k_assemble<unsigned int>, grid_rows(rows_per_rank, nranks, first_rank, elems), dim3(kBlock), 0,
                            s, reinterpret_cast<const unsigned int*>(d_gathered), (long long)rows_per_rank, nranks,
                            elems, height, band_rows, first_rank, reinterpret_cast<unsigned int*>(d_frame));
     } else {   // 1-byte pixels, rows of any width
         const int elems = (int)row_bytes;
-        hipLaunchKernelGGL(k_assemble<unsigned char>, dim3(grid_for((long long)height * elems)), dim3(kBlock), 0,
+        hipLaunchKernelGGL(k_assemble<unsigned char>, grid_rows(rows_per_rank, nranks, first_rank, elems), dim3(kBlock), 0,
                            s, d_gathered, (long long)rows_per_rank, nranks, elems, height, band_rows, first_rank,
                            d_frame);
     }
@@ -685,16 +705,16 @@ hipError_t launch_assemble_grey(const uint8_t* d_gathered, size_t rows_per_rank,
 {
     const dim3 blk(kBlock);
     if (f32) {
-        hipLaunchKernelGGL((k_assemble_grey<float, float4>), dim3(grid_for((long long)height * width)), blk, 0, s,
+        hipLaunchKernelGGL((k_assemble_grey<float, float4>), grid_rows(rows_per_rank, nranks, first_rank, width), blk, 0, s,
                            reinterpret_cast<const float*>(d_gathered), (long long)rows_per_rank, nranks, width, height,
                            band_rows, first_rank, reinterpret_cast<float4*>(d_frame));
     } else if (width % 4 == 0) {
         const int elems = width / 4;
-        hipLaunchKernelGGL((k_assemble_grey<unsigned int, uint4>), dim3(grid_for((long long)height * elems)), blk, 0,
+        hipLaunchKernelGGL((k_assemble_grey<unsigned int, uint4>), grid_rows(rows_per_rank, nranks, first_rank, elems), blk, 0,
                            s, reinterpret_cast<const unsigned int*>(d_gathered), (long long)rows_per_rank, nranks,
                            elems, height, band_rows, first_rank, reinterpret_cast<uint4*>(d_frame));
     } else {
-        hipLaunchKernelGGL((k_assemble_grey<unsigned char, unsigned int>), dim3(grid_for((long long)height * width)),
+        hipLaunchKernelGGL((k_assemble_grey<unsigned char, unsigned int>), grid_rows(rows_per_rank, nranks, first_rank, width),
                            blk, 0, s, d_gathered, (long long)rows_per_rank, nranks, width, height, band_rows, first_rank,
                            reinterpret_cast<unsigned int*>(d_frame));
     }
