@@ -2200,6 +2200,8 @@ try {
     if (!p || !d_gathered || !d_frame) return fail(VR_ERR_INVALID, "vr_assemble_frame: null argument");
     if (first_rank < 0 || first_rank > nranks) return fail(VR_ERR_INVALID, "vr_assemble_frame: first_rank %d", first_rank);
     if (first_rank == nranks) return VR_OK;   // every rank's rows are in place
+    if (nranks > 0 && rows_per_rank > (size_t)(INT_MAX / nranks))   // the kernels index rows in 32 bits
+        return fail(VR_ERR_INVALID, "vr_assemble_frame: rows_per_rank %zu x %d ranks", rows_per_rank, nranks);
     if (gathered_format < 0 || gathered_format > 5 || frame_format < 0 || frame_format > 5)
         return fail(VR_ERR_INVALID, "vr_assemble_frame: bad format %d -> %d", gathered_format, frame_format);
     if (gathered_format != frame_format && grey_of(frame_format) != gathered_format)

@@ -304,35 +304,57 @@ __global__ __launch_bounds__(kBlock) void k_pack_recipe(const float* __restrict_
 // its (b / nranks)-th band.  16-byte chunks when rows allow it.  Rows of ranks
 // below first_rank are left as they are (rendered in place into the frame,
 // vr.h VR_TARGET_BANDS_IN_PLACE).
+//
 // Row q (from rank first_rank's slot on) of the gathered band sets -> its
 // frame row y: rank r's slot holds its bands lb = 0, 1, ... packed, and band
-// lb of rank r is frame band lb * nranks + r.  False for slot rows past the
+// lb of rank r is frame band lb * nranks + r.  -1 for slot rows past the
 // frame (a rank with fewer rows than the slot).  Block-uniform: the divisions
 // are scalar, once per row.
-__device__ __forceinline__ bool assembled_row(long long q, long long rows_per_rank, int nranks, int band_rows,
-                                              int first_rank, int height, long long& y)
+__device__ __forceinline__ int assembled_row(int q, int rows_per_rank, int nranks, int band_rows, int first_rank,
+                                             int height)
 {
-    const long long r = first_rank + q / rows_per_rank, lr = q % rows_per_rank;
-    const long long lb = lr / band_rows, rr = lr - lb * band_rows;
-    y = (lb * nranks + r) * band_rows + rr;
-    return y < height;
+    const int r = first_rank + q / rows_per_rank, lr = q % rows_per_rank;
+    const int lb = lr / band_rows, rr = lr - lb * band_rows;
+    const int y = (lb * nranks + r) * band_rows + rr;
+    return y < height ? y : -1;
+}
+
+// The assembly kernels (vr_assemble_frame): rows x elements.  A small grid
+// (~2 workgroups per CU, launch_assemble*) whose lanes each move kAsmBatch
+// rows' elements with all the loads in flight before the first store: the
+// assembly runs beside the other render stream's march, which holds most of
+// the wave slots, so a grid of one-element lanes waits several rounds of
+// slots and memory round trips (~16 us for 7/8 of a 1080p frame, profiles/r05).
+constexpr int kAsmBatch = 8;
+template <typename S, typename D, typename F>
+__device__ __forceinline__ void assemble_rows(const S* __restrict__ src, int rows_per_rank, int nranks, int row_elems,
+                                              int height, int band_rows, int first_rank, D* __restrict__ dst, F expand)
+{
+    const int rows = (nranks - first_rank) * rows_per_rank;
+    const int e = blockIdx.x * kBlock + threadIdx.x;
+    if (e >= row_elems) return;
+    const size_t base = (size_t)first_rank * rows_per_rank;
+    for (int q0 = blockIdx.y; q0 < rows; q0 += gridDim.y * kAsmBatch) {
+        S v[kAsmBatch];
+        int y[kAsmBatch];
+#pragma unroll
+        for (int j = 0; j < kAsmBatch; ++j) {
+            const int q = q0 + j * (int)gridDim.y;
+            y[j] = q < rows ? assembled_row(q, rows_per_rank, nranks, band_rows, first_rank, height) : -1;
+            if (y[j] >= 0) v[j] = src[(base + q) * row_elems + e];
+        }
+#pragma unroll
+        for (int j = 0; j < kAsmBatch; ++j)
+            if (y[j] >= 0) dst[(size_t)y[j] * row_elems + e] = expand(v[j]);
+    }
 }
 
 template <typename T>
-__global__ __launch_bounds__(kBlock) void k_assemble(const T* __restrict__ src, long long rows_per_rank,
-                                                     int nranks, int row_elems, int height, int band_rows,
-                                                     int first_rank, T* __restrict__ dst)
+__global__ __launch_bounds__(kBlock) void k_assemble(const T* __restrict__ src, int rows_per_rank, int nranks,
+                                                     int row_elems, int height, int band_rows, int first_rank,
+                                                     T* __restrict__ dst)
 {
-    // one gathered row per blockIdx.y (its frame row from block-uniform
-    // scalar arithmetic: no per-element division), elements across x
-    const long long rows = (long long)(nranks - first_rank) * rows_per_rank;
-    const int e = blockIdx.x * kBlock + threadIdx.x;
-    for (long long q = blockIdx.y; q < rows; q += gridDim.y) {
-        long long y;
-        if (!assembled_row(q, rows_per_rank, nranks, band_rows, first_rank, height, y) || e >= row_elems) continue;
-        const long long sr = (long long)first_rank * rows_per_rank + q;
-        dst[y * row_elems + e] = src[sr * row_elems + e];
-    }
+    assemble_rows(src, rows_per_rank, nranks, row_elems, height, band_rows, first_rank, dst, [](T v) { return v; });
 }
 
 // Grey band sets -> RGBA frame (vr_assemble_frame): element e of frame row y
@@ -366,26 +388,23 @@ __device__ __forceinline__ float4 grey_expand<float, float4>(float v)
     return make_float4(v, v, v, 1.0f);
 }
 template <typename S, typename D>
-__global__ __launch_bounds__(kBlock) void k_assemble_grey(const S* __restrict__ src, long long rows_per_rank,
+__global__ __launch_bounds__(kBlock) void k_assemble_grey(const S* __restrict__ src, int rows_per_rank,
                                                           int nranks, int row_elems, int height, int band_rows,
                                                           int first_rank, D* __restrict__ dst)
 {
-    const long long rows = (long long)(nranks - first_rank) * rows_per_rank;
-    const int e = blockIdx.x * kBlock + threadIdx.x;
-    for (long long q = blockIdx.y; q < rows; q += gridDim.y) {
-        long long y;
-        if (!assembled_row(q, rows_per_rank, nranks, band_rows, first_rank, height, y) || e >= row_elems) continue;
-        const long long sr = (long long)first_rank * rows_per_rank + q;
-        dst[y * row_elems + e] = grey_expand<S, D>(src[sr * row_elems + e]);
-    }
+    assemble_rows(src, rows_per_rank, nranks, row_elems, height, band_rows, first_rank, dst,
+                  [](S v) { return grey_expand<S, D>(v); });
 }
 
-// rows x elements grid of the assembly kernels: one row per blockIdx.y
-// (grid-stride past 65535 rows), ceil(elems / kBlock) blocks across
+// grid of the assembly kernels: ceil(elems / kBlock) workgroups across a row,
+// rows over blockIdx.y -- about 512 workgroups in all (2 per CU), at most one
+// batch of rows per workgroup row more than needed
 dim3 grid_rows(size_t rows_per_rank, int nranks, int first_rank, long long elems)
 {
     const long long rows = (long long)(nranks - first_rank) * (long long)rows_per_rank;
-    return dim3((unsigned)((elems + kBlock - 1) / kBlock), (unsigned)std::max(1LL, std::min(rows, 65535LL)));
+    const long long gx = (elems + kBlock - 1) / kBlock;
+    const long long gy = std::max(1LL, std::min({rows, (512 + gx - 1) / gx, 65535LL}));
+    return dim3((unsigned)gx, (unsigned)gy);
 }
 
 int grid_for(long long n)
@@ -684,17 +703,17 @@ hipError_t launch_assemble(const uint8_t* d_gathered, size_t rows_per_rank, int 
     if (row_bytes % 16 == 0) {
         const int elems = (int)(row_bytes / 16);
         hipLaunchKernelGGL(k_assemble<uint4>, grid_rows(rows_per_rank, nranks, first_rank, elems), dim3(kBlock), 0, s,
-                           reinterpret_cast<const uint4*>(d_gathered), (long long)rows_per_rank, nranks, elems,
+                           reinterpret_cast<const uint4*>(d_gathered), (int)rows_per_rank, nranks, elems,
                            height, band_rows, first_rank, reinterpret_cast<uint4*>(d_frame));
     } else if (row_bytes % 4 == 0) {
         const int elems = (int)(row_bytes / 4);
         hipLaunchKernelGGL(k_assemble<unsigned int>, grid_rows(rows_per_rank, nranks, first_rank, elems), dim3(kBlock), 0,
-                           s, reinterpret_cast<const unsigned int*>(d_gathered), (long long)rows_per_rank, nranks,
+                           s, reinterpret_cast<const unsigned int*>(d_gathered), (int)rows_per_rank, nranks,
                            elems, height, band_rows, first_rank, reinterpret_cast<unsigned int*>(d_frame));
     } else {   // 1-byte pixels, rows of any width
         const int elems = (int)row_bytes;
         hipLaunchKernelGGL(k_assemble<unsigned char>, grid_rows(rows_per_rank, nranks, first_rank, elems), dim3(kBlock), 0,
-                           s, d_gathered, (long long)rows_per_rank, nranks, elems, height, band_rows, first_rank,
+                           s, d_gathered, (int)rows_per_rank, nranks, elems, height, band_rows, first_rank,
                            d_frame);
     }
     return hipGetLastError();
@@ -706,16 +725,16 @@ hipError_t launch_assemble_grey(const uint8_t* d_gathered, size_t rows_per_rank,
     const dim3 blk(kBlock);
     if (f32) {
         hipLaunchKernelGGL((k_assemble_grey<float, float4>), grid_rows(rows_per_rank, nranks, first_rank, width), blk, 0, s,
-                           reinterpret_cast<const float*>(d_gathered), (long long)rows_per_rank, nranks, width, height,
+                           reinterpret_cast<const float*>(d_gathered), (int)rows_per_rank, nranks, width, height,
                            band_rows, first_rank, reinterpret_cast<float4*>(d_frame));
     } else if (width % 4 == 0) {
         const int elems = width / 4;
         hipLaunchKernelGGL((k_assemble_grey<unsigned int, uint4>), grid_rows(rows_per_rank, nranks, first_rank, elems), blk, 0,
-                           s, reinterpret_cast<const unsigned int*>(d_gathered), (long long)rows_per_rank, nranks,
+                           s, reinterpret_cast<const unsigned int*>(d_gathered), (int)rows_per_rank, nranks,
                            elems, height, band_rows, first_rank, reinterpret_cast<uint4*>(d_frame));
     } else {
         hipLaunchKernelGGL((k_assemble_grey<unsigned char, unsigned int>), grid_rows(rows_per_rank, nranks, first_rank, width),
-                           blk, 0, s, d_gathered, (long long)rows_per_rank, nranks, width, height, band_rows, first_rank,
+                           blk, 0, s, d_gathered, (int)rows_per_rank, nranks, width, height, band_rows, first_rank,
                            reinterpret_cast<unsigned int*>(d_frame));
     }
     return hipGetLastError();
