@@ -282,6 +282,10 @@ def main() -> int:
     ap.add_argument("--render-streams", type=int, default=2, choices=[1, 2],
                     help="N > 1 (native loop): 2 = consecutive frames render on two alternating streams and overlap "
                          "(vr_shard_set_render_streams; the default), 1 = one render stream")
+    ap.add_argument("--exchange", default="render", choices=["render", "comm"],
+                    help="N > 1 (native loop, 2 render streams): each frame's exchange on its render stream, over one "
+                         "communicator per buffer parity, no events (the default), or on a communication stream "
+                         "ordered by events (vr_shard_set_exchange_streams)")
     ap.add_argument("--spin", action="store_true",
                     help="moving camera: every frame gets new shader data, phi += 1.6 deg (the reference's "
                          "held A/D key, TestMain.cpp:171-184, :222-224), queued natively (vr_render_sequence "
@@ -370,7 +374,8 @@ def main() -> int:
         # communicator init) and the bench exits non-zero.
         try:
             pipe = vrdist.RcclBandPipeline(r, W, H, fmt, band_rows=16, world=world, rank=rank,
-                                           render_streams=args.render_streams)
+                                           render_streams=args.render_streams,
+                                           exchange_on_render=args.exchange == "render")
         except vr.VRError as e:
             print(f"rank {rank}: native RCCL frame loop unavailable: {e}", file=sys.stderr, flush=True)
             raise SystemExit(3)
@@ -594,6 +599,8 @@ def main() -> int:
                                                       and r.get_option("shadow_defer") == 1 else ""),
                        "parallelism": f"bands16x{world}" + (", 2 frames in flight" if args.inflight == 2 else "")
                                       + (f", {args.render_streams} render stream{'s' if args.render_streams > 1 else ''}"
+                                         + (f", exchange on {args.exchange} stream{'s' if args.exchange == 'render' else ''}"
+                                            if args.render_streams == 2 else "")
                                          if native else ""),
                        "collective": collective_label,
                        "executed_steps_per_frame": frame_steps},

@@ -149,13 +149,13 @@ vr_status vr_shard_set_solo(vr_shard* sh, int on);
  * thread issues the renders, so the host time per frame is the longer half
  * instead of the sum.  Results are identical.                             */
 vr_status vr_shard_set_host_threads(vr_shard* sh, int n);
-/* Where the exchange runs (with 2 render streams): 0 (default) = on the
- * shard's communication stream, ordered after each render by events;
- * 1 = on the frame's own render stream, after its render, over one
- * communicator per buffer parity (the second split from the first at the
- * first such run, collectively): no event per frame, the host cost of a
- * frame is its launches alone.  Every rank must choose the same.  Results
- * are identical.                                                          */
+/* Where the exchange runs (with 2 render streams): 1 (default) = on the
+ * frame's own render stream, after its render, over one communicator per
+ * buffer parity (the second split from the first at the first such run,
+ * collectively): no event per frame, the host cost of a frame is its
+ * launches alone (host_threads does not apply); 0 = on the shard's
+ * communication stream, ordered after each render by events.  Every rank
+ * must choose the same.  Results are identical.                           */
 vr_status vr_shard_set_exchange_streams(vr_shard* sh, int on_render);
 int       vr_shard_aborted(vr_shard* sh);
 /* Self-test of the deadline loop on the host (no GPU, no RCCL): mode 0 a

@@ -39,8 +39,9 @@ def main():
     ap.add_argument("--streams", default="1,2", help="--native: render streams to compare")
     ap.add_argument("--rounds", type=int, default=3, help="--native: interleaved rounds")
     ap.add_argument("--threads", type=int, default=1, help="--native: host threads of the frame loop (1 or 2)")
-    ap.add_argument("--on-render", action="store_true",
-                    help="--native: the exchange on the render streams (vr_shard_set_exchange_streams 1)")
+    ap.add_argument("--exchange", default="render", choices=["render", "comm"],
+                    help="--native: the exchange on the render streams (default) or on a communication stream "
+                         "(vr_shard_set_exchange_streams 1 / 0)")
     ap.add_argument("--gate-ms", type=float, default=0.0,
                     help="--native: hold the stream with a spin kernel of this many ms while the host queues the "
                          "frames, so the timing is the GPU's alone (not the host's)")
@@ -107,7 +108,7 @@ def native(a):
             k, v = o.split("=")
             r.set_option(k, int(v))
         print(f"native frame streams: {a.size}^3, {W}x{H}x{a.steps}, {a.frames} frames per timing, "
-              f"{a.threads} host thread(s), gate {a.gate_ms} ms, exchange on {'render' if a.on_render else 'comm'} "
+              f"{a.threads} host thread(s), gate {a.gate_ms} ms, exchange on {a.exchange} "
               "streams, "
               f"variant {r.kernel_variant} {' '.join(a.opt)}", flush=True)
         streams = [int(v) for v in a.streams.split(",")]
@@ -121,7 +122,7 @@ def native(a):
                 for ns in streams:
                     p = RcclBandPipeline(r, W, H, vr.FMT_RGBA8_UNORM, band_rows=a.band_rows, world=n, rank=first,
                                          loopback=True, solo=True, render_streams=ns, host_threads=a.threads,
-                                         exchange_on_render=a.on_render)
+                                         exchange_on_render=a.exchange == "render")
                     p.run_frames(8)   # region lists, code objects
                     p.barrier()
                     pipes[(first, ns)] = p

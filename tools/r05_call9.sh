@@ -12,13 +12,13 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_distributed.py tests/test_g
     --timeout-method thread -k "assembl or band or shard or rccl or loopback or solo or frame or pipeline or sharder" > $O/c9_tests.log 2>&1; rc=$?
 tail -3 $O/c9_tests.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_solo8c -o solo8 -- \
-    python -u tools/band_scaling.py --native --ns 8 --streams 2 --frames 100 --rounds 2 --on-render \
+    python -u tools/band_scaling.py --native --ns 8 --streams 2 --frames 100 --rounds 2 --exchange render \
     > $O/c9_prof_solo8.txt 2>&1 || { tail -20 $O/c9_prof_solo8.txt; exit 2; }
-for orr in "--on-render"; do
+for orr in "--exchange render"; do
   timeout -k 10 300 python -u tools/band_scaling.py --native --all-ranks --ns 1,4,8 --frames 100 --rounds 3 $orr \
       > $O/c9_native_c5${orr}.txt 2>&1 || { cat $O/c9_native_c5${orr}.txt; exit 3; }
   grep -v amdgpu.ids $O/c9_native_c5${orr}.txt
 done
 timeout -k 10 300 python -u tools/band_scaling.py --native --all-ranks --ns 1,8 --size 128 --width 3840 --height 2160 --steps 256 \
-    --frames 40 --rounds 3 --on-render > $O/c9_native_c4_onr.txt 2>&1; rc=$?
+    --frames 40 --rounds 3 --exchange render > $O/c9_native_c4_onr.txt 2>&1; rc=$?
 grep -v amdgpu.ids $O/c9_native_c4_onr.txt; exit $rc

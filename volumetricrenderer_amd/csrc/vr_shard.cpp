@@ -164,7 +164,7 @@ struct vr_shard {
     // exchange (and rank 0's assembly) follows its render on render_stream[p],
     // over a communicator of its own per parity (comm for p = 0, comm2 for
     // p = 1, split from comm at the first such run), with no events at all
-    bool on_render = false;
+    bool on_render = true;   // vr_shard_set_exchange_streams
     ncclComm_t comm2 = nullptr;
     uint8_t* local[2] = {};           // rank > 0: band sets (gformat)
     uint8_t* gathered[2] = {};        // rank 0: nranks slots of rows_per_rank rows (gformat)

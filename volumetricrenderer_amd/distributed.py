@@ -285,7 +285,7 @@ class RcclBandPipeline:
 
     def __init__(self, renderer, width: int, height: int, fmt: int, band_rows: int = 16, world: int = 1,
                  rank: int = 0, group=None, loopback: bool = False, timeout_s: float | None = None,
-                 render_streams: int = 2, solo: bool = False, host_threads: int = 1, exchange_on_render: bool = False):
+                 render_streams: int = 2, solo: bool = False, host_threads: int = 1, exchange_on_render: bool = True):
         """loopback: one process renders all `world` ranks' band sets on its
         GPU and assembles them (no communicator; tests and rehearsals).
         solo (loopback only, any rank): each frame renders only this rank's
@@ -296,8 +296,9 @@ class RcclBandPipeline:
         (vr_shard_set_render_streams).
         host_threads: 2 = a worker thread issues every frame's exchange half
         (vr_shard_set_host_threads).
-        exchange_on_render: each frame's exchange follows its render on the
-        frame's render stream, over a communicator per buffer parity, with no
+        exchange_on_render: True (default) = each frame's exchange follows its
+        render on the frame's render stream, over a communicator per buffer
+        parity, with no events; False = on a communication stream, ordered by
         events (vr_shard_set_exchange_streams; every rank the same).
         timeout_s: deadline of every host wait on a collective, from the
         communicator init on (vr_shard_set_timeout; default VR_SHARD_TIMEOUT_S
