@@ -523,7 +523,8 @@ __device__ __forceinline__ unsigned march_pixel(const MarchArgs& a, const FastCt
 #endif
 struct DensityK {
     float gs, lac, gain, f0, wf, scale;
-    float lat_sy, lat_sz, lat_c;   // TABLE 3: the lattice table's byte-offset fma constants
+    float lat_sy, lat_sz, lat_nc;   // TABLE 3: the lattice table's byte-offset fma constants (lat_nc = -lat_c)
+    float wt_nc;                    // TABLE >= 2: noise::worley9_nc(wt_lo)
 };
 template <int TABLE>
 __device__ __forceinline__ DensityK density_k(const ProcParams& p, float scale)
@@ -538,10 +539,12 @@ __device__ __forceinline__ DensityK density_k(const ProcParams& p, float scale)
     if constexpr (TABLE == 3) {
         k.lat_sy = noise::in_vgpr(p.lat_sy);
         k.lat_sz = noise::in_vgpr(p.lat_sz);
-        k.lat_c = noise::in_vgpr(p.lat_c);
+        k.lat_nc = noise::in_vgpr(-p.lat_c);
     } else {
-        k.lat_sy = k.lat_sz = k.lat_c = 0.0f;
+        k.lat_sy = k.lat_sz = k.lat_nc = 0.0f;
     }
+    // the negated constant terms make the offset fmas v_fmamk (literal 8 / 16)
+    k.wt_nc = TABLE >= 2 ? noise::in_vgpr(noise::worley9_nc(p.wt_lo)) : 0.0f;
     return k;
 }
 
@@ -572,7 +575,7 @@ __device__ __forceinline__ float fbm_lat(const ProcParams& p, const DensityK& k,
     float x = qx * f, y = qy * f, z = qz * f;
     float xs = floorf(x), ys = floorf(y), zs = floorf(z);
     auto word = __builtin_amdgcn_raw_buffer_load_b64(
-        rsrc, (unsigned)fmaf(zs, k.lat_sz, fmaf(ys, k.lat_sy, fmaf(xs, 8.0f, -k.lat_c))), 0, 0);
+        rsrc, (unsigned)fmaf(zs, k.lat_sz, fmaf(ys, k.lat_sy, fmaf(xs, 8.0f, k.lat_nc))), 0, 0);
     const int n = OCT > 0 ? OCT : p.octaves;
     auto octave = [&](int o) {
         const uint2 w = make_uint2(word[0], word[1]);
@@ -582,7 +585,7 @@ __device__ __forceinline__ float fbm_lat(const ProcParams& p, const DensityK& k,
             x = qx * f; y = qy * f; z = qz * f;
             xs = floorf(x); ys = floorf(y); zs = floorf(z);
             word = __builtin_amdgcn_raw_buffer_load_b64(
-                rsrc, (unsigned)fmaf(zs, k.lat_sz, fmaf(ys, k.lat_sy, fmaf(xs, 8.0f, -k.lat_c))), 0, 0);
+                rsrc, (unsigned)fmaf(zs, k.lat_sz, fmaf(ys, k.lat_sy, fmaf(xs, 8.0f, k.lat_nc))), 0, 0);
         }
         const float pn = noise::perlin_lat(gp, w, cx, cy, cz, cxs, cys, czs);
         fbm = fmaf(amp, pn, fbm);
@@ -638,8 +641,8 @@ __device__ __forceinline__ float proc_density(const ProcParams& p, const Density
     float f1;
     if constexpr (TABLE >= 2) {
         bool full;
-        if constexpr (WC) f1 = noise::cellular_table9_cached(wt, p.wt_lo, qx * wf, qy * wf, qz * wf, full, *wc) + 1.0f;
-        else f1 = noise::cellular_table9(wt, p.wt_lo, qx * wf, qy * wf, qz * wf, full) + 1.0f;
+        if constexpr (WC) f1 = noise::cellular_table9_cached(wt, k.wt_nc, qx * wf, qy * wf, qz * wf, full, *wc) + 1.0f;
+        else f1 = noise::cellular_table9(wt, k.wt_nc, qx * wf, qy * wf, qz * wf, full) + 1.0f;
         if (p.count_evals == 2) cells += full ? 35u : 8u;
     } else {
         if constexpr (TABLE == 1) f1 = noise::cellular_table(wt, p.wt_lo, p.wt_n, p.wt_pz, qx * wf, qy * wf, qz * wf) + 1.0f;

@@ -335,13 +335,22 @@ __device__ inline float cellular_table(const float4* __restrict__ tab, int lo, i
 // (tools/worley_prune_model.py): 94 % of wave-steps need the cube only.
 constexpr int kWorleyN = 9, kWorleyPz = 83;
 constexpr float kPruneR = 0.3962f;
-__device__ inline float cellular_table9_full(const float4* __restrict__ tab, int lo, float x, float y, float z)
+// The table's base byte offset term, negated: -16 lo (1 + kWorleyN + kWorleyPz)
+// for the cube's (floor) cells.  Negated once per kernel (pinned in a VGPR,
+// DensityK::wt_nc), so that fmaf(x, 16, nc) is one v_fmamk with a literal
+// instead of a v_fma whose 16.0 sits in an SGPR (half issue rate, sec. 5.5).
+__device__ __forceinline__ float worley9_nc(int lo) { return -(float)(16 * lo * (1 + kWorleyN + kWorleyPz)); }
+// Cell distances are finite (table entries and sample coordinates are), so
+// the minimum starts from the first cell instead of FLT_MAX: the same value,
+// one min operand fewer.
+__device__ inline float cellular_table9_full(const float4* __restrict__ tab, float nc, float x, float y, float z)
 {
     const float xr = rintf(x), yr = rintf(y), zr = rintf(z);
-    const float c = (float)(16 * (1 + lo) * (1 + kWorleyN + kWorleyPz));
-    const float fo = fmaf(zr, (float)(16 * kWorleyPz), fmaf(yr, (float)(16 * kWorleyN), fmaf(xr, 16.0f, -c)));
+    // cells rint - 1 ..: the base one cell lower on every axis (exact small integers)
+    const float ncf = nc - (float)(16 * (1 + kWorleyN + kWorleyPz));
+    const float fo = fmaf(zr, (float)(16 * kWorleyPz), fmaf(yr, (float)(16 * kWorleyN), fmaf(xr, 16.0f, ncf)));
     const float4* t0 = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(tab) + (int)fo);
-    float d0 = 3.402823466e+38f;
+    float d0 = 0.0f;
 #pragma unroll
     for (int xi = -1; xi <= 1; ++xi) {
         const float xcf = (xr + (float)xi) - x;
@@ -355,7 +364,8 @@ __device__ inline float cellular_table9_full(const float4* __restrict__ tab, int
                 const float xd = fmaf(cc.x, cc.w, xcf);
                 const float yd = fmaf(cc.y, cc.w, ycf);
                 const float zd = fmaf(cc.z, cc.w, zcf);
-                d0 = fminf(d0, fmaf(zd, zd, fmaf(yd, yd, xd * xd)));
+                const float dd = fmaf(zd, zd, fmaf(yd, yd, xd * xd));
+                d0 = (xi == -1 && yi == -1 && zi == -1) ? dd : fminf(d0, dd);
             }
         }
     }
@@ -363,17 +373,16 @@ __device__ inline float cellular_table9_full(const float4* __restrict__ tab, int
 }
 // `full` (out): this lane evaluated all 27 cells after the cube's 8 (35 cell
 // evaluations instead of 8) -- what vr option "count" = 2 sums.
-__device__ inline float cellular_table9(const float4* __restrict__ tab, int lo, float x, float y, float z, bool& full)
+__device__ inline float cellular_table9(const float4* __restrict__ tab, float nc, float x, float y, float z, bool& full)
 {
     const float xf = floorf(x), yf = floorf(y), zf = floorf(z);
     // cellular()'s xcf = (integer cell coordinate) - x for the cube's two cells per axis
     const float x0 = xf - x, x1 = (xf + 1.0f) - x;
     const float y0 = yf - y, y1 = (yf + 1.0f) - y;
     const float z0 = zf - z, z1 = (zf + 1.0f) - z;
-    const float c = (float)(16 * lo * (1 + kWorleyN + kWorleyPz));
-    const float fo = fmaf(zf, (float)(16 * kWorleyPz), fmaf(yf, (float)(16 * kWorleyN), fmaf(xf, 16.0f, -c)));
+    const float fo = fmaf(zf, (float)(16 * kWorleyPz), fmaf(yf, (float)(16 * kWorleyN), fmaf(xf, 16.0f, nc)));
     const float4* t0 = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(tab) + (int)fo);
-    float d0 = 3.402823466e+38f;
+    float d0 = 0.0f;
 #pragma unroll
     for (int xi = 0; xi <= 1; ++xi) {
 #pragma unroll
@@ -384,7 +393,8 @@ __device__ inline float cellular_table9(const float4* __restrict__ tab, int lo, 
                 const float xd = fmaf(cc.x, cc.w, xi ? x1 : x0);
                 const float yd = fmaf(cc.y, cc.w, yi ? y1 : y0);
                 const float zd = fmaf(cc.z, cc.w, zi ? z1 : z0);
-                d0 = fminf(d0, fmaf(zd, zd, fmaf(yd, yd, xd * xd)));
+                const float dd = fmaf(zd, zd, fmaf(yd, yd, xd * xd));
+                d0 = (xi | yi | zi) == 0 ? dd : fminf(d0, dd);
             }
         }
     }
@@ -392,7 +402,7 @@ __device__ inline float cellular_table9(const float4* __restrict__ tab, int lo, 
     const float bound = fmaf(2.0f, fminf(gx, fminf(gy, gz)), fmaf(gz, gz, fmaf(gy, gy, fmaf(gx, gx, 1.0f))));
     const float e = __builtin_amdgcn_sqrtf(d0) + kPruneR;
     full = e * e > bound;
-    if (full) d0 = fminf(d0, cellular_table9_full(tab, lo, x, y, z));
+    if (full) d0 = fminf(d0, cellular_table9_full(tab, nc, x, y, z));
     return d0 - 1.0f;
 }
 
@@ -406,22 +416,21 @@ struct WorleyCube {
     int fo = -1;   // byte offset of the cached cube's base entry (-1: none)
     float4 c[8];
 };
-__device__ inline float cellular_table9_cached(const float4* __restrict__ tab, int lo, float x, float y, float z,
+__device__ inline float cellular_table9_cached(const float4* __restrict__ tab, float nc, float x, float y, float z,
                                                bool& full, WorleyCube& wc)
 {
     const float xf = floorf(x), yf = floorf(y), zf = floorf(z);
     const float x0 = xf - x, x1 = (xf + 1.0f) - x;
     const float y0 = yf - y, y1 = (yf + 1.0f) - y;
     const float z0 = zf - z, z1 = (zf + 1.0f) - z;
-    const float c = (float)(16 * lo * (1 + kWorleyN + kWorleyPz));
-    const int fo = (int)fmaf(zf, (float)(16 * kWorleyPz), fmaf(yf, (float)(16 * kWorleyN), fmaf(xf, 16.0f, -c)));
+    const int fo = (int)fmaf(zf, (float)(16 * kWorleyPz), fmaf(yf, (float)(16 * kWorleyN), fmaf(xf, 16.0f, nc)));
     if (fo != wc.fo) {
         wc.fo = fo;
         const float4* t0 = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(tab) + fo);
 #pragma unroll
         for (int k = 0; k < 8; ++k) wc.c[k] = t0[(k & 1) * kWorleyPz + ((k >> 1) & 1) * kWorleyN + (k >> 2)];
     }
-    float d0 = 3.402823466e+38f;
+    float d0 = 0.0f;
 #pragma unroll
     for (int xi = 0; xi <= 1; ++xi) {
 #pragma unroll
@@ -432,7 +441,8 @@ __device__ inline float cellular_table9_cached(const float4* __restrict__ tab, i
                 const float xd = fmaf(cc.x, cc.w, xi ? x1 : x0);
                 const float yd = fmaf(cc.y, cc.w, yi ? y1 : y0);
                 const float zd = fmaf(cc.z, cc.w, zi ? z1 : z0);
-                d0 = fminf(d0, fmaf(zd, zd, fmaf(yd, yd, xd * xd)));
+                const float dd = fmaf(zd, zd, fmaf(yd, yd, xd * xd));
+                d0 = (xi | yi | zi) == 0 ? dd : fminf(d0, dd);
             }
         }
     }
@@ -440,7 +450,7 @@ __device__ inline float cellular_table9_cached(const float4* __restrict__ tab, i
     const float bound = fmaf(2.0f, fminf(gx, fminf(gy, gz)), fmaf(gz, gz, fmaf(gy, gy, fmaf(gx, gx, 1.0f))));
     const float e = __builtin_amdgcn_sqrtf(d0) + kPruneR;
     full = e * e > bound;
-    if (full) d0 = fminf(d0, cellular_table9_full(tab, lo, x, y, z));
+    if (full) d0 = fminf(d0, cellular_table9_full(tab, nc, x, y, z));
     return d0 - 1.0f;
 }
 

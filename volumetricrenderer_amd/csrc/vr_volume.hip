@@ -809,7 +809,7 @@ __global__ __launch_bounds__(256) void k_selftest_worley(int seed, unsigned long
             for (int b = 0; b < 3; ++b) c[b] = fminf(fmaxf(p[b] + r * (2.0f * unit() - 1.0f), 0.51f), 7.49f);
         }
         bool full;
-        const float got = noise::cellular_table9(tab, 0, c[0], c[1], c[2], full);
+        const float got = noise::cellular_table9(tab, noise::worley9_nc(0), c[0], c[1], c[2], full);
         const float want = noise::cellular(seed, c[0], c[1], c[2]);
         miss += __float_as_uint(got) != __float_as_uint(want);
     }
