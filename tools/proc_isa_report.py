@@ -66,28 +66,61 @@ def mix(body, lines):
     return cls, cyc, ops
 
 
+def basic_blocks(body, lo, hi):
+    """Label-delimited line ranges [a, b) inside [lo, hi]."""
+    cuts = [i for i in range(lo, hi + 1) if re.match(r"^\.LBB\S+:", body[i])]
+    edges = sorted(set([lo] + cuts + [hi + 1]))
+    return [(a, b) for a, b in zip(edges, edges[1:]) if b > a]
+
+
 def report(path, want, octaves, cells, pmc):
     body = kernel_body(path, want)
     ls = loops(body)
     regions = [(a, b, count(body, range(a, b + 1))) for a, b in ls]
-    oct_ = max((r for r in regions if r[2]["LDS"] == 8 and r[2]["VMEM"] == 1), key=lambda r: r[2]["VALU"])
-    samp = min((r for r in regions if r[2]["LDS"] == 16 and r[0] <= oct_[0] and r[1] >= oct_[1]),
-               key=lambda r: r[1] - r[0])
-    full = min((r for r in regions if r[2]["LDS"] == 43 and r[0] <= samp[0] and r[1] >= samp[1]),
-               key=lambda r: r[1] - r[0])
-    L_oct = set(range(oct_[0], oct_[1] + 1))
-    L_rest = set(range(samp[0], samp[1] + 1)) - L_oct
-    L_full = set(range(full[0], full[1] + 1)) - set(range(samp[0], samp[1] + 1))
     p_full = max(0.0, (cells - 8.0) / 27.0)
-    parts = [("octave x %d" % octaves, L_oct, octaves), ("rest of the sample", L_rest, 1.0),
-             ("27-cell block x %.3f" % p_full, L_full, p_full)]
+    allb = basic_blocks(body, 0, len(body) - 1)
+    nld = lambda a, b: sum(1 for x in instrs(body, range(a, b)) if x.startswith("buffer_load_dwordx2"))
+    fb = max(allb, key=lambda ab: nld(*ab))
+    if nld(*fb) < 2:   # the octave loop (fbm_lat<0>) is the hot one
+        oct_ = max((r for r in regions if r[2]["LDS"] == 8 and r[2]["VMEM"] == 1), key=lambda r: r[2]["VALU"])
+        samp = min((r for r in regions if r[2]["LDS"] == 16 and r[0] <= oct_[0] and r[1] >= oct_[1]),
+                   key=lambda r: r[1] - r[0])
+        full = min((r for r in regions if r[2]["LDS"] == 43 and r[0] <= samp[0] and r[1] >= samp[1]),
+                   key=lambda r: r[1] - r[0])
+        L_oct = set(range(oct_[0], oct_[1] + 1))
+        L_rest = set(range(samp[0], samp[1] + 1)) - L_oct
+        L_full = set(range(full[0], full[1] + 1)) - set(range(samp[0], samp[1] + 1))
+        parts = [("octave x %d" % octaves, L_oct, octaves), ("rest of the sample", L_rest, 1.0),
+                 ("27-cell block x %.3f" % p_full, L_full, p_full)]
+    else:
+        # fbm_lat<OCT> fully unrolled: the basic block with the lattice loads of
+        # every octave; the sample loop is the smallest loop around it (its
+        # nested loops -- the p.octaves != OCT fallback -- and the fallback's
+        # other lattice-load blocks excluded), and the 27-cell block its basic
+        # blocks of >= 20 LDS reads
+        samp = min((r for r in regions if r[0] <= fb[0] and r[1] >= fb[1] - 1), key=lambda r: r[1] - r[0])
+        inner = [r for r in regions if samp[0] <= r[0] and r[1] <= samp[1] and (r[0], r[1]) != (samp[0], samp[1])]
+        blocks = basic_blocks(body, samp[0], samp[1])
+        L_oct = set(range(*fb))
+        L_full = set()
+        excl = set()
+        for a, b in blocks:
+            if (a, b) != fb and any(x.startswith("v_rndne_f32") for x in instrs(body, range(a, b))):
+                L_full |= set(range(a, b))   # cellular_table9_full: rintf per axis
+            elif (a, b) != fb and nld(a, b):
+                excl |= set(range(a, b))
+        for a, b, _ in inner:
+            excl |= set(range(a, b + 1))
+        L_rest = set(range(samp[0], samp[1] + 1)) - L_oct - L_full - excl
+        parts = [("fbm, %d octaves unrolled" % octaves, L_oct, 1.0), ("rest of the sample", L_rest, 1.0),
+                 ("27-cell block x %.3f" % p_full, L_full, p_full)]
     tot_cls, tot_cyc = collections.Counter(), collections.Counter()
     print(f"{body[0].split(':')[0]}")
     for name, L, w in parts:
         cls, cyc, ops = mix(body, L)
         print(f"  {name:24s} per pass: {sum(cls.values()):4d} VALU, {sum(cyc.values()):7.1f} issue cycles; "
               + ", ".join(f"{k} {cls[k]}" for k in ("flop", "int", "conv", "sel", "move")))
-        if name.startswith("octave") or name.startswith("rest"):
+        if name.startswith(("octave", "fbm", "rest")):
             print("      " + ", ".join(f"{op} {k}" for op, k in ops.most_common(12)))
         for k in cls:
             tot_cls[k] += w * cls[k]

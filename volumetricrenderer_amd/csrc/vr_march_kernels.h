@@ -559,6 +559,9 @@ __device__ __forceinline__ DensityK density_k(const ProcParams& p, float scale)
 #ifndef VR_FBM_UNROLL_BY
 #define VR_FBM_UNROLL_BY 1
 #endif
+#ifndef VR_FBM_PREFETCH   // fbm_lat<0>: the next octave's lattice word loaded during this one
+#define VR_FBM_PREFETCH 1
+#endif
 #ifndef VR_FBM_UNROLL
 // the primary marches' fBm with the recipe's 4 octaves unrolled (no
 // loop-carried register copies): config 2 -4 % at 4 waves per SIMD
@@ -571,6 +574,23 @@ __device__ __forceinline__ float fbm_lat(const ProcParams& p, const DensityK& k,
                                          float qz)
 {
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p.lat, (short)0, (int)p.lat_bytes, 0x00020000);
+#if !VR_FBM_PREFETCH
+    if constexpr (OCT == 0) {   // no loop-carried prefetch: each octave loads its own word
+        float f = k.f0, amp = 1.0f, fbm = 0.0f;
+#pragma unroll VR_FBM_UNROLL_BY
+        for (int o = 0; o < p.octaves; ++o) {
+            const float x = qx * f, y = qy * f, z = qz * f;
+            const float xs = floorf(x), ys = floorf(y), zs = floorf(z);
+            const auto w = __builtin_amdgcn_raw_buffer_load_b64(
+                rsrc, (unsigned)fmaf(zs, k.lat_sz, fmaf(ys, k.lat_sy, fmaf(xs, 8.0f, k.lat_nc))), 0, 0);
+            const float pn = noise::perlin_lat(gp, make_uint2(w[0], w[1]), x, y, z, xs, ys, zs);
+            fbm = fmaf(amp, pn, fbm);
+            f = f * k.lac;
+            amp = amp * k.gain;
+        }
+        return fbm;
+    }
+#endif
     float f = k.f0, amp = 1.0f, fbm = 0.0f;
     float x = qx * f, y = qy * f, z = qz * f;
     float xs = floorf(x), ys = floorf(y), zs = floorf(z);
