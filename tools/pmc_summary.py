@@ -5,6 +5,7 @@ import glob
 import json
 import sys
 
+CPI = 2.74   # --cpi
 
 def load(tag, kernel="march"):
     agg = collections.defaultdict(list)
@@ -20,9 +21,17 @@ def derived(c):
     d = {}
     if "GRBM_GUI_ACTIVE" in c:
         d["gpu_cycles_per_xcd"] = c["GRBM_GUI_ACTIVE"] / 8
-    if "SQ_ACTIVE_INST_VALU" in c and "GRBM_GUI_ACTIVE" in c:
-        # quad-cycles of VALU issue over all SIMDs vs SIMD quad-cycles available
-        d["valu_busy"] = c["SQ_ACTIVE_INST_VALU"] / (1024 * c["GRBM_GUI_ACTIVE"] / 8 / 4)
+    if "SQ_INSTS_VALU" in c and "GRBM_GUI_ACTIVE" in c:
+        # VALU wave-instructions per SIMD-cycle (1,024 SIMDs; GRBM_GUI_ACTIVE
+        # sums the 8 XCDs), and the VALU issue utilisation: that times the
+        # kernel's mean calibrated SIMD cycles per wave64 instruction (its
+        # static opcode mix weighted by tools/isa_cost.py, profiles/valu_calib.txt;
+        # --cpi, default 2.74 = the procedural density's, tools/proc_isa_report.py).
+        # (Round 4's valu_busy divided SQ_ACTIVE_INST_VALU, a per-wave
+        # count, by per-SIMD quad-cycles and read above 1.)
+        ipc = c["SQ_INSTS_VALU"] / (1024 * c["GRBM_GUI_ACTIVE"] / 8)
+        d["valu_insts_per_simd_cycle"] = ipc
+        d["valu_issue_util"] = ipc * CPI
     for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_LDS"):
         if k in c and "SQ_WAVE_CYCLES" in c:
             d[k + "_frac"] = c[k] / c["SQ_WAVE_CYCLES"]
@@ -53,8 +62,13 @@ def derived(c):
 
 
 if __name__ == "__main__":
-    # TAG or TAG:KERNEL (substring of the kernel name; default "march")
-    for arg in sys.argv[1:]:
+    # TAG or TAG:KERNEL (substring of the kernel name; default "march") [--cpi X]
+    args = sys.argv[1:]
+    if "--cpi" in args:
+        i = args.index("--cpi")
+        CPI = float(args[i + 1])
+        del args[i:i + 2]
+    for arg in args:
         tag, _, kern = arg.partition(":")
         c = load(tag, kern or "march")
         print(arg, json.dumps({k: round(v, 4) for k, v in {**c, **derived(c)}.items()}, indent=0))

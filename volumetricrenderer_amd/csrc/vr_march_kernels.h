@@ -560,7 +560,7 @@ __device__ __forceinline__ DensityK density_k(const ProcParams& p, float scale)
 #define VR_FBM_UNROLL_BY 1
 #endif
 #ifndef VR_FBM_PREFETCH   // fbm_lat<0>: the next octave's lattice word loaded during this one
-#define VR_FBM_PREFETCH 1
+#define VR_FBM_PREFETCH 0   // off: config 3 -0.7 % (the shadow pass: 10 % fewer issue cycles, its loads now wait), profiles/r05/ab_nopf.txt
 #endif
 #ifndef VR_FBM_UNROLL
 // the primary marches' fBm with the recipe's 4 octaves unrolled (no
