@@ -31,7 +31,11 @@ def loops(body):
             tgt = m.group(1) or m.group(2)
             if tgt in labels and labels[tgt] < i:
                 out.append((labels[tgt], i))
-    return out
+    # several back edges to one header are one loop (to its last back edge)
+    last = {}
+    for a, b in out:
+        last[a] = max(b, last.get(a, b))
+    return sorted(last.items())
 
 
 def instrs(body, lines):
@@ -69,6 +73,8 @@ def mix(body, lines):
 def basic_blocks(body, lo, hi):
     """Label-delimited line ranges [a, b) inside [lo, hi]."""
     cuts = [i for i in range(lo, hi + 1) if re.match(r"^\.LBB\S+:", body[i])]
+    # a block also ends after a branch (exec-masked ifs fall through)
+    cuts += [i + 1 for i in range(lo, hi) if re.search(r"\bs_(cbranch_\w+|branch)\b", body[i])]
     edges = sorted(set([lo] + cuts + [hi + 1]))
     return [(a, b) for a, b in zip(edges, edges[1:]) if b > a]
 
@@ -83,13 +89,20 @@ def report(path, want, octaves, cells, pmc):
     fb = max(allb, key=lambda ab: nld(*ab))
     if nld(*fb) < 2:   # the octave loop (fbm_lat<0>) is the hot one
         oct_ = max((r for r in regions if r[2]["LDS"] == 8 and r[2]["VMEM"] == 1), key=lambda r: r[2]["VALU"])
-        samp = min((r for r in regions if r[2]["LDS"] == 16 and r[0] <= oct_[0] and r[1] >= oct_[1]),
-                   key=lambda r: r[1] - r[0])
-        full = min((r for r in regions if r[2]["LDS"] == 43 and r[0] <= samp[0] and r[1] >= samp[1]),
+        samp = min((r for r in regions if r[2]["LDS"] >= 16 and r[0] <= oct_[0] and r[1] >= oct_[1]),
                    key=lambda r: r[1] - r[0])
         L_oct = set(range(oct_[0], oct_[1] + 1))
-        L_rest = set(range(samp[0], samp[1] + 1)) - L_oct
-        L_full = set(range(full[0], full[1] + 1)) - set(range(samp[0], samp[1] + 1))
+        L_samp = set(range(samp[0], samp[1] + 1))
+        if samp[2]["LDS"] >= 43:   # the 27-cell block inside the sample loop: its rintf blocks
+            L_full = set()
+            for a, b in basic_blocks(body, samp[0], samp[1]):
+                if not (L_oct & set(range(a, b))) and any(x.startswith("v_rndne_f32") for x in instrs(body, range(a, b))):
+                    L_full |= set(range(a, b))
+        else:   # a loop of its own around the sample loop
+            full = min((r for r in regions if r[2]["LDS"] >= 43 and r[0] <= samp[0] and r[1] >= samp[1]),
+                       key=lambda r: r[1] - r[0])
+            L_full = set(range(full[0], full[1] + 1)) - L_samp
+        L_rest = L_samp - L_oct - L_full
         parts = [("octave x %d" % octaves, L_oct, octaves), ("rest of the sample", L_rest, 1.0),
                  ("27-cell block x %.3f" % p_full, L_full, p_full)]
     else:
@@ -109,6 +122,11 @@ def report(path, want, octaves, cells, pmc):
                 L_full |= set(range(a, b))   # cellular_table9_full: rintf per axis
             elif (a, b) != fb and nld(a, b):
                 excl |= set(range(a, b))
+        if not L_full:   # the 27-cell block without rintf of its own: its >= 20 LDS reads
+            for a, b in blocks:
+                if (a, b) != fb and sum(1 for x in instrs(body, range(a, b)) if x.startswith("ds_read")) >= 20:
+                    L_full |= set(range(a, b))
+            excl -= L_full
         for a, b, _ in inner:
             excl |= set(range(a, b + 1))
         L_rest = set(range(samp[0], samp[1] + 1)) - L_oct - L_full - excl
