@@ -286,6 +286,8 @@ def main() -> int:
                     help="N > 1 (native loop, 2 render streams): each frame's exchange on its render stream, over one "
                          "communicator per buffer parity, no events (the default), or on a communication stream "
                          "ordered by events (vr_shard_set_exchange_streams)")
+    ap.add_argument("--inflight-probe", action="store_true",
+                    help="N = 1: also time the same frames with two in flight (frames_in_flight_2 in the line)")
     ap.add_argument("--spin", action="store_true",
                     help="moving camera: every frame gets new shader data, phi += 1.6 deg (the reference's "
                          "held A/D key, TestMain.cpp:171-184, :222-224), queued natively (vr_render_sequence "
@@ -484,11 +486,13 @@ def main() -> int:
     # The same K frames with two in flight (consecutive frames on two
     # alternating streams and targets, the reference's 2 frames in flight,
     # VulkanRenderer.cpp:13), timed after the main window under the same clock
-    # (N = 1).  Launches then overlap, so their durations no longer measure a
-    # frame: the headline keeps one stream, whose per-launch time the roofline
-    # and the rocprof profile use.
+    # (N = 1; --inflight-probe).  Launches then overlap, so their durations no
+    # longer measure a frame: the headline keeps one stream, whose per-launch
+    # time the roofline and the rocprof profile use -- and the probe is opt-in,
+    # so that the default run's rocprof average holds only one-stream launches.
     inflight2 = None
-    if world == 1 and not native and not args.spin and proc is None and args.inflight == 1:
+    if (world == 1 and not native and not args.spin and proc is None and args.inflight == 1
+            and args.inflight_probe):
         sh2 = vrdist.BandSharder(r, W, H, fmt, band_rows=16, world=1, rank=0, inflight=2)
         sh2.run_frames(args.warmup)
         torch.cuda.synchronize()
