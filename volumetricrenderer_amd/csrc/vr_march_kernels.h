@@ -629,10 +629,65 @@ __device__ __forceinline__ float fbm_lat(const ProcParams& p, const DensityK& k,
     return fbm;
 }
 
+// The recipe's density (TABLE 3, OCT octaves unrolled) in three phases: the
+// lattice words of every octave are loaded first, the Worley cube is computed
+// while they are in flight (its LDS reads and ~100 VALU ops hide the global
+// load latency that fbm_lat<OCT> waits out at its first octave), then the
+// octaves.  The same operations on the same values as proc_density: the fBm
+// and F1 are independent until the final combine.
+#ifndef VR_PROC_PHASES
+#define VR_PROC_PHASES 0
+#endif
+#ifndef VR_PHASE_FENCE
+#define VR_PHASE_FENCE 1
+#endif
+template <int OCT>
+__device__ __forceinline__ float proc_density_phased(const ProcParams& p, const DensityK& k, const float4* wt,
+                                                     float px, float py, float pz, unsigned& cells)
+{
+    const float qx = px * k.gs, qy = py * k.gs, qz = pz * k.gs;
+    const float4* gp = wt + noise::kWorleyN * noise::kWorleyPz;
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p.lat, (short)0, (int)p.lat_bytes, 0x00020000);
+    float X[OCT], Y[OCT], Z[OCT], XS[OCT], YS[OCT], ZS[OCT];
+    uint2 W[OCT];
+    float f = k.f0;
+#pragma unroll
+    for (int o = 0; o < OCT; ++o) {
+        if (o > 0) f = f * k.lac;
+        X[o] = qx * f; Y[o] = qy * f; Z[o] = qz * f;
+        XS[o] = floorf(X[o]); YS[o] = floorf(Y[o]); ZS[o] = floorf(Z[o]);
+        const auto w = __builtin_amdgcn_raw_buffer_load_b64(
+            rsrc, (unsigned)fmaf(ZS[o], k.lat_sz, fmaf(YS[o], k.lat_sy, fmaf(XS[o], 8.0f, k.lat_nc))), 0, 0);
+        W[o] = make_uint2(w[0], w[1]);
+    }
+#if VR_PHASE_FENCE
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+    const float wf = k.wf;
+    bool full;
+    const float f1 = noise::cellular_table9(wt, k.wt_nc, qx * wf, qy * wf, qz * wf, full) + 1.0f;
+    if (p.count_evals == 2) cells += full ? 35u : 8u;
+#if VR_PHASE_FENCE
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+    float amp = 1.0f, fbm = 0.0f;
+#pragma unroll
+    for (int o = 0; o < OCT; ++o) {
+        const float pn = noise::perlin_lat(gp, W[o], X[o], Y[o], Z[o], XS[o], YS[o], ZS[o]);
+        fbm = fmaf(amp, pn, fbm);
+        amp = amp * k.gain;
+    }
+    return fmaxf(fbm * (1.0f - f1), 0.0f) * k.scale;
+}
+
 template <int TABLE, bool WC = false, bool UNROLL = false>
 __device__ __forceinline__ float proc_density(const ProcParams& p, const DensityK& k, const float4* wt, float px,
                                               float py, float pz, unsigned& cells, noise::WorleyCube* wc = nullptr)
 {
+#if VR_PROC_PHASES && VR_FBM_UNROLL
+    if constexpr (TABLE == 3 && UNROLL && !WC)
+        if (p.octaves == VR_FBM_UNROLL) return proc_density_phased<VR_FBM_UNROLL>(p, k, wt, px, py, pz, cells);
+#endif
     const float qx = px * k.gs, qy = py * k.gs, qz = pz * k.gs;
     float fbm = 0.0f;
     if constexpr (TABLE == 3) {

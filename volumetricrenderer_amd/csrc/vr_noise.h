@@ -333,6 +333,9 @@ __device__ inline float cellular_table(const float4* __restrict__ tab, int lo, i
 // kPruneR - jitter = 5.6e-5 in distance, >> fp32 rounding of the distance
 // sums), so the result is bit-identical to cellular().  Modelled on config 2
 // (tools/worley_prune_model.py): 94 % of wave-steps need the cube only.
+#ifndef VR_CUBE_BATCH
+#define VR_CUBE_BATCH 0
+#endif
 constexpr int kWorleyN = 9, kWorleyPz = 83;
 constexpr float kPruneR = 0.3962f;
 // The table's base byte offset term, negated: -16 lo (1 + kWorleyN + kWorleyPz)
@@ -382,6 +385,18 @@ __device__ inline float cellular_table9(const float4* __restrict__ tab, float nc
     const float z0 = zf - z, z1 = (zf + 1.0f) - z;
     const float fo = fmaf(zf, (float)(16 * kWorleyPz), fmaf(yf, (float)(16 * kWorleyN), fmaf(xf, 16.0f, nc)));
     const float4* t0 = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(tab) + (int)fo);
+#if VR_CUBE_BATCH
+    // the cube's 8 LDS reads all in flight before the first use (one LDS round
+    // trip per sample instead of up to 8): the empty asm takes every entry as
+    // an operand, so the reads are issued ahead of it and used after it
+    // entry k = xi * 4 + yi * 2 + zi, as native 4-vectors (register tuples for the asm)
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    const v4f* tv = reinterpret_cast<const v4f*>(t0);
+    v4f c0 = tv[0], c1 = tv[kWorleyPz], c2 = tv[kWorleyN], c3 = tv[kWorleyN + kWorleyPz];
+    v4f c4 = tv[1], c5 = tv[1 + kWorleyPz], c6 = tv[1 + kWorleyN], c7 = tv[1 + kWorleyN + kWorleyPz];
+    asm volatile("" : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3), "+v"(c4), "+v"(c5), "+v"(c6), "+v"(c7));
+    const v4f cv[8] = {c0, c1, c2, c3, c4, c5, c6, c7};
+#endif
     float d0 = 0.0f;
 #pragma unroll
     for (int xi = 0; xi <= 1; ++xi) {
@@ -389,7 +404,12 @@ __device__ inline float cellular_table9(const float4* __restrict__ tab, float nc
         for (int yi = 0; yi <= 1; ++yi) {
 #pragma unroll
             for (int zi = 0; zi <= 1; ++zi) {
+#if VR_CUBE_BATCH
+                const v4f cq = cv[xi * 4 + yi * 2 + zi];
+                const float4 cc = make_float4(cq.x, cq.y, cq.z, cq.w);
+#else
                 const float4 cc = t0[zi * kWorleyPz + yi * kWorleyN + xi];
+#endif
                 const float xd = fmaf(cc.x, cc.w, xi ? x1 : x0);
                 const float yd = fmaf(cc.y, cc.w, yi ? y1 : y0);
                 const float zd = fmaf(cc.z, cc.w, zi ? z1 : z0);
