@@ -636,7 +636,7 @@ __device__ __forceinline__ float fbm_lat(const ProcParams& p, const DensityK& k,
 // octaves.  The same operations on the same values as proc_density: the fBm
 // and F1 are independent until the final combine.
 #ifndef VR_PROC_PHASES
-#define VR_PROC_PHASES 0
+#define VR_PROC_PHASES 1   // config 2 -2.8 %, config 3 -1.7 % (profiles/r05/ab_phases.txt)
 #endif
 #ifndef VR_PHASE_FENCE
 #define VR_PHASE_FENCE 1
@@ -1950,6 +1950,9 @@ constexpr int kScanThreads = 1024;
     for (unsigned k = lane; k * 64u < n; k += 64u) d.map[c0 + k] = make_uint4(e0 + k * 64u, 0u, min(64u, n - k * 64u), 0u);
 }
 
+#ifndef VR_SHADOW_PHASED   // the shadow pass's density through proc_density_phased (unrolled octaves)
+#define VR_SHADOW_PHASED 0
+#endif
 #ifndef VR_SHADOW_ATTR
 #ifdef VR_SHADOW_WAVES   // timing experiments: the shadow pass built for this many waves per SIMD
 #define VR_SHADOW_ATTR __attribute__((amdgpu_waves_per_eu(VR_SHADOW_WAVES)))
@@ -1983,7 +1986,7 @@ __global__ __launch_bounds__(kThreads) VR_SHADOW_ATTR void proc_shadow_eval(cons
                 // of the loops they take the pass from 75 to 86 VGPRs (6 -> 5
                 // waves per SIMD) and it ran 0.4 % slower (profiles/r05)
                 const DensityK dk = density_k<TABLE>(p, a.scale);
-                sl = sl + proc_density<TABLE, WC>(p, dk, wt, q0, q1, q2, cells, &wc);
+                sl = sl + proc_density<TABLE, WC, (VR_SHADOW_PHASED != 0)>(p, dk, wt, q0, q1, q2, cells, &wc);
                 ++evals;
             }
         }
