@@ -1950,8 +1950,14 @@ constexpr int kScanThreads = 1024;
     for (unsigned k = lane; k * 64u < n; k += 64u) d.map[c0 + k] = make_uint4(e0 + k * 64u, 0u, min(64u, n - k * 64u), 0u);
 }
 
-#ifndef VR_SHADOW_PHASED   // the shadow pass's density through proc_density_phased (unrolled octaves)
-#define VR_SHADOW_PHASED 0
+// the shadow pass's density through proc_density_phased (unrolled octaves),
+// held to 5 waves per SIMD: config 3 -2.3 % (profiles/r05/ab_shadow_phased.txt;
+// 4 waves, uncapped at 107 VGPRs: level)
+#ifndef VR_SHADOW_PHASED
+#define VR_SHADOW_PHASED 1
+#endif
+#if VR_SHADOW_PHASED && !defined(VR_SHADOW_WAVES)
+#define VR_SHADOW_WAVES 5
 #endif
 #ifndef VR_SHADOW_ATTR
 #ifdef VR_SHADOW_WAVES   // timing experiments: the shadow pass built for this many waves per SIMD
