@@ -171,12 +171,6 @@ struct vr_shard {
     uint8_t* frame[2] = {};           // rank 0
     hipEvent_t rendered[2] = {}, done[2] = {};
     hipEvent_t tail[2] = {};          // rank 0: the end of the render streams' frames (vr_shard_run_frames)
-    // rank 0, exchange on the render streams: the assembly on a stream of its
-    // own (timing experiment, VR_SHARD_ASM_CUS = n: n CUs for it and the rest
-    // for the render streams; VR_SHARD_ASM_PRIO = 1: a high-priority stream)
-    hipStream_t asm_stream = nullptr;
-    hipEvent_t asm_in[2] = {}, asm_done[2] = {};
-    bool asm_pending[2] = {};
     hipEvent_t fence = nullptr;       // vr_shard_barrier: the caller's stream -> comm stream
     int* token = nullptr;             // [0]: vr_shard_barrier's all-reduced int; [1..7]:
                                       // vr_shard_share_volume's agreement vector
@@ -285,10 +279,7 @@ void release(vr_shard* sh)
     for (hipStream_t rs : sh->render_stream)
         if (rs) (void)hipStreamSynchronize(rs);
     if (sh->comm_stream) (void)hipStreamSynchronize(sh->comm_stream);
-    if (sh->asm_stream) (void)hipStreamSynchronize(sh->asm_stream);
     for (int p = 0; p < 2; ++p) {
-        if (sh->asm_in[p]) (void)hipEventDestroy(sh->asm_in[p]);
-        if (sh->asm_done[p]) (void)hipEventDestroy(sh->asm_done[p]);
         if (sh->local[p]) (void)hipFree(sh->local[p]);
         if (sh->gathered[p]) (void)hipFree(sh->gathered[p]);
         if (sh->frame[p]) (void)hipFree(sh->frame[p]);
@@ -302,7 +293,6 @@ void release(vr_shard* sh)
     if (sh->comm2) (void)ncclCommDestroy(sh->comm2);
     if (sh->comm) (void)ncclCommDestroy(sh->comm);   // an aborted communicator is already gone
     if (sh->comm_stream) (void)hipStreamDestroy(sh->comm_stream);
-    if (sh->asm_stream) (void)hipStreamDestroy(sh->asm_stream);
     for (hipStream_t rs : sh->render_stream)
         if (rs) (void)hipStreamDestroy(rs);
     delete sh;
@@ -434,8 +424,6 @@ vr_status one_frame_on_render(vr_shard* sh, int p, hipStream_t rs, hipEvent_t t0
             if (sh->rows_of[r] > 0) VR_TRY(vr_render(sh->ctx, &t, rs));
         }
     }
-    const bool side = r0 && sh->asm_stream && sh->nranks > 1;
-    if (side && sh->asm_pending[p]) HIP_TRY(hipStreamWaitEvent(rs, sh->asm_done[p], 0));   // gathered[p] read
     if (sh->nranks > 1 && !sh->loopback) {
         ncclComm_t c = p == 0 ? sh->comm : sh->comm2;
         NCCL_TRY(ncclGroupStart());
@@ -449,18 +437,9 @@ vr_status one_frame_on_render(vr_shard* sh, int p, hipStream_t rs, hipEvent_t t0
         }
         NCCL_TRY(ncclGroupEnd());
     }
-    if (side) {   // the other ranks' rows on the assembly stream, after the receive
-        HIP_TRY(hipEventRecord(sh->asm_in[p], rs));
-        HIP_TRY(hipStreamWaitEvent(sh->asm_stream, sh->asm_in[p], 0));
-        VR_TRY(vr_assemble_frame_ranks(sh->ctx, sh->gathered[p], sh->gformat, (size_t)sh->rows_per_rank, sh->nranks,
-                                       1, sh->width, sh->height, sh->band_rows, sh->format, sh->frame[p],
-                                       sh->asm_stream));
-        HIP_TRY(hipEventRecord(sh->asm_done[p], sh->asm_stream));
-        sh->asm_pending[p] = true;
-    } else if (r0 && sh->nranks > 1) {
+    if (r0 && sh->nranks > 1)
         VR_TRY(vr_assemble_frame_ranks(sh->ctx, sh->gathered[p], sh->gformat, (size_t)sh->rows_per_rank, sh->nranks,
                                        1, sh->width, sh->height, sh->band_rows, sh->format, sh->frame[p], rs));
-    }
     sh->last = p;
     return VR_OK;
 }
@@ -536,36 +515,7 @@ try {
     hip_ok(e, "hipGetDevice");
     sh->device = dev;
     hip_ok(hipStreamCreateWithFlags(&sh->comm_stream, hipStreamNonBlocking), "comm stream");
-    const char* ecus = std::getenv("VR_SHARD_ASM_CUS");
-    const char* eprio = std::getenv("VR_SHARD_ASM_PRIO");
-    const int acus = ecus ? std::atoi(ecus) : 0, aprio = eprio ? std::atoi(eprio) : 0;
-    if (rank == 0 && nranks > 1 && acus > 0) {
-        int ncu = 0;
-        hip_ok(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev), "CU count");
-        const int n = std::min(std::max(acus, 1), std::max(ncu / 2, 1));
-        std::vector<uint32_t> ma((ncu + 31) / 32, 0u), mr((ncu + 31) / 32, 0u);
-        for (int i = 0, k = 0; i < ncu; ++i) {   // every (ncu / n)-th CU for the assembly
-            const bool a = k < n && i % std::max(ncu / n, 1) == 0;
-            k += a;
-            (a ? ma : mr)[i / 32] |= 1u << (i % 32);
-        }
-        hip_ok(hipExtStreamCreateWithCUMask(&sh->asm_stream, (uint32_t)ma.size(), ma.data()), "assembly stream");
-        for (hipStream_t& rs : sh->render_stream)
-            hip_ok(hipExtStreamCreateWithCUMask(&rs, (uint32_t)mr.size(), mr.data()), "render stream");
-    } else {
-        if (rank == 0 && nranks > 1 && aprio) {
-            int lo = 0, hi = 0;
-            hip_ok(hipDeviceGetStreamPriorityRange(&lo, &hi), "priorities");
-            hip_ok(hipStreamCreateWithPriority(&sh->asm_stream, hipStreamNonBlocking, hi), "assembly stream");
-        }
-        for (hipStream_t& rs : sh->render_stream)
-            hip_ok(hipStreamCreateWithFlags(&rs, hipStreamNonBlocking), "render stream");
-    }
-    if (sh->asm_stream)
-        for (int p = 0; p < 2; ++p) {
-            hip_ok(hipEventCreateWithFlags(&sh->asm_in[p], hipEventDisableTiming), "event");
-            hip_ok(hipEventCreateWithFlags(&sh->asm_done[p], hipEventDisableTiming), "event");
-        }
+    for (hipStream_t& rs : sh->render_stream) hip_ok(hipStreamCreateWithFlags(&rs, hipStreamNonBlocking), "render stream");
     hip_ok(hipEventCreateWithFlags(&sh->fence, hipEventDisableTiming), "event");
     if (hip_ok(hipMalloc(&sh->token, 8 * sizeof(int)), "barrier token"))
         hip_ok(hipMemset(sh->token, 0, 8 * sizeof(int)), "barrier token");
@@ -712,10 +662,6 @@ try {
         }
         // join: the caller's stream after both render streams' last frames
         for (int q = 0; q < 2; ++q) {
-            if (sh->asm_pending[q]) {   // (and their assemblies)
-                HIP_TRY(hipStreamWaitEvent(sh->render_stream[q], sh->asm_done[q], 0));
-                sh->asm_pending[q] = false;
-            }
             HIP_TRY(hipEventRecord(sh->tail[q], sh->render_stream[q]));
             HIP_TRY(hipStreamWaitEvent(s, sh->tail[q], 0));
             // a later comm-stream frame of parity q waits for this one
