@@ -117,7 +117,11 @@ def native(a):
             res = {ns: [] for ns in streams}   # per stream count: per round, the slowest rank's ms/frame
             per_rank = {ns: {} for ns in streams}   # per stream count, rank: ms/frame per round
             host = {ns: [] for ns in streams}
-            pipes = {}
+            # one rank's pipeline at a time: its streams get HIP's hardware
+            # queues to themselves (GPU_MAX_HW_QUEUES = 4 per process), as in
+            # the N-process run; pipelines of all ranks alive at once would
+            # share queues and serialise each other's render streams
+            per_round = {ns: [[] for _ in range(a.rounds)] for ns in streams}
             for first in (range(n) if a.all_ranks else (0,)):
                 for ns in streams:
                     p = RcclBandPipeline(r, W, H, vr.FMT_RGBA8_UNORM, band_rows=a.band_rows, world=n, rank=first,
@@ -125,12 +129,7 @@ def native(a):
                                          exchange_on_render=a.exchange == "render")
                     p.run_frames(8)   # region lists, code objects
                     p.barrier()
-                    pipes[(first, ns)] = p
-            for _ in range(a.rounds):
-                for ns in streams:
-                    worst, hmax = 0.0, 0.0
-                    for first in (range(n) if a.all_ranks else (0,)):
-                        p = pipes[(first, ns)]
+                    for k in range(a.rounds):
                         p.run_frames(4)
                         p.barrier()
                         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -140,13 +139,13 @@ def native(a):
                         p.run_frames(a.frames)
                         e1.record()
                         torch.cuda.synchronize()
-                        worst = max(worst, e0.elapsed_time(e1) / a.frames)
-                        per_rank[ns].setdefault(first, []).append(e0.elapsed_time(e1) / a.frames)
-                        hmax = max(hmax, p.host_ms)
-                    res[ns].append(worst)
-                    host[ns].append(hmax)
-            for p in pipes.values():
-                p.close()
+                        ms = e0.elapsed_time(e1) / a.frames
+                        per_round[ns][k].append(ms)
+                        per_rank[ns].setdefault(first, []).append(ms)
+                        host[ns].append(p.host_ms)
+                    p.close()
+            for ns in streams:
+                res[ns] = [max(v) for v in per_round[ns]]
             for ns in streams:
                 t = float(np.median(res[ns]))
                 if n == 1:
