@@ -633,8 +633,9 @@ try {
     const bool on_render = sh->on_render && two;
     if (on_render && frames > 0) {
         // the parity-1 communicator, once, split from the first (collective:
-        // every rank runs its first such frames together)
-        if (!sh->loopback && sh->nranks > 1 && !sh->comm2) {
+        // every rank runs its first such frames together; a one-rank
+        // communicator splits too, so its test covers the call)
+        if (!sh->loopback && !sh->comm2) {
             ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
             cfg.blocking = 0;
             const ncclResult_t r = ncclCommSplit(sh->comm, 0, sh->rank, &sh->comm2, &cfg);
