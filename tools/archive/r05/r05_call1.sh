@@ -2,7 +2,7 @@
 # round 5, call 1: the two-render-stream shard (parity), per-rank frame
 # streams 1 vs 2 render streams (configs 5 and 4), the default bench line
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 O=gpurun_out/r05
 mkdir -p $O
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp

@@ -3,7 +3,7 @@
 # the lerps) A/B on every config; the shard tests with the exchange on the
 # render streams as the default
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 O=gpurun_out/r05
 mkdir -p $O
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp

@@ -4,7 +4,7 @@
 # and one kernel trace of the N=8 rank-0 solo loop with a single stream
 # (the assembly kernel alone)
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 O=gpurun_out/r05
 mkdir -p $O
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp

@@ -2,7 +2,7 @@
 # round 5, call 12: the shadow pass's fBm loop without the loop-carried
 # lattice prefetch (no rotation copies) A/B on config 3
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 O=gpurun_out/r05
 mkdir -p $O
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp

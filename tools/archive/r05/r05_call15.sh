@@ -3,7 +3,7 @@
 # occupancy A/B (waves cap 4 / none / 5), the default bench line and its
 # rocprofv3 kernel statistics
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 O=gpurun_out/r05
 mkdir -p $O
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp

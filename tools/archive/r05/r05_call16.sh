@@ -3,7 +3,7 @@
 # they fly) and the batched Worley cube reads: procedural parity with each
 # variant library, then the A/B on configs 2 and 3
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 O=gpurun_out/r05
 mkdir -p $O
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp

@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 5, call 17: the shadow pass through the phased density (4 / 5 waves)
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 O=gpurun_out/r05
 mkdir -p $O
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp

@@ -2,7 +2,7 @@
 # round 5, call 2: smoke with the build id, the exception guard and the
 # spinning / region tests, then the host cost per frame of the native loop
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 O=gpurun_out/r05
 mkdir -p $O
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp

@@ -2,7 +2,7 @@
 # round 5, call 20: per-rank frame streams rehearsed one rank's pipeline at a
 # time (its streams on hardware queues of their own), configs 5 and 4
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 O=gpurun_out/r05
 mkdir -p $O
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp

@@ -2,7 +2,7 @@
 # round 5, call 3: host cost per frame (pieces), the region / procedural /
 # shard tests after the first-render retire events, per-rank frame streams
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 O=gpurun_out/r05
 mkdir -p $O
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp

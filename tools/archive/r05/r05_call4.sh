@@ -4,7 +4,7 @@
 # v2 = + 4 octaves unrolled, v3 = v2 + occupancy-constrained), tests after
 # the first-render retire events, per-rank frame streams
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 O=gpurun_out/r05
 mkdir -p $O
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp

@@ -3,7 +3,7 @@
 # the host-cost cuts (launch cache, rank 0 in place), lanes per ray swept
 # (the auto split was chosen for one stream), configs 5 and 4
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 O=gpurun_out/r05
 mkdir -p $O
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp

@@ -4,7 +4,7 @@
 # exchange on the comm stream vs on the render streams, configs 5 and 4;
 # procedural A/B of the default build against round 4's
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 O=gpurun_out/r05
 mkdir -p $O
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp

@@ -4,7 +4,7 @@
 # the render streams, and the deferred-shadow primary march's unroll /
 # occupancy A/B (config 3)
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 O=gpurun_out/r05
 mkdir -p $O
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp

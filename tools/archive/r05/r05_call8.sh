@@ -4,7 +4,7 @@
 # streams per rank (configs 5 and 4, exchange on render / comm streams) and a
 # kernel trace of the N=8 rank-0 loop
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 O=gpurun_out/r05
 mkdir -p $O
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp

@@ -2,7 +2,7 @@
 # round 5, final: the whole GPU suite, smoke(), the default bench line and its
 # rocprofv3 kernel statistics, the two-in-flight probe, per-rank frame streams
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 O=gpurun_out/r05
 mkdir -p $O
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
