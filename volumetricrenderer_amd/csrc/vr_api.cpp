@@ -201,6 +201,7 @@ struct Ctx {
         size_t cap = 0;            // entries
         TileMap map{};             // host copy: nwx (and off[] for host builds)
         int most = 0;              // the longest per-XCD list (sizes the launch)
+        int most_work = 0;         // the most tiles with work of one XCD
         int nwork = 0;             // tiles with estimated work
         int seg_len = 0;           // segments: steps per segment the lists were built for (0 = none)
         int nseg_tiles = 0;        // segmented tiles (slots of SegArgs.info)
@@ -246,6 +247,7 @@ struct Ctx {
     // loop) then skips the basis, plan and list bookkeeping and only launches.
     unsigned long long gen = 1;
     int launch_cache = 1;
+    int skip_idle = std::getenv("VR_EXP_SKIP_IDLE") ? std::atoi(std::getenv("VR_EXP_SKIP_IDLE")) : 0;   // timing only
     struct Cached {
         bool valid = false;
         unsigned long long gen = 0;
@@ -1359,6 +1361,8 @@ static void poll_region_header(Ctx* c)
     Ctx::RegionBuf& rb = c->region[c->rg_buf];
     rb.nwork = c->h_rghdr[9];
     rb.most = c->h_rghdr[10];
+    rb.most_work = 0;
+    for (int x = 0; x < 8; ++x) rb.most_work = std::max(rb.most_work, c->h_rghdr[kRegionWork + x]);
 }
 
 // Pick the buffer for new lists, sized for n entries: the one the current
@@ -1484,6 +1488,7 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
         rb.upload_stream = stream;
         rb.nwork = nwork;
         rb.most = most;
+        rb.most_work = 0;   // known once the build completes (poll_region_header)
         rb.map = TileMap{};
         rb.map.nwx = std::max(1, (most + tpw - 1) / tpw);
         rb.seg_len = 0;
@@ -1616,6 +1621,7 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     std::memset(hdr, 0, kRegionHeader * sizeof(int));
     unsigned* info = rb.h + kRegionHeader;
     unsigned* list = info + 2 * (size_t)nslots;
+    int most_work = 0;
     TileMap m{};
     size_t pos = 0, most = 0;
     int slot = 0;
@@ -1640,6 +1646,12 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     hdr[9] = (int)work.size();
     hdr[10] = (int)most;
     hdr[11] = (int)pos;
+    for (int x = 0; x < 8; ++x) {   // work tiles lead each XCD's list (after its segments)
+        int nw = 0;
+        for (const T& t : xl[x]) nw += t.cost >= 1.0;
+        hdr[kRegionWork + x] = nw;
+        most_work = std::max(most_work, nw);
+    }
     hdr[kRegionSegTiles] = nslots;
     HIP_TRY(hipMemcpyAsync(rb.d, rb.h, (n + kRegionHeader) * sizeof(unsigned), hipMemcpyHostToDevice, stream));
     if (!rb.uploaded) HIP_TRY(hipEventCreateWithFlags(&rb.uploaded, hipEventDisableTiming));
@@ -1647,6 +1659,7 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     rb.upload_stream = stream;
     rb.map = m;
     rb.most = (int)most;
+    rb.most_work = most_work;
     rb.nwork = (int)work.size();
     rb.seg_len = L;
     rb.nseg_tiles = nslots;
@@ -1993,6 +2006,7 @@ try {
     a.pitch = (long long)pitch;
     a.format = tfmt;
     a.bands_in_place = in_place && t->band_rows > 0 ? 1 : 0;
+    a.skip_idle = c->skip_idle;
     a.step_counter = reinterpret_cast<unsigned long long*>(t->step_counter);
     HIP_TRY(hipSetDevice(c->device));
     if (c->proc.enabled) {
@@ -2105,6 +2119,7 @@ try {
         sc.tiles = rb.d + kRegionHeader + 2 * (size_t)rb.icap;
         sc.hdr = reinterpret_cast<const int*>(rb.d);
         sc.map = rb.map;
+        if (a.skip_idle && rb.most_work > 0) sc.map.nwx = std::max(1, (rb.most_work + tpw - 1) / tpw);
         if (rb.seg_len > 0) {
             // segmented lists (one lane per ray): the terms scratch must hold
             // every segmented tile's rays at this frame's max_steps
@@ -2143,7 +2158,7 @@ try {
             if (K == 0) K = auto_split(c, rb.nwork);
             if (K > 1) {
                 const int ktpw = tpw;
-                const int most = rb.most;
+                const int most = a.skip_idle && rb.most_work > 0 ? rb.most_work : rb.most;
                 sc.split = K;
                 sc.map.nwx = std::max(1, (most * K + ktpw - 1) / ktpw);
             }

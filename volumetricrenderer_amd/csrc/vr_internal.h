@@ -208,6 +208,8 @@ struct MarchArgs {
     void* out;
     long long pitch;
     int format;
+    int skip_idle;               // timing experiment (VR_EXP_SKIP_IDLE): regions launches march only the
+                                 // tiles with estimated work (the others are not written)
     int bands_in_place;          // vr.h VR_TARGET_BANDS_IN_PLACE: packed row orow is stored at its frame row
     unsigned long long* step_counter;
     ProcParams proc;
@@ -231,9 +233,11 @@ struct TileMap {
 //   [0..8]   off[]: XCD x renders the entries [off[x], off[x+1])
 //   [9]      tiles with estimated work    [10] the longest list
 //   [11]     entries                       [12] segmented tiles (kRegionSegTiles)
+//   [16..23] tiles with estimated work of XCD x (kRegionWork; they lead its list)
 // Built on the host (vr_api.cpp build_regions) or, for a moving camera, on
 // the GPU (vr_regions.hip launch_region_build, the same dealing; no segments).
-constexpr int kRegionHeader = 16;
+constexpr int kRegionHeader = 24;
+constexpr int kRegionWork = 16;
 constexpr int kRegionSegTiles = 12;
 // Ray segments (vr_march_kernels.h march_regions_seg / seg_resolve)
 struct SegArgs {

@@ -1124,7 +1124,7 @@ __device__ __forceinline__ void regions_body(const MarchArgs& a, const unsigned*
 {
     const int xcd = blockIdx.x & 7;
     const int w = (int)(blockIdx.x >> 3) * WGW + (threadIdx.x >> 6);
-    const int begin = hdr[xcd], count = hdr[xcd + 1] - begin;
+    const int begin = hdr[xcd], count = a.skip_idle ? hdr[kRegionWork + xcd] : hdr[xcd + 1] - begin;
     if ((int)(blockIdx.x >> 3) * WGW >= count) return;   // whole workgroup, before the barrier
 #ifdef VR_TIMELINE
     const unsigned long long t_begin = __builtin_amdgcn_s_memrealtime();
@@ -1409,7 +1409,7 @@ __global__ __launch_bounds__(kThreads) void march_regions_split(const MarchArgs 
     extern __shared__ __attribute__((aligned(16))) unsigned lds[];
     const int xcd = blockIdx.x & 7;
     const int w = (int)(blockIdx.x >> 3) * (kThreads / 64) + (threadIdx.x >> 6);
-    const int begin = hdr[xcd], units = (hdr[xcd + 1] - begin) * K;
+    const int begin = hdr[xcd], units = (a.skip_idle ? hdr[kRegionWork + xcd] : hdr[xcd + 1] - begin) * K;
     if ((int)(blockIdx.x >> 3) * (kThreads / 64) >= units) return;   // whole workgroup, before the barrier
     const FastCtx f = fast_prologue<LAYOUT>(a, lds);
 #ifdef VR_TIMELINE

@@ -46,7 +46,7 @@ struct RgScratch {
     unsigned* vals_in;
     unsigned long long* bin_cost;   // [kAngleBins], zeroed by rg_wedges after use
     unsigned char* bin_xcd;         // [kAngleBins]
-    unsigned* counts;               // [8] per XCD, [8] tiles with work; zeroed by rg_header after use
+    unsigned* counts;               // [8] per XCD, [8] tiles with work, [16..23] work per XCD; zeroed by rg_header
     void* sort_tmp;
     size_t sort_bytes;
 };
@@ -151,6 +151,7 @@ __global__ __launch_bounds__(256) void rg_keys(const RegionBuild b, RgScratch s)
     }
     s.keys_in[i] = xcd << 28 | k;
     atomicAdd(&s.counts[xcd], 1u);
+    if (!idle) atomicAdd(&s.counts[kRegionWork + xcd], 1u);   // work tiles lead each list
 }
 
 // 5. header: off[0..8], tiles with work, longest list; counters zeroed
@@ -170,6 +171,10 @@ __global__ __launch_bounds__(64) void rg_header(RgScratch s, int* hdr, int* hdr_
     hdr[10] = most;
     hdr[11] = n;
     s.counts[8] = 0u;
+    for (int x = 0; x < 8; ++x) {
+        hdr[kRegionWork + x] = (int)s.counts[kRegionWork + x];
+        s.counts[kRegionWork + x] = 0u;
+    }
     if (hdr_host)
         for (int j = 0; j < kRegionHeader; ++j) hdr_host[j] = hdr[j];
 }
@@ -236,7 +241,7 @@ hipError_t launch_region_build(const RegionBuild& b, void* scratch, unsigned* d_
     RgScratch s = carve(scratch, n, sb);
     const dim3 grid((unsigned)((n + 255) / 256));
     {   // the per-block maxima, per-bin sums and counters start at zero
-        const size_t zb = static_cast<size_t>(reinterpret_cast<char*>(s.counts + 16) - static_cast<char*>(scratch));
+        const size_t zb = static_cast<size_t>(reinterpret_cast<char*>(s.counts + kRegionWork + 8) - static_cast<char*>(scratch));
         const hipError_t z = hipMemsetAsync(scratch, 0, zb, st);
         if (z != hipSuccess) return z;
     }
