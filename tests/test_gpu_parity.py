@@ -1395,6 +1395,65 @@ def test_region_order_bitexact(r, oracle, vol128, layout, order):
         r.set_layout_preference(0)
 
 
+@pytest.mark.parametrize("fmt", [0, 1, 3])   # RGBA32F, RGBA8_UNORM, R8_UNORM
+def test_empty_tiles_filled_not_marched(r, oracle, vol128, fmt):
+    """Option empty_fill (default 1): the regions lists put the tiles no ray
+    of which can meet the box (vr_internal.h tile_is_empty: the box in front of
+    the eye and outside one side plane of the tile's pixel-edge frustum) last,
+    and the march writes them with the uncovered value instead of marching
+    them.  Every pixel must come out as the full march writes it: the same
+    bytes with the option on and off (targets pre-filled with a sentinel, so a
+    pixel either run skips shows), across rotated models, bands (8- and 16-row;
+    12-row bands are never classified), and GPU-built lists; and the oracle
+    for two of them."""
+    r.set_volume(vol128)
+    r.set_march(vr.march_defaults())
+    views = [(0.0, 0.0), (20.0, -15.0), (45.0, 30.0), (90.0, 0.0), (200.0, 60.0), (300.0, -80.0)]
+    cases = [(640, 360, {}), (1920, 1080, dict(band_rows=16, band_stride=8, band_first=3)),
+             (333, 197, dict(band_rows=8, band_stride=3, band_first=1)),
+             (500, 300, dict(band_rows=12, band_stride=2, band_first=0))]
+    seen_empty = 0
+    r.set_option("region_interval", 1)   # lists for every camera (stale lists are marched whole)
+    try:
+        for phi, theta in views:
+            for W, H, band in cases:
+                osd, gsd = vr.reference_shader_data(W / H, phi, theta)
+                r.set_shader_data(osd, gsd)
+                outs = []
+                for fill in (1, 0):
+                    r.set_option("empty_fill", fill)
+                    out = r.alloc_target(W, H, fmt, **band)
+                    out.view(torch.uint8).fill_(0x5A)
+                    r.render(W, H, fmt, out=out, **band)
+                    torch.cuda.synchronize()
+                    if fill:
+                        e = r.get_option("region_empty_tiles")
+                        seen_empty += max(e, 0)
+                        if band.get("band_rows", 0) == 12:
+                            assert e == 0
+                    outs.append(out.cpu().numpy())
+                assert_exact(outs[0], outs[1])
+        assert seen_empty > 0
+        r.set_option("empty_fill", 1)
+        for phi, theta in [(0.0, 0.0), (45.0, 30.0)]:
+            osd, gsd = vr.reference_shader_data(16 / 9, phi, theta)
+            img, ref, c, st = render_both(r, oracle, vol128, 640, 360, osd, gsd, fmt=fmt)
+            assert_exact(img, ref)
+            assert c == st
+        for i in range(1, 4):   # GPU-built lists every render
+            osd, gsd = vr.reference_shader_data(16 / 9, 20.0 + 7 * SPIN_DEG * i, -15.0)
+            img, ref, c, st = render_both(r, oracle, vol128, 640, 360, osd, gsd, fmt=fmt)
+            assert_exact(img, ref)
+            assert c == st
+        torch.cuda.synchronize()
+        img, ref, c, st = render_both(r, oracle, vol128, 640, 360, osd, gsd, fmt=fmt)   # sized from the build
+        assert_exact(img, ref)
+        assert r.get_option("region_empty_tiles") > 0
+    finally:
+        r.set_option("region_interval", 32)
+        r.set_option("empty_fill", 1)
+
+
 # ---- BASELINE config 4: 3840x2160, 256 steps, 128^3 recipe volume ----
 
 @pytest.fixture(scope="module")

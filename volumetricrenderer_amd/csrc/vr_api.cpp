@@ -86,7 +86,7 @@ constexpr int kMaxDeferMiB = 4 << 10;
 constexpr size_t kMaxTermsBytes = (size_t)1 << 30;   // ray segments: the terms scratch (slots x max_steps x 64 floats)
 // retired deferred scratch buffers kept before a device sync frees them
 constexpr size_t kMaxDeferRetired = 4;
-constexpr int kRegionKeyLen = 35;
+constexpr int kRegionKeyLen = 39;
 // auto split (lanes per ray) from the frame share's tiles with work: K = 1 at
 // >= 6000, 2 at >= 1400, else 4.  Measured on 1/N of the 1080p frame at 512^3
 // (~7,500 tiles with work): K = 1, 2, 2, 4 at N = 1, 2, 4, 8.
@@ -201,8 +201,9 @@ struct Ctx {
         size_t cap = 0;            // entries
         TileMap map{};             // host copy: nwx (and off[] for host builds)
         int most = 0;              // the longest per-XCD list (sizes the launch)
-        int most_work = 0;         // the most tiles with work of one XCD
+        int most_marched = 0;         // the most marched entries of one XCD (hdr[kRegionWork + x])
         int nwork = 0;             // tiles with estimated work
+        int nempty = -1;           // empty tiles (tile_is_empty) in the lists (-1: GPU build not yet complete)
         int seg_len = 0;           // segments: steps per segment the lists were built for (0 = none)
         int nseg_tiles = 0;        // segmented tiles (slots of SegArgs.info)
         int icap = 0;              // info entries before the list
@@ -226,6 +227,7 @@ struct Ctx {
     int region_cur = -1;           // buffer of the current lists (-1 = none)
     int region_slot = -1;          // the last render stream's slot in them (note_region_stream)
     float region_key[kRegionKeyLen] = {};   // geometry the current lists were built for
+    bool region_exact = false;   // the current lists were built for this render's camera (their empty tiles hold)
     long long renders_since_build = 0;
     // procedural cost sort: the geometry whose order d_sort holds (n per pixel
     // depends only on it, not on the medium), valid until the buffer changes
@@ -247,7 +249,7 @@ struct Ctx {
     // loop) then skips the basis, plan and list bookkeeping and only launches.
     unsigned long long gen = 1;
     int launch_cache = 1;
-    int skip_idle = std::getenv("VR_EXP_SKIP_IDLE") ? std::atoi(std::getenv("VR_EXP_SKIP_IDLE")) : 0;   // timing only
+    int empty_fill = 1;          // option "empty_fill": regions launches fill the lists' empty tiles, not march them
     struct Cached {
         bool valid = false;
         unsigned long long gen = 0;
@@ -478,6 +480,8 @@ const char* variant_name(const Plan& p)
 }
 
 }  // namespace
+
+static void poll_region_header(Ctx* c);
 
 extern "C" {
 
@@ -983,6 +987,12 @@ try {
         c->launch_cache = value;
         return VR_OK;
     }
+    if (n == "empty_fill") {   // regions: fill the lists' empty tiles instead of marching them
+        if (value < 0 || value > 1) return fail(VR_ERR_INVALID, "vr_set_option: empty_fill is 0 or 1");
+        c->empty_fill = value;
+        ++c->gen;
+        return VR_OK;
+    }
     if (n == "inject_throw") {   // test hook: the next vr_render throws in its host path
         if (value < 0 || value > 2)
             return fail(VR_ERR_INVALID, "vr_set_option: inject_throw is 0, 1 (std::runtime_error) or 2 (std::bad_alloc)");
@@ -1158,6 +1168,10 @@ try {
     if (n == "uniform_skip") return c->uniform_skip;
     if (n == "region_work_tiles")   // read-only: tiles with estimated work in the current region lists
         return c->region_cur >= 0 ? c->region[c->region_cur].nwork : -1;
+    if (n == "region_empty_tiles") {   // read-only: tiles of the current lists that are filled, not marched
+        poll_region_header(c);   // (a completed GPU build's counts)
+        return c->region_cur >= 0 ? c->region[c->region_cur].nempty : -1;
+    }
     if (n == "uniform_mask") {   // read-only
         if (!c->d_planar || resolve_uniform(c) != VR_OK) return -1;
         return c->uniform_mask;
@@ -1165,6 +1179,7 @@ try {
     if (n == "supertile") return c->supertile;
     if (n == "lat") return c->lat;
     if (n == "launch_cache") return c->launch_cache;
+    if (n == "empty_fill") return c->empty_fill;
     if (n == "launch_cache_hits") return (int)std::min<long long>(c->lc_hits, 0x7fffffff);
     if (n == "experiments") return VR_EXPERIMENTS;   // read-only: the measured-slower variants are built
     if (n == "region_interval") return c->region_interval;
@@ -1361,8 +1376,12 @@ static void poll_region_header(Ctx* c)
     Ctx::RegionBuf& rb = c->region[c->rg_buf];
     rb.nwork = c->h_rghdr[9];
     rb.most = c->h_rghdr[10];
-    rb.most_work = 0;
-    for (int x = 0; x < 8; ++x) rb.most_work = std::max(rb.most_work, c->h_rghdr[kRegionWork + x]);
+    rb.most_marched = 0;
+    rb.nempty = 0;
+    for (int x = 0; x < 8; ++x) {
+        rb.most_marched = std::max(rb.most_marched, c->h_rghdr[kRegionWork + x]);
+        rb.nempty += c->h_rghdr[x + 1] - c->h_rghdr[x] - c->h_rghdr[kRegionWork + x];
+    }
 }
 
 // Pick the buffer for new lists, sized for n entries: the one the current
@@ -1424,11 +1443,18 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     for (float v : {(float)a.max_steps, a.step_size, (float)cpx, (float)cprow}) key[kn++] = v;
     for (const float* v : {a.org, a.o, a.px, a.py, a.box_min, a.box_max})
         for (int k = 0; k < 3; ++k) key[kn++] = v[k];
+    for (int k = 0; k < 4; ++k) key[kn++] = a.r3[k];   // the clip w row (tile_is_empty)
     ++c->renders_since_build;
     poll_region_header(c);
     const bool same_grid = c->region_cur >= 0 && std::memcmp(key, c->region_key, grid_part * sizeof(float)) == 0;
-    if (same_grid && (std::memcmp(key, c->region_key, sizeof key) == 0 || c->renders_since_build < c->region_interval))
+    const bool exact = same_grid && std::memcmp(key, c->region_key, sizeof key) == 0;
+    if (exact || (same_grid && c->renders_since_build < c->region_interval)) {
+        // lists of an older camera order the work of this one correctly, but
+        // their empty tiles are that camera's: they are then marched too
+        c->region_exact = exact;
         return note_region_stream(c->region[c->region_cur], stream, &c->region_slot);
+    }
+    c->region_exact = true;   // (either build below is for this key)
 
     const int S = c->supertile;
     // a moved camera over the same target (no segments): the lists come from
@@ -1468,6 +1494,8 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
             g.org[k] = a.org[k]; g.o[k] = a.o[k]; g.px[k] = a.px[k]; g.py[k] = a.py[k];
             g.box_min[k] = a.box_min[k]; g.box_max[k] = a.box_max[k];
         }
+        for (int k = 0; k < 4; ++k) g.r3[k] = a.r3[k];
+        g.height = a.height;
         g.ccx = (cpx + 0.5) / 8.0; g.ccy = (cprow + 0.5) / 8.0;
         g.ctx = (cpx >> 3) / S; g.cty = (cprow >> 3) / S;
         g.supertile = S; g.wedges = c->wedges; g.order = c->region_order;
@@ -1488,7 +1516,8 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
         rb.upload_stream = stream;
         rb.nwork = nwork;
         rb.most = most;
-        rb.most_work = 0;   // known once the build completes (poll_region_header)
+        rb.most_marched = 0;   // known once the build completes (poll_region_header)
+        rb.nempty = -1;
         rb.map = TileMap{};
         rb.map.nwx = std::max(1, (most + tpw - 1) / tpw);
         rb.seg_len = 0;
@@ -1585,7 +1614,21 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
         for (auto& l : xl) std::sort(l.begin(), l.end(), inside_out);
     }
     std::sort(idle.begin(), idle.end(), inside_out);
-    for (size_t i = 0; i < idle.size(); ++i) xl[i % 8].push_back(idle[i]);
+    // idle tiles some ray of which may meet the box, dealt round-robin after
+    // the work, then the empty ones (tile_is_empty: filled, not marched),
+    // likewise -- the GPU build's order
+    std::vector<T> empty_tiles;
+    {
+        std::vector<T> edge;
+        for (const T& t : idle)
+            (tile_is_empty(a.org, a.o, a.px, a.py, a.box_min, a.box_max, a.r3, a.width, a.out_rows, a.height,
+                           a.band_rows, a.band_stride, a.band_first, (int)(t.id & 0xffffu), (int)(t.id >> 16))
+                 ? empty_tiles : edge).push_back(t);
+        for (size_t i = 0; i < edge.size(); ++i) xl[i % 8].push_back(edge[i]);
+    }
+    std::vector<int> marched(8);
+    for (int x = 0; x < 8; ++x) marched[x] = (int)xl[x].size();
+    for (size_t i = 0; i < empty_tiles.size(); ++i) xl[i % 8].push_back(empty_tiles[i]);
 
     // segments (option "segment", L steps): a tile with work estimated at
     // >= 2L steps is marched as round(cost / L) segments (at most 127; as many
@@ -1621,7 +1664,7 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     std::memset(hdr, 0, kRegionHeader * sizeof(int));
     unsigned* info = rb.h + kRegionHeader;
     unsigned* list = info + 2 * (size_t)nslots;
-    int most_work = 0;
+    int most_marched = 0;
     TileMap m{};
     size_t pos = 0, most = 0;
     int slot = 0;
@@ -1646,11 +1689,10 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     hdr[9] = (int)work.size();
     hdr[10] = (int)most;
     hdr[11] = (int)pos;
-    for (int x = 0; x < 8; ++x) {   // work tiles lead each XCD's list (after its segments)
-        int nw = 0;
-        for (const T& t : xl[x]) nw += t.cost >= 1.0;
-        hdr[kRegionWork + x] = nw;
-        most_work = std::max(most_work, nw);
+    for (int x = 0; x < 8; ++x) {   // the marched entries lead each XCD's list (with segments: all of them)
+        const int nm = L > 0 ? m.off[x + 1] - m.off[x] : marched[x];
+        hdr[kRegionWork + x] = nm;
+        most_marched = std::max(most_marched, nm);
     }
     hdr[kRegionSegTiles] = nslots;
     HIP_TRY(hipMemcpyAsync(rb.d, rb.h, (n + kRegionHeader) * sizeof(unsigned), hipMemcpyHostToDevice, stream));
@@ -1659,7 +1701,8 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     rb.upload_stream = stream;
     rb.map = m;
     rb.most = (int)most;
-    rb.most_work = most_work;
+    rb.most_marched = most_marched;
+    rb.nempty = L > 0 ? 0 : (int)empty_tiles.size();
     rb.nwork = (int)work.size();
     rb.seg_len = L;
     rb.nseg_tiles = nslots;
@@ -2006,7 +2049,7 @@ try {
     a.pitch = (long long)pitch;
     a.format = tfmt;
     a.bands_in_place = in_place && t->band_rows > 0 ? 1 : 0;
-    a.skip_idle = c->skip_idle;
+    a.empty_fill = 0;   // set with the schedule (regions, default kernels)
     a.step_counter = reinterpret_cast<unsigned long long*>(t->step_counter);
     HIP_TRY(hipSetDevice(c->device));
     if (c->proc.enabled) {
@@ -2119,7 +2162,11 @@ try {
         sc.tiles = rb.d + kRegionHeader + 2 * (size_t)rb.icap;
         sc.hdr = reinterpret_cast<const int*>(rb.d);
         sc.map = rb.map;
-        if (a.skip_idle && rb.most_work > 0) sc.map.nwx = std::max(1, (rb.most_work + tpw - 1) / tpw);
+        // the default kernels march the lists' first hdr[kRegionWork + x] entries
+        // and fill the rest (tile_is_empty); the experiments' kernels march all
+        const bool fill = c->empty_fill && c->region_exact && !sc.slab && rb.seg_len == 0 && !lat_on(c, pl.layout);
+        a.empty_fill = fill ? 1 : 0;
+        if (fill && rb.most_marched > 0) sc.map.nwx = std::max(1, (rb.most_marched + tpw - 1) / tpw);
         if (rb.seg_len > 0) {
             // segmented lists (one lane per ray): the terms scratch must hold
             // every segmented tile's rays at this frame's max_steps
@@ -2158,7 +2205,7 @@ try {
             if (K == 0) K = auto_split(c, rb.nwork);
             if (K > 1) {
                 const int ktpw = tpw;
-                const int most = a.skip_idle && rb.most_work > 0 ? rb.most_work : rb.most;
+                const int most = a.empty_fill && rb.most_marched > 0 ? rb.most_marched : rb.most;
                 sc.split = K;
                 sc.map.nwx = std::max(1, (most * K + ktpw - 1) / ktpw);
             }

@@ -208,8 +208,8 @@ struct MarchArgs {
     void* out;
     long long pitch;
     int format;
-    int skip_idle;               // timing experiment (VR_EXP_SKIP_IDLE): regions launches march only the
-                                 // tiles with estimated work (the others are not written)
+    int empty_fill;              // regions lists: march each XCD's first hdr[kRegionWork + x] entries, fill the
+                                 // rest (tiles no ray of which meets the box) with the uncovered value
     int bands_in_place;          // vr.h VR_TARGET_BANDS_IN_PLACE: packed row orow is stored at its frame row
     unsigned long long* step_counter;
     ProcParams proc;
@@ -233,7 +233,10 @@ struct TileMap {
 //   [0..8]   off[]: XCD x renders the entries [off[x], off[x+1])
 //   [9]      tiles with estimated work    [10] the longest list
 //   [11]     entries                       [12] segmented tiles (kRegionSegTiles)
-//   [16..23] tiles with estimated work of XCD x (kRegionWork; they lead its list)
+//   [16..23] marched tiles of XCD x (kRegionWork): its list holds the tiles
+//            with estimated work, then the other tiles some ray of which may
+//            meet the box, then the empty ones (tile_is_empty) -- those last
+//            are written with the uncovered value, not marched
 // Built on the host (vr_api.cpp build_regions) or, for a moving camera, on
 // the GPU (vr_regions.hip launch_region_build, the same dealing; no segments).
 constexpr int kRegionHeader = 24;
@@ -247,13 +250,73 @@ struct SegArgs {
 };
 struct RegionBuild {
     int tw, th, width, out_rows, band_rows, band_stride, band_first, max_steps;
+    int height;
     float step_size;
     float org[3], o[3], px[3], py[3], box_min[3], box_max[3];
+    float r3[4];           // row 3 of P*V*M (clip w), for tile_is_empty
     double ccx, ccy;       // box-centre tile (fractional), S x S block of it
     int ctx, cty;
     int supertile, wedges;
     int order;             // option region_order: 0 inside-out, 1 longest tile first, 2 longest S x S block first
 };
+// True when no ray of tile (tx, ty) of the target can be covered (setup_ray,
+// vr_march_kernels.h), so the march would write the uncovered value at every
+// pixel of it.  Conservative, in double: the box lies wholly in front of the
+// camera (clip w > 0 at its 8 corners: no line through the eye meets it
+// behind), and one side plane of the tile's frustum -- through the eye and
+// two corner rays of the tile's pixel-edge rectangle, half a pixel outside
+// every pixel centre -- has all 8 box corners strictly outside.  The pixel
+// centre rays then pass half a pixel or more from any point of the box; the
+// fp32 ray setup cannot close that.  Tiles whose rows span two bands (band
+// rows not a multiple of 8) are never empty.  Host and GPU list builds.
+__host__ __device__ inline bool tile_is_empty(const float org[3], const float o[3], const float px[3], const float py[3],
+                                              const float bmin[3], const float bmax[3], const float r3[4], int width,
+                                              int out_rows, int height, int band_rows, int band_stride, int band_first,
+                                              int tx, int ty)
+{
+    if (band_rows > 0 && band_rows % 8 != 0) return false;
+    const int x0 = tx * 8, x1 = x0 + 8 < width ? x0 + 8 : width;
+    const int r0 = ty * 8, rows = r0 + 8 < out_rows ? 8 : out_rows - r0;
+    if (x1 <= x0 || rows <= 0) return true;   // no pixels
+    int y0 = r0;
+    if (band_rows > 0) {
+        const int bl = r0 / band_rows;
+        y0 = (band_first + bl * band_stride) * band_rows + (r0 - bl * band_rows);
+    }
+    if (y0 >= height) return true;   // rows past the frame: never stored
+    double c[8][3];
+    for (int k = 0; k < 8; ++k) {
+        c[k][0] = (double)((k & 1) ? bmax[0] : bmin[0]) - (double)org[0];
+        c[k][1] = (double)((k & 2) ? bmax[1] : bmin[1]) - (double)org[1];
+        c[k][2] = (double)((k & 4) ? bmax[2] : bmin[2]) - (double)org[2];
+        const double w = (double)r3[0] * (c[k][0] + (double)org[0]) + (double)r3[1] * (c[k][1] + (double)org[1]) +
+                         (double)r3[2] * (c[k][2] + (double)org[2]) + (double)r3[3];
+        if (!(w > 1e-6)) return false;   // some of the box at or behind the eye
+    }
+    const double fxs[4] = {(double)x0, (double)x1, (double)x1, (double)x0};
+    const double fys[4] = {(double)y0, (double)y0, (double)(y0 + rows), (double)(y0 + rows)};
+    double d[4][3], m[3];
+    for (int j = 0; j < 3; ++j)
+        m[j] = (double)o[j] + 0.5 * (x0 + x1) * (double)px[j] + (y0 + 0.5 * rows) * (double)py[j];
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 3; ++j) d[i][j] = (double)o[j] + fxs[i] * (double)px[j] + fys[i] * (double)py[j];
+    for (int i = 0; i < 4; ++i) {
+        const double* a = d[i];
+        const double* b = d[(i + 1) & 3];
+        double n[3] = {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
+        const double sm = n[0] * m[0] + n[1] * m[1] + n[2] * m[2];
+        if (sm == 0.0) continue;
+        if (sm > 0.0) { n[0] = -n[0]; n[1] = -n[1]; n[2] = -n[2]; }   // outward: away from the tile's centre ray
+        const double nn = sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+        bool out = true;
+        for (int k = 0; k < 8 && out; ++k) {
+            const double cl = sqrt(c[k][0] * c[k][0] + c[k][1] * c[k][1] + c[k][2] * c[k][2]);
+            out = n[0] * c[k][0] + n[1] * c[k][1] + n[2] * c[k][2] > 1e-9 * nn * cl;
+        }
+        if (out) return true;
+    }
+    return false;
+}
 size_t region_build_bytes(int ntiles);
 hipError_t region_build_preload();   // load the build's code object (first host build, once)
 // h_hdr (optional, host-mapped): a copy of the header, for sizing later launches

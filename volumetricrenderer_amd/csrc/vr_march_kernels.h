@@ -1118,13 +1118,35 @@ __global__ __launch_bounds__(kThreads) void march_rings(const MarchArgs a, int c
 // (DESIGN.md sec. 5.3).  XCD = blockIdx % 8 is a speed-only assumption.
 // WGW waves per workgroup (option wg_waves): the waves of one workgroup run on
 // one CU and share its L1, and they render consecutive list entries.
+// The regions lists' empty tiles (MarchArgs.empty_fill; vr_internal.h
+// tile_is_empty): XCD x's entries [marched, count) after the marched ones.
+// Wave w of the XCD writes the uncovered value -- what the march stores for a
+// ray that misses (setup_ray, store_pixel) -- to the pixels of entries
+// marched + w, marched + w + nwx, ...: one store per lane, no ray setup.
+__device__ __forceinline__ void fill_empty_tiles(const MarchArgs& a, const unsigned* __restrict__ tiles, int begin,
+                                                 int marched, int count, int w, int nwx)
+{
+    const int lane = threadIdx.x & 63, lx = lane & 7, ly = lane >> 3;
+    for (int k = marched + w; w < nwx && k < count; k += nwx) {
+        const unsigned t = tiles[begin + k];
+        const int x = (int)(t & 0xffffu) * 8 + lx, orow = (int)(t >> 16) * 8 + ly;
+        if (x < a.width && orow < a.out_rows) {
+            const int bl = orow / a.band_rows;
+            const int y = (a.band_first + bl * a.band_stride) * a.band_rows + (orow - bl * a.band_rows);
+            if (y < a.height) store_pixel(a, x, orow, false, 0.0f);
+        }
+    }
+}
+
 template <int LAYOUT, int WRAP, bool EARLY, bool ZO, int WGW, int UM>
 __device__ __forceinline__ void regions_body(const MarchArgs& a, const unsigned* __restrict__ tiles, const int* __restrict__ hdr, int nwx,
                                              unsigned* lds)
 {
     const int xcd = blockIdx.x & 7;
     const int w = (int)(blockIdx.x >> 3) * WGW + (threadIdx.x >> 6);
-    const int begin = hdr[xcd], count = a.skip_idle ? hdr[kRegionWork + xcd] : hdr[xcd + 1] - begin;
+    const int begin = hdr[xcd], all = hdr[xcd + 1] - begin;
+    const int count = a.empty_fill ? min(hdr[kRegionWork + xcd], all) : all;   // marched entries
+    if (a.empty_fill) fill_empty_tiles(a, tiles, begin, count, all, w, nwx);
     if ((int)(blockIdx.x >> 3) * WGW >= count) return;   // whole workgroup, before the barrier
 #ifdef VR_TIMELINE
     const unsigned long long t_begin = __builtin_amdgcn_s_memrealtime();
@@ -1409,7 +1431,10 @@ __global__ __launch_bounds__(kThreads) void march_regions_split(const MarchArgs 
     extern __shared__ __attribute__((aligned(16))) unsigned lds[];
     const int xcd = blockIdx.x & 7;
     const int w = (int)(blockIdx.x >> 3) * (kThreads / 64) + (threadIdx.x >> 6);
-    const int begin = hdr[xcd], units = (a.skip_idle ? hdr[kRegionWork + xcd] : hdr[xcd + 1] - begin) * K;
+    const int begin = hdr[xcd], all = hdr[xcd + 1] - begin;
+    const int marched = a.empty_fill ? min(hdr[kRegionWork + xcd], all) : all;
+    if (a.empty_fill) fill_empty_tiles(a, tiles, begin, marched, all, w, nwx);
+    const int units = marched * K;
     if ((int)(blockIdx.x >> 3) * (kThreads / 64) >= units) return;   // whole workgroup, before the barrier
     const FastCtx f = fast_prologue<LAYOUT>(a, lds);
 #ifdef VR_TIMELINE

@@ -16,9 +16,10 @@
 //   2. rg_wedges: one workgroup scans the bins' work and cuts it into
 //      8 x wedges equal quantiles; wedge k goes to XCD k % 8 (as the host
 //      cuts tiles sorted by angle);
-//   3. rg_keys: the sort key of a tile -- XCD, idle flag (tiles without
-//      estimated work go after the XCD's work, dealt round-robin), ring, angle
-//      bin, place in block -- and the per-XCD counts;
+//   3. rg_keys: the sort key of a tile -- XCD, empty flag (tile_is_empty:
+//      filled, not marched, last), idle flag (tiles without estimated work go
+//      after the XCD's work, dealt round-robin), ring, angle bin, place in
+//      block -- and the per-XCD counts (all, and marched);
 //   4. hipcub::DeviceRadixSort::SortPairs: keys -> the concatenated lists;
 //   5. rg_header: the per-XCD offsets, tiles with work and the longest list,
 //      into the list buffer's header (and host-mapped memory, which the host
@@ -88,6 +89,9 @@ __global__ __launch_bounds__(256) void rg_tiles(const RegionBuild b, RgScratch s
     const int ring = min(max(abs(sx - b.ctx), abs(sy - b.cty)), 2047);
     const int sub = (ty % S) * S + tx % S;
     const bool work = cost >= 1.0;
+    // tiles no ray of which meets the box go last (filled, not marched)
+    const bool empty = !work && tile_is_empty(b.org, b.o, b.px, b.py, b.box_min, b.box_max, b.r3, b.width, b.out_rows,
+                                              b.height, b.band_rows, b.band_stride, b.band_first, tx, ty);
     if (work) {
         atomicAdd(&s.bin_cost[abin], (unsigned long long)(cost * kCostScale));
         atomicAdd(&s.counts[8], 1u);
@@ -96,7 +100,8 @@ __global__ __launch_bounds__(256) void rg_tiles(const RegionBuild b, RgScratch s
             atomicMax(&s.bmax[b.order == 2 ? sy * bw + sx : i], (unsigned)fmin(cost * 16.0, 4294967295.0));
         }
     }
-    s.keys_in[i] = (work ? 0u : 1u) << 27 | (unsigned)ring << 16 | (unsigned)abin << 4 | (unsigned)sub;
+    s.keys_in[i] = (empty ? 1u : 0u) << 28 | (work ? 0u : 1u) << 27 | (unsigned)ring << 16 | (unsigned)abin << 4 |
+                   (unsigned)sub;
     s.vals_in[i] = ((unsigned)ty << 16) | (unsigned)tx;
 }
 
@@ -140,7 +145,7 @@ __global__ __launch_bounds__(256) void rg_keys(const RegionBuild b, RgScratch s)
     const int i = (int)(blockIdx.x * 256 + threadIdx.x);
     if (i >= b.tw * b.th) return;
     unsigned k = s.keys_in[i];
-    const bool idle = (k >> 27) & 1u;
+    const bool idle = (k >> 27) & 1u;   // (bit 28: empty, which implies idle)
     const unsigned xcd = idle ? (unsigned)(i % 8) : (unsigned)s.bin_xcd[(k >> 4) & (kAngleBins - 1)];
     if (b.order != 0 && !idle) {
         const int S = b.supertile, ty = i / b.tw, tx = i - ty * b.tw;
@@ -149,9 +154,9 @@ __global__ __launch_bounds__(256) void rg_keys(const RegionBuild b, RgScratch s)
         const unsigned q = (unsigned)fmin(1023.0, c * 1023.0 / (double)max(b.max_steps, 1));
         k = (1023u - q) << 17 | ((unsigned)blk & 0x1fffu) << 4 | (k & 0xfu);
     }
-    s.keys_in[i] = xcd << 28 | k;
+    s.keys_in[i] = xcd << 29 | k;
     atomicAdd(&s.counts[xcd], 1u);
-    if (!idle) atomicAdd(&s.counts[kRegionWork + xcd], 1u);   // work tiles lead each list
+    if (!((k >> 28) & 1u)) atomicAdd(&s.counts[kRegionWork + xcd], 1u);   // marched: work, then other non-empty
 }
 
 // 5. header: off[0..8], tiles with work, longest list; counters zeroed
@@ -251,7 +256,7 @@ hipError_t launch_region_build(const RegionBuild& b, void* scratch, unsigned* d_
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     size_t bytes = s.sort_bytes;
-    e = hipcub::DeviceRadixSort::SortPairs(s.sort_tmp, bytes, s.keys_in, s.keys_out, s.vals_in, d_list, n, 0, 31, st);
+    e = hipcub::DeviceRadixSort::SortPairs(s.sort_tmp, bytes, s.keys_in, s.keys_out, s.vals_in, d_list, n, 0, 32, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(rg_header, dim3(1), dim3(64), 0, st, s, d_hdr, h_hdr, n);
     return hipGetLastError();
