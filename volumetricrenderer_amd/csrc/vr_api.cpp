@@ -2166,7 +2166,10 @@ try {
         // and fill the rest (tile_is_empty); the experiments' kernels march all
         const bool fill = c->empty_fill && c->region_exact && !sc.slab && rb.seg_len == 0 && !lat_on(c, pl.layout);
         a.empty_fill = fill ? 1 : 0;
-        if (fill && rb.most_marched > 0) sc.map.nwx = std::max(1, (rb.most_marched + tpw - 1) / tpw);
+        // Waves: as many as before (the list over tiles_per_wave), but no more
+        // than marched entries -- the waves that held only empty tiles go;
+        // each marched tile keeps a wave of its own where it had one
+        if (fill && rb.most_marched > 0) sc.map.nwx = std::max(1, std::min(sc.map.nwx, rb.most_marched));
         if (rb.seg_len > 0) {
             // segmented lists (one lane per ray): the terms scratch must hold
             // every segmented tile's rays at this frame's max_steps
@@ -2205,9 +2208,11 @@ try {
             if (K == 0) K = auto_split(c, rb.nwork);
             if (K > 1) {
                 const int ktpw = tpw;
-                const int most = a.empty_fill && rb.most_marched > 0 ? rb.most_marched : rb.most;
+                const int most = rb.most;
                 sc.split = K;
                 sc.map.nwx = std::max(1, (most * K + ktpw - 1) / ktpw);
+                if (a.empty_fill && rb.most_marched > 0)   // (as above, in split units)
+                    sc.map.nwx = std::max(1, std::min(sc.map.nwx, rb.most_marched * K));
             }
         }
     }
