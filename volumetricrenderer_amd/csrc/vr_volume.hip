@@ -7,6 +7,7 @@
 // All are HBM-bound streaming kernels: wide coalesced accesses, grid-stride.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 #include "vr_internal.h"
 #include "vr_noise.h"
@@ -403,7 +404,11 @@ dim3 grid_rows(size_t rows_per_rank, int nranks, int first_rank, long long elems
 {
     const long long rows = (long long)(nranks - first_rank) * (long long)rows_per_rank;
     const long long gx = (elems + kBlock - 1) / kBlock;
-    const long long gy = std::max(1LL, std::min({rows, (512 + gx - 1) / gx, 65535LL}));
+    static const long long target = [] {   // timing experiments: VR_ASM_WGS workgroups in all
+        const char* e = std::getenv("VR_ASM_WGS");
+        return e && std::atoll(e) > 0 ? std::atoll(e) : 512LL;
+    }();
+    const long long gy = std::max(1LL, std::min({rows, (target + gx - 1) / gx, 65535LL}));
     return dim3((unsigned)gx, (unsigned)gy);
 }
 
