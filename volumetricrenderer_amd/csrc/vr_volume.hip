@@ -320,12 +320,10 @@ __device__ __forceinline__ int assembled_row(int q, int rows_per_rank, int nrank
     return y < height ? y : -1;
 }
 
-// The assembly kernels (vr_assemble_frame): rows x elements.  A small grid
-// (~2 workgroups per CU, launch_assemble*) whose lanes each move kAsmBatch
-// rows' elements with all the loads in flight before the first store: the
-// assembly runs beside the other render stream's march, which holds most of
-// the wave slots, so a grid of one-element lanes waits several rounds of
-// slots and memory round trips (~16 us for 7/8 of a 1080p frame, profiles/r05).
+// The assembly kernels (vr_assemble_frame): rows x elements.  Each lane moves
+// up to kAsmBatch rows' elements with all the loads in flight before the
+// first store (frames taller than the grid); the frame row comes from
+// block-uniform scalar arithmetic, with no per-element division.
 constexpr int kAsmBatch = 8;
 template <typename S, typename D, typename F>
 __device__ __forceinline__ void assemble_rows(const S* __restrict__ src, int rows_per_rank, int nranks, int row_elems,
@@ -398,16 +396,14 @@ __global__ __launch_bounds__(kBlock) void k_assemble_grey(const S* __restrict__ 
 }
 
 // grid of the assembly kernels: ceil(elems / kBlock) workgroups across a row,
-// rows over blockIdx.y -- about 512 workgroups in all (2 per CU), at most one
-// batch of rows per workgroup row more than needed
+// rows over blockIdx.y -- about 2048 workgroups in all, so 7/8 of a 1080p
+// frame is one row per workgroup row (more, smaller workgroups run faster
+// beside the other stream's march: profiles/r05/assembly_grid.txt)
 dim3 grid_rows(size_t rows_per_rank, int nranks, int first_rank, long long elems)
 {
     const long long rows = (long long)(nranks - first_rank) * (long long)rows_per_rank;
     const long long gx = (elems + kBlock - 1) / kBlock;
-    static const long long target = [] {   // timing experiments: VR_ASM_WGS workgroups in all
-        const char* e = std::getenv("VR_ASM_WGS");
-        return e && std::atoll(e) > 0 ? std::atoll(e) : 512LL;
-    }();
+    constexpr long long target = 2048;   // rank 0 at N = 8: 0.0212 ms/frame, 0.0215 at 1024, 0.0220 at 512, 0.0245 at 128
     const long long gy = std::max(1LL, std::min({rows, (target + gx - 1) / gx, 65535LL}));
     return dim3((unsigned)gx, (unsigned)gy);
 }
