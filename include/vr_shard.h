@@ -157,6 +157,19 @@ vr_status vr_shard_set_host_threads(vr_shard* sh, int n);
  * communication stream, ordered after each render by events.  Every rank
  * must choose the same.  Results are identical.                           */
 vr_status vr_shard_set_exchange_streams(vr_shard* sh, int on_render);
+/* Rank 0 as a compositor: 1 = rank 0 renders no bands and only receives and
+ * assembles; ranks 1..N-1 render the interleaved band sets of a world of N-1
+ * renderers (rank r: band_stride N-1, band_first r-1).  0 = every rank
+ * renders (band_stride N, band_first rank) and rank 0 renders its own bands
+ * in place.  Default: 1 from 8 ranks on (the assembly of 7/8 of a frame
+ * beside rank 0's render made it the slowest rank).  Every rank must choose
+ * the same, before its first frames (band buffers are resized).  Results are
+ * identical. */
+vr_status vr_shard_set_compositor(vr_shard* sh, int on);
+int       vr_shard_get_compositor(vr_shard* sh);
+/* This rank's band set: band_stride and band_first of its vr_render target
+ * (rank 0 as a compositor: stride N-1, first -1, no rows). */
+vr_status vr_shard_bands(vr_shard* sh, int* band_stride, int* band_first);
 int       vr_shard_aborted(vr_shard* sh);
 /* Self-test of the deadline loop on the host (no GPU, no RCCL): mode 0 a
  * state that completes after 5 polls, 1 one that fails at the 3rd, 2 one that

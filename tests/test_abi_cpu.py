@@ -32,7 +32,7 @@ def test_shard_library_exports_every_declared_symbol():
     from volumetricrenderer_amd import _lib
     lib = _lib.load_shard()
     declared = header_functions("vr_shard.h")
-    assert len(declared) == 22
+    assert len(declared) == 25
     for name in declared:
         assert hasattr(lib, name), name
     assert sorted(declared) == _lib.shard_exported_symbols()
@@ -46,6 +46,11 @@ def test_shard_library_exports_every_declared_symbol():
     with pytest.raises(_lib.VRError):
         _lib.shard_call("vr_shard_set_solo", None, 1)
     assert _lib.shard_call("vr_shard_get_render_streams", None) == 0
+    with pytest.raises(_lib.VRError):
+        _lib.shard_call("vr_shard_set_compositor", None, 1)
+    with pytest.raises(_lib.VRError):
+        _lib.shard_call("vr_shard_bands", None, None, None)
+    assert _lib.shard_call("vr_shard_get_compositor", None) == -1
 
 
 def test_shard_deadline_loop_selftest():

@@ -254,15 +254,18 @@ def test_native_share_volume(world, loopback):
 SPIN_DEG = 1.6   # TestMain.cpp:171-184, :222-224: the held A/D key, 100 deg/s x 0.016 s
 
 
-@pytest.mark.parametrize("fmt,render_streams,threads,on_render", [(0, 2, 1, False), (1, 2, 1, False), (1, 1, 1, False),
-                                                                  (1, 2, 2, False), (0, 2, 1, True)])
-def test_native_loopback_spinning_8_ranks(oracle, fmt, render_streams, threads, on_render):
+@pytest.mark.parametrize("fmt,render_streams,threads,on_render,compositor",
+                         [(0, 2, 1, False, None), (1, 2, 1, False, None), (1, 1, 1, False, None),
+                          (1, 2, 2, False, None), (0, 2, 1, True, None), (1, 2, 1, True, False),
+                          (1, 1, 1, True, True)])
+def test_native_loopback_spinning_8_ranks(oracle, fmt, render_streams, threads, on_render, compositor):
     """A moving camera through the native 8-rank frame loop (loopback: this
     process renders every rank's interleaved band set): 40 frames, frame i
     with its own shader data (vr_shard_run_frames, phi += 1.6 deg), 2 in
     flight, on two alternating render streams (the default) or one.  Frames
     1, 33 and 40, assembled on rank 0, equal the oracle's whole frame bit for
-    bit (RGBA32F and RGBA8)."""
+    bit (RGBA32F and RGBA8).  At 8 ranks rank 0 is a compositor by default
+    (renders no bands); compositor=False keeps it rendering in place."""
     import sys
     sys.path.insert(0, ROOT)
     import volumetricrenderer_amd as vr
@@ -275,7 +278,10 @@ def test_native_loopback_spinning_8_ranks(oracle, fmt, render_streams, threads, 
         r.set_shader_data(*cams[0])
         r.set_march(vr.march_defaults())
         pl = RcclBandPipeline(r, W, H, fmt, band_rows=16, world=8, rank=0, loopback=True,
-                              render_streams=render_streams, host_threads=threads, exchange_on_render=on_render)
+                              render_streams=render_streams, host_threads=threads, exchange_on_render=on_render,
+                              compositor=compositor)
+        assert pl.compositor == (compositor is not False)
+        assert pl.my_rows == (0 if pl.compositor else pl.rows_per_rank)
         got, done = {}, 0
         try:
             for stop in (1, 33, 40):
@@ -300,10 +306,10 @@ def band_set_of(frame, rank, world, band_rows):
     return frame[rows]
 
 
-@pytest.mark.parametrize("render_streams,interval,threads,on_render", [(2, 3, 1, False), (2, 32, 1, False),
-                                                                       (1, 3, 1, False), (2, 3, 2, False),
-                                                                       (2, 3, 1, True)])
-def test_native_solo_rank_spinning(oracle, render_streams, interval, threads, on_render):
+@pytest.mark.parametrize("render_streams,interval,threads,on_render,compositor",
+                         [(2, 3, 1, False, None), (2, 32, 1, False, None), (1, 3, 1, False, None),
+                          (2, 3, 2, False, None), (2, 3, 1, True, None), (2, 3, 1, True, True)])
+def test_native_solo_rank_spinning(oracle, render_streams, interval, threads, on_render, compositor):
     """One rank of a 4-rank frame loop rehearsed alone (vr_shard_set_solo:
     its band set only, no exchange) with a moving camera: 24 frames with their
     own shader data on two alternating render streams, the region lists
@@ -323,7 +329,10 @@ def test_native_solo_rank_spinning(oracle, render_streams, interval, threads, on
         r.set_shader_data(*cams[0])
         r.set_march(vr.march_defaults())
         pl = RcclBandPipeline(r, W, H, 1, band_rows=16, world=world, rank=rank, loopback=True, solo=True,
-                              render_streams=render_streams, host_threads=threads, exchange_on_render=on_render)
+                              render_streams=render_streams, host_threads=threads, exchange_on_render=on_render,
+                              compositor=compositor)
+        stride, first = pl.band_stride, pl.band_first
+        assert (stride, first) == ((world - 1, rank - 1) if compositor else (world, rank))
         got, done = {}, 0
         try:
             for stop in (1, 7, 20, 24):
@@ -338,7 +347,7 @@ def test_native_solo_rank_spinning(oracle, render_streams, interval, threads, on
     for i, img in got.items():
         obj, glob = vr.shader_data_arrays(*cams[i - 1])
         ref, _ = oracle.render(vol, obj, glob, oracle.from_params(vr.march_defaults()), W, H, 1)
-        want = band_set_of(ref, rank, world, 16)[..., 0]
+        want = band_set_of(ref, first, stride, 16)[..., 0]
         assert img.shape == want.shape and np.array_equal(img.cpu().numpy(), want), i
 
 

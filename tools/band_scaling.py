@@ -39,6 +39,9 @@ def main():
     ap.add_argument("--streams", default="1,2", help="--native: render streams to compare")
     ap.add_argument("--rounds", type=int, default=3, help="--native: interleaved rounds")
     ap.add_argument("--threads", type=int, default=1, help="--native: host threads of the frame loop (1 or 2)")
+    ap.add_argument("--compositor", default="auto", choices=["auto", "on", "off"],
+                    help="--native: rank 0 renders no bands and only assembles (vr_shard_set_compositor; auto: the "
+                         "library's default, on from 8 ranks)")
     ap.add_argument("--exchange", default="render", choices=["render", "comm"],
                     help="--native: the exchange on the render streams (default) or on a communication stream "
                          "(vr_shard_set_exchange_streams 1 / 0)")
@@ -126,7 +129,8 @@ def native(a):
                 for ns in streams:
                     p = RcclBandPipeline(r, W, H, vr.FMT_RGBA8_UNORM, band_rows=a.band_rows, world=n, rank=first,
                                          loopback=True, solo=True, render_streams=ns, host_threads=a.threads,
-                                         exchange_on_render=a.exchange == "render")
+                                         exchange_on_render=a.exchange == "render",
+                                         compositor=None if a.compositor == "auto" else a.compositor == "on")
                     p.run_frames(8)   # region lists, code objects
                     p.barrier()
                     for k in range(a.rounds):

@@ -219,10 +219,14 @@ _SHARD_SIGS = {
     "vr_shard_set_solo": (ctypes.c_int, [_vp, ctypes.c_int]),
     "vr_shard_set_host_threads": (ctypes.c_int, [_vp, ctypes.c_int]),
     "vr_shard_set_exchange_streams": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "vr_shard_set_compositor": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "vr_shard_get_compositor": (ctypes.c_int, [_vp]),
+    "vr_shard_bands": (ctypes.c_int, [_vp, c_int_p, c_int_p]),
     "vr_shard_poll_selftest": (ctypes.c_int, [ctypes.c_int, ctypes.c_double, c_int_p]),
 }
 # shard functions whose int return is a value, not a vr_status
-_SHARD_VALUE_RETURNS = {"vr_shard_aborted", "vr_shard_poll_selftest", "vr_shard_get_render_streams"}
+_SHARD_VALUE_RETURNS = {"vr_shard_aborted", "vr_shard_poll_selftest", "vr_shard_get_render_streams",
+                        "vr_shard_get_compositor"}
 _shard_lib = None
 
 

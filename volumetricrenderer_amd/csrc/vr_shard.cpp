@@ -155,6 +155,11 @@ struct vr_shard {
     size_t gpitch = 0;                // tight band-set rows
     int my_rows = 0, rows_per_rank = 0;
     std::vector<int> rows_of;         // packed rows of every rank
+    // compositor (vr_shard_set_compositor): rank 0 renders no bands and only
+    // assembles; ranks 1..N-1 render the band sets of a world of N-1 renderers
+    // (rank r: band_first r - 1), received into gather slot r - 1
+    bool compositor = false;
+    bool started = false;             // a run has queued frames (the geometry is fixed)
     ncclComm_t comm = nullptr;
     hipStream_t comm_stream = nullptr;
     hipStream_t render_stream[2] = {};   // one per parity (render_streams == 2)
@@ -308,6 +313,22 @@ void release(vr_shard* sh)
 // exchange -> the next render of the parity with rendered[p] / done[p].
 bool others_here(const vr_shard* sh) { return sh->loopback && !sh->solo; }
 
+// Band geometry: renderers, a rank's band set (stride, first) and its gather slot.
+int renderers(const vr_shard* sh) { return sh->compositor ? sh->nranks - 1 : sh->nranks; }
+int band_first_of(const vr_shard* sh, int r) { return sh->compositor ? r - 1 : r; }
+uint8_t* slot_of(const vr_shard* sh, int p, int r)
+{
+    return sh->gathered[p] + (size_t)band_first_of(sh, r) * sh->rows_per_rank * sh->gpitch;
+}
+// the assembly: every renderer's rows, or (rank 0 rendering in place) all but rank 0's
+vr_status assemble(vr_shard* sh, int p, hipStream_t s)
+{
+    VR_TRY(vr_assemble_frame_ranks(sh->ctx, sh->gathered[p], sh->gformat, (size_t)sh->rows_per_rank, renderers(sh),
+                                   sh->compositor ? 0 : 1, sh->width, sh->height, sh->band_rows, sh->format,
+                                   sh->frame[p], s));
+    return VR_OK;
+}
+
 // The render-stream half of frame (parity p): wait for the exchange that last
 // read the parity's buffers (not rank 0, which renders in place), render, and
 // (not rank 0) mark the render for the exchange.
@@ -319,8 +340,8 @@ vr_status render_half(vr_shard* sh, int p, hipStream_t s, hipEvent_t t0, hipEven
     t.width = sh->width;
     t.height = sh->height;
     t.band_rows = sh->band_rows;
-    t.band_stride = sh->nranks;
-    t.band_first = sh->rank;
+    t.band_stride = renderers(sh);
+    t.band_first = band_first_of(sh, sh->rank);
     if (r0) {   // in place: the frame's own rows, the frame's format
         t.format = sh->format | VR_TARGET_BANDS_IN_PLACE;
         t.pixels = sh->frame[p];
@@ -337,8 +358,8 @@ vr_status render_half(vr_shard* sh, int p, hipStream_t s, hipEvent_t t0, hipEven
         t.format = sh->gformat;
         t.row_pitch = sh->gpitch;
         for (int r = 1; r < sh->nranks; ++r) {
-            t.band_first = r;
-            t.pixels = sh->gathered[p] + (size_t)r * sh->rows_per_rank * sh->gpitch;
+            t.band_first = band_first_of(sh, r);
+            t.pixels = slot_of(sh, p, r);
             if (sh->rows_of[r] > 0) VR_TRY(vr_render(sh->ctx, &t, s));
         }
     }
@@ -362,8 +383,8 @@ vr_status comm_half(vr_shard* sh, int p)
         if (r0) {
             for (int r = 1; r < sh->nranks; ++r)
                 if (sh->rows_of[r] > 0)
-                    NCCL_TRY(ncclRecv(sh->gathered[p] + (size_t)r * sh->rows_per_rank * sh->gpitch,
-                                      (size_t)sh->rows_of[r] * sh->gpitch, ncclUint8, r, sh->comm, sh->comm_stream));
+                    NCCL_TRY(ncclRecv(slot_of(sh, p, r), (size_t)sh->rows_of[r] * sh->gpitch, ncclUint8, r, sh->comm,
+                                      sh->comm_stream));
         } else if (sh->my_rows > 0) {
             NCCL_TRY(ncclSend(sh->local[p], (size_t)sh->my_rows * sh->gpitch, ncclUint8, 0, sh->comm,
                               sh->comm_stream));
@@ -371,9 +392,7 @@ vr_status comm_half(vr_shard* sh, int p)
         NCCL_TRY(ncclGroupEnd());
     }
     if (r0 && sh->nranks > 1)   // (a solo rehearsal expands whatever its slots hold: the same work)
-        VR_TRY(vr_assemble_frame_ranks(sh->ctx, sh->gathered[p], sh->gformat, (size_t)sh->rows_per_rank, sh->nranks,
-                                       1, sh->width, sh->height, sh->band_rows, sh->format, sh->frame[p],
-                                       sh->comm_stream));
+        SH_TRY(assemble(sh, p, sh->comm_stream));
     if (!r0 || here) {
         HIP_TRY(hipEventRecord(sh->done[p], sh->comm_stream));
         sh->pending[p] = true;
@@ -401,8 +420,8 @@ vr_status one_frame_on_render(vr_shard* sh, int p, hipStream_t rs, hipEvent_t t0
     t.width = sh->width;
     t.height = sh->height;
     t.band_rows = sh->band_rows;
-    t.band_stride = sh->nranks;
-    t.band_first = sh->rank;
+    t.band_stride = renderers(sh);
+    t.band_first = band_first_of(sh, sh->rank);
     if (r0) {
         t.format = sh->format | VR_TARGET_BANDS_IN_PLACE;
         t.pixels = sh->frame[p];
@@ -419,8 +438,8 @@ vr_status one_frame_on_render(vr_shard* sh, int p, hipStream_t rs, hipEvent_t t0
         t.format = sh->gformat;
         t.row_pitch = sh->gpitch;
         for (int r = 1; r < sh->nranks; ++r) {
-            t.band_first = r;
-            t.pixels = sh->gathered[p] + (size_t)r * sh->rows_per_rank * sh->gpitch;
+            t.band_first = band_first_of(sh, r);
+            t.pixels = slot_of(sh, p, r);
             if (sh->rows_of[r] > 0) VR_TRY(vr_render(sh->ctx, &t, rs));
         }
     }
@@ -430,17 +449,52 @@ vr_status one_frame_on_render(vr_shard* sh, int p, hipStream_t rs, hipEvent_t t0
         if (r0) {
             for (int r = 1; r < sh->nranks; ++r)
                 if (sh->rows_of[r] > 0)
-                    NCCL_TRY(ncclRecv(sh->gathered[p] + (size_t)r * sh->rows_per_rank * sh->gpitch,
-                                      (size_t)sh->rows_of[r] * sh->gpitch, ncclUint8, r, c, rs));
+                    NCCL_TRY(ncclRecv(slot_of(sh, p, r), (size_t)sh->rows_of[r] * sh->gpitch, ncclUint8, r, c, rs));
         } else if (sh->my_rows > 0) {
             NCCL_TRY(ncclSend(sh->local[p], (size_t)sh->my_rows * sh->gpitch, ncclUint8, 0, c, rs));
         }
         NCCL_TRY(ncclGroupEnd());
     }
-    if (r0 && sh->nranks > 1)
-        VR_TRY(vr_assemble_frame_ranks(sh->ctx, sh->gathered[p], sh->gformat, (size_t)sh->rows_per_rank, sh->nranks,
-                                       1, sh->width, sh->height, sh->band_rows, sh->format, sh->frame[p], rs));
+    if (r0 && sh->nranks > 1) SH_TRY(assemble(sh, p, rs));
     sh->last = p;
+    return VR_OK;
+}
+
+// Rank 0 as a compositor from this many ranks on (vr_shard_set_compositor):
+// at N = 8 a rank's 1/8 band set renders in ~0.017 ms and rank 0's, with the
+// assembly of the other 7/8 of the frame beside it, in ~0.021; as one of 7
+// renderers a rank takes ~0.019-0.020 (profiles/r05/compositor_*.txt)
+constexpr int kCompositorRanks = 8;
+
+void set_geometry(vr_shard* sh, bool compositor)
+{
+    sh->compositor = compositor && sh->nranks >= 2;
+    const int R = renderers(sh);
+    sh->rows_of.assign(sh->nranks, 0);
+    for (int r = 0; r < sh->nranks; ++r)
+        if (!sh->compositor || r > 0)
+            sh->rows_of[r] = vr_band_rows_packed(sh->height, sh->band_rows, R, band_first_of(sh, r));
+    sh->my_rows = sh->rows_of[sh->rank];
+    // band 0 is the first renderer's: it has the most rows
+    sh->rows_per_rank = vr_band_rows_packed(sh->height, sh->band_rows, R, 0);
+}
+
+// rank 0's gather slots / another rank's band sets, for the current geometry
+vr_status alloc_band_buffers(vr_shard* sh)
+{
+    for (int p = 0; p < 2; ++p) {
+        uint8_t*& b = sh->rank == 0 ? sh->gathered[p] : sh->local[p];
+        if (b) (void)hipFree(b);
+        b = nullptr;
+        const size_t bytes = sh->rank == 0 ? (size_t)sh->nranks * sh->rows_per_rank * sh->gpitch
+                                           : (size_t)std::max(sh->my_rows, 1) * sh->gpitch;
+        const hipError_t e = hipMalloc(&b, std::max(bytes, (size_t)1));
+        if (e != hipSuccess) {
+            b = nullptr;
+            return fail(e == hipErrorOutOfMemory ? VR_ERR_OOM : VR_ERR_HIP, "vr_shard: band buffers: %s",
+                        hipGetErrorString(e));
+        }
+    }
     return VR_OK;
 }
 
@@ -500,9 +554,7 @@ try {
     sh->pitch = (size_t)width * sh->bpp;
     sh->gformat = format == VR_FMT_RGBA32F ? VR_FMT_R32F : format == VR_FMT_RGBA8_SRGB ? VR_FMT_R8_SRGB : VR_FMT_R8_UNORM;
     sh->gpitch = (size_t)width * (format == VR_FMT_RGBA32F ? 4 : 1);
-    for (int r = 0; r < nranks; ++r) sh->rows_of.push_back(vr_band_rows_packed(height, band_rows, nranks, r));
-    sh->my_rows = sh->rows_of[rank];
-    sh->rows_per_rank = sh->rows_of[0];   // band 0 is rank 0's: it has the most rows
+    set_geometry(sh, nranks >= kCompositorRanks);
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     vr_status st = VR_OK;
@@ -523,13 +575,9 @@ try {
         hip_ok(hipEventCreateWithFlags(&sh->rendered[p], hipEventDisableTiming), "event");
         hip_ok(hipEventCreateWithFlags(&sh->done[p], hipEventDisableTiming), "event");
         hip_ok(hipEventCreateWithFlags(&sh->tail[p], hipEventDisableTiming), "event");
-        if (rank == 0) {
-            hip_ok(hipMalloc(&sh->gathered[p], (size_t)nranks * sh->rows_per_rank * sh->gpitch), "gather buffer");
-            hip_ok(hipMalloc(&sh->frame[p], (size_t)height * sh->pitch), "frame buffer");
-        } else {
-            hip_ok(hipMalloc(&sh->local[p], (size_t)std::max(sh->my_rows, 1) * sh->gpitch), "band buffer");
-        }
+        if (rank == 0) hip_ok(hipMalloc(&sh->frame[p], (size_t)height * sh->pitch), "frame buffer");
     }
+    if (st == VR_OK) st = alloc_band_buffers(sh);
     if (st != VR_OK) {
         const std::string msg = g_err;
         release(sh);
@@ -626,6 +674,7 @@ try {
     int next = 0;
     const auto h0 = std::chrono::steady_clock::now();
     const bool two = sh->render_streams == 2;
+    if (frames > 0) sh->started = true;   // the band geometry is fixed from here
     if (two && frames > 0) {   // the render streams start after the caller's queued work (e.g. the volume)
         HIP_TRY(hipEventRecord(sh->fence, s));
         for (hipStream_t rs : sh->render_stream) HIP_TRY(hipStreamWaitEvent(rs, sh->fence, 0));
@@ -996,6 +1045,35 @@ try {
     return VR_OK;
 } catch (...) {
     return caught_exception("vr_shard_copy_frame");
+}
+
+vr_status vr_shard_set_compositor(vr_shard* sh, int on)
+try {
+    if (!sh || on < 0 || on > 1) return fail(VR_ERR_INVALID, "vr_shard_set_compositor: bad argument");
+    if (on && sh->nranks < 2) return fail(VR_ERR_INVALID, "vr_shard_set_compositor: needs 2 or more ranks");
+    if ((on == 1) == sh->compositor) return VR_OK;
+    if (sh->started) return fail(VR_ERR_INVALID, "vr_shard_set_compositor: set before the first frames");
+    set_geometry(sh, on == 1);
+    return alloc_band_buffers(sh);
+} catch (...) {
+    return caught_exception("vr_shard_set_compositor");
+}
+
+int vr_shard_get_compositor(vr_shard* sh)
+try {
+    return sh ? (sh->compositor ? 1 : 0) : -1;
+} catch (...) {
+    return -1;
+}
+
+vr_status vr_shard_bands(vr_shard* sh, int* band_stride, int* band_first)
+try {
+    if (!sh) return fail(VR_ERR_INVALID, "vr_shard_bands: null");
+    if (band_stride) *band_stride = renderers(sh);
+    if (band_first) *band_first = band_first_of(sh, sh->rank);
+    return VR_OK;
+} catch (...) {
+    return caught_exception("vr_shard_bands");
 }
 
 vr_status vr_shard_rows(vr_shard* sh, int* my_rows, int* rows_per_rank)

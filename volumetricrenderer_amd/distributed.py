@@ -285,7 +285,8 @@ class RcclBandPipeline:
 
     def __init__(self, renderer, width: int, height: int, fmt: int, band_rows: int = 16, world: int = 1,
                  rank: int = 0, group=None, loopback: bool = False, timeout_s: float | None = None,
-                 render_streams: int = 2, solo: bool = False, host_threads: int = 1, exchange_on_render: bool = True):
+                 render_streams: int = 2, solo: bool = False, host_threads: int = 1, exchange_on_render: bool = True,
+                 compositor: bool | None = None):
         """loopback: one process renders all `world` ranks' band sets on its
         GPU and assembles them (no communicator; tests and rehearsals).
         solo (loopback only, any rank): each frame renders only this rank's
@@ -296,6 +297,9 @@ class RcclBandPipeline:
         (vr_shard_set_render_streams).
         host_threads: 2 = a worker thread issues every frame's exchange half
         (vr_shard_set_host_threads).
+        compositor: rank 0 renders no bands and only assembles, ranks 1..N-1
+        render the band sets of N-1 renderers (vr_shard_set_compositor; None =
+        the library's default: on from 8 ranks; every rank the same).
         exchange_on_render: True (default) = each frame's exchange follows its
         render on the frame's render stream, over a communicator per buffer
         parity, with no events; False = on a communication stream, ordered by
@@ -357,6 +361,8 @@ class RcclBandPipeline:
             _lib.shard_call("vr_shard_set_render_streams", h, int(render_streams))
             _lib.shard_call("vr_shard_set_host_threads", h, int(host_threads))
             _lib.shard_call("vr_shard_set_exchange_streams", h, 1 if exchange_on_render else 0)
+            if compositor is not None:
+                _lib.shard_call("vr_shard_set_compositor", h, 1 if compositor else 0)
             if solo:
                 _lib.shard_call("vr_shard_set_solo", h, 1)
         except _lib.VRError:
@@ -372,6 +378,10 @@ class RcclBandPipeline:
         mine, per = ctypes.c_int(), ctypes.c_int()
         _lib.shard_call("vr_shard_rows", h, ctypes.byref(mine), ctypes.byref(per))
         self.my_rows, self.rows_per_rank = mine.value, per.value
+        stride, first = ctypes.c_int(), ctypes.c_int()
+        _lib.shard_call("vr_shard_bands", h, ctypes.byref(stride), ctypes.byref(first))
+        self.band_stride, self.band_first = stride.value, first.value   # this rank's band set (vr_render target)
+        self.compositor = bool(_lib.shard_call("vr_shard_get_compositor", h))
 
     @property
     def render_streams(self) -> int:
