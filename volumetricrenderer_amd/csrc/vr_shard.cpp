@@ -460,11 +460,15 @@ vr_status one_frame_on_render(vr_shard* sh, int p, hipStream_t rs, hipEvent_t t0
     return VR_OK;
 }
 
-// Rank 0 as a compositor from this many ranks on (vr_shard_set_compositor):
-// at N = 8 a rank's 1/8 band set renders in ~0.017 ms and rank 0's, with the
-// assembly of the other 7/8 of the frame beside it, in ~0.021; as one of 7
-// renderers a rank takes ~0.019-0.020 (profiles/r05/compositor_*.txt)
+// Rank 0 as a compositor by default (vr_shard_set_compositor) from this many
+// ranks on, for frames of at most kCompositorPixels.  Config 5 (1080p) at
+// N = 8: rank 0 rendering its own 1/8 beside the assembly of the other 7/8
+// takes 0.0208 ms per frame against 0.0165 on the other ranks; as a
+// compositor the slowest of 7 renderers takes 0.0198.  Config 4 (4K): the
+// render dominates -- 0.0535 against 0.0565 as a compositor -- so larger
+// frames keep rank 0 rendering (profiles/r05/compositor_ab.txt).
 constexpr int kCompositorRanks = 8;
+constexpr long long kCompositorPixels = 2560LL * 1440LL;
 
 void set_geometry(vr_shard* sh, bool compositor)
 {
@@ -554,7 +558,7 @@ try {
     sh->pitch = (size_t)width * sh->bpp;
     sh->gformat = format == VR_FMT_RGBA32F ? VR_FMT_R32F : format == VR_FMT_RGBA8_SRGB ? VR_FMT_R8_SRGB : VR_FMT_R8_UNORM;
     sh->gpitch = (size_t)width * (format == VR_FMT_RGBA32F ? 4 : 1);
-    set_geometry(sh, nranks >= kCompositorRanks);
+    set_geometry(sh, nranks >= kCompositorRanks && (long long)width * height <= kCompositorPixels);
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     vr_status st = VR_OK;
