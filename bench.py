@@ -359,10 +359,10 @@ def main() -> int:
         local_cells = int(counter.item())
         r.set_option("count", 0)
     red_dev = "cuda" if args.backend == "nccl" and not native else "cpu"
-    tot = torch.tensor([local_steps], dtype=torch.int64, device=red_dev)
+    tot = torch.tensor([local_steps, local_evals, local_cells or 0], dtype=torch.int64, device=red_dev)
     if world > 1:
         dist.all_reduce(tot)
-    frame_steps = int(tot.item())
+    frame_steps, frame_evals, frame_cells = (int(v) for v in tot.tolist())
 
     # HIP events around the march launch of every 4th frame: the sample of
     # launch durations the roofline uses.  Two event records per frame cost a
@@ -540,7 +540,15 @@ def main() -> int:
         # its duration is not a frame's -- the roofline takes the wall time per frame
         overlap = native and args.render_streams == 2
         roof_ms = ms_per_step if overlap else kern_ms
-        roofline = roofline_of(r, proc, shadow, variant, local_steps, local_evals, local_cells, roof_ms)
+        compositor = native and pipe is not None and pipe.compositor
+        if compositor:   # rank 0 renders nothing: the per-GPU figure is a renderer's average share
+            nr = world - 1
+            roofline = roofline_of(r, proc, shadow, variant, frame_steps // nr, frame_evals // nr,
+                                   (frame_cells // nr) if local_cells is not None else None, roof_ms)
+            roofline["achieved_def"] += (f"; rank 0 is a compositor (vr_shard_set_compositor): the work is the "
+                                         f"frame's over its {nr} rendering ranks")
+        else:
+            roofline = roofline_of(r, proc, shadow, variant, local_steps, local_evals, local_cells, roof_ms)
         if overlap:
             roofline["achieved_def"] += ("; renders overlap (two render streams, vr_shard_set_render_streams), so "
                                          "the time is the wall time per frame of the timed window, not a launch's "
@@ -601,7 +609,8 @@ def main() -> int:
                                   else "reference (TestMain.cpp:219-245)"),
                        "kernel": r.kernel_variant + ("_deferred" if proc is not None and shadow > 0
                                                       and r.get_option("shadow_defer") == 1 else ""),
-                       "parallelism": f"bands16x{world}" + (", 2 frames in flight" if args.inflight == 2 else "")
+                       "parallelism": (f"bands16x{world - 1}, rank 0 compositing" if compositor else f"bands16x{world}")
+                                      + (", 2 frames in flight" if args.inflight == 2 else "")
                                       + (f", {args.render_streams} render stream{'s' if args.render_streams > 1 else ''}"
                                          + (f", exchange on {args.exchange} stream{'s' if args.exchange == 'render' else ''}"
                                             if args.render_streams == 2 else "")
