@@ -1,7 +1,7 @@
 #!/bin/bash
 # occupancy A/B of the primary procedural marches after the phased density
 set -o pipefail
-cd "$(dirname "$0")/../.."
+cd "$(dirname "$0")/../../.."
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 mkdir -p gpurun_out/r05
 L=volumetricrenderer_amd

@@ -1,7 +1,7 @@
 #!/bin/bash
 # rank 0's assembly grid size at N = 8 (config 5, solo rank 0)
 set -o pipefail
-cd "$(dirname "$0")/../.."
+cd "$(dirname "$0")/../../.."
 O=gpurun_out/r05
 mkdir -p $O
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp

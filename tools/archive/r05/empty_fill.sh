@@ -2,7 +2,7 @@
 # empty tiles filled, not marched: the parity test, the whole GPU suite, then
 # per-rank frame streams with the option on / off, and the bench line
 set -o pipefail
-cd "$(dirname "$0")/../.."
+cd "$(dirname "$0")/../../.."
 O=gpurun_out/r05
 mkdir -p $O
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp

@@ -1,7 +1,7 @@
 #!/bin/bash
 # timing bound: regions launches without the idle (no estimated work) tiles
 set -o pipefail
-cd "$(dirname "$0")/../.."
+cd "$(dirname "$0")/../../.."
 O=gpurun_out/r05
 mkdir -p $O
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
