@@ -93,6 +93,12 @@ constexpr int kRegionKeyLen = 39;
 // K = 2 beats K = 1 by 17 % at N = 2 and K = 4 by 2-5 % at N = 4; at 4K x 256
 // (4x the tiles) it keeps K = 1 up to N = 4.
 constexpr long long kSplitOneLane = 6000, kSplitTwoLanes = 1400;
+// With consecutive frames overlapping on two streams (option frames_overlap,
+// set by vr_shard_run_frames) the next frame's waves fill the SIMDs while this
+// one's longest rays finish, so one lane per ray pays from fewer tiles on:
+// K = 1 from 2500 (1080p at 512^3, N = 2: 0.0583 ms per frame at K = 1 against
+// 0.0632 at K = 2; on one stream 0.0921 against 0.0744; profiles/r05/split_overlap.txt)
+constexpr long long kSplitOneLaneOverlap = 2500;
 
 struct Plan {
     int layout, wrap;
@@ -250,6 +256,7 @@ struct Ctx {
     unsigned long long gen = 1;
     int launch_cache = 1;
     int empty_fill = 1;          // option "empty_fill": regions launches fill the lists' empty tiles, not march them
+    int frames_overlap = 0;      // option "frames_overlap": consecutive renders overlap (auto split rule)
     struct Cached {
         bool valid = false;
         unsigned long long gen = 0;
@@ -987,6 +994,12 @@ try {
         c->launch_cache = value;
         return VR_OK;
     }
+    if (n == "frames_overlap") {   // the caller overlaps consecutive frames on two streams (auto split)
+        if (value < 0 || value > 1) return fail(VR_ERR_INVALID, "vr_set_option: frames_overlap is 0 or 1");
+        if (c->frames_overlap != value) ++c->gen;
+        c->frames_overlap = value;
+        return VR_OK;
+    }
     if (n == "empty_fill") {   // regions: fill the lists' empty tiles instead of marching them
         if (value < 0 || value > 1) return fail(VR_ERR_INVALID, "vr_set_option: empty_fill is 0 or 1");
         c->empty_fill = value;
@@ -1180,6 +1193,7 @@ try {
     if (n == "lat") return c->lat;
     if (n == "launch_cache") return c->launch_cache;
     if (n == "empty_fill") return c->empty_fill;
+    if (n == "frames_overlap") return c->frames_overlap;
     if (n == "launch_cache_hits") return (int)std::min<long long>(c->lc_hits, 0x7fffffff);
     if (n == "experiments") return VR_EXPERIMENTS;   // read-only: the measured-slower variants are built
     if (n == "region_interval") return c->region_interval;
@@ -1356,7 +1370,7 @@ static bool lat_on(const Ctx* c, int layout)
 static int auto_split(const Ctx* c, long long nwork)
 {
     if (c->split > 0) return c->split;
-    return nwork >= kSplitOneLane ? 1 : nwork >= kSplitTwoLanes ? 2 : 4;
+    return nwork >= (c->frames_overlap ? kSplitOneLaneOverlap : kSplitOneLane) ? 1 : nwork >= kSplitTwoLanes ? 2 : 4;
 }
 
 // The lists of the GPU build that last completed (host-mapped header, read

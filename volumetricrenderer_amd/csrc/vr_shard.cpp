@@ -679,6 +679,20 @@ try {
     const auto h0 = std::chrono::steady_clock::now();
     const bool two = sh->render_streams == 2;
     if (frames > 0) sh->started = true;   // the band geometry is fixed from here
+    // two render streams: tell the ctx its consecutive renders overlap (its
+    // auto split rule), for this run
+    struct OverlapHint {
+        void* ctx;
+        int prev;
+        OverlapHint(void* c, bool on) : ctx(c), prev(on ? vr_get_option(c, "frames_overlap") : -1)
+        {
+            if (prev == 0) (void)vr_set_option(ctx, "frames_overlap", 1);
+        }
+        ~OverlapHint()
+        {
+            if (prev == 0) (void)vr_set_option(ctx, "frames_overlap", 0);
+        }
+    } overlap_hint(sh->ctx, two && frames > 0);
     if (two && frames > 0) {   // the render streams start after the caller's queued work (e.g. the volume)
         HIP_TRY(hipEventRecord(sh->fence, s));
         for (hipStream_t rs : sh->render_stream) HIP_TRY(hipStreamWaitEvent(rs, sh->fence, 0));
