@@ -577,7 +577,7 @@ def main() -> int:
                 if lookups:
                     # the unit that binds config 5: the texture
                     # address pipe, ~1 cycle per L1 lookup (quad x distinct 128-B line)
-                    rate = lookups / (kern_ms * 1e-3) / 1e9
+                    rate = lookups / (roof_ms * 1e-3) / 1e9   # (the wall time per frame when launches overlap)
                     ta = {"achieved": round(rate, 1), "peak": TA_PEAK_GLOOKUPS, "unit": "G L1 lookups/s",
                           "frac": round(rate / TA_PEAK_GLOOKUPS, 4), "lookups_per_launch": lookups,
                           "ta_busy_pmc": tj.get("ta_busy"),
@@ -630,8 +630,8 @@ def main() -> int:
             **({"frames_in_flight_2": inflight2} if inflight2 else {}),
             "kernel_ms_mean_max_rank": round(kern_ms_max, 5),
             "roofline": dict(roofline, traffic=traffic,
-                             **({"traffic_GBs": round(traffic / (kern_ms * 1e-3) / 1e9, 1),
-                                 "traffic_frac": round(traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                             **({"traffic_GBs": round(traffic / (roof_ms * 1e-3) / 1e9, 1),
+                                 "traffic_frac": round(traffic / (roof_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                                  "traffic_def": "PMC HBM bytes per launch (profiles/traffic.json) / the same "
                                                 "mean kernel duration: the bytes the kernel really moves"}
                                 if traffic else {}),
