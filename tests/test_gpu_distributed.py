@@ -286,6 +286,10 @@ def test_native_loopback_spinning_8_ranks(oracle, fmt, render_streams, threads, 
         try:
             for stop in (1, 33, 40):
                 pl.run_frames(stop - done, cameras=cams[done:stop])
+                if stop == 1:   # the band geometry is fixed once frames are queued
+                    from volumetricrenderer_amd import _lib
+                    with pytest.raises(vr.VRError):
+                        _lib.shard_call("vr_shard_set_compositor", pl._h, 0 if pl.compositor else 1)
                 assert pl.host_ms >= 0.0
                 done = stop
                 got[stop] = pl.frame()

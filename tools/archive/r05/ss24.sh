@@ -1,7 +1,7 @@
 #!/bin/bash
 # split K / tiles per wave at N = 2 and 4 after empty-tile fill (config 5)
 set -o pipefail
-cd "$(dirname "$0")/../.."
+cd "$(dirname "$0")/../../.."
 O=gpurun_out/r05
 mkdir -p $O
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
