@@ -257,7 +257,6 @@ struct Ctx {
     int launch_cache = 1;
     int empty_fill = 1;          // option "empty_fill": regions launches fill the lists' empty tiles, not march them
     int frames_overlap = 0;      // option "frames_overlap": consecutive renders overlap (auto split rule)
-    int wave_prio = 0;           // option "wave_prio": regions waves issue by list position
     struct Cached {
         bool valid = false;
         unsigned long long gen = 0;
@@ -995,12 +994,6 @@ try {
         c->launch_cache = value;
         return VR_OK;
     }
-    if (n == "wave_prio") {
-        if (value < 0 || value > 1) return fail(VR_ERR_INVALID, "vr_set_option: wave_prio is 0 or 1");
-        if (c->wave_prio != value) ++c->gen;
-        c->wave_prio = value;
-        return VR_OK;
-    }
     if (n == "frames_overlap") {   // the caller overlaps consecutive frames on two streams (auto split)
         if (value < 0 || value > 1) return fail(VR_ERR_INVALID, "vr_set_option: frames_overlap is 0 or 1");
         if (c->frames_overlap != value) ++c->gen;
@@ -1201,7 +1194,6 @@ try {
     if (n == "launch_cache") return c->launch_cache;
     if (n == "empty_fill") return c->empty_fill;
     if (n == "frames_overlap") return c->frames_overlap;
-    if (n == "wave_prio") return c->wave_prio;
     if (n == "launch_cache_hits") return (int)std::min<long long>(c->lc_hits, 0x7fffffff);
     if (n == "experiments") return VR_EXPERIMENTS;   // read-only: the measured-slower variants are built
     if (n == "region_interval") return c->region_interval;
@@ -2072,7 +2064,6 @@ try {
     a.format = tfmt;
     a.bands_in_place = in_place && t->band_rows > 0 ? 1 : 0;
     a.empty_fill = 0;   // set with the schedule (regions, default kernels)
-    a.wave_prio = c->wave_prio;
     a.step_counter = reinterpret_cast<unsigned long long*>(t->step_counter);
     HIP_TRY(hipSetDevice(c->device));
     if (c->proc.enabled) {

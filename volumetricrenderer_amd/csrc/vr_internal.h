@@ -208,7 +208,6 @@ struct MarchArgs {
     void* out;
     long long pitch;
     int format;
-    int wave_prio;               // regions: issue priority by list position (the longest tiles lead each list)
     int empty_fill;              // regions lists: march each XCD's first hdr[kRegionWork + x] entries, fill the
                                  // rest (tiles no ray of which meets the box) with the uncovered value
     int bands_in_place;          // vr.h VR_TARGET_BANDS_IN_PLACE: packed row orow is stored at its frame row

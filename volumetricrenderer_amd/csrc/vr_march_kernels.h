@@ -1118,20 +1118,6 @@ __global__ __launch_bounds__(kThreads) void march_rings(const MarchArgs a, int c
 // (DESIGN.md sec. 5.3).  XCD = blockIdx % 8 is a speed-only assumption.
 // WGW waves per workgroup (option wg_waves): the waves of one workgroup run on
 // one CU and share its L1, and they render consecutive list entries.
-// Issue priority of a wave marching entry k of its XCD's list of `count`
-// (MarchArgs.wave_prio): the lists lead with the longest tiles, whose rays are
-// the frame's critical path (each step waits a gather round trip in a queue
-// every wave shares), so their waves issue first on their SIMD: the first
-// 1/16 of the list at 3, the next 1/16 at 2, the next 1/8 at 1, the rest at 0.
-__device__ __forceinline__ void set_list_prio(int k, int count)
-{
-    const int q = (16 * k) / (count > 0 ? count : 1);
-    if (q < 1) __builtin_amdgcn_s_setprio(3);
-    else if (q < 2) __builtin_amdgcn_s_setprio(2);
-    else if (q < 4) __builtin_amdgcn_s_setprio(1);
-    else __builtin_amdgcn_s_setprio(0);
-}
-
 // The regions lists' empty tiles (MarchArgs.empty_fill; vr_internal.h
 // tile_is_empty): XCD x's entries [marched, count) after the marched ones.
 // Wave w of the XCD writes the uncovered value -- what the march stores for a
@@ -1169,7 +1155,6 @@ __device__ __forceinline__ void regions_body(const MarchArgs& a, const unsigned*
     const int lane = threadIdx.x & 63;
     unsigned long long steps = 0;
     for (int k = w; w < nwx && k < count; k += nwx) {   // the grid rounds nwx up to whole workgroups
-        if (a.wave_prio) set_list_prio(k, count);
         const unsigned t = tiles[begin + k];
         const int tx = (int)(t & 0xffffu), ty = (int)(t >> 16);
         steps += march_pixel<LAYOUT, WRAP, EARLY, ZO, UM>(a, f, tx * 8 + lane_x<LAYOUT>(lane),
@@ -1459,7 +1444,6 @@ __global__ __launch_bounds__(kThreads) void march_regions_split(const MarchArgs 
     const int px = ((rho >> 2) % (SW / 2)) * 2 + (rho & 1), py = ((rho >> 2) / (SW / 2)) * 2 + ((rho >> 1) & 1);
     unsigned long long steps = 0;
     for (int u = w; w < nwx && u < units; u += nwx) {
-        if (a.wave_prio) set_list_prio(u, units);
         const unsigned t = tiles[begin + u / K];
         const int s = u % K;
         const int x = (int)(t & 0xffffu) * 8 + (s % NSX) * SW + px, orow = (int)(t >> 16) * 8 + (s / NSX) * SH + py;
