@@ -541,6 +541,7 @@ def main() -> int:
         overlap = native and args.render_streams == 2
         roof_ms = ms_per_step if overlap else kern_ms
         compositor = native and pipe is not None and pipe.compositor
+        rows_part = native and pipe is not None and pipe.partition == "rows"
         if compositor:   # rank 0 renders nothing: the per-GPU figure is a renderer's average share
             nr = world - 1
             roofline = roofline_of(r, proc, shadow, variant, frame_steps // nr, frame_evals // nr,
@@ -609,7 +610,9 @@ def main() -> int:
                                   else "reference (TestMain.cpp:219-245)"),
                        "kernel": r.kernel_variant + ("_deferred" if proc is not None and shadow > 0
                                                       and r.get_option("shadow_defer") == 1 else ""),
-                       "parallelism": (f"bands16x{world - 1}, rank 0 compositing" if compositor else f"bands16x{world}")
+                       "parallelism": ((f"row ranges x{world - 1}" if rows_part else f"bands16x{world - 1}")
+                                       + ", rank 0 compositing" if compositor
+                                       else (f"row ranges x{world}" if rows_part else f"bands16x{world}"))
                                       + (", 2 frames in flight" if args.inflight == 2 else "")
                                       + (f", {args.render_streams} render stream{'s' if args.render_streams > 1 else ''}"
                                          + (f", exchange on {args.exchange} stream{'s' if args.exchange == 'render' else ''}"

@@ -148,10 +148,18 @@ typedef struct {
  * into the frame (vr_shard.h), and the assembly skips them
  * (vr_assemble_frame_ranks).                                               */
 #define VR_TARGET_BANDS_IN_PLACE 0x100
+/* OR'ed into vr_target.format: the target is one contiguous range of frame
+ * rows, [band_first, band_first + band_rows), instead of a band set.
+ * band_first must be a multiple of 8 and band_stride must be 1; rows past
+ * `height` are not written.  The rows are packed from row 0 of `pixels`, or
+ * stored at their frame rows with VR_TARGET_BANDS_IN_PLACE.  The multi-GPU
+ * loop's balanced row ranges (vr_shard.h vr_shard_balance_rows).            */
+#define VR_TARGET_ROW_RANGE 0x200
 
 typedef struct {
     int32_t   width, height;
-    int32_t   format;        /* vr_format, optionally | VR_TARGET_BANDS_IN_PLACE */
+    int32_t   format;        /* vr_format, optionally | VR_TARGET_BANDS_IN_PLACE
+                              * and/or VR_TARGET_ROW_RANGE                   */
     int32_t   band_rows, band_stride, band_first;
     void*     pixels;
     size_t    row_pitch;     /* bytes; 0 = tightly packed                  */
@@ -256,6 +264,18 @@ vr_status vr_assemble_frame_ranks(void* ctx, const void* d_gathered, int gathere
                                   int frame_format, void* d_frame, void* stream);
 /* rows that vr_render writes for a band set (for sizing buffers)          */
 int vr_band_rows_packed(int height, int band_rows, int band_stride, int band_first);
+/* Split the frame's rows into `parts` contiguous ranges of equal estimated
+ * march work for the ctx's current camera and march constants (host, double;
+ * the same inputs give the same split on every rank).  row_begin[parts + 1]:
+ * range k is [row_begin[k], row_begin[k + 1]); row_begin[0] = 0,
+ * row_begin[parts] = height, the others multiples of 8 or height
+ * (VR_TARGET_ROW_RANGE).  The estimate per ray that meets the box is
+ * n^(row_pow / 100) + row_setup, n its a3 step count (frag.glsl:46), sampled
+ * every 8th pixel of every 8th row (vr_set_option "row_pow", default 130,
+ * and "row_setup", default 40: long rays cost more than their steps, the
+ * longest waves bound a small share's launch); range 0 takes
+ * "row_first_pct" (default 100) % of a mean share.                        */
+vr_status vr_row_partition(void* ctx, int width, int height, int parts, int* row_begin);
 
 /* ---- introspection: the kernel variant vr_render will launch ----------- */
 /* returns a static string, e.g. "grid_pad16_clamp"                        */

@@ -171,6 +171,26 @@ int       vr_shard_get_compositor(vr_shard* sh);
 /* This rank's band set: band_stride and band_first of its vr_render target
  * (rank 0 as a compositor: stride N-1, first -1, no rows). */
 vr_status vr_shard_bands(vr_shard* sh, int* band_stride, int* band_first);
+/* Contiguous row ranges instead of interleaved band sets.  Renderer k (rank
+ * k, or rank k + 1 with rank 0 as a compositor) renders frame rows
+ * [row_begin[k], row_begin[k + 1]) (vr.h VR_TARGET_ROW_RANGE); rank 0 gathers
+ * them at their own rows of a grey frame and expands the rows below its own
+ * range in one launch.  A rank's rays then cover one slab of the volume, and
+ * its L2s serve its rows' neighbours: the 4K frame of a 128^3 grid (config 4)
+ * at 8 ranks takes 0.0480 ms per frame against 0.0562 with 16-row bands
+ * (DESIGN.md sec. 7.3).  Rank 0 rendering in place takes a smaller share of
+ * the work (2 % less per other rank): it also expands the other ranks' rows.  row_begin[renderers + 1]: 0, non-decreasing,
+ * multiples of 8, the frame height last; NULL = back to band sets.  Every
+ * rank must set the same ranges, before its first frames; a later
+ * vr_shard_set_compositor returns the shard to band sets.
+ * vr_shard_balance_rows: the ranges of equal estimated work for the ctx's
+ * current camera (vr_row_partition), computed by rank 0 and broadcast -- a
+ * collective: every rank calls it.  vr_shard_partition: 1 = row ranges,
+ * 0 = band sets.  vr_shard_row_range: a rank's range (row ranges only). */
+vr_status vr_shard_set_rows(vr_shard* sh, const int* row_begin);
+vr_status vr_shard_balance_rows(vr_shard* sh);
+int       vr_shard_partition(vr_shard* sh);
+vr_status vr_shard_row_range(vr_shard* sh, int rank, int* row_first, int* rows);
 int       vr_shard_aborted(vr_shard* sh);
 /* Self-test of the deadline loop on the host (no GPU, no RCCL): mode 0 a
  * state that completes after 5 polls, 1 one that fails at the 3rd, 2 one that

@@ -211,6 +211,55 @@ def test_native_pipeline_loopback_ranks(world, band_rows, fmt, W, render_streams
             pl.close()
 
 
+@pytest.mark.parametrize("world,compositor,fmt,W,render_streams", [(2, False, 1, 500, 2), (5, False, 0, 499, 1),
+                                                                   (8, True, 1, 500, 2), (8, False, 2, 500, 2),
+                                                                   (3, True, 1, 499, 1)])
+def test_native_pipeline_loopback_row_ranges(world, compositor, fmt, W, render_streams):
+    """The loop's contiguous row ranges (vr_shard_balance_rows): every
+    renderer's range rendered by this process into a grey frame, rank 0's
+    own range in place (or none, as a compositor), the rows below rank 0's
+    expanded in one launch.  The frame equals a plain render; the ranges tile
+    the frame in rank order."""
+    import ctypes
+    import sys
+    sys.path.insert(0, ROOT)
+    import volumetricrenderer_amd as vr
+    from volumetricrenderer_amd import _lib
+    from volumetricrenderer_amd.distributed import RcclBandPipeline
+    H = 283
+    with vr.Renderer(0) as r:
+        r.generate_volume(vr.volume_recipe_defaults(size=64))
+        osd, gsd = vr.reference_shader_data(W / H, -30.0, 40.0)
+        r.set_shader_data(osd, gsd)
+        r.set_march(vr.march_defaults())
+        pl = RcclBandPipeline(r, W, H, fmt, band_rows=16, world=world, rank=0, loopback=True,
+                              render_streams=render_streams, compositor=compositor, partition="rows")
+        try:
+            assert pl.row_range is None   # balanced at the first frames
+            pl.run_frames(3)
+            assert _lib.shard_call("vr_shard_partition", pl._h) == 1
+            nxt = 0
+            for k in range(world):
+                r0, n = ctypes.c_int(), ctypes.c_int()
+                _lib.shard_call("vr_shard_row_range", pl._h, k, ctypes.byref(r0), ctypes.byref(n))
+                if compositor and k == 0:
+                    assert n.value == 0
+                    continue
+                assert r0.value == nxt and (r0.value % 8 == 0)
+                nxt = r0.value + n.value
+            assert nxt == H
+            assert pl.row_range == ((0, 0) if compositor else pl.row_range) and pl.my_rows == pl.row_range[1]
+            pl.barrier()
+            got = pl.frame()
+            full = r.render(W, H, fmt)
+            torch.cuda.synchronize()
+            assert np.array_equal(got.cpu().numpy(), full.cpu().numpy())
+            with pytest.raises(vr.VRError):   # fixed once frames are queued
+                _lib.shard_call("vr_shard_set_rows", pl._h, None)
+        finally:
+            pl.close()
+
+
 @pytest.mark.parametrize("world,loopback", [(1, False), (4, True)])
 def test_native_share_volume(world, loopback):
     """vr_shard_share_volume: rank 0's device volume installed through the
@@ -310,16 +359,20 @@ def band_set_of(frame, rank, world, band_rows):
     return frame[rows]
 
 
-@pytest.mark.parametrize("render_streams,interval,threads,on_render,compositor",
-                         [(2, 3, 1, False, None), (2, 32, 1, False, None), (1, 3, 1, False, None),
-                          (2, 3, 2, False, None), (2, 3, 1, True, None), (2, 3, 1, True, True)])
-def test_native_solo_rank_spinning(oracle, render_streams, interval, threads, on_render, compositor):
+@pytest.mark.parametrize("render_streams,interval,threads,on_render,compositor,partition",
+                         [(2, 3, 1, False, None, "bands"), (2, 32, 1, False, None, "bands"),
+                          (1, 3, 1, False, None, "bands"), (2, 3, 2, False, None, "bands"),
+                          (2, 3, 1, True, None, "bands"), (2, 3, 1, True, True, "bands"),
+                          (2, 3, 1, True, None, "rows"), (2, 3, 1, True, True, "rows")])
+def test_native_solo_rank_spinning(oracle, render_streams, interval, threads, on_render, compositor, partition):
     """One rank of a 4-rank frame loop rehearsed alone (vr_shard_set_solo:
     its band set only, no exchange) with a moving camera: 24 frames with their
     own shader data on two alternating render streams, the region lists
     rebuilt on the GPU every `interval` renders while the previous frame is
     still in flight on the other stream (per-stream retire events).  The band
-    set of frames 1, 7, 20 and 24 equals the rows of the oracle's frame."""
+    set of frames 1, 7, 20 and 24 equals the rows of the oracle's frame.
+    partition="rows": the rank's contiguous row range instead, balanced for
+    the first frame's camera and kept for the others."""
     import sys
     sys.path.insert(0, ROOT)
     import volumetricrenderer_amd as vr
@@ -334,7 +387,7 @@ def test_native_solo_rank_spinning(oracle, render_streams, interval, threads, on
         r.set_march(vr.march_defaults())
         pl = RcclBandPipeline(r, W, H, 1, band_rows=16, world=world, rank=rank, loopback=True, solo=True,
                               render_streams=render_streams, host_threads=threads, exchange_on_render=on_render,
-                              compositor=compositor)
+                              compositor=compositor, partition=partition)
         stride, first = pl.band_stride, pl.band_first
         assert (stride, first) == ((world - 1, rank - 1) if compositor else (world, rank))
         got, done = {}, 0
@@ -351,7 +404,10 @@ def test_native_solo_rank_spinning(oracle, render_streams, interval, threads, on
     for i, img in got.items():
         obj, glob = vr.shader_data_arrays(*cams[i - 1])
         ref, _ = oracle.render(vol, obj, glob, oracle.from_params(vr.march_defaults()), W, H, 1)
-        want = band_set_of(ref, first, stride, 16)[..., 0]
+        if partition == "rows":
+            want = ref[pl.row_range[0]:pl.row_range[0] + pl.row_range[1], :, 0]
+        else:
+            want = band_set_of(ref, first, stride, 16)[..., 0]
         assert img.shape == want.shape and np.array_equal(img.cpu().numpy(), want), i
 
 

@@ -1820,3 +1820,62 @@ def test_bands_in_place_and_partial_assembly(oracle, vol128, fmt):
                   ctypes.c_void_p(frame.data_ptr()), None)
         torch.cuda.synchronize()
         assert np.array_equal(frame.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("fmt", [0, 1, 3])
+def test_row_ranges_match_the_frame(oracle, vol128, fmt):
+    """VR_TARGET_ROW_RANGE (vr.h): contiguous row ranges -- the multi-GPU
+    loop's balanced partition (vr_shard_balance_rows) -- packed or in place,
+    equal the whole frame's rows bit for bit; ranges run past the frame's
+    last row without writing there, and a range's first row must be a
+    multiple of 8.  vr_row_partition's ranges tile the frame, its boundaries
+    are multiples of 8, and the executed steps of the ranges are balanced
+    (each within 35 % of the mean: 8-row granules of a 203-row frame)."""
+    import ctypes
+    from volumetricrenderer_amd import _lib
+    W, H = 333, 203
+    with vr.Renderer(0) as rr:
+        rr.set_volume(vol128)
+        rr.set_shader_data(*vr.reference_shader_data(W / H, 25.0, 15.0))
+        rr.set_march(vr.march_defaults())
+        full = rr.render(W, H, fmt)
+        sc = torch.zeros(1, dtype=torch.int64, device="cuda")
+        rr.render(W, H, fmt, step_counter=sc)
+        want = full.cpu().numpy()
+        for first, n in ((0, 8), (0, 64), (40, 57), (96, 107), (200, 64), (8, 1)):
+            got = rr.render_rows(W, H, fmt, first, n)
+            torch.cuda.synchronize()
+            assert np.array_equal(got.cpu().numpy(), want[first:first + n]), (first, n)
+        # in place: every range of a partition into a prefilled frame
+        frame = rr.alloc_target(W, H, fmt)
+        frame.fill_(float("nan") if frame.dtype == torch.float32 else 0xAB)
+        rb = rr.row_partition(W, H, 5)
+        assert rb[0] == 0 and rb[-1] == H and all(b % 8 == 0 for b in rb[1:-1])
+        assert all(a <= b for a, b in zip(rb, rb[1:]))
+        for k in range(5):
+            if rb[k + 1] > rb[k]:
+                rr.render_rows(W, H, fmt, rb[k], rb[k + 1] - rb[k], out=frame, in_place=True)
+        torch.cuda.synchronize()
+        assert np.array_equal(frame.cpu().numpy(), want)
+        # the ranges' executed steps: balanced
+        steps = []
+        for k in range(5):
+            c = torch.zeros(1, dtype=torch.int64, device="cuda")
+            out = rr.alloc_target(W, max(1, rb[k + 1] - rb[k]), fmt)
+            t = _lib.Target(width=W, height=H, format=fmt | _lib.TARGET_ROW_RANGE, band_rows=max(1, rb[k + 1] - rb[k]),
+                            band_stride=1, band_first=rb[k], pixels=out.data_ptr(),
+                            row_pitch=out.stride(0) * out.element_size(), step_counter=c.data_ptr())
+            _lib.call("vr_render", rr._ctx, ctypes.byref(t), None)
+            torch.cuda.synchronize()
+            steps.append(int(c.item()))
+        assert sum(steps) == int(sc.item())
+        mean = sum(steps) / 5
+        assert max(abs(s - mean) for s in steps) <= 0.35 * mean, (rb, steps)
+        for bad in ((4, 16, 1), (0, 16, 2), (0, 0, 1)):   # first not a multiple of 8, stride, no rows
+            t = _lib.Target(width=W, height=H, format=fmt | _lib.TARGET_ROW_RANGE, band_rows=bad[1],
+                            band_stride=bad[2], band_first=bad[0], pixels=full.data_ptr(),
+                            row_pitch=full.stride(0) * full.element_size(), step_counter=None)
+            with pytest.raises(vr.VRError):
+                _lib.call("vr_render", rr._ctx, ctypes.byref(t), None)
+        with pytest.raises(vr.VRError):
+            rr.row_partition(W, H, 0)

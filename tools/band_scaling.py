@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--ns", default="1,2,4,8")
     ap.add_argument("--band-rows", type=int, default=16)
     ap.add_argument("--all-ranks", action="store_true", help="time every rank's band set, report the slowest")
+    ap.add_argument("--rank", type=int, default=0, help="--native without --all-ranks: the rank to rehearse")
     ap.add_argument("--native", action="store_true", help="per-rank frame streams through the native loop (solo)")
     ap.add_argument("--streams", default="1,2", help="--native: render streams to compare")
     ap.add_argument("--rounds", type=int, default=3, help="--native: interleaved rounds")
@@ -42,6 +43,8 @@ def main():
     ap.add_argument("--compositor", default="auto", choices=["auto", "on", "off"],
                     help="--native: rank 0 renders no bands and only assembles (vr_shard_set_compositor; auto: the "
                          "library's default, on from 8 ranks)")
+    ap.add_argument("--partition", default="auto", choices=["auto", "bands", "rows"],
+                    help="--native: interleaved band sets or balanced contiguous row ranges (RcclBandPipeline)")
     ap.add_argument("--exchange", default="render", choices=["render", "comm"],
                     help="--native: the exchange on the render streams (default) or on a communication stream "
                          "(vr_shard_set_exchange_streams 1 / 0)")
@@ -111,7 +114,7 @@ def native(a):
             k, v = o.split("=")
             r.set_option(k, int(v))
         print(f"native frame streams: {a.size}^3, {W}x{H}x{a.steps}, {a.frames} frames per timing, "
-              f"{a.threads} host thread(s), gate {a.gate_ms} ms, exchange on {a.exchange} "
+              f"{a.threads} host thread(s), gate {a.gate_ms} ms, partition {a.partition}, exchange on {a.exchange} "
               "streams, "
               f"variant {r.kernel_variant} {' '.join(a.opt)}", flush=True)
         streams = [int(v) for v in a.streams.split(",")]
@@ -125,12 +128,13 @@ def native(a):
             # the N-process run; pipelines of all ranks alive at once would
             # share queues and serialise each other's render streams
             per_round = {ns: [[] for _ in range(a.rounds)] for ns in streams}
-            for first in (range(n) if a.all_ranks else (0,)):
+            for first in (range(n) if a.all_ranks else (min(a.rank, n - 1),)):
                 for ns in streams:
                     p = RcclBandPipeline(r, W, H, vr.FMT_RGBA8_UNORM, band_rows=a.band_rows, world=n, rank=first,
                                          loopback=True, solo=True, render_streams=ns, host_threads=a.threads,
                                          exchange_on_render=a.exchange == "render",
-                                         compositor=None if a.compositor == "auto" else a.compositor == "on")
+                                         compositor=None if a.compositor == "auto" else a.compositor == "on",
+                                         partition=a.partition)
                     p.run_frames(8)   # region lists, code objects
                     p.barrier()
                     for k in range(a.rounds):

@@ -40,6 +40,7 @@ GREY_OF = {FMT_RGBA32F: FMT_R32F, FMT_RGBA8_UNORM: FMT_R8_UNORM, FMT_RGBA8_SRGB:
 FLOAT_FORMATS = (FMT_RGBA32F, FMT_R32F)
 # OR'ed into a target's format: bands written at their frame rows (include/vr.h)
 TARGET_BANDS_IN_PLACE = 0x100
+TARGET_ROW_RANGE = 0x200   # vr.h VR_TARGET_ROW_RANGE
 
 c_float_p = ctypes.POINTER(ctypes.c_float)
 c_int_p = ctypes.POINTER(ctypes.c_int)
@@ -133,6 +134,7 @@ _SIGS = {
     "vr_assemble_frame_ranks": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
                                                ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, _vp]),
     "vr_band_rows_packed": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "vr_row_partition": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_int_p]),
     "vr_kernel_variant": (ctypes.c_char_p, [_vp]),
     "vr_set_layout_preference": (ctypes.c_int, [_vp, ctypes.c_int]),
     "vr_set_option": (ctypes.c_int, [_vp, ctypes.c_char_p, ctypes.c_int]),
@@ -222,11 +224,15 @@ _SHARD_SIGS = {
     "vr_shard_set_compositor": (ctypes.c_int, [_vp, ctypes.c_int]),
     "vr_shard_get_compositor": (ctypes.c_int, [_vp]),
     "vr_shard_bands": (ctypes.c_int, [_vp, c_int_p, c_int_p]),
+    "vr_shard_set_rows": (ctypes.c_int, [_vp, c_int_p]),
+    "vr_shard_balance_rows": (ctypes.c_int, [_vp]),
+    "vr_shard_partition": (ctypes.c_int, [_vp]),
+    "vr_shard_row_range": (ctypes.c_int, [_vp, ctypes.c_int, c_int_p, c_int_p]),
     "vr_shard_poll_selftest": (ctypes.c_int, [ctypes.c_int, ctypes.c_double, c_int_p]),
 }
 # shard functions whose int return is a value, not a vr_status
 _SHARD_VALUE_RETURNS = {"vr_shard_aborted", "vr_shard_poll_selftest", "vr_shard_get_render_streams",
-                        "vr_shard_get_compositor"}
+                        "vr_shard_get_compositor", "vr_shard_partition"}
 _shard_lib = None
 
 

@@ -257,6 +257,9 @@ struct Ctx {
     int launch_cache = 1;
     int empty_fill = 1;          // option "empty_fill": regions launches fill the lists' empty tiles, not march them
     int frames_overlap = 0;      // option "frames_overlap": consecutive renders overlap (auto split rule)
+    // vr_row_partition's work model: a ray costs steps^(row_pow / 100) + row_setup
+    int row_setup = 40, row_pow = 130;   // config 4 at 8 ranks, profiles/r05/row_ranges_c4.txt
+    int row_first_pct = 100;     // range 0's share of the work, % of the mean (the loop's rank 0 also assembles)
     struct Cached {
         bool valid = false;
         unsigned long long gen = 0;
@@ -955,6 +958,70 @@ try {
     return -1;
 }
 
+// Balanced contiguous row ranges (vr.h; the multi-GPU loop's row partition,
+// DESIGN.md sec. 7.3).  Work of an 8-row strip: over the rays through pixel
+// (8i + 4, 8s + 4), the a3 step count of the box chord (frag.glsl:42-46, as
+// the region build's estimate: double, no clip test) plus kRaySetup for a ray
+// that meets the box, kRayMiss for one that does not.  Boundary k is the strip
+// edge nearest to the k/parts quantile of the prefix sums.
+vr_status vr_row_partition(void* p, int width, int height, int parts, int* row_begin)
+try {
+    if (!p || !row_begin) return fail(VR_ERR_INVALID, "vr_row_partition: null argument");
+    if (width <= 0 || height <= 0 || parts <= 0 || parts > 4096)
+        return fail(VR_ERR_INVALID, "vr_row_partition: bad frame %dx%d or parts %d", width, height, parts);
+    Ctx* c = as_ctx(p);
+    if (!c->has_camera) return fail(VR_ERR_NO_CAMERA, "vr_row_partition: no shader data (vr_set_shader_data)");
+    RayBasis b;
+    if (!make_ray_basis(c->obj, c->glob, width, height, &b))
+        return fail(VR_ERR_INVALID, "vr_row_partition: Projection*View is singular");
+    const double kRaySetup = (double)c->row_setup, kRayMiss = 2.0, pw = c->row_pow / 100.0;
+    const vr_march_params& m = c->march;
+    const double step = (1.0 / (double)m.max_steps) * (double)m.step_scale;
+    const int ns = (height + 7) / 8;
+    std::vector<double> prefix((size_t)ns + 1, 0.0);
+    for (int s = 0; s < ns; ++s) {
+        const double fy = std::min(8.0 * s + 4.0, height - 0.5);
+        double w = 0.0;
+        for (int x = 4; x < width + 4; x += 8) {
+            const double fx = std::min((double)x, width - 0.5);
+            double d[3], len = 0.0;
+            for (int k = 0; k < 3; ++k) {
+                d[k] = (double)b.o[k] + fx * (double)b.px[k] + fy * (double)b.py[k];
+                len += d[k] * d[k];
+            }
+            len = std::sqrt(len);
+            double tn = -INFINITY, tf = INFINITY;
+            for (int k = 0; k < 3; ++k) {
+                const double ta = ((double)m.box_min[k] - (double)b.org[k]) * len / d[k];
+                const double tb = ((double)m.box_max[k] - (double)b.org[k]) * len / d[k];
+                tn = std::max(tn, std::min(ta, tb));
+                tf = std::min(tf, std::max(ta, tb));
+            }
+            const bool hit = tn <= tf && std::isfinite(tf) && tf > 0.0;
+            w += hit ? std::pow(std::min((double)m.max_steps, (tf - std::max(tn, 0.0)) / step), pw) + kRaySetup
+                     : kRayMiss;
+        }
+        prefix[(size_t)s + 1] = prefix[(size_t)s] + w;
+    }
+    const double total = prefix[(size_t)ns];
+    row_begin[0] = 0;
+    int j = 0;
+    // range 0 takes f of a mean share, the others equal shares of the rest
+    const double f = parts > 1 ? c->row_first_pct / 100.0 : 1.0, g = parts > 1 ? (parts - f) / (parts - 1) : 1.0;
+    for (int k = 1; k < parts; ++k) {
+        const double target = total * (f + (k - 1) * g) / parts;
+        while (j < ns && prefix[(size_t)j + 1] < target) ++j;
+        // strip edge j or j + 1, whichever prefix is nearer the quantile
+        int e = j;
+        if (j < ns && prefix[(size_t)j + 1] - target < target - prefix[(size_t)j]) e = j + 1;
+        row_begin[k] = std::max(row_begin[k - 1], std::min(8 * e, height));
+    }
+    row_begin[parts] = height;
+    return VR_OK;
+} catch (...) {
+    return caught_exception("vr_row_partition");
+}
+
 vr_status vr_set_layout_preference(void* p, int pref)
 try {
     if (!p || pref < 0 || pref >= kNumLayouts) return fail(VR_ERR_INVALID, "vr_set_layout_preference: bad argument");
@@ -992,6 +1059,12 @@ try {
     if (n == "launch_cache") {
         if (value < 0 || value > 1) return fail(VR_ERR_INVALID, "vr_set_option: launch_cache is 0 or 1");
         c->launch_cache = value;
+        return VR_OK;
+    }
+    if (n == "row_setup" || n == "row_pow" || n == "row_first_pct") {   // vr_row_partition's work model
+        if (value < 0 || value > 1000 || (n == "row_pow" && value < 50) || (n == "row_first_pct" && value > 100))
+            return fail(VR_ERR_INVALID, "vr_set_option: %s out of range", n.c_str());
+        (n == "row_setup" ? c->row_setup : n == "row_pow" ? c->row_pow : c->row_first_pct) = value;
         return VR_OK;
     }
     if (n == "frames_overlap") {   // the caller overlaps consecutive frames on two streams (auto split)
@@ -1194,6 +1267,9 @@ try {
     if (n == "launch_cache") return c->launch_cache;
     if (n == "empty_fill") return c->empty_fill;
     if (n == "frames_overlap") return c->frames_overlap;
+    if (n == "row_setup") return c->row_setup;
+    if (n == "row_pow") return c->row_pow;
+    if (n == "row_first_pct") return c->row_first_pct;
     if (n == "launch_cache_hits") return (int)std::min<long long>(c->lc_hits, 0x7fffffff);
     if (n == "experiments") return VR_EXPERIMENTS;   // read-only: the measured-slower variants are built
     if (n == "region_interval") return c->region_interval;
@@ -1279,7 +1355,7 @@ void box_centre_pixel(const Ctx* c, const MarchArgs& a, int* px, int* prow)
     }
     const int y = (int)std::min(std::max(sy, 0.0), (double)(a.height - 1));
     int row = y;
-    if (a.band_rows > 0 && a.band_stride > 1) {   // the nearest of this rank's packed rows
+    if (a.band_rows > 0 && (a.band_stride > 1 || a.band_first > 0)) {   // the nearest of this rank's packed rows
         const int b = y / a.band_rows;
         const int sel = b >= a.band_first ? (b - a.band_first) / a.band_stride : 0;
         row = sel * a.band_rows + y % a.band_rows;
@@ -1944,8 +2020,9 @@ try {
         return fail(VR_ERR_NO_VOLUME, "vr_render: no volume (vr_set_volume / vr_generate_volume)");
     if (!c->has_camera) return fail(VR_ERR_NO_CAMERA, "vr_render: no shader data (vr_set_shader_data)");
     if (t->width <= 0 || t->height <= 0) return fail(VR_ERR_INVALID, "vr_render: bad size %dx%d", t->width, t->height);
-    const int tfmt = t->format & ~VR_TARGET_BANDS_IN_PLACE;
+    const int tfmt = t->format & ~(VR_TARGET_BANDS_IN_PLACE | VR_TARGET_ROW_RANGE);
     const bool in_place = (t->format & VR_TARGET_BANDS_IN_PLACE) != 0;
+    const bool row_range = (t->format & VR_TARGET_ROW_RANGE) != 0;
     if (tfmt < 0 || tfmt > 5) return fail(VR_ERR_INVALID, "vr_render: bad format %d", t->format);
     if (!t->pixels) return fail(VR_ERR_INVALID, "vr_render: pixels is null");
     const int bpp = format_bytes(tfmt);
@@ -1954,6 +2031,9 @@ try {
         return fail(VR_ERR_INVALID, "vr_render: pitch/alignment (pitch %zu, bpp %d)", pitch, bpp);
     if (t->band_rows < 0 || (t->band_rows > 0 && (t->band_stride <= 0 || t->band_first < 0)))
         return fail(VR_ERR_INVALID, "vr_render: bad band selection");
+    if (row_range && (t->band_rows <= 0 || t->band_stride != 1 || t->band_first % 8 != 0))
+        return fail(VR_ERR_INVALID, "vr_render: bad row range (rows %d, stride %d, first row %d: need rows > 0, "
+                    "stride 1, first a multiple of 8)", t->band_rows, t->band_stride, t->band_first);
 
     if (c->inject_throw) {
         const int k = c->inject_throw;
@@ -2050,19 +2130,24 @@ try {
     }
     a.width = t->width;
     a.height = t->height;
-    if (t->band_rows > 0) {
+    if (row_range) {
+        // rows [first, first + n) = the 8-row bands from first / 8 on, cut at n
+        // rows: the kernels' band-row mapping as it is
+        a.band_rows = 8; a.band_stride = 1; a.band_first = t->band_first / 8;
+    } else if (t->band_rows > 0) {
         a.band_rows = t->band_rows; a.band_stride = t->band_stride; a.band_first = t->band_first;
     } else {
         a.band_rows = t->height; a.band_stride = 1; a.band_first = 0;
     }
     a.out_rows = band_rows_packed(t->height, a.band_rows, a.band_stride, a.band_first);
+    if (row_range) a.out_rows = std::min(a.out_rows, t->band_rows);
     a.tiles_x = (t->width + 15) / 16;
     a.tiles_y = (a.out_rows + 15) / 16;
     a.num_blocks = 8 * ((a.tiles_y + 7) / 8) * a.tiles_x;
     a.out = t->pixels;
     a.pitch = (long long)pitch;
     a.format = tfmt;
-    a.bands_in_place = in_place && t->band_rows > 0 ? 1 : 0;
+    a.bands_in_place = in_place && (t->band_rows > 0 || row_range) ? 1 : 0;
     a.empty_fill = 0;   // set with the schedule (regions, default kernels)
     a.step_counter = reinterpret_cast<unsigned long long*>(t->step_counter);
     HIP_TRY(hipSetDevice(c->device));

@@ -159,6 +159,10 @@ struct vr_shard {
     // assembles; ranks 1..N-1 render the band sets of a world of N-1 renderers
     // (rank r: band_first r - 1), received into gather slot r - 1
     bool compositor = false;
+    // balanced row ranges (vr_shard_set_rows / vr_shard_balance_rows): renderer
+    // k renders frame rows [row_begin[k], row_begin[k + 1]) (VR_TARGET_ROW_RANGE)
+    // and rank 0 gathers them into a grey frame; empty = interleaved band sets
+    std::vector<int> row_begin;
     bool started = false;             // a run has queued frames (the geometry is fixed)
     ncclComm_t comm = nullptr;
     hipStream_t comm_stream = nullptr;
@@ -316,13 +320,50 @@ bool others_here(const vr_shard* sh) { return sh->loopback && !sh->solo; }
 // Band geometry: renderers, a rank's band set (stride, first) and its gather slot.
 int renderers(const vr_shard* sh) { return sh->compositor ? sh->nranks - 1 : sh->nranks; }
 int band_first_of(const vr_shard* sh, int r) { return sh->compositor ? r - 1 : r; }
+bool rows_mode(const vr_shard* sh) { return !sh->row_begin.empty(); }
+// rank 0's gather buffer: a slot of rows_per_rank rows per rank, or (row
+// ranges) a grey frame that every renderer's range lands in at its own rows
+size_t gather_rows(const vr_shard* sh)
+{
+    return rows_mode(sh) ? (size_t)sh->height : (size_t)sh->nranks * sh->rows_per_rank;
+}
 uint8_t* slot_of(const vr_shard* sh, int p, int r)
 {
+    if (rows_mode(sh)) return sh->gathered[p] + (size_t)sh->row_begin[band_first_of(sh, r)] * sh->gpitch;
     return sh->gathered[p] + (size_t)band_first_of(sh, r) * sh->rows_per_rank * sh->gpitch;
 }
+// rank r's render target: its band set or its row range (format and buffer set by the caller)
+vr_target target_of(const vr_shard* sh, int r)
+{
+    vr_target t{};
+    t.width = sh->width;
+    t.height = sh->height;
+    if (rows_mode(sh)) {
+        const int k = band_first_of(sh, r);
+        if (k < 0) return t;   // the compositor renders nothing
+        t.band_rows = sh->row_begin[k + 1] - sh->row_begin[k];
+        t.band_stride = 1;
+        t.band_first = sh->row_begin[k];
+    } else {
+        t.band_rows = sh->band_rows;
+        t.band_stride = renderers(sh);
+        t.band_first = band_first_of(sh, r);
+    }
+    return t;
+}
+int range_flag(const vr_shard* sh) { return rows_mode(sh) ? VR_TARGET_ROW_RANGE : 0; }
 // the assembly: every renderer's rows, or (rank 0 rendering in place) all but rank 0's
 vr_status assemble(vr_shard* sh, int p, hipStream_t s)
 {
+    if (rows_mode(sh)) {   // the other ranks' ranges are contiguous: one expansion of the rows below rank 0's
+        const int start = sh->compositor ? 0 : sh->row_begin[1];
+        const int n = sh->height - start;
+        if (n > 0)
+            VR_TRY(vr_assemble_frame_ranks(sh->ctx, sh->gathered[p] + (size_t)start * sh->gpitch, sh->gformat, (size_t)n,
+                                           1, 0, sh->width, n, n, sh->format, sh->frame[p] + (size_t)start * sh->pitch,
+                                           s));
+        return VR_OK;
+    }
     VR_TRY(vr_assemble_frame_ranks(sh->ctx, sh->gathered[p], sh->gformat, (size_t)sh->rows_per_rank, renderers(sh),
                                    sh->compositor ? 0 : 1, sh->width, sh->height, sh->band_rows, sh->format,
                                    sh->frame[p], s));
@@ -336,18 +377,13 @@ vr_status render_half(vr_shard* sh, int p, hipStream_t s, hipEvent_t t0, hipEven
 {
     const bool r0 = sh->rank == 0, here = others_here(sh);
     if ((!r0 || here) && sh->pending[p]) HIP_TRY(hipStreamWaitEvent(s, sh->done[p], 0));
-    vr_target t{};
-    t.width = sh->width;
-    t.height = sh->height;
-    t.band_rows = sh->band_rows;
-    t.band_stride = renderers(sh);
-    t.band_first = band_first_of(sh, sh->rank);
+    vr_target t = target_of(sh, sh->rank);
     if (r0) {   // in place: the frame's own rows, the frame's format
-        t.format = sh->format | VR_TARGET_BANDS_IN_PLACE;
+        t.format = sh->format | VR_TARGET_BANDS_IN_PLACE | range_flag(sh);
         t.pixels = sh->frame[p];
         t.row_pitch = sh->pitch;
     } else {
-        t.format = sh->gformat;
+        t.format = sh->gformat | range_flag(sh);
         t.pixels = sh->local[p];
         t.row_pitch = sh->gpitch;
     }
@@ -355,10 +391,10 @@ vr_status render_half(vr_shard* sh, int p, hipStream_t s, hipEvent_t t0, hipEven
     if (sh->my_rows > 0) VR_TRY(vr_render(sh->ctx, &t, s));
     if (t1) HIP_TRY(hipEventRecord(t1, s));
     if (here) {   // the other ranks' band sets, rendered here into their gather slots
-        t.format = sh->gformat;
-        t.row_pitch = sh->gpitch;
         for (int r = 1; r < sh->nranks; ++r) {
-            t.band_first = band_first_of(sh, r);
+            t = target_of(sh, r);
+            t.format = sh->gformat | range_flag(sh);
+            t.row_pitch = sh->gpitch;
             t.pixels = slot_of(sh, p, r);
             if (sh->rows_of[r] > 0) VR_TRY(vr_render(sh->ctx, &t, s));
         }
@@ -416,18 +452,13 @@ vr_status one_frame(vr_shard* sh, int p, hipStream_t s, hipEvent_t t0, hipEvent_
 vr_status one_frame_on_render(vr_shard* sh, int p, hipStream_t rs, hipEvent_t t0, hipEvent_t t1)
 {
     const bool r0 = sh->rank == 0, here = others_here(sh);
-    vr_target t{};
-    t.width = sh->width;
-    t.height = sh->height;
-    t.band_rows = sh->band_rows;
-    t.band_stride = renderers(sh);
-    t.band_first = band_first_of(sh, sh->rank);
+    vr_target t = target_of(sh, sh->rank);
     if (r0) {
-        t.format = sh->format | VR_TARGET_BANDS_IN_PLACE;
+        t.format = sh->format | VR_TARGET_BANDS_IN_PLACE | range_flag(sh);
         t.pixels = sh->frame[p];
         t.row_pitch = sh->pitch;
     } else {
-        t.format = sh->gformat;
+        t.format = sh->gformat | range_flag(sh);
         t.pixels = sh->local[p];
         t.row_pitch = sh->gpitch;
     }
@@ -435,10 +466,10 @@ vr_status one_frame_on_render(vr_shard* sh, int p, hipStream_t rs, hipEvent_t t0
     if (sh->my_rows > 0) VR_TRY(vr_render(sh->ctx, &t, rs));
     if (t1) HIP_TRY(hipEventRecord(t1, rs));
     if (here) {
-        t.format = sh->gformat;
-        t.row_pitch = sh->gpitch;
         for (int r = 1; r < sh->nranks; ++r) {
-            t.band_first = band_first_of(sh, r);
+            t = target_of(sh, r);
+            t.format = sh->gformat | range_flag(sh);
+            t.row_pitch = sh->gpitch;
             t.pixels = slot_of(sh, p, r);
             if (sh->rows_of[r] > 0) VR_TRY(vr_render(sh->ctx, &t, rs));
         }
@@ -474,13 +505,18 @@ void set_geometry(vr_shard* sh, bool compositor)
 {
     sh->compositor = compositor && sh->nranks >= 2;
     const int R = renderers(sh);
+    if ((int)sh->row_begin.size() != R + 1) sh->row_begin.clear();   // ranges of another renderer count
     sh->rows_of.assign(sh->nranks, 0);
     for (int r = 0; r < sh->nranks; ++r)
-        if (!sh->compositor || r > 0)
-            sh->rows_of[r] = vr_band_rows_packed(sh->height, sh->band_rows, R, band_first_of(sh, r));
+        if (!sh->compositor || r > 0) {
+            const int k = band_first_of(sh, r);
+            sh->rows_of[r] = rows_mode(sh) ? sh->row_begin[k + 1] - sh->row_begin[k]
+                                           : vr_band_rows_packed(sh->height, sh->band_rows, R, k);
+        }
     sh->my_rows = sh->rows_of[sh->rank];
-    // band 0 is the first renderer's: it has the most rows
-    sh->rows_per_rank = vr_band_rows_packed(sh->height, sh->band_rows, R, 0);
+    // band 0 is the first renderer's: it has the most rows (ranges: the longest)
+    sh->rows_per_rank = rows_mode(sh) ? *std::max_element(sh->rows_of.begin(), sh->rows_of.end())
+                                      : vr_band_rows_packed(sh->height, sh->band_rows, R, 0);
 }
 
 // rank 0's gather slots / another rank's band sets, for the current geometry
@@ -490,7 +526,7 @@ vr_status alloc_band_buffers(vr_shard* sh)
         uint8_t*& b = sh->rank == 0 ? sh->gathered[p] : sh->local[p];
         if (b) (void)hipFree(b);
         b = nullptr;
-        const size_t bytes = sh->rank == 0 ? (size_t)sh->nranks * sh->rows_per_rank * sh->gpitch
+        const size_t bytes = sh->rank == 0 ? gather_rows(sh) * sh->gpitch
                                            : (size_t)std::max(sh->my_rows, 1) * sh->gpitch;
         const hipError_t e = hipMalloc(&b, std::max(bytes, (size_t)1));
         if (e != hipSuccess) {
@@ -1092,6 +1128,108 @@ try {
     return VR_OK;
 } catch (...) {
     return caught_exception("vr_shard_bands");
+}
+
+vr_status vr_shard_set_rows(vr_shard* sh, const int* row_begin)
+try {
+    if (!sh) return fail(VR_ERR_INVALID, "vr_shard_set_rows: null");
+    const int R = renderers(sh);
+    std::vector<int> rb;
+    if (row_begin) {
+        rb.assign(row_begin, row_begin + R + 1);
+        bool ok = rb[0] == 0 && rb[R] == sh->height;
+        for (int k = 1; k <= R && ok; ++k) ok = rb[k] >= rb[k - 1] && (rb[k] % 8 == 0 || rb[k] == sh->height);
+        if (!ok) return fail(VR_ERR_INVALID, "vr_shard_set_rows: need %d + 1 non-decreasing row starts from 0 to %d, "
+                             "multiples of 8", R, sh->height);
+    }
+    if (rb == sh->row_begin) return VR_OK;
+    if (sh->started) return fail(VR_ERR_INVALID, "vr_shard_set_rows: set before the first frames");
+    sh->row_begin = rb;
+    set_geometry(sh, sh->compositor);
+    return alloc_band_buffers(sh);
+} catch (...) {
+    return caught_exception("vr_shard_set_rows");
+}
+
+// Rank 0's vr_row_partition, on every rank: broadcast with a failure flag
+// (a rank-0 failure reaches every rank after the one collective, not a hang).
+vr_status vr_shard_balance_rows(vr_shard* sh)
+try {
+    if (!sh) return fail(VR_ERR_INVALID, "vr_shard_balance_rows: null");
+    if (sh->loopback && sh->rank != 0 && !sh->solo)
+        return fail(VR_ERR_INVALID, "vr_shard_balance_rows: rank %d is not connected (vr_shard_connect)", sh->rank);
+    SH_TRY(check_usable(sh, "vr_shard_balance_rows"));
+    const int R = renderers(sh);
+    std::vector<int> rb((size_t)R + 2, 0);   // [0]: failed, [1..R+1]: row starts
+    vr_status mine = VR_OK;
+    std::string msg;
+    if (sh->rank == 0 || sh->loopback) {
+        // rank 0 rendering in place also expands the other (N-1)/N of the
+        // frame: its range takes 2 % less than a mean share per other rank
+        // (config 4: 0.0461 ms per frame at 8 ranks with 85 %, 0.0491 with
+        // 100 %; profiles/r05/row_ranges_c4.txt)
+        const int prev = vr_get_option(sh->ctx, "row_first_pct");
+        const int pct = sh->compositor ? 100 : std::max(50, 100 - 2 * (sh->nranks - 1));
+        (void)vr_set_option(sh->ctx, "row_first_pct", pct);
+        mine = vr_row_partition(sh->ctx, sh->width, sh->height, R, rb.data() + 1);
+        (void)vr_set_option(sh->ctx, "row_first_pct", prev);
+        if (mine != VR_OK) {
+            msg = vr_last_error();
+            rb[0] = 1;
+        }
+    }
+    if (sh->nranks > 1 && !sh->loopback) {
+        HIP_TRY(hipSetDevice(sh->device));
+        int* d = nullptr;
+        HIP_TRY(hipMalloc(&d, rb.size() * sizeof(int)));
+        hipError_t he = hipMemcpyAsync(d, rb.data(), rb.size() * sizeof(int), hipMemcpyHostToDevice, sh->comm_stream);
+        vr_status st = VR_OK;
+        ncclResult_t nr = ncclSuccess;
+        if (he == hipSuccess) {
+            nr = ncclBroadcast(d, d, rb.size(), ncclInt32, 0, sh->comm, sh->comm_stream);
+            if (nr == ncclInProgress) {
+                st = settle(sh, "vr_shard_balance_rows: broadcast");
+                nr = ncclSuccess;
+            }
+        }
+        if (he == hipSuccess && nr == ncclSuccess && st == VR_OK)
+            he = hipMemcpyAsync(rb.data(), d, rb.size() * sizeof(int), hipMemcpyDeviceToHost, sh->comm_stream);
+        if (he == hipSuccess && nr == ncclSuccess && st == VR_OK)
+            st = wait_stream(sh, sh->comm_stream, "vr_shard_balance_rows: broadcast");
+        if (!sh->aborted) (void)hipFree(d);
+        if (st != VR_OK) return st;
+        if (nr != ncclSuccess) {
+            abort_comm(sh);
+            return fail(VR_ERR_COMM, "vr_shard_balance_rows: ncclBroadcast: %s", ncclGetErrorString(nr));
+        }
+        if (he != hipSuccess) return fail(VR_ERR_HIP, "vr_shard_balance_rows: %s", hipGetErrorString(he));
+    }
+    if (rb[0]) {
+        if (mine != VR_OK) return fail(mine, "vr_shard_balance_rows: vr_row_partition: %s", msg.c_str());
+        return fail(VR_ERR_INVALID, "vr_shard_balance_rows: rank 0's partition failed");
+    }
+    return vr_shard_set_rows(sh, rb.data() + 1);
+} catch (...) {
+    return caught_exception("vr_shard_balance_rows");
+}
+
+int vr_shard_partition(vr_shard* sh)
+try {
+    return sh ? (rows_mode(sh) ? 1 : 0) : -1;
+} catch (...) {
+    return -1;
+}
+
+vr_status vr_shard_row_range(vr_shard* sh, int rank, int* row_first, int* rows)
+try {
+    if (!sh || rank < 0 || rank >= sh->nranks) return fail(VR_ERR_INVALID, "vr_shard_row_range: bad argument");
+    if (!rows_mode(sh)) return fail(VR_ERR_INVALID, "vr_shard_row_range: the shard renders band sets (vr_shard_set_rows)");
+    const int k = band_first_of(sh, rank);
+    if (row_first) *row_first = k < 0 ? 0 : sh->row_begin[k];
+    if (rows) *rows = k < 0 ? 0 : sh->row_begin[k + 1] - sh->row_begin[k];
+    return VR_OK;
+} catch (...) {
+    return caught_exception("vr_shard_row_range");
 }
 
 vr_status vr_shard_rows(vr_shard* sh, int* my_rows, int* rows_per_rank)

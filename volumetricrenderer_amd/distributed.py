@@ -286,7 +286,7 @@ class RcclBandPipeline:
     def __init__(self, renderer, width: int, height: int, fmt: int, band_rows: int = 16, world: int = 1,
                  rank: int = 0, group=None, loopback: bool = False, timeout_s: float | None = None,
                  render_streams: int = 2, solo: bool = False, host_threads: int = 1, exchange_on_render: bool = True,
-                 compositor: bool | None = None):
+                 compositor: bool | None = None, partition: str = "auto"):
         """loopback: one process renders all `world` ranks' band sets on its
         GPU and assembles them (no communicator; tests and rehearsals).
         solo (loopback only, any rank): each frame renders only this rank's
@@ -300,6 +300,13 @@ class RcclBandPipeline:
         compositor: rank 0 renders no bands and only assembles, ranks 1..N-1
         render the band sets of N-1 renderers (vr_shard_set_compositor; None =
         the library's default: on from 8 ranks; every rank the same).
+        partition: "bands" = interleaved band sets of `band_rows` rows (stride
+        = the renderers); "rows" = contiguous row ranges of equal estimated
+        work for the camera set at the first run_frames (vr_shard_balance_rows,
+        collective); "auto" (default) = "rows" from 8 ranks on for frames of
+        more than 2560 x 1440 pixels (config 4 at 8 ranks: 0.0480 ms per frame
+        against 0.0562 with 16-row bands; equal or slightly slower at 2 and 4
+        ranks), else "bands".
         exchange_on_render: True (default) = each frame's exchange follows its
         render on the frame's render stream, over a communicator per buffer
         parity, with no events; False = on a communication stream, ordered by
@@ -375,6 +382,15 @@ class RcclBandPipeline:
                 _lib.shard_call("vr_shard_destroy", h)
                 raise
         self._h = h
+        if partition not in ("auto", "bands", "rows"):
+            raise ValueError(f"RcclBandPipeline: partition {partition!r}: 'auto', 'bands' or 'rows'")
+        self.partition = (("rows" if world >= 8 and width * height > 2560 * 1440 else "bands") if partition == "auto"
+                          else partition)
+        self._balanced = self.partition == "bands"
+        self._geometry()
+
+    def _geometry(self) -> None:
+        h = self._h
         mine, per = ctypes.c_int(), ctypes.c_int()
         _lib.shard_call("vr_shard_rows", h, ctypes.byref(mine), ctypes.byref(per))
         self.my_rows, self.rows_per_rank = mine.value, per.value
@@ -382,6 +398,19 @@ class RcclBandPipeline:
         _lib.shard_call("vr_shard_bands", h, ctypes.byref(stride), ctypes.byref(first))
         self.band_stride, self.band_first = stride.value, first.value   # this rank's band set (vr_render target)
         self.compositor = bool(_lib.shard_call("vr_shard_get_compositor", h))
+        self.row_range = None   # (first frame row, rows) of this rank with row ranges
+        if _lib.shard_call("vr_shard_partition", h) == 1:
+            r0, n = ctypes.c_int(), ctypes.c_int()
+            _lib.shard_call("vr_shard_row_range", h, self.rank, ctypes.byref(r0), ctypes.byref(n))
+            self.row_range = (r0.value, n.value)
+
+    def balance_rows(self) -> None:
+        """Collective: contiguous row ranges of equal estimated work for the
+        renderer's current camera (vr_shard_balance_rows: rank 0 computes,
+        every rank receives).  run_frames calls it once with partition="rows"."""
+        _lib.shard_call("vr_shard_balance_rows", self._h)
+        self._balanced = True
+        self._geometry()
 
     @property
     def render_streams(self) -> int:
@@ -409,6 +438,12 @@ class RcclBandPipeline:
         from .renderer import _stream_handle
         ms = ctypes.c_float()
         host = ctypes.c_double()
+        if cameras is not None:
+            cameras = list(cameras)
+        if not self._balanced and k > 0:
+            if cameras:   # the ranges follow the first frame's camera
+                self.r.set_shader_data(*cameras[0])
+            self.balance_rows()
         if cameras is None:
             _lib.shard_call("vr_shard_run_frames", self._h, k, None, None, _stream_handle(stream), sample_every,
                             ctypes.byref(ms) if sample_every > 0 else None, ctypes.byref(host))

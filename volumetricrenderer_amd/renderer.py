@@ -292,6 +292,29 @@ class Renderer:
         call("vr_render", self._ctx, ctypes.byref(t), _stream_handle(stream))
         return out
 
+    def render_rows(self, width: int, height: int, fmt: int, first_row: int, rows: int,
+                    out: torch.Tensor | None = None, in_place: bool = False, stream=None) -> torch.Tensor:
+        """Frame rows [first_row, first_row + rows) of the width x height frame
+        (vr.h VR_TARGET_ROW_RANGE; first_row a multiple of 8): packed from row
+        0 of `out`, or at their own rows of a whole-frame `out` (in_place)."""
+        n = max(0, min(rows, height - first_row))
+        if out is None:
+            out = self.alloc_target(width, height if in_place else n, fmt)
+        self._check_target(width, height if in_place else n, fmt, out, 0, 1, 0)
+        flags = _lib.TARGET_ROW_RANGE | (_lib.TARGET_BANDS_IN_PLACE if in_place else 0)
+        t = Target(width=width, height=height, format=fmt | flags, band_rows=rows, band_stride=1,
+                   band_first=first_row, pixels=out.data_ptr(), row_pitch=out.stride(0) * out.element_size(),
+                   step_counter=None)
+        call("vr_render", self._ctx, ctypes.byref(t), _stream_handle(stream))
+        return out
+
+    def row_partition(self, width: int, height: int, parts: int) -> list[int]:
+        """vr_row_partition: parts + 1 row starts of contiguous ranges of equal
+        estimated march work for the current camera."""
+        rb = (ctypes.c_int * (parts + 1))()
+        call("vr_row_partition", self._ctx, width, height, parts, rb)
+        return list(rb)
+
     def render_sequence(self, width: int, height: int, fmt: int, out: torch.Tensor, cameras, band_rows: int = 0,
                         band_stride: int = 1, band_first: int = 0, stream=None) -> torch.Tensor:
         """The reference's frame loop with a moving camera (TestMain.cpp:173-256):
