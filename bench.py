@@ -230,6 +230,24 @@ def other_config(name, steps, warmup):
         el = time.perf_counter() - t0
         kern_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev if e is not None]))
         variant = r.kernel_variant
+        # grid media: the same frames two in flight, as the headline's loop runs
+        # them -- consecutive frames alternate two streams and two targets
+        inflight2 = None
+        if proc is None:
+            streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+            outs = [out, r.alloc_target(W, H, fmt)]
+            launches = [r.prepare_render(W, H, fmt, outs[k], stream=streams[k]) for k in range(2)]
+            for i in range(warmup):
+                launches[i & 1]()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i in range(steps):
+                launches[i & 1]()
+            torch.cuda.synchronize()
+            el2 = time.perf_counter() - t0
+            inflight2 = {"ms_per_step": round(el2 / steps * 1e3, 4), "value": round(W * H * S * steps / el2 / 1e6, 3),
+                         "def": "the same frames, consecutive frames alternating two streams and two targets, wall "
+                                "time per frame"}
         defer = proc is not None and shadow > 0 and r.get_option("shadow_defer_last") == 1
         res = {"metric": f"Mray/s (= W*H*steps/s) at {W}x{H} x {S} steps",
                "value": round(W * H * S * steps / el / 1e6, 3), "unit": "Mray/s", "steps": steps,
@@ -240,7 +258,8 @@ def other_config(name, steps, warmup):
                           "baseline_config_index": cfg_idx,
                           "kernel": variant + ("_deferred" if defer else ""),
                           "executed_steps_per_frame": nsteps},
-               "roofline": roofline_of(r, proc, shadow, variant, nsteps, evals, cells, kern_ms)}
+               "roofline": roofline_of(r, proc, shadow, variant, nsteps, evals, cells, kern_ms),
+               **({"frames_in_flight_2": inflight2} if inflight2 else {})}
         if defer:
             res["shadow_defer_scratch_MB"] = round(r.get_option("shadow_defer_kib") / 1024.0, 1)
         vol = r.get_volume() if proc is None else None
@@ -257,7 +276,7 @@ def main() -> int:
     os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="grid512", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -273,6 +292,11 @@ def main() -> int:
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch sharder's backend; gloo: rehearse the N>1 path with several ranks on one GPU")
     ap.add_argument("--pipeline1", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--n1-loop", default="native", choices=["native", "sharder"],
+                    help="N = 1, grid media: native (default) = the frame loop of N > 1 (libvr_shard over a "
+                         "one-rank communicator: 2 render streams, 2 frames in flight as the reference keeps them, "
+                         "VulkanRenderer.cpp:13); sharder = one stream through BandSharder (rounds 1-5's N = 1 line, "
+                         "whose launches do not overlap; always for a procedural medium)")
     ap.add_argument("--layout", type=int, default=0, help="vr layout preference (0 = auto; 15 = COL48)")
     ap.add_argument("--slab", action="store_true", help="COL48 layout + the LDS-slab march (vr_march_slab.hip)")
     ap.add_argument("--opt", action="append", default=[], help="vr option NAME=VALUE (experiments)")
@@ -299,9 +323,13 @@ def main() -> int:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     ndev = torch.cuda.device_count()
     dev = local % max(1, ndev)
-    # --pipeline1: the native frame loop with a one-rank communicator at N = 1
-    # (a rehearsal of the N > 1 host path on one GPU; not the default N = 1 line)
-    native = (world > 1 and args.sharder == "native") or args.pipeline1
+    # N = 1: the native frame loop with a one-rank communicator, the same loop
+    # as N > 1 (--n1-loop sharder / --inflight 2: the BandSharder paths)
+    # (grid media: a procedural medium's frames cannot overlap, and its renders
+    # run ~10 % slower inside the loop than through BandSharder)
+    native = ((world > 1 and args.sharder == "native") or args.pipeline1
+              or (world == 1 and args.n1_loop == "native" and args.inflight == 1
+                  and CONFIGS[args.config][0] is not None))
     if native and ndev < world:
         raise SystemExit(f"--sharder native needs one GPU per rank ({world} ranks, {ndev} GPUs); "
                          "use --sharder torch --backend gloo to rehearse on fewer GPUs")
@@ -467,19 +495,29 @@ def main() -> int:
     # loads ("_u" kernels).  For comparison, the same K
     # frames with every channel loaded, timed after the main window (N = 1).
     all_loaded = None
-    if world == 1 and not native and not args.spin and "_u" in r.kernel_variant:
+    if world == 1 and not args.spin and "_u" in r.kernel_variant:
         skipped_variant = r.kernel_variant
         r.set_option("uniform_skip", 0)
-        sharder.run_frames(args.warmup)
-        torch.cuda.synchronize()
-        ev2 = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-               if i % ev_every == 0 else None for i in range(args.steps)]
-        t1 = time.perf_counter()
-        sharder.run_frames(args.steps, events=ev2)
-        torch.cuda.synchronize()
-        el2 = time.perf_counter() - t1
+        if native:   # the same loop as the headline
+            pipe.run_frames(args.warmup)
+            pipe.barrier(stream)
+            t1 = time.perf_counter()
+            k2 = pipe.run_frames(args.steps, stream=stream, sample_every=ev_every)
+            pipe.barrier(stream)
+            torch.cuda.synchronize()
+            el2 = time.perf_counter() - t1
+        else:
+            sharder.run_frames(args.warmup)
+            torch.cuda.synchronize()
+            ev2 = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                   if i % ev_every == 0 else None for i in range(args.steps)]
+            t1 = time.perf_counter()
+            sharder.run_frames(args.steps, events=ev2)
+            torch.cuda.synchronize()
+            el2 = time.perf_counter() - t1
+            k2 = float(np.mean([e[0].elapsed_time(e[1]) for e in ev2 if e is not None]))
         all_loaded = {"kernel": r.kernel_variant, "ms_per_step": round(el2 / args.steps * 1e3, 4),
-                      "kernel_ms_mean": round(float(np.mean([e[0].elapsed_time(e[1]) for e in ev2 if e is not None])), 5),
+                      "kernel_ms_mean": round(k2, 5),
                       "value": round(W * H * S * args.steps / el2 / 1e6, 3)}
         r.set_option("uniform_skip", 1)
         assert r.kernel_variant == skipped_variant
@@ -508,7 +546,7 @@ def main() -> int:
     # the other BASELINE configs, timed in this process after the headline
     # window (N = 1 only; a multi-GPU run keeps to the headline)
     others, other_cpu = {}, {}
-    if world == 1 and not native and not args.spin and args.config == "grid512" and not args.no_other_configs:
+    if world == 1 and not args.spin and args.config == "grid512" and not args.no_other_configs:
         for name in ("grid4k", "cloud", "cloud_shadow"):
             others[name], other_cpu[name] = other_config(name, args.steps, args.warmup)
     # the measured HBM roofline of this box: one-pass 16-B-per-lane streams of
@@ -532,13 +570,15 @@ def main() -> int:
             collective_label = (f"torch.distributed gather to rank 0 ({backend}"
                                 + (", host-staged: band sets copied through host memory)" if backend == "gloo"
                                    else ", device buffers)"))
+    # vr_shard_run_frames renders a procedural medium on one stream (its frames cannot overlap)
+    streams_eff = 1 if proc is not None else args.render_streams
     if rank == 0:
         ms_per_step = el / args.steps * 1e3
         value = W * H * S * args.steps / el / 1e6
         variant = r.kernel_variant
         # two render streams (native loop, N > 1): a launch overlaps the next, so
         # its duration is not a frame's -- the roofline takes the wall time per frame
-        overlap = native and args.render_streams == 2
+        overlap = native and streams_eff == 2
         roof_ms = ms_per_step if overlap else kern_ms
         compositor = native and pipe is not None and pipe.compositor
         rows_part = native and pipe is not None and pipe.partition == "rows"
@@ -610,14 +650,19 @@ def main() -> int:
                                   else "reference (TestMain.cpp:219-245)"),
                        "kernel": r.kernel_variant + ("_deferred" if proc is not None and shadow > 0
                                                       and r.get_option("shadow_defer") == 1 else ""),
-                       "parallelism": ((f"row ranges x{world - 1}" if rows_part else f"bands16x{world - 1}")
-                                       + ", rank 0 compositing" if compositor
-                                       else (f"row ranges x{world}" if rows_part else f"bands16x{world}"))
-                                      + (", 2 frames in flight" if args.inflight == 2 else "")
-                                      + (f", {args.render_streams} render stream{'s' if args.render_streams > 1 else ''}"
-                                         + (f", exchange on {args.exchange} stream{'s' if args.exchange == 'render' else ''}"
-                                            if args.render_streams == 2 else "")
-                                         if native else ""),
+                       "parallelism": (("one GPU, the native frame loop (libvr_shard, one-rank communicator)"
+                                        + (", 2 render streams: 2 frames in flight" if streams_eff == 2
+                                           else ", 1 render stream (a procedural medium's frames do not overlap)"
+                                           if proc is not None else ", 1 render stream"))
+                                       if native and world == 1 else
+                                       ((f"row ranges x{world - 1}" if rows_part else f"bands16x{world - 1}")
+                                        + ", rank 0 compositing" if compositor
+                                        else (f"row ranges x{world}" if rows_part else f"bands16x{world}"))
+                                       + (", 2 frames in flight" if args.inflight == 2 else "")
+                                       + (f", {args.render_streams} render stream{'s' if args.render_streams > 1 else ''}"
+                                          + (f", exchange on {args.exchange} stream{'s' if args.exchange == 'render' else ''}"
+                                             if args.render_streams == 2 else "")
+                                          if native else "")),
                        "collective": collective_label,
                        "executed_steps_per_frame": frame_steps},
             "executed_steps_per_s": round(frame_steps * args.steps / el, 1),

@@ -1243,6 +1243,7 @@ try {
     if (n == "shadow_defer_mib") return c->shadow_defer_mib;
     if (n == "shadow_defer_entries") return (int)c->defer_entries;
     if (n == "shadow_defer_last") return c->defer_last;   // read-only
+    if (n == "procedural") return c->proc.enabled ? 1 : 0;   // read-only: a procedural medium is set
     if (n == "shadow_defer_kib")                          // read-only: the scratch held now, KiB
         return (int)std::min<size_t>((c->defer_bytes + 1023) / 1024, 0x7fffffff);
     if (n == "slab_cap") return c->slab_cap;

@@ -118,8 +118,8 @@ vr_status caught_exception(const char* fn) noexcept
 
 // Poll `state()` -- 0 done, 1 pending, 2 failed -- until it is not pending or
 // `timeout_s` has passed: 0 done, 1 failed, 2 timed out.  Spins for the first
-// 2 ms (a barrier at the end of a timed window costs microseconds), then
-// sleeps 50 us between polls.  Shared by the collective waits and the CPU
+// 20 ms (a barrier at the end of a timed window of frames costs microseconds,
+// not a sleep's granularity), then sleeps 50 us between polls.  Shared by the collective waits and the CPU
 // self-test of the deadline logic (vr_shard_poll_selftest).
 template <class State>
 int poll_until(State state, double timeout_s)
@@ -132,7 +132,7 @@ int poll_until(State state, double timeout_s)
         if (st == 2) return 1;
         const double el = std::chrono::duration<double>(clk::now() - t0).count();
         if (el > timeout_s) return 2;
-        if (el > 2e-3) std::this_thread::sleep_for(std::chrono::microseconds(50));
+        if (el > 20e-3) std::this_thread::sleep_for(std::chrono::microseconds(50));
     }
 }
 
@@ -713,7 +713,10 @@ try {
     }
     int next = 0;
     const auto h0 = std::chrono::steady_clock::now();
-    const bool two = sh->render_streams == 2;
+    // a procedural medium's frames cannot overlap (the ctx's cost-sort and
+    // shadow scratch serve one frame at a time; vr_render orders them across
+    // streams): they take one render stream, without the cross-stream waits
+    const bool two = sh->render_streams == 2 && vr_get_option(sh->ctx, "procedural") != 1;
     if (frames > 0) sh->started = true;   // the band geometry is fixed from here
     // two render streams: tell the ctx its consecutive renders overlap (its
     // auto split rule), for this run
