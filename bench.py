@@ -277,7 +277,7 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="grid512", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
@@ -364,7 +364,13 @@ def main() -> int:
     march = vr.march_defaults(max_steps=S)
     r.set_march(march)
     fmt = vr.FMT_RGBA8_UNORM
-    sharder = vrdist.BandSharder(r, W, H, fmt, band_rows=16, world=world, rank=rank, inflight=args.inflight)
+    # N = 1, a procedural medium without shadow rays: two frames in flight
+    # through BandSharder (frames reusing the cost order only read the ctx's
+    # scratch and overlap; the native loop's procedural renders ran ~10 % slower)
+    proc_inflight2 = (world == 1 and not native and proc is not None and shadow == 0 and args.n1_loop == "native"
+                      and args.inflight == 1 and not args.spin)
+    sharder = vrdist.BandSharder(r, W, H, fmt, band_rows=16, world=world, rank=rank,
+                                 inflight=2 if proc_inflight2 else args.inflight)
     stream = torch.cuda.current_stream()
 
     # executed ray-steps per launch (this rank's bands), one untimed pass
@@ -422,7 +428,9 @@ def main() -> int:
         # RCCL barrier + synchronisation on both sides of the timed frames.  A
         # gloo barrier across 8 processes costs a sizeable fraction of a
         # millisecond -- several 1/8-frames -- so it stays outside the clock.
-        pipe.run_frames(args.warmup, cameras=sd[:args.warmup] if sd else None)
+        # (sampling every warmup frame creates the loop's timing events now,
+        # outside the window: ceil(steps / ev_every) pairs, created on first use)
+        pipe.run_frames(args.warmup, cameras=sd[:args.warmup] if sd else None, sample_every=1)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -578,7 +586,7 @@ def main() -> int:
         variant = r.kernel_variant
         # two render streams (native loop, N > 1): a launch overlaps the next, so
         # its duration is not a frame's -- the roofline takes the wall time per frame
-        overlap = native and streams_eff == 2
+        overlap = (native and streams_eff == 2) or proc_inflight2 or (world == 1 and args.inflight == 2)
         roof_ms = ms_per_step if overlap else kern_ms
         compositor = native and pipe is not None and pipe.compositor
         rows_part = native and pipe is not None and pipe.partition == "rows"
@@ -658,7 +666,8 @@ def main() -> int:
                                        ((f"row ranges x{world - 1}" if rows_part else f"bands16x{world - 1}")
                                         + ", rank 0 compositing" if compositor
                                         else (f"row ranges x{world}" if rows_part else f"bands16x{world}"))
-                                       + (", 2 frames in flight" if args.inflight == 2 else "")
+                                       + (", 2 frames in flight (two streams and targets)"
+                                          if args.inflight == 2 or proc_inflight2 else "")
                                        + (f", {args.render_streams} render stream{'s' if args.render_streams > 1 else ''}"
                                           + (f", exchange on {args.exchange} stream{'s' if args.exchange == 'render' else ''}"
                                              if args.render_streams == 2 else "")

@@ -135,8 +135,9 @@ vr_status vr_shard_set_timeout(vr_shard* sh, double seconds);
  * alternating by buffer parity, renders of consecutive frames overlap;
  * 1 = every render on the caller's stream, after the previous one.  Results
  * are identical.  Switching waits (host) for the frames in flight.  A
- * procedural medium's frames always take one stream: its scratch serves one
- * frame at a time, so they cannot overlap (two streams cost 12 % in waits). */
+ * procedural medium with shadow rays always takes one stream: each of its
+ * frames writes the ctx's deferred-shadow scratch, so they cannot overlap
+ * (two streams cost 12 % in waits). */
 vr_status vr_shard_set_render_streams(vr_shard* sh, int n);
 int       vr_shard_get_render_streams(vr_shard* sh);
 /* Per-rank rehearsal on one GPU (an unconnected shard, any rank): 1 = each

@@ -512,3 +512,39 @@ def test_frames_in_flight_then_one_stream_paths(oracle):
         want, _ = oracle.render_procedural(oracle.procedural_from(r.procedural), obj, glob, oracle.from_params(m),
                                            W, H, 0)
         assert np.array_equal(f.cpu().numpy(), want)
+
+
+def test_procedural_frames_in_flight_readers_and_writers(oracle):
+    """A procedural medium without shadow rays, two frames in flight
+    (BandSharder inflight=2): frames that reuse the camera's cost order only
+    read the ctx's scratch and overlap on two streams; a frame with a new
+    camera rebuilds the order (writes) and must wait for the reader still in
+    flight on the other stream, and the next readers for it.  Every frame of
+    both cameras equals the oracle's; then the same with shadow rays (every
+    frame writes, one stream)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import volumetricrenderer_amd as vr
+    from volumetricrenderer_amd.distributed import BandSharder
+    W, H = 320, 180
+    m = vr.march_defaults(max_steps=32)
+    cams = [vr.reference_shader_data(W / H, a, 5.0) for a in (15.0, 55.0)]
+    with vr.Renderer(0) as r:
+        r.set_march(m)
+        r.set_procedural(shadow_steps=0)
+        assert r.get_option("procedural") == 1
+        p = oracle.procedural_from(r.procedural)
+        sh = BandSharder(r, W, H, 0, inflight=2)
+        want = []
+        for c in cams:
+            obj, glob = vr.shader_data_arrays(*c)
+            want.append(oracle.render_procedural(p, obj, glob, oracle.from_params(m), W, H, 0)[0])
+        for k, c in ((5, 0), (4, 1), (3, 0)):
+            r.set_shader_data(*cams[c])
+            f = sh.run_frames(k)
+            torch.cuda.current_stream().synchronize()
+            assert sh._launch2 is not None
+            assert np.array_equal(f.cpu().numpy(), want[c]), (k, c)
+            assert all(np.array_equal(t.cpu().numpy(), want[c]) for t in sh._targets2), (k, c)
+        r.set_procedural(shadow_steps=4)
+        assert r.get_option("procedural") == 2

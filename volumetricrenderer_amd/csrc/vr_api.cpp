@@ -156,20 +156,29 @@ struct Ctx {
     unsigned defer_entries = 0;    // option "shadow_defer_entries": entry capacity override (tests; 0 = sized from the frame)
     int defer_last = 0;            // the last procedural render ran the deferred passes
     // outgrown scratch buffers: queued frames may still use them.  Each gets an
-    // event recorded on the render stream of the frame that outgrew it, after
-    // that stream has waited for the last procedural render (proc_ev), and is
-    // freed by a later ensure_defer once the event has completed
+    // event recorded on the render stream of the writing frame that outgrew it,
+    // after that stream has waited for every earlier procedural render
+    // (proc_uses), and is freed by a later ensure_defer once the event has
+    // completed
     struct Retired {
         void* p;
         hipEvent_t ev;             // nullptr until recorded
     };
     std::vector<Retired> defer_retired;
-    // the procedural scratch (d_sort, d_defer, d_lat) serves one frame at a
-    // time: a procedural render on another stream than the last one waits
-    // for it (frames in flight on alternating streams, vr_shard.cpp)
-    hipEvent_t proc_ev = nullptr;
-    hipStream_t proc_stream = nullptr;
-    bool proc_pending = false;
+    // The procedural scratch (d_sort, d_defer) is written by a frame that
+    // sorts (SORT_BUILD) or defers its shadow rays, and only read by a frame
+    // that reuses the order.  A writer waits for every earlier procedural
+    // render on other streams; a reader only for the last writer.  So frames
+    // that reuse one camera's order overlap on alternating streams (2 in
+    // flight), and a frame that writes never races a reader.
+    struct ProcUse {
+        hipStream_t s;
+        hipEvent_t ev;     // recorded after the stream's last procedural render
+    };
+    std::vector<ProcUse> proc_uses;      // one per stream (at most kMaxProcStreams)
+    hipEvent_t proc_wev = nullptr;       // after the last writer
+    hipStream_t proc_wstream = nullptr;
+    bool proc_wpending = false;
     unsigned long long* h_need = nullptr;   // host-mapped [entries, records] written by the last sorting frame
     unsigned long long* d_need = nullptr;   // its device address
     hipEvent_t need_ev = nullptr;
@@ -646,7 +655,8 @@ try {
     if (c->d_rg) (void)hipFree(c->d_rg);
     if (c->h_rghdr) (void)hipHostFree(c->h_rghdr);
     if (c->rg_ev) (void)hipEventDestroy(c->rg_ev);
-    if (c->proc_ev) (void)hipEventDestroy(c->proc_ev);
+    for (auto& u : c->proc_uses) (void)hipEventDestroy(u.ev);
+    if (c->proc_wev) (void)hipEventDestroy(c->proc_wev);
     if (c->d_terms) (void)hipFree(c->d_terms);
     if (c->d_mm) (void)hipFree(c->d_mm);
     if (c->h_mm) (void)hipHostFree(c->h_mm);
@@ -1243,7 +1253,10 @@ try {
     if (n == "shadow_defer_mib") return c->shadow_defer_mib;
     if (n == "shadow_defer_entries") return (int)c->defer_entries;
     if (n == "shadow_defer_last") return c->defer_last;   // read-only
-    if (n == "procedural") return c->proc.enabled ? 1 : 0;   // read-only: a procedural medium is set
+    // read-only: 0 = a grid medium; 1 = procedural, frames that reuse one
+    // camera's order only read the ctx's scratch (they overlap on two
+    // streams); 2 = procedural with shadow rays (deferred: every frame writes)
+    if (n == "procedural") return !c->proc.enabled ? 0 : c->proc.shadow_steps > 0 && c->shadow_defer ? 2 : 1;
     if (n == "shadow_defer_kib")                          // read-only: the scratch held now, KiB
         return (int)std::min<size_t>((c->defer_bytes + 1023) / 1024, 0x7fffffff);
     if (n == "slab_cap") return c->slab_cap;
@@ -2207,23 +2220,51 @@ try {
         std::vector<float> built = reuse == SORT_BUILD ? key : c->sort_key;
         c->sort_key.clear();   // valid again only once this launch is queued
         const bool report = use_defer && reuse == SORT_BUILD;   // proc_scan writes the frame's need
-        if (c->proc_pending && c->proc_stream != static_cast<hipStream_t>(stream)) {
-            const vr_status sw = stream_wait_pending(static_cast<hipStream_t>(stream), c->proc_ev);
+        const hipStream_t ps = static_cast<hipStream_t>(stream);
+        constexpr size_t kMaxProcStreams = 8;
+        bool known = false;
+        for (const auto& u : c->proc_uses) known = known || u.s == ps;
+        // a ninth stream is treated as a writer: it waits for every render
+        const bool writes = reuse == SORT_BUILD || use_defer || (!known && c->proc_uses.size() >= kMaxProcStreams);
+        if (writes) {
+            for (const auto& u : c->proc_uses)
+                if (u.s != ps) {
+                    const vr_status sw = stream_wait_pending(ps, u.ev);
+                    if (sw != VR_OK) return sw;
+                }
+        } else if (c->proc_wpending && c->proc_wstream != ps) {
+            const vr_status sw = stream_wait_pending(ps, c->proc_wev);
             if (sw != VR_OK) return sw;
         }
-        // a scratch this frame outgrew: free once every earlier frame has run
-        // (this stream now follows the last procedural render)
+        // a scratch this (writing) frame outgrew: free once every earlier frame
+        // has run (this stream now follows every earlier procedural render)
         for (auto& q : c->defer_retired)
-            if (!q.ev) {
+            if (writes && !q.ev) {
                 HIP_TRY(hipEventCreateWithFlags(&q.ev, hipEventDisableTiming));
                 HIP_TRY(hipEventRecord(q.ev, static_cast<hipStream_t>(stream)));
             }
         HIP_TRY(launch_march_procedural(a, m.early_out > 0.0f, sort_buf, reuse, sc, static_cast<hipStream_t>(stream),
                                         use_defer ? &defer : nullptr, report ? c->d_need : nullptr));
-        if (!c->proc_ev) HIP_TRY(hipEventCreateWithFlags(&c->proc_ev, hipEventDisableTiming));
-        HIP_TRY(hipEventRecord(c->proc_ev, static_cast<hipStream_t>(stream)));
-        c->proc_stream = static_cast<hipStream_t>(stream);
-        c->proc_pending = true;
+        Ctx::ProcUse* mine = nullptr;
+        for (auto& u : c->proc_uses)
+            if (u.s == ps) mine = &u;
+        if (!mine) {
+            if (c->proc_uses.size() >= kMaxProcStreams) {   // (this render waited for all of them)
+                for (auto& u : c->proc_uses) (void)hipEventDestroy(u.ev);
+                c->proc_uses.clear();
+            }
+            Ctx::ProcUse u{ps, nullptr};
+            HIP_TRY(hipEventCreateWithFlags(&u.ev, hipEventDisableTiming));
+            c->proc_uses.push_back(u);
+            mine = &c->proc_uses.back();
+        }
+        HIP_TRY(hipEventRecord(mine->ev, ps));
+        if (writes) {
+            if (!c->proc_wev) HIP_TRY(hipEventCreateWithFlags(&c->proc_wev, hipEventDisableTiming));
+            HIP_TRY(hipEventRecord(c->proc_wev, ps));
+            c->proc_wstream = ps;
+            c->proc_wpending = true;
+        }
         if (report) {
             HIP_TRY(hipEventRecord(c->need_ev, static_cast<hipStream_t>(stream)));
             c->need_pending = true;

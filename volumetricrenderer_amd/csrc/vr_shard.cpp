@@ -713,10 +713,10 @@ try {
     }
     int next = 0;
     const auto h0 = std::chrono::steady_clock::now();
-    // a procedural medium's frames cannot overlap (the ctx's cost-sort and
-    // shadow scratch serve one frame at a time; vr_render orders them across
-    // streams): they take one render stream, without the cross-stream waits
-    const bool two = sh->render_streams == 2 && vr_get_option(sh->ctx, "procedural") != 1;
+    // a procedural medium with deferred shadow rays writes the ctx's scratch
+    // every frame, so its frames cannot overlap (vr_render orders them across
+    // streams): one render stream, without the cross-stream waits
+    const bool two = sh->render_streams == 2 && vr_get_option(sh->ctx, "procedural") != 2;
     if (frames > 0) sh->started = true;   // the band geometry is fixed from here
     // two render streams: tell the ctx its consecutive renders overlap (its
     // auto split rule), for this run

@@ -157,9 +157,10 @@ class BandSharder:
         gather buffers and frames are double-buffered.  Each buffer of a
         parity is reused only after the stream order has retired its last
         reader.  Returns the last frame (rank 0) or band set."""
-        proc = getattr(self.r, "procedural", None)
-        if (self.world == 1 and self.inflight == 2 and hasattr(self.r, "prepare_render") and
-                (proc is None or not proc.enabled)):
+        # (a procedural medium with deferred shadow rays writes the ctx's
+        # scratch every frame: its frames cannot overlap, one stream below)
+        overlap_ok = not hasattr(self.r, "get_option") or self.r.get_option("procedural") != 2
+        if self.world == 1 and self.inflight == 2 and hasattr(self.r, "prepare_render") and overlap_ok:
             # one rank, grid medium, inflight 2 (throughput mode): consecutive
             # frames alternate between two streams and two targets, so frame
             # i+1's waves fill the SIMDs while frame i's last, longest rays
@@ -167,9 +168,9 @@ class BandSharder:
             # profiles/r04/inflight_ab.txt; each launch then overlaps the next,
             # so per-launch kernel times no longer measure one frame, and the
             # default stays one stream).  The grid render's only shared state
-            # is the read-only region lists; the procedural medium's cost-sort
-            # and shadow scratch belong to the context and serve one frame at a
-            # time, so it keeps one stream (below).  Both streams start after
+            # is the read-only region lists; a procedural frame that reuses the
+            # cost order only reads the ctx's scratch, and vr_render orders a
+            # writing frame after every reader.  Both streams start after
             # the caller's stream and the caller's stream waits for both.
             if getattr(self, "_launch2", None) is None:
                 self._streams2 = [torch.cuda.Stream(self.local.device), torch.cuda.Stream(self.local.device)]
