@@ -20,8 +20,11 @@
  * the install), and the first procedural render of a
  * larger target allocates the context's cost-sort scratch (with shadow rays
  * also the deferred-shadow scratch, option "shadow_defer") after a device
- * synchronisation.  That scratch belongs to the context: renders of one
- * vr_ctx on different streams must not overlap (order them with events).
+ * synchronisation.  That scratch belongs to the context.  vr_render orders
+ * procedural renders of one vr_ctx across streams itself: a frame that
+ * writes the scratch (a new cost order, deferred shadow rays) waits for every
+ * earlier procedural render, and a frame that only reads it (the same camera's
+ * order) waits for the last writer, so readers overlap on alternating streams.
  */
 #ifndef VR_H
 #define VR_H
