@@ -279,6 +279,12 @@ int vr_band_rows_packed(int height, int band_rows, int band_stride, int band_fir
  * longest waves bound a small share's launch); range 0 takes
  * "row_first_pct" (default 100) % of a mean share.                        */
 vr_status vr_row_partition(void* ctx, int width, int height, int parts, int* row_begin);
+/* vr_row_partition corrected by measurement: range k of the previous split
+ * prev_begin[parts + 1] took prev_ms[k] (any unit, >= 0; 0 = not measured);
+ * each of its strips' estimated work is scaled by prev_ms[k] / (the model's
+ * work of range k), and the frame is split again (vr_shard_rebalance_rows). */
+vr_status vr_row_partition_measured(void* ctx, int width, int height, int parts, const int* prev_begin,
+                                    const double* prev_ms, int* row_begin);
 
 /* ---- introspection: the kernel variant vr_render will launch ----------- */
 /* returns a static string, e.g. "grid_pad16_clamp"                        */

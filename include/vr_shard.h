@@ -184,14 +184,22 @@ vr_status vr_shard_bands(vr_shard* sh, int* band_stride, int* band_first);
  * (DESIGN.md sec. 7.3).  Rank 0 rendering in place takes a smaller share of
  * the work (2 % less per other rank): it also expands the other ranks' rows.  row_begin[renderers + 1]: 0, non-decreasing,
  * multiples of 8, the frame height last; NULL = back to band sets.  Every
- * rank must set the same ranges, before its first frames; a later
- * vr_shard_set_compositor returns the shard to band sets.
+ * rank must set the same ranges.  The choice of band sets or ranges is fixed
+ * by the first frames; new ranges between runs wait for the frames in flight.
+ * A later vr_shard_set_compositor returns the shard to band sets.
  * vr_shard_balance_rows: the ranges of equal estimated work for the ctx's
  * current camera (vr_row_partition), computed by rank 0 and broadcast -- a
  * collective: every rank calls it.  vr_shard_partition: 1 = row ranges,
  * 0 = band sets.  vr_shard_row_range: a rank's range (row ranges only). */
 vr_status vr_shard_set_rows(vr_shard* sh, const int* row_begin);
 vr_status vr_shard_balance_rows(vr_shard* sh);
+/* Collective, between runs, with row ranges: every rank passes its measured
+ * time per frame (e.g. vr_shard_run's kernel_ms); rank 0 splits the frame
+ * again with the ranges' times (vr_row_partition_measured) and every rank
+ * takes the new ranges.  The frames in flight finish first.  The model's
+ * split leaves ranks 2 and 5 of config 4 at 8 ranks 8-10 % above the others;
+ * one measured round evens them. */
+vr_status vr_shard_rebalance_rows(vr_shard* sh, double my_ms);
 int       vr_shard_partition(vr_shard* sh);
 vr_status vr_shard_row_range(vr_shard* sh, int rank, int* row_first, int* rows);
 int       vr_shard_aborted(vr_shard* sh);

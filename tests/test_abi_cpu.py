@@ -32,7 +32,7 @@ def test_shard_library_exports_every_declared_symbol():
     from volumetricrenderer_amd import _lib
     lib = _lib.load_shard()
     declared = header_functions("vr_shard.h")
-    assert len(declared) == 29
+    assert len(declared) == 30
     for name in declared:
         assert hasattr(lib, name), name
     assert sorted(declared) == _lib.shard_exported_symbols()
@@ -52,6 +52,7 @@ def test_shard_library_exports_every_declared_symbol():
         _lib.shard_call("vr_shard_bands", None, None, None)
     assert _lib.shard_call("vr_shard_get_compositor", None) == -1
     for f, args in (("vr_shard_set_rows", (None, None)), ("vr_shard_balance_rows", (None,)),
+                    ("vr_shard_rebalance_rows", (None, 1.0)),
                     ("vr_shard_row_range", (None, 0, None, None))):
         with pytest.raises(_lib.VRError):
             _lib.shard_call(f, *args)

@@ -548,3 +548,40 @@ def test_procedural_frames_in_flight_readers_and_writers(oracle):
             assert all(np.array_equal(t.cpu().numpy(), want[c]) for t in sh._targets2), (k, c)
         r.set_procedural(shadow_steps=4)
         assert r.get_option("procedural") == 2
+
+
+def test_row_partition_measured_and_one_rank_rebalance():
+    """vr_row_partition_measured: with the model's own split and times equal
+    to its estimate the split stays (to a strip); a range measured twice as
+    slow shrinks and the others grow.  vr_shard_rebalance_rows over a one-rank
+    RCCL communicator (the all-reduce of the times and the broadcast run for
+    real) keeps the whole frame and the frames stay exact."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import volumetricrenderer_amd as vr
+    from volumetricrenderer_amd.distributed import RcclBandPipeline
+    W, H = 640, 360
+    with vr.Renderer(0) as r:
+        r.generate_volume(vr.volume_recipe_defaults(size=64))
+        r.set_shader_data(*vr.reference_shader_data(W / H, 10.0, 20.0))
+        r.set_march(vr.march_defaults())
+        rb = r.row_partition(W, H, 4)
+        same = r.row_partition_measured(W, H, rb, [1.0, 1.0, 1.0, 1.0])
+        assert all(abs(a - b) <= 8 for a, b in zip(rb, same)), (rb, same)
+        slow0 = r.row_partition_measured(W, H, rb, [2.0, 1.0, 1.0, 1.0])
+        assert slow0[1] < rb[1] and slow0[0] == 0 and slow0[-1] == H, (rb, slow0)
+        with pytest.raises(vr.VRError):
+            r.row_partition_measured(W, H, [0, 7, H], [1.0, 1.0])   # not a multiple of 8
+        pl = RcclBandPipeline(r, W, H, 1, band_rows=16, world=1, rank=0, partition="rows")
+        try:
+            pl.run_frames(3)
+            assert pl.row_range == (0, H)
+            assert pl.rebalance_rows(frames=4) == (0, H)
+            pl.run_frames(3)
+            pl.barrier()
+            got = pl.frame()
+            full = r.render(W, H, 1)
+            torch.cuda.synchronize()
+            assert np.array_equal(got.cpu().numpy(), full.cpu().numpy())
+        finally:
+            pl.close()

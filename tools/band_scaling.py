@@ -43,6 +43,9 @@ def main():
     ap.add_argument("--compositor", default="auto", choices=["auto", "on", "off"],
                     help="--native: rank 0 renders no bands and only assembles (vr_shard_set_compositor; auto: the "
                          "library's default, on from 8 ranks)")
+    ap.add_argument("--rebalance", action="store_true",
+                    help="--native --all-ranks, row ranges: a second pass with the ranges split again by every "
+                         "rank's measured render time (vr_row_partition_measured, as vr_shard_rebalance_rows does)")
     ap.add_argument("--partition", default="auto", choices=["auto", "bands", "rows"],
                     help="--native: interleaved band sets or balanced contiguous row ranges (RcclBandPipeline)")
     ap.add_argument("--exchange", default="render", choices=["render", "comm"],
@@ -103,7 +106,6 @@ def main():
 
 def native(a):
     """Per-rank frame streams of the native loop (solo rehearsal), 1 vs 2 render streams."""
-    from volumetricrenderer_amd.distributed import RcclBandPipeline
     W, H = a.width, a.height
     with vr.Renderer(0) as r:
         r.generate_volume(vr.scaled_recipe(a.size))
@@ -120,52 +122,75 @@ def native(a):
         streams = [int(v) for v in a.streams.split(",")]
         base = {}
         for n in [int(v) for v in a.ns.split(",")]:
-            res = {ns: [] for ns in streams}   # per stream count: per round, the slowest rank's ms/frame
-            per_rank = {ns: {} for ns in streams}   # per stream count, rank: ms/frame per round
-            host = {ns: [] for ns in streams}
-            # one rank's pipeline at a time: its streams get HIP's hardware
-            # queues to themselves (GPU_MAX_HW_QUEUES = 4 per process), as in
-            # the N-process run; pipelines of all ranks alive at once would
-            # share queues and serialise each other's render streams
-            per_round = {ns: [[] for _ in range(a.rounds)] for ns in streams}
-            for first in (range(n) if a.all_ranks else (min(a.rank, n - 1),)):
-                for ns in streams:
-                    p = RcclBandPipeline(r, W, H, vr.FMT_RGBA8_UNORM, band_rows=a.band_rows, world=n, rank=first,
-                                         loopback=True, solo=True, render_streams=ns, host_threads=a.threads,
-                                         exchange_on_render=a.exchange == "render",
-                                         compositor=None if a.compositor == "auto" else a.compositor == "on",
-                                         partition=a.partition)
-                    p.run_frames(8)   # region lists, code objects
-                    p.barrier()
-                    for k in range(a.rounds):
-                        p.run_frames(4)
-                        p.barrier()
-                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                        if a.gate_ms > 0:   # ~2.1 GHz shader clock under this load
-                            torch.cuda._sleep(int(a.gate_ms * 1e-3 * 2.1e9))
-                        e0.record()
-                        p.run_frames(a.frames)
-                        e1.record()
-                        torch.cuda.synchronize()
-                        ms = e0.elapsed_time(e1) / a.frames
-                        per_round[ns][k].append(ms)
-                        per_rank[ns].setdefault(first, []).append(ms)
-                        host[ns].append(p.host_ms)
-                    p.close()
-            for ns in streams:
-                res[ns] = [max(v) for v in per_round[ns]]
-            for ns in streams:
-                t = float(np.median(res[ns]))
-                if n == 1:
-                    base[ns] = t
-                b = base.get(ns)
-                eff = f", efficiency {b / n / t:.2f} (vs N=1, same streams)" if b else ""
-                print(f"N={n} render_streams {ns}: slowest rank {t:.4f} ms/frame (rounds "
-                      + " ".join(f"{v:.4f}" for v in res[ns]) + f"), host {max(host[ns]):.4f} ms/frame{eff}",
+            info = one_n(a, r, W, H, n, streams, base, None)
+            if a.rebalance and a.all_ranks and n > 1 and info["ranges"]:
+                first_r = min(info["ranges"])   # 0, or 1 with rank 0 as a compositor
+                prev = [info["ranges"][k][0] for k in sorted(info["ranges"])] + [H]
+                ms = [info["kms"][k] for k in sorted(info["ranges"])]
+                pct = 100 if first_r == 1 else max(50, 100 - 2 * (n - 1))
+                old = r.get_option("row_first_pct")
+                r.set_option("row_first_pct", pct)
+                new = r.row_partition_measured(W, H, prev, ms)
+                r.set_option("row_first_pct", old)
+                print(f"  rebalanced: ranges {prev} -> {new} (render ms per rank " + " ".join(f"{v:.4f}" for v in ms) + ")",
                       flush=True)
-                if a.all_ranks and n > 1:
-                    print("  per rank (median ms/frame): " + " ".join(
-                        f"{k}:{float(np.median(v)):.4f}" for k, v in sorted(per_rank[ns].items())), flush=True)
+                one_n(a, r, W, H, n, streams, base, new)
+
+
+def one_n(a, r, W, H, n, streams, base, rows):
+    """One world size's per-rank frame streams; rows: explicit row starts."""
+    from volumetricrenderer_amd.distributed import RcclBandPipeline
+    res = {ns: [] for ns in streams}   # per stream count: per round, the slowest rank's ms/frame
+    per_rank = {ns: {} for ns in streams}   # per stream count, rank: ms/frame per round
+    host = {ns: [] for ns in streams}
+    # one rank's pipeline at a time: its streams get HIP's hardware
+    # queues to themselves (GPU_MAX_HW_QUEUES = 4 per process), as in
+    # the N-process run; pipelines of all ranks alive at once would
+    # share queues and serialise each other's render streams
+    per_round = {ns: [[] for _ in range(a.rounds)] for ns in streams}
+    ranges, kms = {}, {}
+    for first in (range(n) if a.all_ranks else (min(a.rank, n - 1),)):
+        for ns in streams:
+            p = RcclBandPipeline(r, W, H, vr.FMT_RGBA8_UNORM, band_rows=a.band_rows, world=n, rank=first,
+                                 loopback=True, solo=True, render_streams=ns, host_threads=a.threads,
+                                 exchange_on_render=a.exchange == "render",
+                                 compositor=None if a.compositor == "auto" else a.compositor == "on",
+                                 partition="rows" if rows else a.partition, rows=rows)
+            p.run_frames(8)   # region lists, code objects
+            p.barrier()
+            for k in range(a.rounds):
+                p.run_frames(4)
+                p.barrier()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                if a.gate_ms > 0:   # ~2.1 GHz shader clock under this load
+                    torch.cuda._sleep(int(a.gate_ms * 1e-3 * 2.1e9))
+                e0.record()
+                p.run_frames(a.frames)
+                e1.record()
+                torch.cuda.synchronize()
+                ms = e0.elapsed_time(e1) / a.frames
+                per_round[ns][k].append(ms)
+                per_rank[ns].setdefault(first, []).append(ms)
+                host[ns].append(p.host_ms)
+            if p.row_range is not None and ns == streams[-1] and not (p.compositor and first == 0):
+                ranges[first] = p.row_range
+                kms[first] = p.run_frames(16, sample_every=1)
+            p.close()
+    for ns in streams:
+        res[ns] = [max(v) for v in per_round[ns]]
+    for ns in streams:
+        t = float(np.median(res[ns]))
+        if n == 1:
+            base[ns] = t
+        b = base.get(ns)
+        eff = f", efficiency {b / n / t:.2f} (vs N=1, same streams)" if b else ""
+        print(f"N={n} render_streams {ns}{' rebalanced' if rows else ''}: slowest rank {t:.4f} ms/frame (rounds "
+              + " ".join(f"{v:.4f}" for v in res[ns]) + f"), host {max(host[ns]):.4f} ms/frame{eff}",
+              flush=True)
+        if a.all_ranks and n > 1:
+            print("  per rank (median ms/frame): " + " ".join(
+                f"{k}:{float(np.median(v)):.4f}" for k, v in sorted(per_rank[ns].items())), flush=True)
+    return {"ranges": ranges, "kms": kms}
 
 
 if __name__ == "__main__":

@@ -135,6 +135,8 @@ _SIGS = {
                                                ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, _vp]),
     "vr_band_rows_packed": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "vr_row_partition": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_int_p]),
+    "vr_row_partition_measured": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_int_p,
+                                                 ctypes.POINTER(ctypes.c_double), c_int_p]),
     "vr_kernel_variant": (ctypes.c_char_p, [_vp]),
     "vr_set_layout_preference": (ctypes.c_int, [_vp, ctypes.c_int]),
     "vr_set_option": (ctypes.c_int, [_vp, ctypes.c_char_p, ctypes.c_int]),
@@ -226,6 +228,7 @@ _SHARD_SIGS = {
     "vr_shard_bands": (ctypes.c_int, [_vp, c_int_p, c_int_p]),
     "vr_shard_set_rows": (ctypes.c_int, [_vp, c_int_p]),
     "vr_shard_balance_rows": (ctypes.c_int, [_vp]),
+    "vr_shard_rebalance_rows": (ctypes.c_int, [_vp, ctypes.c_double]),
     "vr_shard_partition": (ctypes.c_int, [_vp]),
     "vr_shard_row_range": (ctypes.c_int, [_vp, ctypes.c_int, c_int_p, c_int_p]),
     "vr_shard_poll_selftest": (ctypes.c_int, [ctypes.c_int, ctypes.c_double, c_int_p]),

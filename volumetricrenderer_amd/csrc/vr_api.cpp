@@ -974,24 +974,33 @@ try {
 // the region build's estimate: double, no clip test) plus kRaySetup for a ray
 // that meets the box, kRayMiss for one that does not.  Boundary k is the strip
 // edge nearest to the k/parts quantile of the prefix sums.
-vr_status vr_row_partition(void* p, int width, int height, int parts, int* row_begin)
-try {
-    if (!p || !row_begin) return fail(VR_ERR_INVALID, "vr_row_partition: null argument");
+// prev / prev_ms (vr_row_partition_measured): every strip of range k of the
+// previous partition `prev` is weighted by prev_ms[k] / (the model's work of
+// range k), so the split follows the measured times where the model is off
+static vr_status row_partition(void* p, int width, int height, int parts, const int* prev, const double* prev_ms,
+                               int* row_begin, const char* fn)
+{
+    if (!p || !row_begin) return fail(VR_ERR_INVALID, "%s: null argument", fn);
     if (width <= 0 || height <= 0 || parts <= 0 || parts > 4096)
-        return fail(VR_ERR_INVALID, "vr_row_partition: bad frame %dx%d or parts %d", width, height, parts);
+        return fail(VR_ERR_INVALID, "%s: bad frame %dx%d or parts %d", fn, width, height, parts);
+    if (prev) {
+        bool ok = prev[0] == 0 && prev[parts] == height;
+        for (int k = 1; k <= parts && ok; ++k) ok = prev[k] >= prev[k - 1] && (prev[k] % 8 == 0 || prev[k] == height);
+        for (int k = 0; k < parts && ok; ++k) ok = std::isfinite(prev_ms[k]) && prev_ms[k] >= 0.0;
+        if (!ok) return fail(VR_ERR_INVALID, "%s: bad previous partition or times", fn);
+    }
     Ctx* c = as_ctx(p);
-    if (!c->has_camera) return fail(VR_ERR_NO_CAMERA, "vr_row_partition: no shader data (vr_set_shader_data)");
+    if (!c->has_camera) return fail(VR_ERR_NO_CAMERA, "%s: no shader data (vr_set_shader_data)", fn);
     RayBasis b;
     if (!make_ray_basis(c->obj, c->glob, width, height, &b))
-        return fail(VR_ERR_INVALID, "vr_row_partition: Projection*View is singular");
+        return fail(VR_ERR_INVALID, "%s: Projection*View is singular", fn);
     const double kRaySetup = (double)c->row_setup, kRayMiss = 2.0, pw = c->row_pow / 100.0;
     const vr_march_params& m = c->march;
     const double step = (1.0 / (double)m.max_steps) * (double)m.step_scale;
     const int ns = (height + 7) / 8;
-    std::vector<double> prefix((size_t)ns + 1, 0.0);
+    std::vector<double> w((size_t)ns, 0.0);
     for (int s = 0; s < ns; ++s) {
         const double fy = std::min(8.0 * s + 4.0, height - 0.5);
-        double w = 0.0;
         for (int x = 4; x < width + 4; x += 8) {
             const double fx = std::min((double)x, width - 0.5);
             double d[3], len = 0.0;
@@ -1008,11 +1017,21 @@ try {
                 tf = std::min(tf, std::max(ta, tb));
             }
             const bool hit = tn <= tf && std::isfinite(tf) && tf > 0.0;
-            w += hit ? std::pow(std::min((double)m.max_steps, (tf - std::max(tn, 0.0)) / step), pw) + kRaySetup
-                     : kRayMiss;
+            w[(size_t)s] += hit ? std::pow(std::min((double)m.max_steps, (tf - std::max(tn, 0.0)) / step), pw) + kRaySetup
+                                : kRayMiss;
         }
-        prefix[(size_t)s + 1] = prefix[(size_t)s] + w;
     }
+    if (prev) {   // measured / modelled time of each previous range, on its strips
+        for (int k = 0; k < parts; ++k) {
+            const int s0 = prev[k] / 8, s1 = std::min(ns, (prev[k + 1] + 7) / 8);
+            double est = 0.0;
+            for (int s = s0; s < s1; ++s) est += w[(size_t)s];
+            if (s1 > s0 && est > 0.0 && prev_ms[k] > 0.0)
+                for (int s = s0; s < s1; ++s) w[(size_t)s] *= prev_ms[k] / est;
+        }
+    }
+    std::vector<double> prefix((size_t)ns + 1, 0.0);
+    for (int s = 0; s < ns; ++s) prefix[(size_t)s + 1] = prefix[(size_t)s] + w[(size_t)s];
     const double total = prefix[(size_t)ns];
     row_begin[0] = 0;
     int j = 0;
@@ -1028,8 +1047,22 @@ try {
     }
     row_begin[parts] = height;
     return VR_OK;
+}
+
+vr_status vr_row_partition(void* p, int width, int height, int parts, int* row_begin)
+try {
+    return row_partition(p, width, height, parts, nullptr, nullptr, row_begin, "vr_row_partition");
 } catch (...) {
     return caught_exception("vr_row_partition");
+}
+
+vr_status vr_row_partition_measured(void* p, int width, int height, int parts, const int* prev_begin,
+                                    const double* prev_ms, int* row_begin)
+try {
+    if (!prev_begin || !prev_ms) return fail(VR_ERR_INVALID, "vr_row_partition_measured: null argument");
+    return row_partition(p, width, height, parts, prev_begin, prev_ms, row_begin, "vr_row_partition_measured");
+} catch (...) {
+    return caught_exception("vr_row_partition_measured");
 }
 
 vr_status vr_set_layout_preference(void* p, int pref)

@@ -34,6 +34,7 @@
 // later collective call on that shard fails at once.
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -1146,7 +1147,16 @@ try {
                              "multiples of 8", R, sh->height);
     }
     if (rb == sh->row_begin) return VR_OK;
-    if (sh->started) return fail(VR_ERR_INVALID, "vr_shard_set_rows: set before the first frames");
+    if (sh->started) {
+        // new ranges between runs (vr_shard_rebalance_rows): the frames in
+        // flight still use the band buffers; the interleaved / row-range mode
+        // itself is fixed once frames are queued
+        if (rb.empty() != sh->row_begin.empty())
+            return fail(VR_ERR_INVALID, "vr_shard_set_rows: band sets or row ranges are chosen before the first frames");
+        for (hipStream_t rs : sh->render_stream) HIP_TRY(hipStreamSynchronize(rs));
+        HIP_TRY(hipStreamSynchronize(sh->comm_stream));
+        HIP_TRY(hipDeviceSynchronize());   // (frames rendered on the caller's stream)
+    }
     sh->row_begin = rb;
     set_geometry(sh, sh->compositor);
     return alloc_band_buffers(sh);
@@ -1154,14 +1164,16 @@ try {
     return caught_exception("vr_shard_set_rows");
 }
 
-// Rank 0's vr_row_partition, on every rank: broadcast with a failure flag
-// (a rank-0 failure reaches every rank after the one collective, not a hang).
-vr_status vr_shard_balance_rows(vr_shard* sh)
-try {
-    if (!sh) return fail(VR_ERR_INVALID, "vr_shard_balance_rows: null");
-    if (sh->loopback && sh->rank != 0 && !sh->solo)
-        return fail(VR_ERR_INVALID, "vr_shard_balance_rows: rank %d is not connected (vr_shard_connect)", sh->rank);
-    SH_TRY(check_usable(sh, "vr_shard_balance_rows"));
+}  // extern "C"
+
+namespace {
+
+// Rank 0's partition, on every rank: broadcast with a failure flag (a rank-0
+// failure reaches every rank after the one collective, not a hang).  all_ms
+// (every rank's measured ms, by rank): vr_row_partition_measured over the
+// current ranges; else vr_row_partition.
+vr_status share_partition(vr_shard* sh, const std::vector<double>* all_ms, const char* fn)
+{
     const int R = renderers(sh);
     std::vector<int> rb((size_t)R + 2, 0);   // [0]: failed, [1..R+1]: row starts
     vr_status mine = VR_OK;
@@ -1174,7 +1186,15 @@ try {
         const int prev = vr_get_option(sh->ctx, "row_first_pct");
         const int pct = sh->compositor ? 100 : std::max(50, 100 - 2 * (sh->nranks - 1));
         (void)vr_set_option(sh->ctx, "row_first_pct", pct);
-        mine = vr_row_partition(sh->ctx, sh->width, sh->height, R, rb.data() + 1);
+        if (all_ms) {
+            std::vector<double> ms((size_t)R, 0.0);
+            for (int r = 0; r < sh->nranks; ++r)
+                if (band_first_of(sh, r) >= 0) ms[(size_t)band_first_of(sh, r)] = (*all_ms)[(size_t)r];
+            mine = vr_row_partition_measured(sh->ctx, sh->width, sh->height, R, sh->row_begin.data(), ms.data(),
+                                             rb.data() + 1);
+        } else {
+            mine = vr_row_partition(sh->ctx, sh->width, sh->height, R, rb.data() + 1);
+        }
         (void)vr_set_option(sh->ctx, "row_first_pct", prev);
         if (mine != VR_OK) {
             msg = vr_last_error();
@@ -1191,29 +1211,82 @@ try {
         if (he == hipSuccess) {
             nr = ncclBroadcast(d, d, rb.size(), ncclInt32, 0, sh->comm, sh->comm_stream);
             if (nr == ncclInProgress) {
-                st = settle(sh, "vr_shard_balance_rows: broadcast");
+                st = settle(sh, fn);
                 nr = ncclSuccess;
             }
         }
         if (he == hipSuccess && nr == ncclSuccess && st == VR_OK)
             he = hipMemcpyAsync(rb.data(), d, rb.size() * sizeof(int), hipMemcpyDeviceToHost, sh->comm_stream);
-        if (he == hipSuccess && nr == ncclSuccess && st == VR_OK)
-            st = wait_stream(sh, sh->comm_stream, "vr_shard_balance_rows: broadcast");
+        if (he == hipSuccess && nr == ncclSuccess && st == VR_OK) st = wait_stream(sh, sh->comm_stream, fn);
         if (!sh->aborted) (void)hipFree(d);
         if (st != VR_OK) return st;
         if (nr != ncclSuccess) {
             abort_comm(sh);
-            return fail(VR_ERR_COMM, "vr_shard_balance_rows: ncclBroadcast: %s", ncclGetErrorString(nr));
+            return fail(VR_ERR_COMM, "%s: ncclBroadcast: %s", fn, ncclGetErrorString(nr));
         }
-        if (he != hipSuccess) return fail(VR_ERR_HIP, "vr_shard_balance_rows: %s", hipGetErrorString(he));
+        if (he != hipSuccess) return fail(VR_ERR_HIP, "%s: %s", fn, hipGetErrorString(he));
     }
     if (rb[0]) {
-        if (mine != VR_OK) return fail(mine, "vr_shard_balance_rows: vr_row_partition: %s", msg.c_str());
-        return fail(VR_ERR_INVALID, "vr_shard_balance_rows: rank 0's partition failed");
+        if (mine != VR_OK) return fail(mine, "%s: %s", fn, msg.c_str());
+        return fail(VR_ERR_INVALID, "%s: rank 0's partition failed", fn);
     }
     return vr_shard_set_rows(sh, rb.data() + 1);
+}
+
+}  // namespace
+
+extern "C" {
+
+vr_status vr_shard_balance_rows(vr_shard* sh)
+try {
+    if (!sh) return fail(VR_ERR_INVALID, "vr_shard_balance_rows: null");
+    if (sh->loopback && sh->rank != 0 && !sh->solo)
+        return fail(VR_ERR_INVALID, "vr_shard_balance_rows: rank %d is not connected (vr_shard_connect)", sh->rank);
+    SH_TRY(check_usable(sh, "vr_shard_balance_rows"));
+    return share_partition(sh, nullptr, "vr_shard_balance_rows");
 } catch (...) {
     return caught_exception("vr_shard_balance_rows");
+}
+
+// Collective: every rank's measured ms (one all-reduce of a vector holding
+// each rank's own entry), then rank 0's measured partition, broadcast.
+vr_status vr_shard_rebalance_rows(vr_shard* sh, double my_ms)
+try {
+    if (!sh || !std::isfinite(my_ms) || my_ms < 0.0) return fail(VR_ERR_INVALID, "vr_shard_rebalance_rows: bad argument");
+    if (sh->loopback) return fail(VR_ERR_INVALID, "vr_shard_rebalance_rows: needs the ranks' times (a connected shard)");
+    if (!rows_mode(sh)) return fail(VR_ERR_INVALID, "vr_shard_rebalance_rows: the shard renders band sets");
+    SH_TRY(check_usable(sh, "vr_shard_rebalance_rows"));
+    HIP_TRY(hipSetDevice(sh->device));
+    std::vector<double> ms((size_t)sh->nranks, 0.0);
+    ms[(size_t)sh->rank] = my_ms;
+    if (sh->nranks > 1) {
+        double* d = nullptr;
+        HIP_TRY(hipMalloc(&d, ms.size() * sizeof(double)));
+        hipError_t he = hipMemcpyAsync(d, ms.data(), ms.size() * sizeof(double), hipMemcpyHostToDevice, sh->comm_stream);
+        vr_status st = VR_OK;
+        ncclResult_t nr = ncclSuccess;
+        if (he == hipSuccess) {
+            nr = ncclAllReduce(d, d, ms.size(), ncclFloat64, ncclSum, sh->comm, sh->comm_stream);
+            if (nr == ncclInProgress) {
+                st = settle(sh, "vr_shard_rebalance_rows: all-reduce");
+                nr = ncclSuccess;
+            }
+        }
+        if (he == hipSuccess && nr == ncclSuccess && st == VR_OK)
+            he = hipMemcpyAsync(ms.data(), d, ms.size() * sizeof(double), hipMemcpyDeviceToHost, sh->comm_stream);
+        if (he == hipSuccess && nr == ncclSuccess && st == VR_OK)
+            st = wait_stream(sh, sh->comm_stream, "vr_shard_rebalance_rows: all-reduce");
+        if (!sh->aborted) (void)hipFree(d);
+        if (st != VR_OK) return st;
+        if (nr != ncclSuccess) {
+            abort_comm(sh);
+            return fail(VR_ERR_COMM, "vr_shard_rebalance_rows: ncclAllReduce: %s", ncclGetErrorString(nr));
+        }
+        if (he != hipSuccess) return fail(VR_ERR_HIP, "vr_shard_rebalance_rows: %s", hipGetErrorString(he));
+    }
+    return share_partition(sh, &ms, "vr_shard_rebalance_rows");
+} catch (...) {
+    return caught_exception("vr_shard_rebalance_rows");
 }
 
 int vr_shard_partition(vr_shard* sh)

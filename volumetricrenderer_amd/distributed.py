@@ -287,7 +287,7 @@ class RcclBandPipeline:
     def __init__(self, renderer, width: int, height: int, fmt: int, band_rows: int = 16, world: int = 1,
                  rank: int = 0, group=None, loopback: bool = False, timeout_s: float | None = None,
                  render_streams: int = 2, solo: bool = False, host_threads: int = 1, exchange_on_render: bool = True,
-                 compositor: bool | None = None, partition: str = "auto"):
+                 compositor: bool | None = None, partition: str = "auto", rows: list[int] | None = None):
         """loopback: one process renders all `world` ranks' band sets on its
         GPU and assembles them (no communicator; tests and rehearsals).
         solo (loopback only, any rank): each frame renders only this rank's
@@ -308,6 +308,8 @@ class RcclBandPipeline:
         more than 2560 x 1440 pixels (config 4 at 8 ranks: 0.0480 ms per frame
         against 0.0562 with 16-row bands; equal or slightly slower at 2 and 4
         ranks), else "bands".
+        rows: explicit row starts for partition "rows" (renderers + 1 entries,
+        vr_shard_set_rows; every rank the same) instead of the balanced split.
         exchange_on_render: True (default) = each frame's exchange follows its
         render on the frame's render stream, over a communicator per buffer
         parity, with no events; False = on a communication stream, ordered by
@@ -388,6 +390,11 @@ class RcclBandPipeline:
         self.partition = (("rows" if world >= 8 and width * height > 2560 * 1440 else "bands") if partition == "auto"
                           else partition)
         self._balanced = self.partition == "bands"
+        if rows is not None:
+            if self.partition != "rows":
+                raise ValueError("RcclBandPipeline: rows needs partition 'rows'")
+            _lib.shard_call("vr_shard_set_rows", h, (ctypes.c_int * len(rows))(*rows))
+            self._balanced = True
         self._geometry()
 
     def _geometry(self) -> None:
@@ -404,6 +411,18 @@ class RcclBandPipeline:
             r0, n = ctypes.c_int(), ctypes.c_int()
             _lib.shard_call("vr_shard_row_range", h, self.rank, ctypes.byref(r0), ctypes.byref(n))
             self.row_range = (r0.value, n.value)
+
+    def rebalance_rows(self, frames: int = 16, stream=None) -> list[int]:
+        """Collective, with row ranges: render `frames` frames with every
+        render sampled, then split the frame again by every rank's measured
+        render time (vr_shard_rebalance_rows).  Returns the new row starts
+        (this rank's view: its own range is self.row_range)."""
+        if self.partition != "rows":
+            raise ValueError("rebalance_rows: the pipeline renders band sets")
+        ms = self.run_frames(frames, stream=stream, sample_every=1)
+        _lib.shard_call("vr_shard_rebalance_rows", self._h, float(ms))
+        self._geometry()
+        return self.row_range
 
     def balance_rows(self) -> None:
         """Collective: contiguous row ranges of equal estimated work for the

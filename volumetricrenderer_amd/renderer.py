@@ -315,6 +315,15 @@ class Renderer:
         call("vr_row_partition", self._ctx, width, height, parts, rb)
         return list(rb)
 
+    def row_partition_measured(self, width: int, height: int, prev: list[int], prev_ms: list[float]) -> list[int]:
+        """vr_row_partition_measured: the split again, range k of `prev` having
+        taken prev_ms[k]."""
+        parts = len(prev) - 1
+        rb = (ctypes.c_int * (parts + 1))()
+        call("vr_row_partition_measured", self._ctx, width, height, parts, (ctypes.c_int * (parts + 1))(*prev),
+             (ctypes.c_double * parts)(*prev_ms), rb)
+        return list(rb)
+
     def render_sequence(self, width: int, height: int, fmt: int, out: torch.Tensor, cameras, band_rows: int = 0,
                         band_stride: int = 1, band_first: int = 0, stream=None) -> torch.Tensor:
         """The reference's frame loop with a moving camera (TestMain.cpp:173-256):
