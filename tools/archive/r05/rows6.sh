@@ -1,0 +1,12 @@
+#!/bin/bash
+set -o pipefail
+cd "$(dirname "$0")/../../.."
+O=gpurun_out/r05
+mkdir -p $O
+export PYTHONUNBUFFERED=1 TMPDIR=/tmp
+for o in "--opt row_model=1" "--opt row_model=1 --opt row_pow=100 --opt row_setup=20" "--opt row_model=1 --opt row_pow=115 --opt row_setup=40" "--opt row_model=0"; do
+  echo "== rows $o"
+  timeout -k 10 300 python -u tools/band_scaling.py --native --all-ranks --ns 8 --streams 2 --size 128 --width 3840 --height 2160 \
+      --steps 256 --frames 40 --rounds 3 --partition rows $o > $O/rows6.txt 2>&1 || { cat $O/rows6.txt; exit 3; }
+  grep -v amdgpu.ids $O/rows6.txt | grep -A1 "N="
+done
