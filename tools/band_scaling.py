@@ -43,6 +43,8 @@ def main():
     ap.add_argument("--compositor", default="auto", choices=["auto", "on", "off"],
                     help="--native: rank 0 renders no bands and only assembles (vr_shard_set_compositor; auto: the "
                          "library's default, on from 8 ranks)")
+    ap.add_argument("--rows", action="append", default=[],
+                    help="--native, row ranges: explicit row starts (comma list, renderers + 1 entries); repeatable")
     ap.add_argument("--rebalance", action="store_true",
                     help="--native --all-ranks, row ranges: a second pass with the ranges split again by every "
                          "rank's measured render time (vr_row_partition_measured, as vr_shard_rebalance_rows does)")
@@ -121,7 +123,11 @@ def native(a):
               f"variant {r.kernel_variant} {' '.join(a.opt)}", flush=True)
         streams = [int(v) for v in a.streams.split(",")]
         base = {}
-        for n in [int(v) for v in a.ns.split(",")]:
+        for rows in a.rows:
+            rl = [int(v) for v in rows.split(",")]
+            print(f"  rows {rl}", flush=True)
+            one_n(a, r, W, H, len(rl) - 1 + (1 if a.compositor == "on" else 0), streams, base, rl)
+        for n in ([] if a.rows else [int(v) for v in a.ns.split(",")]):
             info = one_n(a, r, W, H, n, streams, base, None)
             if a.rebalance and a.all_ranks and n > 1 and info["ranges"]:
                 first_r = min(info["ranges"])   # 0, or 1 with rank 0 as a compositor
