@@ -303,9 +303,10 @@ def main() -> int:
     ap.add_argument("--inflight", type=int, default=1, choices=[1, 2],
                     help="N = 1, grid medium: 2 = consecutive frames alternate two streams and targets (throughput "
                          "mode; per-launch kernel times then overlap the next frame)")
-    ap.add_argument("--render-streams", type=int, default=2, choices=[1, 2],
-                    help="N > 1 (native loop): 2 = consecutive frames render on two alternating streams and overlap "
-                         "(vr_shard_set_render_streams; the default), 1 = one render stream")
+    ap.add_argument("--render-streams", type=int, default=None, choices=[1, 2, 3, 4],
+                    help="native loop: n = 2..4 consecutive frames render on n alternating streams and overlap "
+                         "(vr_shard_set_render_streams), 1 = one render stream; default: RcclBandPipeline's (3 for "
+                         "frames above 2560x1440, else 2)")
     ap.add_argument("--exchange", default="render", choices=["render", "comm"],
                     help="N > 1 (native loop, 2 render streams): each frame's exchange on its render stream, over one "
                          "communicator per buffer parity, no events (the default), or on a communication stream "
@@ -579,7 +580,8 @@ def main() -> int:
                                 + (", host-staged: band sets copied through host memory)" if backend == "gloo"
                                    else ", device buffers)"))
     # vr_shard_run_frames renders a procedural medium on one stream (its frames cannot overlap)
-    streams_eff = 1 if proc is not None else args.render_streams
+    rs = pipe.render_streams if pipe is not None else (args.render_streams or 1)
+    streams_eff = 1 if proc is not None else rs
     if rank == 0:
         ms_per_step = el / args.steps * 1e3
         value = W * H * S * args.steps / el / 1e6
@@ -659,7 +661,7 @@ def main() -> int:
                        "kernel": r.kernel_variant + ("_deferred" if proc is not None and shadow > 0
                                                       and r.get_option("shadow_defer") == 1 else ""),
                        "parallelism": (("one GPU, the native frame loop (libvr_shard, one-rank communicator)"
-                                        + (", 2 render streams: 2 frames in flight" if streams_eff == 2
+                                        + (f", {streams_eff} render streams: {streams_eff} frames in flight" if streams_eff >= 2
                                            else ", 1 render stream (a procedural medium's frames do not overlap)"
                                            if proc is not None else ", 1 render stream"))
                                        if native and world == 1 else
@@ -668,9 +670,9 @@ def main() -> int:
                                         else (f"row ranges x{world}" if rows_part else f"bands16x{world}"))
                                        + (", 2 frames in flight (two streams and targets)"
                                           if args.inflight == 2 or proc_inflight2 else "")
-                                       + (f", {args.render_streams} render stream{'s' if args.render_streams > 1 else ''}"
+                                       + (f", {rs} render stream{'s' if rs > 1 else ''}"
                                           + (f", exchange on {args.exchange} stream{'s' if args.exchange == 'render' else ''}"
-                                             if args.render_streams == 2 else "")
+                                             if rs >= 2 else "")
                                           if native else "")),
                        "collective": collective_label,
                        "executed_steps_per_frame": frame_steps},

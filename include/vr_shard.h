@@ -131,8 +131,10 @@ vr_status vr_shard_rows(vr_shard* sh, int* my_rows, int* rows_per_rank);
  * instead of waiting forever.  Every later collective on the shard fails at
  * once (vr_shard_aborted = 1); vr_shard_destroy still frees it. */
 vr_status vr_shard_set_timeout(vr_shard* sh, double seconds);
-/* Render streams of vr_shard_run: 2 (the default) = two streams of the shard,
- * alternating by buffer parity, renders of consecutive frames overlap;
+/* Render streams of vr_shard_run, 1 to 4: n >= 2 = frame i renders on stream
+ * i mod n of the shard with buffer set i mod n, so n consecutive frames are in
+ * flight and their renders overlap (with the exchange on the render streams;
+ * on the communication stream at most 2); the default is 2;
  * 1 = every render on the caller's stream, after the previous one.  Results
  * are identical.  Switching waits (host) for the frames in flight.  A
  * procedural medium with shadow rays always takes one stream: each of its

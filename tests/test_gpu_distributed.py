@@ -76,8 +76,9 @@ def test_gloo_ranks_on_one_gpu_assemble_the_frame(world, share):
     assert all(r == ("ok", True) for r in res), res
 
 
-@pytest.mark.parametrize("fmt,band_rows,on_render", [(1, 16, False), (0, 8, False), (1, 16, True)])
-def test_rccl_pipeline_one_rank(fmt, band_rows, on_render):
+@pytest.mark.parametrize("fmt,band_rows,on_render,streams", [(1, 16, False, 2), (0, 8, False, 2), (1, 16, True, 2),
+                                                             (1, 16, True, 4)])
+def test_rccl_pipeline_one_rank(fmt, band_rows, on_render, streams):
     """The native frame loop (libvr_shard.so) with a one-rank RCCL
     communicator: render into the gather slot, (no peers), assemble, 2 frames
     in flight.  The frame equals a plain render; the kernel-time sample is
@@ -92,7 +93,8 @@ def test_rccl_pipeline_one_rank(fmt, band_rows, on_render):
         osd, gsd = vr.reference_shader_data(W / H, 10.0, 20.0)
         r.set_shader_data(osd, gsd)
         r.set_march(vr.march_defaults())
-        pl = RcclBandPipeline(r, W, H, fmt, band_rows=band_rows, world=1, rank=0, exchange_on_render=on_render)
+        pl = RcclBandPipeline(r, W, H, fmt, band_rows=band_rows, world=1, rank=0, exchange_on_render=on_render,
+                              render_streams=streams)
         try:
             assert pl.my_rows == pl.rows_per_rank == vr.band_rows_packed(H, band_rows, 1, 0) >= H
             ms = pl.run_frames(5, sample_every=2)
@@ -177,7 +179,7 @@ def test_rccl_init_deadline_when_a_peer_never_joins():
             _lib.shard_call("vr_shard_destroy", h)
 
 
-@pytest.mark.parametrize("render_streams", [1, 2])
+@pytest.mark.parametrize("render_streams", [1, 2, 3, 4])
 @pytest.mark.parametrize("world,band_rows,fmt,W", [(2, 16, 1, 500), (3, 16, 0, 500), (8, 16, 1, 500), (5, 7, 1, 500),
                                                    (3, 16, 2, 499), (4, 16, 0, 499)])
 def test_native_pipeline_loopback_ranks(world, band_rows, fmt, W, render_streams):
@@ -212,8 +214,8 @@ def test_native_pipeline_loopback_ranks(world, band_rows, fmt, W, render_streams
 
 
 @pytest.mark.parametrize("world,compositor,fmt,W,render_streams", [(2, False, 1, 500, 2), (5, False, 0, 499, 1),
-                                                                   (8, True, 1, 500, 2), (8, False, 2, 500, 2),
-                                                                   (3, True, 1, 499, 1)])
+                                                                   (8, True, 1, 500, 2), (8, False, 2, 500, 4),
+                                                                   (3, True, 1, 499, 3)])
 def test_native_pipeline_loopback_row_ranges(world, compositor, fmt, W, render_streams):
     """The loop's contiguous row ranges (vr_shard_balance_rows): every
     renderer's range rendered by this process into a grey frame, rank 0's
@@ -306,7 +308,7 @@ SPIN_DEG = 1.6   # TestMain.cpp:171-184, :222-224: the held A/D key, 100 deg/s x
 @pytest.mark.parametrize("fmt,render_streams,threads,on_render,compositor",
                          [(0, 2, 1, False, None), (1, 2, 1, False, None), (1, 1, 1, False, None),
                           (1, 2, 2, False, None), (0, 2, 1, True, None), (1, 2, 1, True, False),
-                          (1, 1, 1, True, True)])
+                          (1, 1, 1, True, True), (1, 3, 1, True, None), (0, 4, 1, True, False)])
 def test_native_loopback_spinning_8_ranks(oracle, fmt, render_streams, threads, on_render, compositor):
     """A moving camera through the native 8-rank frame loop (loopback: this
     process renders every rank's interleaved band set): 40 frames, frame i

@@ -21,6 +21,8 @@ timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-other-configs --n1-l
 timeout -k 10 400 python -u tools/band_scaling.py --native --all-ranks --ns 1,2,4,8 --streams 2 --frames 100 --rounds 3 \
     > $O/final_native_c5.txt 2>&1; rc=$?
 grep -v amdgpu.ids $O/final_native_c5.txt; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 400 python -u tools/band_scaling.py --native --all-ranks --ns 1,8 --streams 2 --size 128 --width 3840 \
+timeout -k 10 400 python -u tools/band_scaling.py --native --all-ranks --ns 1,2,4,8 --streams 3 --size 128 --width 3840 \
     --height 2160 --steps 256 --frames 40 --rounds 3 > $O/final_native_c4.txt 2>&1; rc=$?
-grep -v amdgpu.ids $O/final_native_c4.txt; exit $rc
+grep -v amdgpu.ids $O/final_native_c4.txt; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u bench.py --config grid4k --no-cpu-baseline > $O/final_bench_grid4k.json 2> $O/final_bench_grid4k.err; rc=$?
+tail -c 300 $O/final_bench_grid4k.json; exit $rc

@@ -53,6 +53,9 @@
 
 static_assert(sizeof(ncclUniqueId) == VR_SHARD_ID_BYTES, "ncclUniqueId size");
 
+// frames in flight per rank, at most (vr_shard_set_render_streams)
+constexpr int kMaxFramesInFlight = 4;
+
 namespace {
 
 thread_local std::string g_err;
@@ -167,7 +170,9 @@ struct vr_shard {
     bool started = false;             // a run has queued frames (the geometry is fixed)
     ncclComm_t comm = nullptr;
     hipStream_t comm_stream = nullptr;
-    hipStream_t render_stream[2] = {};   // one per parity (render_streams == 2)
+    // render streams: frame i renders on stream i mod render_streams with the
+    // buffer set of that index (the comm-stream paths use at most 2)
+    hipStream_t render_stream[kMaxFramesInFlight] = {};
     int render_streams = 2;           // 1: every frame renders on the caller's stream
     int host_threads = 1;             // 2: a second host thread issues the exchange half of every frame
     // exchange on the render streams (vr_shard_set_exchange_streams): frame i's
@@ -176,15 +181,16 @@ struct vr_shard {
     // p = 1, split from comm at the first such run), with no events at all
     bool on_render = true;   // vr_shard_set_exchange_streams
     ncclComm_t comm2 = nullptr;
-    uint8_t* local[2] = {};           // rank > 0: band sets (gformat)
-    uint8_t* gathered[2] = {};        // rank 0: nranks slots of rows_per_rank rows (gformat)
-    uint8_t* frame[2] = {};           // rank 0
-    hipEvent_t rendered[2] = {}, done[2] = {};
-    hipEvent_t tail[2] = {};          // rank 0: the end of the render streams' frames (vr_shard_run_frames)
+    ncclComm_t comm_more[kMaxFramesInFlight - 2] = {};   // streams 2.. (split like comm2)
+    uint8_t* local[kMaxFramesInFlight] = {};      // rank > 0: band sets (gformat)
+    uint8_t* gathered[kMaxFramesInFlight] = {};   // rank 0: nranks slots of rows_per_rank rows (gformat)
+    uint8_t* frame[kMaxFramesInFlight] = {};      // rank 0
+    hipEvent_t rendered[kMaxFramesInFlight] = {}, done[kMaxFramesInFlight] = {};
+    hipEvent_t tail[kMaxFramesInFlight] = {};     // the end of the render streams' frames (vr_shard_run_frames)
     hipEvent_t fence = nullptr;       // vr_shard_barrier: the caller's stream -> comm stream
     int* token = nullptr;             // [0]: vr_shard_barrier's all-reduced int; [1..7]:
                                       // vr_shard_share_volume's agreement vector
-    bool pending[2] = {};             // done[p] recorded and not yet waited on
+    bool pending[kMaxFramesInFlight] = {};        // done[p] recorded and not yet waited on
     int last = -1;                    // parity of the last frame
     bool loopback = false;            // one process emulates all ranks (no RCCL)
     bool solo = false;                // loopback rehearsal of one rank: its own band set only, no exchange
@@ -197,6 +203,12 @@ namespace {
 
 void abort_comm(vr_shard* sh)
 {
+    if (sh)
+        for (ncclComm_t& c : sh->comm_more)
+            if (c) {
+                (void)ncclCommAbort(c);
+                c = nullptr;
+            }
     if (sh && sh->comm2) {
         (void)ncclCommAbort(sh->comm2);
         sh->comm2 = nullptr;
@@ -213,7 +225,8 @@ int comm_state(vr_shard* sh)
 {
     if (!sh->comm) return sh->aborted ? 2 : 0;
     int st = 0;
-    for (ncclComm_t c : {sh->comm, sh->comm2}) {
+    for (int i = -2; i < kMaxFramesInFlight - 2; ++i) {
+        const ncclComm_t c = i == -2 ? sh->comm : i == -1 ? sh->comm2 : sh->comm_more[i];
         if (!c) continue;
         ncclResult_t r = ncclSuccess;
         if (ncclCommGetAsyncError(c, &r) != ncclSuccess) return 2;
@@ -289,7 +302,7 @@ void release(vr_shard* sh)
     for (hipStream_t rs : sh->render_stream)
         if (rs) (void)hipStreamSynchronize(rs);
     if (sh->comm_stream) (void)hipStreamSynchronize(sh->comm_stream);
-    for (int p = 0; p < 2; ++p) {
+    for (int p = 0; p < kMaxFramesInFlight; ++p) {
         if (sh->local[p]) (void)hipFree(sh->local[p]);
         if (sh->gathered[p]) (void)hipFree(sh->gathered[p]);
         if (sh->frame[p]) (void)hipFree(sh->frame[p]);
@@ -300,6 +313,8 @@ void release(vr_shard* sh)
     for (hipEvent_t e : sh->timing) (void)hipEventDestroy(e);
     if (sh->fence) (void)hipEventDestroy(sh->fence);
     if (sh->token) (void)hipFree(sh->token);
+    for (ncclComm_t c : sh->comm_more)
+        if (c) (void)ncclCommDestroy(c);
     if (sh->comm2) (void)ncclCommDestroy(sh->comm2);
     if (sh->comm) (void)ncclCommDestroy(sh->comm);   // an aborted communicator is already gone
     if (sh->comm_stream) (void)hipStreamDestroy(sh->comm_stream);
@@ -476,7 +491,7 @@ vr_status one_frame_on_render(vr_shard* sh, int p, hipStream_t rs, hipEvent_t t0
         }
     }
     if (sh->nranks > 1 && !sh->loopback) {
-        ncclComm_t c = p == 0 ? sh->comm : sh->comm2;
+        ncclComm_t c = p == 0 ? sh->comm : p == 1 ? sh->comm2 : sh->comm_more[p - 2];
         NCCL_TRY(ncclGroupStart());
         if (r0) {
             for (int r = 1; r < sh->nranks; ++r)
@@ -523,7 +538,7 @@ void set_geometry(vr_shard* sh, bool compositor)
 // rank 0's gather slots / another rank's band sets, for the current geometry
 vr_status alloc_band_buffers(vr_shard* sh)
 {
-    for (int p = 0; p < 2; ++p) {
+    for (int p = 0; p < kMaxFramesInFlight; ++p) {
         uint8_t*& b = sh->rank == 0 ? sh->gathered[p] : sh->local[p];
         if (b) (void)hipFree(b);
         b = nullptr;
@@ -612,7 +627,7 @@ try {
     hip_ok(hipEventCreateWithFlags(&sh->fence, hipEventDisableTiming), "event");
     if (hip_ok(hipMalloc(&sh->token, 8 * sizeof(int)), "barrier token"))
         hip_ok(hipMemset(sh->token, 0, 8 * sizeof(int)), "barrier token");
-    for (int p = 0; p < 2 && st == VR_OK; ++p) {
+    for (int p = 0; p < kMaxFramesInFlight && st == VR_OK; ++p) {
         hip_ok(hipEventCreateWithFlags(&sh->rendered[p], hipEventDisableTiming), "event");
         hip_ok(hipEventCreateWithFlags(&sh->done[p], hipEventDisableTiming), "event");
         hip_ok(hipEventCreateWithFlags(&sh->tail[p], hipEventDisableTiming), "event");
@@ -717,7 +732,9 @@ try {
     // a procedural medium with deferred shadow rays writes the ctx's scratch
     // every frame, so its frames cannot overlap (vr_render orders them across
     // streams): one render stream, without the cross-stream waits
-    const bool two = sh->render_streams == 2 && vr_get_option(sh->ctx, "procedural") != 2;
+    const int P = vr_get_option(sh->ctx, "procedural") == 2 ? 1
+                  : sh->on_render ? sh->render_streams : std::min(sh->render_streams, 2);
+    const bool two = P >= 2;   // frames overlap on P render streams
     if (frames > 0) sh->started = true;   // the band geometry is fixed from here
     // two render streams: tell the ctx its consecutive renders overlap (its
     // auto split rule), for this run
@@ -739,37 +756,40 @@ try {
     }
     const bool on_render = sh->on_render && two;
     if (on_render && frames > 0) {
-        // the parity-1 communicator, once, split from the first (collective:
-        // every rank runs its first such frames together; a one-rank
-        // communicator splits too, so its test covers the call)
-        if (!sh->loopback && !sh->comm2) {
+        // the communicators of streams 1..P-1, once each, split from the
+        // first (collective: every rank runs its first such frames together,
+        // in the same order; a one-rank communicator splits too, so its test
+        // covers the call)
+        for (int q = 1; q < P && !sh->loopback; ++q) {
+            ncclComm_t& cq = q == 1 ? sh->comm2 : sh->comm_more[q - 2];
+            if (cq) continue;
             ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
             cfg.blocking = 0;
-            const ncclResult_t r = ncclCommSplit(sh->comm, 0, sh->rank, &sh->comm2, &cfg);
+            const ncclResult_t r = ncclCommSplit(sh->comm, 0, sh->rank, &cq, &cfg);
             if (r != ncclSuccess && r != ncclInProgress) {
-                sh->comm2 = nullptr;
+                cq = nullptr;
                 abort_comm(sh);
                 return fail(VR_ERR_COMM, "vr_shard_run: ncclCommSplit: %s; communicator aborted", ncclGetErrorString(r));
             }
             SH_TRY(settle(sh, "vr_shard_run: ncclCommSplit"));
         }
-        // the parities' buffers were last used by frames of the comm-stream
-        // path, if any: their exchanges must be done
-        for (int q = 0; q < 2; ++q)
+        // the buffer sets were last used by frames of the comm-stream path,
+        // if any: their exchanges must be done
+        for (int q = 0; q < kMaxFramesInFlight; ++q)
             if (sh->pending[q]) {
                 for (hipStream_t rs : sh->render_stream) HIP_TRY(hipStreamWaitEvent(rs, sh->done[q], 0));
                 sh->pending[q] = false;
             }
         for (int i = 0; i < frames; ++i) {
-            const int p = sh->last < 0 ? 0 : sh->last ^ 1;
+            const int p = sh->last < 0 ? 0 : (sh->last + 1) % P;
             const bool samp = kernel_ms && i % sample_every == 0;
             hipEvent_t t0 = samp ? sh->timing[2 * next] : nullptr, t1 = samp ? sh->timing[2 * next + 1] : nullptr;
             if (samp) ++next;
             if (osd) VR_TRY(vr_set_shader_data(sh->ctx, &osd[i], &gsd[i]));   // this frame's camera
             SH_TRY(one_frame_on_render(sh, p, sh->render_stream[p], t0, t1));
         }
-        // join: the caller's stream after both render streams' last frames
-        for (int q = 0; q < 2; ++q) {
+        // join: the caller's stream after every render stream's last frame
+        for (int q = 0; q < P; ++q) {
             HIP_TRY(hipEventRecord(sh->tail[q], sh->render_stream[q]));
             HIP_TRY(hipStreamWaitEvent(s, sh->tail[q], 0));
             // a later comm-stream frame of parity q waits for this one
@@ -783,7 +803,7 @@ try {
         // Frame i's exchange is issued after its render (rendered[p] recorded);
         // frame i's render after frame i-2's exchange (done[p] recorded, and
         // rendered[p] no longer awaited).
-        const int p0 = sh->last < 0 ? 0 : sh->last ^ 1;
+        const int p0 = sh->last < 0 ? 0 : (sh->last + 1) % 2;
         std::atomic<int> rdone{0}, cdone{0};
         std::atomic<bool> stop{false};
         vr_status wst = VR_OK;
@@ -833,7 +853,7 @@ try {
         sh->last = (p0 + frames - 1) & 1;
     } else {
         for (int i = 0; i < frames; ++i) {
-            const int p = sh->last < 0 ? 0 : sh->last ^ 1;
+            const int p = sh->last < 0 ? 0 : (sh->last + 1) % 2;
             const bool samp = kernel_ms && i % sample_every == 0;
             hipEvent_t t0 = samp ? sh->timing[2 * next] : nullptr, t1 = samp ? sh->timing[2 * next + 1] : nullptr;
             if (samp) ++next;
@@ -850,7 +870,7 @@ try {
             HIP_TRY(hipEventRecord(sh->done[sh->last], sh->comm_stream));
             sh->pending[sh->last] = true;
             if (two)
-                for (int q = 0; q < 2; ++q) {
+                for (int q = 0; q < 2; ++q) {   // (the comm-stream paths use streams 0 and 1)
                     HIP_TRY(hipEventRecord(sh->tail[q], sh->render_stream[q]));
                     HIP_TRY(hipStreamWaitEvent(s, sh->tail[q], 0));
                 }
@@ -1001,11 +1021,12 @@ try {
 
 vr_status vr_shard_set_render_streams(vr_shard* sh, int n)
 try {
-    if (!sh || (n != 1 && n != 2)) return fail(VR_ERR_INVALID, "vr_shard_set_render_streams: need a shard and n = 1 or 2");
+    if (!sh || n < 1 || n > kMaxFramesInFlight)
+        return fail(VR_ERR_INVALID, "vr_shard_set_render_streams: need a shard and n in 1..%d", kMaxFramesInFlight);
     if (n != sh->render_streams && sh->last >= 0) {
         // frames of the old arrangement may still be in flight: the next
-        // frame's stream must see them (each parity's done[] covers its render)
-        for (int p = 0; p < 2; ++p)
+        // frame's stream must see them (each set's done[] covers its render)
+        for (int p = 0; p < kMaxFramesInFlight; ++p)
             if (sh->pending[p]) SH_TRY(wait_event(sh, sh->done[p], "vr_shard_set_render_streams"));
     }
     sh->render_streams = n;

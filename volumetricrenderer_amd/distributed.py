@@ -286,16 +286,19 @@ class RcclBandPipeline:
 
     def __init__(self, renderer, width: int, height: int, fmt: int, band_rows: int = 16, world: int = 1,
                  rank: int = 0, group=None, loopback: bool = False, timeout_s: float | None = None,
-                 render_streams: int = 2, solo: bool = False, host_threads: int = 1, exchange_on_render: bool = True,
+                 render_streams: int | None = None, solo: bool = False, host_threads: int = 1, exchange_on_render: bool = True,
                  compositor: bool | None = None, partition: str = "auto", rows: list[int] | None = None):
         """loopback: one process renders all `world` ranks' band sets on its
         GPU and assembles them (no communicator; tests and rehearsals).
         solo (loopback only, any rank): each frame renders only this rank's
         band set, without an exchange -- one rank's frame period on one GPU
         (vr_shard_set_solo; tools/band_scaling.py --native).
-        render_streams: 2 (default) = consecutive frames render on two
-        alternating streams and overlap; 1 = on the caller's stream, in turn
-        (vr_shard_set_render_streams).
+        render_streams: n = 2..4 consecutive frames render on n alternating
+        streams and overlap; 1 = on the caller's stream, in turn
+        (vr_shard_set_render_streams).  None (default): 3 for frames of more
+        than 2560 x 1440 pixels (config 4 at 8 ranks: 0.0431 ms per frame
+        against 0.0486 with 2; 4 streams exceed the process's 4 hardware
+        queues and lose), else 2 (config 5: equal).
         host_threads: 2 = a worker thread issues every frame's exchange half
         (vr_shard_set_host_threads).
         compositor: rank 0 renders no bands and only assembles, ranks 1..N-1
@@ -368,6 +371,8 @@ class RcclBandPipeline:
         if timeout_s is not None:
             _lib.shard_call("vr_shard_set_timeout", h, float(timeout_s))
         try:
+            if render_streams is None:
+                render_streams = 3 if width * height > 2560 * 1440 else 2
             _lib.shard_call("vr_shard_set_render_streams", h, int(render_streams))
             _lib.shard_call("vr_shard_set_host_threads", h, int(host_threads))
             _lib.shard_call("vr_shard_set_exchange_streams", h, 1 if exchange_on_render else 0)
