@@ -588,7 +588,7 @@ def main() -> int:
         variant = r.kernel_variant
         # two render streams (native loop, N > 1): a launch overlaps the next, so
         # its duration is not a frame's -- the roofline takes the wall time per frame
-        overlap = (native and streams_eff == 2) or proc_inflight2 or (world == 1 and args.inflight == 2)
+        overlap = (native and streams_eff >= 2) or proc_inflight2 or (world == 1 and args.inflight == 2)
         roof_ms = ms_per_step if overlap else kern_ms
         compositor = native and pipe is not None and pipe.compositor
         rows_part = native and pipe is not None and pipe.partition == "rows"
@@ -601,7 +601,7 @@ def main() -> int:
         else:
             roofline = roofline_of(r, proc, shadow, variant, local_steps, local_evals, local_cells, roof_ms)
         if overlap:
-            roofline["achieved_def"] += ("; renders overlap (two render streams, vr_shard_set_render_streams), so "
+            roofline["achieved_def"] += (f"; renders overlap ({streams_eff} render streams or two in flight), so "
                                          "the time is the wall time per frame of the timed window, not a launch's "
                                          "duration (kernel_ms_mean: the overlapping launches' mean)")
         if roofline["bound"] == "hbm":
