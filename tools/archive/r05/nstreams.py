@@ -2,7 +2,7 @@
 (prepare_render launchers, no exchange): does a third frame in flight help?"""
 import os, sys
 import numpy as np, torch
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))))
 import volumetricrenderer_amd as vr
 for size, W, H, S, stride, first in ((512, 1920, 1080, 128, 7, 0), (128, 3840, 2160, 256, 8, 1), (512, 1920, 1080, 128, 1, 0)):
     with vr.Renderer(0) as r:
