@@ -182,7 +182,70 @@ def cpu_baseline(volume_host, osd, gsd, march, width, height, budget_s=10.0, pro
                       f"executed steps/s {steps / el:.4g}"}
 
 
-def other_config(name, steps, warmup):
+def clock_warm(launch, ms, chunk=8):
+    """Declared pre-warm (bench.py --clock-warm-ms, verdict r05 #1): queue
+    frames in chunks until `ms` of continuous load have passed on the host
+    clock, before the --warmup frames.  The GPU's frame period settles over
+    the first ~20-40 ms of load, after an idle gap or host-side set-up alike,
+    while the sampled shader clock reads ~2.35-2.4 GHz throughout
+    (profiles/r06/warmup_trace.txt), so a frame count cannot size it.
+    Returns the frames it queued."""
+    if ms <= 0:
+        return 0
+    n = 0
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < ms:
+        for _ in range(chunk):
+            launch()
+        n += chunk
+        torch.cuda.synchronize()
+    return n
+
+
+def clock_warm_ranks(run8, settle, ms, world, dev="cpu"):
+    """clock_warm for a collective frame loop: one timed chunk of 8 frames
+    sizes the rest, agreed over the ranks (every rank must queue the same
+    frames).  Returns the frames queued."""
+    if ms <= 0:
+        return 0
+    run8()      # the first chunk may pay one-time set-up (e.g. the frame loop's communicator split)
+    settle()
+    t0 = time.perf_counter()
+    run8()      # the second sizes the rest
+    settle()
+    chunks = max(0, int(np.ceil(ms / max(1e-3, (time.perf_counter() - t0) * 1e3))) - 1)
+    if world > 1:
+        ct = torch.tensor([chunks], dtype=torch.int64, device=dev)
+        dist.all_reduce(ct, op=dist.ReduceOp.MAX)
+        chunks = int(ct.item())
+    for _ in range(chunks):
+        run8()
+    settle()
+    return 8 * (chunks + 2)
+
+
+def clock_warm_obj(ms, frames):
+    return {"ms": ms, "frames": frames,
+            "def": "untimed frames of this config queued back to back for this many ms of continuous load before "
+                   "the --warmup frames (the frame period settles over the first ~20-40 ms of load; "
+                   "profiles/r06/warmup_trace.txt)"}
+
+
+def frame_check_of(got, ref):
+    """'exact' when the pipeline's frame equals a plain one-GPU render
+    bit for bit, else a description of the mismatch (bench.py exits 4)."""
+    torch.cuda.synchronize()
+    a, b = got.cpu().numpy(), ref.cpu().numpy()
+    if a.shape != b.shape:
+        return f"MISMATCH: shape {a.shape} vs {b.shape}"
+    bad = np.any(a != b, axis=-1) if a.ndim == 3 else a != b
+    if not bad.any():
+        return "exact"
+    rows = np.nonzero(bad.any(axis=1))[0]
+    return f"MISMATCH: {int(bad.sum())} pixels differ in {rows.size} rows (first row {int(rows[0])})"
+
+
+def other_config(name, steps, warmup, warm_ms=0.0):
     """Time one more BASELINE config on this GPU in the same process, after the
     headline window (verdict r03 #6): ms/frame, kernel ms (HIP events on its
     stream, every 4th frame), the roofline object.  Returns the result and the
@@ -214,6 +277,7 @@ def other_config(name, steps, warmup):
         evals, cells = (units(1), units(2)) if proc is not None else (nsteps, None)
         r.set_option("count", 0)
         launch = r.prepare_render(W, H, fmt, out)
+        warm_frames = clock_warm(launch, warm_ms)
         for _ in range(warmup):
             launch()
         torch.cuda.synchronize()
@@ -259,6 +323,7 @@ def other_config(name, steps, warmup):
                           "kernel": variant + ("_deferred" if defer else ""),
                           "executed_steps_per_frame": nsteps},
                "roofline": roofline_of(r, proc, shadow, variant, nsteps, evals, cells, kern_ms),
+               "clock_warm": clock_warm_obj(warm_ms, warm_frames),
                **({"frames_in_flight_2": inflight2} if inflight2 else {})}
         if defer:
             res["shadow_defer_scratch_MB"] = round(r.get_option("shadow_defer_kib") / 1024.0, 1)
@@ -277,7 +342,10 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--clock-warm-ms", type=float, default=150.0,
+                    help="before each config's --warmup frames, queue untimed frames for this many ms of continuous "
+                         "load (declared in the line as clock_warm; 0 = off)")
     ap.add_argument("--config", default="grid512", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
@@ -403,6 +471,10 @@ def main() -> int:
     # launch durations the roofline uses.  Two event records per frame cost a
     # few microseconds of queue time between frames (and, at N > 1, host time)
     ev_every = 4
+    warm_frames = 0
+    busy_ms_frame = None
+    frame_check = None
+    window = None
     pipe = None
     if native:
         # No silent fallback: a multi-GPU number must come from the path its
@@ -431,18 +503,47 @@ def main() -> int:
         # millisecond -- several 1/8-frames -- so it stays outside the clock.
         # (sampling every warmup frame creates the loop's timing events now,
         # outside the window: ceil(steps / ev_every) pairs, created on first use)
+        if not args.spin:   # (a spinning camera's frames are all distinct: its warm-up stays the frame count)
+            warm_frames = clock_warm_ranks(lambda: pipe.run_frames(8), lambda: pipe.barrier(stream),
+                                           args.clock_warm_ms, world, red_dev)
         pipe.run_frames(args.warmup, cameras=sd[:args.warmup] if sd else None, sample_every=1)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         pipe.barrier(stream)
+        e_w0, e_w1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
+        e_w0.record(stream)
         kern_ms = pipe.run_frames(args.steps, stream=stream, sample_every=ev_every,
                                   cameras=sd[args.warmup:] if sd else None)
+        e_w1.record(stream)   # the caller's stream joins every render stream's last frame
+        t_q = time.perf_counter()
         host_el = pipe.host_ms * args.steps * 1e-3
         pipe.barrier(stream)
+        t_b = time.perf_counter()
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
+        window = {"host_queue_ms": round((t_q - t0) * 1e3, 4), "host_barrier_ms": round((t_b - t0) * 1e3, 4),
+                  "gpu_window_ms": round(e_w0.elapsed_time(e_w1), 4), "host_window_ms": round(el * 1e3, 4),
+                  "def": "the timed window on the host clock (t0 -> frames queued -> barrier returned -> synchronized) "
+                         "and on the GPU clock (HIP events on the caller's stream before the first frame and after "
+                         "the join of the render streams)"}
+        if world > 1:
+            dist.barrier()
+        # parity of the timed path (verdict r05 #2): rank 0's last frame of the
+        # window -- RCCL-gathered and assembled at N > 1 -- against a plain
+        # one-GPU render of the same camera, untimed
+        got = pipe.frame(stream)
+        if rank == 0:
+            frame_check = frame_check_of(got, r.render(W, H, fmt))
+        # untimed, after the window: the same K frames with every render
+        # sampled, for the GPU busy time per frame (the union of the renders'
+        # intervals; overlapping frames count once: vr_shard_sampled_busy)
+        pipe.run_frames(args.steps, stream=stream, sample_every=1, cameras=sd[args.warmup:] if sd else None)
+        busy_ms, _span = pipe.sampled_busy()
+        busy_ms_frame = busy_ms / args.steps
+        pipe.barrier(stream)
+        torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
     elif args.spin:
@@ -487,6 +588,8 @@ def main() -> int:
                 sampled.append(int(counter.item()))
         local_steps = frame_steps = int(round(float(np.mean(sampled))))
     else:
+        warm_frames = clock_warm_ranks(lambda: sharder.run_frames(8), torch.cuda.synchronize, args.clock_warm_ms, world,
+                                       red_dev)
         sharder.run_frames(args.warmup)
         if world > 1:
             dist.barrier()
@@ -500,6 +603,9 @@ def main() -> int:
             dist.barrier()
         el = time.perf_counter() - t0
         kern_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev if e is not None]))
+        got = sharder.frame()   # collective: a frame gathered as the window's were, untimed
+        if rank == 0:
+            frame_check = frame_check_of(got, r.render(W, H, fmt))
     # A uniform channel (the recipe's constant G) is a constant tap with no
     # loads ("_u" kernels).  For comparison, the same K
     # frames with every channel loaded, timed after the main window (N = 1).
@@ -557,7 +663,7 @@ def main() -> int:
     others, other_cpu = {}, {}
     if world == 1 and not args.spin and args.config == "grid512" and not args.no_other_configs:
         for name in ("grid4k", "cloud", "cloud_shadow"):
-            others[name], other_cpu[name] = other_config(name, args.steps, args.warmup)
+            others[name], other_cpu[name] = other_config(name, args.steps, args.warmup, args.clock_warm_ms)
     # the measured HBM roofline of this box: one-pass 16-B-per-lane streams of
     # 2 GiB (past the 256 MiB Infinity Cache), read-only and copy, 4 / 8 / 16
     # loads in flight per lane; the larger rate is the denominator
@@ -565,10 +671,10 @@ def main() -> int:
     if rank == 0:
         for kind in ("read", "copy"):
             bw[kind] = r.measure_bandwidth(kind, 0, 2 << 30, 10)
-    tt = torch.tensor([el, kern_ms], dtype=torch.float64, device=red_dev)
+    tt = torch.tensor([el, kern_ms, busy_ms_frame or 0.0], dtype=torch.float64, device=red_dev)
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-    el, kern_ms_max = float(tt[0]), float(tt[1])
+    el, kern_ms_max, busy_max = float(tt[0]), float(tt[1]), float(tt[2])
 
     collective_label = None
     if world > 1:
@@ -604,6 +710,16 @@ def main() -> int:
             roofline["achieved_def"] += (f"; renders overlap ({streams_eff} render streams or two in flight), so "
                                          "the time is the wall time per frame of the timed window, not a launch's "
                                          "duration (kernel_ms_mean: the overlapping launches' mean)")
+        if busy_ms_frame and not compositor:
+            # the same units over the GPU busy time per frame (union of the
+            # renders' intervals, overlapping frames counted once)
+            fb = roofline["achieved"] * roof_ms / busy_ms_frame / roofline["peak"]
+            roofline.update({"kernel_busy_ms_per_frame": round(busy_ms_frame, 5), "frac_busy": round(fb, 4),
+                             "kernel_busy_def": "union of the render intervals of K untimed frames run after the "
+                                                "window with every render bracketed by HIP events on its render "
+                                                "stream (vr_shard_sampled_busy) / K; frac_busy = the same "
+                                                "algorithmic units / that time / peak"
+                                                + (f"; max over ranks {busy_max:.5f} ms" if world > 1 else "")})
         if roofline["bound"] == "hbm":
             pk_kind = max(bw, key=lambda k: bw[k][0])
             pk = bw[pk_kind][0]
@@ -685,6 +801,13 @@ def main() -> int:
                                "GPU's queue is full)"} if args.spin and not native else {}),
             **({"region_lists": {"gpu_builds": r.get_option("region_gpu_builds"),
                                  "interval": r.get_option("region_interval")}} if args.spin and proc is None else {}),
+            "frame_check": frame_check,
+            **({"frame_check_def": "rank 0's last frame of the timed window ("
+                                   + ("RCCL-gathered and assembled" if world > 1 else "the frame loop's")
+                                   + ") against a plain one-GPU vr_render of the same camera, untimed: 'exact' = "
+                                     "bit-identical"} if frame_check else {}),
+            "clock_warm": clock_warm_obj(args.clock_warm_ms if warm_frames else 0.0, warm_frames),
+            **({"window": window} if window else {}),
             **({"all_channels_loaded": all_loaded} if all_loaded else {}),
             **({"frames_in_flight_2": inflight2} if inflight2 else {}),
             "kernel_ms_mean_max_rank": round(kern_ms_max, 5),
@@ -705,13 +828,17 @@ def main() -> int:
                 others[name]["cpu_baseline"] = cpu_baseline(vol_o, osd_o, gsd_o, march_o, W_o, H_o,
                                                             args.cpu_budget_other, procedural=proc_o)
         print(json.dumps(out), file=json_out, flush=True)
+    rc = 0
+    if rank == 0 and frame_check is not None and frame_check != "exact":
+        print(f"bench.py: frame check failed: {frame_check}", file=sys.stderr, flush=True)
+        rc = 4
     if native:
         pipe.close()
     sharder.close()
     r.close()
     if world > 1:
         dist.destroy_process_group()
-    return 0
+    return rc
 
 
 if __name__ == "__main__":

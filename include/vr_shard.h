@@ -205,6 +205,14 @@ vr_status vr_shard_rebalance_rows(vr_shard* sh, double my_ms);
 int       vr_shard_partition(vr_shard* sh);
 vr_status vr_shard_row_range(vr_shard* sh, int rank, int* row_first, int* rows);
 int       vr_shard_aborted(vr_shard* sh);
+/* The last vr_shard_run_frames call that sampled renders (sample_every > 0):
+ * the union of the sampled renders' intervals (busy_ms; renders that overlap
+ * on several render streams count once) and the span from the first sampled
+ * start to the last sampled end (span_ms), both totals in ms on the GPU's
+ * clock.  With sample_every = 1, busy_ms / frames is the GPU time per frame
+ * the renders held the machine (bench.py roofline.kernel_busy_ms_per_frame).
+ * New (no reference counterpart). */
+vr_status vr_shard_sampled_busy(vr_shard* sh, double* busy_ms, double* span_ms);
 /* Self-test of the deadline loop on the host (no GPU, no RCCL): mode 0 a
  * state that completes after 5 polls, 1 one that fails at the 3rd, 2 one that
  * never completes.  Returns 0 done, 1 failed, 2 deadline (-1 bad mode) and

@@ -587,3 +587,48 @@ def test_row_partition_measured_and_one_rank_rebalance():
             assert np.array_equal(got.cpu().numpy(), full.cpu().numpy())
         finally:
             pl.close()
+
+
+def test_timed_path_config5_native_loop_512(oracle):
+    """Verdict r05 #2: the exact path bench.py times at N = 1 -- the native
+    frame loop (RcclBandPipeline, world 1, default 2 render streams with the
+    exchange on the render streams, frames_overlap on, which moves the auto
+    split threshold) at BASELINE config 5's size: 512^3 recipe volume,
+    1920 x 1080 x 128, RGBA8 UNORM, reference camera.  The frames of both
+    render streams (3 and 4 frames run) equal the oracle's whole frame bit for
+    bit, and the executed-step count of a render under the loop's split rule
+    equals the oracle's (1.674e7)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import volumetricrenderer_amd as vr
+    from volumetricrenderer_amd.distributed import RcclBandPipeline
+    W, H, fmt = 1920, 1080, vr.FMT_RGBA8_UNORM
+    with vr.Renderer(0) as r:
+        r.generate_volume(vr.scaled_recipe(512))
+        vol = r.get_volume()
+        osd, gsd = vr.reference_shader_data(1280.0 / 720.0)
+        r.set_shader_data(osd, gsd)
+        march = vr.march_defaults(max_steps=128)
+        r.set_march(march)
+        obj, glob = vr.shader_data_arrays(osd, gsd)
+        ref, ref_steps = oracle.render(vol, obj, glob, oracle.from_params(march), W, H, oracle.FMT_RGBA8_UNORM)
+        pl = RcclBandPipeline(r, W, H, fmt, band_rows=16, world=1, rank=0)
+        try:
+            assert pl.render_streams == 2 and not pl.compositor and pl.partition == "bands"
+            for k in (3, 4):   # the last frame on render stream 0, then on stream 1
+                ms = pl.run_frames(k, sample_every=1)
+                assert ms > 0
+                assert r.get_option("frames_overlap") == 1   # the loop's split rule is in force
+                busy, span = pl.sampled_busy()
+                assert 0 < busy <= span + 1e-3
+                got = pl.frame()
+                torch.cuda.synchronize()
+                assert np.array_equal(got.cpu().numpy(), ref), k
+            assert "col48" in r.kernel_variant
+            counter = torch.zeros(1, dtype=torch.int64, device="cuda")
+            r.render(W, H, fmt, step_counter=counter)
+            torch.cuda.synchronize()
+            assert int(counter.item()) == ref_steps
+        finally:
+            pl.close()
+        assert r.get_option("frames_overlap") == 0   # restored with the pipeline

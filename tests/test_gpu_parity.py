@@ -400,8 +400,8 @@ def test_slab_march_bitexact(r, oracle, vol128, cap):
     0 = every channel falls back.  Bit-exact vs the oracle with step counts:
     the reference view and rotated views at 128^3, odd extents, a 200^3
     random volume on a small frame (big boxes), early-out, MediaScroll offsets
-    inside the clamp-exact range (the non-zero-offset kernel)."""
-    need_experiments(r, "slab")
+    inside the clamp-exact range (the non-zero-offset kernel).  The slab
+    march is in the default library (option slab, off by default)."""
     r.set_volume(vol128)
     r.set_layout_preference(15)
     r.set_option("slab", 1)

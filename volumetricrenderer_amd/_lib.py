@@ -218,6 +218,7 @@ _SHARD_SIGS = {
     "vr_shard_share_volume": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp]),
     "vr_shard_set_timeout": (ctypes.c_int, [_vp, ctypes.c_double]),
     "vr_shard_aborted": (ctypes.c_int, [_vp]),
+    "vr_shard_sampled_busy": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     "vr_shard_set_render_streams": (ctypes.c_int, [_vp, ctypes.c_int]),
     "vr_shard_get_render_streams": (ctypes.c_int, [_vp]),
     "vr_shard_set_solo": (ctypes.c_int, [_vp, ctypes.c_int]),

@@ -1093,7 +1093,7 @@ try {
                                                    value == SCHED_XCDROWS)) ||
                               (n == "wg_waves" && value != 4) || (n == "lat" && value != 0) ||
                               (n == "segment" && value != 0) ||
-                              (n == "slab" && value != 0) || (n == "sort_reuse" && value != 0) ||
+                              (n == "sort_reuse" && value != 0) ||
                               (n == "proc_enum" && value != 0);
     if (experimental && !VR_EXPERIMENTS)
         return fail(VR_ERR_INVALID, "vr_set_option: %s = %d is built only with VR_EXPERIMENTS (make EXPERIMENTS=1; "

@@ -70,11 +70,12 @@ __host__ __device__ constexpr bool is_b4_family(int l)
 
 // Variants measured slower than the defaults and kept as the record of that
 // (DESIGN.md sec. 4, 5.1-5.4): the layouts other than the auto ones, the
-// queue / strided / XCD-row schedules, 8- and 16-wave workgroups, the LDS
-// slab, the latency-mode march (lat), ray segments (segment), and the
-// procedural sort_reuse / proc_enum options.  They are
-// compiled only with VR_EXPERIMENTS=1 (make EXPERIMENTS=1); the default
-// library refuses their options.
+// queue / strided / XCD-row schedules, 8- and 16-wave workgroups, the
+// latency-mode march (lat), ray segments (segment), and the procedural
+// sort_reuse / proc_enum options.  They are compiled only with
+// VR_EXPERIMENTS=1 (make EXPERIMENTS=1); the default library refuses their
+// options.  The LDS slab march (north star; option slab, off by default) is
+// in every build so that its parity test runs in the default GPU suite.
 #ifndef VR_EXPERIMENTS
 #define VR_EXPERIMENTS 0
 #endif

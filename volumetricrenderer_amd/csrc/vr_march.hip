@@ -157,9 +157,7 @@ hipError_t launch_march(const MarchArgs& a, int layout, int wrap, bool early, co
     switch (layout) {
     case LAYOUT_BRICK4832: return launch_lw<LAYOUT_BRICK4832, WRAP_CLAMP>(a, early, sc, s);
     case LAYOUT_COL48:
-#if VR_EXPERIMENTS
         if (sc.kind == SCHED_REGIONS && sc.slab && sc.split <= 1) return launch_march_slab(a, early, sc, s);
-#endif
         return launch_lw<LAYOUT_COL48, WRAP_CLAMP>(a, early, sc, s);
 #if VR_EXPERIMENTS
     case LAYOUT_BRICK4: return launch_lw<LAYOUT_BRICK4, WRAP_CLAMP>(a, early, sc, s);

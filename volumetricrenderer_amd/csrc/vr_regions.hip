@@ -195,7 +195,11 @@ RgScratch carve(void* scratch, int n, size_t sort_bytes)
     s.bin_cost = reinterpret_cast<unsigned long long*>(p + o);
     o = up(o + kAngleBins * sizeof(unsigned long long));
     s.counts = reinterpret_cast<unsigned*>(p + o);
-    o = up(o + 16 * sizeof(unsigned));
+    // counts: the lists' entries per XCD [0, 8), work markers, then the
+    // marched entries per XCD [kRegionWork, kRegionWork + 8)
+    constexpr size_t kCountWords = (size_t)kRegionWork + 8;
+    static_assert(kCountWords * sizeof(unsigned) <= 256, "counts must fit one 256-B slot of the scratch");
+    o = up(o + kCountWords * sizeof(unsigned));
     s.bin_xcd = reinterpret_cast<unsigned char*>(p + o);
     o = up(o + kAngleBins);
     s.keys_in = reinterpret_cast<unsigned*>(p + o);

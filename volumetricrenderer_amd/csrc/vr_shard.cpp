@@ -195,6 +195,14 @@ struct vr_shard {
     bool loopback = false;            // one process emulates all ranks (no RCCL)
     bool solo = false;                // loopback rehearsal of one rank: its own band set only, no exchange
     std::vector<hipEvent_t> timing;   // sampled render brackets (pairs)
+    double sampled_busy_ms = 0.0;     // the last run's sampled renders: union of their intervals
+    double sampled_span_ms = 0.0;     // and first start -> last end (vr_shard_sampled_busy)
+    // the ctx's option frames_overlap before this pipeline first ran frames on
+    // 2+ render streams (-1: not changed).  It stays set while the pipeline
+    // overlaps frames -- a set / reset per run would invalidate the ctx's
+    // launch cache twice per run -- and is restored by vr_shard_destroy or a
+    // switch to one render stream.
+    int overlap_prev = -1;
     double timeout_s = 120.0;         // deadline of every host wait on a collective
     bool aborted = false;             // the communicator was aborted (error or deadline)
 };
@@ -297,8 +305,15 @@ vr_status check_usable(vr_shard* sh, const char* what)
     return VR_OK;
 }
 
+void restore_overlap(vr_shard* sh)
+{
+    if (sh->overlap_prev == 0) (void)vr_set_option(sh->ctx, "frames_overlap", 0);
+    sh->overlap_prev = -1;
+}
+
 void release(vr_shard* sh)
 {
+    restore_overlap(sh);
     for (hipStream_t rs : sh->render_stream)
         if (rs) (void)hipStreamSynchronize(rs);
     if (sh->comm_stream) (void)hipStreamSynchronize(sh->comm_stream);
@@ -737,19 +752,12 @@ try {
     const bool two = P >= 2;   // frames overlap on P render streams
     if (frames > 0) sh->started = true;   // the band geometry is fixed from here
     // two render streams: tell the ctx its consecutive renders overlap (its
-    // auto split rule), for this run
-    struct OverlapHint {
-        void* ctx;
-        int prev;
-        OverlapHint(void* c, bool on) : ctx(c), prev(on ? vr_get_option(c, "frames_overlap") : -1)
-        {
-            if (prev == 0) (void)vr_set_option(ctx, "frames_overlap", 1);
-        }
-        ~OverlapHint()
-        {
-            if (prev == 0) (void)vr_set_option(ctx, "frames_overlap", 0);
-        }
-    } overlap_hint(sh->ctx, two && frames > 0);
+    // auto split rule), from this pipeline's first such run until it is
+    // destroyed or set to one render stream (restore_overlap)
+    if (two && frames > 0 && sh->overlap_prev < 0) {
+        sh->overlap_prev = vr_get_option(sh->ctx, "frames_overlap");
+        if (sh->overlap_prev == 0) VR_TRY(vr_set_option(sh->ctx, "frames_overlap", 1));
+    }
     if (two && frames > 0) {   // the render streams start after the caller's queued work (e.g. the volume)
         HIP_TRY(hipEventRecord(sh->fence, s));
         for (hipStream_t rs : sh->render_stream) HIP_TRY(hipStreamWaitEvent(rs, sh->fence, 0));
@@ -827,6 +835,20 @@ try {
                 stop.store(true, std::memory_order_release);
             }
         });
+        // if anything below throws, the worker is stopped and joined before
+        // the exception leaves (a joinable std::thread's destructor would
+        // call std::terminate past the function-try-block)
+        struct JoinGuard {
+            std::thread& t;
+            std::atomic<bool>& stop;
+            ~JoinGuard()
+            {
+                if (t.joinable()) {
+                    stop.store(true, std::memory_order_release);
+                    t.join();
+                }
+            }
+        } join_guard{worker, stop};
         vr_status mst = VR_OK;
         for (int i = 0; i < frames && mst == VR_OK; ++i) {
             if (i >= 2 && !wait_host([&] { return cdone.load(std::memory_order_acquire) >= i - 1; }, stop, sh->timeout_s))
@@ -882,13 +904,35 @@ try {
                           : 0.0;
     if (kernel_ms) {
         double sum = 0.0;
+        std::vector<std::pair<double, double>> iv;   // sampled renders on one clock: ms after the first start
         for (int k = 0; k < next; ++k) {
             SH_TRY(wait_event(sh, sh->timing[2 * k + 1], "vr_shard_run: sampled render"));
-            float ms = 0.0f;
+            float ms = 0.0f, a = 0.0f, b = 0.0f;
             HIP_TRY(hipEventElapsedTime(&ms, sh->timing[2 * k], sh->timing[2 * k + 1]));
+            HIP_TRY(hipEventElapsedTime(&a, sh->timing[0], sh->timing[2 * k]));
+            HIP_TRY(hipEventElapsedTime(&b, sh->timing[0], sh->timing[2 * k + 1]));
             sum += ms;
+            iv.emplace_back(a, b);
         }
         *kernel_ms = next ? (float)(sum / next) : 0.0f;
+        // busy: the union of the sampled intervals (overlapping renders on
+        // several streams count once); with sample_every = 1, the GPU time
+        // the run's renders held the machine
+        std::sort(iv.begin(), iv.end());
+        double busy = 0.0, lo = 0.0, hi = -1.0, end = 0.0;
+        for (const auto& x : iv) {
+            if (x.first > hi) {
+                if (hi >= lo) busy += hi - lo;
+                lo = x.first;
+                hi = x.second;
+            } else {
+                hi = std::max(hi, x.second);
+            }
+            end = std::max(end, x.second);
+        }
+        if (hi >= lo && !iv.empty()) busy += hi - lo;
+        sh->sampled_busy_ms = busy;
+        sh->sampled_span_ms = iv.empty() ? 0.0 : end - iv.front().first;
     }
     return VR_OK;
 } catch (...) {
@@ -1030,6 +1074,7 @@ try {
             if (sh->pending[p]) SH_TRY(wait_event(sh, sh->done[p], "vr_shard_set_render_streams"));
     }
     sh->render_streams = n;
+    if (n == 1) restore_overlap(sh);   // the frames no longer overlap
     return VR_OK;
 } catch (...) {
     return caught_exception("vr_shard_set_render_streams");
@@ -1076,6 +1121,16 @@ try {
 }
 
 int vr_shard_aborted(vr_shard* sh) { return sh && sh->aborted ? 1 : 0; }
+
+vr_status vr_shard_sampled_busy(vr_shard* sh, double* busy_ms, double* span_ms)
+try {
+    if (!sh || !busy_ms || !span_ms) return fail(VR_ERR_INVALID, "vr_shard_sampled_busy: null argument");
+    *busy_ms = sh->sampled_busy_ms;
+    *span_ms = sh->sampled_span_ms;
+    return VR_OK;
+} catch (...) {
+    return caught_exception("vr_shard_sampled_busy");
+}
 
 // CPU self-test of the deadline logic (no HIP, no RCCL): mode 0 -- the state
 // settles after a few polls; 1 -- it reports an error; 2 -- it never settles

@@ -397,7 +397,16 @@ class RcclBandPipeline:
         self._balanced = self.partition == "bands"
         if rows is not None:
             if self.partition != "rows":
+                _lib.shard_call("vr_shard_destroy", h)
                 raise ValueError("RcclBandPipeline: rows needs partition 'rows'")
+            # vr_shard_set_rows reads renderers + 1 ints: the
+            # renderer count is the band stride of the current geometry
+            stride, first = ctypes.c_int(), ctypes.c_int()
+            _lib.shard_call("vr_shard_bands", h, ctypes.byref(stride), ctypes.byref(first))
+            if len(rows) != stride.value + 1:
+                _lib.shard_call("vr_shard_destroy", h)
+                raise ValueError(f"RcclBandPipeline: rows needs {stride.value + 1} entries (renderers + 1), "
+                                 f"got {len(rows)}")
             _lib.shard_call("vr_shard_set_rows", h, (ctypes.c_int * len(rows))(*rows))
             self._balanced = True
         self._geometry()
@@ -424,7 +433,14 @@ class RcclBandPipeline:
         (this rank's view: its own range is self.row_range)."""
         if self.partition != "rows":
             raise ValueError("rebalance_rows: the pipeline renders band sets")
-        ms = self.run_frames(frames, stream=stream, sample_every=1)
+        # measured on one render stream: with frames in flight, a sampled
+        # render's bracket also holds the overlapping frames' work (ADVICE r05)
+        streams = self.render_streams
+        self.render_streams = 1
+        try:
+            ms = self.run_frames(frames, stream=stream, sample_every=1)
+        finally:
+            self.render_streams = streams
         _lib.shard_call("vr_shard_rebalance_rows", self._h, float(ms))
         self._geometry()
         return self.row_range
@@ -482,6 +498,16 @@ class RcclBandPipeline:
                             ctypes.byref(ms) if sample_every > 0 else None, ctypes.byref(host))
         self.host_ms = host.value
         return ms.value if sample_every > 0 else None
+
+    def sampled_busy(self) -> tuple[float, float]:
+        """(busy, span) in ms of the last run_frames call that sampled renders:
+        the union of the sampled renders' intervals (overlapping renders count
+        once) and first start -> last end, on the GPU's clock
+        (vr_shard_sampled_busy).  With sample_every=1, busy / frames is the GPU
+        time per frame."""
+        busy, span = ctypes.c_double(), ctypes.c_double()
+        _lib.shard_call("vr_shard_sampled_busy", self._h, ctypes.byref(busy), ctypes.byref(span))
+        return busy.value, span.value
 
     def share_volume(self, vol=None, stream=None) -> None:
         """Collective, once per volume: rank 0's RGBA8 volume (a contiguous
