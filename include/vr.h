@@ -336,19 +336,10 @@ vr_status vr_set_layout_preference(void* ctx, int pref);
  *                     (ring around the projected box centre, then angle).
  *   "wg_waves"        4 (default), 8, 16: waves per workgroup of the regions
  *                     march (col48, brick4832, cornerh).
- *   "segment"         VR_EXPERIMENTS builds only (measured slower, DESIGN.md
- *                     sec. 7.1).  0 (off, the default) or 4-4096 steps, regions schedule
- *                     (col48, brick4832, cornerh): tiles whose estimated work
- *                     is at least 2L steps are marched as segments of L steps,
- *                     one wave each, and a resolve pass adds each ray's stored
- *                     terms in step order (bit-exact).  For small frame shares
- *                     (N GPUs), whose time is their longest rays.  Scratch:
- *                     segmented tiles x max_steps x 256 bytes, at most 1 GiB
- *                     per context (grown inside vr_render, with a device sync,
- *                     when a frame needs more).  Read-only
- *                     "region_segment_tiles": segmented tiles of the lists.
  *   "slab"            0/1, col48 + regions: the per-wave LDS slab march
- *                     (default 0); "slab_cap" 0-32 chunks per channel.
+ *                     (the north star's "per-tile density slabs staged in
+ *                     LDS", bit-exact; measured slower, so 0 is the
+ *                     default); "slab_cap" 0-32 chunks per channel.
  *   "split"           regions schedule, brick4/448/488/zpair/corner8: lanes per ray
  *                     (1, 2, 4, 8; each lane marches every K-th step and the
  *                     terms are summed in step order, bit-exact); 0 = auto,
@@ -391,11 +382,6 @@ vr_status vr_set_layout_preference(void* ctx, int pref);
  *                     Read-only: "shadow_defer_kib" the scratch held now,
  *                     "shadow_defer_last" 1 if the last procedural render ran
  *                     the deferred passes.
- *   "lat"             VR_EXPERIMENTS builds only (measured slower, DESIGN.md
- *                     sec. 7.1): regions schedule, col48 / brick4832 / cornerh,
- *                     the latency-mode march ("split" lanes per ray, 2-4
- *                     rounds of loads in flight; bit-exact): 0 = off (the only
- *                     value the default library accepts), 2/3/4 = that depth.
  *   "lattice"         procedural medium, sorted schedule: 1 = the fBm reads its
  *                     per-cell gradient-pair offsets from a lattice table in
  *                     global memory (the default; built when the seed or the

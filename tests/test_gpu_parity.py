@@ -229,63 +229,6 @@ def test_every_layout_bitexact(r, oracle, vol128, layout, name):
         r.set_layout_preference(0)
 
 
-@pytest.mark.parametrize("layout", [15, 12, 14, 1])
-@pytest.mark.parametrize("seg", [4, 16, 48])
-def test_ray_segments_bitexact(r, oracle, vol128, layout, seg):
-    """Ray segments (option segment = L): the tiles
-    estimated at >= 2L steps are marched as segments of L steps whose terms
-    seg_resolve adds in step order -- exact against the oracle, step counts
-    included: the recipe volume (G uniform: the _uG kernel), a rotated cube,
-    bands, short rays (max_steps 7 < L), early-out (the sum stops at the same
-    step), 300 steps (up to 75 segments), lists reused for a larger
-    max_steps (the terms scratch grows), a random volume (every channel
-    loaded) and per-tap MediaScroll offsets.  Layout 1 (planar) has no
-    segmented kernel: the option leaves it on its plain path.  Measured
-    slower than step-split rays: built only with VR_EXPERIMENTS."""
-    need_experiments(r, "segment")
-    r.set_layout_preference(layout)
-    r.set_option("schedule", 5)
-    r.set_option("segment", seg)
-    assert r.get_option("segment") == seg
-    r.set_option("region_interval", 1)   # new lists for every new frame geometry
-    try:
-        osd, gsd = vr.reference_shader_data(16 / 9, 25.0, -40.0)
-        for W, H, band, march in [(333, 187, {}, vr.march_defaults()),
-                                  (640, 360, dict(band_rows=16, band_stride=3, band_first=2), vr.march_defaults()),
-                                  (320, 180, {}, vr.march_defaults(max_steps=7)),
-                                  (320, 180, {}, vr.march_defaults(early_out=0.6, density=4.0)),
-                                  (320, 180, {}, vr.march_defaults(max_steps=300))]:
-            img, ref, c, s = render_both(r, oracle, vol128, W, H, osd, gsd, march=march, **band)
-            assert_exact(img, ref)
-            assert c == s
-            if layout != 1 and march.max_steps >= 4 * seg:
-                assert r.get_option("region_segment_tiles") > 0
-        assert layout != 1 or r.get_option("region_segment_tiles") == 0
-        # lists built at 64 steps, reused (interval 32) at 300: the terms scratch grows
-        r.set_option("region_interval", 32)
-        for ms in (64, 300):
-            img, ref, c, s = render_both(r, oracle, vol128, 300, 200, osd, gsd, march=vr.march_defaults(max_steps=ms))
-            assert_exact(img, ref)
-            assert c == s
-        rng = np.random.default_rng(seg + layout)
-        vol = rng.integers(0, 256, size=(40, 52, 36, 4), dtype=np.uint8)
-        osd, gsd = vr.reference_shader_data(16 / 9, 30.0, 5.0)
-        img, ref, c, s = render_both(r, oracle, vol, 200, 112, osd, gsd)
-        assert_exact(img, ref)
-        assert c == s
-        gsd.media_scroll[1 * 4 + 1] = 0.01
-        gsd.media_scroll[2 * 4 + 2] = -0.02
-        for m in (vr.march_defaults(), vr.march_defaults(early_out=0.6)):
-            img, ref, c, s = render_both(r, oracle, vol, 160, 90, osd, gsd, march=m)
-            assert_exact(img, ref)
-            assert c == s
-    finally:
-        r.set_option("region_interval", 32)
-        r.set_option("segment", 0)
-        r.set_option("schedule", -1)
-        r.set_layout_preference(0)
-
-
 @pytest.mark.parametrize("layout", [15, 12, 14, 16])
 def test_uniform_channel_skip_bitexact(r, oracle, layout):
     """A channel whose texels are all equal (the reference recipe's G,
@@ -1285,67 +1228,16 @@ def test_split_rays_bitexact(r, oracle, vol128, layout, split):
         r.set_layout_preference(0)
 
 
-@pytest.mark.parametrize("layout", [15, 12, 14])
-@pytest.mark.parametrize("split,lat", [(1, 2), (1, 4), (2, 3), (4, 2), (4, 3), (4, 4), (8, 3)])
-def test_latency_march_bitexact(r, oracle, vol128, layout, split, lat):
-    """The latency-mode march for small frame shares (vr_march_lat.hip: K =
-    split lanes per ray, `lat` rounds of loads in flight):
-    exact against the oracle with step counts -- the recipe volume (G uniform:
-    the _uG kernel), a rotated cube, bands, short rays (fewer steps than the
-    pipeline's rounds), early-out, a random volume (every channel loaded) and
-    per-tap MediaScroll offsets inside the clamp-exact range.  Measured
-    slower than the split march: built only with VR_EXPERIMENTS."""
-    need_experiments(r, "lat")
-    r.set_layout_preference(layout)
-    r.set_option("schedule", 5)
-    r.set_option("split", split)
-    r.set_option("lat", lat)
-    try:
-        osd, gsd = vr.reference_shader_data(16 / 9, 25.0, -40.0)
-        for W, H, band, march in [(333, 187, {}, vr.march_defaults()),
-                                  (640, 360, dict(band_rows=16, band_stride=3, band_first=2), vr.march_defaults()),
-                                  (320, 180, {}, vr.march_defaults(max_steps=7)),
-                                  (320, 180, {}, vr.march_defaults(max_steps=2)),
-                                  (320, 180, {}, vr.march_defaults(early_out=0.6, density=4.0))]:
-            img, ref, c, s = render_both(r, oracle, vol128, W, H, osd, gsd, march=march, **band)
-            assert r.kernel_variant.endswith(f"_lat{lat}")
-            assert_exact(img, ref)
-            assert c == s
-        rng = np.random.default_rng(split * 10 + lat)
-        vol = rng.integers(0, 256, size=(40, 52, 36, 4), dtype=np.uint8)
-        osd, gsd = vr.reference_shader_data(16 / 9, 30.0, 5.0)
-        img, ref, c, s = render_both(r, oracle, vol, 200, 112, osd, gsd)
-        assert_exact(img, ref)
-        assert c == s
-        gsd.media_scroll[1 * 4 + 1] = 0.01
-        gsd.media_scroll[2 * 4 + 2] = -0.02
-        for m in (vr.march_defaults(), vr.march_defaults(early_out=0.6)):
-            img, ref, c, s = render_both(r, oracle, vol, 160, 90, osd, gsd, march=m)
-            assert "_lat" in r.kernel_variant
-            assert_exact(img, ref)
-            assert c == s
-    finally:
-        r.set_option("lat", 0)
-        r.set_option("split", 0)
-        r.set_option("schedule", -1)
-        r.set_layout_preference(0)
-
-
 @pytest.mark.parametrize("layout", [15, 12, 5, 14])
-@pytest.mark.parametrize("seg", [0, 24])
-def test_auto_split_at_one_eighth_band_share(r, oracle, vol128, layout, seg):
+def test_auto_split_at_one_eighth_band_share(r, oracle, vol128, layout):
     """The multi-GPU config-5 path: auto split (split=0) turns on for a 1/8
     band share of a 1080p frame, with col48 (the auto
     layout past the Infinity Cache since round 3), brick4832 (before it),
-    corner8 and cornerh (the auto layout for cache-resident volumes); and ray
-    segments of 24 steps on that share (sec. 7.1; corner8 has none).  Exact,
+    corner8 and cornerh (the auto layout for cache-resident volumes).  Exact,
     step counts too."""
-    if seg:
-        need_experiments(r, "segment")
     r.set_layout_preference(layout)
     r.set_option("schedule", 5)
     r.set_option("split", 0)
-    r.set_option("segment", seg)
     try:
         osd, gsd = vr.reference_shader_data(16 / 9)
         for first in (0, 5):
@@ -1353,10 +1245,7 @@ def test_auto_split_at_one_eighth_band_share(r, oracle, vol128, layout, seg):
                                          band_rows=16, band_stride=8, band_first=first)
             assert_exact(img, ref)
             assert c == s
-            if seg and layout != 5:
-                assert r.get_option("region_segment_tiles") > 0
     finally:
-        r.set_option("segment", 0)
         r.set_option("schedule", -1)
         r.set_layout_preference(0)
 

@@ -30,7 +30,7 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--steps", type=int, default=128)
     ap.add_argument("--frames", type=int, default=20)
-    ap.add_argument("--variants", default="-1:0:0", help="comma list of schedule:tiles_per_wave:split[:wedges[:lat[:segment]]]")
+    ap.add_argument("--variants", default="-1:0:0", help="comma list of schedule:tiles_per_wave:split[:wedges]")
     ap.add_argument("--opt", action="append", default=[], help="vr option NAME=VALUE, set first")
     ap.add_argument("--ns", default="1,2,4,8")
     ap.add_argument("--band-rows", type=int, default=16)
@@ -73,10 +73,6 @@ def main():
             vals = [int(v) for v in var.split(":")]
             sched, tpw, split = vals[:3]
             wedges = vals[3] if len(vals) > 3 else 0
-            lat = vals[4] if len(vals) > 4 else 0
-            seg = vals[5] if len(vals) > 5 else 0
-            r.set_option("lat", lat)
-            r.set_option("segment", seg)
             r.set_option("schedule", sched)
             r.set_option("tiles_per_wave", tpw)
             r.set_option("split", split)
@@ -102,7 +98,7 @@ def main():
                 if a.all_ranks:
                     print(f"  N={n} band_rows {a.band_rows}: per-rank ms " + " ".join(f"{v:.4f}" for v in ts), flush=True)
                 base = base or t
-                print(f"{' '.join(a.opt)} schedule {sched} tpw {tpw} split {split} wedges {wedges} lat {lat} seg {seg} N={n}: rank-0 bands {t:.4f} ms, whole/N {base / n:.4f} ms, "
+                print(f"{' '.join(a.opt)} schedule {sched} tpw {tpw} split {split} wedges {wedges} N={n}: rank-0 bands {t:.4f} ms, whole/N {base / n:.4f} ms, "
                       f"efficiency {base / n / t:.2f}", flush=True)
 
 

@@ -83,7 +83,6 @@ constexpr int kMaxRegionStreams = 4;
 // 3840 x 2160 x 256); a frame needing more marches its last waves' shadow rays
 // in place
 constexpr int kMaxDeferMiB = 4 << 10;
-constexpr size_t kMaxTermsBytes = (size_t)1 << 30;   // ray segments: the terms scratch (slots x max_steps x 64 floats)
 // retired deferred scratch buffers kept before a device sync frees them
 constexpr size_t kMaxDeferRetired = 4;
 constexpr int kRegionKeyLen = 39;
@@ -191,15 +190,11 @@ struct Ctx {
     int slab = 0;                  // COL48 + regions: the LDS slab march (vr_march_slab.hip)
     int proc_enum = 0;             // procedural sort: 1 = 64x64-region enumeration with shadow rays too
     int slab_cap = kSlabMaxChunks; // its chunks per channel (<= kSlabMaxChunks; smaller forces the fallback)
-    int segment = 0;               // regions: ray segments of L steps for the long tiles (0 = off)
     // regions: each XCD's list 0 = inside-out (ring, angle); 1 = longest tile first;
     // 2 = longest S x S block first (the default since round 4)
     int region_order = 2;
-    float* d_terms = nullptr;      // segments: the per-step terms (SegArgs.terms)
-    size_t terms_bytes = 0;
     int wg_waves = 4;              // regions: waves per workgroup (4, 8, 16)
     int supertile = 2;             // regions: list order by S x S blocks of tiles (1 = per tile; 2 measured 1 % faster)
-    int lat = 0;                   // regions: latency-mode march, rounds of loads in flight (0 = off, 2-4; VR_EXPERIMENTS)
     int region_interval = kRegionRebuildInterval;   // option "region_interval": renders a moved camera reuses the lists
     int region_gpu = 1;            // option "region_gpu": 1 = a moved camera's lists are rebuilt on the GPU
     void* d_rg = nullptr;          // GPU list build scratch (region_build_bytes), zeroed when allocated
@@ -219,9 +214,6 @@ struct Ctx {
         int most_marched = 0;         // the most marched entries of one XCD (hdr[kRegionWork + x])
         int nwork = 0;             // tiles with estimated work
         int nempty = -1;           // empty tiles (tile_is_empty) in the lists (-1: GPU build not yet complete)
-        int seg_len = 0;           // segments: steps per segment the lists were built for (0 = none)
-        int nseg_tiles = 0;        // segmented tiles (slots of SegArgs.info)
-        int icap = 0;              // info entries before the list
         // The streams that rendered with these lists, and per stream an event
         // recorded after its FIRST render with them (one event per stream and
         // build, never one per render).  These lists are rewritten two builds
@@ -657,7 +649,6 @@ try {
     if (c->rg_ev) (void)hipEventDestroy(c->rg_ev);
     for (auto& u : c->proc_uses) (void)hipEventDestroy(u.ev);
     if (c->proc_wev) (void)hipEventDestroy(c->proc_wev);
-    if (c->d_terms) (void)hipFree(c->d_terms);
     if (c->d_mm) (void)hipFree(c->d_mm);
     if (c->h_mm) (void)hipHostFree(c->h_mm);
     if (c->mm_ready) (void)hipEventDestroy(c->mm_ready);
@@ -1091,7 +1082,7 @@ try {
     // variants measured slower than the defaults (vr_internal.h VR_EXPERIMENTS)
     const bool experimental = (n == "schedule" && (value == SCHED_QUEUE || value == SCHED_STRIDED ||
                                                    value == SCHED_XCDROWS)) ||
-                              (n == "wg_waves" && value != 4) || (n == "lat" && value != 0) ||
+                              (n == "wg_waves" && value != 4) ||
                               (n == "segment" && value != 0) ||
                               (n == "sort_reuse" && value != 0) ||
                               (n == "proc_enum" && value != 0);
@@ -1207,12 +1198,6 @@ try {
         c->region_order = value;
         return VR_OK;
     }
-    if (n == "segment") {
-        if (value != 0 && (value < 4 || value > 4096))
-            return fail(VR_ERR_INVALID, "vr_set_option: segment is 0 (off) or 4-4096 steps");
-        c->segment = value;
-        return VR_OK;
-    }
     if (n == "wg_waves") {
         if (value != 4 && value != 8 && value != 16) return fail(VR_ERR_INVALID, "vr_set_option: wg_waves is 4, 8 or 16");
         c->wg_waves = value;
@@ -1231,12 +1216,6 @@ try {
     if (n == "region_gpu") {
         if (value < 0 || value > 1) return fail(VR_ERR_INVALID, "vr_set_option: region_gpu is 0 or 1");
         c->region_gpu = value;
-        return VR_OK;
-    }
-    if (n == "lat") {
-        if (value != 0 && value != 2 && value != 3 && value != 4)
-            return fail(VR_ERR_INVALID, "vr_set_option: lat is 0 (off), 2, 3 or 4 (rounds in flight)");
-        c->lat = value;
         return VR_OK;
     }
     if (n == "uniform_skip") {
@@ -1293,9 +1272,7 @@ try {
     if (n == "shadow_defer_kib")                          // read-only: the scratch held now, KiB
         return (int)std::min<size_t>((c->defer_bytes + 1023) / 1024, 0x7fffffff);
     if (n == "slab_cap") return c->slab_cap;
-    if (n == "segment") return c->segment;
     if (n == "region_order") return c->region_order;
-    if (n == "region_segment_tiles") return c->region_cur >= 0 ? c->region[c->region_cur].nseg_tiles : 0;
     if (n == "sort_reuse") return c->sort_reuse;
     if (n == "wg_waves") return c->wg_waves;
     if (n == "uniform_skip") return c->uniform_skip;
@@ -1310,7 +1287,6 @@ try {
         return c->uniform_mask;
     }
     if (n == "supertile") return c->supertile;
-    if (n == "lat") return c->lat;
     if (n == "launch_cache") return c->launch_cache;
     if (n == "empty_fill") return c->empty_fill;
     if (n == "frames_overlap") return c->frames_overlap;
@@ -1327,8 +1303,6 @@ try {
     (void)caught_exception("vr_get_option");
     return -1;
 }
-
-static bool lat_on(const Ctx* c, int layout);
 
 const char* vr_kernel_variant(void* p)
 try {
@@ -1354,27 +1328,23 @@ try {
         (pl.layout == LAYOUT_COL48 || pl.layout == LAYOUT_BRICK4832 || pl.layout == LAYOUT_CORNERH ||
          pl.layout == LAYOUT_COL48Z))
         ch = um == 1 ? 0 : um == 2 ? 1 : um == 4 ? 2 : 3;
-    // the latency-mode march (small frame shares, vr_march_lat.hip) when it is forced on
-    const int lat = kind == SCHED_REGIONS && lat_on(c, pl.layout) ? c->lat : 0;
-    if (ch < 0 && lat == 0) return variant_name(pl);
-    // built once, thread-safe (a function-local static): every layout x early x channel x depth
+    if (ch < 0) return variant_name(pl);
+    // built once, thread-safe (a function-local static): every layout x early x channel
     struct Names {
-        std::string n[kNumLayouts][2][5][5];
+        std::string n[kNumLayouts][2][5];
     };
     static const Names table = [] {
         Names t;
         for (int l = 1; l < kNumLayouts; ++l)
             for (int e = 0; e < 2; ++e)
-                for (int u = 0; u < 5; ++u)
-                    for (int d = 0; d < 5; ++d) {
-                        std::string v = variant_name(Plan{l, WRAP_CLAMP, e == 1});
-                        if (u > 0) v += std::string("_u") + "RGBA"[u - 1];
-                        if (d > 0) v += "_lat" + std::to_string(d);
-                        t.n[l][e][u][d] = v;
-                    }
+                for (int u = 0; u < 5; ++u) {
+                    std::string v = variant_name(Plan{l, WRAP_CLAMP, e == 1});
+                    if (u > 0) v += std::string("_u") + "RGBA"[u - 1];
+                    t.n[l][e][u] = v;
+                }
         return t;
     }();
-    return table.n[pl.layout][pl.early ? 1 : 0][ch + 1][lat].c_str();
+    return table.n[pl.layout][pl.early ? 1 : 0][ch + 1].c_str();
 } catch (...) {
     (void)caught_exception("vr_kernel_variant");
     return "error";
@@ -1477,18 +1447,6 @@ vr_status note_region_render(Ctx* c, hipStream_t s)
     return VR_OK;
 }
 
-// the latency-mode march (vr_march_lat.hip, built with VR_EXPERIMENTS) for this layout
-static bool lat_on(const Ctx* c, int layout)
-{
-#if VR_EXPERIMENTS
-    return c->lat > 0 && lat_supported(layout);
-#else
-    (void)c;
-    (void)layout;
-    return false;
-#endif
-}
-
 // lanes per ray of a regions frame: option split, or auto from the tiles with work
 static int auto_split(const Ctx* c, long long nwork)
 {
@@ -1569,12 +1527,12 @@ static vr_status next_region_buf(Ctx* c, size_t n, bool host_staging, hipStream_
     return VR_OK;
 }
 
-vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow, int seg_len, hipStream_t stream)
+vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow, hipStream_t stream)
 {
     const int tw = (a.width + 7) >> 3, th = (a.out_rows + 7) >> 3;
     float key[kRegionKeyLen] = {(float)tw, (float)th, (float)a.width, (float)a.height, (float)a.out_rows,
                                 (float)a.band_rows, (float)a.band_stride, (float)a.band_first, (float)tpw,
-                                (float)c->wedges, (float)(seg_len + 65536 * c->region_order), (float)c->split, (float)c->supertile};
+                                (float)c->wedges, (float)(65536 * c->region_order), (float)c->split, (float)c->supertile};
     constexpr int grid_part = 13;   // the part a reused list must match
     int kn = grid_part;
     for (float v : {(float)a.max_steps, a.step_size, (float)cpx, (float)cprow}) key[kn++] = v;
@@ -1594,11 +1552,11 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     c->region_exact = true;   // (either build below is for this key)
 
     const int S = c->supertile;
-    // a moved camera over the same target (no segments): the lists come from
+    // a moved camera over the same target: the lists come from
     // the GPU build on the render stream (vr_regions.hip) -- no host loop, no
     // host wait; tiles with work and the longest list are the last completed
     // build's (they size the launch, not the result)
-    if (same_grid && c->region_gpu && seg_len == 0 && th < 65536 && tw < 65536) {
+    if (same_grid && c->region_gpu && th < 65536 && tw < 65536) {
         const size_t n = (size_t)tw * th;
         const Ctx::RegionBuf& cur = c->region[c->region_cur];
         const int nwork = cur.nwork, most = cur.most;
@@ -1657,9 +1615,6 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
         rb.nempty = -1;
         rb.map = TileMap{};
         rb.map.nwx = std::max(1, (most + tpw - 1) / tpw);
-        rb.seg_len = 0;
-        rb.nseg_tiles = 0;
-        rb.icap = 0;
         rb.nstreams = 0;
         const vr_status st = note_region_stream(rb, stream, &c->region_slot);
         if (st != VR_OK) return st;
@@ -1767,57 +1722,22 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     for (int x = 0; x < 8; ++x) marched[x] = (int)xl[x].size();
     for (size_t i = 0; i < empty_tiles.size(); ++i) xl[i % 8].push_back(empty_tiles[i]);
 
-    // segments (option "segment", L steps): a tile with work estimated at
-    // >= 2L steps is marched as round(cost / L) segments (at most 127; as many
-    // tiles as kMaxTermsBytes of terms hold at this max_steps), segment-major
-    // (the first segments of an XCD's long tiles, then the second, ...) ahead
-    // of its whole tiles; the info of XCD x's segmented tiles is contiguous
-    const int L = seg_len;
-    const size_t slot_bytes = (size_t)std::max(a.max_steps, 1) * 64 * sizeof(float);
-    const int slot_cap = L > 0 ? (int)std::min<size_t>(kMaxTermsBytes / slot_bytes, (size_t)1 << 24) : 0;
-    struct SegT { unsigned id; int nseg; };
-    std::vector<std::vector<SegT>> segx(8);
-    std::vector<std::vector<unsigned>> wholex(8);
-    int nslots = 0;
     size_t nent = 0;
-    for (int x = 0; x < 8; ++x)
-        for (const T& t : xl[x]) {
-            const int ns = L > 0 && t.cost >= 2.0 * L ? (int)std::min(127.0, std::floor(t.cost / L + 0.5)) : 1;
-            if (ns >= 2 && nslots < slot_cap) {
-                segx[x].push_back({t.id, ns});
-                ++nslots;
-                nent += (size_t)ns;
-            } else {
-                wholex[x].push_back(t.id);
-                ++nent;
-            }
-        }
-    const size_t n = 2 * (size_t)nslots + nent;   // words after the header
+    for (int x = 0; x < 8; ++x) nent += xl[x].size();
+    const size_t n = nent;   // words after the header
     int b = 0;
     const vr_status st0 = next_region_buf(c, n, true, stream, &b);
     if (st0 != VR_OK) return st0;
     Ctx::RegionBuf& rb = c->region[b];
     int* hdr = reinterpret_cast<int*>(rb.h);
     std::memset(hdr, 0, kRegionHeader * sizeof(int));
-    unsigned* info = rb.h + kRegionHeader;
-    unsigned* list = info + 2 * (size_t)nslots;
+    unsigned* list = rb.h + kRegionHeader;
     int most_marched = 0;
     TileMap m{};
     size_t pos = 0, most = 0;
-    int slot = 0;
     for (int x = 0; x < 8; ++x) {
         m.off[x] = (int)pos;
-        int maxns = 0;
-        for (const SegT& q : segx[x]) maxns = std::max(maxns, q.nseg);
-        for (int sg = 0; sg < maxns; ++sg)
-            for (size_t j = 0; j < segx[x].size(); ++j)
-                if (sg < segx[x][j].nseg) list[pos++] = 0x80000000u | ((unsigned)sg << 24) | (unsigned)(slot + (int)j);
-        for (const SegT& q : segx[x]) {
-            info[2 * slot] = q.id;
-            info[2 * slot + 1] = (unsigned)q.nseg;
-            ++slot;
-        }
-        for (unsigned id : wholex[x]) list[pos++] = id;
+        for (const T& t : xl[x]) list[pos++] = t.id;
         most = std::max(most, pos - (size_t)m.off[x]);
     }
     m.off[8] = (int)pos;
@@ -1826,12 +1746,11 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     hdr[9] = (int)work.size();
     hdr[10] = (int)most;
     hdr[11] = (int)pos;
-    for (int x = 0; x < 8; ++x) {   // the marched entries lead each XCD's list (with segments: all of them)
-        const int nm = L > 0 ? m.off[x + 1] - m.off[x] : marched[x];
+    for (int x = 0; x < 8; ++x) {   // the marched entries lead each XCD's list
+        const int nm = marched[x];
         hdr[kRegionWork + x] = nm;
         most_marched = std::max(most_marched, nm);
     }
-    hdr[kRegionSegTiles] = nslots;
     HIP_TRY(hipMemcpyAsync(rb.d, rb.h, (n + kRegionHeader) * sizeof(unsigned), hipMemcpyHostToDevice, stream));
     if (!rb.uploaded) HIP_TRY(hipEventCreateWithFlags(&rb.uploaded, hipEventDisableTiming));
     HIP_TRY(hipEventRecord(rb.uploaded, stream));
@@ -1839,11 +1758,8 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     rb.map = m;
     rb.most = (int)most;
     rb.most_marched = most_marched;
-    rb.nempty = L > 0 ? 0 : (int)empty_tiles.size();
+    rb.nempty = (int)empty_tiles.size();
     rb.nwork = (int)work.size();
-    rb.seg_len = L;
-    rb.nseg_tiles = nslots;
-    rb.icap = nslots;
     rb.nstreams = 0;
     const vr_status st = note_region_stream(rb, stream, &c->region_slot);
     if (st != VR_OK) return st;
@@ -2202,7 +2118,7 @@ try {
         // schedule 0 = one 8x8 tile per wave in row order, 4 = in rings;
         // otherwise (auto) the cost-sorted schedule
         void* sort_buf = nullptr;
-        Schedule sc{c->schedule == SCHED_RINGS ? SCHED_RINGS : SCHED_STATIC, 0, 0, 1, 1, nullptr, nullptr, {}, 1, 0, 4, 0, nullptr};
+        Schedule sc{c->schedule == SCHED_RINGS ? SCHED_RINGS : SCHED_STATIC, 0, 0, 1, 1, nullptr, nullptr, {}, 1, 0, 4, nullptr};
         if (sc.kind == SCHED_RINGS) box_centre_pixel(c, a, &sc.center_x, &sc.center_y);
         // the sort passes enumerate whole 64x64 regions (vr_march_kernels.h sort_pixel)
         if (c->schedule != SCHED_STATIC && c->schedule != SCHED_RINGS && a.width < 65536 && a.out_rows < 65536 &&
@@ -2318,63 +2234,28 @@ try {
     const int tpw = c->tiles_per_wave > 0 ? c->tiles_per_wave
                     : kind == SCHED_REGIONS ? (pl.layout == LAYOUT_COL48 ? 3 : 2)
                     : kind == SCHED_RINGS ? 2 : 1;
-    Schedule sc{kind, 0, 0, tpw, c->waves_per_simd, c->d_heads, nullptr, {}, 1, 0, c->wg_waves, 0, nullptr};
+    Schedule sc{kind, 0, 0, tpw, c->waves_per_simd, c->d_heads, nullptr, {}, 1, 0, c->wg_waves, nullptr};
     sc.slab = pl.layout == LAYOUT_COL48 && c->slab;
     a.slab_cap = c->slab_cap;
     if (kind == SCHED_RINGS || kind == SCHED_REGIONS) box_centre_pixel(c, a, &sc.center_x, &sc.center_y);
     if (kind == SCHED_REGIONS) {
         const bool splittable = is_b4_family(pl.layout) || pl.layout == LAYOUT_ZPAIR || pl.layout == LAYOUT_CORNER8 ||
                                 pl.layout == LAYOUT_CORNERH || pl.layout == LAYOUT_COL48Z;
-        // ray segments for the long tiles (march_regions_seg instances)
-        const bool segable = !sc.slab && (pl.layout == LAYOUT_COL48 || pl.layout == LAYOUT_BRICK4832 ||
-                                          pl.layout == LAYOUT_CORNERH);
-        const int seg_len = segable ? c->segment : 0;
-        const vr_status st = build_regions(c, a, tpw, sc.center_x, sc.center_y, seg_len,
-                                           static_cast<hipStream_t>(stream));
+        const vr_status st = build_regions(c, a, tpw, sc.center_x, sc.center_y, static_cast<hipStream_t>(stream));
         if (st != VR_OK) return st;
         const Ctx::RegionBuf& rb = c->region[c->region_cur];
-        sc.tiles = rb.d + kRegionHeader + 2 * (size_t)rb.icap;
+        sc.tiles = rb.d + kRegionHeader;
         sc.hdr = reinterpret_cast<const int*>(rb.d);
         sc.map = rb.map;
         // the default kernels march the lists' first hdr[kRegionWork + x] entries
-        // and fill the rest (tile_is_empty); the experiments' kernels march all
-        const bool fill = c->empty_fill && c->region_exact && !sc.slab && rb.seg_len == 0 && !lat_on(c, pl.layout);
+        // and fill the rest (tile_is_empty); the slab march marches all
+        const bool fill = c->empty_fill && c->region_exact && !sc.slab;
         a.empty_fill = fill ? 1 : 0;
         // Waves: as many as before (the list over tiles_per_wave), but no more
         // than marched entries -- the waves that held only empty tiles go;
         // each marched tile keeps a wave of its own where it had one
         if (fill && rb.most_marched > 0) sc.map.nwx = std::max(1, std::min(sc.map.nwx, rb.most_marched));
-        if (rb.seg_len > 0) {
-            // segmented lists (one lane per ray): the terms scratch must hold
-            // every segmented tile's rays at this frame's max_steps
-            const size_t need = (size_t)rb.nseg_tiles * (size_t)std::max(a.max_steps, 1) * 64 * sizeof(float);
-            if (need > c->terms_bytes) {
-                if (c->d_terms) {
-                    HIP_TRY(hipDeviceSynchronize());   // growth only: queued frames may use the old scratch
-                    (void)hipFree(c->d_terms);
-                }
-                c->d_terms = nullptr;
-                c->terms_bytes = 0;
-                const size_t want = std::max(need, std::min(need + need / 4, kMaxTermsBytes));
-                if (hipMalloc(&c->d_terms, want) != hipSuccess) {
-                    (void)hipGetLastError();
-                    return fail(VR_ERR_OOM, "vr_render: segment terms (%zu bytes)", want);
-                }
-                c->terms_bytes = want;
-            }
-            sc.seg.terms = c->d_terms;
-            sc.seg.info = reinterpret_cast<const uint2*>(rb.d + kRegionHeader);
-            sc.seg.len = rb.seg_len;
-            sc.seg_tiles = rb.nseg_tiles;
-        } else if (lat_on(c, pl.layout) && !sc.slab) {
-            // step-split rays on the latency-mode march
-            // (vr_march_lat.hip): K lanes per ray, c->lat rounds of loads in flight
-            const int K = c->split > 0 ? c->split : auto_split(c, rb.nwork);
-            const int most = rb.most;
-            sc.lat = c->lat;
-            sc.split = K;
-            sc.map.nwx = std::max(1, (most * K + tpw - 1) / tpw);
-        } else if (splittable) {
+        if (splittable) {
             // step-split rays: K lanes per ray when the frame
             // share is too small to fill the GPU with one-lane-per-ray waves
             int K = c->split;
@@ -2391,7 +2272,7 @@ try {
         }
     }
     HIP_TRY(launch_march(a, pl.layout, pl.wrap, pl.early, sc, hs));
-    if (c->launch_cache && sc.seg_tiles == 0 && sc.lat == 0) {   // remember it (not the experiments' scratch paths)
+    if (c->launch_cache) {   // remember it
         Ctx::Cached& e = c->lc[c->lc_next];
         c->lc_next = (c->lc_next + 1) % (int)(sizeof c->lc / sizeof c->lc[0]);
         e.valid = true;

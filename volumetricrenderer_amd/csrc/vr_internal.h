@@ -70,9 +70,8 @@ __host__ __device__ constexpr bool is_b4_family(int l)
 
 // Variants measured slower than the defaults and kept as the record of that
 // (DESIGN.md sec. 4, 5.1-5.4): the layouts other than the auto ones, the
-// queue / strided / XCD-row schedules, 8- and 16-wave workgroups, the
-// latency-mode march (lat), ray segments (segment), and the procedural
-// sort_reuse / proc_enum options.  They are compiled only with
+// queue / strided / XCD-row schedules, 8- and 16-wave workgroups, and the
+// procedural sort_reuse / proc_enum options.  They are compiled only with
 // VR_EXPERIMENTS=1 (make EXPERIMENTS=1); the default library refuses their
 // options.  The LDS slab march (north star; option slab, off by default) is
 // in every build so that its parity test runs in the default GPU suite.
@@ -229,26 +228,18 @@ struct TileMap {
     int nwx;
 };
 // The regions schedule's lists in device memory: a header of kRegionHeader
-// ints, the segmented tiles' info (SegArgs.info, `icap` uint2 entries; option
-// "segment"), then the list entries.  The header:
+// ints, then the list entries.  The header:
 //   [0..8]   off[]: XCD x renders the entries [off[x], off[x+1])
 //   [9]      tiles with estimated work    [10] the longest list
-//   [11]     entries                       [12] segmented tiles (kRegionSegTiles)
+//   [11]     entries
 //   [16..23] marched tiles of XCD x (kRegionWork): its list holds the tiles
 //            with estimated work, then the other tiles some ray of which may
 //            meet the box, then the empty ones (tile_is_empty) -- those last
 //            are written with the uncovered value, not marched
 // Built on the host (vr_api.cpp build_regions) or, for a moving camera, on
-// the GPU (vr_regions.hip launch_region_build, the same dealing; no segments).
+// the GPU (vr_regions.hip launch_region_build, the same dealing).
 constexpr int kRegionHeader = 24;
 constexpr int kRegionWork = 16;
-constexpr int kRegionSegTiles = 12;
-// Ray segments (vr_march_kernels.h march_regions_seg / seg_resolve)
-struct SegArgs {
-    float* terms;          // [slot][max_steps][64]: each ray's per-step terms
-    const uint2* info;     // [slot]: {tile (ty << 16 | tx), segments}
-    int len;               // L, steps per segment (0 = no segments)
-};
 struct RegionBuild {
     int tw, th, width, out_rows, band_rows, band_stride, band_first, max_steps;
     int height;
@@ -335,10 +326,7 @@ struct Schedule {
     int split;             // regions: lanes per ray (1, 2, 4, 8; BRICK4 / CORNER8 only)
     int slab;              // regions + COL48: the LDS slab march (vr_march_slab.hip)
     int wg_waves;          // regions (one lane per ray): waves per workgroup, 4 (default), 8 or 16
-    int lat;               // regions: latency-mode march (vr_march_lat.hip), rounds of loads in flight (0 = off)
     const int* hdr;        // regions: the lists' device header (kRegionHeader; off[x] per XCD)
-    SegArgs seg = {};      // regions: ray segments of the long tiles (seg.len 0 = none)
-    int seg_tiles = 0;     // regions: segmented tiles (the resolve pass's waves)
 };
 
 // Cost-sort scratch of the procedural march (vr_march.hip launch_march_procedural),
@@ -393,10 +381,6 @@ hipError_t launch_assemble_grey(const uint8_t* d_gathered, size_t rows_per_rank,
                                 int band_rows, bool f32, int first_rank, uint8_t* d_frame, hipStream_t s);
 hipError_t launch_march_corner8(const MarchArgs& a, int layout, bool early, const Schedule& sc,
                                 hipStream_t s);   // CORNER8 / CORNERH, vr_march_c8.hip
-// latency-mode march for small frame shares (vr_march_lat.hip): sc.split lanes per
-// ray, sc.lat rounds of loads in flight; lat_supported(layout) says which layouts
-hipError_t launch_march_lat(const MarchArgs& a, int layout, bool early, const Schedule& sc, hipStream_t s);
-bool lat_supported(int layout);
 hipError_t launch_march_slab(const MarchArgs& a, bool early, const Schedule& sc, hipStream_t s);   // vr_march_slab.hip
 constexpr int kSlabMaxChunks = 32;   // per channel and wave (64 B each): 8 KiB of LDS per wave
 // sort_buf (sort_layout) selects the cost-sorted schedule; null = 8x8

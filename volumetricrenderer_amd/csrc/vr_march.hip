@@ -150,10 +150,6 @@ hipError_t launch_march_procedural(const MarchArgs& a, bool early, void* sort_bu
 hipError_t launch_march(const MarchArgs& a, int layout, int wrap, bool early, const Schedule& sc, hipStream_t s)
 {
     if (a.width <= 0 || a.out_rows <= 0) return hipSuccess;
-#if VR_EXPERIMENTS
-    if (sc.kind == SCHED_REGIONS && sc.lat > 0 && lat_supported(layout))
-        return launch_march_lat(a, layout, early, sc, s);   // vr_march_lat.hip
-#endif
     switch (layout) {
     case LAYOUT_BRICK4832: return launch_lw<LAYOUT_BRICK4832, WRAP_CLAMP>(a, early, sc, s);
     case LAYOUT_COL48:

@@ -1,9 +1,10 @@
 // vr_march_c8.hip -- the CORNER8 / CORNERH (cache-resident volume) instantiations of
-// the ray march.  A separate translation unit because it is built with
-// -fno-slp-vectorize: the SLP vectoriser packs pairs of scalar lerps into
-// v_pk_* ops whose operands then need v_mov pairs; for this VALU-bound
-// kernel that is 5 % slower at 128^3 (0.097 -> 0.092 ms), while the brick
-// kernels gain from it.
+// the ray march, in a translation unit of their own so that they compile in
+// parallel with vr_march.hip's.  Like vr_march.hip it is built with
+// -fno-slp-vectorize (Makefile FLAGS_*): the SLP vectoriser packs pairs of
+// scalar lerps into v_pk_* ops, no faster than two plain ones on gfx950, whose
+// operands then need v_mov pairs -- 5 % slower for this VALU-bound kernel at
+// 128^3 (0.097 -> 0.092 ms without it).
 #include "vr_march_kernels.h"
 
 namespace vr {

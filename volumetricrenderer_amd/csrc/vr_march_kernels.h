@@ -1188,169 +1188,6 @@ __global__ __launch_bounds__(kThreads) VR_UM_ATTR void march_regions_u(const Mar
     regions_body<LAYOUT, WRAP, EARLY, ZO, kThreads / 64, UM>(a, tiles, hdr, nwx, lds);
 }
 
-#if VR_EXPERIMENTS   // measured slower than step-split rays
-// ---- ray segments (regions schedule, option "segment") ----
-// With a small frame share (N GPUs) a launch ends with its longest rays: a
-// wave marching a 200-step ray alone on its SIMD issues ~100 VALU ops per
-// step whatever the memory system does, so neither more loads in flight nor
-// more waves shorten it.  A long tile is therefore marched as segments of L
-// steps, one wave each: segment s of a ray computes the terms of steps
-// [sL, sL + L) (the last segment: to the ray's end) and stores them; the
-// resolve pass then adds each ray's terms in step order, so acc is the
-// reference's sequential sum (frag.glsl:71-73) bit for bit, early-out and
-// step count included.  A segment reaches its first point by the same s*L
-// fp32 adds as the reference loop (:74), never as P0 + sL * step.
-// List entry of a segment: bit 31, segment index in bits 24-30, the tile's
-// slot in bits 0-23; SegArgs.info[slot] = {tile (ty << 16 | tx), segments}.
-template <int LAYOUT, bool ZO, int UM>
-__device__ __forceinline__ void march_pixel_seg(const MarchArgs& a, const FastCtx& f, int x, int orow, int s0, int s1,
-                                                float* __restrict__ terms)
-{
-    const Ray r = setup_ray(a, x, orow);
-    float uv[4] = {};
-    if constexpr (UM != 0)
-        for (int t = 0; t < 4; ++t)
-            if ((UM >> t) & 1) uv[t] = noise::in_vgpr(a.uval[t]);
-    const int e = min(s1, r.n);
-    if (s0 >= e) return;
-    f2 pxy = r.pxy;
-    float pz = r.pz;
-    for (int j = 0; j < s0; ++j) { pxy = pxy + r.sxy; pz = pz + r.sz; }   // :74, s0 times
-    const float scale = LAYOUT == LAYOUT_CORNERH ? f.scale : a.scale;
-    if constexpr (LAYOUT != LAYOUT_CORNERH) {
-        // march_pixel's pipelined loop: step i+1's loads issued before step i's blend
-        TapRaw c0 = fetch_u<UM, 0, LAYOUT, ZO>(a, f, pxy, pz), c1 = fetch_u<UM, 1, LAYOUT, ZO>(a, f, pxy, pz);
-        TapRaw c2 = fetch_u<UM, 2, LAYOUT, ZO>(a, f, pxy, pz), c3 = fetch_u<UM, 3, LAYOUT, ZO>(a, f, pxy, pz);
-        for (int i = s0; i < e; ++i) {
-            const f2 cxy = pxy;
-            const float cz = pz;
-            pxy = pxy + r.sxy;
-            pz = pz + r.sz;
-            const bool more = i + 1 < e;
-            const f2 qxy = more ? pxy : cxy;
-            const float qz = more ? pz : cz;
-            const TapRaw n0 = fetch_u<UM, 0, LAYOUT, ZO>(a, f, qxy, qz), n1 = fetch_u<UM, 1, LAYOUT, ZO>(a, f, qxy, qz);
-            const TapRaw n2 = fetch_u<UM, 2, LAYOUT, ZO>(a, f, qxy, qz), n3 = fetch_u<UM, 3, LAYOUT, ZO>(a, f, qxy, qz);
-            const float t0 = blend_u<UM, 0, LAYOUT>(c0, uv), t1 = blend_u<UM, 1, LAYOUT>(c1, uv);
-            const float t2 = blend_u<UM, 2, LAYOUT>(c2, uv), t3 = blend_u<UM, 3, LAYOUT>(c3, uv);
-            terms[(size_t)i * 64] = ((t0 * t1) * (t2 + t3)) * scale;                    // :71-73's term
-            c0 = n0; c1 = n1; c2 = n2; c3 = n3;
-        }
-    } else {
-        for (int i = s0; i < e; ++i) {
-            const float t0 = blend_u<UM, 0, LAYOUT>(fetch_u<UM, 0, LAYOUT, ZO>(a, f, pxy, pz), uv);
-            const float t1 = blend_u<UM, 1, LAYOUT>(fetch_u<UM, 1, LAYOUT, ZO>(a, f, pxy, pz), uv);
-            const float t2 = blend_u<UM, 2, LAYOUT>(fetch_u<UM, 2, LAYOUT, ZO>(a, f, pxy, pz), uv);
-            const float t3 = blend_u<UM, 3, LAYOUT>(fetch_u<UM, 3, LAYOUT, ZO>(a, f, pxy, pz), uv);
-            terms[(size_t)i * 64] = ((t0 * t1) * (t2 + t3)) * scale;
-            pxy = pxy + r.sxy;
-            pz = pz + r.sz;
-        }
-    }
-}
-
-// Regions schedule with segments: a list entry is a whole tile (march_pixel)
-// or one segment of a long tile (march_pixel_seg; no pixel store, no steps:
-// seg_resolve does both)
-template <int LAYOUT, int WRAP, bool EARLY, bool ZO, int UM>
-__global__ __launch_bounds__(kThreads) void march_regions_seg(const MarchArgs a, const unsigned* __restrict__ tiles,
-                                                             const int* __restrict__ hdr, int nwx, SegArgs sg)
-{
-    extern __shared__ __attribute__((aligned(16))) unsigned lds[];
-    const int xcd = blockIdx.x & 7;
-    const int w = (int)(blockIdx.x >> 3) * (kThreads / 64) + (threadIdx.x >> 6);
-    const int begin = hdr[xcd], count = hdr[xcd + 1] - begin;
-    if ((int)(blockIdx.x >> 3) * (kThreads / 64) >= count) return;   // whole workgroup, before the barrier
-    const FastCtx f = fast_prologue<LAYOUT>(a, lds);
-    const int lane = threadIdx.x & 63;
-    const int lx = lane_x<LAYOUT>(lane), ly = lane_y<LAYOUT>(lane);
-    unsigned long long steps = 0;
-    for (int k = w; w < nwx && k < count; k += nwx) {
-        const unsigned t = tiles[begin + k];
-        if (t >> 31) {
-            const unsigned slot = t & 0xffffffu;
-            const int seg = (int)((t >> 24) & 0x7fu);
-            const uint2 inf = sg.info[slot];
-            const int s0 = seg * sg.len, s1 = seg + 1 >= (int)inf.y ? a.max_steps : s0 + sg.len;
-            march_pixel_seg<LAYOUT, ZO, UM>(a, f, (int)(inf.x & 0xffffu) * 8 + lx, (int)(inf.x >> 16) * 8 + ly, s0, s1,
-                                            sg.terms + (size_t)slot * (size_t)a.max_steps * 64 + lane);
-        } else {
-            steps += march_pixel<LAYOUT, WRAP, EARLY, ZO, UM>(a, f, (int)(t & 0xffffu) * 8 + lx, (int)(t >> 16) * 8 + ly);
-        }
-    }
-    if (a.step_counter) add_steps(a, steps);
-}
-
-// The segmented tiles' rays: each lane adds its ray's stored terms in step
-// order (kSegBatch loads in flight), with march_pixel's early-out and step
-// count, then the epilogue (:76-80) and the store.  One wave per tile.
-constexpr int kSegBatch = 32;
-template <int LAYOUT, bool EARLY>
-__global__ __launch_bounds__(256) void seg_resolve(const MarchArgs a, const int* __restrict__ hdr, SegArgs sg)
-{
-    const int slot = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
-    if (slot >= hdr[kRegionSegTiles]) return;
-    const int lane = threadIdx.x & 63;
-    const uint2 inf = sg.info[slot];
-    const int x = (int)(inf.x & 0xffffu) * 8 + lane_x<LAYOUT>(lane), orow = (int)(inf.x >> 16) * 8 + lane_y<LAYOUT>(lane);
-    const Ray r = setup_ray(a, x, orow);
-    const float* __restrict__ tp = sg.terms + (size_t)slot * (size_t)a.max_steps * 64 + lane;
-    float acc = 0.0f;
-    int i = 0;
-    bool stop = false;
-    // the wave's longest ray: batches of kSegBatch loads, all in flight
-    // before the first add (a batch costs one memory round trip)
-    int nmax = r.n;
-    for (int off = 32; off > 0; off >>= 1) nmax = max(nmax, __shfl_xor(nmax, off));
-    for (int b = 0; b < nmax && !stop; b += kSegBatch) {
-        float v[kSegBatch];
-#pragma unroll
-        for (int j = 0; j < kSegBatch; ++j) v[j] = b + j < r.n ? tp[(size_t)(b + j) * 64] : 0.0f;
-#pragma unroll
-        for (int j = 0; j < kSegBatch; ++j) {
-            if (b + j < r.n && !stop) {
-                acc = acc + v[j];
-                ++i;
-                if constexpr (EARLY) stop = acc > a.acc_limit;
-            }
-        }
-    }
-    if (r.live) {
-        const float at = acc * a.step_size;
-        store_pixel(a, x, orow, r.n >= 0, 1.0f - spec_expf(a.density * fminf(-at, 0.0f)));
-    }
-    if (a.step_counter) add_steps(a, r.n > 0 ? (unsigned long long)i : 0ull);
-}
-
-template <int L, int W>
-void launch_regions_seg(const MarchArgs& a, bool early, const Schedule& sc, size_t lds, hipStream_t s)
-{
-    const dim3 grid((unsigned)(8 * ((sc.map.nwx + 3) / 4))), block(kThreads);
-    const int um = a.umask;
-    if (!early && a.zero_offsets && (um == 1 || um == 2 || um == 4 || um == 8)) {
-#define VR_SG(U) hipLaunchKernelGGL((march_regions_seg<L, W, false, true, U>), grid, block, lds, s, a, sc.tiles, sc.hdr, sc.map.nwx, sc.seg)
-        if (um == 1) VR_SG(1);
-        else if (um == 2) VR_SG(2);
-        else if (um == 4) VR_SG(4);
-        else VR_SG(8);
-#undef VR_SG
-    } else if (early && a.zero_offsets) {
-        hipLaunchKernelGGL((march_regions_seg<L, W, true, true, 0>), grid, block, lds, s, a, sc.tiles, sc.hdr, sc.map.nwx, sc.seg);
-    } else if (early) {
-        hipLaunchKernelGGL((march_regions_seg<L, W, true, false, 0>), grid, block, lds, s, a, sc.tiles, sc.hdr, sc.map.nwx, sc.seg);
-    } else if (a.zero_offsets) {
-        hipLaunchKernelGGL((march_regions_seg<L, W, false, true, 0>), grid, block, lds, s, a, sc.tiles, sc.hdr, sc.map.nwx, sc.seg);
-    } else {
-        hipLaunchKernelGGL((march_regions_seg<L, W, false, false, 0>), grid, block, lds, s, a, sc.tiles, sc.hdr, sc.map.nwx, sc.seg);
-    }
-    if (sc.seg_tiles > 0) {
-        const dim3 rgrid((unsigned)((sc.seg_tiles + 3) / 4));
-        if (early) hipLaunchKernelGGL((seg_resolve<L, true>), rgrid, dim3(256), 0, s, a, sc.hdr, sc.seg);
-        else hipLaunchKernelGGL((seg_resolve<L, false>), rgrid, dim3(256), 0, s, a, sc.hdr, sc.seg);
-    }
-}
-
-#endif   // VR_EXPERIMENTS
 
 // ---- step-split rays (regions schedule) ----
 // A wave whose rays march alone on their SIMD waits ~110 dependent memory
@@ -2159,14 +1996,6 @@ hipError_t launch_lw(const MarchArgs& a, bool early, const Schedule& sc, hipStre
             hipLaunchKernelGGL((march_rings<L, W, false, false>), grid, block, lds, s, a, cx, cy, nw, npos);
         return hipGetLastError();
     }
-#if VR_EXPERIMENTS
-    if constexpr (L == LAYOUT_COL48 || L == LAYOUT_BRICK4832 || L == LAYOUT_CORNERH) {
-        if (sc.kind == SCHED_REGIONS && sc.seg.len > 0) {
-            launch_regions_seg<L, W>(a, early, sc, lds, s);
-            return hipGetLastError();
-        }
-    }
-#endif
     if constexpr (is_b4_family(L) || L == LAYOUT_ZPAIR || L == LAYOUT_CORNER8 || L == LAYOUT_CORNERH ||
                   L == LAYOUT_COL48Z) {
         if (sc.kind == SCHED_REGIONS && sc.split > 1) {
