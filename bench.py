@@ -697,13 +697,16 @@ def main() -> int:
         overlap = (native and streams_eff >= 2) or proc_inflight2 or (world == 1 and args.inflight == 2)
         roof_ms = ms_per_step if overlap else kern_ms
         compositor = native and pipe is not None and pipe.compositor
+        lead = pipe.lead_rows if compositor else 0   # rank 0's lead rows beside its assembly
         rows_part = native and pipe is not None and pipe.partition == "rows"
         if compositor:   # rank 0 renders nothing: the per-GPU figure is a renderer's average share
             nr = world - 1
             roofline = roofline_of(r, proc, shadow, variant, frame_steps // nr, frame_evals // nr,
                                    (frame_cells // nr) if local_cells is not None else None, roof_ms)
             roofline["achieved_def"] += (f"; rank 0 is a compositor (vr_shard_set_compositor): the work is the "
-                                         f"frame's over its {nr} rendering ranks")
+                                         f"frame's over its {nr} rendering ranks"
+                                         + (f" (rank 0 also renders the frame's first {lead} rows, "
+                                            "vr_shard_balance_lead)" if lead else ""))
         else:
             roofline = roofline_of(r, proc, shadow, variant, local_steps, local_evals, local_cells, roof_ms)
         if overlap:
@@ -782,7 +785,7 @@ def main() -> int:
                                            if proc is not None else ", 1 render stream"))
                                        if native and world == 1 else
                                        ((f"row ranges x{world - 1}" if rows_part else f"bands16x{world - 1}")
-                                        + ", rank 0 compositing" if compositor
+                                        + ", rank 0 compositing" + (f" + {lead} lead rows" if lead else "") if compositor
                                         else (f"row ranges x{world}" if rows_part else f"bands16x{world}"))
                                        + (", 2 frames in flight (two streams and targets)"
                                           if args.inflight == 2 or proc_inflight2 else "")

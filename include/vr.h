@@ -286,6 +286,13 @@ vr_status vr_row_partition(void* ctx, int width, int height, int parts, int* row
 vr_status vr_row_partition_measured(void* ctx, int width, int height, int parts, const int* prev_begin,
                                     const double* prev_ms, int* row_begin);
 
+/* The estimate vr_row_partition splits: the march work of every 8-row strip
+ * of a width x height frame for the ctx's current camera and march constants
+ * (strip_work[nstrips], nstrips = ceil(height / 8); host, double; the same
+ * inputs give the same values on every rank).  vr_shard_balance_lead sizes
+ * rank 0's lead rows from it.  New (no reference counterpart).            */
+vr_status vr_row_work(void* ctx, int width, int height, double* strip_work, int nstrips);
+
 /* ---- introspection: the kernel variant vr_render will launch ----------- */
 /* returns a static string, e.g. "grid_pad16_clamp"                        */
 const char* vr_kernel_variant(void* ctx);

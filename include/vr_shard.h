@@ -213,6 +213,21 @@ int       vr_shard_aborted(vr_shard* sh);
  * the renders held the machine (bench.py roofline.kernel_busy_ms_per_frame).
  * New (no reference counterpart). */
 vr_status vr_shard_sampled_busy(vr_shard* sh, double* busy_ms, double* span_ms);
+/* Rank 0's lead rows (round 6; new, no reference counterpart): with rank 0 as
+ * a compositor over band sets, rank 0 also renders the frame rows
+ * [0, rows) in place -- a row range beside its assembly -- and renderer k's
+ * band set starts below them (frame band rows/band_rows + k - 1, stride
+ * nranks - 1).  rows: a multiple of band_rows below the frame height; 0 = none
+ * (the default).  Set before the first frames; vr_shard_set_compositor(0)
+ * and row ranges clear it.  vr_shard_balance_lead (collective) sizes it for
+ * the ctx's camera: rank 0 counts as pct % of a renderer, and of every lead
+ * of whole bands it takes the one whose largest estimated cost -- rank 0's
+ * lead work / (pct / 100), or a renderer's band-set work (vr_row_work) -- is
+ * smallest, and broadcasts it.  vr_shard_bands reports band_first -1 for rank 0
+ * and the offset sets of the renderers. */
+vr_status vr_shard_set_lead_rows(vr_shard* sh, int rows);
+int       vr_shard_get_lead_rows(vr_shard* sh);
+vr_status vr_shard_balance_lead(vr_shard* sh, int pct);
 /* Self-test of the deadline loop on the host (no GPU, no RCCL): mode 0 a
  * state that completes after 5 polls, 1 one that fails at the 3rd, 2 one that
  * never completes.  Returns 0 done, 1 failed, 2 deadline (-1 bad mode) and

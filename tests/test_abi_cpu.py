@@ -32,7 +32,7 @@ def test_shard_library_exports_every_declared_symbol():
     from volumetricrenderer_amd import _lib
     lib = _lib.load_shard()
     declared = header_functions("vr_shard.h")
-    assert len(declared) == 31
+    assert len(declared) == 34
     for name in declared:
         assert hasattr(lib, name), name
     assert sorted(declared) == _lib.shard_exported_symbols()
@@ -77,6 +77,15 @@ def test_shard_deadline_loop_selftest():
     with pytest.raises(_lib.VRError):
         _lib.shard_call("vr_shard_set_timeout", None, 1.0)
     assert _lib.shard_call("vr_shard_aborted", None) == 0
+    # round 6: lead rows and the sampled busy time refuse a null shard
+    with pytest.raises(_lib.VRError):
+        _lib.shard_call("vr_shard_set_lead_rows", None, 16)
+    with pytest.raises(_lib.VRError):
+        _lib.shard_call("vr_shard_balance_lead", None, 80)
+    assert _lib.shard_call("vr_shard_get_lead_rows", None) == -1
+    b, sp = ctypes.c_double(), ctypes.c_double()
+    with pytest.raises(_lib.VRError):
+        _lib.shard_call("vr_shard_sampled_busy", None, ctypes.byref(b), ctypes.byref(sp))
     assert _lib.STATUS_NAMES[7] == "VR_ERR_TIMEOUT" and _lib.STATUS_NAMES[8] == "VR_ERR_COMM"
 
 

@@ -213,6 +213,61 @@ def test_native_pipeline_loopback_ranks(world, band_rows, fmt, W, render_streams
             pl.close()
 
 
+@pytest.mark.parametrize("world,fmt,W,render_streams,lead", [(2, 1, 500, 2, 16), (3, 0, 499, 1, 112),
+                                                              (8, 1, 500, 2, "pct80"), (8, 2, 500, 3, 48),
+                                                              (8, 1, 499, 2, 272), (4, 1, 500, 4, "pct50"),
+                                                              (8, 0, 500, 2, 0)])
+def test_native_pipeline_loopback_lead_rows(world, fmt, W, render_streams, lead):
+    """Rank 0 as a compositor that also renders the frame's lead rows in place
+    (vr_shard_set_lead_rows / vr_shard_balance_lead; verdict r05 #5): the
+    renderers' band sets start below the lead rows (vr_shard_bands reports
+    the offset sets), the assembly expands the frame below them, and the frame
+    equals a plain render -- explicit lead rows (0, one band, up to a quarter
+    of the frame) and a lead sized from the camera (pct of a mean share), on
+    1-4 render streams.  Bad lead rows are refused."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import volumetricrenderer_amd as vr
+    from volumetricrenderer_amd import _lib
+    from volumetricrenderer_amd.distributed import RcclBandPipeline
+    H = 283
+    with vr.Renderer(0) as r:
+        r.generate_volume(vr.volume_recipe_defaults(size=64))
+        osd, gsd = vr.reference_shader_data(W / H, -30.0, 40.0)
+        r.set_shader_data(osd, gsd)
+        r.set_march(vr.march_defaults())
+        kw = dict(lead_pct=int(lead[3:])) if isinstance(lead, str) else dict(lead_rows=lead)
+        pl = RcclBandPipeline(r, W, H, fmt, band_rows=16, world=world, rank=0, loopback=True,
+                              render_streams=render_streams, compositor=True, **kw)
+        try:
+            for bad in (8, -16, 288):   # not whole bands / negative / past the frame
+                with pytest.raises(vr.VRError):
+                    _lib.shard_call("vr_shard_set_lead_rows", pl._h, bad)
+            pl.run_frames(3)
+            pl.barrier()
+            lr = pl.lead_rows
+            if isinstance(lead, str):   # (the balance may choose no lead rows on a small frame)
+                assert lr >= 0 and lr % 16 == 0, lr
+            else:
+                assert lr == lead
+            assert pl.my_rows == lr and pl.band_first == -1
+            assert pl.rows_per_rank == vr.band_rows_packed(H, 16, world - 1, lr // 16)
+            got = pl.frame()
+            full = r.render(W, H, fmt)
+            torch.cuda.synchronize()
+            assert np.array_equal(got.cpu().numpy(), full.cpu().numpy())
+            with pytest.raises(vr.VRError):   # the geometry is fixed once frames are queued
+                _lib.shard_call("vr_shard_set_lead_rows", pl._h, lr + 16)
+        finally:
+            pl.close()
+    with vr.Renderer(0) as r:   # lead rows need the compositor over band sets
+        r.generate_volume(vr.volume_recipe_defaults(size=32))
+        r.set_shader_data(osd, gsd)
+        with pytest.raises(ValueError):
+            RcclBandPipeline(r, W, H, fmt, band_rows=16, world=world, rank=0, loopback=True, compositor=False,
+                             lead_rows=16)
+
+
 @pytest.mark.parametrize("world,compositor,fmt,W,render_streams", [(2, False, 1, 500, 2), (5, False, 0, 499, 1),
                                                                    (8, True, 1, 500, 2), (8, False, 2, 500, 4),
                                                                    (3, True, 1, 499, 3)])
@@ -308,7 +363,8 @@ SPIN_DEG = 1.6   # TestMain.cpp:171-184, :222-224: the held A/D key, 100 deg/s x
 @pytest.mark.parametrize("fmt,render_streams,threads,on_render,compositor",
                          [(0, 2, 1, False, None), (1, 2, 1, False, None), (1, 1, 1, False, None),
                           (1, 2, 2, False, None), (0, 2, 1, True, None), (1, 2, 1, True, False),
-                          (1, 1, 1, True, True), (1, 3, 1, True, None), (0, 4, 1, True, False)])
+                          (1, 1, 1, True, True), (1, 3, 1, True, None), (0, 4, 1, True, False),
+                          (1, 2, 1, True, "lead")])
 def test_native_loopback_spinning_8_ranks(oracle, fmt, render_streams, threads, on_render, compositor):
     """A moving camera through the native 8-rank frame loop (loopback: this
     process renders every rank's interleaved band set): 40 frames, frame i
@@ -316,7 +372,9 @@ def test_native_loopback_spinning_8_ranks(oracle, fmt, render_streams, threads, 
     flight, on two alternating render streams (the default) or one.  Frames
     1, 33 and 40, assembled on rank 0, equal the oracle's whole frame bit for
     bit (RGBA32F and RGBA8).  At 8 ranks rank 0 is a compositor by default
-    (renders no bands); compositor=False keeps it rendering in place."""
+    (renders no bands); compositor=False keeps it rendering in place;
+    "lead": the compositor also renders 48 lead rows in place, and the band
+    sets start below them, for the moving camera."""
     import sys
     sys.path.insert(0, ROOT)
     import volumetricrenderer_amd as vr
@@ -330,9 +388,10 @@ def test_native_loopback_spinning_8_ranks(oracle, fmt, render_streams, threads, 
         r.set_march(vr.march_defaults())
         pl = RcclBandPipeline(r, W, H, fmt, band_rows=16, world=8, rank=0, loopback=True,
                               render_streams=render_streams, host_threads=threads, exchange_on_render=on_render,
-                              compositor=compositor)
+                              compositor=True if compositor == "lead" else compositor,
+                              lead_rows=48 if compositor == "lead" else None)
         assert pl.compositor == (compositor is not False)
-        assert pl.my_rows == (0 if pl.compositor else pl.rows_per_rank)
+        assert pl.my_rows == (pl.lead_rows if pl.compositor else pl.rows_per_rank)
         got, done = {}, 0
         try:
             for stop in (1, 33, 40):
@@ -341,6 +400,8 @@ def test_native_loopback_spinning_8_ranks(oracle, fmt, render_streams, threads, 
                     from volumetricrenderer_amd import _lib
                     with pytest.raises(vr.VRError):
                         _lib.shard_call("vr_shard_set_compositor", pl._h, 0 if pl.compositor else 1)
+                    if compositor == "lead":
+                        assert pl.lead_rows == 48 and pl.my_rows == pl.lead_rows
                 assert pl.host_ms >= 0.0
                 done = stop
                 got[stop] = pl.frame()
@@ -365,7 +426,8 @@ def band_set_of(frame, rank, world, band_rows):
                          [(2, 3, 1, False, None, "bands"), (2, 32, 1, False, None, "bands"),
                           (1, 3, 1, False, None, "bands"), (2, 3, 2, False, None, "bands"),
                           (2, 3, 1, True, None, "bands"), (2, 3, 1, True, True, "bands"),
-                          (2, 3, 1, True, None, "rows"), (2, 3, 1, True, True, "rows")])
+                          (2, 3, 1, True, None, "rows"), (2, 3, 1, True, True, "rows"),
+                          (2, 3, 1, True, True, "lead")])
 def test_native_solo_rank_spinning(oracle, render_streams, interval, threads, on_render, compositor, partition):
     """One rank of a 4-rank frame loop rehearsed alone (vr_shard_set_solo:
     its band set only, no exchange) with a moving camera: 24 frames with their
@@ -374,7 +436,9 @@ def test_native_solo_rank_spinning(oracle, render_streams, interval, threads, on
     still in flight on the other stream (per-stream retire events).  The band
     set of frames 1, 7, 20 and 24 equals the rows of the oracle's frame.
     partition="rows": the rank's contiguous row range instead, balanced for
-    the first frame's camera and kept for the others."""
+    the first frame's camera and kept for the others.  "lead": band sets
+    below rank 0's lead rows (vr_shard_balance_lead at the first frame; on
+    this small frame the balance may choose no lead)."""
     import sys
     sys.path.insert(0, ROOT)
     import volumetricrenderer_amd as vr
@@ -389,12 +453,20 @@ def test_native_solo_rank_spinning(oracle, render_streams, interval, threads, on
         r.set_march(vr.march_defaults())
         pl = RcclBandPipeline(r, W, H, 1, band_rows=16, world=world, rank=rank, loopback=True, solo=True,
                               render_streams=render_streams, host_threads=threads, exchange_on_render=on_render,
-                              compositor=compositor, partition=partition)
+                              compositor=compositor, partition="bands" if partition == "lead" else partition,
+                              lead_pct=60 if partition == "lead" else None)
+        if partition == "lead":
+            pl.run_frames(1, cameras=cams[:1])   # sizes the lead rows for the first camera
+            assert pl.lead_rows >= 0 and pl.lead_rows % 16 == 0
         stride, first = pl.band_stride, pl.band_first
-        assert (stride, first) == ((world - 1, rank - 1) if compositor else (world, rank))
-        got, done = {}, 0
+        lead_band = pl.lead_rows // 16
+        assert (stride, first) == ((world - 1, rank - 1 + lead_band) if compositor else (world, rank))
+        got, done = {}, (1 if partition == "lead" else 0)
         try:
             for stop in (1, 7, 20, 24):
+                if stop <= done:
+                    got[stop] = pl.frame()
+                    continue
                 pl.run_frames(stop - done, cameras=cams[done:stop])
                 done = stop
                 got[stop] = pl.frame()
@@ -410,6 +482,10 @@ def test_native_solo_rank_spinning(oracle, render_streams, interval, threads, on
             want = ref[pl.row_range[0]:pl.row_range[0] + pl.row_range[1], :, 0]
         else:
             want = band_set_of(ref, first, stride, 16)[..., 0]
+            # (a set holding the frame's last, partial band has that band's
+            # rows past the frame packed too: vr_band_rows_packed counts whole bands)
+            assert img.shape[0] == vr.band_rows_packed(H, 16, stride, first)
+            img = img[:want.shape[0]]
         assert img.shape == want.shape and np.array_equal(img.cpu().numpy(), want), i
 
 

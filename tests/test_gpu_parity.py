@@ -1741,6 +1741,16 @@ def test_row_ranges_match_the_frame(oracle, vol128, fmt):
         rb = rr.row_partition(W, H, 5)
         assert rb[0] == 0 and rb[-1] == H and all(b % 8 == 0 for b in rb[1:-1])
         assert all(a <= b for a, b in zip(rb, rb[1:]))
+        # the strip work it splits (vr_row_work): boundary k sits at the strip
+        # edge nearest the k/5 quantile of the prefix sums
+        sw = np.array(rr.row_work(W, H))
+        assert sw.shape == ((H + 7) // 8,) and (sw > 0).all()
+        pre = np.concatenate([[0.0], np.cumsum(sw)])
+        for k in range(1, 5):
+            e = int(np.argmin(np.abs(pre - pre[-1] * k / 5)))
+            assert abs(rb[k] // 8 - e) <= 1, (k, rb, e)
+        with pytest.raises(vr.VRError):   # nstrips must be ceil(H / 8)
+            _lib.call("vr_row_work", rr._ctx, W, H, (ctypes.c_double * 3)(), 3)
         for k in range(5):
             if rb[k + 1] > rb[k]:
                 rr.render_rows(W, H, fmt, rb[k], rb[k + 1] - rb[k], out=frame, in_place=True)

@@ -48,6 +48,9 @@ def main():
     ap.add_argument("--rebalance", action="store_true",
                     help="--native --all-ranks, row ranges: a second pass with the ranges split again by every "
                          "rank's measured render time (vr_row_partition_measured, as vr_shard_rebalance_rows does)")
+    ap.add_argument("--lead-pct", type=int, default=-1,
+                    help="--native, compositor over band sets: rank 0 also renders lead rows, counted as this %% of a "
+                         "renderer (vr_shard_balance_lead); -1 = the pipeline's auto choice, 0 = no lead rows")
     ap.add_argument("--partition", default="auto", choices=["auto", "bands", "rows"],
                     help="--native: interleaved band sets or balanced contiguous row ranges (RcclBandPipeline)")
     ap.add_argument("--exchange", default="render", choices=["render", "comm"],
@@ -157,9 +160,12 @@ def one_n(a, r, W, H, n, streams, base, rows):
                                  loopback=True, solo=True, render_streams=ns, host_threads=a.threads,
                                  exchange_on_render=a.exchange == "render",
                                  compositor=None if a.compositor == "auto" else a.compositor == "on",
-                                 partition="rows" if rows else a.partition, rows=rows)
+                                 partition="rows" if rows else a.partition, rows=rows,
+                                 lead_pct="auto" if a.lead_pct < 0 else (a.lead_pct or None))
             p.run_frames(8)   # region lists, code objects
             p.barrier()
+            if first == 0 and p.lead_rows and ns == streams[0]:
+                print(f"  N={n}: rank 0 lead rows {p.lead_rows}", flush=True)
             for k in range(a.rounds):
                 p.run_frames(4)
                 p.barrier()

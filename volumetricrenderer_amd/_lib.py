@@ -135,6 +135,7 @@ _SIGS = {
                                                ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, _vp]),
     "vr_band_rows_packed": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "vr_row_partition": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_int_p]),
+    "vr_row_work": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
     "vr_row_partition_measured": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_int_p,
                                                  ctypes.POINTER(ctypes.c_double), c_int_p]),
     "vr_kernel_variant": (ctypes.c_char_p, [_vp]),
@@ -219,6 +220,9 @@ _SHARD_SIGS = {
     "vr_shard_set_timeout": (ctypes.c_int, [_vp, ctypes.c_double]),
     "vr_shard_aborted": (ctypes.c_int, [_vp]),
     "vr_shard_sampled_busy": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
+    "vr_shard_set_lead_rows": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "vr_shard_get_lead_rows": (ctypes.c_int, [_vp]),
+    "vr_shard_balance_lead": (ctypes.c_int, [_vp, ctypes.c_int]),
     "vr_shard_set_render_streams": (ctypes.c_int, [_vp, ctypes.c_int]),
     "vr_shard_get_render_streams": (ctypes.c_int, [_vp]),
     "vr_shard_set_solo": (ctypes.c_int, [_vp, ctypes.c_int]),
@@ -236,7 +240,7 @@ _SHARD_SIGS = {
 }
 # shard functions whose int return is a value, not a vr_status
 _SHARD_VALUE_RETURNS = {"vr_shard_aborted", "vr_shard_poll_selftest", "vr_shard_get_render_streams",
-                        "vr_shard_get_compositor", "vr_shard_partition"}
+                        "vr_shard_get_compositor", "vr_shard_partition", "vr_shard_get_lead_rows"}
 _shard_lib = None
 
 

@@ -7,23 +7,13 @@
 // step replaces the EnqueueRenderPass + vkCmdDrawIndexed path of
 // TestMain.cpp:194-217.  No exception crosses the ABI; errors go through
 // vr_last_error().
-#include <algorithm>
-#include <cmath>
-#include <cstdarg>
-#include <cstdio>
-#include <cstring>
-#include <exception>
-#include <new>
-#include <stdexcept>
-#include <string>
-#include <vector>
+//
+// The context type and the shared helpers are in vr_ctx.h; the options, the
+// region lists / row partition and the procedural scratch live in
+// vr_options.cpp, vr_regions_host.cpp and vr_proc_host.cpp.
+#include "vr_ctx.h"
 
-#include "../../include/vr.h"
-#include "vr_internal.h"
-
-using namespace vr;
-
-namespace {
+namespace vrapi {
 
 thread_local std::string g_err;
 
@@ -56,228 +46,6 @@ vr_status caught_exception(const char* fn) noexcept
     }
 }
 
-#define HIP_TRY(expr)                                                                        \
-    do {                                                                                     \
-        hipError_t e_ = (expr);                                                              \
-        if (e_ != hipSuccess)                                                                \
-            return fail(e_ == hipErrorOutOfMemory ? VR_ERR_OOM : VR_ERR_HIP, "%s: %s (%s:%d)", \
-                        #expr, hipGetErrorString(e_), __FILE__, __LINE__);                   \
-    } while (0)
-
-constexpr int kDefaultSchedule = -1;     // -1 auto, 0 static tiles, 1 persistent queue, 2 strided
-constexpr int kDefaultWavesPerSimd = 4;
-constexpr int kDefaultTilesPerWave = 0;   // 0 = auto: 2 for rings and regions, 1 for strided (measured)
-constexpr int kDefaultWedges = 8;         // regions schedule: wedges per XCD (measured; 4 until round 4)
-// a moving camera reuses the current (still complete, maybe less balanced)
-// region lists for this many renders before they are rebuilt
-constexpr int kRegionRebuildInterval = 32;
-// Procedural cost sort under a moving camera: with option sort_reuse = R > 0 a
-// frame with the same target and march settings but another camera marches the
-// order built for an older one, for R renders after the build (vr_render; the
-// march then also checks the pixels the old order left out, so every frame
-// stays exact).
-constexpr size_t kSortKeyGridPart = 11;   // leading sort-key entries a stale order must match
-constexpr int kMaxRegionStreams = 4;
-// largest deferred-shadow scratch (option "shadow_defer_mib"): the scratch is
-// sized from the frame (ensure_defer: ~0.35 GB at 1080p x 128, ~2.7 GB at
-// 3840 x 2160 x 256); a frame needing more marches its last waves' shadow rays
-// in place
-constexpr int kMaxDeferMiB = 4 << 10;
-// retired deferred scratch buffers kept before a device sync frees them
-constexpr size_t kMaxDeferRetired = 4;
-constexpr int kRegionKeyLen = 39;
-// auto split (lanes per ray) from the frame share's tiles with work: K = 1 at
-// >= 6000, 2 at >= 1400, else 4.  Measured on 1/N of the 1080p frame at 512^3
-// (~7,500 tiles with work): K = 1, 2, 2, 4 at N = 1, 2, 4, 8.
-// K = 2 beats K = 1 by 17 % at N = 2 and K = 4 by 2-5 % at N = 4; at 4K x 256
-// (4x the tiles) it keeps K = 1 up to N = 4.
-constexpr long long kSplitOneLane = 6000, kSplitTwoLanes = 1400;
-// With consecutive frames overlapping on two streams (option frames_overlap,
-// set by vr_shard_run_frames) the next frame's waves fill the SIMDs while this
-// one's longest rays finish, so one lane per ray pays from fewer tiles on:
-// K = 1 from 2500 (1080p at 512^3, N = 2: 0.0583 ms per frame at K = 1 against
-// 0.0632 at K = 2; on one stream 0.0921 against 0.0744; profiles/r05/split_overlap.txt)
-constexpr long long kSplitOneLaneOverlap = 2500;
-
-struct Plan {
-    int layout, wrap;
-    bool early;
-};
-
-struct Ctx {
-    int device = 0;
-    // volume (channel planes; see vr_internal.h Layout)
-    int nx = 0, ny = 0, nz = 0;
-    uint8_t* d_planar = nullptr;   // canonical planes (LAYOUT_PLANAR)
-    int uniform_mask = 0;          // channels whose every texel is uniform_val[c] (install_volume)
-    uint8_t uniform_val[4] = {};
-    // the install's per-plane min / max scan, read back asynchronously and
-    // resolved at first use (resolve_uniform): no host wait inside the install,
-    // so a collective volume share keeps its deadline (vr_shard.cpp)
-    unsigned* d_mm = nullptr;      // device [min x 4, max x 4]
-    unsigned* h_mm = nullptr;      // pinned copy
-    hipEvent_t mm_ready = nullptr;
-    bool mm_pending = false;
-    int uniform_skip = 1;          // option "uniform_skip": 0 = load uniform channels anyway
-    uint8_t* d_fast = nullptr;     // one fast layout, built from d_planar
-    int fast_layout = 0;           // which one (0 = none)
-    size_t fast_plane_bytes = 0;
-    // uniforms
-    bool has_camera = false;
-    float obj[48];
-    float glob[36];
-    vr_march_params march;
-    int layout_pref = 0;           // 0 = auto (kDefaultFastLayout), else a Layout
-    // schedule of the march kernel (vr_set_option "schedule", "waves_per_simd")
-    int schedule = kDefaultSchedule;
-    int waves_per_simd = kDefaultWavesPerSimd;
-    int tiles_per_wave = kDefaultTilesPerWave;
-    int* d_heads = nullptr;        // 8 queue heads (+ padding), zeroed per launch
-    vr_procedural proc{};          // procedural medium (configs 2/3), off by default
-    int count = 0;                 // step_counter: 0 = executed ray-steps, 1 = density evaluations,
-                                   // 2 = Worley cells computed (procedural)
-    void* d_sort = nullptr;        // procedural cost-sort scratch (sort_layout), grown on demand
-    size_t sort_bytes = 0;
-    // deferred shadow rays (option "shadow_defer", vr_internal.h ShadowDefer):
-    // counter, per-wave step counts and records, entries; grown on demand
-    int shadow_defer_mib = kMaxDeferMiB;   // largest deferred-shadow scratch; a frame needing more compacts in-wave
-    int shadow_blocks = 0;         // option "shadow_blocks": workgroups of the deferred shadow pass (0 = auto)
-    int shadow_defer = 1;          // measured 1.25 -> 0.99 ms at config 3
-    int shadow_cache = 0;          // deferred shadow pass: Worley cube cached in registers per lane
-    void* d_defer = nullptr;
-    size_t defer_bytes = 0;
-    unsigned long long defer_ent_cap = 0;   // entries / step records / waves the current scratch holds
-    unsigned defer_rec_cap = 0, defer_waves = 0;
-    // entries / step records per pixel-step (per wave-step) of the frame: 5/4 of
-    // the largest need seen (proc_scan -> need_host); 1/12 and 1/8 until one is
-    double want_ent = 0.0, want_rec = 0.0;
-    double need_pixsteps = 0.0, need_wavesteps = 0.0;   // of the frame whose need is pending
-    unsigned defer_entries = 0;    // option "shadow_defer_entries": entry capacity override (tests; 0 = sized from the frame)
-    int defer_last = 0;            // the last procedural render ran the deferred passes
-    // outgrown scratch buffers: queued frames may still use them.  Each gets an
-    // event recorded on the render stream of the writing frame that outgrew it,
-    // after that stream has waited for every earlier procedural render
-    // (proc_uses), and is freed by a later ensure_defer once the event has
-    // completed
-    struct Retired {
-        void* p;
-        hipEvent_t ev;             // nullptr until recorded
-    };
-    std::vector<Retired> defer_retired;
-    // The procedural scratch (d_sort, d_defer) is written by a frame that
-    // sorts (SORT_BUILD) or defers its shadow rays, and only read by a frame
-    // that reuses the order.  A writer waits for every earlier procedural
-    // render on other streams; a reader only for the last writer.  So frames
-    // that reuse one camera's order overlap on alternating streams (2 in
-    // flight), and a frame that writes never races a reader.
-    struct ProcUse {
-        hipStream_t s;
-        hipEvent_t ev;     // recorded after the stream's last procedural render
-    };
-    std::vector<ProcUse> proc_uses;      // one per stream (at most kMaxProcStreams)
-    hipEvent_t proc_wev = nullptr;       // after the last writer
-    hipStream_t proc_wstream = nullptr;
-    bool proc_wpending = false;
-    unsigned long long* h_need = nullptr;   // host-mapped [entries, records] written by the last sorting frame
-    unsigned long long* d_need = nullptr;   // its device address
-    hipEvent_t need_ev = nullptr;
-    bool need_pending = false;
-    // regions schedule (build_regions): per-XCD tile lists, double-buffered
-    // so a rebuild never waits for more than the render that last used the
-    // other buffer (2 frames in flight, VulkanRenderer.cpp:13)
-    int wedges = kDefaultWedges;   // wedges per XCD
-    int split = 0;                 // lanes per ray: 0 = auto, 1, 2, 4, 8
-    int slab = 0;                  // COL48 + regions: the LDS slab march (vr_march_slab.hip)
-    int proc_enum = 0;             // procedural sort: 1 = 64x64-region enumeration with shadow rays too
-    int slab_cap = kSlabMaxChunks; // its chunks per channel (<= kSlabMaxChunks; smaller forces the fallback)
-    // regions: each XCD's list 0 = inside-out (ring, angle); 1 = longest tile first;
-    // 2 = longest S x S block first (the default since round 4)
-    int region_order = 2;
-    int wg_waves = 4;              // regions: waves per workgroup (4, 8, 16)
-    int supertile = 2;             // regions: list order by S x S blocks of tiles (1 = per tile; 2 measured 1 % faster)
-    int region_interval = kRegionRebuildInterval;   // option "region_interval": renders a moved camera reuses the lists
-    int region_gpu = 1;            // option "region_gpu": 1 = a moved camera's lists are rebuilt on the GPU
-    void* d_rg = nullptr;          // GPU list build scratch (region_build_bytes), zeroed when allocated
-    size_t rg_bytes = 0;
-    int* h_rghdr = nullptr;        // host-mapped copy of the last GPU build's header (kRegionHeader ints)
-    hipEvent_t rg_ev = nullptr;    // recorded after that build
-    bool rg_pending = false;
-    int rg_buf = -1;               // the region buffer it built
-    long long gpu_builds = 0;      // read-only option "region_gpu_builds"
-    bool rg_preloaded = false;     // region_build_preload done
-    struct RegionBuf {
-        unsigned* d = nullptr;     // device: kRegionHeader ints (off[9], tiles with work, longest, tiles), then the list
-        unsigned* h = nullptr;     // pinned staging copy (host builds)
-        size_t cap = 0;            // entries
-        TileMap map{};             // host copy: nwx (and off[] for host builds)
-        int most = 0;              // the longest per-XCD list (sizes the launch)
-        int most_marched = 0;         // the most marched entries of one XCD (hdr[kRegionWork + x])
-        int nwork = 0;             // tiles with estimated work
-        int nempty = -1;           // empty tiles (tile_is_empty) in the lists (-1: GPU build not yet complete)
-        // The streams that rendered with these lists, and per stream an event
-        // recorded after its FIRST render with them (one event per stream and
-        // build, never one per render).  These lists are rewritten two builds
-        // later; by then every stream that used them has either rendered with
-        // the newer lists -- and the newer lists' first-render event on that
-        // stream follows all its renders with these -- or it is the rebuilding
-        // stream itself, whose order covers them.  A stream that is neither
-        // costs a device sync (as do more than kMaxRegionStreams streams).  An
-        // event is never recorded on a remembered stream, which the caller may
-        // have destroyed since (r04's abort), only on the rendering one.
-        hipStream_t streams[kMaxRegionStreams] = {};
-        hipEvent_t used[kMaxRegionStreams] = {};
-        bool first_rec[kMaxRegionStreams] = {};   // used[i] recorded after stream i's first render
-        int nstreams = 0;          // -1: more streams than tracked
-        hipEvent_t uploaded = nullptr;   // the list upload (on streams[0]); other streams wait for it
-        hipStream_t upload_stream = nullptr;
-    } region[2];
-    int region_cur = -1;           // buffer of the current lists (-1 = none)
-    int region_slot = -1;          // the last render stream's slot in them (note_region_stream)
-    float region_key[kRegionKeyLen] = {};   // geometry the current lists were built for
-    bool region_exact = false;   // the current lists were built for this render's camera (their empty tiles hold)
-    long long renders_since_build = 0;
-    // procedural cost sort: the geometry whose order d_sort holds (n per pixel
-    // depends only on it, not on the medium), valid until the buffer changes
-    std::vector<float> sort_key;
-    long long renders_since_sort = 0;   // renders with a stale order since it was built
-    int sort_reuse = 0;                 // option "sort_reuse": renders a stale order serves (0 = sort every changed frame)
-    // Perlin lattice table of the procedural march (noise::perlin_lattice_entry),
-    // built when (seed, lo, n) changes; option "lattice" 0 turns it off
-    int lattice = 1;
-    // option "inject_throw" (tests of the exception guard): the next vr_render
-    // throws std::runtime_error (1) or std::bad_alloc (2) in its host path
-    int inject_throw = 0;
-    // Launch cache of the grid march (option "launch_cache", default 1): the
-    // last few renders' kernel arguments keyed by target and stream, valid
-    // while `gen` is unchanged -- every call that can change a grid launch
-    // (shader data, march constants, volume, options, a region-list build or
-    // a GPU build's sizing) bumps it.  A repeated render of an unchanged frame
-    // (the static camera of a frame stream; the two parities of the multi-GPU
-    // loop) then skips the basis, plan and list bookkeeping and only launches.
-    unsigned long long gen = 1;
-    int launch_cache = 1;
-    int empty_fill = 1;          // option "empty_fill": regions launches fill the lists' empty tiles, not march them
-    int frames_overlap = 0;      // option "frames_overlap": consecutive renders overlap (auto split rule)
-    // vr_row_partition's work model: a ray costs steps^(row_pow / 100) + row_setup
-    int row_setup = 40, row_pow = 130;   // config 4 at 8 ranks, profiles/r05/row_ranges_c4.txt
-    int row_first_pct = 100;     // range 0's share of the work, % of the mean (the loop's rank 0 also assembles)
-    struct Cached {
-        bool valid = false;
-        unsigned long long gen = 0;
-        vr_target t{};
-        hipStream_t stream = nullptr;
-        MarchArgs a{};
-        Plan pl{};
-        Schedule sc{};
-        int kind = 0;
-        int slot = -1;   // the stream's slot in the region lists (note_region_render)
-    } lc[4];
-    int lc_next = 0;
-    long long lc_hits = 0;         // read-only option "launch_cache_hits"
-    uint2* d_lat = nullptr;
-    size_t lat_cap = 0;            // bytes allocated
-    long long lat_key[3] = {0, 0, -1};
-};
 
 // Auto layout (measured): CORNERH (16 B per texel: one load
 // and four v_fma_mix_f32 per tap, no byte conversions, arithmetic index) and
@@ -490,13 +258,11 @@ const char* variant_name(const Plan& p)
     return names[p.layout][p.early ? 1 : 0];
 }
 
-}  // namespace
+}  // namespace vrapi
 
-static void poll_region_header(Ctx* c);
+using namespace vrapi;
 
 extern "C" {
-
-static vr_status release_defer(Ctx* c);
 
 const char* vr_last_error(void) { return g_err.c_str(); }
 int vr_abi_version(void) { return VR_ABI_VERSION; }
@@ -528,81 +294,6 @@ try {
     return VR_OK;
 } catch (...) {
     return caught_exception("vr_volume_recipe_defaults");
-}
-
-vr_status vr_procedural_defaults(vr_procedural* p)
-try {
-    if (!p) return fail(VR_ERR_INVALID, "vr_procedural_defaults: null");
-    std::memset(p, 0, sizeof *p);
-    p->enabled = 0;
-    p->grid_scale = 128.0f;     // TestMain.cpp:51 grid, frequencies in texel units
-    p->octaves = 4;
-    p->freq0 = 0.19f;           // TestMain.cpp:61
-    p->lacunarity = 2.0f;
-    p->gain = 0.5f;
-    p->seed_fbm = 3;
-    p->worley_freq = 0.03f;     // TestMain.cpp:60
-    p->seed_worley = 2;
-    p->shadow_steps = 0;
-    const double n = std::sqrt(1.0 + 1.0 + 4.0);
-    p->sun_dir[0] = (float)(1.0 / n); p->sun_dir[1] = (float)(1.0 / n); p->sun_dir[2] = (float)(2.0 / n);
-    return VR_OK;
-} catch (...) {
-    return caught_exception("vr_procedural_defaults");
-}
-
-constexpr long long kMaxWorleyTableBytes = 32 << 10;   // LDS per workgroup for the cell table
-
-// z pitch of the Worley cell table (entries): the smallest pz >= n*n for which
-// no two cells at most one apart on each axis share a ds_read_b128 bank slot
-// (index mod 16), fewest aliases among cells two apart.  The lanes of a sorted
-// wave sit in neighbouring cells; with pz = n*n (81 = 1 mod 16) cells
-// (x+1, y, z-1) and (x, y, z) collide.
-int worley_z_pitch(int n)
-{
-    int best = n * n, best_al = 1 << 30;
-    for (int pz = n * n; pz < n * n + 16; ++pz) {
-        int al1 = 0, al2 = 0;
-        for (int dz = -2; dz <= 2; ++dz)
-            for (int dy = -2; dy <= 2; ++dy)
-                for (int dx = -2; dx <= 2; ++dx) {
-                    if (!dx && !dy && !dz) continue;
-                    if (((dx + n * dy + pz * dz) % 16 + 16) % 16) continue;
-                    (std::abs(dx) <= 1 && std::abs(dy) <= 1 && std::abs(dz) <= 1 ? al1 : al2) += 1;
-                }
-        const int score = al1 * 1000 + al2;
-        if (score < best_al) { best_al = score; best = pz; }
-    }
-    return best;
-}
-
-vr_status vr_set_procedural(void* ctx, const vr_procedural* p)
-try {
-    if (!ctx || !p) return fail(VR_ERR_INVALID, "vr_set_procedural: null argument");
-    if (p->enabled) {
-        if (p->octaves < 0 || p->octaves > 16) return fail(VR_ERR_INVALID, "vr_set_procedural: octaves in [0,16]");
-        if (p->shadow_steps < 0 || p->shadow_steps > 256)
-            return fail(VR_ERR_INVALID, "vr_set_procedural: shadow_steps in [0,256]");
-        const double l = std::sqrt((double)p->sun_dir[0] * p->sun_dir[0] + (double)p->sun_dir[1] * p->sun_dir[1] +
-                                   (double)p->sun_dir[2] * p->sun_dir[2]);
-        if (p->shadow_steps > 0 && !(l > 0.0)) return fail(VR_ERR_INVALID, "vr_set_procedural: zero sun_dir");
-        if (p->reserved) return fail(VR_ERR_INVALID, "vr_set_procedural: reserved must be 0");
-        if (!std::isfinite(p->grid_scale) || !std::isfinite(p->freq0) || !std::isfinite(p->lacunarity) ||
-            !std::isfinite(p->gain) || !std::isfinite(p->worley_freq) || !std::isfinite(p->sun_dir[0]) ||
-            !std::isfinite(p->sun_dir[1]) || !std::isfinite(p->sun_dir[2]))
-            return fail(VR_ERR_INVALID, "vr_set_procedural: parameters must be finite");
-    }
-    Ctx* c = as_ctx(ctx);
-    ++c->gen;
-    c->proc = *p;
-    if (p->enabled && p->shadow_steps > 0) {   // normalise in double, round once
-        const double l = std::sqrt((double)p->sun_dir[0] * p->sun_dir[0] + (double)p->sun_dir[1] * p->sun_dir[1] +
-                                   (double)p->sun_dir[2] * p->sun_dir[2]);
-        for (int a = 0; a < 3; ++a) c->proc.sun_dir[a] = (float)((double)p->sun_dir[a] / l);
-    }
-    return VR_OK;
-} catch (...) {
-    return caught_exception("vr_set_procedural");
 }
 
 vr_status vr_create(int device, void** out)
@@ -959,1021 +650,6 @@ try {
     return -1;
 }
 
-// Balanced contiguous row ranges (vr.h; the multi-GPU loop's row partition,
-// DESIGN.md sec. 7.3).  Work of an 8-row strip: over the rays through pixel
-// (8i + 4, 8s + 4), the a3 step count of the box chord (frag.glsl:42-46, as
-// the region build's estimate: double, no clip test) plus kRaySetup for a ray
-// that meets the box, kRayMiss for one that does not.  Boundary k is the strip
-// edge nearest to the k/parts quantile of the prefix sums.
-// prev / prev_ms (vr_row_partition_measured): every strip of range k of the
-// previous partition `prev` is weighted by prev_ms[k] / (the model's work of
-// range k), so the split follows the measured times where the model is off
-static vr_status row_partition(void* p, int width, int height, int parts, const int* prev, const double* prev_ms,
-                               int* row_begin, const char* fn)
-{
-    if (!p || !row_begin) return fail(VR_ERR_INVALID, "%s: null argument", fn);
-    if (width <= 0 || height <= 0 || parts <= 0 || parts > 4096)
-        return fail(VR_ERR_INVALID, "%s: bad frame %dx%d or parts %d", fn, width, height, parts);
-    if (prev) {
-        bool ok = prev[0] == 0 && prev[parts] == height;
-        for (int k = 1; k <= parts && ok; ++k) ok = prev[k] >= prev[k - 1] && (prev[k] % 8 == 0 || prev[k] == height);
-        for (int k = 0; k < parts && ok; ++k) ok = std::isfinite(prev_ms[k]) && prev_ms[k] >= 0.0;
-        if (!ok) return fail(VR_ERR_INVALID, "%s: bad previous partition or times", fn);
-    }
-    Ctx* c = as_ctx(p);
-    if (!c->has_camera) return fail(VR_ERR_NO_CAMERA, "%s: no shader data (vr_set_shader_data)", fn);
-    RayBasis b;
-    if (!make_ray_basis(c->obj, c->glob, width, height, &b))
-        return fail(VR_ERR_INVALID, "%s: Projection*View is singular", fn);
-    const double kRaySetup = (double)c->row_setup, kRayMiss = 2.0, pw = c->row_pow / 100.0;
-    const vr_march_params& m = c->march;
-    const double step = (1.0 / (double)m.max_steps) * (double)m.step_scale;
-    const int ns = (height + 7) / 8;
-    std::vector<double> w((size_t)ns, 0.0);
-    for (int s = 0; s < ns; ++s) {
-        const double fy = std::min(8.0 * s + 4.0, height - 0.5);
-        for (int x = 4; x < width + 4; x += 8) {
-            const double fx = std::min((double)x, width - 0.5);
-            double d[3], len = 0.0;
-            for (int k = 0; k < 3; ++k) {
-                d[k] = (double)b.o[k] + fx * (double)b.px[k] + fy * (double)b.py[k];
-                len += d[k] * d[k];
-            }
-            len = std::sqrt(len);
-            double tn = -INFINITY, tf = INFINITY;
-            for (int k = 0; k < 3; ++k) {
-                const double ta = ((double)m.box_min[k] - (double)b.org[k]) * len / d[k];
-                const double tb = ((double)m.box_max[k] - (double)b.org[k]) * len / d[k];
-                tn = std::max(tn, std::min(ta, tb));
-                tf = std::min(tf, std::max(ta, tb));
-            }
-            const bool hit = tn <= tf && std::isfinite(tf) && tf > 0.0;
-            w[(size_t)s] += hit ? std::pow(std::min((double)m.max_steps, (tf - std::max(tn, 0.0)) / step), pw) + kRaySetup
-                                : kRayMiss;
-        }
-    }
-    if (prev) {   // measured / modelled time of each previous range, on its strips
-        for (int k = 0; k < parts; ++k) {
-            const int s0 = prev[k] / 8, s1 = std::min(ns, (prev[k + 1] + 7) / 8);
-            double est = 0.0;
-            for (int s = s0; s < s1; ++s) est += w[(size_t)s];
-            if (s1 > s0 && est > 0.0 && prev_ms[k] > 0.0)
-                for (int s = s0; s < s1; ++s) w[(size_t)s] *= prev_ms[k] / est;
-        }
-    }
-    std::vector<double> prefix((size_t)ns + 1, 0.0);
-    for (int s = 0; s < ns; ++s) prefix[(size_t)s + 1] = prefix[(size_t)s] + w[(size_t)s];
-    const double total = prefix[(size_t)ns];
-    row_begin[0] = 0;
-    int j = 0;
-    // range 0 takes f of a mean share, the others equal shares of the rest
-    const double f = parts > 1 ? c->row_first_pct / 100.0 : 1.0, g = parts > 1 ? (parts - f) / (parts - 1) : 1.0;
-    for (int k = 1; k < parts; ++k) {
-        const double target = total * (f + (k - 1) * g) / parts;
-        while (j < ns && prefix[(size_t)j + 1] < target) ++j;
-        // strip edge j or j + 1, whichever prefix is nearer the quantile
-        int e = j;
-        if (j < ns && prefix[(size_t)j + 1] - target < target - prefix[(size_t)j]) e = j + 1;
-        row_begin[k] = std::max(row_begin[k - 1], std::min(8 * e, height));
-    }
-    row_begin[parts] = height;
-    return VR_OK;
-}
-
-vr_status vr_row_partition(void* p, int width, int height, int parts, int* row_begin)
-try {
-    return row_partition(p, width, height, parts, nullptr, nullptr, row_begin, "vr_row_partition");
-} catch (...) {
-    return caught_exception("vr_row_partition");
-}
-
-vr_status vr_row_partition_measured(void* p, int width, int height, int parts, const int* prev_begin,
-                                    const double* prev_ms, int* row_begin)
-try {
-    if (!prev_begin || !prev_ms) return fail(VR_ERR_INVALID, "vr_row_partition_measured: null argument");
-    return row_partition(p, width, height, parts, prev_begin, prev_ms, row_begin, "vr_row_partition_measured");
-} catch (...) {
-    return caught_exception("vr_row_partition_measured");
-}
-
-vr_status vr_set_layout_preference(void* p, int pref)
-try {
-    if (!p || pref < 0 || pref >= kNumLayouts) return fail(VR_ERR_INVALID, "vr_set_layout_preference: bad argument");
-    if (pref > 0 && !layout_built(pref))
-        return fail(VR_ERR_INVALID, "vr_set_layout_preference: layout %d is built only with VR_EXPERIMENTS "
-                                    "(make EXPERIMENTS=1; measured slower, DESIGN.md sec. 4)", pref);
-    Ctx* c = as_ctx(p);
-    ++c->gen;
-    HIP_TRY(hipSetDevice(c->device));
-    c->layout_pref = pref;
-    vr_status st = ensure_fast_layout(c, nullptr);
-    if (st == VR_OK && hipDeviceSynchronize() != hipSuccess) return fail(VR_ERR_HIP, "vr_set_layout_preference: sync");
-    return st;
-} catch (...) {
-    return caught_exception("vr_set_layout_preference");
-}
-
-vr_status vr_set_option(void* p, const char* name, int value)
-try {
-    if (!p || !name) return fail(VR_ERR_INVALID, "vr_set_option: null argument");
-    Ctx* c = as_ctx(p);
-    ++c->gen;
-    const std::string n(name);
-    // variants measured slower than the defaults (vr_internal.h VR_EXPERIMENTS)
-    const bool experimental = (n == "schedule" && (value == SCHED_QUEUE || value == SCHED_STRIDED ||
-                                                   value == SCHED_XCDROWS)) ||
-                              (n == "wg_waves" && value != 4) ||
-                              (n == "segment" && value != 0) ||
-                              (n == "sort_reuse" && value != 0) ||
-                              (n == "proc_enum" && value != 0);
-    if (experimental && !VR_EXPERIMENTS)
-        return fail(VR_ERR_INVALID, "vr_set_option: %s = %d is built only with VR_EXPERIMENTS (make EXPERIMENTS=1; "
-                                    "measured slower, DESIGN.md)", name, value);
-    if (n == "layout") return vr_set_layout_preference(p, value);
-    if (n == "launch_cache") {
-        if (value < 0 || value > 1) return fail(VR_ERR_INVALID, "vr_set_option: launch_cache is 0 or 1");
-        c->launch_cache = value;
-        return VR_OK;
-    }
-    if (n == "row_setup" || n == "row_pow" || n == "row_first_pct") {   // vr_row_partition's work model
-        if (value < 0 || value > 1000 || (n == "row_pow" && value < 50) || (n == "row_first_pct" && value > 100))
-            return fail(VR_ERR_INVALID, "vr_set_option: %s out of range", n.c_str());
-        (n == "row_setup" ? c->row_setup : n == "row_pow" ? c->row_pow : c->row_first_pct) = value;
-        return VR_OK;
-    }
-    if (n == "frames_overlap") {   // the caller overlaps consecutive frames on two streams (auto split)
-        if (value < 0 || value > 1) return fail(VR_ERR_INVALID, "vr_set_option: frames_overlap is 0 or 1");
-        if (c->frames_overlap != value) ++c->gen;
-        c->frames_overlap = value;
-        return VR_OK;
-    }
-    if (n == "empty_fill") {   // regions: fill the lists' empty tiles instead of marching them
-        if (value < 0 || value > 1) return fail(VR_ERR_INVALID, "vr_set_option: empty_fill is 0 or 1");
-        c->empty_fill = value;
-        ++c->gen;
-        return VR_OK;
-    }
-    if (n == "inject_throw") {   // test hook: the next vr_render throws in its host path
-        if (value < 0 || value > 2)
-            return fail(VR_ERR_INVALID, "vr_set_option: inject_throw is 0, 1 (std::runtime_error) or 2 (std::bad_alloc)");
-        c->inject_throw = value;
-        return VR_OK;
-    }
-    if (n == "schedule") {
-        if (value < -1 || value > 5)
-            return fail(VR_ERR_INVALID, "vr_set_option: schedule is -1 (auto), 0 (static), 1 (queue), "
-                                        "2 (strided), 3 (xcd rows), 4 (rings) or 5 (regions)");
-        c->schedule = value;
-        return VR_OK;
-    }
-    if (n == "waves_per_simd") {
-        if (value < 1 || value > 8) return fail(VR_ERR_INVALID, "vr_set_option: waves_per_simd in [1, 8]");
-        c->waves_per_simd = value;
-        return VR_OK;
-    }
-    if (n == "tiles_per_wave") {
-        if (value < 0 || value > 64)
-            return fail(VR_ERR_INVALID, "vr_set_option: tiles_per_wave in [1, 64], or 0 for auto");
-        c->tiles_per_wave = value;
-        return VR_OK;
-    }
-    if (n == "split") {
-        if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8)
-            return fail(VR_ERR_INVALID, "vr_set_option: split is 0 (auto), 1, 2, 4 or 8");
-        c->split = value;
-        return VR_OK;
-    }
-    if (n == "wedges") {
-        if (value < 1 || value > 64) return fail(VR_ERR_INVALID, "vr_set_option: wedges in [1, 64]");
-        c->wedges = value;
-        return VR_OK;
-    }
-    if (n == "proc_enum") {
-        if (value < 0 || value > 1) return fail(VR_ERR_INVALID, "vr_set_option: proc_enum is 0 or 1");
-        c->proc_enum = value;
-        return VR_OK;
-    }
-    if (n == "shadow_defer_mib") {
-        if (value < 0) return fail(VR_ERR_INVALID, "vr_set_option: shadow_defer_mib >= 0");
-        c->shadow_defer_mib = value;
-        return value == 0 ? release_defer(c) : VR_OK;
-    }
-    if (n == "shadow_defer_entries") {
-        if (value < 0) return fail(VR_ERR_INVALID, "vr_set_option: shadow_defer_entries >= 0");
-        c->defer_entries = (unsigned)value;
-        return release_defer(c);
-    }
-    if (n == "shadow_cache") {
-        if (value < 0 || value > 2)
-            return fail(VR_ERR_INVALID, "vr_set_option: shadow_cache is 0 (lane per entry), 1 (+ register Worley cube) "
-                                        "or 2 (8 lanes per entry)");
-        c->shadow_cache = value;
-        return VR_OK;
-    }
-    if (n == "shadow_blocks") {
-        if (value < 0 || value > 65536) return fail(VR_ERR_INVALID, "vr_set_option: shadow_blocks in [0, 65536]");
-        c->shadow_blocks = value;
-        return VR_OK;
-    }
-    if (n == "shadow_defer") {
-        if (value < 0 || value > 1) return fail(VR_ERR_INVALID, "vr_set_option: shadow_defer is 0 or 1");
-        c->shadow_defer = value;
-        return value == 0 ? release_defer(c) : VR_OK;
-    }
-    if (n == "slab") {
-        if (value < 0 || value > 1) return fail(VR_ERR_INVALID, "vr_set_option: slab is 0 or 1");
-        c->slab = value;
-        return VR_OK;
-    }
-    if (n == "slab_cap") {
-        if (value < 0 || value > kSlabMaxChunks)
-            return fail(VR_ERR_INVALID, "vr_set_option: slab_cap in [0, %d]", kSlabMaxChunks);
-        c->slab_cap = value;
-        return VR_OK;
-    }
-    if (n == "region_order") {
-        if (value < 0 || value > 2)
-            return fail(VR_ERR_INVALID, "vr_set_option: region_order is 0 (inside-out), 1 (longest tile first) or "
-                                        "2 (longest block first)");
-        c->region_order = value;
-        return VR_OK;
-    }
-    if (n == "wg_waves") {
-        if (value != 4 && value != 8 && value != 16) return fail(VR_ERR_INVALID, "vr_set_option: wg_waves is 4, 8 or 16");
-        c->wg_waves = value;
-        return VR_OK;
-    }
-    if (n == "supertile") {
-        if (value != 1 && value != 2 && value != 4) return fail(VR_ERR_INVALID, "vr_set_option: supertile is 1, 2 or 4");
-        c->supertile = value;
-        return VR_OK;
-    }
-    if (n == "region_interval") {
-        if (value < 1 || value > 1 << 20) return fail(VR_ERR_INVALID, "vr_set_option: region_interval in [1, 2^20]");
-        c->region_interval = value;
-        return VR_OK;
-    }
-    if (n == "region_gpu") {
-        if (value < 0 || value > 1) return fail(VR_ERR_INVALID, "vr_set_option: region_gpu is 0 or 1");
-        c->region_gpu = value;
-        return VR_OK;
-    }
-    if (n == "uniform_skip") {
-        if (value < 0 || value > 1) return fail(VR_ERR_INVALID, "vr_set_option: uniform_skip is 0 or 1");
-        c->uniform_skip = value;
-        return VR_OK;
-    }
-    if (n == "sort_reuse") {
-        if (value < 0 || value > 64) return fail(VR_ERR_INVALID, "vr_set_option: sort_reuse in [0, 64] renders");
-        c->sort_reuse = value;
-        return VR_OK;
-    }
-    if (n == "count") {
-        if (value < 0 || value > 2)
-            return fail(VR_ERR_INVALID, "vr_set_option: count is 0 (steps), 1 (evals) or 2 (Worley cells)");
-        c->count = value;
-        return VR_OK;
-    }
-    if (n == "lattice") {
-        if (value < 0 || value > 1) return fail(VR_ERR_INVALID, "vr_set_option: lattice is 0 or 1");
-        c->lattice = value;
-        return VR_OK;
-    }
-    return fail(VR_ERR_INVALID, "vr_set_option: unknown option '%s'", name);
-} catch (...) {
-    return caught_exception("vr_set_option");
-}
-
-int vr_get_option(void* p, const char* name)
-try {
-    if (!p || !name) return -1;
-    Ctx* c = as_ctx(p);
-    const std::string n(name);
-    if (n == "layout") return c->fast_layout ? c->fast_layout : LAYOUT_PLANAR;
-    if (n == "schedule") return c->schedule;
-    if (n == "waves_per_simd") return c->waves_per_simd;
-    if (n == "tiles_per_wave") return c->tiles_per_wave;
-    if (n == "count") return c->count;
-    if (n == "wedges") return c->wedges;
-    if (n == "split") return c->split;
-    if (n == "lattice") return c->lattice;
-    if (n == "slab") return c->slab;
-    if (n == "proc_enum") return c->proc_enum;
-    if (n == "shadow_defer") return c->shadow_defer;
-    if (n == "shadow_blocks") return c->shadow_blocks;
-    if (n == "shadow_cache") return c->shadow_cache;
-    if (n == "shadow_defer_mib") return c->shadow_defer_mib;
-    if (n == "shadow_defer_entries") return (int)c->defer_entries;
-    if (n == "shadow_defer_last") return c->defer_last;   // read-only
-    // read-only: 0 = a grid medium; 1 = procedural, frames that reuse one
-    // camera's order only read the ctx's scratch (they overlap on two
-    // streams); 2 = procedural with shadow rays (deferred: every frame writes)
-    if (n == "procedural") return !c->proc.enabled ? 0 : c->proc.shadow_steps > 0 && c->shadow_defer ? 2 : 1;
-    if (n == "shadow_defer_kib")                          // read-only: the scratch held now, KiB
-        return (int)std::min<size_t>((c->defer_bytes + 1023) / 1024, 0x7fffffff);
-    if (n == "slab_cap") return c->slab_cap;
-    if (n == "region_order") return c->region_order;
-    if (n == "sort_reuse") return c->sort_reuse;
-    if (n == "wg_waves") return c->wg_waves;
-    if (n == "uniform_skip") return c->uniform_skip;
-    if (n == "region_work_tiles")   // read-only: tiles with estimated work in the current region lists
-        return c->region_cur >= 0 ? c->region[c->region_cur].nwork : -1;
-    if (n == "region_empty_tiles") {   // read-only: tiles of the current lists that are filled, not marched
-        poll_region_header(c);   // (a completed GPU build's counts)
-        return c->region_cur >= 0 ? c->region[c->region_cur].nempty : -1;
-    }
-    if (n == "uniform_mask") {   // read-only
-        if (!c->d_planar || resolve_uniform(c) != VR_OK) return -1;
-        return c->uniform_mask;
-    }
-    if (n == "supertile") return c->supertile;
-    if (n == "launch_cache") return c->launch_cache;
-    if (n == "empty_fill") return c->empty_fill;
-    if (n == "frames_overlap") return c->frames_overlap;
-    if (n == "row_setup") return c->row_setup;
-    if (n == "row_pow") return c->row_pow;
-    if (n == "row_first_pct") return c->row_first_pct;
-    if (n == "launch_cache_hits") return (int)std::min<long long>(c->lc_hits, 0x7fffffff);
-    if (n == "experiments") return VR_EXPERIMENTS;   // read-only: the measured-slower variants are built
-    if (n == "region_interval") return c->region_interval;
-    if (n == "region_gpu") return c->region_gpu;
-    if (n == "region_gpu_builds") return (int)std::min<long long>(c->gpu_builds, 0x7fffffff);   // read-only
-    return -1;
-} catch (...) {
-    (void)caught_exception("vr_get_option");
-    return -1;
-}
-
-const char* vr_kernel_variant(void* p)
-try {
-    if (!p) return "none";
-    Ctx* c = as_ctx(p);
-    if (c->proc.enabled) {
-        if (c->schedule == SCHED_STATIC) return c->proc.shadow_steps > 0 ? "procedural_shadow_tiles" : "procedural_tiles";
-        if (c->schedule == SCHED_RINGS) return c->proc.shadow_steps > 0 ? "procedural_shadow_rings" : "procedural_rings";
-        return c->proc.shadow_steps > 0 ? "procedural_shadow" : "procedural";
-    }
-    if (!c->d_planar || !c->has_camera) return "none";
-    if (resolve_uniform(c) != VR_OK) return "none";
-    MarchArgs a{};
-    Plan pl{};
-    make_plan(c, &a, &pl);
-    const int kind = c->schedule >= 0 ? c->schedule : SCHED_REGIONS;
-    if (pl.layout == LAYOUT_COL48 && c->slab && kind == SCHED_REGIONS && c->split <= 1)
-        return pl.early ? "grid_col48_slab_clamp_early" : "grid_col48_slab_clamp";
-    const int um = c->uniform_skip ? c->uniform_mask : 0;
-    int ch = -1;   // one uniform channel, no loads for it (launch_lw / launch_lat_kd): "_u" + the channel
-    if (kind == SCHED_REGIONS && !pl.early && a.zero_offsets && c->wg_waves == 4 &&
-        (um == 1 || um == 2 || um == 4 || um == 8) &&
-        (pl.layout == LAYOUT_COL48 || pl.layout == LAYOUT_BRICK4832 || pl.layout == LAYOUT_CORNERH ||
-         pl.layout == LAYOUT_COL48Z))
-        ch = um == 1 ? 0 : um == 2 ? 1 : um == 4 ? 2 : 3;
-    if (ch < 0) return variant_name(pl);
-    // built once, thread-safe (a function-local static): every layout x early x channel
-    struct Names {
-        std::string n[kNumLayouts][2][5];
-    };
-    static const Names table = [] {
-        Names t;
-        for (int l = 1; l < kNumLayouts; ++l)
-            for (int e = 0; e < 2; ++e)
-                for (int u = 0; u < 5; ++u) {
-                    std::string v = variant_name(Plan{l, WRAP_CLAMP, e == 1});
-                    if (u > 0) v += std::string("_u") + "RGBA"[u - 1];
-                    t.n[l][e][u] = v;
-                }
-        return t;
-    }();
-    return table.n[pl.layout][pl.early ? 1 : 0][ch + 1].c_str();
-} catch (...) {
-    (void)caught_exception("vr_kernel_variant");
-    return "error";
-}
-
-// Target pixel (x, packed output row) under the projected box centre: the
-// centre of the ring schedule.  Model, View, Projection are column-major
-// (vr_object_shader_data); the product is applied to the box-centre point.
-void box_centre_pixel(const Ctx* c, const MarchArgs& a, int* px, int* prow)
-{
-    const float* M = c->obj;
-    const float* V = c->obj + 16;
-    const float* P = c->obj + 32;
-    double v[4] = {0.5 * ((double)a.box_min[0] + a.box_max[0]), 0.5 * ((double)a.box_min[1] + a.box_max[1]),
-                   0.5 * ((double)a.box_min[2] + a.box_max[2]), 1.0};
-    for (const float* m : {M, V, P}) {
-        double o[4];
-        for (int r = 0; r < 4; ++r) o[r] = m[r] * v[0] + m[4 + r] * v[1] + m[8 + r] * v[2] + m[12 + r] * v[3];
-        for (int r = 0; r < 4; ++r) v[r] = o[r];
-    }
-    double sx = 0.5 * a.width, sy = 0.5 * a.height;
-    if (v[3] > 0.0) {
-        sx = (v[0] / v[3] * 0.5 + 0.5) * a.width;
-        sy = (v[1] / v[3] * 0.5 + 0.5) * a.height;
-    }
-    const int y = (int)std::min(std::max(sy, 0.0), (double)(a.height - 1));
-    int row = y;
-    if (a.band_rows > 0 && (a.band_stride > 1 || a.band_first > 0)) {   // the nearest of this rank's packed rows
-        const int b = y / a.band_rows;
-        const int sel = b >= a.band_first ? (b - a.band_first) / a.band_stride : 0;
-        row = sel * a.band_rows + y % a.band_rows;
-    }
-    *px = (int)std::min(std::max(sx, 0.0), (double)(a.width - 1));
-    *prow = std::min(std::max(row, 0), std::max(a.out_rows - 1, 0));
-}
-
-// Regions schedule (SCHED_REGIONS): deal the 8x8 tiles of
-// the target to the 8 XCDs as contiguous angular wedges around the projected
-// box centre, `wedges` per XCD, with equal estimated work, so that the tiles
-// one L2 serves are mostly neighbours (their rays read the same bricks).  The
-// work estimate of a tile is the longest a3 step count of the rays through its
-// 4 corners (double, no clip test; one ray per tile corner of the frame).
-// Each XCD walks its tiles inside-out (Chebyshev ring, then angle), so its
-// longest rays start first; tiles without estimated work (background, or a
-// silhouette edge missing every corner) follow, dealt round-robin.  Every tile
-// is in exactly one list whatever the estimate, so a list built for an older
-// camera stays correct: a moving camera reuses it for kRegionRebuildInterval
-// renders.  Rebuilds go to the other of two buffers, once the renders that
-// last read it are done (an event recorded when it was retired, on its one
-// render stream; a device sync if several streams used it), uploaded on the
-// render stream.
-//
-// `s` waits for `ev` unless it has already completed (an event recorded on a
-// stream the caller has destroyed since is complete: no wait is queued for it)
-static vr_status stream_wait_pending(hipStream_t s, hipEvent_t ev)
-{
-    const hipError_t q = hipEventQuery(ev);
-    if (q == hipSuccess) return VR_OK;
-    if (q != hipErrorNotReady) return fail(VR_ERR_HIP, "vr_render: event query: %s", hipGetErrorString(q));
-    (void)hipGetLastError();   // not an error: still queued
-    HIP_TRY(hipStreamWaitEvent(s, ev, 0));
-    return VR_OK;
-}
-
-// The render stream s uses the lists: *slot = its index in rb.streams (-1:
-// untracked, more streams than kMaxRegionStreams)
-vr_status note_region_stream(Ctx::RegionBuf& rb, hipStream_t s, int* slot)
-{
-    *slot = -1;
-    if (rb.nstreams < 0) return VR_OK;
-    for (int i = 0; i < rb.nstreams; ++i)
-        if (rb.streams[i] == s) {
-            *slot = i;
-            return VR_OK;
-        }
-    if (s != rb.upload_stream) {   // first use on another stream
-        const vr_status st = stream_wait_pending(s, rb.uploaded);
-        if (st != VR_OK) return st;
-    }
-    if (rb.nstreams == kMaxRegionStreams) {
-        rb.nstreams = -1;
-        return VR_OK;
-    }
-    if (!rb.used[rb.nstreams]) HIP_TRY(hipEventCreateWithFlags(&rb.used[rb.nstreams], hipEventDisableTiming));
-    rb.first_rec[rb.nstreams] = false;
-    *slot = rb.nstreams;
-    rb.streams[rb.nstreams++] = s;
-    return VR_OK;
-}
-
-// After a regions launch on stream s (slot c->region_slot of the current
-// lists): the stream's first render with these lists records its event
-vr_status note_region_render(Ctx* c, hipStream_t s)
-{
-    if (c->region_cur < 0 || c->region_slot < 0) return VR_OK;
-    Ctx::RegionBuf& rb = c->region[c->region_cur];
-    if (c->region_slot >= rb.nstreams || rb.first_rec[c->region_slot]) return VR_OK;
-    HIP_TRY(hipEventRecord(rb.used[c->region_slot], s));
-    rb.first_rec[c->region_slot] = true;
-    return VR_OK;
-}
-
-// lanes per ray of a regions frame: option split, or auto from the tiles with work
-static int auto_split(const Ctx* c, long long nwork)
-{
-    if (c->split > 0) return c->split;
-    return nwork >= (c->frames_overlap ? kSplitOneLaneOverlap : kSplitOneLane) ? 1 : nwork >= kSplitTwoLanes ? 2 : 4;
-}
-
-// The lists of the GPU build that last completed (host-mapped header, read
-// once its event is done -- never waited for): tiles with work and the longest
-// list, which size the next launches of the same target.
-static void poll_region_header(Ctx* c)
-{
-    if (!c->rg_pending) return;
-    const hipError_t q = hipEventQuery(c->rg_ev);
-    if (q == hipErrorNotReady) {
-        (void)hipGetLastError();   // not an error: the build is still queued
-        return;
-    }
-    c->rg_pending = false;
-    ++c->gen;   // the next launches are sized from the completed build
-    if (q != hipSuccess) return;
-    Ctx::RegionBuf& rb = c->region[c->rg_buf];
-    rb.nwork = c->h_rghdr[9];
-    rb.most = c->h_rghdr[10];
-    rb.most_marched = 0;
-    rb.nempty = 0;
-    for (int x = 0; x < 8; ++x) {
-        rb.most_marched = std::max(rb.most_marched, c->h_rghdr[kRegionWork + x]);
-        rb.nempty += c->h_rghdr[x + 1] - c->h_rghdr[x] - c->h_rghdr[kRegionWork + x];
-    }
-}
-
-// Pick the buffer for new lists, sized for n entries: the one the current
-// lists replaced (two builds old), once the renders that used it are done --
-// the new lists are written on `stream` (GPU build, or the upload of a host
-// build), so `stream` waits for the other streams' renders (RegionBuf);
-// host_staging: the host also rewrites that buffer's pinned staging copy,
-// once its last upload has run.
-static vr_status next_region_buf(Ctx* c, size_t n, bool host_staging, hipStream_t stream, int* out)
-{
-    c->region_slot = -1;
-    const int b = c->region_cur < 0 ? 0 : c->region_cur ^ 1;
-    Ctx::RegionBuf& rb = c->region[b];
-    if (c->rg_pending && c->rg_buf == b) {   // a GPU build into this buffer is still queued
-        HIP_TRY(hipEventSynchronize(c->rg_ev));
-        poll_region_header(c);
-    }
-    if (host_staging && rb.uploaded && rb.h) HIP_TRY(hipEventSynchronize(rb.uploaded));   // the staging copy is free
-    const Ctx::RegionBuf* newer = c->region_cur >= 0 ? &c->region[c->region_cur] : nullptr;
-    bool sync = rb.nstreams < 0;
-    for (int i = 0; i < rb.nstreams && !sync; ++i) {
-        if (rb.streams[i] == stream) continue;   // this stream's order covers its renders
-        int j = -1;
-        for (int k = 0; newer && k < newer->nstreams; ++k)
-            if (newer->streams[k] == rb.streams[i] && newer->first_rec[k]) j = k;
-        if (j < 0) {
-            sync = true;   // a stream that never rendered with the newer lists
-        } else {
-            const vr_status st = stream_wait_pending(stream, newer->used[j]);
-            if (st != VR_OK) return st;
-        }
-    }
-    if (sync) HIP_TRY(hipDeviceSynchronize());
-    rb.nstreams = 0;
-    if (n > rb.cap) {
-        if (rb.d) {
-            HIP_TRY(hipStreamSynchronize(stream));   // the stream may have queued work on the old list
-            (void)hipFree(rb.d);
-        }
-        if (rb.h) (void)hipHostFree(rb.h);
-        rb.d = rb.h = nullptr;
-        rb.cap = 0;
-        HIP_TRY(hipMalloc(&rb.d, (n + kRegionHeader) * sizeof(unsigned)));
-        HIP_TRY(hipHostMalloc(&rb.h, (n + kRegionHeader) * sizeof(unsigned), hipHostMallocDefault));
-        rb.cap = n;
-    }
-    *out = b;
-    return VR_OK;
-}
-
-vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow, hipStream_t stream)
-{
-    const int tw = (a.width + 7) >> 3, th = (a.out_rows + 7) >> 3;
-    float key[kRegionKeyLen] = {(float)tw, (float)th, (float)a.width, (float)a.height, (float)a.out_rows,
-                                (float)a.band_rows, (float)a.band_stride, (float)a.band_first, (float)tpw,
-                                (float)c->wedges, (float)(65536 * c->region_order), (float)c->split, (float)c->supertile};
-    constexpr int grid_part = 13;   // the part a reused list must match
-    int kn = grid_part;
-    for (float v : {(float)a.max_steps, a.step_size, (float)cpx, (float)cprow}) key[kn++] = v;
-    for (const float* v : {a.org, a.o, a.px, a.py, a.box_min, a.box_max})
-        for (int k = 0; k < 3; ++k) key[kn++] = v[k];
-    for (int k = 0; k < 4; ++k) key[kn++] = a.r3[k];   // the clip w row (tile_is_empty)
-    ++c->renders_since_build;
-    poll_region_header(c);
-    const bool same_grid = c->region_cur >= 0 && std::memcmp(key, c->region_key, grid_part * sizeof(float)) == 0;
-    const bool exact = same_grid && std::memcmp(key, c->region_key, sizeof key) == 0;
-    if (exact || (same_grid && c->renders_since_build < c->region_interval)) {
-        // lists of an older camera order the work of this one correctly, but
-        // their empty tiles are that camera's: they are then marched too
-        c->region_exact = exact;
-        return note_region_stream(c->region[c->region_cur], stream, &c->region_slot);
-    }
-    c->region_exact = true;   // (either build below is for this key)
-
-    const int S = c->supertile;
-    // a moved camera over the same target: the lists come from
-    // the GPU build on the render stream (vr_regions.hip) -- no host loop, no
-    // host wait; tiles with work and the longest list are the last completed
-    // build's (they size the launch, not the result)
-    if (same_grid && c->region_gpu && th < 65536 && tw < 65536) {
-        const size_t n = (size_t)tw * th;
-        const Ctx::RegionBuf& cur = c->region[c->region_cur];
-        const int nwork = cur.nwork, most = cur.most;
-        const size_t need = region_build_bytes((int)n);
-        if (need > c->rg_bytes) {
-            if (c->d_rg) {
-                // the last build may have been queued on another stream
-                if (c->rg_pending) HIP_TRY(hipEventSynchronize(c->rg_ev));
-                HIP_TRY(hipStreamSynchronize(stream));
-                (void)hipFree(c->d_rg);
-            }
-            c->d_rg = nullptr;
-            c->rg_bytes = 0;
-            HIP_TRY(hipMalloc(&c->d_rg, need));   // every build zeroes its own counters (launch_region_build)
-            c->rg_bytes = need;
-        }
-        if (!c->h_rghdr) {
-            HIP_TRY(hipHostMalloc(&c->h_rghdr, kRegionHeader * sizeof(int), hipHostMallocMapped));
-            HIP_TRY(hipEventCreateWithFlags(&c->rg_ev, hipEventDisableTiming));
-        }
-        int b = 0;
-        const vr_status st0 = next_region_buf(c, n, false, stream, &b);
-        if (st0 != VR_OK) return st0;
-        Ctx::RegionBuf& rb = c->region[b];
-        RegionBuild g{};
-        g.tw = tw; g.th = th; g.width = a.width; g.out_rows = a.out_rows;
-        g.band_rows = a.band_rows; g.band_stride = a.band_stride; g.band_first = a.band_first;
-        g.max_steps = a.max_steps; g.step_size = a.step_size;
-        for (int k = 0; k < 3; ++k) {
-            g.org[k] = a.org[k]; g.o[k] = a.o[k]; g.px[k] = a.px[k]; g.py[k] = a.py[k];
-            g.box_min[k] = a.box_min[k]; g.box_max[k] = a.box_max[k];
-        }
-        for (int k = 0; k < 4; ++k) g.r3[k] = a.r3[k];
-        g.height = a.height;
-        g.ccx = (cpx + 0.5) / 8.0; g.ccy = (cprow + 0.5) / 8.0;
-        g.ctx = (cpx >> 3) / S; g.cty = (cprow >> 3) / S;
-        g.supertile = S; g.wedges = c->wedges; g.order = c->region_order;
-        int* dev_hdr = nullptr;
-        HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&dev_hdr), c->h_rghdr, 0));
-        // one build scratch per context: a build on another stream waits for the last one
-        if (c->gpu_builds > 0) {
-            const vr_status sw = stream_wait_pending(stream, c->rg_ev);
-            if (sw != VR_OK) return sw;
-        }
-        HIP_TRY(launch_region_build(g, c->d_rg, rb.d + kRegionHeader, reinterpret_cast<int*>(rb.d), dev_hdr, stream));
-        HIP_TRY(hipEventRecord(c->rg_ev, stream));
-        c->rg_pending = true;
-        c->rg_buf = b;
-        ++c->gpu_builds;
-        if (!rb.uploaded) HIP_TRY(hipEventCreateWithFlags(&rb.uploaded, hipEventDisableTiming));
-        HIP_TRY(hipEventRecord(rb.uploaded, stream));
-        rb.upload_stream = stream;
-        rb.nwork = nwork;
-        rb.most = most;
-        rb.most_marched = 0;   // known once the build completes (poll_region_header)
-        rb.nempty = -1;
-        rb.map = TileMap{};
-        rb.map.nwx = std::max(1, (most + tpw - 1) / tpw);
-        rb.nstreams = 0;
-        const vr_status st = note_region_stream(rb, stream, &c->region_slot);
-        if (st != VR_OK) return st;
-        c->region_cur = b;
-        std::memcpy(c->region_key, key, sizeof key);
-        c->renders_since_build = 0;
-        ++c->gen;   // new lists: cached launches point at the old ones
-        return VR_OK;
-    }
-
-    // a host build (a new target or band set) is already the slow path: load the
-    // GPU build's code object here, not at the first GPU rebuild mid-sequence
-    if (c->region_gpu && !c->rg_preloaded) {
-        HIP_TRY(region_build_preload());
-        c->rg_preloaded = true;
-    }
-    // a3 step estimate of the ray through pixel-corner (fx, fy) of the packed target
-    auto steps_at = [&](double fx, int orow) {
-        const int bl = orow / a.band_rows;
-        const double fy = (double)((a.band_first + bl * a.band_stride) * a.band_rows + (orow - bl * a.band_rows));
-        double d[3], len = 0.0;
-        for (int k = 0; k < 3; ++k) {
-            d[k] = a.o[k] + fx * a.px[k] + fy * a.py[k];
-            len += d[k] * d[k];
-        }
-        len = std::sqrt(len);
-        double tn = -INFINITY, tf = INFINITY;
-        for (int k = 0; k < 3; ++k) {
-            const double ta = (a.box_min[k] - a.org[k]) * len / d[k], tb = (a.box_max[k] - a.org[k]) * len / d[k];
-            tn = std::max(tn, std::min(ta, tb));
-            tf = std::min(tf, std::max(ta, tb));
-        }
-        return (tn <= tf && std::isfinite(tf)) ? std::min((double)a.max_steps, (tf - tn) / a.step_size) : 0.0;
-    };
-    std::vector<double> corner((size_t)(tw + 1) * (th + 1));
-    for (int j = 0; j <= th; ++j) {
-        const int orow = std::min(j * 8, a.out_rows);   // the row a packed-row edge starts
-        for (int i = 0; i <= tw; ++i) corner[(size_t)j * (tw + 1) + i] = steps_at(std::min(i * 8, a.width), orow);
-    }
-    // supertile S: tiles are ordered by S x S blocks (angle and ring of the
-    // block, then row-major inside it), so consecutive entries -- the waves of
-    // one workgroup, on one CU -- are a compact block sharing the CU's L1
-    struct T { unsigned id; double cost, ang; int ring, sub; };
-    std::vector<T> work, idle;
-    const double ccx = (cpx + 0.5) / 8.0, ccy = (cprow + 0.5) / 8.0;
-    const int ctx = (cpx >> 3) / S, cty = (cprow >> 3) / S;
-    for (int ty = 0; ty < th; ++ty)
-        for (int tx = 0; tx < tw; ++tx) {
-            const double* c0 = &corner[(size_t)ty * (tw + 1) + tx];
-            const double cost = std::max(std::max(c0[0], c0[1]), std::max(c0[tw + 1], c0[tw + 2]));
-            const int sx = tx / S, sy = ty / S;
-            const T t{((unsigned)ty << 16) | (unsigned)tx, cost,
-                      std::atan2(sy * S + 0.5 * S - ccy, sx * S + 0.5 * S - ccx),
-                      std::max(std::abs(sx - ctx), std::abs(sy - cty)), (ty % S) * S + tx % S};
-            (cost >= 1.0 ? work : idle).push_back(t);
-        }
-    std::sort(work.begin(), work.end(), [](const T& u, const T& v) { return u.ang != v.ang ? u.ang < v.ang : u.sub < v.sub; });
-    double total = 0.0;
-    for (const T& t : work) total += t.cost;
-    std::vector<std::vector<T>> xl(8);
-    const int K = 8 * c->wedges;
-    double run = 0.0;
-    for (const T& t : work) {   // wedge k = the k-th K-quantile of the work, dealt to XCD k % 8
-        xl[std::min(K - 1, (int)((run + 0.5 * t.cost) / total * K)) % 8].push_back(t);
-        run += t.cost;
-    }
-    auto inside_out = [](const T& u, const T& v) {
-        return u.ring != v.ring ? u.ring < v.ring : u.ang != v.ang ? u.ang < v.ang : u.sub < v.sub;
-    };
-    if (c->region_order == 1) {   // longest estimated work first (LPT), inside-out among equals
-        for (auto& l : xl)
-            std::stable_sort(l.begin(), l.end(), [&](const T& u, const T& v) {
-                return u.cost != v.cost ? u.cost > v.cost : inside_out(u, v);
-            });
-    } else if (c->region_order == 2) {   // S x S blocks by their longest tile, a block's tiles together
-        const int bw = (tw + S - 1) / S;
-        std::vector<double> bmax((size_t)bw * ((th + S - 1) / S), 0.0);
-        auto bidx = [&](const T& t) { return (size_t)((t.id >> 16) / S) * bw + (size_t)((t.id & 0xffffu) / S); };
-        for (const auto& l : xl)
-            for (const T& t : l) bmax[bidx(t)] = std::max(bmax[bidx(t)], t.cost);
-        for (auto& l : xl)
-            std::stable_sort(l.begin(), l.end(), [&](const T& u, const T& v) {
-                const double cu = bmax[bidx(u)], cv = bmax[bidx(v)];
-                if (cu != cv) return cu > cv;
-                if (bidx(u) != bidx(v)) return bidx(u) < bidx(v);
-                return u.sub < v.sub;
-            });
-    } else {
-        for (auto& l : xl) std::sort(l.begin(), l.end(), inside_out);
-    }
-    std::sort(idle.begin(), idle.end(), inside_out);
-    // idle tiles some ray of which may meet the box, dealt round-robin after
-    // the work, then the empty ones (tile_is_empty: filled, not marched),
-    // likewise -- the GPU build's order
-    std::vector<T> empty_tiles;
-    {
-        std::vector<T> edge;
-        for (const T& t : idle)
-            (tile_is_empty(a.org, a.o, a.px, a.py, a.box_min, a.box_max, a.r3, a.width, a.out_rows, a.height,
-                           a.band_rows, a.band_stride, a.band_first, (int)(t.id & 0xffffu), (int)(t.id >> 16))
-                 ? empty_tiles : edge).push_back(t);
-        for (size_t i = 0; i < edge.size(); ++i) xl[i % 8].push_back(edge[i]);
-    }
-    std::vector<int> marched(8);
-    for (int x = 0; x < 8; ++x) marched[x] = (int)xl[x].size();
-    for (size_t i = 0; i < empty_tiles.size(); ++i) xl[i % 8].push_back(empty_tiles[i]);
-
-    size_t nent = 0;
-    for (int x = 0; x < 8; ++x) nent += xl[x].size();
-    const size_t n = nent;   // words after the header
-    int b = 0;
-    const vr_status st0 = next_region_buf(c, n, true, stream, &b);
-    if (st0 != VR_OK) return st0;
-    Ctx::RegionBuf& rb = c->region[b];
-    int* hdr = reinterpret_cast<int*>(rb.h);
-    std::memset(hdr, 0, kRegionHeader * sizeof(int));
-    unsigned* list = rb.h + kRegionHeader;
-    int most_marched = 0;
-    TileMap m{};
-    size_t pos = 0, most = 0;
-    for (int x = 0; x < 8; ++x) {
-        m.off[x] = (int)pos;
-        for (const T& t : xl[x]) list[pos++] = t.id;
-        most = std::max(most, pos - (size_t)m.off[x]);
-    }
-    m.off[8] = (int)pos;
-    m.nwx = std::max(1, (int)((most + tpw - 1) / tpw));
-    for (int x = 0; x < 9; ++x) hdr[x] = m.off[x];
-    hdr[9] = (int)work.size();
-    hdr[10] = (int)most;
-    hdr[11] = (int)pos;
-    for (int x = 0; x < 8; ++x) {   // the marched entries lead each XCD's list
-        const int nm = marched[x];
-        hdr[kRegionWork + x] = nm;
-        most_marched = std::max(most_marched, nm);
-    }
-    HIP_TRY(hipMemcpyAsync(rb.d, rb.h, (n + kRegionHeader) * sizeof(unsigned), hipMemcpyHostToDevice, stream));
-    if (!rb.uploaded) HIP_TRY(hipEventCreateWithFlags(&rb.uploaded, hipEventDisableTiming));
-    HIP_TRY(hipEventRecord(rb.uploaded, stream));
-    rb.upload_stream = stream;
-    rb.map = m;
-    rb.most = (int)most;
-    rb.most_marched = most_marched;
-    rb.nempty = (int)empty_tiles.size();
-    rb.nwork = (int)work.size();
-    rb.nstreams = 0;
-    const vr_status st = note_region_stream(rb, stream, &c->region_slot);
-    if (st != VR_OK) return st;
-    c->region_cur = b;
-    std::memcpy(c->region_key, key, sizeof key);
-    c->renders_since_build = 0;
-    ++c->gen;   // new lists: cached launches point at the old ones
-    return VR_OK;
-}
-
-// Perlin lattice table (global memory) of the procedural march: the fBm's
-// octave o samples lattice coordinates P * grid_scale * f_o with P in the
-// box, [0, 1]^3 up to rounding; the table covers the cells of every octave,
-// with 2 cells of margin, when that is at most 2^24 cells (byte offsets
-// then stay exact in fp32; 128 MiB).  Built on `s` and waited for when the
-// seed or the range changes (a parameter change, not per frame).
-static vr_status ensure_lattice(Ctx* c, ProcParams* q, hipStream_t s)
-{
-    double lo_c = 0.0, hi_c = 0.0;
-    float f = q->freq0;
-    for (int o = 0; o < q->octaves; ++o) {
-        const double G = (double)q->grid_scale * (double)f;
-        lo_c = std::min(lo_c, G);
-        hi_c = std::max(hi_c, G);
-        f = f * q->lacunarity;
-    }
-    if (!(hi_c - lo_c < 1.0e4) || q->octaves <= 0) return VR_OK;
-    const long long lo = (long long)std::floor(lo_c) - 2, n = (long long)std::ceil(hi_c) + 2 - lo + 1;
-    if (n * n * n > (1ll << 24)) return VR_OK;
-    const size_t bytes = (size_t)(n * n * n) * sizeof(uint2);
-    if (!(c->lat_key[0] == q->seed_fbm && c->lat_key[1] == lo && c->lat_key[2] == n)) {
-        // renders queued on other streams may still read the old table
-        HIP_TRY(hipDeviceSynchronize());
-        c->lat_key[2] = -1;
-        if (bytes > c->lat_cap) {
-            if (c->d_lat) (void)hipFree(c->d_lat);
-            c->d_lat = nullptr;
-            c->lat_cap = 0;
-            if (hipMalloc(&c->d_lat, bytes) != hipSuccess) return fail(VR_ERR_OOM, "vr_render: lattice table");
-            c->lat_cap = bytes;
-        }
-        HIP_TRY(launch_perlin_lattice(c->d_lat, q->seed_fbm, (int)lo, (int)n, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        c->lat_key[0] = q->seed_fbm;
-        c->lat_key[1] = lo;
-        c->lat_key[2] = n;
-    }
-    q->lat = c->d_lat;
-    q->lat_bytes = (unsigned)bytes;
-    q->lat_c = (float)(8 * lo * (1 + n + n * n));
-    q->lat_sy = (float)(8 * n);
-    q->lat_sz = (float)(8 * n * n);
-    return VR_OK;
-}
-
-// Scratch of the deferred shadow passes (ShadowDefer), sized from the frame:
-// [chunk count | per-wave step counts, entry counts, first chunks | chunk map |
-// step records | entries].  Sorted wave w owns the entries [went[w],
-// went[w+1]) and step records [wrec[w], wrec[w+1]) that proc_scan lays out
-// from the cost histogram (the sum of its lanes' step-count bounds), so a
-// frame needs about its executed lane-steps of entries: 16.7 M (0.27 GB) at
-// 1080p x 128 where the old per-wave worst case (64 x max_steps) took 4.2 GB.
-// The capacity follows the largest need seen (written by every sorting frame
-// into host-mapped memory, read once its event has completed: no host wait),
-// x 5/4; before one is known it starts at pixels x max_steps / 16 entries.
-// A wave beyond the capacity marches its shadow rays in place, so a frame
-// larger than the scratch is still exact, and the next one gets more.
-// Growing keeps the outgrown buffer until the frames queued before the growth
-// have run (an event, Ctx::Retired; queued frames on other streams may still
-// use it): vr_render never waits for the device.
-// *ok = false (and VR_OK): no usable scratch (shadow_defer_mib too small, or
-// the allocation failed) -- the render then takes the in-wave compaction.
-static vr_status release_defer(Ctx* c)
-{
-    if (!c->d_defer && c->defer_retired.empty()) return VR_OK;
-    HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipDeviceSynchronize());   // an option change, not a frame: queued renders may use the scratch
-    if (c->d_defer) (void)hipFree(c->d_defer);
-    for (const auto& q : c->defer_retired) {
-        (void)hipFree(q.p);
-        if (q.ev) (void)hipEventDestroy(q.ev);
-    }
-    c->defer_retired.clear();
-    c->d_defer = nullptr;
-    c->defer_bytes = 0;
-    c->defer_ent_cap = 0;
-    c->defer_rec_cap = 0;
-    c->defer_waves = 0;
-    c->want_ent = c->want_rec = 0.0;
-    return VR_OK;
-}
-
-static vr_status ensure_defer(Ctx* c, const MarchArgs& a, void* sort_buf, ShadowDefer* d, bool* ok)
-{
-    *ok = false;
-    // free the outgrown buffers whose frames have run
-    for (size_t i = 0; i < c->defer_retired.size();) {
-        Ctx::Retired& q = c->defer_retired[i];
-        const hipError_t st = q.ev ? hipEventQuery(q.ev) : hipErrorNotReady;
-        if (st == hipSuccess) {
-            (void)hipFree(q.p);
-            (void)hipEventDestroy(q.ev);
-            c->defer_retired.erase(c->defer_retired.begin() + (long)i);
-        } else {
-            if (q.ev) (void)hipGetLastError();   // not an error: still queued
-            ++i;
-        }
-    }
-    if (c->shadow_defer_mib == 0) return VR_OK;
-    const SortLayout L = sort_layout(a.width, a.out_rows);
-    const unsigned long long pixels = (unsigned long long)a.width * (unsigned long long)a.out_rows;
-    if (!c->h_need) {
-        HIP_TRY(hipHostMalloc(&c->h_need, 2 * sizeof(unsigned long long), hipHostMallocMapped));
-        HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->d_need), c->h_need, 0));
-        HIP_TRY(hipEventCreateWithFlags(&c->need_ev, hipEventDisableTiming));
-    }
-    if (c->need_pending) {   // the last sorting frame's need, if it has run
-        const hipError_t q = hipEventQuery(c->need_ev);
-        if (q == hipSuccess) {
-            c->need_pending = false;
-            c->want_ent = std::max(c->want_ent, 1.25 * (double)c->h_need[0] / c->need_pixsteps);
-            c->want_rec = std::max(c->want_rec, 1.25 * (double)c->h_need[1] / c->need_wavesteps);
-        } else if (q == hipErrorNotReady) {
-            (void)hipGetLastError();   // not an error: the frame is still queued
-        } else {
-            return fail(VR_ERR_HIP, "vr_render: need event: %s", hipGetErrorString(q));
-        }
-    }
-    const unsigned long long steps = (unsigned long long)std::max(a.max_steps, 1);
-    constexpr unsigned long long kMaxCap = 0xffff0000ull;   // entry / record indices stay 32-bit
-    const double pixsteps = (double)pixels * (double)steps, wavesteps = (double)L.waves * (double)steps;
-    unsigned long long ent = (unsigned long long)std::min(4.0e9, pixsteps * std::max(c->want_ent, 1.0 / 12.0));
-    unsigned long long rec = (unsigned long long)std::min(4.0e9, wavesteps * std::max(c->want_rec, 0.125));
-    ent = std::max(ent, 4096ull);
-    rec = std::max(rec, 1024ull);
-    if (c->defer_entries) ent = c->defer_entries;   // test override
-    auto up = [](size_t v) { return (v + 255) & ~(size_t)255; };
-    struct Off { size_t ws, wc, wk, map, rec, ent, bytes; };
-    auto layout = [&](unsigned long long e, unsigned long long r, unsigned w) {
-        Off o{};
-        o.ws = 256;
-        o.wc = up(o.ws + (size_t)w * 4);
-        o.wk = up(o.wc + (size_t)w * 4);
-        o.map = up(o.wk + (size_t)w * 4);
-        o.rec = up(o.map + (size_t)(e / 64 + w) * sizeof(uint4));
-        o.ent = up(o.rec + (size_t)r * sizeof(uint4));
-        o.bytes = o.ent + (size_t)e * sizeof(float4);
-        return o;
-    };
-    const unsigned waves = std::max(L.waves, c->defer_waves);
-    const bool fits = c->d_defer && L.waves <= c->defer_waves && rec <= c->defer_rec_cap &&
-                      (c->defer_entries ? ent == c->defer_ent_cap : ent <= c->defer_ent_cap);
-    if (!fits) {
-        if (c->d_defer && !c->defer_entries) {   // grow by at least 1/4: a slowly growing need reallocates rarely
-            ent = std::max(ent, c->defer_ent_cap + c->defer_ent_cap / 4);
-            rec = std::max(rec, (unsigned long long)c->defer_rec_cap + c->defer_rec_cap / 4);
-        }
-        ent = std::min(ent, kMaxCap);
-        rec = std::min(rec, kMaxCap);
-        const size_t limit = (size_t)c->shadow_defer_mib << 20;
-        if (layout(ent, rec, waves).bytes > limit) {   // fewer entries: the last waves march in place
-            const size_t base = layout(0, rec, waves).bytes + 256;
-            ent = base < limit ? (limit - base) / (sizeof(float4) + sizeof(uint4) / 64 + 1) : 0;
-        }
-        void* nb = nullptr;
-        const Off o = layout(ent, rec, waves);
-        if (ent < 4096 || o.bytes > limit || hipMalloc(&nb, o.bytes) != hipSuccess) {
-            (void)hipGetLastError();   // clear an allocation error; keep what there is
-            if (!c->d_defer || L.waves > c->defer_waves) return VR_OK;
-        } else {
-            if (c->d_defer) {
-                c->defer_retired.push_back({c->d_defer, nullptr});   // its event: vr_render, before the launch
-                if (c->defer_retired.size() > kMaxDeferRetired) {   // rare: a device sync frees them
-                    HIP_TRY(hipDeviceSynchronize());
-                    for (const auto& q : c->defer_retired) {
-                        (void)hipFree(q.p);
-                        if (q.ev) (void)hipEventDestroy(q.ev);
-                    }
-                    c->defer_retired.clear();   // the device is idle: the old scratch too
-                }
-            }
-            c->d_defer = nb;
-            c->defer_bytes = o.bytes;
-            c->defer_ent_cap = ent;
-            c->defer_rec_cap = (unsigned)rec;
-            c->defer_waves = waves;
-        }
-    }
-    const Off o = layout(c->defer_ent_cap, c->defer_rec_cap, c->defer_waves);
-    *ok = true;
-    char* b = static_cast<char*>(c->d_defer);
-    char* sb = static_cast<char*>(sort_buf);
-    d->count = reinterpret_cast<unsigned*>(b);
-    d->wsteps = reinterpret_cast<unsigned*>(b + o.ws);
-    d->wcount = reinterpret_cast<unsigned*>(b + o.wc);
-    d->wchunk = reinterpret_cast<unsigned*>(b + o.wk);
-    d->map = reinterpret_cast<uint4*>(b + o.map);
-    d->rec = reinterpret_cast<uint4*>(b + o.rec);
-    d->ent = reinterpret_cast<float4*>(b + o.ent);
-    d->went = reinterpret_cast<const unsigned long long*>(sb + L.went);
-    d->wrec = reinterpret_cast<const unsigned*>(sb + L.wrec);
-    d->ent_cap = c->defer_ent_cap;
-    d->rec_cap = c->defer_rec_cap;
-    d->map_cap = (unsigned)(c->defer_ent_cap / 64 + c->defer_waves);
-    d->waves = L.waves;
-    // the shadow pass's grid: ~2-3 chunks per wave rather than one persistent
-    // round (1,536 workgroups at 6 per CU), so the hardware dispatcher balances
-    // the tail -- 3/8 of the sorted waves measured 0.90-0.91 ms against 0.98 at
-    // config 3 (profiles/r03/ab_shadow_blocks_*.txt)
-    d->worley_cache = c->shadow_cache;
-    d->eval_blocks = c->shadow_blocks ? (unsigned)c->shadow_blocks
-                                      : (unsigned)std::max<size_t>(kShadowEvalBlocks, (size_t)L.waves * 3 / 8);
-    return VR_OK;
-}
 
 vr_status vr_render(void* p, const vr_target* t, void* stream)
 try {

@@ -163,6 +163,11 @@ struct vr_shard {
     // assembles; ranks 1..N-1 render the band sets of a world of N-1 renderers
     // (rank r: band_first r - 1), received into gather slot r - 1
     bool compositor = false;
+    // compositor with band sets: rank 0 also renders the lead rows [0,
+    // lead_rows) of the frame in place (a multiple of band_rows; 0 = none),
+    // and the renderers' band sets cover the rows below them
+    // (vr_shard_set_lead_rows / vr_shard_balance_lead)
+    int lead_rows = 0;
     // balanced row ranges (vr_shard_set_rows / vr_shard_balance_rows): renderer
     // k renders frame rows [row_begin[k], row_begin[k + 1]) (VR_TARGET_ROW_RANGE)
     // and rank 0 gathers them into a grey frame; empty = interleaved band sets
@@ -352,6 +357,11 @@ bool others_here(const vr_shard* sh) { return sh->loopback && !sh->solo; }
 int renderers(const vr_shard* sh) { return sh->compositor ? sh->nranks - 1 : sh->nranks; }
 int band_first_of(const vr_shard* sh, int r) { return sh->compositor ? r - 1 : r; }
 bool rows_mode(const vr_shard* sh) { return !sh->row_begin.empty(); }
+// the renderers' band sets start below rank 0's lead rows: frame band b0 + k
+// is renderer k's first (a band set over the whole frame, band_first >= stride)
+int lead_band(const vr_shard* sh) { return sh->lead_rows / sh->band_rows; }
+int set_first_of(const vr_shard* sh, int r) { return band_first_of(sh, r) + lead_band(sh); }
+bool leads(const vr_shard* sh, int r) { return r == 0 && sh->lead_rows > 0; }
 // rank 0's gather buffer: a slot of rows_per_rank rows per rank, or (row
 // ranges) a grey frame that every renderer's range lands in at its own rows
 size_t gather_rows(const vr_shard* sh)
@@ -375,14 +385,18 @@ vr_target target_of(const vr_shard* sh, int r)
         t.band_rows = sh->row_begin[k + 1] - sh->row_begin[k];
         t.band_stride = 1;
         t.band_first = sh->row_begin[k];
+    } else if (leads(sh, r)) {   // rank 0's lead rows (VR_TARGET_ROW_RANGE)
+        t.band_rows = sh->lead_rows;
+        t.band_stride = 1;
+        t.band_first = 0;
     } else {
         t.band_rows = sh->band_rows;
         t.band_stride = renderers(sh);
-        t.band_first = band_first_of(sh, r);
+        t.band_first = set_first_of(sh, r);
     }
     return t;
 }
-int range_flag(const vr_shard* sh) { return rows_mode(sh) ? VR_TARGET_ROW_RANGE : 0; }
+int range_flag(const vr_shard* sh, int r) { return rows_mode(sh) || leads(sh, r) ? VR_TARGET_ROW_RANGE : 0; }
 // the assembly: every renderer's rows, or (rank 0 rendering in place) all but rank 0's
 vr_status assemble(vr_shard* sh, int p, hipStream_t s)
 {
@@ -395,9 +409,13 @@ vr_status assemble(vr_shard* sh, int p, hipStream_t s)
                                            s));
         return VR_OK;
     }
+    // (rank 0's lead rows, rendered in place, are above the band sets: the
+    // assembly expands the frame below them, where renderer k's set is the
+    // sub-frame's band set k)
+    const int lead = sh->lead_rows;
     VR_TRY(vr_assemble_frame_ranks(sh->ctx, sh->gathered[p], sh->gformat, (size_t)sh->rows_per_rank, renderers(sh),
-                                   sh->compositor ? 0 : 1, sh->width, sh->height, sh->band_rows, sh->format,
-                                   sh->frame[p], s));
+                                   sh->compositor ? 0 : 1, sh->width, sh->height - lead, sh->band_rows, sh->format,
+                                   sh->frame[p] + (size_t)lead * sh->pitch, s));
     return VR_OK;
 }
 
@@ -410,11 +428,11 @@ vr_status render_half(vr_shard* sh, int p, hipStream_t s, hipEvent_t t0, hipEven
     if ((!r0 || here) && sh->pending[p]) HIP_TRY(hipStreamWaitEvent(s, sh->done[p], 0));
     vr_target t = target_of(sh, sh->rank);
     if (r0) {   // in place: the frame's own rows, the frame's format
-        t.format = sh->format | VR_TARGET_BANDS_IN_PLACE | range_flag(sh);
+        t.format = sh->format | VR_TARGET_BANDS_IN_PLACE | range_flag(sh, sh->rank);
         t.pixels = sh->frame[p];
         t.row_pitch = sh->pitch;
     } else {
-        t.format = sh->gformat | range_flag(sh);
+        t.format = sh->gformat | range_flag(sh, sh->rank);
         t.pixels = sh->local[p];
         t.row_pitch = sh->gpitch;
     }
@@ -424,7 +442,7 @@ vr_status render_half(vr_shard* sh, int p, hipStream_t s, hipEvent_t t0, hipEven
     if (here) {   // the other ranks' band sets, rendered here into their gather slots
         for (int r = 1; r < sh->nranks; ++r) {
             t = target_of(sh, r);
-            t.format = sh->gformat | range_flag(sh);
+            t.format = sh->gformat | range_flag(sh, r);
             t.row_pitch = sh->gpitch;
             t.pixels = slot_of(sh, p, r);
             if (sh->rows_of[r] > 0) VR_TRY(vr_render(sh->ctx, &t, s));
@@ -485,11 +503,11 @@ vr_status one_frame_on_render(vr_shard* sh, int p, hipStream_t rs, hipEvent_t t0
     const bool r0 = sh->rank == 0, here = others_here(sh);
     vr_target t = target_of(sh, sh->rank);
     if (r0) {
-        t.format = sh->format | VR_TARGET_BANDS_IN_PLACE | range_flag(sh);
+        t.format = sh->format | VR_TARGET_BANDS_IN_PLACE | range_flag(sh, sh->rank);
         t.pixels = sh->frame[p];
         t.row_pitch = sh->pitch;
     } else {
-        t.format = sh->gformat | range_flag(sh);
+        t.format = sh->gformat | range_flag(sh, sh->rank);
         t.pixels = sh->local[p];
         t.row_pitch = sh->gpitch;
     }
@@ -499,7 +517,7 @@ vr_status one_frame_on_render(vr_shard* sh, int p, hipStream_t rs, hipEvent_t t0
     if (here) {
         for (int r = 1; r < sh->nranks; ++r) {
             t = target_of(sh, r);
-            t.format = sh->gformat | range_flag(sh);
+            t.format = sh->gformat | range_flag(sh, r);
             t.row_pitch = sh->gpitch;
             t.pixels = slot_of(sh, p, r);
             if (sh->rows_of[r] > 0) VR_TRY(vr_render(sh->ctx, &t, rs));
@@ -537,17 +555,19 @@ void set_geometry(vr_shard* sh, bool compositor)
     sh->compositor = compositor && sh->nranks >= 2;
     const int R = renderers(sh);
     if ((int)sh->row_begin.size() != R + 1) sh->row_begin.clear();   // ranges of another renderer count
+    if (!sh->compositor || rows_mode(sh)) sh->lead_rows = 0;          // lead rows: compositor + band sets only
     sh->rows_of.assign(sh->nranks, 0);
     for (int r = 0; r < sh->nranks; ++r)
         if (!sh->compositor || r > 0) {
             const int k = band_first_of(sh, r);
             sh->rows_of[r] = rows_mode(sh) ? sh->row_begin[k + 1] - sh->row_begin[k]
-                                           : vr_band_rows_packed(sh->height, sh->band_rows, R, k);
+                                           : vr_band_rows_packed(sh->height, sh->band_rows, R, set_first_of(sh, r));
         }
+    if (leads(sh, 0)) sh->rows_of[0] = sh->lead_rows;
     sh->my_rows = sh->rows_of[sh->rank];
     // band 0 is the first renderer's: it has the most rows (ranges: the longest)
     sh->rows_per_rank = rows_mode(sh) ? *std::max_element(sh->rows_of.begin(), sh->rows_of.end())
-                                      : vr_band_rows_packed(sh->height, sh->band_rows, R, 0);
+                                      : vr_band_rows_packed(sh->height, sh->band_rows, R, lead_band(sh));
 }
 
 // rank 0's gather slots / another rank's band sets, for the current geometry
@@ -1204,7 +1224,7 @@ vr_status vr_shard_bands(vr_shard* sh, int* band_stride, int* band_first)
 try {
     if (!sh) return fail(VR_ERR_INVALID, "vr_shard_bands: null");
     if (band_stride) *band_stride = renderers(sh);
-    if (band_first) *band_first = band_first_of(sh, sh->rank);
+    if (band_first) *band_first = leads(sh, sh->rank) ? -1 : set_first_of(sh, sh->rank);
     return VR_OK;
 } catch (...) {
     return caught_exception("vr_shard_bands");
@@ -1244,6 +1264,39 @@ try {
 
 namespace {
 
+// Rank 0's ints to every rank over the shard's communicator (after a
+// connect; a no-op in loopback or with one rank): v[0] is rank 0's failure
+// flag, so a rank-0 failure reaches every rank after the one collective.
+vr_status bcast_ints(vr_shard* sh, std::vector<int>& rb, const char* fn)
+{
+    if (sh->nranks > 1 && !sh->loopback) {
+        HIP_TRY(hipSetDevice(sh->device));
+        int* d = nullptr;
+        HIP_TRY(hipMalloc(&d, rb.size() * sizeof(int)));
+        hipError_t he = hipMemcpyAsync(d, rb.data(), rb.size() * sizeof(int), hipMemcpyHostToDevice, sh->comm_stream);
+        vr_status st = VR_OK;
+        ncclResult_t nr = ncclSuccess;
+        if (he == hipSuccess) {
+            nr = ncclBroadcast(d, d, rb.size(), ncclInt32, 0, sh->comm, sh->comm_stream);
+            if (nr == ncclInProgress) {
+                st = settle(sh, fn);
+                nr = ncclSuccess;
+            }
+        }
+        if (he == hipSuccess && nr == ncclSuccess && st == VR_OK)
+            he = hipMemcpyAsync(rb.data(), d, rb.size() * sizeof(int), hipMemcpyDeviceToHost, sh->comm_stream);
+        if (he == hipSuccess && nr == ncclSuccess && st == VR_OK) st = wait_stream(sh, sh->comm_stream, fn);
+        if (!sh->aborted) (void)hipFree(d);
+        if (st != VR_OK) return st;
+        if (nr != ncclSuccess) {
+            abort_comm(sh);
+            return fail(VR_ERR_COMM, "%s: ncclBroadcast: %s", fn, ncclGetErrorString(nr));
+        }
+        if (he != hipSuccess) return fail(VR_ERR_HIP, "%s: %s", fn, hipGetErrorString(he));
+    }
+    return VR_OK;
+}
+
 // Rank 0's partition, on every rank: broadcast with a failure flag (a rank-0
 // failure reaches every rank after the one collective, not a hang).  all_ms
 // (every rank's measured ms, by rank): vr_row_partition_measured over the
@@ -1277,31 +1330,7 @@ vr_status share_partition(vr_shard* sh, const std::vector<double>* all_ms, const
             rb[0] = 1;
         }
     }
-    if (sh->nranks > 1 && !sh->loopback) {
-        HIP_TRY(hipSetDevice(sh->device));
-        int* d = nullptr;
-        HIP_TRY(hipMalloc(&d, rb.size() * sizeof(int)));
-        hipError_t he = hipMemcpyAsync(d, rb.data(), rb.size() * sizeof(int), hipMemcpyHostToDevice, sh->comm_stream);
-        vr_status st = VR_OK;
-        ncclResult_t nr = ncclSuccess;
-        if (he == hipSuccess) {
-            nr = ncclBroadcast(d, d, rb.size(), ncclInt32, 0, sh->comm, sh->comm_stream);
-            if (nr == ncclInProgress) {
-                st = settle(sh, fn);
-                nr = ncclSuccess;
-            }
-        }
-        if (he == hipSuccess && nr == ncclSuccess && st == VR_OK)
-            he = hipMemcpyAsync(rb.data(), d, rb.size() * sizeof(int), hipMemcpyDeviceToHost, sh->comm_stream);
-        if (he == hipSuccess && nr == ncclSuccess && st == VR_OK) st = wait_stream(sh, sh->comm_stream, fn);
-        if (!sh->aborted) (void)hipFree(d);
-        if (st != VR_OK) return st;
-        if (nr != ncclSuccess) {
-            abort_comm(sh);
-            return fail(VR_ERR_COMM, "%s: ncclBroadcast: %s", fn, ncclGetErrorString(nr));
-        }
-        if (he != hipSuccess) return fail(VR_ERR_HIP, "%s: %s", fn, hipGetErrorString(he));
-    }
+    SH_TRY(bcast_ints(sh, rb, fn));
     if (rb[0]) {
         if (mine != VR_OK) return fail(mine, "%s: %s", fn, msg.c_str());
         return fail(VR_ERR_INVALID, "%s: rank 0's partition failed", fn);
@@ -1363,6 +1392,82 @@ try {
     return share_partition(sh, &ms, "vr_shard_rebalance_rows");
 } catch (...) {
     return caught_exception("vr_shard_rebalance_rows");
+}
+
+vr_status vr_shard_set_lead_rows(vr_shard* sh, int rows)
+try {
+    if (!sh) return fail(VR_ERR_INVALID, "vr_shard_set_lead_rows: null");
+    if (rows < 0 || rows % sh->band_rows != 0 || rows >= sh->height)
+        return fail(VR_ERR_INVALID, "vr_shard_set_lead_rows: %d rows: a multiple of the band rows (%d) below the "
+                                    "frame height %d", rows, sh->band_rows, sh->height);
+    if (rows > 0 && (!sh->compositor || rows_mode(sh)))
+        return fail(VR_ERR_INVALID, "vr_shard_set_lead_rows: lead rows need rank 0 as a compositor over band sets");
+    if (rows == sh->lead_rows) return VR_OK;
+    if (sh->started) return fail(VR_ERR_INVALID, "vr_shard_set_lead_rows: set before the first frames");
+    sh->lead_rows = rows;
+    set_geometry(sh, sh->compositor);
+    return alloc_band_buffers(sh);
+} catch (...) {
+    return caught_exception("vr_shard_set_lead_rows");
+}
+
+int vr_shard_get_lead_rows(vr_shard* sh) { return sh ? sh->lead_rows : -1; }
+
+// Collective: rank 0 sizes its lead rows for the ctx's camera and every rank
+// takes them.  Rank 0 counts as pct % of a renderer (the rest of its time is
+// the assembly): over every lead of whole bands, the estimated work per row
+// (vr_row_work, the row partition's model) gives rank 0's cost -- the lead
+// rows' work / (pct / 100) -- and each renderer's -- the work of its band set
+// below the lead --, and the lead with the smallest largest cost wins.  The
+// renderers' band counts are part of that: a lead that leaves a whole number
+// of bands per renderer keeps them level.
+vr_status vr_shard_balance_lead(vr_shard* sh, int pct)
+try {
+    if (!sh || pct < 0 || pct > 100) return fail(VR_ERR_INVALID, "vr_shard_balance_lead: bad argument");
+    if (sh->loopback && sh->rank != 0 && !sh->solo)
+        return fail(VR_ERR_INVALID, "vr_shard_balance_lead: rank %d is not connected (vr_shard_connect)", sh->rank);
+    if (!sh->compositor || rows_mode(sh))
+        return fail(VR_ERR_INVALID, "vr_shard_balance_lead: lead rows need rank 0 as a compositor over band sets");
+    SH_TRY(check_usable(sh, "vr_shard_balance_lead"));
+    std::vector<int> v(2, 0);   // [0]: failed, [1]: lead rows
+    vr_status mine = VR_OK;
+    std::string msg;
+    if ((sh->rank == 0 || sh->loopback) && pct > 0) {
+        const int H = sh->height, br = sh->band_rows, R = renderers(sh), nb = (H + br - 1) / br;
+        const int ns = (H + 7) / 8;
+        std::vector<double> sw((size_t)ns, 0.0);
+        mine = vr_row_work(sh->ctx, sh->width, H, sw.data(), ns);
+        if (mine != VR_OK) {
+            msg = vr_last_error();
+            v[0] = 1;
+        } else {
+            std::vector<double> band((size_t)nb, 0.0);   // work per band: its rows' share of their strips
+            for (int y = 0; y < H; ++y) band[(size_t)(y / br)] += sw[(size_t)(y / 8)] / 8.0;
+            double best = INFINITY;
+            for (int lb = 0; lb + R <= nb; ++lb) {
+                double cost = 0.0;
+                for (int b = 0; b < lb; ++b) cost += band[(size_t)b];
+                cost /= pct / 100.0;
+                for (int k = 0; k < R; ++k) {
+                    double ck = 0.0;
+                    for (int b = lb + k; b < nb; b += R) ck += band[(size_t)b];
+                    cost = std::max(cost, ck);
+                }
+                if (cost < best) {
+                    best = cost;
+                    v[1] = lb * br;
+                }
+            }
+        }
+    }
+    SH_TRY(bcast_ints(sh, v, "vr_shard_balance_lead"));
+    if (v[0]) {
+        if (mine != VR_OK) return fail(mine, "vr_shard_balance_lead: %s", msg.c_str());
+        return fail(VR_ERR_INVALID, "vr_shard_balance_lead: rank 0's partition failed");
+    }
+    return vr_shard_set_lead_rows(sh, v[1]);
+} catch (...) {
+    return caught_exception("vr_shard_balance_lead");
 }
 
 int vr_shard_partition(vr_shard* sh)

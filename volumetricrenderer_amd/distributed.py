@@ -274,6 +274,12 @@ class BandSharder:
         self._pipe = None
 
 
+# rank 0's lead rows beside its assembly when it is a compositor over band
+# sets: it counts as this % of a renderer (vr_shard_balance_lead; DESIGN.md
+# sec. 7.5: 40 chose 288 rows at config 5 / 8 ranks, the measured best)
+AUTO_LEAD_PCT = 40
+
+
 class RcclBandPipeline:
     """The native multi-GPU frame loop (libvr_shard.so, include/vr_shard.h):
     the same interleaved bands and gather to rank 0 as :class:`BandSharder`,
@@ -287,7 +293,8 @@ class RcclBandPipeline:
     def __init__(self, renderer, width: int, height: int, fmt: int, band_rows: int = 16, world: int = 1,
                  rank: int = 0, group=None, loopback: bool = False, timeout_s: float | None = None,
                  render_streams: int | None = None, solo: bool = False, host_threads: int = 1, exchange_on_render: bool = True,
-                 compositor: bool | None = None, partition: str = "auto", rows: list[int] | None = None):
+                 compositor: bool | None = None, partition: str = "auto", rows: list[int] | None = None,
+                 lead_pct: int | str | None = "auto", lead_rows: int | None = None):
         """loopback: one process renders all `world` ranks' band sets on its
         GPU and assembles them (no communicator; tests and rehearsals).
         solo (loopback only, any rank): each frame renders only this rank's
@@ -313,6 +320,15 @@ class RcclBandPipeline:
         ranks), else "bands".
         rows: explicit row starts for partition "rows" (renderers + 1 entries,
         vr_shard_set_rows; every rank the same) instead of the balanced split.
+        lead_pct / lead_rows (compositor over band sets only): rank 0 also
+        renders the frame's first rows in place, beside its assembly, and the
+        renderers' band sets cover the rest -- sized at the first run_frames
+        for the camera with rank 0 counted as lead_pct % of a renderer
+        (vr_shard_balance_lead, collective), or lead_rows explicit rows (a
+        multiple of band_rows; vr_shard_set_lead_rows).  "auto" (default):
+        lead_pct AUTO_LEAD_PCT whenever rank 0 is a compositor over band sets
+        (config 5 at 8 ranks: slowest rank 0.0191-0.0197 ms per frame against
+        0.0203-0.0204 without), else none; None: none.
         exchange_on_render: True (default) = each frame's exchange follows its
         render on the frame's render stream, over a communicator per buffer
         parity, with no events; False = on a communication stream, ordered by
@@ -409,6 +425,22 @@ class RcclBandPipeline:
                                  f"got {len(rows)}")
             _lib.shard_call("vr_shard_set_rows", h, (ctypes.c_int * len(rows))(*rows))
             self._balanced = True
+        self._lead_pct = None
+        if lead_pct == "auto":
+            lead_pct = (AUTO_LEAD_PCT if lead_rows is None and self.partition == "bands"
+                        and bool(_lib.shard_call("vr_shard_get_compositor", h)) else None)
+        if lead_pct is not None or lead_rows is not None:
+            if not bool(_lib.shard_call("vr_shard_get_compositor", h)) or self.partition != "bands":
+                _lib.shard_call("vr_shard_destroy", h)
+                raise ValueError("RcclBandPipeline: lead rows need rank 0 as a compositor over band sets")
+            if lead_rows is not None:
+                try:
+                    _lib.shard_call("vr_shard_set_lead_rows", h, int(lead_rows))
+                except _lib.VRError:
+                    _lib.shard_call("vr_shard_destroy", h)
+                    raise
+            else:
+                self._lead_pct = int(lead_pct)
         self._geometry()
 
     def _geometry(self) -> None:
@@ -420,6 +452,7 @@ class RcclBandPipeline:
         _lib.shard_call("vr_shard_bands", h, ctypes.byref(stride), ctypes.byref(first))
         self.band_stride, self.band_first = stride.value, first.value   # this rank's band set (vr_render target)
         self.compositor = bool(_lib.shard_call("vr_shard_get_compositor", h))
+        self.lead_rows = _lib.shard_call("vr_shard_get_lead_rows", h)   # rank 0's lead rows (0: none)
         self.row_range = None   # (first frame row, rows) of this rank with row ranges
         if _lib.shard_call("vr_shard_partition", h) == 1:
             r0, n = ctypes.c_int(), ctypes.c_int()
@@ -485,6 +518,12 @@ class RcclBandPipeline:
             if cameras:   # the ranges follow the first frame's camera
                 self.r.set_shader_data(*cameras[0])
             self.balance_rows()
+        if self._lead_pct is not None and k > 0:   # rank 0's lead rows, for the first frame's camera
+            if cameras:
+                self.r.set_shader_data(*cameras[0])
+            _lib.shard_call("vr_shard_balance_lead", self._h, self._lead_pct)
+            self._lead_pct = None
+            self._geometry()
         if cameras is None:
             _lib.shard_call("vr_shard_run_frames", self._h, k, None, None, _stream_handle(stream), sample_every,
                             ctypes.byref(ms) if sample_every > 0 else None, ctypes.byref(host))

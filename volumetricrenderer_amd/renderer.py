@@ -315,6 +315,15 @@ class Renderer:
         call("vr_row_partition", self._ctx, width, height, parts, rb)
         return list(rb)
 
+    def row_work(self, width: int, height: int) -> list[float]:
+        """The estimated march work of every 8-row strip (vr_row_work: the
+        model vr_row_partition splits and vr_shard_balance_lead sizes rank 0's
+        lead rows from)."""
+        ns = (height + 7) // 8
+        out = (ctypes.c_double * ns)()
+        call("vr_row_work", self._ctx, width, height, out, ns)
+        return list(out)
+
     def row_partition_measured(self, width: int, height: int, prev: list[int], prev_ms: list[float]) -> list[int]:
         """vr_row_partition_measured: the split again, range k of `prev` having
         taken prev_ms[k]."""
