@@ -297,7 +297,7 @@ def other_config(name, steps, warmup, warm_ms=0.0):
         # grid media: the same frames two in flight, as the headline's loop runs
         # them -- consecutive frames alternate two streams and two targets
         inflight2 = None
-        if proc is None:
+        if True:   # (a procedural medium too since round 6: per-stream deferred scratch)
             streams = [torch.cuda.Stream(), torch.cuda.Stream()]
             outs = [out, r.alloc_target(W, H, fmt)]
             launches = [r.prepare_render(W, H, fmt, outs[k], stream=streams[k]) for k in range(2)]
@@ -313,18 +313,38 @@ def other_config(name, steps, warmup, warm_ms=0.0):
                          "def": "the same frames, consecutive frames alternating two streams and two targets, wall "
                                 "time per frame"}
         defer = proc is not None and shadow > 0 and r.get_option("shadow_defer_last") == 1
+        # config 2 (procedural, no shadow rays) runs two in flight, as its own
+        # N = 1 line does (bench.py --config cloud; 0.1606 against 0.1662 ms on
+        # one stream, profiles/r06/c10); the others keep one stream (config 3
+        # two in flight: 0.783 against 0.756; config 4 level)
+        two = proc is not None and shadow == 0 and inflight2 is not None
+        one_stream = None
+        roof_ms = kern_ms
+        if two:
+            one_stream = {"ms_per_step": round(el / steps * 1e3, 4), "value": round(W * H * S * steps / el / 1e6, 3),
+                          "kernel_ms_mean": round(kern_ms, 5),
+                          "def": "the same frames on one stream (launches do not overlap)"}
+            el = el2
+            roof_ms = el2 / steps * 1e3
+            inflight2 = None
         res = {"metric": f"Mray/s (= W*H*steps/s) at {W}x{H} x {S} steps",
                "value": round(W * H * S * steps / el / 1e6, 3), "unit": "Mray/s", "steps": steps,
                "ms_per_step": round(el / steps * 1e3, 4), "kernel_ms_mean": round(kern_ms, 5),
+               **({"frames_in_flight": 2} if two else {}),
                "config": {"workload": (f"{name}: {N}^3 RGBA8 grid, {W}x{H}, {S} steps, RGBA8 out" if proc is None
                                        else f"{name}: procedural {proc.octaves}-octave Perlin-Worley cloud, "
                                             f"{W}x{H}, {S} steps, shadow {shadow} steps, RGBA8 out"),
                           "baseline_config_index": cfg_idx,
                           "kernel": variant + ("_deferred" if defer else ""),
                           "executed_steps_per_frame": nsteps},
-               "roofline": roofline_of(r, proc, shadow, variant, nsteps, evals, cells, kern_ms),
+               "roofline": roofline_of(r, proc, shadow, variant, nsteps, evals, cells, roof_ms),
                "clock_warm": clock_warm_obj(warm_ms, warm_frames),
-               **({"frames_in_flight_2": inflight2} if inflight2 else {})}
+               **({"frames_in_flight_2": inflight2} if inflight2 else {}),
+               **({"one_stream": one_stream} if one_stream else {})}
+        if two:
+            res["roofline"]["achieved_def"] += ("; two frames in flight on alternating streams, so the time is the "
+                                                "wall time per frame of the window (kernel_ms_mean: the one-stream "
+                                                "launches' mean)")
         if defer:
             res["shadow_defer_scratch_MB"] = round(r.get_option("shadow_defer_kib") / 1024.0, 1)
         vol = r.get_volume() if proc is None else None

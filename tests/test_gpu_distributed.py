@@ -518,8 +518,8 @@ def test_one_rank_frames_in_flight(oracle):
     """BandSharder at world 1 with inflight=2 (bench.py --inflight 2): grid
     frames alternate two streams and two targets (two frames in flight);
     each target's frame equals the oracle's, and the caller's stream waits
-    for both.  The procedural medium keeps one stream (its scratch is the
-    context's): its frames are exact as well."""
+    for both.  The procedural medium with deferred shadow rays runs two in
+    flight too since round 6 (per-stream deferred scratch): exact as well."""
     import sys
     sys.path.insert(0, ROOT)
     import volumetricrenderer_amd as vr
@@ -548,7 +548,8 @@ def test_one_rank_frames_in_flight(oracle):
         torch.cuda.synchronize()
         ref2, _ = oracle.render_procedural(p, obj, glob, oracle.from_params(m), W, H, 0)
         assert np.array_equal(frame.cpu().numpy(), ref2)
-        assert getattr(sh2, "_launch2", None) is None
+        assert getattr(sh2, "_launch2", None) is not None
+        assert all(np.array_equal(t.cpu().numpy(), ref2) for t in sh2._targets2)
 
 
 def test_frames_in_flight_then_one_stream_paths(oracle):
@@ -598,8 +599,9 @@ def test_procedural_frames_in_flight_readers_and_writers(oracle):
     read the ctx's scratch and overlap on two streams; a frame with a new
     camera rebuilds the order (writes) and must wait for the reader still in
     flight on the other stream, and the next readers for it.  Every frame of
-    both cameras equals the oracle's; then the same with shadow rays (every
-    frame writes, one stream)."""
+    both cameras equals the oracle's; then the same with deferred shadow rays,
+    two in flight as well (round 6: a reusing frame writes only its stream's
+    deferred scratch set)."""
     import sys
     sys.path.insert(0, ROOT)
     import volumetricrenderer_amd as vr
@@ -624,8 +626,24 @@ def test_procedural_frames_in_flight_readers_and_writers(oracle):
             assert sh._launch2 is not None
             assert np.array_equal(f.cpu().numpy(), want[c]), (k, c)
             assert all(np.array_equal(t.cpu().numpy(), want[c]) for t in sh._targets2), (k, c)
+        # deferred shadow rays (round 6): a frame that reuses the order writes
+        # only its stream's scratch set, so these overlap on two streams too
         r.set_procedural(shadow_steps=4)
         assert r.get_option("procedural") == 2
+        p = oracle.procedural_from(r.procedural)
+        want = []
+        for c in cams:
+            obj, glob = vr.shader_data_arrays(*c)
+            want.append(oracle.render_procedural(p, obj, glob, oracle.from_params(m), W, H, 0)[0])
+        sh2 = BandSharder(r, W, H, 0, inflight=2)
+        for k, c in ((5, 0), (4, 1), (3, 0), (6, 1)):
+            r.set_shader_data(*cams[c])
+            f = sh2.run_frames(k)
+            torch.cuda.current_stream().synchronize()
+            assert sh2._launch2 is not None and r.get_option("shadow_defer_last") == 1
+            assert np.array_equal(f.cpu().numpy(), want[c]), (k, c)
+            assert all(np.array_equal(t.cpu().numpy(), want[c]) for t in sh2._targets2), (k, c)
+        assert r.get_option("shadow_defer_kib") > 0
 
 
 def test_row_partition_measured_and_one_rank_rebalance():

@@ -327,7 +327,8 @@ try {
     if (c->d_heads) (void)hipFree(c->d_heads);
     if (c->d_sort) (void)hipFree(c->d_sort);
     (void)hipDeviceSynchronize();   // queued renders may still read the region lists and the scratch
-    if (c->d_defer) (void)hipFree(c->d_defer);
+    for (const auto& ds : c->defer_sets)
+        if (ds.d) (void)hipFree(ds.d);
     for (const auto& q : c->defer_retired) {
         (void)hipFree(q.p);
         if (q.ev) (void)hipEventDestroy(q.ev);
@@ -838,8 +839,10 @@ try {
                          a.proc.wt_n > 0;
         // a stale order's keys do not bound the new step counts: no deferred ranges
         if (reuse == SORT_STALE) use_defer = false;
+        bool defer_shared = false;
         if (use_defer) {
-            const vr_status st = ensure_defer(c, a, sort_buf, &defer, &use_defer);
+            const vr_status st = ensure_defer(c, a, sort_buf, static_cast<hipStream_t>(stream), &defer, &use_defer,
+                                              &defer_shared);
             if (st != VR_OK) return st;
         }
         std::vector<float> built = reuse == SORT_BUILD ? key : c->sort_key;
@@ -849,8 +852,11 @@ try {
         constexpr size_t kMaxProcStreams = 8;
         bool known = false;
         for (const auto& u : c->proc_uses) known = known || u.s == ps;
-        // a ninth stream is treated as a writer: it waits for every render
-        const bool writes = reuse == SORT_BUILD || use_defer || (!known && c->proc_uses.size() >= kMaxProcStreams);
+        // a ninth stream is treated as a writer: it waits for every render.
+        // A deferred frame that reuses the order writes only its stream's
+        // scratch set: a reader of the shared sort scratch (round 6)
+        const bool writes = reuse == SORT_BUILD || (use_defer && defer_shared) ||
+                            (!known && c->proc_uses.size() >= kMaxProcStreams);
         if (writes) {
             for (const auto& u : c->proc_uses)
                 if (u.s != ps) {
@@ -861,10 +867,12 @@ try {
             const vr_status sw = stream_wait_pending(ps, c->proc_wev);
             if (sw != VR_OK) return sw;
         }
-        // a scratch this (writing) frame outgrew: free once every earlier frame
-        // has run (this stream now follows every earlier procedural render)
+        // a scratch this frame outgrew: free once every earlier frame that used
+        // it has run -- after the waits above if it writes (this stream then
+        // follows every earlier procedural render), else on its own stream,
+        // the only one that used its set
         for (auto& q : c->defer_retired)
-            if (writes && !q.ev) {
+            if (!q.ev) {
                 HIP_TRY(hipEventCreateWithFlags(&q.ev, hipEventDisableTiming));
                 HIP_TRY(hipEventRecord(q.ev, static_cast<hipStream_t>(stream)));
             }

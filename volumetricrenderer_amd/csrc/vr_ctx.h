@@ -115,10 +115,19 @@ struct Ctx {
     int shadow_blocks = 0;         // option "shadow_blocks": workgroups of the deferred shadow pass (0 = auto)
     int shadow_defer = 1;          // measured 1.25 -> 0.99 ms at config 3
     int shadow_cache = 0;          // deferred shadow pass: Worley cube cached in registers per lane
-    void* d_defer = nullptr;
-    size_t defer_bytes = 0;
-    unsigned long long defer_ent_cap = 0;   // entries / step records / waves the current scratch holds
-    unsigned defer_rec_cap = 0, defer_waves = 0;
+    // The deferred passes' scratch, one set per render stream (round 6): a
+    // frame that reuses the cost order writes only its stream's set, so it
+    // reads the shared sort scratch like any reader and overlaps the frames
+    // of other streams (config 3 with 2 frames in flight).  Past
+    // kMaxDeferSets streams a frame shares set 0 and renders as a writer.
+    struct DeferSet {
+        hipStream_t s = nullptr;
+        void* d = nullptr;
+        size_t bytes = 0;
+        unsigned long long ent_cap = 0;   // entries / step records / waves it holds
+        unsigned rec_cap = 0, waves = 0;
+    };
+    std::vector<DeferSet> defer_sets;
     // entries / step records per pixel-step (per wave-step) of the frame: 5/4 of
     // the largest need seen (proc_scan -> need_host); 1/12 and 1/8 until one is
     double want_ent = 0.0, want_rec = 0.0;
@@ -126,10 +135,10 @@ struct Ctx {
     unsigned defer_entries = 0;    // option "shadow_defer_entries": entry capacity override (tests; 0 = sized from the frame)
     int defer_last = 0;            // the last procedural render ran the deferred passes
     // outgrown scratch buffers: queued frames may still use them.  Each gets an
-    // event recorded on the render stream of the writing frame that outgrew it,
-    // after that stream has waited for every earlier procedural render
-    // (proc_uses), and is freed by a later ensure_defer once the event has
-    // completed
+    // event recorded on the render stream of the frame that outgrew it -- after
+    // that stream has waited for every earlier procedural render if the frame
+    // writes, else on its own stream, the only one that used its set -- and is
+    // freed by a later ensure_defer once the event has completed
     struct Retired {
         void* p;
         hipEvent_t ev;             // nullptr until recorded
@@ -280,6 +289,7 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
 int worley_z_pitch(int n);
 vr_status ensure_lattice(Ctx* c, ProcParams* q, hipStream_t s);
 vr_status release_defer(Ctx* c);
-vr_status ensure_defer(Ctx* c, const MarchArgs& a, void* sort_buf, ShadowDefer* d, bool* ok);
+vr_status ensure_defer(Ctx* c, const MarchArgs& a, void* sort_buf, hipStream_t s, ShadowDefer* d, bool* ok, bool* shared);
+constexpr size_t kMaxDeferSets = 4;
 
 }  // namespace vrapi

@@ -218,10 +218,15 @@ try {
     if (n == "shadow_defer_last") return c->defer_last;   // read-only
     // read-only: 0 = a grid medium; 1 = procedural, frames that reuse one
     // camera's order only read the ctx's scratch (they overlap on two
-    // streams); 2 = procedural with shadow rays (deferred: every frame writes)
+    // streams); 2 = procedural with deferred shadow rays (round 6: a frame
+    // that reuses the order writes only its stream's scratch set, so these
+    // overlap too)
     if (n == "procedural") return !c->proc.enabled ? 0 : c->proc.shadow_steps > 0 && c->shadow_defer ? 2 : 1;
-    if (n == "shadow_defer_kib")                          // read-only: the scratch held now, KiB
-        return (int)std::min<size_t>((c->defer_bytes + 1023) / 1024, 0x7fffffff);
+    if (n == "shadow_defer_kib") {                        // read-only: the scratch held now (every stream's set), KiB
+        size_t b = 0;
+        for (const auto& ds : c->defer_sets) b += ds.bytes;
+        return (int)std::min<size_t>((b + 1023) / 1024, 0x7fffffff);
+    }
     if (n == "slab_cap") return c->slab_cap;
     if (n == "region_order") return c->region_order;
     if (n == "sort_reuse") return c->sort_reuse;

@@ -92,27 +92,25 @@ vr_status ensure_lattice(Ctx* c, ProcParams* q, hipStream_t s)
 // the allocation failed) -- the render then takes the in-wave compaction.
 vr_status release_defer(Ctx* c)
 {
-    if (!c->d_defer && c->defer_retired.empty()) return VR_OK;
+    if (c->defer_sets.empty() && c->defer_retired.empty()) return VR_OK;
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipDeviceSynchronize());   // an option change, not a frame: queued renders may use the scratch
-    if (c->d_defer) (void)hipFree(c->d_defer);
+    for (const auto& ds : c->defer_sets)
+        if (ds.d) (void)hipFree(ds.d);
     for (const auto& q : c->defer_retired) {
         (void)hipFree(q.p);
         if (q.ev) (void)hipEventDestroy(q.ev);
     }
     c->defer_retired.clear();
-    c->d_defer = nullptr;
-    c->defer_bytes = 0;
-    c->defer_ent_cap = 0;
-    c->defer_rec_cap = 0;
-    c->defer_waves = 0;
+    c->defer_sets.clear();
     c->want_ent = c->want_rec = 0.0;
     return VR_OK;
 }
 
-vr_status ensure_defer(Ctx* c, const MarchArgs& a, void* sort_buf, ShadowDefer* d, bool* ok)
+vr_status ensure_defer(Ctx* c, const MarchArgs& a, void* sort_buf, hipStream_t s, ShadowDefer* d, bool* ok, bool* shared)
 {
     *ok = false;
+    *shared = false;
     // free the outgrown buffers whose frames have run
     for (size_t i = 0; i < c->defer_retired.size();) {
         Ctx::Retired& q = c->defer_retired[i];
@@ -167,13 +165,28 @@ vr_status ensure_defer(Ctx* c, const MarchArgs& a, void* sort_buf, ShadowDefer* 
         o.bytes = o.ent + (size_t)e * sizeof(float4);
         return o;
     };
-    const unsigned waves = std::max(L.waves, c->defer_waves);
-    const bool fits = c->d_defer && L.waves <= c->defer_waves && rec <= c->defer_rec_cap &&
-                      (c->defer_entries ? ent == c->defer_ent_cap : ent <= c->defer_ent_cap);
+    // this stream's set (a new one for a new stream, up to kMaxDeferSets)
+    Ctx::DeferSet* set = nullptr;
+    for (auto& x : c->defer_sets)
+        if (x.s == s) set = &x;
+    if (!set) {
+        if (c->defer_sets.size() < kMaxDeferSets) {
+            c->defer_sets.push_back(Ctx::DeferSet{});
+            set = &c->defer_sets.back();
+            set->s = s;
+        } else {
+            set = &c->defer_sets[0];   // shared: the frame renders as a writer
+            *shared = true;
+        }
+    }
+    Ctx::DeferSet& ds = *set;
+    const unsigned waves = std::max(L.waves, ds.waves);
+    const bool fits = ds.d && L.waves <= ds.waves && rec <= ds.rec_cap &&
+                      (c->defer_entries ? ent == ds.ent_cap : ent <= ds.ent_cap);
     if (!fits) {
-        if (c->d_defer && !c->defer_entries) {   // grow by at least 1/4: a slowly growing need reallocates rarely
-            ent = std::max(ent, c->defer_ent_cap + c->defer_ent_cap / 4);
-            rec = std::max(rec, (unsigned long long)c->defer_rec_cap + c->defer_rec_cap / 4);
+        if (ds.d && !c->defer_entries) {   // grow by at least 1/4: a slowly growing need reallocates rarely
+            ent = std::max(ent, ds.ent_cap + ds.ent_cap / 4);
+            rec = std::max(rec, (unsigned long long)ds.rec_cap + ds.rec_cap / 4);
         }
         ent = std::min(ent, kMaxCap);
         rec = std::min(rec, kMaxCap);
@@ -186,10 +199,10 @@ vr_status ensure_defer(Ctx* c, const MarchArgs& a, void* sort_buf, ShadowDefer* 
         const Off o = layout(ent, rec, waves);
         if (ent < 4096 || o.bytes > limit || hipMalloc(&nb, o.bytes) != hipSuccess) {
             (void)hipGetLastError();   // clear an allocation error; keep what there is
-            if (!c->d_defer || L.waves > c->defer_waves) return VR_OK;
+            if (!ds.d || L.waves > ds.waves) return VR_OK;
         } else {
-            if (c->d_defer) {
-                c->defer_retired.push_back({c->d_defer, nullptr});   // its event: vr_render, before the launch
+            if (ds.d) {
+                c->defer_retired.push_back({ds.d, nullptr});   // its event: vr_render, before the launch
                 if (c->defer_retired.size() > kMaxDeferRetired) {   // rare: a device sync frees them
                     HIP_TRY(hipDeviceSynchronize());
                     for (const auto& q : c->defer_retired) {
@@ -199,16 +212,16 @@ vr_status ensure_defer(Ctx* c, const MarchArgs& a, void* sort_buf, ShadowDefer* 
                     c->defer_retired.clear();   // the device is idle: the old scratch too
                 }
             }
-            c->d_defer = nb;
-            c->defer_bytes = o.bytes;
-            c->defer_ent_cap = ent;
-            c->defer_rec_cap = (unsigned)rec;
-            c->defer_waves = waves;
+            ds.d = nb;
+            ds.bytes = o.bytes;
+            ds.ent_cap = ent;
+            ds.rec_cap = (unsigned)rec;
+            ds.waves = waves;
         }
     }
-    const Off o = layout(c->defer_ent_cap, c->defer_rec_cap, c->defer_waves);
+    const Off o = layout(ds.ent_cap, ds.rec_cap, ds.waves);
     *ok = true;
-    char* b = static_cast<char*>(c->d_defer);
+    char* b = static_cast<char*>(ds.d);
     char* sb = static_cast<char*>(sort_buf);
     d->count = reinterpret_cast<unsigned*>(b);
     d->wsteps = reinterpret_cast<unsigned*>(b + o.ws);
@@ -219,9 +232,9 @@ vr_status ensure_defer(Ctx* c, const MarchArgs& a, void* sort_buf, ShadowDefer* 
     d->ent = reinterpret_cast<float4*>(b + o.ent);
     d->went = reinterpret_cast<const unsigned long long*>(sb + L.went);
     d->wrec = reinterpret_cast<const unsigned*>(sb + L.wrec);
-    d->ent_cap = c->defer_ent_cap;
-    d->rec_cap = c->defer_rec_cap;
-    d->map_cap = (unsigned)(c->defer_ent_cap / 64 + c->defer_waves);
+    d->ent_cap = ds.ent_cap;
+    d->rec_cap = ds.rec_cap;
+    d->map_cap = (unsigned)(ds.ent_cap / 64 + ds.waves);
     d->waves = L.waves;
     // the shadow pass's grid: ~2-3 chunks per wave rather than one persistent
     // round (1,536 workgroups at 6 per CU), so the hardware dispatcher balances

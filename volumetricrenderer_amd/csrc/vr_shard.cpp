@@ -764,9 +764,10 @@ try {
     }
     int next = 0;
     const auto h0 = std::chrono::steady_clock::now();
-    // a procedural medium with deferred shadow rays writes the ctx's scratch
-    // every frame, so its frames cannot overlap (vr_render orders them across
-    // streams): one render stream, without the cross-stream waits
+    // a procedural medium with deferred shadow rays renders on one stream:
+    // its frames could overlap since round 6 (a frame that reuses the cost
+    // order writes only its stream's deferred scratch set), but two in flight
+    // measured slower (config 3: 0.783 against 0.756 ms, profiles/r06/c10)
     const int P = vr_get_option(sh->ctx, "procedural") == 2 ? 1
                   : sh->on_render ? sh->render_streams : std::min(sh->render_streams, 2);
     const bool two = P >= 2;   // frames overlap on P render streams

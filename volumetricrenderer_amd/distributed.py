@@ -157,10 +157,10 @@ class BandSharder:
         gather buffers and frames are double-buffered.  Each buffer of a
         parity is reused only after the stream order has retired its last
         reader.  Returns the last frame (rank 0) or band set."""
-        # (a procedural medium with deferred shadow rays writes the ctx's
-        # scratch every frame: its frames cannot overlap, one stream below)
-        overlap_ok = not hasattr(self.r, "get_option") or self.r.get_option("procedural") != 2
-        if self.world == 1 and self.inflight == 2 and hasattr(self.r, "prepare_render") and overlap_ok:
+        # (a procedural medium with deferred shadow rays overlaps too since
+        # round 6: a frame that reuses the cost order writes only its
+        # stream's deferred scratch set)
+        if self.world == 1 and self.inflight == 2 and hasattr(self.r, "prepare_render"):
             # one rank, grid medium, inflight 2 (throughput mode): consecutive
             # frames alternate between two streams and two targets, so frame
             # i+1's waves fill the SIMDs while frame i's last, longest rays
