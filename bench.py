@@ -41,6 +41,7 @@ import volumetricrenderer_amd as vr  # noqa: E402
 from volumetricrenderer_amd import distributed as vrdist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+GATE_CYCLES = int(2e-3 * 2.1e9)   # ~2 ms of torch.cuda._sleep at ~2.1 GHz: the host queues K frames behind it
 FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: fp32 vector peak
 TA_PEAK_GLOOKUPS = 256 * 2.4   # L1 tag lookups: 1 per CU-cycle at 2.4 GHz (tools/tcp_calib.hip)
 BYTES_PER_STEP = 32        # 4 trilinear taps x 8 texels x 1 B
@@ -304,11 +305,20 @@ def other_config(name, steps, warmup, warm_ms=0.0):
             for i in range(warmup):
                 launches[i & 1]()
             torch.cuda.synchronize()
+            cur = torch.cuda.current_stream()
+            g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             t0 = time.perf_counter()
+            g0.record(cur)
+            for st_ in streams:
+                st_.wait_event(g0)
             for i in range(steps):
                 launches[i & 1]()
+            for st_ in streams:
+                cur.wait_stream(st_)
+            g1.record(cur)
             torch.cuda.synchronize()
             el2 = time.perf_counter() - t0
+            gpu2_ms = g0.elapsed_time(g1)
             inflight2 = {"ms_per_step": round(el2 / steps * 1e3, 4), "value": round(W * H * S * steps / el2 / 1e6, 3),
                          "def": "the same frames, consecutive frames alternating two streams and two targets, wall "
                                 "time per frame"}
@@ -325,7 +335,7 @@ def other_config(name, steps, warmup, warm_ms=0.0):
                           "kernel_ms_mean": round(kern_ms, 5),
                           "def": "the same frames on one stream (launches do not overlap)"}
             el = el2
-            roof_ms = el2 / steps * 1e3
+            roof_ms = gpu2_ms / steps   # the window on the GPU clock (HIP events), per frame
             inflight2 = None
         res = {"metric": f"Mray/s (= W*H*steps/s) at {W}x{H} x {S} steps",
                "value": round(W * H * S * steps / el / 1e6, 3), "unit": "Mray/s", "steps": steps,
@@ -342,9 +352,11 @@ def other_config(name, steps, warmup, warm_ms=0.0):
                **({"frames_in_flight_2": inflight2} if inflight2 else {}),
                **({"one_stream": one_stream} if one_stream else {})}
         if two:
+            res["gpu_window_ms"] = round(gpu2_ms, 4)
             res["roofline"]["achieved_def"] += ("; two frames in flight on alternating streams, so the time is the "
-                                                "wall time per frame of the window (kernel_ms_mean: the one-stream "
-                                                "launches' mean)")
+                                                "timed window on the GPU clock (HIP events on the caller's stream "
+                                                "around the frames, gpu_window_ms) per frame (kernel_ms_mean: the "
+                                                "one-stream launches' mean)")
         if defer:
             res["shadow_defer_scratch_MB"] = round(r.get_option("shadow_defer_kib") / 1024.0, 1)
         vol = r.get_volume() if proc is None else None
@@ -493,6 +505,7 @@ def main() -> int:
     ev_every = 4
     warm_frames = 0
     busy_ms_frame = None
+    gated_ms_frame = None
     frame_check = None
     window = None
     pipe = None
@@ -556,9 +569,24 @@ def main() -> int:
         got = pipe.frame(stream)
         if rank == 0:
             frame_check = frame_check_of(got, r.render(W, H, fmt))
-        # untimed, after the window: the same K frames with every render
-        # sampled, for the GPU busy time per frame (the union of the renders'
-        # intervals; overlapping frames count once: vr_shard_sampled_busy)
+        # untimed, after the window: the same K frames gated -- queued behind
+        # a ~2 ms spin on the caller's stream, so the GPU never waits for the
+        # host between them -- with HIP events after the spin and after the
+        # join of the render streams: the GPU time per frame the roofline
+        # divides by (the timed window's own GPU clock also holds the first
+        # frame's launch latency)
+        g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(stream):
+            torch.cuda._sleep(GATE_CYCLES)
+        g0.record(stream)
+        pipe.run_frames(args.steps, stream=stream, cameras=sd[args.warmup:] if sd else None)
+        g1.record(stream)
+        pipe.barrier(stream)
+        torch.cuda.synchronize()
+        gated_ms_frame = g0.elapsed_time(g1) / args.steps
+        # and with every render sampled: the GPU busy time per frame (the
+        # union of the renders' intervals; overlapping frames count once:
+        # vr_shard_sampled_busy; the per-render events slow the frames a little)
         pipe.run_frames(args.steps, stream=stream, sample_every=1, cameras=sd[args.warmup:] if sd else None)
         busy_ms, _span = pipe.sampled_busy()
         busy_ms_frame = busy_ms / args.steps
@@ -715,7 +743,11 @@ def main() -> int:
         # two render streams (native loop, N > 1): a launch overlaps the next, so
         # its duration is not a frame's -- the roofline takes the wall time per frame
         overlap = (native and streams_eff >= 2) or proc_inflight2 or (world == 1 and args.inflight == 2)
-        roof_ms = ms_per_step if overlap else kern_ms
+        # overlapping launches: the window on the GPU clock (HIP events on the
+        # caller's stream around the frames) per frame -- what the kernel trace's
+        # first-start-to-last-end span measures -- else the launches' mean
+        roof_ms = ((gated_ms_frame or (window["gpu_window_ms"] / args.steps if window else ms_per_step))
+                   if overlap else kern_ms)
         compositor = native and pipe is not None and pipe.compositor
         lead = pipe.lead_rows if compositor else 0   # rank 0's lead rows beside its assembly
         rows_part = native and pipe is not None and pipe.partition == "rows"
@@ -731,8 +763,16 @@ def main() -> int:
             roofline = roofline_of(r, proc, shadow, variant, local_steps, local_evals, local_cells, roof_ms)
         if overlap:
             roofline["achieved_def"] += (f"; renders overlap ({streams_eff} render streams or two in flight), so "
-                                         "the time is the wall time per frame of the timed window, not a launch's "
-                                         "duration (kernel_ms_mean: the overlapping launches' mean)")
+                                         "the time is the timed window per frame, not a launch's duration "
+                                         "(kernel_ms_mean: the overlapping launches' mean)"
+                                         + (": the GPU time per frame of the same K frames run again after the window, "
+                                            "gated (queued behind a ~2 ms spin on the caller's stream so the GPU never "
+                                            "waits for the host; HIP events after the spin and after the join of the "
+                                            "render streams: gpu_ms_per_frame_gated); the timed window's own clocks are "
+                                            "in window, and ms_per_step is the host clock's"
+                                            if gated_ms_frame else ": its wall time"))
+        if gated_ms_frame:
+            roofline["gpu_ms_per_frame_gated"] = round(gated_ms_frame, 5)
         if busy_ms_frame and not compositor:
             # the same units over the GPU busy time per frame (union of the
             # renders' intervals, overlapping frames counted once)

@@ -98,8 +98,18 @@ def main():
                 cw = obj["clock_warm"]["frames"]
         if name == "grid512_all_channels":
             first = a.warmup
+        elif obj and obj.get("frames_in_flight") == 2:
+            # config 2: the one-stream window and its warm-up come first, then the
+            # two-in-flight window the line reports (bench.py other_config)
+            first = cw + 2 * a.warmup + a.steps
         else:
             first = cw + a.warmup
+        gated = None
+        if name == "grid512" and obj and "gpu_ms_per_frame_gated" in obj.get("roofline", {}):
+            # bench.py: the same K frames again, gated, after the window (the roofline's time)
+            g = fr[first + a.steps:first + 2 * a.steps]
+            giv = [(s_, e_) for f in g for (s_, e_, _) in f]
+            gated = (max(e_ for _, e_ in giv) - min(s_ for s_, _ in giv)) / a.steps / 1e6
         timed = fr[first:first + a.steps]
         iv = [(s, e) for f in timed for (s, e, _) in f]
         t_first, t_last = min(s for s, _ in iv), max(e for _, e in iv)
@@ -124,9 +134,20 @@ def main():
                 ro = obj["roofline"]
                 ms_line = obj["ms_per_step"]
                 # the line's achieved x its time = the algorithmic units per frame
-                t_used = ms_line if "wall time per frame" in ro.get("achieved_def", "") else obj["kernel_ms_mean"]
+                if "gpu_window_ms" in ro.get("achieved_def", ""):
+                    t_used = (obj.get("window", {}).get("gpu_window_ms") or obj.get("gpu_window_ms")) / a.steps
+                elif "window" in ro.get("achieved_def", ""):
+                    t_used = ms_line
+                else:
+                    t_used = obj["kernel_ms_mean"]
                 units = ro["achieved"] * t_used
-                for label, t in (("trace wall", wall), ("trace busy", busy)):
+                if "gpu_ms_per_frame_gated" in ro:
+                    t_used = ro["gpu_ms_per_frame_gated"]
+                    units = ro["achieved"] * t_used
+                checks = [("trace wall", wall), ("trace busy", busy)]
+                if gated is not None:
+                    checks.append(("trace wall of the gated pass", gated))
+                for label, t in checks:
                     frac = units / t / ro["peak"]
                     print(f"  roofline: line frac {ro['frac']:.4f} (time {t_used:.4f} ms); {label} {t:.4f} ms -> "
                           f"frac {frac:.4f} ({frac / ro['frac'] - 1:+.1%})")
