@@ -566,9 +566,10 @@ def main() -> int:
         # parity of the timed path (verdict r05 #2): rank 0's last frame of the
         # window -- RCCL-gathered and assembled at N > 1 -- against a plain
         # one-GPU render of the same camera, untimed
+        # (the copy now, the reference render after the passes below: a plain
+        # render's other target geometry would make the loop's next frame
+        # rebuild its region lists on the host)
         got = pipe.frame(stream)
-        if rank == 0:
-            frame_check = frame_check_of(got, r.render(W, H, fmt))
         # untimed, after the window: the same K frames gated -- queued behind
         # a ~2 ms spin on the caller's stream, so the GPU never waits for the
         # host between them -- with HIP events after the spin and after the
@@ -592,6 +593,10 @@ def main() -> int:
         busy_ms_frame = busy_ms / args.steps
         pipe.barrier(stream)
         torch.cuda.synchronize()
+        if rank == 0:
+            if sd:   # the window's last camera (the passes above ended on it too)
+                r.set_shader_data(*sd[-1])
+            frame_check = frame_check_of(got, r.render(W, H, fmt))
         if world > 1:
             dist.barrier()
     elif args.spin:
@@ -773,6 +778,8 @@ def main() -> int:
                                             if gated_ms_frame else ": its wall time"))
         if gated_ms_frame:
             roofline["gpu_ms_per_frame_gated"] = round(gated_ms_frame, 5)
+            # the same units over the host wall time per frame of the timed window
+            roofline["frac_wall"] = round(roofline["achieved"] * roof_ms / ms_per_step / roofline["peak"], 4)
         if busy_ms_frame and not compositor:
             # the same units over the GPU busy time per frame (union of the
             # renders' intervals, overlapping frames counted once)
@@ -788,6 +795,8 @@ def main() -> int:
             pk = bw[pk_kind][0]
             roofline.update({"peak_measured": round(pk, 1), "peak_measured_kind": pk_kind,
                              "frac_measured": round(roofline["achieved"] / pk, 4),
+                             **({"frac_measured_wall": round(roofline["achieved"] * roof_ms / ms_per_step / pk, 4)}
+                                if gated_ms_frame else {}),
                              "peak_read": round(bw["read"][0], 1), "peak_copy": round(bw["copy"][0], 1),
                              "peak_measured_def": "the larger of a read-only stream (loads folded into a register, "
                                                   "bytes read / time) and a float4 copy (read + written bytes / time): "
