@@ -886,8 +886,12 @@ def main() -> int:
             "roofline": dict(roofline, traffic=traffic,
                              **({"traffic_GBs": round(traffic / (roof_ms * 1e-3) / 1e9, 1),
                                  "traffic_frac": round(traffic / (roof_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                                 "traffic_def": "PMC HBM bytes per launch (profiles/traffic.json) / the same "
-                                                "mean kernel duration: the bytes the kernel really moves"}
+                                 "traffic_def": "PMC bytes per frame (profiles/traffic.json: FETCH_SIZE x 2 + "
+                                                "WRITE_SIZE, re-collected on this build in round 6) / the same "
+                                                "time per frame; FETCH_SIZE counts the L2's fabric requests, "
+                                                "Infinity-Cache hits included, and its x2 gfx950 correction is "
+                                                "calibrated for 16-B-per-lane streams, not the march's 8-B "
+                                                "gathers: an upper bound of the HBM bytes"}
                                 if traffic else {}),
                              **({"ta_lookup": ta} if ta else {})),
         }
