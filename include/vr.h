@@ -333,7 +333,10 @@ vr_status vr_set_layout_preference(void* ctx, int pref);
  *   "tiles_per_wave"  1-64, strided, ring and region schedules; 0 = auto,
  *                     the default: 2 for rings, 3 for regions on the col48
  *                     layout and 2 on the others, 1 for strided.
- *   "wedges"          1-64, regions schedule: wedges per XCD (default 8).
+ *   "wedges"          1-64, regions schedule: wedges per XCD; 0 = auto (the
+ *                     default): 4 while frames_overlap is set (frames in
+ *                     flight on several streams), else 8.  vr_get_option
+ *                     returns the count in force.
  *   "supertile"       1, 2, 4, regions schedule: the tile lists are ordered by
  *                     S x S blocks of 8x8 tiles (default 2), so a workgroup's
  *                     waves render one block.

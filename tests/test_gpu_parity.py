@@ -1145,7 +1145,6 @@ def test_regions_schedule_every_pixel_once(r, oracle, vol128, wedges):
     tile exactly once -- the output buffer is pre-filled with a sentinel --
     and they are rebuilt when the geometry changes (camera, size, bands)."""
     W, H = 328, 200
-    wedges0 = r.get_option("wedges")
     r.set_option("schedule", 5)
     r.set_option("wedges", wedges)
     try:
@@ -1170,7 +1169,7 @@ def test_regions_schedule_every_pixel_once(r, oracle, vol128, wedges):
             assert int(cnt.item()) == steps
     finally:
         r.set_option("schedule", -1)
-        r.set_option("wedges", wedges0)
+        r.set_option("wedges", 0)  # back to auto (vr_ctx.h wedges_of)
 
 
 def test_regions_lists_across_streams(r, oracle, vol128):

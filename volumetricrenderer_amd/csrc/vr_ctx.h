@@ -39,6 +39,10 @@ constexpr int kDefaultSchedule = -1;     // -1 auto, 0 static tiles, 1 persisten
 constexpr int kDefaultWavesPerSimd = 4;
 constexpr int kDefaultTilesPerWave = 0;   // 0 = auto: 2 for rings and regions, 1 for strided (measured)
 constexpr int kDefaultWedges = 8;         // regions schedule: wedges per XCD (measured; 4 until round 4)
+// with consecutive frames overlapping (option frames_overlap): 4 -- config 5
+// 0.1050 against 0.1078 ms per frame on the GPU clock (4 rounds), 0.0187 against
+// 0.0193-0.0196 at 8 ranks; config 4 level (profiles/r06/c17, c18)
+constexpr int kDefaultWedgesOverlap = 4;
 // a moving camera reuses the current (still complete, maybe less balanced)
 // region lists for this many renders before they are rebuilt
 constexpr int kRegionRebuildInterval = 32;
@@ -165,7 +169,7 @@ struct Ctx {
     // regions schedule (build_regions): per-XCD tile lists, double-buffered
     // so a rebuild never waits for more than the render that last used the
     // other buffer (2 frames in flight, VulkanRenderer.cpp:13)
-    int wedges = kDefaultWedges;   // wedges per XCD
+    int wedges = 0;                // wedges per XCD; 0 = auto (wedges_of)
     int split = 0;                 // lanes per ray: 0 = auto, 1, 2, 4, 8
     int slab = 0;                  // COL48 + regions: the LDS slab march (vr_march_slab.hip)
     int proc_enum = 0;             // procedural sort: 1 = 64x64-region enumeration with shadow rays too
@@ -277,6 +281,10 @@ vr_status make_plan(Ctx* c, MarchArgs* a, Plan* p);
 const char* variant_name(const Plan& p);
 
 // ---- vr_regions_host.cpp
+inline int wedges_of(const Ctx* c)
+{
+    return c->wedges > 0 ? c->wedges : c->frames_overlap ? kDefaultWedgesOverlap : kDefaultWedges;
+}
 void box_centre_pixel(const Ctx* c, const MarchArgs& a, int* px, int* prow);
 vr_status stream_wait_pending(hipStream_t s, hipEvent_t ev);
 vr_status note_region_stream(Ctx::RegionBuf& rb, hipStream_t s, int* slot);

@@ -95,7 +95,7 @@ try {
         return VR_OK;
     }
     if (n == "wedges") {
-        if (value < 1 || value > 64) return fail(VR_ERR_INVALID, "vr_set_option: wedges in [1, 64]");
+        if (value < 0 || value > 64) return fail(VR_ERR_INVALID, "vr_set_option: wedges in [0 (auto), 64]");
         c->wedges = value;
         return VR_OK;
     }
@@ -205,7 +205,7 @@ try {
     if (n == "waves_per_simd") return c->waves_per_simd;
     if (n == "tiles_per_wave") return c->tiles_per_wave;
     if (n == "count") return c->count;
-    if (n == "wedges") return c->wedges;
+    if (n == "wedges") return wedges_of(c);   // (the effective count; set 0 for auto)
     if (n == "split") return c->split;
     if (n == "lattice") return c->lattice;
     if (n == "slab") return c->slab;

@@ -188,7 +188,7 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     const int tw = (a.width + 7) >> 3, th = (a.out_rows + 7) >> 3;
     float key[kRegionKeyLen] = {(float)tw, (float)th, (float)a.width, (float)a.height, (float)a.out_rows,
                                 (float)a.band_rows, (float)a.band_stride, (float)a.band_first, (float)tpw,
-                                (float)c->wedges, (float)(65536 * c->region_order), (float)c->split, (float)c->supertile};
+                                (float)wedges_of(c), (float)(65536 * c->region_order), (float)c->split, (float)c->supertile};
     constexpr int grid_part = 13;   // the part a reused list must match
     int kn = grid_part;
     for (float v : {(float)a.max_steps, a.step_size, (float)cpx, (float)cprow}) key[kn++] = v;
@@ -249,7 +249,7 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
         g.height = a.height;
         g.ccx = (cpx + 0.5) / 8.0; g.ccy = (cprow + 0.5) / 8.0;
         g.ctx = (cpx >> 3) / S; g.cty = (cprow >> 3) / S;
-        g.supertile = S; g.wedges = c->wedges; g.order = c->region_order;
+        g.supertile = S; g.wedges = wedges_of(c); g.order = c->region_order;
         int* dev_hdr = nullptr;
         HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&dev_hdr), c->h_rghdr, 0));
         // one build scratch per context: a build on another stream waits for the last one
@@ -331,7 +331,7 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     double total = 0.0;
     for (const T& t : work) total += t.cost;
     std::vector<std::vector<T>> xl(8);
-    const int K = 8 * c->wedges;
+    const int K = 8 * wedges_of(c);
     double run = 0.0;
     for (const T& t : work) {   // wedge k = the k-th K-quantile of the work, dealt to XCD k % 8
         xl[std::min(K - 1, (int)((run + 0.5 * t.cost) / total * K)) % 8].push_back(t);
