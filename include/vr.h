@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define VR_ABI_VERSION 1
+#define VR_ABI_VERSION 2
 
 typedef enum {
     VR_OK = 0,
@@ -140,6 +140,12 @@ typedef struct {
 /* A render target.  `pixels` is a DEVICE pointer that the caller owns.
  * With band_rows > 0 only bands b = band_first, band_first + band_stride, ...
  * are rendered.  Band b covers frame rows [b*band_rows, (b+1)*band_rows).
+ * band_flip (ABI 2) shifts every second band of the set: its k-th band is
+ * band_first + k*band_stride + (k odd ? band_flip : 0), |band_flip| <
+ * band_stride.  A world of S renderers with flips S-1-2i (renderer i) deals
+ * the bands serpentine: forwards in even periods of S bands, backwards in odd
+ * ones, so a cost that drifts down the frame does not load one renderer
+ * more in every period (vr_shard.h vr_shard_set_serpentine).
  * The bands are written packed and in order, from row 0 of `pixels`; the
  * rows of a last, partial band that lie past `height` are left untouched.
  * This is how the frame is split across GPUs.  band_rows = 0 renders the whole
@@ -167,6 +173,8 @@ typedef struct {
     void*     pixels;
     size_t    row_pitch;     /* bytes; 0 = tightly packed                  */
     uint64_t* step_counter;
+    int32_t   band_flip;     /* 0 = plain band set; see above              */
+    int32_t   reserved;      /* must be 0                                  */
 } vr_target;
 
 /* ---- context (replaces Renderer::Init/Shutdown, VulkanRenderer.h:68-72) */
@@ -261,12 +269,16 @@ vr_status vr_assemble_frame(void* ctx, const void* d_gathered, int gathered_form
                             void* d_frame, void* stream);
 /* vr_assemble_frame for the ranks first_rank .. nranks-1 only: the rows of
  * ranks below first_rank are left untouched (rendered in place, with
- * VR_TARGET_BANDS_IN_PLACE); their gather slots are not read.             */
+ * VR_TARGET_BANDS_IN_PLACE); their gather slots are not read.
+ * frame_format | VR_ASSEMBLE_SERPENTINE: rank r rendered its set with
+ * band_flip nranks-1-2r (the serpentine deal, vr_target).                 */
+#define VR_ASSEMBLE_SERPENTINE 0x400
 vr_status vr_assemble_frame_ranks(void* ctx, const void* d_gathered, int gathered_format, size_t rows_per_rank,
                                   int nranks, int first_rank, int width, int height, int band_rows,
                                   int frame_format, void* d_frame, void* stream);
-/* rows that vr_render writes for a band set (for sizing buffers)          */
-int vr_band_rows_packed(int height, int band_rows, int band_stride, int band_first);
+/* rows that vr_render writes for a band set (for sizing buffers): whole
+ * bands, the set's last partial one included                             */
+int vr_band_rows_packed(int height, int band_rows, int band_stride, int band_first, int band_flip);
 /* Split the frame's rows into `parts` contiguous ranges of equal estimated
  * march work for the ctx's current camera and march constants (host, double;
  * the same inputs give the same split on every rank).  row_begin[parts + 1]:

@@ -173,9 +173,20 @@ vr_status vr_shard_set_exchange_streams(vr_shard* sh, int on_render);
  * Results are identical. */
 vr_status vr_shard_set_compositor(vr_shard* sh, int on);
 int       vr_shard_get_compositor(vr_shard* sh);
-/* This rank's band set: band_stride and band_first of its vr_render target
- * (rank 0 as a compositor: stride N-1, first -1, no rows). */
-vr_status vr_shard_bands(vr_shard* sh, int* band_stride, int* band_first);
+/* This rank's band set: band_stride, band_first and band_flip of its
+ * vr_render target (rank 0 as a compositor: stride N-1, first -1, no rows). */
+vr_status vr_shard_bands(vr_shard* sh, int* band_stride, int* band_first, int* band_flip);
+/* Serpentine band sets (round 6; new, no reference counterpart): 1 (the
+ * default) = renderer k of R deals its bands forwards in even periods of R
+ * bands and backwards in odd ones (vr.h vr_target.band_flip R-1-2k), and the
+ * assembly follows (VR_ASSEMBLE_SERPENTINE); 0 = the plain interleave, band
+ * k + jR.  With the plain interleave renderer 0 takes the first band of every
+ * period, and below the cube's widest rows the work per band falls down the
+ * frame, so it was the slowest of 7 in every config-5 rehearsal at 8 ranks
+ * (DESIGN.md sec. 7.5).  Every rank must choose the same, before its first
+ * frames.  Results are identical. */
+vr_status vr_shard_set_serpentine(vr_shard* sh, int on);
+int       vr_shard_get_serpentine(vr_shard* sh);
 /* Contiguous row ranges instead of interleaved band sets.  Renderer k (rank
  * k, or rank k + 1 with rank 0 as a compositor) renders frame rows
  * [row_begin[k], row_begin[k + 1]) (vr.h VR_TARGET_ROW_RANGE); rank 0 gathers

@@ -32,7 +32,7 @@ def test_shard_library_exports_every_declared_symbol():
     from volumetricrenderer_amd import _lib
     lib = _lib.load_shard()
     declared = header_functions("vr_shard.h")
-    assert len(declared) == 34
+    assert len(declared) == 36
     for name in declared:
         assert hasattr(lib, name), name
     assert sorted(declared) == _lib.shard_exported_symbols()
@@ -49,8 +49,11 @@ def test_shard_library_exports_every_declared_symbol():
     with pytest.raises(_lib.VRError):
         _lib.shard_call("vr_shard_set_compositor", None, 1)
     with pytest.raises(_lib.VRError):
-        _lib.shard_call("vr_shard_bands", None, None, None)
+        _lib.shard_call("vr_shard_bands", None, None, None, None)
     assert _lib.shard_call("vr_shard_get_compositor", None) == -1
+    with pytest.raises(_lib.VRError):
+        _lib.shard_call("vr_shard_set_serpentine", None, 1)
+    assert _lib.shard_call("vr_shard_get_serpentine", None) == -1
     for f, args in (("vr_shard_set_rows", (None, None)), ("vr_shard_balance_rows", (None,)),
                     ("vr_shard_rebalance_rows", (None, 1.0)),
                     ("vr_shard_row_range", (None, 0, None, None))):
@@ -102,8 +105,8 @@ def test_abi_struct_layouts():
     assert ctypes.sizeof(_lib.GlobalShaderData) == 144
     assert _lib.GlobalShaderData.media_scroll.offset == 80  # std140
     assert ctypes.sizeof(_lib.MarchParams) == 88
-    assert ctypes.sizeof(_lib.Target) == 48
-    assert _lib.load().vr_abi_version() == 1
+    assert ctypes.sizeof(_lib.Target) == 56
+    assert _lib.load().vr_abi_version() == 2
 
 
 def test_no_device_is_a_clean_error():
@@ -148,6 +151,42 @@ def test_band_rows_packed():
             assert rows == [rows_for_rank(H, 16, n, k) for k in range(n)]
             assert sum(rows) >= H and sum(rows) - H < 16
     assert vr.band_rows_packed(1080, 0, 1, 0) == 1080
+
+
+def flipped_bands(H, br, stride, first, flip):
+    """The frame bands of a band set with its odd bands shifted by flip
+    (vr.h vr_target.band_flip), by enumeration."""
+    nb, out, k = -(-H // br), [], 0
+    while True:
+        b = first + k * stride + (flip if k % 2 else 0)
+        if b >= nb:
+            if first + k * stride >= nb and first + (k + 1) * stride + flip >= nb:
+                return out
+        else:
+            out.append(b)
+        k += 1
+
+
+def test_band_rows_packed_serpentine():
+    """vr_band_rows_packed with band_flip: the serpentine deal of S renderers
+    (flip S-1-2i) covers every band of the frame exactly once, and each set's
+    packed rows are its whole bands; bad flips are refused."""
+    import volumetricrenderer_amd as vr
+    for H in (16, 17, 100, 720, 1080, 792, 2160):
+        for S in (2, 3, 7, 8):
+            seen = []
+            for i in range(S):
+                bands = flipped_bands(H, 16, S, i, S - 1 - 2 * i)
+                assert bands == sorted(bands)
+                assert vr.band_rows_packed(H, 16, S, i, S - 1 - 2 * i) == 16 * len(bands), (H, S, i)
+                seen += bands
+            assert sorted(seen) == list(range(-(-H // 16)))
+    # an offset set (below a lead of 18 bands) with a negative and a positive flip
+    for flip in (-6, -1, 1, 6):
+        assert vr.band_rows_packed(1080, 16, 7, 20, flip) == 16 * len(flipped_bands(1080, 16, 7, 20, flip))
+    for bad in ((1080, 16, 7, 0, 7), (1080, 16, 7, 0, -7), (1080, 16, 1, 0, 1), (1080, 0, 7, 0, 1)):
+        with pytest.raises(ValueError):
+            vr.band_rows_packed(*bad)
 
 
 def test_header_layouts_match_ctypes(tmp_path):

@@ -179,15 +179,26 @@ def test_rccl_init_deadline_when_a_peer_never_joins():
             _lib.shard_call("vr_shard_destroy", h)
 
 
+def slot_rows(vr, H, band_rows, renderers, first0=0, serpentine=True):
+    """Rows of a gather slot: the largest renderer's band set (serpentine:
+    renderer k's odd bands shifted by R-1-2k, vr_shard_set_serpentine)."""
+    R = renderers
+    return max(vr.band_rows_packed(H, band_rows, R, first0 + k, (R - 1 - 2 * k) if serpentine and R > 1 else 0)
+               for k in range(R))
+
+
 @pytest.mark.parametrize("render_streams", [1, 2, 3, 4])
-@pytest.mark.parametrize("world,band_rows,fmt,W", [(2, 16, 1, 500), (3, 16, 0, 500), (8, 16, 1, 500), (5, 7, 1, 500),
-                                                   (3, 16, 2, 499), (4, 16, 0, 499)])
-def test_native_pipeline_loopback_ranks(world, band_rows, fmt, W, render_streams):
+@pytest.mark.parametrize("world,band_rows,fmt,W,serp", [(2, 16, 1, 500, None), (3, 16, 0, 500, None),
+                                                        (8, 16, 1, 500, None), (5, 7, 1, 500, None),
+                                                        (3, 16, 2, 499, None), (4, 16, 0, 499, None),
+                                                        (8, 16, 1, 500, False), (3, 16, 0, 499, False)])
+def test_native_pipeline_loopback_ranks(world, band_rows, fmt, W, render_streams, serp):
     """The native frame loop's N-rank data layout (grey band sets in gather
     slots of rank 0's row count, expanded by vr_assemble_frame) with every
     rank's bands rendered by this one process: the frame equals a plain
     render.  Width 499 takes the per-pixel expansion, 500 the 4-pixel one.
-    With 1 render stream and with 2 (consecutive frames overlap)."""
+    With 1 render stream and with 2 (consecutive frames overlap).  Band sets
+    serpentine (the default) and plain (serp False)."""
     import sys
     sys.path.insert(0, ROOT)
     import volumetricrenderer_amd as vr
@@ -199,10 +210,12 @@ def test_native_pipeline_loopback_ranks(world, band_rows, fmt, W, render_streams
         r.set_shader_data(osd, gsd)
         r.set_march(vr.march_defaults())
         pl = RcclBandPipeline(r, W, H, fmt, band_rows=band_rows, world=world, rank=0, loopback=True,
-                              render_streams=render_streams)
+                              render_streams=render_streams, serpentine=serp)
         try:
             assert pl.render_streams == render_streams
-            assert pl.rows_per_rank == vr.band_rows_packed(H, band_rows, world, 0)
+            assert pl.serpentine == (serp is not False)
+            R = world - 1 if pl.compositor else world
+            assert pl.rows_per_rank == slot_rows(vr, H, band_rows, R, 0, pl.serpentine)
             pl.run_frames(3)
             pl.barrier()   # loopback: a stream synchronisation
             got = pl.frame()
@@ -251,7 +264,7 @@ def test_native_pipeline_loopback_lead_rows(world, fmt, W, render_streams, lead)
             else:
                 assert lr == lead
             assert pl.my_rows == lr and pl.band_first == -1
-            assert pl.rows_per_rank == vr.band_rows_packed(H, 16, world - 1, lr // 16)
+            assert pl.rows_per_rank == slot_rows(vr, H, 16, world - 1, lr // 16)
             got = pl.frame()
             full = r.render(W, H, fmt)
             torch.cuda.synchronize()
@@ -391,7 +404,9 @@ def test_native_loopback_spinning_8_ranks(oracle, fmt, render_streams, threads, 
                               compositor=True if compositor == "lead" else compositor,
                               lead_rows=48 if compositor == "lead" else None)
         assert pl.compositor == (compositor is not False)
-        assert pl.my_rows == (pl.lead_rows if pl.compositor else pl.rows_per_rank)
+        # (rank 0 rendering its own serpentine set 0: flip 7; the slot holds the largest set)
+        assert pl.my_rows == (pl.lead_rows if pl.compositor else vr.band_rows_packed(H, 16, 8, 0, 7))
+        assert pl.rows_per_rank == slot_rows(vr, H, 16, 7 if pl.compositor else 8, pl.lead_rows // 16)
         got, done = {}, 0
         try:
             for stop in (1, 33, 40):
@@ -414,11 +429,13 @@ def test_native_loopback_spinning_8_ranks(oracle, fmt, render_streams, threads, 
         assert np.array_equal(img.cpu().numpy(), ref), i
 
 
-def band_set_of(frame, rank, world, band_rows):
-    """The packed rows of `rank`'s interleaved bands in a whole frame (vr.h)."""
+def band_set_of(frame, rank, world, band_rows, flip=0):
+    """The packed rows of `rank`'s interleaved bands in a whole frame (vr.h;
+    flip: the set's odd bands shifted, vr_target.band_flip)."""
     H = frame.shape[0]
-    rows = [y for b in range(rank, (H + band_rows - 1) // band_rows, world)
-            for y in range(b * band_rows, min(H, (b + 1) * band_rows))]
+    nb = (H + band_rows - 1) // band_rows
+    bands = [b for k in range(nb + 1) for b in [rank + k * world + (flip if k % 2 else 0)] if b < nb]
+    rows = [y for b in bands for y in range(b * band_rows, min(H, (b + 1) * band_rows))]
     return frame[rows]
 
 
@@ -458,9 +475,13 @@ def test_native_solo_rank_spinning(oracle, render_streams, interval, threads, on
         if partition == "lead":
             pl.run_frames(1, cameras=cams[:1])   # sizes the lead rows for the first camera
             assert pl.lead_rows >= 0 and pl.lead_rows % 16 == 0
-        stride, first = pl.band_stride, pl.band_first
+        stride, first, flip = pl.band_stride, pl.band_first, pl.band_flip
         lead_band = pl.lead_rows // 16
         assert (stride, first) == ((world - 1, rank - 1 + lead_band) if compositor else (world, rank))
+        k = rank - 1 if compositor else rank   # the renderer index: serpentine by default
+        assert pl.serpentine
+        if partition != "rows":   # (the row ranges are set at the first run)
+            assert flip == stride - 1 - 2 * k
         got, done = {}, (1 if partition == "lead" else 0)
         try:
             for stop in (1, 7, 20, 24):
@@ -481,10 +502,10 @@ def test_native_solo_rank_spinning(oracle, render_streams, interval, threads, on
         if partition == "rows":
             want = ref[pl.row_range[0]:pl.row_range[0] + pl.row_range[1], :, 0]
         else:
-            want = band_set_of(ref, first, stride, 16)[..., 0]
+            want = band_set_of(ref, first, stride, 16, flip)[..., 0]
             # (a set holding the frame's last, partial band has that band's
             # rows past the frame packed too: vr_band_rows_packed counts whole bands)
-            assert img.shape[0] == vr.band_rows_packed(H, 16, stride, first)
+            assert img.shape[0] == vr.band_rows_packed(H, 16, stride, first, flip)
             img = img[:want.shape[0]]
         assert img.shape == want.shape and np.array_equal(img.cpu().numpy(), want), i
 

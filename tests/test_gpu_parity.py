@@ -511,6 +511,102 @@ def test_grey_targets_and_expanding_assembly(r, oracle, vol128, fmt):
         r.set_procedural(enabled=0)
 
 
+def serpentine_rows(H, br, stride, first, flip, rows):
+    """Frame row of each of a band set's `rows` packed rows (vr.h
+    vr_target.band_flip: band k is first + k*stride, + flip for odd k); -1
+    past the frame."""
+    out = []
+    for j in range(rows):
+        k = j // br
+        y = (first + k * stride + (flip if k % 2 else 0)) * br + j % br
+        out.append(y if y < H else -1)
+    return np.array(out)
+
+
+def test_serpentine_band_sets_and_assembly(r, oracle, vol128):
+    """Band sets with flipped odd bands (vr_target.band_flip), as the
+    multi-GPU loop deals them serpentine (vr_shard_set_serpentine): each of S
+    renderers' sets (flip S-1-2i) holds its frame rows bit-exact against the
+    oracle's frame, their step counts sum to the frame's, grey sets gathered
+    and expanded with VR_ASSEMBLE_SERPENTINE equal the frame, and a set
+    below a lead of rows (first = lead bands + i) and an in-place set land at
+    their own rows.  Grid (regions and static schedules) and procedural media;
+    band heights 16, 8 and 24, partial last bands."""
+    import ctypes
+    from volumetricrenderer_amd import _lib
+    r.set_volume(vol128)
+    cases = [(320, 200, 16, 3, False, -1), (333, 197, 8, 7, False, -1), (320, 200, 24, 2, False, 0),
+             (200, 150, 16, 3, True, -1)]
+    try:
+        for W, H, br, S, proc, sched in cases:
+            osd, gsd = vr.reference_shader_data(W / H, 15.0, 5.0)
+            march = vr.march_defaults(max_steps=64)
+            r.set_shader_data(osd, gsd)
+            r.set_march(march)
+            r.set_option("schedule", sched)
+            obj, glob = vr.shader_data_arrays(osd, gsd)
+            if proc:
+                # (no shadow rays: a small frame's deferred-scratch need, per
+                # pixel-step, would size the later 1080p frames' scratch)
+                r.set_procedural(shadow_steps=0)
+                ref, steps = oracle.render_procedural(oracle.procedural_from(r.procedural), obj, glob,
+                                                      oracle.from_params(march), W, H, 0)
+            else:
+                r.set_procedural(enabled=0)
+                ref, steps = oracle.render(vol128, obj, glob, oracle.march(64), W, H, oracle.FMT_RGBA32F)
+            fmt, g = vr.FMT_RGBA32F, vr.GREY_OF[vr.FMT_RGBA32F]
+            rows_max = max(vr.band_rows_packed(H, br, S, i, S - 1 - 2 * i) for i in range(S))
+            gathered = torch.zeros((S, rows_max, W), dtype=torch.float32, device="cuda")
+            total = 0
+            for i in range(S):
+                fl = S - 1 - 2 * i
+                rows = vr.band_rows_packed(H, br, S, i, fl)
+                cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+                out = r.alloc_target(W, H, fmt, br, S, i, fl)
+                out.fill_(float("nan"))
+                r.render(W, H, fmt, out=out, band_rows=br, band_stride=S, band_first=i, band_flip=fl, step_counter=cnt)
+                r.render(W, H, g, out=gathered[i, :rows], band_rows=br, band_stride=S, band_first=i, band_flip=fl)
+                torch.cuda.synchronize()
+                total += int(cnt.item())
+                ys = serpentine_rows(H, br, S, i, fl, rows)
+                assert_exact(out.cpu().numpy()[ys >= 0], ref[ys[ys >= 0]])
+            assert total == steps
+            frame = r.assemble_frame(gathered, g, S, W, H, br, fmt, serpentine=True)
+            torch.cuda.synchronize()
+            assert_exact(frame.cpu().numpy(), ref)
+            # below a lead of two bands: renderer i's set starts at band 2 + i
+            lead = 2
+            for i in range(S):
+                fl = S - 1 - 2 * i
+                out = r.render(W, H, fmt, band_rows=br, band_stride=S, band_first=lead + i, band_flip=fl)
+                torch.cuda.synchronize()
+                ys = serpentine_rows(H, br, S, lead + i, fl, out.shape[0])
+                assert_exact(out.cpu().numpy()[ys >= 0], ref[ys[ys >= 0]])
+            # in place: renderer S-1's rows at their frame rows, the rest untouched
+            frame = r.alloc_target(W, H, fmt)
+            frame.fill_(float("nan"))
+            fl = S - 1 - 2 * (S - 1)
+            t = _lib.Target(width=W, height=H, format=fmt | _lib.TARGET_BANDS_IN_PLACE, band_rows=br, band_stride=S,
+                            band_first=S - 1, pixels=frame.data_ptr(), row_pitch=frame.stride(0) * frame.element_size(),
+                            step_counter=None, band_flip=fl)
+            _lib.call("vr_render", r._ctx, ctypes.byref(t), None)
+            torch.cuda.synchronize()
+            got = frame.cpu().numpy()
+            mine = serpentine_rows(H, br, S, S - 1, fl, vr.band_rows_packed(H, br, S, S - 1, fl))
+            mine = mine[mine >= 0]
+            assert_exact(got[mine], ref[mine])
+            assert np.isnan(np.delete(got, mine, axis=0)).all()
+        buf = torch.zeros((64, 64, 4), device="cuda")
+        for stride, flip, fmt in ((3, 3, 0), (3, -3, 0), (1, 1, 0), (3, 1, 0x200)):   # |flip| >= stride, row range
+            t = _lib.Target(width=64, height=64, format=fmt, band_rows=16, band_stride=stride, band_first=0,
+                            pixels=buf.data_ptr(), row_pitch=0, step_counter=None, band_flip=flip)
+            with pytest.raises(vr.VRError):
+                _lib.call("vr_render", r._ctx, ctypes.byref(t), None)
+    finally:
+        r.set_procedural(enabled=0)
+        r.set_option("schedule", -1)
+
+
 def test_volume_generator_matches_oracle(r, oracle):
     for literal in (True, False):
         rec = vr.volume_recipe_defaults(size=48, literal_overwrite=int(literal))

@@ -56,6 +56,8 @@ def main():
     ap.add_argument("--exchange", default="render", choices=["render", "comm"],
                     help="--native: the exchange on the render streams (default) or on a communication stream "
                          "(vr_shard_set_exchange_streams 1 / 0)")
+    ap.add_argument("--serpentine", default="auto", choices=["auto", "on", "off"],
+                    help="--native: band sets dealt serpentine (vr_shard_set_serpentine; auto = the library default)")
     ap.add_argument("--gate-ms", type=float, default=0.0,
                     help="--native: hold the stream with a spin kernel of this many ms while the host queues the "
                          "frames, so the timing is the GPU's alone (not the host's)")
@@ -119,7 +121,7 @@ def native(a):
         print(f"native frame streams: {a.size}^3, {W}x{H}x{a.steps}, {a.frames} frames per timing, "
               f"{a.threads} host thread(s), gate {a.gate_ms} ms, partition {a.partition}, exchange on {a.exchange} "
               "streams, "
-              f"variant {r.kernel_variant} {' '.join(a.opt)}", flush=True)
+              f"variant {r.kernel_variant} serpentine {a.serpentine} {' '.join(a.opt)}", flush=True)
         streams = [int(v) for v in a.streams.split(",")]
         base = {}
         for rows in a.rows:
@@ -161,7 +163,8 @@ def one_n(a, r, W, H, n, streams, base, rows):
                                  exchange_on_render=a.exchange == "render",
                                  compositor=None if a.compositor == "auto" else a.compositor == "on",
                                  partition="rows" if rows else a.partition, rows=rows,
-                                 lead_pct="auto" if a.lead_pct < 0 else (a.lead_pct or None))
+                                 lead_pct="auto" if a.lead_pct < 0 else (a.lead_pct or None),
+                                 serpentine=None if a.serpentine == "auto" else a.serpentine == "on")
             p.run_frames(8)   # region lists, code objects
             p.barrier()
             if first == 0 and p.lead_rows and ns == streams[0]:

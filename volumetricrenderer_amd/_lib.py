@@ -41,6 +41,7 @@ FLOAT_FORMATS = (FMT_RGBA32F, FMT_R32F)
 # OR'ed into a target's format: bands written at their frame rows (include/vr.h)
 TARGET_BANDS_IN_PLACE = 0x100
 TARGET_ROW_RANGE = 0x200   # vr.h VR_TARGET_ROW_RANGE
+ASSEMBLE_SERPENTINE = 0x400   # vr.h: OR'ed into vr_assemble_frame's frame format
 
 c_float_p = ctypes.POINTER(ctypes.c_float)
 c_int_p = ctypes.POINTER(ctypes.c_int)
@@ -94,7 +95,8 @@ class Target(ctypes.Structure):
     _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32), ("format", ctypes.c_int32),
                 ("band_rows", ctypes.c_int32), ("band_stride", ctypes.c_int32),
                 ("band_first", ctypes.c_int32), ("pixels", ctypes.c_void_p),
-                ("row_pitch", ctypes.c_size_t), ("step_counter", ctypes.c_void_p)]
+                ("row_pitch", ctypes.c_size_t), ("step_counter", ctypes.c_void_p),
+                ("band_flip", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 _vp = ctypes.c_void_p
@@ -133,7 +135,7 @@ _SIGS = {
                                          ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, _vp]),
     "vr_assemble_frame_ranks": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
                                                ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, _vp]),
-    "vr_band_rows_packed": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "vr_band_rows_packed": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "vr_row_partition": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_int_p]),
     "vr_row_work": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
     "vr_row_partition_measured": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_int_p,
@@ -230,7 +232,9 @@ _SHARD_SIGS = {
     "vr_shard_set_exchange_streams": (ctypes.c_int, [_vp, ctypes.c_int]),
     "vr_shard_set_compositor": (ctypes.c_int, [_vp, ctypes.c_int]),
     "vr_shard_get_compositor": (ctypes.c_int, [_vp]),
-    "vr_shard_bands": (ctypes.c_int, [_vp, c_int_p, c_int_p]),
+    "vr_shard_bands": (ctypes.c_int, [_vp, c_int_p, c_int_p, c_int_p]),
+    "vr_shard_set_serpentine": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "vr_shard_get_serpentine": (ctypes.c_int, [_vp]),
     "vr_shard_set_rows": (ctypes.c_int, [_vp, c_int_p]),
     "vr_shard_balance_rows": (ctypes.c_int, [_vp]),
     "vr_shard_rebalance_rows": (ctypes.c_int, [_vp, ctypes.c_double]),
@@ -240,7 +244,8 @@ _SHARD_SIGS = {
 }
 # shard functions whose int return is a value, not a vr_status
 _SHARD_VALUE_RETURNS = {"vr_shard_aborted", "vr_shard_poll_selftest", "vr_shard_get_render_streams",
-                        "vr_shard_get_compositor", "vr_shard_partition", "vr_shard_get_lead_rows"}
+                        "vr_shard_get_compositor", "vr_shard_partition", "vr_shard_get_lead_rows",
+                        "vr_shard_get_serpentine"}
 _shard_lib = None
 
 

@@ -200,13 +200,19 @@ bool clamp_is_exact(const Ctx* c, const float S[4][3], const float T[4][3])
     return true;
 }
 
-int band_rows_packed(int height, int band_rows, int band_stride, int band_first)
+int band_rows_packed(int height, int band_rows, int band_stride, int band_first, int band_flip)
 {
     if (band_rows <= 0) return height;
     if (band_stride <= 0) band_stride = 1;
     const int nb = (height + band_rows - 1) / band_rows;
     if (band_first < 0 || band_first >= nb) return 0;
-    const int nsel = (nb - 1 - band_first) / band_stride + 1;
+    int nsel = (nb - 1 - band_first) / band_stride + 1;
+    // flipped: the set's bands still increase (|flip| < stride); drop a last
+    // odd band the flip pushed past the frame, add one it pulled in
+    if (band_flip != 0) {
+        while (nsel > 0 && set_band(nsel - 1, band_first, band_stride, band_flip) >= nb) --nsel;
+        while (set_band(nsel, band_first, band_stride, band_flip) < nb) ++nsel;
+    }
     return nsel * band_rows;
 }
 
@@ -643,9 +649,10 @@ try {
     return caught_exception("vr_set_march");
 }
 
-int vr_band_rows_packed(int height, int band_rows, int band_stride, int band_first)
+int vr_band_rows_packed(int height, int band_rows, int band_stride, int band_first, int band_flip)
 try {
-    return band_rows_packed(height, band_rows, band_stride, band_first);
+    if (band_flip != 0 && (band_rows <= 0 || band_stride < 2 || std::abs(band_flip) >= band_stride)) return -1;
+    return band_rows_packed(height, band_rows, band_stride, band_first, band_flip);
 } catch (...) {
     (void)caught_exception("vr_band_rows_packed");
     return -1;
@@ -674,6 +681,10 @@ try {
     if (row_range && (t->band_rows <= 0 || t->band_stride != 1 || t->band_first % 8 != 0))
         return fail(VR_ERR_INVALID, "vr_render: bad row range (rows %d, stride %d, first row %d: need rows > 0, "
                     "stride 1, first a multiple of 8)", t->band_rows, t->band_stride, t->band_first);
+    if (t->band_flip != 0 && (row_range || t->band_rows <= 0 || t->band_stride < 2 || std::abs(t->band_flip) >= t->band_stride))
+        return fail(VR_ERR_INVALID, "vr_render: band_flip %d needs a band set with |flip| < stride (%d)", t->band_flip,
+                    t->band_stride);
+    if (t->reserved != 0) return fail(VR_ERR_INVALID, "vr_render: vr_target.reserved must be 0");
 
     if (c->inject_throw) {
         const int k = c->inject_throw;
@@ -776,10 +787,11 @@ try {
         a.band_rows = 8; a.band_stride = 1; a.band_first = t->band_first / 8;
     } else if (t->band_rows > 0) {
         a.band_rows = t->band_rows; a.band_stride = t->band_stride; a.band_first = t->band_first;
+        a.band_flip = t->band_flip;
     } else {
         a.band_rows = t->height; a.band_stride = 1; a.band_first = 0;
     }
-    a.out_rows = band_rows_packed(t->height, a.band_rows, a.band_stride, a.band_first);
+    a.out_rows = band_rows_packed(t->height, a.band_rows, a.band_stride, a.band_first, a.band_flip);
     if (row_range) a.out_rows = std::min(a.out_rows, t->band_rows);
     a.tiles_x = (t->width + 15) / 16;
     a.tiles_y = (a.out_rows + 15) / 16;
@@ -1008,6 +1020,8 @@ try {
     if (first_rank == nranks) return VR_OK;   // every rank's rows are in place
     if (nranks > 0 && rows_per_rank > (size_t)(INT_MAX / nranks))   // the kernels index rows in 32 bits
         return fail(VR_ERR_INVALID, "vr_assemble_frame: rows_per_rank %zu x %d ranks", rows_per_rank, nranks);
+    const bool serp = (frame_format & VR_ASSEMBLE_SERPENTINE) != 0;
+    frame_format &= ~VR_ASSEMBLE_SERPENTINE;
     if (gathered_format < 0 || gathered_format > 5 || frame_format < 0 || frame_format > 5)
         return fail(VR_ERR_INVALID, "vr_assemble_frame: bad format %d -> %d", gathered_format, frame_format);
     if (gathered_format != frame_format && grey_of(frame_format) != gathered_format)
@@ -1018,25 +1032,25 @@ try {
         if (nranks <= 0 || width <= 0 || height <= 0 || band_rows <= 0)
             return fail(VR_ERR_INVALID, "vr_assemble_frame: bad geometry");
         for (int r = first_rank; r < nranks; ++r)
-            if ((size_t)band_rows_packed(height, band_rows, nranks, r) > rows_per_rank)
+            if ((size_t)band_rows_packed(height, band_rows, nranks, r, serp ? nranks - 1 - 2 * r : 0) > rows_per_rank)
                 return fail(VR_ERR_INVALID, "vr_assemble_frame: rows_per_rank %zu too small for rank %d", rows_per_rank, r);
         Ctx* c = as_ctx(p);
         HIP_TRY(hipSetDevice(c->device));
         HIP_TRY(launch_assemble(static_cast<const uint8_t*>(d_gathered), rows_per_rank, nranks, width, height,
                                 band_rows, bpp, first_rank, static_cast<uint8_t*>(d_frame),
-                                static_cast<hipStream_t>(stream)));
+                                static_cast<hipStream_t>(stream), serp));
         return VR_OK;
     }
     if (nranks <= 0 || width <= 0 || height <= 0 || band_rows <= 0)
         return fail(VR_ERR_INVALID, "vr_assemble_frame: bad geometry");
     for (int r = first_rank; r < nranks; ++r)
-        if ((size_t)band_rows_packed(height, band_rows, nranks, r) > rows_per_rank)
+        if ((size_t)band_rows_packed(height, band_rows, nranks, r, serp ? nranks - 1 - 2 * r : 0) > rows_per_rank)
             return fail(VR_ERR_INVALID, "vr_assemble_frame: rows_per_rank %zu too small for rank %d", rows_per_rank, r);
     Ctx* c = as_ctx(p);
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(launch_assemble_grey(static_cast<const uint8_t*>(d_gathered), rows_per_rank, nranks, width, height,
                                  band_rows, frame_format == VR_FMT_RGBA32F, first_rank, static_cast<uint8_t*>(d_frame),
-                                 static_cast<hipStream_t>(stream)));
+                                 static_cast<hipStream_t>(stream), serp));
     return VR_OK;
 } catch (...) {
     return caught_exception("vr_assemble_frame_ranks");

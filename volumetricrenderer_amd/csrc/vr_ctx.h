@@ -60,7 +60,7 @@ constexpr int kMaxRegionStreams = 4;
 constexpr int kMaxDeferMiB = 4 << 10;
 // retired deferred scratch buffers kept before a device sync frees them
 constexpr size_t kMaxDeferRetired = 4;
-constexpr int kRegionKeyLen = 39;
+constexpr int kRegionKeyLen = 40;
 // auto split (lanes per ray) from the frame share's tiles with work: K = 1 at
 // >= 6000, 2 at >= 1400, else 4.  Measured on 1/N of the 1080p frame at 512^3
 // (~7,500 tiles with work): K = 1, 2, 2, 4 at N = 1, 2, 4, 8.
@@ -276,7 +276,7 @@ vr_status install_volume(Ctx* c, const uint8_t* d_rgba, int nx, int ny, int nz, 
 vr_status resolve_uniform(Ctx* c);
 void tap_constants(const Ctx* c, float S[4][3], float T[4][3]);
 bool clamp_is_exact(const Ctx* c, const float S[4][3], const float T[4][3]);
-int band_rows_packed(int height, int band_rows, int band_stride, int band_first);
+int band_rows_packed(int height, int band_rows, int band_stride, int band_first, int band_flip = 0);
 vr_status make_plan(Ctx* c, MarchArgs* a, Plan* p);
 const char* variant_name(const Plan& p);
 

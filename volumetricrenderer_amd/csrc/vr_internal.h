@@ -204,6 +204,7 @@ struct MarchArgs {
     LayoutGeom geom;             // fast layouts
     // target
     int width, height, band_rows, band_stride, band_first, out_rows;
+    int band_flip;               // vr_target.band_flip: odd bands of the set shifted (set_band)
     int tiles_x, tiles_y, num_blocks;   // static schedule: 16x16 tiles
     void* out;
     long long pitch;
@@ -215,6 +216,13 @@ struct MarchArgs {
     ProcParams proc;
     int slab_cap;                // LDS slab march (COL48): chunks per channel the slab holds
 };
+
+// The frame band of a band set's k-th band (vr_target): band_first + k *
+// band_stride, every odd one shifted by band_flip (the serpentine deal)
+__host__ __device__ inline int set_band(int k, int first, int stride, int flip)
+{
+    return first + k * stride + ((k & 1) ? flip : 0);
+}
 
 // How the march kernel maps tiles to waves.
 enum ScheduleKind : int {
@@ -242,7 +250,7 @@ constexpr int kRegionHeader = 24;
 constexpr int kRegionWork = 16;
 struct RegionBuild {
     int tw, th, width, out_rows, band_rows, band_stride, band_first, max_steps;
-    int height;
+    int height, band_flip;
     float step_size;
     float org[3], o[3], px[3], py[3], box_min[3], box_max[3];
     float r3[4];           // row 3 of P*V*M (clip w), for tile_is_empty
@@ -264,7 +272,7 @@ struct RegionBuild {
 __host__ __device__ inline bool tile_is_empty(const float org[3], const float o[3], const float px[3], const float py[3],
                                               const float bmin[3], const float bmax[3], const float r3[4], int width,
                                               int out_rows, int height, int band_rows, int band_stride, int band_first,
-                                              int tx, int ty)
+                                              int band_flip, int tx, int ty)
 {
     if (band_rows > 0 && band_rows % 8 != 0) return false;
     const int x0 = tx * 8, x1 = x0 + 8 < width ? x0 + 8 : width;
@@ -273,7 +281,7 @@ __host__ __device__ inline bool tile_is_empty(const float org[3], const float o[
     int y0 = r0;
     if (band_rows > 0) {
         const int bl = r0 / band_rows;
-        y0 = (band_first + bl * band_stride) * band_rows + (r0 - bl * band_rows);
+        y0 = set_band(bl, band_first, band_stride, band_flip) * band_rows + (r0 - bl * band_rows);
     }
     if (y0 >= height) return true;   // rows past the frame: never stored
     double c[8][3];
@@ -378,7 +386,8 @@ __host__ __device__ constexpr int format_bytes(int f) { return f == 0 ? 16 : f <
 __host__ __device__ constexpr int grey_of(int f) { return f == 0 ? 5 : f == 1 ? 3 : f == 2 ? 4 : -1; }
 // grey band sets (1 B or fp32 per pixel) -> RGBA frame rows (vr_assemble_frame)
 hipError_t launch_assemble_grey(const uint8_t* d_gathered, size_t rows_per_rank, int nranks, int width, int height,
-                                int band_rows, bool f32, int first_rank, uint8_t* d_frame, hipStream_t s);
+                                int band_rows, bool f32, int first_rank, uint8_t* d_frame, hipStream_t s,
+                                bool serp = false);
 hipError_t launch_march_corner8(const MarchArgs& a, int layout, bool early, const Schedule& sc,
                                 hipStream_t s);   // CORNER8 / CORNERH, vr_march_c8.hip
 hipError_t launch_march_slab(const MarchArgs& a, bool early, const Schedule& sc, hipStream_t s);   // vr_march_slab.hip
@@ -419,7 +428,7 @@ hipError_t launch_pack_recipe(const float* d_g1, const float* d_g2, const float*
                               uint8_t* d_rgba, hipStream_t s);
 hipError_t launch_assemble(const uint8_t* d_gathered, size_t rows_per_rank, int nranks,
                            int width, int height, int band_rows, int bpp, int first_rank, uint8_t* d_frame,
-                           hipStream_t s);
+                           hipStream_t s, bool serp = false);   // serp: vr.h VR_ASSEMBLE_SERPENTINE
 int noise_partials_needed(int nx, int ny, int nz);
 // 16-B-per-lane grid-stride copy of `bytes` (a multiple of 16): the measured HBM roofline
 hipError_t launch_stream_copy(const void* src, void* dst, size_t bytes, hipStream_t s);

@@ -295,7 +295,7 @@ __device__ __forceinline__ Ray setup_ray(const MarchArgs& a, int x, int orow)
     int y = 0;
     if (inside) {
         const int bl = orow / a.band_rows;
-        y = (a.band_first + bl * a.band_stride) * a.band_rows + (orow - bl * a.band_rows);
+        y = set_band(bl, a.band_first, a.band_stride, a.band_flip) * a.band_rows + (orow - bl * a.band_rows);
     }
     r.live = inside && y < a.height;
     if (!r.live) return r;
@@ -354,7 +354,7 @@ __device__ __forceinline__ void store_pixel(const MarchArgs& a, int x, int orow,
     int trow = orow;
     if (a.bands_in_place) {   // the band's frame row (vr.h VR_TARGET_BANDS_IN_PLACE)
         const int bl = orow / a.band_rows;
-        trow = (a.band_first + bl * a.band_stride) * a.band_rows + (orow - bl * a.band_rows);
+        trow = set_band(bl, a.band_first, a.band_stride, a.band_flip) * a.band_rows + (orow - bl * a.band_rows);
     }
     char* row = (char*)a.out + (long long)trow * a.pitch;
     if (a.format == 0 || a.format == 5) {
@@ -1132,7 +1132,7 @@ __device__ __forceinline__ void fill_empty_tiles(const MarchArgs& a, const unsig
         const int x = (int)(t & 0xffffu) * 8 + lx, orow = (int)(t >> 16) * 8 + ly;
         if (x < a.width && orow < a.out_rows) {
             const int bl = orow / a.band_rows;
-            const int y = (a.band_first + bl * a.band_stride) * a.band_rows + (orow - bl * a.band_rows);
+            const int y = set_band(bl, a.band_first, a.band_stride, a.band_flip) * a.band_rows + (orow - bl * a.band_rows);
             if (y < a.height) store_pixel(a, x, orow, false, 0.0f);
         }
     }
@@ -1495,7 +1495,7 @@ __device__ __forceinline__ void proc_fill_background(const MarchArgs& a, const u
         int x, orow;
         if (!sort_pixel(a, i, &x, &orow) || keys[i] != 0) continue;
         const int bl = orow / a.band_rows;
-        const int y = (a.band_first + bl * a.band_stride) * a.band_rows + (orow - bl * a.band_rows);
+        const int y = set_band(bl, a.band_first, a.band_stride, a.band_flip) * a.band_rows + (orow - bl * a.band_rows);
         if (y < a.height) store_pixel(a, x, orow, false, 0.0f);
     }
 }

@@ -55,7 +55,7 @@ struct RgScratch {
 __device__ double steps_at(const RegionBuild& b, double fx, int orow)
 {
     const int bl = orow / b.band_rows;
-    const double fy = (double)((b.band_first + bl * b.band_stride) * b.band_rows + (orow - bl * b.band_rows));
+    const double fy = (double)(set_band(bl, b.band_first, b.band_stride, b.band_flip) * b.band_rows + (orow - bl * b.band_rows));
     double d[3], len = 0.0;
     for (int k = 0; k < 3; ++k) {
         d[k] = (double)b.o[k] + fx * (double)b.px[k] + fy * (double)b.py[k];
@@ -91,7 +91,7 @@ __global__ __launch_bounds__(256) void rg_tiles(const RegionBuild b, RgScratch s
     const bool work = cost >= 1.0;
     // tiles no ray of which meets the box go last (filled, not marched)
     const bool empty = !work && tile_is_empty(b.org, b.o, b.px, b.py, b.box_min, b.box_max, b.r3, b.width, b.out_rows,
-                                              b.height, b.band_rows, b.band_stride, b.band_first, tx, ty);
+                                              b.height, b.band_rows, b.band_stride, b.band_first, b.band_flip, tx, ty);
     if (work) {
         atomicAdd(&s.bin_cost[abin], (unsigned long long)(cost * kCostScale));
         atomicAdd(&s.counts[8], 1u);

@@ -28,7 +28,7 @@ void box_centre_pixel(const Ctx* c, const MarchArgs& a, int* px, int* prow)
     }
     const int y = (int)std::min(std::max(sy, 0.0), (double)(a.height - 1));
     int row = y;
-    if (a.band_rows > 0 && (a.band_stride > 1 || a.band_first > 0)) {   // the nearest of this rank's packed rows
+    if (a.band_rows > 0 && (a.band_stride > 1 || a.band_first > 0)) {   // near this rank's packed rows (flips aside)
         const int b = y / a.band_rows;
         const int sel = b >= a.band_first ? (b - a.band_first) / a.band_stride : 0;
         row = sel * a.band_rows + y % a.band_rows;
@@ -188,8 +188,9 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     const int tw = (a.width + 7) >> 3, th = (a.out_rows + 7) >> 3;
     float key[kRegionKeyLen] = {(float)tw, (float)th, (float)a.width, (float)a.height, (float)a.out_rows,
                                 (float)a.band_rows, (float)a.band_stride, (float)a.band_first, (float)tpw,
-                                (float)wedges_of(c), (float)(65536 * c->region_order), (float)c->split, (float)c->supertile};
-    constexpr int grid_part = 13;   // the part a reused list must match
+                                (float)wedges_of(c), (float)(65536 * c->region_order), (float)c->split, (float)c->supertile,
+                                (float)a.band_flip};
+    constexpr int grid_part = 14;   // the part a reused list must match
     int kn = grid_part;
     for (float v : {(float)a.max_steps, a.step_size, (float)cpx, (float)cprow}) key[kn++] = v;
     for (const float* v : {a.org, a.o, a.px, a.py, a.box_min, a.box_max})
@@ -239,7 +240,7 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
         Ctx::RegionBuf& rb = c->region[b];
         RegionBuild g{};
         g.tw = tw; g.th = th; g.width = a.width; g.out_rows = a.out_rows;
-        g.band_rows = a.band_rows; g.band_stride = a.band_stride; g.band_first = a.band_first;
+        g.band_rows = a.band_rows; g.band_stride = a.band_stride; g.band_first = a.band_first; g.band_flip = a.band_flip;
         g.max_steps = a.max_steps; g.step_size = a.step_size;
         for (int k = 0; k < 3; ++k) {
             g.org[k] = a.org[k]; g.o[k] = a.o[k]; g.px[k] = a.px[k]; g.py[k] = a.py[k];
@@ -290,7 +291,7 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
     // a3 step estimate of the ray through pixel-corner (fx, fy) of the packed target
     auto steps_at = [&](double fx, int orow) {
         const int bl = orow / a.band_rows;
-        const double fy = (double)((a.band_first + bl * a.band_stride) * a.band_rows + (orow - bl * a.band_rows));
+        const double fy = (double)(set_band(bl, a.band_first, a.band_stride, a.band_flip) * a.band_rows + (orow - bl * a.band_rows));
         double d[3], len = 0.0;
         for (int k = 0; k < 3; ++k) {
             d[k] = a.o[k] + fx * a.px[k] + fy * a.py[k];
@@ -370,7 +371,8 @@ vr_status build_regions(Ctx* c, const MarchArgs& a, int tpw, int cpx, int cprow,
         std::vector<T> edge;
         for (const T& t : idle)
             (tile_is_empty(a.org, a.o, a.px, a.py, a.box_min, a.box_max, a.r3, a.width, a.out_rows, a.height,
-                           a.band_rows, a.band_stride, a.band_first, (int)(t.id & 0xffffu), (int)(t.id >> 16))
+                           a.band_rows, a.band_stride, a.band_first, a.band_flip, (int)(t.id & 0xffffu),
+                           (int)(t.id >> 16))
                  ? empty_tiles : edge).push_back(t);
         for (size_t i = 0; i < edge.size(); ++i) xl[i % 8].push_back(edge[i]);
     }

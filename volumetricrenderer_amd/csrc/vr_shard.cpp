@@ -168,6 +168,10 @@ struct vr_shard {
     // and the renderers' band sets cover the rows below them
     // (vr_shard_set_lead_rows / vr_shard_balance_lead)
     int lead_rows = 0;
+    // serpentine band sets (vr_shard_set_serpentine): renderer k's odd bands
+    // shifted by R - 1 - 2k (vr_target.band_flip), so the deal runs backwards
+    // in every other period of R bands
+    bool serpentine = true;
     // balanced row ranges (vr_shard_set_rows / vr_shard_balance_rows): renderer
     // k renders frame rows [row_begin[k], row_begin[k + 1]) (VR_TARGET_ROW_RANGE)
     // and rank 0 gathers them into a grey frame; empty = interleaved band sets
@@ -362,6 +366,15 @@ bool rows_mode(const vr_shard* sh) { return !sh->row_begin.empty(); }
 int lead_band(const vr_shard* sh) { return sh->lead_rows / sh->band_rows; }
 int set_first_of(const vr_shard* sh, int r) { return band_first_of(sh, r) + lead_band(sh); }
 bool leads(const vr_shard* sh, int r) { return r == 0 && sh->lead_rows > 0; }
+// the k-th band of a set (vr.h vr_target.band_flip)
+int set_band(int k, int first, int stride, int flip) { return first + k * stride + ((k & 1) ? flip : 0); }
+// rank r's band_flip: R - 1 - 2k for renderer k of a serpentine band-set deal
+int flip_of(const vr_shard* sh, int r)
+{
+    const int R = renderers(sh), k = band_first_of(sh, r);
+    if (!sh->serpentine || rows_mode(sh) || leads(sh, r) || k < 0 || R < 2) return 0;
+    return R - 1 - 2 * k;
+}
 // rank 0's gather buffer: a slot of rows_per_rank rows per rank, or (row
 // ranges) a grey frame that every renderer's range lands in at its own rows
 size_t gather_rows(const vr_shard* sh)
@@ -393,6 +406,7 @@ vr_target target_of(const vr_shard* sh, int r)
         t.band_rows = sh->band_rows;
         t.band_stride = renderers(sh);
         t.band_first = set_first_of(sh, r);
+        t.band_flip = flip_of(sh, r);
     }
     return t;
 }
@@ -413,9 +427,10 @@ vr_status assemble(vr_shard* sh, int p, hipStream_t s)
     // assembly expands the frame below them, where renderer k's set is the
     // sub-frame's band set k)
     const int lead = sh->lead_rows;
+    const int serp = sh->serpentine && renderers(sh) > 1 ? VR_ASSEMBLE_SERPENTINE : 0;
     VR_TRY(vr_assemble_frame_ranks(sh->ctx, sh->gathered[p], sh->gformat, (size_t)sh->rows_per_rank, renderers(sh),
-                                   sh->compositor ? 0 : 1, sh->width, sh->height - lead, sh->band_rows, sh->format,
-                                   sh->frame[p] + (size_t)lead * sh->pitch, s));
+                                   sh->compositor ? 0 : 1, sh->width, sh->height - lead, sh->band_rows,
+                                   sh->format | serp, sh->frame[p] + (size_t)lead * sh->pitch, s));
     return VR_OK;
 }
 
@@ -561,13 +576,16 @@ void set_geometry(vr_shard* sh, bool compositor)
         if (!sh->compositor || r > 0) {
             const int k = band_first_of(sh, r);
             sh->rows_of[r] = rows_mode(sh) ? sh->row_begin[k + 1] - sh->row_begin[k]
-                                           : vr_band_rows_packed(sh->height, sh->band_rows, R, set_first_of(sh, r));
+                                           : vr_band_rows_packed(sh->height, sh->band_rows, R, set_first_of(sh, r),
+                                                                 flip_of(sh, r));
         }
+    // a gather slot holds the largest set (ranges: the longest range); rank
+    // 0's lead rows are rendered in place, not gathered
+    sh->rows_per_rank = 0;
+    for (int r = 0; r < sh->nranks; ++r)
+        if (!leads(sh, r)) sh->rows_per_rank = std::max(sh->rows_per_rank, sh->rows_of[r]);
     if (leads(sh, 0)) sh->rows_of[0] = sh->lead_rows;
     sh->my_rows = sh->rows_of[sh->rank];
-    // band 0 is the first renderer's: it has the most rows (ranges: the longest)
-    sh->rows_per_rank = rows_mode(sh) ? *std::max_element(sh->rows_of.begin(), sh->rows_of.end())
-                                      : vr_band_rows_packed(sh->height, sh->band_rows, R, lead_band(sh));
 }
 
 // rank 0's gather slots / another rank's band sets, for the current geometry
@@ -1221,14 +1239,34 @@ try {
     return -1;
 }
 
-vr_status vr_shard_bands(vr_shard* sh, int* band_stride, int* band_first)
+vr_status vr_shard_bands(vr_shard* sh, int* band_stride, int* band_first, int* band_flip)
 try {
     if (!sh) return fail(VR_ERR_INVALID, "vr_shard_bands: null");
     if (band_stride) *band_stride = renderers(sh);
     if (band_first) *band_first = leads(sh, sh->rank) ? -1 : set_first_of(sh, sh->rank);
+    if (band_flip) *band_flip = flip_of(sh, sh->rank);
     return VR_OK;
 } catch (...) {
     return caught_exception("vr_shard_bands");
+}
+
+vr_status vr_shard_set_serpentine(vr_shard* sh, int on)
+try {
+    if (!sh || on < 0 || on > 1) return fail(VR_ERR_INVALID, "vr_shard_set_serpentine: bad argument");
+    if ((on == 1) == sh->serpentine) return VR_OK;
+    if (sh->started) return fail(VR_ERR_INVALID, "vr_shard_set_serpentine: set before the first frames");
+    sh->serpentine = on == 1;
+    set_geometry(sh, sh->compositor);
+    return alloc_band_buffers(sh);
+} catch (...) {
+    return caught_exception("vr_shard_set_serpentine");
+}
+
+int vr_shard_get_serpentine(vr_shard* sh)
+try {
+    return sh ? (sh->serpentine ? 1 : 0) : -1;
+} catch (...) {
+    return -1;
 }
 
 vr_status vr_shard_set_rows(vr_shard* sh, const int* row_begin)
@@ -1449,9 +1487,11 @@ try {
                 double cost = 0.0;
                 for (int b = 0; b < lb; ++b) cost += band[(size_t)b];
                 cost /= pct / 100.0;
-                for (int k = 0; k < R; ++k) {
+                for (int k = 0; k < R; ++k) {   // renderer k's set below the lead (flip_of)
+                    const int fl = sh->serpentine && R > 1 ? R - 1 - 2 * k : 0;
                     double ck = 0.0;
-                    for (int b = lb + k; b < nb; b += R) ck += band[(size_t)b];
+                    for (int j = 0, b = lb + k; b < nb; b = lb + set_band(++j, k, R, fl))
+                        ck += band[(size_t)b];
                     cost = std::max(cost, ck);
                 }
                 if (cost < best) {

@@ -308,15 +308,16 @@ __global__ __launch_bounds__(kBlock) void k_pack_recipe(const float* __restrict_
 //
 // Row q (from rank first_rank's slot on) of the gathered band sets -> its
 // frame row y: rank r's slot holds its bands lb = 0, 1, ... packed, and band
-// lb of rank r is frame band lb * nranks + r.  -1 for slot rows past the
+// lb of rank r is frame band lb * nranks + r -- or, serpentine (vr_target
+// band_flip nranks - 1 - 2r), lb * nranks + nranks - 1 - r for odd lb.  -1 for slot rows past the
 // frame (a rank with fewer rows than the slot).  Block-uniform: the divisions
 // are scalar, once per row.
 __device__ __forceinline__ int assembled_row(int q, int rows_per_rank, int nranks, int band_rows, int first_rank,
-                                             int height)
+                                             int serp, int height)
 {
     const int r = first_rank + q / rows_per_rank, lr = q % rows_per_rank;
     const int lb = lr / band_rows, rr = lr - lb * band_rows;
-    const int y = (lb * nranks + r) * band_rows + rr;
+    const int y = (lb * nranks + ((serp && (lb & 1)) ? nranks - 1 - r : r)) * band_rows + rr;
     return y < height ? y : -1;
 }
 
@@ -327,7 +328,8 @@ __device__ __forceinline__ int assembled_row(int q, int rows_per_rank, int nrank
 constexpr int kAsmBatch = 8;
 template <typename S, typename D, typename F>
 __device__ __forceinline__ void assemble_rows(const S* __restrict__ src, int rows_per_rank, int nranks, int row_elems,
-                                              int height, int band_rows, int first_rank, D* __restrict__ dst, F expand)
+                                              int height, int band_rows, int first_rank, int serp, D* __restrict__ dst,
+                                              F expand)
 {
     const int rows = (nranks - first_rank) * rows_per_rank;
     const int e = blockIdx.x * kBlock + threadIdx.x;
@@ -339,7 +341,7 @@ __device__ __forceinline__ void assemble_rows(const S* __restrict__ src, int row
 #pragma unroll
         for (int j = 0; j < kAsmBatch; ++j) {
             const int q = q0 + j * (int)gridDim.y;
-            y[j] = q < rows ? assembled_row(q, rows_per_rank, nranks, band_rows, first_rank, height) : -1;
+            y[j] = q < rows ? assembled_row(q, rows_per_rank, nranks, band_rows, first_rank, serp, height) : -1;
             if (y[j] >= 0) v[j] = src[(base + q) * row_elems + e];
         }
 #pragma unroll
@@ -351,9 +353,10 @@ __device__ __forceinline__ void assemble_rows(const S* __restrict__ src, int row
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_assemble(const T* __restrict__ src, int rows_per_rank, int nranks,
                                                      int row_elems, int height, int band_rows, int first_rank,
-                                                     T* __restrict__ dst)
+                                                     int serp, T* __restrict__ dst)
 {
-    assemble_rows(src, rows_per_rank, nranks, row_elems, height, band_rows, first_rank, dst, [](T v) { return v; });
+    assemble_rows(src, rows_per_rank, nranks, row_elems, height, band_rows, first_rank, serp, dst,
+                  [](T v) { return v; });
 }
 
 // Grey band sets -> RGBA frame (vr_assemble_frame): element e of frame row y
@@ -389,9 +392,9 @@ __device__ __forceinline__ float4 grey_expand<float, float4>(float v)
 template <typename S, typename D>
 __global__ __launch_bounds__(kBlock) void k_assemble_grey(const S* __restrict__ src, int rows_per_rank,
                                                           int nranks, int row_elems, int height, int band_rows,
-                                                          int first_rank, D* __restrict__ dst)
+                                                          int first_rank, int serp, D* __restrict__ dst)
 {
-    assemble_rows(src, rows_per_rank, nranks, row_elems, height, band_rows, first_rank, dst,
+    assemble_rows(src, rows_per_rank, nranks, row_elems, height, band_rows, first_rank, serp, dst,
                   [](S v) { return grey_expand<S, D>(v); });
 }
 
@@ -698,44 +701,44 @@ hipError_t launch_stream_copy(const void* src, void* dst, size_t bytes, hipStrea
 }
 
 hipError_t launch_assemble(const uint8_t* d_gathered, size_t rows_per_rank, int nranks, int width, int height,
-                           int band_rows, int bpp, int first_rank, uint8_t* d_frame, hipStream_t s)
+                           int band_rows, int bpp, int first_rank, uint8_t* d_frame, hipStream_t s, bool serp)
 {
     const long long row_bytes = (long long)width * bpp;
     if (row_bytes % 16 == 0) {
         const int elems = (int)(row_bytes / 16);
         hipLaunchKernelGGL(k_assemble<uint4>, grid_rows(rows_per_rank, nranks, first_rank, elems), dim3(kBlock), 0, s,
                            reinterpret_cast<const uint4*>(d_gathered), (int)rows_per_rank, nranks, elems,
-                           height, band_rows, first_rank, reinterpret_cast<uint4*>(d_frame));
+                           height, band_rows, first_rank, (int)serp, reinterpret_cast<uint4*>(d_frame));
     } else if (row_bytes % 4 == 0) {
         const int elems = (int)(row_bytes / 4);
         hipLaunchKernelGGL(k_assemble<unsigned int>, grid_rows(rows_per_rank, nranks, first_rank, elems), dim3(kBlock), 0,
                            s, reinterpret_cast<const unsigned int*>(d_gathered), (int)rows_per_rank, nranks,
-                           elems, height, band_rows, first_rank, reinterpret_cast<unsigned int*>(d_frame));
+                           elems, height, band_rows, first_rank, (int)serp, reinterpret_cast<unsigned int*>(d_frame));
     } else {   // 1-byte pixels, rows of any width
         const int elems = (int)row_bytes;
         hipLaunchKernelGGL(k_assemble<unsigned char>, grid_rows(rows_per_rank, nranks, first_rank, elems), dim3(kBlock), 0,
-                           s, d_gathered, (int)rows_per_rank, nranks, elems, height, band_rows, first_rank,
+                           s, d_gathered, (int)rows_per_rank, nranks, elems, height, band_rows, first_rank, (int)serp,
                            d_frame);
     }
     return hipGetLastError();
 }
 
 hipError_t launch_assemble_grey(const uint8_t* d_gathered, size_t rows_per_rank, int nranks, int width, int height,
-                                int band_rows, bool f32, int first_rank, uint8_t* d_frame, hipStream_t s)
+                                int band_rows, bool f32, int first_rank, uint8_t* d_frame, hipStream_t s, bool serp)
 {
     const dim3 blk(kBlock);
     if (f32) {
         hipLaunchKernelGGL((k_assemble_grey<float, float4>), grid_rows(rows_per_rank, nranks, first_rank, width), blk, 0, s,
                            reinterpret_cast<const float*>(d_gathered), (int)rows_per_rank, nranks, width, height,
-                           band_rows, first_rank, reinterpret_cast<float4*>(d_frame));
+                           band_rows, first_rank, (int)serp, reinterpret_cast<float4*>(d_frame));
     } else if (width % 4 == 0) {
         const int elems = width / 4;
         hipLaunchKernelGGL((k_assemble_grey<unsigned int, uint4>), grid_rows(rows_per_rank, nranks, first_rank, elems), blk, 0,
                            s, reinterpret_cast<const unsigned int*>(d_gathered), (int)rows_per_rank, nranks,
-                           elems, height, band_rows, first_rank, reinterpret_cast<uint4*>(d_frame));
+                           elems, height, band_rows, first_rank, (int)serp, reinterpret_cast<uint4*>(d_frame));
     } else {
         hipLaunchKernelGGL((k_assemble_grey<unsigned char, unsigned int>), grid_rows(rows_per_rank, nranks, first_rank, width),
-                           blk, 0, s, d_gathered, (int)rows_per_rank, nranks, width, height, band_rows, first_rank,
+                           blk, 0, s, d_gathered, (int)rows_per_rank, nranks, width, height, band_rows, first_rank, (int)serp,
                            reinterpret_cast<unsigned int*>(d_frame));
     }
     return hipGetLastError();

@@ -294,7 +294,8 @@ class RcclBandPipeline:
                  rank: int = 0, group=None, loopback: bool = False, timeout_s: float | None = None,
                  render_streams: int | None = None, solo: bool = False, host_threads: int = 1, exchange_on_render: bool = True,
                  compositor: bool | None = None, partition: str = "auto", rows: list[int] | None = None,
-                 lead_pct: int | str | None = "auto", lead_rows: int | None = None):
+                 lead_pct: int | str | None = "auto", lead_rows: int | None = None,
+                 serpentine: bool | None = None):
         """loopback: one process renders all `world` ranks' band sets on its
         GPU and assembles them (no communicator; tests and rehearsals).
         solo (loopback only, any rank): each frame renders only this rank's
@@ -329,6 +330,9 @@ class RcclBandPipeline:
         lead_pct AUTO_LEAD_PCT whenever rank 0 is a compositor over band sets
         (config 5 at 8 ranks: slowest rank 0.0191-0.0197 ms per frame against
         0.0203-0.0204 without), else none; None: none.
+        serpentine: band sets dealt forwards and backwards in turn (vr.h
+        vr_target.band_flip; vr_shard_set_serpentine; None = the library's
+        default, on; every rank the same).
         exchange_on_render: True (default) = each frame's exchange follows its
         render on the frame's render stream, over a communicator per buffer
         parity, with no events; False = on a communication stream, ordered by
@@ -394,6 +398,8 @@ class RcclBandPipeline:
             _lib.shard_call("vr_shard_set_exchange_streams", h, 1 if exchange_on_render else 0)
             if compositor is not None:
                 _lib.shard_call("vr_shard_set_compositor", h, 1 if compositor else 0)
+            if serpentine is not None:
+                _lib.shard_call("vr_shard_set_serpentine", h, 1 if serpentine else 0)
             if solo:
                 _lib.shard_call("vr_shard_set_solo", h, 1)
         except _lib.VRError:
@@ -418,7 +424,7 @@ class RcclBandPipeline:
             # vr_shard_set_rows reads renderers + 1 ints: the
             # renderer count is the band stride of the current geometry
             stride, first = ctypes.c_int(), ctypes.c_int()
-            _lib.shard_call("vr_shard_bands", h, ctypes.byref(stride), ctypes.byref(first))
+            _lib.shard_call("vr_shard_bands", h, ctypes.byref(stride), ctypes.byref(first), None)
             if len(rows) != stride.value + 1:
                 _lib.shard_call("vr_shard_destroy", h)
                 raise ValueError(f"RcclBandPipeline: rows needs {stride.value + 1} entries (renderers + 1), "
@@ -448,9 +454,11 @@ class RcclBandPipeline:
         mine, per = ctypes.c_int(), ctypes.c_int()
         _lib.shard_call("vr_shard_rows", h, ctypes.byref(mine), ctypes.byref(per))
         self.my_rows, self.rows_per_rank = mine.value, per.value
-        stride, first = ctypes.c_int(), ctypes.c_int()
-        _lib.shard_call("vr_shard_bands", h, ctypes.byref(stride), ctypes.byref(first))
-        self.band_stride, self.band_first = stride.value, first.value   # this rank's band set (vr_render target)
+        stride, first, flip = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _lib.shard_call("vr_shard_bands", h, ctypes.byref(stride), ctypes.byref(first), ctypes.byref(flip))
+        # this rank's band set (vr_render target)
+        self.band_stride, self.band_first, self.band_flip = stride.value, first.value, flip.value
+        self.serpentine = bool(_lib.shard_call("vr_shard_get_serpentine", h))
         self.compositor = bool(_lib.shard_call("vr_shard_get_compositor", h))
         self.lead_rows = _lib.shard_call("vr_shard_get_lead_rows", h)   # rank 0's lead rows (0: none)
         self.row_range = None   # (first frame row, rows) of this rank with row ranges

@@ -100,8 +100,14 @@ def reference_shader_data(aspect: float = 1280.0 / 720.0, phi_deg: float = 0.0, 
     return osd, gsd
 
 
-def band_rows_packed(height: int, band_rows: int, band_stride: int = 1, band_first: int = 0) -> int:
-    return _lib.load().vr_band_rows_packed(height, band_rows, band_stride, band_first)
+def band_rows_packed(height: int, band_rows: int, band_stride: int = 1, band_first: int = 0,
+                     band_flip: int = 0) -> int:
+    """Rows vr_render writes for a band set (vr_band_rows_packed); band_flip
+    shifts the set's odd bands (vr.h vr_target.band_flip)."""
+    n = _lib.load().vr_band_rows_packed(height, band_rows, band_stride, band_first, band_flip)
+    if n < 0:
+        raise ValueError(f"bad band set: rows {band_rows}, stride {band_stride}, flip {band_flip}")
+    return n
 
 
 def shader_data_arrays(osd: ObjectShaderData, gsd: GlobalShaderData):
@@ -240,9 +246,9 @@ class Renderer:
 
     # -- the hot path ------------------------------------------------------
     def alloc_target(self, width: int, height: int, fmt: int = FMT_RGBA8_UNORM, band_rows: int = 0,
-                     band_stride: int = 1, band_first: int = 0) -> torch.Tensor:
+                     band_stride: int = 1, band_first: int = 0, band_flip: int = 0) -> torch.Tensor:
         """(rows, width, 4) for the RGBA formats, (rows, width) for the grey ones."""
-        rows = band_rows_packed(height, band_rows, band_stride, band_first)
+        rows = band_rows_packed(height, band_rows, band_stride, band_first, band_flip)
         dev = torch.device("cuda", self.device)
         if fmt not in BYTES_PER_PIXEL:
             raise ValueError(f"unknown format {fmt}")
@@ -250,7 +256,8 @@ class Renderer:
         return torch.empty(shape, dtype=torch.float32 if fmt in FLOAT_FORMATS else torch.uint8, device=dev)
 
     def _check_target(self, width: int, height: int, fmt: int, out: torch.Tensor, band_rows: int,
-                      band_stride: int, band_first: int, step_counter: torch.Tensor | None = None) -> None:
+                      band_stride: int, band_first: int, step_counter: torch.Tensor | None = None,
+                      band_flip: int = 0) -> None:
         """The kernel writes band_rows_packed(...) rows of `width` pixels of
         BYTES_PER_PIXEL[fmt] bytes through a raw pointer: refuse any tensor it
         would write past, or that lives on another device."""
@@ -261,7 +268,7 @@ class Renderer:
         want_dtype = torch.float32 if fmt in FLOAT_FORMATS else torch.uint8
         if out.dtype != want_dtype:
             raise ValueError(f"format {fmt} needs a {want_dtype} target, got {out.dtype}")
-        rows = band_rows_packed(height, band_rows, band_stride, band_first)
+        rows = band_rows_packed(height, band_rows, band_stride, band_first, band_flip)
         if CHANNELS[fmt] == 4:
             if out.dim() != 3 or out.shape[0] < rows or out.shape[1] != width or out.shape[2] != 4:
                 raise ValueError(f"render target must be shaped ({rows}, {width}, 4) (at least {rows} rows), "
@@ -281,14 +288,16 @@ class Renderer:
 
     def render(self, width: int, height: int, fmt: int = FMT_RGBA8_UNORM, out: torch.Tensor | None = None,
                band_rows: int = 0, band_stride: int = 1, band_first: int = 0, stream=None,
-               step_counter: torch.Tensor | None = None) -> torch.Tensor:
-        """Launch the march kernel (asynchronous on `stream`); returns `out`."""
+               step_counter: torch.Tensor | None = None, band_flip: int = 0) -> torch.Tensor:
+        """Launch the march kernel (asynchronous on `stream`); returns `out`.
+        band_flip: the set's odd bands shifted (vr.h vr_target.band_flip)."""
         if out is None:
-            out = self.alloc_target(width, height, fmt, band_rows, band_stride, band_first)
-        self._check_target(width, height, fmt, out, band_rows, band_stride, band_first, step_counter)
+            out = self.alloc_target(width, height, fmt, band_rows, band_stride, band_first, band_flip)
+        self._check_target(width, height, fmt, out, band_rows, band_stride, band_first, step_counter, band_flip)
         t = Target(width=width, height=height, format=fmt, band_rows=band_rows, band_stride=band_stride,
                    band_first=band_first, pixels=out.data_ptr(), row_pitch=out.stride(0) * out.element_size(),
-                   step_counter=step_counter.data_ptr() if step_counter is not None else None)
+                   step_counter=step_counter.data_ptr() if step_counter is not None else None,
+                   band_flip=band_flip)
         call("vr_render", self._ctx, ctypes.byref(t), _stream_handle(stream))
         return out
 
@@ -402,16 +411,20 @@ class Renderer:
             raise ValueError(f"frame must be a {fdtype} tensor shaped {fshape}")
 
     def assemble_frame(self, gathered: torch.Tensor, gathered_fmt: int, nranks: int, width: int, height: int,
-                       band_rows: int, frame_fmt: int, frame: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+                       band_rows: int, frame_fmt: int, frame: torch.Tensor | None = None, stream=None,
+                       serpentine: bool = False) -> torch.Tensor:
         """vr_assemble_frame: [rank][packed rows] band sets in `gathered_fmt`
-        (e.g. grey) scattered and expanded into a `frame_fmt` frame."""
+        (e.g. grey) scattered and expanded into a `frame_fmt` frame.
+        serpentine: rank r rendered with band_flip nranks-1-2r
+        (VR_ASSEMBLE_SERPENTINE)."""
         if frame is None:
             shape = (height, width, 4) if CHANNELS[frame_fmt] == 4 else (height, width)
             frame = torch.empty(shape, dtype=torch.float32 if frame_fmt in FLOAT_FORMATS else torch.uint8,
                                 device=gathered.device)
         self._check_assemble_frame(gathered, gathered_fmt, nranks, width, height, frame, frame_fmt)
         call("vr_assemble_frame", self._ctx, ctypes.c_void_p(gathered.data_ptr()), gathered_fmt, gathered.shape[1],
-             nranks, width, height, band_rows, frame_fmt, ctypes.c_void_p(frame.data_ptr()), _stream_handle(stream))
+             nranks, width, height, band_rows, frame_fmt | (_lib.ASSEMBLE_SERPENTINE if serpentine else 0),
+             ctypes.c_void_p(frame.data_ptr()), _stream_handle(stream))
         return frame
 
     def prepare_assemble_frame(self, gathered: torch.Tensor, gathered_fmt: int, nranks: int, width: int, height: int,
