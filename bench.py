@@ -756,6 +756,7 @@ def main() -> int:
         compositor = native and pipe is not None and pipe.compositor
         lead = pipe.lead_rows if compositor else 0   # rank 0's lead rows beside its assembly
         rows_part = native and pipe is not None and pipe.partition == "rows"
+        serp = " serpentine" if native and pipe is not None and getattr(pipe, "serpentine", False) else ""
         if compositor:   # rank 0 renders nothing: the per-GPU figure is a renderer's average share
             nr = world - 1
             roofline = roofline_of(r, proc, shadow, variant, frame_steps // nr, frame_evals // nr,
@@ -853,9 +854,9 @@ def main() -> int:
                                            else ", 1 render stream (a procedural medium's frames do not overlap)"
                                            if proc is not None else ", 1 render stream"))
                                        if native and world == 1 else
-                                       ((f"row ranges x{world - 1}" if rows_part else f"bands16x{world - 1}")
+                                       ((f"row ranges x{world - 1}" if rows_part else f"bands16x{world - 1}{serp}")
                                         + ", rank 0 compositing" + (f" + {lead} lead rows" if lead else "") if compositor
-                                        else (f"row ranges x{world}" if rows_part else f"bands16x{world}"))
+                                        else (f"row ranges x{world}" if rows_part else f"bands16x{world}{serp}"))
                                        + (", 2 frames in flight (two streams and targets)"
                                           if args.inflight == 2 or proc_inflight2 else "")
                                        + (f", {rs} render stream{'s' if rs > 1 else ''}"

@@ -276,8 +276,10 @@ class BandSharder:
 
 # rank 0's lead rows beside its assembly when it is a compositor over band
 # sets: it counts as this % of a renderer (vr_shard_balance_lead; DESIGN.md
-# sec. 7.5: 40 chose 288 rows at config 5 / 8 ranks, the measured best)
-AUTO_LEAD_PCT = 40
+# sec. 7.5: with serpentine band sets 60 chooses 304 rows at config 5 / 8
+# ranks, the measured best -- 0.0174-0.0179 ms per frame against 0.0179-0.0184
+# at 40 (288 rows) and 0.0225 at 80 (336 rows))
+AUTO_LEAD_PCT = 60
 
 
 class RcclBandPipeline:
@@ -328,8 +330,9 @@ class RcclBandPipeline:
         (vr_shard_balance_lead, collective), or lead_rows explicit rows (a
         multiple of band_rows; vr_shard_set_lead_rows).  "auto" (default):
         lead_pct AUTO_LEAD_PCT whenever rank 0 is a compositor over band sets
-        (config 5 at 8 ranks: slowest rank 0.0191-0.0197 ms per frame against
-        0.0203-0.0204 without), else none; None: none.
+        (config 5 at 8 ranks, serpentine band sets: slowest rank 0.0174-0.0179
+        ms per frame; 0.0203-0.0204 with no lead rows and the plain deal,
+        DESIGN.md sec. 7.5), else none; None: none.
         serpentine: band sets dealt forwards and backwards in turn (vr.h
         vr_target.band_flip; vr_shard_set_serpentine; None = the library's
         default, on; every rank the same).
