@@ -166,10 +166,11 @@ vr_status vr_shard_set_exchange_streams(vr_shard* sh, int on_render);
  * assembles; ranks 1..N-1 render the interleaved band sets of a world of N-1
  * renderers (rank r: band_stride N-1, band_first r-1).  0 = every rank
  * renders (band_stride N, band_first rank) and rank 0 renders its own bands
- * in place.  Default: 1 from 8 ranks on for frames of at most 2560 x 1440
- * pixels (there the assembly of 7/8 of a frame beside rank 0's render made
- * it the slowest rank; a 4K frame's render outweighs it).  Every rank must
- * choose the same, before its first frames (band buffers are resized).
+ * in place.  Default: 1 from 8 ranks on (the assembly of 7/8 of a frame
+ * beside rank 0's render made it the slowest rank; with lead rows,
+ * vr_shard_balance_lead, a compositor also beats row ranges at 4K).  Every
+ * rank must choose the same, before its first frames (band buffers are
+ * resized).
  * Results are identical. */
 vr_status vr_shard_set_compositor(vr_shard* sh, int on);
 int       vr_shard_get_compositor(vr_shard* sh);

@@ -1482,7 +1482,9 @@ def test_config4_4k_256_bands(r, oracle, config4, fmt):
 def test_config4_8_rank_loopback(r, config4):
     """Config 4 through the native 8-rank frame loop in loopback (every rank's
     interleaved band set rendered on this GPU into its gather slot, then
-    vr_assemble_bands): the assembled frame equals a plain render."""
+    vr_assemble_bands): the assembled frame equals a plain render -- with the
+    defaults (serpentine band sets below rank 0's lead rows) and with row
+    ranges."""
     import os
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -1492,10 +1494,13 @@ def test_config4_8_rank_loopback(r, config4):
     r.set_volume(vol)
     r.set_shader_data(osd, gsd)
     r.set_march(march)
-    for fmt in (1, 0):
-        pl = RcclBandPipeline(r, W, H, fmt, band_rows=16, world=8, rank=0, loopback=True)
+    for fmt, part in ((1, "auto"), (0, "auto"), (1, "rows")):
+        pl = RcclBandPipeline(r, W, H, fmt, band_rows=16, world=8, rank=0, loopback=True, partition=part)
         try:
             pl.run_frames(3)
+            if part == "auto":   # the 8-rank default: serpentine band sets, rank 0 compositing + lead rows
+                assert pl.partition == "bands" and pl.compositor and pl.serpentine and pl.render_streams == 3
+                assert pl.lead_rows > 0 and pl.lead_rows % 16 == 0, pl.lead_rows
             got = pl.frame()
             full = r.render(W, H, fmt)
             torch.cuda.synchronize()

@@ -16,6 +16,8 @@ import argparse
 import os
 import sys
 
+import time
+
 import numpy as np
 import torch
 
@@ -40,7 +42,7 @@ def main():
     ap.add_argument("--streams", default="1,2", help="--native: render streams to compare")
     ap.add_argument("--rounds", type=int, default=3, help="--native: interleaved rounds")
     ap.add_argument("--threads", type=int, default=1, help="--native: host threads of the frame loop (1 or 2)")
-    ap.add_argument("--compositor", default="auto", choices=["auto", "on", "off"],
+    ap.add_argument("--compositor", default="auto", choices=["auto", "on", "off", "on8"],
                     help="--native: rank 0 renders no bands and only assembles (vr_shard_set_compositor; auto: the "
                          "library's default, on from 8 ranks)")
     ap.add_argument("--rows", action="append", default=[],
@@ -58,6 +60,8 @@ def main():
                          "(vr_shard_set_exchange_streams 1 / 0)")
     ap.add_argument("--serpentine", default="auto", choices=["auto", "on", "off"],
                     help="--native: band sets dealt serpentine (vr_shard_set_serpentine; auto = the library default)")
+    ap.add_argument("--clock-warm-ms", type=float, default=150.0,
+                    help="--native: whole frames for this long before the first timing (bench.py --clock-warm-ms)")
     ap.add_argument("--gate-ms", type=float, default=0.0,
                     help="--native: hold the stream with a spin kernel of this many ms while the host queues the "
                          "frames, so the timing is the GPU's alone (not the host's)")
@@ -123,6 +127,15 @@ def native(a):
               "streams, "
               f"variant {r.kernel_variant} serpentine {a.serpentine} {' '.join(a.opt)}", flush=True)
         streams = [int(v) for v in a.streams.split(",")]
+        if a.clock_warm_ms > 0:   # the GPU settles over the first 20-40 ms of load
+            out = r.alloc_target(W, H, vr.FMT_RGBA8_UNORM)
+            t0, k = time.perf_counter(), 0
+            while (time.perf_counter() - t0) * 1e3 < a.clock_warm_ms:
+                for _ in range(8):
+                    r.render(W, H, vr.FMT_RGBA8_UNORM, out=out)
+                torch.cuda.synchronize()
+                k += 8
+            print(f"  clock warm: {k} whole frames, {a.clock_warm_ms:.0f} ms", flush=True)
         base = {}
         for rows in a.rows:
             rl = [int(v) for v in rows.split(",")]
@@ -161,9 +174,11 @@ def one_n(a, r, W, H, n, streams, base, rows):
             p = RcclBandPipeline(r, W, H, vr.FMT_RGBA8_UNORM, band_rows=a.band_rows, world=n, rank=first,
                                  loopback=True, solo=True, render_streams=ns, host_threads=a.threads,
                                  exchange_on_render=a.exchange == "render",
-                                 compositor=None if a.compositor == "auto" else a.compositor == "on",
+                                 compositor=(None if a.compositor == "auto" or n < 2 or (a.compositor == "on8" and n < 8)
+                                             else a.compositor in ("on", "on8")),
                                  partition="rows" if rows else a.partition, rows=rows,
-                                 lead_pct="auto" if a.lead_pct < 0 else (a.lead_pct or None),
+                                 lead_pct=("auto" if a.lead_pct < 0 or n < 2 or (a.compositor == "on8" and n < 8)
+                                           else (a.lead_pct or None)),
                                  serpentine=None if a.serpentine == "auto" else a.serpentine == "on")
             p.run_frames(8)   # region lists, code objects
             p.barrier()

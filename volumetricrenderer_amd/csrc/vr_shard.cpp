@@ -556,14 +556,14 @@ vr_status one_frame_on_render(vr_shard* sh, int p, hipStream_t rs, hipEvent_t t0
 }
 
 // Rank 0 as a compositor by default (vr_shard_set_compositor) from this many
-// ranks on, for frames of at most kCompositorPixels.  Config 5 (1080p) at
-// N = 8: rank 0 rendering its own 1/8 beside the assembly of the other 7/8
-// takes 0.0208 ms per frame against 0.0165 on the other ranks; as a
-// compositor the slowest of 7 renderers takes 0.0198.  Config 4 (4K): the
-// render dominates -- 0.0535 against 0.0565 as a compositor -- so larger
-// frames keep rank 0 rendering (profiles/r05/compositor_ab.txt).
+// ranks on.  Config 5 (1080p) at N = 8: rank 0 rendering its own 1/8 beside
+// the assembly of the other 7/8 takes 0.0208 ms per frame against 0.0165 on
+// the other ranks; as a compositor the slowest of 7 renderers takes 0.0198
+// (profiles/r05/compositor_ab.txt).  Round 6: a compositor that also renders
+// lead rows (vr_shard_balance_lead) beside serpentine band sets beats row
+// ranges at 4K too -- config 4 at N = 8 0.0402-0.0406 against 0.0431-0.0434
+// (profiles/r06/c4_lead/) -- so the default no longer depends on the size.
 constexpr int kCompositorRanks = 8;
-constexpr long long kCompositorPixels = 2560LL * 1440LL;
 
 void set_geometry(vr_shard* sh, bool compositor)
 {
@@ -663,7 +663,7 @@ try {
     sh->pitch = (size_t)width * sh->bpp;
     sh->gformat = format == VR_FMT_RGBA32F ? VR_FMT_R32F : format == VR_FMT_RGBA8_SRGB ? VR_FMT_R8_SRGB : VR_FMT_R8_UNORM;
     sh->gpitch = (size_t)width * (format == VR_FMT_RGBA32F ? 4 : 1);
-    set_geometry(sh, nranks >= kCompositorRanks && (long long)width * height <= kCompositorPixels);
+    set_geometry(sh, nranks >= kCompositorRanks);
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     vr_status st = VR_OK;

@@ -276,10 +276,13 @@ class BandSharder:
 
 # rank 0's lead rows beside its assembly when it is a compositor over band
 # sets: it counts as this % of a renderer (vr_shard_balance_lead; DESIGN.md
-# sec. 7.5: with serpentine band sets 60 chooses 304 rows at config 5 / 8
-# ranks, the measured best -- 0.0174-0.0179 ms per frame against 0.0179-0.0184
-# at 40 (288 rows) and 0.0225 at 80 (336 rows))
+# sec. 7.5).  With serpentine band sets, config 5 (1080p) at 8 ranks: 60
+# chooses 304 rows, the measured best -- 0.0174-0.0179 ms per frame against
+# 0.0179-0.0184 at 40 (288 rows) and 0.0225 at 80 (336 rows).  Config 4 (4K):
+# 80 chooses 688 rows -- 0.0400-0.0406 against 0.0407 at 60, 0.0421 at 40 and
+# 0.0464 at 95 -- so frames past 2560 x 1440 take AUTO_LEAD_PCT_LARGE.
 AUTO_LEAD_PCT = 60
+AUTO_LEAD_PCT_LARGE = 80
 
 
 class RcclBandPipeline:
@@ -317,10 +320,10 @@ class RcclBandPipeline:
         partition: "bands" = interleaved band sets of `band_rows` rows (stride
         = the renderers); "rows" = contiguous row ranges of equal estimated
         work for the camera set at the first run_frames (vr_shard_balance_rows,
-        collective); "auto" (default) = "rows" from 8 ranks on for frames of
-        more than 2560 x 1440 pixels (config 4 at 8 ranks: 0.0480 ms per frame
-        against 0.0562 with 16-row bands; equal or slightly slower at 2 and 4
-        ranks), else "bands".
+        collective); "auto" (default) = "bands".  Row ranges were the 4K
+        default at 8 ranks until serpentine band sets with rank 0's lead rows
+        beat them (config 4: 0.0402-0.0406 ms per frame against 0.0431-0.0434,
+        DESIGN.md sec. 7.5).
         rows: explicit row starts for partition "rows" (renderers + 1 entries,
         vr_shard_set_rows; every rank the same) instead of the balanced split.
         lead_pct / lead_rows (compositor over band sets only): rank 0 also
@@ -329,10 +332,11 @@ class RcclBandPipeline:
         for the camera with rank 0 counted as lead_pct % of a renderer
         (vr_shard_balance_lead, collective), or lead_rows explicit rows (a
         multiple of band_rows; vr_shard_set_lead_rows).  "auto" (default):
-        lead_pct AUTO_LEAD_PCT whenever rank 0 is a compositor over band sets
-        (config 5 at 8 ranks, serpentine band sets: slowest rank 0.0174-0.0179
-        ms per frame; 0.0203-0.0204 with no lead rows and the plain deal,
-        DESIGN.md sec. 7.5), else none; None: none.
+        lead_pct AUTO_LEAD_PCT (AUTO_LEAD_PCT_LARGE past 2560 x 1440 pixels)
+        whenever rank 0 is a compositor over band sets (config 5 at 8 ranks,
+        serpentine band sets: slowest rank 0.0174-0.0179 ms per frame;
+        0.0203-0.0204 with no lead rows and the plain deal; config 4
+        0.0400-0.0406), else none; None: none.
         serpentine: band sets dealt forwards and backwards in turn (vr.h
         vr_target.band_flip; vr_shard_set_serpentine; None = the library's
         default, on; every rank the same).
@@ -417,8 +421,7 @@ class RcclBandPipeline:
         self._h = h
         if partition not in ("auto", "bands", "rows"):
             raise ValueError(f"RcclBandPipeline: partition {partition!r}: 'auto', 'bands' or 'rows'")
-        self.partition = (("rows" if world >= 8 and width * height > 2560 * 1440 else "bands") if partition == "auto"
-                          else partition)
+        self.partition = "bands" if partition == "auto" else partition
         self._balanced = self.partition == "bands"
         if rows is not None:
             if self.partition != "rows":
@@ -436,7 +439,8 @@ class RcclBandPipeline:
             self._balanced = True
         self._lead_pct = None
         if lead_pct == "auto":
-            lead_pct = (AUTO_LEAD_PCT if lead_rows is None and self.partition == "bands"
+            lead_pct = ((AUTO_LEAD_PCT_LARGE if width * height > 2560 * 1440 else AUTO_LEAD_PCT)
+                        if lead_rows is None and self.partition == "bands"
                         and bool(_lib.shard_call("vr_shard_get_compositor", h)) else None)
         if lead_pct is not None or lead_rows is not None:
             if not bool(_lib.shard_call("vr_shard_get_compositor", h)) or self.partition != "bands":
