@@ -1842,7 +1842,13 @@ __global__ __launch_bounds__(kThreads) VR_SHADOW_ATTR void proc_shadow_eval(cons
     unsigned evals = 0, cells = 0;
     for (unsigned c = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6); c < chunks; c += gridDim.x * (kThreads / 64)) {
         const uint4 mc = d.map[c];   // wave-uniform
+#if defined(VR_COUNT_SLOTS) && VR_COUNT_SLOTS == 2
+        if (lane == 0) evals += 64u * (unsigned)S;   // lane-slots of the chunk (timing experiment)
+#endif
         if (lane >= mc.z) continue;
+#if defined(VR_COUNT_SLOTS) && VR_COUNT_SLOTS == 1
+        evals += (unsigned)S;   // slots of the entry (timing experiment)
+#endif
         float4* e = d.ent + mc.x + lane;
         const float4 en = *e;
         float q0 = en.x, q1 = en.y, q2 = en.z, sl = 0.0f;
@@ -1855,7 +1861,9 @@ __global__ __launch_bounds__(kThreads) VR_SHADOW_ATTR void proc_shadow_eval(cons
                 // waves per SIMD) and it ran 0.4 % slower (profiles/r05)
                 const DensityK dk = density_k<TABLE>(p, a.scale);
                 sl = sl + proc_density<TABLE, WC, (VR_SHADOW_PHASED != 0)>(p, dk, wt, q0, q1, q2, cells, &wc);
+#ifndef VR_COUNT_SLOTS
                 ++evals;
+#endif
             }
         }
         const float tl = spec_expf(-(sl * p.od));
