@@ -41,7 +41,13 @@ import volumetricrenderer_amd as vr  # noqa: E402
 from volumetricrenderer_amd import distributed as vrdist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-GATE_CYCLES = int(2e-3 * 2.1e9)   # ~2 ms of torch.cuda._sleep at ~2.1 GHz: the host queues K frames behind it
+# the roofline's gated pass queues its K frames behind this many frames of the
+# same loop (~0.8 ms of GPU work at config 5): the host queues the K frames
+# meanwhile, so the GPU never waits for it between them.  Round 6 first gated
+# with a ~2 ms sleep kernel (torch.cuda._sleep), which let the clocks drop:
+# the pass then ran ~2 % slower than the timed window itself
+# (profiles/r06/final3/trace_frames.txt: 0.1055 against 0.1035 ms per frame).
+GATE_FRAMES = 8
 FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: fp32 vector peak
 TA_PEAK_GLOOKUPS = 256 * 2.4   # L1 tag lookups: 1 per CU-cycle at 2.4 GHz (tools/tcp_calib.hip)
 BYTES_PER_STEP = 32        # 4 trilinear taps x 8 texels x 1 B
@@ -571,14 +577,15 @@ def main() -> int:
         # rebuild its region lists on the host)
         got = pipe.frame(stream)
         # untimed, after the window: the same K frames gated -- queued behind
-        # a ~2 ms spin on the caller's stream, so the GPU never waits for the
-        # host between them -- with HIP events after the spin and after the
-        # join of the render streams: the GPU time per frame the roofline
-        # divides by (the timed window's own GPU clock also holds the first
-        # frame's launch latency)
+        # GATE_FRAMES frames of the loop, so the GPU never waits for the host
+        # between them and runs at the window's clocks -- with HIP events after
+        # the gate's frames (the caller's stream joins the render streams) and
+        # after the K frames' join: the GPU time per frame the roofline divides
+        # by (the timed window's own GPU clock also holds the first frame's
+        # launch latency)
         g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        with torch.cuda.stream(stream):
-            torch.cuda._sleep(GATE_CYCLES)
+        pipe.run_frames(GATE_FRAMES, stream=stream,
+                        cameras=[sd[args.warmup + i % args.steps] for i in range(GATE_FRAMES)] if sd else None)
         g0.record(stream)
         pipe.run_frames(args.steps, stream=stream, cameras=sd[args.warmup:] if sd else None)
         g1.record(stream)
@@ -772,13 +779,15 @@ def main() -> int:
                                          "the time is the timed window per frame, not a launch's duration "
                                          "(kernel_ms_mean: the overlapping launches' mean)"
                                          + (": the GPU time per frame of the same K frames run again after the window, "
-                                            "gated (queued behind a ~2 ms spin on the caller's stream so the GPU never "
-                                            "waits for the host; HIP events after the spin and after the join of the "
-                                            "render streams: gpu_ms_per_frame_gated); the timed window's own clocks are "
+                                            f"gated (queued behind {GATE_FRAMES} frames of the loop, so the GPU never "
+                                            "waits for the host and keeps its clocks; HIP events after the gate's frames "
+                                            "and after the join of the render streams: gpu_ms_per_frame_gated, "
+                                            "gate_frames); the timed window's own clocks are "
                                             "in window, and ms_per_step is the host clock's"
                                             if gated_ms_frame else ": its wall time"))
         if gated_ms_frame:
             roofline["gpu_ms_per_frame_gated"] = round(gated_ms_frame, 5)
+            roofline["gate_frames"] = GATE_FRAMES
             # the same units over the host wall time per frame of the timed window
             roofline["frac_wall"] = round(roofline["achieved"] * roof_ms / ms_per_step / roofline["peak"], 4)
         if busy_ms_frame and not compositor:

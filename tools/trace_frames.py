@@ -107,7 +107,8 @@ def main():
         gated = None
         if name == "grid512" and obj and "gpu_ms_per_frame_gated" in obj.get("roofline", {}):
             # bench.py: the same K frames again, gated, after the window (the roofline's time)
-            g = fr[first + a.steps:first + 2 * a.steps]   # (the frame check's render comes after the passes)
+            gf = obj["roofline"].get("gate_frames", 0)   # frames of the loop before the gated ones
+            g = fr[first + a.steps + gf:first + 2 * a.steps + gf]   # (the frame check's render comes after the passes)
             giv = [(s_, e_) for f in g for (s_, e_, _) in f]
             gated = (max(e_ for _, e_ in giv) - min(s_ for s_, _ in giv)) / a.steps / 1e6
         timed = fr[first:first + a.steps]
