@@ -76,7 +76,7 @@ public:
     // Render the whole frame (or a band set) into a device buffer.
     void EnqueueRenderPass(const Rect2D& rect, vr_format fmt, void* d_pixels, void* stream = nullptr,
                            uint64_t* d_step_counter = nullptr, int band_rows = 0, int band_stride = 1,
-                           int band_first = 0)
+                           int band_first = 0, int band_flip = 0)
     {
         vr_target t{};
         t.width = rect.width;
@@ -85,6 +85,7 @@ public:
         t.band_rows = band_rows;
         t.band_stride = band_stride;
         t.band_first = band_first;
+        t.band_flip = band_flip;   // vr.h: odd bands of the set shifted (the serpentine deal)
         t.pixels = d_pixels;
         t.row_pitch = 0;
         t.step_counter = d_step_counter;
